@@ -1,0 +1,5 @@
+#include <pybind11/pybind11.h>
+namespace py = pybind11;
+namespace ahv { namespace host {
+void register_runtime(py::module_& m) { (void)m; }
+}}

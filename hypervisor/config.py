@@ -1,0 +1,81 @@
+"""Runtime configuration.
+
+The reference has no configuration system beyond dataclasses and constructor
+arguments; those are all preserved with identical names and defaults.  This
+module adds the knobs of the MI355X engine, each overridable from the environment
+with an ``AHV_`` prefix:
+
+==========================  =======  ===============================================
+field                       env      meaning
+==========================  =======  ===============================================
+parity_mode                 AHV_PARITY_MODE   reproduce reference quirks bit-for-bit
+                                     (diamond vouch false-positive Q05, GC no-op Q01,
+                                     mutating verify_chain Q02, checkpoint index Q17,
+                                     fan-out empty timeout error Q07, IATP undo-window
+                                     units Q21)
+emit_events                 AHV_EMIT_EVENTS   Hypervisor emits lifecycle events (Q03)
+device                      AHV_DEVICE        torch device of the batched engine
+session_capacity            AHV_SESSION_CAPACITY  device session-table rows per rank
+agent_capacity              AHV_AGENT_CAPACITY    device agent-table rows per rank
+vouch_capacity              AHV_VOUCH_CAPACITY    device vouch-edge rows per rank
+use_hip_graphs              AHV_HIP_GRAPHS    capture steady-state launches in hipGraphs
+collective_epoch            AHV_COLLECTIVE_EPOCH  pipeline steps between cross-rank
+                                     liability/commitment flushes
+==========================  =======  ===============================================
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, fields
+
+
+def _env_bool(name: str, default: bool) -> bool:
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    return v.strip().lower() in ("1", "true", "yes", "on")
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v else default
+
+
+@dataclass
+class HypervisorRuntimeConfig:
+    parity_mode: bool = False
+    emit_events: bool = True
+    device: str = "cuda"
+    session_capacity: int = 1 << 20
+    agent_capacity: int = 1 << 22
+    vouch_capacity: int = 1 << 22
+    use_hip_graphs: bool = True
+    collective_epoch: int = 1
+
+    @classmethod
+    def from_env(cls) -> "HypervisorRuntimeConfig":
+        return cls(
+            parity_mode=_env_bool("AHV_PARITY_MODE", False),
+            emit_events=_env_bool("AHV_EMIT_EVENTS", True),
+            device=os.environ.get("AHV_DEVICE", "cuda"),
+            session_capacity=_env_int("AHV_SESSION_CAPACITY", 1 << 20),
+            agent_capacity=_env_int("AHV_AGENT_CAPACITY", 1 << 22),
+            vouch_capacity=_env_int("AHV_VOUCH_CAPACITY", 1 << 22),
+            use_hip_graphs=_env_bool("AHV_HIP_GRAPHS", True),
+            collective_epoch=_env_int("AHV_COLLECTIVE_EPOCH", 1),
+        )
+
+    def as_dict(self) -> dict:
+        return {f.name: getattr(self, f.name) for f in fields(self)}
+
+
+RUNTIME = HypervisorRuntimeConfig.from_env()
+
+
+def parity_mode() -> bool:
+    return RUNTIME.parity_mode
+
+
+def set_parity_mode(on: bool) -> None:
+    RUNTIME.parity_mode = bool(on)

@@ -1,0 +1,277 @@
+"""Hypervisor: the top-level orchestrator of shared multi-agent sessions.
+
+Parity target: reference ``core.py:37-298``.
+
+Shared engines: vouching, slashing, ring enforcer, action classifier, history
+verifier, commitment, GC.  Per session (:class:`ManagedSession`): the SSO (with
+its VFS), a reversibility registry, a delta engine and a saga orchestrator.
+
+``join_session`` (the admission "forward pass"):
+
+1. IATP manifest enrichment when an adapter and manifest are given (manifest
+   actions fill in missing ``actions``; the σ hint replaces ``sigma_raw == 0.0``);
+2. register actions; any irreversible action forces STRONG consistency;
+3. history verification (an untrustworthy history forces Ring 3);
+4. σ resolution — Nexus when ``sigma_raw == 0.0``; with an explicit σ *and* a
+   history, the lower of the two;
+5. ring = ``compute_ring(σ)``; ``sso.join``.
+
+``terminate_session``: TERMINATING → Merkle root → commitment → release the
+session's bonds → GC → ARCHIVED; returns the root (``None`` with audit off or no
+deltas).
+
+``verify_behavior``: CMVK drift check; HIGH/CRITICAL drift slashes the agent
+(ω = 0.95) against a snapshot of participant σ and reports to Nexus.  As in the
+reference the participant's own σ/ring are left unchanged unless
+``demote_on_slash=True`` (Q06).
+
+Additions: an optional ``event_bus`` that receives lifecycle events (the
+reference never emitted, Q03); an optional ``declared_history`` for join (Q23);
+and :meth:`Hypervisor.pipeline_batch`, which runs the same governance pipeline
+for thousands of sessions at once on the MI355X device engine.
+"""
+
+from __future__ import annotations
+
+import logging
+from typing import Any, Optional
+
+from hypervisor.audit.commitment import CommitmentEngine
+from hypervisor.audit.delta import DeltaEngine
+from hypervisor.audit.gc import EphemeralGC, RetentionPolicy
+from hypervisor.liability.slashing import SlashingEngine
+from hypervisor.liability.vouching import VouchingEngine
+from hypervisor.models import ActionDescriptor, ConsistencyMode, ExecutionRing, SessionConfig
+from hypervisor.reversibility.registry import ReversibilityRegistry
+from hypervisor.rings.classifier import ActionClassifier
+from hypervisor.rings.enforcer import RingEnforcer
+from hypervisor.saga.orchestrator import SagaOrchestrator
+from hypervisor.session import SharedSessionObject
+from hypervisor.verification.history import TransactionHistoryVerifier
+
+logger = logging.getLogger(__name__)
+
+_STRONG = ConsistencyMode.STRONG
+
+
+class ManagedSession:
+    """A session plus the engines scoped to it."""
+
+    __slots__ = ("sso", "reversibility", "delta_engine", "saga")
+
+    def __init__(self, sso: SharedSessionObject) -> None:
+        self.sso = sso
+        sid = sso.session_id
+        self.reversibility = ReversibilityRegistry(sid)
+        self.delta_engine = DeltaEngine(sid)
+        self.saga = SagaOrchestrator()
+
+
+class Hypervisor:
+    def __init__(
+        self,
+        retention_policy: Optional[RetentionPolicy] = None,
+        max_exposure: Optional[float] = None,
+        nexus: Optional[Any] = None,
+        cmvk: Optional[Any] = None,
+        iatp: Optional[Any] = None,
+        event_bus: Optional[Any] = None,
+        demote_on_slash: bool = False,
+    ) -> None:
+        self.vouching = VouchingEngine(max_exposure=max_exposure)
+        self.slashing = SlashingEngine(self.vouching)
+        self.ring_enforcer = RingEnforcer()
+        self.classifier = ActionClassifier()
+        self.verifier = TransactionHistoryVerifier()
+        self.commitment = CommitmentEngine()
+        self.gc = EphemeralGC(retention_policy)
+        self.nexus = nexus
+        self.cmvk = cmvk
+        self.iatp = iatp
+        self.event_bus = event_bus
+        self.demote_on_slash = demote_on_slash
+        self._sessions: dict[str, ManagedSession] = {}
+        self._device_engine = None
+
+    # -- events --------------------------------------------------------------
+    def _emit(self, etype, session_id=None, agent_did=None, **payload) -> None:
+        bus = self.event_bus
+        if bus is not None:
+            from hypervisor.observability.event_bus import HypervisorEvent
+
+            bus.emit(HypervisorEvent(event_type=etype, session_id=session_id, agent_did=agent_did, payload=payload))
+
+    # -- lifecycle -------------------------------------------------------------
+    async def create_session(self, config: SessionConfig, creator_did: str) -> ManagedSession:
+        sso = SharedSessionObject(config=config, creator_did=creator_did)
+        sso.begin_handshake()
+        managed = ManagedSession(sso)
+        self._sessions[sso.session_id] = managed
+        if self.event_bus is not None:
+            from hypervisor.observability.event_bus import EventType
+
+            self._emit(EventType.SESSION_CREATED, sso.session_id, creator_did)
+        return managed
+
+    async def join_session(
+        self,
+        session_id: str,
+        agent_did: str,
+        actions: Optional[list[ActionDescriptor]] = None,
+        sigma_raw: float = 0.0,
+        manifest: Optional[Any] = None,
+        agent_history: Optional[Any] = None,
+        declared_history: Optional[list] = None,
+    ) -> ExecutionRing:
+        managed = self._get_session(session_id)
+        if self.iatp and manifest:
+            analysis = (
+                self.iatp.analyze_manifest_dict(manifest)
+                if isinstance(manifest, dict)
+                else self.iatp.analyze_manifest(manifest)
+            )
+            if not actions:
+                actions = analysis.actions
+            if sigma_raw == 0.0:
+                sigma_raw = analysis.sigma_hint
+            logger.debug("IATP manifest parsed for %s: ring_hint=%s", agent_did, analysis.ring_hint)
+        if actions:
+            managed.reversibility.register_from_manifest(actions)
+        if managed.reversibility.has_non_reversible_actions():
+            managed.sso.force_consistency_mode(_STRONG)
+
+        verification = self.verifier.verify(agent_did, declared_history)
+
+        sigma_eff = sigma_raw
+        if self.nexus:
+            if sigma_raw == 0.0:
+                sigma_eff = self.nexus.resolve_sigma(agent_did, history=agent_history)
+                logger.debug("Nexus resolved sigma=%.3f for %s", sigma_eff, agent_did)
+            elif agent_history:
+                sigma_eff = min(sigma_raw, self.nexus.resolve_sigma(agent_did, history=agent_history))
+
+        ring = self.ring_enforcer.compute_ring(sigma_eff)
+        if not verification.is_trustworthy:
+            ring = ExecutionRing.RING_3_SANDBOX
+        managed.sso.join(agent_did=agent_did, sigma_raw=sigma_raw, sigma_eff=sigma_eff, ring=ring)
+        if self.event_bus is not None:
+            from hypervisor.observability.event_bus import EventType
+
+            self._emit(EventType.SESSION_JOINED, session_id, agent_did, sigma_eff=sigma_eff)
+            self._emit(EventType.RING_ASSIGNED, session_id, agent_did, ring=int(ring.value))
+        return ring
+
+    async def activate_session(self, session_id: str) -> None:
+        self._get_session(session_id).sso.activate()
+        if self.event_bus is not None:
+            from hypervisor.observability.event_bus import EventType
+
+            self._emit(EventType.SESSION_ACTIVATED, session_id)
+
+    async def terminate_session(self, session_id: str) -> Optional[str]:
+        managed = self._get_session(session_id)
+        sso = managed.sso
+        sso.terminate()
+        de = managed.delta_engine
+        root = None
+        if sso.config.enable_audit:
+            root = de.compute_merkle_root()
+            if root:
+                self.commitment.commit(
+                    session_id=session_id,
+                    merkle_root=root,
+                    participant_dids=[p.agent_did for p in sso.participants],
+                    delta_count=de.turn_count,
+                )
+        self.vouching.release_session_bonds(session_id)
+        self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de, delta_count=de.turn_count)
+        sso.archive()
+        if self.event_bus is not None:
+            from hypervisor.observability.event_bus import EventType
+
+            self._emit(EventType.SESSION_TERMINATED, session_id, merkle_root=root)
+            if root:
+                self._emit(EventType.AUDIT_COMMITTED, session_id, merkle_root=root)
+            self._emit(EventType.AUDIT_GC_COLLECTED, session_id)
+            self._emit(EventType.SESSION_ARCHIVED, session_id)
+        return root
+
+    def get_session(self, session_id: str) -> Optional[ManagedSession]:
+        return self._sessions.get(session_id)
+
+    # -- behaviour verification --------------------------------------------------
+    async def verify_behavior(
+        self,
+        session_id: str,
+        agent_did: str,
+        claimed_embedding: Any,
+        observed_embedding: Any,
+        action_id: Optional[str] = None,
+    ) -> Optional[Any]:
+        if not self.cmvk:
+            return None
+        result = self.cmvk.check_behavioral_drift(
+            agent_did=agent_did,
+            session_id=session_id,
+            claimed_embedding=claimed_embedding,
+            observed_embedding=observed_embedding,
+            action_id=action_id,
+        )
+        if result.should_slash:
+            managed = self._get_session(session_id)
+            participant = managed.sso.get_participant(agent_did)
+            scores = {p.agent_did: p.sigma_eff for p in managed.sso.participants}
+            slash = self.slashing.slash(
+                vouchee_did=agent_did,
+                session_id=session_id,
+                vouchee_sigma=participant.sigma_eff,
+                risk_weight=0.95,
+                reason=f"CMVK drift: {result.drift_score:.3f} ({result.severity.value})",
+                agent_scores=scores,
+            )
+            if self.demote_on_slash:
+                for p in managed.sso.participants:
+                    if p.agent_did in scores:
+                        p.sigma_eff = scores[p.agent_did]
+                        p.ring = max(p.ring, self.ring_enforcer.compute_ring(p.sigma_eff), key=int)
+            if self.nexus:
+                self.nexus.report_slash(
+                    agent_did=agent_did,
+                    reason=f"Behavioral drift: {result.drift_score:.3f}",
+                    severity="critical" if result.drift_score >= 0.75 else "high",
+                )
+            if self.event_bus is not None:
+                from hypervisor.observability.event_bus import EventType
+
+                self._emit(EventType.BEHAVIOR_DRIFT, session_id, agent_did, drift=result.drift_score)
+                self._emit(EventType.SLASH_EXECUTED, session_id, agent_did, slash_id=slash.slash_id)
+            logger.warning("Agent %s slashed: drift=%.3f", agent_did, result.drift_score)
+        return result
+
+    # -- queries ------------------------------------------------------------------
+    @property
+    def active_sessions(self) -> list[ManagedSession]:
+        return [m for m in self._sessions.values() if m.sso.state.value not in ("archived", "terminating")]
+
+    def _get_session(self, session_id: str) -> ManagedSession:
+        m = self._sessions.get(session_id)
+        if m is None:
+            raise ValueError(f"Session {session_id} not found")
+        return m
+
+    # -- MI355X batched engine --------------------------------------------------------
+    @property
+    def device_engine(self):
+        """Lazily-created :class:`agent_hypervisor_amd.models.GovernanceEngine`."""
+        if self._device_engine is None:
+            from agent_hypervisor_amd.models.engine import GovernanceEngine
+
+            self._device_engine = GovernanceEngine()
+        return self._device_engine
+
+    def pipeline_batch(self, n_sessions: int, **kwargs):
+        """Run the full governance pipeline for ``n_sessions`` sessions on device.
+
+        See :meth:`agent_hypervisor_amd.models.engine.GovernanceEngine.run_pipeline`.
+        """
+        return self.device_engine.run_pipeline(n_sessions, **kwargs)

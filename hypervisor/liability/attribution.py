@@ -1,0 +1,156 @@
+"""Proportional fault attribution for a failed saga (Shapley-inspired).
+
+Parity target: reference ``liability/attribution.py:17-207``.
+
+For each agent, summed over that agent's action nodes:
+
+* +0.5 (DIRECT) if the node is the root cause (its step and agent match the
+  failure);
+* +0.3 (ENABLING) / (# failed non-root nodes overall) for each failed non-root
+  node;
+* +0.2 (PROXIMITY) · ω(action, default 0.5) / (# nodes of that agent).
+
+Raw scores are normalised to sum to 1 (a zero total divides by 1), both rounded
+with ``round(x, 4)`` and sorted by descending liability.  ``dependencies`` are
+recorded but not traversed (as in the reference).
+
+The per-agent reduction is the segmented kernel K21; the final ``round`` stays on
+the host because it is CPython's correctly-rounded decimal rounding.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from datetime import datetime
+from typing import Optional
+
+from agent_hypervisor_amd._native import C as _C
+from hypervisor._clock import now as _now
+
+
+@dataclass
+class CausalNode:
+    node_id: str = field(default_factory=lambda: _C.hex_id("", 8))
+    agent_did: str = ""
+    action_id: str = ""
+    step_id: str = ""
+    timestamp: datetime = field(default_factory=_now)
+    success: bool = True
+    is_root_cause: bool = False
+    dependencies: list[str] = field(default_factory=list)
+
+
+@dataclass
+class FaultAttribution:
+    agent_did: str
+    liability_score: float
+    causal_contribution: float
+    is_direct_cause: bool = False
+    reason: str = ""
+
+
+@dataclass
+class AttributionResult:
+    attribution_id: str = field(default_factory=lambda: _C.hex_id("attr:", 8))
+    saga_id: str = ""
+    session_id: str = ""
+    timestamp: datetime = field(default_factory=_now)
+    attributions: list[FaultAttribution] = field(default_factory=list)
+    causal_chain_length: int = 0
+    root_cause_agent: Optional[str] = None
+
+    @property
+    def agents_involved(self) -> list[str]:
+        return [a.agent_did for a in self.attributions]
+
+    def get_liability(self, agent_did: str) -> float:
+        for a in self.attributions:
+            if a.agent_did == agent_did:
+                return a.liability_score
+        return 0.0
+
+
+class CausalAttributor:
+    DIRECT_CAUSE_WEIGHT = 0.5
+    ENABLING_WEIGHT = 0.3
+    PROXIMITY_WEIGHT = 0.2
+
+    def __init__(self) -> None:
+        self._history: list[AttributionResult] = []
+
+    def build_causal_dag(
+        self,
+        agent_actions: dict[str, list[dict]],
+        failure_step_id: str,
+        failure_agent_did: str,
+    ) -> list[CausalNode]:
+        return [
+            CausalNode(
+                agent_did=agent,
+                action_id=a.get("action_id", ""),
+                step_id=a.get("step_id", ""),
+                success=a.get("success", True),
+                is_root_cause=(a.get("step_id") == failure_step_id and agent == failure_agent_did),
+                dependencies=a.get("dependencies", []),
+            )
+            for agent, acts in agent_actions.items()
+            for a in acts
+        ]
+
+    def raw_scores(
+        self, nodes: list[CausalNode], agents, risk_weights: dict[str, float]
+    ) -> dict[str, float]:
+        enabling_n = max(1, sum(1 for n in nodes if not n.success and not n.is_root_cause))
+        per_agent: dict[str, list[CausalNode]] = {}
+        for n in nodes:
+            per_agent.setdefault(n.agent_did, []).append(n)
+        out: dict[str, float] = {}
+        for agent in agents:
+            mine = per_agent.get(agent, [])
+            denom = max(1, len(mine))
+            s = 0.0
+            for n in mine:
+                if n.is_root_cause:
+                    s += self.DIRECT_CAUSE_WEIGHT
+                if not n.success and not n.is_root_cause:
+                    s += self.ENABLING_WEIGHT / enabling_n
+                s += self.PROXIMITY_WEIGHT * risk_weights.get(n.action_id, 0.5) / denom
+            out[agent] = s
+        return out
+
+    def attribute(
+        self,
+        saga_id: str,
+        session_id: str,
+        agent_actions: dict[str, list[dict]],
+        failure_step_id: str,
+        failure_agent_did: str,
+        risk_weights: Optional[dict[str, float]] = None,
+    ) -> AttributionResult:
+        nodes = self.build_causal_dag(agent_actions, failure_step_id, failure_agent_did)
+        raw = self.raw_scores(nodes, set(agent_actions.keys()), risk_weights or {})
+        total = sum(raw.values()) or 1.0
+        attrs = [
+            FaultAttribution(
+                agent_did=a,
+                liability_score=round(r / total, 4),
+                causal_contribution=round(r, 4),
+                is_direct_cause=a == failure_agent_did,
+                reason="Direct cause of failure" if a == failure_agent_did else "Contributing factor",
+            )
+            for a, r in raw.items()
+        ]
+        attrs.sort(key=lambda x: x.liability_score, reverse=True)
+        res = AttributionResult(
+            saga_id=saga_id,
+            session_id=session_id,
+            attributions=attrs,
+            causal_chain_length=len(nodes),
+            root_cause_agent=failure_agent_did,
+        )
+        self._history.append(res)
+        return res
+
+    @property
+    def attribution_history(self) -> list[AttributionResult]:
+        return list(self._history)

@@ -1,0 +1,174 @@
+"""Intent locks: declared READ / WRITE / EXCLUSIVE intent with contention and
+deadlock detection.
+
+Parity target: reference ``session/intent_locks.py:18-215``.
+
+* Compatibility: only READ+READ coexist; an agent never conflicts with its own
+  locks.
+* On conflict the wait-for graph ``_wait_for`` (agent → agents it waits on) is
+  searched from the blocking agents; reaching the requester raises
+  :class:`DeadlockError`, otherwise :class:`LockContentionError`.
+* ``_wait_for`` keeps the reference's name and shape because callers (and the
+  reference tests) populate it directly.  With ``record_waits=True`` the manager
+  also records wait edges itself on contention.
+
+A per-resource index keeps every lookup O(locks on that resource) instead of the
+reference's O(all locks) scans.  The batched contention check is kernel K20.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from datetime import datetime
+from enum import Enum
+from typing import Optional
+
+from agent_hypervisor_amd._native import C as _C
+from hypervisor._clock import now as _now
+
+
+class LockIntent(str, Enum):
+    READ = "read"
+    WRITE = "write"
+    EXCLUSIVE = "exclusive"
+
+
+def _lock_id() -> str:
+    return _C.hex_id("lock:", 8)
+
+
+@dataclass
+class IntentLock:
+    lock_id: str = field(default_factory=_lock_id)
+    agent_did: str = ""
+    session_id: str = ""
+    resource_path: str = ""
+    intent: LockIntent = LockIntent.READ
+    acquired_at: datetime = field(default_factory=_now)
+    is_active: bool = True
+    saga_step_id: Optional[str] = None
+
+
+class LockContentionError(Exception):
+    """The requested intent conflicts with active locks held by other agents."""
+
+
+class DeadlockError(Exception):
+    """Waiting for the blocking agents would close a cycle in the wait-for graph."""
+
+
+class IntentLockManager:
+    def __init__(self, record_waits: bool = False) -> None:
+        self._locks: dict[str, IntentLock] = {}
+        self._resource_locks: dict[str, list[str]] = {}
+        self._wait_for: dict[str, set[str]] = {}
+        self._record_waits = record_waits
+
+    # -- acquire / release ----------------------------------------------
+    def acquire(
+        self,
+        agent_did: str,
+        session_id: str,
+        resource_path: str,
+        intent: LockIntent,
+        saga_step_id: Optional[str] = None,
+    ) -> IntentLock:
+        conflicts = self._check_contention(resource_path, agent_did, intent)
+        if conflicts:
+            blockers = {c.agent_did for c in conflicts}
+            if self._would_deadlock(agent_did, blockers):
+                raise DeadlockError(
+                    f"Deadlock detected: {agent_did} would wait on "
+                    f"{blockers} which are waiting on {agent_did}"
+                )
+            if self._record_waits:
+                self._wait_for.setdefault(agent_did, set()).update(blockers)
+            raise LockContentionError(
+                f"Lock contention on {resource_path}: {agent_did} ({intent.value}) "
+                f"conflicts with {', '.join(c.agent_did for c in conflicts)}"
+            )
+        lock = IntentLock(
+            agent_did=agent_did,
+            session_id=session_id,
+            resource_path=resource_path,
+            intent=intent,
+            saga_step_id=saga_step_id,
+        )
+        self._locks[lock.lock_id] = lock
+        self._resource_locks.setdefault(resource_path, []).append(lock.lock_id)
+        return lock
+
+    def release(self, lock_id: str) -> None:
+        lock = self._locks.get(lock_id)
+        if lock is None:
+            return
+        lock.is_active = False
+        ids = self._resource_locks.get(lock.resource_path)
+        if ids and lock_id in ids:
+            ids.remove(lock_id)
+        self._wait_for.pop(lock.agent_did, None)
+
+    def _release_where(self, pred) -> int:
+        victims = [l.lock_id for l in self._locks.values() if l.is_active and pred(l)]
+        for lid in victims:
+            self.release(lid)
+        return len(victims)
+
+    def release_agent_locks(self, agent_did: str, session_id: str) -> int:
+        return self._release_where(lambda l: l.agent_did == agent_did and l.session_id == session_id)
+
+    def release_session_locks(self, session_id: str) -> int:
+        return self._release_where(lambda l: l.session_id == session_id)
+
+    # -- queries ------------------------------------------------------------
+    def get_agent_locks(self, agent_did: str, session_id: str) -> list[IntentLock]:
+        return [
+            l
+            for l in self._locks.values()
+            if l.is_active and l.agent_did == agent_did and l.session_id == session_id
+        ]
+
+    def get_resource_locks(self, resource_path: str) -> list[IntentLock]:
+        out = []
+        for lid in self._resource_locks.get(resource_path, ()):
+            l = self._locks.get(lid)
+            if l is not None and l.is_active:
+                out.append(l)
+        return out
+
+    def _check_contention(self, resource_path: str, agent_did: str, intent: LockIntent) -> list[IntentLock]:
+        return [
+            l
+            for l in self.get_resource_locks(resource_path)
+            if l.agent_did != agent_did and not self._is_compatible(l.intent, intent)
+        ]
+
+    @staticmethod
+    def _is_compatible(existing: LockIntent, requested: LockIntent) -> bool:
+        return existing == LockIntent.READ and requested == LockIntent.READ
+
+    def _would_deadlock(self, agent_did: str, blocking_agents: set[str]) -> bool:
+        seen: set[str] = set()
+        frontier = list(blocking_agents)
+        while frontier:
+            a = frontier.pop()
+            if a == agent_did:
+                return True
+            if a in seen:
+                continue
+            seen.add(a)
+            frontier.extend(self._wait_for.get(a, ()))
+        return False
+
+    @property
+    def active_lock_count(self) -> int:
+        return sum(1 for l in self._locks.values() if l.is_active)
+
+    @property
+    def contention_points(self) -> list[str]:
+        pts = []
+        for path, ids in self._resource_locks.items():
+            holders = {self._locks[i].agent_did for i in ids if i in self._locks and self._locks[i].is_active}
+            if len(holders) > 1:
+                pts.append(path)
+        return pts
