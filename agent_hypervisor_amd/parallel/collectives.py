@@ -1,0 +1,176 @@
+"""Cross-rank governance views under session sharding (SURVEY §2.13, X01–X10).
+
+Every liability invariant of the reference is session-scoped, so the per-session
+pipeline needs no communication; only agent-global and job-global views do.  They
+are computed here with ``torch.distributed`` (backend ``"nccl"`` = RCCL over
+xGMI on MI355X, ``"gloo"`` in the CPU test harness) on an epoch cadence, never on
+the per-session critical path.
+
+=====  =====================================  ===============================
+X      view                                    collective
+=====  =====================================  ===============================
+X01    Σ active bonded by voucher (liability)  all_reduce(SUM) over [A] fp64
+X02    slash effects on agent σ                all_reduce(MIN) blacklist +
+                                               all_reduce(PROD) clip factors
+X03    ledger risk partials                    all_reduce(SUM) fixed-point i64
+X04    job counters (stats endpoint)           all_reduce(SUM) [6] i64
+X05    earliest-session ring of an agent       all_reduce(MIN) packed i64 key
+X06    Merkle commitments                      all_gather (slot, root, count)
+X08    cache invalidation                      broadcast of agent ids
+X09    latency histograms                      gather to rank 0 (all_reduce SUM)
+=====  =====================================  ===============================
+
+All functions are no-ops returning the local value when no process group is
+initialised (single rank).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+FIXED_POINT_SCALE = 1 << 40  # X03: risk partials as int64 fixed point
+
+
+def _ready() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def world() -> int:
+    return dist.get_world_size() if _ready() else 1
+
+
+# -- X04 ----------------------------------------------------------------------------
+def pipeline_stats(engine, batch=None) -> torch.Tensor:
+    """Counters of the governance pipeline as int64[6] on the engine device:
+    sessions, ok, participants, deltas, commitments, archived.
+
+    When the batch was launched with a ``stats`` accumulator the kernel already
+    reduced them; otherwise they are reduced from the session table rows."""
+    t = engine.sessions
+    s = batch.slots() if batch is not None else torch.arange(t.capacity, device=t.sess_state.device)
+    st = t.sess_state.index_select(0, s)
+    out = torch.stack([
+        torch.tensor(s.numel(), device=st.device, dtype=torch.int64),
+        (t.status.index_select(0, s) == 0).sum(),
+        t.part_count.index_select(0, s).sum(),
+        t.delta_count.index_select(0, s).sum(),
+        (t.committed_at_us.index_select(0, s) > 0).sum(),
+        (st == 4).sum(),
+    ]).to(torch.int64)
+    return out
+
+
+def allreduce_stats(stats: torch.Tensor) -> torch.Tensor:
+    if _ready():
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+    return stats
+
+
+# -- X01 ----------------------------------------------------------------------------
+def allreduce_exposure(exposure: torch.Tensor) -> torch.Tensor:
+    """Σ active bonded amount per voucher over every rank's sessions ([A] fp64)."""
+    if _ready():
+        dist.all_reduce(exposure, op=dist.ReduceOp.SUM)
+    return exposure
+
+
+# -- X02 ----------------------------------------------------------------------------
+def merge_slash_effects(
+    sigma: torch.Tensor, blacklist: torch.Tensor, clip_factor: torch.Tensor, floor: float = 0.05
+) -> torch.Tensor:
+    """Exact cross-rank merge of slash effects on agent σ.
+
+    ``blacklist`` is 1 where a rank blacklisted the agent (σ → 0); ``clip_factor``
+    is the product Π(1−ω) of clips a rank applied (1 where none).  Because
+    ``max(max(x·a, F)·b, F) = max(x·a·b, F)`` for a, b ≤ 1, multiplying the
+    factors across ranks and flooring once equals applying every clip in turn.
+    """
+    bl = blacklist.to(torch.int32).clone()
+    cf = clip_factor.clone()
+    if _ready():
+        dist.all_reduce(bl, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cf, op=dist.ReduceOp.PRODUCT)
+    touched = cf < 1.0
+    out = torch.where(touched, torch.clamp(sigma * cf, min=floor), sigma)
+    return torch.where(bl > 0, torch.zeros_like(out), out)
+
+
+# -- X03 ----------------------------------------------------------------------------
+def allreduce_risk(partial_risk: torch.Tensor, counts: Optional[torch.Tensor] = None):
+    """Sum per-agent ledger risk partials across ranks deterministically.
+
+    fp64 partials are converted to int64 fixed point (2^-40 resolution) so the
+    reduction is associative; the clamp to [0, 1] happens after the sum, as in
+    LiabilityLedger.compute_risk_profile."""
+    fx = torch.round(partial_risk * FIXED_POINT_SCALE).to(torch.int64)
+    if _ready():
+        dist.all_reduce(fx, op=dist.ReduceOp.SUM)
+        if counts is not None:
+            dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+    risk = (fx.to(torch.float64) / FIXED_POINT_SCALE).clamp(0.0, 1.0)
+    return (risk, counts) if counts is not None else risk
+
+
+# -- X05 ----------------------------------------------------------------------------
+def earliest_ring(create_seq: torch.Tensor, ring: torch.Tensor) -> torch.Tensor:
+    """Ring of each agent in its earliest-created session across ranks.
+
+    Key = (global creation sequence << 8) | ring; the MIN key wins."""
+    key = (create_seq.to(torch.int64) << 8) | ring.to(torch.int64)
+    if _ready():
+        dist.all_reduce(key, op=dist.ReduceOp.MIN)
+    return key & 0xFF
+
+
+# -- X06 ----------------------------------------------------------------------------
+def allgather_commitments(slots: torch.Tensor, roots: torch.Tensor, counts: torch.Tensor):
+    """Gather every rank's (slot, 32-byte root, delta count) commitment records.
+
+    Returns (rank, slot, root, count) tensors concatenated over ranks."""
+    n = torch.tensor([slots.numel()], device=slots.device, dtype=torch.int64)
+    if not _ready():
+        r = torch.zeros_like(slots, dtype=torch.int32)
+        return r, slots, roots, counts
+    w = dist.get_world_size()
+    sizes = [torch.zeros_like(n) for _ in range(w)]
+    dist.all_gather(sizes, n)
+    m = int(max(int(s.item()) for s in sizes))
+    rec = torch.zeros((m, 10), dtype=torch.int32, device=slots.device)
+    k = slots.numel()
+    rec[:k, 0] = slots.to(torch.int32)
+    rec[:k, 1] = counts.to(torch.int32)
+    rec[:k, 2:] = roots.to(torch.int32)
+    out = [torch.empty_like(rec) for _ in range(w)]
+    dist.all_gather(out, rec)
+    ranks, sl, rt, ct = [], [], [], []
+    for r, (sz, blk) in enumerate(zip(sizes, out)):
+        c = int(sz.item())
+        ranks.append(torch.full((c,), r, dtype=torch.int32, device=slots.device))
+        sl.append(blk[:c, 0])
+        ct.append(blk[:c, 1])
+        rt.append(blk[:c, 2:])
+    return torch.cat(ranks), torch.cat(sl), torch.cat(rt), torch.cat(ct)
+
+
+# -- X08 ----------------------------------------------------------------------------
+def broadcast_invalidations(agent_ids: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """Broadcast a list of agent ids whose cached σ must be dropped (Nexus cache)."""
+    if not _ready():
+        return agent_ids
+    n = torch.tensor([agent_ids.numel()], dtype=torch.int64, device=agent_ids.device)
+    dist.broadcast(n, src)
+    buf = agent_ids if dist.get_rank() == src else torch.empty(int(n.item()), dtype=agent_ids.dtype,
+                                                               device=agent_ids.device)
+    dist.broadcast(buf, src)
+    return buf
+
+
+# -- X09 ----------------------------------------------------------------------------
+def reduce_histogram(hist: torch.Tensor) -> torch.Tensor:
+    """Element-wise sum of per-rank latency histograms (every rank gets the total)."""
+    if _ready():
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+    return hist

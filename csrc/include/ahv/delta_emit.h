@@ -1,0 +1,280 @@
+// Canonical SemanticDelta payload emission into a hashing "sink".
+//
+// One emitter, two sinks:
+//   * HostSink        — streams bytes into SHA-256 (host twin / CPU tests);
+//   * WaveWindowSink  — (ahv/wave_sink.h) assembles a 256-byte window of each
+//     lane's message in LDS per pass and compresses it on the device.
+//
+// Emitter contract: before writing a segment the emitter calls `s.want(len)`
+// with the segment's exact byte length; a false answer means the sink skipped
+// the segment (its bytes are outside the current window) and nothing is written.
+//
+// Byte-exact with json.dumps(sort_keys=True) of the reference payload
+// (audit/delta.py:43-63); pool strings are stored pre-escaped (JSON body without
+// quotes) by the host interner (agent_hypervisor_amd/utils/interner.py).
+#pragma once
+
+#include "ahv/canon_json.h"
+#include "ahv/sha256.h"
+
+namespace ahv {
+
+// Interned string pool: id -> JSON-escaped bytes (no surrounding quotes).
+struct StrPool {
+  const uint8_t* bytes;
+  const int64_t* off;
+  const int32_t* len;
+};
+
+// civil-from-days (proleptic Gregorian), days since 1970-01-01.
+AHV_HD void civil_from_days(int64_t z, int32_t& y, uint32_t& m, uint32_t& d) {
+  z += 719468;
+  const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+  const uint32_t doe = static_cast<uint32_t>(z - era * 146097);
+  const uint32_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const uint32_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const uint32_t mp = (5 * doy + 2) / 153;
+  d = doy - (153 * mp + 2) / 5 + 1;
+  m = mp < 10 ? mp + 3 : mp - 9;
+  y = static_cast<int32_t>(yoe) + static_cast<int32_t>(era) * 400 + (m <= 2 ? 1 : 0);
+}
+
+// Broken-down UTC instant.
+struct UtcParts {
+  uint32_t year, month, day, secs, micro;
+};
+
+AHV_HD UtcParts utc_parts(int64_t us) {
+  int64_t days = us / 86400000000LL;
+  int64_t rem = us - days * 86400000000LL;
+  if (rem < 0) { rem += 86400000000LL; --days; }
+  int32_t y; uint32_t mo, d;
+  civil_from_days(days, y, mo, d);
+  return UtcParts{static_cast<uint32_t>(y), mo, d, static_cast<uint32_t>(rem / 1000000),
+                  static_cast<uint32_t>(rem % 1000000)};
+}
+
+// Host helper: datetime.isoformat() text of an epoch-µs UTC instant.
+AHV_HD uint32_t iso_utc(int64_t us, uint8_t* out) {
+  const UtcParts t = utc_parts(us);
+  uint32_t n = 0;
+  auto d2 = [&](uint32_t v) { out[n++] = '0' + v / 10; out[n++] = '0' + v % 10; };
+  d2((t.year / 100) % 100); d2(t.year % 100);
+  out[n++] = '-'; d2(t.month); out[n++] = '-'; d2(t.day);
+  out[n++] = 'T'; d2(t.secs / 3600); out[n++] = ':'; d2((t.secs / 60) % 60); out[n++] = ':'; d2(t.secs % 60);
+  if (t.micro) { out[n++] = '.'; d2(t.micro / 10000); d2((t.micro / 100) % 100); d2(t.micro % 100); }
+  out[n++] = '+'; out[n++] = '0'; out[n++] = '0'; out[n++] = ':'; out[n++] = '0'; out[n++] = '0';
+  return n;
+}
+
+// ---------------------------------------------------------------- host sink
+
+struct HostSink {
+  Sha256Stream h;
+  uint32_t scratch[8][8];
+  AHV_HD bool want(uint32_t) { return true; }
+  AHV_HD void byte(uint8_t b) { h.put(b); }
+  AHV_HD bool any(bool b) const { return b; }
+  template <class Emit>
+  AHV_HD void hash(Emit&& emit, uint32_t out[8]) {
+    h.init();
+    emit(*this);
+    h.final(out);
+  }
+  AHV_HD void stash(int j, const uint32_t d[8]) {
+    for (int k = 0; k < 8; ++k) scratch[j][k] = d[k];
+  }
+  AHV_HD void load(int j, uint32_t d[8]) const {
+    for (int k = 0; k < 8; ++k) d[k] = scratch[j][k];
+  }
+  AHV_HD void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const { merkle_node(l, r, out); }
+};
+
+// Level-wise Merkle root over `m` (≤ 8) digests stashed in the sink's scratch
+// slots 0..m-1 (reference audit/delta.py:117-134: odd node duplicated).
+template <class Sink>
+AHV_HD void merkle_root_stashed(Sink& s, int m, uint32_t root[8]) {
+  while (m > 1) {
+    const int half = (m + 1) >> 1;
+    for (int j = 0; j < half; ++j) {
+      uint32_t l[8], r[8], o[8];
+      s.load(2 * j, l);
+      s.load((2 * j + 1 < m) ? 2 * j + 1 : 2 * j, r);
+      s.node(l, r, o);
+      s.stash(j, o);
+    }
+    m = half;
+  }
+  s.load(0, root);
+}
+
+// ------------------------------------------------------------ emission API
+
+template <class Sink>
+AHV_HD void emit_lit(Sink& s, const char* lit, uint32_t n) {
+  if (!s.want(n)) return;
+  for (uint32_t i = 0; i < n; ++i) s.byte(static_cast<uint8_t>(lit[i]));
+}
+
+template <class Sink, size_t N>
+AHV_HD void emit_lit(Sink& s, const char (&lit)[N]) {
+  emit_lit(s, lit, static_cast<uint32_t>(N - 1));
+}
+
+// Pool string id as a JSON value: "…" or null.
+template <class Sink>
+AHV_HD void emit_pool_str(Sink& s, const StrPool& pool, int32_t id) {
+  if (id < 0) {
+    emit_lit(s, canon::K_NULL);
+    return;
+  }
+  const uint32_t n = static_cast<uint32_t>(pool.len[id]);
+  if (!s.want(n + 2)) return;
+  const uint8_t* p = pool.bytes + pool.off[id];
+  s.byte('"');
+  for (uint32_t i = 0; i < n; ++i) s.byte(p[i]);
+  s.byte('"');
+}
+
+// Decimal digits, most significant first (no local digit array: an array indexed
+// by a runtime position would live in scratch memory on the device).
+template <class Sink>
+AHV_HD void emit_uint(Sink& s, uint64_t v) {
+  if (!s.want(canon::dec_digits(v))) return;
+  uint64_t p = 1;
+  while (v / p >= 10) p *= 10;
+  for (; p; p /= 10) s.byte(static_cast<uint8_t>('0' + (v / p) % 10));
+}
+
+template <class Sink>
+AHV_HD void emit_hex_digest_quoted(Sink& s, const uint32_t d[8]) {
+  if (!s.want(66)) return;
+  s.byte('"');
+  // one digest word per iteration (a fully unrolled 64-char body keeps all 64
+  // characters live in VGPRs at once)
+#pragma nounroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w = (k == i) ? d[k] : w;
+#pragma nounroll
+    for (int j = 7; j >= 0; --j) s.byte(static_cast<uint8_t>(hex_nibble((w >> (4 * j)) & 15u)));
+  }
+  s.byte('"');
+}
+
+// "session:xxxxxxxx-xxxx-xxxx-xxxx-xxxxxxxxxxxx" from 4 big-endian uuid words.
+template <class Sink>
+AHV_HD void emit_session_uuid_quoted(Sink& s, const uint32_t u[4]) {
+  if (!s.want(46)) return;
+  const char* pre = "\"session:";
+  for (int i = 0; i < 9; ++i) s.byte(static_cast<uint8_t>(pre[i]));
+#pragma nounroll
+  for (int k = 0; k < 32; ++k) {
+    if (k == 8 || k == 12 || k == 16 || k == 20) s.byte('-');
+    const uint32_t q = k >> 3;
+    const uint32_t w = q == 0 ? u[0] : q == 1 ? u[1] : q == 2 ? u[2] : u[3];
+    s.byte(static_cast<uint8_t>(hex_nibble((w >> (28 - 4 * (k & 7))) & 15u)));
+  }
+  s.byte('"');
+}
+
+template <class Sink>
+AHV_HD void emit_2d(Sink& s, uint32_t v) {
+  s.byte(static_cast<uint8_t>('0' + v / 10));
+  s.byte(static_cast<uint8_t>('0' + v % 10));
+}
+
+// datetime.isoformat() text, quoted, straight into the sink.
+template <class Sink>
+AHV_HD void emit_iso_quoted(Sink& s, int64_t us) {
+  const UtcParts t = utc_parts(us);
+  if (!s.want(t.micro ? 34u : 27u)) return;
+  s.byte('"');
+  emit_2d(s, (t.year / 100) % 100);
+  emit_2d(s, t.year % 100);
+  s.byte('-'); emit_2d(s, t.month);
+  s.byte('-'); emit_2d(s, t.day);
+  s.byte('T'); emit_2d(s, t.secs / 3600);
+  s.byte(':'); emit_2d(s, (t.secs / 60) % 60);
+  s.byte(':'); emit_2d(s, t.secs % 60);
+  if (t.micro) {
+    s.byte('.');
+    emit_2d(s, t.micro / 10000);
+    emit_2d(s, (t.micro / 100) % 100);
+    emit_2d(s, t.micro % 100);
+  }
+  const char* tz = "+00:00\"";
+  for (int i = 0; i < 7; ++i) s.byte(static_cast<uint8_t>(tz[i]));
+}
+
+// One change object {"content_hash", "operation", "path", "previous_hash"}.
+struct ChangeIds {
+  int32_t path, op, content_hash, previous_hash;  // pool ids, -1 = null
+};
+
+// Session identity: either a pool string (API-created sessions) or a device
+// uuid4 (engine-minted sessions).
+struct SessionIdent {
+  int32_t str_id;    // >= 0: pool string id of the full session id
+  uint32_t uuid[4];  // else: 4 uuid words, rendered as "session:<uuid>"
+};
+
+// A digest passed by value (no pointers to register arrays: those would force
+// the array into scratch memory on the device).
+struct Digest {
+  uint32_t v[8];
+};
+
+// The full canonical payload of one delta.
+template <class Sink>
+AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, int32_t agent_id, const ChangeIds* ch,
+                               uint32_t nch, int32_t delta_id_str, uint32_t turn, bool has_parent,
+                               const Digest parent, const SessionIdent sid, int64_t ts_us) {
+  emit_lit(s, canon::K_OPEN_AGENT);
+  emit_pool_str(s, pool, agent_id);
+  emit_lit(s, canon::K_CHANGES);
+  for (uint32_t c = 0; c < nch; ++c) {
+    if (c) emit_lit(s, canon::K_CH_SEP);
+    emit_lit(s, canon::K_CH_OPEN);
+    emit_pool_str(s, pool, ch[c].content_hash);
+    emit_lit(s, canon::K_CH_OP);
+    emit_pool_str(s, pool, ch[c].op);
+    emit_lit(s, canon::K_CH_PATH);
+    emit_pool_str(s, pool, ch[c].path);
+    emit_lit(s, canon::K_CH_PREV);
+    emit_pool_str(s, pool, ch[c].previous_hash);
+    emit_lit(s, canon::K_CH_CLOSE);
+  }
+  emit_lit(s, canon::K_DELTA_ID);
+  if (delta_id_str >= 0) {
+    emit_pool_str(s, pool, delta_id_str);
+  } else {
+    emit_lit(s, "\"delta:", 7);
+    emit_uint(s, turn);
+    emit_lit(s, "\"", 1);
+  }
+  emit_lit(s, canon::K_PARENT);
+  if (has_parent) emit_hex_digest_quoted(s, parent.v);
+  else emit_lit(s, canon::K_NULL);
+  emit_lit(s, canon::K_SESSION);
+  if (sid.str_id >= 0) emit_pool_str(s, pool, sid.str_id);
+  else emit_session_uuid_quoted(s, sid.uuid);
+  emit_lit(s, canon::K_TS);
+  emit_iso_quoted(s, ts_us);
+  emit_lit(s, canon::K_TURN);
+  emit_uint(s, turn);
+  emit_lit(s, canon::K_CLOSE);
+}
+
+template <class Sink>
+AHV_HD void emit_delta_and_hash(Sink& s, const StrPool& pool, int32_t agent_id, const ChangeIds* ch,
+                                uint32_t nch, int32_t delta_id_str, uint32_t turn,
+                                bool has_parent, const Digest parent, const SessionIdent sid, int64_t ts_us,
+                                uint32_t out[8]) {
+  s.hash([=](Sink& k) {
+    emit_delta_payload(k, pool, agent_id, ch, nch, delta_id_str, turn, has_parent, parent, sid, ts_us);
+  }, out);
+}
+
+}  // namespace ahv
