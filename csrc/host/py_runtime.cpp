@@ -67,10 +67,14 @@ class StringPool {
     const int32_t id = static_cast<int32_t>(raw_.size());
     ids_.emplace(s, id);
     raw_.push_back(s);
+    // every string starts 16-byte aligned so kernels read it with 16-byte loads
+    bytes_.resize((bytes_.size() + 15) & ~size_t(15), 0);
     offsets_.push_back(static_cast<int64_t>(bytes_.size()));
     const size_t before = bytes_.size();
     escape_json_utf8(s, bytes_);
     lengths_.push_back(static_cast<int32_t>(bytes_.size() - before));
+    // keep the pool a multiple of 16 bytes: kernels read whole 16-byte chunks
+    bytes_.resize((bytes_.size() + 15) & ~size_t(15), 0);
     return id;
   }
 

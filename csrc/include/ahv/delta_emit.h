@@ -73,6 +73,8 @@ struct HostSink {
   Sha256Stream h;
   uint32_t scratch[8][8];
   AHV_HD bool want(uint32_t) { return true; }
+  template <class T>
+  AHV_HD void launder(T&) const {}
   AHV_HD void byte(uint8_t b) { h.put(b); }
   AHV_HD bool any(bool b) const { return b; }
   template <class Emit>
@@ -87,8 +89,48 @@ struct HostSink {
   AHV_HD void load(int j, uint32_t d[8]) const {
     for (int k = 0; k < 8; ++k) d[k] = scratch[j][k];
   }
-  AHV_HD void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const { merkle_node(l, r, out); }
+  AHV_HD void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const {
+    uint32_t t[8];  // out may alias l or r
+    merkle_node(l, r, t);
+    for (int k = 0; k < 8; ++k) out[k] = t[k];
+  }
 };
+
+// Merkle root of `n` leaves read by `leaf(i, out)`, with the reference's level-wise
+// odd-node duplication (audit/delta.py:117-134), computed as a binary counter:
+// after k leaves the sink's scratch slot L holds the subtree of level L for every
+// set bit L of k, so only ⌊log2 n⌋+1 digests are ever stored.  At the end the
+// partial subtrees are folded from the lowest level up; a subtree that is short
+// of its left neighbour's level is first self-paired (H(x, x)) once per missing
+// level, which is exactly what the level-wise algorithm does to the last node of
+// every odd level.
+template <class Sink, class Leaf>
+AHV_HD void merkle_root_counter(Sink& s, uint32_t n, Leaf&& leaf, uint32_t root[8]) {
+  for (uint32_t k = 0; k < n; ++k) {
+    uint32_t carry[8];
+    leaf(k, carry);
+    uint32_t lvl = 0;
+    while ((k >> lvl) & 1u) {
+      uint32_t left[8];
+      s.load(static_cast<int>(lvl), left);
+      s.node(left, carry, carry);
+      ++lvl;
+    }
+    s.stash(static_cast<int>(lvl), carry);
+  }
+  uint32_t lvl = 0;
+  while (!((n >> lvl) & 1u)) ++lvl;
+  s.load(static_cast<int>(lvl), root);
+  uint32_t cur = lvl;
+  for (uint32_t L = lvl + 1; (n >> L) != 0; ++L) {
+    if (!((n >> L) & 1u)) continue;
+    for (; cur < L; ++cur) s.node(root, root, root);
+    uint32_t left[8];
+    s.load(static_cast<int>(L), left);
+    s.node(left, root, root);
+    cur = L + 1;
+  }
+}
 
 // Level-wise Merkle root over `m` (≤ 8) digests stashed in the sink's scratch
 // slots 0..m-1 (reference audit/delta.py:117-134: odd node duplicated).
@@ -121,19 +163,60 @@ AHV_HD void emit_lit(Sink& s, const char (&lit)[N]) {
   emit_lit(s, lit, static_cast<uint32_t>(N - 1));
 }
 
-// Pool string id as a JSON value: "…" or null.
+// A resolved pool string: 16-byte aligned pointer + length (-1 = null).
+struct StrRef {
+  const uint8_t* p;
+  int32_t n;
+};
+
+AHV_HD StrRef pool_ref(const StrPool& pool, int32_t id) {
+  if (id < 0) return StrRef{nullptr, -1};
+  return StrRef{pool.bytes + pool.off[id], pool.len[id]};
+}
+
+struct alignas(16) U4 {
+  uint32_t a, b, c, d;
+};
+
+// Up to 4 bytes of a little-endian memory word, in memory order.
 template <class Sink>
-AHV_HD void emit_pool_str(Sink& s, const StrPool& pool, int32_t id) {
-  if (id < 0) {
+AHV_HD void emit_word_le(Sink& s, uint32_t w, uint32_t cnt) {
+  const uint32_t m = cnt < 4u ? cnt : 4u;
+  for (uint32_t j = 0; j < m; ++j) s.byte(static_cast<uint8_t>(w >> (8 * j)));
+}
+
+// Quoted string body from 16-byte aligned storage, read 16 bytes per load with
+// the next chunk prefetched (a byte-per-load loop waits a full memory latency per
+// character on the device).
+template <class Sink>
+AHV_HD void emit_str_ref(Sink& s, StrRef r) {
+  if (r.n < 0) {
     emit_lit(s, canon::K_NULL);
     return;
   }
-  const uint32_t n = static_cast<uint32_t>(pool.len[id]);
+  const uint32_t n = static_cast<uint32_t>(r.n);
   if (!s.want(n + 2)) return;
-  const uint8_t* p = pool.bytes + pool.off[id];
   s.byte('"');
-  for (uint32_t i = 0; i < n; ++i) s.byte(p[i]);
+  const U4* q = reinterpret_cast<const U4*>(r.p);
+  const uint32_t chunks = (n + 15) / 16;
+  // one 16-byte load per chunk (loop-carried prefetch copies made the compiler keep the chunk in scratch)
+  for (uint32_t c = 0; c < chunks; ++c) {
+    const U4 cur = q[c];
+    const uint32_t left = n - 16 * c;
+    // four named words (no indexing into the chunk: a runtime index would put
+    // it in scratch memory on the device)
+    emit_word_le(s, cur.a, left);
+    emit_word_le(s, cur.b, left > 4 ? left - 4 : 0);
+    emit_word_le(s, cur.c, left > 8 ? left - 8 : 0);
+    emit_word_le(s, cur.d, left > 12 ? left - 12 : 0);
+  }
   s.byte('"');
+}
+
+// Pool string id as a JSON value: "…" or null.
+template <class Sink>
+AHV_HD void emit_pool_str(Sink& s, const StrPool& pool, int32_t id) {
+  emit_str_ref(s, pool_ref(pool, id));
 }
 
 // Decimal digits, most significant first (no local digit array: an array indexed
@@ -152,11 +235,9 @@ AHV_HD void emit_hex_digest_quoted(Sink& s, const uint32_t d[8]) {
   s.byte('"');
   // one digest word per iteration (a fully unrolled 64-char body keeps all 64
   // characters live in VGPRs at once)
-#pragma nounroll
-  for (int i = 0; i < 8; ++i) {
-    uint32_t w = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) w = (k == i) ? d[k] : w;
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w = d[i];
 #pragma nounroll
     for (int j = 7; j >= 0; --j) s.byte(static_cast<uint8_t>(hex_nibble((w >> (4 * j)) & 15u)));
   }
@@ -169,12 +250,14 @@ AHV_HD void emit_session_uuid_quoted(Sink& s, const uint32_t u[4]) {
   if (!s.want(46)) return;
   const char* pre = "\"session:";
   for (int i = 0; i < 9; ++i) s.byte(static_cast<uint8_t>(pre[i]));
+  // 128-bit id as two 64-bit halves, nibbles by shifting (no array selection)
+  const uint64_t hi = (static_cast<uint64_t>(u[0]) << 32) | u[1];
+  const uint64_t lo = (static_cast<uint64_t>(u[2]) << 32) | u[3];
 #pragma nounroll
   for (int k = 0; k < 32; ++k) {
     if (k == 8 || k == 12 || k == 16 || k == 20) s.byte('-');
-    const uint32_t q = k >> 3;
-    const uint32_t w = q == 0 ? u[0] : q == 1 ? u[1] : q == 2 ? u[2] : u[3];
-    s.byte(static_cast<uint8_t>(hex_nibble((w >> (28 - 4 * (k & 7))) & 15u)));
+    const uint64_t src = k < 16 ? hi : lo;
+    s.byte(static_cast<uint8_t>(hex_nibble(static_cast<uint32_t>(src >> (60 - 4 * (k & 15))) & 15u)));
   }
   s.byte('"');
 }
@@ -228,11 +311,21 @@ struct Digest {
 
 // The full canonical payload of one delta.
 template <class Sink>
-AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, int32_t agent_id, const ChangeIds* ch,
+AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const ChangeIds* ch,
                                uint32_t nch, int32_t delta_id_str, uint32_t turn, bool has_parent,
-                               const Digest parent, const SessionIdent sid, int64_t ts_us) {
+                               Digest parent, SessionIdent sid, int64_t ts_us) {
+  // The device sink calls this once per window pass; laundering the inputs stops
+  // the compiler from hoisting every derived character (64 hex digits, uuid,
+  // timestamp digits) out of the pass loop and keeping them all live in VGPRs.
+  s.launder(agent.n);
+  s.launder(turn);
+  s.launder(ts_us);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s.launder(parent.v[k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s.launder(sid.uuid[k]);
   emit_lit(s, canon::K_OPEN_AGENT);
-  emit_pool_str(s, pool, agent_id);
+  emit_str_ref(s, agent);
   emit_lit(s, canon::K_CHANGES);
   for (uint32_t c = 0; c < nch; ++c) {
     if (c) emit_lit(s, canon::K_CH_SEP);
@@ -268,12 +361,12 @@ AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, int32_t agent_id, c
 }
 
 template <class Sink>
-AHV_HD void emit_delta_and_hash(Sink& s, const StrPool& pool, int32_t agent_id, const ChangeIds* ch,
+AHV_HD void emit_delta_and_hash(Sink& s, const StrPool& pool, StrRef agent, const ChangeIds* ch,
                                 uint32_t nch, int32_t delta_id_str, uint32_t turn,
                                 bool has_parent, const Digest parent, const SessionIdent sid, int64_t ts_us,
                                 uint32_t out[8]) {
   s.hash([=](Sink& k) {
-    emit_delta_payload(k, pool, agent_id, ch, nch, delta_id_str, turn, has_parent, parent, sid, ts_us);
+    emit_delta_payload(k, pool, agent, ch, nch, delta_id_str, turn, has_parent, parent, sid, ts_us);
   }, out);
 }
 

@@ -142,7 +142,7 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   sid.str_id = -1;
 #pragma unroll
   for (int k = 0; k < 4; ++k) sid.uuid[k] = u[k];
-  const int32_t did = a.agent_did[agent];
+  const StrRef did = pool_ref(a.pool, a.agent_did[agent]);  // resolved once per session
   Digest prev;
   uint32_t* hrow = t.delta_hash + slot * a.dmax * 8;
   for (int d = 0; d < a.deltas; ++d) {
@@ -192,13 +192,13 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   // same lane above) into the sink's digest scratch (LDS on the device).
   uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (a.deltas > 0) {
-    for (int d = 0; d < a.deltas; ++d) {
-      uint32_t h[8];
+    merkle_root_counter(
+        sink, static_cast<uint32_t>(a.deltas),
+        [&](uint32_t d, uint32_t h[8]) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) h[k] = hrow[d * 8 + k];
-      sink.stash(d, h);
-    }
-    merkle_root_stashed(sink, a.deltas, root);
+          for (int k = 0; k < 8; ++k) h[k] = hrow[d * 8 + k];
+        },
+        root);
   }
   const bool committed = a.audit && a.deltas > 0;
 #pragma unroll

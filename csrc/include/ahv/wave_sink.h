@@ -25,9 +25,12 @@
 
 namespace ahv {
 
-constexpr int kWinBlocks = 4;
-constexpr uint32_t kWinBytes = kWinBlocks * 64;  // 256
-constexpr int kWinWords = kWinBlocks * 16;       // 64
+// 2 blocks (8 KiB of LDS per wave) keeps LDS from capping occupancy below what
+// the VGPR budget allows (3 waves/SIMD at ≤ 168 VGPRs); each extra pass only
+// re-walks the segment lengths, its bytes outside the window are skipped whole.
+constexpr int kWinBlocks = 2;
+constexpr uint32_t kWinBytes = kWinBlocks * 64;  // 128
+constexpr int kWinWords = kWinBlocks * 16;       // 32
 constexpr int kWaveLanes = 64;
 
 static __shared__ uint32_t g_ring[kWinWords * kWaveLanes];
@@ -38,24 +41,29 @@ struct WaveWindowSink {
   uint32_t lo;   // window start of the current pass
 
   // Does the next `len` bytes overlap the window?  If not, skip them.
-  __device__ bool want(uint32_t len) {
+  __device__ __forceinline__ bool want(uint32_t len) {
     if (pos + len > lo && pos < lo + kWinBytes) return true;
     pos += len;
     return false;
   }
 
-  __device__ void byte(uint8_t b) {
+  __device__ __forceinline__ void byte(uint8_t b) {
     const uint32_t rel = pos - lo;
     if (rel < kWinBytes)
       reinterpret_cast<uint8_t*>(g_ring)[(((rel >> 2) * kWaveLanes + lane) << 2) + (3u - (rel & 3u))] = b;
     ++pos;
   }
 
-  __device__ bool any(bool b) const { return __any(b); }
+  __device__ __forceinline__ bool any(bool b) const { return __any(b); }
+
+  // Make a value opaque to loop-invariant code motion (see emit_delta_payload).
+  __device__ __forceinline__ void launder(uint32_t& x) const { asm volatile("" : "+v"(x)); }
+  __device__ __forceinline__ void launder(int32_t& x) const { asm volatile("" : "+v"(x)); }
+  __device__ __forceinline__ void launder(int64_t& x) const { asm volatile("" : "+v"(x)); }
 
   // Hash the message produced by `emit(*this)`.
   template <class Emit>
-  __device__ void hash(Emit&& emit, uint32_t out[8]) {
+  __device__ __forceinline__ void hash(Emit&& emit, uint32_t out[8]) {
     uint32_t st[8];
     sha256_init(st);
     lo = 0;
@@ -95,16 +103,16 @@ struct WaveWindowSink {
   }
 
   // Merkle digest scratch: slot j (< 8) lives in window words 8j..8j+7.
-  __device__ void stash(int j, const uint32_t d[8]) {
+  __device__ __forceinline__ void stash(int j, const uint32_t d[8]) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) g_ring[(8 * j + k) * kWaveLanes + lane] = d[k];
   }
-  __device__ void load(int j, uint32_t d[8]) const {
+  __device__ __forceinline__ void load(int j, uint32_t d[8]) const {
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = g_ring[(8 * j + k) * kWaveLanes + lane];
   }
   // Merkle interior node; the three compressions share one loop body.
-  __device__ void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const {
+  __device__ __forceinline__ void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const {
     uint32_t st[8];
     sha256_init(st);
 #pragma nounroll
