@@ -1,0 +1,114 @@
+"""Audit kernels: K11/K12 batched SHA-256, K09 segmented Merkle roots, K10
+non-mutating chain verification (reference audit/delta.py, session/sso.py:214,
+saga/checkpoint.py:32-36)."""
+
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+
+from agent_hypervisor_amd.ops._launch import launch
+
+u8, i32, i64 = torch.uint8, torch.int32, torch.int64
+
+
+def pack_bytes(msgs: Sequence[bytes], device="cpu") -> tuple[torch.Tensor, torch.Tensor]:
+    """Byte arena + offsets[n+1] for a list of messages."""
+    offs = [0]
+    for m in msgs:
+        offs.append(offs[-1] + len(m))
+    arena = b"".join(msgs) or b"\0"
+    data = torch.frombuffer(bytearray(arena), dtype=u8).to(device)
+    return data, torch.tensor(offs, dtype=i64, device=device)
+
+
+def digests_to_hex(d: torch.Tensor) -> list[str]:
+    return ["".join(f"{w & 0xFFFFFFFF:08x}" for w in row) for row in d.cpu().tolist()]
+
+
+def hex_to_digests(hexes: Sequence[str], device="cpu") -> torch.Tensor:
+    rows = [[int(h[8 * k : 8 * k + 8], 16) for k in range(8)] for h in hexes]
+    t = torch.tensor(rows, dtype=torch.int64).to(torch.int32) if rows else torch.zeros((0, 8), dtype=i32)
+    return t.to(device)
+
+
+def sha256_many(data: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
+    """SHA-256 of every message [offsets[i], offsets[i+1]) → int32 [n, 8] words."""
+    n = offsets.numel() - 1
+    out = torch.empty((n, 8), dtype=i32, device=data.device)
+    launch("hash_many", {"n": n}, dict(bytes=data, offsets=offsets, digest=out), dict(bytes=u8, offsets=i64))
+    return out
+
+
+def content_hashes(contents: Sequence[str], device="cpu") -> list[str]:
+    """K11: sha256(content.encode()).hexdigest() for many VFS contents."""
+    data, offs = pack_bytes([c.encode() for c in contents], device)
+    return digests_to_hex(sha256_many(data, offs))
+
+
+def goal_hashes(goals: Sequence[str], step_ids: Sequence[str], device="cpu") -> list[str]:
+    """K12: SemanticCheckpoint.compute_goal_hash for many (goal, step) pairs."""
+    data, offs = pack_bytes([f"{g}:{s}".encode() for g, s in zip(goals, step_ids)], device)
+    return [h[:16] for h in digests_to_hex(sha256_many(data, offs))]
+
+
+def merkle_roots(offsets: torch.Tensor, leaves: torch.Tensor) -> torch.Tensor:
+    """K09: Merkle root of each chain of leaf digests (zeros for empty chains)."""
+    chains = offsets.numel() - 1
+    root = torch.empty((chains, 8), dtype=i32, device=leaves.device)
+    scratch = torch.empty_like(leaves)
+    launch(
+        "merkle",
+        {"chains": chains},
+        dict(offsets=offsets, leaves=leaves, scratch=scratch, root=root),
+        dict(offsets=i32, leaves=i32),
+    )
+    return root
+
+
+def verify_chains(
+    data: torch.Tensor,
+    offsets: torch.Tensor,
+    stored: torch.Tensor,
+    parent: torch.Tensor,
+    has_parent: torch.Tensor,
+    chain_offsets: torch.Tensor,
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """K10: per-delta and per-chain integrity of canonical payloads vs stored
+    digests and parent links → (delta_ok u8 [D], chain_ok u8 [C])."""
+    D = offsets.numel() - 1
+    Cn = chain_offsets.numel() - 1
+    dok = torch.empty(D, dtype=u8, device=data.device)
+    cok = torch.empty(Cn, dtype=u8, device=data.device)
+    launch(
+        "verify",
+        {"deltas": D, "chains": Cn},
+        dict(bytes=data, offsets=offsets, stored=stored, parent=parent, has_parent=has_parent,
+             chain_offsets=chain_offsets, delta_ok=dok, chain_ok=cok),
+        dict(bytes=u8, offsets=i64, stored=i32, parent=i32, has_parent=u8, chain_offsets=i32),
+    )
+    return dok, cok
+
+
+def pack_delta_engines(engines, device="cpu"):
+    """Pack DeltaEngine chains for :func:`verify_chains` / :func:`merkle_roots`."""
+    from hypervisor.audit.delta import canonical_payload
+
+    payloads, stored, parent, has_parent, chain_offs = [], [], [], [], [0]
+    for de in engines:
+        for d in de.deltas:
+            payloads.append(canonical_payload(d))
+            stored.append(d.delta_hash if len(d.delta_hash) == 64 else "0" * 64)
+            parent.append(d.parent_hash if d.parent_hash and len(d.parent_hash) == 64 else "0" * 64)
+            has_parent.append(1 if d.parent_hash is not None else 0)
+        chain_offs.append(len(payloads))
+    data, offs = pack_bytes(payloads, device)
+    return (
+        data,
+        offs,
+        hex_to_digests(stored, device),
+        hex_to_digests(parent, device),
+        torch.tensor(has_parent, dtype=u8, device=device),
+        torch.tensor(chain_offs, dtype=i32, device=device),
+    )

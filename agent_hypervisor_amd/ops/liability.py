@@ -1,0 +1,188 @@
+"""Joint-liability kernels K03–K07 (reference liability/vouching.py,
+liability/slashing.py).
+
+A batch describes ``S`` sessions, each with ≤ 16 participants addressed by a
+local index, and its vouch edges in creation order as CSR arrays
+(``offsets[S+1]``, ``voucher``/``vouchee`` local indices, ``bonded`` amounts,
+``active`` flags, ``expiry_us`` (-1 = none)).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from agent_hypervisor_amd.ops._launch import launch
+
+TILE = 16
+f64, u8, i32, i64 = torch.float64, torch.uint8, torch.int32, torch.int64
+
+
+@dataclass
+class VouchBatch:
+    offsets: torch.Tensor  # i32 [S+1]
+    voucher: torch.Tensor  # u8 [E]
+    vouchee: torch.Tensor  # u8 [E]
+    bonded: torch.Tensor  # f64 [E]
+    active: torch.Tensor  # u8 [E]
+    expiry_us: torch.Tensor  # i64 [E]
+    released_us: torch.Tensor  # i64 [E]
+
+    @property
+    def sessions(self) -> int:
+        return self.offsets.numel() - 1
+
+    @property
+    def device(self) -> torch.device:
+        return self.offsets.device
+
+    def to(self, device) -> "VouchBatch":
+        return VouchBatch(*(getattr(self, f).to(device) for f in self.__dataclass_fields__))
+
+    def clone(self) -> "VouchBatch":
+        return VouchBatch(*(getattr(self, f).clone() for f in self.__dataclass_fields__))
+
+    def _csr(self, now_us: int, **extra) -> tuple[dict, dict]:
+        t = dict(offsets=self.offsets, voucher=self.voucher, vouchee=self.vouchee, bonded=self.bonded,
+                 active=self.active, expiry_us=self.expiry_us, released_us=self.released_us)
+        t.update(extra)
+        return {"sessions": self.sessions, "now_us": int(now_us)}, t
+
+
+_CSR_DT = dict(offsets=i32, voucher=u8, vouchee=u8, bonded=f64, active=u8, expiry_us=i64, released_us=i64,
+               tiles=f64, sigma=f64, omega=f64, sigma_eff=f64, released=i32)
+
+
+def build_tiles(vb: VouchBatch, now_us: int) -> torch.Tensor:
+    """Dense [S,16,16] live-bond tiles (row voucher, col vouchee), creation-order sums."""
+    tiles = torch.empty((vb.sessions, TILE, TILE), dtype=f64, device=vb.device)
+    s, t = vb._csr(now_us, tiles=tiles, sigma=None, omega=None, sigma_eff=None, released=None)
+    launch("build_tiles", s, t, _CSR_DT)
+    return tiles
+
+
+def bond_tiles(tiles: torch.Tensor, sigma: torch.Tensor, omega: torch.Tensor):
+    """K03/K04 on fp64 MFMA: (σ_eff [S,16], exposure [S,16], bonded_in [S,16]).
+
+    σ_eff = min(σ + ω·Σ_voucher bonded, 1) per vouchee; exposure = Σ bonded per
+    voucher.  Sums run in tile order (≤ 1-ulp-level differences from the
+    creation-order reference; :func:`sigma_eff_exact` is bit-exact)."""
+    S = tiles.shape[0]
+    out = [torch.empty((S, TILE), dtype=f64, device=tiles.device) for _ in range(3)]
+    launch(
+        "bond_tiles",
+        {"sessions": S},
+        dict(tiles=tiles, sigma=sigma, omega=omega, sigma_eff=out[0], exposure=out[1], bonded_in=out[2]),
+        dict(tiles=f64, sigma=f64, omega=f64),
+    )
+    return tuple(out)
+
+
+def sigma_eff_exact(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us: int) -> torch.Tensor:
+    """K03 creation-order path: bit-identical to VouchingEngine.compute_sigma_eff."""
+    out = torch.empty((vb.sessions, TILE), dtype=f64, device=vb.device)
+    s, t = vb._csr(now_us, tiles=None, sigma=sigma, omega=omega, sigma_eff=out, released=None)
+    launch("sigma_eff_csr", s, t, _CSR_DT)
+    return out
+
+
+def release_bonds(vb: VouchBatch, now_us: int) -> torch.Tensor:
+    """K07: release every active bond of each session (in place); returns counts."""
+    out = torch.empty(vb.sessions, dtype=i32, device=vb.device)
+    s, t = vb._csr(now_us, tiles=None, sigma=None, omega=None, sigma_eff=None, released=out)
+    launch("release_bonds", s, t, _CSR_DT)
+    return out
+
+
+ADMIT_OK, ADMIT_SELF, ADMIT_LOW_SIGMA, ADMIT_CYCLE, ADMIT_EXPOSURE = range(5)
+
+
+def vouch_admit(
+    vb: VouchBatch,
+    r_offsets: torch.Tensor,
+    r_voucher: torch.Tensor,
+    r_vouchee: torch.Tensor,
+    r_sigma: torch.Tensor,
+    r_pct: torch.Tensor,
+    now_us: int,
+    max_exposure: float = 0.80,
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """K05: admit vouch requests per session in order → (code u8, bonded f64)."""
+    n = r_voucher.numel()
+    code = torch.empty(n, dtype=u8, device=vb.device)
+    bonded = torch.empty(n, dtype=f64, device=vb.device)
+    launch(
+        "vouch_admit",
+        {"sessions": vb.sessions, "now_us": int(now_us), "max_exposure": float(max_exposure)},
+        dict(e_offsets=vb.offsets, e_voucher=vb.voucher, e_vouchee=vb.vouchee, e_bonded=vb.bonded,
+             e_active=vb.active, e_expiry=vb.expiry_us, r_offsets=r_offsets, r_voucher=r_voucher,
+             r_vouchee=r_vouchee, r_sigma=r_sigma, r_pct=r_pct, r_bonded=bonded, code=code),
+        dict(e_offsets=i32, e_voucher=u8, e_vouchee=u8, e_bonded=f64, e_active=u8, e_expiry=i64,
+             r_offsets=i32, r_voucher=u8, r_vouchee=u8, r_sigma=f64, r_pct=f64),
+    )
+    return code, bonded
+
+
+@dataclass
+class SlashOutcome:
+    scores: torch.Tensor  # f64 [S,16] (NaN = absent)
+    clip_count: torch.Tensor  # i32 [S]
+    clip_voucher: torch.Tensor  # u8 [S, cap]
+    clip_depth: torch.Tensor  # u8 [S, cap]
+    clip_before: torch.Tensor  # f64 [S, cap]
+    clip_after: torch.Tensor  # f64 [S, cap]
+
+
+def slash(
+    vb: VouchBatch,
+    target: torch.Tensor,
+    omega: torch.Tensor,
+    scores: torch.Tensor,
+    now_us: int,
+    clip_cap: int = 64,
+) -> SlashOutcome:
+    """K06: slash ``target[s]`` in every session (cascade ≤ 2), mutating ``vb``
+    (bonds released) and ``scores`` in place, like SlashingEngine.slash."""
+    S = vb.sessions
+    dev = vb.device
+    offs = (torch.arange(S, dtype=i32, device=dev) * clip_cap).contiguous()
+    out = SlashOutcome(
+        scores=scores,
+        clip_count=torch.zeros(S, dtype=i32, device=dev),
+        clip_voucher=torch.zeros((S, clip_cap), dtype=u8, device=dev),
+        clip_depth=torch.zeros((S, clip_cap), dtype=u8, device=dev),
+        clip_before=torch.zeros((S, clip_cap), dtype=f64, device=dev),
+        clip_after=torch.zeros((S, clip_cap), dtype=f64, device=dev),
+    )
+    launch(
+        "slash",
+        {"sessions": S, "now_us": int(now_us), "clip_cap": int(clip_cap)},
+        dict(offsets=vb.offsets, voucher=vb.voucher, vouchee=vb.vouchee, active=vb.active,
+             expiry_us=vb.expiry_us, released_us=vb.released_us, target=target, omega=omega, scores=scores,
+             clip_offsets=offs, clip_count=out.clip_count, clip_voucher=out.clip_voucher,
+             clip_depth=out.clip_depth, clip_before=out.clip_before, clip_after=out.clip_after),
+        dict(target=u8, omega=f64, scores=f64),
+    )
+    return out
+
+
+def from_engine(engine, sessions: list[str], participants: list[list[str]], device="cpu") -> VouchBatch:
+    """Pack a :class:`hypervisor.liability.vouching.VouchingEngine`'s edges of the
+    given sessions (with each session's participant order) into a VouchBatch."""
+    offsets, vr, ve, bd, ac, ex, rel = [0], [], [], [], [], [], []
+    from hypervisor._clock import to_us
+
+    for sid, parts in zip(sessions, participants):
+        idx = {d: k for k, d in enumerate(parts)}
+        for v in engine._by_session.get(sid, []):
+            vr.append(idx[v.voucher_did])
+            ve.append(idx[v.vouchee_did])
+            bd.append(v.bonded_amount)
+            ac.append(1 if v.is_active else 0)
+            ex.append(to_us(v.expiry) if v.expiry is not None else -1)
+            rel.append(to_us(v.released_at) if v.released_at is not None else 0)
+        offsets.append(len(vr))
+    mk = lambda xs, dt: torch.tensor(xs, dtype=dt, device=device)  # noqa: E731
+    return VouchBatch(mk(offsets, i32), mk(vr, u8), mk(ve, u8), mk(bd, f64), mk(ac, u8), mk(ex, i64), mk(rel, i64))

@@ -1,0 +1,176 @@
+// Batched audit kernels: many-message SHA-256 (K11 content
+// hashes, K12 goal hashes), segmented Merkle roots (K09) and non-mutating chain
+// verification (K10) over canonical payloads stored in a byte arena.
+//
+// The standalone hash kernel reads each lane's message straight from global
+// memory (aligned 16-byte loads with byte funnel-shifting for unaligned starts);
+// the fused pipeline kernel (pipeline.hip) instead renders its payloads in LDS.
+#include "ahv/delta_emit.h"
+#include "ahv/kernels.h"
+#include "ahv/launch.h"
+#include "ahv/sha256.h"
+
+namespace ahv {
+
+namespace {
+constexpr int kBlock = 256;
+inline dim3 grid1(int64_t n, int per_block = kBlock) {
+  const int64_t b = (n + per_block - 1) / per_block;
+  return dim3(static_cast<uint32_t>(b > 0 ? b : 1));
+}
+
+// Byte i of the message as a big-endian-ready value (bounds-checked).
+AHV_HD uint32_t msg_byte(const uint8_t* p, int64_t len, int64_t i) { return i < len ? p[i] : 0u; }
+
+// SHA-256 of bytes [p, p+len) with standard padding; block words gathered from
+// 4-byte loads where the message is aligned.
+AHV_HD void sha256_span(const uint8_t* p, int64_t len, uint32_t out[8]) {
+  sha256_init(out);
+  const int64_t total = ((len + 8) / 64 + 1) * 64;
+  const uint64_t bits = static_cast<uint64_t>(len) * 8u;
+  for (int64_t b = 0; b < total; b += 64) {
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int64_t i = b + 4 * k;
+      uint32_t v;
+      if (i + 4 <= len && ((reinterpret_cast<uintptr_t>(p + i) & 3) == 0)) {
+        v = bswap32(*reinterpret_cast<const uint32_t*>(p + i));
+      } else {
+        v = 0;
+        for (int j = 0; j < 4; ++j) {
+          const int64_t x = i + j;
+          uint32_t byte;
+          if (x < len) byte = p[x];
+          else if (x == len) byte = 0x80;
+          else if (x >= total - 8) byte = static_cast<uint32_t>((bits >> (8 * (total - 1 - x))) & 0xff);
+          else byte = 0;
+          v = (v << 8) | byte;
+        }
+      }
+      w[k] = v;
+    }
+    sha256_compress(out, w);
+  }
+}
+}  // namespace
+
+// ------------------------------------------------------------ K11 / K12
+
+AHV_HD void hash_many_elem(const HashManyArgs& a, int64_t i) {
+  const int64_t o = a.offsets[i];
+  sha256_span(a.bytes + o, a.offsets[i + 1] - o, a.digest + i * 8);
+}
+__global__ void hash_many_kernel(HashManyArgs a) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    hash_many_elem(a, i);
+}
+void launch_hash_many(const HashManyArgs& a, hipStream_t st) {
+  if (a.n <= 0) return;
+  hipLaunchKernelGGL(hash_many_kernel, grid1(a.n, 64), dim3(64), 0, st, a);
+  check_hip(hipGetLastError(), "hash_many_kernel");
+}
+void hash_many_host(const HashManyArgs& a) { for (int64_t i = 0; i < a.n; ++i) hash_many_elem(a, i); }
+
+// ------------------------------------------------------------------ K09
+// One lane per chain: binary-counter Merkle (delta_emit.h merkle_root_counter)
+// with its ≤ log2(n)+1 partial subtrees parked in the chain's rows of `scratch`.
+
+struct GlobalStash {
+  uint32_t* rows;  // this chain's scratch rows
+  AHV_HD void stash(int j, const uint32_t d[8]) {
+    for (int k = 0; k < 8; ++k) rows[j * 8 + k] = d[k];
+  }
+  AHV_HD void load(int j, uint32_t d[8]) const {
+    for (int k = 0; k < 8; ++k) d[k] = rows[j * 8 + k];
+  }
+  AHV_HD void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const {
+    uint32_t t[8];
+    merkle_node(l, r, t);
+    for (int k = 0; k < 8; ++k) out[k] = t[k];
+  }
+};
+
+AHV_HD void merkle_elem(const MerkleArgs& a, int64_t c) {
+  const int32_t b = a.offsets[c], e = a.offsets[c + 1];
+  uint32_t* root = a.root + c * 8;
+  if (e <= b) {
+    for (int k = 0; k < 8; ++k) root[k] = 0;
+    return;
+  }
+  GlobalStash gs{a.scratch + static_cast<int64_t>(b) * 8};
+  uint32_t r[8];
+  merkle_root_counter(
+      gs, static_cast<uint32_t>(e - b),
+      [&](uint32_t i, uint32_t h[8]) {
+        for (int k = 0; k < 8; ++k) h[k] = a.leaves[(static_cast<int64_t>(b) + i) * 8 + k];
+      },
+      r);
+  for (int k = 0; k < 8; ++k) root[k] = r[k];
+}
+__global__ void merkle_kernel(MerkleArgs a) {
+  for (int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; c < a.chains;
+       c += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    merkle_elem(a, c);
+}
+void launch_merkle(const MerkleArgs& a, hipStream_t st) {
+  if (a.chains <= 0) return;
+  hipLaunchKernelGGL(merkle_kernel, grid1(a.chains, 64), dim3(64), 0, st, a);
+  check_hip(hipGetLastError(), "merkle_kernel");
+}
+void merkle_host(const MerkleArgs& a) { for (int64_t c = 0; c < a.chains; ++c) merkle_elem(a, c); }
+
+// ------------------------------------------------------------------ K10
+// Embarrassingly parallel over deltas (one lane recomputes one digest), then a
+// per-chain AND that also checks every parent link against the predecessor's
+// stored digest.  Nothing is written back to the stored digests (fix of the
+// reference's self-"repairing" verify_chain).
+
+AHV_HD void verify_delta_elem(const VerifyArgs& a, int64_t i) {
+  uint32_t h[8];
+  const int64_t o = a.offsets[i];
+  sha256_span(a.bytes + o, a.offsets[i + 1] - o, h);
+  bool ok = true;
+  for (int k = 0; k < 8; ++k) ok = ok && h[k] == a.stored[i * 8 + k];
+  a.delta_ok[i] = ok ? 1 : 0;
+}
+AHV_HD void verify_chain_elem(const VerifyArgs& a, int64_t c) {
+  bool ok = true;
+  for (int32_t i = a.chain_offsets[c]; i < a.chain_offsets[c + 1]; ++i) {
+    ok = ok && a.delta_ok[i];
+    if (i == a.chain_offsets[c]) {
+      ok = ok && !a.has_parent[i];
+    } else {
+      ok = ok && a.has_parent[i];
+      for (int k = 0; k < 8; ++k) ok = ok && a.parent[static_cast<int64_t>(i) * 8 + k] == a.stored[static_cast<int64_t>(i - 1) * 8 + k];
+    }
+  }
+  a.chain_ok[c] = ok ? 1 : 0;
+}
+__global__ void verify_delta_kernel(VerifyArgs a) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.deltas;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    verify_delta_elem(a, i);
+}
+__global__ void verify_chain_kernel(VerifyArgs a) {
+  for (int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; c < a.chains;
+       c += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    verify_chain_elem(a, c);
+}
+void launch_verify(const VerifyArgs& a, hipStream_t st) {
+  if (a.deltas > 0) {
+    hipLaunchKernelGGL(verify_delta_kernel, grid1(a.deltas, 64), dim3(64), 0, st, a);
+    check_hip(hipGetLastError(), "verify_delta_kernel");
+  }
+  if (a.chains > 0) {
+    hipLaunchKernelGGL(verify_chain_kernel, grid1(a.chains), dim3(kBlock), 0, st, a);
+    check_hip(hipGetLastError(), "verify_chain_kernel");
+  }
+}
+void verify_host(const VerifyArgs& a) {
+  for (int64_t i = 0; i < a.deltas; ++i) verify_delta_elem(a, i);
+  for (int64_t c = 0; c < a.chains; ++c) verify_chain_elem(a, c);
+}
+
+}  // namespace ahv

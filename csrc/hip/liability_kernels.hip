@@ -1,0 +1,315 @@
+// Batched joint-liability kernels (SURVEY §2.14 K03–K07).
+//
+// Representation: a session's participants have local indices 0..15 (the
+// reference's max_participants default is 10; rows are padded to 16), its vouch
+// edges live in creation order in a CSR edge list, and for scoring the live
+// bonds are summed into a dense 16×16 fp64 tile (row = voucher, col = vouchee).
+//
+// K03/K04 on MFMA: with a wave per session tile, the column sums (Σ bonded for
+// each vouchee → σ_eff) and row sums (exposure of each voucher) are two chains of
+// four v_mfma_f64_16x16x4_f64 against an all-ones operand.  fp64 MFMA sums the
+// 16 terms in tile order; the reference sums in vouch-creation order, so the MFMA
+// path agrees to within an ulp-level tolerance while `sigma_eff_csr` (one lane
+// per vouchee, creation order) is the bit-exact path.
+#include "ahv/kernels.h"
+#include "ahv/launch.h"
+#include "ahv/semantics.h"
+
+namespace ahv {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int kBlock = 256;
+inline dim3 grid1(int64_t n, int per_block = kBlock) {
+  const int64_t b = (n + per_block - 1) / per_block;
+  return dim3(static_cast<uint32_t>(b > 0 ? b : 1));
+}
+AHV_HD bool live_edge(const uint8_t* active, const int64_t* expiry, int64_t e, int64_t now) {
+  return active[e] && (expiry == nullptr || expiry[e] < 0 || now <= expiry[e]);
+}
+}  // namespace
+
+// ------------------------------------------------------------ K03/K04 MFMA
+
+__global__ __launch_bounds__(64) void bond_tiles_mfma_kernel(BondTileArgs a) {
+  const int64_t s = blockIdx.x;
+  if (s >= a.sessions) return;
+  const int l = threadIdx.x;
+  const int r = l >> 4, c = l & 15;
+  const double* T = a.tiles + s * kTile * kTile;
+  f64x4 col = {0.0, 0.0, 0.0, 0.0};
+  f64x4 row = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    // B operand (k = voucher 4t+r, j = vouchee c): Σ_k 1·T[k][j] → column sums
+    const double b = T[(4 * t + r) * kTile + c];
+    col = __builtin_amdgcn_mfma_f64_16x16x4f64(1.0, b, col, 0, 0, 0);
+    // A operand (i = voucher c, k = vouchee 4t+r): Σ_k T[i][k]·1 → row sums
+    const double av = T[c * kTile + 4 * t + r];
+    row = __builtin_amdgcn_mfma_f64_16x16x4f64(av, 1.0, row, 0, 0, 0);
+  }
+  // D layout: col = lane&15, row = (lane>>4) + 4*reg.  Every row of `col` holds the
+  // column sums; lanes 0..15 (reg 0) write them.  Column 0 of `row` holds every
+  // row sum: lanes 0,16,32,48 write rows r + 4*reg.
+  if (r == 0) {
+    const double bonded = col[0];
+    a.bonded_in[s * kTile + c] = bonded;
+    a.sigma_eff[s * kTile + c] = sigma_eff_combine(a.sigma[s * kTile + c], a.omega[s], bonded);
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a.exposure[s * kTile + r + 4 * q] = row[q];
+  }
+}
+
+void launch_bond_tiles(const BondTileArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  hipLaunchKernelGGL(bond_tiles_mfma_kernel, dim3(static_cast<uint32_t>(a.sessions)), dim3(64), 0, st, a);
+  check_hip(hipGetLastError(), "bond_tiles_mfma_kernel");
+}
+
+void bond_tiles_host(const BondTileArgs& a) {
+  for (int64_t s = 0; s < a.sessions; ++s) {
+    const double* T = a.tiles + s * kTile * kTile;
+    for (int j = 0; j < kTile; ++j) {
+      double cs = 0.0, rs = 0.0;
+      for (int k = 0; k < kTile; ++k) {
+        cs += T[k * kTile + j];
+        rs += T[j * kTile + k];
+      }
+      a.bonded_in[s * kTile + j] = cs;
+      a.sigma_eff[s * kTile + j] = sigma_eff_combine(a.sigma[s * kTile + j], a.omega[s], cs);
+      a.exposure[s * kTile + j] = rs;
+    }
+  }
+}
+
+// ------------------------------------------------------ tile build (CSR → dense)
+// One wave per session; lane j owns tile entries j, j+64, j+128, j+192 and sums
+// the matching live edges in creation order (deterministic).
+
+AHV_HD void build_tile_entry(const VouchCsrArgs& a, int64_t s, int idx) {
+  const int v = idx / kTile, e = idx % kTile;
+  double acc = 0.0;
+  for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
+    if (a.voucher[k] == v && a.vouchee[k] == e && live_edge(a.active, a.expiry_us, k, a.now_us)) acc += a.bonded[k];
+  a.tiles[s * kTile * kTile + idx] = acc;
+}
+
+__global__ __launch_bounds__(64) void build_tiles_kernel(VouchCsrArgs a) {
+  const int64_t s = blockIdx.x;
+  if (s >= a.sessions) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) build_tile_entry(a, s, threadIdx.x + 64 * q);
+}
+void launch_build_tiles(const VouchCsrArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  hipLaunchKernelGGL(build_tiles_kernel, dim3(static_cast<uint32_t>(a.sessions)), dim3(64), 0, st, a);
+  check_hip(hipGetLastError(), "build_tiles_kernel");
+}
+void build_tiles_host(const VouchCsrArgs& a) {
+  for (int64_t s = 0; s < a.sessions; ++s)
+    for (int idx = 0; idx < kTile * kTile; ++idx) build_tile_entry(a, s, idx);
+}
+
+// --------------------------------------------------- K03 exact (creation order)
+
+AHV_HD void sigma_eff_csr_elem(const VouchCsrArgs& a, int64_t i) {
+  const int64_t s = i / kTile;
+  const int e = static_cast<int>(i % kTile);
+  double contrib = 0.0;
+  for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
+    if (a.vouchee[k] == e && live_edge(a.active, a.expiry_us, k, a.now_us)) contrib += a.bonded[k];
+  a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[s], contrib);
+}
+__global__ void sigma_eff_csr_kernel(VouchCsrArgs a) {
+  const int64_t n = a.sessions * kTile;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    sigma_eff_csr_elem(a, i);
+}
+void launch_sigma_eff_csr(const VouchCsrArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  hipLaunchKernelGGL(sigma_eff_csr_kernel, grid1(a.sessions * kTile), dim3(kBlock), 0, st, a);
+  check_hip(hipGetLastError(), "sigma_eff_csr_kernel");
+}
+void sigma_eff_csr_host(const VouchCsrArgs& a) {
+  for (int64_t i = 0; i < a.sessions * kTile; ++i) sigma_eff_csr_elem(a, i);
+}
+
+// ------------------------------------------------------------------ K07
+
+AHV_HD void release_elem(const VouchCsrArgs& a, int64_t s) {
+  int32_t n = 0;
+  for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k) {
+    if (a.active[k]) {
+      a.active[k] = 0;
+      a.released_us[k] = a.now_us;
+      ++n;
+    }
+  }
+  a.released[s] = n;
+}
+__global__ void release_kernel(VouchCsrArgs a) {
+  for (int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; s < a.sessions;
+       s += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    release_elem(a, s);
+}
+void launch_release(const VouchCsrArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  hipLaunchKernelGGL(release_kernel, grid1(a.sessions), dim3(kBlock), 0, st, a);
+  check_hip(hipGetLastError(), "release_kernel");
+}
+void release_host(const VouchCsrArgs& a) { for (int64_t s = 0; s < a.sessions; ++s) release_elem(a, s); }
+
+// ------------------------------------------------------------------ K05
+// Requests of a session are admitted in order; admitted ones become live edges
+// for the following requests.  Live adjacency as a 16×16 bit matrix held in four
+// 64-bit words (row v occupies bits 16·(v mod 4) … of word v/4).
+
+AHV_HD uint32_t adj_row(const uint64_t w[4], int v) {
+  const uint64_t x = (v >> 2) == 0 ? w[0] : (v >> 2) == 1 ? w[1] : (v >> 2) == 2 ? w[2] : w[3];
+  return static_cast<uint32_t>((x >> (16 * (v & 3))) & 0xffffu);
+}
+AHV_HD void adj_set(uint64_t w[4], int v, int e) {
+  const uint64_t bit = 1ull << (16 * (v & 3) + e);
+  if ((v >> 2) == 0) w[0] |= bit;
+  else if ((v >> 2) == 1) w[1] |= bit;
+  else if ((v >> 2) == 2) w[2] |= bit;
+  else w[3] |= bit;
+}
+
+AHV_HD void vouch_admit_session(const VouchAdmitArgs& a, int64_t s) {
+  uint64_t adj[4] = {0, 0, 0, 0};
+  for (int32_t k = a.e_offsets[s]; k < a.e_offsets[s + 1]; ++k)
+    if (live_edge(a.e_active, a.e_expiry, k, a.now_us)) adj_set(adj, a.e_voucher[k], a.e_vouchee[k]);
+  for (int32_t q = a.r_offsets[s]; q < a.r_offsets[s + 1]; ++q) {
+    const int v = a.r_voucher[q], e = a.r_vouchee[q];
+    const double sig = a.r_sigma[q];
+    uint8_t code = 0;
+    double bonded = 0.0;
+    if (v == e) {
+      code = 1;
+    } else if (sig < kMinVoucherSigma) {
+      code = 2;
+    } else {
+      // cycle: voucher reachable from vouchee through live edges
+      uint32_t reach = adj_row(adj, e), seen = 0;
+      while (reach & ~seen) {
+        const uint32_t fresh = reach & ~seen;
+        seen |= fresh;
+        for (int u = 0; u < kTile; ++u)
+          if ((fresh >> u) & 1u) reach |= adj_row(adj, u);
+      }
+      if ((reach >> v) & 1u) {
+        code = 3;
+      } else {
+        double pct = a.r_pct[q];
+        pct = pct < 0.0 ? 0.0 : (pct > 1.0 ? 1.0 : pct);
+        bonded = sig * pct;
+        double cur = 0.0;  // exposure in creation order: existing live edges, then admitted requests
+        for (int32_t k = a.e_offsets[s]; k < a.e_offsets[s + 1]; ++k)
+          if (a.e_voucher[k] == v && live_edge(a.e_active, a.e_expiry, k, a.now_us)) cur += a.e_bonded[k];
+        for (int32_t p = a.r_offsets[s]; p < q; ++p)
+          if (a.code[p] == 0 && a.r_voucher[p] == v) cur += a.r_bonded[p];
+        if (cur + bonded > sig * a.max_exposure) code = 4;
+      }
+    }
+    a.code[q] = code;
+    a.r_bonded[q] = code == 0 ? bonded : 0.0;
+    if (code == 0) adj_set(adj, v, e);
+  }
+}
+__global__ void vouch_admit_kernel(VouchAdmitArgs a) {
+  for (int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; s < a.sessions;
+       s += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    vouch_admit_session(a, s);
+}
+void launch_vouch_admit(const VouchAdmitArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  hipLaunchKernelGGL(vouch_admit_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
+  check_hip(hipGetLastError(), "vouch_admit_kernel");
+}
+void vouch_admit_host(const VouchAdmitArgs& a) { for (int64_t s = 0; s < a.sessions; ++s) vouch_admit_session(a, s); }
+
+// ------------------------------------------------------------------ K06
+// Depth-first cascade exactly as SlashingEngine.slash recurses: clip every live
+// voucher of the current vouchee in creation order (releasing the bond), then
+// descend into clipped vouchers left below floor+0.01 that still have live
+// vouchers, up to depth 2.  Clip records are written in reference history order
+// of the *clips* (parent clips before the child slash's clips).
+
+AHV_HD double score_of(const double* sc, int v) {
+  const double x = sc[v];
+  return x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
+}
+
+AHV_HD bool has_live_voucher(const SlashArgs& a, int64_t s, int who) {
+  for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
+    if (a.vouchee[k] == who && live_edge(a.active, a.expiry_us, k, a.now_us)) return true;
+  return false;
+}
+
+AHV_HD void slash_session(const SlashArgs& a, int64_t s) {
+  double* sc = a.scores + s * kTile;
+  const double omega = a.omega[s];
+  const int32_t base = a.clip_offsets[s];
+  int32_t nclip = 0;
+  // explicit stack of (vouchee, depth, first clip, next clip to examine)
+  int st_who[kMaxCascadeDepth + 1], st_first[kMaxCascadeDepth + 1], st_next[kMaxCascadeDepth + 1],
+      st_end[kMaxCascadeDepth + 1];
+  int sp = 0;
+  auto do_slash = [&](int who, int depth) {
+    sc[who] = 0.0;
+    const int32_t first = nclip;
+    for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k) {
+      if (a.vouchee[k] != who || !live_edge(a.active, a.expiry_us, k, a.now_us)) continue;
+      const int v = a.voucher[k];
+      const double before = score_of(sc, v);
+      const double after = clip_sigma(before, omega);
+      sc[v] = after;
+      if (nclip < a.clip_cap) {
+        a.clip_voucher[base + nclip] = static_cast<uint8_t>(v);
+        a.clip_depth[base + nclip] = static_cast<uint8_t>(depth);
+        a.clip_before[base + nclip] = before;
+        a.clip_after[base + nclip] = after;
+      }
+      ++nclip;
+      a.active[k] = 0;
+      a.released_us[k] = a.now_us;
+    }
+    st_who[sp] = who;
+    st_first[sp] = first;
+    st_next[sp] = first;
+    st_end[sp] = nclip;
+    ++sp;
+  };
+  do_slash(a.target[s], 0);
+  while (sp > 0) {
+    const int top = sp - 1;
+    const int depth = top;
+    if (depth >= kMaxCascadeDepth || st_next[top] >= st_end[top]) {
+      --sp;
+      continue;
+    }
+    const int32_t ci = st_next[top]++;
+    if (ci >= a.clip_cap) continue;
+    const int v = a.clip_voucher[base + ci];
+    if (a.clip_after[base + ci] < kCascadeBelow && has_live_voucher(a, s, v)) do_slash(v, depth + 1);
+  }
+  a.clip_count[s] = nclip;
+}
+__global__ void slash_kernel(SlashArgs a) {
+  for (int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; s < a.sessions;
+       s += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    slash_session(a, s);
+}
+void launch_slash(const SlashArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
+  check_hip(hipGetLastError(), "slash_kernel");
+}
+void slash_host(const SlashArgs& a) { for (int64_t s = 0; s < a.sessions; ++s) slash_session(a, s); }
+
+}  // namespace ahv

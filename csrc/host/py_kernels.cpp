@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "ahv/kernels.h"
 #include "ahv/launch.h"
 #include "ahv/pipeline.h"
 
@@ -89,7 +90,186 @@ static PipelineArgs pipeline_args(const py::dict& d) {
   return a;
 }
 
+// ---------------------------------------------------------------------------
+// Generic binding: every kernel gets `<name>(args: dict, stream: int)` (device)
+// and `<name>_host(args: dict)` (CPU twin).  Field readers below map dict keys
+// to struct members by name.
+
+#define P(field, T) a.field = ptr<T>(d, #field)
+#define V(field, T) a.field = val<T>(d, #field)
+
+static RingGateArgs to_ring_gate(const py::dict& d) {
+  RingGateArgs a{};
+  V(n, int64_t); P(sigma, const double); P(consensus, const uint8_t); P(ring, uint8_t);
+  return a;
+}
+static RingCheckArgs to_ring_check(const py::dict& d) {
+  RingCheckArgs a{};
+  V(n, int64_t); P(agent_ring, const uint8_t); P(action_flags, const uint8_t); P(sigma, const double);
+  P(consensus, const uint8_t); P(witness, const uint8_t); P(required, uint8_t); P(reason, uint8_t);
+  return a;
+}
+static FsmArgs to_fsm(const py::dict& d) {
+  FsmArgs a{};
+  V(n, int64_t); V(kind, int32_t); V(now_us, int64_t); P(state, uint8_t); P(target, const uint8_t);
+  P(ok, uint8_t); P(started_us, int64_t); P(completed_us, int64_t);
+  return a;
+}
+static FanoutArgs to_fanout(const py::dict& d) {
+  FanoutArgs a{};
+  V(groups, int64_t); P(offsets, const int32_t); P(policy, const uint8_t); P(succeeded, const uint8_t);
+  P(satisfied, uint8_t); P(success_count, int32_t); P(compensate, uint8_t);
+  return a;
+}
+static BreachArgs to_breach(const py::dict& d) {
+  BreachArgs a{};
+  V(n, int64_t); V(window_cap, int32_t); V(window_us, int64_t); V(cooldown_us, int64_t);
+  P(now_us, const int64_t); P(agent_ring, const uint8_t); P(new_called, const uint8_t); P(ts, int64_t);
+  P(called, uint8_t); P(head, int32_t); P(count, int32_t); P(total, int64_t); P(tripped, uint8_t);
+  P(tripped_at_us, int64_t); P(severity, uint8_t); P(rate, double); P(hits, int32_t); P(event, uint8_t);
+  return a;
+}
+static BucketArgs to_bucket(const py::dict& d) {
+  BucketArgs a{};
+  V(n, int64_t); V(now_us, int64_t); P(tokens, double); P(last_us, int64_t); P(capacity, const double);
+  P(rate, const double); P(cost, const double); P(ok, uint8_t);
+  return a;
+}
+static ExpiryArgs to_expiry(const py::dict& d) {
+  ExpiryArgs a{};
+  V(n, int64_t); V(now_us, int64_t); P(active, uint8_t); P(expires_us, const int64_t);
+  P(released_us, int64_t); P(expired, uint8_t);
+  return a;
+}
+static LedgerArgs to_ledger(const py::dict& d) {
+  LedgerArgs a{};
+  V(agents, int64_t); P(offsets, const int32_t); P(type, const uint8_t); P(severity, const double);
+  P(raw_risk, double); P(risk, double); P(recommendation, uint8_t); P(slash_count, int32_t);
+  P(quarantine_count, int32_t); P(clean_count, int32_t); P(fault_avg, double);
+  return a;
+}
+static DriftArgs to_drift(const py::dict& d) {
+  DriftArgs a{};
+  V(n, int64_t); V(low, double); V(medium, double); V(high, double); V(critical, double);
+  P(drift, const double); P(severity, uint8_t);
+  return a;
+}
+static AttributionArgs to_attribution(const py::dict& d) {
+  AttributionArgs a{};
+  V(cases, int64_t); P(node_offsets, const int32_t); P(agent_offsets, const int32_t);
+  P(agent_of_node, const int32_t); P(success, const uint8_t); P(root_cause, const uint8_t);
+  P(risk_weight, const double); P(raw, double); P(node_count, int32_t);
+  return a;
+}
+static BondTileArgs to_bond_tiles(const py::dict& d) {
+  BondTileArgs a{};
+  V(sessions, int64_t); P(tiles, const double); P(sigma, const double); P(omega, const double);
+  P(sigma_eff, double); P(exposure, double); P(bonded_in, double);
+  return a;
+}
+static VouchCsrArgs to_vouch_csr(const py::dict& d) {
+  VouchCsrArgs a{};
+  V(sessions, int64_t); V(now_us, int64_t); P(offsets, const int32_t); P(voucher, const uint8_t);
+  P(vouchee, const uint8_t); P(bonded, const double); P(active, uint8_t); P(expiry_us, const int64_t);
+  P(released_us, int64_t); P(tiles, double); P(sigma, const double); P(omega, const double);
+  P(sigma_eff, double); P(released, int32_t);
+  return a;
+}
+static VouchAdmitArgs to_vouch_admit(const py::dict& d) {
+  VouchAdmitArgs a{};
+  V(sessions, int64_t); V(now_us, int64_t); V(max_exposure, double); P(e_offsets, const int32_t);
+  P(e_voucher, const uint8_t); P(e_vouchee, const uint8_t); P(e_bonded, const double);
+  P(e_active, const uint8_t); P(e_expiry, const int64_t); P(r_offsets, const int32_t);
+  P(r_voucher, const uint8_t); P(r_vouchee, const uint8_t); P(r_sigma, const double); P(r_pct, const double);
+  P(r_bonded, double); P(code, uint8_t);
+  return a;
+}
+static SlashArgs to_slash(const py::dict& d) {
+  SlashArgs a{};
+  V(sessions, int64_t); V(now_us, int64_t); P(offsets, const int32_t); P(voucher, const uint8_t);
+  P(vouchee, const uint8_t); P(active, uint8_t); P(expiry_us, const int64_t); P(released_us, int64_t);
+  P(target, const uint8_t); P(omega, const double); P(scores, double); P(clip_offsets, int32_t);
+  P(clip_count, int32_t); P(clip_voucher, uint8_t); P(clip_depth, uint8_t); P(clip_before, double);
+  P(clip_after, double); V(clip_cap, int32_t);
+  return a;
+}
+static HashManyArgs to_hash_many(const py::dict& d) {
+  HashManyArgs a{};
+  V(n, int64_t); P(bytes, const uint8_t); P(offsets, const int64_t); P(digest, uint32_t);
+  return a;
+}
+static MerkleArgs to_merkle(const py::dict& d) {
+  MerkleArgs a{};
+  V(chains, int64_t); P(offsets, const int32_t); P(leaves, const uint32_t); P(scratch, uint32_t);
+  P(root, uint32_t);
+  return a;
+}
+static VerifyArgs to_verify(const py::dict& d) {
+  VerifyArgs a{};
+  V(deltas, int64_t); V(chains, int64_t); P(bytes, const uint8_t); P(offsets, const int64_t);
+  P(stored, const uint32_t); P(parent, const uint32_t); P(has_parent, const uint8_t);
+  P(chain_offsets, const int32_t); P(delta_ok, uint8_t); P(chain_ok, uint8_t);
+  return a;
+}
+static VClockArgs to_vclock(const py::dict& d) {
+  VClockArgs a{};
+  V(groups, int64_t); V(A, int32_t); V(strict, int32_t); P(offsets, const int32_t); P(op, const uint8_t);
+  P(path, const int32_t); P(agent, const int32_t); P(agent_col, const int32_t); P(path_clock, uint32_t);
+  P(agent_clock, uint32_t); P(ok, uint8_t);
+  return a;
+}
+static LockArgs to_locks(const py::dict& d) {
+  LockArgs a{};
+  V(n, int64_t); P(res_offsets, const int32_t); P(lock_agent, const int32_t); P(lock_intent, const uint8_t);
+  P(req_res, const int32_t); P(req_agent, const int32_t); P(req_intent, const uint8_t); P(conflicts, int32_t);
+  return a;
+}
+#undef P
+#undef V
+
+template <class A>
+static void bind_pair(py::module_& m, const char* name, A (*conv)(const py::dict&),
+                      void (*dev)(const A&, hipStream_t), void (*host)(const A&)) {
+  m.def(
+      name,
+      [conv, dev](const py::dict& d, uintptr_t stream) {
+        A a = conv(d);
+        py::gil_scoped_release nogil;
+        dev(a, reinterpret_cast<hipStream_t>(stream));
+      },
+      py::arg("args"), py::arg("stream"));
+  m.def(
+      (std::string(name) + "_host").c_str(),
+      [conv, host](const py::dict& d) {
+        A a = conv(d);
+        py::gil_scoped_release nogil;
+        host(a);
+      },
+      py::arg("args"));
+}
+
 void register_kernels(py::module_& m) {
+  bind_pair(m, "ring_gate", to_ring_gate, launch_ring_gate, ring_gate_host);
+  bind_pair(m, "ring_check", to_ring_check, launch_ring_check, ring_check_host);
+  bind_pair(m, "fsm", to_fsm, launch_fsm, fsm_host);
+  bind_pair(m, "fanout", to_fanout, launch_fanout, fanout_host);
+  bind_pair(m, "breach", to_breach, launch_breach, breach_host);
+  bind_pair(m, "bucket", to_bucket, launch_bucket, bucket_host);
+  bind_pair(m, "expiry", to_expiry, launch_expiry, expiry_host);
+  bind_pair(m, "ledger", to_ledger, launch_ledger, ledger_host);
+  bind_pair(m, "drift", to_drift, launch_drift, drift_host);
+  bind_pair(m, "attribution", to_attribution, launch_attribution, attribution_host);
+  bind_pair(m, "bond_tiles", to_bond_tiles, launch_bond_tiles, bond_tiles_host);
+  bind_pair(m, "build_tiles", to_vouch_csr, launch_build_tiles, build_tiles_host);
+  bind_pair(m, "sigma_eff_csr", to_vouch_csr, launch_sigma_eff_csr, sigma_eff_csr_host);
+  bind_pair(m, "release_bonds", to_vouch_csr, launch_release, release_host);
+  bind_pair(m, "vouch_admit", to_vouch_admit, launch_vouch_admit, vouch_admit_host);
+  bind_pair(m, "slash", to_slash, launch_slash, slash_host);
+  bind_pair(m, "hash_many", to_hash_many, launch_hash_many, hash_many_host);
+  bind_pair(m, "merkle", to_merkle, launch_merkle, merkle_host);
+  bind_pair(m, "verify", to_verify, launch_verify, verify_host);
+  bind_pair(m, "vclock", to_vclock, launch_vclock, vclock_host);
+  bind_pair(m, "locks", to_locks, launch_locks, locks_host);
   m.def(
       "pipeline",
       [](const py::dict& d, uintptr_t stream) {

@@ -1,0 +1,322 @@
+// Argument blocks of the batched governance kernels and their
+// launcher / host-twin declarations.  Pointers are device pointers for the
+// `launch_*` entry points and host pointers for the `*_host` twins.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ahv/hd.h"
+
+namespace ahv {
+
+// K01 ring gate
+struct RingGateArgs {
+  int64_t n;
+  const double* sigma;
+  const uint8_t* consensus;  // may be null (no consensus)
+  uint8_t* ring;
+};
+void launch_ring_gate(const RingGateArgs&, hipStream_t);
+void ring_gate_host(const RingGateArgs&);
+
+// K02 ring check
+struct RingCheckArgs {
+  int64_t n;
+  const uint8_t* agent_ring;
+  const uint8_t* action_flags;  // ActionFlag bits
+  const double* sigma;
+  const uint8_t* consensus;
+  const uint8_t* witness;
+  uint8_t* required;
+  uint8_t* reason;
+};
+void launch_ring_check(const RingCheckArgs&, hipStream_t);
+void ring_check_host(const RingCheckArgs&);
+
+// K13 saga / step FSM
+struct FsmArgs {
+  int64_t n;
+  int32_t kind;  // 0 step, 1 saga
+  int64_t now_us;
+  uint8_t* state;
+  const uint8_t* target;
+  uint8_t* ok;
+  int64_t* started_us;    // may be null
+  int64_t* completed_us;  // may be null
+};
+void launch_fsm(const FsmArgs&, hipStream_t);
+void fsm_host(const FsmArgs&);
+
+// K15 fan-out policy
+struct FanoutArgs {
+  int64_t groups;
+  const int32_t* offsets;   // [groups+1] branch ranges
+  const uint8_t* policy;    // [groups]
+  const uint8_t* succeeded; // [branches]
+  uint8_t* satisfied;       // [groups]
+  int32_t* success_count;   // [groups]
+  uint8_t* compensate;      // [branches]
+};
+void launch_fanout(const FanoutArgs&, hipStream_t);
+void fanout_host(const FanoutArgs&);
+
+// K16 breach window
+struct BreachArgs {
+  int64_t n;           // profiles receiving one call each
+  int32_t window_cap;  // ring capacity (reference deque maxlen 1000)
+  int64_t window_us;
+  int64_t cooldown_us;
+  const int64_t* now_us;      // [n] call timestamps
+  const uint8_t* agent_ring;  // [n] caller's current ring
+  const uint8_t* new_called;  // [n] ring being called
+  int64_t* ts;                // [n, cap]
+  uint8_t* called;            // [n, cap]
+  int32_t* head;              // [n]
+  int32_t* count;             // [n]
+  int64_t* total;             // [n]
+  uint8_t* tripped;           // [n]
+  int64_t* tripped_at_us;     // [n]
+  uint8_t* severity;          // [n] out 0 none .. 4 critical
+  double* rate;               // [n] out
+  int32_t* hits;              // [n] out
+  uint8_t* event;             // [n] out 1 = BreachEvent produced
+};
+void launch_breach(const BreachArgs&, hipStream_t);
+void breach_host(const BreachArgs&);
+
+// K17 token bucket
+struct BucketArgs {
+  int64_t n;
+  int64_t now_us;
+  double* tokens;
+  int64_t* last_us;
+  const double* capacity;
+  const double* rate;
+  const double* cost;
+  uint8_t* ok;
+};
+void launch_bucket(const BucketArgs&, hipStream_t);
+void bucket_host(const BucketArgs&);
+
+// K18 expiry tick
+struct ExpiryArgs {
+  int64_t n;
+  int64_t now_us;
+  uint8_t* active;
+  const int64_t* expires_us;  // < 0 = never
+  int64_t* released_us;       // may be null
+  uint8_t* expired;
+};
+void launch_expiry(const ExpiryArgs&, hipStream_t);
+void expiry_host(const ExpiryArgs&);
+
+// K22 ledger risk
+struct LedgerArgs {
+  int64_t agents;
+  const int32_t* offsets;  // [agents+1]
+  const uint8_t* type;     // LedgerType per entry
+  const double* severity;
+  double* raw_risk;
+  double* risk;
+  uint8_t* recommendation;
+  int32_t* slash_count;
+  int32_t* quarantine_count;
+  int32_t* clean_count;
+  double* fault_avg;
+};
+void launch_ledger(const LedgerArgs&, hipStream_t);
+void ledger_host(const LedgerArgs&);
+
+// K22 drift severity
+struct DriftArgs {
+  int64_t n;
+  double low, medium, high, critical;
+  const double* drift;
+  uint8_t* severity;
+};
+void launch_drift(const DriftArgs&, hipStream_t);
+void drift_host(const DriftArgs&);
+
+// K21 attribution raw scores
+struct AttributionArgs {
+  int64_t cases;
+  const int32_t* node_offsets;   // [cases+1]
+  const int32_t* agent_offsets;  // [cases+1] into raw / node_count
+  const int32_t* agent_of_node;  // local agent index of each node
+  const uint8_t* success;
+  const uint8_t* root_cause;
+  const double* risk_weight;     // ω of each node's action (default 0.5)
+  double* raw;
+  int32_t* node_count;
+};
+void launch_attribution(const AttributionArgs&, hipStream_t);
+void attribution_host(const AttributionArgs&);
+
+// ---------------------------------------------------------------- liability
+// Session-local vouch graphs: participants of a session have local indices
+// 0..15; edges are stored per session in creation order (CSR).
+
+constexpr int kTile = 16;
+
+// K03 / K04 — σ_eff and exposure from dense per-session bond tiles (f64 MFMA)
+struct BondTileArgs {
+  int64_t sessions;
+  const double* tiles;   // [S, 16, 16] live bonded amount, row = voucher, col = vouchee
+  const double* sigma;   // [S, 16] vouchee σ
+  const double* omega;   // [S] risk weight of the action being scored
+  double* sigma_eff;     // [S, 16] out
+  double* exposure;      // [S, 16] out: Σ bonded by voucher (row sums)
+  double* bonded_in;     // [S, 16] out: Σ bonded for vouchee (column sums)
+};
+void launch_bond_tiles(const BondTileArgs&, hipStream_t);
+void bond_tiles_host(const BondTileArgs&);
+
+// Edge-list (CSR) form: build the tiles, creation-order parity path, release.
+struct VouchCsrArgs {
+  int64_t sessions;
+  int64_t now_us;
+  const int32_t* offsets;  // [S+1]
+  const uint8_t* voucher;  // [E] local index
+  const uint8_t* vouchee;  // [E]
+  const double* bonded;    // [E]
+  uint8_t* active;         // [E]
+  const int64_t* expiry_us;  // [E], < 0 = none
+  int64_t* released_us;    // [E]
+  double* tiles;           // [S,16,16] out (build)
+  const double* sigma;     // [S,16] (sigma_eff_csr)
+  const double* omega;     // [S]
+  double* sigma_eff;       // [S,16] out (sigma_eff_csr)
+  int32_t* released;       // [S] out (release)
+};
+void launch_build_tiles(const VouchCsrArgs&, hipStream_t);
+void build_tiles_host(const VouchCsrArgs&);
+void launch_sigma_eff_csr(const VouchCsrArgs&, hipStream_t);
+void sigma_eff_csr_host(const VouchCsrArgs&);
+void launch_release(const VouchCsrArgs&, hipStream_t);
+void release_host(const VouchCsrArgs&);
+
+// K05 — admit new vouch requests (per session, in request order)
+struct VouchAdmitArgs {
+  int64_t sessions;
+  int64_t now_us;
+  double max_exposure;
+  // existing edges (CSR, creation order); admitted requests are appended by
+  // the caller from the `code` output (0 = admitted)
+  const int32_t* e_offsets;
+  const uint8_t* e_voucher;
+  const uint8_t* e_vouchee;
+  const double* e_bonded;
+  const uint8_t* e_active;
+  const int64_t* e_expiry;
+  // requests (CSR per session)
+  const int32_t* r_offsets;
+  const uint8_t* r_voucher;
+  const uint8_t* r_vouchee;
+  const double* r_sigma;    // voucher σ
+  const double* r_pct;      // bond pct (already defaulted)
+  double* r_bonded;         // out
+  uint8_t* code;            // out: 0 ok, 1 self, 2 low σ, 3 cycle, 4 exposure
+};
+void launch_vouch_admit(const VouchAdmitArgs&, hipStream_t);
+void vouch_admit_host(const VouchAdmitArgs&);
+
+// K06 — slash cascade (per session)
+struct SlashArgs {
+  int64_t sessions;
+  int64_t now_us;
+  const int32_t* offsets;   // edges CSR
+  const uint8_t* voucher;
+  const uint8_t* vouchee;
+  uint8_t* active;
+  const int64_t* expiry_us;
+  int64_t* released_us;
+  const uint8_t* target;    // [S] local index of the violator
+  const double* omega;      // [S]
+  double* scores;           // [S,16] in/out agent_scores (σ), NaN = absent
+  int32_t* clip_offsets;    // [S] base offset of the session's clip records
+  int32_t* clip_count;      // [S] out
+  uint8_t* clip_voucher;    // [cap] out
+  uint8_t* clip_depth;      // [cap] out
+  double* clip_before;      // [cap] out
+  double* clip_after;       // [cap] out
+  int32_t clip_cap;         // records per session
+};
+void launch_slash(const SlashArgs&, hipStream_t);
+void slash_host(const SlashArgs&);
+
+// ------------------------------------------------------------------ audit
+
+// K11 / K12 — SHA-256 of variable-length messages (offsets into a byte arena)
+struct HashManyArgs {
+  int64_t n;
+  const uint8_t* bytes;
+  const int64_t* offsets;  // [n+1]
+  uint32_t* digest;        // [n, 8]
+};
+void launch_hash_many(const HashManyArgs&, hipStream_t);
+void hash_many_host(const HashManyArgs&);
+
+// K09 — Merkle roots of many chains of leaf digests (segmented)
+struct MerkleArgs {
+  int64_t chains;
+  const int32_t* offsets;  // [chains+1] leaf ranges
+  const uint32_t* leaves;  // [L, 8]
+  uint32_t* scratch;       // [L, 8] level buffer
+  uint32_t* root;          // [chains, 8] (zeros for empty chains)
+};
+void launch_merkle(const MerkleArgs&, hipStream_t);
+void merkle_host(const MerkleArgs&);
+
+// K10 — verify chains: recompute each stored delta's digest from its canonical
+// payload (byte arena) and check parent links, without mutating anything.
+struct VerifyArgs {
+  int64_t deltas;
+  int64_t chains;
+  const uint8_t* bytes;
+  const int64_t* offsets;       // [deltas+1] canonical payloads
+  const uint32_t* stored;       // [deltas, 8] stored digests
+  const uint32_t* parent;       // [deltas, 8] stored parent digests
+  const uint8_t* has_parent;    // [deltas]
+  const int32_t* chain_offsets; // [chains+1]
+  uint8_t* delta_ok;            // [deltas] out
+  uint8_t* chain_ok;            // [chains] out
+};
+void launch_verify(const VerifyArgs&, hipStream_t);
+void verify_host(const VerifyArgs&);
+
+// ---------------------------------------------------------------- sessions
+
+// K19 — vector clocks: dense clocks [paths, A] and [agents, A] (A ≤ 64, one
+// component per lane of a wave).  Independent groups (sessions) run in parallel,
+// one wave each; a group's operations apply in order.
+struct VClockArgs {
+  int64_t groups;
+  int32_t A;               // clock width (agents of the session), ≤ 64
+  int32_t strict;
+  const int32_t* offsets;  // [groups+1] operation ranges
+  const uint8_t* op;       // [n] 0 read, 1 write
+  const int32_t* path;     // [n] row in path_clock
+  const int32_t* agent;    // [n] row in agent_clock
+  const int32_t* agent_col;  // [n] the agent's own component index
+  uint32_t* path_clock;    // [P, A]
+  uint32_t* agent_clock;   // [G, A]
+  uint8_t* ok;             // [n] out (0 = causal violation rejected the write)
+};
+void vclock_host(const VClockArgs&);
+void launch_vclock(const VClockArgs&, hipStream_t);
+
+// K20 — intent-lock contention mask for requests against active locks
+struct LockArgs {
+  int64_t n;                  // requests
+  const int32_t* res_offsets; // [R+1] active locks per resource (CSR)
+  const int32_t* lock_agent;  // [L]
+  const uint8_t* lock_intent; // [L] 0 read 1 write 2 exclusive
+  const int32_t* req_res;     // [n]
+  const int32_t* req_agent;   // [n]
+  const uint8_t* req_intent;  // [n]
+  int32_t* conflicts;         // [n] out: number of conflicting locks
+};
+void launch_locks(const LockArgs&, hipStream_t);
+void locks_host(const LockArgs&);
+
+}  // namespace ahv

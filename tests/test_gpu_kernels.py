@@ -1,0 +1,249 @@
+"""gfx950 kernels K01–K22 == their host twins (same element bodies, run on the
+CPU in tests/test_kernels_host.py against the Python engines)."""
+
+from __future__ import annotations
+
+import random
+
+import pytest
+import torch
+
+from agent_hypervisor_amd.ops import audit as A
+from agent_hypervisor_amd.ops import ledger as L
+from agent_hypervisor_amd.ops import liability as LI
+from agent_hypervisor_amd.ops import rings as R
+from agent_hypervisor_amd.ops import saga as SG
+from agent_hypervisor_amd.ops import security as SEC
+from agent_hypervisor_amd.ops import session as SE
+
+pytestmark = pytest.mark.gpu
+f64, u8, i32, i64 = torch.float64, torch.uint8, torch.int32, torch.int64
+
+
+def _both(fn, *tensors):
+    """Run ``fn`` on CPU copies and on cuda copies of ``tensors``; returns both
+    (outputs, mutated inputs) on the CPU."""
+    cpu = [t.clone() for t in tensors]
+    dev = [t.clone().cuda() for t in tensors]
+    out_c = fn(*cpu)
+    out_d = fn(*dev)
+    torch.cuda.synchronize()
+    return (out_c, cpu), (_to_cpu(out_d), [t.cpu() for t in dev])
+
+
+def _to_cpu(x):
+    if isinstance(x, torch.Tensor):
+        return x.cpu()
+    if isinstance(x, (tuple, list)):
+        return type(x)(_to_cpu(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_cpu(v) for k, v in x.items()}
+    if hasattr(x, "__dataclass_fields__"):
+        return {k: _to_cpu(getattr(x, k)) for k in x.__dataclass_fields__}
+    return x
+
+
+def _eq(a, b, exact=True):
+    a, b = _to_cpu(a), _to_cpu(b)
+    if isinstance(a, torch.Tensor):
+        if exact:
+            assert torch.equal(a, b) or (a.is_floating_point() and torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0)))
+        else:
+            torch.testing.assert_close(a, b, rtol=0, atol=1e-12, equal_nan=True)
+    elif isinstance(a, (tuple, list)):
+        for x, y in zip(a, b):
+            _eq(x, y, exact)
+    elif isinstance(a, dict):
+        for k in a:
+            _eq(a[k], b[k], exact)
+    else:
+        assert a == b
+
+
+def _check(fn, *tensors, exact=True):
+    (oc, ic), (od, idv) = _both(fn, *tensors)
+    _eq(oc, od, exact)
+    _eq(ic, idv, exact)
+
+
+def test_ring_kernels(cuda_device):
+    g = torch.Generator().manual_seed(0)
+    n = 100_000
+    sig = torch.rand(n, dtype=f64, generator=g)
+    cons = torch.randint(0, 2, (n,), dtype=u8, generator=g)
+    _check(lambda s, c: R.ring_gate(s, c), sig, cons)
+    ring = torch.randint(0, 4, (n,), dtype=u8, generator=g)
+    flags = torch.randint(0, 8, (n,), dtype=u8, generator=g)
+    wit = torch.randint(0, 2, (n,), dtype=u8, generator=g)
+    _check(lambda *t: R.ring_check(*t), ring, flags, sig, cons, wit)
+
+
+def _vouch_batch(S, seed):
+    rng = random.Random(seed)
+    offs, vr, ve, bd, ac, ex = [0], [], [], [], [], []
+    for _ in range(S):
+        for _ in range(rng.randint(0, 40)):
+            a, b = rng.sample(range(16), 2)
+            vr.append(a)
+            ve.append(b)
+            bd.append(rng.uniform(0.0, 0.4))
+            ac.append(int(rng.random() < 0.9))
+            ex.append(rng.choice([-1, -1, 50, 150]))
+        offs.append(len(vr))
+    return LI.VouchBatch(torch.tensor(offs, dtype=i32), torch.tensor(vr, dtype=u8), torch.tensor(ve, dtype=u8),
+                         torch.tensor(bd, dtype=f64), torch.tensor(ac, dtype=u8), torch.tensor(ex, dtype=i64),
+                         torch.zeros(len(vr), dtype=i64))
+
+
+def test_liability_kernels(cuda_device):
+    S = 2048
+    vb = _vouch_batch(S, 1)
+    g = torch.Generator().manual_seed(1)
+    sigma = torch.rand((S, 16), dtype=f64, generator=g)
+    omega = torch.rand(S, dtype=f64, generator=g)
+    fields = list(vb.__dataclass_fields__)
+
+    def mk(*t):
+        return LI.VouchBatch(*t[: len(fields)])
+
+    _check(lambda *t: LI.build_tiles(mk(*t), 100), *[getattr(vb, f) for f in fields])
+    _check(lambda *t: LI.sigma_eff_exact(mk(*t[:-2]), t[-2], t[-1], 100), *[getattr(vb, f) for f in fields],
+           sigma, omega)
+    tiles = LI.build_tiles(vb, 100)
+    # MFMA sums in tile order; host twin sums sequentially — same terms, fp64
+    _check(lambda t, s, o: LI.bond_tiles(t, s, o), tiles, sigma, omega, exact=False)
+    ref = LI.sigma_eff_exact(vb, sigma, omega, 100)
+    se, _, _ = LI.bond_tiles(tiles.cuda(), sigma.cuda(), omega.cuda())
+    torch.testing.assert_close(se.cpu(), ref, rtol=0, atol=1e-12)
+    _check(lambda *t: LI.release_bonds(mk(*t), 100), *[getattr(vb, f) for f in fields])
+    tgt = torch.randint(0, 16, (S,), dtype=u8, generator=g)
+    scores = torch.rand((S, 16), dtype=f64, generator=g)
+    scores[scores < 0.1] = float("nan")
+    _check(lambda *t: LI.slash(mk(*t[:-3]), t[-3], t[-2], t[-1], 100), *[getattr(vb, f) for f in fields],
+           tgt, omega, scores)
+    # admission
+    rng = random.Random(2)
+    r_off, rv, re_, rs, rp = [0], [], [], [], []
+    for _ in range(S):
+        for _ in range(rng.randint(0, 12)):
+            rv.append(rng.randrange(16))
+            re_.append(rng.randrange(16))
+            rs.append(rng.uniform(0.3, 1.0))
+            rp.append(rng.choice([0.1, 0.2, 0.5]))
+        r_off.append(len(rv))
+    _check(lambda *t: LI.vouch_admit(mk(*t[: len(fields)]), *t[len(fields):], 100),
+           *[getattr(vb, f) for f in fields], torch.tensor(r_off, dtype=i32), torch.tensor(rv, dtype=u8),
+           torch.tensor(re_, dtype=u8), torch.tensor(rs, dtype=f64), torch.tensor(rp, dtype=f64))
+
+
+def test_audit_kernels(cuda_device):
+    import hashlib
+
+    rng = random.Random(3)
+    msgs = [bytes(rng.randrange(256) for _ in range(rng.choice([0, 1, 55, 56, 64, 119, 200, 1500])))
+            for _ in range(3000)]
+    data, offs = A.pack_bytes(msgs)
+    dig = A.sha256_many(data.cuda(), offs.cuda())
+    assert A.digests_to_hex(dig) == [hashlib.sha256(m).hexdigest() for m in msgs]
+    # merkle over ragged chains
+    leaves = torch.randint(-(2**31), 2**31 - 1, (5000, 8), dtype=i32)
+    cuts = sorted(rng.sample(range(1, 5000), 700))
+    moffs = torch.tensor([0] + cuts + [5000], dtype=i32)
+    _check(lambda o, l: A.merkle_roots(o, l), moffs, leaves)
+    # verify: chains of random payloads with correct links, some tampered
+    pays = [bytes(rng.randrange(256) for _ in range(rng.randint(100, 400))) for _ in range(4000)]
+    hexes = [hashlib.sha256(p).hexdigest() for p in pays]
+    chain_offs = [0] + sorted(rng.sample(range(1, 4000), 500)) + [4000]
+    parent, has_parent = [], []
+    for c in range(len(chain_offs) - 1):
+        for i in range(chain_offs[c], chain_offs[c + 1]):
+            has_parent.append(int(i != chain_offs[c]))
+            parent.append(hexes[i - 1] if i != chain_offs[c] else "0" * 64)
+    for k in rng.sample(range(4000), 40):
+        hexes[k] = "ab" * 32
+    d, o = A.pack_bytes(pays)
+    _check(lambda *t: A.verify_chains(*t), d, o, A.hex_to_digests(hexes), A.hex_to_digests(parent),
+           torch.tensor(has_parent, dtype=u8), torch.tensor(chain_offs, dtype=i32))
+
+
+def test_saga_kernels(cuda_device):
+    g = torch.Generator().manual_seed(4)
+    n = 50_000
+    st = torch.randint(0, 7, (n,), dtype=u8, generator=g)
+    tg = torch.randint(0, 7, (n,), dtype=u8, generator=g)
+    _check(lambda s, t, a, b: SG.transition(s, t, 9, started_us=a, completed_us=b), st, tg,
+           torch.zeros(n, dtype=i64), torch.zeros(n, dtype=i64))
+    st5 = torch.randint(0, 5, (n,), dtype=u8, generator=g)
+    tg5 = torch.randint(0, 5, (n,), dtype=u8, generator=g)
+    _check(lambda s, t, b: SG.transition(s, t, 9, saga=True, completed_us=b), st5, tg5, torch.zeros(n, dtype=i64))
+    G = 10_000
+    sizes = torch.randint(0, 9, (G,), generator=g)
+    offs = torch.cat([torch.zeros(1, dtype=torch.int64), sizes.cumsum(0)]).to(i32)
+    _check(lambda o, p, s: SG.fanout_policy(o, p, s), offs, torch.randint(0, 3, (G,), dtype=u8, generator=g),
+           torch.randint(0, 2, (int(offs[-1]),), dtype=u8, generator=g))
+
+
+def test_security_kernels(cuda_device):
+    g = torch.Generator().manual_seed(5)
+    n, cap = 4096, 64
+    prof = SEC.BreachProfiles.allocate(n, cap)
+    fields = list(prof.__dataclass_fields__)
+    t = torch.zeros(n, dtype=i64)
+    cpu_p = SEC.BreachProfiles(*[getattr(prof, f).clone() for f in fields])
+    dev_p = SEC.BreachProfiles(*[getattr(prof, f).clone().cuda() for f in fields])
+    for step in range(80):
+        t = t + torch.randint(100_000, 20_000_000, (n,), generator=g)
+        ar = torch.randint(1, 4, (n,), dtype=u8, generator=g)
+        cr = torch.randint(0, 4, (n,), dtype=u8, generator=g)
+        oc = SEC.breach_record(cpu_p, t, ar, cr)
+        od = SEC.breach_record(dev_p, t.cuda(), ar.cuda(), cr.cuda())
+        _eq(oc, od)
+    _eq(cpu_p, dev_p)
+    m = 100_000
+    _check(lambda *a: SEC.token_bucket(*a, 1_000_000), torch.rand(m, dtype=f64, generator=g) * 10,
+           torch.zeros(m, dtype=i64), torch.full((m,), 10.0, dtype=f64), torch.rand(m, dtype=f64, generator=g),
+           torch.rand(m, dtype=f64, generator=g) * 3)
+    _check(lambda a, e, r: SEC.expiry_tick(a, e, 500, r), torch.randint(0, 2, (m,), dtype=u8, generator=g),
+           torch.randint(-1, 1000, (m,), dtype=i64, generator=g), torch.zeros(m, dtype=i64))
+
+
+def test_ledger_kernels(cuda_device):
+    g = torch.Generator().manual_seed(6)
+    A_ = 20_000
+    sizes = torch.randint(0, 12, (A_,), generator=g)
+    offs = torch.cat([torch.zeros(1, dtype=torch.int64), sizes.cumsum(0)]).to(i32)
+    E = int(offs[-1])
+    _check(lambda o, t, s: L.risk_profiles(o, t, s), offs, torch.randint(0, 9, (E,), dtype=u8, generator=g),
+           torch.rand(E, dtype=f64, generator=g))
+    _check(lambda d: L.drift_severity(d), torch.rand(100_000, dtype=f64, generator=g))
+    C = 5000
+    nn = torch.randint(1, 12, (C,), generator=g)
+    na = torch.randint(1, 6, (C,), generator=g)
+    noffs = torch.cat([torch.zeros(1, dtype=torch.int64), nn.cumsum(0)]).to(i32)
+    aoffs = torch.cat([torch.zeros(1, dtype=torch.int64), na.cumsum(0)]).to(i32)
+    aon = torch.cat([torch.randint(0, int(na[c]), (int(nn[c]),), generator=g) for c in range(C)]).to(i32)
+    N = int(noffs[-1])
+    _check(lambda *t: L.attribution_raw(*t), noffs, aoffs, aon, torch.randint(0, 2, (N,), dtype=u8, generator=g),
+           torch.randint(0, 2, (N,), dtype=u8, generator=g), torch.rand(N, dtype=f64, generator=g))
+
+
+def test_session_kernels(cuda_device):
+    g = torch.Generator().manual_seed(7)
+    G, P, Ag, per = 512, 6, 40, 50
+    offs = torch.arange(0, (G + 1) * per, per, dtype=i32)
+    n = G * per
+    grp = torch.arange(n) // per
+    op = torch.randint(0, 2, (n,), dtype=u8, generator=g)
+    col = torch.randint(0, Ag, (n,), generator=g)
+    path = (grp * P + torch.randint(0, P, (n,), generator=g)).to(i32)
+    agent = (grp * Ag + col).to(i32)
+    _check(lambda *t: SE.vector_clock_ops(*t), offs, op, path, agent, col.to(i32),
+           torch.zeros((G * P, Ag), dtype=i32), torch.zeros((G * Ag, Ag), dtype=i32))
+    R_, Lk = 1000, 8000
+    rs = torch.randint(0, 16, (R_,), generator=g)
+    roffs = torch.cat([torch.zeros(1, dtype=torch.int64), rs.cumsum(0)]).to(i32)
+    Lk = int(roffs[-1])
+    m = 50_000
+    _check(lambda *t: SE.lock_conflicts(*t), roffs, torch.randint(0, 30, (Lk,), dtype=i32, generator=g),
+           torch.randint(0, 3, (Lk,), dtype=u8, generator=g), torch.randint(0, R_, (m,), dtype=i32, generator=g),
+           torch.randint(0, 30, (m,), dtype=i32, generator=g), torch.randint(0, 3, (m,), dtype=u8, generator=g))
