@@ -48,7 +48,7 @@ def _sources() -> list[Path]:
 
 
 def _headers_mtime() -> float:
-    newest = 0.0
+    newest = Path(__file__).stat().st_mtime  # compiler flags live here
     for h in (CSRC / "include").rglob("*.h"):
         newest = max(newest, h.stat().st_mtime)
     return newest
@@ -87,6 +87,9 @@ def _compile_cmd(src: Path, obj: Path) -> list[str]:
         "hip",
         f"--offload-arch={ARCH}",
         "-O3",
+        # Governance arithmetic must round exactly like CPython (no a*b+c fusion):
+        # σ_eff, clips, risk and token refills are compared bit-for-bit.
+        "-ffp-contract=off",
         "-std=c++17",
         "-fPIC",
         "-fvisibility=hidden",
