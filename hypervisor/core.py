@@ -250,6 +250,19 @@ class Hypervisor:
 
     # -- queries ------------------------------------------------------------------
     @property
+    def sessions(self) -> list[ManagedSession]:
+        """Every managed session (including archived ones), in creation order."""
+        return list(self._sessions.values())
+
+    def find_saga(self, saga_id: str):
+        """(managed session, saga) owning ``saga_id``, or (None, None)."""
+        for m in self._sessions.values():
+            s = m.saga.get_saga(saga_id)
+            if s is not None:
+                return m, s
+        return None, None
+
+    @property
     def active_sessions(self) -> list[ManagedSession]:
         return [m for m in self._sessions.values() if m.sso.state.value not in ("archived", "terminating")]
 

@@ -144,6 +144,12 @@ class VouchingEngine:
                 contrib += v.bonded_amount
         return min(vouchee_sigma + risk_weight * contrib, 1.0)
 
+    def records(self, session_id: Optional[str] = None) -> list[VouchRecord]:
+        """All vouch records (active or not), optionally of one session."""
+        if session_id is not None:
+            return list(self._session_records(session_id))
+        return list(self._vouches.values())
+
     def get_vouchers_for(self, agent_did: str, session_id: str) -> list[VouchRecord]:
         return self._active_vouches_for(agent_did, session_id)
 

@@ -142,6 +142,11 @@ class SagaOrchestrator:
         return self._sagas.get(saga_id)
 
     @property
+    def sagas(self) -> list[Saga]:
+        """Every saga of this orchestrator, in creation order."""
+        return list(self._sagas.values())
+
+    @property
     def active_sagas(self) -> list[Saga]:
         return [
             s for s in self._sagas.values() if s.state in (SagaState.RUNNING, SagaState.COMPENSATING)
