@@ -79,3 +79,11 @@ def parity_mode() -> bool:
 
 def set_parity_mode(on: bool) -> None:
     RUNTIME.parity_mode = bool(on)
+
+
+def reload() -> HypervisorRuntimeConfig:
+    """Re-read every ``AHV_`` variable into the live :data:`RUNTIME` object."""
+    fresh = HypervisorRuntimeConfig.from_env()
+    for f in fields(fresh):
+        setattr(RUNTIME, f.name, getattr(fresh, f.name))
+    return RUNTIME
