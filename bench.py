@@ -84,6 +84,8 @@ def main() -> None:
     ap.add_argument("--deltas", type=int, default=3)
     ap.add_argument("--scalar-iters", type=int, default=2000)
     ap.add_argument("--no-scalar", action="store_true")
+    ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                    help="cpu runs the host twin of the kernel over gloo (multi-process CPU rehearsal)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,10 +93,20 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if dev.type == "cuda":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
 
     from agent_hypervisor_amd.models.engine import GovernanceEngine
     from agent_hypervisor_amd.parallel.collectives import allreduce_stats
@@ -115,23 +127,23 @@ def main() -> None:
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
 
     # per-step latency distribution (synchronised steps, untimed for throughput)
     lat = []
     for _ in range(max(3, min(10, args.steps))):
         t0 = time.perf_counter()
         step()
-        torch.cuda.synchronize(dev)
+        sync()
         lat.append(time.perf_counter() - t0)
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
