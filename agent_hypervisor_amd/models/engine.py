@@ -13,10 +13,11 @@ with all state in :mod:`agent_hypervisor_amd.models.tables` SoA tensors.  Ids
 (session / saga / step uuid4) are minted on device from a counter-based
 generator, timestamps come from one injected ``now_us`` per batch (N09), and
 every digest is byte-identical to what the scalar path computes for the same
-ids and timestamps (``tests/test_engine_cpu.py``, ``tests/test_gpu_kernels.py``).
+ids and timestamps (``tests/test_engine_host.py``, ``tests/test_gpu_pipeline.py``).
 
 Multi-GPU: one engine per rank; sessions are sharded by rank (P01), see
-:mod:`agent_hypervisor_amd.parallel.sharding`.
+:mod:`agent_hypervisor_amd.parallel.directory`.  Steady-state batches can be
+captured in a hipGraph with :class:`agent_hypervisor_amd.runtime.graphs.PipelineGraph`.
 """
 
 from __future__ import annotations
@@ -172,6 +173,7 @@ class GovernanceEngine:
         self.creator_id = self.interner.intern(creator_did)
         self._next_slot = 0
         self._id_counter = 0
+        self._last_specs = None
         self._change_cache: dict = {}
 
     # -- agents ----------------------------------------------------------------
@@ -217,12 +219,19 @@ class GovernanceEngine:
         max_participants: int = 10,
         min_sigma_eff: float = 0.60,
         stats: Optional[torch.Tensor] = None,
+        cursor: Optional[torch.Tensor] = None,
     ) -> PipelineBatch:
         """Run the full governance pipeline for ``n`` new sessions (asynchronously
         on the current stream).
 
         ``stats`` (int64[6], on the engine device) accumulates the batch counters
         sessions / ok / participants / deltas / commitments / archived.
+
+        ``cursor`` (int64[3] on the engine device: slot_base, id_base, now_us)
+        makes the launch read its bases from device memory instead of the host
+        counters — the graph-capturable form used by
+        :class:`agent_hypervisor_amd.runtime.graphs.PipelineGraph`, which also
+        advances the cursor on the device.  The host counters are not touched.
         """
         if stats is not None and (stats.dtype != torch.int64 or stats.numel() != 6 or stats.device != self.device):
             raise ValueError("stats must be an int64[6] tensor on the engine device")
@@ -237,6 +246,7 @@ class GovernanceEngine:
         if agents.numel() != n:
             raise ValueError("agents must have one entry per session")
         specs = changes or REFERENCE_CHANGES
+        self._last_specs = list(specs)
         ch = self._changes(deltas, specs)
         pool_b, pool_o, pool_l = self.interner.device_view(self.device)
         now = int(now_us if now_us is not None else _clock.now_us())
@@ -252,6 +262,12 @@ class GovernanceEngine:
             pool_bytes=pool_b, pool_off=pool_o, pool_len=pool_l, stats=stats,
         )
         tensors.update({k: getattr(self.sessions, k) for k in SessionTable.COLUMNS})
+        if cursor is not None:
+            if cursor.dtype != torch.int64 or cursor.numel() != 3 or cursor.device != self.device:
+                raise ValueError("cursor must be an int64[3] tensor on the engine device")
+            tensors["cursor"] = cursor
+            _pipeline_op.run(scalars, tensors)
+            return PipelineBatch(self, -1, n, -1, -1, deltas, list(specs), agents)
         _pipeline_op.run(scalars, tensors)
         self._next_slot = (slot_base + n) % cap
         self._id_counter = id_base + 3 * n

@@ -84,6 +84,8 @@ def main() -> None:
     ap.add_argument("--deltas", type=int, default=3)
     ap.add_argument("--scalar-iters", type=int, default=2000)
     ap.add_argument("--no-scalar", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step from a captured hipGraph (device cursor + RCCL counters)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                     help="cpu runs the host twin of the kernel over gloo (multi-process CPU rehearsal)")
     args = ap.parse_args()
@@ -124,6 +126,25 @@ def main() -> None:
         agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
         eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=stats)
         return allreduce_stats(stats)
+
+    if args.graph:
+        from agent_hypervisor_amd.runtime.graphs import PipelineGraph
+
+        reduce = None
+        if world > 1 and dev.type == "cuda":
+            from agent_hypervisor_amd.parallel.rccl import Communicator
+
+            comm = Communicator.from_process_group(device=local)
+            reduce = comm.all_reduce
+        elif world > 1:
+            reduce = allreduce_stats
+        buf = torch.zeros(S, dtype=torch.int32, device=dev)
+        pg = PipelineGraph(eng, S, buf, deltas=args.deltas, stats=stats,
+                           refresh_agents=lambda: buf.random_(0, args.agents), reduce=reduce)
+
+        def step():  # noqa: F811 - graph-replay form of the same step
+            pg.step()
+            return stats
 
     for _ in range(args.warmup):
         step()

@@ -49,6 +49,55 @@ void launch_pipeline(const PipelineArgs& a, hipStream_t stream) {
   check_hip(hipGetLastError(), "governance_pipeline_kernel launch");
 }
 
+// ---------------------------------------------------------- cursor kernels
+// wall_clock64() is the constant-rate counter (hipDeviceAttributeWallClockRate);
+// the host pairs one sample with its own UTC clock once, after which captured
+// graphs stamp every replay with device-side "now" and no host round trip.
+
+__global__ void pipeline_clock_kernel(int64_t* cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz) {
+  const int64_t ticks = static_cast<int64_t>(wall_clock64()) - base_clk;
+  cursor[2] = base_us + ticks * 1000 / rate_khz;
+}
+
+__global__ void pipeline_advance_kernel(int64_t* cursor, int64_t n, int64_t capacity) {
+  cursor[0] = (cursor[0] + n) % capacity;
+  cursor[1] += 3 * n;
+}
+
+__global__ void wall_clock_kernel(int64_t* out) { *out = static_cast<int64_t>(wall_clock64()); }
+
+void launch_pipeline_clock(int64_t* cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz, hipStream_t s) {
+  if (rate_khz <= 0) throw std::invalid_argument("wall clock rate must be positive");
+  hipLaunchKernelGGL(pipeline_clock_kernel, dim3(1), dim3(1), 0, s, cursor, base_us, base_clk, rate_khz);
+  check_hip(hipGetLastError(), "pipeline_clock_kernel");
+}
+
+void launch_pipeline_advance(int64_t* cursor, int64_t n, int64_t capacity, hipStream_t s) {
+  if (capacity <= 0) throw std::invalid_argument("capacity must be positive");
+  hipLaunchKernelGGL(pipeline_advance_kernel, dim3(1), dim3(1), 0, s, cursor, n, capacity);
+  check_hip(hipGetLastError(), "pipeline_advance_kernel");
+}
+
+int64_t device_wall_clock(int device) {
+  check_hip(hipSetDevice(device), "hipSetDevice");
+  int64_t* d = nullptr;
+  check_hip(hipMalloc(&d, sizeof(int64_t)), "hipMalloc");
+  hipLaunchKernelGGL(wall_clock_kernel, dim3(1), dim3(1), 0, nullptr, d);
+  int64_t v = 0;
+  const hipError_t e1 = hipGetLastError();
+  const hipError_t e2 = hipMemcpy(&v, d, sizeof(v), hipMemcpyDeviceToHost);
+  hipFree(d);
+  check_hip(e1, "wall_clock_kernel");
+  check_hip(e2, "hipMemcpy wall clock");
+  return v;
+}
+
+int64_t device_wall_clock_rate_khz(int device) {
+  int rate = 0;
+  check_hip(hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, device), "wall clock rate");
+  return rate;
+}
+
 void pipeline_host(const PipelineArgs& a) {
   HostSink sink;
   for (int64_t i = 0; i < a.n; ++i) {

@@ -1,5 +1,150 @@
+// N06 — RCCL communicator over xGMI, owned by C++.
+//
+// torch.distributed("nccl") is RCCL too; this direct wrapper exists so the
+// governance collectives (X01–X09) can be enqueued on *our* HIP streams and
+// captured inside the engine's hipGraphs without a ProcessGroup in the loop.
+// The unique id is exchanged by the caller (agent_hypervisor_amd/parallel/rccl.py
+// broadcasts it over any torch.distributed group, gloo included).
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "ahv/launch.h"
+
 namespace py = pybind11;
-namespace ahv { namespace host {
-void register_comm(py::module_& m) { (void)m; }
-}}
+
+namespace ahv {
+namespace host {
+namespace {
+
+void check_nccl(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+ncclDataType_t to_dtype(const std::string& s) {
+  if (s == "int8") return ncclInt8;
+  if (s == "uint8") return ncclUint8;
+  if (s == "int32") return ncclInt32;
+  if (s == "uint32") return ncclUint32;
+  if (s == "int64") return ncclInt64;
+  if (s == "uint64") return ncclUint64;
+  if (s == "float16") return ncclFloat16;
+  if (s == "bfloat16") return ncclBfloat16;
+  if (s == "float32") return ncclFloat32;
+  if (s == "float64") return ncclFloat64;
+  throw std::invalid_argument("unsupported RCCL dtype " + s);
+}
+
+ncclRedOp_t to_op(const std::string& s) {
+  if (s == "sum") return ncclSum;
+  if (s == "prod") return ncclProd;
+  if (s == "max") return ncclMax;
+  if (s == "min") return ncclMin;
+  throw std::invalid_argument("unsupported RCCL reduction " + s);
+}
+
+inline void* vp(uintptr_t p) { return reinterpret_cast<void*>(p); }
+inline hipStream_t sp(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+class RcclComm {
+ public:
+  RcclComm(int rank, int world, const py::bytes& uid, int device) : rank_(rank), world_(world), device_(device) {
+    std::string raw = uid;
+    if (raw.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("bad RCCL unique id length");
+    ncclUniqueId id;
+    std::memcpy(&id, raw.data(), sizeof(id));
+    check_hip(hipSetDevice(device), "hipSetDevice");
+    py::gil_scoped_release nogil;
+    check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  }
+  ~RcclComm() {
+    if (comm_) ncclCommDestroy(comm_);
+  }
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  void all_reduce(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, const std::string& op,
+                  uintptr_t stream) {
+    live();
+    check_nccl(ncclAllReduce(vp(send), vp(recv), count, to_dtype(dt), to_op(op), comm_, sp(stream)), "ncclAllReduce");
+  }
+  void all_gather(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, uintptr_t stream) {
+    live();
+    check_nccl(ncclAllGather(vp(send), vp(recv), count, to_dtype(dt), comm_, sp(stream)), "ncclAllGather");
+  }
+  void reduce_scatter(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, const std::string& op,
+                      uintptr_t stream) {
+    live();
+    check_nccl(ncclReduceScatter(vp(send), vp(recv), count, to_dtype(dt), to_op(op), comm_, sp(stream)),
+               "ncclReduceScatter");
+  }
+  void broadcast(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, int root, uintptr_t stream) {
+    live();
+    check_nccl(ncclBroadcast(vp(send), vp(recv), count, to_dtype(dt), root, comm_, sp(stream)), "ncclBroadcast");
+  }
+  // Point-to-point all-to-all of equal blocks (session re-sharding, P08): block
+  // b of `send` goes to rank b, block b of `recv` comes from rank b.
+  void all_to_all(uintptr_t send, uintptr_t recv, size_t block_count, const std::string& dt, size_t elem_bytes,
+                  uintptr_t stream) {
+    live();
+    const ncclDataType_t t = to_dtype(dt);
+    const size_t stride = block_count * elem_bytes;
+    check_nccl(ncclGroupStart(), "ncclGroupStart");
+    for (int r = 0; r < world_; ++r) {
+      check_nccl(ncclSend(static_cast<char*>(vp(send)) + r * stride, block_count, t, r, comm_, sp(stream)), "ncclSend");
+      check_nccl(ncclRecv(static_cast<char*>(vp(recv)) + r * stride, block_count, t, r, comm_, sp(stream)), "ncclRecv");
+    }
+    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  void destroy() {
+    if (comm_) {
+      check_nccl(ncclCommDestroy(comm_), "ncclCommDestroy");
+      comm_ = nullptr;
+    }
+  }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  int device() const { return device_; }
+
+ private:
+  void live() const {
+    if (!comm_) throw std::runtime_error("RCCL communicator was destroyed");
+  }
+  ncclComm_t comm_ = nullptr;
+  int rank_, world_, device_;
+};
+
+}  // namespace
+
+void register_comm(py::module_& m) {
+  m.def("rccl_unique_id", []() {
+    ncclUniqueId id;
+    check_nccl(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+  });
+  m.def("rccl_version", []() {
+    int v = 0;
+    check_nccl(ncclGetVersion(&v), "ncclGetVersion");
+    return v;
+  });
+  py::class_<RcclComm, std::unique_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init<int, int, const py::bytes&, int>(), py::arg("rank"), py::arg("world"), py::arg("unique_id"),
+           py::arg("device"))
+      .def("all_reduce", &RcclComm::all_reduce, py::call_guard<py::gil_scoped_release>())
+      .def("all_gather", &RcclComm::all_gather, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("all_to_all", &RcclComm::all_to_all, py::call_guard<py::gil_scoped_release>())
+      .def("destroy", &RcclComm::destroy)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("device", &RcclComm::device);
+}
+
+}  // namespace host
+}  // namespace ahv

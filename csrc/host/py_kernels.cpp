@@ -61,6 +61,7 @@ static PipelineArgs pipeline_args(const py::dict& d) {
   a.pool.off = ptr<const int64_t>(d, "pool_off");
   a.pool.len = ptr<const int32_t>(d, "pool_len");
   a.stats = ptr<unsigned long long>(d, "stats");
+  a.cursor = d.contains("cursor") ? ptr<const int64_t>(d, "cursor") : nullptr;
   SessionTables& t = a.t;
   t.sess_uuid = ptr<uint32_t>(d, "sess_uuid");
   t.sess_state = ptr<uint8_t>(d, "sess_state");
@@ -287,6 +288,22 @@ void register_kernels(py::module_& m) {
         pipeline_host(a);
       },
       py::arg("args"), "Run the same per-session pipeline body on the CPU (host twin).");
+  m.def(
+      "pipeline_clock",
+      [](uintptr_t cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz, uintptr_t stream) {
+        launch_pipeline_clock(reinterpret_cast<int64_t*>(cursor), base_us, base_clk, rate_khz,
+                              reinterpret_cast<hipStream_t>(stream));
+      },
+      "Stamp cursor[2] (now_us) from the device wall clock on `stream`.");
+  m.def(
+      "pipeline_advance",
+      [](uintptr_t cursor, int64_t n, int64_t capacity, uintptr_t stream) {
+        launch_pipeline_advance(reinterpret_cast<int64_t*>(cursor), n, capacity,
+                                reinterpret_cast<hipStream_t>(stream));
+      },
+      "Advance cursor slot/id bases by one batch of `n` sessions on `stream`.");
+  m.def("device_wall_clock", &device_wall_clock, py::arg("device"));
+  m.def("device_wall_clock_rate_khz", &device_wall_clock_rate_khz, py::arg("device"));
   m.attr("PIPE_MAX_PARTICIPANTS") = kMaxParticipants;
   m.attr("PIPE_MAX_DELTAS") = kMaxDeltasPipeline;
   m.attr("PIPE_MAX_CHANGES") = kMaxChanges;

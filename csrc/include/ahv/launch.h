@@ -18,4 +18,11 @@ struct PipelineArgs;
 void launch_pipeline(const PipelineArgs& a, hipStream_t stream);
 void pipeline_host(const PipelineArgs& a);
 
+// Device time base and cursor maintenance for graph-captured pipelines (N07/N09).
+// cursor = int64[3] {slot_base, id_base, now_us}.
+void launch_pipeline_clock(int64_t* cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz, hipStream_t s);
+void launch_pipeline_advance(int64_t* cursor, int64_t n, int64_t capacity, hipStream_t s);
+int64_t device_wall_clock(int device);  // one synchronous sample of wall_clock64()
+int64_t device_wall_clock_rate_khz(int device);
+
 }  // namespace ahv

@@ -83,7 +83,18 @@ struct PipelineArgs {
   StrPool pool;
   SessionTables t;
   unsigned long long* stats;     // [kPipeStats] batch counters (X04), accumulated, or null
+  // Device-resident cursor {slot_base, id_base, now_us} (int64[3]) or null.  When
+  // set it overrides the three scalars above, so a launch captured in a hipGraph
+  // stays correct on replay: the clock kernel refreshes now_us and the advance
+  // kernel moves slot/id bases on the device (runtime/graphs.py, N07/N09).
+  const int64_t* cursor;
 };
+
+AHV_HD inline int64_t pipe_slot_base(const PipelineArgs& a) { return a.cursor ? a.cursor[0] : a.slot_base; }
+AHV_HD inline uint64_t pipe_id_base(const PipelineArgs& a) {
+  return a.cursor ? static_cast<uint64_t>(a.cursor[1]) : a.id_base;
+}
+AHV_HD inline int64_t pipe_now_us(const PipelineArgs& a) { return a.cursor ? a.cursor[2] : a.now_us; }
 
 // Per-session counters reduced into PipelineArgs::stats:
 // sessions, ok, participants, deltas, commitments, archived.
@@ -95,14 +106,15 @@ struct PipeCounters {
 // Per-session body.  `i` is the batch index.
 template <class Sink>
 AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sink) {
-  const int64_t slot = (a.slot_base + i) % a.capacity;
+  const int64_t slot = (pipe_slot_base(a) + i) % a.capacity;
   const SessionTables& t = a.t;
-  const int64_t now = a.now_us;
+  const int64_t now = pipe_now_us(a);
+  const uint64_t id_base = pipe_id_base(a);
   int32_t status = PIPE_OK;
 
   // ---- create_session + begin_handshake -------------------------------------
   uint32_t u[4];
-  uuid4_words(a.seed, a.id_base + 3 * static_cast<uint64_t>(i), u);
+  uuid4_words(a.seed, id_base + 3 * static_cast<uint64_t>(i), u);
 #pragma unroll
   for (int k = 0; k < 4; ++k) t.sess_uuid[slot * 4 + k] = u[k];
   uint8_t state = SS_CREATED;
@@ -159,8 +171,8 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
 
   // ---- saga: create, add_step, execute_step (executor is a device no-op) ----------
   uint32_t su[4], stu[4];
-  uuid4_words(a.seed, a.id_base + 3 * static_cast<uint64_t>(i) + 1, su);
-  uuid4_words(a.seed, a.id_base + 3 * static_cast<uint64_t>(i) + 2, stu);
+  uuid4_words(a.seed, id_base + 3 * static_cast<uint64_t>(i) + 1, su);
+  uuid4_words(a.seed, id_base + 3 * static_cast<uint64_t>(i) + 2, stu);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     t.saga_uuid[slot * 4 + k] = su[k];
