@@ -28,6 +28,12 @@ def load():
 
         if os.environ.get("AHV_SKIP_AUTOBUILD") != "1" and _build.needs_build():
             _build.build()
+        # torch-ROCm ships its own libamdhip64 / libhsa-runtime64 / librccl.  Load
+        # them first so the extension's NEEDED sonames bind to the *same* runtime
+        # objects torch uses; importing _C first would pull a second HIP runtime
+        # from /opt/rocm (and a second RCCL that sees no devices).
+        import torch  # noqa: F401
+
         _C = importlib.import_module("agent_hypervisor_amd._C")
         return _C
 

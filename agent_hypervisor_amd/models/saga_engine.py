@@ -1,0 +1,197 @@
+"""SagaBatchEngine: thousands of saga chains with compensation per launch
+(BASELINE config 4 — "10-step compensation chains, hipGraph-captured step loop").
+
+Semantics are the reference orchestrator's (saga/orchestrator.py:61-198), run
+for every saga of a batch at once — see ``csrc/include/ahv/saga_batch.h``.
+Executor and compensator outcomes are device tables (:class:`SagaOutcomes`),
+either supplied by the caller or drawn synthetically.
+
+Two launch shapes over the same element functions:
+
+* ``fused`` — one kernel runs each saga's whole chain (fastest);
+* ``step loop`` — the orchestrator's loop structure, one launch per phase and
+  step (init, K × execute, decide, K × compensate, finish), captured once into
+  a hipGraph and replayed (N07).  Results are identical to the fused path.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from datetime import datetime
+from typing import Optional
+
+import torch
+
+from agent_hypervisor_amd._native import C
+from hypervisor import _clock
+
+u8, i32, i64 = torch.uint8, torch.int32, torch.int64
+
+STEP_NAMES = ("pending", "executing", "committed", "compensating", "compensated", "compensation_failed", "failed")
+SAGA_NAMES = ("running", "compensating", "completed", "failed", "escalated")
+ERR_NONE, ERR_EXEC, ERR_TIMEOUT, ERR_NO_UNDO, ERR_COMP, ERR_COMP_TIMEOUT = range(6)
+NEVER = 255  # fail_attempts value: the step never succeeds
+
+
+@dataclass
+class SagaOutcomes:
+    """Per-(saga, step) executor / compensator behaviour, [S, K] u8 each."""
+
+    fail_attempts: torch.Tensor
+    fail_kind: torch.Tensor
+    comp_fail: torch.Tensor
+    has_undo: torch.Tensor
+    max_retries: torch.Tensor
+
+    @classmethod
+    def synthetic(cls, sagas: int, steps: int, p_fail: float = 0.02, p_comp_fail: float = 0.05,
+                  p_no_undo: float = 0.05, max_retries: int = 0, seed: int = 0, device="cpu") -> "SagaOutcomes":
+        """Random outcomes: each step fails outright with ``p_fail`` (retries do
+        not help), a compensation fails with ``p_comp_fail``, and a step lacks an
+        Undo_API with ``p_no_undo``."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        shape = (sagas, steps)
+        fa = torch.where(torch.rand(shape, generator=g) < p_fail, NEVER, 0).to(u8)
+        fk = torch.randint(1, 3, shape, generator=g, dtype=u8)
+        cf = torch.where(torch.rand(shape, generator=g) < p_comp_fail, torch.randint(1, 3, shape, generator=g), 0)
+        hu = (torch.rand(shape, generator=g) >= p_no_undo).to(u8)
+        mr = torch.full(shape, max_retries, dtype=u8)
+        return cls(*(t.to(u8).to(device) for t in (fa, fk, cf, hu, mr)))
+
+    def to(self, device) -> "SagaOutcomes":
+        return SagaOutcomes(*(getattr(self, f).to(device) for f in self.__dataclass_fields__))
+
+
+class SagaBatchEngine:
+    def __init__(self, sagas: int, steps: int = 10, device: str = "cuda", compensate: bool = True) -> None:
+        if not 1 <= steps <= 64:
+            raise ValueError("steps must be in [1, 64]")
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and not torch.cuda.is_available():
+            raise RuntimeError("SagaBatchEngine asked for a HIP device but none is visible")
+        self.S, self.K, self.compensate = sagas, steps, compensate
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=self.device)  # noqa: E731
+        sk = (sagas, steps)
+        self.step_state, self.retry_count, self.step_error = z(sk, u8), z(sk, u8), z(sk, u8)
+        self.started_us, self.completed_us = z(sk, i64), z(sk, i64)
+        self.saga_state, self.saga_completed_us = z(sagas, u8), z(sagas, i64)
+        self.failed_step, self.comp_failed, self.tick = z(sagas, i32), z(sagas, i32), z(sagas, i32)
+        self.stats = z(4, i64)
+        self.now_us = 0
+        self._graph = None
+        self._graph_outcomes = None
+
+    # -- argument block ------------------------------------------------------------
+    def _args(self, o: SagaOutcomes, now_us: int) -> dict:
+        for f in o.__dataclass_fields__:
+            t = getattr(o, f)
+            if t.shape != (self.S, self.K) or t.dtype != u8 or t.device != self.device or not t.is_contiguous():
+                raise ValueError(f"outcome table {f} must be contiguous u8 [{self.S}, {self.K}] on {self.device}")
+        d = dict(sagas=self.S, steps=self.K, compensate=int(self.compensate), now_us=int(now_us))
+        for f in o.__dataclass_fields__:
+            d[f] = getattr(o, f).data_ptr()
+        for f in ("step_state", "retry_count", "step_error", "started_us", "completed_us", "saga_state",
+                  "saga_completed_us", "failed_step", "comp_failed", "tick", "stats"):
+            d[f] = getattr(self, f).data_ptr()
+        return d
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    # -- fused ---------------------------------------------------------------------
+    def run(self, outcomes: SagaOutcomes, now_us: Optional[int] = None) -> torch.Tensor:
+        """Run every saga's chain in one launch; returns the [4] i64 counters
+        (completed, escalated, failed, compensated steps) of this batch."""
+        self.now_us = int(now_us if now_us is not None else _clock.now_us())
+        self.stats.zero_()
+        a = self._args(outcomes, self.now_us)
+        if self.device.type == "cuda":
+            C.saga_fused(a, self._stream())
+        else:
+            C.saga_fused_host(a)
+        return self.stats
+
+    # -- step loop -----------------------------------------------------------------
+    def _phase(self, a: dict, phase: int, k: int = 0) -> None:
+        if self.device.type == "cuda":
+            C.saga_phase(a, phase, k, self._stream())
+        else:
+            C.saga_phase_host(a, phase, k)
+
+    def _loop(self, a: dict) -> None:
+        self.stats.zero_()
+        self._phase(a, 0)
+        for k in range(self.K):
+            self._phase(a, 1, k)
+        self._phase(a, 2)
+        for k in range(self.K - 1, -1, -1):
+            self._phase(a, 3, k)
+        self._phase(a, 4)
+
+    def run_step_loop(self, outcomes: SagaOutcomes, now_us: Optional[int] = None, graph: bool = True) -> torch.Tensor:
+        """Orchestrator-shaped execution: 2K+3 launches, replayed from a hipGraph
+        on GPU when ``graph`` (captured on first use for these outcome tables)."""
+        self.now_us = int(now_us if now_us is not None else _clock.now_us())
+        a = self._args(outcomes, self.now_us)
+        if self.device.type != "cuda" or not graph:
+            self._loop(a)
+            return self.stats
+        if self._graph is None or self._graph_outcomes is not outcomes or self._graph_now != self.now_us:
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                self._loop(a)  # warm-up outside capture
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            torch.cuda.synchronize(self.device)
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._loop(a)
+            self._graph_outcomes, self._graph_now = outcomes, self.now_us
+        self._graph.replay()
+        return self.stats
+
+    def replay(self) -> torch.Tensor:
+        """Re-run the captured step loop (same outcome tables and time base)."""
+        if self._graph is None:
+            raise RuntimeError("no captured step loop")
+        self._graph.replay()
+        return self.stats
+
+    # -- host view -----------------------------------------------------------------
+    def materialize(self, s: int, saga_id: str = "", session_id: str = ""):
+        """Scalar-API :class:`hypervisor.saga.state_machine.Saga` for saga ``s``."""
+        from hypervisor.saga.state_machine import Saga, SagaState, SagaStep, StepState
+
+        st = self.step_state[s].cpu().tolist()
+        err = self.step_error[s].cpu().tolist()
+        rc = self.retry_count[s].cpu().tolist()
+        t0 = self.started_us[s].cpu().tolist()
+        t1 = self.completed_us[s].cpu().tolist()
+        ts = lambda us: _clock.from_us(us) if us else None  # noqa: E731
+        saga = Saga(saga_id=saga_id or f"saga:batch-{s}", session_id=session_id,
+                    state=SagaState(SAGA_NAMES[int(self.saga_state[s])]), created_at=_clock.from_us(self.now_us),
+                    completed_at=ts(int(self.saga_completed_us[s])))
+        for k in range(self.K):
+            step = SagaStep(step_id=f"step:{s}:{k}", action_id=f"action-{k}", agent_did="", execute_api="",
+                            state=StepState(STEP_NAMES[st[k]]), started_at=ts(t0[k]), completed_at=ts(t1[k]),
+                            retry_count=rc[k], error=self.error_text(err[k], k))
+            saga.steps.append(step)
+        nf = int(self.comp_failed[s])
+        if saga.state is SagaState.ESCALATED:
+            saga.error = f"{nf} step(s) failed compensation — Joint Liability slashing triggered"
+        return saga
+
+    @staticmethod
+    def error_text(code: int, k: int) -> Optional[str]:
+        return {
+            ERR_NONE: None,
+            ERR_EXEC: "executor failed",
+            ERR_TIMEOUT: f"Step step:{k} timed out",
+            ERR_NO_UNDO: "No Undo_API available",
+            ERR_COMP: "Compensation failed",
+            ERR_COMP_TIMEOUT: "Compensation timed out",
+        }[code]
+
+    def synchronize(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

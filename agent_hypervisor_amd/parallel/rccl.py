@@ -60,10 +60,15 @@ class Communicator:
             rank, world = dist.get_rank(group), dist.get_world_size(group)
         else:
             rank, world = 0, 1
+        dev = torch.cuda.current_device() if device is None else device
+        # RCCL's bootstrap queries the current HIP device: make sure torch has
+        # created its context on it first (torch initialises HIP lazily).
+        torch.cuda.set_device(dev)
+        torch.empty(1, device=torch.device("cuda", dev)).zero_()
+        torch.cuda.synchronize(dev)
         uid = [C.rccl_unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0, group=group)
-        dev = torch.cuda.current_device() if device is None else device
         return cls(rank, world, uid[0], dev)
 
     @staticmethod

@@ -9,6 +9,8 @@
 #include <pybind11/stl.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -121,7 +123,23 @@ class RcclComm {
 
 }  // namespace
 
+static std::string so_of(const void* sym) {
+  Dl_info info{};
+  if (dladdr(sym, &info) && info.dli_fname) return info.dli_fname;
+  return "?";
+}
+
 void register_comm(py::module_& m) {
+  m.def(
+      "runtime_libraries",
+      []() {
+        py::dict d;
+        d["hip"] = so_of(reinterpret_cast<const void*>(&hipGetDeviceCount));
+        d["rccl"] = so_of(reinterpret_cast<const void*>(&ncclGetUniqueId));
+        return d;
+      },
+      "Paths of the shared objects that provide HIP and RCCL to this extension "
+      "(they must be the ones torch loaded).");
   m.def("rccl_unique_id", []() {
     ncclUniqueId id;
     check_nccl(ncclGetUniqueId(&id), "ncclGetUniqueId");

@@ -10,6 +10,7 @@
 #include "ahv/kernels.h"
 #include "ahv/launch.h"
 #include "ahv/pipeline.h"
+#include "ahv/saga_batch.h"
 
 namespace py = pybind11;
 
@@ -225,6 +226,16 @@ static LockArgs to_locks(const py::dict& d) {
   P(req_res, const int32_t); P(req_agent, const int32_t); P(req_intent, const uint8_t); P(conflicts, int32_t);
   return a;
 }
+static SagaBatchArgs to_saga(const py::dict& d) {
+  SagaBatchArgs a{};
+  V(sagas, int64_t); V(steps, int32_t); V(compensate, int32_t); V(now_us, int64_t);
+  P(fail_attempts, const uint8_t); P(fail_kind, const uint8_t); P(comp_fail, const uint8_t);
+  P(has_undo, const uint8_t); P(max_retries, const uint8_t); P(step_state, uint8_t); P(retry_count, uint8_t);
+  P(step_error, uint8_t); P(started_us, int64_t); P(completed_us, int64_t); P(saga_state, uint8_t);
+  P(saga_completed_us, int64_t); P(failed_step, int32_t); P(comp_failed, int32_t); P(tick, int32_t);
+  P(stats, unsigned long long);
+  return a;
+}
 #undef P
 #undef V
 
@@ -271,6 +282,23 @@ void register_kernels(py::module_& m) {
   bind_pair(m, "verify", to_verify, launch_verify, verify_host);
   bind_pair(m, "vclock", to_vclock, launch_vclock, vclock_host);
   bind_pair(m, "locks", to_locks, launch_locks, locks_host);
+  bind_pair(m, "saga_fused", to_saga, launch_saga_fused, saga_fused_host);
+  m.def(
+      "saga_phase",
+      [](const py::dict& d, int phase, int k, uintptr_t stream) {
+        SagaBatchArgs a = to_saga(d);
+        py::gil_scoped_release nogil;
+        launch_saga_phase(a, phase, k, reinterpret_cast<hipStream_t>(stream));
+      },
+      py::arg("args"), py::arg("phase"), py::arg("k"), py::arg("stream"));
+  m.def(
+      "saga_phase_host",
+      [](const py::dict& d, int phase, int k) {
+        SagaBatchArgs a = to_saga(d);
+        py::gil_scoped_release nogil;
+        saga_phase_host(a, phase, k);
+      },
+      py::arg("args"), py::arg("phase"), py::arg("k"));
   m.def(
       "pipeline",
       [](const py::dict& d, uintptr_t stream) {

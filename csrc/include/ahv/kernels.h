@@ -319,4 +319,12 @@ struct LockArgs {
 void launch_locks(const LockArgs&, hipStream_t);
 void locks_host(const LockArgs&);
 
+// ------------------------------------------------------------------- sagas
+// K13/K14 batched saga chains (args and semantics in ahv/saga_batch.h)
+struct SagaBatchArgs;
+void launch_saga_fused(const SagaBatchArgs&, hipStream_t);
+void saga_fused_host(const SagaBatchArgs&);
+void launch_saga_phase(const SagaBatchArgs&, int phase, int k, hipStream_t);
+void saga_phase_host(const SagaBatchArgs&, int phase, int k);
+
 }  // namespace ahv
