@@ -4,7 +4,7 @@ saga/checkpoint.py:32-36)."""
 
 from __future__ import annotations
 
-from typing import Sequence
+from typing import Optional, Sequence
 
 import torch
 
@@ -89,6 +89,67 @@ def verify_chains(
         dict(bytes=u8, offsets=i64, stored=i32, parent=i32, has_parent=u8, chain_offsets=i32),
     )
     return dok, cok
+
+
+_PARENT_MARK = "@@ahv-parent-field@@"
+
+
+def _split_payload(d) -> tuple[bytes, bytes]:
+    """Canonical payload of ``d`` split around its parent_hash value."""
+    import dataclasses
+
+    from hypervisor.audit.delta import canonical_payload
+
+    marked = dataclasses.replace(d, parent_hash=_PARENT_MARK)
+    text = canonical_payload(marked).decode("ascii")
+    import json
+
+    pieces = text.split(json.dumps(_PARENT_MARK))
+    if len(pieces) != 2:
+        raise ValueError(f"delta {d.delta_id} contains the parent placeholder text")
+    return pieces[0].encode(), pieces[1].encode()
+
+
+def pack_chains(chains, device="cpu") -> dict:
+    """Pack lists of SemanticDelta (one list per chain) for :func:`chain_hashes`:
+    each payload is stored as (prefix, suffix) around the parent field."""
+    parts, pre_off, pre_len, suf_off, suf_len, offs = [], [], [], [], [], [0]
+    pos = 0
+    for chain in chains:
+        for d in chain:
+            pre, suf = _split_payload(d)
+            pre_off.append(pos)
+            pre_len.append(len(pre))
+            parts.append(pre)
+            pos += len(pre)
+            suf_off.append(pos)
+            suf_len.append(len(suf))
+            parts.append(suf)
+            pos += len(suf)
+        offs.append(len(pre_off))
+    arena = b"".join(parts) or b"\0"
+    t = lambda xs, dt: torch.tensor(xs, dtype=dt, device=device)  # noqa: E731
+    return dict(
+        bytes=torch.frombuffer(bytearray(arena), dtype=u8).to(device),
+        chain_offsets=t(offs, i32), pre_off=t(pre_off, i64), pre_len=t(pre_len, i32),
+        suf_off=t(suf_off, i64), suf_len=t(suf_len, i32),
+    )
+
+
+def chain_hashes(packed: dict, seed_parent: Optional[torch.Tensor] = None,
+                 has_seed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K08: re-derive every delta hash of every chain (parent links recomputed
+    from the chain itself) → int32 [D, 8]."""
+    D = packed["pre_off"].numel()
+    out = torch.empty((D, 8), dtype=i32, device=packed["bytes"].device)
+    launch(
+        "chain_hash",
+        {"chains": packed["chain_offsets"].numel() - 1},
+        dict(packed, seed_parent=seed_parent, has_seed=has_seed, digest=out),
+        dict(bytes=u8, chain_offsets=i32, pre_off=i64, pre_len=i32, suf_off=i64, suf_len=i32,
+             seed_parent=i32, has_seed=u8),
+    )
+    return out
 
 
 def pack_delta_engines(engines, device="cpu"):

@@ -226,6 +226,13 @@ static LockArgs to_locks(const py::dict& d) {
   P(req_res, const int32_t); P(req_agent, const int32_t); P(req_intent, const uint8_t); P(conflicts, int32_t);
   return a;
 }
+static ChainHashArgs to_chain_hash(const py::dict& d) {
+  ChainHashArgs a{};
+  V(chains, int64_t); P(chain_offsets, const int32_t); P(bytes, const uint8_t); P(pre_off, const int64_t);
+  P(pre_len, const int32_t); P(suf_off, const int64_t); P(suf_len, const int32_t);
+  P(seed_parent, const uint32_t); P(has_seed, const uint8_t); P(digest, uint32_t);
+  return a;
+}
 static SagaBatchArgs to_saga(const py::dict& d) {
   SagaBatchArgs a{};
   V(sagas, int64_t); V(steps, int32_t); V(compensate, int32_t); V(now_us, int64_t);
@@ -283,6 +290,7 @@ void register_kernels(py::module_& m) {
   bind_pair(m, "vclock", to_vclock, launch_vclock, vclock_host);
   bind_pair(m, "locks", to_locks, launch_locks, locks_host);
   bind_pair(m, "saga_fused", to_saga, launch_saga_fused, saga_fused_host);
+  bind_pair(m, "chain_hash", to_chain_hash, launch_chain_hash, chain_hash_host);
   m.def(
       "saga_phase",
       [](const py::dict& d, int phase, int k, uintptr_t stream) {

@@ -284,6 +284,25 @@ struct VerifyArgs {
 void launch_verify(const VerifyArgs&, hipStream_t);
 void verify_host(const VerifyArgs&);
 
+// K08 — delta hash chains: digest_i = sha256(prefix_i ‖ parent_i ‖ suffix_i)
+// where parent_i is the JSON text `null` for a chain's first delta (or the
+// quoted hex of seed_parent when has_seed) and `"<hex of digest_{i-1}>"`
+// otherwise.  Serial within a chain, one lane per chain.
+struct ChainHashArgs {
+  int64_t chains;
+  const int32_t* chain_offsets;  // [chains+1] delta ranges
+  const uint8_t* bytes;          // arena
+  const int64_t* pre_off;        // [D]
+  const int32_t* pre_len;        // [D]
+  const int64_t* suf_off;        // [D]
+  const int32_t* suf_len;        // [D]
+  const uint32_t* seed_parent;   // [chains, 8] or null
+  const uint8_t* has_seed;       // [chains] or null
+  uint32_t* digest;              // [D, 8] out
+};
+void launch_chain_hash(const ChainHashArgs&, hipStream_t);
+void chain_hash_host(const ChainHashArgs&);
+
 // ---------------------------------------------------------------- sessions
 
 // K19 — vector clocks: dense clocks [paths, A] and [agents, A] (A ≤ 64, one

@@ -11,7 +11,7 @@ mkdir -p $OUT
 STEPS=${STEPS:-all}
 echo "[gpu_check] $(date) host=$(hostname) steps=$STEPS"
 rocm-smi --showproductname > $OUT/rocm_smi.txt 2>&1 || true
-run_tests() { timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1; }
+run_tests() { timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1; }
 run_smoke() { timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1; }
 run_bench() { timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-10} --warmup 2 ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; }
 run_prof() {

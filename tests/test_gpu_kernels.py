@@ -161,6 +161,20 @@ def test_audit_kernels(cuda_device):
             parent.append(hexes[i - 1] if i != chain_offs[c] else "0" * 64)
     for k in rng.sample(range(4000), 40):
         hexes[k] = "ab" * 32
+    # K08 chain re-derivation: device == host on real delta chains
+    from hypervisor.audit.delta import DeltaEngine, VFSChange
+
+    chains = []
+    for s in range(300):
+        de = DeltaEngine(f"session:{s}")
+        for t in range(rng.randint(1, 12)):
+            de.capture(f"did:a{t}", [VFSChange(f"/p{t}", "modify", f"h{t}", f"g{t}")])
+        chains.append(de.deltas)
+    packed = A.pack_chains(chains)
+    hc = A.chain_hashes(packed)
+    hd = A.chain_hashes({k: v.cuda() for k, v in packed.items()})
+    assert torch.equal(hc, hd.cpu())
+    assert A.digests_to_hex(hc) == [d.delta_hash for c in chains for d in c]
     d, o = A.pack_bytes(pays)
     _check(lambda *t: A.verify_chains(*t), d, o, A.hex_to_digests(hexes), A.hex_to_digests(parent),
            torch.tensor(has_parent, dtype=u8), torch.tensor(chain_offs, dtype=i32))

@@ -18,8 +18,8 @@ from hypervisor import _clock
 T0 = datetime(2026, 6, 1, 9, 0, tzinfo=timezone.utc)
 
 
-def _engine(device, seed=11):
-    eng = GovernanceEngine(device=device, session_capacity=1000, agent_capacity=256, seed=seed)
+def _engine(device, seed=11, capacity=1000):
+    eng = GovernanceEngine(device=device, session_capacity=capacity, agent_capacity=256, seed=seed)
     eng.register_synthetic_agents(200, seed=3)
     return eng
 
@@ -60,7 +60,7 @@ def test_wraparound_cursor_cpu():
 @pytest.mark.gpu
 def test_graph_replay_matches_host_twin(cuda_device):
     n = 4096
-    dev_eng = _engine(str(cuda_device), seed=99)
+    dev_eng = _engine(str(cuda_device), seed=99, capacity=10_000)
     agents = torch.randint(0, 200, (n,), dtype=torch.int32, device=cuda_device)
     stats = torch.zeros(6, dtype=torch.int64, device=cuda_device)
     pg = PipelineGraph(dev_eng, n, agents, stats=stats)
@@ -70,7 +70,7 @@ def test_graph_replay_matches_host_twin(cuda_device):
     torch.cuda.synchronize(cuda_device)
     assert stats.tolist()[:2] == [n, n]
     last = pg.last_batch()
-    host = _engine("cpu", seed=99)
+    host = _engine("cpu", seed=99, capacity=10_000)
     host._next_slot, host._id_counter = last.slot_base, last.id_base
     ref = host.run_pipeline(n, agents=agents.cpu(), deltas=3, now_us=last.now_us)
     assert torch.equal(last.roots().cpu(), ref.roots())

@@ -246,6 +246,20 @@ def _delta_engines(n=12, seed=9):
     return engines
 
 
+def test_chain_hashes_rederive_delta_engine_chains():
+    engines = _delta_engines(seed=21)
+    packed = A.pack_chains([de.deltas for de in engines])
+    got = A.digests_to_hex(A.chain_hashes(packed))
+    want = [d.delta_hash for de in engines for d in de.deltas]
+    assert got == want
+    # continuing a chain from a seed parent: hash the tail of each chain alone
+    tails = [de.deltas[2:] for de in engines if len(de.deltas) > 2]
+    seeds = [de.deltas[1].delta_hash for de in engines if len(de.deltas) > 2]
+    p2 = A.pack_chains(tails)
+    got2 = A.chain_hashes(p2, A.hex_to_digests(seeds), torch.ones(len(seeds), dtype=u8))
+    assert A.digests_to_hex(got2) == [d.delta_hash for t in tails for d in t]
+
+
 def test_merkle_roots_match_delta_engine():
     engines = _delta_engines()
     leaves, offs = [], [0]
