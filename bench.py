@@ -79,7 +79,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--sessions", type=int, default=1 << 18, help="sessions per GPU per step")
+    ap.add_argument("--sessions", type=int, default=1 << 20, help="sessions per GPU per step")
     ap.add_argument("--agents", type=int, default=1 << 20, help="synthetic agents per GPU")
     ap.add_argument("--deltas", type=int, default=3)
     ap.add_argument("--scalar-iters", type=int, default=2000)

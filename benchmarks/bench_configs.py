@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Batched device benchmarks for BASELINE.json configs 2–5.
+
+  config2  10k concurrent sessions: full governance pipeline (ring gate +
+           Merkle audit) + σ_eff on fp64 MFMA bond tiles + ring re-gate,
+           hipGraph-replayed — latency per batch and sessions/s
+  config3  1M agents / 100k sessions sharded over the ranks (DP) with the
+           cross-session vouch exposure all-reduce (X01, [A] fp64 over RCCL)
+  config4  saga orchestrator: 10-step compensation chains, fused kernel and
+           the hipGraph-captured step loop
+  config5  liability slash storm: 10M vouch-bond updates (K06 cascade, bonds
+           released) + σ_eff recompute + full delta re-chain (K08) and Merkle
+           roots (K09) of the affected sessions
+
+Each prints one JSON line per measurement.  ``--device cpu`` runs the host
+twins at small scale (harness check).  Multi-rank: launch with
+``torch.distributed.run`` (config3 is the one that communicates).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from agent_hypervisor_amd.models.engine import GovernanceEngine  # noqa: E402
+from agent_hypervisor_amd.models.saga_engine import SagaBatchEngine, SagaOutcomes  # noqa: E402
+from agent_hypervisor_amd.ops import audit as A  # noqa: E402
+from agent_hypervisor_amd.ops import liability as LI  # noqa: E402
+from agent_hypervisor_amd.ops import rings as R  # noqa: E402
+from agent_hypervisor_amd.parallel import collectives as X  # noqa: E402
+from agent_hypervisor_amd.parallel.directory import shard_counts  # noqa: E402
+from agent_hypervisor_amd.runtime.graphs import PipelineGraph  # noqa: E402
+
+f64, u8, i32, i64 = torch.float64, torch.uint8, torch.int32, torch.int64
+
+
+class Ctx:
+    def __init__(self, device: str):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if device == "cuda":
+            torch.cuda.set_device(local)
+            self.dev = torch.device("cuda", local)
+        else:
+            self.dev = torch.device("cpu")
+        if self.world > 1 and not dist.is_initialized():
+            if self.dev.type == "cuda":
+                dist.init_process_group("nccl", rank=self.rank, world_size=self.world, device_id=self.dev)
+            else:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+
+    def sync(self):
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def timed(self, fn, steps: int, warmup: int) -> tuple[float, list[float]]:
+        for _ in range(warmup):
+            fn()
+        self.sync()
+        lat = []
+        for _ in range(max(3, min(10, steps))):
+            t0 = time.perf_counter()
+            fn()
+            self.sync()
+            lat.append(time.perf_counter() - t0)
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        self.sync()
+        self.barrier()
+        el = time.perf_counter() - t0
+        if self.world > 1:
+            e = torch.tensor([el], dtype=f64, device=self.dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el, lat
+
+    def emit(self, **kw):
+        if self.rank == 0:
+            kw.setdefault("n_gpus", self.world)
+            kw.setdefault("device", str(self.dev))
+            print(json.dumps(kw), flush=True)
+
+
+def random_vouch_batch(S: int, edges_per_session: int, dev, seed: int = 0) -> LI.VouchBatch:
+    g = torch.Generator().manual_seed(seed)
+    E = S * edges_per_session
+    vr = torch.randint(0, 16, (E,), generator=g, dtype=torch.int64)
+    ve = (vr + torch.randint(1, 16, (E,), generator=g)) % 16  # never self
+    return LI.VouchBatch(
+        offsets=(torch.arange(S + 1, dtype=i64) * edges_per_session).to(i32).to(dev),
+        voucher=vr.to(u8).to(dev), vouchee=ve.to(u8).to(dev),
+        bonded=(torch.rand(E, generator=g, dtype=f64) * 0.2).to(dev),
+        active=torch.ones(E, dtype=u8, device=dev), expiry_us=torch.full((E,), -1, dtype=i64, device=dev),
+        released_us=torch.zeros(E, dtype=i64, device=dev),
+    )
+
+
+# ------------------------------------------------------------------ config 2
+
+
+def config2(ctx: Ctx, args):
+    S = args.sessions or 10_000
+    eng = GovernanceEngine(device=str(ctx.dev), session_capacity=4 * S, agent_capacity=max(S, 1024), seed=0xC2)
+    eng.register_synthetic_agents(max(S, 1024), seed=2)
+    agents = torch.randint(0, max(S, 1024), (S,), dtype=i32, device=ctx.dev)
+    stats = torch.zeros(6, dtype=i64, device=ctx.dev)
+    pg = PipelineGraph(eng, S, agents, stats=stats)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    tiles = (torch.rand((S, 16, 16), generator=g, dtype=f64) * 0.05).to(ctx.dev)
+    sigma = torch.rand((S, 16), generator=g, dtype=f64).to(ctx.dev)
+    omega = torch.full((S,), 0.5, dtype=f64, device=ctx.dev)
+
+    def step():
+        pg.step()
+        se, expo, _ = LI.bond_tiles(tiles, sigma, omega)
+        R.ring_gate(se.reshape(-1))
+
+    el, lat = ctx.timed(step, args.steps, args.warmup)
+    ctx.emit(config="config2", what="pipeline+sigma_eff(MFMA)+ring_gate", sessions_per_step=S,
+             batch_p50_ms=statistics.median(lat) * 1e3, ms_per_step=el / args.steps * 1e3,
+             sessions_per_s=S * ctx.world * args.steps / el, graph=pg.use_graph,
+             ok=int(stats[1].item()) == S)
+
+
+# ------------------------------------------------------------------ config 3
+
+
+def config3(ctx: Ctx, args):
+    A_ = args.agents or 1_000_000
+    S = shard_counts(args.sessions or 100_000, ctx.world)[ctx.rank]
+    eng = GovernanceEngine(device=str(ctx.dev), session_capacity=4 * S, agent_capacity=A_, seed=0xC3 + ctx.rank)
+    eng.register_synthetic_agents(A_, seed=7)  # the same global agent population on every rank
+    gen = torch.Generator(device=ctx.dev).manual_seed(11 + ctx.rank)
+    stats = torch.zeros(6, dtype=i64, device=ctx.dev)
+    vb = random_vouch_batch(S, 8, ctx.dev, seed=ctx.rank)
+    # participants of each session → global agent ids (for the agent-indexed exposure view)
+    members = torch.randint(0, A_, (S, 16), device=ctx.dev, generator=gen)
+    sigma = eng.agents.sigma[members]
+    omega = torch.full((S,), 0.5, dtype=f64, device=ctx.dev)
+    exposure = torch.zeros(A_, dtype=f64, device=ctx.dev)
+
+    def step():
+        stats.zero_()
+        agents = torch.randint(0, A_, (S,), device=ctx.dev, dtype=i32, generator=gen)
+        eng.run_pipeline(S, agents=agents, stats=stats)
+        tiles = LI.build_tiles(vb, 0)
+        _, expo, _ = LI.bond_tiles(tiles, sigma, omega)
+        exposure.zero_()
+        exposure.index_add_(0, members.reshape(-1), expo.reshape(-1))
+        X.allreduce_exposure(exposure)  # X01 over RCCL / xGMI
+        X.allreduce_stats(stats)
+
+    el, lat = ctx.timed(step, args.steps, args.warmup)
+    ctx.emit(config="config3", what="pipeline+vouch tiles+exposure all_reduce[A]", agents=A_,
+             sessions_global=args.sessions or 100_000, sessions_per_rank=S, exposure_bytes=A_ * 8,
+             batch_p50_ms=statistics.median(lat) * 1e3, ms_per_step=el / args.steps * 1e3,
+             sessions_per_s=(args.sessions or 100_000) * args.steps / el, scaling="strong",
+             parallelism=f"dp{ctx.world}")
+
+
+# ------------------------------------------------------------------ config 4
+
+
+def config4(ctx: Ctx, args):
+    S = args.sessions or 1_000_000
+    K = 10
+    o = SagaOutcomes.synthetic(S, K, p_fail=0.03, p_comp_fail=0.05, p_no_undo=0.05, max_retries=1,
+                               seed=ctx.rank).to(ctx.dev)
+    fused = SagaBatchEngine(S, K, device=str(ctx.dev))
+    el, lat = ctx.timed(lambda: fused.run(o, now_us=1), args.steps, args.warmup)
+    st = fused.stats.cpu().tolist()
+    ctx.emit(config="config4", mode="fused", sagas=S, steps_per_saga=K, ms_per_batch=el / args.steps * 1e3,
+             batch_p50_ms=statistics.median(lat) * 1e3, sagas_per_s=S * ctx.world * args.steps / el,
+             completed=st[0], escalated=st[1], compensated_steps=st[3])
+    loop = SagaBatchEngine(S, K, device=str(ctx.dev))
+    loop.run_step_loop(o, now_us=1)
+    el, lat = ctx.timed(loop.replay if ctx.dev.type == "cuda" else (lambda: loop.run_step_loop(o, now_us=1)),
+                        args.steps, args.warmup)
+    ctx.emit(config="config4", mode="hipgraph_step_loop", launches_per_batch=2 * K + 3, sagas=S,
+             ms_per_batch=el / args.steps * 1e3, batch_p50_ms=statistics.median(lat) * 1e3,
+             sagas_per_s=S * ctx.world * args.steps / el)
+
+
+# ------------------------------------------------------------------ config 5
+
+
+def config5(ctx: Ctx, args):
+    E_total = args.edges or 10_000_000
+    per = 16
+    S = E_total // per
+    vb0 = random_vouch_batch(S, per, ctx.dev, seed=5)
+    g = torch.Generator().manual_seed(9)
+    tgt = torch.randint(0, 16, (S,), generator=g, dtype=u8).to(ctx.dev)
+    omega = torch.full((S,), 0.95, dtype=f64, device=ctx.dev)
+    scores0 = torch.rand((S, 16), generator=g, dtype=f64).to(ctx.dev)
+    # audit chains of the same sessions (3 deltas each) for the re-chain
+    D = args.deltas or 3
+    from hypervisor.audit.delta import DeltaEngine, VFSChange
+
+    proto = DeltaEngine("session:slash-storm")
+    for k in range(D):
+        proto.capture("did:mesh:agent", [VFSChange(f"/f{k}", "add", f"h{k}")])
+    one = A.pack_chains([proto.deltas])
+    # every session re-chains the same-shaped payloads (tiled arena → S chains)
+    chains_n = S
+    Lb = one["bytes"].numel()
+    packed = {
+        "bytes": one["bytes"].to(ctx.dev),
+        "chain_offsets": (torch.arange(chains_n + 1, dtype=i64) * D).to(i32).to(ctx.dev),
+        "pre_off": one["pre_off"].repeat(chains_n).to(ctx.dev),
+        "pre_len": one["pre_len"].repeat(chains_n).to(ctx.dev),
+        "suf_off": one["suf_off"].repeat(chains_n).to(ctx.dev),
+        "suf_len": one["suf_len"].repeat(chains_n).to(ctx.dev),
+    }
+    leaves_offs = packed["chain_offsets"]
+
+    def step():
+        vb = vb0.clone()
+        out = LI.slash(vb, tgt, omega, scores0.clone(), 1)
+        se = LI.sigma_eff_exact(vb, out.scores.nan_to_num(0.0), omega, 1)
+        digests = A.chain_hashes(packed)
+        A.merkle_roots(leaves_offs, digests)
+        return se
+
+    el, lat = ctx.timed(step, args.steps, args.warmup)
+    ctx.emit(config="config5", what="slash cascade + sigma_eff + re-chain + merkle", bond_edges=S * per,
+             sessions=S, deltas_rechained=S * D, arena_bytes=Lb, ms_per_storm=el / args.steps * 1e3,
+             storm_p50_ms=statistics.median(lat) * 1e3, bond_updates_per_s=S * per * ctx.world * args.steps / el)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("configs", nargs="*", default=["config2", "config3", "config4", "config5"])
+    ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sessions", type=int, default=0, help="override the config's session/saga count")
+    ap.add_argument("--agents", type=int, default=0)
+    ap.add_argument("--edges", type=int, default=0)
+    ap.add_argument("--deltas", type=int, default=0)
+    args = ap.parse_args()
+    ctx = Ctx(args.device)
+    for c in args.configs:
+        {"config2": config2, "config3": config3, "config4": config4, "config5": config5}[c](ctx, args)
+    if ctx.world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
