@@ -71,27 +71,49 @@ class SagaBatchEngine:
             raise RuntimeError("SagaBatchEngine asked for a HIP device but none is visible")
         self.S, self.K, self.compensate = sagas, steps, compensate
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=self.device)  # noqa: E731
-        sk = (sagas, steps)
-        self.step_state, self.retry_count, self.step_error = z(sk, u8), z(sk, u8), z(sk, u8)
-        self.started_us, self.completed_us = z(sk, i64), z(sk, i64)
+        # per-step state is step-major [K, S] (coalesced per-step access, see
+        # saga_batch.h saga_elem); the public views below are [S, K]
+        ks = (steps, sagas)
+        self._step_state, self._retry_count, self._step_error = z(ks, u8), z(ks, u8), z(ks, u8)
+        self._started_us, self._completed_us = z(ks, i64), z(ks, i64)
         self.saga_state, self.saga_completed_us = z(sagas, u8), z(sagas, i64)
         self.failed_step, self.comp_failed, self.tick = z(sagas, i32), z(sagas, i32), z(sagas, i32)
         self.stats = z(4, i64)
         self.now_us = 0
         self._graph = None
         self._graph_outcomes = None
+        self._prep_src = None
+        self._prep = None
+
+    step_state = property(lambda self: self._step_state.t())
+    retry_count = property(lambda self: self._retry_count.t())
+    step_error = property(lambda self: self._step_error.t())
+    started_us = property(lambda self: self._started_us.t())
+    completed_us = property(lambda self: self._completed_us.t())
 
     # -- argument block ------------------------------------------------------------
-    def _args(self, o: SagaOutcomes, now_us: int) -> dict:
+    def _prepared(self, o: SagaOutcomes) -> dict:
+        """Outcome tables transposed once to the kernels' [K, S] layout (cached,
+        so captured graphs keep reading live buffers)."""
+        if self._prep_src is o:
+            return self._prep
+        prep = {}
         for f in o.__dataclass_fields__:
             t = getattr(o, f)
-            if t.shape != (self.S, self.K) or t.dtype != u8 or t.device != self.device or not t.is_contiguous():
-                raise ValueError(f"outcome table {f} must be contiguous u8 [{self.S}, {self.K}] on {self.device}")
+            if t.shape != (self.S, self.K) or t.dtype != u8 or t.device != self.device:
+                raise ValueError(f"outcome table {f} must be u8 [{self.S}, {self.K}] on {self.device}")
+            prep[f] = t.t().contiguous()
+        self._prep_src, self._prep = o, prep
+        return prep
+
+    def _args(self, o: SagaOutcomes, now_us: int) -> dict:
+        prep = self._prepared(o)
         d = dict(sagas=self.S, steps=self.K, compensate=int(self.compensate), now_us=int(now_us))
-        for f in o.__dataclass_fields__:
-            d[f] = getattr(o, f).data_ptr()
-        for f in ("step_state", "retry_count", "step_error", "started_us", "completed_us", "saga_state",
-                  "saga_completed_us", "failed_step", "comp_failed", "tick", "stats"):
+        for f, t in prep.items():
+            d[f] = t.data_ptr()
+        for f in ("_step_state", "_retry_count", "_step_error", "_started_us", "_completed_us"):
+            d[f[1:]] = getattr(self, f).data_ptr()
+        for f in ("saga_state", "saga_completed_us", "failed_step", "comp_failed", "tick", "stats"):
             d[f] = getattr(self, f).data_ptr()
         return d
 

@@ -45,13 +45,13 @@ struct SagaBatchArgs {
   int32_t steps;         // K
   int32_t compensate;    // compensate on failure (else saga → FAILED)
   int64_t now_us;
-  // inputs [S*K]
+  // inputs [K, S] (step-major, see saga_elem)
   const uint8_t* fail_attempts;
   const uint8_t* fail_kind;
   const uint8_t* comp_fail;
   const uint8_t* has_undo;
   const uint8_t* max_retries;
-  // state [S*K]
+  // state [K, S]
   uint8_t* step_state;
   uint8_t* retry_count;
   uint8_t* step_error;
@@ -66,9 +66,16 @@ struct SagaBatchArgs {
   unsigned long long* stats;  // [4] completed, escalated, failed, compensated steps (or null)
 };
 
+// Per-step tables are step-major, [K][S]: lane s of a wave touches element
+// k*S + s, so every per-step access of a wave is one contiguous (coalesced)
+// segment instead of a stride-K gather.
+AHV_HD inline int64_t saga_elem(const SagaBatchArgs& a, int64_t s, int k) {
+  return static_cast<int64_t>(k) * a.sagas + s;
+}
+
 AHV_HD inline void saga_init(const SagaBatchArgs& a, int64_t s) {
   for (int k = 0; k < a.steps; ++k) {
-    const int64_t e = s * a.steps + k;
+    const int64_t e = saga_elem(a, s, k);
     a.step_state[e] = ST_PENDING;
     a.retry_count[e] = 0;
     a.step_error[e] = SE_NONE;
@@ -85,7 +92,7 @@ AHV_HD inline void saga_init(const SagaBatchArgs& a, int64_t s) {
 // Forward pass for step k (no-op once the saga has stopped).
 AHV_HD inline void saga_exec_step(const SagaBatchArgs& a, int64_t s, int k, int32_t& tick) {
   if (a.saga_state[s] != SG_RUNNING || a.failed_step[s] >= 0) return;
-  const int64_t e = s * a.steps + k;
+  const int64_t e = saga_elem(a, s, k);
   const int attempts = 1 + a.max_retries[e];
   const int fails = a.fail_attempts[e];
   uint8_t st = a.step_state[e];
@@ -128,7 +135,7 @@ AHV_HD inline void saga_decide(const SagaBatchArgs& a, int64_t s, int32_t& tick)
 // Compensation of step k (called for k = K-1 … 0).
 AHV_HD inline void saga_comp_step(const SagaBatchArgs& a, int64_t s, int k, int32_t& tick) {
   if (a.saga_state[s] != SG_COMPENSATING) return;
-  const int64_t e = s * a.steps + k;
+  const int64_t e = saga_elem(a, s, k);
   if (a.step_state[e] != ST_COMMITTED) return;
   if (!a.has_undo[e]) {
     a.step_state[e] = ST_COMPENSATION_FAILED;  // direct assignment, no completion stamp (reference)
@@ -163,7 +170,7 @@ AHV_HD inline SagaCounters saga_counters(const SagaBatchArgs& a, int64_t s) {
   c.completed = g == SG_COMPLETED;
   c.escalated = g == SG_ESCALATED;
   c.failed = g == SG_FAILED;
-  for (int k = 0; k < a.steps; ++k) c.compensated += a.step_state[s * a.steps + k] == ST_COMPENSATED;
+  for (int k = 0; k < a.steps; ++k) c.compensated += a.step_state[saga_elem(a, s, k)] == ST_COMPENSATED;
   return c;
 }
 
