@@ -1,0 +1,383 @@
+"""On-disk session-state + Merkle-audit format and resume.
+
+The reference keeps everything in memory (state_machine.py:1-6 promises crash
+recovery that does not exist).  Two checkpoint kinds share one layout — a
+directory with a versioned ``manifest.json`` listing every file with its
+SHA-256:
+
+engine checkpoint (device tables of a :class:`GovernanceEngine`)
+    ``tables.safetensors``  every SoA column (sessions, agents, vouch edges),
+                            columnar, loaded with a loader that executes nothing
+    ``interner.json``       the string pool in id order (ids are positions)
+    ``engine.json``         counters, seed, capacities, change specs
+
+hypervisor checkpoint (the scalar :class:`hypervisor.Hypervisor` state)
+    ``sessions.jsonl``      one record per session: config, lifecycle, VFS
+                            files/ACLs, reversibility entries, sagas (full step
+                            state), and the audit log as *canonical-JSON delta
+                            records* — the exact bytes that were hashed, so the
+                            log verifies itself
+    ``liability.json``      vouch records in creation order
+    ``commitments.json``    Merkle commitments
+
+Resume = verify file digests → load tables / rebuild the interner (or the
+sessions) → re-verify every audit chain (hashes from the stored payloads,
+parent links, Merkle roots against commitments) → continue.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+from datetime import datetime
+from typing import Any, Optional
+
+import torch
+
+FORMAT = "ahv-checkpoint"
+VERSION = 1
+
+
+class CheckpointError(Exception):
+    """Missing, corrupt or inconsistent checkpoint."""
+
+
+# ------------------------------------------------------------------ helpers
+
+
+def _sha(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def _write_manifest(d: str, kind: str, files: list[str], extra: Optional[dict] = None) -> None:
+    man = {
+        "format": FORMAT,
+        "version": VERSION,
+        "kind": kind,
+        "files": {f: _sha(os.path.join(d, f)) for f in files},
+        **(extra or {}),
+    }
+    tmp = os.path.join(d, "manifest.json.tmp")
+    with open(tmp, "w") as f:
+        json.dump(man, f, indent=2, sort_keys=True)
+    os.replace(tmp, os.path.join(d, "manifest.json"))  # manifest last: a checkpoint is complete iff it exists
+
+
+def read_manifest(d: str, kind: str) -> dict:
+    p = os.path.join(d, "manifest.json")
+    if not os.path.exists(p):
+        raise CheckpointError(f"{d}: no manifest.json (incomplete checkpoint)")
+    with open(p) as f:
+        man = json.load(f)
+    if man.get("format") != FORMAT:
+        raise CheckpointError(f"{d}: not an {FORMAT} directory")
+    if man.get("version", 0) > VERSION:
+        raise CheckpointError(f"{d}: format version {man['version']} is newer than supported {VERSION}")
+    if man.get("kind") != kind:
+        raise CheckpointError(f"{d}: checkpoint kind {man.get('kind')!r}, expected {kind!r}")
+    for f, digest in man["files"].items():
+        fp = os.path.join(d, f)
+        if not os.path.exists(fp):
+            raise CheckpointError(f"{d}: missing {f}")
+        if _sha(fp) != digest:
+            raise CheckpointError(f"{d}: {f} is corrupt (sha256 mismatch)")
+    return man
+
+
+def _iso(t: Optional[datetime]) -> Optional[str]:
+    return t.isoformat() if t is not None else None
+
+
+def _dt(s: Optional[str]) -> Optional[datetime]:
+    return datetime.fromisoformat(s) if s else None
+
+
+def _jsonable(x: Any) -> Any:
+    try:
+        json.dumps(x)
+        return x
+    except (TypeError, ValueError):
+        return {"__repr__": repr(x)}
+
+
+# ------------------------------------------------------------ engine tables
+
+
+def save_engine(engine, d: str) -> str:
+    """Write an engine checkpoint into directory ``d`` (created)."""
+    from safetensors.torch import save_file
+
+    from agent_hypervisor_amd.models.tables import SessionTable
+
+    os.makedirs(d, exist_ok=True)
+    engine.synchronize()
+    tensors = {f"sessions.{k}": getattr(engine.sessions, k).detach().cpu().contiguous() for k in SessionTable.COLUMNS}
+    n = engine.agents.count
+    tensors["agents.sigma"] = engine.agents.sigma[:n].cpu().contiguous()
+    tensors["agents.did"] = engine.agents.did[:n].cpu().contiguous()
+    v = engine.vouches
+    for f in ("voucher", "vouchee", "session", "bonded", "pct", "active", "expiry_us", "released_us"):
+        tensors[f"vouches.{f}"] = getattr(v, f)[: v.count].cpu().contiguous()
+    save_file(tensors, os.path.join(d, "tables.safetensors"), metadata={"format": FORMAT, "version": str(VERSION)})
+    with open(os.path.join(d, "interner.json"), "w") as f:
+        json.dump([engine.interner.str(i) for i in range(len(engine.interner))], f)
+    meta = {
+        "session_capacity": engine.sessions.capacity,
+        "dmax": engine.sessions.dmax,
+        "agent_capacity": engine.agents.capacity,
+        "agent_count": n,
+        "vouch_capacity": int(v.voucher.numel()),
+        "vouch_count": v.count,
+        "seed": engine.seed,
+        "creator_id": engine.creator_id,
+        "next_slot": engine._next_slot,
+        "id_counter": engine._id_counter,
+        "last_specs": engine._last_specs,
+    }
+    with open(os.path.join(d, "engine.json"), "w") as f:
+        json.dump(meta, f, indent=2)
+    _write_manifest(d, "engine", ["tables.safetensors", "interner.json", "engine.json"])
+    return d
+
+
+def load_engine(d: str, device: Optional[str] = None, verify: bool = True):
+    """Resume a :class:`GovernanceEngine` from ``d``; with ``verify`` the Merkle
+    root of every archived session is recomputed on ``device`` from its stored
+    delta digests (K09) and compared with the stored root."""
+    from safetensors.torch import load_file
+
+    from agent_hypervisor_amd.models.engine import GovernanceEngine
+    from agent_hypervisor_amd.models.tables import SessionTable
+
+    read_manifest(d, "engine")
+    with open(os.path.join(d, "engine.json")) as f:
+        meta = json.load(f)
+    with open(os.path.join(d, "interner.json")) as f:
+        strings = json.load(f)
+    eng = GovernanceEngine(device=device, session_capacity=meta["session_capacity"],
+                           agent_capacity=meta["agent_capacity"], vouch_capacity=meta["vouch_capacity"],
+                           dmax=meta["dmax"], seed=meta["seed"], creator_did=strings[meta["creator_id"]])
+    ids = eng.interner.intern_many(strings)
+    if ids != list(range(len(strings))):
+        raise CheckpointError("interner ids do not reproduce (pool was not empty?)")
+    t = load_file(os.path.join(d, "tables.safetensors"))
+    for k in SessionTable.COLUMNS:
+        getattr(eng.sessions, k).copy_(t[f"sessions.{k}"])
+    n = meta["agent_count"]
+    eng.agents.sigma[:n].copy_(t["agents.sigma"])
+    eng.agents.did[:n].copy_(t["agents.did"])
+    eng.agents.count = n
+    vc = meta["vouch_count"]
+    for f_ in ("voucher", "vouchee", "session", "bonded", "pct", "active", "expiry_us", "released_us"):
+        getattr(eng.vouches, f_)[:vc].copy_(t[f"vouches.{f_}"])
+    eng.vouches.count = vc
+    eng._next_slot, eng._id_counter = meta["next_slot"], meta["id_counter"]
+    eng._last_specs = [tuple(x) for x in meta["last_specs"]] if meta["last_specs"] else None
+    if verify:
+        bad = verify_engine_audit(eng)
+        if bad:
+            raise CheckpointError(f"{bad} archived session(s) fail Merkle re-verification")
+    return eng
+
+
+def verify_engine_audit(eng) -> int:
+    """Recompute Merkle roots of archived sessions from their delta digests; returns mismatches."""
+    from agent_hypervisor_amd.ops import audit as A
+
+    t = eng.sessions
+    rows = torch.nonzero((t.sess_state == 4) & (t.delta_count > 0)).flatten()
+    if rows.numel() == 0:
+        return 0
+    counts = t.delta_count[rows].to(torch.int64)
+    offs = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=rows.device)
+    offs[1:] = torch.cumsum(counts, 0)
+    # gather leaves [Σcount, 8] in chain order
+    dmax = t.dmax
+    mask = torch.arange(dmax, device=rows.device)[None, :] < counts[:, None]
+    leaves = t.delta_hash[rows][mask].contiguous()
+    roots = A.merkle_roots(offs.to(torch.int32), leaves)
+    return int((roots != t.merkle_root[rows]).any(dim=1).sum())
+
+
+# ------------------------------------------------------- hypervisor (scalar)
+
+
+def _session_record(m) -> dict:
+    sso = m.sso
+    cfg = sso.config
+    return {
+        "session_id": sso.session_id,
+        "creator_did": sso.creator_did,
+        "state": sso.state.value,
+        "consistency_mode": sso.consistency_mode.value,
+        "config": {
+            "consistency_mode": cfg.consistency_mode.value,
+            "max_participants": cfg.max_participants,
+            "max_duration_seconds": cfg.max_duration_seconds,
+            "min_sigma_eff": cfg.min_sigma_eff,
+            "enable_audit": cfg.enable_audit,
+            "enable_blockchain_commitment": cfg.enable_blockchain_commitment,
+        },
+        "created_at": _iso(sso.created_at),
+        "terminated_at": _iso(sso.terminated_at),
+        "participants": [
+            {"agent_did": p.agent_did, "ring": int(p.ring.value), "sigma_raw": p.sigma_raw, "sigma_eff": p.sigma_eff,
+             "joined_at": _iso(p.joined_at), "is_active": p.is_active}
+            for p in sso._participants.values()
+        ],
+        "vfs": {
+            "files": dict(sso.vfs._files),
+            "permissions": {k: sorted(v) for k, v in sso.vfs._permissions.items()},
+        },
+        "reversibility": [
+            {"action_id": e.action_id, "execute_api": e.execute_api, "undo_api": e.undo_api,
+             "reversibility": e.reversibility.value, "undo_window_seconds": e.undo_window_seconds,
+             "compensation_method": e.compensation_method, "undo_api_healthy": e.undo_api_healthy}
+            for e in m.reversibility.entries
+        ],
+        "sagas": [
+            {**{k: v for k, v in g.to_dict().items() if k != "steps"},
+             "steps": [
+                 {"step_id": s.step_id, "action_id": s.action_id, "agent_did": s.agent_did,
+                  "execute_api": s.execute_api, "undo_api": s.undo_api, "state": s.state.value, "error": s.error,
+                  "started_at": _iso(s.started_at), "completed_at": _iso(s.completed_at),
+                  "timeout_seconds": s.timeout_seconds, "max_retries": s.max_retries, "retry_count": s.retry_count,
+                  "execute_result": _jsonable(s.execute_result),
+                  "compensation_result": _jsonable(s.compensation_result)}
+                 for s in g.steps
+             ]}
+            for g in m.saga.sagas
+        ],
+        "turn_count": m.delta_engine.turn_count,
+        "audit": m.delta_engine.export_records(),
+    }
+
+
+def save_hypervisor(hv, d: str) -> str:
+    """Write the scalar hypervisor's state as a checkpoint directory."""
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "sessions.jsonl"), "w") as f:
+        for m in hv.sessions:
+            f.write(json.dumps(_session_record(m), sort_keys=True) + "\n")
+    with open(os.path.join(d, "liability.json"), "w") as f:
+        json.dump([
+            {"vouch_id": v.vouch_id, "voucher_did": v.voucher_did, "vouchee_did": v.vouchee_did,
+             "session_id": v.session_id, "bonded_sigma_pct": v.bonded_sigma_pct, "bonded_amount": v.bonded_amount,
+             "created_at": _iso(v.created_at), "expiry": _iso(v.expiry), "is_active": v.is_active,
+             "released_at": _iso(v.released_at)}
+            for v in hv.vouching.records()
+        ], f)
+    with open(os.path.join(d, "commitments.json"), "w") as f:
+        json.dump([
+            {"session_id": c.session_id, "merkle_root": c.merkle_root, "participant_dids": c.participant_dids,
+             "delta_count": c.delta_count, "committed_at": _iso(c.committed_at),
+             "blockchain_tx_id": c.blockchain_tx_id, "committed_to": c.committed_to}
+            for c in hv.commitment.all_commitments()
+        ], f)
+    _write_manifest(d, "hypervisor", ["sessions.jsonl", "liability.json", "commitments.json"],
+                    {"sessions": len(hv.sessions)})
+    return d
+
+
+def _delta_from_record(rec: dict):
+    from hypervisor.audit.delta import SemanticDelta, VFSChange
+
+    p = json.loads(rec["payload"])
+    d = SemanticDelta(
+        delta_id=p["delta_id"], turn_id=p["turn_id"], session_id=p["session_id"], agent_did=p["agent_did"],
+        timestamp=datetime.fromisoformat(p["timestamp"]),
+        changes=[VFSChange(path=c["path"], operation=c["operation"], content_hash=c["content_hash"],
+                           previous_hash=c["previous_hash"]) for c in p["changes"]],
+        parent_hash=p["parent_hash"], delta_hash=rec["delta_hash"],
+    )
+    if hashlib.sha256(rec["payload"].encode()).hexdigest() != rec["delta_hash"]:
+        raise CheckpointError(f"delta {d.delta_id} of {d.session_id}: stored hash does not match its payload")
+    return d
+
+
+def load_hypervisor(d: str, hv=None, verify: bool = True):
+    """Resume a :class:`hypervisor.Hypervisor` from ``d`` (into ``hv`` if given)."""
+    from hypervisor.audit.commitment import CommitmentRecord
+    from hypervisor.core import Hypervisor, ManagedSession
+    from hypervisor.liability.vouching import VouchRecord
+    from hypervisor.models import (
+        ActionDescriptor,
+        ConsistencyMode,
+        ExecutionRing,
+        ReversibilityLevel,
+        SessionConfig,
+        SessionParticipant,
+        SessionState,
+    )
+    from hypervisor.saga.state_machine import Saga, SagaState, SagaStep, StepState
+    from hypervisor.session import SharedSessionObject
+
+    read_manifest(d, "hypervisor")
+    hv = hv or Hypervisor()
+    with open(os.path.join(d, "sessions.jsonl")) as f:
+        records = [json.loads(line) for line in f if line.strip()]
+    for r in records:
+        cfg = dict(r["config"])
+        cfg["consistency_mode"] = ConsistencyMode(cfg["consistency_mode"])
+        sso = SharedSessionObject(SessionConfig(**cfg), creator_did=r["creator_did"], session_id=r["session_id"])
+        sso.state = SessionState(r["state"])
+        sso.consistency_mode = ConsistencyMode(r["consistency_mode"])
+        sso.created_at = _dt(r["created_at"])
+        sso.terminated_at = _dt(r["terminated_at"])
+        for p in r["participants"]:
+            sso._participants[p["agent_did"]] = SessionParticipant(
+                agent_did=p["agent_did"], ring=ExecutionRing(p["ring"]), sigma_raw=p["sigma_raw"],
+                sigma_eff=p["sigma_eff"], joined_at=_dt(p["joined_at"]), is_active=p["is_active"])
+        sso.vfs._files = dict(r["vfs"]["files"])
+        sso.vfs._permissions = {k: set(v) for k, v in r["vfs"]["permissions"].items()}
+        m = ManagedSession(sso)
+        for e in r["reversibility"]:
+            m.reversibility.register(ActionDescriptor(
+                action_id=e["action_id"], name=e["action_id"], execute_api=e["execute_api"], undo_api=e["undo_api"],
+                reversibility=ReversibilityLevel(e["reversibility"]), undo_window_seconds=e["undo_window_seconds"],
+                compensation_method=e["compensation_method"]))
+            if not e["undo_api_healthy"]:
+                m.reversibility.mark_undo_unhealthy(e["action_id"])
+        for g in r["sagas"]:
+            saga = Saga(saga_id=g["saga_id"], session_id=g["session_id"], state=SagaState(g["state"]),
+                        created_at=_dt(g["created_at"]), completed_at=_dt(g["completed_at"]), error=g["error"])
+            for s in g["steps"]:
+                saga.steps.append(SagaStep(
+                    step_id=s["step_id"], action_id=s["action_id"], agent_did=s["agent_did"],
+                    execute_api=s["execute_api"], undo_api=s["undo_api"], state=StepState(s["state"]),
+                    execute_result=s["execute_result"], compensation_result=s["compensation_result"],
+                    error=s["error"], started_at=_dt(s["started_at"]), completed_at=_dt(s["completed_at"]),
+                    timeout_seconds=s["timeout_seconds"], max_retries=s["max_retries"], retry_count=s["retry_count"]))
+            m.saga._sagas[saga.saga_id] = saga
+        m.delta_engine._deltas = [_delta_from_record(x) for x in r["audit"]]
+        m.delta_engine._turn_counter = r["turn_count"]
+        if verify and not m.delta_engine.verify_chain():
+            raise CheckpointError(f"session {sso.session_id}: audit chain fails verification")
+        hv._sessions[sso.session_id] = m
+    with open(os.path.join(d, "liability.json")) as f:
+        for v in json.load(f):
+            rec = VouchRecord(vouch_id=v["vouch_id"], voucher_did=v["voucher_did"], vouchee_did=v["vouchee_did"],
+                              session_id=v["session_id"], bonded_sigma_pct=v["bonded_sigma_pct"],
+                              bonded_amount=v["bonded_amount"], created_at=_dt(v["created_at"]),
+                              expiry=_dt(v["expiry"]), is_active=v["is_active"], released_at=_dt(v["released_at"]))
+            hv.vouching._vouches[rec.vouch_id] = rec
+            hv.vouching._by_session.setdefault(rec.session_id, []).append(rec)
+    with open(os.path.join(d, "commitments.json")) as f:
+        for c in json.load(f):
+            rec = CommitmentRecord(session_id=c["session_id"], merkle_root=c["merkle_root"],
+                                   participant_dids=c["participant_dids"], delta_count=c["delta_count"],
+                                   committed_at=_dt(c["committed_at"]), blockchain_tx_id=c["blockchain_tx_id"],
+                                   committed_to=c["committed_to"])
+            hv.commitment._commitments[rec.session_id] = rec
+            if verify:
+                m = hv.get_session(rec.session_id)
+                de = m.delta_engine if m is not None else None
+                complete = de is not None and de.deltas and len(de.deltas) == de.turn_count  # nothing pruned by GC
+                if complete and de.compute_merkle_root() != rec.merkle_root:
+                    raise CheckpointError(f"session {rec.session_id}: Merkle root differs from its commitment")
+    return hv

@@ -1,0 +1,151 @@
+"""§5.4 on-disk session-state + Merkle-audit format: save → load round trips
+for the scalar hypervisor and the device engine, corruption detection, and
+resuming work after a restore."""
+
+from __future__ import annotations
+
+import json
+import os
+
+import pytest
+import torch
+
+from agent_hypervisor_amd.models.engine import GovernanceEngine
+from agent_hypervisor_amd.runtime.checkpoint import (
+    CheckpointError,
+    load_engine,
+    load_hypervisor,
+    save_engine,
+    save_hypervisor,
+)
+from hypervisor import Hypervisor, SessionConfig
+from hypervisor.audit.delta import VFSChange
+from hypervisor.models import ActionDescriptor, ReversibilityLevel
+
+
+async def _populated() -> Hypervisor:
+    hv = Hypervisor()
+    for k in range(3):
+        m = await hv.create_session(SessionConfig(max_participants=5), "did:admin")
+        sid = m.sso.session_id
+        acts = [ActionDescriptor("w", "w", "/w", undo_api="/u", reversibility=ReversibilityLevel.PARTIAL)]
+        await hv.join_session(sid, f"did:a{k}", actions=acts, sigma_raw=0.8)
+        await hv.join_session(sid, f"did:b{k}", sigma_raw=0.4)
+        await hv.activate_session(sid)
+        m.sso.vfs.write("/doc.md", f"v{k}", f"did:a{k}")
+        m.sso.vfs.set_permissions("/doc.md", {f"did:a{k}"}, f"did:a{k}")
+        hv.vouching.vouch(f"did:a{k}", f"did:b{k}", sid, 0.8)
+        for t in range(k + 2):
+            m.delta_engine.capture(f"did:a{k}", [VFSChange(f"/f{t}", "add", f"h{t}")])
+        g = m.saga.create_saga(sid)
+        st = m.saga.add_step(g.saga_id, "deploy", f"did:a{k}", "/d", undo_api="/ud")
+
+        async def ex():
+            return {"ok": k}
+
+        await m.saga.execute_step(g.saga_id, st.step_id, ex)
+        if k == 0:
+            await hv.terminate_session(sid)
+    return hv
+
+
+async def test_hypervisor_round_trip(tmp_path):
+    hv = await _populated()
+    d = save_hypervisor(hv, str(tmp_path / "ck"))
+    man = json.load(open(os.path.join(d, "manifest.json")))
+    assert man["format"] == "ahv-checkpoint" and man["kind"] == "hypervisor" and man["sessions"] == 3
+    hv2 = load_hypervisor(d)
+    assert [m.sso.session_id for m in hv2.sessions] == [m.sso.session_id for m in hv.sessions]
+    for a, b in zip(hv.sessions, hv2.sessions):
+        assert a.sso.state == b.sso.state and a.sso.participant_count == b.sso.participant_count
+        assert a.sso.vfs._files == b.sso.vfs._files
+        assert a.sso.vfs.get_permissions("/doc.md") == b.sso.vfs.get_permissions("/doc.md")
+        assert [d.delta_hash for d in a.delta_engine.deltas] == [d.delta_hash for d in b.delta_engine.deltas]
+        assert a.delta_engine.compute_merkle_root() == b.delta_engine.compute_merkle_root()
+        assert [g.to_dict() for g in a.saga.sagas] == [g.to_dict() for g in b.saga.sagas]
+        assert b.saga.sagas[0].steps[0].execute_result == a.saga.sagas[0].steps[0].execute_result
+        assert b.reversibility.get("w").undo_api == "/u"
+    assert len(hv2.vouching.records()) == 3
+    assert hv2.commitment.commitment_count == 1
+    first = hv.sessions[0].sso.session_id
+    assert hv2.commitment.verify(first, hv.commitment.get_commitment(first).merkle_root)
+
+
+async def test_resume_continues_chains(tmp_path):
+    hv = await _populated()
+    d = save_hypervisor(hv, str(tmp_path / "ck"))
+    hv2 = load_hypervisor(d)
+    live = hv2.sessions[1]
+    live.delta_engine.capture("did:a1", [VFSChange("/after-restore", "add", "x")])
+    assert live.delta_engine.verify_chain() and live.delta_engine.turn_count == 4
+    root = await hv2.terminate_session(live.sso.session_id)
+    assert root == live.delta_engine.compute_merkle_root()
+
+
+async def test_corruption_detected(tmp_path):
+    hv = await _populated()
+    d = save_hypervisor(hv, str(tmp_path / "ck"))
+    p = os.path.join(d, "sessions.jsonl")
+    text = open(p).read()
+    assert '"creator_did": "did:admin"' in text
+    open(p, "w").write(text.replace('"creator_did": "did:admin"', '"creator_did": "did:evil"', 1))
+    with pytest.raises(CheckpointError, match="corrupt"):
+        load_hypervisor(d)
+
+
+async def test_tampered_payload_with_fixed_manifest_fails_chain_check(tmp_path):
+    from agent_hypervisor_amd.runtime import checkpoint as ck
+
+    hv = await _populated()
+    d = save_hypervisor(hv, str(tmp_path / "ck"))
+    p = os.path.join(d, "sessions.jsonl")
+    text = open(p).read().replace('\\"/f1\\"', '\\"/evil\\"', 1)
+    open(p, "w").write(text)
+    ck._write_manifest(d, "hypervisor", ["sessions.jsonl", "liability.json", "commitments.json"], {"sessions": 3})
+    with pytest.raises(CheckpointError, match="does not match its payload"):
+        load_hypervisor(d)
+
+
+def test_missing_manifest_and_kind(tmp_path):
+    with pytest.raises(CheckpointError, match="manifest"):
+        load_hypervisor(str(tmp_path))
+    eng = GovernanceEngine(device="cpu", session_capacity=64, agent_capacity=64, seed=1)
+    eng.register_synthetic_agents(10)
+    d = save_engine(eng, str(tmp_path / "eng"))
+    with pytest.raises(CheckpointError, match="kind"):
+        load_hypervisor(d)
+
+
+def test_engine_round_trip_and_resume(tmp_path):
+    eng = GovernanceEngine(device="cpu", session_capacity=512, agent_capacity=1024, seed=42)
+    eng.register_synthetic_agents(300, seed=5)
+    eng.run_pipeline(200, deltas=3)
+    b = eng.run_pipeline(100, deltas=3)
+    d = save_engine(eng, str(tmp_path / "eng"))
+    eng2 = load_engine(d, device="cpu")
+    assert eng2.interner.str(eng2.creator_id) == "did:mesh:admin" and eng2.agents.count == 300
+    for k in ("merkle_root", "delta_hash", "sess_uuid", "part_sigma_eff"):
+        assert torch.equal(getattr(eng.sessions, k), getattr(eng2.sessions, k))
+    # continuing on the restored engine produces exactly what the original would
+    n1 = eng.run_pipeline(50, deltas=3, now_us=10**15)
+    n2 = eng2.run_pipeline(50, deltas=3, now_us=10**15)
+    assert torch.equal(n1.roots(), n2.roots()) and n1.session_id(3) == n2.session_id(3)
+    assert b.materialize(7).delta_engine.verify_chain()
+
+
+def test_engine_tamper_detected_by_merkle_reverify(tmp_path):
+    from safetensors.torch import load_file, save_file
+
+    from agent_hypervisor_amd.runtime import checkpoint as ck
+
+    eng = GovernanceEngine(device="cpu", session_capacity=128, agent_capacity=128, seed=3)
+    eng.register_synthetic_agents(50)
+    eng.run_pipeline(64, deltas=3)
+    d = save_engine(eng, str(tmp_path / "eng"))
+    p = os.path.join(d, "tables.safetensors")
+    t = load_file(p)
+    t["sessions.delta_hash"][5, 1, 0] ^= 1
+    save_file(t, p)
+    ck._write_manifest(d, "engine", ["tables.safetensors", "interner.json", "engine.json"])
+    with pytest.raises(CheckpointError, match="Merkle"):
+        load_engine(d, device="cpu")
