@@ -220,12 +220,16 @@ class GovernanceEngine:
         min_sigma_eff: float = 0.60,
         stats: Optional[torch.Tensor] = None,
         cursor: Optional[torch.Tensor] = None,
+        events=None,
     ) -> PipelineBatch:
         """Run the full governance pipeline for ``n`` new sessions (asynchronously
         on the current stream).
 
         ``stats`` (int64[6], on the engine device) accumulates the batch counters
         sessions / ok / participants / deltas / commitments / archived.
+
+        ``events`` (:class:`agent_hypervisor_amd.runtime.events.DeviceEventRing`)
+        collects the lifecycle events of every session on the device (N08).
 
         ``cursor`` (int64[3] on the engine device: slot_base, id_base, now_us)
         makes the launch read its bases from device memory instead of the host
@@ -262,6 +266,10 @@ class GovernanceEngine:
             pool_bytes=pool_b, pool_off=pool_o, pool_len=pool_l, stats=stats,
         )
         tensors.update({k: getattr(self.sessions, k) for k in SessionTable.COLUMNS})
+        if events is not None:  # DeviceEventRing (N08): lifecycle records appended by the kernel
+            ev_scalars, ev_tensors = events.kernel_args()
+            scalars.update(ev_scalars)
+            tensors.update(ev_tensors)
         if cursor is not None:
             if cursor.dtype != torch.int64 or cursor.numel() != 3 or cursor.device != self.device:
                 raise ValueError("cursor must be an int64[3] tensor on the engine device")

@@ -1,0 +1,91 @@
+"""Device event ring buffer.
+
+The batched pipeline kernel appends compact lifecycle records — one 64-bit
+atomic per wave reserves the wave's slots — into SoA tensors owned here.  The
+host drains them on its own cadence into :class:`HypervisorEventBus` events
+(the same event types the scalar facade publishes), so kernels can emit events
+without a host round trip per session.
+
+Records past ``capacity`` are dropped (counted by :attr:`DeviceEventRing.dropped`);
+size the ring for one drain interval (≈8 records per session).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from hypervisor import _clock
+from hypervisor.observability.event_bus import EVENT_FROM_CODE, HypervisorEvent
+
+u8, i32, i64 = torch.uint8, torch.int32, torch.int64
+
+
+class DeviceEventRing:
+    def __init__(self, capacity: int, device) -> None:
+        dev = torch.device(device)
+        self.capacity = int(capacity)
+        self.device = dev
+        self.type = torch.zeros(capacity, dtype=u8, device=dev)
+        self.slot = torch.zeros(capacity, dtype=i32, device=dev)
+        self.agent = torch.zeros(capacity, dtype=i32, device=dev)
+        self.ts_us = torch.zeros(capacity, dtype=i64, device=dev)
+        self.aux = torch.zeros(capacity, dtype=i32, device=dev)
+        self.cursor = torch.zeros(1, dtype=i64, device=dev)  # read as unsigned 64-bit by kernels
+        self.total_dropped = 0
+
+    def kernel_args(self) -> tuple[dict, dict]:
+        """(scalars, tensors) entries for a pipeline launch."""
+        return ({"ev_capacity": self.capacity},
+                {"ev_type": self.type, "ev_slot": self.slot, "ev_agent": self.agent, "ev_ts_us": self.ts_us,
+                 "ev_aux": self.aux, "ev_cursor": self.cursor})
+
+    @property
+    def pending(self) -> int:
+        return min(int(self.cursor.item()), self.capacity)
+
+    @property
+    def dropped(self) -> int:
+        return max(0, int(self.cursor.item()) - self.capacity)
+
+    def snapshot(self) -> dict[str, torch.Tensor]:
+        """Host copies of the pending records (does not reset)."""
+        n = self.pending
+        return {k: getattr(self, k)[:n].cpu() for k in ("type", "slot", "agent", "ts_us", "aux")}
+
+    def reset(self) -> None:
+        self.total_dropped += self.dropped
+        self.cursor.zero_()
+
+    def drain(self, engine, bus=None, limit: Optional[int] = None) -> list[HypervisorEvent]:
+        """Convert pending records to events (published on ``bus`` if given) and
+        reset the ring.  Events are ordered by (timestamp, slot, emission order)."""
+        snap = self.snapshot()
+        self.reset()
+        n = snap["type"].numel()
+        if n == 0:
+            return []
+        order = sorted(range(n), key=lambda j: (int(snap["ts_us"][j]), int(snap["slot"][j]), j))
+        if limit is not None:
+            order = order[:limit]
+        t = engine.sessions
+        sid_cache: dict[int, str] = {}
+        out = []
+        for j in order:
+            slot = int(snap["slot"][j])
+            sid = sid_cache.get(slot)
+            if sid is None:
+                w = t.sess_uuid[slot].cpu().tolist()
+                h = "".join(f"{x & 0xFFFFFFFF:08x}" for x in w)
+                sid = sid_cache[slot] = f"session:{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:]}"
+            a = int(snap["agent"][j])
+            did = engine.interner.str(int(engine.agents.did[a])) if a >= 0 else None
+            et = EVENT_FROM_CODE[int(snap["type"][j])]
+            payload = {"ring": int(snap["aux"][j])} if et.value == "ring.assigned" else {}
+            ev = HypervisorEvent(event_type=et, timestamp=_clock.from_us(int(snap["ts_us"][j])), session_id=sid,
+                                 agent_did=did, payload=payload)
+            out.append(ev)
+            if bus is not None:
+                bus.emit(ev)
+        return out

@@ -39,6 +39,27 @@ __global__ __launch_bounds__(kWaveLanes, 3) void governance_pipeline_kernel(Pipe
       if (lane == 0 && s) atomicAdd(a.stats + k, static_cast<unsigned long long>(s));
     }
   }
+  if (a.ev.cursor) {
+    // one 64-bit atomic reserves the whole wave's records; lanes write at their
+    // exclusive prefix offset
+    const uint32_t nev = i < a.n ? pipeline_event_count(a, i, c) : 0u;
+    uint32_t incl = nev;
+#pragma unroll
+    for (int off = 1; off < kWaveLanes; off <<= 1) {
+      const uint32_t y = __shfl_up(incl, off, kWaveLanes);
+      if (lane >= static_cast<uint32_t>(off)) incl += y;
+    }
+    const uint32_t total = __shfl(incl, kWaveLanes - 1, kWaveLanes);
+    unsigned long long base = 0;
+    if (lane == 0 && total) base = atomicAdd(a.ev.cursor, static_cast<unsigned long long>(total));
+    base = __shfl(base, 0, kWaveLanes);
+    if (i < a.n) {
+      const unsigned long long first = base + (incl - nev);
+      pipeline_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
+        event_store(a.ev, first + k, static_cast<int32_t>(slot), e);
+      });
+    }
+  }
 }
 
 void launch_pipeline(const PipelineArgs& a, hipStream_t stream) {
@@ -104,6 +125,13 @@ void pipeline_host(const PipelineArgs& a) {
     const PipeCounters c = pipeline_session(a, i, sink);
     if (a.stats)
       for (int k = 0; k < kPipeStats; ++k) a.stats[k] += c.v[k];
+    if (a.ev.cursor) {
+      const unsigned long long first = *a.ev.cursor;
+      *a.ev.cursor += pipeline_event_count(a, i, c);
+      pipeline_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
+        event_store(a.ev, first + k, static_cast<int32_t>(slot), e);
+      });
+    }
   }
 }
 

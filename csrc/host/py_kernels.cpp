@@ -63,6 +63,15 @@ static PipelineArgs pipeline_args(const py::dict& d) {
   a.pool.len = ptr<const int32_t>(d, "pool_len");
   a.stats = ptr<unsigned long long>(d, "stats");
   a.cursor = d.contains("cursor") ? ptr<const int64_t>(d, "cursor") : nullptr;
+  if (d.contains("ev_cursor") && !d["ev_cursor"].is_none()) {
+    a.ev.type = ptr<uint8_t>(d, "ev_type");
+    a.ev.slot = ptr<int32_t>(d, "ev_slot");
+    a.ev.agent = ptr<int32_t>(d, "ev_agent");
+    a.ev.ts_us = ptr<int64_t>(d, "ev_ts_us");
+    a.ev.aux = ptr<int32_t>(d, "ev_aux");
+    a.ev.cursor = ptr<unsigned long long>(d, "ev_cursor");
+    a.ev.capacity = val<int64_t>(d, "ev_capacity");
+  }
   SessionTables& t = a.t;
   t.sess_uuid = ptr<uint32_t>(d, "sess_uuid");
   t.sess_state = ptr<uint8_t>(d, "sess_state");

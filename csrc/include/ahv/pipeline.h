@@ -12,6 +12,7 @@
 #pragma once
 
 #include "ahv/delta_emit.h"
+#include "ahv/events.h"
 #include "ahv/semantics.h"
 
 namespace ahv {
@@ -88,6 +89,8 @@ struct PipelineArgs {
   // stays correct on replay: the clock kernel refreshes now_us and the advance
   // kernel moves slot/id bases on the device (runtime/graphs.py, N07/N09).
   const int64_t* cursor;
+  // Device event ring (N08); ev.cursor == null disables event emission.
+  EventRing ev;
 };
 
 AHV_HD inline int64_t pipe_slot_base(const PipelineArgs& a) { return a.cursor ? a.cursor[0] : a.slot_base; }
@@ -239,6 +242,38 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   c.v[4] = committed ? 1u : 0u;
   c.v[5] = state == SS_ARCHIVED ? 1u : 0u;
   return c;
+}
+
+// ---- lifecycle events (N08) --------------------------------------------------------
+// The records the scalar Hypervisor facade publishes for the same pipeline when it
+// has an event bus: created → joined → ring_assigned → activated → terminated →
+// audit.committed → gc_collected → archived (fewer when a stage was refused).
+
+AHV_HD inline uint32_t pipeline_event_count(const PipelineArgs& a, int64_t i, const PipeCounters& c) {
+  const int64_t slot = (pipe_slot_base(a) + i) % a.capacity;
+  return 1u + (c.v[2] ? 3u : 0u) + (a.t.sess_terminated_us[slot] ? 1u : 0u) + c.v[4] + 2u * c.v[5];
+}
+
+template <class Put>
+AHV_HD inline void pipeline_events(const PipelineArgs& a, int64_t i, const PipeCounters& c, Put&& put) {
+  const int64_t slot = (pipe_slot_base(a) + i) % a.capacity;
+  const SessionTables& t = a.t;
+  const int32_t agent = a.session_agent[i];
+  const int64_t t0 = t.sess_created_us[slot];
+  const int64_t te = t.sess_terminated_us[slot];
+  uint32_t k = 0;
+  put(k++, slot, EventRec{EV_SESSION_CREATED, -1, t0, 0});
+  if (c.v[2]) {
+    put(k++, slot, EventRec{EV_SESSION_JOINED, agent, t0, 0});
+    put(k++, slot, EventRec{EV_RING_ASSIGNED, agent, t0, t.part_ring[slot * kMaxParticipants]});
+    put(k++, slot, EventRec{EV_SESSION_ACTIVATED, -1, t0, 0});
+  }
+  if (te) put(k++, slot, EventRec{EV_SESSION_TERMINATED, -1, te, 0});
+  if (c.v[4]) put(k++, slot, EventRec{EV_AUDIT_COMMITTED, -1, te, 0});
+  if (c.v[5]) {
+    put(k++, slot, EventRec{EV_AUDIT_GC_COLLECTED, -1, te, 0});
+    put(k++, slot, EventRec{EV_SESSION_ARCHIVED, -1, te, 0});
+  }
 }
 
 }  // namespace ahv
