@@ -44,6 +44,16 @@ __global__ __launch_bounds__(kBlock) void saga_fused_kernel(SagaBatchArgs a) {
   add_counters(a, c, active);
 }
 
+// One instantiation per step count: the chain's state lives in registers.
+template <int K>
+__global__ __launch_bounds__(kBlock) void saga_fused_regs_kernel(SagaBatchArgs a) {
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const bool active = s < a.sagas;
+  SagaCounters c{0, 0, 0, 0};
+  if (active) c = saga_run_chain_regs<K>(a, s);
+  add_counters(a, c, active);
+}
+
 // phase 0 init, 1 execute step k, 2 decide, 3 compensate step k, 4 finish (+counters)
 __global__ __launch_bounds__(kBlock) void saga_phase_kernel(SagaBatchArgs a, int phase, int k) {
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -72,14 +82,23 @@ static void check_args(const SagaBatchArgs& a) {
 void launch_saga_fused(const SagaBatchArgs& a, hipStream_t st) {
   check_args(a);
   if (a.sagas <= 0) return;
-  hipLaunchKernelGGL(saga_fused_kernel, grid_for(a.sagas), dim3(kBlock), 0, st, a);
+  switch (a.steps) {
+#define AHV_SAGA_LAUNCH(K)                                                                       \
+  case K:                                                                                        \
+    hipLaunchKernelGGL(saga_fused_regs_kernel<K>, grid_for(a.sagas), dim3(kBlock), 0, st, a); \
+    break;
+    AHV_SAGA_REG_CASES(AHV_SAGA_LAUNCH)
+#undef AHV_SAGA_LAUNCH
+    default:
+      hipLaunchKernelGGL(saga_fused_kernel, grid_for(a.sagas), dim3(kBlock), 0, st, a);
+  }
   check_hip(hipGetLastError(), "saga_fused_kernel");
 }
 
 void saga_fused_host(const SagaBatchArgs& a) {
   check_args(a);
   for (int64_t s = 0; s < a.sagas; ++s) {
-    const SagaCounters c = saga_run_chain(a, s);
+    const SagaCounters c = saga_run_chain_fused(a, s);
     if (a.stats) {
       a.stats[0] += c.completed;
       a.stats[1] += c.escalated;

@@ -174,6 +174,112 @@ AHV_HD inline SagaCounters saga_counters(const SagaBatchArgs& a, int64_t s) {
   return c;
 }
 
+// Register-resident whole chain for a compile-time step count: the outcome
+// tables are read once and every state column is written once (all coalesced,
+// step-major), with the whole per-saga state machine in registers in between.
+// Produces exactly what saga_run_chain produces.
+template <int K>
+AHV_HD inline SagaCounters saga_run_chain_regs(const SagaBatchArgs& a, int64_t s) {
+  uint8_t st[K], rc[K], er[K];
+  int64_t t0[K], t1[K];
+  uint8_t fa[K], fk[K], cf[K], hu[K], mr[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t e = saga_elem(a, s, k);
+    fa[k] = a.fail_attempts[e];
+    fk[k] = a.fail_kind[e];
+    cf[k] = a.comp_fail[e];
+    hu[k] = a.has_undo[e];
+    mr[k] = a.max_retries[e];
+    st[k] = ST_PENDING;
+    rc[k] = 0;
+    er[k] = SE_NONE;
+    t0[k] = 0;
+    t1[k] = 0;
+  }
+  const int64_t now = a.now_us;
+  int32_t tick = 0, failed = -1, compf = 0;
+  uint8_t g = SG_RUNNING;
+  int64_t gdone = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (failed < 0) {
+      const int attempts = 1 + mr[k];
+      const int fails = fa[k];
+      for (int at = 0; at < attempts; ++at) {
+        rc[k] = static_cast<uint8_t>(at);
+        t0[k] = now + (tick++);
+        t1[k] = now + (tick++);
+        if (fails == 255 || at < fails) {
+          st[k] = ST_FAILED;
+          er[k] = fk[k] == 2 ? SE_EXEC_TIMEOUT : SE_EXEC_FAILED;
+          if (at < attempts - 1) {
+            st[k] = ST_PENDING;
+            er[k] = SE_NONE;
+          }
+        } else {
+          st[k] = ST_COMMITTED;
+          break;
+        }
+      }
+      if (st[k] == ST_FAILED) failed = k;
+    }
+  }
+  if (failed < 0) {
+    g = SG_COMPLETED;
+    gdone = now + (tick++);
+  } else if (a.compensate) {
+    g = SG_COMPENSATING;
+  } else {
+    g = SG_FAILED;
+    gdone = now + (tick++);
+  }
+  if (g == SG_COMPENSATING) {
+#pragma unroll
+    for (int k = K - 1; k >= 0; --k) {
+      if (st[k] != ST_COMMITTED) continue;
+      if (!hu[k]) {
+        st[k] = ST_COMPENSATION_FAILED;
+        er[k] = SE_NO_UNDO;
+        ++compf;
+        continue;
+      }
+      if (cf[k] == 0) {
+        st[k] = ST_COMPENSATED;
+      } else {
+        st[k] = ST_COMPENSATION_FAILED;
+        er[k] = cf[k] == 2 ? SE_COMP_TIMEOUT : SE_COMP_FAILED;
+        ++compf;
+      }
+      t1[k] = now + (tick++);
+    }
+    g = compf > 0 ? SG_ESCALATED : SG_COMPLETED;
+    gdone = now + (tick++);
+  }
+  SagaCounters c{g == SG_COMPLETED, g == SG_ESCALATED, g == SG_FAILED, 0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t e = saga_elem(a, s, k);
+    a.step_state[e] = st[k];
+    a.retry_count[e] = rc[k];
+    a.step_error[e] = er[k];
+    a.started_us[e] = t0[k];
+    a.completed_us[e] = t1[k];
+    c.compensated += st[k] == ST_COMPENSATED;
+  }
+  a.saga_state[s] = g;
+  a.saga_completed_us[s] = gdone;
+  a.failed_step[s] = failed;
+  a.comp_failed[s] = compf;
+  a.tick[s] = tick;
+  return c;
+}
+
+constexpr int kMaxRegSagaSteps = 16;
+
+#define AHV_SAGA_REG_CASES(X) \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+
 // Whole chain for one saga (fused path).
 AHV_HD inline SagaCounters saga_run_chain(const SagaBatchArgs& a, int64_t s) {
   saga_init(a, s);
@@ -184,6 +290,19 @@ AHV_HD inline SagaCounters saga_run_chain(const SagaBatchArgs& a, int64_t s) {
   saga_finish(a, s, tick);
   a.tick[s] = tick;
   return saga_counters(a, s);
+}
+
+// Fused chain: register-resident for K ≤ 16, generic (global-memory state) beyond.
+AHV_HD inline SagaCounters saga_run_chain_fused(const SagaBatchArgs& a, int64_t s) {
+  switch (a.steps) {
+#define AHV_SAGA_CASE(K) \
+  case K:                \
+    return saga_run_chain_regs<K>(a, s);
+    AHV_SAGA_REG_CASES(AHV_SAGA_CASE)
+#undef AHV_SAGA_CASE
+    default:
+      return saga_run_chain(a, s);
+  }
 }
 
 }  // namespace ahv
