@@ -33,6 +33,7 @@ from agent_hypervisor_amd._native import C
 from agent_hypervisor_amd.models.tables import AgentTable, SessionTable, VouchTable
 from agent_hypervisor_amd.ops import pipeline as _pipeline_op
 from agent_hypervisor_amd.utils.interner import Interner
+from agent_hypervisor_amd.utils.stats import SpreadCounters
 from hypervisor import _clock
 from hypervisor.config import RUNTIME
 
@@ -46,6 +47,8 @@ def resolve_device(device: Optional[str]) -> torch.device:
             "GovernanceEngine requested a HIP device but torch.cuda.is_available() is False; "
             "pass device='cpu' explicitly to run the host twin"
         )
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())  # tensors report an explicit index
     return d
 
 
@@ -175,6 +178,7 @@ class GovernanceEngine:
         self._id_counter = 0
         self._last_specs = None
         self._change_cache: dict = {}
+        self._spread = SpreadCounters(6, self.device)
 
     # -- agents ----------------------------------------------------------------
     def register_agents(self, dids: Sequence[str], sigmas) -> torch.Tensor:
@@ -263,7 +267,8 @@ class GovernanceEngine:
         tensors = dict(
             session_agent=agents, agent_sigma=self.agents.sigma, agent_did=self.agents.did, changes=ch,
             vouch_offsets=None, vouch_active=None, vouch_released_us=None,
-            pool_bytes=pool_b, pool_off=pool_o, pool_len=pool_l, stats=stats,
+            pool_bytes=pool_b, pool_off=pool_o, pool_len=pool_l,
+            stats=self._spread.begin() if stats is not None else None,
         )
         tensors.update({k: getattr(self.sessions, k) for k in SessionTable.COLUMNS})
         if events is not None:  # DeviceEventRing (N08): lifecycle records appended by the kernel
@@ -275,8 +280,12 @@ class GovernanceEngine:
                 raise ValueError("cursor must be an int64[3] tensor on the engine device")
             tensors["cursor"] = cursor
             _pipeline_op.run(scalars, tensors)
+            if stats is not None:
+                self._spread.add_into(stats)
             return PipelineBatch(self, -1, n, -1, -1, deltas, list(specs), agents)
         _pipeline_op.run(scalars, tensors)
+        if stats is not None:
+            self._spread.add_into(stats)
         self._next_slot = (slot_base + n) % cap
         self._id_counter = id_base + 3 * n
         return PipelineBatch(self, slot_base, n, id_base, now, deltas, list(specs), agents)

@@ -23,6 +23,7 @@ from typing import Optional
 import torch
 
 from agent_hypervisor_amd._native import C
+from agent_hypervisor_amd.utils.stats import SpreadCounters
 from hypervisor import _clock
 
 u8, i32, i64 = torch.uint8, torch.int32, torch.int64
@@ -66,9 +67,9 @@ class SagaBatchEngine:
     def __init__(self, sagas: int, steps: int = 10, device: str = "cuda", compensate: bool = True) -> None:
         if not 1 <= steps <= 64:
             raise ValueError("steps must be in [1, 64]")
-        self.device = torch.device(device)
-        if self.device.type == "cuda" and not torch.cuda.is_available():
-            raise RuntimeError("SagaBatchEngine asked for a HIP device but none is visible")
+        from agent_hypervisor_amd.models.engine import resolve_device
+
+        self.device = resolve_device(device)
         self.S, self.K, self.compensate = sagas, steps, compensate
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=self.device)  # noqa: E731
         # per-step state is step-major [K, S] (coalesced per-step access, see
@@ -79,6 +80,7 @@ class SagaBatchEngine:
         self.saga_state, self.saga_completed_us = z(sagas, u8), z(sagas, i64)
         self.failed_step, self.comp_failed, self.tick = z(sagas, i32), z(sagas, i32), z(sagas, i32)
         self.stats = z(4, i64)
+        self._spread = SpreadCounters(4, self.device)
         self.now_us = 0
         self._graph = None
         self._graph_outcomes = None
@@ -113,8 +115,9 @@ class SagaBatchEngine:
             d[f] = t.data_ptr()
         for f in ("_step_state", "_retry_count", "_step_error", "_started_us", "_completed_us"):
             d[f[1:]] = getattr(self, f).data_ptr()
-        for f in ("saga_state", "saga_completed_us", "failed_step", "comp_failed", "tick", "stats"):
+        for f in ("saga_state", "saga_completed_us", "failed_step", "comp_failed", "tick"):
             d[f] = getattr(self, f).data_ptr()
+        d["stats"] = self._spread.buf.data_ptr()
         return d
 
     def _stream(self) -> int:
@@ -125,13 +128,13 @@ class SagaBatchEngine:
         """Run every saga's chain in one launch; returns the [4] i64 counters
         (completed, escalated, failed, compensated steps) of this batch."""
         self.now_us = int(now_us if now_us is not None else _clock.now_us())
-        self.stats.zero_()
         a = self._args(outcomes, self.now_us)
+        self._spread.begin()
         if self.device.type == "cuda":
             C.saga_fused(a, self._stream())
         else:
             C.saga_fused_host(a)
-        return self.stats
+        return self._spread.copy_into(self.stats)
 
     # -- step loop -----------------------------------------------------------------
     def _phase(self, a: dict, phase: int, k: int = 0) -> None:
@@ -141,7 +144,7 @@ class SagaBatchEngine:
             C.saga_phase_host(a, phase, k)
 
     def _loop(self, a: dict) -> None:
-        self.stats.zero_()
+        self._spread.begin()
         self._phase(a, 0)
         for k in range(self.K):
             self._phase(a, 1, k)
@@ -149,6 +152,7 @@ class SagaBatchEngine:
         for k in range(self.K - 1, -1, -1):
             self._phase(a, 3, k)
         self._phase(a, 4)
+        self._spread.copy_into(self.stats)
 
     def run_step_loop(self, outcomes: SagaOutcomes, now_us: Optional[int] = None, graph: bool = True) -> torch.Tensor:
         """Orchestrator-shaped execution: 2K+3 launches, replayed from a hipGraph

@@ -36,7 +36,8 @@ __global__ __launch_bounds__(kWaveLanes, 3) void governance_pipeline_kernel(Pipe
 #pragma unroll
     for (int k = 0; k < kPipeStats; ++k) {
       const uint32_t s = wave_sum(c.v[k]);
-      if (lane == 0 && s) atomicAdd(a.stats + k, static_cast<unsigned long long>(s));
+      if (lane == 0 && s)
+        atomicAdd(a.stats + (blockIdx.x % kStatSpread) * kPipeStats + k, static_cast<unsigned long long>(s));
     }
   }
   if (a.ev.cursor) {

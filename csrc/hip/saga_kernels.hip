@@ -31,7 +31,9 @@ __device__ __forceinline__ void add_counters(const SagaBatchArgs& a, SagaCounter
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t s = wave_sum(v[k]);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(a.stats + k, static_cast<unsigned long long>(s));
+    if ((threadIdx.x & 63) == 0 && s)
+      atomicAdd(a.stats + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) % kStatSpread) * 4 + k,
+                static_cast<unsigned long long>(s));
   }
 }
 }  // namespace
