@@ -6,8 +6,10 @@ host drains them on its own cadence into :class:`HypervisorEventBus` events
 (the same event types the scalar facade publishes), so kernels can emit events
 without a host round trip per session.
 
-Records past ``capacity`` are dropped (counted by :attr:`DeviceEventRing.dropped`);
-size the ring for one drain interval (≈8 records per session).
+The ring is split into 64 segments (one per workgroup residue, so appends
+contend on 64 cursors instead of one); records past a segment's end are
+dropped (counted by :attr:`DeviceEventRing.dropped`).  Size the ring for one
+drain interval (≈8 records per session, plus slack for segment imbalance).
 """
 
 from __future__ import annotations
@@ -16,6 +18,7 @@ from typing import Optional
 
 import torch
 
+from agent_hypervisor_amd.utils.stats import SPREAD
 from hypervisor import _clock
 from hypervisor.observability.event_bus import EVENT_FROM_CODE, HypervisorEvent
 
@@ -25,14 +28,16 @@ u8, i32, i64 = torch.uint8, torch.int32, torch.int64
 class DeviceEventRing:
     def __init__(self, capacity: int, device) -> None:
         dev = torch.device(device)
-        self.capacity = int(capacity)
+        capacity = -(-int(capacity) // SPREAD) * SPREAD  # whole segments
+        self.capacity = capacity
+        self.segment = capacity // SPREAD
         self.device = dev
         self.type = torch.zeros(capacity, dtype=u8, device=dev)
         self.slot = torch.zeros(capacity, dtype=i32, device=dev)
         self.agent = torch.zeros(capacity, dtype=i32, device=dev)
         self.ts_us = torch.zeros(capacity, dtype=i64, device=dev)
         self.aux = torch.zeros(capacity, dtype=i32, device=dev)
-        self.cursor = torch.zeros(1, dtype=i64, device=dev)  # read as unsigned 64-bit by kernels
+        self.cursor = torch.zeros(SPREAD, dtype=i64, device=dev)  # read as unsigned 64-bit by kernels
         self.total_dropped = 0
 
     def kernel_args(self) -> tuple[dict, dict]:
@@ -41,18 +46,23 @@ class DeviceEventRing:
                 {"ev_type": self.type, "ev_slot": self.slot, "ev_agent": self.agent, "ev_ts_us": self.ts_us,
                  "ev_aux": self.aux, "ev_cursor": self.cursor})
 
+    def _counts(self) -> list[int]:
+        return [int(c) for c in self.cursor.cpu().tolist()]
+
     @property
     def pending(self) -> int:
-        return min(int(self.cursor.item()), self.capacity)
+        return sum(min(c, self.segment) for c in self._counts())
 
     @property
     def dropped(self) -> int:
-        return max(0, int(self.cursor.item()) - self.capacity)
+        return sum(max(0, c - self.segment) for c in self._counts())
 
     def snapshot(self) -> dict[str, torch.Tensor]:
-        """Host copies of the pending records (does not reset)."""
-        n = self.pending
-        return {k: getattr(self, k)[:n].cpu() for k in ("type", "slot", "agent", "ts_us", "aux")}
+        """Host copies of the pending records, segment by segment (does not reset)."""
+        counts = self._counts()
+        idx = torch.cat([torch.arange(min(c, self.segment)) + g * self.segment for g, c in enumerate(counts)])
+        idx = idx.to(self.type.device)
+        return {k: getattr(self, k).index_select(0, idx).cpu() for k in ("type", "slot", "agent", "ts_us", "aux")}
 
     def reset(self) -> None:
         self.total_dropped += self.dropped

@@ -51,13 +51,14 @@ __global__ __launch_bounds__(kWaveLanes, 3) void governance_pipeline_kernel(Pipe
       if (lane >= static_cast<uint32_t>(off)) incl += y;
     }
     const uint32_t total = __shfl(incl, kWaveLanes - 1, kWaveLanes);
+    const int seg = static_cast<int>(blockIdx.x % kStatSpread);
     unsigned long long base = 0;
-    if (lane == 0 && total) base = atomicAdd(a.ev.cursor, static_cast<unsigned long long>(total));
+    if (lane == 0 && total) base = atomicAdd(a.ev.cursor + seg, static_cast<unsigned long long>(total));
     base = __shfl(base, 0, kWaveLanes);
     if (i < a.n) {
       const unsigned long long first = base + (incl - nev);
       pipeline_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
-        event_store(a.ev, first + k, static_cast<int32_t>(slot), e);
+        event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
       });
     }
   }
@@ -127,10 +128,11 @@ void pipeline_host(const PipelineArgs& a) {
     if (a.stats)
       for (int k = 0; k < kPipeStats; ++k) a.stats[k] += c.v[k];
     if (a.ev.cursor) {
-      const unsigned long long first = *a.ev.cursor;
-      *a.ev.cursor += pipeline_event_count(a, i, c);
+      const int seg = static_cast<int>((i / kWaveLanes) % kStatSpread);  // the device's workgroup mapping
+      const unsigned long long first = a.ev.cursor[seg];
+      a.ev.cursor[seg] += pipeline_event_count(a, i, c);
       pipeline_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
-        event_store(a.ev, first + k, static_cast<int32_t>(slot), e);
+        event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
       });
     }
   }

@@ -22,17 +22,22 @@ enum EventCode : uint8_t {
   EV_AUDIT_GC_COLLECTED = 37,
 };
 
-// Structure-of-arrays ring of `capacity` records; `cursor` counts every append
-// ever reserved (records past capacity are dropped and show up as cursor > cap).
+// Structure-of-arrays records split into kStatSpread segments of
+// `capacity / kStatSpread` records; workgroup b appends to segment
+// b % kStatSpread through cursor[segment] (one hot address per segment instead
+// of one for the whole grid).  A cursor counts every append ever reserved in its
+// segment; records past the segment's end are dropped (cursor > segment size).
 struct EventRing {
   uint8_t* type;
   int32_t* slot;    // session table row
   int32_t* agent;   // agent id (-1 = none); DIDs resolve through the agent table
   int64_t* ts_us;
   int32_t* aux;     // e.g. ring for RING_ASSIGNED, delta index for DELTA_CAPTURED
-  unsigned long long* cursor;
-  int64_t capacity;
+  unsigned long long* cursor;  // [kStatSpread]
+  int64_t capacity;            // total records (multiple of kStatSpread)
 };
+
+AHV_HD inline int64_t event_segment_size(const EventRing& r) { return r.capacity / kStatSpread; }
 
 struct EventRec {
   uint8_t type;
@@ -41,8 +46,11 @@ struct EventRec {
   int32_t aux;
 };
 
-AHV_HD inline void event_store(const EventRing& r, unsigned long long at, int32_t slot, const EventRec& e) {
-  if (at >= static_cast<unsigned long long>(r.capacity)) return;
+// `at` is the position within segment `seg`.
+AHV_HD inline void event_store(const EventRing& r, int seg, unsigned long long pos, int32_t slot, const EventRec& e) {
+  const int64_t segsz = event_segment_size(r);
+  if (pos >= static_cast<unsigned long long>(segsz)) return;
+  const int64_t at = seg * segsz + static_cast<int64_t>(pos);
   r.type[at] = e.type;
   r.slot[at] = slot;
   r.agent[at] = e.agent;

@@ -25,7 +25,7 @@ def test_event_codes_match_python_enum():
         assert EVENT_CODE[EventType[name]] == int(code), name
 
 
-def _run(device, n=300, cap=10_000):
+def _run(device, n=300, cap=40_000):
     eng = GovernanceEngine(device=device, session_capacity=1024, agent_capacity=512, seed=5)
     eng.register_synthetic_agents(400, seed=2)
     ring = DeviceEventRing(cap, device)
@@ -47,10 +47,11 @@ def test_host_twin_emits_scalar_sequence():
 
 
 def test_ring_overflow_counts_drops():
-    eng, ring, _ = _run("cpu", n=100, cap=50)
-    assert ring.pending == 50 and ring.dropped == 750
+    eng, ring, _ = _run("cpu", n=100, cap=50)  # rounds up to 64 records = 64 segments of 1
+    # sessions 0..63 append to segment 0, 64..99 to segment 1 (workgroup residues)
+    assert ring.pending == 2 and ring.dropped == 798
     ring.drain(eng)
-    assert ring.total_dropped == 750
+    assert ring.total_dropped == 798
 
 
 @pytest.mark.gpu
@@ -61,7 +62,7 @@ def test_device_ring_matches_host(cuda_device):
     eng_h = GovernanceEngine(device="cpu", session_capacity=n, agent_capacity=4096, seed=9)
     eng_h.register_synthetic_agents(4096, seed=1)
     agents = torch.randint(0, 4096, (n,), dtype=torch.int32)
-    rd, rh = DeviceEventRing(8 * n, cuda_device), DeviceEventRing(8 * n, "cpu")
+    rd, rh = DeviceEventRing(8 * n * 2, cuda_device), DeviceEventRing(8 * n * 2, "cpu")
     eng_d.run_pipeline(n, agents=agents.to(cuda_device), events=rd, now_us=123)
     eng_h.run_pipeline(n, agents=agents, events=rh, now_us=123)
     torch.cuda.synchronize(cuda_device)
