@@ -286,5 +286,10 @@ class Hypervisor:
         """Run the full governance pipeline for ``n_sessions`` sessions on device.
 
         See :meth:`agent_hypervisor_amd.models.engine.GovernanceEngine.run_pipeline`.
+        With no agents registered yet, a synthetic population (random-init σ) the
+        size of the batch is registered first.
         """
-        return self.device_engine.run_pipeline(n_sessions, **kwargs)
+        eng = self.device_engine
+        if eng.agents.count == 0:
+            eng.register_synthetic_agents(min(max(n_sessions, 1), eng.agents.capacity))
+        return eng.run_pipeline(n_sessions, **kwargs)
