@@ -109,7 +109,7 @@ int64_t device_wall_clock(int device) {
   int64_t v = 0;
   const hipError_t e1 = hipGetLastError();
   const hipError_t e2 = hipMemcpy(&v, d, sizeof(v), hipMemcpyDeviceToHost);
-  hipFree(d);
+  (void)hipFree(d);
   check_hip(e1, "wall_clock_kernel");
   check_hip(e2, "hipMemcpy wall clock");
   return v;

@@ -37,7 +37,7 @@ struct EventRing {
   int64_t capacity;            // total records (multiple of kStatSpread)
 };
 
-AHV_HD inline int64_t event_segment_size(const EventRing& r) { return r.capacity / kStatSpread; }
+AHV_HD int64_t event_segment_size(const EventRing& r) { return r.capacity / kStatSpread; }
 
 struct EventRec {
   uint8_t type;
@@ -47,7 +47,7 @@ struct EventRec {
 };
 
 // `at` is the position within segment `seg`.
-AHV_HD inline void event_store(const EventRing& r, int seg, unsigned long long pos, int32_t slot, const EventRec& e) {
+AHV_HD void event_store(const EventRing& r, int seg, unsigned long long pos, int32_t slot, const EventRec& e) {
   const int64_t segsz = event_segment_size(r);
   if (pos >= static_cast<unsigned long long>(segsz)) return;
   const int64_t at = seg * segsz + static_cast<int64_t>(pos);

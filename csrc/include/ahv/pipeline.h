@@ -93,11 +93,11 @@ struct PipelineArgs {
   EventRing ev;
 };
 
-AHV_HD inline int64_t pipe_slot_base(const PipelineArgs& a) { return a.cursor ? a.cursor[0] : a.slot_base; }
-AHV_HD inline uint64_t pipe_id_base(const PipelineArgs& a) {
+AHV_HD int64_t pipe_slot_base(const PipelineArgs& a) { return a.cursor ? a.cursor[0] : a.slot_base; }
+AHV_HD uint64_t pipe_id_base(const PipelineArgs& a) {
   return a.cursor ? static_cast<uint64_t>(a.cursor[1]) : a.id_base;
 }
-AHV_HD inline int64_t pipe_now_us(const PipelineArgs& a) { return a.cursor ? a.cursor[2] : a.now_us; }
+AHV_HD int64_t pipe_now_us(const PipelineArgs& a) { return a.cursor ? a.cursor[2] : a.now_us; }
 
 // Per-session counters reduced into PipelineArgs::stats:
 // sessions, ok, participants, deltas, commitments, archived.
@@ -249,13 +249,13 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
 // has an event bus: created → joined → ring_assigned → activated → terminated →
 // audit.committed → gc_collected → archived (fewer when a stage was refused).
 
-AHV_HD inline uint32_t pipeline_event_count(const PipelineArgs& a, int64_t i, const PipeCounters& c) {
+AHV_HD uint32_t pipeline_event_count(const PipelineArgs& a, int64_t i, const PipeCounters& c) {
   const int64_t slot = (pipe_slot_base(a) + i) % a.capacity;
   return 1u + (c.v[2] ? 3u : 0u) + (a.t.sess_terminated_us[slot] ? 1u : 0u) + c.v[4] + 2u * c.v[5];
 }
 
 template <class Put>
-AHV_HD inline void pipeline_events(const PipelineArgs& a, int64_t i, const PipeCounters& c, Put&& put) {
+AHV_HD void pipeline_events(const PipelineArgs& a, int64_t i, const PipeCounters& c, Put&& put) {
   const int64_t slot = (pipe_slot_base(a) + i) % a.capacity;
   const SessionTables& t = a.t;
   const int32_t agent = a.session_agent[i];

@@ -69,11 +69,11 @@ struct SagaBatchArgs {
 // Per-step tables are step-major, [K][S]: lane s of a wave touches element
 // k*S + s, so every per-step access of a wave is one contiguous (coalesced)
 // segment instead of a stride-K gather.
-AHV_HD inline int64_t saga_elem(const SagaBatchArgs& a, int64_t s, int k) {
+AHV_HD int64_t saga_elem(const SagaBatchArgs& a, int64_t s, int k) {
   return static_cast<int64_t>(k) * a.sagas + s;
 }
 
-AHV_HD inline void saga_init(const SagaBatchArgs& a, int64_t s) {
+AHV_HD void saga_init(const SagaBatchArgs& a, int64_t s) {
   for (int k = 0; k < a.steps; ++k) {
     const int64_t e = saga_elem(a, s, k);
     a.step_state[e] = ST_PENDING;
@@ -90,7 +90,7 @@ AHV_HD inline void saga_init(const SagaBatchArgs& a, int64_t s) {
 }
 
 // Forward pass for step k (no-op once the saga has stopped).
-AHV_HD inline void saga_exec_step(const SagaBatchArgs& a, int64_t s, int k, int32_t& tick) {
+AHV_HD void saga_exec_step(const SagaBatchArgs& a, int64_t s, int k, int32_t& tick) {
   if (a.saga_state[s] != SG_RUNNING || a.failed_step[s] >= 0) return;
   const int64_t e = saga_elem(a, s, k);
   const int attempts = 1 + a.max_retries[e];
@@ -119,7 +119,7 @@ AHV_HD inline void saga_exec_step(const SagaBatchArgs& a, int64_t s, int k, int3
 }
 
 // After the forward pass: COMPLETED, or enter compensation / FAILED.
-AHV_HD inline void saga_decide(const SagaBatchArgs& a, int64_t s, int32_t& tick) {
+AHV_HD void saga_decide(const SagaBatchArgs& a, int64_t s, int32_t& tick) {
   if (a.saga_state[s] != SG_RUNNING) return;
   if (a.failed_step[s] < 0) {
     a.saga_state[s] = SG_COMPLETED;
@@ -133,7 +133,7 @@ AHV_HD inline void saga_decide(const SagaBatchArgs& a, int64_t s, int32_t& tick)
 }
 
 // Compensation of step k (called for k = K-1 … 0).
-AHV_HD inline void saga_comp_step(const SagaBatchArgs& a, int64_t s, int k, int32_t& tick) {
+AHV_HD void saga_comp_step(const SagaBatchArgs& a, int64_t s, int k, int32_t& tick) {
   if (a.saga_state[s] != SG_COMPENSATING) return;
   const int64_t e = saga_elem(a, s, k);
   if (a.step_state[e] != ST_COMMITTED) return;
@@ -154,7 +154,7 @@ AHV_HD inline void saga_comp_step(const SagaBatchArgs& a, int64_t s, int k, int3
   a.completed_us[e] = a.now_us + (tick++);
 }
 
-AHV_HD inline void saga_finish(const SagaBatchArgs& a, int64_t s, int32_t& tick) {
+AHV_HD void saga_finish(const SagaBatchArgs& a, int64_t s, int32_t& tick) {
   if (a.saga_state[s] != SG_COMPENSATING) return;
   a.saga_state[s] = a.comp_failed[s] > 0 ? SG_ESCALATED : SG_COMPLETED;
   a.saga_completed_us[s] = a.now_us + (tick++);
@@ -164,7 +164,7 @@ struct SagaCounters {
   uint32_t completed, escalated, failed, compensated;
 };
 
-AHV_HD inline SagaCounters saga_counters(const SagaBatchArgs& a, int64_t s) {
+AHV_HD SagaCounters saga_counters(const SagaBatchArgs& a, int64_t s) {
   SagaCounters c{0, 0, 0, 0};
   const uint8_t g = a.saga_state[s];
   c.completed = g == SG_COMPLETED;
@@ -179,7 +179,7 @@ AHV_HD inline SagaCounters saga_counters(const SagaBatchArgs& a, int64_t s) {
 // step-major), with the whole per-saga state machine in registers in between.
 // Produces exactly what saga_run_chain produces.
 template <int K>
-AHV_HD inline SagaCounters saga_run_chain_regs(const SagaBatchArgs& a, int64_t s) {
+AHV_HD SagaCounters saga_run_chain_regs(const SagaBatchArgs& a, int64_t s) {
   uint8_t st[K], rc[K], er[K];
   int64_t t0[K], t1[K];
   uint8_t fa[K], fk[K], cf[K], hu[K], mr[K];
@@ -281,7 +281,7 @@ constexpr int kMaxRegSagaSteps = 16;
   X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 
 // Whole chain for one saga (fused path).
-AHV_HD inline SagaCounters saga_run_chain(const SagaBatchArgs& a, int64_t s) {
+AHV_HD SagaCounters saga_run_chain(const SagaBatchArgs& a, int64_t s) {
   saga_init(a, s);
   int32_t tick = 0;
   for (int k = 0; k < a.steps; ++k) saga_exec_step(a, s, k, tick);
@@ -293,7 +293,7 @@ AHV_HD inline SagaCounters saga_run_chain(const SagaBatchArgs& a, int64_t s) {
 }
 
 // Fused chain: register-resident for K ≤ 16, generic (global-memory state) beyond.
-AHV_HD inline SagaCounters saga_run_chain_fused(const SagaBatchArgs& a, int64_t s) {
+AHV_HD SagaCounters saga_run_chain_fused(const SagaBatchArgs& a, int64_t s) {
   switch (a.steps) {
 #define AHV_SAGA_CASE(K) \
   case K:                \
