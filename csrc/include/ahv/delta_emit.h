@@ -83,6 +83,12 @@ struct HostSink {
     emit(*this);
     h.final(out);
   }
+  // The host streams every byte; the midstate modes only change the device's
+  // work, never the digest, so the host twin ignores them.
+  template <class Emit, class Mid>
+  AHV_HD void hash_mid(Emit&& emit, uint32_t out[8], Mid&, int) {
+    hash(emit, out);
+  }
   AHV_HD void stash(int j, const uint32_t d[8]) {
     for (int k = 0; k < 8; ++k) scratch[j][k] = d[k];
   }
@@ -360,14 +366,23 @@ AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const
   emit_lit(s, canon::K_CLOSE);
 }
 
+// Midstate reuse across the deltas of one session.  The payload's first 64 bytes
+// are `{"agent_did": "<did>", "changes": [{"content_hash": ` cut at 64 — fixed
+// text plus the agent DID — whenever the escaped DID is ≥ kMidstateMinDid bytes,
+// so every delta of the session shares its first SHA-256 block.  Mode 1 hashes
+// normally and captures the state after block 0 in `mid`; mode 2 resumes from
+// `mid` at byte 64 (one compression and part of the emission saved per delta).
+constexpr int32_t kMidstateMinDid = 16;
+enum MidMode : int { MID_OFF = 0, MID_CAPTURE = 1, MID_RESUME = 2 };
+
 template <class Sink>
 AHV_HD void emit_delta_and_hash(Sink& s, const StrPool& pool, StrRef agent, const ChangeIds* ch,
                                 uint32_t nch, int32_t delta_id_str, uint32_t turn,
                                 bool has_parent, const Digest parent, const SessionIdent sid, int64_t ts_us,
-                                uint32_t out[8]) {
-  s.hash([=](Sink& k) {
+                                uint32_t out[8], Digest& mid, int mid_mode) {
+  s.hash_mid([=](Sink& k) {
     emit_delta_payload(k, pool, agent, ch, nch, delta_id_str, turn, has_parent, parent, sid, ts_us);
-  }, out);
+  }, out, mid, mid_mode);
 }
 
 }  // namespace ahv

@@ -158,12 +158,14 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
 #pragma unroll
   for (int k = 0; k < 4; ++k) sid.uuid[k] = u[k];
   const StrRef did = pool_ref(a.pool, a.agent_did[agent]);  // resolved once per session
-  Digest prev;
+  Digest prev, mid;
   uint32_t* hrow = t.delta_hash + slot * a.dmax * 8;
+  const bool share_block0 = did.n >= kMidstateMinDid;  // every delta's block 0 is the same bytes
   for (int d = 0; d < a.deltas; ++d) {
     uint32_t h[8];
+    const int mode = !share_block0 ? MID_OFF : (d == 0 ? MID_CAPTURE : MID_RESUME);
     emit_delta_and_hash(sink, a.pool, did, a.changes + d * a.nch, static_cast<uint32_t>(a.nch), -1,
-                        static_cast<uint32_t>(d + 1), d > 0, prev, sid, now + d + 1, h);
+                        static_cast<uint32_t>(d + 1), d > 0, prev, sid, now + d + 1, h, mid, mode);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       prev.v[k] = h[k];

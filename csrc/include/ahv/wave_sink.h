@@ -21,6 +21,7 @@
 // block reads are conflict-free ds_read_b32.  16 KiB per wave → 10 waves/CU.
 #pragma once
 
+#include "ahv/delta_emit.h"
 #include "ahv/sha256.h"
 
 namespace ahv {
@@ -64,9 +65,24 @@ struct WaveWindowSink {
   // Hash the message produced by `emit(*this)`.
   template <class Emit>
   __device__ __forceinline__ void hash(Emit&& emit, uint32_t out[8]) {
+    Digest unused;
+    hash_mid(emit, out, unused, MID_OFF);
+  }
+
+  // As hash(), with midstate capture (MID_CAPTURE: state after block 0 → mid)
+  // or resumption (MID_RESUME: start from mid at byte 64, skipping block 0's
+  // emission and compression).  The mode may differ per lane.
+  template <class Emit>
+  __device__ __forceinline__ void hash_mid(Emit&& emit, uint32_t out[8], Digest& mid, int mode) {
     uint32_t st[8];
-    sha256_init(st);
-    lo = 0;
+    if (mode == MID_RESUME) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) st[k] = mid.v[k];
+      lo = 64;
+    } else {
+      sha256_init(st);
+      lo = 0;
+    }
     uint32_t total = 0;  // padded length, known after the first pass
     bool first = true;
     while (first || __any(lo < total)) {
@@ -93,6 +109,10 @@ struct WaveWindowSink {
 #pragma unroll
           for (int k = 0; k < 16; ++k) w[k] = g_ring[(blk * 16 + k) * kWaveLanes + lane];
           sha256_compress(st, w);
+          if (mode == MID_CAPTURE && lo == 0 && blk == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) mid.v[k] = st[k];
+          }
         }
       }
       first = false;
@@ -111,24 +131,20 @@ struct WaveWindowSink {
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = g_ring[(8 * j + k) * kWaveLanes + lane];
   }
-  // Merkle interior node; the three compressions share one loop body.
+  // Merkle interior node: two data blocks (hex of l, hex of r) share one loop
+  // body; the third is the constant padding block of a 128-byte message, whose
+  // message schedule (and K+W sums) the compiler folds to immediates.
   __device__ __forceinline__ void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const {
     uint32_t st[8];
     sha256_init(st);
 #pragma nounroll
-    for (int blk = 0; blk < 3; ++blk) {
+    for (int blk = 0; blk < 2; ++blk) {
       uint32_t w[16];
-      if (blk < 2) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) word_to_hex_words(blk == 0 ? l[k] : r[k], w[2 * k], w[2 * k + 1]);
-      } else {
-        w[0] = 0x80000000u;
-#pragma unroll
-        for (int k = 1; k < 15; ++k) w[k] = 0u;
-        w[15] = 1024u;
-      }
+      for (int k = 0; k < 8; ++k) word_to_hex_words(blk == 0 ? l[k] : r[k], w[2 * k], w[2 * k + 1]);
       sha256_compress(st, w);
     }
+    sha256_compress_pad_only(st, 128);
 #pragma unroll
     for (int k = 0; k < 8; ++k) out[k] = st[k];
   }
