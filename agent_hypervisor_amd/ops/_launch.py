@@ -15,6 +15,7 @@ from typing import Optional
 import torch
 
 from agent_hypervisor_amd._native import C
+from agent_hypervisor_amd.utils import faults as _faults
 
 
 def _check(name: str, key: str, t: torch.Tensor, dtype: Optional[torch.dtype]) -> None:
@@ -37,12 +38,16 @@ def launch(name: str, scalars: dict, tensors: dict, dtypes: Optional[dict] = Non
             continue
         _check(name, k, t, dtypes.get(k))
         args[k] = t.data_ptr()
+    if _faults.active() and not _faults.before_launch(name):
+        return dev  # injected fault: launch dropped
     if dev.type == "cuda":
         getattr(C, name)(args, torch.cuda.current_stream(dev).cuda_stream)
     elif dev.type == "cpu":
         getattr(C, name + "_host")(args)
     else:
         raise ValueError(f"{name}: unsupported device {dev}")
+    if _faults.active():
+        _faults.after_launch(name, tensors)
     return dev
 
 

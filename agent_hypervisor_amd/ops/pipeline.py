@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 
 from agent_hypervisor_amd._native import C
+from agent_hypervisor_amd.utils import faults as _faults
 
 
 def run(scalars: dict, tensors: dict[str, torch.Tensor | None]) -> None:
@@ -27,9 +28,13 @@ def run(scalars: dict, tensors: dict[str, torch.Tensor | None]) -> None:
         if not t.is_contiguous():
             raise ValueError(f"pipeline argument {k} must be contiguous")
         args[k] = t.data_ptr()
+    if _faults.active() and not _faults.before_launch("pipeline"):
+        return  # injected fault: launch dropped
     if dev.type == "cuda":
         C.pipeline(args, torch.cuda.current_stream(dev).cuda_stream)
     elif dev.type == "cpu":
         C.pipeline_host(args)
     else:
         raise ValueError(f"unsupported device {dev}")
+    if _faults.active():
+        _faults.after_launch("pipeline", tensors)

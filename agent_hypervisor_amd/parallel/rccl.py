@@ -115,3 +115,11 @@ class Communicator:
 
     def destroy(self) -> None:
         self._c.destroy()
+
+    def async_error(self) -> str:
+        """RCCL's asynchronous error text ("" while healthy)."""
+        return self._c.async_error()
+
+    def abort(self) -> None:
+        """Abort (not wait for) pending collectives — used by the watchdog when a peer is lost."""
+        self._c.abort()

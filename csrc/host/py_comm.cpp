@@ -109,6 +109,22 @@ class RcclComm {
       comm_ = nullptr;
     }
   }
+  // Asynchronous error state of the communicator (failure detection, §5.3):
+  // "" while healthy, else RCCL's error text.
+  std::string async_error() const {
+    if (!comm_) return "destroyed";
+    ncclResult_t st = ncclSuccess;
+    check_nccl(ncclCommGetAsyncError(comm_, &st), "ncclCommGetAsyncError");
+    return st == ncclSuccess || st == ncclInProgress ? std::string() : std::string(ncclGetErrorString(st));
+  }
+  // Tear down a communicator whose peers may be gone; pending collectives are
+  // cancelled instead of waited for.
+  void abort() {
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return device_; }
@@ -159,6 +175,8 @@ void register_comm(py::module_& m) {
       .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("all_to_all", &RcclComm::all_to_all, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &RcclComm::destroy)
+      .def("async_error", &RcclComm::async_error)
+      .def("abort", &RcclComm::abort)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("device", &RcclComm::device);

@@ -15,6 +15,7 @@ def test_rccl_world1_collectives(cuda_device):
     assert Communicator.version() > 0
     comm = Communicator.from_process_group(device=cuda_device.index or 0)
     assert comm.world == 1 and comm.rank == 0
+    assert comm.async_error() == ""  # healthy (watchdog input, §5.3)
     x = torch.arange(10, dtype=torch.float64, device=cuda_device)
     assert torch.equal(comm.all_reduce(x.clone()), x)
     assert torch.equal(comm.all_reduce(x.clone(), op="max"), x)
