@@ -112,3 +112,9 @@ __all__ = [
     "KillSwitch",
     "KillResult",
 ]
+
+# AHV_TRACE=1: instrument the host stages with roctx ranges + span log (§5.1)
+from agent_hypervisor_amd.utils import tracing as _tracing  # noqa: E402
+
+if _tracing.enabled():
+    _tracing.instrument()
