@@ -403,6 +403,9 @@ def create_app(hypervisor: Optional[Hypervisor] = None, event_bus: Optional[Hype
                                allow_headers=["*"])
     application.state.hv = ApiState(bus=event_bus or HypervisorEventBus(), hv=hypervisor)
     application.include_router(router)
+    from hypervisor.api.dashboard import router as dashboard_router
+
+    application.include_router(dashboard_router)
     return application
 
 

@@ -34,7 +34,7 @@ def test_health_and_stats(client):
 def test_route_count_matches_reference(client):
     paths = client.get("/openapi.json").json()["paths"]
     routes = {(m.upper(), p) for p, ops in paths.items() for m in ops}
-    routes.discard(("POST", "/api/v1/engine/pipeline"))
+    routes -= {("POST", "/api/v1/engine/pipeline"), ("GET", "/dashboard"), ("GET", "/api/v1/dashboard/summary")}
     assert len(routes) == 21
 
 
@@ -146,3 +146,20 @@ def test_pipeline_batch_endpoint_cpu(client, monkeypatch):
     assert r.status_code == 200, r.text
     body = r.json()
     assert body["completed"] == 256 and body["device"] == "cpu" and len(body["sample_merkle_root"]) == 64
+
+
+def test_dashboard_page_and_live_summary(client):
+    page = client.get("/dashboard")
+    assert page.status_code == 200 and "Agent Hypervisor" in page.text and "/api/v1/dashboard/summary" in page.text
+    sid = _session(client)
+    client.post(f"/api/v1/sessions/{sid}/join", json={"agent_did": "did:a", "sigma_raw": 0.8})
+    client.post(f"/api/v1/sessions/{sid}/vouch", json={"voucher_did": "did:hi", "vouchee_did": "did:a",
+                                                        "voucher_sigma": 0.9})
+    client.post(f"/api/v1/sessions/{sid}/sagas")
+    s = client.get("/api/v1/dashboard/summary").json()
+    assert s["overview"]["sessions"] == 1 and s["overview"]["participants"] == 1
+    assert s["rings"] == {"RING_2_STANDARD": 1}
+    assert s["sagas"]["by_state"] == {"running": 1}
+    assert s["liability"]["top_exposure"][0]["agent_did"] == "did:hi"
+    assert s["events"]["recent"][0]["event_type"] in {"saga.created", "liability.vouch_created"}
+    assert s["engine"] is None
