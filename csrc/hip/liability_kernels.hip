@@ -123,15 +123,47 @@ AHV_HD void sigma_eff_csr_elem(const VouchCsrArgs& a, int64_t i) {
     if (a.vouchee[k] == e && live_edge(a.active, a.expiry_us, k, a.now_us)) contrib += a.bonded[k];
   a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[s], contrib);
 }
-__global__ void sigma_eff_csr_kernel(VouchCsrArgs a) {
-  const int64_t n = a.sessions * kTile;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    sigma_eff_csr_elem(a, i);
+// Device: one lane per session walks its edges once in creation order and adds
+// each live bond into an LDS accumulator row of its vouchee (per-vouchee sums in
+// creation order — the same additions, in the same order, as the element form
+// above), then the block writes σ_eff for its 64×16 (session, vouchee) pairs
+// coalesced.  Edge fields are staged through LDS with coalesced loads.
+constexpr int kSigmaLdsEdges = 1024;
+
+__global__ __launch_bounds__(64) void sigma_eff_csr_kernel(VouchCsrArgs a) {
+  __shared__ uint8_t s_ve[kSigmaLdsEdges], s_lv[kSigmaLdsEdges];
+  __shared__ double s_bd[kSigmaLdsEdges];
+  __shared__ double s_acc[64 * (kTile + 1)];
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t s1 = s0 + 64 < a.sessions ? s0 + 64 : a.sessions;
+  const int64_t s = s0 + threadIdx.x;
+  const int32_t e0 = a.offsets[s0], e1 = a.offsets[s1];
+  if (e1 - e0 > kSigmaLdsEdges) {  // uniform per block: element form
+    for (int64_t i = s0 * kTile + threadIdx.x; i < s1 * kTile; i += 64) sigma_eff_csr_elem(a, i);
+    return;
+  }
+  for (int32_t k = e0 + threadIdx.x; k < e1; k += 64) {
+    s_ve[k - e0] = a.vouchee[k];
+    s_lv[k - e0] = live_edge(a.active, a.expiry_us, k, a.now_us) ? 1 : 0;
+    s_bd[k - e0] = a.bonded[k];
+  }
+  double* acc = s_acc + threadIdx.x * (kTile + 1);
+#pragma unroll
+  for (int j = 0; j < kTile; ++j) acc[j] = 0.0;
+  __syncthreads();
+  if (s < a.sessions) {
+    for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
+      if (s_lv[k - e0]) acc[s_ve[k - e0]] += s_bd[k - e0];
+  }
+  __syncthreads();
+  for (int64_t i = s0 * kTile + threadIdx.x; i < s1 * kTile; i += 64) {
+    const int64_t row = i / kTile - s0;
+    a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[i / kTile], s_acc[row * (kTile + 1) + i % kTile]);
+  }
 }
 void launch_sigma_eff_csr(const VouchCsrArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
-  hipLaunchKernelGGL(sigma_eff_csr_kernel, grid1(a.sessions * kTile), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(sigma_eff_csr_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
   check_hip(hipGetLastError(), "sigma_eff_csr_kernel");
 }
 void sigma_eff_csr_host(const VouchCsrArgs& a) {
@@ -240,35 +272,47 @@ void vouch_admit_host(const VouchAdmitArgs& a) { for (int64_t s = 0; s < a.sessi
 // vouchers, up to depth 2.  Clip records are written in reference history order
 // of the *clips* (parent clips before the child slash's clips).
 
-AHV_HD double score_of(const double* sc, int v) {
-  const double x = sc[v];
-  return x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
-}
+// Edge access for one session's CSR range.  The host twin (and blocks whose
+// edge range does not fit LDS) read the global arrays; the LDS view serves the
+// staged copy: voucher, vouchee and a precomputed `live` byte per edge.
+struct GlobalEdges {
+  const SlashArgs* a;
+  AHV_HD int voucher(int32_t k) const { return a->voucher[k]; }
+  AHV_HD int vouchee(int32_t k) const { return a->vouchee[k]; }
+  AHV_HD bool live(int32_t k) const { return live_edge(a->active, a->expiry_us, k, a->now_us); }
+  AHV_HD void release(int32_t k) const {
+    a->active[k] = 0;
+    a->released_us[k] = a->now_us;
+  }
+};
 
-AHV_HD bool has_live_voucher(const SlashArgs& a, int64_t s, int who) {
-  for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
-    if (a.vouchee[k] == who && live_edge(a.active, a.expiry_us, k, a.now_us)) return true;
+template <class Edges>
+AHV_HD bool has_live_voucher(const Edges& ed, int32_t b, int32_t e, int who) {
+  for (int32_t k = b; k < e; ++k)
+    if (ed.vouchee(k) == who && ed.live(k)) return true;
   return false;
 }
 
-AHV_HD void slash_session(const SlashArgs& a, int64_t s) {
-  double* sc = a.scores + s * kTile;
+// `sc` is the session's 16 scores (global row or LDS row, stride `ss`).
+template <class Edges>
+AHV_HD void slash_session_t(const SlashArgs& a, int64_t s, const Edges& ed, double* sc, int ss) {
+  const int32_t b = a.offsets[s], e = a.offsets[s + 1];
   const double omega = a.omega[s];
   const int32_t base = a.clip_offsets[s];
   int32_t nclip = 0;
-  // explicit stack of (vouchee, depth, first clip, next clip to examine)
-  int st_who[kMaxCascadeDepth + 1], st_first[kMaxCascadeDepth + 1], st_next[kMaxCascadeDepth + 1],
-      st_end[kMaxCascadeDepth + 1];
+  // explicit DFS stack, depth ≤ kMaxCascadeDepth (= 2): scalar slots, no arrays
+  int32_t next0 = 0, end0 = 0, next1 = 0, end1 = 0;
   int sp = 0;
   auto do_slash = [&](int who, int depth) {
-    sc[who] = 0.0;
+    sc[who * ss] = 0.0;
     const int32_t first = nclip;
-    for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k) {
-      if (a.vouchee[k] != who || !live_edge(a.active, a.expiry_us, k, a.now_us)) continue;
-      const int v = a.voucher[k];
-      const double before = score_of(sc, v);
+    for (int32_t k = b; k < e; ++k) {
+      if (ed.vouchee(k) != who || !ed.live(k)) continue;
+      const int v = ed.voucher(k);
+      const double x = sc[v * ss];
+      const double before = x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
       const double after = clip_sigma(before, omega);
-      sc[v] = after;
+      sc[v * ss] = after;
       if (nclip < a.clip_cap) {
         a.clip_voucher[base + nclip] = static_cast<uint8_t>(v);
         a.clip_depth[base + nclip] = static_cast<uint8_t>(depth);
@@ -276,35 +320,87 @@ AHV_HD void slash_session(const SlashArgs& a, int64_t s) {
         a.clip_after[base + nclip] = after;
       }
       ++nclip;
-      a.active[k] = 0;
-      a.released_us[k] = a.now_us;
+      ed.release(k);
     }
-    st_who[sp] = who;
-    st_first[sp] = first;
-    st_next[sp] = first;
-    st_end[sp] = nclip;
+    if (sp == 0) {
+      next0 = first;
+      end0 = nclip;
+    } else if (sp == 1) {
+      next1 = first;
+      end1 = nclip;
+    }  // a depth-2 frame never expands, so it needs no cursor
+    static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
     ++sp;
   };
   do_slash(a.target[s], 0);
   while (sp > 0) {
-    const int top = sp - 1;
-    const int depth = top;
-    if (depth >= kMaxCascadeDepth || st_next[top] >= st_end[top]) {
+    const int depth = sp - 1;
+    int32_t& nx = depth == 0 ? next0 : next1;
+    const int32_t en = depth == 0 ? end0 : end1;
+    if (depth >= kMaxCascadeDepth || nx >= en) {
       --sp;
       continue;
     }
-    const int32_t ci = st_next[top]++;
+    const int32_t ci = nx++;
     if (ci >= a.clip_cap) continue;
     const int v = a.clip_voucher[base + ci];
-    if (a.clip_after[base + ci] < kCascadeBelow && has_live_voucher(a, s, v)) do_slash(v, depth + 1);
+    if (a.clip_after[base + ci] < kCascadeBelow && has_live_voucher(ed, b, e, v)) do_slash(v, depth + 1);
   }
   a.clip_count[s] = nclip;
 }
-__global__ void slash_kernel(SlashArgs a) {
-  for (int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; s < a.sessions;
-       s += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    slash_session(a, s);
+
+AHV_HD void slash_session(const SlashArgs& a, int64_t s) {
+  slash_session_t(a, s, GlobalEdges{&a}, a.scores + s * kTile, 1);
 }
+
+// Device: a workgroup of 64 sessions stages its contiguous edge range
+// (voucher, vouchee, live) and its 64×16 score rows in LDS with coalesced loads,
+// runs the cascades out of LDS (one lane per session), and writes the scores
+// back coalesced.  Releases go straight to global (sparse).  A block whose edge
+// range exceeds the staging buffer falls back to the global-memory path.
+constexpr int kSlashLdsEdges = 2048;
+constexpr int kScorePad = kTile + 1;  // 17 doubles per row: spreads a column over banks
+
+struct LdsEdges {
+  const SlashArgs* a;
+  int32_t e0;
+  const uint8_t* vr;
+  const uint8_t* ve;
+  uint8_t* lv;
+  __device__ int voucher(int32_t k) const { return vr[k - e0]; }
+  __device__ int vouchee(int32_t k) const { return ve[k - e0]; }
+  __device__ bool live(int32_t k) const { return lv[k - e0] != 0; }
+  __device__ void release(int32_t k) const {
+    lv[k - e0] = 0;
+    a->active[k] = 0;
+    a->released_us[k] = a->now_us;
+  }
+};
+
+__global__ __launch_bounds__(64) void slash_kernel(SlashArgs a) {
+  __shared__ uint8_t s_vr[kSlashLdsEdges], s_ve[kSlashLdsEdges], s_lv[kSlashLdsEdges];
+  __shared__ double s_sc[64 * kScorePad];
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t s1 = s0 + 64 < a.sessions ? s0 + 64 : a.sessions;
+  const int64_t s = s0 + threadIdx.x;
+  const int32_t e0 = a.offsets[s0], e1 = a.offsets[s1];
+  if (e1 - e0 > kSlashLdsEdges) {  // uniform per block
+    if (s < a.sessions) slash_session(a, s);
+    return;
+  }
+  for (int32_t k = e0 + threadIdx.x; k < e1; k += 64) {
+    s_vr[k - e0] = a.voucher[k];
+    s_ve[k - e0] = a.vouchee[k];
+    s_lv[k - e0] = live_edge(a.active, a.expiry_us, k, a.now_us) ? 1 : 0;
+  }
+  const int64_t nsc = (s1 - s0) * kTile;
+  for (int64_t j = threadIdx.x; j < nsc; j += 64) s_sc[(j / kTile) * kScorePad + j % kTile] = a.scores[s0 * kTile + j];
+  __syncthreads();
+  if (s < a.sessions) slash_session_t(a, s, LdsEdges{&a, e0, s_vr, s_ve, s_lv}, s_sc + threadIdx.x * kScorePad, 1);
+  __syncthreads();
+  for (int64_t j = threadIdx.x; j < nsc; j += 64) a.scores[s0 * kTile + j] = s_sc[(j / kTile) * kScorePad + j % kTile];
+}
+
 void launch_slash(const SlashArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
   hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
