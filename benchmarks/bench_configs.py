@@ -37,6 +37,7 @@ from agent_hypervisor_amd.models.saga_engine import SagaBatchEngine, SagaOutcome
 from agent_hypervisor_amd.ops import audit as A  # noqa: E402
 from agent_hypervisor_amd.ops import liability as LI  # noqa: E402
 from agent_hypervisor_amd.ops import rings as R  # noqa: E402
+from agent_hypervisor_amd.parallel import agent_shard as AS  # noqa: E402
 from agent_hypervisor_amd.parallel import collectives as X  # noqa: E402
 from agent_hypervisor_amd.parallel.directory import shard_counts  # noqa: E402
 from agent_hypervisor_amd.runtime.graphs import PipelineGraph  # noqa: E402
@@ -155,21 +156,34 @@ def config3(ctx: Ctx, args):
     members = torch.randint(0, A_, (S, 16), device=ctx.dev, generator=gen)
     sigma = eng.agents.sigma[members]
     omega = torch.full((S,), 0.5, dtype=f64, device=ctx.dev)
-    exposure = torch.zeros(A_, dtype=f64, device=ctx.dev)
+    # double-buffered exposure view: step i's exchange runs on a side stream (P03)
+    # while step i+1's pipeline kernel runs; owner mode reduce-scatters so each
+    # rank keeps only the agents it owns (P02), half the all-reduce traffic
+    exposure = [torch.zeros(A_, dtype=f64, device=ctx.dev) for _ in range(2)]
+    comm = [AS.OverlappedCollective(ctx.dev) for _ in range(2)]
+    owned = {}
+    exchange = (lambda t: owned.__setitem__("view", AS.reduce_to_owners(t))) if args.owner_reduce \
+        else X.allreduce_exposure
+    it = [0]
 
     def step():
+        cur = it[0] & 1
+        it[0] += 1
         stats.zero_()
         agents = torch.randint(0, A_, (S,), device=ctx.dev, dtype=i32, generator=gen)
         eng.run_pipeline(S, agents=agents, stats=stats)
         tiles = LI.build_tiles(vb, 0)
         _, expo, _ = LI.bond_tiles(tiles, sigma, omega)
-        exposure.zero_()
-        exposure.index_add_(0, members.reshape(-1), expo.reshape(-1))
-        X.allreduce_exposure(exposure)  # X01 over RCCL / xGMI
+        comm[cur].wait()  # buffer reuse: the exchange from two steps ago is done
+        exposure[cur].zero_()
+        exposure[cur].index_add_(0, members.reshape(-1), expo.reshape(-1))
+        comm[cur].launch(exchange, exposure[cur])  # X01 over RCCL / xGMI, overlapped
         X.allreduce_stats(stats)
 
     el, lat = ctx.timed(step, args.steps, args.warmup)
-    ctx.emit(config="config3", what="pipeline+vouch tiles+exposure all_reduce[A]", agents=A_,
+    ctx.emit(config="config3", what="pipeline+vouch tiles+exposure " + ("reduce_scatter to owners" if args.owner_reduce
+                                                                          else "all_reduce[A]") + " (overlapped)",
+             agents=A_,
              sessions_global=args.sessions or 100_000, sessions_per_rank=S, exposure_bytes=A_ * 8,
              batch_p50_ms=statistics.median(lat) * 1e3, ms_per_step=el / args.steps * 1e3,
              sessions_per_s=(args.sessions or 100_000) * args.steps / el, scaling="strong",
@@ -256,6 +270,7 @@ def main():
     ap.add_argument("--agents", type=int, default=0)
     ap.add_argument("--edges", type=int, default=0)
     ap.add_argument("--deltas", type=int, default=0)
+    ap.add_argument("--owner-reduce", action="store_true", help="config3: reduce-scatter exposure to agent owners")
     args = ap.parse_args()
     ctx = Ctx(args.device)
     for c in args.configs:
