@@ -1,10 +1,12 @@
 // Batched governance pipeline kernel (gfx950) and its host twin.
 //
-// Geometry: one wave (64 lanes) per workgroup, one session per lane, a 16 KiB LDS
-// message ring per wave (ahv/wave_sink.h) → LDS allows 10 waves per CU; the SHA
-// rounds are pure VALU (v_alignbit / v_bfi / v_add3), so ≥2 waves per SIMD keep
-// the issue slots busy.  A launch of n sessions is ⌈n/64⌉ workgroups: the 256
-// CUs are saturated from ~160k sessions per batch (10 waves × 256 CUs × 64).
+// Geometry: one wave (64 lanes) per workgroup, one session per lane, a
+// kWinBlocks-block LDS message window per wave (ahv/wave_sink.h: 12.5 KiB for 3
+// blocks → 12 waves per CU, 3 per SIMD).  The SHA rounds are pure VALU
+// (v_alignbit / v_bitop3 / v_add3); a wave alone issues a VALU op every 4
+// cycles against the SIMD's 2, so ≥2 waves per SIMD keep the issue slots busy
+// (measured SHA-256 ceiling: scripts/exp/sha_sol.hip).  A launch of n sessions is
+// ⌈n/64⌉ workgroups: the 256 CUs are saturated from ~200k sessions per batch.
 // There is no inter-workgroup data reuse, so no XCD remapping is needed.
 //
 // Batch counters (collective X04 input) are reduced across the wave with DPP
@@ -23,17 +25,17 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// (64 threads, ≥MinWaves waves per SIMD).  MinWaves = 4 caps the allocation at
-// 128 VGPRs (16 waves per CU) at the price of a small spill; measured 1.3-1.5 %
-// faster than MinWaves = 3 (168 VGPRs).  Both are instantiated; AHV_PIPE_WAVES=3
-// selects the other one for A/B runs.
+// (64 threads, ≥MinWaves waves per SIMD).  The LDS window already caps residency
+// at 16 / kWinBlocks·… waves per SIMD (4 for 2 blocks, 3 for 3), so MinWaves
+// matches it: the VGPR budget is 128 or 168 registers, without spills.
+// Both are instantiated; AHV_PIPE_WAVES=3|4 overrides the choice for A/B runs.
 template <int MinWaves>
 __global__ __launch_bounds__(kWaveLanes, MinWaves) void governance_pipeline_kernel(PipelineArgs a) {
   const uint32_t lane = threadIdx.x;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
   PipeCounters c{};
   if (i < a.n) {
-    WaveWindowSink sink;
+    WordWindowSink sink;
     sink.lane = lane;
     c = pipeline_session(a, i, sink);
   }
@@ -72,7 +74,8 @@ __global__ __launch_bounds__(kWaveLanes, MinWaves) void governance_pipeline_kern
 static int pipeline_waves() {
   static const int w = [] {
     const char* e = std::getenv("AHV_PIPE_WAVES");
-    return e && std::atoi(e) == 3 ? 3 : 4;
+    if (e && (std::atoi(e) == 3 || std::atoi(e) == 4)) return std::atoi(e);
+    return kWinBlocks <= 2 ? 4 : 3;
   }();
   return w;
 }

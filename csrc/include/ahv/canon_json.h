@@ -24,6 +24,7 @@ constexpr char K_CH_PREV[] = ", \"previous_hash\": ";            // then <json s
 constexpr char K_CH_CLOSE[] = "}";
 constexpr char K_CH_SEP[] = ", ";
 constexpr char K_DELTA_ID[] = "], \"delta_id\": ";               // then <json str>
+constexpr char K_DELTA_PFX[] = "\"delta:";                        // then <int> "
 constexpr char K_PARENT[] = ", \"parent_hash\": ";               // then null | "<64 hex>"
 constexpr char K_SESSION[] = ", \"session_id\": ";               // then <json str>
 constexpr char K_TS[] = ", \"timestamp\": ";                     // then <json str>

@@ -2,12 +2,14 @@
 //
 // One emitter, two sinks:
 //   * HostSink        — streams bytes into SHA-256 (host twin / CPU tests);
-//   * WaveWindowSink  — (ahv/wave_sink.h) assembles a 256-byte window of each
-//     lane's message in LDS per pass and compresses it on the device.
+//   * WordWindowSink  — (ahv/wave_sink.h) assembles a window of each lane's
+//     message in LDS, a 32-bit word at a time, and compresses it on the device.
 //
-// Emitter contract: before writing a segment the emitter calls `s.want(len)`
+// Emitter contract: before writing a segment the emitter calls `s.seg(len)`
 // with the segment's exact byte length; a false answer means the sink skipped
 // the segment (its bytes are outside the current window) and nothing is written.
+// Bytes are handed over in big-endian chunks: `put4(v)` = 4 bytes, `put(v, n)`
+// = the top n ∈ [0, 4] bytes of v (the rest of v zero; n may differ per lane).
 //
 // Byte-exact with json.dumps(sort_keys=True) of the reference payload
 // (audit/delta.py:43-63); pool strings are stored pre-escaped (JSON body without
@@ -72,11 +74,16 @@ AHV_HD uint32_t iso_utc(int64_t us, uint8_t* out) {
 struct HostSink {
   Sha256Stream h;
   uint32_t scratch[8][8];
-  AHV_HD bool want(uint32_t) { return true; }
+  AHV_HD bool seg(uint32_t) { return true; }
+  AHV_HD void put4(uint32_t v) {
+    for (int j = 0; j < 4; ++j) h.put(static_cast<uint8_t>(v >> (24 - 8 * j)));
+  }
+  AHV_HD void put(uint32_t v, uint32_t n) {
+    for (uint32_t j = 0; j < n; ++j) h.put(static_cast<uint8_t>(v >> (24 - 8 * j)));
+  }
+  AHV_HD bool any(bool b) const { return b; }
   template <class T>
   AHV_HD void launder(T&) const {}
-  AHV_HD void byte(uint8_t b) { h.put(b); }
-  AHV_HD bool any(bool b) const { return b; }
   template <class Emit>
   AHV_HD void hash(Emit&& emit, uint32_t out[8]) {
     h.init();
@@ -138,6 +145,41 @@ AHV_HD void merkle_root_counter(Sink& s, uint32_t n, Leaf&& leaf, uint32_t root[
   }
 }
 
+// Level-wise Merkle root of `n` leaves read by `leaf(i, out)` (reference
+// audit/delta.py:117-134: odd node duplicated), with every interior node hashed
+// at ONE call site: level 1 reads the leaves, later levels work in place on the
+// sink's scratch slots (node j overwrites slot j after reading 2j and 2j+1).
+// Needs ⌈n/2⌉ scratch slots.
+template <class Sink, class Leaf>
+AHV_HD void merkle_root_levels(Sink& s, uint32_t n, Leaf&& leaf, uint32_t root[8]) {
+  if (n == 1) {
+    leaf(0, root);
+    return;
+  }
+  uint32_t m = n;
+  bool from_leaves = true;
+  while (m > 1) {
+    const uint32_t half = (m + 1) >> 1;
+#pragma nounroll
+    for (uint32_t j = 0; j < half; ++j) {
+      const uint32_t ri = 2 * j + 1 < m ? 2 * j + 1 : 2 * j;
+      uint32_t l[8], r[8], o[8];
+      if (from_leaves) {
+        leaf(2 * j, l);
+        leaf(ri, r);
+      } else {
+        s.load(static_cast<int>(2 * j), l);
+        s.load(static_cast<int>(ri), r);
+      }
+      s.node(l, r, o);
+      s.stash(static_cast<int>(j), o);
+    }
+    m = half;
+    from_leaves = false;
+  }
+  s.load(0, root);
+}
+
 // Level-wise Merkle root over `m` (≤ 8) digests stashed in the sink's scratch
 // slots 0..m-1 (reference audit/delta.py:117-134: odd node duplicated).
 template <class Sink>
@@ -158,15 +200,32 @@ AHV_HD void merkle_root_stashed(Sink& s, int m, uint32_t root[8]) {
 
 // ------------------------------------------------------------ emission API
 
-template <class Sink>
-AHV_HD void emit_lit(Sink& s, const char* lit, uint32_t n) {
-  if (!s.want(n)) return;
-  for (uint32_t i = 0; i < n; ++i) s.byte(static_cast<uint8_t>(lit[i]));
+// Byte i of a literal as the top byte of a word (0 past the end).
+template <size_t N>
+AHV_HD constexpr uint32_t lit_byte(const char (&lit)[N], size_t i) {
+  return i < N - 1 ? static_cast<uint32_t>(static_cast<uint8_t>(lit[i])) : 0u;
 }
 
+// A compile-time literal as whole big-endian words plus a tail chunk (after
+// inlining every word is an immediate).
 template <class Sink, size_t N>
 AHV_HD void emit_lit(Sink& s, const char (&lit)[N]) {
-  emit_lit(s, lit, static_cast<uint32_t>(N - 1));
+  constexpr uint32_t n = static_cast<uint32_t>(N - 1);
+  if (!s.seg(n)) return;
+#pragma unroll
+  for (uint32_t i = 0; i + 4 <= n; i += 4)
+    s.put4(lit_byte(lit, i) << 24 | lit_byte(lit, i + 1) << 16 | lit_byte(lit, i + 2) << 8 | lit_byte(lit, i + 3));
+  constexpr uint32_t t = n & 3u;
+  if (t) {
+    const uint32_t i = n & ~3u;
+    s.put(lit_byte(lit, i) << 24 | lit_byte(lit, i + 1) << 16 | lit_byte(lit, i + 2) << 8, t);
+  }
+}
+
+// One ASCII byte (a segment of its own).
+template <class Sink>
+AHV_HD void emit_char(Sink& s, uint32_t c) {
+  if (s.seg(1)) s.put(c << 24, 1);
 }
 
 // A resolved pool string: 16-byte aligned pointer + length (-1 = null).
@@ -184,16 +243,24 @@ struct alignas(16) U4 {
   uint32_t a, b, c, d;
 };
 
-// Up to 4 bytes of a little-endian memory word, in memory order.
-template <class Sink>
-AHV_HD void emit_word_le(Sink& s, uint32_t w, uint32_t cnt) {
-  const uint32_t m = cnt < 4u ? cnt : 4u;
-  for (uint32_t j = 0; j < m; ++j) s.byte(static_cast<uint8_t>(w >> (8 * j)));
+AHV_HD uint32_t bswap_word(uint32_t w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(0u, w, 0x00010203u);
+#else
+  return bswap32(w);
+#endif
 }
 
-// Quoted string body from 16-byte aligned storage, read 16 bytes per load with
-// the next chunk prefetched (a byte-per-load loop waits a full memory latency per
-// character on the device).
+// Top `cnt` bytes (clamped to [0, 4]) of a little-endian memory word, in memory order.
+template <class Sink>
+AHV_HD void emit_word_le(Sink& s, uint32_t w, int32_t cnt) {
+  const uint32_t m = cnt <= 0 ? 0u : (cnt >= 4 ? 4u : static_cast<uint32_t>(cnt));
+  const uint32_t keep = m >= 4u ? 0xffffffffu : ~(0xffffffffu >> (8u * m));
+  s.put(bswap_word(w) & keep, m);
+}
+
+// Quoted string body from 16-byte aligned storage, 16 bytes per load; the byte
+// count may differ per lane (lanes past their end hand over zero bytes).
 template <class Sink>
 AHV_HD void emit_str_ref(Sink& s, StrRef r) {
   if (r.n < 0) {
@@ -201,22 +268,21 @@ AHV_HD void emit_str_ref(Sink& s, StrRef r) {
     return;
   }
   const uint32_t n = static_cast<uint32_t>(r.n);
-  if (!s.want(n + 2)) return;
-  s.byte('"');
+  if (!s.seg(n + 2)) return;
+  s.put(0x22u << 24, 1);
   const U4* q = reinterpret_cast<const U4*>(r.p);
   const uint32_t chunks = (n + 15) / 16;
-  // one 16-byte load per chunk (loop-carried prefetch copies made the compiler keep the chunk in scratch)
   for (uint32_t c = 0; c < chunks; ++c) {
     const U4 cur = q[c];
-    const uint32_t left = n - 16 * c;
+    const int32_t left = static_cast<int32_t>(n - 16 * c);
     // four named words (no indexing into the chunk: a runtime index would put
     // it in scratch memory on the device)
     emit_word_le(s, cur.a, left);
-    emit_word_le(s, cur.b, left > 4 ? left - 4 : 0);
-    emit_word_le(s, cur.c, left > 8 ? left - 8 : 0);
-    emit_word_le(s, cur.d, left > 12 ? left - 12 : 0);
+    emit_word_le(s, cur.b, left - 4);
+    emit_word_le(s, cur.c, left - 8);
+    emit_word_le(s, cur.d, left - 12);
   }
-  s.byte('"');
+  s.put(0x22u << 24, 1);
 }
 
 // Pool string id as a JSON value: "…" or null.
@@ -229,72 +295,75 @@ AHV_HD void emit_pool_str(Sink& s, const StrPool& pool, int32_t id) {
 // by a runtime position would live in scratch memory on the device).
 template <class Sink>
 AHV_HD void emit_uint(Sink& s, uint64_t v) {
-  if (!s.want(canon::dec_digits(v))) return;
+  if (!s.seg(canon::dec_digits(v))) return;
   uint64_t p = 1;
   while (v / p >= 10) p *= 10;
-  for (; p; p /= 10) s.byte(static_cast<uint8_t>('0' + (v / p) % 10));
+  for (; p; p /= 10) s.put(static_cast<uint32_t>('0' + (v / p) % 10) << 24, 1);
 }
 
+// "<64 hex>" of a digest: 16 SWAR hex words between the quotes.
 template <class Sink>
 AHV_HD void emit_hex_digest_quoted(Sink& s, const uint32_t d[8]) {
-  if (!s.want(66)) return;
-  s.byte('"');
-  // one digest word per iteration (a fully unrolled 64-char body keeps all 64
-  // characters live in VGPRs at once)
+  if (!s.seg(66)) return;
+  s.put(0x22u << 24, 1);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const uint32_t w = d[i];
-#pragma nounroll
-    for (int j = 7; j >= 0; --j) s.byte(static_cast<uint8_t>(hex_nibble((w >> (4 * j)) & 15u)));
+    uint32_t hi, lo;
+    word_to_hex_words(d[i], hi, lo);
+    s.put4(hi);
+    s.put4(lo);
   }
-  s.byte('"');
+  s.put(0x22u << 24, 1);
 }
 
 // "session:xxxxxxxx-xxxx-xxxx-xxxx-xxxxxxxxxxxx" from 4 big-endian uuid words.
 template <class Sink>
 AHV_HD void emit_session_uuid_quoted(Sink& s, const uint32_t u[4]) {
-  if (!s.want(46)) return;
-  const char* pre = "\"session:";
-  for (int i = 0; i < 9; ++i) s.byte(static_cast<uint8_t>(pre[i]));
-  // 128-bit id as two 64-bit halves, nibbles by shifting (no array selection)
-  const uint64_t hi = (static_cast<uint64_t>(u[0]) << 32) | u[1];
-  const uint64_t lo = (static_cast<uint64_t>(u[2]) << 32) | u[3];
-#pragma nounroll
-  for (int k = 0; k < 32; ++k) {
-    if (k == 8 || k == 12 || k == 16 || k == 20) s.byte('-');
-    const uint64_t src = k < 16 ? hi : lo;
-    s.byte(static_cast<uint8_t>(hex_nibble(static_cast<uint32_t>(src >> (60 - 4 * (k & 15))) & 15u)));
-  }
-  s.byte('"');
+  if (!s.seg(46)) return;
+  s.put4(0x22736573u);  // "ses
+  s.put4(0x73696f6eu);  // sion
+  s.put(0x3a000000u, 1);  // :
+  uint32_t hi, lo;
+  word_to_hex_words(u[0], hi, lo);
+  s.put4(hi);
+  s.put4(lo);
+  s.put(0x2d000000u, 1);
+  word_to_hex_words(u[1], hi, lo);
+  s.put4(hi);
+  s.put(0x2d000000u, 1);
+  s.put4(lo);
+  s.put(0x2d000000u, 1);
+  word_to_hex_words(u[2], hi, lo);
+  s.put4(hi);
+  s.put(0x2d000000u, 1);
+  s.put4(lo);
+  word_to_hex_words(u[3], hi, lo);
+  s.put4(hi);
+  s.put4(lo);
+  s.put(0x22000000u, 1);
 }
 
-template <class Sink>
-AHV_HD void emit_2d(Sink& s, uint32_t v) {
-  s.byte(static_cast<uint8_t>('0' + v / 10));
-  s.byte(static_cast<uint8_t>('0' + v % 10));
-}
+// Two decimal digits of v < 100 as the top half of a word.
+AHV_HD uint32_t dig2(uint32_t v) { return (('0' + v / 10) << 24) | (('0' + v % 10) << 16); }
 
 // datetime.isoformat() text, quoted, straight into the sink.
 template <class Sink>
 AHV_HD void emit_iso_quoted(Sink& s, int64_t us) {
   const UtcParts t = utc_parts(us);
-  if (!s.want(t.micro ? 34u : 27u)) return;
-  s.byte('"');
-  emit_2d(s, (t.year / 100) % 100);
-  emit_2d(s, t.year % 100);
-  s.byte('-'); emit_2d(s, t.month);
-  s.byte('-'); emit_2d(s, t.day);
-  s.byte('T'); emit_2d(s, t.secs / 3600);
-  s.byte(':'); emit_2d(s, (t.secs / 60) % 60);
-  s.byte(':'); emit_2d(s, t.secs % 60);
+  if (!s.seg(t.micro ? 34u : 27u)) return;
+  // "YYYY-MM-DDTHH:MM:SS
+  s.put(0x22000000u | (dig2((t.year / 100) % 100) >> 8), 3);
+  s.put(dig2(t.year % 100) | 0x2d00u | ((t.month / 10) + '0'), 4);
+  s.put((('0' + t.month % 10) << 24) | 0x2d0000u | (dig2(t.day) >> 16), 4);
+  s.put(0x54000000u | (dig2(t.secs / 3600) >> 8) | 0x3au, 4);
+  s.put(dig2((t.secs / 60) % 60) | 0x3a00u | ('0' + (t.secs % 60) / 10), 4);
+  s.put(static_cast<uint32_t>('0' + t.secs % 10) << 24, 1);
   if (t.micro) {
-    s.byte('.');
-    emit_2d(s, t.micro / 10000);
-    emit_2d(s, (t.micro / 100) % 100);
-    emit_2d(s, t.micro % 100);
+    s.put(0x2e000000u | (dig2(t.micro / 10000) >> 8) | ('0' + (t.micro / 1000) % 10), 4);
+    s.put((('0' + (t.micro / 100) % 10) << 24) | (dig2(t.micro % 100) >> 8), 3);
   }
-  const char* tz = "+00:00\"";
-  for (int i = 0; i < 7; ++i) s.byte(static_cast<uint8_t>(tz[i]));
+  s.put4(0x2b30303au);  // +00:
+  s.put(0x30302200u, 3);  // 00"
 }
 
 // One change object {"content_hash", "operation", "path", "previous_hash"}.
@@ -320,12 +389,11 @@ template <class Sink>
 AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const ChangeIds* ch,
                                uint32_t nch, int32_t delta_id_str, uint32_t turn, bool has_parent,
                                Digest parent, SessionIdent sid, int64_t ts_us) {
-  // The device sink calls this once per window pass; laundering the inputs stops
-  // the compiler from hoisting every derived character (64 hex digits, uuid,
-  // timestamp digits) out of the pass loop and keeping them all live in VGPRs.
+  // The device sink calls this once per window pass; laundering the per-lane
+  // inputs stops the compiler from hoisting every derived hex word (parent
+  // digest, uuid) out of the pass loop and keeping them all live in VGPRs.
+  // (turn and the timestamp are wave-uniform: their digits live in SGPRs.)
   s.launder(agent.n);
-  s.launder(turn);
-  s.launder(ts_us);
 #pragma unroll
   for (int k = 0; k < 8; ++k) s.launder(parent.v[k]);
 #pragma unroll
@@ -349,9 +417,9 @@ AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const
   if (delta_id_str >= 0) {
     emit_pool_str(s, pool, delta_id_str);
   } else {
-    emit_lit(s, "\"delta:", 7);
+    emit_lit(s, canon::K_DELTA_PFX);
     emit_uint(s, turn);
-    emit_lit(s, "\"", 1);
+    emit_char(s, 0x22u);
   }
   emit_lit(s, canon::K_PARENT);
   if (has_parent) emit_hex_digest_quoted(s, parent.v);
@@ -367,12 +435,15 @@ AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const
 }
 
 // Midstate reuse across the deltas of one session.  The payload's first 64 bytes
-// are `{"agent_did": "<did>", "changes": [{"content_hash": ` cut at 64 — fixed
-// text plus the agent DID — whenever the escaped DID is ≥ kMidstateMinDid bytes,
-// so every delta of the session shares its first SHA-256 block.  Mode 1 hashes
+// are `{"agent_did": "<did>", "changes": [{"content_hash": ` (47 + |did| bytes) or,
+// with no changes, `{"agent_did": "<did>", "changes": [], "delta_id": "delta:`
+// (52 + |did|) cut at 64 — fixed text plus the agent DID — whenever the escaped
+// DID is ≥ kMidstateMinDid bytes, so every delta of the session shares its first
+// SHA-256 block.  (At 16 bytes, byte 63 would be the first byte of the first
+// content hash value, '"' or 'n', which may differ between deltas.)  Mode 1 hashes
 // normally and captures the state after block 0 in `mid`; mode 2 resumes from
 // `mid` at byte 64 (one compression and part of the emission saved per delta).
-constexpr int32_t kMidstateMinDid = 16;
+constexpr int32_t kMidstateMinDid = 17;
 enum MidMode : int { MID_OFF = 0, MID_CAPTURE = 1, MID_RESUME = 2 };
 
 template <class Sink>

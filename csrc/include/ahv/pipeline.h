@@ -18,7 +18,7 @@
 namespace ahv {
 
 constexpr int kMaxParticipants = 16;  // participant row width (max_participants ≤ 16)
-constexpr int kMaxDeltasPipeline = 8;
+constexpr int kMaxDeltasPipeline = 8;  // ⌈8/2⌉ Merkle scratch slots fit the LDS window
 constexpr int kMaxChanges = 4;
 
 // SoA device tables (one row per session slot).  All pointers are device
@@ -206,10 +206,10 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
     status = PIPE_BAD_TERMINATE;
   }
   // Merkle root: leaves re-read from this session's delta_hash row (written by this
-  // same lane above) into the sink's digest scratch (LDS on the device).
+  // same lane above); interior levels in the sink's digest scratch (LDS on the device).
   uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (a.deltas > 0) {
-    merkle_root_counter(
+    merkle_root_levels(
         sink, static_cast<uint32_t>(a.deltas),
         [&](uint32_t d, uint32_t h[8]) {
 #pragma unroll

@@ -122,13 +122,28 @@ AHV_HD void sha256_compress_pad_only(uint32_t st[8], uint64_t total_bytes) {
 // Lowercase hex of a nibble, as an ASCII byte.
 AHV_HD uint32_t hex_nibble(uint32_t n) { return n + (n < 10u ? 0x30u : 0x57u); }
 
+// Four hex chars from two bytes laid out as x = [Bh Bh Bl Bl] (SWAR): spread
+// the nibbles to one per byte, then add '0' and, where the nibble is ≥ 10, the
+// extra 0x27 that lands on 'a' — per byte, with no carry between bytes.
+AHV_HD uint32_t hex4_spread(uint32_t x) {
+  const uint32_t n = ((x >> 4) & 0x0F000F00u) | (x & 0x000F000Fu);
+  const uint32_t m = ((n + 0x06060606u) >> 4) & 0x01010101u;
+  return n + 0x30303030u + m * 0x27u;
+}
+
 // Expand one digest word into 8 lowercase-hex ASCII chars packed as two
-// big-endian message words (first char in the most significant byte).
+// big-endian message words (first char in the most significant byte).  On the
+// device the byte duplication is one v_perm_b32 per half (~9 VALU per 4 chars
+// instead of ~5 per char for the nibble-at-a-time form).
 AHV_HD void word_to_hex_words(uint32_t v, uint32_t& hi, uint32_t& lo) {
-  hi = (hex_nibble((v >> 28) & 15u) << 24) | (hex_nibble((v >> 24) & 15u) << 16) |
-       (hex_nibble((v >> 20) & 15u) << 8) | hex_nibble((v >> 16) & 15u);
-  lo = (hex_nibble((v >> 12) & 15u) << 24) | (hex_nibble((v >> 8) & 15u) << 16) |
-       (hex_nibble((v >> 4) & 15u) << 8) | hex_nibble(v & 15u);
+#if defined(__HIP_DEVICE_COMPILE__)
+  hi = hex4_spread(__builtin_amdgcn_perm(0u, v, 0x03030202u));
+  lo = hex4_spread(__builtin_amdgcn_perm(0u, v, 0x01010000u));
+#else
+  const uint32_t b3 = v >> 24, b2 = (v >> 16) & 0xffu, b1 = (v >> 8) & 0xffu, b0 = v & 0xffu;
+  hi = hex4_spread(b3 * 0x01010000u | b2 * 0x0101u);
+  lo = hex4_spread(b1 * 0x01010000u | b0 * 0x0101u);
+#endif
 }
 
 // Digest (8 words) -> 64 ASCII hex chars as 16 big-endian message words.

@@ -1,24 +1,31 @@
-// WaveWindowSink: per-lane SHA-256 of an emitted message, assembled in LDS.
+// WordWindowSink: per-lane SHA-256 of an emitted message, assembled in LDS one
+// 32-bit word at a time.
 //
-// The message is produced by an *emitter* (ahv/delta_emit.h) that knows each
-// segment's length before writing it.  Hashing runs in passes over a 4-block
-// (256-byte) window per lane:
+// The message is produced by an *emitter* (ahv/delta_emit.h) that hands over
+// big-endian chunks of 1–4 bytes and announces each segment's byte length
+// first.  Each lane keeps a funnel: the `sh/8` pending bytes of the word being
+// filled sit left-aligned in `carry`; a 4-byte chunk v always completes exactly
+// one word, `carry | v >> sh`, and leaves `v << (32 - sh)` pending (one
+// v_alignbit).  So a 4-byte chunk costs ~3 VALU + one ds_write_b32 whatever the
+// lane's byte phase — lanes whose messages are shifted by a different DID
+// length run the same instructions.
 //
-//   pass k: run the emitter; bytes whose position falls in [256k, 256k+256) are
-//           stored to LDS, whole segments outside the window are skipped by
-//           length (no per-byte work); append the SHA padding bytes that fall
-//           in the window; compress the window's complete blocks.
+// Hashing runs in passes over a window of kWinBlocks SHA blocks:
 //
-// Typical governance deltas (≈ 330 bytes → 6 blocks) take two passes.  The
-// point of the design is code shape on CDNA: there is exactly one compression
-// site in the loop (a kernel with many inlined 64-round compressions blew the
-// VGPR budget; non-inlined calls spilled around every call site), every lane
-// runs the same loop trip count (wave-uniform `__any`), and lanes whose messages
-// differ in length only mask the tail blocks.
+//   pass k: zero the window; run the emitter — words whose index falls in the
+//           window land in LDS, all others in a trash row (an unsigned min, no
+//           branch), segments wholly before or after the window are skipped by
+//           length for every lane at once (`__all`); flush the pending word
+//           with the 0x80 pad byte, write the bit length; compress the
+//           window's blocks that belong to the lane's padded message.
 //
-// LDS layout [word][lane] (word w of lane l at dword w*64 + l): a wave-wide
-// ds_write_b8 touches 64 distinct dwords on bank l mod 32 — conflict-free — and
-// block reads are conflict-free ds_read_b32.  16 KiB per wave → 10 waves/CU.
+// A ~330-byte governance delta (6 blocks) takes 2 passes with a 3-block window.
+// There is one compression site in the loop (a kernel with several inlined
+// 64-round compressions overflows the VGPR budget and the instruction cache).
+//
+// LDS layout [word][lane] (word w of lane l at dword w*64 + l, row kWinWords is
+// the trash row): every ds_write_b32 / ds_read_b32 of a wave touches 64
+// consecutive dwords — conflict-free.
 #pragma once
 
 #include "ahv/delta_emit.h"
@@ -26,33 +33,57 @@
 
 namespace ahv {
 
-// 2 blocks (8 KiB of LDS per wave) keeps LDS from capping occupancy below what
-// the VGPR budget allows (3 waves/SIMD at ≤ 168 VGPRs); each extra pass only
-// re-walks the segment lengths, its bytes outside the window are skipped whole.
-constexpr int kWinBlocks = 2;
-constexpr uint32_t kWinBytes = kWinBlocks * 64;  // 128
-constexpr int kWinWords = kWinBlocks * 16;       // 32
+#ifndef AHV_WIN_BLOCKS
+#define AHV_WIN_BLOCKS 3
+#endif
+constexpr int kWinBlocks = AHV_WIN_BLOCKS;
+constexpr int kWinWords = kWinBlocks * 16;
 constexpr int kWaveLanes = 64;
 
-static __shared__ uint32_t g_ring[kWinWords * kWaveLanes];
+static __shared__ uint32_t g_win[(kWinWords + 1) * kWaveLanes];
 
-struct WaveWindowSink {
+struct WordWindowSink {
   uint32_t lane;
-  uint32_t pos;  // position of the next emitted byte
-  uint32_t lo;   // window start of the current pass
+  int32_t rel;     // index of the word being filled, relative to the window start
+  uint32_t sh;     // 8 × bytes pending in `carry` (0, 8, 16, 24)
+  uint32_t carry;  // pending bytes, left-aligned
+  int32_t lo;      // window start (word index), wave-uniform
 
-  // Does the next `len` bytes overlap the window?  If not, skip them.
-  __device__ __forceinline__ bool want(uint32_t len) {
-    if (pos + len > lo && pos < lo + kWinBytes) return true;
-    pos += len;
-    return false;
+  __device__ __forceinline__ void store(int32_t r, uint32_t v) const {
+    const uint32_t u = static_cast<uint32_t>(r);  // negative → huge → trash row
+    const uint32_t slot = u < static_cast<uint32_t>(kWinWords) ? u : static_cast<uint32_t>(kWinWords);
+    g_win[slot * kWaveLanes + lane] = v;
   }
 
-  __device__ __forceinline__ void byte(uint8_t b) {
-    const uint32_t rel = pos - lo;
-    if (rel < kWinBytes)
-      reinterpret_cast<uint8_t*>(g_ring)[(((rel >> 2) * kWaveLanes + lane) << 2) + (3u - (rel & 3u))] = b;
-    ++pos;
+  // Segment of `len` bytes: false (and the position advanced) when it lies
+  // wholly outside the window for every lane of the wave.
+  __device__ __forceinline__ bool seg(uint32_t len) {
+    const uint32_t tot = (sh >> 3) + len;
+    const int32_t last = rel + static_cast<int32_t>((tot - 1) >> 2);  // word holding the last byte
+    if (__all(last < 0 || rel >= kWinWords)) {
+      rel += static_cast<int32_t>(tot >> 2);
+      sh = (tot & 3u) << 3;
+      carry = 0;  // its word is outside the window
+      return false;
+    }
+    return true;
+  }
+
+  __device__ __forceinline__ void put4(uint32_t v) {
+    store(rel, carry | (v >> sh));
+    carry = __builtin_amdgcn_alignbit(v, 0u, sh);
+    ++rel;
+  }
+
+  // n ∈ [0, 4] bytes (top of v, rest zero); n may differ per lane.
+  __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+    const uint32_t w = carry | (v >> sh);
+    const uint32_t tot = sh + 8u * n;
+    const bool full = tot >= 32u;
+    store(full ? rel : kWinWords, w);
+    carry = full ? __builtin_amdgcn_alignbit(v, 0u, sh) : w;
+    rel += full ? 1 : 0;
+    sh = tot & 31u;
   }
 
   __device__ __forceinline__ bool any(bool b) const { return __any(b); }
@@ -70,44 +101,42 @@ struct WaveWindowSink {
   }
 
   // As hash(), with midstate capture (MID_CAPTURE: state after block 0 → mid)
-  // or resumption (MID_RESUME: start from mid at byte 64, skipping block 0's
-  // emission and compression).  The mode may differ per lane.
+  // or resumption (MID_RESUME: start from mid at word 16, skipping block 0's
+  // emission and compression).  The mode is wave-uniform.
   template <class Emit>
   __device__ __forceinline__ void hash_mid(Emit&& emit, uint32_t out[8], Digest& mid, int mode) {
     uint32_t st[8];
     if (mode == MID_RESUME) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) st[k] = mid.v[k];
-      lo = 64;
+      lo = 16;
     } else {
       sha256_init(st);
       lo = 0;
     }
-    uint32_t total = 0;  // padded length, known after the first pass
+    int32_t total = 0;  // padded length in words, known after the first pass
     bool first = true;
     while (first || __any(lo < total)) {
-      if (first || lo < total) {
-        pos = 0;
-        emit(*this);
-        const uint32_t L = pos;
-        total = ((L + 8u) / 64u + 1u) * 64u;
-        // padding bytes [L, total) that fall in this window
-        const uint32_t a = L > lo ? L : lo;
-        const uint32_t e = total < lo + kWinBytes ? total : lo + kWinBytes;
-        const uint64_t bits = static_cast<uint64_t>(L) * 8u;
-        for (uint32_t p = a; p < e; ++p) {
-          uint8_t b = 0;
-          if (p == L) b = 0x80;
-          else if (p >= total - 8) b = static_cast<uint8_t>(bits >> (8 * (total - 1 - p)));
-          pos = p;
-          byte(b);
-        }
-        // complete blocks of this window
-        const uint32_t nb = ((e > lo ? e : lo) - lo) >> 6;
-        for (uint32_t blk = 0; blk < nb; ++blk) {
+#pragma unroll
+      for (int k = 0; k < kWinWords; ++k) g_win[k * kWaveLanes + lane] = 0u;
+      rel = -lo;
+      sh = 0;
+      carry = 0;
+      emit(*this);
+      const uint32_t L = static_cast<uint32_t>(rel + lo) * 4u + (sh >> 3);  // message bytes
+      total = static_cast<int32_t>(((L + 8u) / 64u + 1u) * 16u);
+      // pad byte, flushed with the pending word (the zeroed window supplies the rest)
+      put(0x80000000u, 1);
+      store(sh ? rel : kWinWords, carry);
+      const uint64_t bits = static_cast<uint64_t>(L) * 8u;
+      store(total - 2 - lo, static_cast<uint32_t>(bits >> 32));
+      store(total - 1 - lo, static_cast<uint32_t>(bits));
+#pragma nounroll
+      for (int blk = 0; blk < kWinBlocks; ++blk) {
+        if (lo + 16 * blk < total) {
           uint32_t w[16];
 #pragma unroll
-          for (int k = 0; k < 16; ++k) w[k] = g_ring[(blk * 16 + k) * kWaveLanes + lane];
+          for (int k = 0; k < 16; ++k) w[k] = g_win[(blk * 16 + k) * kWaveLanes + lane];
           sha256_compress(st, w);
           if (mode == MID_CAPTURE && lo == 0 && blk == 0) {
 #pragma unroll
@@ -116,20 +145,20 @@ struct WaveWindowSink {
         }
       }
       first = false;
-      lo += kWinBytes;
+      lo += kWinWords;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) out[k] = st[k];
   }
 
-  // Merkle digest scratch: slot j (< 8) lives in window words 8j..8j+7.
+  // Merkle digest scratch: slot j (< kWinWords / 8) lives in window words 8j..8j+7.
   __device__ __forceinline__ void stash(int j, const uint32_t d[8]) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) g_ring[(8 * j + k) * kWaveLanes + lane] = d[k];
+    for (int k = 0; k < 8; ++k) g_win[(8 * j + k) * kWaveLanes + lane] = d[k];
   }
   __device__ __forceinline__ void load(int j, uint32_t d[8]) const {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = g_ring[(8 * j + k) * kWaveLanes + lane];
+    for (int k = 0; k < 8; ++k) d[k] = g_win[(8 * j + k) * kWaveLanes + lane];
   }
   // Merkle interior node: two data blocks (hex of l, hex of r) share one loop
   // body; the third is the constant padding block of a 128-byte message, whose
