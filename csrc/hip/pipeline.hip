@@ -1,7 +1,7 @@
 // Batched governance pipeline kernel (gfx950) and its host twin.
 //
 // Geometry: one wave (64 lanes) per workgroup, one session per lane, a
-// kWinBlocks-block LDS message window per wave (ahv/wave_sink.h: 12.5 KiB for 3
+// 3-block LDS message window per wave (ahv/wave_sink.h: 12.5 KiB for 3
 // blocks → 12 waves per CU, 3 per SIMD).  The SHA rounds are pure VALU
 // (v_alignbit / v_bitop3 / v_add3); a wave alone issues a VALU op every 4
 // cycles against the SIMD's 2, so ≥2 waves per SIMD keep the issue slots busy
@@ -25,17 +25,18 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// (64 threads, ≥MinWaves waves per SIMD).  The LDS window already caps residency
-// at 16 / kWinBlocks·… waves per SIMD (4 for 2 blocks, 3 for 3), so MinWaves
-// matches it: the VGPR budget is 128 or 168 registers, without spills.
-// Both are instantiated; AHV_PIPE_WAVES=3|4 overrides the choice for A/B runs.
-template <int MinWaves>
+// (64 threads, ≥MinWaves waves per SIMD).  The LDS window caps residency (8.4 KiB
+// for 2 blocks → 4 waves per SIMD; 12.5 KiB for 3 blocks → 3), so MinWaves
+// matches it: the VGPR budget is 128 or 168 registers.  Both shapes are
+// instantiated; AHV_PIPE_WIN=2|3 selects one for A/B runs.
+template <int MinWaves, int WinBlocks>
 __global__ __launch_bounds__(kWaveLanes, MinWaves) void governance_pipeline_kernel(PipelineArgs a) {
   const uint32_t lane = threadIdx.x;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
   PipeCounters c{};
   if (i < a.n) {
-    WordWindowSink sink;
+    WordWindowSink<WinBlocks> sink;
+    sink.g_win = win_lds<WinBlocks>();
     sink.lane = lane;
     c = pipeline_session(a, i, sink);
   }
@@ -71,11 +72,10 @@ __global__ __launch_bounds__(kWaveLanes, MinWaves) void governance_pipeline_kern
   }
 }
 
-static int pipeline_waves() {
+static int pipeline_window() {
   static const int w = [] {
-    const char* e = std::getenv("AHV_PIPE_WAVES");
-    if (e && (std::atoi(e) == 3 || std::atoi(e) == 4)) return std::atoi(e);
-    return kWinBlocks <= 2 ? 4 : 3;
+    const char* e = std::getenv("AHV_PIPE_WIN");
+    return e && std::atoi(e) == 2 ? 2 : 3;
   }();
   return w;
 }
@@ -84,8 +84,8 @@ void launch_pipeline(const PipelineArgs& a, hipStream_t stream) {
   if (a.n <= 0) return;
   const int64_t blocks = (a.n + kWaveLanes - 1) / kWaveLanes;
   const dim3 grid(static_cast<uint32_t>(blocks)), block(kWaveLanes);
-  if (pipeline_waves() == 4) hipLaunchKernelGGL(governance_pipeline_kernel<4>, grid, block, 0, stream, a);
-  else hipLaunchKernelGGL(governance_pipeline_kernel<3>, grid, block, 0, stream, a);
+  if (pipeline_window() == 2) hipLaunchKernelGGL((governance_pipeline_kernel<4, 2>), grid, block, 0, stream, a);
+  else hipLaunchKernelGGL((governance_pipeline_kernel<3, 3>), grid, block, 0, stream, a);
   check_hip(hipGetLastError(), "governance_pipeline_kernel launch");
 }
 

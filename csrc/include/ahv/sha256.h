@@ -128,7 +128,9 @@ AHV_HD uint32_t hex_nibble(uint32_t n) { return n + (n < 10u ? 0x30u : 0x57u); }
 AHV_HD uint32_t hex4_spread(uint32_t x) {
   const uint32_t n = ((x >> 4) & 0x0F000F00u) | (x & 0x000F000Fu);
   const uint32_t m = ((n + 0x06060606u) >> 4) & 0x01010101u;
-  return n + 0x30303030u + m * 0x27u;
+  // m·0x27 as shift-adds (full-rate v_lshl_add_u32, not a quarter-rate v_mul_lo_u32)
+  const uint32_t m3 = (m << 1) + m, m7 = (m << 2) + m3;
+  return n + 0x30303030u + (m << 5) + m7;
 }
 
 // Expand one digest word into 8 lowercase-hex ASCII chars packed as two

@@ -4,10 +4,11 @@
 // The message is produced by an *emitter* (ahv/delta_emit.h) that hands over
 // big-endian chunks of 1–4 bytes and announces each segment's byte length
 // first.  Each lane keeps a funnel: the `sh/8` pending bytes of the word being
-// filled sit left-aligned in `carry`; a 4-byte chunk v always completes exactly
-// one word, `carry | v >> sh`, and leaves `v << (32 - sh)` pending (one
-// v_alignbit).  So a 4-byte chunk costs ~3 VALU + one ds_write_b32 whatever the
-// lane's byte phase — lanes whose messages are shifted by a different DID
+// filled sit right-aligned in `prev` (the tail of the previous chunk); a 4-byte
+// chunk v always completes exactly one word, ({prev, v} >> sh)[31:0] — a single
+// v_alignbit — and leaves its own tail pending (`prev = v`).  So a 4-byte chunk
+// costs ~3 VALU (funnel, trash clamp, address step) + one ds_write_b32 whatever
+// the lane's byte phase — lanes whose messages are shifted by a different DID
 // length run the same instructions.
 //
 // Hashing runs in passes over a window of kWinBlocks SHA blocks:
@@ -33,26 +34,41 @@
 
 namespace ahv {
 
-#ifndef AHV_WIN_BLOCKS
-#define AHV_WIN_BLOCKS 3
-#endif
-constexpr int kWinBlocks = AHV_WIN_BLOCKS;
-constexpr int kWinWords = kWinBlocks * 16;
 constexpr int kWaveLanes = 64;
 
-static __shared__ uint32_t g_win[(kWinWords + 1) * kWaveLanes];
+// The window of one wave: (W·16 + 1) rows of 64 lanes (one LDS array per
+// window size; a kernel instantiates exactly one).
+template <int WinBlocks>
+__device__ __forceinline__ uint32_t* win_lds() {
+  __shared__ uint32_t buf[(WinBlocks * 16 + 1) * kWaveLanes];
+  return buf;
+}
 
+template <int WinBlocks>
 struct WordWindowSink {
+  static constexpr int kWinBlocks = WinBlocks;
+  static constexpr int kWinWords = WinBlocks * 16;
+  uint32_t* g_win;  // win_lds<WinBlocks>()
   uint32_t lane;
   int32_t rel;     // index of the word being filled, relative to the window start
-  uint32_t sh;     // 8 × bytes pending in `carry` (0, 8, 16, 24)
-  uint32_t carry;  // pending bytes, left-aligned
+  uint32_t addr;   // its LDS byte offset, (rel·64 + lane)·4 mod 2^32 (negative rel wraps high)
+  uint32_t trash;  // (kWinWords·64 + lane)·4, this lane's trash-row offset
+  uint32_t sh;     // 8 × bytes pending (0, 8, 16, 24)
+  uint32_t prev;   // the pending bytes, RIGHT-aligned (the tail of the last chunk)
   int32_t lo;      // window start (word index), wave-uniform
 
+  // Word at LDS byte offset `a` (already relative to the window); anything
+  // outside [0, kWinWords) rows — including wrapped negatives — hits the trash row.
+  __device__ __forceinline__ void store_at(uint32_t a, uint32_t v) const {
+    const uint32_t c = a < trash ? a : trash;
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(g_win) + c) = v;
+  }
   __device__ __forceinline__ void store(int32_t r, uint32_t v) const {
-    const uint32_t u = static_cast<uint32_t>(r);  // negative → huge → trash row
-    const uint32_t slot = u < static_cast<uint32_t>(kWinWords) ? u : static_cast<uint32_t>(kWinWords);
-    g_win[slot * kWaveLanes + lane] = v;
+    store_at((static_cast<uint32_t>(r) * kWaveLanes + lane) * 4u, v);
+  }
+  __device__ __forceinline__ void seek(int32_t r) {
+    rel = r;
+    addr = (static_cast<uint32_t>(r) * kWaveLanes + lane) * 4u;
   }
 
   // Segment of `len` bytes: false (and the position advanced) when it lies
@@ -61,28 +77,32 @@ struct WordWindowSink {
     const uint32_t tot = (sh >> 3) + len;
     const int32_t last = rel + static_cast<int32_t>((tot - 1) >> 2);  // word holding the last byte
     if (__all(last < 0 || rel >= kWinWords)) {
-      rel += static_cast<int32_t>(tot >> 2);
-      sh = (tot & 3u) << 3;
-      carry = 0;  // its word is outside the window
+      seek(rel + static_cast<int32_t>(tot >> 2));
+      sh = (tot & 3u) << 3;  // `prev` is stale, but its word lies outside the window
       return false;
     }
     return true;
   }
 
+  // Funnel: the completed word is the pending sh/8 bytes followed by the head of
+  // v, i.e. ({prev, v} >> sh)[31:0] — one v_alignbit; the new pending bytes are
+  // the tail of v, so `prev = v`.
   __device__ __forceinline__ void put4(uint32_t v) {
-    store(rel, carry | (v >> sh));
-    carry = __builtin_amdgcn_alignbit(v, 0u, sh);
+    store_at(addr, __builtin_amdgcn_alignbit(prev, v, sh));
+    prev = v;
     ++rel;
+    addr += kWaveLanes * 4u;
   }
 
-  // n ∈ [0, 4] bytes (top of v, rest zero); n may differ per lane.
+  // n ∈ [0, 4] bytes at the top of v (the low bytes of v are ignored); n may
+  // differ per lane.  The pending tail becomes ({prev, v} >> (32 − 8n))[31:0].
   __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
-    const uint32_t w = carry | (v >> sh);
     const uint32_t tot = sh + 8u * n;
     const bool full = tot >= 32u;
-    store(full ? rel : kWinWords, w);
-    carry = full ? __builtin_amdgcn_alignbit(v, 0u, sh) : w;
+    store_at(full ? addr : trash, __builtin_amdgcn_alignbit(prev, v, sh));
+    prev = n ? __builtin_amdgcn_alignbit(prev, v, 32u - 8u * n) : prev;
     rel += full ? 1 : 0;
+    addr += full ? kWaveLanes * 4u : 0u;
     sh = tot & 31u;
   }
 
@@ -119,15 +139,17 @@ struct WordWindowSink {
     while (first || __any(lo < total)) {
 #pragma unroll
       for (int k = 0; k < kWinWords; ++k) g_win[k * kWaveLanes + lane] = 0u;
-      rel = -lo;
+      trash = (static_cast<uint32_t>(kWinWords) * kWaveLanes + lane) * 4u;
+      seek(-lo);
       sh = 0;
-      carry = 0;
+      prev = 0;
       emit(*this);
       const uint32_t L = static_cast<uint32_t>(rel + lo) * 4u + (sh >> 3);  // message bytes
       total = static_cast<int32_t>(((L + 8u) / 64u + 1u) * 16u);
-      // pad byte, flushed with the pending word (the zeroed window supplies the rest)
+      // pad byte, then the pending word flushed left-aligned (the zeroed window
+      // supplies the zero bytes up to the length words)
       put(0x80000000u, 1);
-      store(sh ? rel : kWinWords, carry);
+      store_at(sh ? addr : trash, __builtin_amdgcn_alignbit(prev, 0u, sh));
       const uint64_t bits = static_cast<uint64_t>(L) * 8u;
       store(total - 2 - lo, static_cast<uint32_t>(bits >> 32));
       store(total - 1 - lo, static_cast<uint32_t>(bits));
