@@ -9,6 +9,7 @@
 #include "ahv/kernels.h"
 #include "ahv/launch.h"
 #include "ahv/sha256.h"
+#include "ahv/wave_sink.h"
 
 namespace ahv {
 
@@ -75,86 +76,58 @@ void hash_many_host(const HashManyArgs& a) { for (int64_t i = 0; i < a.n; ++i) h
 
 // ------------------------------------------------------------------ K08
 // The message is virtual: prefix bytes, then the parent field text, then the
-// suffix bytes — assembled word by word without materialising it.
+// suffix bytes.  One lane per chain (serial along the chain); the device
+// assembles each message a 32-bit word at a time in the wave's LDS window
+// (ahv/wave_sink.h) — aligned word loads of the arena funnel-shifted to the
+// span offset, SWAR hex for the parent — the host twin streams the same bytes.
 
 namespace {
-struct ChainMsg {
-  const uint8_t* pre;
-  int64_t lp;
-  const uint32_t* parent;  // null → JSON null
-  const uint8_t* suf;
-  int64_t ls;
-  AHV_HD int64_t mid_len() const { return parent ? 66 : 4; }
-  AHV_HD int64_t len() const { return lp + mid_len() + ls; }
-  AHV_HD uint32_t mid_byte(int64_t j) const {
-    if (!parent) return static_cast<uint32_t>("null"[j]);
-    if (j == 0 || j == 65) return '"';
-    const int64_t n = j - 1;  // nibble index, big-endian within each word
-    const uint32_t w = parent[n >> 3];
-    const uint32_t nib = (w >> (28 - 4 * (n & 7))) & 0xfu;
-    return nib < 10 ? '0' + nib : 'a' + nib - 10;
-  }
-  AHV_HD uint32_t byte(int64_t i) const {
-    if (i < lp) return pre[i];
-    i -= lp;
-    if (i < mid_len()) return mid_byte(i);
-    return suf[i - mid_len()];
-  }
-};
-
-AHV_HD void sha256_chain_msg(const ChainMsg& m, uint32_t out[8]) {
-  sha256_init(out);
-  const int64_t len = m.len();
-  const int64_t total = ((len + 8) / 64 + 1) * 64;
-  const uint64_t bits = static_cast<uint64_t>(len) * 8u;
-  for (int64_t b = 0; b < total; b += 64) {
-    uint32_t w[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      uint32_t v = 0;
-      for (int j = 0; j < 4; ++j) {
-        const int64_t x = b + 4 * k + j;
-        uint32_t byte;
-        if (x < len) byte = m.byte(x);
-        else if (x == len) byte = 0x80;
-        else if (x >= total - 8) byte = static_cast<uint32_t>((bits >> (8 * (total - 1 - x))) & 0xff);
-        else byte = 0;
-        v = (v << 8) | byte;
-      }
-      w[k] = v;
-    }
-    sha256_compress(out, w);
-  }
+template <class Sink>
+AHV_HD void chain_emit(Sink& s, const ChainHashArgs& a, int32_t i, bool have, const Digest& prev) {
+  emit_span(s, a.bytes + a.pre_off[i], static_cast<uint32_t>(a.pre_len[i]));
+  if (have) emit_hex_digest_quoted(s, prev.v);
+  else emit_lit(s, canon::K_NULL);
+  emit_span(s, a.bytes + a.suf_off[i], static_cast<uint32_t>(a.suf_len[i]));
 }
-}  // namespace
 
-AHV_HD void chain_hash_elem(const ChainHashArgs& a, int64_t c) {
-  uint32_t prev[8];
+template <class Sink>
+AHV_HD void chain_hash_elem(const ChainHashArgs& a, int64_t c, Sink& sink) {
+  Digest prev;
   bool have = a.has_seed && a.seed_parent && a.has_seed[c];
   if (have)
-    for (int k = 0; k < 8; ++k) prev[k] = a.seed_parent[c * 8 + k];
+    for (int k = 0; k < 8; ++k) prev.v[k] = a.seed_parent[c * 8 + k];
   for (int32_t i = a.chain_offsets[c]; i < a.chain_offsets[c + 1]; ++i) {
-    ChainMsg m{a.bytes + a.pre_off[i], a.pre_len[i], have ? prev : nullptr, a.bytes + a.suf_off[i], a.suf_len[i]};
     uint32_t h[8];
-    sha256_chain_msg(m, h);
+    const bool hv = have;
+    const Digest pv = prev;
+    sink.hash([&](Sink& k) { chain_emit(k, a, i, hv, pv); }, h);
     for (int k = 0; k < 8; ++k) {
       a.digest[static_cast<int64_t>(i) * 8 + k] = h[k];
-      prev[k] = h[k];
+      prev.v[k] = h[k];
     }
     have = true;
   }
 }
-__global__ void chain_hash_kernel(ChainHashArgs a) {
-  for (int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; c < a.chains;
-       c += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    chain_hash_elem(a, c);
+}  // namespace
+
+// One wave per 64 chains; lanes whose chains are shorter idle (masked) while
+// the wave finishes its longest chain.
+__global__ __launch_bounds__(kWaveLanes, 3) void chain_hash_kernel(ChainHashArgs a) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * kWaveLanes + threadIdx.x;
+  WordWindowSink<3> sink;
+  sink.g_win = win_lds<3>();
+  sink.lane = threadIdx.x;
+  if (c < a.chains) chain_hash_elem(a, c, sink);
 }
 void launch_chain_hash(const ChainHashArgs& a, hipStream_t st) {
   if (a.chains <= 0) return;
-  hipLaunchKernelGGL(chain_hash_kernel, grid1(a.chains, 64), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(chain_hash_kernel, grid1(a.chains, kWaveLanes), dim3(kWaveLanes), 0, st, a);
   check_hip(hipGetLastError(), "chain_hash_kernel");
 }
-void chain_hash_host(const ChainHashArgs& a) { for (int64_t c = 0; c < a.chains; ++c) chain_hash_elem(a, c); }
+void chain_hash_host(const ChainHashArgs& a) {
+  HostSink sink;
+  for (int64_t c = 0; c < a.chains; ++c) chain_hash_elem(a, c, sink);
+}
 
 // ------------------------------------------------------------------ K09
 // One lane per chain: binary-counter Merkle (delta_emit.h merkle_root_counter)

@@ -285,6 +285,30 @@ AHV_HD void emit_str_ref(Sink& s, StrRef r) {
   s.put(0x22u << 24, 1);
 }
 
+// Raw bytes [p, p+n) (already JSON text) as one segment, read as aligned 32-bit
+// words and funnel-shifted to the span's byte offset.  Never reads past the word
+// holding the span's last byte.
+template <class Sink>
+AHV_HD void emit_span(Sink& s, const uint8_t* p, uint32_t n) {
+  if (!s.seg(n) || n == 0) return;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
+  const uint32_t sh = static_cast<uint32_t>(a & 3u) * 8u;
+  const uint32_t words = (n + (sh >> 3) + 3u) >> 2;  // aligned words touched
+  uint32_t cur = w[0];
+  for (uint32_t k = 0; 4u * k < n; ++k) {
+    const uint32_t nxt = k + 1 < words ? w[k + 1] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t le = __builtin_amdgcn_alignbit(nxt, cur, sh);
+#else
+    const uint32_t le = sh ? (cur >> sh) | (nxt << (32u - sh)) : cur;
+#endif
+    const uint32_t left = n - 4u * k;
+    s.put(bswap_word(le), left < 4u ? left : 4u);
+    cur = nxt;
+  }
+}
+
 // Pool string id as a JSON value: "…" or null.
 template <class Sink>
 AHV_HD void emit_pool_str(Sink& s, const StrPool& pool, int32_t id) {

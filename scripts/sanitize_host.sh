@@ -21,6 +21,6 @@ for s in "${SRCS[@]}"; do
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -fsanitize=address,undefined "${OBJS[@]}" -o "$OUT/host_selftest" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -fsanitize=address,undefined -fno-gpu-sanitize "${OBJS[@]}" -o "$OUT/host_selftest" \
   -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 "$OUT/host_selftest"
