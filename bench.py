@@ -111,7 +111,7 @@ def main() -> None:
             torch.cuda.synchronize(dev)
 
     from agent_hypervisor_amd.models.engine import GovernanceEngine
-    from agent_hypervisor_amd.parallel.collectives import allreduce_stats
+    from agent_hypervisor_amd.parallel.collectives import allreduce_stats  # noqa: F401 (graph mode)
 
     S = args.sessions
     eng = GovernanceEngine(
@@ -121,11 +121,30 @@ def main() -> None:
     g = torch.Generator(device=dev).manual_seed(77 + rank)
     stats = torch.zeros(6, dtype=torch.int64, device=dev)
 
+    # X04 counters: double-buffered so step i's all-reduce (RCCL, on its own
+    # stream) overlaps step i+1's pipeline kernel; a buffer is reused only after
+    # its collective from two steps back has completed (a stream wait, no host sync).
+    bufs = [torch.zeros(6, dtype=torch.int64, device=dev) for _ in range(2)]
+    works: list = [None, None]
+    it = [0]
+
     def step():
-        stats.zero_()
+        b = it[0] & 1
+        it[0] += 1
+        if works[b] is not None:
+            works[b].wait()
+        st = bufs[b]
+        st.zero_()
         agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
-        eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=stats)
-        return allreduce_stats(stats)
+        eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
+        works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if world > 1 else None
+        return st
+
+    def drain():
+        for k in range(2):
+            if works[k] is not None:
+                works[k].wait()
+                works[k] = None
 
     if args.graph:
         from agent_hypervisor_amd.runtime.graphs import PipelineGraph
@@ -146,8 +165,12 @@ def main() -> None:
             pg.step()
             return stats
 
+        def drain():  # noqa: F811 - the graph's collective is in-stream
+            pass
+
     for _ in range(args.warmup):
         step()
+    drain()
     sync()
 
     # per-step latency distribution (synchronised steps, untimed for throughput)
@@ -155,6 +178,7 @@ def main() -> None:
     for _ in range(max(3, min(10, args.steps))):
         t0 = time.perf_counter()
         step()
+        drain()
         sync()
         lat.append(time.perf_counter() - t0)
 
@@ -164,6 +188,7 @@ def main() -> None:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
+    drain()
     sync()
     if world > 1:
         dist.barrier()

@@ -123,47 +123,50 @@ AHV_HD void sigma_eff_csr_elem(const VouchCsrArgs& a, int64_t i) {
     if (a.vouchee[k] == e && live_edge(a.active, a.expiry_us, k, a.now_us)) contrib += a.bonded[k];
   a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[s], contrib);
 }
-// Device: one lane per session walks its edges once in creation order and adds
-// each live bond into an LDS accumulator row of its vouchee (per-vouchee sums in
-// creation order — the same additions, in the same order, as the element form
-// above), then the block writes σ_eff for its 64×16 (session, vouchee) pairs
-// coalesced.  Edge fields are staged through LDS with coalesced loads.
-constexpr int kSigmaLdsEdges = 1024;
+// Device: a 256-thread block owns 16 sessions; thread (session, vouchee) walks
+// its session's edges in creation order and adds the live bonds of its vouchee —
+// the element form above, the same additions in the same order.  The block's
+// edge range is staged in LDS with coalesced loads (liveness precomputed); the
+// 16 threads of a session read the same edge (a broadcast), and one pad slot
+// per 16 edges puts the 4 sessions of a wave on different banks.  σ and σ_eff
+// rows are read/written coalesced, one (session, vouchee) per thread.
+constexpr int kSigmaSessions = 16;  // sessions per block (× kTile threads)
+constexpr int kSigmaLdsEdges = 2048;
 
-__global__ __launch_bounds__(64) void sigma_eff_csr_kernel(VouchCsrArgs a) {
-  __shared__ uint8_t s_ve[kSigmaLdsEdges], s_lv[kSigmaLdsEdges];
-  __shared__ double s_bd[kSigmaLdsEdges];
-  __shared__ double s_acc[64 * (kTile + 1)];
-  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * 64;
-  const int64_t s1 = s0 + 64 < a.sessions ? s0 + 64 : a.sessions;
-  const int64_t s = s0 + threadIdx.x;
+__device__ __forceinline__ int32_t pad_edge(int32_t i) { return i + (i >> 4); }
+
+__global__ __launch_bounds__(kSigmaSessions * kTile) void sigma_eff_csr_kernel(VouchCsrArgs a) {
+  __shared__ uint8_t s_ve[kSigmaLdsEdges + kSigmaLdsEdges / 16];
+  __shared__ double s_bd[kSigmaLdsEdges + kSigmaLdsEdges / 16];  // 0.0 for a dead edge
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * kSigmaSessions;
+  const int64_t s1 = s0 + kSigmaSessions < a.sessions ? s0 + kSigmaSessions : a.sessions;
+  const int64_t i = s0 * kTile + threadIdx.x;  // (session, vouchee) element
   const int32_t e0 = a.offsets[s0], e1 = a.offsets[s1];
-  if (e1 - e0 > kSigmaLdsEdges) {  // uniform per block: element form
-    for (int64_t i = s0 * kTile + threadIdx.x; i < s1 * kTile; i += 64) sigma_eff_csr_elem(a, i);
+  if (e1 - e0 > kSigmaLdsEdges) {  // uniform per block: element form from global memory
+    if (i < s1 * kTile) sigma_eff_csr_elem(a, i);
     return;
   }
-  for (int32_t k = e0 + threadIdx.x; k < e1; k += 64) {
-    s_ve[k - e0] = a.vouchee[k];
-    s_lv[k - e0] = live_edge(a.active, a.expiry_us, k, a.now_us) ? 1 : 0;
-    s_bd[k - e0] = a.bonded[k];
-  }
-  double* acc = s_acc + threadIdx.x * (kTile + 1);
-#pragma unroll
-  for (int j = 0; j < kTile; ++j) acc[j] = 0.0;
-  __syncthreads();
-  if (s < a.sessions) {
-    for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
-      if (s_lv[k - e0]) acc[s_ve[k - e0]] += s_bd[k - e0];
+  for (int32_t k = e0 + threadIdx.x; k < e1; k += kSigmaSessions * kTile) {
+    const int32_t j = pad_edge(k - e0);
+    const bool live = live_edge(a.active, a.expiry_us, k, a.now_us);
+    s_ve[j] = live ? a.vouchee[k] : 0xff;  // a dead edge matches no vouchee
+    s_bd[j] = a.bonded[k];
   }
   __syncthreads();
-  for (int64_t i = s0 * kTile + threadIdx.x; i < s1 * kTile; i += 64) {
-    const int64_t row = i / kTile - s0;
-    a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[i / kTile], s_acc[row * (kTile + 1) + i % kTile]);
+  if (i < s1 * kTile) {
+    const int64_t s = i / kTile;
+    const uint32_t e = static_cast<uint32_t>(i % kTile);
+    double contrib = 0.0;
+    for (int32_t k = a.offsets[s] - e0; k < a.offsets[s + 1] - e0; ++k) {
+      const int32_t j = pad_edge(k);
+      if (s_ve[j] == e) contrib += s_bd[j];
+    }
+    a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[s], contrib);
   }
 }
 void launch_sigma_eff_csr(const VouchCsrArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
-  hipLaunchKernelGGL(sigma_eff_csr_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(sigma_eff_csr_kernel, grid1(a.sessions, kSigmaSessions), dim3(kSigmaSessions * kTile), 0, st, a);
   check_hip(hipGetLastError(), "sigma_eff_csr_kernel");
 }
 void sigma_eff_csr_host(const VouchCsrArgs& a) {
@@ -361,24 +364,29 @@ AHV_HD void slash_session(const SlashArgs& a, int64_t s) {
 constexpr int kSlashLdsEdges = 2048;
 constexpr int kScorePad = kTile + 1;  // 17 doubles per row: spreads a column over banks
 
+// (A 4-byte pad per 16 staged edges removes the 21 % LDS conflict cycles but
+// costs a workgroup per CU of occupancy: measured 454 → 515 µs, so not used.)
+__device__ __forceinline__ int32_t pad16(int32_t i) { return i; }
+constexpr int kSlashLdsBytes = kSlashLdsEdges;
+
 struct LdsEdges {
   const SlashArgs* a;
   int32_t e0;
   const uint8_t* vr;
   const uint8_t* ve;
   uint8_t* lv;
-  __device__ int voucher(int32_t k) const { return vr[k - e0]; }
-  __device__ int vouchee(int32_t k) const { return ve[k - e0]; }
-  __device__ bool live(int32_t k) const { return lv[k - e0] != 0; }
+  __device__ int voucher(int32_t k) const { return vr[pad16(k - e0)]; }
+  __device__ int vouchee(int32_t k) const { return ve[pad16(k - e0)]; }
+  __device__ bool live(int32_t k) const { return lv[pad16(k - e0)] != 0; }
   __device__ void release(int32_t k) const {
-    lv[k - e0] = 0;
+    lv[pad16(k - e0)] = 0;
     a->active[k] = 0;
     a->released_us[k] = a->now_us;
   }
 };
 
 __global__ __launch_bounds__(64) void slash_kernel(SlashArgs a) {
-  __shared__ uint8_t s_vr[kSlashLdsEdges], s_ve[kSlashLdsEdges], s_lv[kSlashLdsEdges];
+  __shared__ uint8_t s_vr[kSlashLdsBytes], s_ve[kSlashLdsBytes], s_lv[kSlashLdsBytes];
   __shared__ double s_sc[64 * kScorePad];
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * 64;
   const int64_t s1 = s0 + 64 < a.sessions ? s0 + 64 : a.sessions;
@@ -389,9 +397,10 @@ __global__ __launch_bounds__(64) void slash_kernel(SlashArgs a) {
     return;
   }
   for (int32_t k = e0 + threadIdx.x; k < e1; k += 64) {
-    s_vr[k - e0] = a.voucher[k];
-    s_ve[k - e0] = a.vouchee[k];
-    s_lv[k - e0] = live_edge(a.active, a.expiry_us, k, a.now_us) ? 1 : 0;
+    const int32_t j = pad16(k - e0);
+    s_vr[j] = a.voucher[k];
+    s_ve[j] = a.vouchee[k];
+    s_lv[j] = live_edge(a.active, a.expiry_us, k, a.now_us) ? 1 : 0;
   }
   const int64_t nsc = (s1 - s0) * kTile;
   for (int64_t j = threadIdx.x; j < nsc; j += 64) s_sc[(j / kTile) * kScorePad + j % kTile] = a.scores[s0 * kTile + j];
