@@ -287,6 +287,10 @@ struct GlobalEdges {
     a->active[k] = 0;
     a->released_us[k] = a->now_us;
   }
+  // the cascade walk re-reads the session's own clip records
+  AHV_HD void note_clip(int32_t, int, bool) const {}
+  AHV_HD int clip_voucher(int32_t base, int32_t ci) const { return a->clip_voucher[base + ci]; }
+  AHV_HD bool clip_cascades(int32_t base, int32_t ci) const { return a->clip_after[base + ci] < kCascadeBelow; }
 };
 
 template <class Edges>
@@ -297,6 +301,11 @@ AHV_HD bool has_live_voucher(const Edges& ed, int32_t b, int32_t e, int who) {
 }
 
 // `sc` is the session's 16 scores (global row or LDS row, stride `ss`).
+// The recursion is one loop over scalar state: a pending slash (who, depth) is
+// run, which pushes its frame (its clip range); the walk then takes the next
+// clip of the top frame and, if that voucher cascades, makes it the pending
+// slash.  (A lambda called from two sites made the compiler address the frame
+// slots through a pointer — scratch memory on the device, ~2 µs per step.)
 template <class Edges>
 AHV_HD void slash_session_t(const SlashArgs& a, int64_t s, const Edges& ed, double* sc, int ss) {
   const int32_t b = a.offsets[s], e = a.offsets[s + 1];
@@ -304,50 +313,60 @@ AHV_HD void slash_session_t(const SlashArgs& a, int64_t s, const Edges& ed, doub
   const int32_t base = a.clip_offsets[s];
   int32_t nclip = 0;
   // explicit DFS stack, depth ≤ kMaxCascadeDepth (= 2): scalar slots, no arrays
+  static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
   int32_t next0 = 0, end0 = 0, next1 = 0, end1 = 0;
   int sp = 0;
-  auto do_slash = [&](int who, int depth) {
-    sc[who * ss] = 0.0;
-    const int32_t first = nclip;
-    for (int32_t k = b; k < e; ++k) {
-      if (ed.vouchee(k) != who || !ed.live(k)) continue;
-      const int v = ed.voucher(k);
-      const double x = sc[v * ss];
-      const double before = x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
-      const double after = clip_sigma(before, omega);
-      sc[v * ss] = after;
-      if (nclip < a.clip_cap) {
-        a.clip_voucher[base + nclip] = static_cast<uint8_t>(v);
-        a.clip_depth[base + nclip] = static_cast<uint8_t>(depth);
-        a.clip_before[base + nclip] = before;
-        a.clip_after[base + nclip] = after;
+  int who = a.target[s], who_depth = 0;
+  bool pending = true;
+  for (;;) {
+    if (pending) {
+      pending = false;
+      sc[who * ss] = 0.0;
+      const int32_t first = nclip;
+      for (int32_t k = b; k < e; ++k) {
+        if (ed.vouchee(k) != who || !ed.live(k)) continue;
+        const int v = ed.voucher(k);
+        const double x = sc[v * ss];
+        const double before = x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
+        const double after = clip_sigma(before, omega);
+        sc[v * ss] = after;
+        ed.note_clip(nclip, v, after < kCascadeBelow);
+        if (nclip < a.clip_cap) {
+          a.clip_voucher[base + nclip] = static_cast<uint8_t>(v);
+          a.clip_depth[base + nclip] = static_cast<uint8_t>(who_depth);
+          a.clip_before[base + nclip] = before;
+          a.clip_after[base + nclip] = after;
+        }
+        ++nclip;
+        ed.release(k);
       }
-      ++nclip;
-      ed.release(k);
+      // push the frame (a depth-2 frame never expands, so it needs no cursor)
+      if (who_depth == 0) {
+        next0 = first;
+        end0 = nclip;
+      } else if (who_depth == 1) {
+        next1 = first;
+        end1 = nclip;
+      }
+      sp = who_depth + 1;
     }
-    if (sp == 0) {
-      next0 = first;
-      end0 = nclip;
-    } else if (sp == 1) {
-      next1 = first;
-      end1 = nclip;
-    }  // a depth-2 frame never expands, so it needs no cursor
-    static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
-    ++sp;
-  };
-  do_slash(a.target[s], 0);
-  while (sp > 0) {
+    if (sp == 0) break;
     const int depth = sp - 1;
-    int32_t& nx = depth == 0 ? next0 : next1;
+    const int32_t nx = depth == 0 ? next0 : next1;
     const int32_t en = depth == 0 ? end0 : end1;
     if (depth >= kMaxCascadeDepth || nx >= en) {
       --sp;
       continue;
     }
-    const int32_t ci = nx++;
-    if (ci >= a.clip_cap) continue;
-    const int v = a.clip_voucher[base + ci];
-    if (a.clip_after[base + ci] < kCascadeBelow && has_live_voucher(ed, b, e, v)) do_slash(v, depth + 1);
+    if (depth == 0) next0 = nx + 1;
+    else next1 = nx + 1;
+    if (nx >= a.clip_cap) continue;
+    const int v = ed.clip_voucher(base, nx);
+    if (ed.clip_cascades(base, nx) && has_live_voucher(ed, b, e, v)) {
+      who = v;
+      who_depth = depth + 1;
+      pending = true;
+    }
   }
   a.clip_count[s] = nclip;
 }
@@ -363,6 +382,8 @@ AHV_HD void slash_session(const SlashArgs& a, int64_t s) {
 // range exceeds the staging buffer falls back to the global-memory path.
 constexpr int kSlashLdsEdges = 2048;
 constexpr int kScorePad = kTile + 1;  // 17 doubles per row: spreads a column over banks
+constexpr int kSlashClipLds = 16;    // clip records per lane cached in LDS
+constexpr int kClipPad = kSlashClipLds + 4;
 
 // (A 4-byte pad per 16 staged edges removes the 21 % LDS conflict cycles but
 // costs a workgroup per CU of occupancy: measured 454 → 515 µs, so not used.)
@@ -383,11 +404,25 @@ struct LdsEdges {
     a->active[k] = 0;
     a->released_us[k] = a->now_us;
   }
+  // This lane's first kSlashClipLds clip records as (voucher | cascade<<7) bytes
+  // in LDS: the cascade walk reads them back instead of waiting on a global
+  // read-after-write of its own records (~2 µs per step of the walk).
+  uint8_t* cl;
+  __device__ void note_clip(int32_t i, int v, bool cascade) const {
+    if (i < kSlashClipLds) cl[i] = static_cast<uint8_t>(v | (cascade ? 0x80 : 0));
+  }
+  __device__ int clip_voucher(int32_t base, int32_t ci) const {
+    return ci < kSlashClipLds ? (cl[ci] & 0x7f) : a->clip_voucher[base + ci];
+  }
+  __device__ bool clip_cascades(int32_t base, int32_t ci) const {
+    return ci < kSlashClipLds ? (cl[ci] & 0x80) != 0 : a->clip_after[base + ci] < kCascadeBelow;
+  }
 };
 
 __global__ __launch_bounds__(64) void slash_kernel(SlashArgs a) {
   __shared__ uint8_t s_vr[kSlashLdsBytes], s_ve[kSlashLdsBytes], s_lv[kSlashLdsBytes];
   __shared__ double s_sc[64 * kScorePad];
+  __shared__ uint8_t s_cl[64 * kClipPad];
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * 64;
   const int64_t s1 = s0 + 64 < a.sessions ? s0 + 64 : a.sessions;
   const int64_t s = s0 + threadIdx.x;
@@ -405,7 +440,7 @@ __global__ __launch_bounds__(64) void slash_kernel(SlashArgs a) {
   const int64_t nsc = (s1 - s0) * kTile;
   for (int64_t j = threadIdx.x; j < nsc; j += 64) s_sc[(j / kTile) * kScorePad + j % kTile] = a.scores[s0 * kTile + j];
   __syncthreads();
-  if (s < a.sessions) slash_session_t(a, s, LdsEdges{&a, e0, s_vr, s_ve, s_lv}, s_sc + threadIdx.x * kScorePad, 1);
+  if (s < a.sessions) slash_session_t(a, s, LdsEdges{&a, e0, s_vr, s_ve, s_lv, s_cl + threadIdx.x * kClipPad}, s_sc + threadIdx.x * kScorePad, 1);
   __syncthreads();
   for (int64_t j = threadIdx.x; j < nsc; j += 64) a.scores[s0 * kTile + j] = s_sc[(j / kTile) * kScorePad + j % kTile];
 }
