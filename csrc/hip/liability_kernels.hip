@@ -11,6 +11,8 @@
 // 16 terms in tile order; the reference sums in vouch-creation order, so the MFMA
 // path agrees to within an ulp-level tolerance while `sigma_eff_csr` (one lane
 // per vouchee, creation order) is the bit-exact path.
+#include <cstdlib>
+
 #include "ahv/kernels.h"
 #include "ahv/launch.h"
 #include "ahv/semantics.h"
@@ -445,9 +447,136 @@ __global__ __launch_bounds__(64) void slash_kernel(SlashArgs a) {
   for (int64_t j = threadIdx.x; j < nsc; j += 64) a.scores[s0 * kTile + j] = s_sc[(j / kTile) * kScorePad + j % kTile];
 }
 
+// Group-cooperative form: 16 lanes per session (4 sessions per wave, 16 per
+// 256-thread block).  Lane j holds edges j, j+16, j+32, j+48 of its session in
+// registers (voucher, vouchee, live) and the session's score σ[j]; "which live
+// edges vouch for `who`" is one ballot per 16 edges instead of a serial scan,
+// and clips walk the ballot's set bits in edge (= creation) order, reading the
+// voucher and its current σ with lane shuffles — the same clips, in the same
+// order, with the same fp64 arithmetic as slash_session_t.  The cascade walk
+// reads the group's clip list from LDS.  Sessions with more than
+// kGroupEdges edges fall back to the one-lane global-memory form.
+constexpr int kWaveLanes = 64;
+constexpr int kSlashGroup = 16;
+constexpr int kGroupChunks = 4;
+constexpr int kGroupEdges = kSlashGroup * kGroupChunks;  // 64
+constexpr int kSlashGroupsPerBlock = 16;
+
+__global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_group_kernel(SlashArgs a) {
+  __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
+  const int g = threadIdx.x / kSlashGroup;       // group in block
+  const int j = threadIdx.x % kSlashGroup;       // lane in group
+  const int gw = (threadIdx.x % kWaveLanes) / kSlashGroup;  // group in wave
+  const int gl0 = gw * kSlashGroup;              // first wave lane of the group
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kSlashGroupsPerBlock + g;
+  if (s >= a.sessions) return;
+  const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
+  if (n > kGroupEdges) {
+    if (j == 0) slash_session(a, s);
+    return;
+  }
+  auto group_bits = [&](bool p) -> uint32_t {
+    return static_cast<uint32_t>((__ballot(p) >> gl0) & 0xffffu);
+  };
+  int vr[kGroupChunks], ve[kGroupChunks];
+  bool lv[kGroupChunks];
+#pragma unroll
+  for (int c = 0; c < kGroupChunks; ++c) {
+    const int32_t i = c * kSlashGroup + j;
+    const bool in = i < n;
+    vr[c] = in ? a.voucher[b + i] : 0;
+    ve[c] = in ? a.vouchee[b + i] : -1;
+    lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
+  }
+  double sc = a.scores[s * kTile + j];
+  const double omega = a.omega[s];
+  const int32_t base = a.clip_offsets[s];
+  uint8_t* cl = s_cl[g];
+  int32_t nclip = 0;
+  static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
+  int32_t next0 = 0, end0 = 0, next1 = 0, end1 = 0;
+  int sp = 0;
+  int who = a.target[s], who_depth = 0;
+  bool pending = true;
+  for (;;) {
+    if (pending) {
+      pending = false;
+      if (j == who) sc = 0.0;
+      const int32_t first = nclip;
+#pragma unroll
+      for (int c = 0; c < kGroupChunks; ++c) {
+        uint32_t m = group_bits(ve[c] == who && lv[c]);
+        while (m) {
+          const int k = __builtin_ctz(m);
+          m &= m - 1;
+          const int v = __shfl(vr[c], gl0 + k, kWaveLanes);
+          const double x = __shfl(sc, gl0 + v, kWaveLanes);
+          const double before = x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
+          const double after = clip_sigma(before, omega);
+          if (j == v) sc = after;
+          if (j == 0) {
+            if (nclip < kGroupEdges) cl[nclip] = static_cast<uint8_t>(v | (after < kCascadeBelow ? 0x80 : 0));
+            if (nclip < a.clip_cap) {
+              a.clip_voucher[base + nclip] = static_cast<uint8_t>(v);
+              a.clip_depth[base + nclip] = static_cast<uint8_t>(who_depth);
+              a.clip_before[base + nclip] = before;
+              a.clip_after[base + nclip] = after;
+            }
+          }
+          if (j == k) {
+            lv[c] = false;
+            a.active[b + c * kSlashGroup + k] = 0;
+            a.released_us[b + c * kSlashGroup + k] = a.now_us;
+          }
+          ++nclip;
+        }
+      }
+      if (who_depth == 0) {
+        next0 = first;
+        end0 = nclip;
+      } else if (who_depth == 1) {
+        next1 = first;
+        end1 = nclip;
+      }
+      sp = who_depth + 1;
+    }
+    if (sp == 0) break;
+    const int depth = sp - 1;
+    const int32_t nx = depth == 0 ? next0 : next1;
+    const int32_t en = depth == 0 ? end0 : end1;
+    if (depth >= kMaxCascadeDepth || nx >= en) {
+      --sp;
+      continue;
+    }
+    if (depth == 0) next0 = nx + 1;
+    else next1 = nx + 1;
+    if (nx >= a.clip_cap) continue;
+    const int c8 = cl[nx];  // the LDS write by the group's lane 0 is visible: same wave
+    const int v = c8 & 0x7f;
+    if (!(c8 & 0x80)) continue;
+    bool any_live = false;
+#pragma unroll
+    for (int c = 0; c < kGroupChunks; ++c) any_live = any_live || group_bits(ve[c] == v && lv[c]) != 0u;
+    if (any_live) {
+      who = v;
+      who_depth = depth + 1;
+      pending = true;
+    }
+  }
+  a.scores[s * kTile + j] = sc;
+  if (j == 0) a.clip_count[s] = nclip;
+}
+
 void launch_slash(const SlashArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
-  hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
+  static const bool per_lane = [] {
+    const char* e = std::getenv("AHV_SLASH_PER_LANE");
+    return e && std::atoi(e) == 1;
+  }();
+  if (per_lane) hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(slash_group_kernel, grid1(a.sessions, kSlashGroupsPerBlock),
+                       dim3(kSlashGroup * kSlashGroupsPerBlock), 0, st, a);
   check_hip(hipGetLastError(), "slash_kernel");
 }
 void slash_host(const SlashArgs& a) { for (int64_t s = 0; s < a.sessions; ++s) slash_session(a, s); }
