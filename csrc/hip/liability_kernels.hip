@@ -99,11 +99,44 @@ AHV_HD void build_tile_entry(const VouchCsrArgs& a, int64_t s, int idx) {
   a.tiles[s * kTile * kTile + idx] = acc;
 }
 
+// Device: the session's edges are staged once in LDS as a (voucher·16 + vouchee)
+// key (0xffff = not live: every byte value is a real entry) and the bond; every lane then walks them in
+// creation order for its 4 entries — all 64 lanes read the same edge (an LDS
+// broadcast) instead of 5 global loads per edge per entry.
+constexpr int kTileLdsEdges = 512;
+
 __global__ __launch_bounds__(64) void build_tiles_kernel(VouchCsrArgs a) {
+  __shared__ uint16_t s_key[kTileLdsEdges];
+  __shared__ double s_bd[kTileLdsEdges];
   const int64_t s = blockIdx.x;
   if (s >= a.sessions) return;
+  const int32_t b = a.offsets[s], n = a.offsets[s + 1] - b;
+  if (n > kTileLdsEdges) {  // uniform per block
 #pragma unroll
-  for (int q = 0; q < 4; ++q) build_tile_entry(a, s, threadIdx.x + 64 * q);
+    for (int q = 0; q < 4; ++q) build_tile_entry(a, s, threadIdx.x + 64 * q);
+    return;
+  }
+  for (int32_t k = threadIdx.x; k < n; k += 64) {
+    const bool live = live_edge(a.active, a.expiry_us, b + k, a.now_us);
+    s_key[k] = live ? static_cast<uint16_t>(a.voucher[b + k] * kTile + a.vouchee[b + k]) : 0xffffu;
+    s_bd[k] = a.bonded[b + k];
+  }
+  __syncthreads();
+  const uint32_t i0 = threadIdx.x;
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+  for (int32_t k = 0; k < n; ++k) {
+    const uint32_t key = s_key[k];
+    const double bd = s_bd[k];
+    if (key == i0) acc0 += bd;
+    if (key == i0 + 64) acc1 += bd;
+    if (key == i0 + 128) acc2 += bd;
+    if (key == i0 + 192) acc3 += bd;
+  }
+  double* t = a.tiles + s * kTile * kTile;
+  t[i0] = acc0;
+  t[i0 + 64] = acc1;
+  t[i0 + 128] = acc2;
+  t[i0 + 192] = acc3;
 }
 void launch_build_tiles(const VouchCsrArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
