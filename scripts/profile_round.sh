@@ -32,8 +32,12 @@ pmc pipe_lds governance "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_IN
 pmc cfg_mfma "bond_tiles|sigma_eff|slash|build_tiles|chain_hash|merkle|saga" \
   "SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES" \
   python3 benchmarks/bench_configs.py --steps 2 --warmup 1 &&
-pmc cfg_mem "bond_tiles|sigma_eff|slash|build_tiles|chain_hash|merkle|saga" "FETCH_SIZE WRITE_SIZE GRBM_GUI_ACTIVE" \
-  python3 benchmarks/bench_configs.py --steps 2 --warmup 1
+pmc cfg_fetch "bond_tiles|sigma_eff|slash|build_tiles|chain_hash|merkle|saga" "FETCH_SIZE GRBM_GUI_ACTIVE" \
+  python3 benchmarks/bench_configs.py --steps 2 --warmup 1 &&
+pmc cfg_write "bond_tiles|sigma_eff|slash|build_tiles|chain_hash|merkle|saga" "WRITE_SIZE GRBM_GUI_ACTIVE" \
+  python3 benchmarks/bench_configs.py --steps 2 --warmup 1 &&
+pmc cfg_stall "slash|sigma_eff|build_tiles|chain_hash|merkle" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" \
+  python3 benchmarks/bench_configs.py config5 config3 --steps 2 --warmup 1
 rc=$?
 step "done rc=$rc"
 tail -1 $OUT/bench.log 2>/dev/null
