@@ -21,17 +21,34 @@ class Interner:
         self._pool = C.StringPool()
         self._uploaded: dict[str, tuple[int, tuple[torch.Tensor, torch.Tensor, torch.Tensor]]] = {}
 
+    # Python strings may hold lone surrogates (json.dumps escapes them as \udXXX);
+    # they have no strict UTF-8 form, so such strings cross to the native pool in
+    # surrogatepass UTF-8, which the native escaper decodes to the same code point.
+    @staticmethod
+    def _b(s: str) -> bytes:
+        return s.encode("utf-8", "surrogatepass")
+
     def intern(self, s: str) -> int:
-        return self._pool.intern(s)
+        try:
+            return self._pool.intern(s)
+        except TypeError:
+            return self._pool.intern(self._b(s))
 
     def intern_many(self, items: Iterable[str]) -> list[int]:
-        return self._pool.intern_many(list(items))
+        items = list(items)
+        try:
+            return self._pool.intern_many(items)
+        except TypeError:
+            return self._pool.intern_many([self._b(s) for s in items])
 
     def lookup(self, s: str) -> int:
-        return self._pool.lookup(s)
+        try:
+            return self._pool.lookup(s)
+        except TypeError:
+            return self._pool.lookup(self._b(s))
 
     def str(self, i: int) -> str:
-        return self._pool.str(int(i))
+        return self._pool.str(int(i)).decode("utf-8", "surrogatepass")
 
     def escaped(self, i: int) -> bytes:
         return self._pool.escaped(int(i))

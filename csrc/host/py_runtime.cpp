@@ -145,7 +145,8 @@ void register_runtime(py::module_& m) {
       .def("intern", &StringPool::intern)
       .def("intern_many", &StringPool::intern_many)
       .def("lookup", &StringPool::lookup)
-      .def("str", &StringPool::str)
+      // bytes (UTF-8, lone surrogates in surrogatepass form): the Python wrapper decodes
+      .def("str", [](const StringPool& p, int32_t id) { return py::bytes(p.str(id)); })
       .def("escaped", &StringPool::escaped)
       .def("bytes_view", &StringPool::bytes_view)
       .def("offsets_view", &StringPool::offsets_view)
