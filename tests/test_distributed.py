@@ -178,18 +178,23 @@ def test_collectives_are_noops_single_rank():
 
 
 @pytest.mark.slow
-def test_bench_two_ranks_over_gloo():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_ranks_over_gloo(world):
+    """The driver's scaling run (N = 1, 2, 4, 8 ranks of bench.py) rehearsed on the
+    CPU: the same launcher, rank/env handling, double-buffered async X04
+    all-reduce, max-over-ranks timing and the one JSON line from rank 0."""
     port = _free_port()
-    env = dict(os.environ, OMP_NUM_THREADS="2", AHV_SKIP_AUTOBUILD="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    env = dict(os.environ, OMP_NUM_THREADS="1", AHV_SKIP_AUTOBUILD="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--device", "cpu", "--sessions", "256", "--agents", "2048", "--steps", "2",
+           "--gpus", str(world), "--device", "cpu", "--sessions", "256", "--agents", "2048", "--steps", "3",
            "--warmup", "1", "--no-scalar"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 512
-    assert out["last_step_counters"]["sessions"] == 512 and out["last_step_counters"]["ok"] == 512
-    assert out["value"] > 0 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["n_gpus"] == world and out["config"]["parallelism"] == f"dp{world}"
+    assert out["config"]["global_batch"] == 256 * world
+    assert out["last_step_counters"]["sessions"] == 256 * world and out["last_step_counters"]["ok"] == 256 * world
+    assert out["value"] > 0 and out["steps"] == 3 and out["warmup"] == 1
