@@ -8,7 +8,8 @@
 //
 // for every session of a batch; each lane owns one session.  The per-session body
 // is `pipeline_session<Sink>` below, instantiated on the device with the LDS
-// WaveRingSink and on the host with HostSink (the CPU twin used by tests).
+// WordWindowSink (ahv/wave_sink.h) and on the host with HostSink (the CPU twin
+// used by tests).
 #pragma once
 
 #include "ahv/delta_emit.h"
