@@ -211,7 +211,9 @@ AHV_HD constexpr uint32_t lit_byte(const char (&lit)[N], size_t i) {
 template <class Sink, size_t N>
 AHV_HD void emit_lit(Sink& s, const char (&lit)[N]) {
   constexpr uint32_t n = static_cast<uint32_t>(N - 1);
-  if (!s.seg(n)) return;
+  // A short literal is cheaper to emit than to test against the window (its
+  // out-of-window words land in the trash row); longer ones are skipped whole.
+  if (n > 8 && !s.seg(n)) return;
 #pragma unroll
   for (uint32_t i = 0; i + 4 <= n; i += 4)
     s.put4(lit_byte(lit, i) << 24 | lit_byte(lit, i + 1) << 16 | lit_byte(lit, i + 2) << 8 | lit_byte(lit, i + 3));
