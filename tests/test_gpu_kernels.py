@@ -78,11 +78,11 @@ def test_ring_kernels(cuda_device):
     _check(lambda *t: R.ring_check(*t), ring, flags, sig, cons, wit)
 
 
-def _vouch_batch(S, seed):
+def _vouch_batch(S, seed, lo=0, hi=40):
     rng = random.Random(seed)
     offs, vr, ve, bd, ac, ex = [0], [], [], [], [], []
     for _ in range(S):
-        for _ in range(rng.randint(0, 40)):
+        for _ in range(rng.randint(lo, hi)):
             a, b = rng.sample(range(16), 2)
             vr.append(a)
             ve.append(b)
@@ -134,6 +134,32 @@ def test_liability_kernels(cuda_device):
     _check(lambda *t: LI.vouch_admit(mk(*t[: len(fields)]), *t[len(fields):], 100),
            *[getattr(vb, f) for f in fields], torch.tensor(r_off, dtype=i32), torch.tensor(rv, dtype=u8),
            torch.tensor(re_, dtype=u8), torch.tensor(rs, dtype=f64), torch.tensor(rp, dtype=f64))
+
+
+def test_liability_kernels_large_sessions(cuda_device):
+    """Sessions past every staging limit: > 64 edges (slash falls back from the
+    16-lane group form to one lane), > 512 (tile build reads global memory),
+    > 2048 per 16-session block (σ_eff element form), mixed with small ones in
+    the same blocks; duplicate (voucher, vouchee) pairs compound."""
+    S = 96
+    vb = _vouch_batch(S, 7, lo=0, hi=700)
+    fields = list(vb.__dataclass_fields__)
+    g = torch.Generator().manual_seed(7)
+    sigma = torch.rand((S, 16), dtype=f64, generator=g)
+    omega = torch.rand(S, dtype=f64, generator=g)
+
+    def mk(*t):
+        return LI.VouchBatch(*t[: len(fields)])
+
+    assert int((vb.offsets[1:] - vb.offsets[:-1]).max()) > 512
+    _check(lambda *t: LI.build_tiles(mk(*t), 100), *[getattr(vb, f) for f in fields])
+    _check(lambda *t: LI.sigma_eff_exact(mk(*t[:-2]), t[-2], t[-1], 100), *[getattr(vb, f) for f in fields],
+           sigma, omega)
+    tgt = torch.randint(0, 16, (S,), dtype=u8, generator=g)
+    scores = torch.rand((S, 16), dtype=f64, generator=g)
+    scores[scores < 0.1] = float("nan")
+    _check(lambda *t: LI.slash(mk(*t[:-3]), t[-3], t[-2], t[-1], 100), *[getattr(vb, f) for f in fields],
+           tgt, omega, scores)
 
 
 def test_audit_kernels(cuda_device):
