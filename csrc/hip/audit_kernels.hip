@@ -130,8 +130,9 @@ void chain_hash_host(const ChainHashArgs& a) {
 }
 
 // ------------------------------------------------------------------ K09
-// One lane per chain: binary-counter Merkle (delta_emit.h merkle_root_counter)
-// with its ≤ log2(n)+1 partial subtrees parked in the chain's rows of `scratch`.
+// One lane per chain: level-wise Merkle (delta_emit.h merkle_root_levels, one
+// node-hash site) with its ⌈n/2⌉ interior digests parked in the chain's rows of
+// `scratch` (a chain of n leaves owns n scratch rows).
 
 struct GlobalStash {
   uint32_t* rows;  // this chain's scratch rows
@@ -157,7 +158,7 @@ AHV_HD void merkle_elem(const MerkleArgs& a, int64_t c) {
   }
   GlobalStash gs{a.scratch + static_cast<int64_t>(b) * 8};
   uint32_t r[8];
-  merkle_root_counter(
+  merkle_root_levels(
       gs, static_cast<uint32_t>(e - b),
       [&](uint32_t i, uint32_t h[8]) {
         for (int k = 0; k < 8; ++k) h[k] = a.leaves[(static_cast<int64_t>(b) + i) * 8 + k];
@@ -165,7 +166,7 @@ AHV_HD void merkle_elem(const MerkleArgs& a, int64_t c) {
       r);
   for (int k = 0; k < 8; ++k) root[k] = r[k];
 }
-__global__ void merkle_kernel(MerkleArgs a) {
+__global__ __launch_bounds__(kWaveLanes) void merkle_kernel(MerkleArgs a) {
   for (int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; c < a.chains;
        c += static_cast<int64_t>(gridDim.x) * blockDim.x)
     merkle_elem(a, c);
@@ -227,6 +228,14 @@ void launch_verify(const VerifyArgs& a, hipStream_t st) {
 void verify_host(const VerifyArgs& a) {
   for (int64_t i = 0; i < a.deltas; ++i) verify_delta_elem(a, i);
   for (int64_t c = 0; c < a.chains; ++c) verify_chain_elem(a, c);
+}
+
+
+void kernels_audit(std::vector<KernelEntry>& out) {
+  out.push_back({"chain_hash_kernel", reinterpret_cast<const void*>(&chain_hash_kernel)});
+  out.push_back({"merkle_kernel", reinterpret_cast<const void*>(&merkle_kernel)});
+  out.push_back({"hash_many_kernel", reinterpret_cast<const void*>(&hash_many_kernel)});
+  out.push_back({"verify_delta_kernel", reinterpret_cast<const void*>(&verify_delta_kernel)});
 }
 
 }  // namespace ahv

@@ -614,4 +614,14 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
 }
 void slash_host(const SlashArgs& a) { for (int64_t s = 0; s < a.sessions; ++s) slash_session(a, s); }
 
+
+void kernels_liability(std::vector<KernelEntry>& out) {
+  out.push_back({"slash_group_kernel", reinterpret_cast<const void*>(&slash_group_kernel)});
+  out.push_back({"slash_kernel", reinterpret_cast<const void*>(&slash_kernel)});
+  out.push_back({"sigma_eff_csr_kernel", reinterpret_cast<const void*>(&sigma_eff_csr_kernel)});
+  out.push_back({"build_tiles_kernel", reinterpret_cast<const void*>(&build_tiles_kernel)});
+  out.push_back({"bond_tiles_mfma_kernel", reinterpret_cast<const void*>(&bond_tiles_mfma_kernel)});
+  out.push_back({"vouch_admit_kernel", reinterpret_cast<const void*>(&vouch_admit_kernel)});
+}
+
 }  // namespace ahv

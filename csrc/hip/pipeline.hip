@@ -155,4 +155,10 @@ void pipeline_host(const PipelineArgs& a) {
   }
 }
 
+
+void kernels_pipeline(std::vector<KernelEntry>& out) {
+  out.push_back({"governance_pipeline_kernel<3,3>", reinterpret_cast<const void*>(&governance_pipeline_kernel<3, 3>)});
+  out.push_back({"governance_pipeline_kernel<4,2>", reinterpret_cast<const void*>(&governance_pipeline_kernel<4, 2>)});
+}
+
 }  // namespace ahv

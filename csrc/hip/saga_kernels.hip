@@ -142,4 +142,10 @@ void saga_phase_host(const SagaBatchArgs& a, int phase, int k) {
   }
 }
 
+
+void kernels_saga(std::vector<KernelEntry>& out) {
+  out.push_back({"saga_fused_regs_kernel<10>", reinterpret_cast<const void*>(&saga_fused_regs_kernel<10>)});
+  out.push_back({"saga_phase_kernel", reinterpret_cast<const void*>(&saga_phase_kernel)});
+}
+
 }  // namespace ahv

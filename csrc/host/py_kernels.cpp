@@ -347,6 +347,29 @@ void register_kernels(py::module_& m) {
                                 reinterpret_cast<hipStream_t>(stream));
       },
       "Advance cursor slot/id bases by one batch of `n` sessions on `stream`.");
+  m.def(
+      "kernel_attributes",
+      []() {
+        std::vector<KernelEntry> ks;
+        kernels_pipeline(ks);
+        kernels_audit(ks);
+        kernels_liability(ks);
+        kernels_saga(ks);
+        py::list out;
+        for (const auto& k : ks) {
+          hipFuncAttributes fa{};
+          check_hip(hipFuncGetAttributes(&fa, k.fn), k.name);
+          py::dict d;
+          d["name"] = k.name;
+          d["vgprs"] = fa.numRegs;
+          d["scratch_bytes"] = static_cast<int64_t>(fa.localSizeBytes);
+          d["lds_bytes"] = static_cast<int64_t>(fa.sharedSizeBytes);
+          d["max_threads"] = fa.maxThreadsPerBlock;
+          out.append(d);
+        }
+        return out;
+      },
+      "Resources of the hot kernels (hipFuncGetAttributes): VGPRs, scratch, static LDS.");
   m.def("device_wall_clock", &device_wall_clock, py::arg("device"));
   m.def("device_wall_clock_rate_khz", &device_wall_clock_rate_khz, py::arg("device"));
   m.attr("PIPE_MAX_PARTICIPANTS") = kMaxParticipants;

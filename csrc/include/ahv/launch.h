@@ -5,6 +5,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "ahv/hd.h"
 
@@ -24,5 +25,17 @@ void launch_pipeline_clock(int64_t* cursor, int64_t base_us, int64_t base_clk, i
 void launch_pipeline_advance(int64_t* cursor, int64_t n, int64_t capacity, hipStream_t s);
 int64_t device_wall_clock(int device);  // one synchronous sample of wall_clock64()
 int64_t device_wall_clock_rate_khz(int device);
+
+// Kernel registry for resource introspection (hipFuncGetAttributes): every
+// kernel translation unit lists its hot kernels; tests assert no scratch spills
+// and the designed LDS footprint (agent_hypervisor_amd._C.kernel_attributes).
+struct KernelEntry {
+  const char* name;
+  const void* fn;
+};
+void kernels_pipeline(std::vector<KernelEntry>& out);
+void kernels_audit(std::vector<KernelEntry>& out);
+void kernels_liability(std::vector<KernelEntry>& out);
+void kernels_saga(std::vector<KernelEntry>& out);
 
 }  // namespace ahv
