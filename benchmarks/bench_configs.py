@@ -247,7 +247,10 @@ def config5(ctx: Ctx, args):
     leaves_offs = packed["chain_offsets"]
 
     def step():
-        vb = vb0.clone()
+        # fresh storm state: the slash mutates only `active`, `released_us` and the
+        # scores, so only those are reset (the CSR topology and bonds are shared)
+        vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, vb0.active.clone(),
+                           vb0.expiry_us, vb0.released_us.clone())
         out = LI.slash(vb, tgt, omega, scores0.clone(), 1)
         se = LI.sigma_eff_exact(vb, out.scores.nan_to_num(0.0), omega, 1)
         digests = A.chain_hashes(packed)
