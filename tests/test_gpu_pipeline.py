@@ -81,3 +81,39 @@ def test_pipeline_large_batch_runs(cuda_device):
     eng.run_pipeline(1 << 18, stats=stats)
     torch.cuda.synchronize()
     assert stats[0].item() == 1 << 18 and stats[1].item() == 1 << 18
+
+
+_ADV = list('abcXYZ019:/-_. "\\{}') + ["\n", "\t", "\x00", "\x7f", "é", "中", "\U0001F600", "\ud800"]
+
+
+def _adv_text(rng, lo, hi):
+    return "".join(rng.choice(_ADV) for _ in range(rng.randint(lo, hi)))
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_pipeline_adversarial_text_device(cuda_device, case):
+    """Random DIDs (1–200 characters: JSON escapes, astral characters, lone
+    surrogates), 0–3 change objects with long or null fields, 1–8 deltas and
+    whole-second timestamps: every lane's message has its own byte phase and
+    length (1–20+ SHA blocks, many window passes).  The host twin these are
+    compared with is pinned to the reference package byte for byte by
+    tests/test_differential_reference.py."""
+    import random
+
+    rng = random.Random(100 + case)
+    dids = list(dict.fromkeys(_adv_text(rng, 1, 200) for _ in range(64)))
+    specs = []
+    for _ in range(rng.randint(0, 3)):
+        p = _adv_text(rng, 0, 120).replace("{", "{{").replace("}", "}}") + "{i}"
+        o = _adv_text(rng, 1, 8).replace("{", "{{").replace("}", "}}")
+        hsh = None if rng.random() < 0.3 else _adv_text(rng, 0, 70).replace("{", "{{").replace("}", "}}")
+        specs.append((p, o, hsh))
+    deltas = rng.randint(1, 8)
+    now = 1_767_225_600_000_000 - 2 if case % 2 else NOW
+    d, h = _pair(dids=dids, sig=[0.9] * len(dids), cap=2048)
+    n = 640
+    agents = torch.randint(0, len(dids), (n,), dtype=torch.int32, generator=torch.Generator().manual_seed(case))
+    bd = d.run_pipeline(n, agents=agents.to(cuda_device), deltas=deltas, now_us=now, changes=specs or None)
+    bh = h.run_pipeline(n, agents=agents, deltas=deltas, now_us=now, changes=specs or None)
+    torch.cuda.synchronize()
+    _assert_tables_equal(d, h, bd, bh)
