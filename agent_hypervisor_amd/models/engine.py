@@ -29,7 +29,7 @@ from typing import Optional, Sequence
 
 import torch
 
-from agent_hypervisor_amd._native import C
+from agent_hypervisor_amd._native import C  # noqa: F401 - loads the native extension (fails loudly when missing)
 from agent_hypervisor_amd.models.tables import AgentTable, SessionTable, VouchTable
 from agent_hypervisor_amd.ops import pipeline as _pipeline_op
 from agent_hypervisor_amd.utils.interner import Interner

@@ -17,7 +17,6 @@ Two launch shapes over the same element functions:
 from __future__ import annotations
 
 from dataclasses import dataclass
-from datetime import datetime
 from typing import Optional
 
 import torch

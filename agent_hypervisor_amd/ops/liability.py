@@ -10,7 +10,6 @@ local index, and its vouch edges in creation order as CSR arrays
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional
 
 import torch
 

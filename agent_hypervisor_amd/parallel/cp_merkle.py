@@ -20,7 +20,6 @@ top levels.  The delta *chain* hash stays serial; only the tree parallelises.
 from __future__ import annotations
 
 import math
-from typing import Optional
 
 import torch
 import torch.distributed as dist
