@@ -93,14 +93,18 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # AHV_BENCH_FORCE_DIST=1 (under torch.distributed.run) takes the multi-rank path
+    # — process group, async RCCL counter all-reduce, barriers, max-over-ranks —
+    # even with one rank, so the code the 8-GPU run executes is exercised on 1 GPU.
+    multi = world > 1 or os.environ.get("AHV_BENCH_FORCE_DIST") == "1"
+    if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if args.device == "cuda":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1:
+    if multi:
         if dev.type == "cuda":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -137,7 +141,7 @@ def main() -> None:
         st.zero_()
         agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
         eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
-        works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if world > 1 else None
+        works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if multi else None
         return st
 
     def drain():
@@ -150,12 +154,12 @@ def main() -> None:
         from agent_hypervisor_amd.runtime.graphs import PipelineGraph
 
         reduce = None
-        if world > 1 and dev.type == "cuda":
+        if multi and dev.type == "cuda":
             from agent_hypervisor_amd.parallel.rccl import Communicator
 
             comm = Communicator.from_process_group(device=local)
             reduce = comm.all_reduce
-        elif world > 1:
+        elif multi:
             reduce = allreduce_stats
         buf = torch.zeros(S, dtype=torch.int32, device=dev)
         pg = PipelineGraph(eng, S, buf, deltas=args.deltas, stats=stats,
@@ -182,7 +186,7 @@ def main() -> None:
         sync()
         lat.append(time.perf_counter() - t0)
 
-    if world > 1:
+    if multi:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -190,11 +194,11 @@ def main() -> None:
         last = step()
     drain()
     sync()
-    if world > 1:
+    if multi:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    if world > 1:
+    if multi:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -236,7 +240,7 @@ def main() -> None:
             "last_step_counters": dict(zip(["sessions", "ok", "participants", "deltas", "commits", "archived"], totals)),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 

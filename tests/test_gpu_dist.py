@@ -1,0 +1,39 @@
+"""The multi-rank bench path on a real GPU: ``bench.py`` under
+``torch.distributed.run`` with ``AHV_BENCH_FORCE_DIST=1`` takes the exact code the
+driver's 8-GPU scaling run executes — RCCL process group bound to the device,
+double-buffered async X04 all-reduce, barriers, max-over-ranks timing — with
+one rank, eager and hipGraph-replay forms (the graph captures the collective
+through the C++ RCCL communicator)."""
+
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_bench_rccl_path_one_rank(cuda_device, graph):
+    env = dict(os.environ, AHV_BENCH_FORCE_DIST="1", AHV_SKIP_AUTOBUILD="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--sessions", "65536", "--agents", "65536", "--steps", "3", "--warmup", "1",
+           "--no-scalar"] + (["--graph"] if graph else [])
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["last_step_counters"]["sessions"] == 65536
+    assert out["last_step_counters"]["ok"] == 65536 and out["value"] > 0
