@@ -273,12 +273,20 @@ AHV_HD void emit_str_ref(Sink& s, StrRef r) {
   if (!s.seg(n + 2)) return;
   s.put(0x22u << 24, 1);
   const U4* q = reinterpret_cast<const U4*>(r.p);
-  const uint32_t chunks = (n + 15) / 16;
-  for (uint32_t c = 0; c < chunks; ++c) {
+  const uint32_t full = n / 16;
+  // whole 16-byte chunks as four 4-byte puts (one v_alignbit each in the sink);
+  // four named words, no indexing into the chunk (a runtime index would put it
+  // in scratch memory on the device)
+  for (uint32_t c = 0; c < full; ++c) {
     const U4 cur = q[c];
-    const int32_t left = static_cast<int32_t>(n - 16 * c);
-    // four named words (no indexing into the chunk: a runtime index would put
-    // it in scratch memory on the device)
+    s.put4(bswap_word(cur.a));
+    s.put4(bswap_word(cur.b));
+    s.put4(bswap_word(cur.c));
+    s.put4(bswap_word(cur.d));
+  }
+  if (n & 15u) {
+    const U4 cur = q[full];
+    const int32_t left = static_cast<int32_t>(n & 15u);
     emit_word_le(s, cur.a, left);
     emit_word_le(s, cur.b, left - 4);
     emit_word_le(s, cur.c, left - 8);
@@ -297,17 +305,24 @@ AHV_HD void emit_span(Sink& s, const uint8_t* p, uint32_t n) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
   const uint32_t sh = static_cast<uint32_t>(a & 3u) * 8u;
   const uint32_t words = (n + (sh >> 3) + 3u) >> 2;  // aligned words touched
-  uint32_t cur = w[0];
-  for (uint32_t k = 0; 4u * k < n; ++k) {
-    const uint32_t nxt = k + 1 < words ? w[k + 1] : 0u;
+  auto funnel = [sh](uint32_t lo, uint32_t hi) -> uint32_t {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const uint32_t le = __builtin_amdgcn_alignbit(nxt, cur, sh);
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
 #else
-    const uint32_t le = sh ? (cur >> sh) | (nxt << (32u - sh)) : cur;
+    return sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
 #endif
-    const uint32_t left = n - 4u * k;
-    s.put(bswap_word(le), left < 4u ? left : 4u);
+  };
+  uint32_t cur = w[0];
+  const uint32_t full = n >> 2;
+  // whole 4-byte chunks: the cheap funnel put (one v_alignbit in the sink)
+  for (uint32_t k = 0; k < full; ++k) {
+    const uint32_t nxt = k + 1 < words ? w[k + 1] : 0u;
+    s.put4(bswap_word(funnel(cur, nxt)));
     cur = nxt;
+  }
+  if (n & 3u) {
+    const uint32_t nxt = full + 1 < words ? w[full + 1] : 0u;
+    s.put(bswap_word(funnel(cur, nxt)), n & 3u);
   }
 }
 
