@@ -62,20 +62,28 @@ def build_tiles(vb: VouchBatch, now_us: int) -> torch.Tensor:
     return tiles
 
 
-def bond_tiles(tiles: torch.Tensor, sigma: torch.Tensor, omega: torch.Tensor):
+def bond_tiles(tiles: torch.Tensor, sigma: torch.Tensor, omega: torch.Tensor,
+               members: "torch.Tensor | None" = None, agent_exposure: "torch.Tensor | None" = None):
     """K03/K04 on fp64 MFMA: (σ_eff [S,16], exposure [S,16], bonded_in [S,16]).
 
     σ_eff = min(σ + ω·Σ_voucher bonded, 1) per vouchee; exposure = Σ bonded per
     voucher.  Sums run in tile order (≤ 1-ulp-level differences from the
-    creation-order reference; :func:`sigma_eff_exact` is bit-exact)."""
+    creation-order reference; :func:`sigma_eff_exact` is bit-exact).
+
+    With ``members`` (int64 [S,16] global agent ids) and ``agent_exposure``
+    (f64 [A]), each participant's exposure is also added into the agent-indexed
+    vector by the same kernel (the X01 input; fp64 atomics on the device, so the
+    summation order across sessions is unspecified there)."""
     S = tiles.shape[0]
     out = [torch.empty((S, TILE), dtype=f64, device=tiles.device) for _ in range(3)]
-    launch(
-        "bond_tiles",
-        {"sessions": S},
-        dict(tiles=tiles, sigma=sigma, omega=omega, sigma_eff=out[0], exposure=out[1], bonded_in=out[2]),
-        dict(tiles=f64, sigma=f64, omega=f64),
-    )
+    tensors = dict(tiles=tiles, sigma=sigma, omega=omega, sigma_eff=out[0], exposure=out[1], bonded_in=out[2])
+    dtypes = dict(tiles=f64, sigma=f64, omega=f64)
+    if members is not None:
+        if agent_exposure is None or tuple(members.shape) != (S, TILE):
+            raise ValueError("members must be int64 [S, 16] and come with agent_exposure")
+        tensors.update(members=members, agent_exposure=agent_exposure)
+        dtypes.update(members=torch.int64, agent_exposure=f64)
+    launch("bond_tiles", {"sessions": S}, tensors, dtypes)
     return tuple(out)
 
 

@@ -61,7 +61,12 @@ __global__ __launch_bounds__(64) void bond_tiles_mfma_kernel(BondTileArgs a) {
   }
   if (c == 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) a.exposure[s * kTile + r + 4 * q] = row[q];
+    for (int q = 0; q < 4; ++q) {
+      a.exposure[s * kTile + r + 4 * q] = row[q];
+      // fused agent-indexed scatter (X01 input): one hardware fp64 atomic per
+      // participant instead of a separate index_add pass over [S, 16]
+      if (a.members) unsafeAtomicAdd(a.agent_exposure + a.members[s * kTile + r + 4 * q], row[q]);
+    }
   }
 }
 
@@ -83,6 +88,7 @@ void bond_tiles_host(const BondTileArgs& a) {
       a.bonded_in[s * kTile + j] = cs;
       a.sigma_eff[s * kTile + j] = sigma_eff_combine(a.sigma[s * kTile + j], a.omega[s], cs);
       a.exposure[s * kTile + j] = rs;
+      if (a.members) a.agent_exposure[a.members[s * kTile + j]] += rs;
     }
   }
 }

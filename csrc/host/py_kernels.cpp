@@ -176,6 +176,9 @@ static BondTileArgs to_bond_tiles(const py::dict& d) {
   BondTileArgs a{};
   V(sessions, int64_t); P(tiles, const double); P(sigma, const double); P(omega, const double);
   P(sigma_eff, double); P(exposure, double); P(bonded_in, double);
+  if (d.contains("members")) {
+    P(members, const int64_t); P(agent_exposure, double);
+  }
   return a;
 }
 static VouchCsrArgs to_vouch_csr(const py::dict& d) {

@@ -167,6 +167,10 @@ struct BondTileArgs {
   double* sigma_eff;     // [S, 16] out
   double* exposure;      // [S, 16] out: Σ bonded by voucher (row sums)
   double* bonded_in;     // [S, 16] out: Σ bonded for vouchee (column sums)
+  // optional X01 input: add each participant's exposure into an agent-indexed
+  // vector (fp64 atomics on the device; session order on the host), or null
+  const int64_t* members;   // [S, 16] global agent id of each participant
+  double* agent_exposure;   // [A] accumulated
 };
 void launch_bond_tiles(const BondTileArgs&, hipStream_t);
 void bond_tiles_host(const BondTileArgs&);

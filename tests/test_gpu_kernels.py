@@ -115,6 +115,15 @@ def test_liability_kernels(cuda_device):
     ref = LI.sigma_eff_exact(vb, sigma, omega, 100)
     se, _, _ = LI.bond_tiles(tiles.cuda(), sigma.cuda(), omega.cuda())
     torch.testing.assert_close(se.cpu(), ref, rtol=0, atol=1e-12)
+    # fused agent-indexed exposure scatter (X01 input) == index_add of the per-session rows
+    members = torch.randint(0, 500, (S, 16), generator=g)
+    agent_x = torch.zeros(500, dtype=f64, device="cuda")
+    _, expo, _ = LI.bond_tiles(tiles.cuda(), sigma.cuda(), omega.cuda(), members=members.cuda(), agent_exposure=agent_x)
+    want = torch.zeros(500, dtype=f64).index_add_(0, members.reshape(-1), expo.cpu().reshape(-1))
+    torch.testing.assert_close(agent_x.cpu(), want, rtol=1e-12, atol=1e-12)
+    host_x = torch.zeros(500, dtype=f64)
+    LI.bond_tiles(tiles, sigma, omega, members=members, agent_exposure=host_x)
+    torch.testing.assert_close(host_x, want, rtol=1e-12, atol=1e-12)
     _check(lambda *t: LI.release_bonds(mk(*t), 100), *[getattr(vb, f) for f in fields])
     tgt = torch.randint(0, 16, (S,), dtype=u8, generator=g)
     scores = torch.rand((S, 16), dtype=f64, generator=g)
