@@ -255,7 +255,7 @@ def config5(ctx: Ctx, args):
         vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, vb0.active.clone(),
                            vb0.expiry_us, vb0.released_us.clone())
         out = LI.slash(vb, tgt, omega, scores0.clone(), 1, clip_cap=per)  # ≤ one clip per edge
-        se = LI.sigma_eff_exact(vb, out.scores.nan_to_num(0.0), omega, 1)
+        se = LI.sigma_eff_exact(vb, out.scores, omega, 1)  # NaN (absent) reads as 0.0
         digests = A.chain_hashes(packed)
         A.merkle_roots(leaves_offs, digests)
         return se

@@ -30,6 +30,9 @@ inline dim3 grid1(int64_t n, int per_block = kBlock) {
 AHV_HD bool live_edge(const uint8_t* active, const int64_t* expiry, int64_t e, int64_t now) {
   return active[e] && (expiry == nullptr || expiry[e] < 0 || now <= expiry[e]);
 }
+// σ of the batched encoding: NaN marks an agent absent from agent_scores, which the
+// reference reads as 0.0 (as the slash kernel does), so no caller has to scrub NaNs.
+AHV_HD double score_or_zero(double x) { return x != x ? 0.0 : x; }
 }  // namespace
 
 // ------------------------------------------------------------ K03/K04 MFMA
@@ -162,7 +165,7 @@ AHV_HD void sigma_eff_csr_elem(const VouchCsrArgs& a, int64_t i) {
   double contrib = 0.0;
   for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
     if (a.vouchee[k] == e && live_edge(a.active, a.expiry_us, k, a.now_us)) contrib += a.bonded[k];
-  a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[s], contrib);
+  a.sigma_eff[i] = sigma_eff_combine(score_or_zero(a.sigma[i]), a.omega[s], contrib);
 }
 // Device: a 256-thread block owns 16 sessions; thread (session, vouchee) walks
 // its session's edges in creation order and adds the live bonds of its vouchee —
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(kSigmaSessions * kTile) void sigma_eff_csr_kernel(V
       const int32_t j = pad_edge(k);
       if (s_ve[j] == e) contrib += s_bd[j];
     }
-    a.sigma_eff[i] = sigma_eff_combine(a.sigma[i], a.omega[s], contrib);
+    a.sigma_eff[i] = sigma_eff_combine(score_or_zero(a.sigma[i]), a.omega[s], contrib);
   }
 }
 void launch_sigma_eff_csr(const VouchCsrArgs& a, hipStream_t st) {
