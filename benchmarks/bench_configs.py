@@ -168,18 +168,33 @@ def config3(ctx: Ctx, args):
     exchange = (lambda t: owned.__setitem__("view", AS.reduce_to_owners(t))) if args.owner_reduce \
         else X.allreduce_exposure
     it = [0]
+    # P03: the liability stage (tile build + fp64 MFMA σ_eff/exposure) does not
+    # read this step's pipeline output, and 100 k sessions fill only half the
+    # GPU's wave slots, so the stage runs on a second stream beside the pipeline
+    side = torch.cuda.Stream(ctx.dev) if ctx.dev.type == "cuda" else None
 
-    def step():
-        cur = it[0] & 1
-        it[0] += 1
-        stats.zero_()
-        agents = torch.randint(0, A_, (S,), device=ctx.dev, dtype=i32, generator=gen)
-        eng.run_pipeline(S, agents=agents, stats=stats)
+    def liability_stage(cur):
         tiles = LI.build_tiles(vb, 0)
         comm[cur].wait()  # buffer reuse: the exchange from two steps ago is done
         exposure[cur].zero_()
         # σ_eff / exposure on fp64 MFMA; exposure scattered into the agent vector in-kernel
         LI.bond_tiles(tiles, sigma, omega, members=members, agent_exposure=exposure[cur])
+
+    def step():
+        cur = it[0] & 1
+        it[0] += 1
+        main = torch.cuda.current_stream(ctx.dev) if side is not None else None
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                liability_stage(cur)
+        stats.zero_()
+        agents = torch.randint(0, A_, (S,), device=ctx.dev, dtype=i32, generator=gen)
+        eng.run_pipeline(S, agents=agents, stats=stats)
+        if side is None:
+            liability_stage(cur)
+        else:
+            main.wait_stream(side)
         comm[cur].launch(exchange, exposure[cur])  # X01 over RCCL / xGMI, overlapped
         X.allreduce_stats(stats)
 
