@@ -263,16 +263,31 @@ def config5(ctx: Ctx, args):
         "suf_len": one["suf_len"].repeat(chains_n).to(ctx.dev),
     }
     leaves_offs = packed["chain_offsets"]
+    # P03: the audit stage (re-chain + Merkle: SHA-issue-bound, fills the GPU) and the
+    # liability stage (slash cascade + σ_eff: latency-bound CSR walks) are
+    # independent, so they run on two streams and share the CUs
+    side = torch.cuda.Stream(ctx.dev) if ctx.dev.type == "cuda" else None
+
+    def audit_stage():
+        digests = A.chain_hashes(packed)
+        A.merkle_roots(leaves_offs, digests)
 
     def step():
+        main = torch.cuda.current_stream(ctx.dev) if side is not None else None
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                audit_stage()
         # fresh storm state: the slash mutates only `active`, `released_us` and the
         # scores, so only those are reset (the CSR topology and bonds are shared)
         vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, vb0.active.clone(),
                            vb0.expiry_us, vb0.released_us.clone())
         out = LI.slash(vb, tgt, omega, scores0.clone(), 1, clip_cap=per)  # ≤ one clip per edge
         se = LI.sigma_eff_exact(vb, out.scores, omega, 1)  # NaN (absent) reads as 0.0
-        digests = A.chain_hashes(packed)
-        A.merkle_roots(leaves_offs, digests)
+        if side is None:
+            audit_stage()
+        else:
+            main.wait_stream(side)
         return se
 
     el, lat = ctx.timed(step, args.steps, args.warmup)
