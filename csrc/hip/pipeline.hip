@@ -106,6 +106,28 @@ __global__ void pipeline_advance_kernel(int64_t* cursor, int64_t n, int64_t capa
 
 __global__ void wall_clock_kernel(int64_t* out) { *out = static_cast<int64_t>(wall_clock64()); }
 
+// Spread-counter fold: one wave, lane = spread row.  Each row is read and zeroed
+// in place (the next launch starts from zero without a fill), summed across the
+// wave and added (or copied) into out[k].  One launch instead of zero + reduce + add.
+__global__ __launch_bounds__(kWaveLanes) void spread_fold_kernel(unsigned long long* spread, unsigned long long* out,
+                                                                 int k, int accumulate) {
+  static_assert(kStatSpread == kWaveLanes, "one spread row per lane");
+  const int lane = threadIdx.x;
+  for (int j = 0; j < k; ++j) {
+    unsigned long long v = spread[lane * k + j];
+    spread[lane * k + j] = 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWaveLanes);
+    if (lane == 0) out[j] = accumulate ? out[j] + v : v;
+  }
+}
+
+void launch_spread_fold(unsigned long long* spread, unsigned long long* out, int k, bool accumulate, hipStream_t s) {
+  if (k <= 0 || k > 64) throw std::invalid_argument("spread fold: k out of range");
+  hipLaunchKernelGGL(spread_fold_kernel, dim3(1), dim3(kWaveLanes), 0, s, spread, out, k, accumulate ? 1 : 0);
+  check_hip(hipGetLastError(), "spread_fold_kernel");
+}
+
 void launch_pipeline_clock(int64_t* cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz, hipStream_t s) {
   if (rate_khz <= 0) throw std::invalid_argument("wall clock rate must be positive");
   hipLaunchKernelGGL(pipeline_clock_kernel, dim3(1), dim3(1), 0, s, cursor, base_us, base_clk, rate_khz);

@@ -337,6 +337,14 @@ void register_kernels(py::module_& m) {
       },
       py::arg("args"), "Run the same per-session pipeline body on the CPU (host twin).");
   m.def(
+      "spread_fold",
+      [](uintptr_t spread, uintptr_t out, int k, bool accumulate, uintptr_t stream) {
+        launch_spread_fold(reinterpret_cast<unsigned long long*>(spread), reinterpret_cast<unsigned long long*>(out), k,
+                           accumulate, reinterpret_cast<hipStream_t>(stream));
+      },
+      py::arg("spread"), py::arg("out"), py::arg("k"), py::arg("accumulate"), py::arg("stream"),
+      "Fold [64, k] spread counters into out[k] (add or copy) and zero them, on `stream`.");
+  m.def(
       "pipeline_clock",
       [](uintptr_t cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz, uintptr_t stream) {
         launch_pipeline_clock(reinterpret_cast<int64_t*>(cursor), base_us, base_clk, rate_khz,

@@ -19,6 +19,9 @@ struct PipelineArgs;
 void launch_pipeline(const PipelineArgs& a, hipStream_t stream);
 void pipeline_host(const PipelineArgs& a);
 
+// Fold [kStatSpread, k] spread counters into out[k] and re-zero them (one wave).
+void launch_spread_fold(unsigned long long* spread, unsigned long long* out, int k, bool accumulate, hipStream_t s);
+
 // Device time base and cursor maintenance for graph-captured pipelines (N07/N09).
 // cursor = int64[3] {slot_base, id_base, now_us}.
 void launch_pipeline_clock(int64_t* cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz, hipStream_t s);

@@ -296,3 +296,22 @@ def test_session_kernels(cuda_device):
     _check(lambda *t: SE.lock_conflicts(*t), roffs, torch.randint(0, 30, (Lk,), dtype=i32, generator=g),
            torch.randint(0, 3, (Lk,), dtype=u8, generator=g), torch.randint(0, R_, (m,), dtype=i32, generator=g),
            torch.randint(0, 30, (m,), dtype=i32, generator=g), torch.randint(0, 3, (m,), dtype=u8, generator=g))
+
+
+def test_spread_fold(cuda_device):
+    """Single-wave spread-counter fold: sum of the 64 rows added / copied, rows re-zeroed."""
+    from agent_hypervisor_amd.utils.stats import SpreadCounters
+
+    sc = SpreadCounters(6, cuda_device)
+    rows = torch.randint(0, 1 << 40, (64, 6), dtype=torch.int64)
+    sc.buf.copy_(rows)
+    out = torch.arange(6, dtype=torch.int64, device=cuda_device)
+    sc.add_into(out)
+    torch.cuda.synchronize()
+    assert out.cpu().tolist() == (rows.sum(0) + torch.arange(6)).tolist()
+    assert int(sc.buf.abs().sum()) == 0
+    sc.buf.copy_(rows)
+    sc.copy_into(out)
+    torch.cuda.synchronize()
+    assert out.cpu().tolist() == rows.sum(0).tolist()
+    assert int(sc.buf.abs().sum()) == 0
