@@ -11,7 +11,8 @@ X      view                                    collective
 =====  =====================================  ===============================
 X01    Σ active bonded by voucher (liability)  all_reduce(SUM) over [A] fp64
 X02    slash effects on agent σ                all_reduce(MIN) blacklist +
-                                               all_reduce(PROD) clip factors
+                                               all_reduce(PROD) clip factors,
+                                               or sparse all_gather (id, factor)
 X03    ledger risk partials                    all_reduce(SUM) fixed-point i64
 X04    job counters (stats endpoint)           all_reduce(SUM) [6] i64
 X05    earliest-session ring of an agent       all_reduce(MIN) packed i64 key
@@ -21,11 +22,14 @@ X09    latency histograms                      gather to rank 0 (all_reduce SUM)
 =====  =====================================  ===============================
 
 All functions are no-ops returning the local value when no process group is
-initialised (single rank).
+initialised (single rank).  A thread may instead install an in-process
+:class:`~agent_hypervisor_amd.parallel.fake.FakeGroup` (``fake.run_ranks``), which
+runs the same merge math over simulated ranks for unit tests.
 """
 
 from __future__ import annotations
 
+import threading
 from typing import Optional
 
 import torch
@@ -33,13 +37,34 @@ import torch.distributed as dist
 
 FIXED_POINT_SCALE = 1 << 40  # X03: risk partials as int64 fixed point
 
+_thread = threading.local()
+
+
+def set_thread_group(group) -> None:
+    """Install (or clear, with None) this thread's in-process fake communicator."""
+    _thread.group = group
+
+
+def _comm():
+    """The communicator of this thread: its fake group if one is installed, else
+    ``torch.distributed`` (same method names for the calls used here)."""
+    g = getattr(_thread, "group", None)
+    return g if g is not None else dist
+
 
 def _ready() -> bool:
+    g = getattr(_thread, "group", None)
+    if g is not None:
+        return g.get_world_size() > 1
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 def world() -> int:
-    return dist.get_world_size() if _ready() else 1
+    return _comm().get_world_size() if _ready() else 1
+
+
+def rank() -> int:
+    return _comm().get_rank() if _ready() else 0
 
 
 # -- X04 ----------------------------------------------------------------------------
@@ -65,7 +90,7 @@ def pipeline_stats(engine, batch=None) -> torch.Tensor:
 
 def allreduce_stats(stats: torch.Tensor) -> torch.Tensor:
     if _ready():
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+        _comm().all_reduce(stats, op=dist.ReduceOp.SUM)
     return stats
 
 
@@ -73,7 +98,7 @@ def allreduce_stats(stats: torch.Tensor) -> torch.Tensor:
 def allreduce_exposure(exposure: torch.Tensor) -> torch.Tensor:
     """Σ active bonded amount per voucher over every rank's sessions ([A] fp64)."""
     if _ready():
-        dist.all_reduce(exposure, op=dist.ReduceOp.SUM)
+        _comm().all_reduce(exposure, op=dist.ReduceOp.SUM)
     return exposure
 
 
@@ -91,11 +116,68 @@ def merge_slash_effects(
     bl = blacklist.to(torch.int32).clone()
     cf = clip_factor.clone()
     if _ready():
-        dist.all_reduce(bl, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cf, op=dist.ReduceOp.PRODUCT)
+        _comm().all_reduce(bl, op=dist.ReduceOp.MAX)
+        _comm().all_reduce(cf, op=dist.ReduceOp.PRODUCT)
     touched = cf < 1.0
     out = torch.where(touched, torch.clamp(sigma * cf, min=floor), sigma)
     return torch.where(bl > 0, torch.zeros_like(out), out)
+
+
+def merge_slash_sparse(
+    sigma: torch.Tensor, blacklist_ids: torch.Tensor, clip_ids: torch.Tensor, clip_factors: torch.Tensor,
+    floor: float = 0.05,
+) -> torch.Tensor:
+    """Sparse form of X02 for slash storms that touch few agents.
+
+    Each rank contributes only the agents it slashed — ``blacklist_ids`` (int32) and
+    ``(clip_ids, clip_factors)`` pairs (int32, fp64 Π(1−ω) per rank, duplicates
+    allowed) — instead of a dense [A] vector.  The pairs are all-gathered (padded to
+    the longest rank's list) and PROD-scattered locally into a factor vector, then
+    applied with the same single floor as the dense merge, so the result is
+    identical to :func:`merge_slash_effects` on the densified inputs.  Returns the
+    merged σ (a new tensor; ``sigma`` is not modified)."""
+    dev = sigma.device
+    bl = blacklist_ids.to(device=dev, dtype=torch.int64).reshape(-1)
+    ci = clip_ids.to(device=dev, dtype=torch.int64).reshape(-1)
+    cf = clip_factors.to(device=dev, dtype=torch.float64).reshape(-1)
+    if ci.numel() != cf.numel():
+        raise ValueError("clip_ids and clip_factors must have the same length")
+    if _ready():
+        c = _comm()
+        w = c.get_world_size()
+        n = torch.tensor([bl.numel(), ci.numel()], dtype=torch.int64, device=dev)
+        sizes = [torch.zeros_like(n) for _ in range(w)]
+        c.all_gather(sizes, n)
+        mb = max(int(t[0]) for t in sizes)
+        mc = max(int(t[1]) for t in sizes)
+        pb = torch.full((max(mb, 1),), -1, dtype=torch.int64, device=dev)
+        pb[: bl.numel()] = bl
+        pi = torch.full((max(mc, 1),), -1, dtype=torch.int64, device=dev)
+        pi[: ci.numel()] = ci
+        pf = torch.ones(max(mc, 1), dtype=torch.float64, device=dev)
+        pf[: cf.numel()] = cf
+        gb = [torch.empty_like(pb) for _ in range(w)]
+        gi = [torch.empty_like(pi) for _ in range(w)]
+        gf = [torch.empty_like(pf) for _ in range(w)]
+        c.all_gather(gb, pb)
+        c.all_gather(gi, pi)
+        c.all_gather(gf, pf)
+        bl = torch.cat(gb)
+        bl = bl[bl >= 0]
+        ci = torch.cat(gi)
+        cf = torch.cat(gf)
+        keep = ci >= 0
+        ci, cf = ci[keep], cf[keep]
+    factor = torch.ones_like(sigma, dtype=torch.float64)
+    if ci.numel():
+        factor.index_reduce_(0, ci, cf, "prod")
+    touched = torch.zeros(sigma.numel(), dtype=torch.bool, device=dev)
+    touched[ci] = True
+    touched &= factor < 1.0
+    out = torch.where(touched, torch.clamp(sigma * factor, min=floor), sigma)
+    if bl.numel():
+        out[bl] = 0.0
+    return out
 
 
 # -- X03 ----------------------------------------------------------------------------
@@ -107,9 +189,9 @@ def allreduce_risk(partial_risk: torch.Tensor, counts: Optional[torch.Tensor] = 
     LiabilityLedger.compute_risk_profile."""
     fx = torch.round(partial_risk * FIXED_POINT_SCALE).to(torch.int64)
     if _ready():
-        dist.all_reduce(fx, op=dist.ReduceOp.SUM)
+        _comm().all_reduce(fx, op=dist.ReduceOp.SUM)
         if counts is not None:
-            dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+            _comm().all_reduce(counts, op=dist.ReduceOp.SUM)
     risk = (fx.to(torch.float64) / FIXED_POINT_SCALE).clamp(0.0, 1.0)
     return (risk, counts) if counts is not None else risk
 
@@ -121,7 +203,7 @@ def earliest_ring(create_seq: torch.Tensor, ring: torch.Tensor) -> torch.Tensor:
     Key = (global creation sequence << 8) | ring; the MIN key wins."""
     key = (create_seq.to(torch.int64) << 8) | ring.to(torch.int64)
     if _ready():
-        dist.all_reduce(key, op=dist.ReduceOp.MIN)
+        _comm().all_reduce(key, op=dist.ReduceOp.MIN)
     return key & 0xFF
 
 
@@ -134,9 +216,9 @@ def allgather_commitments(slots: torch.Tensor, roots: torch.Tensor, counts: torc
     if not _ready():
         r = torch.zeros_like(slots, dtype=torch.int32)
         return r, slots, roots, counts
-    w = dist.get_world_size()
+    w = _comm().get_world_size()
     sizes = [torch.zeros_like(n) for _ in range(w)]
-    dist.all_gather(sizes, n)
+    _comm().all_gather(sizes, n)
     m = int(max(int(s.item()) for s in sizes))
     rec = torch.zeros((m, 10), dtype=torch.int32, device=slots.device)
     k = slots.numel()
@@ -144,7 +226,7 @@ def allgather_commitments(slots: torch.Tensor, roots: torch.Tensor, counts: torc
     rec[:k, 1] = counts.to(torch.int32)
     rec[:k, 2:] = roots.to(torch.int32)
     out = [torch.empty_like(rec) for _ in range(w)]
-    dist.all_gather(out, rec)
+    _comm().all_gather(out, rec)
     ranks, sl, rt, ct = [], [], [], []
     for r, (sz, blk) in enumerate(zip(sizes, out)):
         c = int(sz.item())
@@ -161,10 +243,10 @@ def broadcast_invalidations(agent_ids: torch.Tensor, src: int = 0) -> torch.Tens
     if not _ready():
         return agent_ids
     n = torch.tensor([agent_ids.numel()], dtype=torch.int64, device=agent_ids.device)
-    dist.broadcast(n, src)
-    buf = agent_ids if dist.get_rank() == src else torch.empty(int(n.item()), dtype=agent_ids.dtype,
+    _comm().broadcast(n, src)
+    buf = agent_ids if _comm().get_rank() == src else torch.empty(int(n.item()), dtype=agent_ids.dtype,
                                                                device=agent_ids.device)
-    dist.broadcast(buf, src)
+    _comm().broadcast(buf, src)
     return buf
 
 
@@ -172,5 +254,5 @@ def broadcast_invalidations(agent_ids: torch.Tensor, src: int = 0) -> torch.Tens
 def reduce_histogram(hist: torch.Tensor) -> torch.Tensor:
     """Element-wise sum of per-rank latency histograms (every rank gets the total)."""
     if _ready():
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+        _comm().all_reduce(hist, op=dist.ReduceOp.SUM)
     return hist

@@ -103,6 +103,12 @@ def _collectives_worker(rank: int, world: int, port: int) -> None:
         bl = torch.tensor([0, 0, rank], dtype=torch.uint8)
         out = X.merge_slash_effects(sigma, bl, cf)
         assert out.tolist() == [pytest.approx(0.2), 0.9, 0.0]
+        # X02 sparse: the same clips as (id, factor) pairs, ragged across ranks
+        ci = torch.tensor([0] if rank == 0 else [0, 1, 1], dtype=torch.int32)
+        cfs = torch.tensor([0.5] if rank == 0 else [0.5, 0.9, 0.9], dtype=torch.float64)
+        bli = torch.tensor([] if rank == 0 else [2], dtype=torch.int32)
+        out = X.merge_slash_sparse(sigma, bli, ci, cfs)
+        assert out.tolist() == [pytest.approx(0.2), pytest.approx(0.9 * 0.81), 0.0]
         # X03 deterministic risk
         r, c = X.allreduce_risk(torch.tensor([0.15, 0.6], dtype=torch.float64),
                                 torch.tensor([1, 2], dtype=torch.int32))

@@ -1,0 +1,137 @@
+"""The X01–X10 merge math over the in-process fake-rank world.
+
+Same functions as the gloo (tests/test_distributed.py) and RCCL runs, at world
+sizes up to 8 without spawning processes; the fake group reduces in rank order,
+so every result is deterministic."""
+
+from __future__ import annotations
+
+import threading
+
+import pytest
+import torch
+
+from agent_hypervisor_amd.parallel import collectives as X
+from agent_hypervisor_amd.parallel.fake import FakeGroup, run_ranks
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_counters_exposure_histograms(world):
+    def body(rank):
+        assert X.world() == world and X.rank() == rank
+        st = X.allreduce_stats(torch.arange(6, dtype=torch.int64) * (rank + 1))
+        e = X.allreduce_exposure(torch.full((3,), 0.5, dtype=torch.float64))
+        h = X.reduce_histogram(torch.ones(4, dtype=torch.int64))
+        return st.tolist(), e.tolist(), h.tolist()
+
+    tri = world * (world + 1) // 2
+    for st, e, h in run_ranks(world, body):
+        assert st == [k * tri for k in range(6)]
+        assert e == [0.5 * world] * 3
+        assert h == [world] * 4
+
+
+def _slash_inputs(world, A=64, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    sigma = torch.rand(A, generator=g, dtype=torch.float64)
+    per_rank = []
+    for _ in range(world):
+        k = int(torch.randint(0, 12, (1,), generator=g))
+        ids = torch.randint(0, A, (k,), generator=g, dtype=torch.int32)
+        om = torch.rand(k, generator=g, dtype=torch.float64) * 0.9
+        bl = torch.randint(0, A, (int(torch.randint(0, 3, (1,), generator=g)),), generator=g, dtype=torch.int32)
+        per_rank.append((ids, 1.0 - om, bl))
+    return sigma, per_rank
+
+
+def _sequential(sigma, per_rank, floor=0.05):
+    """Every clip applied one at a time with its own floor (the scalar engine's order)."""
+    s = sigma.clone()
+    for ids, f, _ in per_rank:
+        for i, x in zip(ids.tolist(), f.tolist()):
+            s[i] = max(s[i].item() * x, floor)
+    for _, _, bl in per_rank:
+        s[bl.long()] = 0.0
+    return s
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_slash_merge_dense_and_sparse_match_sequential(world):
+    sigma, per_rank = _slash_inputs(world, seed=world)
+    want = _sequential(sigma, per_rank)
+
+    def body(rank):
+        ids, f, bl = per_rank[rank]
+        cf = torch.ones_like(sigma)
+        cf.index_reduce_(0, ids.long(), f, "prod")
+        blv = torch.zeros(sigma.numel(), dtype=torch.uint8)
+        blv[bl.long()] = 1
+        dense = X.merge_slash_effects(sigma, blv, cf)
+        sparse = X.merge_slash_sparse(sigma, bl, ids, f)
+        return dense, sparse
+
+    for dense, sparse in run_ranks(world, body):
+        torch.testing.assert_close(sparse, dense, rtol=0, atol=0)
+        torch.testing.assert_close(dense, want, rtol=1e-12, atol=1e-15)
+
+
+def test_risk_is_rank_order_independent():
+    parts = [torch.tensor([0.1 * (r + 1), 1e-9 * r, 0.3], dtype=torch.float64) for r in range(5)]
+
+    def run(order):
+        return run_ranks(5, lambda r: X.allreduce_risk(parts[order[r]]))[0]
+
+    a = run([0, 1, 2, 3, 4])
+    b = run([4, 2, 0, 3, 1])
+    assert torch.equal(a, b)
+    assert a.tolist()[2] == 1.0  # clamped after the sum
+
+
+def test_earliest_ring_commitments_broadcast():
+    world = 4
+
+    def body(rank):
+        ring = X.earliest_ring(torch.tensor([10 - rank]), torch.tensor([rank % 3]))
+        k = rank + 1
+        rk, sl, rt, ct = X.allgather_commitments(torch.arange(k, dtype=torch.int64) + 10 * rank,
+                                                 torch.full((k, 8), rank, dtype=torch.int32), torch.full((k,), 2))
+        ids = torch.tensor([4, 5], dtype=torch.int32) if rank == 1 else torch.empty(0, dtype=torch.int32)
+        b = X.broadcast_invalidations(ids, src=1)
+        return ring.tolist(), rk.tolist(), sl.tolist(), b.tolist()
+
+    for ring, rk, sl, b in run_ranks(world, body):
+        assert ring == [0]  # rank 3 created first (seq 7), ring 3 % 3 = 0
+        assert rk == [0, 1, 1, 2, 2, 2, 3, 3, 3, 3]
+        assert sl == [0, 10, 11, 20, 21, 22, 30, 31, 32, 33]
+        assert b == [4, 5]
+
+
+def test_failing_rank_does_not_deadlock():
+    def body(rank):
+        if rank == 2:
+            raise RuntimeError("rank 2 lost")
+        X.allreduce_stats(torch.zeros(6, dtype=torch.int64))
+        return rank
+
+    with pytest.raises(RuntimeError, match="rank 2 lost"):
+        run_ranks(4, body)
+    assert X.world() == 1  # the calling thread never had a fake group installed
+
+
+def test_group_is_thread_local():
+    g = FakeGroup(2)
+    seen = []
+
+    def other():
+        seen.append(X.world())
+
+    X.set_thread_group(g)
+    g._local.rank = 0
+    try:
+        t = threading.Thread(target=other)
+        t.start()
+        t.join()
+        assert X.world() == 2
+    finally:
+        X.set_thread_group(None)
+    assert seen == [1]
