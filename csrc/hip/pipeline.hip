@@ -109,21 +109,28 @@ __global__ void wall_clock_kernel(int64_t* out) { *out = static_cast<int64_t>(wa
 // Spread-counter fold: one wave, lane = spread row.  Each row is read and zeroed
 // in place (the next launch starts from zero without a fill), summed across the
 // wave and added (or copied) into out[k].  One launch instead of zero + reduce + add.
+constexpr int kMaxFold = 8;
+
 __global__ __launch_bounds__(kWaveLanes) void spread_fold_kernel(unsigned long long* spread, unsigned long long* out,
                                                                  int k, int accumulate) {
   static_assert(kStatSpread == kWaveLanes, "one spread row per lane");
   const int lane = threadIdx.x;
-  for (int j = 0; j < k; ++j) {
-    unsigned long long v = spread[lane * k + j];
+  // all loads issued before the first use: one memory latency, not k
+  unsigned long long v[kMaxFold];
+#pragma unroll
+  for (int j = 0; j < kMaxFold; ++j) v[j] = j < k ? spread[lane * k + j] : 0ull;
+#pragma unroll
+  for (int j = 0; j < kMaxFold; ++j) {
+    if (j >= k) break;
     spread[lane * k + j] = 0;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWaveLanes);
-    if (lane == 0) out[j] = accumulate ? out[j] + v : v;
+    for (int off = 32; off > 0; off >>= 1) v[j] += __shfl_xor(v[j], off, kWaveLanes);
+    if (lane == 0) out[j] = accumulate ? out[j] + v[j] : v[j];
   }
 }
 
 void launch_spread_fold(unsigned long long* spread, unsigned long long* out, int k, bool accumulate, hipStream_t s) {
-  if (k <= 0 || k > 64) throw std::invalid_argument("spread fold: k out of range");
+  if (k <= 0 || k > kMaxFold) throw std::invalid_argument("spread fold: k out of range");
   hipLaunchKernelGGL(spread_fold_kernel, dim3(1), dim3(kWaveLanes), 0, s, spread, out, k, accumulate ? 1 : 0);
   check_hip(hipGetLastError(), "spread_fold_kernel");
 }
