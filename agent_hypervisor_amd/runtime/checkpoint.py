@@ -321,6 +321,8 @@ def load_hypervisor(d: str, hv=None, verify: bool = True):
     hv = hv or Hypervisor()
     with open(os.path.join(d, "sessions.jsonl")) as f:
         records = [json.loads(line) for line in f if line.strip()]
+    if getattr(hv, "_store", None) is not None:
+        return _load_device(hv, d, records, verify)
     for r in records:
         cfg = dict(r["config"])
         cfg["consistency_mode"] = ConsistencyMode(cfg["consistency_mode"])
@@ -380,4 +382,189 @@ def load_hypervisor(d: str, hv=None, verify: bool = True):
                 complete = de is not None and de.deltas and len(de.deltas) == de.turn_count  # nothing pruned by GC
                 if complete and de.compute_merkle_root() != rec.merkle_root:
                     raise CheckpointError(f"session {rec.session_id}: Merkle root differs from its commitment")
+    return hv
+
+
+def _load_device(hv, d: str, records: list, verify: bool):
+    """Restore into a device-backed hypervisor: rows are scattered straight into
+    the store tables (one bulk tensor write per column), the canonical-JSON audit
+    records into the payload arena, and the device then re-verifies every chain
+    (K10 over the restored records) and every Merkle root against its commitment
+    (K09)."""
+    from hypervisor import _device
+    from hypervisor._clock import to_us
+    from hypervisor.core import ManagedSession
+    from hypervisor.models import (
+        ActionDescriptor,
+        ConsistencyMode,
+        ExecutionRing,
+        ReversibilityLevel,
+        SessionConfig,
+        SessionState,
+    )
+    from hypervisor.saga.state_machine import SagaState, StepState
+
+    st = hv._store
+    P = st.caps["P"]
+    rows: dict = {}
+
+    def put(col, i, v):
+        ix, vs = rows.setdefault(col, ([], []))
+        ix.append(i)
+        vs.append(v)
+
+    def us(t):
+        return to_us(_dt(t)) if t else 0
+
+    with open(os.path.join(d, "commitments.json")) as f:
+        commits = {c["session_id"]: c for c in json.load(f)}
+    sess_list = []
+    for r in records:
+        cfg = dict(r["config"])
+        cfg["consistency_mode"] = ConsistencyMode(cfg["consistency_mode"])
+        config = SessionConfig(**cfg)
+        sso = _device.DeviceSession(st, config, r["creator_did"], session_id=r["session_id"], create=False)
+        s = sso.slot
+        modes = {ConsistencyMode.EVENTUAL: 0, ConsistencyMode.STRONG: 1}
+        for col, v in (
+            ("s_state", list(SessionState).index(SessionState(r["state"]))),
+            ("s_mode", modes[ConsistencyMode(r["consistency_mode"])]),
+            ("s_audit", int(bool(config.enable_audit))), ("s_maxpart", int(config.max_participants)),
+            ("s_minsig", float(config.min_sigma_eff)), ("s_creator", st.agent_id(r["creator_did"])),
+            ("s_created", us(r["created_at"])), ("s_terminated", us(r["terminated_at"])),
+            ("s_pcount", len(r["participants"])), ("s_pactive", sum(1 for p in r["participants"] if p["is_active"])),
+            ("s_dcount", len(r["audit"])), ("s_released", 0), ("s_retained", 0),
+        ):
+            put(col, s, v)
+        if len(r["participants"]) > P:
+            raise CheckpointError(f"session {r['session_id']}: more participants than the store's row width {P}")
+        for k, p in enumerate(r["participants"]):
+            row = s * P + k
+            put("p_agent", row, st.agent_id(p["agent_did"]))
+            put("p_ring", row, int(p["ring"]))
+            put("p_active", row, int(bool(p["is_active"])))
+            put("p_sraw", row, float(p["sigma_raw"]))
+            put("p_seff", row, float(p["sigma_eff"]))
+            put("p_joined", row, us(p["joined_at"]))
+        de = _device.DeviceDeltaEngine(st, s, r["session_id"])
+        prev_idx, prev_view = -1, None
+        for rec in r["audit"]:
+            payload = rec["payload"].encode()
+            if hashlib.sha256(payload).hexdigest() != rec["delta_hash"]:
+                raise CheckpointError(f"session {r['session_id']}: stored hash does not match its payload")
+            p = json.loads(payload)
+            didx = st.alloc_delta()
+            off = st.payload_append(payload)
+            ts = datetime.fromisoformat(p["timestamp"])
+            from hypervisor.audit.delta import VFSChange
+
+            changes = [VFSChange(path=c["path"], operation=c["operation"], content_hash=c["content_hash"],
+                                 previous_hash=c["previous_hash"]) for c in p["changes"]]
+            view = _device.DeviceDelta(de, p["delta_id"], p["turn_id"], p["session_id"], p["agent_did"], ts, changes,
+                                       prev_view)
+            view.__dict__.update(_didx=didx, _poff=off, _plen=len(payload), _dev_hash=rec["delta_hash"])
+            if p["parent_hash"] != (prev_view.device_hash() if prev_view is not None else None):
+                view.parent_hash = p["parent_hash"]  # keep what the record says; verify will flag it
+            words = [int(rec["delta_hash"][8 * k: 8 * k + 8], 16) for k in range(8)]
+            for col, v in (("d_sess", s), ("d_turn", int(p["turn_id"])), ("d_prev", prev_idx), ("d_ts", to_us(ts)),
+                           ("d_off", off), ("d_len", len(payload))):
+                put(col, didx, v)
+            for k, w in enumerate(words):
+                put("d_hash", 8 * didx + k, w)
+            de._deltas.append(view)
+            prev_idx, prev_view = didx, view
+        de._turn_counter = r["turn_count"]
+        put("s_dlast", s, prev_idx)
+        if prev_view is not None:
+            for k, w in enumerate(_device._words(prev_view.device_hash())):
+                put("s_head", 8 * s + k, w)
+        c = commits.get(r["session_id"])
+        if c is not None:
+            put("s_committed", s, us(c["committed_at"]))
+            put("s_commit_n", s, int(c["delta_count"]))
+            for k, w in enumerate(_device._words(c["merkle_root"])):
+                put("s_root", 8 * s + k, w)
+            hv.commitment.register(sso)
+        saga_orch = _device.DeviceSagaOrchestrator(st)
+        for g in r["sagas"]:
+            gslot = st.alloc("G")
+            saga = _device.DeviceSaga(st, gslot, g["saga_id"], g["session_id"])
+            saga.error = g["error"]
+            put("g_state", gslot, list(SagaState).index(SagaState(g["state"])))
+            put("g_created", gslot, us(g["created_at"]))
+            put("g_completed", gslot, us(g["completed_at"]))
+            put("g_nsteps", gslot, len(g["steps"]))
+            for sd in g["steps"]:
+                tslot = st.alloc("T")
+                step = _device.DeviceSagaStep(
+                    st, tslot, step_id=sd["step_id"], action_id=sd["action_id"], agent_did=sd["agent_did"],
+                    execute_api=sd["execute_api"], undo_api=sd["undo_api"], timeout_seconds=sd["timeout_seconds"],
+                    max_retries=sd["max_retries"])
+                step.__dict__.update(execute_result=sd["execute_result"],
+                                     compensation_result=sd["compensation_result"], error=sd["error"])
+                for col, v in (("t_saga", gslot), ("t_state", list(StepState).index(StepState(sd["state"]))),
+                               ("t_undo", int(bool(sd["undo_api"]))), ("t_started", us(sd["started_at"])),
+                               ("t_completed", us(sd["completed_at"])), ("t_retry", int(sd["retry_count"])),
+                               ("t_maxretry", int(sd["max_retries"]))):
+                    put(col, tslot, v)
+                saga.steps.append(step)
+            saga_orch._sagas[saga.saga_id] = saga
+        m = ManagedSession(sso, de, saga_orch)
+        for e in r["reversibility"]:
+            m.reversibility.register(ActionDescriptor(
+                action_id=e["action_id"], name=e["action_id"], execute_api=e["execute_api"], undo_api=e["undo_api"],
+                reversibility=ReversibilityLevel(e["reversibility"]), undo_window_seconds=e["undo_window_seconds"],
+                compensation_method=e["compensation_method"]))
+            if not e["undo_api_healthy"]:
+                m.reversibility.mark_undo_unhealthy(e["action_id"])
+        sso.vfs._files = dict(r["vfs"]["files"])
+        sso.vfs._permissions = {k: set(v) for k, v in r["vfs"]["permissions"].items()}
+        hv._sessions[sso.session_id] = m
+        sess_list.append(m)
+    # vouch bonds: edges in creation order, linked per liability session
+    ve = hv.vouching
+    tails: dict = {}
+    with open(os.path.join(d, "liability.json")) as f:
+        vouches = json.load(f)
+    for v in vouches:
+        vs = st.liability_id(ve._tenant, v["session_id"])
+        e = st.alloc("E")
+        for col, val in (("e_voucher", st.agent_id(v["voucher_did"])), ("e_vouchee", st.agent_id(v["vouchee_did"])),
+                         ("e_vsess", vs), ("e_next", -1), ("e_active", int(bool(v["is_active"]))),
+                         ("e_bonded", float(v["bonded_amount"])), ("e_pct", float(v["bonded_sigma_pct"])),
+                         ("e_expiry", us(v["expiry"]) if v["expiry"] else -1),
+                         ("e_released", us(v["released_at"]) if v["released_at"] else -1),
+                         ("e_created", us(v["created_at"]))):
+            put(col, e, val)
+        if vs in tails:
+            put("e_next", tails[vs], e)
+        else:
+            put("v_head", vs, e)
+        tails[vs] = e
+        put("v_tail", vs, e)
+        rec = _device.DeviceVouchRecord(st, e, v["vouch_id"], v["voucher_did"], v["vouchee_did"], v["session_id"],
+                                        v["bonded_sigma_pct"], v["bonded_amount"], _dt(v["created_at"]),
+                                        _dt(v["expiry"]))
+        ve._by_id[rec.vouch_id] = rec
+        ve._by_edge[e] = rec
+        ve._order.append(rec)
+    # later writes to one index win (e_next of an edge that gained a successor)
+    st.write_rows(rows)
+    for sid, c in commits.items():
+        if hv.get_session(sid) is None:
+            from hypervisor.audit.commitment import CommitmentRecord
+
+            hv.commitment._commitments[sid] = CommitmentRecord(
+                session_id=sid, merkle_root=c["merkle_root"], participant_dids=c["participant_dids"],
+                delta_count=c["delta_count"], committed_at=_dt(c["committed_at"]),
+                blockchain_tx_id=c["blockchain_tx_id"], committed_to=c["committed_to"])
+    if verify:
+        for m in sess_list:
+            de = m.delta_engine
+            if not de.verify_chain():  # K10 on the device over the restored records
+                raise CheckpointError(f"session {m.sso.session_id}: audit chain fails verification")
+            c = commits.get(m.sso.session_id)
+            complete = de.deltas and len(de.deltas) == de.turn_count
+            if c is not None and complete and de.compute_merkle_root() != c["merkle_root"]:
+                raise CheckpointError(f"session {m.sso.session_id}: Merkle root differs from its commitment")
     return hv

@@ -97,12 +97,46 @@ def _compile_cmd(src: Path, obj: Path) -> list[str]:
         "-Wno-unused-command-line-argument",
         "-DPYBIND11_DETAILED_ERROR_MESSAGES",
         *_includes(),
+        "-MMD",
+        "-MF",
+        str(obj.with_suffix(".d")),
         "-c",
         str(src),
         "-o",
         str(obj),
     ]
     return cmd
+
+
+def _deps(obj: Path) -> list[Path] | None:
+    """Headers an object was compiled from (its -MMD depfile), or None if unknown."""
+    d = obj.with_suffix(".d")
+    if not d.exists():
+        return None
+    text = d.read_text().replace("\\\n", " ")
+    out = []
+    for tok in text.split(":", 1)[-1].split():
+        if tok.endswith((".h", ".hpp", ".cuh", ".inc")):
+            out.append(Path(tok))
+    return out
+
+
+def _stale(src: Path, obj: Path) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    if src.stat().st_mtime > t or Path(__file__).stat().st_mtime > t:
+        return True
+    deps = _deps(obj)
+    if deps is None:
+        return _headers_mtime() > t
+    for h in deps:
+        try:
+            if h.stat().st_mtime > t:
+                return True
+        except FileNotFoundError:
+            return True
+    return False
 
 
 def _link_cmd(objs: list[Path], out: Path) -> list[str]:
@@ -126,9 +160,13 @@ def needs_build() -> bool:
     if not out.exists():
         return True
     t = out.stat().st_mtime
-    if _headers_mtime() > t:
-        return True
-    return any(s.stat().st_mtime > t for s in _sources())
+    if not BUILD.exists():  # fresh checkout with a shipped .so: trust it unless sources are newer
+        return _headers_mtime() > t or any(s.stat().st_mtime > t for s in _sources())
+    for s in _sources():
+        o = BUILD / (s.parent.name + "_" + s.stem + ".o")
+        if _stale(s, o) or (o.exists() and o.stat().st_mtime > t):
+            return True
+    return False
 
 
 def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
@@ -140,14 +178,13 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         if clean:
             for o in BUILD.glob("*.o"):
                 o.unlink()
-        hdr_t = _headers_mtime()
         srcs = _sources()
         todo: list[tuple[Path, Path]] = []
         objs: list[Path] = []
         for s in srcs:
             o = BUILD / (s.parent.name + "_" + s.stem + ".o")
             objs.append(o)
-            if not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr_t):
+            if _stale(s, o):
                 todo.append((s, o))
         jobs = jobs or min(len(todo) or 1, int(os.environ.get("MAX_JOBS", "8")), 16)
         t0 = time.time()

@@ -52,6 +52,11 @@ _STAGES = (
     ("hypervisor.core", "Hypervisor", "verify_behavior", "hypervisor.verify_behavior"),
     ("hypervisor.saga.orchestrator", "SagaOrchestrator", "execute_step", "saga.execute_step"),
     ("hypervisor.saga.orchestrator", "SagaOrchestrator", "compensate", "saga.compensate"),
+    ("hypervisor._device", "DeviceSagaOrchestrator", "execute_step", "saga.execute_step"),
+    ("hypervisor._device", "DeviceSagaOrchestrator", "compensate", "saga.compensate"),
+    ("hypervisor._device", "DeviceDeltaEngine", "capture", "audit.capture"),
+    ("hypervisor._device", "DeviceDeltaEngine", "verify_chain", "audit.verify_chain"),
+    ("hypervisor._device", "DeviceSlashingEngine", "slash", "liability.slash"),
     ("agent_hypervisor_amd.models.engine", "GovernanceEngine", "run_pipeline", "engine.run_pipeline"),
     ("agent_hypervisor_amd.models.saga_engine", "SagaBatchEngine", "run", "saga_engine.run"),
     ("agent_hypervisor_amd.models.saga_engine", "SagaBatchEngine", "run_step_loop", "saga_engine.run_step_loop"),

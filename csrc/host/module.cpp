@@ -14,6 +14,7 @@ void register_audit(py::module_& m);
 void register_runtime(py::module_& m);
 void register_kernels(py::module_& m);
 void register_comm(py::module_& m);
+void register_store(py::module_& m);
 }  // namespace host
 }  // namespace ahv
 
@@ -24,4 +25,5 @@ PYBIND11_MODULE(_C, m) {
   ahv::host::register_runtime(m);
   ahv::host::register_kernels(m);
   ahv::host::register_comm(m);
+  ahv::host::register_store(m);
 }

@@ -210,12 +210,16 @@ static int utc_isoformat(PyObject* dt, char* out) {
 // Render the canonical payload of a SemanticDelta-like object.  Returns false
 // (without a Python error set) when a field has a type json.dumps would render
 // differently than this fast path; raises on attribute errors.
-static bool render_delta(PyObject* d, std::string& out) {
+//
+// With `null_parent_at` set, `parent_hash` is not read: the payload is rendered
+// with a `null` parent and the byte offset of that `null` is stored, so the
+// device store can splice the chain head's digest in (csrc/host/py_store.cpp).
+bool render_delta(PyObject* d, std::string& out, size_t* null_parent_at = nullptr) {
   Names* nm = names();
   Ref agent(PyObject_GetAttr(d, nm->agent_did));
   Ref changes(PyObject_GetAttr(d, nm->changes));
   Ref delta_id(PyObject_GetAttr(d, nm->delta_id));
-  Ref parent(PyObject_GetAttr(d, nm->parent_hash));
+  Ref parent(null_parent_at ? (Py_INCREF(Py_None), Py_None) : PyObject_GetAttr(d, nm->parent_hash));
   Ref session(PyObject_GetAttr(d, nm->session_id));
   Ref ts(PyObject_GetAttr(d, nm->timestamp));
   Ref turn(PyObject_GetAttr(d, nm->turn_id));
@@ -261,6 +265,7 @@ static bool render_delta(PyObject* d, std::string& out) {
   out.append(canon::K_DELTA_ID);
   if (!append_json_opt_str(out, delta_id.p)) return false;
   out.append(canon::K_PARENT);
+  if (null_parent_at) *null_parent_at = out.size();
   if (!append_json_opt_str(out, parent.p)) return false;
   out.append(canon::K_SESSION);
   if (!append_json_opt_str(out, session.p)) return false;

@@ -1,0 +1,1402 @@
+// Device-authoritative governance state store and its command
+// processor, written once for the gfx950 worker and the CPU twin.
+//
+// The public `Hypervisor` API (reference core.py:69-227, liability/vouching.py:
+// 61-184, liability/slashing.py:63-143, audit/delta.py:85-152, saga/
+// state_machine.py + orchestrator.py) runs as a stream of small commands against
+// SoA tables resident in HBM:
+//
+//   sessions   lifecycle state, config, participant rows (ring, σ_raw, σ_eff),
+//              audit chain head, Merkle root, commitment, GC/bond counters
+//   deltas     arena of audit deltas (session, turn, parent link, timestamp,
+//              SHA-256 digest, canonical-JSON payload bytes = the on-disk record)
+//   vouches    bond edges in creation order, linked per liability session
+//   sagas/steps  saga and step FSM rows (K13), timestamps, retry counters
+//
+// A command is one 512-byte slot (64 little-endian u64 words) in a ring the
+// host writes through the PCIe BAR (fine-grained device memory); a resident
+// single-wave worker (csrc/hip/store_worker.hip) polls the ring, executes the
+// command with `store_exec` and writes a 512-byte result slot into pinned host
+// memory.  The host twin (csrc/host/py_store.cpp, device='cpu') calls
+// `store_exec` directly on host-memory tables, so one body defines the
+// semantics for both.  Strings never reach the device: DIDs and session ids are
+// interned ids, error texts are formatted on the host from returned codes.
+//
+// Slot layout:  w[0] seq (written last), w[1] op, w[2] checksum (xor of w[1],
+// w[3..63]), w[3..15] = a[0..12] scalar args, w[16..63] = 384 inline payload
+// bytes (index lists, score pairs).  Larger variable data lives in the staging
+// area (fine-grained device memory), addressed by (offset, length) args.
+#pragma once
+
+#include "ahv/hd.h"
+#include "ahv/semantics.h"
+#include "ahv/sha256.h"
+
+namespace ahv {
+namespace store {
+
+constexpr int kSlotWords = 64;
+constexpr int kArgs = 13;
+constexpr int kInlineWords = 48;  // w[16..63]
+constexpr int kResWords = 64;     // result slot: r[0] seq, r[1] status, r[2..63] values
+
+enum Op : uint32_t {
+  OP_NOP = 0,
+  OP_STOP = 1,
+  OP_FLUSH = 2,    // release: make table writes visible to other agents (torch, kernels)
+  OP_ACQUIRE = 3,  // acquire: see rows other kernels wrote (batched pipeline)
+
+  OP_SESS_CREATE = 10,
+  OP_SESS_JOIN = 11,
+  OP_SESS_LEAVE = 12,
+  OP_SESS_ACTIVATE = 13,
+  OP_SESS_TERMINATE = 14,
+  OP_SESS_ARCHIVE = 15,
+  OP_SESS_UPDATE_RING = 16,
+  OP_SESS_SET_MODE = 17,
+  OP_SESS_READ = 18,
+  OP_SESS_SET_SIGMA = 19,
+  OP_SESS_CLOSE = 20,  // Hypervisor.terminate_session: terminate+root+commit+release+GC+archive
+  OP_SESS_HANDSHAKE = 21,
+
+  OP_DELTA_CAPTURE = 30,
+  OP_DELTA_MERKLE = 31,
+  OP_DELTA_VERIFY = 32,
+  OP_DELTA_READ = 33,
+
+  OP_VOUCH = 40,
+  OP_SIGMA_EFF = 41,
+  OP_EXPOSURE = 42,
+  OP_RELEASE_BOND = 43,
+  OP_RELEASE_SESSION = 44,
+  OP_VOUCH_LIST = 45,
+  OP_EDGE_READ = 46,
+  OP_SLASH = 47,
+
+  OP_SAGA_CREATE = 60,
+  OP_STEP_ADD = 61,
+  OP_STEP_TRANSITION = 62,
+  OP_STEP_SET = 63,
+  OP_SAGA_TRANSITION = 64,
+  OP_SAGA_READ = 65,
+  OP_SAGA_PLAN = 66,
+  OP_STEP_READ = 67,
+};
+
+// Status codes in r[1] (0 = ok).  Op-specific codes are small positive ints.
+enum Status : uint64_t {
+  ST_OK = 0,
+  ST_BAD_STATE = 1,
+  ST_NOT_FOUND = 2,
+  ST_BAD_ARG = 90,
+  ST_SCRATCH = 91,   // scratch too small for this request
+  ST_BAD_OP = 99,
+};
+
+// Vouch rejection codes (VouchingEngine.vouch check order).
+enum VouchCode : uint64_t { V_OK = 0, V_SELF = 1, V_LOW_SIGMA = 2, V_CYCLE = 3, V_EXPOSURE = 4, V_FULL = 5 };
+
+// Join codes extend semantics.h JoinCode.
+constexpr uint64_t JOIN_ROWS = 5;  // participant row table exhausted
+
+// --------------------------------------------------------------- tables
+
+// X-macro: (name, element type, extent) where extent names a capacity:
+// S sessions, SP session×participant rows, S8/S4 session×digest/uuid words,
+// D deltas, D8 delta×digest words, E vouch edges, V liability sessions,
+// G sagas, T steps, SCR scratch bytes (cap X).
+#define AHV_STORE_COLUMNS(X)       \
+  X(s_state, uint8_t, S)           \
+  X(s_mode, uint8_t, S)            \
+  X(s_audit, uint8_t, S)           \
+  X(s_maxpart, int32_t, S)         \
+  X(s_minsig, double, S)           \
+  X(s_creator, int32_t, S)         \
+  X(s_created, int64_t, S)         \
+  X(s_terminated, int64_t, S)      \
+  X(s_pcount, int32_t, S)          \
+  X(s_pactive, int32_t, S)         \
+  X(s_dcount, int32_t, S)          \
+  X(s_dlast, int32_t, S)           \
+  X(s_committed, int64_t, S)       \
+  X(s_commit_n, int32_t, S)        \
+  X(s_released, int32_t, S)        \
+  X(s_retained, int32_t, S)        \
+  X(s_uuid, uint32_t, S4)          \
+  X(s_head, uint32_t, S8)          \
+  X(s_root, uint32_t, S8)          \
+  X(p_agent, int32_t, SP)          \
+  X(p_ring, uint8_t, SP)           \
+  X(p_active, uint8_t, SP)         \
+  X(p_sraw, double, SP)            \
+  X(p_seff, double, SP)            \
+  X(p_joined, int64_t, SP)         \
+  X(d_sess, int32_t, D)            \
+  X(d_turn, int32_t, D)            \
+  X(d_prev, int32_t, D)            \
+  X(d_ts, int64_t, D)              \
+  X(d_off, int64_t, D)             \
+  X(d_len, int32_t, D)             \
+  X(d_hash, uint32_t, D8)          \
+  X(e_voucher, int32_t, E)         \
+  X(e_vouchee, int32_t, E)         \
+  X(e_vsess, int32_t, E)           \
+  X(e_next, int32_t, E)            \
+  X(e_active, uint8_t, E)          \
+  X(e_bonded, double, E)           \
+  X(e_pct, double, E)              \
+  X(e_expiry, int64_t, E)          \
+  X(e_released, int64_t, E)        \
+  X(e_created, int64_t, E)         \
+  X(v_head, int32_t, V)            \
+  X(v_tail, int32_t, V)            \
+  X(g_state, uint8_t, G)           \
+  X(g_created, int64_t, G)         \
+  X(g_completed, int64_t, G)       \
+  X(g_nsteps, int32_t, G)          \
+  X(t_saga, int32_t, T)            \
+  X(t_state, uint8_t, T)           \
+  X(t_undo, uint8_t, T)            \
+  X(t_started, int64_t, T)         \
+  X(t_completed, int64_t, T)       \
+  X(t_retry, int32_t, T)           \
+  X(t_maxretry, int32_t, T)        \
+  X(scratch, uint8_t, SCR)
+
+struct Caps {
+  int64_t S, P, D, E, V, G, T, X, B;  // B = payload arena bytes
+};
+
+struct Tables {
+#define AHV_DECL(name, type, ext) type* name;
+  AHV_STORE_COLUMNS(AHV_DECL)
+#undef AHV_DECL
+  uint8_t* payload;  // [B] canonical-JSON audit records (fine-grained device memory)
+  const uint8_t* staging;  // host-written variable-length inputs
+  Caps cap;
+};
+
+// ------------------------------------------------------ execution context
+
+// SIMT context: the worker runs one wave (lane 0..63); the host twin is one lane.
+// `lds` is a word buffer in LDS on the device (a thread-local array on the host)
+// used to stage audit payloads as big-endian SHA message words.
+constexpr int kLdsWords = 4096;  // 16 KiB: payloads up to 16 KiB − 72 B hash from LDS
+
+struct Lanes {
+  int lane;
+  int n;
+  uint32_t* lds;
+  AHV_HD bool leader() const { return lane == 0; }
+  AHV_HD void sync() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __syncthreads();
+#endif
+  }
+};
+
+// Result / bulk-output stores.  On the device these land in pinned host memory,
+// so they are system-scope stores (vector stores that bypass the caches).
+AHV_HD void out64(uint64_t* p, uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  *p = v;
+#endif
+}
+
+// Loads of host-written fine-grained memory (payload arena, staging area): the
+// host writes these bytes through the BAR between commands, so the device must
+// not serve them from a cache line it filled earlier — system-scope loads bypass
+// L1/L2 (one round trip to HBM each; they are issued in parallel).
+AHV_HD uint32_t ld32f(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __hip_atomic_load(static_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  return *static_cast<const uint32_t*>(p);
+#endif
+}
+AHV_HD uint64_t ld64f(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __hip_atomic_load(static_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  return *static_cast<const uint64_t*>(p);
+#endif
+}
+
+AHV_HD uint64_t dbits(double d) {
+  union { double d; uint64_t u; } x;
+  x.d = d;
+  return x.u;
+}
+AHV_HD double bitsd(uint64_t u) {
+  union { double d; uint64_t u; } x;
+  x.u = u;
+  return x.d;
+}
+
+struct Cmd {
+  uint32_t op;
+  uint64_t a[kArgs];
+  const uint64_t* inl;  // inline payload words (kInlineWords)
+};
+
+// Broadcast a value from lane 0 (device: readfirstlane-style shuffle).
+template <class T>
+AHV_HD T bcast(const Lanes& L, T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (sizeof(T) == 8) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    u = __shfl(u, 0);
+    T r;
+    __builtin_memcpy(&r, &u, 8);
+    return r;
+  } else {
+    return static_cast<T>(__shfl(static_cast<int>(v), 0));
+  }
+#else
+  (void)L;
+  return v;
+#endif
+}
+
+// ------------------------------------------------------------- helpers
+
+AHV_HD void load8(const uint32_t* src, uint32_t d[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] = src[k];
+}
+AHV_HD void store8(uint32_t* dst, const uint32_t d[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dst[k] = d[k];
+}
+
+// SHA-256 of `n` bytes at `p` (any alignment) on one lane; big-endian word
+// assembly four bytes at a time.
+AHV_HD void sha256_mem(const uint8_t* p, uint64_t n, uint32_t out[8]) {
+  sha256_init(out);
+  uint32_t blk[16];
+  uint64_t i = 0;
+  while (n - i >= 64) {
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const uint8_t* q = p + i + 4 * w;
+      blk[w] = (uint32_t(q[0]) << 24) | (uint32_t(q[1]) << 16) | (uint32_t(q[2]) << 8) | uint32_t(q[3]);
+    }
+    sha256_compress(out, blk);
+    i += 64;
+  }
+  // tail + padding (one or two blocks)
+  uint8_t tail[128];
+  const uint64_t r = n - i;
+  for (uint64_t k = 0; k < r; ++k) tail[k] = p[i + k];
+  tail[r] = 0x80;
+  const uint64_t padded = (r + 9 <= 64) ? 64 : 128;
+  for (uint64_t k = r + 1; k < padded; ++k) tail[k] = 0;
+  const uint64_t bits = n * 8;
+  for (int k = 0; k < 8; ++k) tail[padded - 1 - k] = static_cast<uint8_t>(bits >> (8 * k));
+  for (uint64_t b = 0; b < padded; b += 64) {
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const uint8_t* q = tail + b + 4 * w;
+      blk[w] = (uint32_t(q[0]) << 24) | (uint32_t(q[1]) << 16) | (uint32_t(q[2]) << 8) | uint32_t(q[3]);
+    }
+    sha256_compress(out, blk);
+  }
+}
+
+// SHA-256 of `n` bytes of fine-grained memory at 4-byte-aligned `p`.
+AHV_HD void sha256_fine(const uint8_t* p, uint64_t n, uint32_t out[8]) {
+  sha256_init(out);
+  uint32_t blk[16];
+  const uint64_t nblk = (n + 9 + 63) / 64;
+  for (uint64_t b = 0; b < nblk; ++b) {
+    for (int w = 0; w < 16; ++w) {
+      const uint64_t o = 64 * b + 4 * w;
+      uint32_t x = 0;
+      if (o + 4 <= n) {
+        x = bswap32(ld32f(p + o));
+      } else if (o < n) {
+        x = bswap32(ld32f(p + o)) & (0xffffffffu << (8 * (4 - (n - o))));
+      }
+      if (o <= n && n < o + 4) x |= 0x80u << (8 * (3 - (n - o)));
+      if (b == nblk - 1 && w == 14) x |= static_cast<uint32_t>((n * 8) >> 32);
+      if (b == nblk - 1 && w == 15) x |= static_cast<uint32_t>(n * 8);
+      blk[w] = x;
+    }
+    sha256_compress(out, blk);
+  }
+}
+
+AHV_HD void hex_digest(const uint32_t d[8], uint8_t out[64]) {
+  for (int i = 0; i < 8; ++i) {
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t nib = (d[i] >> (28 - 4 * j)) & 15u;
+      out[8 * i + j] = static_cast<uint8_t>(hex_nibble(nib));
+    }
+  }
+}
+
+// Live vouch: active and not expired at `now` (VouchRecord.is_live, reference
+// vouching.py:34-38 + the `_active_vouches_for` filter).
+AHV_HD bool edge_live(const Tables& t, int32_t e, int64_t now) {
+  return t.e_active[e] && (t.e_expiry[e] < 0 || now <= t.e_expiry[e]);
+}
+
+// Participant row of `agent` in session `s` (all rows, active or not), or -1.
+AHV_HD int32_t find_part(const Tables& t, int64_t s, int32_t agent) {
+  const int32_t n = t.s_pcount[s];
+  const int64_t base = s * t.cap.P;
+  for (int32_t k = 0; k < n; ++k)
+    if (t.p_agent[base + k] == agent) return k;
+  return -1;
+}
+
+// An int32 index list argument: ≤ 96 entries inline in the command, else in
+// the staging area at `off`.
+struct IndexList {
+  const int32_t* p;
+  bool fine;
+  AHV_HD int32_t operator[](uint64_t i) const {
+    return fine ? static_cast<int32_t>(ld32f(p + i)) : p[i];
+  }
+};
+
+AHV_HD IndexList index_list(const Tables& t, const Cmd& c, uint64_t n, uint64_t off) {
+  if (n <= 2 * kInlineWords) return IndexList{reinterpret_cast<const int32_t*>(c.inl), false};
+  return IndexList{reinterpret_cast<const int32_t*>(t.staging + off), true};
+}
+
+// Merkle root (reference audit/delta.py:117-134) over `n` digests in `lv`
+// (scratch, n*8 words), level by level with odd duplication; SIMT across the
+// lanes within a level (the worker is a single wave, so a barrier inside the
+// lane-strided loop is wave-uniform).  Parent i overwrites slot i: within a
+// pass every lane reads its two children before any lane writes, and the slots
+// a pass writes ([p·n, (p+1)·n)) lie below every child slot of later passes.
+// The root is left in lv[0..7].
+AHV_HD void merkle_inplace(const Lanes& L, uint32_t* lv, int64_t n) {
+  while (n > 1) {
+    const int64_t m = (n + 1) / 2;
+    for (int64_t i0 = 0; i0 < m; i0 += L.n) {
+      const int64_t i = i0 + L.lane;
+      uint32_t o[8];
+      if (i < m) {
+        uint32_t l[8], r[8];
+        load8(lv + 16 * i, l);
+        if (2 * i + 1 < n) load8(lv + 16 * i + 8, r);
+        else load8(lv + 16 * i, r);
+        merkle_node(l, r, o);
+      }
+      L.sync();
+      if (i < m) store8(lv + 8 * i, o);
+      L.sync();
+    }
+    n = m;
+  }
+}
+
+// Stage `n` payload bytes at `src` (64-byte aligned) into L.lds as big-endian
+// SHA-256 message words, splice the quoted hex of `head` into a 66-byte hole at
+// byte `hole` (also written back to `src`, so the stored record is complete),
+// and append the SHA padding.  Returns the number of 64-byte blocks, or -1 when
+// the message does not fit the LDS buffer.  All lanes participate.
+AHV_HD int64_t stage_message(const Lanes& L, uint8_t* src, uint64_t n, int64_t hole, const uint32_t* head) {
+  const uint64_t nblk = (n + 9 + 63) / 64;
+  if (nblk * 16 > static_cast<uint64_t>(kLdsWords)) return -1;
+  const uint64_t nw = nblk * 16;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+  for (uint64_t i = L.lane; i < nw; i += L.n) {
+    uint32_t w = 0;
+    const uint64_t b = 4 * i;
+    if (b + 4 <= n) {
+      w = bswap32(ld32f(s32 + i));
+    } else if (b < n) {
+      const uint32_t raw = bswap32(ld32f(s32 + i));
+      const uint32_t keep = static_cast<uint32_t>(n - b);  // 1..3 leading bytes
+      w = raw & (0xffffffffu << (8 * (4 - keep)));
+    }
+    if (b <= n && n < b + 4) w |= 0x80u << (8 * (3 - (n - b)));  // padding marker
+    if (i == nw - 2) w |= static_cast<uint32_t>((n * 8) >> 32);
+    if (i == nw - 1) w |= static_cast<uint32_t>(n * 8);
+    L.lds[i] = w;
+  }
+  L.sync();
+  if (hole >= 0) {
+    // 66 bytes: '"', 64 lowercase hex digits of head (big-endian word order), '"'
+    for (int k = L.lane; k < 66; k += L.n) {
+      uint32_t ch;
+      if (k == 0 || k == 65) {
+        ch = 0x22u;
+      } else {
+        const int nib = k - 1;
+        ch = hex_nibble((head[nib >> 3] >> (28 - 4 * (nib & 7))) & 15u);
+      }
+      const uint64_t b = static_cast<uint64_t>(hole) + k;
+      src[b] = static_cast<uint8_t>(ch);
+      uint8_t* lb = reinterpret_cast<uint8_t*>(L.lds);
+      lb[(b & ~uint64_t(3)) | (3 - (b & 3))] = static_cast<uint8_t>(ch);
+    }
+    L.sync();
+  }
+  return static_cast<int64_t>(nblk);
+}
+
+AHV_HD void sha256_lds_blocks(const uint32_t* w, int64_t nblk, uint32_t out[8]) {
+  sha256_init(out);
+  for (int64_t b = 0; b < nblk; ++b) sha256_compress(out, w + 16 * b);
+}
+
+// ------------------------------------------------------------- session ops
+
+AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
+  if (!L.leader()) return;
+  const int64_t s = static_cast<int64_t>(c.a[0]);
+  if (s < 0 || s >= t.cap.S) {
+    if (L.leader()) out64(r + 1, ST_BAD_ARG);
+    return;
+  }
+  switch (c.op) {
+    case OP_SESS_CREATE: {
+      t.s_state[s] = SS_HANDSHAKING;  // create + begin_handshake (Hypervisor.create_session)
+      t.s_mode[s] = static_cast<uint8_t>(c.a[3]);
+      t.s_audit[s] = static_cast<uint8_t>(c.a[6]);
+      t.s_maxpart[s] = static_cast<int32_t>(c.a[4]);
+      t.s_minsig[s] = bitsd(c.a[5]);
+      t.s_creator[s] = static_cast<int32_t>(c.a[1]);
+      t.s_created[s] = static_cast<int64_t>(c.a[2]);
+      t.s_terminated[s] = 0;
+      t.s_pcount[s] = 0;
+      t.s_pactive[s] = 0;
+      t.s_dcount[s] = 0;
+      t.s_dlast[s] = -1;
+      t.s_committed[s] = 0;
+      t.s_commit_n[s] = 0;
+      t.s_released[s] = 0;
+      t.s_retained[s] = 0;
+      t.s_uuid[4 * s + 0] = static_cast<uint32_t>(c.a[7] >> 32);
+      t.s_uuid[4 * s + 1] = static_cast<uint32_t>(c.a[7]);
+      t.s_uuid[4 * s + 2] = static_cast<uint32_t>(c.a[8] >> 32);
+      t.s_uuid[4 * s + 3] = static_cast<uint32_t>(c.a[8]);
+      for (int k = 0; k < 8; ++k) {
+        t.s_head[8 * s + k] = 0;
+        t.s_root[8 * s + k] = 0;
+      }
+      if (c.a[9]) t.s_state[s] = SS_CREATED;  // bare SharedSessionObject (no handshake yet)
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SESS_HANDSHAKE: {
+      const uint8_t st = t.s_state[s];
+      if (st != SS_CREATED) {
+        out64(r + 2, st);
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
+      t.s_state[s] = SS_HANDSHAKING;
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SESS_JOIN: {
+      // a1 agent, a2 σ_raw, a3 σ_eff, a4 flags (bit0 trustworthy, bit1 explicit ring), a5 ring, a6 now
+      const int32_t agent = static_cast<int32_t>(c.a[1]);
+      const double sraw = bitsd(c.a[2]);
+      const double seff = bitsd(c.a[3]);
+      const uint8_t st = t.s_state[s];
+      uint8_t ring = (c.a[4] & 2u) ? static_cast<uint8_t>(c.a[5]) : ring_from_sigma(seff, false);  // K01
+      if (!(c.a[4] & 2u) && !(c.a[4] & 1u)) ring = RING3;  // untrustworthy history → sandbox
+      const bool dup = find_part(t, s, agent) >= 0;
+      const int32_t active = t.s_pactive[s];
+      uint64_t code = join_check(st, dup, active, t.s_maxpart[s], seff, t.s_minsig[s], ring);
+      if (code == JOIN_OK && t.s_pcount[s] >= t.cap.P) code = JOIN_ROWS;
+      if (code == JOIN_OK) {
+        const int64_t row = s * t.cap.P + t.s_pcount[s];
+        t.p_agent[row] = agent;
+        t.p_ring[row] = ring;
+        t.p_active[row] = 1;
+        t.p_sraw[row] = sraw;
+        t.p_seff[row] = seff;
+        t.p_joined[row] = static_cast<int64_t>(c.a[6]);
+        t.s_pcount[s] += 1;
+        t.s_pactive[s] = active + 1;
+      }
+      out64(r + 2, ring);
+      out64(r + 3, st);
+      out64(r + 4, static_cast<uint64_t>(active));
+      out64(r + 5, static_cast<uint64_t>(t.s_maxpart[s]));
+      out64(r + 6, dbits(t.s_minsig[s]));
+      out64(r + 1, code);
+      return;
+    }
+    case OP_SESS_LEAVE: {
+      const int32_t k = find_part(t, s, static_cast<int32_t>(c.a[1]));
+      if (k < 0) {
+        out64(r + 1, ST_NOT_FOUND);
+        return;
+      }
+      const int64_t row = s * t.cap.P + k;
+      if (t.p_active[row]) {
+        t.p_active[row] = 0;
+        t.s_pactive[s] -= 1;
+      }
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SESS_UPDATE_RING:
+    case OP_SESS_SET_SIGMA: {
+      const int32_t k = find_part(t, s, static_cast<int32_t>(c.a[1]));
+      if (k < 0) {
+        out64(r + 1, ST_NOT_FOUND);
+        return;
+      }
+      const int64_t row = s * t.cap.P + k;
+      if (c.op == OP_SESS_UPDATE_RING) {
+        t.p_ring[row] = static_cast<uint8_t>(c.a[2]);
+      } else {
+        t.p_seff[row] = bitsd(c.a[2]);
+        if (c.a[3] & 1u) t.p_ring[row] = static_cast<uint8_t>(c.a[4]);
+      }
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SESS_SET_MODE:
+      t.s_mode[s] = static_cast<uint8_t>(c.a[1]);
+      out64(r + 1, ST_OK);
+      return;
+    case OP_SESS_ACTIVATE: {
+      const uint8_t st = t.s_state[s];
+      out64(r + 2, st);
+      if (st != SS_HANDSHAKING) {
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
+      if (t.s_pcount[s] == 0) {  // counts inactive rows too (reference session/__init__.py:81)
+        out64(r + 1, 3);
+        return;
+      }
+      t.s_state[s] = SS_ACTIVE;
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SESS_TERMINATE: {
+      const uint8_t st = t.s_state[s];
+      out64(r + 2, st);
+      if (!((session_op_allowed_from(OP_TERMINATE) >> st) & 1u)) {
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
+      t.s_state[s] = SS_TERMINATING;
+      t.s_terminated[s] = static_cast<int64_t>(c.a[1]);
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SESS_ARCHIVE: {
+      const uint8_t st = t.s_state[s];
+      out64(r + 2, st);
+      if (st != SS_TERMINATING) {
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
+      t.s_state[s] = SS_ARCHIVED;
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SESS_READ: {
+      // header → r[2..], participant rows → bulk at a[1] (stride 40 bytes)
+      out64(r + 2, t.s_state[s]);
+      out64(r + 3, t.s_mode[s]);
+      out64(r + 4, static_cast<uint64_t>(t.s_pcount[s]));
+      out64(r + 5, static_cast<uint64_t>(t.s_pactive[s]));
+      out64(r + 6, static_cast<uint64_t>(t.s_created[s]));
+      out64(r + 7, static_cast<uint64_t>(t.s_terminated[s]));
+      out64(r + 8, static_cast<uint64_t>(t.s_dcount[s]));
+      out64(r + 9, static_cast<uint64_t>(t.s_maxpart[s]));
+      out64(r + 10, dbits(t.s_minsig[s]));
+      out64(r + 11, t.s_audit[s]);
+      out64(r + 12, static_cast<uint64_t>(t.s_committed[s]));
+      out64(r + 13, static_cast<uint64_t>(t.s_commit_n[s]));
+      out64(r + 14, static_cast<uint64_t>(static_cast<int64_t>(t.s_creator[s])));
+      out64(r + 15, static_cast<uint64_t>(t.s_released[s]));
+      out64(r + 16, static_cast<uint64_t>(t.s_retained[s]));
+      for (int k = 0; k < 4; ++k) out64(r + 17 + k, (uint64_t(t.s_uuid[4 * s + k])));
+      for (int k = 0; k < 8; ++k) out64(r + 21 + k, uint64_t(t.s_root[8 * s + k]));
+      for (int k = 0; k < 8; ++k) out64(r + 29 + k, uint64_t(t.s_head[8 * s + k]));
+      if (bulk) {
+        uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[1]);
+        const int32_t n = t.s_pcount[s];
+        for (int32_t k = 0; k < n; ++k) {
+          const int64_t row = s * t.cap.P + k;
+          out64(b + 5 * k + 0, static_cast<uint64_t>(static_cast<int64_t>(t.p_agent[row])));
+          out64(b + 5 * k + 1, uint64_t(t.p_ring[row]) | (uint64_t(t.p_active[row]) << 8));
+          out64(b + 5 * k + 2, dbits(t.p_sraw[row]));
+          out64(b + 5 * k + 3, dbits(t.p_seff[row]));
+          out64(b + 5 * k + 4, static_cast<uint64_t>(t.p_joined[row]));
+        }
+      }
+      out64(r + 1, ST_OK);
+      return;
+    }
+    default:
+      break;
+  }
+}
+
+// Collect a session's delta digests into scratch (in capture order) from the
+// arena indices the host recorded at capture time; every index is validated
+// against the chain (owner session, turn, count).  Returns the count or -1.
+AHV_HD int64_t gather_leaves(const Lanes& L, const Tables& t, int64_t s, const IndexList& idx, int64_t n,
+                             uint32_t* lv, int64_t cutoff, int64_t* expired_out) {
+  int bad = 0;
+  int64_t expired = 0;
+  for (int64_t i = L.lane; i < n; i += L.n) {
+    const int32_t d = idx[i];
+    if (d < 0 || d >= t.cap.D || t.d_sess[d] != s || t.d_turn[d] != i + 1) {
+      bad = 1;
+      continue;
+    }
+    load8(t.d_hash + 8 * static_cast<int64_t>(d), lv + 8 * i);
+    if (t.d_ts[d] < cutoff) ++expired;
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  bad = __any(bad) ? 1 : 0;
+  for (int o = 32; o > 0; o >>= 1) expired += __shfl_xor(expired, o);
+#endif
+  L.sync();
+  if (expired_out) *expired_out = expired;
+  return bad ? -1 : n;
+}
+
+// ------------------------------------------------------------- vouch ops
+
+// K07: release every still-active edge of liability session `v` (reference
+// vouching.py:176-184); returns the count.
+AHV_HD int32_t release_vsess(const Tables& t, int32_t v, int64_t now) {
+  int32_t n = 0;
+  if (v < 0 || v >= t.cap.V) return 0;
+  for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e]) {
+    if (t.e_active[e]) {
+      t.e_active[e] = 0;
+      t.e_released[e] = now;
+      ++n;
+    }
+  }
+  return n;
+}
+
+// Does voucher→vouchee close a cycle among the live edges of `v`?  Non-parity:
+// true reachability; parity: the reference BFS that also flags diamonds (Q05).
+// Work arrays in scratch; returns 2 when scratch is too small.
+AHV_HD int creates_cycle(const Tables& t, int32_t v, int32_t voucher, int32_t vouchee, int64_t now, bool parity) {
+  int32_t* from = reinterpret_cast<int32_t*>(t.scratch);
+  const int64_t cap = t.cap.X / 16;
+  int32_t* to = from + cap;
+  int32_t* q = to + cap;
+  int32_t* seen = q + cap;
+  int64_t m = 0;
+  for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e]) {
+    if (!edge_live(t, e, now)) continue;
+    if (m >= cap) return 2;
+    from[m] = t.e_voucher[e];
+    to[m] = t.e_vouchee[e];
+    ++m;
+  }
+  for (int64_t i = 0; i < m; ++i)
+    if (from[i] == vouchee && to[i] == voucher) return 1;
+  int64_t qh = 0, qt = 0, ns = 0;
+  auto is_seen = [&](int32_t a) {
+    for (int64_t k = 0; k < ns; ++k)
+      if (seen[k] == a) return true;
+    return false;
+  };
+  if (parity) {
+    seen[ns++] = voucher;
+    q[qt++] = vouchee;
+    while (qh < qt) {
+      const int32_t cur = q[qh++];
+      if (is_seen(cur)) return 1;
+      if (ns >= cap) return 2;
+      seen[ns++] = cur;
+      for (int64_t i = 0; i < m; ++i) {
+        if (from[i] != cur || is_seen(to[i])) continue;
+        if (qt >= cap) return 2;
+        q[qt++] = to[i];
+      }
+    }
+    return 0;
+  }
+  seen[ns++] = vouchee;
+  q[qt++] = vouchee;
+  while (qh < qt) {
+    const int32_t cur = q[qh++];
+    for (int64_t i = 0; i < m; ++i) {
+      if (from[i] != cur) continue;
+      const int32_t nx = to[i];
+      if (nx == voucher) return 1;
+      if (!is_seen(nx)) {
+        if (ns >= cap || qt >= cap) return 2;
+        seen[ns++] = nx;
+        q[qt++] = nx;
+      }
+    }
+  }
+  return 0;
+}
+
+AHV_HD double exposure_of(const Tables& t, int32_t v, int32_t voucher, int64_t now) {
+  double cur = 0.0;
+  for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e])
+    if (t.e_voucher[e] == voucher && edge_live(t, e, now)) cur += t.e_bonded[e];
+  return cur;
+}
+
+// Slash working set in scratch: (agent, σ) score pairs, then the clip list.
+struct Scores {
+  int32_t* agent;
+  double* sigma;
+  int64_t n, cap;
+  AHV_HD int64_t find(int32_t a) const {
+    for (int64_t k = 0; k < n; ++k)
+      if (agent[k] == a) return k;
+    return -1;
+  }
+  AHV_HD double get(int32_t a) const {
+    const int64_t k = find(a);
+    return k < 0 ? 0.0 : sigma[k];
+  }
+  AHV_HD bool set(int32_t a, double v) {
+    int64_t k = find(a);
+    if (k < 0) {
+      if (n >= cap) return false;
+      k = n++;
+      agent[k] = a;
+    }
+    sigma[k] = v;
+    return true;
+  }
+};
+
+AHV_HD bool has_live_vouchers(const Tables& t, int32_t v, int32_t agent, int64_t now) {
+  for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e])
+    if (t.e_vouchee[e] == agent && edge_live(t, e, now)) return true;
+  return false;
+}
+
+// K06 — SlashingEngine.slash with its cascade (reference slashing.py:63-143),
+// pre-order like the recursion: one record per slash (frame) followed by its
+// clips, then the children of each clip in clip order (a child is eligible when
+// its σ after the clip is < SIGMA_FLOOR + 0.01 and it still has live vouchers
+// *at that moment*, i.e. after earlier siblings' subtrees released bonds).
+// Output u64 words: per frame [vouchee, depth, nclips, σ_before bits] then per
+// clip [voucher, before bits, after bits, edge].  Clips are mirrored in scratch
+// (clip_v/clip_a) so the descent never reads back the host-memory output.
+// Returns words written, or -1 when an output/scratch bound is hit.
+AHV_HD int64_t slash_cascade(const Tables& t, int32_t v, int32_t root, double root_sigma, double w, int64_t now,
+                             Scores& sc, int32_t* clip_v, double* clip_a, int64_t clip_cap, uint64_t* out,
+                             int64_t out_cap, int start_depth) {
+  constexpr int kDepth = 3;  // MAX_CASCADE_DEPTH 2 → frames at depth 0..2
+  struct Frame {
+    int64_t base;  // first clip of this frame in clip_v/clip_a
+    int32_t nclips, next;
+  } fr[kDepth];
+  int64_t wpos = 0, ncl = 0;
+  if (start_depth < 0) start_depth = 0;
+  if (start_depth > kDepth - 1) start_depth = kDepth - 1;
+  int depth = start_depth;
+  int32_t vouchee = root;
+  double before = root_sigma;
+  for (;;) {
+    if (wpos + 4 > out_cap) return -1;
+    const int64_t hdr = wpos;
+    out64(out + hdr + 0, static_cast<uint64_t>(static_cast<int64_t>(vouchee)));
+    out64(out + hdr + 1, static_cast<uint64_t>(depth));
+    out64(out + hdr + 3, dbits(before));
+    wpos += 4;
+    if (!sc.set(vouchee, 0.0)) return -1;
+    const int64_t base = ncl;
+    for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e]) {
+      if (t.e_vouchee[e] != vouchee || !edge_live(t, e, now)) continue;
+      const int32_t vr = t.e_voucher[e];
+      const double b = sc.get(vr);
+      double a = b * (1.0 - w);
+      if (a < 0.05) a = 0.05;  // clip_sigma: max(σ·(1−ω), SIGMA_FLOOR)
+      if (!sc.set(vr, a) || ncl >= clip_cap || wpos + 4 > out_cap) return -1;
+      out64(out + wpos + 0, static_cast<uint64_t>(static_cast<int64_t>(vr)));
+      out64(out + wpos + 1, dbits(b));
+      out64(out + wpos + 2, dbits(a));
+      out64(out + wpos + 3, static_cast<uint64_t>(static_cast<int64_t>(e)));
+      wpos += 4;
+      clip_v[ncl] = vr;
+      clip_a[ncl] = a;
+      ++ncl;
+      t.e_active[e] = 0;  // release_bond
+      t.e_released[e] = now;
+    }
+    out64(out + hdr + 2, static_cast<uint64_t>(ncl - base));
+    fr[depth].base = base;
+    fr[depth].nclips = static_cast<int32_t>(ncl - base);
+    fr[depth].next = 0;
+    bool descended = false;
+    for (;;) {
+      if (depth < kDepth - 1) {
+        Frame& f = fr[depth];
+        while (f.next < f.nclips) {
+          const int64_t k = f.base + f.next;
+          f.next += 1;
+          if (clip_a[k] < 0.05 + 0.01 && has_live_vouchers(t, v, clip_v[k], now)) {
+            vouchee = clip_v[k];
+            before = clip_a[k];
+            depth += 1;
+            descended = true;
+            break;
+          }
+        }
+        if (descended) break;
+      }
+      if (depth == start_depth) return wpos;
+      depth -= 1;
+    }
+  }
+}
+
+AHV_HD void exec_vouch(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
+  if (!L.leader()) return;
+  switch (c.op) {
+    case OP_VOUCH: {
+      // a0 vsess, a1 voucher, a2 vouchee, a3 σ bits, a4 pct bits (NaN = default),
+      // a5 expiry µs (-1 none), a6 now, a7 max_exposure bits, a8 parity, a9 edge index
+      const int32_t v = static_cast<int32_t>(c.a[0]);
+      const int32_t vr = static_cast<int32_t>(c.a[1]), ve = static_cast<int32_t>(c.a[2]);
+      const double sigma = bitsd(c.a[3]);
+      const int64_t now = static_cast<int64_t>(c.a[6]);
+      const int64_t e = static_cast<int64_t>(c.a[9]);
+      if (v < 0 || v >= t.cap.V || e < 0 || e >= t.cap.E) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      if (vr == ve) {
+        out64(r + 1, V_SELF);
+        return;
+      }
+      if (sigma < 0.50) {
+        out64(r + 1, V_LOW_SIGMA);
+        return;
+      }
+      const int cyc = creates_cycle(t, v, vr, ve, now, c.a[8] != 0);
+      if (cyc == 2) {
+        out64(r + 1, ST_SCRATCH);
+        return;
+      }
+      if (cyc) {
+        out64(r + 1, V_CYCLE);
+        return;
+      }
+      double pct = bitsd(c.a[4]);
+      if (pct != pct) pct = 0.20;  // DEFAULT_BOND_PCT
+      pct = pct < 0.0 ? 0.0 : (pct > 1.0 ? 1.0 : pct);
+      const double bonded = sigma * pct;
+      const double current = exposure_of(t, v, vr, now);
+      const double limit = sigma * bitsd(c.a[7]);
+      out64(r + 2, dbits(current));
+      out64(r + 3, dbits(bonded));
+      out64(r + 4, dbits(limit));
+      out64(r + 5, dbits(pct));
+      if (current + bonded > limit) {
+        out64(r + 1, V_EXPOSURE);
+        return;
+      }
+      t.e_voucher[e] = vr;
+      t.e_vouchee[e] = ve;
+      t.e_vsess[e] = v;
+      t.e_next[e] = -1;
+      t.e_active[e] = 1;
+      t.e_bonded[e] = bonded;
+      t.e_pct[e] = pct;
+      t.e_expiry[e] = static_cast<int64_t>(c.a[5]);
+      t.e_released[e] = -1;
+      t.e_created[e] = now;
+      const int32_t tail = t.v_tail[v];
+      if (tail < 0) t.v_head[v] = static_cast<int32_t>(e);
+      else t.e_next[tail] = static_cast<int32_t>(e);
+      t.v_tail[v] = static_cast<int32_t>(e);
+      out64(r + 1, V_OK);
+      return;
+    }
+    case OP_SIGMA_EFF: {
+      // a0 vsess, a1 vouchee, a2 σ bits, a3 ω bits, a4 now — sum in creation order (K03 scalar path)
+      const int32_t v = static_cast<int32_t>(c.a[0]);
+      const int32_t ve = static_cast<int32_t>(c.a[1]);
+      const int64_t now = static_cast<int64_t>(c.a[4]);
+      double contrib = 0.0;
+      if (v >= 0 && v < t.cap.V)
+        for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e])
+          if (t.e_vouchee[e] == ve && edge_live(t, e, now)) contrib += t.e_bonded[e];
+      double s = bitsd(c.a[2]) + bitsd(c.a[3]) * contrib;
+      if (s > 1.0) s = 1.0;
+      out64(r + 2, dbits(s));
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_EXPOSURE: {
+      const int32_t v = static_cast<int32_t>(c.a[0]);
+      const double x = (v >= 0 && v < t.cap.V)
+                           ? exposure_of(t, v, static_cast<int32_t>(c.a[1]), static_cast<int64_t>(c.a[2]))
+                           : 0.0;
+      out64(r + 2, dbits(x));
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_RELEASE_BOND: {
+      const int64_t e = static_cast<int64_t>(c.a[0]);
+      if (e < 0 || e >= t.cap.E) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      t.e_active[e] = 0;
+      t.e_released[e] = static_cast<int64_t>(c.a[1]);
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_RELEASE_SESSION: {
+      const int32_t n = release_vsess(t, static_cast<int32_t>(c.a[0]), static_cast<int64_t>(c.a[1]));
+      out64(r + 2, static_cast<uint64_t>(n));
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_VOUCH_LIST: {
+      // a0 vsess, a1 filter (0 all, 1 live by vouchee a2, 2 live by voucher a2, 3 live), a3 now,
+      // a4 bulk offset, a5 bulk capacity (edges).  Rows: [edge, voucher, vouchee, flags|released?]
+      const int32_t v = static_cast<int32_t>(c.a[0]);
+      const int64_t now = static_cast<int64_t>(c.a[3]);
+      const int32_t who = static_cast<int32_t>(c.a[2]);
+      uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[4]);
+      int64_t n = 0;
+      if (v >= 0 && v < t.cap.V) {
+        for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e]) {
+          const bool live = edge_live(t, e, now);
+          bool keep = true;
+          switch (c.a[1]) {
+            case 1: keep = live && t.e_vouchee[e] == who; break;
+            case 2: keep = live && t.e_voucher[e] == who; break;
+            case 3: keep = live; break;
+            default: break;
+          }
+          if (!keep) continue;
+          if (n < static_cast<int64_t>(c.a[5])) {
+            uint64_t* row = b + 8 * n;
+            out64(row + 0, static_cast<uint64_t>(static_cast<int64_t>(e)));
+            out64(row + 1, static_cast<uint64_t>(static_cast<int64_t>(t.e_voucher[e])));
+            out64(row + 2, static_cast<uint64_t>(static_cast<int64_t>(t.e_vouchee[e])));
+            out64(row + 3, uint64_t(t.e_active[e]));
+            out64(row + 4, dbits(t.e_bonded[e]));
+            out64(row + 5, dbits(t.e_pct[e]));
+            out64(row + 6, static_cast<uint64_t>(t.e_expiry[e]));
+            out64(row + 7, static_cast<uint64_t>(t.e_released[e]));
+          }
+          ++n;
+        }
+      }
+      out64(r + 2, static_cast<uint64_t>(n));
+      out64(r + 1, n > static_cast<int64_t>(c.a[5]) ? ST_SCRATCH : ST_OK);
+      return;
+    }
+    case OP_EDGE_READ: {
+      const int64_t e = static_cast<int64_t>(c.a[0]);
+      if (e < 0 || e >= t.cap.E) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      out64(r + 2, t.e_active[e]);
+      out64(r + 3, static_cast<uint64_t>(t.e_released[e]));
+      out64(r + 4, dbits(t.e_bonded[e]));
+      out64(r + 5, dbits(t.e_pct[e]));
+      out64(r + 6, static_cast<uint64_t>(t.e_expiry[e]));
+      out64(r + 7, static_cast<uint64_t>(static_cast<int64_t>(t.e_voucher[e])));
+      out64(r + 8, static_cast<uint64_t>(static_cast<int64_t>(t.e_vouchee[e])));
+      out64(r + 9, static_cast<uint64_t>(static_cast<int64_t>(t.e_vsess[e])));
+      out64(r + 10, static_cast<uint64_t>(t.e_created[e]));
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SLASH: {
+      // a0 vsess, a1 vouchee, a2 σ_before bits, a3 ω bits, a4 now, a5 nscores (pairs in staging at a6),
+      // a7 bulk offset of the record stream, a8 its capacity (words), a9 bulk offset of the scores out
+      const int32_t v = static_cast<int32_t>(c.a[0]);
+      const int64_t now = static_cast<int64_t>(c.a[4]);
+      const int64_t ns = static_cast<int64_t>(c.a[5]);
+      const int64_t cap = t.cap.X / 24;  // scratch: agents i32, σ f64, clip agents i32, clip σ f64
+      Scores sc;
+      sc.agent = reinterpret_cast<int32_t*>(t.scratch);
+      sc.sigma = reinterpret_cast<double*>(t.scratch + 8 * cap);
+      int32_t* clip_v = reinterpret_cast<int32_t*>(t.scratch + 16 * cap);
+      double* clip_a = reinterpret_cast<double*>(t.scratch + 16 * cap + 8 * (cap / 2));
+      sc.cap = cap;
+      sc.n = 0;
+      if (ns > cap || v < 0 || v >= t.cap.V) {
+        out64(r + 1, ST_SCRATCH);
+        return;
+      }
+      const uint64_t* pairs = reinterpret_cast<const uint64_t*>(t.staging + c.a[6]);
+      for (int64_t k = 0; k < ns; ++k) {
+        sc.agent[k] = static_cast<int32_t>(ld64f(pairs + 2 * k));
+        sc.sigma[k] = bitsd(ld64f(pairs + 2 * k + 1));
+      }
+      sc.n = ns;
+      uint64_t* out = reinterpret_cast<uint64_t*>(bulk + c.a[7]);
+      const int64_t words = slash_cascade(t, v, static_cast<int32_t>(c.a[1]), bitsd(c.a[2]), bitsd(c.a[3]), now,
+                                          sc, clip_v, clip_a, cap / 2, out, static_cast<int64_t>(c.a[8]),
+                                          static_cast<int>(c.a[10]));
+      if (words < 0) {
+        out64(r + 1, ST_SCRATCH);
+        return;
+      }
+      uint64_t* so = reinterpret_cast<uint64_t*>(bulk + c.a[9]);
+      for (int64_t k = 0; k < sc.n; ++k) {
+        out64(so + 2 * k, static_cast<uint64_t>(static_cast<int64_t>(sc.agent[k])));
+        out64(so + 2 * k + 1, dbits(sc.sigma[k]));
+      }
+      out64(r + 2, static_cast<uint64_t>(words));
+      out64(r + 3, static_cast<uint64_t>(sc.n));
+      out64(r + 1, ST_OK);
+      return;
+    }
+    default:
+      break;
+  }
+}
+
+// ------------------------------------------------------------- saga ops
+
+AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
+  if (!L.leader()) return;
+  switch (c.op) {
+    case OP_SAGA_CREATE: {
+      const int64_t g = static_cast<int64_t>(c.a[0]);
+      if (g < 0 || g >= t.cap.G) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      t.g_state[g] = SG_RUNNING;
+      t.g_created[g] = static_cast<int64_t>(c.a[1]);
+      t.g_completed[g] = 0;
+      t.g_nsteps[g] = 0;
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_STEP_ADD: {
+      const int64_t g = static_cast<int64_t>(c.a[0]), st = static_cast<int64_t>(c.a[1]);
+      if (g < 0 || g >= t.cap.G || st < 0 || st >= t.cap.T) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      t.t_saga[st] = static_cast<int32_t>(g);
+      t.t_state[st] = ST_PENDING;
+      t.t_undo[st] = static_cast<uint8_t>(c.a[2]);
+      t.t_maxretry[st] = static_cast<int32_t>(c.a[3]);
+      t.t_retry[st] = 0;
+      t.t_started[st] = 0;
+      t.t_completed[st] = 0;
+      t.g_nsteps[g] += 1;
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_STEP_TRANSITION: {
+      // a0 step, a1 to-state, a2 now, a3 retry count (≥0 sets retry_count first)
+      const int64_t st = static_cast<int64_t>(c.a[0]);
+      const uint8_t to = static_cast<uint8_t>(c.a[1]);
+      const uint8_t from = t.t_state[st];
+      if (static_cast<int64_t>(c.a[3]) >= 0) t.t_retry[st] = static_cast<int32_t>(c.a[3]);
+      out64(r + 2, from);
+      if (!((step_transitions(from) >> to) & 1u)) {  // K13
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
+      t.t_state[st] = to;
+      if (to == ST_EXECUTING) t.t_started[st] = static_cast<int64_t>(c.a[2]);
+      else if (step_stamps_completed(to)) t.t_completed[st] = static_cast<int64_t>(c.a[2]);
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_STEP_SET: {
+      // direct write outside the FSM (reference orchestrator.py:124/134 retry reset, :167 no-undo)
+      const int64_t st = static_cast<int64_t>(c.a[0]);
+      t.t_state[st] = static_cast<uint8_t>(c.a[1]);
+      if (static_cast<int64_t>(c.a[2]) >= 0) t.t_retry[st] = static_cast<int32_t>(c.a[2]);
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SAGA_TRANSITION: {
+      const int64_t g = static_cast<int64_t>(c.a[0]);
+      const uint8_t to = static_cast<uint8_t>(c.a[1]);
+      const uint8_t from = t.g_state[g];
+      out64(r + 2, from);
+      if (!((saga_transitions(from) >> to) & 1u)) {
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
+      t.g_state[g] = to;
+      if (saga_terminal(to)) t.g_completed[g] = static_cast<int64_t>(c.a[2]);
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_STEP_READ: {
+      const int64_t st = static_cast<int64_t>(c.a[0]);
+      if (st < 0 || st >= t.cap.T) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      out64(r + 2, t.t_state[st]);
+      out64(r + 3, static_cast<uint64_t>(static_cast<int64_t>(t.t_retry[st])));
+      out64(r + 4, static_cast<uint64_t>(t.t_started[st]));
+      out64(r + 5, static_cast<uint64_t>(t.t_completed[st]));
+      out64(r + 6, static_cast<uint64_t>(static_cast<int64_t>(t.t_saga[st])));
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_SAGA_READ:
+    case OP_SAGA_PLAN: {
+      // a0 saga, a1 nsteps, a2 staging offset of step indices (if > inline), a3 bulk offset
+      const int64_t g = static_cast<int64_t>(c.a[0]);
+      const uint64_t n = c.a[1];
+      const IndexList idx = index_list(t, c, n, c.a[2]);
+      uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[3]);
+      out64(r + 2, t.g_state[g]);
+      out64(r + 3, static_cast<uint64_t>(t.g_created[g]));
+      out64(r + 4, static_cast<uint64_t>(t.g_completed[g]));
+      out64(r + 5, static_cast<uint64_t>(t.g_nsteps[g]));
+      if (c.op == OP_SAGA_READ) {
+        for (uint64_t k = 0; k < n; ++k) {
+          const int32_t st = idx[k];
+          out64(b + 4 * k + 0, uint64_t(t.t_state[st]) | (uint64_t(static_cast<uint32_t>(t.t_retry[st])) << 8));
+          out64(b + 4 * k + 1, static_cast<uint64_t>(t.t_started[st]));
+          out64(b + 4 * k + 2, static_cast<uint64_t>(t.t_completed[st]));
+          out64(b + 4 * k + 3, static_cast<uint64_t>(t.t_saga[st] == g));
+        }
+      } else {
+        // K14: committed steps in reverse order
+        uint64_t m = 0;
+        for (uint64_t k = n; k-- > 0;) {
+          const int32_t st = idx[k];
+          if (t.t_state[st] == ST_COMMITTED) out64(b + m++, k);
+        }
+        out64(r + 6, m);
+      }
+      out64(r + 1, ST_OK);
+      return;
+    }
+    default:
+      break;
+  }
+}
+
+// ------------------------------------------------------------- audit ops
+
+AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
+  switch (c.op) {
+    case OP_DELTA_CAPTURE: {
+      // a0 session, a1 delta index, a2 turn, a3 ts, a4 payload offset, a5 payload length,
+      // a6 parent-hole offset in the payload (-1: turn 1, "null" already written)
+      const int64_t s = static_cast<int64_t>(c.a[0]);
+      const int64_t d = static_cast<int64_t>(c.a[1]);
+      const int32_t turn = static_cast<int32_t>(c.a[2]);
+      const int64_t hole = static_cast<int64_t>(c.a[6]);
+      int ok = 0;
+      int32_t prev = -1;
+      if (L.leader()) {
+        ok = !(s < 0 || s >= t.cap.S || d < 0 || d >= t.cap.D || turn != t.s_dcount[s] + 1 ||
+               c.a[4] + c.a[5] > static_cast<uint64_t>(t.cap.B));
+        if (ok) {
+          prev = t.s_dlast[s];
+          if (hole >= 0 && prev < 0) ok = 0;
+        }
+      }
+      if (!bcast(L, ok)) {
+        if (L.leader()) out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      uint8_t* p = t.payload + c.a[4];
+      const int64_t nblk = stage_message(L, p, c.a[5], hole, t.s_head + 8 * s);  // K08 staging
+      if (!L.leader()) return;
+      uint32_t h[8];
+      if (nblk >= 0) sha256_lds_blocks(L.lds, nblk, h);  // the serial chain: one lane, LDS-fed
+      else sha256_mem(p, c.a[5], h);                      // oversized record
+      t.d_sess[d] = static_cast<int32_t>(s);
+      t.d_turn[d] = turn;
+      t.d_prev[d] = prev;
+      t.d_ts[d] = static_cast<int64_t>(c.a[3]);
+      t.d_off[d] = static_cast<int64_t>(c.a[4]);
+      t.d_len[d] = static_cast<int32_t>(c.a[5]);
+      store8(t.d_hash + 8 * d, h);
+      store8(t.s_head + 8 * s, h);
+      t.s_dlast[s] = static_cast<int32_t>(d);
+      t.s_dcount[s] = turn;
+      for (int k = 0; k < 8; ++k) out64(r + 2 + k, h[k]);
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_DELTA_MERKLE:
+    case OP_SESS_CLOSE: {
+      // MERKLE: a0 session, a1 n, a2 staging offset of indices.
+      // CLOSE:  a0 session, a1 n, a2 staging offset, a3 now, a4 vsess (-1 none),
+      //         a5 retention cutoff µs, a6 audit flag
+      const int64_t s = static_cast<int64_t>(c.a[0]);
+      const int64_t n = static_cast<int64_t>(c.a[1]);
+      if (s < 0 || s >= t.cap.S || 8 * 4 * n > t.cap.X) {
+        if (L.leader()) out64(r + 1, s < 0 || s >= t.cap.S ? ST_BAD_ARG : ST_SCRATCH);
+        return;
+      }
+      const bool close = c.op == OP_SESS_CLOSE;
+      const uint8_t st0 = bcast(L, L.leader() ? t.s_state[s] : uint8_t(0));
+      if (close && !((session_op_allowed_from(OP_TERMINATE) >> st0) & 1u)) {
+        if (L.leader()) {
+          out64(r + 2, st0);
+          out64(r + 1, ST_BAD_STATE);
+        }
+        return;
+      }
+      if (n != bcast(L, L.leader() ? static_cast<int64_t>(t.s_dcount[s]) : int64_t(0))) {
+        if (L.leader()) out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      uint32_t* lv = reinterpret_cast<uint32_t*>(t.scratch);
+      int64_t expired = 0;
+      const int64_t cutoff = close ? static_cast<int64_t>(c.a[5]) : INT64_MIN;
+      const int64_t got = gather_leaves(L, t, s, index_list(t, c, static_cast<uint64_t>(n), c.a[2]), n, lv, cutoff,
+                                        &expired);
+      if (got < 0) {
+        if (L.leader()) out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      const bool want_root = n > 0 && (!close || c.a[6]);
+      if (want_root) merkle_inplace(L, lv, n);  // K09
+      if (!L.leader()) return;
+      uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (want_root) load8(lv, root);
+      for (int k = 0; k < 8; ++k) out64(r + 3 + k, root[k]);
+      out64(r + 2, want_root ? 1u : 0u);
+      if (close) {
+        const int64_t now = static_cast<int64_t>(c.a[3]);
+        t.s_state[s] = SS_TERMINATING;
+        t.s_terminated[s] = now;
+        if (want_root) {  // CommitmentEngine.commit
+          store8(t.s_root + 8 * s, root);
+          t.s_committed[s] = now;
+          t.s_commit_n[s] = static_cast<int32_t>(n);
+        }
+        const int32_t rel = release_vsess(t, static_cast<int32_t>(static_cast<int64_t>(c.a[4])), now);  // K07
+        t.s_released[s] = rel;
+        t.s_retained[s] = static_cast<int32_t>(n - expired);  // EphemeralGC retention
+        t.s_state[s] = SS_ARCHIVED;
+        out64(r + 11, static_cast<uint64_t>(rel));
+        out64(r + 12, static_cast<uint64_t>(expired));
+      }
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_DELTA_VERIFY: {
+      // K10 over host-presented records (the views the API handed out, possibly
+      // tampered): a0 session, a1 n, a2 staging offset of the record table, a3
+      // parity (reference verify: re-hash then compare links only, Q02), a4 bulk
+      // offset for the re-hashed digests.  Record (11 u64): payload offset in
+      // staging, length, arena index, presented digest (4 u64 = 8 u32 BE words),
+      // presented parent (4 u64; all-ones = null).
+      const int64_t s = static_cast<int64_t>(c.a[0]);
+      const int64_t n = static_cast<int64_t>(c.a[1]);
+      const uint64_t* rec = reinterpret_cast<const uint64_t*>(t.staging + c.a[2]);
+      const bool parity = c.a[3] != 0;
+      // scratch: re-hashed [n][8], presented digests [n][8], presented parents [n][8], ok flags
+      uint32_t* rh = reinterpret_cast<uint32_t*>(t.scratch);
+      uint8_t* okv = t.scratch + 96 * n;
+      if (97 * n > t.cap.X || s < 0 || s >= t.cap.S) {
+        if (L.leader()) out64(r + 1, ST_SCRATCH);
+        return;
+      }
+      uint64_t* b = bulk ? reinterpret_cast<uint64_t*>(bulk + c.a[4]) : nullptr;
+      for (int64_t i = L.lane; i < n; i += L.n) {  // SIMT: one record per lane
+        uint64_t q[11];
+        for (int k = 0; k < 11; ++k) q[k] = ld64f(rec + 11 * i + k);
+        uint32_t h[8];
+        sha256_fine(t.staging + q[0], q[1], h);
+        store8(rh + 8 * i, h);
+        const uint32_t* ph = reinterpret_cast<const uint32_t*>(q + 3);
+        const int64_t d = static_cast<int64_t>(q[2]);
+        bool ok = d >= 0 && d < t.cap.D && t.d_sess[d] == s;
+        for (int k = 0; k < 8; ++k) {
+          ok = ok && h[k] == ph[k];
+          if (d >= 0 && d < t.cap.D) ok = ok && t.d_hash[8 * d + k] == ph[k];  // device-held chain
+        }
+        okv[i] = ok ? 1 : 0;
+        if (b)
+          for (int k = 0; k < 8; ++k) out64(b + 8 * i + k, h[k]);
+        // presented digest/parent of record i kept for the link pass
+        store8(rh + 8 * (n + i), ph);
+        store8(rh + 8 * (2 * n + i), reinterpret_cast<const uint32_t*>(q + 7));
+      }
+      L.sync();
+      if (!L.leader()) return;
+      int64_t bad = -1;
+      for (int64_t i = 0; i < n && bad < 0; ++i) {
+        const uint32_t* pp = rh + 8 * (2 * n + i);
+        if (!parity && !okv[i]) bad = i;
+        if (i == 0) {
+          for (int k = 0; k < 8; ++k)
+            if (pp[k] != 0xffffffffu) bad = 0;
+        } else {
+          const uint32_t* prevh = parity ? rh + 8 * (i - 1) : rh + 8 * (n + i - 1);
+          for (int k = 0; k < 8; ++k)
+            if (pp[k] != prevh[k]) bad = i;
+        }
+      }
+      out64(r + 2, bad < 0 ? 1u : 0u);
+      out64(r + 3, static_cast<uint64_t>(bad));
+      out64(r + 1, ST_OK);
+      return;
+    }
+    case OP_DELTA_READ: {
+      // a0 n, a1 staging offset of indices, a2 bulk offset: rows [turn, prev, ts, 8 hash words]
+      if (!L.leader()) return;
+      const uint64_t n = c.a[0];
+      const IndexList idx = index_list(t, c, n, c.a[1]);
+      uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[2]);
+      for (uint64_t k = 0; k < n; ++k) {
+        const int32_t d = idx[k];
+        out64(b + 12 * k + 0, static_cast<uint64_t>(static_cast<int64_t>(t.d_turn[d])));
+        out64(b + 12 * k + 1, static_cast<uint64_t>(static_cast<int64_t>(t.d_prev[d])));
+        out64(b + 12 * k + 2, static_cast<uint64_t>(t.d_ts[d]));
+        out64(b + 12 * k + 3, static_cast<uint64_t>(static_cast<int64_t>(t.d_sess[d])));
+        for (int w = 0; w < 8; ++w) out64(b + 12 * k + 4 + w, t.d_hash[8 * static_cast<int64_t>(d) + w]);
+      }
+      out64(r + 1, ST_OK);
+      return;
+    }
+    default:
+      break;
+  }
+}
+
+// ------------------------------------------------------------- dispatch
+
+// Execute one command.  All lanes of the wave call this with the same command;
+// lane 0 owns the scalar logic, the SIMT sections (Merkle levels, leaf gathers,
+// verify hashes) use every lane.  Returns false for OP_STOP.
+AHV_HD bool store_exec(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
+  if (c.op >= 10 && c.op < 30 && c.op != OP_SESS_CLOSE) {
+    exec_sess(L, t, c, r, bulk);
+  } else if ((c.op >= 30 && c.op < 40) || c.op == OP_SESS_CLOSE) {
+    exec_delta(L, t, c, r, bulk);
+  } else if (c.op >= 40 && c.op < 60) {
+    exec_vouch(L, t, c, r, bulk);
+  } else if (c.op >= 60 && c.op < 80) {
+    exec_saga(L, t, c, r, bulk);
+  } else if (c.op == OP_STOP) {
+    if (L.leader()) out64(r + 1, ST_OK);
+    return false;
+  } else if (c.op == OP_NOP || c.op == OP_FLUSH || c.op == OP_ACQUIRE) {
+    if (L.leader()) out64(r + 1, ST_OK);
+  } else {
+    if (L.leader()) out64(r + 1, ST_BAD_OP);
+  }
+  return true;
+}
+
+}  // namespace store
+}  // namespace ahv

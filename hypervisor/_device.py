@@ -1,0 +1,996 @@
+"""Device-backed engines: the public API over the gfx950 state store.
+
+``Hypervisor(device="cuda")`` (or ``"cpu"`` for the host twin of the same
+command processor) swaps its stateful engines for the classes below.  Each is a
+subclass of the host engine it replaces — same methods, same exceptions and
+messages — but holds no governance state of its own: every read and write is a
+command against :class:`agent_hypervisor_amd.models.store.GovernanceStore`
+(``csrc/include/ahv/store.h``):
+
+=============================  ===============================================
+engine                         device commands (kernel ids)
+=============================  ===============================================
+:class:`DeviceSession`         lifecycle FSM, join admission + ring gate (K01)
+:class:`DeviceDeltaEngine`     chain-linked SHA-256 capture (K08), Merkle root
+                               (K09), verification of presented records (K10)
+:class:`DeviceVouchingEngine`  vouch admission with cycle/exposure checks (K05),
+                               σ_eff (K03), exposure (K04), bond release (K07)
+:class:`DeviceSlashingEngine`  slash + cascade (K06)
+:class:`DeviceSagaOrchestrator` step / saga FSM (K13), compensation plan (K14)
+:class:`DeviceCommitmentEngine` commitments written by the terminate command
+=============================  ===============================================
+
+What stays on the host is what is not governance state: interned-id lookups
+(DIDs, session/vouch/saga ids → rows), the Python objects callers hand in
+(executors, results, VFS file contents) and error-message formatting.  Returned
+records (participants, vouch records, deltas, sagas) are *views*: their state
+fields are read from the device when accessed.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import json
+import struct
+from datetime import datetime, timedelta
+from typing import Any, Callable, Optional
+
+from agent_hypervisor_amd._native import C as _C
+from agent_hypervisor_amd.models import store as _st
+from agent_hypervisor_amd.models.store import GovernanceStore, bitsd, dbits
+from hypervisor import config as _cfg
+from hypervisor._clock import from_us, now as _now, to_us
+from hypervisor.audit.commitment import CommitmentEngine, CommitmentRecord
+from hypervisor.audit.delta import DeltaEngine, SemanticDelta, VFSChange, _payload_json
+from hypervisor.liability.slashing import SlashingEngine, SlashResult, VoucherClip
+from hypervisor.liability.vouching import VouchingEngine, VouchingError, VouchRecord
+from hypervisor.models import ConsistencyMode, ExecutionRing, SessionConfig, SessionParticipant, SessionState
+from hypervisor.saga._timeout import await_with_timeout
+from hypervisor.saga.orchestrator import SagaOrchestrator, SagaTimeoutError
+from hypervisor.saga.state_machine import (
+    SAGA_TRANSITIONS,
+    STEP_TRANSITIONS,
+    Saga,
+    SagaState,
+    SagaStateError,
+    SagaStep,
+    StepState,
+)
+from hypervisor.session import SessionLifecycleError, SessionParticipantError, SharedSessionObject
+from hypervisor.session.sso import SessionVFS
+
+_STATES = list(SessionState)
+_STEPS = list(StepState)
+_SAGAS = list(SagaState)
+_RINGS = list(ExecutionRing)
+_MODE = {ConsistencyMode.EVENTUAL: 0, ConsistencyMode.STRONG: 1}
+_MODES = [ConsistencyMode.EVENTUAL, ConsistencyMode.STRONG]
+_NAN = dbits(float("nan"))
+
+
+def _u64(v: int) -> int:
+    return v & 0xFFFFFFFFFFFFFFFF
+
+
+def _i64(v: int) -> int:
+    v &= 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def _hex(words) -> str:
+    return "".join(f"{int(w) & 0xFFFFFFFF:08x}" for w in words)
+
+
+def _words(hexstr: str) -> list[int]:
+    return [int(hexstr[8 * k: 8 * k + 8], 16) for k in range(8)]
+
+
+def _lifecycle(state_code: int, *allowed: SessionState) -> SessionLifecycleError:
+    st = _STATES[state_code] if state_code < len(_STATES) else state_code
+    val = st.value if isinstance(st, SessionState) else str(st)
+    return SessionLifecycleError(f"Operation not allowed in state {val}. Allowed: {[s.value for s in allowed]}")
+
+
+def _check(res: tuple, what: str) -> tuple:
+    if res[0] in (_st.ST_BAD_ARG, _st.ST_SCRATCH) or res[0] >= 90:
+        raise _st.StoreError(f"store command {what} failed with status {res[0]}")
+    return res
+
+
+# ------------------------------------------------------------------ sessions
+
+
+class DeviceSession(SharedSessionObject):
+    """A :class:`SharedSessionObject` whose lifecycle and participants live on the device."""
+
+    def __init__(
+        self,
+        store: GovernanceStore,
+        config: SessionConfig,
+        creator_did: str,
+        session_id: Optional[str] = None,
+        handshake: bool = True,
+        slot: Optional[int] = None,
+        create: bool = True,
+    ) -> None:
+        self._store = store
+        self.session_id = session_id or _C.uuid4("session:")
+        self.creator_did = creator_did
+        self.config = config
+        self.vfs_namespace = "/sessions/" + self.session_id
+        self.vfs = SessionVFS(self.session_id, namespace=self.vfs_namespace)
+        self._vfs_snapshots: dict[str, Any] = {}
+        self.slot = store.alloc("S") if slot is None else slot
+        if create:
+            u = self.session_id.rsplit(":", 1)[-1].replace("-", "")
+            try:
+                hi, lo = int(u[:16], 16), int(u[16:32], 16)
+            except ValueError:
+                hi = lo = 0
+            store.post(
+                _st.OP_SESS_CREATE,
+                [
+                    self.slot, store.agent_id(creator_did), to_us(_now()), _MODE[config.consistency_mode],
+                    int(config.max_participants), dbits(config.min_sigma_eff), int(bool(config.enable_audit)),
+                    _i64(hi), _i64(lo), 0 if handshake else 1,
+                ],
+            )
+
+    # -- device reads -----------------------------------------------------------
+    def _read(self, with_parts: bool = False):
+        r = self._store.call(_st.OP_SESS_READ, [self.slot, 0], 36)
+        parts = []
+        if with_parts and r[3]:
+            raw = self._store.bulk(0, 40 * r[3])
+            for k in range(r[3]):
+                a, fl, sr, se, j = struct.unpack_from("<qQddq", raw, 40 * k)
+                parts.append((a, fl & 0xFF, (fl >> 8) & 0xFF, sr, se, j))
+        return r, parts
+
+    def _participant(self, row) -> SessionParticipant:
+        a, ring, active, sr, se, j = row
+        return SessionParticipant(
+            agent_did=self._store.did(a), ring=_RINGS[ring], sigma_raw=sr, sigma_eff=se,
+            joined_at=from_us(j), is_active=bool(active),
+        )
+
+    @property
+    def state(self) -> SessionState:
+        return _STATES[self._store.call(_st.OP_SESS_READ, [self.slot, 0], 2)[1]]
+
+    @state.setter
+    def state(self, value) -> None:  # the base class never assigns on this path
+        raise AttributeError("device session state changes only through lifecycle methods")
+
+    @property
+    def consistency_mode(self) -> ConsistencyMode:
+        return _MODES[self._store.call(_st.OP_SESS_READ, [self.slot, 0], 3)[2]]
+
+    @consistency_mode.setter
+    def consistency_mode(self, mode) -> None:
+        self.force_consistency_mode(mode)
+
+    @property
+    def created_at(self) -> datetime:
+        return from_us(self._store.call(_st.OP_SESS_READ, [self.slot, 0], 6)[5])
+
+    @created_at.setter
+    def created_at(self, v) -> None:
+        raise AttributeError("created_at is recorded by the device")
+
+    @property
+    def terminated_at(self) -> Optional[datetime]:
+        t = self._store.call(_st.OP_SESS_READ, [self.slot, 0], 7)[6]
+        return from_us(t) if t else None
+
+    @terminated_at.setter
+    def terminated_at(self, v) -> None:
+        raise AttributeError("terminated_at is recorded by the device")
+
+    @property
+    def _participants(self) -> dict[str, SessionParticipant]:
+        _, parts = self._read(True)
+        return {p.agent_did: p for p in (self._participant(r) for r in parts)}
+
+    @property
+    def participants(self) -> list[SessionParticipant]:
+        _, parts = self._read(True)
+        return [self._participant(r) for r in parts if r[2]]
+
+    @property
+    def participant_count(self) -> int:
+        return self._store.call(_st.OP_SESS_READ, [self.slot, 0], 5)[4]
+
+    # -- lifecycle ---------------------------------------------------------------
+    def begin_handshake(self) -> None:
+        r = self._store.call(_st.OP_SESS_HANDSHAKE, [self.slot], 2)
+        if r[0]:
+            raise _lifecycle(r[1], SessionState.CREATED)
+
+    def activate(self) -> None:
+        r = self._store.call(_st.OP_SESS_ACTIVATE, [self.slot], 2)
+        if r[0] == _st.ST_BAD_STATE:
+            raise _lifecycle(r[1], SessionState.HANDSHAKING)
+        if r[0] == 3:
+            raise SessionLifecycleError("Cannot activate session with no participants")
+        _check(r, "activate")
+
+    def _join(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> int:
+        r = self._store.call(
+            _st.OP_SESS_JOIN,
+            [self.slot, self._store.agent_id(agent_did), dbits(sigma_raw), dbits(sigma_eff), flags, ring,
+             to_us(_now())],
+            6,
+        )
+        code = r[0]
+        if code == 0:
+            return r[1]
+        if code == 1:
+            raise _lifecycle(r[2], SessionState.HANDSHAKING, SessionState.ACTIVE)
+        if code == 2:
+            raise SessionParticipantError(f"Agent {agent_did} already in session")
+        if code in (3, 5):
+            raise SessionParticipantError(f"Session at capacity ({self.config.max_participants})")
+        if code == 4:
+            raise SessionParticipantError(f"σ_eff {sigma_eff:.2f} below minimum {bitsd(r[5]):.2f}")
+        raise _st.StoreError(f"join failed with status {code}")
+
+    def join(self, agent_did: str, sigma_raw: float = 0.0, sigma_eff: float = 0.0,
+             ring: ExecutionRing = ExecutionRing.RING_3_SANDBOX) -> SessionParticipant:
+        self._join(agent_did, sigma_raw, sigma_eff, 2, int(ring))
+        return SessionParticipant(agent_did=agent_did, ring=ring, sigma_raw=sigma_raw, sigma_eff=sigma_eff)
+
+    def join_gated(self, agent_did: str, sigma_raw: float, sigma_eff: float, trustworthy: bool) -> ExecutionRing:
+        """Join with the ring computed on the device (K01 ring gate); returns the ring."""
+        return _RINGS[self._join(agent_did, sigma_raw, sigma_eff, 1 if trustworthy else 0, 0)]
+
+    def leave(self, agent_did: str) -> None:
+        r = self._store.call(_st.OP_SESS_LEAVE, [self.slot, self._store.agent_id(agent_did)], 1)
+        if r[0]:
+            raise SessionParticipantError(f"Agent {agent_did} not in session")
+
+    def get_participant(self, agent_did: str) -> SessionParticipant:
+        p = self._participants.get(agent_did)
+        if p is None:
+            raise SessionParticipantError(f"Agent {agent_did} not in session")
+        return p
+
+    def update_ring(self, agent_did: str, new_ring: ExecutionRing) -> None:
+        r = self._store.call(_st.OP_SESS_UPDATE_RING, [self.slot, self._store.agent_id(agent_did), int(new_ring)], 1)
+        if r[0]:
+            raise SessionParticipantError(f"Agent {agent_did} not in session")
+
+    def set_sigma(self, agent_did: str, sigma_eff: float, ring: Optional[ExecutionRing] = None) -> None:
+        args = [self.slot, self._store.agent_id(agent_did), dbits(sigma_eff), 1 if ring is not None else 0,
+                int(ring) if ring is not None else 0]
+        if self._store.call(_st.OP_SESS_SET_SIGMA, args, 1)[0]:
+            raise SessionParticipantError(f"Agent {agent_did} not in session")
+
+    def force_consistency_mode(self, mode: ConsistencyMode) -> None:
+        self._store.post(_st.OP_SESS_SET_MODE, [self.slot, _MODE[ConsistencyMode(mode)]])
+
+    def terminate(self) -> None:
+        r = self._store.call(_st.OP_SESS_TERMINATE, [self.slot, to_us(_now())], 2)
+        if r[0]:
+            raise _lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
+
+    def archive(self) -> None:
+        r = self._store.call(_st.OP_SESS_ARCHIVE, [self.slot], 2)
+        if r[0]:
+            raise _lifecycle(r[1], SessionState.TERMINATING)
+
+    def create_vfs_snapshot(self, snapshot_id: Optional[str] = None) -> str:
+        r, parts = self._read(True)
+        if r[1] != 2:
+            raise _lifecycle(r[1], SessionState.ACTIVE)
+        sid = self.vfs.create_snapshot(snapshot_id)
+        self._vfs_snapshots[sid] = {
+            "created_at": _now().isoformat(),
+            "participant_states": {
+                self._store.did(p[0]): {"ring": p[1], "sigma_eff": p[4]} for p in parts
+            },
+        }
+        return sid
+
+    def restore_vfs_snapshot(self, snapshot_id: str, agent_did: str) -> None:
+        st = self.state
+        if st is not SessionState.ACTIVE:
+            raise _lifecycle(_STATES.index(st), SessionState.ACTIVE)
+        self.vfs.restore_snapshot(snapshot_id, agent_did)
+
+    def __repr__(self) -> str:
+        r, _ = self._read(False)
+        return (
+            f"SharedSessionObject(id={self.session_id!r}, state={_STATES[r[1]].value}, "
+            f"participants={r[4]}, mode={_MODES[r[2]].value}, device_slot={self.slot})"
+        )
+
+
+# ------------------------------------------------------------------ audit
+
+
+class DeviceDelta(SemanticDelta):
+    """A captured delta whose digest and parent link are held by the device chain."""
+
+    def __init__(self, engine: "DeviceDeltaEngine", delta_id, turn_id, session_id, agent_did, timestamp, changes,
+                 prev: Optional["DeviceDelta"]) -> None:
+        self.__dict__.update(
+            delta_id=delta_id, turn_id=turn_id, session_id=session_id, agent_did=agent_did, timestamp=timestamp,
+            changes=changes, _engine=engine, _prev=prev, _dev_hash=None, _hash_override=None,
+            _parent_override=None, _didx=-1, _poff=-1, _plen=0, _seq=-1,
+        )
+
+    def device_hash(self) -> str:
+        """The digest the device computed for this delta (K08)."""
+        h = self.__dict__["_dev_hash"]
+        if h is None:
+            h = self._engine._resolve(self)
+        return h
+
+    @property
+    def delta_hash(self) -> str:  # type: ignore[override]
+        o = self.__dict__["_hash_override"]
+        return o if o is not None else self.device_hash()
+
+    @delta_hash.setter
+    def delta_hash(self, v: str) -> None:
+        self.__dict__["_hash_override"] = v
+
+    @property
+    def parent_hash(self) -> Optional[str]:  # type: ignore[override]
+        o = self.__dict__["_parent_override"]
+        if o is not None:
+            return None if o is _NULL else o
+        prev = self.__dict__["_prev"]
+        return prev.device_hash() if prev is not None else None
+
+    @parent_hash.setter
+    def parent_hash(self, v: Optional[str]) -> None:
+        self.__dict__["_parent_override"] = _NULL if v is None else v
+
+    def compute_hash(self) -> str:
+        self.delta_hash = _host_digest(self)
+        return self.delta_hash
+
+    def record(self) -> bytes:
+        """The device-held canonical-JSON record (exact hashed bytes)."""
+        return self._engine._store.payload(self._poff, self._plen)
+
+    def __repr__(self) -> str:
+        return f"DeviceDelta(delta_id={self.delta_id!r}, turn_id={self.turn_id}, session_id={self.session_id!r})"
+
+
+_NULL = object()
+
+
+def _render(d) -> bytes:
+    b = _C.delta_payload(d)
+    return b if b is not None else _payload_json(d).encode()
+
+
+def _host_digest(d) -> str:
+    import hashlib
+
+    return hashlib.sha256(_render(d)).hexdigest()
+
+
+class DeviceDeltaEngine(DeltaEngine):
+    """Audit chain of one device session: the device links, hashes and roots it."""
+
+    def __init__(self, store: GovernanceStore, slot: int, session_id: str) -> None:
+        self._store = store
+        self.slot = slot
+        self.session_id = session_id
+        self._deltas: list[DeviceDelta] = []
+        self._turn_counter = 0
+
+    def capture(self, agent_did: str, changes: list[VFSChange], delta_id: Optional[str] = None) -> DeviceDelta:
+        turn = self._turn_counter + 1
+        ts = _now()
+        prev = self._deltas[-1] if self._deltas else None
+        d = DeviceDelta(self, delta_id or f"delta:{turn}", turn, self.session_id, agent_did, ts, changes, prev)
+        didx, off, ln, seq = self._store.capture(self.slot, turn, to_us(ts), d)
+        if didx < 0:  # field types the native renderer defers to json.dumps
+            raw = _payload_json(_NullParent(d)).encode()
+            at = raw.index(b'"parent_hash": null') + len(b'"parent_hash": ')
+            didx, off, ln, seq = self._store._c.capture_bytes(self.slot, turn, to_us(ts), raw, at)
+        d.__dict__.update(_didx=didx, _poff=off, _plen=ln, _seq=seq)
+        self._turn_counter = turn
+        self._deltas.append(d)
+        return d
+
+    def _resolve(self, d: DeviceDelta) -> str:
+        r = self._store.result(d._seq, 9)
+        if r is None:  # result slot recycled: read the arena row
+            n, off, inl = self._store.index_args([d._didx])
+            self._store.call(_st.OP_DELTA_READ, [n, off, 0], 1, inl)
+            raw = self._store.bulk(0, 96)
+            r = (0,) + struct.unpack_from("<8Q", raw, 32)
+        if r[0]:
+            raise _st.StoreError(f"device capture of {d.delta_id} failed with status {r[0]}")
+        h = _hex(r[1:9])
+        d.__dict__["_dev_hash"] = h
+        return h
+
+    def _indices(self) -> list[int]:
+        return [d._didx for d in self._deltas]
+
+    def compute_merkle_root(self) -> Optional[str]:
+        if not self._deltas:
+            return None
+        n, off, inl = self._store.index_args(self._indices())
+        r = _check(self._store.call(_st.OP_DELTA_MERKLE, [self.slot, n, off], 10, inl), "merkle")
+        return _hex(r[2:10]) if r[1] else None
+
+    def verify_chain(self) -> bool:
+        if not self._deltas:
+            return True
+        parity = _cfg.parity_mode()
+        blobs, recs = [], []
+        pos = 0
+        for d in self._deltas:
+            raw = _render(d)
+            blobs.append(raw)
+            ph = d.parent_hash
+            try:
+                hw = _words(d.delta_hash)
+            except (ValueError, TypeError):
+                hw = [0] * 8
+            try:
+                pw = [0xFFFFFFFF] * 8 if ph is None else _words(ph)
+            except (ValueError, TypeError):
+                pw = [0] * 8
+            recs.append((pos, len(raw), d._didx, hw, pw))
+            pos += (len(raw) + 63) & ~63
+        data = b"".join(b + b"\0" * (((len(b) + 63) & ~63) - len(b)) for b in blobs)
+        base = self._store.stage(data)
+        table = b"".join(
+            struct.pack("<QQq8I8I", base + o, ln, didx, *hw, *pw) for (o, ln, didx, hw, pw) in recs
+        )
+        toff = self._store.stage(table)
+        r = _check(self._store.call(_st.OP_DELTA_VERIFY, [self.slot, len(recs), toff, int(parity), 0], 3), "verify")
+        if parity:  # reference verify rewrites every stored hash with the recomputed one (Q02)
+            raw = self._store.bulk(0, 64 * len(recs))
+            for i, d in enumerate(self._deltas):
+                d.delta_hash = _hex(struct.unpack_from("<8Q", raw, 64 * i))
+        return bool(r[1])
+
+    @property
+    def deltas(self) -> list[DeviceDelta]:
+        return list(self._deltas)
+
+    @property
+    def turn_count(self) -> int:
+        return self._turn_counter
+
+    def export_records(self) -> list[dict]:
+        return [{"payload": d.record().decode("ascii"), "delta_hash": d.device_hash()} for d in self._deltas]
+
+    def prune_expired(self, retention_days: int) -> int:
+        cutoff = _now() - timedelta(days=retention_days)
+        keep = [d for d in self._deltas if d.timestamp >= cutoff]
+        n = len(self._deltas) - len(keep)
+        self._deltas = keep
+        return n
+
+
+class _NullParent:
+    """Attribute proxy rendering a delta with a null parent (json.dumps fallback)."""
+
+    def __init__(self, d) -> None:
+        self._d = d
+
+    def __getattr__(self, k):
+        return None if k == "parent_hash" else getattr(self._d, k)
+
+
+# ------------------------------------------------------------------ liability
+
+
+class DeviceVouchRecord(VouchRecord):
+    """A vouch edge view: identity on the host, bond state on the device."""
+
+    def __init__(self, store: GovernanceStore, edge: int, vouch_id, voucher_did, vouchee_did, session_id, pct,
+                 bonded, created_at, expiry) -> None:
+        self.__dict__.update(
+            _store=store, edge=edge, vouch_id=vouch_id, voucher_did=voucher_did, vouchee_did=vouchee_did,
+            session_id=session_id, bonded_sigma_pct=pct, bonded_amount=bonded, created_at=created_at,
+            expiry=expiry,
+        )
+
+    def _row(self):
+        return self._store.call(_st.OP_EDGE_READ, [self.edge], 3)
+
+    @property
+    def is_active(self) -> bool:  # type: ignore[override]
+        return bool(self._row()[1])
+
+    @is_active.setter
+    def is_active(self, v: bool) -> None:
+        if not v:
+            self._store.call(_st.OP_RELEASE_BOND, [self.edge, to_us(_now())], 1)
+        elif not self.is_active:
+            raise ValueError("a released bond cannot be re-activated")
+
+    @property
+    def released_at(self) -> Optional[datetime]:  # type: ignore[override]
+        r = self._row()
+        return from_us(_i64(r[2])) if not r[1] and _i64(r[2]) >= 0 else None
+
+    @released_at.setter
+    def released_at(self, v) -> None:
+        pass  # stamped by the device on release
+
+    def __repr__(self) -> str:
+        return (f"VouchRecord(vouch_id={self.vouch_id!r}, voucher_did={self.voucher_did!r}, "
+                f"vouchee_did={self.vouchee_did!r}, session_id={self.session_id!r}, edge={self.edge})")
+
+
+class DeviceVouchingEngine(VouchingEngine):
+    """Bond edges in the device vouch table, linked per (hypervisor, session)."""
+
+    def __init__(self, store: GovernanceStore, tenant: int, max_exposure: Optional[float] = None) -> None:
+        self._store = store
+        self._tenant = tenant
+        self.max_exposure = max_exposure or self.DEFAULT_MAX_EXPOSURE
+        self._by_id: dict[str, DeviceVouchRecord] = {}
+        self._by_edge: dict[int, DeviceVouchRecord] = {}
+        self._order: list[DeviceVouchRecord] = []
+
+    def _v(self, session_id: str, create: bool = False) -> int:
+        if create:
+            return self._store.liability_id(self._tenant, session_id)
+        return self._store.liability_lookup(self._tenant, session_id)
+
+    def vouch(self, voucher_did: str, vouchee_did: str, session_id: str, voucher_sigma: float,
+              bond_pct: Optional[float] = None, expiry: Optional[datetime] = None) -> DeviceVouchRecord:
+        st = self._store
+        v = self._v(session_id, create=True)
+        edge = st.alloc("E")
+        now = _now()
+        r = st.call(
+            _st.OP_VOUCH,
+            [v, st.agent_id(voucher_did), st.agent_id(vouchee_did), dbits(voucher_sigma),
+             _NAN if bond_pct is None else dbits(bond_pct), to_us(expiry) if expiry is not None else -1,
+             to_us(now), dbits(self.max_exposure), int(_cfg.parity_mode()), edge],
+            6,
+        )
+        code = r[0]
+        if code == 1:
+            raise VouchingError("Cannot vouch for yourself")
+        if code == 2:
+            raise VouchingError(
+                f"Voucher σ ({voucher_sigma:.2f}) below minimum ({self.MIN_VOUCHER_SCORE:.2f})"
+            )
+        if code == 3:
+            raise VouchingError(
+                f"Circular vouching detected: {vouchee_did} already vouches for "
+                f"{voucher_did} in session {session_id}"
+            )
+        if code == 4:
+            current, bonded, limit = bitsd(r[1]), bitsd(r[2]), bitsd(r[3])
+            raise VouchingError(
+                f"Voucher {voucher_did} would exceed max exposure "
+                f"({self.max_exposure:.0%} of σ). Current: {current:.3f}, "
+                f"requested: {bonded:.3f}, limit: {limit:.3f}"
+            )
+        _check(r, "vouch")
+        rec = DeviceVouchRecord(st, edge, _C.uuid4("vouch:"), voucher_did, vouchee_did, session_id,
+                                bitsd(r[4]), bitsd(r[2]), now, expiry)
+        self._by_id[rec.vouch_id] = rec
+        self._by_edge[edge] = rec
+        self._order.append(rec)
+        return rec
+
+    @property
+    def _vouches(self) -> dict[str, DeviceVouchRecord]:
+        return dict(self._by_id)
+
+    def compute_sigma_eff(self, vouchee_did: str, session_id: str, vouchee_sigma: float, risk_weight: float) -> float:
+        v = self._v(session_id)
+        r = self._store.call(
+            _st.OP_SIGMA_EFF,
+            [v, self._store.agent_id(vouchee_did), dbits(vouchee_sigma), dbits(risk_weight), to_us(_now())], 2,
+        )
+        return bitsd(r[1])
+
+    def _list(self, session_id: str, flt: int, who: Optional[str]) -> list[DeviceVouchRecord]:
+        v = self._v(session_id)
+        if v < 0:
+            return []
+        cap = 4096
+        r = self._store.call(
+            _st.OP_VOUCH_LIST,
+            [v, flt, self._store.agent_id(who) if who is not None else -1, to_us(_now()), 0, cap], 2,
+        )
+        n = r[1]
+        if n > cap:
+            raise _st.StoreError(f"{n} vouch edges exceed the listing buffer")
+        raw = self._store.bulk(0, 64 * n)
+        return [self._by_edge[struct.unpack_from("<q", raw, 64 * k)[0]] for k in range(n)]
+
+    def records(self, session_id: Optional[str] = None) -> list[DeviceVouchRecord]:
+        if session_id is not None:
+            return self._list(session_id, 0, None)
+        return list(self._order)
+
+    def get_vouchers_for(self, agent_did: str, session_id: str) -> list[DeviceVouchRecord]:
+        return self._list(session_id, 1, agent_did)
+
+    def _active_vouches_for(self, agent_did: str, session_id: str) -> list[DeviceVouchRecord]:
+        return self.get_vouchers_for(agent_did, session_id)
+
+    def get_total_exposure(self, voucher_did: str, session_id: str) -> float:
+        v = self._v(session_id)
+        if v < 0:
+            return 0
+        r = self._store.call(_st.OP_EXPOSURE, [v, self._store.agent_id(voucher_did), to_us(_now())], 2)
+        return bitsd(r[1])
+
+    def release_bond(self, vouch_id: str) -> None:
+        rec = self._by_id.get(vouch_id)
+        if rec is None:
+            raise VouchingError(f"Vouch {vouch_id} not found")
+        self._store.call(_st.OP_RELEASE_BOND, [rec.edge, to_us(_now())], 1)
+
+    def release_session_bonds(self, session_id: str) -> int:
+        v = self._v(session_id)
+        if v < 0:
+            return 0
+        return self._store.call(_st.OP_RELEASE_SESSION, [v, to_us(_now())], 2)[1]
+
+    def _creates_cycle(self, voucher_did: str, vouchee_did: str, session_id: str) -> bool:
+        raise NotImplementedError("the cycle check runs inside the device vouch command (K05)")
+
+
+class DeviceSlashingEngine(SlashingEngine):
+    """SlashingEngine whose blacklist/clip/release/cascade runs on the device (K06)."""
+
+    def __init__(self, vouching_engine: DeviceVouchingEngine) -> None:
+        super().__init__(vouching_engine)
+
+    def slash(self, vouchee_did: str, session_id: str, vouchee_sigma: float, risk_weight: float, reason: str,
+              agent_scores: dict[str, float], cascade_depth: int = 0) -> SlashResult:
+        ve: DeviceVouchingEngine = self._vouching  # type: ignore[assignment]
+        st = ve._store
+        v = ve._v(session_id)
+        if v < 0:  # no bonds were ever posted in this session: blacklist only
+            agent_scores[vouchee_did] = 0.0
+            res = SlashResult(_C.uuid4("slash:"), vouchee_did, vouchee_sigma, 0.0, [], reason, session_id,
+                              cascade_depth=cascade_depth)
+            self._slash_history.append(res)
+            return res
+        pairs = [(st.agent_id(k), float(s)) for k, s in agent_scores.items()]
+        raw = b"".join(struct.pack("<qd", a, s) for a, s in pairs) or b"\0" * 16
+        off = st.stage(raw)
+        out_cap = 1 << 16
+        scores_off = 8 * out_cap
+        r = st.call(
+            _st.OP_SLASH,
+            [v, st.agent_id(vouchee_did), dbits(vouchee_sigma), dbits(risk_weight), to_us(_now()), len(pairs), off,
+             0, out_cap, scores_off, cascade_depth],
+            3,
+        )
+        if r[0]:
+            raise _st.StoreError(f"device slash failed with status {r[0]} (scratch/output bound)")
+        words, nsc = r[1], r[2]
+        stream = struct.unpack(f"<{words}Q", st.bulk(0, 8 * words))
+        sc = st.bulk(scores_off, 16 * nsc)
+        for k in range(nsc):
+            a, s = struct.unpack_from("<qd", sc, 16 * k)
+            agent_scores[st.did(a)] = s
+        # rebuild SlashResults in pre-order; reasons chain "Cascade from <parent>: <reason>"
+        results: list[SlashResult] = []
+        reasons: dict[int, str] = {cascade_depth: reason}
+        parents: dict[int, str] = {}
+        i = 0
+        while i < words:
+            vee, depth, nclips, before = stream[i], stream[i + 1], stream[i + 2], bitsd(stream[i + 3])
+            i += 4
+            did = st.did(_i64(vee))
+            if depth > cascade_depth:
+                reasons[depth] = f"Cascade from {parents[depth - 1]}: {reasons[depth - 1]}"
+            parents[depth] = did
+            clips = []
+            for _ in range(nclips):
+                vr, b, a, e = stream[i], bitsd(stream[i + 1]), bitsd(stream[i + 2]), _i64(stream[i + 3])
+                i += 4
+                rec = ve._by_edge.get(e)
+                clips.append(VoucherClip(st.did(_i64(vr)), b, a, risk_weight, rec.vouch_id if rec else f"edge:{e}"))
+            res = SlashResult(_C.uuid4("slash:"), did, before, 0.0, clips, reasons[depth], session_id,
+                              cascade_depth=int(depth))
+            self._slash_history.append(res)
+            results.append(res)
+        return results[0]
+
+
+class DeviceCommitmentEngine(CommitmentEngine):
+    """Commitments of device sessions are the root/counters the terminate command wrote."""
+
+    def __init__(self, store: GovernanceStore) -> None:
+        super().__init__()
+        self._store = store
+        self._device: dict[str, DeviceSession] = {}
+
+    def _record(self, sso: DeviceSession) -> Optional[CommitmentRecord]:
+        r, parts = sso._read(True)
+        if not r[11]:
+            return None
+        return CommitmentRecord(
+            session_id=sso.session_id, merkle_root=_hex(r[20:28]),
+            participant_dids=[self._store.did(p[0]) for p in parts if p[2]],
+            delta_count=r[12], committed_at=from_us(r[11]),
+        )
+
+    def register(self, sso: DeviceSession) -> None:
+        self._device[sso.session_id] = sso
+
+    def get_commitment(self, session_id: str) -> Optional[CommitmentRecord]:
+        sso = self._device.get(session_id)
+        if sso is not None:
+            return self._record(sso)
+        return super().get_commitment(session_id)
+
+    def verify(self, session_id: str, expected_root: str) -> bool:
+        rec = self.get_commitment(session_id)
+        return rec is not None and rec.merkle_root == expected_root
+
+    @property
+    def _commitments_view(self) -> dict[str, CommitmentRecord]:
+        out = {}
+        for sid, sso in self._device.items():
+            rec = self._record(sso)
+            if rec is not None:
+                out[sid] = rec
+        out.update(self._commitments)
+        return out
+
+    @property
+    def commitment_count(self) -> int:
+        return len(self._commitments_view)
+
+    def all_commitments(self) -> list[CommitmentRecord]:
+        return list(self._commitments_view.values())
+
+
+# ------------------------------------------------------------------ sagas
+
+
+class DeviceSagaStep(SagaStep):
+    """Step view: FSM state, timestamps and retry counter live in the device step table."""
+
+    def __init__(self, store: GovernanceStore, slot: int, **kw) -> None:
+        self.__dict__.update(_store=store, slot=slot, execute_result=None, compensation_result=None, error=None)
+        for k, v in kw.items():
+            self.__dict__[k] = v
+
+    def _row(self):
+        return self._store.call(_st.OP_STEP_READ, [self.slot], 5)
+
+    @property
+    def state(self) -> StepState:  # type: ignore[override]
+        return _STEPS[self._row()[1]]
+
+    @state.setter
+    def state(self, s: StepState) -> None:  # direct write outside the FSM (reference retry reset / no-undo path)
+        self._store.call(_st.OP_STEP_SET, [self.slot, _STEPS.index(StepState(s)), -1], 1)
+
+    @property
+    def retry_count(self) -> int:  # type: ignore[override]
+        return self._row()[2]
+
+    @retry_count.setter
+    def retry_count(self, n: int) -> None:
+        self._store.call(_st.OP_STEP_SET, [self.slot, self._row()[1], int(n)], 1)
+
+    @property
+    def started_at(self) -> Optional[datetime]:  # type: ignore[override]
+        t = self._row()[3]
+        return from_us(t) if t else None
+
+    @started_at.setter
+    def started_at(self, v) -> None:
+        pass
+
+    @property
+    def completed_at(self) -> Optional[datetime]:  # type: ignore[override]
+        t = self._row()[4]
+        return from_us(t) if t else None
+
+    @completed_at.setter
+    def completed_at(self, v) -> None:
+        pass
+
+    def transition(self, new_state: StepState, retry: int = -1) -> None:
+        to = _STEPS.index(StepState(new_state))
+        r = self._store.call(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], 2)
+        if r[0]:
+            frm = _STEPS[r[1]]
+            allowed = STEP_TRANSITIONS.get(frm, ())
+            raise SagaStateError(
+                f"Invalid step transition: {frm.value} → {StepState(new_state).value}. "
+                f"Allowed: {[s.value for s in allowed]}"
+            )
+
+    def __eq__(self, other) -> bool:
+        return self is other
+
+    __hash__ = object.__hash__
+
+    def __repr__(self) -> str:
+        return f"SagaStep(step_id={self.step_id!r}, action_id={self.action_id!r}, slot={self.slot})"
+
+
+class DeviceSaga(Saga):
+    """Saga view: FSM state and timestamps in the device saga table."""
+
+    def __init__(self, store: GovernanceStore, slot: int, saga_id: str, session_id: str) -> None:
+        self.__dict__.update(_store=store, slot=slot, saga_id=saga_id, session_id=session_id, steps=[], error=None)
+
+    def _hdr(self):
+        return self._store.call(_st.OP_SAGA_READ, [self.slot, 0, 0, 0], 5)
+
+    @property
+    def state(self) -> SagaState:  # type: ignore[override]
+        return _SAGAS[self._hdr()[1]]
+
+    @state.setter
+    def state(self, s) -> None:
+        raise AttributeError("saga state changes only through transition()")
+
+    @property
+    def created_at(self) -> datetime:  # type: ignore[override]
+        return from_us(self._hdr()[2])
+
+    @created_at.setter
+    def created_at(self, v) -> None:
+        pass
+
+    @property
+    def completed_at(self) -> Optional[datetime]:  # type: ignore[override]
+        t = self._hdr()[3]
+        return from_us(t) if t else None
+
+    @completed_at.setter
+    def completed_at(self, v) -> None:
+        pass
+
+    def transition(self, new_state: SagaState) -> None:
+        to = _SAGAS.index(SagaState(new_state))
+        r = self._store.call(_st.OP_SAGA_TRANSITION, [self.slot, to, to_us(_now())], 2)
+        if r[0]:
+            frm = _SAGAS[r[1]]
+            allowed = SAGA_TRANSITIONS.get(frm, ())
+            raise SagaStateError(
+                f"Invalid saga transition: {frm.value} → {SagaState(new_state).value}. "
+                f"Allowed: {[s.value for s in allowed]}"
+            )
+
+    def _step_states(self) -> list[StepState]:
+        n, off, inl = self._store.index_args([s.slot for s in self.steps])
+        self._store.call(_st.OP_SAGA_READ, [self.slot, n, off, 0], 1, inl)
+        raw = self._store.bulk(0, 32 * n)
+        return [_STEPS[struct.unpack_from("<Q", raw, 32 * k)[0] & 0xFF] for k in range(n)]
+
+    @property
+    def committed_steps(self) -> list[SagaStep]:
+        return [s for s, stt in zip(self.steps, self._step_states()) if stt is StepState.COMMITTED]
+
+    @property
+    def committed_steps_reversed(self) -> list[SagaStep]:
+        """K14 on the device: committed steps in reverse order."""
+        n, off, inl = self._store.index_args([s.slot for s in self.steps])
+        r = self._store.call(_st.OP_SAGA_PLAN, [self.slot, n, off, 0], 6, inl)
+        m = r[5]
+        raw = self._store.bulk(0, 8 * m)
+        return [self.steps[struct.unpack_from("<Q", raw, 8 * k)[0]] for k in range(m)]
+
+    def __eq__(self, other) -> bool:
+        return self is other
+
+    __hash__ = object.__hash__
+
+    def __repr__(self) -> str:
+        return f"Saga(saga_id={self.saga_id!r}, session_id={self.session_id!r}, slot={self.slot})"
+
+
+class DeviceSagaOrchestrator(SagaOrchestrator):
+    """SagaOrchestrator with the step/saga FSM (K13) and compensation plan (K14) on the device.
+
+    Executors and compensators are user coroutines and stay on the host event
+    loop; every state change they cause is a device command.
+    """
+
+    def __init__(self, store: GovernanceStore) -> None:
+        self._store = store
+        self._sagas: dict[str, DeviceSaga] = {}
+
+    def create_saga(self, session_id: str) -> DeviceSaga:
+        slot = self._store.alloc("G")
+        saga = DeviceSaga(self._store, slot, _C.uuid4("saga:"), session_id)
+        self._store.post(_st.OP_SAGA_CREATE, [slot, to_us(_now())])
+        self._sagas[saga.saga_id] = saga
+        return saga
+
+    def add_step(self, saga_id: str, action_id: str, agent_did: str, execute_api: str,
+                 undo_api: Optional[str] = None, timeout_seconds: int = 300, max_retries: int = 0) -> DeviceSagaStep:
+        saga = self._get_saga(saga_id)
+        slot = self._store.alloc("T")
+        step = DeviceSagaStep(
+            self._store, slot, step_id=_C.uuid4("step:"), action_id=action_id, agent_did=agent_did,
+            execute_api=execute_api, undo_api=undo_api, timeout_seconds=timeout_seconds, max_retries=max_retries,
+        )
+        self._store.post(_st.OP_STEP_ADD, [saga.slot, slot, int(bool(undo_api)), int(max_retries)])
+        saga.steps.append(step)
+        return step
+
+    async def execute_step(self, saga_id: str, step_id: str, executor: Callable[..., Any]) -> Any:
+        saga = self._get_saga(saga_id)
+        step = self._get_step(saga, step_id)
+        attempts = 1 + step.max_retries
+        last: Optional[Exception] = None
+        for attempt in range(attempts):
+            step.transition(StepState.EXECUTING, retry=attempt)
+            try:
+                result = await await_with_timeout(executor(), step.timeout_seconds)
+            except asyncio.TimeoutError:
+                last = SagaTimeoutError(
+                    f"Step {step_id} timed out after {step.timeout_seconds}s "
+                    f"(attempt {attempt + 1}/{attempts})"
+                )
+            except Exception as e:  # executor failure
+                last = e
+            else:
+                step.execute_result = result
+                step.transition(StepState.COMMITTED)
+                return result
+            step.error = str(last)
+            step.transition(StepState.FAILED)
+            if attempt < attempts - 1:
+                step.state = StepState.PENDING
+                step.error = None
+                await asyncio.sleep(self.DEFAULT_RETRY_DELAY_SECONDS * (attempt + 1))
+        if last is not None:
+            raise last
+        raise SagaStateError("Step execution failed with no error captured")
+
+    async def compensate(self, saga_id: str, compensator: Callable[[SagaStep], Any]) -> list[SagaStep]:
+        saga = self._get_saga(saga_id)
+        saga.transition(SagaState.COMPENSATING)
+        failed: list[SagaStep] = []
+        for step in saga.committed_steps_reversed:
+            if not step.undo_api:
+                step.state = StepState.COMPENSATION_FAILED
+                step.error = "No Undo_API available"
+                failed.append(step)
+                continue
+            step.transition(StepState.COMPENSATING)
+            try:
+                res = await await_with_timeout(compensator(step), step.timeout_seconds)
+            except asyncio.TimeoutError:
+                step.error = f"Compensation timed out after {step.timeout_seconds}s"
+            except Exception as e:
+                step.error = f"Compensation failed: {e}"
+            else:
+                step.compensation_result = res
+                step.transition(StepState.COMPENSATED)
+                continue
+            step.transition(StepState.COMPENSATION_FAILED)
+            failed.append(step)
+        if failed:
+            saga.transition(SagaState.ESCALATED)
+            saga.error = f"{len(failed)} step(s) failed compensation — Joint Liability slashing triggered"
+        else:
+            saga.transition(SagaState.COMPLETED)
+        return failed
+
+
+def session_views(store: GovernanceStore, sso: DeviceSession):
+    """(delta engine, saga orchestrator) for a device session."""
+    return DeviceDeltaEngine(store, sso.slot, sso.session_id), DeviceSagaOrchestrator(store)
+
+
+__all__ = [
+    "DeviceSession", "DeviceDelta", "DeviceDeltaEngine", "DeviceVouchRecord", "DeviceVouchingEngine",
+    "DeviceSlashingEngine", "DeviceCommitmentEngine", "DeviceSaga", "DeviceSagaStep", "DeviceSagaOrchestrator",
+]

@@ -15,6 +15,10 @@ parity_mode                 AHV_PARITY_MODE   reproduce reference quirks bit-for
                                      units Q21)
 emit_events                 AHV_EMIT_EVENTS   Hypervisor emits lifecycle events (Q03)
 device                      AHV_DEVICE        torch device of the batched engine
+store                       AHV_STORE         where ``Hypervisor()`` keeps its state: ``auto``
+                                     (the device store on a HIP device when one is
+                                     visible, else the host engines), ``cuda``,
+                                     ``cpu`` (host twin of the device store), ``host``
 session_capacity            AHV_SESSION_CAPACITY  device session-table rows per rank
 agent_capacity              AHV_AGENT_CAPACITY    device agent-table rows per rank
 vouch_capacity              AHV_VOUCH_CAPACITY    device vouch-edge rows per rank
@@ -47,6 +51,7 @@ class HypervisorRuntimeConfig:
     parity_mode: bool = False
     emit_events: bool = True
     device: str = "cuda"
+    store: str = "auto"
     session_capacity: int = 1 << 20
     agent_capacity: int = 1 << 22
     vouch_capacity: int = 1 << 22
@@ -59,6 +64,7 @@ class HypervisorRuntimeConfig:
             parity_mode=_env_bool("AHV_PARITY_MODE", False),
             emit_events=_env_bool("AHV_EMIT_EVENTS", True),
             device=os.environ.get("AHV_DEVICE", "cuda"),
+            store=os.environ.get("AHV_STORE", "auto"),
             session_capacity=_env_int("AHV_SESSION_CAPACITY", 1 << 20),
             agent_capacity=_env_int("AHV_AGENT_CAPACITY", 1 << 22),
             vouch_capacity=_env_int("AHV_VOUCH_CAPACITY", 1 << 22),
@@ -75,6 +81,19 @@ RUNTIME = HypervisorRuntimeConfig.from_env()
 
 def parity_mode() -> bool:
     return RUNTIME.parity_mode
+
+
+def store_mode(device=None) -> str:
+    """Resolve a ``Hypervisor(device=...)`` argument to ``host`` / ``cpu`` / ``cuda[:i]``."""
+    d = RUNTIME.store if device is None else str(device)
+    if d in ("", "auto"):
+        try:
+            import torch
+
+            return "cuda" if torch.cuda.is_available() else "host"
+        except Exception:
+            return "host"
+    return d
 
 
 def set_parity_mode(on: bool) -> None:

@@ -29,6 +29,16 @@ Additions: an optional ``event_bus`` that receives lifecycle events (the
 reference never emitted, Q03); an optional ``declared_history`` for join (Q23);
 and :meth:`Hypervisor.pipeline_batch`, which runs the same governance pipeline
 for thousands of sessions at once on the MI355X device engine.
+
+Device-authoritative mode (``Hypervisor(device="cuda")``, the default when a HIP
+device is visible; ``AHV_STORE``): sessions, participants, the audit chain,
+vouch bonds, sagas and commitments live in the gfx950 state store
+(:mod:`agent_hypervisor_amd.models.store`) and every call below is a command to
+its resident worker (:mod:`hypervisor._device`) — the join ring gate (K01),
+capture hashing (K08), the terminate pipeline (K09 root → commit → K07 bond
+release → GC → archive) and the slash cascade (K06) all run on the device.
+``device="cpu"`` runs the same command processor on the host (twin for tests);
+``device="host"`` keeps the pure host engines.
 """
 
 from __future__ import annotations
@@ -59,12 +69,12 @@ class ManagedSession:
 
     __slots__ = ("sso", "reversibility", "delta_engine", "saga")
 
-    def __init__(self, sso: SharedSessionObject) -> None:
+    def __init__(self, sso: SharedSessionObject, delta_engine=None, saga=None) -> None:
         self.sso = sso
         sid = sso.session_id
         self.reversibility = ReversibilityRegistry(sid)
-        self.delta_engine = DeltaEngine(sid)
-        self.saga = SagaOrchestrator()
+        self.delta_engine = delta_engine if delta_engine is not None else DeltaEngine(sid)
+        self.saga = saga if saga is not None else SagaOrchestrator()
 
 
 class Hypervisor:
@@ -77,13 +87,29 @@ class Hypervisor:
         iatp: Optional[Any] = None,
         event_bus: Optional[Any] = None,
         demote_on_slash: bool = False,
+        device: Optional[str] = None,
     ) -> None:
-        self.vouching = VouchingEngine(max_exposure=max_exposure)
-        self.slashing = SlashingEngine(self.vouching)
+        from hypervisor.config import store_mode
+
+        mode = store_mode(device)
+        self._store = None
+        if mode == "host":
+            self.vouching = VouchingEngine(max_exposure=max_exposure)
+            self.slashing = SlashingEngine(self.vouching)
+            self.commitment = CommitmentEngine()
+        else:
+            from agent_hypervisor_amd.models.store import shared_store
+            from hypervisor import _device
+
+            self._store = shared_store(mode)
+            self._tenant = self._store.new_tenant()
+            self.vouching = _device.DeviceVouchingEngine(self._store, self._tenant, max_exposure)
+            self.slashing = _device.DeviceSlashingEngine(self.vouching)
+            self.commitment = _device.DeviceCommitmentEngine(self._store)
+        self.device = mode
         self.ring_enforcer = RingEnforcer()
         self.classifier = ActionClassifier()
         self.verifier = TransactionHistoryVerifier()
-        self.commitment = CommitmentEngine()
         self.gc = EphemeralGC(retention_policy)
         self.nexus = nexus
         self.cmvk = cmvk
@@ -103,9 +129,15 @@ class Hypervisor:
 
     # -- lifecycle -------------------------------------------------------------
     async def create_session(self, config: SessionConfig, creator_did: str) -> ManagedSession:
-        sso = SharedSessionObject(config=config, creator_did=creator_did)
-        sso.begin_handshake()
-        managed = ManagedSession(sso)
+        if self._store is not None:
+            from hypervisor import _device
+
+            sso = _device.DeviceSession(self._store, config, creator_did)  # created in HANDSHAKING
+            managed = ManagedSession(sso, *_device.session_views(self._store, sso))
+        else:
+            sso = SharedSessionObject(config=config, creator_did=creator_did)
+            sso.begin_handshake()
+            managed = ManagedSession(sso)
         self._sessions[sso.session_id] = managed
         if self.event_bus is not None:
             from hypervisor.observability.event_bus import EventType
@@ -150,10 +182,13 @@ class Hypervisor:
             elif agent_history:
                 sigma_eff = min(sigma_raw, self.nexus.resolve_sigma(agent_did, history=agent_history))
 
-        ring = self.ring_enforcer.compute_ring(sigma_eff)
-        if not verification.is_trustworthy:
-            ring = ExecutionRing.RING_3_SANDBOX
-        managed.sso.join(agent_did=agent_did, sigma_raw=sigma_raw, sigma_eff=sigma_eff, ring=ring)
+        if self._store is not None:  # ring gate (K01) + admission on the device
+            ring = managed.sso.join_gated(agent_did, sigma_raw, sigma_eff, verification.is_trustworthy)
+        else:
+            ring = self.ring_enforcer.compute_ring(sigma_eff)
+            if not verification.is_trustworthy:
+                ring = ExecutionRing.RING_3_SANDBOX
+            managed.sso.join(agent_did=agent_did, sigma_raw=sigma_raw, sigma_eff=sigma_eff, ring=ring)
         if self.event_bus is not None:
             from hypervisor.observability.event_bus import EventType
 
@@ -170,6 +205,8 @@ class Hypervisor:
 
     async def terminate_session(self, session_id: str) -> Optional[str]:
         managed = self._get_session(session_id)
+        if self._store is not None:
+            return self._terminate_device(session_id, managed)
         sso = managed.sso
         sso.terminate()
         de = managed.delta_engine
@@ -186,6 +223,42 @@ class Hypervisor:
         self.vouching.release_session_bonds(session_id)
         self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de, delta_count=de.turn_count)
         sso.archive()
+        if self.event_bus is not None:
+            from hypervisor.observability.event_bus import EventType
+
+            self._emit(EventType.SESSION_TERMINATED, session_id, merkle_root=root)
+            if root:
+                self._emit(EventType.AUDIT_COMMITTED, session_id, merkle_root=root)
+            self._emit(EventType.AUDIT_GC_COLLECTED, session_id)
+            self._emit(EventType.SESSION_ARCHIVED, session_id)
+        return root
+
+    def _terminate_device(self, session_id: str, managed: ManagedSession) -> Optional[str]:
+        """One device command: terminate → Merkle root (K09) → commit → release the
+        session's bonds (K07) → GC retention count → archive."""
+        from datetime import timedelta
+
+        from agent_hypervisor_amd.models import store as _st
+        from hypervisor._clock import now as _now, to_us
+        from hypervisor._device import _check, _hex, _lifecycle
+        from hypervisor.models import SessionState
+
+        sso, de, st = managed.sso, managed.delta_engine, self._store
+        now = _now()
+        v = st.liability_lookup(self._tenant, session_id)
+        cutoff = now - timedelta(days=self.gc.policy.delta_retention_days)
+        n, off, inl = st.index_args(de._indices())
+        r = st.call(
+            _st.OP_SESS_CLOSE,
+            [sso.slot, n, off, to_us(now), v, to_us(cutoff), int(bool(sso.config.enable_audit))], 13, inl,
+        )
+        if r[0] == _st.ST_BAD_STATE:
+            raise _lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
+        _check(r, "terminate")
+        root = _hex(r[2:10]) if r[1] else None
+        if root:
+            self.commitment.register(sso)
+        self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de, delta_count=de.turn_count)
         if self.event_bus is not None:
             from hypervisor.observability.event_bus import EventType
 
@@ -232,8 +305,12 @@ class Hypervisor:
             if self.demote_on_slash:
                 for p in managed.sso.participants:
                     if p.agent_did in scores:
-                        p.sigma_eff = scores[p.agent_did]
-                        p.ring = max(p.ring, self.ring_enforcer.compute_ring(p.sigma_eff), key=int)
+                        new_ring = max(p.ring, self.ring_enforcer.compute_ring(scores[p.agent_did]), key=int)
+                        if self._store is not None:
+                            managed.sso.set_sigma(p.agent_did, scores[p.agent_did], new_ring)
+                        else:
+                            p.sigma_eff = scores[p.agent_did]
+                            p.ring = new_ring
             if self.nexus:
                 self.nexus.report_slash(
                     agent_did=agent_did,

@@ -1,0 +1,56 @@
+"""GPU probe of the device state store: one reference pipeline through
+``Hypervisor(device="cuda")`` checked against host hashing, then p50 latency."""
+import asyncio
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from agent_hypervisor_amd._native import C  # noqa: E402
+from hypervisor import Hypervisor, SessionConfig  # noqa: E402
+from hypervisor.audit.delta import SemanticDelta, VFSChange, delta_digest  # noqa: E402
+
+
+async def one(hv):
+    s = await hv.create_session(config=SessionConfig(enable_audit=True), creator_did="did:mesh:admin")
+    sid = s.sso.session_id
+    await hv.join_session(sid, "did:mesh:a", sigma_raw=0.8)
+    await hv.activate_session(sid)
+    ds = [s.delta_engine.capture("did:mesh:a", [VFSChange(path=f"/f{i}", operation="add", content_hash=f"h{i}")])
+          for i in range(3)]
+    saga = s.saga.create_saga(sid)
+    step = s.saga.add_step(saga.saga_id, "action", "did:mesh:a", "/api/action")
+    await s.saga.execute_step(saga.saga_id, step.step_id, executor=lambda: asyncio.sleep(0))
+    root = await hv.terminate_session(sid)
+    return s, ds, root
+
+
+async def main():
+    dev = sys.argv[1] if len(sys.argv) > 1 else "cuda"
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
+    t0 = time.perf_counter()
+    hv = Hypervisor(device=dev)
+    s, ds, root = await one(hv)
+    print(f"first pipeline (incl. store init) {1e3 * (time.perf_counter() - t0):.1f} ms", flush=True)
+    for d in ds:
+        hd = SemanticDelta(d.delta_id, d.turn_id, d.session_id, d.agent_did, d.timestamp, d.changes, d.parent_hash)
+        assert delta_digest(hd) == d.delta_hash, "device delta digest != host"
+    assert C.merkle_root([d.delta_hash for d in ds]) == root, "device root != host"
+    assert s.delta_engine.verify_chain()
+    print("parity ok", root, flush=True)
+    times = []
+    for i in range(100 + iters):
+        t0 = time.perf_counter_ns()
+        await one(Hypervisor(device=dev))
+        if i >= 100:
+            times.append(time.perf_counter_ns() - t0)
+    p50 = statistics.median(times) / 1e3
+    out = {"device": dev, "p50_us": round(p50, 2), "mean_us": round(statistics.mean(times) / 1e3, 2),
+           "p90_us": round(sorted(times)[int(0.9 * len(times))] / 1e3, 2), "info": hv._store.info()}
+    print(json.dumps(out), flush=True)
+
+
+asyncio.run(main())
