@@ -14,9 +14,18 @@ random-init σ), then a cross-rank RCCL all-reduce of the step's governance
 counters (collective X04) — weak scaling, sessions sharded data-parallel.
 
 Also reported (not the headline value):
-* ``scalar_p50_us`` — p50 of the single-session pipeline through the public
-  ``Hypervisor`` API with the reference harness methodology (host path);
+* ``device_p50_us`` — p50 of the single-session pipeline through the public
+  ``Hypervisor(device="cuda")`` API, reference harness methodology (2,000
+  iterations after warm-up): every state change, ring gate, audit digest,
+  Merkle root, bond release and saga transition is executed by the resident
+  gfx950 store worker (hypervisor/_device.py, csrc/hip/store_worker.hip);
+* ``scalar_p50_us`` — the same harness on the pure host engines (CPU only);
 * ``batch_p50_ms`` — p50 wall time of one synchronised pipeline step.
+
+``vs_baseline`` divides the batched GPU throughput by the reference's
+single-threaded Python pipeline rate — a capability ratio, not a like-for-like
+one; ``device_vs_baseline_p50`` compares like with like (one session, public
+API, same harness).
 
 Launch: ``python bench.py`` (1 GPU) or via ``torch.distributed.run`` for N GPUs.
 """
@@ -42,13 +51,16 @@ BASELINE_P50_US = 267.5
 METRIC = "p50 pipeline latency (µs) + session-ops/sec, bench_hypervisor.py at 1/2/4/8 GPU"
 
 
-def scalar_pipeline_p50(iters: int = 2000) -> tuple[float, float]:
-    """Reference-harness timing of the public-API pipeline (bench_hypervisor.py:217-239)."""
+def scalar_pipeline_p50(iters: int = 2000, device: str = "host") -> tuple[float, float]:
+    """Reference-harness timing of the public-API pipeline (bench_hypervisor.py:217-239).
+
+    ``device="host"``: pure host engines; ``device="cuda"``: the device-authoritative
+    store (every call is a command to the gfx950 worker)."""
     from hypervisor import Hypervisor, SessionConfig
     from hypervisor.audit.delta import VFSChange
 
     async def one():
-        hv = Hypervisor()
+        hv = Hypervisor(device=device)
         s = await hv.create_session(config=SessionConfig(enable_audit=True), creator_did="did:mesh:admin")
         sid = s.sso.session_id
         await hv.join_session(sid, "did:mesh:a", sigma_raw=0.8)
@@ -204,9 +216,11 @@ def main() -> None:
         elapsed = float(e.item())
     totals = last.cpu().tolist()
 
-    scalar_p50 = scalar_mean = None
+    scalar_p50 = scalar_mean = device_p50 = device_mean = None
     if rank == 0 and not args.no_scalar:
-        scalar_p50, scalar_mean = scalar_pipeline_p50(args.scalar_iters)
+        scalar_p50, scalar_mean = scalar_pipeline_p50(args.scalar_iters, "host")
+        if dev.type == "cuda":
+            device_p50, device_mean = scalar_pipeline_p50(args.scalar_iters, "cuda")
 
     if rank == 0:
         total_sessions = S * world * args.steps
@@ -234,6 +248,10 @@ def main() -> None:
                 "deltas_per_session": args.deltas,
             },
             "batch_p50_ms": round(statistics.median(lat) * 1000.0, 4),
+            "vs_baseline_note": "batched GPU throughput / single-threaded Python reference rate (not like-for-like)",
+            "device_p50_us": round(device_p50, 2) if device_p50 is not None else None,
+            "device_mean_us": round(device_mean, 2) if device_mean is not None else None,
+            "device_vs_baseline_p50": round(BASELINE_P50_US / device_p50, 3) if device_p50 else None,
             "scalar_p50_us": round(scalar_p50, 2) if scalar_p50 is not None else None,
             "scalar_mean_us": round(scalar_mean, 2) if scalar_mean is not None else None,
             "scalar_vs_baseline_p50": round(BASELINE_P50_US / scalar_p50, 2) if scalar_p50 else None,

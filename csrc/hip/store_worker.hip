@@ -1,23 +1,37 @@
 // Resident command worker of the device state store (csrc/include/ahv/store.h).
 //
-// One wave (64 lanes) on one CU polls the command ring — 512-byte slots in
-// fine-grained device memory that the host writes through the PCIe BAR — and
-// executes each command against the HBM tables.  Measured on MI355X
-// (scripts/exp/doorbell2.hip, profiles/store_transport_r2.md): one host→device→
-// host round trip of a 512-byte command is ≈3.1 µs p50, against ≈12 µs for a
-// kernel launch + stream sync.
+// One workgroup of two waves on one CU:
 //
-// Lifetime: a resident wave shares its hardware queue with whatever streams HIP
-// maps there, so it must not linger — kernels queued behind it (and any device
-// synchronize) wait until it exits.  The worker therefore exits after
-// `idle_ticks` of the 100 MHz real-time counter without a command, after
-// `max_ticks` in total, or on OP_STOP; the host relaunches it on the next
-// command (≈12 µs).  Every exit path is reached by the whole wave.
+//   wave 0 — command wave: polls the command ring (512-byte slots in fine-grained
+//            device memory the host writes through the PCIe BAR), executes each
+//            command against the HBM tables and writes its result slot.  An
+//            audit capture is only *recorded* here (delta row, chain links) and
+//            queued for wave 1, so lifecycle / saga / liability commands that
+//            follow are answered while the digest is still being computed.
+//   wave 1 — hash engine: pops capture jobs from an LDS ring in order, stages the
+//            record into LDS as SHA-256 message words with the parent digest
+//            spliced in (all 64 lanes), runs the serial compression on lane 0
+//            (the chain is inherently serial: ≈2.4 µs per 64-byte block on one
+//            lane, scripts/exp/doorbell2.hip) and completes the capture's result.
+//
+// Commands that read audit state (Merkle root, verify, terminate, reads, FLUSH,
+// NOP = host drain) wait until wave 1 has drained (`needs_drain`).
+//
+// Measured transport (scripts/exp/doorbell2.hip): one host→device→host round
+// trip of a 512-byte command ≈3.1 µs p50, vs ≈12 µs for a kernel launch + sync.
+//
+// Lifetime: a resident workgroup shares its hardware queue with whatever streams
+// HIP maps there, so it must not linger — kernels queued behind it (and a device
+// synchronize) wait until it exits.  It exits after `idle_ticks` of the 100 MHz
+// real-time counter without a command, after `max_ticks` in total, or on
+// OP_STOP; the host relaunches it on the next command.  Both waves reach the
+// exit: wave 0 drains wave 1, raises `stop`, and waits for wave 1's goodbye
+// before clearing the host-visible `alive` word.
 //
 // Memory: results and bulk outputs go to pinned host memory with system-scope
-// stores; the result's sequence word is written last, after a system release
-// fence.  `tail` (device memory) carries the next expected sequence number
-// across relaunches.
+// stores, the sequence word last after a system release fence; `tail` (pinned
+// host memory) carries the next expected sequence number across relaunches.
+// Waves hand off through LDS with workgroup-scope release/acquire.
 #include <hip/hip_runtime.h>
 
 #include "ahv/store.h"
@@ -25,18 +39,65 @@
 namespace ahv {
 namespace store {
 
+constexpr int kJobs = 64;  // LDS capture-job ring
+
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
-__global__ __launch_bounds__(64) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
-                                                          uint64_t* res, uint8_t* bulk, uint64_t* alive,
-                                                          int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks) {
+__global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
+                                                           uint64_t* res, uint8_t* bulk, uint64_t* alive,
+                                                           int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks) {
   __shared__ uint64_t inl[kInlineWords];
-  __shared__ uint32_t lds[kLdsWords];
-  const int lane = threadIdx.x;
-  const Lanes L{lane, 64, lds};
+  __shared__ uint32_t lds1[kLdsWords];      // wave 1: capture message staging
+  __shared__ uint32_t lds0[kLdsWords / 4];  // wave 0: staging for its own (rare) in-place hashing
+  __shared__ HashJob jobs[kJobs];
+  __shared__ uint32_t q_head, q_done, stop, bye;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) {
+    q_head = 0;
+    q_done = 0;
+    stop = 0;
+    bye = 0;
+  }
+  __syncthreads();  // the only workgroup barrier: both waves pass it once
+
+  if (wave == 1) {
+    // ------------------------------------------------------------ hash engine
+    const Lanes L{lane, 64, lds1};
+    uint32_t done = 0;
+    for (;;) {
+      const uint32_t head = lds_acquire(&q_head);
+      if (head == done) {
+        if (lds_acquire(&stop)) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      const HashJob j = jobs[done % kJobs];
+      uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;
+      capture_finish(L, t, j, r);
+      if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // digest row + result words before the sequence word
+        out64(r, j.seq + 1);
+      }
+      ++done;
+      if (lane == 0) lds_release(&q_done, done);
+    }
+    if (lane == 0) lds_release(&bye, 1u);
+    return;
+  }
+
+  // ------------------------------------------------------------ command wave
+  const Lanes L{lane, 64, lds0};
   uint64_t next = static_cast<uint64_t>(__hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  uint32_t queued = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t last = t0;
   for (;;) {
@@ -57,23 +118,39 @@ __global__ __launch_bounds__(64) void store_worker_kernel(Tables t, const uint64
 #pragma unroll
     for (int k = 0; k < kArgs; ++k) c.a[k] = __shfl(w, 3 + k);
     if (lane >= 16) inl[lane - 16] = w;
-    __syncthreads();
+    L.sync();
     c.inl = inl;
+    if (needs_drain(c.op)) {
+      while (lds_acquire(&q_done) != queued) __builtin_amdgcn_s_sleep(1);
+    }
+    if (c.op == OP_DELTA_CAPTURE) {
+      while (queued - lds_acquire(&q_done) >= static_cast<uint32_t>(kJobs)) __builtin_amdgcn_s_sleep(1);
+    }
     if (c.op == OP_ACQUIRE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     uint64_t* r = res + (next % static_cast<uint64_t>(nslots)) * kResWords;
-    const bool go_on = store_exec(L, t, c, r, bulk);
+    HashJob job;
+    const int rc = store_exec(L, t, c, next, r, bulk, &job);
     if (c.op == OP_FLUSH) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __syncthreads();
-    if (lane == 0) {
-      __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    L.sync();
+    if (rc == EXEC_DEFERRED) {
+      if (lane == 0) {
+        jobs[queued % kJobs] = job;
+        lds_release(&q_head, queued + 1);  // the capture's global row writes precede this release
+      }
+      ++queued;
+    } else if (lane == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       out64(r, next + 1);
     }
+    if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     ++next;
     last = __builtin_amdgcn_s_memrealtime();
-    if (!go_on) break;
+    if (rc == EXEC_STOP) break;
   }
-  __syncthreads();
+  // drain the hash engine, stop it, wait for its goodbye, then release the queue
+  while (lds_acquire(&q_done) != queued) __builtin_amdgcn_s_sleep(1);
+  if (lane == 0) lds_release(&stop, 1u);
+  while (!lds_acquire(&bye)) __builtin_amdgcn_s_sleep(1);
   if (lane == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -83,11 +160,11 @@ __global__ __launch_bounds__(64) void store_worker_kernel(Tables t, const uint64
 }  // namespace store
 }  // namespace ahv
 
-// Host-callable launcher (one wave, one workgroup).
+// Host-callable launcher (one workgroup: command wave + hash-engine wave).
 extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64_t* ring, int64_t nslots,
                                        uint64_t* res, uint8_t* bulk, uint64_t* alive, int64_t* tail,
                                        uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream) {
-  hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(64), 0, stream, *t, ring, nslots, res, bulk,
+  hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(128), 0, stream, *t, ring, nslots, res, bulk,
                      alive, tail, idle_ticks, max_ticks);
   return static_cast<int>(hipGetLastError());
 }

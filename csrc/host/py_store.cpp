@@ -77,9 +77,9 @@ class Store {
       hip_check(hipHostMalloc(reinterpret_cast<void**>(&bulk_), static_cast<size_t>(bulk_cap_), hipHostMallocCoherent),
                 "store bulk");
       hip_check(hipHostMalloc(reinterpret_cast<void**>(&alive_), 64, hipHostMallocCoherent), "store ctl");
-      hip_check(hipMalloc(reinterpret_cast<void**>(&tail_), 64), "store tail");
+      hip_check(hipHostMalloc(reinterpret_cast<void**>(&tail_), 64, hipHostMallocCoherent), "store tail");
       hip_check(hipMemset(ring_, 0, ring_bytes), "memset ring");
-      hip_check(hipMemset(tail_, 0, 64), "memset tail");
+      *tail_ = 0;
       hip_check(hipDeviceSynchronize(), "store init sync");
       hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "store stream");
       idle_ticks_ = static_cast<uint64_t>(idle_us) * 100;   // s_memrealtime: 100 MHz
@@ -111,7 +111,7 @@ class Store {
       (void)hipHostFree(res_);
       (void)hipHostFree(bulk_);
       (void)hipHostFree(alive_);
-      (void)hipFree(tail_);
+      (void)hipHostFree(tail_);
       if (stream_) (void)hipStreamDestroy(stream_);
     } else {
       std::free(ring_);
@@ -128,8 +128,10 @@ class Store {
     if (closed_) return;
     closed_ = true;
     if (gpu_ && launches_ > 0) {
-      const uint64_t q = post_raw(OP_STOP, nullptr, 0, nullptr, 0);
-      wait(q);
+      if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) != 0) {
+        const uint64_t q = post_raw(OP_STOP, nullptr, 0, nullptr, 0);
+        wait(q);
+      }
       hip_check(hipStreamSynchronize(stream_), "store worker drain");
     }
   }
@@ -162,7 +164,7 @@ class Store {
       uint64_t* r = res_ + idx * kResWords;
       thread_local uint32_t lds[kLdsWords];
       const Lanes L{0, 1, lds};
-      store_exec(L, t_, c, r, bulk_);
+      store_exec(L, t_, c, q, r, bulk_, nullptr);
       r[0] = q + 1;
       return q;
     }
@@ -245,8 +247,13 @@ class Store {
     return out;
   }
 
+  // Everything posted so far has completed: on the device a NOP is executed only
+  // after the hash engine's queue has drained, and results complete in order
+  // otherwise.
   void drain() {
-    if (next_ > 0) wait(next_ - 1);
+    if (next_ == 0) return;
+    if (!gpu_) return;
+    wait(post_raw(OP_NOP, nullptr, 0, nullptr, 0));
   }
 
   // Copy bytes into the staging area; returns their offset.  Wrapping first

@@ -188,12 +188,32 @@ struct Lanes {
   int n;
   uint32_t* lds;
   AHV_HD bool leader() const { return lane == 0; }
+  // Lanes of ONE wave exchange data through LDS / global memory: a wave-level
+  // barrier with wavefront-scope fences (the worker runs two waves with
+  // different roles, so a workgroup barrier here would deadlock).
   AHV_HD void sync() const {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
   }
 };
+
+// A capture whose digest is computed by the hash-engine wave (worker) or right
+// away (host twin): everything but the SHA-256 is recorded by the command wave.
+struct HashJob {
+  uint64_t seq;
+  int64_t s, d, off, len, hole;
+  int64_t prev;  // parent delta index (-1 for turn 1)
+};
+
+enum ExecResult : int { EXEC_STOP = 0, EXEC_DONE = 1, EXEC_DEFERRED = 2 };
+
+// Commands that read or reset state the hash engine may still be writing
+// (delta digests, chain heads) or that publish table state wholesale; the
+// command wave drains the hash queue before executing them.
+AHV_HD bool needs_drain(uint32_t op);
 
 // Result / bulk-output stores.  On the device these land in pinned host memory,
 // so they are system-scope stores (vector stores that bypass the caches).
@@ -1190,49 +1210,63 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
 
 // ------------------------------------------------------------- audit ops
 
+// K08, command-wave half: validate, record the delta row and the chain links,
+// and describe the hashing work.  Returns false (result written) on a bad request.
+AHV_HD bool capture_begin(const Lanes& L, const Tables& t, const Cmd& c, uint64_t seq, uint64_t* r, HashJob& j) {
+  if (!L.leader()) return true;
+  // a0 session, a1 delta index, a2 turn, a3 ts, a4 payload offset, a5 payload length,
+  // a6 parent-hole offset in the payload (-1: turn 1, "null" already written)
+  const int64_t s = static_cast<int64_t>(c.a[0]);
+  const int64_t d = static_cast<int64_t>(c.a[1]);
+  const int32_t turn = static_cast<int32_t>(c.a[2]);
+  const int64_t hole = static_cast<int64_t>(c.a[6]);
+  bool ok = !(s < 0 || s >= t.cap.S || d < 0 || d >= t.cap.D || turn != t.s_dcount[s] + 1 ||
+              c.a[4] + c.a[5] > static_cast<uint64_t>(t.cap.B));
+  const int32_t prev = ok ? t.s_dlast[s] : -1;
+  if (ok && hole >= 0 && prev < 0) ok = false;
+  if (ok && hole >= 0 && (hole + 66 > static_cast<int64_t>(c.a[5]))) ok = false;
+  if (!ok) {
+    out64(r + 1, ST_BAD_ARG);
+    return false;
+  }
+  t.d_sess[d] = static_cast<int32_t>(s);
+  t.d_turn[d] = turn;
+  t.d_prev[d] = prev;
+  t.d_ts[d] = static_cast<int64_t>(c.a[3]);
+  t.d_off[d] = static_cast<int64_t>(c.a[4]);
+  t.d_len[d] = static_cast<int32_t>(c.a[5]);
+  t.s_dlast[s] = static_cast<int32_t>(d);
+  t.s_dcount[s] = turn;
+  j.seq = seq;
+  j.s = s;
+  j.d = d;
+  j.off = static_cast<int64_t>(c.a[4]);
+  j.len = static_cast<int64_t>(c.a[5]);
+  j.hole = hole;
+  j.prev = prev;
+  return true;
+}
+
+// K08, hashing half (one wave): stage the record into LDS as message words with
+// the parent's quoted digest spliced in, then the serial SHA-256 on lane 0;
+// writes the digest row, the chain head and the result words r[1..9] (not the
+// sequence word).
+AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, uint64_t* r) {
+  uint8_t* p = t.payload + j.off;
+  const uint32_t* parent = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
+  const int64_t nblk = stage_message(L, p, static_cast<uint64_t>(j.len), j.hole, parent);
+  if (!L.leader()) return;
+  uint32_t h[8];
+  if (nblk >= 0) sha256_lds_blocks(L.lds, nblk, h);
+  else sha256_fine(p, static_cast<uint64_t>(j.len), h);  // record larger than the LDS window
+  store8(t.d_hash + 8 * j.d, h);
+  store8(t.s_head + 8 * j.s, h);
+  for (int k = 0; k < 8; ++k) out64(r + 2 + k, h[k]);
+  out64(r + 1, ST_OK);
+}
+
 AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
   switch (c.op) {
-    case OP_DELTA_CAPTURE: {
-      // a0 session, a1 delta index, a2 turn, a3 ts, a4 payload offset, a5 payload length,
-      // a6 parent-hole offset in the payload (-1: turn 1, "null" already written)
-      const int64_t s = static_cast<int64_t>(c.a[0]);
-      const int64_t d = static_cast<int64_t>(c.a[1]);
-      const int32_t turn = static_cast<int32_t>(c.a[2]);
-      const int64_t hole = static_cast<int64_t>(c.a[6]);
-      int ok = 0;
-      int32_t prev = -1;
-      if (L.leader()) {
-        ok = !(s < 0 || s >= t.cap.S || d < 0 || d >= t.cap.D || turn != t.s_dcount[s] + 1 ||
-               c.a[4] + c.a[5] > static_cast<uint64_t>(t.cap.B));
-        if (ok) {
-          prev = t.s_dlast[s];
-          if (hole >= 0 && prev < 0) ok = 0;
-        }
-      }
-      if (!bcast(L, ok)) {
-        if (L.leader()) out64(r + 1, ST_BAD_ARG);
-        return;
-      }
-      uint8_t* p = t.payload + c.a[4];
-      const int64_t nblk = stage_message(L, p, c.a[5], hole, t.s_head + 8 * s);  // K08 staging
-      if (!L.leader()) return;
-      uint32_t h[8];
-      if (nblk >= 0) sha256_lds_blocks(L.lds, nblk, h);  // the serial chain: one lane, LDS-fed
-      else sha256_mem(p, c.a[5], h);                      // oversized record
-      t.d_sess[d] = static_cast<int32_t>(s);
-      t.d_turn[d] = turn;
-      t.d_prev[d] = prev;
-      t.d_ts[d] = static_cast<int64_t>(c.a[3]);
-      t.d_off[d] = static_cast<int64_t>(c.a[4]);
-      t.d_len[d] = static_cast<int32_t>(c.a[5]);
-      store8(t.d_hash + 8 * d, h);
-      store8(t.s_head + 8 * s, h);
-      t.s_dlast[s] = static_cast<int32_t>(d);
-      t.s_dcount[s] = turn;
-      for (int k = 0; k < 8; ++k) out64(r + 2 + k, h[k]);
-      out64(r + 1, ST_OK);
-      return;
-    }
     case OP_DELTA_MERKLE:
     case OP_SESS_CLOSE: {
       // MERKLE: a0 session, a1 n, a2 staging offset of indices.
@@ -1375,10 +1409,52 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
 
 // ------------------------------------------------------------- dispatch
 
+AHV_HD bool needs_drain(uint32_t op) {
+  if (op == OP_DELTA_CAPTURE) return false;
+  if (op >= 40 && op < 80) return false;  // liability and saga rows: no audit state
+  switch (op) {
+    case OP_SESS_JOIN:
+    case OP_SESS_LEAVE:
+    case OP_SESS_ACTIVATE:
+    case OP_SESS_TERMINATE:
+    case OP_SESS_ARCHIVE:
+    case OP_SESS_UPDATE_RING:
+    case OP_SESS_SET_MODE:
+    case OP_SESS_SET_SIGMA:
+    case OP_SESS_HANDSHAKE:
+      return false;
+    default:
+      return true;
+  }
+}
+
 // Execute one command.  All lanes of the wave call this with the same command;
 // lane 0 owns the scalar logic, the SIMT sections (Merkle levels, leaf gathers,
-// verify hashes) use every lane.  Returns false for OP_STOP.
-AHV_HD bool store_exec(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
+// verify hashes) use every lane.  With `defer` set, a capture's hashing is
+// handed back as a job (EXEC_DEFERRED) for the hash-engine wave; otherwise it
+// is hashed in place.  Returns EXEC_STOP for OP_STOP.
+AHV_HD int store_exec(const Lanes& L, const Tables& t, const Cmd& c, uint64_t seq, uint64_t* r, uint8_t* bulk,
+                      HashJob* defer) {
+  if (c.op == OP_DELTA_CAPTURE) {
+    HashJob j;
+    const bool ok = bcast(L, capture_begin(L, t, c, seq, r, j) ? 1 : 0) != 0;
+    if (!ok) return EXEC_DONE;
+    if (defer) {
+      if (L.leader()) *defer = j;
+      return EXEC_DEFERRED;
+    }
+    // host twin / single-wave: hash now (all lanes need the job)
+    HashJob jb;
+    jb.seq = bcast(L, j.seq);
+    jb.s = bcast(L, j.s);
+    jb.d = bcast(L, j.d);
+    jb.off = bcast(L, j.off);
+    jb.len = bcast(L, j.len);
+    jb.hole = bcast(L, j.hole);
+    jb.prev = bcast(L, j.prev);
+    capture_finish(L, t, jb, r);
+    return EXEC_DONE;
+  }
   if (c.op >= 10 && c.op < 30 && c.op != OP_SESS_CLOSE) {
     exec_sess(L, t, c, r, bulk);
   } else if ((c.op >= 30 && c.op < 40) || c.op == OP_SESS_CLOSE) {
@@ -1389,13 +1465,13 @@ AHV_HD bool store_exec(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
     exec_saga(L, t, c, r, bulk);
   } else if (c.op == OP_STOP) {
     if (L.leader()) out64(r + 1, ST_OK);
-    return false;
+    return EXEC_STOP;
   } else if (c.op == OP_NOP || c.op == OP_FLUSH || c.op == OP_ACQUIRE) {
     if (L.leader()) out64(r + 1, ST_OK);
   } else {
     if (L.leader()) out64(r + 1, ST_BAD_OP);
   }
-  return true;
+  return EXEC_DONE;
 }
 
 }  // namespace store

@@ -53,4 +53,46 @@ async def main():
     print(json.dumps(out), flush=True)
 
 
-asyncio.run(main())
+if __name__ == "__main__" and (len(sys.argv) <= 3 or sys.argv[3] != "breakdown"):
+    asyncio.run(main())
+
+
+async def breakdown(dev: str = "cuda", iters: int = 1000) -> dict:
+    """Median wall time of each API call of the reference pipeline."""
+    import collections
+
+    acc = collections.defaultdict(list)
+
+    def tick(name, t0):
+        acc[name].append(time.perf_counter_ns() - t0)
+        return time.perf_counter_ns()
+
+    for it in range(200 + iters):
+        t = time.perf_counter_ns()
+        hv = Hypervisor(device=dev)
+        t = tick("hv_init", t)
+        s = await hv.create_session(config=SessionConfig(enable_audit=True), creator_did="did:mesh:admin")
+        sid = s.sso.session_id
+        t = tick("create", t)
+        await hv.join_session(sid, "did:mesh:a", sigma_raw=0.8)
+        t = tick("join", t)
+        await hv.activate_session(sid)
+        t = tick("activate", t)
+        for i in range(3):
+            s.delta_engine.capture("did:mesh:a", [VFSChange(path=f"/f{i}", operation="add", content_hash=f"h{i}")])
+            t = tick(f"capture{i}", t)
+        saga = s.saga.create_saga(sid)
+        t = tick("saga_create", t)
+        step = s.saga.add_step(saga.saga_id, "action", "did:mesh:a", "/api/action")
+        t = tick("add_step", t)
+        await s.saga.execute_step(saga.saga_id, step.step_id, executor=lambda: asyncio.sleep(0))
+        t = tick("execute_step", t)
+        await hv.terminate_session(sid)
+        t = tick("terminate", t)
+        if it < 200:
+            acc.clear()
+    return {k: round(statistics.median(v) / 1e3, 2) for k, v in acc.items()}
+
+
+if __name__ == "__main__" and len(sys.argv) > 3 and sys.argv[3] == "breakdown":
+    print(json.dumps(asyncio.run(breakdown(sys.argv[1], int(sys.argv[2])))), flush=True)
