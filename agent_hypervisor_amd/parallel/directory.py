@@ -35,6 +35,7 @@ class SessionDirectory:
     _load: list[int] = field(default_factory=list)
     _sagas: dict[str, str] = field(default_factory=dict)
     _next: int = 0
+    _dead: set = field(default_factory=set)
 
     def __post_init__(self) -> None:
         if self.world < 1:
@@ -43,19 +44,52 @@ class SessionDirectory:
             raise ValueError(f"unknown placement policy {self.policy!r}; valid: {POLICIES}")
         self._load = [0] * self.world
 
+    # -- liveness ----------------------------------------------------------------
+    def mark_dead(self, ranks) -> None:
+        """Exclude failed ranks from placement and rebalancing (failover)."""
+        self._dead.update(int(r) for r in ranks)
+        if len(self._dead) >= self.world:
+            raise RuntimeError("every rank is marked dead")
+
+    def mark_alive(self, rank: int) -> None:
+        self._dead.discard(int(rank))
+
+    @property
+    def live_ranks(self) -> list[int]:
+        return [r for r in range(self.world) if r not in self._dead]
+
     # -- placement -------------------------------------------------------------
+    def next_rank(self, key: Optional[str] = None) -> int:
+        """The rank the next new session goes to (advances round-robin state).
+
+        Used when the owner must mint the session id: place first, then
+        :meth:`assign` the id the owner returned.  Dead ranks are skipped.
+        """
+        live = self.live_ranks
+        if self.policy == "round_robin":
+            for _ in range(self.world):
+                r = self._next
+                self._next = (self._next + 1) % self.world
+                if r not in self._dead:
+                    return r
+            return live[0]
+        if self.policy == "least_loaded":
+            return min(live, key=lambda k: (self._load[k], k))
+        r = stable_rank(key or str(len(self._owner)), self.world)
+        return r if r not in self._dead else live[stable_rank(key or "", len(live))]
+
+    def assign(self, session_id: str, rank: int) -> None:
+        if session_id in self._owner:
+            raise ValueError(f"session {session_id} already placed on rank {self._owner[session_id]}")
+        self._owner[session_id] = rank
+        self._load[rank] += 1
+
     def place(self, session_id: str) -> int:
         """Assign ``session_id`` to a rank (idempotent) and return it."""
         r = self._owner.get(session_id)
         if r is not None:
             return r
-        if self.policy == "round_robin":
-            r = self._next
-            self._next = (self._next + 1) % self.world
-        elif self.policy == "least_loaded":
-            r = min(range(self.world), key=lambda k: (self._load[k], k))
-        else:
-            r = stable_rank(session_id, self.world)
+        r = self.next_rank(session_id)
         self._owner[session_id] = r
         self._load[r] += 1
         return r
@@ -98,13 +132,16 @@ class SessionDirectory:
     def rebalance_plan(self) -> list[tuple[str, int, int]]:
         """Moves (session, from, to) that level the per-rank load to within one
         session; executed with an all-to-all of the session rows (P08)."""
-        target = len(self._owner) // self.world
-        extra = len(self._owner) % self.world
-        want = [target + (1 if k < extra else 0) for k in range(self.world)]
+        live = self.live_ranks
+        target = len(self._owner) // len(live)
+        extra = len(self._owner) % len(live)
+        want = [0] * self.world
+        for i, k in enumerate(live):
+            want[k] = target + (1 if i < extra else 0)
         load = list(self._load)
         donors = {k: [s for s, r in self._owner.items() if r == k] for k in range(self.world)}
         moves = []
-        for dst in range(self.world):
+        for dst in live:
             for src in range(self.world):
                 while load[dst] < want[dst] and load[src] > want[src]:
                     s = donors[src].pop()

@@ -151,29 +151,25 @@ def failover_plan(directory: SessionDirectory, failed: list[int]) -> list[tuple[
     return moves
 
 
-def apply_failover(directory: SessionDirectory, moves: list[tuple[str, int, int]]) -> None:
+def apply_failover(directory: SessionDirectory, moves: list[tuple[str, int, int]],
+                   failed: Optional[list[int]] = None) -> None:
+    """Re-home the moved sessions and mark the failed ranks dead, so placement
+    and rebalancing never target them again (until :meth:`mark_alive`)."""
+    dead = set(failed or []) | {src for _, src, _ in moves}
+    if dead:
+        directory.mark_dead(sorted(dead))
     directory.apply(moves)
 
 
 def rehydrate(checkpoint_dir: str, moves: list[tuple[str, int, int]], rank: int, hv=None):
     """Load the sessions ``moves`` assigns to ``rank`` from the failed rank's
-    checkpoint into ``hv`` (a Hypervisor), verifying their audit chains."""
+    checkpoint into ``hv`` (a Hypervisor, host or device-backed) through the
+    checkpoint loader, which re-verifies their audit chains and roots."""
     from agent_hypervisor_amd.runtime.checkpoint import load_hypervisor
 
-    mine = {s for s, _, dst in moves if dst == rank}
-    restored = load_hypervisor(checkpoint_dir)
+    mine = sorted({s for s, _, dst in moves if dst == rank})
     if hv is None:
         from hypervisor import Hypervisor
 
         hv = Hypervisor()
-    for m in restored.sessions:
-        if m.sso.session_id in mine:
-            hv._sessions[m.sso.session_id] = m
-            c = restored.commitment.get_commitment(m.sso.session_id)
-            if c is not None:
-                hv.commitment._commitments[c.session_id] = c
-    for v in restored.vouching.records():
-        if v.session_id in mine:
-            hv.vouching._vouches[v.vouch_id] = v
-            hv.vouching._by_session.setdefault(v.session_id, []).append(v)
-    return hv
+    return load_hypervisor(checkpoint_dir, hv=hv, sessions=mine)

@@ -300,8 +300,12 @@ def _delta_from_record(rec: dict):
     return d
 
 
-def load_hypervisor(d: str, hv=None, verify: bool = True):
-    """Resume a :class:`hypervisor.Hypervisor` from ``d`` (into ``hv`` if given)."""
+def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
+    """Resume a :class:`hypervisor.Hypervisor` from ``d`` (into ``hv`` if given).
+
+    ``sessions``: restore only these session ids (with their vouch bonds and
+    commitments) — failover re-homes a dead rank's sessions onto survivors this
+    way (:func:`agent_hypervisor_amd.parallel.resilience.rehydrate`)."""
     from hypervisor.audit.commitment import CommitmentRecord
     from hypervisor.core import Hypervisor, ManagedSession
     from hypervisor.liability.vouching import VouchRecord
@@ -321,8 +325,11 @@ def load_hypervisor(d: str, hv=None, verify: bool = True):
     hv = hv or Hypervisor()
     with open(os.path.join(d, "sessions.jsonl")) as f:
         records = [json.loads(line) for line in f if line.strip()]
+    only = set(sessions) if sessions is not None else None
+    if only is not None:
+        records = [r for r in records if r["session_id"] in only]
     if getattr(hv, "_store", None) is not None:
-        return _load_device(hv, d, records, verify)
+        return _load_device(hv, d, records, verify, only)
     for r in records:
         cfg = dict(r["config"])
         cfg["consistency_mode"] = ConsistencyMode(cfg["consistency_mode"])
@@ -363,6 +370,8 @@ def load_hypervisor(d: str, hv=None, verify: bool = True):
         hv._sessions[sso.session_id] = m
     with open(os.path.join(d, "liability.json")) as f:
         for v in json.load(f):
+            if only is not None and v["session_id"] not in only:
+                continue
             rec = VouchRecord(vouch_id=v["vouch_id"], voucher_did=v["voucher_did"], vouchee_did=v["vouchee_did"],
                               session_id=v["session_id"], bonded_sigma_pct=v["bonded_sigma_pct"],
                               bonded_amount=v["bonded_amount"], created_at=_dt(v["created_at"]),
@@ -371,6 +380,8 @@ def load_hypervisor(d: str, hv=None, verify: bool = True):
             hv.vouching._by_session.setdefault(rec.session_id, []).append(rec)
     with open(os.path.join(d, "commitments.json")) as f:
         for c in json.load(f):
+            if only is not None and c["session_id"] not in only:
+                continue
             rec = CommitmentRecord(session_id=c["session_id"], merkle_root=c["merkle_root"],
                                    participant_dids=c["participant_dids"], delta_count=c["delta_count"],
                                    committed_at=_dt(c["committed_at"]), blockchain_tx_id=c["blockchain_tx_id"],
@@ -385,7 +396,7 @@ def load_hypervisor(d: str, hv=None, verify: bool = True):
     return hv
 
 
-def _load_device(hv, d: str, records: list, verify: bool):
+def _load_device(hv, d: str, records: list, verify: bool, only=None):
     """Restore into a device-backed hypervisor: rows are scattered straight into
     the store tables (one bulk tensor write per column), the canonical-JSON audit
     records into the payload arena, and the device then re-verifies every chain
@@ -417,7 +428,7 @@ def _load_device(hv, d: str, records: list, verify: bool):
         return to_us(_dt(t)) if t else 0
 
     with open(os.path.join(d, "commitments.json")) as f:
-        commits = {c["session_id"]: c for c in json.load(f)}
+        commits = {c["session_id"]: c for c in json.load(f) if only is None or c["session_id"] in only}
     sess_list = []
     for r in records:
         cfg = dict(r["config"])
@@ -525,7 +536,7 @@ def _load_device(hv, d: str, records: list, verify: bool):
     ve = hv.vouching
     tails: dict = {}
     with open(os.path.join(d, "liability.json")) as f:
-        vouches = json.load(f)
+        vouches = [v for v in json.load(f) if only is None or v["session_id"] in only]
     for v in vouches:
         vs = st.liability_id(ve._tenant, v["session_id"])
         e = st.alloc("E")

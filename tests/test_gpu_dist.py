@@ -37,3 +37,16 @@ def test_bench_rccl_path_one_rank(cuda_device, graph):
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 1 and out["last_step_counters"]["sessions"] == 65536
     assert out["last_step_counters"]["ok"] == 65536 and out["value"] > 0
+
+
+def test_sharded_hypervisor_rccl_one_rank(cuda_device):
+    """The sharded front-end's collectives (X01/X04/X05 on RCCL, control on gloo)
+    with the device store, under torch.distributed.run — the 8-GPU code path."""
+    env = dict(os.environ, AHV_SKIP_AUTOBUILD="1", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "scripts", "sharded_rccl_check.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["ok"] and out["backend"] == "nccl" and out["store_gpu"]

@@ -1,0 +1,193 @@
+"""Sharded Hypervisor (one process per GPU): every route's answer on 2/4 ranks
+equals the single-rank answer for the same workload (gloo on CPU; the same code
+runs with RCCL on MI355X, tests/test_gpu_dist.py).  Also: the rank-0 REST
+front-end with followers, and failover never placing on a dead rank."""
+
+from __future__ import annotations
+
+import asyncio
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from agent_hypervisor_amd.parallel.directory import SessionDirectory
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+async def scenario(shv) -> dict:
+    """A mixed workload; returns every cross-session answer, ids replaced by creation index."""
+    from hypervisor import SessionConfig
+    from hypervisor.audit.delta import VFSChange
+
+    sids = []
+    for k in range(6):
+        sids.append(await shv.create_session(SessionConfig(max_participants=4), f"did:admin-{k}"))
+    idx = {s: i for i, s in enumerate(sids)}
+    agents = [f"did:agent-{a}" for a in range(5)]
+    rings = []
+    for k, sid in enumerate(sids):
+        for a in range(3):
+            ag = agents[(k + a) % 5]
+            rings.append(int(await shv.join_session(sid, ag, sigma_raw=0.55 + 0.1 * ((k * 3 + a) % 5))))
+        if k % 2 == 0:
+            await shv.activate_session(sid)
+        for d in range(k % 3):
+            await shv.capture(sid, agents[k % 5], [VFSChange(path=f"/f{d}", operation="add", content_hash=f"h{d}")])
+    # liability: session-scoped vouches, one slash cascade
+    errors = []
+    for k, sid in enumerate(sids[:4]):
+        await shv.vouch(agents[k % 5], agents[(k + 1) % 5], sid, 0.9, bond_pct=0.3)
+        await shv.vouch(agents[(k + 2) % 5], agents[(k + 1) % 5], sid, 0.8)
+        try:
+            await shv.vouch(agents[(k + 1) % 5], agents[k % 5], sid, 0.9)  # cycle → rejected on the owner
+        except Exception as e:  # noqa: BLE001
+            errors.append(type(e).__name__)
+    scores = {a: 0.7 for a in agents}
+    sl = await shv.slash(agents[1], sids[0], 0.7, 0.95, "drift", scores)
+    # sagas, routed by id
+    gid = await shv.create_saga(sids[1])
+    st1 = await shv.add_step(gid, "a", agents[1], "/a", undo_api="/u")
+    st2 = await shv.add_step(gid, "b", agents[2], "/b")
+    for st in (st1, st2):
+        await shv.execute_step(gid, st, lambda: asyncio.sleep(0))
+    failed = await shv.compensate(gid, lambda step: asyncio.sleep(0))
+    saga = await shv.get_saga(gid)
+    roots = [await shv.terminate_session(s) is not None for s in sids[3:]]
+    out = {
+        "rings": rings,
+        "errors": errors,
+        "slash": (sl["clips"], sorted(scores.items())),
+        "saga": ([s["state"] for s in saga["steps"]], saga["state"], len(failed)),
+        "roots": roots,
+        "stats": shv.stats(),
+        "agent_ring": [],
+        "liability": [],
+        "sessions": [(idx[d["session_id"]], d["state"], d["participant_count"]) for d in shv.list_sessions()],
+        "sigma": await shv.compute_sigma_eff(agents[2], sids[2], 0.5, 0.65),
+        "exposure": await shv.get_total_exposure(agents[2], sids[2]),
+    }
+    for a in agents + ["did:nobody"]:
+        r = shv.agent_ring(a)
+        out["agent_ring"].append(None if r is None else (r["ring"], idx[r["session_id"]]))
+        lia = shv.agent_liability(a)
+        out["liability"].append((
+            [(v["voucher_did"], v["vouchee_did"], v["bonded_amount"], v["is_active"]) for v in lia["vouches_given"]],
+            [(v["voucher_did"], v["vouchee_did"]) for v in lia["vouches_received"]],
+            lia["total_exposure"],
+        ))
+    with pytest.raises(ValueError):
+        await shv.join_session("session:missing", "did:x", sigma_raw=0.9)
+    return out
+
+
+def _worker(rank: int, world: int, port: int, store: str, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), AHV_STORE=store)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
+
+        shv = ShardedHypervisor(device=store)
+        got = asyncio.run(scenario(shv))
+        owners = shv.directory.load
+        if rank == 0:
+            ref = asyncio.run(scenario(ShardedHypervisor(device=store, single=True)))
+            q.put((got, ref, owners))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,store", [(2, "host"), (4, "host"), (2, "cpu")])
+def test_routes_match_single_rank(world, store):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, store, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, ref, owners = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert owners == [6 // world + (1 if r < 6 % world else 0) for r in range(world)]
+    for key in ref:
+        assert got[key] == ref[key], key
+
+
+def _rest_worker(rank: int, world: int, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), AHV_STORE="host")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor, serve_followers
+
+        shv = ShardedHypervisor()
+        if rank != 0:
+            asyncio.run(serve_followers(shv))
+            return
+        from fastapi.testclient import TestClient
+
+        from hypervisor.api.sharded import create_sharded_app
+
+        app, driver = create_sharded_app(shv)
+        with TestClient(app) as c:
+            sids = [c.post("/api/v1/sessions", json={"creator_did": "did:admin"}).json()["session_id"]
+                    for _ in range(3)]
+            for k, sid in enumerate(sids):
+                r = c.post(f"/api/v1/sessions/{sid}/join", json={"agent_did": "did:a", "sigma_raw": 0.7 + 0.1 * k})
+                assert r.status_code == 200, r.text
+            c.post(f"/api/v1/sessions/{sids[1]}/vouch",
+                   json={"voucher_did": "did:v", "vouchee_did": "did:a", "voucher_sigma": 0.9})
+            out = {
+                "stats": c.get("/api/v1/stats").json(),
+                "ring": c.get("/api/v1/agents/did:a/ring").json(),
+                "liability": c.get("/api/v1/agents/did:v/liability").json(),
+                "session": c.get(f"/api/v1/sessions/{sids[2]}").json(),
+                "missing": c.get("/api/v1/sessions/session:nope").status_code,
+                "owners": [shv.directory.owner(s) for s in sids],
+                "sids": sids,
+            }
+        driver.stop()
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_rest_front_end():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rest_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out["owners"] == [0, 1, 0]
+    assert out["stats"]["total_sessions"] == 3 and out["stats"]["total_participants"] == 3
+    assert out["ring"]["session_id"] == out["sids"][0] and out["ring"]["ring"] == 2
+    assert out["liability"]["total_exposure"] == pytest.approx(0.9 * 0.2)
+    assert out["session"]["rank"] == 0 and out["session"]["participants"][0]["agent_did"] == "did:a"
+    assert out["missing"] == 404
+
+
+def test_failover_never_places_on_dead_rank():
+    from agent_hypervisor_amd.parallel.resilience import apply_failover, failover_plan
+
+    for policy in ("round_robin", "least_loaded", "hash"):
+        d = SessionDirectory(world=4, policy=policy)
+        for k in range(20):
+            d.place(f"s{k}")
+        apply_failover(d, failover_plan(d, [2]), failed=[2])
+        assert d.load[2] == 0 and 2 not in d.live_ranks
+        assert all(d.place(f"new{k}") != 2 for k in range(40))
+        assert all(dst != 2 for _, _, dst in d.rebalance_plan())
