@@ -103,45 +103,72 @@ def allreduce_exposure(exposure: torch.Tensor) -> torch.Tensor:
 
 
 # -- X02 ----------------------------------------------------------------------------
-def merge_slash_effects(
-    sigma: torch.Tensor, blacklist: torch.Tensor, clip_factor: torch.Tensor, floor: float = 0.05
-) -> torch.Tensor:
-    """Exact cross-rank merge of slash effects on agent σ.
+#
+# Merge convention.  Within one rank, slashes run in the reference order: the
+# vouchee is blacklisted (σ → 0) first and its vouchers are clipped after, so an
+# agent blacklisted and then clipped in the same cascade (possible only through
+# a vouch cycle) ends at the floor, as SlashingEngine leaves it.  Across ranks
+# (concurrent sessions, no defined order):
+#   * clips commute: factors Π(1−ω) multiply and the floor is applied once —
+#     exact, because max(max(x·a, F)·b, F) = max(x·a·b, F) for a, b ≤ 1;
+#   * a blacklist zeroes the agent; if every rank that blacklisted it reports the
+#     floor outcome (blacklist-then-clip), the merged σ is the floor.
+# Each rank contributes a blacklist code per agent: 0 none, 1 ended at the floor,
+# 2 ended at 0; codes merge with MAX (the lower outcome wins).
 
-    ``blacklist`` is 1 where a rank blacklisted the agent (σ → 0); ``clip_factor``
-    is the product Π(1−ω) of clips a rank applied (1 where none).  Because
-    ``max(max(x·a, F)·b, F) = max(x·a·b, F)`` for a, b ≤ 1, multiplying the
-    factors across ranks and flooring once equals applying every clip in turn.
-    """
-    bl = blacklist.to(torch.int32).clone()
+
+def _apply_slash(sigma: torch.Tensor, factor: torch.Tensor, touched: torch.Tensor, code: torch.Tensor,
+                 floor: float) -> torch.Tensor:
+    out = torch.where(touched, torch.clamp(sigma * factor, min=floor), sigma)
+    out = torch.where(code == 1, torch.full_like(out, floor), out)
+    return torch.where(code >= 2, torch.zeros_like(out), out)
+
+
+def merge_slash_effects(
+    sigma: torch.Tensor, blacklist: torch.Tensor, clip_factor: torch.Tensor, floor: float = 0.05,
+    floored: Optional[torch.Tensor] = None,
+) -> torch.Tensor:
+    """Exact cross-rank merge of slash effects on agent σ (dense [A] form).
+
+    ``blacklist`` is nonzero where this rank blacklisted the agent; ``floored``
+    (optional) marks the blacklisted agents this rank clipped afterwards (their
+    local outcome is the floor); ``clip_factor`` is the product Π(1−ω) of the
+    clips this rank applied (1 where none).  See the merge convention above."""
+    code = torch.where(blacklist.to(torch.bool), torch.full_like(blacklist, 2, dtype=torch.int32),
+                       torch.zeros_like(blacklist, dtype=torch.int32))
+    if floored is not None:
+        code = torch.where(code.bool() & floored.to(torch.bool), torch.ones_like(code), code)
     cf = clip_factor.clone()
     if _ready():
-        _comm().all_reduce(bl, op=dist.ReduceOp.MAX)
+        _comm().all_reduce(code, op=dist.ReduceOp.MAX)
         _comm().all_reduce(cf, op=dist.ReduceOp.PRODUCT)
-    touched = cf < 1.0
-    out = torch.where(touched, torch.clamp(sigma * cf, min=floor), sigma)
-    return torch.where(bl > 0, torch.zeros_like(out), out)
+    return _apply_slash(sigma, cf, cf < 1.0, code, floor)
 
 
 def merge_slash_sparse(
     sigma: torch.Tensor, blacklist_ids: torch.Tensor, clip_ids: torch.Tensor, clip_factors: torch.Tensor,
-    floor: float = 0.05,
+    floor: float = 0.05, floored_ids: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """Sparse form of X02 for slash storms that touch few agents.
 
-    Each rank contributes only the agents it slashed — ``blacklist_ids`` (int32) and
-    ``(clip_ids, clip_factors)`` pairs (int32, fp64 Π(1−ω) per rank, duplicates
-    allowed) — instead of a dense [A] vector.  The pairs are all-gathered (padded to
-    the longest rank's list) and PROD-scattered locally into a factor vector, then
-    applied with the same single floor as the dense merge, so the result is
-    identical to :func:`merge_slash_effects` on the densified inputs.  Returns the
-    merged σ (a new tensor; ``sigma`` is not modified)."""
+    Each rank contributes only the agents it slashed — ``blacklist_ids`` (int32),
+    ``floored_ids`` (the blacklisted agents it clipped afterwards) and
+    ``(clip_ids, clip_factors)`` pairs (int32, fp64 Π(1−ω), duplicates allowed) —
+    instead of a dense [A] vector.  The lists are all-gathered (padded to the
+    longest rank's list) and applied locally: factors PROD-scattered, blacklist
+    codes MAX-scattered, one floor; identical to :func:`merge_slash_effects` on
+    the densified inputs.  Returns the merged σ (``sigma`` is not modified)."""
     dev = sigma.device
     bl = blacklist_ids.to(device=dev, dtype=torch.int64).reshape(-1)
+    fl = (floored_ids if floored_ids is not None else torch.empty(0)).to(device=dev, dtype=torch.int64).reshape(-1)
     ci = clip_ids.to(device=dev, dtype=torch.int64).reshape(-1)
     cf = clip_factors.to(device=dev, dtype=torch.float64).reshape(-1)
     if ci.numel() != cf.numel():
         raise ValueError("clip_ids and clip_factors must have the same length")
+    # per-rank blacklist codes: 2 (zero) unless floored on this rank (1)
+    bc = torch.full((bl.numel(),), 2, dtype=torch.int64, device=dev)
+    if fl.numel() and bl.numel():
+        bc = torch.where(torch.isin(bl, fl), torch.ones_like(bc), bc)
     if _ready():
         c = _comm()
         w = c.get_world_size()
@@ -152,18 +179,23 @@ def merge_slash_sparse(
         mc = max(int(t[1]) for t in sizes)
         pb = torch.full((max(mb, 1),), -1, dtype=torch.int64, device=dev)
         pb[: bl.numel()] = bl
+        pc = torch.zeros(max(mb, 1), dtype=torch.int64, device=dev)
+        pc[: bc.numel()] = bc
         pi = torch.full((max(mc, 1),), -1, dtype=torch.int64, device=dev)
         pi[: ci.numel()] = ci
         pf = torch.ones(max(mc, 1), dtype=torch.float64, device=dev)
         pf[: cf.numel()] = cf
         gb = [torch.empty_like(pb) for _ in range(w)]
+        gc = [torch.empty_like(pc) for _ in range(w)]
         gi = [torch.empty_like(pi) for _ in range(w)]
         gf = [torch.empty_like(pf) for _ in range(w)]
         c.all_gather(gb, pb)
+        c.all_gather(gc, pc)
         c.all_gather(gi, pi)
         c.all_gather(gf, pf)
-        bl = torch.cat(gb)
-        bl = bl[bl >= 0]
+        bl, bc = torch.cat(gb), torch.cat(gc)
+        keep = bl >= 0
+        bl, bc = bl[keep], bc[keep]
         ci = torch.cat(gi)
         cf = torch.cat(gf)
         keep = ci >= 0
@@ -174,10 +206,45 @@ def merge_slash_sparse(
     touched = torch.zeros(sigma.numel(), dtype=torch.bool, device=dev)
     touched[ci] = True
     touched &= factor < 1.0
-    out = torch.where(touched, torch.clamp(sigma * factor, min=floor), sigma)
+    code = torch.zeros(sigma.numel(), dtype=torch.int64, device=dev)
     if bl.numel():
-        out[bl] = 0.0
-    return out
+        code.index_reduce_(0, bl, bc, "amax")
+    return _apply_slash(sigma, factor, touched, code, floor)
+
+
+def merge_slash_fixed(
+    sigma: torch.Tensor, blacklist_ids: torch.Tensor, pair_ids: torch.Tensor, pair_factors: torch.Tensor,
+    floor: float = 0.05,
+) -> torch.Tensor:
+    """X02 for a slash stage inside a timed step: fixed-capacity buffers (unused
+    entries id −1 / factor 1, the ``slash_clip`` kernel's output) are all-gathered
+    with no size exchange and no host synchronisation, then applied as in
+    :func:`merge_slash_sparse` (blacklist code 2 for every listed vouchee).
+    Every rank must pass buffers of the same capacity.  In place on ``sigma``."""
+    bl = blacklist_ids.to(torch.int64)
+    pi = pair_ids.to(torch.int64)
+    pf = pair_factors
+    if _ready():
+        c = _comm()
+        w = c.get_world_size()
+        gb = [torch.empty_like(bl) for _ in range(w)]
+        gi = [torch.empty_like(pi) for _ in range(w)]
+        gf = [torch.empty_like(pf) for _ in range(w)]
+        c.all_gather(gb, bl)
+        c.all_gather(gi, pi)
+        c.all_gather(gf, pf)
+        bl, pi, pf = torch.cat(gb), torch.cat(gi), torch.cat(gf)
+    valid = pi >= 0
+    idx = torch.where(valid, pi, torch.zeros_like(pi))
+    f = torch.where(valid, pf, torch.ones_like(pf))
+    factor = torch.ones_like(sigma)
+    factor.index_reduce_(0, idx, f, "prod")
+    touched = factor < 1.0
+    code = torch.zeros(sigma.numel(), dtype=torch.int64, device=sigma.device)
+    vb = bl >= 0
+    code.index_reduce_(0, torch.where(vb, bl, torch.zeros_like(bl)), torch.where(vb, 2, 0).to(torch.int64), "amax")
+    sigma.copy_(_apply_slash(sigma, factor, touched, code, floor))
+    return sigma
 
 
 # -- X03 ----------------------------------------------------------------------------

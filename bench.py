@@ -13,6 +13,14 @@ gfx950 launch (device-resident tables, device-minted ids, synthetic agents with
 random-init σ), then a cross-rank RCCL all-reduce of the step's governance
 counters (collective X04) — weak scaling, sessions sharded data-parallel.
 
+Cross-session liability propagation runs inside the same timed step, on a side
+stream overlapping the pipeline kernel (``--no-liability`` turns it off): over a
+resident bond graph of ``--agents`` agents × ``--bond-degree`` edges per rank,
+the K04 exposure partial → X01 all-reduce of the [A] fp64 agent-exposure vector
+(8 MB at 1 M agents) over xGMI, and a K06 slash stage of ``--slash-k`` vouchees
+→ X02 sparse merge (fixed-capacity (agent, factor) all-gather + PROD scatter)
+into the agent σ vector.  Bytes per step of every collective are in the JSON.
+
 Also reported (not the headline value):
 * ``device_p50_us`` — p50 of the single-session pipeline through the public
   ``Hypervisor(device="cuda")`` API, reference harness methodology (2,000
@@ -98,6 +106,9 @@ def main() -> None:
     ap.add_argument("--no-scalar", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from a captured hipGraph (device cursor + RCCL counters)")
+    ap.add_argument("--no-liability", action="store_true", help="skip the X01/X02 liability stage")
+    ap.add_argument("--bond-degree", type=int, default=4, help="resident vouch edges per agent")
+    ap.add_argument("--slash-k", type=int, default=1024, help="vouchees slashed per step (X02 stage)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                     help="cpu runs the host twin of the kernel over gloo (multi-process CPU rehearsal)")
     args = ap.parse_args()
@@ -144,6 +155,44 @@ def main() -> None:
     works: list = [None, None]
     it = [0]
 
+    # Liability stage (X01/X02) on a side stream: resident bonds, exposure, slash storm.
+    liab = None
+    if not args.no_liability:
+        from agent_hypervisor_amd.ops.global_liability import ResidentBonds
+        from agent_hypervisor_amd.parallel.collectives import merge_slash_fixed
+
+        A = args.agents
+        bonds = ResidentBonds(A, args.bond_degree, dev, seed=4242 + rank)
+        k = args.slash_k
+        cap = 16 * k
+        liab = {
+            "bonds": bonds,
+            "expo": torch.zeros(A, dtype=torch.float64, device=dev),
+            "sigma": torch.rand(A, dtype=torch.float64, device=dev, generator=g),
+            "ids": torch.zeros(k, dtype=torch.int32, device=dev),
+            "pid": torch.full((cap,), -1, dtype=torch.int32, device=dev),
+            "pf": torch.ones(cap, dtype=torch.float64, device=dev),
+            "cur": torch.zeros(1, dtype=torch.int64, device=dev),
+            "work": None,
+            "stream": torch.cuda.Stream(dev) if dev.type == "cuda" else None,
+            "gen": torch.Generator(device=dev).manual_seed(99 + rank),
+        }
+        x01_bytes = A * 8
+        x02_bytes = k * 8 + cap * 16  # per rank: blacklist ids (i64) + (id i64, factor f64) pairs
+
+    def liability_step():
+        L = liab
+        if L["work"] is not None:
+            L["work"].wait()  # the previous step's X01 must finish before the buffer is rewritten
+        L["bonds"].exposure(L["expo"])  # K04 partial
+        L["work"] = dist.all_reduce(L["expo"], op=dist.ReduceOp.SUM, async_op=True) if multi else None  # X01
+        L["ids"].random_(0, args.agents, generator=L["gen"])
+        L["cur"].zero_()
+        L["pid"].fill_(-1)
+        L["pf"].fill_(1.0)
+        L["bonds"].slash_clip(L["ids"], 0.95, L["pid"], L["pf"], L["cur"])  # K06 stage
+        merge_slash_fixed(L["sigma"], L["ids"], L["pid"], L["pf"])  # X02
+
     def step():
         b = it[0] & 1
         it[0] += 1
@@ -154,6 +203,14 @@ def main() -> None:
         agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
         eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
         works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if multi else None
+        if liab is not None:
+            if liab["stream"] is not None:
+                liab["stream"].wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(liab["stream"]):
+                    liability_step()
+                torch.cuda.current_stream(dev).wait_stream(liab["stream"])
+            else:
+                liability_step()
         return st
 
     def drain():
@@ -161,6 +218,9 @@ def main() -> None:
             if works[k] is not None:
                 works[k].wait()
                 works[k] = None
+        if liab is not None and liab["work"] is not None:
+            liab["work"].wait()
+            liab["work"] = None
 
     if args.graph:
         from agent_hypervisor_amd.runtime.graphs import PipelineGraph
@@ -256,6 +316,17 @@ def main() -> None:
             "scalar_mean_us": round(scalar_mean, 2) if scalar_mean is not None else None,
             "scalar_vs_baseline_p50": round(BASELINE_P50_US / scalar_p50, 2) if scalar_p50 else None,
             "last_step_counters": dict(zip(["sessions", "ok", "participants", "deltas", "commits", "archived"], totals)),
+            "rccl_ranks": world if (multi and dev.type == "cuda") else 0,
+            "collective_backend": dist.get_backend() if multi else None,
+            "collectives_per_step": {
+                "x04_counters_bytes": 48,
+                "x01_exposure_allreduce_bytes": x01_bytes if liab is not None else 0,
+                "x02_slash_allgather_bytes_per_rank": x02_bytes if liab is not None else 0,
+            },
+            "liability_stage": None if liab is None else {
+                "agents": args.agents, "resident_edges": liab["bonds"].edges, "slash_k": args.slash_k,
+                "bond_graph_bytes": liab["bonds"].nbytes, "in_timed_region": True,
+            },
         }
         print(json.dumps(out), flush=True)
     if multi:

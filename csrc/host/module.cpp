@@ -15,6 +15,7 @@ void register_runtime(py::module_& m);
 void register_kernels(py::module_& m);
 void register_comm(py::module_& m);
 void register_store(py::module_& m);
+void register_global_liability(py::module_& m);
 }  // namespace host
 }  // namespace ahv
 
@@ -26,4 +27,5 @@ PYBIND11_MODULE(_C, m) {
   ahv::host::register_kernels(m);
   ahv::host::register_comm(m);
   ahv::host::register_store(m);
+  ahv::host::register_global_liability(m);
 }

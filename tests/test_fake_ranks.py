@@ -45,7 +45,10 @@ def _slash_inputs(world, A=64, seed=0):
 
 
 def _sequential(sigma, per_rank, floor=0.05):
-    """Every clip applied one at a time with its own floor (the scalar engine's order)."""
+    """The documented cross-rank convention applied naively: every clip one at a
+    time with its own floor (clips commute), then the blacklists (a blacklist
+    from any rank zeroes the agent — no rank here reports a blacklist-then-clip
+    floor outcome; that case is pinned by test_cycle_blacklist_then_clip_floor)."""
     s = sigma.clone()
     for ids, f, _ in per_rank:
         for i, x in zip(ids.tolist(), f.tolist()):
@@ -73,6 +76,65 @@ def test_slash_merge_dense_and_sparse_match_sequential(world):
     for dense, sparse in run_ranks(world, body):
         torch.testing.assert_close(sparse, dense, rtol=0, atol=0)
         torch.testing.assert_close(dense, want, rtol=1e-12, atol=1e-15)
+
+
+def test_cycle_blacklist_then_clip_floor():
+    """within one rank the reference blacklists the vouchee first and
+    clips later, so an agent clipped after its own blacklist (vouch cycle) ends at
+    the floor.  The merge reproduces SlashingEngine exactly on one rank, and a
+    plain blacklist from another rank still wins."""
+    from hypervisor.liability.slashing import SlashingEngine
+    from hypervisor.liability.vouching import VouchingEngine
+
+    ve = VouchingEngine()
+    ve.vouch("did:a", "did:b", "s", 0.9, bond_pct=0.2)
+    ve._creates_cycle = lambda *a: False  # force the cycle the admission check would reject
+    ve.vouch("did:b", "did:a", "s", 0.9, bond_pct=0.2)
+    scores = {"did:a": 0.0, "did:b": 0.5}
+    SlashingEngine(ve).slash("did:b", "s", 0.5, 0.95, "x", scores)
+    # A is clipped, wiped, cascaded (blacklisted → 0); B, blacklisted first, is clipped back to the floor
+    assert scores["did:b"] == 0.05 and scores["did:a"] == 0.0
+
+    ids = {"did:a": 0, "did:b": 1}
+    sigma = torch.tensor([0.0, 0.5], dtype=torch.float64)
+    bl, fl = torch.tensor([1, 0], dtype=torch.int32), torch.tensor([1], dtype=torch.int32)
+    clip_ids = torch.tensor([ids["did:a"], ids["did:b"]], dtype=torch.int32)
+    clip_f = torch.tensor([0.05, 0.05], dtype=torch.float64)
+    got = run_ranks(1, lambda r: X.merge_slash_sparse(sigma, bl, clip_ids, clip_f, floored_ids=fl))[0]
+    assert got.tolist() == [scores["did:a"], scores["did:b"]]
+    cf = torch.ones(2, dtype=torch.float64)
+    cf.index_reduce_(0, clip_ids.long(), clip_f, "prod")
+    dense = run_ranks(1, lambda r: X.merge_slash_effects(sigma, torch.tensor([1, 1]), cf,
+                                                         floored=torch.tensor([0, 1])))[0]
+    assert dense.tolist() == got.tolist()
+
+    def two(rank):  # rank 0 floored B, rank 1 blacklisted B outright → the lower outcome (0) wins
+        if rank == 0:
+            return X.merge_slash_sparse(sigma, bl, clip_ids, clip_f, floored_ids=fl)
+        return X.merge_slash_sparse(sigma, bl, torch.empty(0, dtype=torch.int32), torch.empty(0, dtype=torch.float64))
+
+    for out in run_ranks(2, two):
+        assert out.tolist()[1] == 0.0
+
+
+def test_merge_slash_fixed_matches_sparse():
+    world = 3
+    sigma, per_rank = _slash_inputs(world, seed=7)
+    cap = 16
+
+    def body(rank):
+        ids, f, bl = per_rank[rank]
+        pi = torch.full((cap,), -1, dtype=torch.int32)
+        pf = torch.ones(cap, dtype=torch.float64)
+        pi[: ids.numel()] = ids
+        pf[: f.numel()] = f
+        b = torch.full((4,), -1, dtype=torch.int32)
+        b[: bl.numel()] = bl
+        fixed = X.merge_slash_fixed(sigma.clone(), b, pi, pf)
+        return fixed, X.merge_slash_sparse(sigma, bl, ids, f)
+
+    for fixed, sparse in run_ranks(world, body):
+        torch.testing.assert_close(fixed, sparse, rtol=0, atol=0)
 
 
 def test_risk_is_rank_order_independent():
