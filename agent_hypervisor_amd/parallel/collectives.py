@@ -214,16 +214,24 @@ def merge_slash_sparse(
 
 def merge_slash_fixed(
     sigma: torch.Tensor, blacklist_ids: torch.Tensor, pair_ids: torch.Tensor, pair_factors: torch.Tensor,
-    floor: float = 0.05,
+    floor: float = 0.05, factor: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """X02 for a slash stage inside a timed step: fixed-capacity buffers (unused
     entries id −1 / factor 1, the ``slash_clip`` kernel's output) are all-gathered
-    with no size exchange and no host synchronisation, then applied as in
-    :func:`merge_slash_sparse` (blacklist code 2 for every listed vouchee).
-    Every rank must pass buffers of the same capacity.  In place on ``sigma``."""
-    bl = blacklist_ids.to(torch.int64)
-    pi = pair_ids.to(torch.int64)
-    pf = pair_factors
+    with no size exchange and no host synchronisation, then applied sparsely by
+    the ``x02_apply`` kernels (csrc/hip/global_liability.hip): only touched
+    agents are read or written.  ``factor`` is a persistent all-ones [A] fp64
+    scratch (allocated when omitted).  Every rank must pass buffers of the same
+    capacity.  Updates ``sigma`` in place and returns it.
+
+    Product order across duplicate (agent, factor) pairs is not fixed, so σ may
+    differ from :func:`merge_slash_sparse` in the last bit where an agent is
+    clipped more than once in one step."""
+    from agent_hypervisor_amd.ops._launch import launch
+
+    bl = blacklist_ids.to(torch.int32)
+    pi = pair_ids.to(torch.int32)
+    pf = pair_factors.to(torch.float64)
     if _ready():
         c = _comm()
         w = c.get_world_size()
@@ -234,16 +242,12 @@ def merge_slash_fixed(
         c.all_gather(gi, pi)
         c.all_gather(gf, pf)
         bl, pi, pf = torch.cat(gb), torch.cat(gi), torch.cat(gf)
-    valid = pi >= 0
-    idx = torch.where(valid, pi, torch.zeros_like(pi))
-    f = torch.where(valid, pf, torch.ones_like(pf))
-    factor = torch.ones_like(sigma)
-    factor.index_reduce_(0, idx, f, "prod")
-    touched = factor < 1.0
-    code = torch.zeros(sigma.numel(), dtype=torch.int64, device=sigma.device)
-    vb = bl >= 0
-    code.index_reduce_(0, torch.where(vb, bl, torch.zeros_like(bl)), torch.where(vb, 2, 0).to(torch.int64), "amax")
-    sigma.copy_(_apply_slash(sigma, factor, touched, code, floor))
+    if factor is None:
+        factor = torch.ones_like(sigma)
+    launch("x02_apply", {"npairs": int(pi.numel()), "nbl": int(bl.numel()), "floor": float(floor)},
+           {"pair_id": pi, "pair_f": pf, "bl": bl, "factor": factor, "sigma": sigma},
+           {"pair_id": torch.int32, "pair_f": torch.float64, "bl": torch.int32, "factor": torch.float64,
+            "sigma": torch.float64})
     return sigma
 
 

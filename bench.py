@@ -173,12 +173,13 @@ def main() -> None:
             "pid": torch.full((cap,), -1, dtype=torch.int32, device=dev),
             "pf": torch.ones(cap, dtype=torch.float64, device=dev),
             "cur": torch.zeros(1, dtype=torch.int64, device=dev),
+            "factor": torch.ones(A, dtype=torch.float64, device=dev),
             "work": None,
             "stream": torch.cuda.Stream(dev) if dev.type == "cuda" else None,
             "gen": torch.Generator(device=dev).manual_seed(99 + rank),
         }
         x01_bytes = A * 8
-        x02_bytes = k * 8 + cap * 16  # per rank: blacklist ids (i64) + (id i64, factor f64) pairs
+        x02_bytes = k * 4 + cap * 12  # per rank: blacklist ids (i32) + (id i32, factor f64) pairs
 
     def liability_step():
         L = liab
@@ -191,7 +192,7 @@ def main() -> None:
         L["pid"].fill_(-1)
         L["pf"].fill_(1.0)
         L["bonds"].slash_clip(L["ids"], 0.95, L["pid"], L["pf"], L["cur"])  # K06 stage
-        merge_slash_fixed(L["sigma"], L["ids"], L["pid"], L["pf"])  # X02
+        merge_slash_fixed(L["sigma"], L["ids"], L["pid"], L["pf"], factor=L["factor"])  # X02
 
     def step():
         b = it[0] & 1

@@ -79,7 +79,13 @@ __global__ __launch_bounds__(256) void slash_clip_kernel(ClipArgs a) {
     for (int64_t j = a.offsets[v]; j < a.offsets[v + 1]; ++j) {
       const int32_t e = a.edge[j];
       if (!a.active[e] || (a.expiry[e] >= 0 && a.now_us > a.expiry[e])) continue;
-      a.active[e] = 0;
+      // claim the bond: the same vouchee may appear twice in one storm, and a bond
+      // is released (and its voucher clipped) once — as the sequential engine does
+      const uintptr_t addr = reinterpret_cast<uintptr_t>(a.active + e);
+      unsigned int* word = reinterpret_cast<unsigned int*>(addr & ~uintptr_t(3));
+      const unsigned int shift = static_cast<unsigned int>(addr & 3u) * 8u;
+      const unsigned int old = atomicAnd(word, ~(0xffu << shift));
+      if (((old >> shift) & 0xffu) == 0u) continue;
       a.released[e] = a.now_us;
       const unsigned long long slot = atomicAdd(a.cursor, 1ull);
       if (slot < static_cast<unsigned long long>(a.cap)) {
@@ -88,6 +94,58 @@ __global__ __launch_bounds__(256) void slash_clip_kernel(ClipArgs a) {
       }
     }
   }
+}
+
+// X02 apply, sparse: only the touched agents are read or written.  Phase 1
+// multiplies each gathered clip factor into a persistent all-ones factor vector
+// (CAS loop: fp64 has no atomic multiply); phase 2 takes each product back with
+// an exchange to 1.0 — the first taker of an agent applies σ = max(σ·Π, floor)
+// and later takers see 1.0 and skip — leaving the factor vector all-ones for the
+// next step; phase 3 zeroes the blacklisted agents.  Product order across
+// duplicate pairs is not fixed (fp64 rounding may differ in the last bit from a
+// sequential product; the exact path is collectives.merge_slash_sparse).
+struct X02Args {
+  int64_t npairs, nbl;
+  double floor;
+  const int32_t* pair_id;    // [npairs] (−1 = unused)
+  const double* pair_f;      // [npairs]
+  const int32_t* bl;         // [nbl] (−1 = unused)
+  double* factor;            // [A] all ones between calls
+  double* sigma;             // [A]
+};
+
+__device__ void atomic_mul(double* p, double f) {
+  unsigned long long* a = reinterpret_cast<unsigned long long*>(p);
+  unsigned long long old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), assumed;
+  do {
+    assumed = old;
+    const double nv = __longlong_as_double(static_cast<long long>(assumed)) * f;
+    old = atomicCAS(a, assumed, static_cast<unsigned long long>(__double_as_longlong(nv)));
+  } while (assumed != old);
+}
+
+__global__ __launch_bounds__(256) void x02_mul_kernel(X02Args a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.npairs && a.pair_id[i] >= 0) atomic_mul(a.factor + a.pair_id[i], a.pair_f[i]);
+}
+
+__global__ __launch_bounds__(256) void x02_apply_kernel(X02Args a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.npairs && a.pair_id[i] >= 0) {
+    const int32_t id = a.pair_id[i];
+    const double prod = __longlong_as_double(static_cast<long long>(
+        atomicExch(reinterpret_cast<unsigned long long*>(a.factor + id),
+                   static_cast<unsigned long long>(__double_as_longlong(1.0)))));
+    if (prod < 1.0) {
+      const double v = a.sigma[id] * prod;
+      a.sigma[id] = v < a.floor ? a.floor : v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void x02_blacklist_kernel(X02Args a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.nbl && a.bl[i] >= 0) a.sigma[a.bl[i]] = 0.0;
 }
 
 int grid_for(int64_t n) {
@@ -119,6 +177,12 @@ ClipArgs to_clip(const py::dict& d) {
                   P<double>(d, "pair_factor"), P<unsigned long long>(d, "cursor")};
 }
 
+X02Args to_x02(const py::dict& d) {
+  return X02Args{d["npairs"].cast<int64_t>(), d["nbl"].cast<int64_t>(), d["floor"].cast<double>(),
+                 P<const int32_t>(d, "pair_id"), P<const double>(d, "pair_f"), P<const int32_t>(d, "bl"),
+                 P<double>(d, "factor"), P<double>(d, "sigma")};
+}
+
 }  // namespace
 
 namespace host {
@@ -148,6 +212,37 @@ void register_global_liability(py::module_& m) {
         check_hip(hipGetLastError(), "slash_clip");
       },
       py::arg("args"), py::arg("stream"));
+  m.def(
+      "x02_apply",
+      [](const py::dict& d, uintptr_t stream) {
+        const X02Args a = to_x02(d);
+        py::gil_scoped_release nogil;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        const int gp = static_cast<int>((std::max<int64_t>(a.npairs, 1) + 255) / 256);
+        const int gb = static_cast<int>((std::max<int64_t>(a.nbl, 1) + 255) / 256);
+        hipLaunchKernelGGL(x02_mul_kernel, dim3(gp), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(x02_apply_kernel, dim3(gp), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(x02_blacklist_kernel, dim3(gb), dim3(256), 0, st, a);
+        check_hip(hipGetLastError(), "x02_apply");
+      },
+      py::arg("args"), py::arg("stream"));
+  m.def("x02_apply_host", [](const py::dict& d) {
+    const X02Args a = to_x02(d);
+    for (int64_t i = 0; i < a.npairs; ++i)
+      if (a.pair_id[i] >= 0) a.factor[a.pair_id[i]] *= a.pair_f[i];
+    for (int64_t i = 0; i < a.npairs; ++i) {
+      if (a.pair_id[i] < 0) continue;
+      const int32_t id = a.pair_id[i];
+      const double prod = a.factor[id];
+      a.factor[id] = 1.0;
+      if (prod < 1.0) {
+        const double v = a.sigma[id] * prod;
+        a.sigma[id] = v < a.floor ? a.floor : v;
+      }
+    }
+    for (int64_t i = 0; i < a.nbl; ++i)
+      if (a.bl[i] >= 0) a.sigma[a.bl[i]] = 0.0;
+  });
   m.def("slash_clip_host", [](const py::dict& d) {
     const ClipArgs a = to_clip(d);
     for (int64_t i = 0; i < a.k; ++i) {
