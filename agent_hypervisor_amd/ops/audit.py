@@ -67,6 +67,28 @@ def merkle_roots(offsets: torch.Tensor, leaves: torch.Tensor) -> torch.Tensor:
     return root
 
 
+def merkle_tree_root(leaves: torch.Tensor) -> torch.Tensor:
+    """K09 work-parallel: Merkle root ([8] int32) of ONE chain of ``n`` leaf digests.
+
+    Multi-pass over ``csrc/hip/merkle_tree.hip``: each pass reduces
+    L = min(9, ⌈log2 count⌉) levels with one 256-thread workgroup per aligned
+    2^L-leaf subtree (LDS-resident levels), until one node is left.  Exactly the
+    reference tree (odd duplication, a single leaf is its own root)."""
+    if leaves.dim() != 2 or leaves.shape[1] != 8 or leaves.dtype != torch.int32:
+        raise TypeError("leaves must be an int32 [n, 8] digest tensor")
+    n = leaves.shape[0]
+    if n == 0:
+        raise ValueError("no leaves")
+    cur = leaves.contiguous()
+    while cur.shape[0] > 1:
+        count = cur.shape[0]
+        levels = min(9, (count - 1).bit_length())
+        out = torch.empty(((count + (1 << levels) - 1) >> levels, 8), dtype=torch.int32, device=cur.device)
+        launch("merkle_tree_pass", {"count": count, "levels": levels}, {"in": cur, "out": out})
+        cur = out
+    return cur[0]
+
+
 def verify_chains(
     data: torch.Tensor,
     offsets: torch.Tensor,

@@ -46,7 +46,7 @@ def subtree_root(leaves: torch.Tensor, height: int) -> torch.Tensor:
         raise ValueError("empty block")
     if n > (1 << height):
         raise ValueError(f"{n} leaves exceed a height-{height} block")
-    r = A.merkle_roots(torch.tensor([0, n], dtype=torch.int32, device=leaves.device), leaves.contiguous())
+    r = A.merkle_tree_root(leaves.contiguous()).reshape(1, 8)  # K09 work-parallel (LDS subtrees, multi-pass)
     for _ in range(height - (math.ceil(math.log2(n)) if n > 1 else 0)):
         r = _node(r)
     return r

@@ -381,6 +381,31 @@ static py::object merkle_root(py::handle seq_h) {
 }
 
 // sha256_hex(str | bytes) -> str   (str is UTF-8 encoded, like str.encode())
+// merkle_root_words(ptr, n) -> hex: the reference tree over n digests held as
+// 8 native u32 words each (a CPU int32 [n, 8] tensor's data), with SHA-NI —
+// the host oracle for the device K09 kernels on long chains.
+static py::str merkle_root_words(uintptr_t ptr, int64_t n) {
+  if (n <= 0) throw py::value_error("no leaves");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(ptr);
+  std::vector<uint32_t> level(src, src + static_cast<size_t>(n) * 8);
+  size_t m = static_cast<size_t>(n);
+  {
+    py::gil_scoped_release nogil;
+    while (m > 1) {
+      const size_t half = (m + 1) / 2;
+      for (size_t i = 0; i < half; ++i) {
+        const uint32_t* l = &level[16 * i];
+        const uint32_t* r = (2 * i + 1 < m) ? &level[16 * i + 8] : l;
+        uint32_t o[8];
+        merkle_node_host(l, r, o);
+        std::memcpy(&level[8 * i], o, sizeof o);
+      }
+      m = half;
+    }
+  }
+  return py::reinterpret_steal<py::str>(hex_pystr(level.data()));
+}
+
 static py::object sha256_hex(py::handle v) {
   const char* p = nullptr;
   Py_ssize_t len = 0;
@@ -465,6 +490,8 @@ void register_audit(py::module_& m) {
   m.def("delta_payload", &delta_payload, "Canonical JSON payload bytes of a SemanticDelta");
   m.def("delta_hash", &delta_hash, "SHA-256 hex of the canonical SemanticDelta payload");
   m.def("merkle_root", &merkle_root, "Merkle root over hex leaf hashes (reference semantics)");
+  m.def("merkle_root_words", &merkle_root_words, py::arg("ptr"), py::arg("n"),
+        "Merkle root over n digests given as native u32 words (host SHA-NI oracle)");
   m.def("sha256_hex", &sha256_hex, "SHA-256 hex digest of str (UTF-8) or bytes");
   m.def("uuid4", &uuid4, py::arg("prefix") = std::string(), "prefix + random uuid4 string");
   m.def("hex_id", &hex_id, py::arg("prefix"), py::arg("nchars"), "prefix + random hex digits");

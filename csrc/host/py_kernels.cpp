@@ -366,6 +366,7 @@ void register_kernels(py::module_& m) {
         kernels_audit(ks);
         kernels_liability(ks);
         kernels_saga(ks);
+        kernels_merkle_tree(ks);
         py::list out;
         for (const auto& k : ks) {
           hipFuncAttributes fa{};

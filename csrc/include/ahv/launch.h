@@ -40,5 +40,6 @@ void kernels_pipeline(std::vector<KernelEntry>& out);
 void kernels_audit(std::vector<KernelEntry>& out);
 void kernels_liability(std::vector<KernelEntry>& out);
 void kernels_saga(std::vector<KernelEntry>& out);
+void kernels_merkle_tree(std::vector<KernelEntry>& out);
 
 }  // namespace ahv
