@@ -141,6 +141,11 @@ class SlashOutcome:
     clip_before: torch.Tensor  # f64 [S, cap]
     clip_after: torch.Tensor  # f64 [S, cap]
 
+    @property
+    def truncated(self) -> torch.Tensor:
+        """Sessions whose clip records exceeded the cap (records dropped, state exact)."""
+        return self.clip_count > self.clip_voucher.shape[1]
+
 
 def slash(
     vb: VouchBatch,
@@ -151,7 +156,12 @@ def slash(
     clip_cap: int = 64,
 ) -> SlashOutcome:
     """K06: slash ``target[s]`` in every session (cascade ≤ 2), mutating ``vb``
-    (bonds released) and ``scores`` in place, like SlashingEngine.slash."""
+    (bonds released) and ``scores`` in place, like SlashingEngine.slash.
+
+    At most ``clip_cap`` clip *records* are kept per session (``clip_count`` holds
+    the true count; :attr:`SlashOutcome.truncated` flags sessions whose records
+    were cut).  The cascade itself — scores and releases — never depends on the
+    cap: the walk keeps its own uncapped per-edge bytes."""
     S = vb.sessions
     dev = vb.device
     offs = (torch.arange(S, dtype=i32, device=dev) * clip_cap).contiguous()
@@ -169,7 +179,8 @@ def slash(
         dict(offsets=vb.offsets, voucher=vb.voucher, vouchee=vb.vouchee, active=vb.active,
              expiry_us=vb.expiry_us, released_us=vb.released_us, target=target, omega=omega, scores=scores,
              clip_offsets=offs, clip_count=out.clip_count, clip_voucher=out.clip_voucher,
-             clip_depth=out.clip_depth, clip_before=out.clip_before, clip_after=out.clip_after),
+             clip_depth=out.clip_depth, clip_before=out.clip_before, clip_after=out.clip_after,
+             clip_walk=torch.empty(max(int(vb.voucher.numel()), 1), dtype=u8, device=dev)),
         dict(target=u8, omega=f64, scores=f64),
     )
     return out

@@ -105,6 +105,32 @@ def _jsonable(x: Any) -> Any:
         return {"__repr__": repr(x)}
 
 
+def _staging_dir(d: str) -> str:
+    """A fresh sibling directory to write a checkpoint into before publishing it."""
+    import tempfile
+
+    parent = os.path.dirname(os.path.abspath(d)) or "."
+    os.makedirs(parent, exist_ok=True)
+    return tempfile.mkdtemp(prefix="." + os.path.basename(os.path.abspath(d)) + ".tmp-", dir=parent)
+
+
+def _publish(tmp: str, d: str) -> str:
+    """Replace ``d`` by the complete checkpoint in ``tmp``.  A crash before this
+    point leaves the previous checkpoint intact; the swap itself is two renames
+    (the old directory is removed only after the new one is in place)."""
+    import shutil
+
+    d = os.path.abspath(d)
+    old = None
+    if os.path.exists(d):
+        old = d + ".old-" + os.path.basename(tmp)
+        os.replace(d, old)
+    os.replace(tmp, d)
+    if old is not None:
+        shutil.rmtree(old, ignore_errors=True)
+    return d
+
+
 # ------------------------------------------------------------ engine tables
 
 
@@ -114,7 +140,7 @@ def save_engine(engine, d: str) -> str:
 
     from agent_hypervisor_amd.models.tables import SessionTable
 
-    os.makedirs(d, exist_ok=True)
+    final, d = d, _staging_dir(d)
     engine.synchronize()
     tensors = {f"sessions.{k}": getattr(engine.sessions, k).detach().cpu().contiguous() for k in SessionTable.COLUMNS}
     n = engine.agents.count
@@ -142,7 +168,8 @@ def save_engine(engine, d: str) -> str:
     with open(os.path.join(d, "engine.json"), "w") as f:
         json.dump(meta, f, indent=2)
     _write_manifest(d, "engine", ["tables.safetensors", "interner.json", "engine.json"])
-    return d
+    _publish(d, final)
+    return final
 
 
 def load_engine(d: str, device: Optional[str] = None, verify: bool = True):
@@ -259,8 +286,8 @@ def _session_record(m) -> dict:
 
 
 def save_hypervisor(hv, d: str) -> str:
-    """Write the scalar hypervisor's state as a checkpoint directory."""
-    os.makedirs(d, exist_ok=True)
+    """Write the hypervisor's state as a checkpoint directory (atomically replaced)."""
+    final, d = d, _staging_dir(d)
     with open(os.path.join(d, "sessions.jsonl"), "w") as f:
         for m in hv.sessions:
             f.write(json.dumps(_session_record(m), sort_keys=True) + "\n")
@@ -281,7 +308,8 @@ def save_hypervisor(hv, d: str) -> str:
         ], f)
     _write_manifest(d, "hypervisor", ["sessions.jsonl", "liability.json", "commitments.json"],
                     {"sessions": len(hv.sessions)})
-    return d
+    _publish(d, final)
+    return final
 
 
 def _delta_from_record(rec: dict):

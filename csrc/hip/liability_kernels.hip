@@ -331,10 +331,13 @@ struct GlobalEdges {
     a->active[k] = 0;
     a->released_us[k] = a->now_us;
   }
-  // the cascade walk re-reads the session's own clip records
-  AHV_HD void note_clip(int32_t, int, bool) const {}
-  AHV_HD int clip_voucher(int32_t base, int32_t ci) const { return a->clip_voucher[base + ci]; }
-  AHV_HD bool clip_cascades(int32_t base, int32_t ci) const { return a->clip_after[base + ci] < kCascadeBelow; }
+  // the cascade walk reads back its own (uncapped) walk bytes, indexed from the
+  // session's first edge — independent of how many records the caller kept
+  AHV_HD void note_clip(int32_t b, int32_t i, int v, bool cascade) const {
+    a->clip_walk[b + i] = static_cast<uint8_t>(v | (cascade ? 0x80 : 0));
+  }
+  AHV_HD int clip_voucher(int32_t b, int32_t ci) const { return a->clip_walk[b + ci] & 0x7f; }
+  AHV_HD bool clip_cascades(int32_t b, int32_t ci) const { return (a->clip_walk[b + ci] & 0x80) != 0; }
 };
 
 template <class Edges>
@@ -374,7 +377,7 @@ AHV_HD void slash_session_t(const SlashArgs& a, int64_t s, const Edges& ed, doub
         const double before = x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
         const double after = clip_sigma(before, omega);
         sc[v * ss] = after;
-        ed.note_clip(nclip, v, after < kCascadeBelow);
+        ed.note_clip(b, nclip, v, after < kCascadeBelow);
         if (nclip < a.clip_cap) {
           a.clip_voucher[base + nclip] = static_cast<uint8_t>(v);
           a.clip_depth[base + nclip] = static_cast<uint8_t>(who_depth);
@@ -404,9 +407,8 @@ AHV_HD void slash_session_t(const SlashArgs& a, int64_t s, const Edges& ed, doub
     }
     if (depth == 0) next0 = nx + 1;
     else next1 = nx + 1;
-    if (nx >= a.clip_cap) continue;
-    const int v = ed.clip_voucher(base, nx);
-    if (ed.clip_cascades(base, nx) && has_live_voucher(ed, b, e, v)) {
+    const int v = ed.clip_voucher(b, nx);
+    if (ed.clip_cascades(b, nx) && has_live_voucher(ed, b, e, v)) {
       who = v;
       who_depth = depth + 1;
       pending = true;
@@ -452,14 +454,16 @@ struct LdsEdges {
   // in LDS: the cascade walk reads them back instead of waiting on a global
   // read-after-write of its own records (~2 µs per step of the walk).
   uint8_t* cl;
-  __device__ void note_clip(int32_t i, int v, bool cascade) const {
-    if (i < kSlashClipLds) cl[i] = static_cast<uint8_t>(v | (cascade ? 0x80 : 0));
+  __device__ void note_clip(int32_t b, int32_t i, int v, bool cascade) const {
+    const uint8_t w = static_cast<uint8_t>(v | (cascade ? 0x80 : 0));
+    if (i < kSlashClipLds) cl[i] = w;
+    else a->clip_walk[b + i] = w;  // beyond the LDS cache: the uncapped global walk bytes
   }
-  __device__ int clip_voucher(int32_t base, int32_t ci) const {
-    return ci < kSlashClipLds ? (cl[ci] & 0x7f) : a->clip_voucher[base + ci];
+  __device__ int clip_voucher(int32_t b, int32_t ci) const {
+    return (ci < kSlashClipLds ? cl[ci] : a->clip_walk[b + ci]) & 0x7f;
   }
-  __device__ bool clip_cascades(int32_t base, int32_t ci) const {
-    return ci < kSlashClipLds ? (cl[ci] & 0x80) != 0 : a->clip_after[base + ci] < kCascadeBelow;
+  __device__ bool clip_cascades(int32_t b, int32_t ci) const {
+    return ((ci < kSlashClipLds ? cl[ci] : a->clip_walk[b + ci]) & 0x80) != 0;
   }
 };
 
@@ -592,8 +596,7 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
     }
     if (depth == 0) next0 = nx + 1;
     else next1 = nx + 1;
-    if (nx >= a.clip_cap) continue;
-    const int c8 = cl[nx];  // the LDS write by the group's lane 0 is visible: same wave
+    const int c8 = cl[nx];  // every clip is cached: a group's session has ≤ kGroupEdges edges ≥ clips  // the LDS write by the group's lane 0 is visible: same wave
     const int v = c8 & 0x7f;
     if (!(c8 & 0x80)) continue;
     bool any_live = false;

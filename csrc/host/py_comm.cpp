@@ -11,8 +11,11 @@
 
 #include <dlfcn.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 
@@ -65,75 +68,107 @@ class RcclComm {
     check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
   }
   ~RcclComm() {
+    std::unique_lock<std::timed_mutex> lk(mu_);
     if (comm_) ncclCommDestroy(comm_);
   }
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
 
+  // Every use of comm_ holds mu_: the watchdog thread may abort while another
+  // thread is enqueueing a collective.  abort() raises `abort_req_` first (new
+  // issuers then fail fast) and tears the communicator down if it can take the
+  // lock; otherwise the issuer inside RCCL aborts on its way out, still holding
+  // the lock — ncclCommAbort never runs concurrently with a call on the handle.
+  template <class F>
+  void issue(const char* what, F&& f) {
+    std::unique_lock<std::timed_mutex> lk(mu_);
+    if (!comm_ || abort_req_.load()) {
+      abort_locked();
+      throw std::runtime_error(std::string(what) + ": RCCL communicator was aborted or destroyed");
+    }
+    const ncclResult_t r = f(comm_);
+    if (abort_req_.load()) abort_locked();
+    check_nccl(r, what);
+  }
+
   void all_reduce(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, const std::string& op,
                   uintptr_t stream) {
-    live();
-    check_nccl(ncclAllReduce(vp(send), vp(recv), count, to_dtype(dt), to_op(op), comm_, sp(stream)), "ncclAllReduce");
+    const ncclDataType_t t = to_dtype(dt);
+    const ncclRedOp_t o = to_op(op);
+    issue("ncclAllReduce", [&](ncclComm_t c) { return ncclAllReduce(vp(send), vp(recv), count, t, o, c, sp(stream)); });
   }
   void all_gather(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, uintptr_t stream) {
-    live();
-    check_nccl(ncclAllGather(vp(send), vp(recv), count, to_dtype(dt), comm_, sp(stream)), "ncclAllGather");
+    const ncclDataType_t t = to_dtype(dt);
+    issue("ncclAllGather", [&](ncclComm_t c) { return ncclAllGather(vp(send), vp(recv), count, t, c, sp(stream)); });
   }
   void reduce_scatter(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, const std::string& op,
                       uintptr_t stream) {
-    live();
-    check_nccl(ncclReduceScatter(vp(send), vp(recv), count, to_dtype(dt), to_op(op), comm_, sp(stream)),
-               "ncclReduceScatter");
+    const ncclDataType_t t = to_dtype(dt);
+    const ncclRedOp_t o = to_op(op);
+    issue("ncclReduceScatter",
+          [&](ncclComm_t c) { return ncclReduceScatter(vp(send), vp(recv), count, t, o, c, sp(stream)); });
   }
   void broadcast(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, int root, uintptr_t stream) {
-    live();
-    check_nccl(ncclBroadcast(vp(send), vp(recv), count, to_dtype(dt), root, comm_, sp(stream)), "ncclBroadcast");
+    const ncclDataType_t t = to_dtype(dt);
+    issue("ncclBroadcast", [&](ncclComm_t c) { return ncclBroadcast(vp(send), vp(recv), count, t, root, c, sp(stream)); });
   }
   // Point-to-point all-to-all of equal blocks (session re-sharding, P08): block
   // b of `send` goes to rank b, block b of `recv` comes from rank b.
   void all_to_all(uintptr_t send, uintptr_t recv, size_t block_count, const std::string& dt, size_t elem_bytes,
                   uintptr_t stream) {
-    live();
     const ncclDataType_t t = to_dtype(dt);
     const size_t stride = block_count * elem_bytes;
-    check_nccl(ncclGroupStart(), "ncclGroupStart");
-    for (int r = 0; r < world_; ++r) {
-      check_nccl(ncclSend(static_cast<char*>(vp(send)) + r * stride, block_count, t, r, comm_, sp(stream)), "ncclSend");
-      check_nccl(ncclRecv(static_cast<char*>(vp(recv)) + r * stride, block_count, t, r, comm_, sp(stream)), "ncclRecv");
-    }
-    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+    issue("ncclAllToAll", [&](ncclComm_t c) {
+      ncclResult_t r = ncclGroupStart();
+      for (int k = 0; r == ncclSuccess && k < world_; ++k) {
+        r = ncclSend(static_cast<char*>(vp(send)) + k * stride, block_count, t, k, c, sp(stream));
+        if (r == ncclSuccess) r = ncclRecv(static_cast<char*>(vp(recv)) + k * stride, block_count, t, k, c, sp(stream));
+      }
+      const ncclResult_t e = ncclGroupEnd();
+      return r != ncclSuccess ? r : e;
+    });
   }
   void destroy() {
+    std::unique_lock<std::timed_mutex> lk(mu_);
     if (comm_) {
-      check_nccl(ncclCommDestroy(comm_), "ncclCommDestroy");
+      const ncclResult_t r = ncclCommDestroy(comm_);
       comm_ = nullptr;
+      check_nccl(r, "ncclCommDestroy");
     }
   }
   // Asynchronous error state of the communicator (failure detection, §5.3):
-  // "" while healthy, else RCCL's error text.
-  std::string async_error() const {
-    if (!comm_) return "destroyed";
+  // "" while healthy, else RCCL's error text ("busy" if an enqueue held the lock
+  // for over a second — the caller polls again).
+  std::string async_error() {
+    std::unique_lock<std::timed_mutex> lk(mu_, std::defer_lock);
+    if (!lk.try_lock_for(std::chrono::seconds(1))) return "busy";
+    if (!comm_) return abort_req_.load() ? "aborted" : "destroyed";
     ncclResult_t st = ncclSuccess;
     check_nccl(ncclCommGetAsyncError(comm_, &st), "ncclCommGetAsyncError");
     return st == ncclSuccess || st == ncclInProgress ? std::string() : std::string(ncclGetErrorString(st));
   }
   // Tear down a communicator whose peers may be gone; pending collectives are
-  // cancelled instead of waited for.
+  // cancelled instead of waited for.  Safe from any thread (see issue()).
   void abort() {
-    if (comm_) {
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
-    }
+    abort_req_.store(true);
+    std::unique_lock<std::timed_mutex> lk(mu_, std::defer_lock);
+    if (lk.try_lock_for(std::chrono::seconds(2))) abort_locked();
   }
+  bool aborted() const { return abort_req_.load(); }
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return device_; }
 
  private:
-  void live() const {
-    if (!comm_) throw std::runtime_error("RCCL communicator was destroyed");
+  void abort_locked() {
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
   }
   ncclComm_t comm_ = nullptr;
+  std::timed_mutex mu_;
+  std::atomic<bool> abort_req_{false};
   int rank_, world_, device_;
 };
 
@@ -175,8 +210,9 @@ void register_comm(py::module_& m) {
       .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("all_to_all", &RcclComm::all_to_all, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &RcclComm::destroy)
-      .def("async_error", &RcclComm::async_error)
-      .def("abort", &RcclComm::abort)
+      .def("async_error", &RcclComm::async_error, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("aborted", &RcclComm::aborted)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("device", &RcclComm::device);

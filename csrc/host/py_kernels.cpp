@@ -204,7 +204,7 @@ static SlashArgs to_slash(const py::dict& d) {
   P(vouchee, const uint8_t); P(active, uint8_t); P(expiry_us, const int64_t); P(released_us, int64_t);
   P(target, const uint8_t); P(omega, const double); P(scores, double); P(clip_offsets, int32_t);
   P(clip_count, int32_t); P(clip_voucher, uint8_t); P(clip_depth, uint8_t); P(clip_before, double);
-  P(clip_after, double); V(clip_cap, int32_t);
+  P(clip_after, double); V(clip_cap, int32_t); P(clip_walk, uint8_t);
   return a;
 }
 static HashManyArgs to_hash_many(const py::dict& d) {

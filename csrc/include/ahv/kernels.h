@@ -243,7 +243,9 @@ struct SlashArgs {
   uint8_t* clip_depth;      // [cap] out
   double* clip_before;      // [cap] out
   double* clip_after;       // [cap] out
-  int32_t clip_cap;         // records per session
+  int32_t clip_cap;         // records per session (records beyond it are dropped, not the cascade)
+  uint8_t* clip_walk;       // [E] scratch: the cascade walk's (voucher | cascade<<7) per clip, uncapped —
+                            // a session has at most (its edge count) clips, indexed from its first edge
 };
 void launch_slash(const SlashArgs&, hipStream_t);
 void slash_host(const SlashArgs&);

@@ -149,3 +149,27 @@ def test_engine_tamper_detected_by_merkle_reverify(tmp_path):
     ck._write_manifest(d, "engine", ["tables.safetensors", "interner.json", "engine.json"])
     with pytest.raises(CheckpointError, match="Merkle"):
         load_engine(d, device="cpu")
+
+
+async def test_failed_save_keeps_previous_checkpoint(tmp_path, monkeypatch):
+    """a crash mid-save must not destroy the last good checkpoint."""
+    from agent_hypervisor_amd.runtime import checkpoint as ck
+    from hypervisor import Hypervisor, SessionConfig
+
+    hv = Hypervisor()
+    m = await hv.create_session(SessionConfig(), "did:admin")
+    d = str(tmp_path / "ck")
+    ck.save_hypervisor(hv, d)
+    before = ck.read_manifest(d, "hypervisor")
+    await hv.create_session(SessionConfig(), "did:admin2")
+
+    def boom(*a, **k):
+        raise OSError("disk full")
+
+    monkeypatch.setattr(ck, "_write_manifest", boom)
+    with pytest.raises(OSError):
+        ck.save_hypervisor(hv, d)
+    monkeypatch.undo()
+    assert ck.read_manifest(d, "hypervisor") == before
+    restored = ck.load_hypervisor(d, hv=Hypervisor(device="host"))
+    assert [x.sso.session_id for x in restored.sessions] == [m.sso.session_id]

@@ -51,3 +51,39 @@ def test_rccl_all_reduce_inside_hip_graph(cuda_device):
     torch.cuda.synchronize(cuda_device)
     assert stats.tolist() == [6] * 6
     comm.destroy()
+
+
+def test_abort_from_another_thread_during_collectives(cuda_device):
+    """the watchdog aborts from its own thread while the issuing thread
+    enqueues collectives; every call either completes or fails cleanly."""
+    import threading
+    import time
+
+    from agent_hypervisor_amd.parallel.rccl import Communicator
+
+    comm = Communicator.from_process_group(device=cuda_device.index or 0)
+    x = torch.ones(1 << 16, dtype=torch.float64, device=cuda_device)
+    outcomes = {"ok": 0, "aborted": 0}
+    stop = threading.Event()
+
+    def issuer():
+        while not stop.is_set():
+            try:
+                comm.all_reduce(x)
+                outcomes["ok"] += 1
+            except RuntimeError as e:
+                assert "aborted" in str(e) or "destroyed" in str(e)
+                outcomes["aborted"] += 1
+                break
+
+    t = threading.Thread(target=issuer)
+    t.start()
+    time.sleep(0.05)
+    comm.abort()  # from this (the watchdog's) thread
+    stop.set()
+    t.join(timeout=30)
+    assert not t.is_alive()
+    torch.cuda.synchronize(cuda_device)
+    assert outcomes["ok"] > 0 and comm.async_error() in ("aborted", "destroyed")
+    with pytest.raises(RuntimeError):
+        comm.all_reduce(x)

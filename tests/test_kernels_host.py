@@ -164,7 +164,10 @@ def test_vouch_admit_matches_engine_sequence():
     assert bonded.tolist() == want_bonded
 
 
-def test_slash_cascade_matches_slashing_engine():
+@pytest.mark.parametrize("clip_cap", [64, 1])
+def test_slash_cascade_matches_slashing_engine(clip_cap):
+    """clip_cap=1: records are truncated, but scores, releases and the cascade
+    (which re-reads every clip) still equal SlashingEngine."""
     from hypervisor.liability.slashing import SlashingEngine
 
     ve, sids, parts, sigmas = _random_vouch_world(n_sessions=60, seed=5, expiry=False)
@@ -183,7 +186,7 @@ def test_slash_cascade_matches_slashing_engine():
                 d[did] = sigmas[s][did]
                 scores[s, k] = sigmas[s][did]
         py_scores.append(d)
-    out = LI.slash(vb, torch.tensor(targets, dtype=u8), omega, scores, now_us)
+    out = LI.slash(vb, torch.tensor(targets, dtype=u8), omega, scores, now_us, clip_cap=clip_cap)
     se = SlashingEngine(ve)
     for s, (sid, p) in enumerate(zip(sids, parts)):
         before = len(se.history)
@@ -197,6 +200,9 @@ def test_slash_cascade_matches_slashing_engine():
                 assert out.scores[s, k].item() == py_scores[s][did]
             else:
                 assert torch.isnan(out.scores[s, k])
+        if n > clip_cap:
+            assert out.truncated[s]
+            continue
         got = {(p[out.clip_voucher[s, c].item()], out.clip_before[s, c].item(), out.clip_after[s, c].item())
                for c in range(n)}
         want = {(c.voucher_did, c.sigma_before, c.sigma_after) for r in res for c in r.voucher_clips}
