@@ -107,8 +107,8 @@ void fanout_host(const FanoutArgs& a) { for (int64_t g = 0; g < a.groups; ++g) f
 // ring-buffer window, prune entries older than the window, honour the breaker
 // cooldown, then score the windowed calls against the *current* agent ring.
 
-AHV_HD void breach_elem(const BreachArgs& a, int64_t p) {
-  const int64_t now = a.now_us[p];
+AHV_HD void breach_call(const BreachArgs& a, int64_t p, int64_t c) {
+  const int64_t now = a.now_us[c];
   const int32_t W = a.window_cap;
   int64_t* ts = a.ts + p * W;
   uint8_t* called = a.called + p * W;
@@ -117,35 +117,44 @@ AHV_HD void breach_elem(const BreachArgs& a, int64_t p) {
   // append (deque maxlen semantics: drop the oldest when full)
   if (count == W) { head = (head + 1) % W; --count; }
   const int32_t slot = (head + count) % W;
+  const uint8_t nc = a.new_called[c];
   ts[slot] = now;
-  called[slot] = a.new_called[p];
+  called[slot] = nc;
   ++count;
   a.total[p] += 1;
+  if (a.ring_counts != nullptr && nc < 4) a.ring_counts[p * 4 + nc] += 1;
   // prune calls older than the window
   const int64_t cutoff = now - a.window_us;
   while (count > 0 && ts[head] < cutoff) { head = (head + 1) % W; --count; }
   a.head[p] = head;
   a.count[p] = count;
-  a.severity[p] = 0;
-  a.rate[p] = 0.0;
-  a.event[p] = 0;
+  a.severity[c] = 0;
+  a.rate[c] = 0.0;
+  a.event[c] = 0;
+  if (a.window != nullptr) a.window[c] = count;
   // breaker cooldown suppresses analysis
   if (a.tripped[p] && a.tripped_at_us[p] != 0 && now < a.tripped_at_us[p] + a.cooldown_us) return;
   if (count < 5) return;
-  const uint8_t ring = a.agent_ring[p];
+  const uint8_t ring = a.agent_ring[c];
   int32_t hits = 0;
   for (int32_t k = 0; k < count; ++k) hits += called[(head + k) % W] < ring ? 1 : 0;
   const double rate = static_cast<double>(hits) / static_cast<double>(count);
   const uint8_t sev = breach_severity(rate);
-  a.rate[p] = rate;
-  a.severity[p] = sev;
-  a.hits[p] = hits;
+  a.rate[c] = rate;
+  a.severity[c] = sev;
+  a.hits[c] = hits;
   if (sev == 0) return;
-  a.event[p] = 1;
+  a.event[c] = 1;
   if (sev >= 3) {
     a.tripped[p] = 1;
     a.tripped_at_us[p] = now;
   }
+}
+AHV_HD void breach_elem(const BreachArgs& a, int64_t g) {
+  const int64_t p = a.rows != nullptr ? a.rows[g] : g;
+  const int64_t c0 = a.offsets != nullptr ? a.offsets[g] : g;
+  const int64_t c1 = a.offsets != nullptr ? a.offsets[g + 1] : g + 1;
+  for (int64_t c = c0; c < c1; ++c) breach_call(a, p, c);
 }
 __global__ void breach_kernel(BreachArgs a) { AHV_GRID_STRIDE(p, a.n) breach_elem(a, p); }
 void launch_breach(const BreachArgs& a, hipStream_t s) {
@@ -157,8 +166,16 @@ void breach_host(const BreachArgs& a) { for (int64_t p = 0; p < a.n; ++p) breach
 
 // ------------------------------------------------------------------ K17
 
-AHV_HD void bucket_elem(const BucketArgs& a, int64_t i) {
-  a.ok[i] = token_bucket_consume(a.tokens[i], a.last_us[i], a.capacity[i], a.rate[i], a.now_us, a.cost[i]);
+AHV_HD void bucket_elem(const BucketArgs& a, int64_t g) {
+  const int64_t b = a.rows != nullptr ? a.rows[g] : g;
+  const int64_t c0 = a.offsets != nullptr ? a.offsets[g] : g;
+  const int64_t c1 = a.offsets != nullptr ? a.offsets[g + 1] : g + 1;
+  for (int64_t c = c0; c < c1; ++c) {
+    const uint8_t ok = token_bucket_consume(a.tokens[b], a.last_us[b], a.capacity[b], a.rate[b], a.now_us, a.cost[c]);
+    a.ok[c] = ok;
+    if (a.total != nullptr) a.total[b] += 1;
+    if (a.rejected != nullptr && !ok) a.rejected[b] += 1;
+  }
 }
 __global__ void bucket_kernel(BucketArgs a) { AHV_GRID_STRIDE(i, a.n) bucket_elem(a, i); }
 void launch_bucket(const BucketArgs& a, hipStream_t s) {

@@ -135,15 +135,18 @@ static FanoutArgs to_fanout(const py::dict& d) {
 static BreachArgs to_breach(const py::dict& d) {
   BreachArgs a{};
   V(n, int64_t); V(window_cap, int32_t); V(window_us, int64_t); V(cooldown_us, int64_t);
+  P(rows, const int32_t); P(offsets, const int32_t);
   P(now_us, const int64_t); P(agent_ring, const uint8_t); P(new_called, const uint8_t); P(ts, int64_t);
   P(called, uint8_t); P(head, int32_t); P(count, int32_t); P(total, int64_t); P(tripped, uint8_t);
-  P(tripped_at_us, int64_t); P(severity, uint8_t); P(rate, double); P(hits, int32_t); P(event, uint8_t);
+  P(tripped_at_us, int64_t); P(ring_counts, int64_t); P(severity, uint8_t); P(rate, double); P(hits, int32_t);
+  P(event, uint8_t); P(window, int32_t);
   return a;
 }
 static BucketArgs to_bucket(const py::dict& d) {
   BucketArgs a{};
-  V(n, int64_t); V(now_us, int64_t); P(tokens, double); P(last_us, int64_t); P(capacity, const double);
-  P(rate, const double); P(cost, const double); P(ok, uint8_t);
+  V(n, int64_t); V(now_us, int64_t); P(rows, const int32_t); P(offsets, const int32_t); P(tokens, double);
+  P(last_us, int64_t); P(capacity, const double); P(rate, const double); P(cost, const double);
+  P(total, int64_t); P(rejected, int64_t); P(ok, uint8_t);
   return a;
 }
 static ExpiryArgs to_expiry(const py::dict& d) {

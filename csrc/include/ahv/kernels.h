@@ -61,39 +61,53 @@ void launch_fanout(const FanoutArgs&, hipStream_t);
 void fanout_host(const FanoutArgs&);
 
 // K16 breach window
+// Calls are grouped by profile: group g applies calls [offsets[g], offsets[g+1])
+// in order to profile rows[g] of the resident tables.  With rows/offsets null,
+// group g is one call (index g) on profile g.  Per-call arrays are indexed by
+// call, profile arrays by row.
 struct BreachArgs {
-  int64_t n;           // profiles receiving one call each
+  int64_t n;           // groups (profiles touched)
   int32_t window_cap;  // ring capacity (reference deque maxlen 1000)
   int64_t window_us;
   int64_t cooldown_us;
-  const int64_t* now_us;      // [n] call timestamps
-  const uint8_t* agent_ring;  // [n] caller's current ring
-  const uint8_t* new_called;  // [n] ring being called
-  int64_t* ts;                // [n, cap]
-  uint8_t* called;            // [n, cap]
-  int32_t* head;              // [n]
-  int32_t* count;             // [n]
-  int64_t* total;             // [n]
-  uint8_t* tripped;           // [n]
-  int64_t* tripped_at_us;     // [n]
-  uint8_t* severity;          // [n] out 0 none .. 4 critical
-  double* rate;               // [n] out
-  int32_t* hits;              // [n] out
-  uint8_t* event;             // [n] out 1 = BreachEvent produced
+  const int32_t* rows;        // [n] profile row of each group, or null
+  const int32_t* offsets;     // [n+1] call ranges, or null
+  const int64_t* now_us;      // [calls] call timestamps
+  const uint8_t* agent_ring;  // [calls] caller's current ring
+  const uint8_t* new_called;  // [calls] ring being called
+  int64_t* ts;                // [P, cap]
+  uint8_t* called;            // [P, cap]
+  int32_t* head;              // [P]
+  int32_t* count;             // [P]
+  int64_t* total;             // [P]
+  uint8_t* tripped;           // [P]
+  int64_t* tripped_at_us;     // [P]
+  int64_t* ring_counts;       // [P, 4] calls per called ring, or null
+  uint8_t* severity;          // [calls] out 0 none .. 4 critical
+  double* rate;               // [calls] out
+  int32_t* hits;              // [calls] out
+  uint8_t* event;             // [calls] out 1 = BreachEvent produced
+  int32_t* window;            // [calls] out windowed call count, or null
 };
 void launch_breach(const BreachArgs&, hipStream_t);
 void breach_host(const BreachArgs&);
 
 // K17 token bucket
+// Requests grouped by bucket like BreachArgs (rows/offsets null = one request
+// per bucket, index = row).
 struct BucketArgs {
-  int64_t n;
+  int64_t n;                // groups
   int64_t now_us;
-  double* tokens;
-  int64_t* last_us;
-  const double* capacity;
-  const double* rate;
-  const double* cost;
-  uint8_t* ok;
+  const int32_t* rows;      // [n] or null
+  const int32_t* offsets;   // [n+1] or null
+  double* tokens;           // [B]
+  int64_t* last_us;         // [B]
+  const double* capacity;   // [B]
+  const double* rate;       // [B]
+  const double* cost;       // [requests]
+  int64_t* total;           // [B] requests seen, or null
+  int64_t* rejected;        // [B] requests refused, or null
+  uint8_t* ok;              // [requests] out
 };
 void launch_bucket(const BucketArgs&, hipStream_t);
 void bucket_host(const BucketArgs&);

@@ -242,9 +242,9 @@ static void test_governance() {
       ar[p] = static_cast<uint8_t>(rnd(1, 3));
       nc[p] = static_cast<uint8_t>(rnd(0, 3));
     }
-    BreachArgs b{P, W, 60'000'000, 30'000'000, now.data(), ar.data(), nc.data(), ts.data(), called.data(),
-                 head.data(), cnt.data(), tot.data(), trip.data(), tat.data(), sev.data(), rate.data(),
-                 hits.data(), evt.data()};
+    BreachArgs b{P, W, 60'000'000, 30'000'000, nullptr, nullptr, now.data(), ar.data(), nc.data(), ts.data(),
+                 called.data(), head.data(), cnt.data(), tot.data(), trip.data(), tat.data(), nullptr, sev.data(),
+                 rate.data(), hits.data(), evt.data(), nullptr};
     breach_host(b);
   }
   for (int p = 0; p < P; ++p) CHECK(cnt[p] <= W && tot[p] == 50);

@@ -133,6 +133,39 @@ class CMVKAdapter:
             self._on_drift_detected(res)
         return res
 
+    def record_drift_batch(
+        self,
+        agent_dids,
+        session_ids,
+        drift_scores,
+        action_ids=None,
+        device="cpu",
+    ) -> list[DriftCheckResult]:
+        """Classify many already-computed drift scores (e.g. a bulk verifier's
+        output tensor) with one K22-drift launch on ``device`` and record them
+        like :meth:`check_behavioral_drift` (history, drift callback)."""
+        import torch
+
+        from agent_hypervisor_amd.ops import ledger as LG
+
+        th = self.thresholds
+        d = drift_scores if isinstance(drift_scores, torch.Tensor) else torch.tensor(
+            [float(x) for x in drift_scores], dtype=torch.float64)
+        d = d.to(device=device, dtype=torch.float64).contiguous()
+        sev = LG.drift_severity(d, th.low, th.medium, th.high, th.critical)
+        host = torch.stack([d, sev.to(torch.float64)]).cpu().tolist()
+        out = []
+        for i, (agent, session) in enumerate(zip(agent_dids, session_ids)):
+            s = DriftSeverity(LG.SEVERITY[int(host[1][i])])
+            res = DriftCheckResult(agent_did=agent, session_id=session, drift_score=host[0][i], severity=s,
+                                   passed=s in (DriftSeverity.NONE, DriftSeverity.LOW),
+                                   action_id=action_ids[i] if action_ids else None)
+            self._check_history.append(res)
+            if not res.passed and self._on_drift_detected:
+                self._on_drift_detected(res)
+            out.append(res)
+        return out
+
     def get_agent_drift_history(self, agent_did: str, session_id: Optional[str] = None) -> list[DriftCheckResult]:
         return [
             r

@@ -129,6 +129,9 @@ class CausalAttributor:
     ) -> AttributionResult:
         nodes = self.build_causal_dag(agent_actions, failure_step_id, failure_agent_did)
         raw = self.raw_scores(nodes, set(agent_actions.keys()), risk_weights or {})
+        return self._result(saga_id, session_id, nodes, raw, failure_agent_did)
+
+    def _result(self, saga_id, session_id, nodes, raw: dict[str, float], failure_agent_did) -> AttributionResult:
         total = sum(raw.values()) or 1.0
         attrs = [
             FaultAttribution(
@@ -150,6 +153,42 @@ class CausalAttributor:
         )
         self._history.append(res)
         return res
+
+    def attribute_batch(self, cases, device="cpu") -> list[AttributionResult]:
+        """:meth:`attribute` for many failure cases — dicts of its keyword
+        arguments — with the raw per-agent scores of all cases from one K21
+        launch on ``device``; normalisation and ranking stay on the host."""
+        import torch
+
+        from agent_hypervisor_amd.ops import ledger as LG
+
+        node_off, agent_off, agent_of, succ, root, omega = [0], [0], [], [], [], []
+        per_case = []
+        for c in cases:
+            nodes = self.build_causal_dag(c["agent_actions"], c["failure_step_id"], c["failure_agent_did"])
+            agents = list(c["agent_actions"].keys())
+            col = {a: j for j, a in enumerate(agents)}
+            rw = c.get("risk_weights") or {}
+            for n in nodes:
+                agent_of.append(col[n.agent_did])
+                succ.append(1 if n.success else 0)
+                root.append(1 if n.is_root_cause else 0)
+                omega.append(float(rw.get(n.action_id, 0.5)))
+            node_off.append(len(agent_of))
+            agent_off.append(agent_off[-1] + len(agents))
+            per_case.append((c, nodes, agents))
+        i32 = torch.int32
+        ints = torch.tensor(node_off + agent_off + agent_of, dtype=i32).to(device)
+        C, N = len(per_case), len(agent_of)
+        flags = torch.tensor([succ, root], dtype=torch.uint8).reshape(2, N).to(device)
+        raw = LG.attribution_raw(ints[: C + 1], ints[C + 1: 2 * C + 2], ints[2 * C + 2:], flags[0].contiguous(),
+                                 flags[1].contiguous(), torch.tensor(omega, dtype=torch.float64).to(device))
+        raw = raw.cpu().tolist()
+        out = []
+        for k, (c, nodes, agents) in enumerate(per_case):
+            scores = dict(zip(agents, raw[agent_off[k]: agent_off[k + 1]]))
+            out.append(self._result(c["saga_id"], c["session_id"], nodes, scores, c["failure_agent_did"]))
+        return out
 
     @property
     def attribution_history(self) -> list[AttributionResult]:

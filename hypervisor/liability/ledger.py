@@ -23,6 +23,7 @@ from typing import Optional
 
 from agent_hypervisor_amd._native import C as _C
 from hypervisor._clock import now as _now
+from hypervisor._devsel import device_variant
 
 
 class LedgerEntryType(str, Enum):
@@ -81,7 +82,11 @@ class LiabilityLedger:
     PROBATION_THRESHOLD = 0.3
     DENY_THRESHOLD = 0.6
 
-    def __init__(self) -> None:
+    def __new__(cls, *args, device=None, **kwargs):
+        """``device=...`` → the device-resident DeviceLiabilityLedger (batched kernel path)."""
+        return device_variant(cls, LiabilityLedger, "DeviceLiabilityLedger", device)
+
+    def __init__(self, device=None) -> None:
         self._entries: list[LedgerEntry] = []
         self._by_agent: dict[str, list[LedgerEntry]] = {}
 
@@ -145,6 +150,10 @@ class LiabilityLedger:
             risk_score=round(risk, 4),
             recommendation=self.recommendation_for(risk),
         )
+
+    def compute_risk_profiles(self, agent_dids) -> list[AgentRiskProfile]:
+        """Profiles of many agents (one K22 launch in the device variant)."""
+        return [self.compute_risk_profile(a) for a in agent_dids]
 
     def should_admit(self, agent_did: str) -> tuple[bool, str]:
         prof = self.compute_risk_profile(agent_did)

@@ -19,6 +19,7 @@ from typing import Optional
 
 from agent_hypervisor_amd._native import C as _C
 from hypervisor._clock import now as _now
+from hypervisor._devsel import device_variant
 
 
 class QuarantineReason(str, Enum):
@@ -55,7 +56,11 @@ class QuarantineRecord:
 class QuarantineManager:
     DEFAULT_QUARANTINE_SECONDS = 300
 
-    def __init__(self) -> None:
+    def __new__(cls, *args, device=None, **kwargs):
+        """``device=...`` → the device-resident DeviceQuarantineManager (batched kernel path)."""
+        return device_variant(cls, QuarantineManager, "DeviceQuarantineManager", device)
+
+    def __init__(self, device=None) -> None:
         self._quarantines: dict[str, QuarantineRecord] = {}
 
     def quarantine(
@@ -86,6 +91,11 @@ class QuarantineManager:
         )
         self._quarantines[rec.quarantine_id] = rec
         return rec
+
+    def quarantine_batch(self, requests) -> list[QuarantineRecord]:
+        """``quarantine`` over ``(agent_did, session_id, reason[, details,
+        duration_seconds, forensic_data])`` tuples in order."""
+        return [self.quarantine(*q) for q in requests]
 
     def release(self, agent_did: str, session_id: str) -> Optional[QuarantineRecord]:
         rec = self.get_active_quarantine(agent_did, session_id)

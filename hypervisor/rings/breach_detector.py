@@ -22,6 +22,7 @@ from enum import Enum
 from typing import Optional
 
 from hypervisor._clock import now as _now
+from hypervisor._devsel import device_variant
 from hypervisor.models import ExecutionRing
 
 
@@ -80,7 +81,11 @@ class RingBreachDetector:
     CIRCUIT_BREAKER_COOLDOWN = 30
     MIN_CALLS = 5
 
-    def __init__(self, window_seconds: int = 0) -> None:
+    def __new__(cls, *args, device=None, **kwargs):
+        """``device=...`` → the device-resident DeviceRingBreachDetector (batched kernel path)."""
+        return device_variant(cls, RingBreachDetector, "DeviceRingBreachDetector", device)
+
+    def __init__(self, window_seconds: int = 0, device=None) -> None:
         self._profiles: dict[str, AgentCallProfile] = {}
         self._breach_history: list[BreachEvent] = []
         self.window_seconds = window_seconds or self.WINDOW_SECONDS
@@ -140,6 +145,11 @@ class RingBreachDetector:
         )
         self._breach_history.append(ev)
         return ev
+
+    def record_calls_batch(self, calls, now=None) -> list[Optional[BreachEvent]]:
+        """``record_call`` over ``(agent_did, session_id, agent_ring, called_ring)``
+        tuples in order (the device variant runs them as one K16 launch)."""
+        return [self.record_call(*c) for c in calls]
 
     def is_breaker_tripped(self, agent_did: str, session_id: str) -> bool:
         p = self._profiles.get(f"{agent_did}:{session_id}")

@@ -22,6 +22,7 @@ from typing import Optional
 
 from agent_hypervisor_amd._native import C as _C
 from hypervisor._clock import now as _now
+from hypervisor._devsel import device_variant
 from hypervisor.models import ExecutionRing
 
 
@@ -63,7 +64,11 @@ class RingElevationManager:
     MAX_ELEVATION_TTL = 3600
     DEFAULT_TTL = 300
 
-    def __init__(self) -> None:
+    def __new__(cls, *args, device=None, **kwargs):
+        """``device=...`` → the device-resident DeviceRingElevationManager (batched kernel path)."""
+        return device_variant(cls, RingElevationManager, "DeviceRingElevationManager", device)
+
+    def __init__(self, device=None) -> None:
         self._elevations: dict[str, RingElevation] = {}
         self._by_key: dict[tuple[str, str], list[str]] = {}
         self._parent_map: dict[str, str] = {}
@@ -109,6 +114,17 @@ class RingElevationManager:
         self._elevations[e.elevation_id] = e
         self._by_key.setdefault((agent_did, session_id), []).append(e.elevation_id)
         return e
+
+    def request_elevation_batch(self, requests) -> list:
+        """``request_elevation`` over argument tuples in order → each
+        RingElevation, or the RingElevationError it raised."""
+        out: list = []
+        for q in requests:
+            try:
+                out.append(self.request_elevation(*q))
+            except RingElevationError as e:
+                out.append(e)
+        return out
 
     def get_active_elevation(self, agent_did: str, session_id: str) -> Optional[RingElevation]:
         for eid in self._by_key.get((agent_did, session_id), ()):

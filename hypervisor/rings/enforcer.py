@@ -107,6 +107,46 @@ class RingEnforcer:
             requires_sre_witness=code == REASON_NEEDS_WITNESS,
         )
 
+    def check_batch(
+        self,
+        agent_rings,
+        actions,
+        sigma_effs,
+        has_consensus=None,
+        has_sre_witness=None,
+        device="cpu",
+    ) -> list[RingCheckResult]:
+        """:meth:`check` for many (agent ring, action, σ_eff) triples with one
+        K02 launch on ``device`` (``cpu`` runs the kernel's host twin)."""
+        import torch
+
+        from agent_hypervisor_amd.ops import rings as RG
+
+        n = len(actions)
+        flags = [RG.action_flags(a.is_admin, a.is_read_only, a.required_ring is ExecutionRing.RING_1_PRIVILEGED)
+                 for a in actions]
+        u8 = torch.uint8
+        cons = [bool(x) for x in (has_consensus or [False] * n)]
+        wit = [bool(x) for x in (has_sre_witness or [False] * n)]
+        packed = torch.tensor([[int(ExecutionRing(r).value) for r in agent_rings], flags, cons, wit], dtype=u8)
+        packed = packed.to(device)
+        sig = torch.tensor([float(s) for s in sigma_effs], dtype=torch.float64).to(device)
+        req, reason = RG.ring_check(packed[0], packed[1], sig, packed[2], packed[3])
+        host = torch.stack([req, reason]).cpu().tolist()
+        out = []
+        for i in range(n):
+            ar, required, code = ExecutionRing(agent_rings[i]), ExecutionRing(host[0][i]), host[1][i]
+            out.append(RingCheckResult(
+                allowed=code == REASON_GRANTED,
+                required_ring=required,
+                agent_ring=ar,
+                sigma_eff=float(sigma_effs[i]),
+                reason=self.reason_text(code, ar.value, required.value, float(sigma_effs[i])),
+                requires_consensus=code == REASON_NEEDS_CONSENSUS,
+                requires_sre_witness=code == REASON_NEEDS_WITNESS,
+            ))
+        return out
+
     def compute_ring(self, sigma_eff: float, has_consensus: bool = False) -> ExecutionRing:
         return ExecutionRing.from_sigma_eff(sigma_eff, has_consensus)
 

@@ -19,6 +19,7 @@ from datetime import datetime
 from typing import Optional
 
 from hypervisor._clock import now as _now
+from hypervisor._devsel import device_variant
 from hypervisor.models import ExecutionRing
 
 
@@ -72,7 +73,11 @@ class RateLimitStats:
 
 
 class AgentRateLimiter:
-    def __init__(self, ring_limits: Optional[dict[ExecutionRing, tuple[float, float]]] = None) -> None:
+    def __new__(cls, *args, device=None, **kwargs):
+        """``device=...`` → the device-resident DeviceAgentRateLimiter (batched kernel path)."""
+        return device_variant(cls, AgentRateLimiter, "DeviceAgentRateLimiter", device)
+
+    def __init__(self, ring_limits: Optional[dict[ExecutionRing, tuple[float, float]]] = None, device=None) -> None:
         self._limits = ring_limits or dict(DEFAULT_RING_LIMITS)
         self._buckets: dict[str, TokenBucket] = {}
         self._stats: dict[str, RateLimitStats] = {}
@@ -106,6 +111,11 @@ class AgentRateLimiter:
             return self.check(agent_did, session_id, ring, cost)
         except RateLimitExceeded:
             return False
+
+    def check_batch(self, requests, now=None) -> list[bool]:
+        """``try_check`` over ``(agent_did, session_id, ring[, cost])`` tuples in
+        order (the device variant serves them with one K17 launch)."""
+        return [self.try_check(*q) for q in requests]
 
     def update_ring(self, agent_did: str, session_id: str, new_ring: ExecutionRing) -> None:
         key = f"{agent_did}:{session_id}"

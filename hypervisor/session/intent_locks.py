@@ -25,6 +25,7 @@ from typing import Optional
 
 from agent_hypervisor_amd._native import C as _C
 from hypervisor._clock import now as _now
+from hypervisor._devsel import device_variant
 
 
 class LockIntent(str, Enum):
@@ -58,7 +59,11 @@ class DeadlockError(Exception):
 
 
 class IntentLockManager:
-    def __init__(self, record_waits: bool = False) -> None:
+    def __new__(cls, *args, device=None, **kwargs):
+        """``device=...`` → the device-resident DeviceIntentLockManager (batched kernel path)."""
+        return device_variant(cls, IntentLockManager, "DeviceIntentLockManager", device)
+
+    def __init__(self, record_waits: bool = False, device=None) -> None:
         self._locks: dict[str, IntentLock] = {}
         self._resource_locks: dict[str, list[str]] = {}
         self._wait_for: dict[str, set[str]] = {}
@@ -97,6 +102,17 @@ class IntentLockManager:
         self._locks[lock.lock_id] = lock
         self._resource_locks.setdefault(resource_path, []).append(lock.lock_id)
         return lock
+
+    def acquire_batch(self, requests) -> list:
+        """``acquire`` over ``(agent_did, session_id, resource_path, intent[,
+        saga_step_id])`` tuples in order → each IntentLock or the error raised."""
+        out: list = []
+        for q in requests:
+            try:
+                out.append(self.acquire(*q))
+            except (LockContentionError, DeadlockError) as e:
+                out.append(e)
+        return out
 
     def release(self, lock_id: str) -> None:
         lock = self._locks.get(lock_id)

@@ -235,7 +235,7 @@ def test_saga_kernels(cuda_device):
 def test_security_kernels(cuda_device):
     g = torch.Generator().manual_seed(5)
     n, cap = 4096, 64
-    prof = SEC.BreachProfiles.allocate(n, cap)
+    prof = SEC.BreachProfiles.allocate(n, cap, ring_counts=True)
     fields = list(prof.__dataclass_fields__)
     t = torch.zeros(n, dtype=i64)
     cpu_p = SEC.BreachProfiles(*[getattr(prof, f).clone() for f in fields])

@@ -369,7 +369,7 @@ def test_breach_window_matches_detector():
         _clock.set_clock(lambda: t)
         agent_ring = [rng.choice([1, 2, 3]) for _ in range(n)]
         called = [rng.choice([0, 1, 2, 3]) for _ in range(n)]
-        sev, rate, hits, ev = SEC.breach_record(
+        sev, rate, hits, ev, _ = SEC.breach_record(
             prof, torch.full((n,), _clock.to_us(t), dtype=i64), torch.tensor(agent_ring, dtype=u8),
             torch.tensor(called, dtype=u8),
         )
