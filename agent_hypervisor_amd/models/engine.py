@@ -30,7 +30,7 @@ from typing import Optional, Sequence
 import torch
 
 from agent_hypervisor_amd._native import C  # noqa: F401 - loads the native extension (fails loudly when missing)
-from agent_hypervisor_amd.models.tables import AgentTable, SessionTable, VouchTable
+from agent_hypervisor_amd.models.tables import AgentTable, SessionTable, VouchSlab
 from agent_hypervisor_amd.ops import pipeline as _pipeline_op
 from agent_hypervisor_amd.utils.interner import Interner
 from agent_hypervisor_amd.utils.stats import SpreadCounters
@@ -162,7 +162,7 @@ class GovernanceEngine:
         device: Optional[str] = None,
         session_capacity: Optional[int] = None,
         agent_capacity: Optional[int] = None,
-        vouch_capacity: Optional[int] = None,
+        vouch_stride: int = 16,
         dmax: int = 8,
         seed: Optional[int] = None,
         creator_did: str = "did:mesh:admin",
@@ -171,7 +171,8 @@ class GovernanceEngine:
         self.interner = Interner()
         self.sessions = SessionTable(session_capacity or min(RUNTIME.session_capacity, 1 << 20), self.device, dmax)
         self.agents = AgentTable(agent_capacity or min(RUNTIME.agent_capacity, 1 << 20), self.device)
-        self.vouches = VouchTable.allocate(vouch_capacity or 1024, self.device)
+        self.vouches = VouchSlab(self.sessions.capacity, vouch_stride, self.device)
+        self.gc_retention_us = 90 * 86_400 * 1_000_000  # RetentionPolicy.delta_retention_days
         self.seed = int(seed if seed is not None else int.from_bytes(os.urandom(8), "little") >> 1)
         self.creator_id = self.interner.intern(creator_did)
         self._next_slot = 0
@@ -259,14 +260,17 @@ class GovernanceEngine:
         pool_b, pool_o, pool_l = self.interner.device_view(self.device)
         now = int(now_us if now_us is not None else _clock.now_us())
         slot_base, id_base = self._next_slot, self._id_counter
+        v = self.vouches
         scalars = dict(
+            vouch_stride=v.stride, gc_retention_us=int(self.gc_retention_us),
             n=n, slot_base=slot_base, capacity=cap, deltas=deltas, nch=len(specs), dmax=self.sessions.dmax,
             max_participants=max_participants, min_sigma_eff=float(min_sigma_eff), now_us=now,
             seed=self.seed, id_base=id_base, creator_id=self.creator_id, audit=int(bool(audit)),
         )
         tensors = dict(
             session_agent=agents, agent_sigma=self.agents.sigma, agent_did=self.agents.did, changes=ch,
-            vouch_offsets=None, vouch_active=None, vouch_released_us=None,
+            vouch_count=v.count, vouch_active=v.active if v.allocated else None,
+            vouch_released_us=v.released_us if v.allocated else None,
             pool_bytes=pool_b, pool_off=pool_o, pool_len=pool_l,
             stats=self._spread.begin() if stats is not None else None,
         )
@@ -289,6 +293,12 @@ class GovernanceEngine:
         self._next_slot = (slot_base + n) % cap
         self._id_counter = id_base + 3 * n
         return PipelineBatch(self, slot_base, n, id_base, now, deltas, list(specs), agents)
+
+    def stage_vouches(self, slots, voucher, vouchee, bonded, expiry_us=None) -> torch.Tensor:
+        """Record vouch edges of the sessions in ``slots`` (participant-local
+        voucher/vouchee indices) in the resident slab; the pipeline's terminate
+        stage releases them (K07).  Returns the flat edge indices."""
+        return self.vouches.stage(slots, voucher, vouchee, bonded, expiry_us)
 
     def synchronize(self) -> None:
         if self.device.type == "cuda":

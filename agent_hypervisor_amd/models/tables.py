@@ -15,6 +15,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+from typing import Optional
+
 import torch
 
 P_MAX = 16  # participant row width (kMaxParticipants)
@@ -94,30 +96,59 @@ class AgentTable:
         return ids
 
 
-@dataclass
-class VouchTable:
-    """Vouch edges in creation order (σ_eff sums must follow creation order)."""
+class VouchSlab:
+    """Resident vouch edges of the pipeline's session slots: slot ``s`` owns
+    edges ``[s·stride, s·stride + count[s])`` in creation order.  The pipeline
+    kernel's terminate stage releases the active ones (K07, stamping
+    ``released_us``) and empties the slot for the session that reuses it.
+    Columns are allocated on the first :meth:`stage` (an engine that never
+    vouches carries no slab)."""
 
-    voucher: torch.Tensor
-    vouchee: torch.Tensor
-    session: torch.Tensor
-    bonded: torch.Tensor
-    pct: torch.Tensor
-    active: torch.Tensor
-    expiry_us: torch.Tensor
-    released_us: torch.Tensor
-    count: int = 0
+    COLUMNS = ("voucher", "vouchee", "bonded", "active", "expiry_us", "released_us")
 
-    @classmethod
-    def allocate(cls, capacity: int, device) -> "VouchTable":
-        dev = torch.device(device)
-        return cls(
-            voucher=_z((capacity,), torch.int32, dev),
-            vouchee=_z((capacity,), torch.int32, dev),
-            session=_z((capacity,), torch.int32, dev),
-            bonded=_z((capacity,), torch.float64, dev),
-            pct=_z((capacity,), torch.float64, dev),
-            active=_z((capacity,), torch.uint8, dev),
-            expiry_us=torch.full((capacity,), -1, dtype=torch.int64, device=dev),
-            released_us=_z((capacity,), torch.int64, dev),
-        )
+    def __init__(self, capacity: int, stride: int, device) -> None:
+        self.capacity, self.stride, self.device = capacity, stride, torch.device(device)
+        self.count: Optional[torch.Tensor] = None
+
+    def _alloc(self) -> None:
+        n, dev = self.capacity * self.stride, self.device
+        self.count = _z((self.capacity,), torch.int32, dev)
+        self.voucher = _z((n,), torch.int32, dev)
+        self.vouchee = _z((n,), torch.int32, dev)
+        self.bonded = _z((n,), torch.float64, dev)
+        self.active = _z((n,), torch.uint8, dev)
+        self.expiry_us = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        self.released_us = _z((n,), torch.int64, dev)
+
+    @property
+    def allocated(self) -> bool:
+        return self.count is not None
+
+    def stage(self, slots, voucher, vouchee, bonded, expiry_us=None) -> torch.Tensor:
+        """Append edges (in the given order) to the slabs of ``slots``; returns
+        their flat edge indices.  Raises if a slot would exceed ``stride``."""
+        if not self.allocated:
+            self._alloc()
+        dev = self.device
+        slots = torch.as_tensor(slots, dtype=torch.int64).to(dev)
+        m = slots.numel()
+        order = torch.sort(slots, stable=True).indices
+        ss = slots[order]
+        first = torch.ones(m, dtype=torch.bool, device=dev)
+        if m > 1:
+            first[1:] = ss[1:] != ss[:-1]
+        start = torch.cummax(torch.where(first, torch.arange(m, device=dev), torch.zeros_like(ss)), 0).values
+        rank = torch.empty(m, dtype=torch.int64, device=dev)
+        rank[order] = torch.arange(m, device=dev) - start
+        pos = self.count[slots].to(torch.int64) + rank
+        if m and int(pos.max()) >= self.stride:
+            raise ValueError(f"vouch slab holds {self.stride} edges per session slot")
+        idx = slots * self.stride + pos
+        self.voucher[idx] = torch.as_tensor(voucher, dtype=torch.int32).to(dev)
+        self.vouchee[idx] = torch.as_tensor(vouchee, dtype=torch.int32).to(dev)
+        self.bonded[idx] = torch.as_tensor(bonded, dtype=torch.float64).to(dev)
+        self.active[idx] = 1
+        self.expiry_us[idx] = -1 if expiry_us is None else torch.as_tensor(expiry_us, dtype=torch.int64).to(dev)
+        self.released_us[idx] = 0
+        self.count.index_add_(0, slots, torch.ones(m, dtype=torch.int32, device=dev))
+        return idx

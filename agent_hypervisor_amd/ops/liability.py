@@ -87,6 +87,31 @@ def bond_tiles(tiles: torch.Tensor, sigma: torch.Tensor, omega: torch.Tensor,
     return tuple(out)
 
 
+def bond_fused(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us: int,
+               members: "torch.Tensor | None" = None, agent_exposure: "torch.Tensor | None" = None,
+               bonded_in: bool = False):
+    """K03/K04 straight from the CSR edges on fp64 MFMA (no dense tile):
+    (σ_eff [S,16], exposure [S,16], bonded_in [S,16] or None).
+
+    Same outputs as ``build_tiles`` + ``bond_tiles`` at a fraction of the HBM
+    traffic; sums agree with the creation-order reference to ulp level.  With
+    ``members``/``agent_exposure`` the exposure is also scattered into the
+    agent-indexed vector (X01 input) by the same kernel."""
+    S = vb.sessions
+    dev = vb.device
+    se = torch.empty((S, TILE), dtype=f64, device=dev)
+    ex = torch.empty((S, TILE), dtype=f64, device=dev)
+    bi = torch.empty((S, TILE), dtype=f64, device=dev) if bonded_in else None
+    if members is not None and (agent_exposure is None or tuple(members.shape) != (S, TILE)):
+        raise ValueError("members must be int64 [S, 16] and come with agent_exposure")
+    launch("bond_fused", {"sessions": S, "now_us": int(now_us)},
+           dict(offsets=vb.offsets, voucher=vb.voucher, vouchee=vb.vouchee, bonded=vb.bonded, active=vb.active,
+                expiry_us=vb.expiry_us, sigma=sigma, omega=omega, sigma_eff=se, exposure=ex, bonded_in=bi,
+                members=members, agent_exposure=agent_exposure if members is not None else None),
+           dict(_CSR_DT, exposure=f64, bonded_in=f64, members=torch.int64, agent_exposure=f64))
+    return se, ex, bi
+
+
 def sigma_eff_exact(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us: int) -> torch.Tensor:
     """K03 creation-order path: bit-identical to VouchingEngine.compute_sigma_eff."""
     out = torch.empty((vb.sessions, TILE), dtype=f64, device=vb.device)

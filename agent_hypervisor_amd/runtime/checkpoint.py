@@ -147,8 +147,10 @@ def save_engine(engine, d: str) -> str:
     tensors["agents.sigma"] = engine.agents.sigma[:n].cpu().contiguous()
     tensors["agents.did"] = engine.agents.did[:n].cpu().contiguous()
     v = engine.vouches
-    for f in ("voucher", "vouchee", "session", "bonded", "pct", "active", "expiry_us", "released_us"):
-        tensors[f"vouches.{f}"] = getattr(v, f)[: v.count].cpu().contiguous()
+    if v.allocated:
+        tensors["vouches.count"] = v.count.cpu().contiguous()
+        for f in v.COLUMNS:
+            tensors[f"vouches.{f}"] = getattr(v, f).cpu().contiguous()
     save_file(tensors, os.path.join(d, "tables.safetensors"), metadata={"format": FORMAT, "version": str(VERSION)})
     with open(os.path.join(d, "interner.json"), "w") as f:
         json.dump([engine.interner.str(i) for i in range(len(engine.interner))], f)
@@ -157,8 +159,9 @@ def save_engine(engine, d: str) -> str:
         "dmax": engine.sessions.dmax,
         "agent_capacity": engine.agents.capacity,
         "agent_count": n,
-        "vouch_capacity": int(v.voucher.numel()),
-        "vouch_count": v.count,
+        "vouch_stride": v.stride,
+        "vouch_slab": v.allocated,
+        "gc_retention_us": engine.gc_retention_us,
         "seed": engine.seed,
         "creator_id": engine.creator_id,
         "next_slot": engine._next_slot,
@@ -187,7 +190,7 @@ def load_engine(d: str, device: Optional[str] = None, verify: bool = True):
     with open(os.path.join(d, "interner.json")) as f:
         strings = json.load(f)
     eng = GovernanceEngine(device=device, session_capacity=meta["session_capacity"],
-                           agent_capacity=meta["agent_capacity"], vouch_capacity=meta["vouch_capacity"],
+                           agent_capacity=meta["agent_capacity"], vouch_stride=meta.get("vouch_stride", 16),
                            dmax=meta["dmax"], seed=meta["seed"], creator_did=strings[meta["creator_id"]])
     ids = eng.interner.intern_many(strings)
     if ids != list(range(len(strings))):
@@ -199,10 +202,13 @@ def load_engine(d: str, device: Optional[str] = None, verify: bool = True):
     eng.agents.sigma[:n].copy_(t["agents.sigma"])
     eng.agents.did[:n].copy_(t["agents.did"])
     eng.agents.count = n
-    vc = meta["vouch_count"]
-    for f_ in ("voucher", "vouchee", "session", "bonded", "pct", "active", "expiry_us", "released_us"):
-        getattr(eng.vouches, f_)[:vc].copy_(t[f"vouches.{f_}"])
-    eng.vouches.count = vc
+    if meta.get("vouch_slab"):
+        v = eng.vouches
+        v._alloc()
+        v.count.copy_(t["vouches.count"])
+        for f_ in v.COLUMNS:
+            getattr(v, f_).copy_(t[f"vouches.{f_}"])
+    eng.gc_retention_us = meta.get("gc_retention_us", eng.gc_retention_us)
     eng._next_slot, eng._id_counter = meta["next_slot"], meta["id_counter"]
     eng._last_specs = [tuple(x) for x in meta["last_specs"]] if meta["last_specs"] else None
     if verify:

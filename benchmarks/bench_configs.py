@@ -174,11 +174,13 @@ def config3(ctx: Ctx, args):
     side = torch.cuda.Stream(ctx.dev) if ctx.dev.type == "cuda" else None
 
     def liability_stage(cur):
-        tiles = LI.build_tiles(vb, 0)
         comm[cur].wait()  # buffer reuse: the exchange from two steps ago is done
         exposure[cur].zero_()
         # σ_eff / exposure on fp64 MFMA; exposure scattered into the agent vector in-kernel
-        LI.bond_tiles(tiles, sigma, omega, members=members, agent_exposure=exposure[cur])
+        if args.tiles:  # round-1 pair: dense tile through HBM, then MFMA sums
+            LI.bond_tiles(LI.build_tiles(vb, 0), sigma, omega, members=members, agent_exposure=exposure[cur])
+        else:  # fused: CSR edges → one-hot MFMA products, no tile
+            LI.bond_fused(vb, sigma, omega, 0, members=members, agent_exposure=exposure[cur])
 
     def step():
         cur = it[0] & 1
@@ -199,7 +201,8 @@ def config3(ctx: Ctx, args):
         X.allreduce_stats(stats)
 
     el, lat = ctx.timed(step, args.steps, args.warmup)
-    ctx.emit(config="config3", what="pipeline+vouch tiles+exposure " + ("reduce_scatter to owners" if args.owner_reduce
+    ctx.emit(config="config3", liability="tiles" if args.tiles else "fused",
+             what="pipeline+sigma_eff/exposure+" + ("reduce_scatter to owners" if args.owner_reduce
                                                                           else "all_reduce[A]") + " (overlapped)",
              agents=A_,
              sessions_global=args.sessions or 100_000, sessions_per_rank=S, exposure_bytes=A_ * 8,
@@ -306,6 +309,7 @@ def main():
     ap.add_argument("--agents", type=int, default=0)
     ap.add_argument("--edges", type=int, default=0)
     ap.add_argument("--deltas", type=int, default=0)
+    ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
     ap.add_argument("--owner-reduce", action="store_true", help="config3: reduce-scatter exposure to agent owners")
     args = ap.parse_args()
     ctx = Ctx(args.device)

@@ -1,0 +1,96 @@
+"""K03/K04 liability-stage variants on one GPU (config3 shapes):
+
+* ``tiles``  — build_tiles (CSR → dense [S,16,16] fp64 tile in HBM) + bond_tiles
+  (tile → MFMA column/row sums): round 1's MFMA path;
+* ``csr``    — sigma_eff_csr (one lane per (session, vouchee), creation order,
+  LDS-staged edges; σ_eff only);
+* ``fused``  — bond_fused (CSR edges straight into v_mfma_f64_16x16x4_f64 as
+  one-hot products: σ_eff + exposure + agent scatter, no tile).
+
+``*_ns`` variants skip the agent-indexed exposure scatter (fp64 atomics into the
+[A] vector), the like-for-like comparison with ``csr``.
+
+Prints one JSON line per (variant, S) with µs per call (CUDA events, median of
+``--iters``).  rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE runs of this script give
+the HBM traffic per kernel (profiles/liability_fused_r2.md)."""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from agent_hypervisor_amd.ops import liability as LI  # noqa: E402
+from benchmarks.bench_configs import random_vouch_batch  # noqa: E402
+
+
+def time_us(fn, iters: int) -> float:
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        out.append(a.elapsed_time(b) * 1e3)
+    return statistics.median(out)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sessions", type=int, nargs="*", default=[100_000, 1_250_000])
+    ap.add_argument("--edges-per-session", type=int, default=8)
+    ap.add_argument("--agents", type=int, default=1_000_000)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default="", help="comma list of variants (profiling)")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    only = set(a.only.split(",")) if a.only else {"tiles", "tiles_ns", "csr", "fused", "fused_ns"}
+    for S in a.sessions:
+        vb = random_vouch_batch(S, a.edges_per_session, dev, seed=1)
+        g = torch.Generator(device=dev).manual_seed(2)
+        sigma = torch.rand((S, 16), dtype=torch.float64, device=dev, generator=g)
+        omega = torch.full((S,), 0.5, dtype=torch.float64, device=dev)
+        members = torch.randint(0, a.agents, (S, 16), device=dev, generator=g)
+        ax = torch.zeros(a.agents, dtype=torch.float64, device=dev)
+        ref = LI.sigma_eff_exact(vb, sigma, omega, 0)
+        E = S * a.edges_per_session
+        res = {}
+        if "tiles" in only:
+            def tiles():
+                t = LI.build_tiles(vb, 0)
+                return LI.bond_tiles(t, sigma, omega, members=members, agent_exposure=ax)
+            res["tiles"] = (time_us(tiles, a.iters), (tiles()[0] - ref).abs().max().item())
+        if "tiles_ns" in only:
+            def tiles_ns():
+                return LI.bond_tiles(LI.build_tiles(vb, 0), sigma, omega)
+            res["tiles_ns"] = (time_us(tiles_ns, a.iters), (tiles_ns()[0] - ref).abs().max().item())
+        if "fused_ns" in only:
+            def fused_ns():
+                return LI.bond_fused(vb, sigma, omega, 0)
+            res["fused_ns"] = (time_us(fused_ns, a.iters), (fused_ns()[0] - ref).abs().max().item())
+        if "csr" in only:
+            res["csr"] = (time_us(lambda: LI.sigma_eff_exact(vb, sigma, omega, 0), a.iters), 0.0)
+        if "fused" in only:
+            def fused():
+                return LI.bond_fused(vb, sigma, omega, 0, members=members, agent_exposure=ax)
+            res["fused"] = (time_us(fused, a.iters), (fused()[0] - ref).abs().max().item())
+        for k, (us, err) in res.items():
+            print(json.dumps(dict(variant=k, sessions=S, edges=E, us=round(us, 2),
+                                  edges_per_us=round(E / us, 1), max_abs_err_vs_csr=err,
+                                  outputs={"csr": "sigma_eff"}.get(k, "sigma_eff+exposure" + (
+                                      "" if k.endswith("_ns") else "+agent_scatter")))),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -96,6 +96,114 @@ void bond_tiles_host(const BondTileArgs& a) {
   }
 }
 
+// ------------------------------------------------- K03/K04 fused (CSR → MFMA)
+// Operand layouts of v_mfma_f64_16x16x4_f64 (as in bond_tiles_mfma_kernel):
+// lane l = 16·r + c supplies A[i=c][k=r] and B[k=r][j=c]; it receives
+// D[row=r+4q][col=c] in register q.  A wave owns 16 consecutive sessions (their
+// edges are one contiguous CSR range).  Edges are read 64 at a time, one per
+// lane, fully coalesced (liveness, voucher and vouchee packed into one word);
+// the next 64 are loaded before the current ones are consumed.  For each chunk of
+// 4 edges, lane (r, c) fetches edge 4u+r of the batch with a cross-lane shuffle:
+// A is its bond if the edge lies in session c's CSR range [off_c, off_c+1) — each
+// lane tests its own session, no search — and B is whether the edge's vouchee
+// (voucher) is c.  Two MFMAs per chunk accumulate Σbonded per (session, vouchee)
+// and per (session, voucher).  In-chunk sums are MFMA-ordered, so results agree
+// with the creation-order reference to ulp level (the CSR kernel stays the
+// bit-exact path).
+
+constexpr int kFusedWaves = 4;      // waves per block
+constexpr int kFusedSessions = 16;  // sessions per wave (A rows)
+
+__device__ __forceinline__ void fused_load(const BondFusedArgs& a, int32_t g, int32_t e1, uint32_t& meta, double& bond) {
+  meta = 0u;
+  bond = 0.0;
+  if (g < e1) {
+    const bool live = live_edge(a.active, a.expiry_us, g, a.now_us);
+    meta = live ? (0x10000u | (static_cast<uint32_t>(a.voucher[g]) << 8) | a.vouchee[g]) : 0u;
+    bond = a.bonded[g];
+  }
+}
+
+__global__ __launch_bounds__(64 * kFusedWaves) void bond_fused_mfma_kernel(BondFusedArgs a) {
+  const int wave = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  const int r = l >> 4, c = l & 15;
+  const int64_t s0 = (static_cast<int64_t>(blockIdx.x) * kFusedWaves + wave) * kFusedSessions;
+  if (s0 >= a.sessions) return;  // wave-uniform
+  const int64_t s_end = s0 + kFusedSessions < a.sessions ? s0 + kFusedSessions : a.sessions;
+  const int32_t e0 = a.offsets[s0], e1 = a.offsets[s_end];
+  const int64_t sc = s0 + c;
+  const int32_t off_c = sc < s_end ? a.offsets[sc] : e1;
+  const int32_t off_c1 = sc < s_end ? a.offsets[sc + 1] : e1;
+  f64x4 acc_in = {0.0, 0.0, 0.0, 0.0};
+  f64x4 acc_out = {0.0, 0.0, 0.0, 0.0};
+  uint32_t meta;
+  double bond;
+  fused_load(a, e0 + l, e1, meta, bond);
+  for (int32_t base = e0; base < e1; base += 64) {
+    uint32_t meta_n;
+    double bond_n;
+    fused_load(a, base + 64 + l, e1, meta_n, bond_n);  // next batch in flight
+    // chunks of this batch, rounded up to a multiple of 4 (lanes past e1 carry
+    // meta = 0, bond = 0: padding chunks add exact zeros)
+    const int chunks = (e1 - base) >= 64 ? 16 : ((e1 - base + 15) >> 4) << 2;  // wave-uniform
+    for (int u0 = 0; u0 < chunks; u0 += 4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int src = 4 * (u0 + j) + r;
+        const uint32_t m = __shfl(meta, src, 64);
+        const double b = __shfl(bond, src, 64);
+        const int32_t g = base + src;
+        const double av = ((m >> 16) && g >= off_c && g < off_c1) ? b : 0.0;
+        const double bi = (m & 0xffu) == static_cast<uint32_t>(c) ? 1.0 : 0.0;
+        const double bo = ((m >> 8) & 0xffu) == static_cast<uint32_t>(c) ? 1.0 : 0.0;
+        acc_in = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bi, acc_in, 0, 0, 0);
+        acc_out = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bo, acc_out, 0, 0, 0);
+      }
+    }
+    meta = meta_n;
+    bond = bond_n;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t s = s0 + r + 4 * q;
+    if (s >= s_end) continue;
+    const int64_t o = s * kTile + c;  // 64 consecutive doubles per q across the wave
+    const double bonded = acc_in[q];
+    if (a.bonded_in) a.bonded_in[o] = bonded;
+    a.sigma_eff[o] = sigma_eff_combine(score_or_zero(a.sigma[o]), a.omega[s], bonded);
+    a.exposure[o] = acc_out[q];
+    if (a.members) unsafeAtomicAdd(a.agent_exposure + a.members[o], acc_out[q]);
+  }
+}
+
+void launch_bond_fused(const BondFusedArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  const int64_t per_block = static_cast<int64_t>(kFusedWaves) * kFusedSessions;
+  hipLaunchKernelGGL(bond_fused_mfma_kernel, grid1(a.sessions, static_cast<int>(per_block)), dim3(64 * kFusedWaves),
+                     0, st, a);
+  check_hip(hipGetLastError(), "bond_fused_mfma_kernel");
+}
+
+// Host twin: creation-order sums per (session, vouchee) and (session, voucher).
+void bond_fused_host(const BondFusedArgs& a) {
+  for (int64_t s = 0; s < a.sessions; ++s) {
+    double in[kTile] = {0.0}, out[kTile] = {0.0};
+    for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k) {
+      if (!live_edge(a.active, a.expiry_us, k, a.now_us)) continue;
+      in[a.vouchee[k]] += a.bonded[k];
+      out[a.voucher[k]] += a.bonded[k];
+    }
+    for (int j = 0; j < kTile; ++j) {
+      const int64_t o = s * kTile + j;
+      if (a.bonded_in) a.bonded_in[o] = in[j];
+      a.sigma_eff[o] = sigma_eff_combine(score_or_zero(a.sigma[o]), a.omega[s], in[j]);
+      a.exposure[o] = out[j];
+      if (a.members) a.agent_exposure[a.members[o]] += out[j];
+    }
+  }
+}
+
 // ------------------------------------------------------ tile build (CSR → dense)
 // One wave per session; lane j owns tile entries j, j+64, j+128, j+192 and sums
 // the matching live edges in creation order (deterministic).
@@ -633,6 +741,7 @@ void kernels_liability(std::vector<KernelEntry>& out) {
   out.push_back({"sigma_eff_csr_kernel", reinterpret_cast<const void*>(&sigma_eff_csr_kernel)});
   out.push_back({"build_tiles_kernel", reinterpret_cast<const void*>(&build_tiles_kernel)});
   out.push_back({"bond_tiles_mfma_kernel", reinterpret_cast<const void*>(&bond_tiles_mfma_kernel)});
+  out.push_back({"bond_fused_mfma_kernel", reinterpret_cast<const void*>(&bond_fused_mfma_kernel)});
   out.push_back({"vouch_admit_kernel", reinterpret_cast<const void*>(&vouch_admit_kernel)});
 }
 

@@ -55,9 +55,13 @@ static PipelineArgs pipeline_args(const py::dict& d) {
   a.agent_sigma = ptr<const double>(d, "agent_sigma");
   a.agent_did = ptr<const int32_t>(d, "agent_did");
   a.changes = ptr<const ChangeIds>(d, "changes");
-  a.vouch_offsets = ptr<const int32_t>(d, "vouch_offsets");
+  a.vouch_count = ptr<int32_t>(d, "vouch_count");
+  a.vouch_stride = d.contains("vouch_stride") ? val<int32_t>(d, "vouch_stride") : 0;
   a.vouch_active = ptr<uint8_t>(d, "vouch_active");
   a.vouch_released_us = ptr<int64_t>(d, "vouch_released_us");
+  a.gc_retention_us = d.contains("gc_retention_us") ? val<int64_t>(d, "gc_retention_us") : (int64_t(90) * 86400 * 1000000);
+  if (a.vouch_count && (a.vouch_stride <= 0 || !a.vouch_active || !a.vouch_released_us))
+    throw py::value_error("vouch slab needs stride, active and released_us");
   a.pool.bytes = ptr<const uint8_t>(d, "pool_bytes");
   a.pool.off = ptr<const int64_t>(d, "pool_off");
   a.pool.len = ptr<const int32_t>(d, "pool_len");
@@ -153,6 +157,14 @@ static ExpiryArgs to_expiry(const py::dict& d) {
   ExpiryArgs a{};
   V(n, int64_t); V(now_us, int64_t); P(active, uint8_t); P(expires_us, const int64_t);
   P(released_us, int64_t); P(expired, uint8_t);
+  return a;
+}
+static BondFusedArgs to_bond_fused(const py::dict& d) {
+  BondFusedArgs a{};
+  V(sessions, int64_t); V(now_us, int64_t); P(offsets, const int32_t); P(voucher, const uint8_t);
+  P(vouchee, const uint8_t); P(bonded, const double); P(active, const uint8_t); P(expiry_us, const int64_t);
+  P(sigma, const double); P(omega, const double); P(sigma_eff, double); P(exposure, double); P(bonded_in, double);
+  P(members, const int64_t); P(agent_exposure, double);
   return a;
 }
 static LedgerArgs to_ledger(const py::dict& d) {
@@ -294,6 +306,7 @@ void register_kernels(py::module_& m) {
   bind_pair(m, "drift", to_drift, launch_drift, drift_host);
   bind_pair(m, "attribution", to_attribution, launch_attribution, attribution_host);
   bind_pair(m, "bond_tiles", to_bond_tiles, launch_bond_tiles, bond_tiles_host);
+  bind_pair(m, "bond_fused", to_bond_fused, launch_bond_fused, bond_fused_host);
   bind_pair(m, "build_tiles", to_vouch_csr, launch_build_tiles, build_tiles_host);
   bind_pair(m, "sigma_eff_csr", to_vouch_csr, launch_sigma_eff_csr, sigma_eff_csr_host);
   bind_pair(m, "release_bonds", to_vouch_csr, launch_release, release_host);

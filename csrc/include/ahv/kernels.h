@@ -213,6 +213,31 @@ void sigma_eff_csr_host(const VouchCsrArgs&);
 void launch_release(const VouchCsrArgs&, hipStream_t);
 void release_host(const VouchCsrArgs&);
 
+// K03/K04 fused: CSR edges → fp64 MFMA, no dense tile anywhere.  With 16
+// sessions per wave, a chunk of 4 consecutive edges is one K=4 slice of
+//   bonded_in[i][j] = Σ_k A[i][k]·Bin[k][j],  exposure[i][v] = Σ_k A[i][k]·Bout[k][v]
+// where A[i][k] = live bond of edge k if it belongs to session i (else 0) and
+// Bin/Bout are the one-hot vouchee/voucher of edge k.  σ_eff = min(σ + ω·bonded_in, 1).
+struct BondFusedArgs {
+  int64_t sessions;
+  int64_t now_us;
+  const int32_t* offsets;    // [S+1]
+  const uint8_t* voucher;    // [E]
+  const uint8_t* vouchee;    // [E]
+  const double* bonded;      // [E]
+  const uint8_t* active;     // [E]
+  const int64_t* expiry_us;  // [E] or null (< 0 = none)
+  const double* sigma;       // [S,16] (NaN = absent → 0)
+  const double* omega;       // [S]
+  double* sigma_eff;         // [S,16] out
+  double* exposure;          // [S,16] out (per voucher)
+  double* bonded_in;         // [S,16] out (per vouchee), or null
+  const int64_t* members;    // [S,16] global agent ids, or null
+  double* agent_exposure;    // [A] += exposure (fp64 atomics), with members
+};
+void launch_bond_fused(const BondFusedArgs&, hipStream_t);
+void bond_fused_host(const BondFusedArgs&);
+
 // K05 — admit new vouch requests (per session, in request order)
 struct VouchAdmitArgs {
   int64_t sessions;

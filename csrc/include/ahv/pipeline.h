@@ -79,9 +79,14 @@ struct PipelineArgs {
   const double* agent_sigma;     // [A] σ_raw per agent id
   const int32_t* agent_did;      // [A] pool id of each agent's DID
   const ChangeIds* changes;      // [D * nch] (shared by all sessions)
-  const int32_t* vouch_offsets;  // [cap+1] CSR of the session's vouch edges, or null
-  uint8_t* vouch_active;         // [E] cleared on release
-  int64_t* vouch_released_us;    // [E]
+  // Resident vouch slab (VouchSlab in models/tables.py), or vouch_count == null:
+  // slot s owns edges [s·stride, s·stride + vouch_count[s]); terminate releases
+  // the active ones (K07) and empties the slot for its next session.
+  int32_t* vouch_count;          // [cap]
+  int32_t vouch_stride;          // edges per slot
+  uint8_t* vouch_active;         // [cap·stride] cleared on release
+  int64_t* vouch_released_us;    // [cap·stride]
+  int64_t gc_retention_us;       // RetentionPolicy.delta_retention_days in µs
   StrPool pool;
   SessionTables t;
   unsigned long long* stats;     // [kPipeStats] batch counters (X04), accumulated, or null
@@ -153,28 +158,9 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   if (((session_op_allowed_from(OP_ACTIVATE) >> state) & 1u) && parts > 0) state = SS_ACTIVE;
   else if (status == PIPE_OK) status = PIPE_BAD_ACTIVATE;
 
-  // ---- D × capture: canonical JSON + SHA-256 Merkle chain (K08) -------------------
-  SessionIdent sid;
-  sid.str_id = -1;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) sid.uuid[k] = u[k];
-  const StrRef did = pool_ref(a.pool, a.agent_did[agent]);  // resolved once per session
-  Digest prev, mid;
-  uint32_t* hrow = t.delta_hash + slot * a.dmax * 8;
-  const bool share_block0 = did.n >= kMidstateMinDid;  // every delta's block 0 is the same bytes
-  for (int d = 0; d < a.deltas; ++d) {
-    uint32_t h[8];
-    const int mode = !share_block0 ? MID_OFF : (d == 0 ? MID_CAPTURE : MID_RESUME);
-    emit_delta_and_hash(sink, a.pool, did, a.changes + d * a.nch, static_cast<uint32_t>(a.nch), -1,
-                        static_cast<uint32_t>(d + 1), d > 0, prev, sid, now + d + 1, h, mid, mode);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      prev.v[k] = h[k];
-      hrow[d * 8 + k] = h[k];
-    }
-  }
-  t.delta_count[slot] = a.deltas;
-
+  // The saga and terminate-transition stages read nothing the capture stage
+  // produces (their timestamps are now + D + k), so they run before it: fewer
+  // values stay live across the SHA rounds (no register spill at 168 VGPRs).
   // ---- saga: create, add_step, execute_step (executor is a device no-op) ----------
   uint32_t su[4], stu[4];
   uuid4_words(a.seed, id_base + 3 * static_cast<uint64_t>(i) + 1, su);
@@ -199,13 +185,36 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   t.saga_state[slot] = saga_st;
   t.step_state[slot] = step_st;
 
-  // ---- terminate: Merkle root (K09) → commit → release bonds (K07) → GC → archive --
+  // ---- terminate transition ------------------------------------------------------
   if ((session_op_allowed_from(OP_TERMINATE) >> state) & 1u) {
     state = SS_TERMINATING;
     t.sess_terminated_us[slot] = now + a.deltas + 3;
   } else if (status == PIPE_OK) {
     status = PIPE_BAD_TERMINATE;
   }
+  // ---- D × capture: canonical JSON + SHA-256 Merkle chain (K08) -------------------
+  SessionIdent sid;
+  sid.str_id = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sid.uuid[k] = u[k];
+  const StrRef did = pool_ref(a.pool, a.agent_did[agent]);  // resolved once per session
+  Digest prev, mid;
+  uint32_t* hrow = t.delta_hash + slot * a.dmax * 8;
+  const bool share_block0 = did.n >= kMidstateMinDid;  // every delta's block 0 is the same bytes
+  for (int d = 0; d < a.deltas; ++d) {
+    uint32_t h[8];
+    const int mode = !share_block0 ? MID_OFF : (d == 0 ? MID_CAPTURE : MID_RESUME);
+    emit_delta_and_hash(sink, a.pool, did, a.changes + d * a.nch, static_cast<uint32_t>(a.nch), -1,
+                        static_cast<uint32_t>(d + 1), d > 0, prev, sid, now + d + 1, h, mid, mode);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      prev.v[k] = h[k];
+      hrow[d * 8 + k] = h[k];
+    }
+  }
+  t.delta_count[slot] = a.deltas;
+
+  // ---- terminate: Merkle root (K09) → commit → release bonds (K07) → GC → archive --
   // Merkle root: leaves re-read from this session's delta_hash row (written by this
   // same lane above); interior levels in the sink's digest scratch (LDS on the device).
   uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -222,18 +231,26 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
 #pragma unroll
   for (int k = 0; k < 8; ++k) t.merkle_root[slot * 8 + k] = committed ? root[k] : 0u;
   t.committed_at_us[slot] = committed ? now + a.deltas + 3 : 0;
+  const int64_t t_term = now + a.deltas + 3;
   int32_t released = 0;
-  if (a.vouch_offsets) {
-    for (int32_t e = a.vouch_offsets[slot]; e < a.vouch_offsets[slot + 1]; ++e) {
-      if (a.vouch_active[e]) {
-        a.vouch_active[e] = 0;
-        a.vouch_released_us[e] = now + a.deltas + 3;
+  if (a.vouch_count) {
+    const int64_t e0 = slot * a.vouch_stride;
+    const int32_t ne = a.vouch_count[slot];
+    for (int32_t k = 0; k < ne; ++k) {
+      if (a.vouch_active[e0 + k]) {
+        a.vouch_active[e0 + k] = 0;
+        a.vouch_released_us[e0 + k] = t_term;
         ++released;
       }
     }
+    a.vouch_count[slot] = 0;
   }
   t.bonds_released[slot] = released;
-  t.gc_retained[slot] = a.deltas;  // nothing is older than the retention window
+  // GC (reference audit/gc.py): deltas stamped before terminate − retention expire
+  const int64_t cutoff = t_term - a.gc_retention_us;
+  int32_t retained = 0;
+  for (int d = 0; d < a.deltas; ++d) retained += (now + d + 1 >= cutoff) ? 1 : 0;
+  t.gc_retained[slot] = retained;
   if ((session_op_allowed_from(OP_ARCHIVE) >> state) & 1u) state = SS_ARCHIVED;
   t.sess_state[slot] = state;
   t.status[slot] = status;

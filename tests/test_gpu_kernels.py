@@ -145,6 +145,33 @@ def test_liability_kernels(cuda_device):
            torch.tensor(re_, dtype=u8), torch.tensor(rs, dtype=f64), torch.tensor(rp, dtype=f64))
 
 
+@pytest.mark.parametrize("S,lo,hi", [(2047, 0, 40), (96, 0, 700), (5, 0, 3)])
+def test_bond_fused_mfma(cuda_device, S, lo, hi):
+    """K03/K04 fused CSR → MFMA vs the creation-order CSR path (σ_eff, 1e-12) and
+    the host twin (exposure / bonded_in / agent scatter); ragged tails (S not a
+    multiple of the 16-session wave group), empty and > 512-edge sessions."""
+    vb = _vouch_batch(S, 11 + S, lo=lo, hi=hi)
+    g = torch.Generator().manual_seed(S)
+    sigma = torch.rand((S, 16), dtype=f64, generator=g)
+    sigma[sigma < 0.05] = float("nan")  # absent agents read as 0
+    omega = torch.rand(S, dtype=f64, generator=g)
+    members = torch.randint(0, 300, (S, 16), generator=g)
+    ref = LI.sigma_eff_exact(vb, sigma, omega, 100)
+    hx = torch.zeros(300, dtype=f64)
+    h_se, h_ex, h_bi = LI.bond_fused(vb, sigma, omega, 100, members=members, agent_exposure=hx, bonded_in=True)
+    assert torch.equal(h_se, ref)
+    dx = torch.zeros(300, dtype=f64, device="cuda")
+    d_se, d_ex, d_bi = LI.bond_fused(vb.to("cuda"), sigma.cuda(), omega.cuda(), 100, members=members.cuda(),
+                                     agent_exposure=dx, bonded_in=True)
+    torch.testing.assert_close(d_se.cpu(), ref, rtol=0, atol=1e-12)
+    torch.testing.assert_close(d_ex.cpu(), h_ex, rtol=0, atol=1e-12)
+    torch.testing.assert_close(d_bi.cpu(), h_bi, rtol=0, atol=1e-12)
+    torch.testing.assert_close(dx.cpu(), hx, rtol=1e-12, atol=1e-12)
+    tiles = LI.build_tiles(vb, 100)  # the old two-kernel pair gives the same exposure
+    _, t_ex, _ = LI.bond_tiles(tiles, sigma.nan_to_num(0.0), omega)
+    torch.testing.assert_close(h_ex, t_ex, rtol=0, atol=1e-12)
+
+
 def test_liability_kernels_large_sessions(cuda_device):
     """Sessions past every staging limit: > 64 edges (slash falls back from the
     16-lane group form to one lane), > 512 (tile build reads global memory),

@@ -117,3 +117,27 @@ def test_pipeline_adversarial_text_device(cuda_device, case):
     bh = h.run_pipeline(n, agents=agents, deltas=deltas, now_us=now, changes=specs or None)
     torch.cuda.synchronize()
     _assert_tables_equal(d, h, bd, bh)
+
+
+def test_pipeline_bond_release_and_gc_device(cuda_device):
+    """Resident vouch slab released by the terminate stage, GC retention from
+    timestamps: device tables (slab included) equal the host twin's."""
+    d, h = _pair()
+    g = torch.Generator().manual_seed(5)
+    slots = torch.randint(0, 3000, (5000,), generator=g) % 3000
+    keep = torch.bincount(slots, minlength=3000) <= 16
+    slots = slots[keep[slots]]
+    m = slots.numel()
+    vr, ve = torch.randint(0, 10, (m,), generator=g), torch.randint(0, 10, (m,), generator=g)
+    bd_ = torch.rand(m, generator=g, dtype=torch.float64)
+    for e in (d, h):
+        e.stage_vouches(slots, vr, ve, bd_)
+        e.gc_retention_us = 4
+    agents = torch.randint(0, 300, (3000,), dtype=torch.int32, generator=g)
+    bd = d.run_pipeline(3000, agents=agents.to(cuda_device), now_us=NOW)
+    bh = h.run_pipeline(3000, agents=agents, now_us=NOW)
+    torch.cuda.synchronize()
+    _assert_tables_equal(d, h, bd, bh)
+    assert int(h.sessions.bonds_released[bh.slots()].sum()) == m
+    for col in ("count",) + d.vouches.COLUMNS:
+        assert torch.equal(getattr(d.vouches, col).cpu(), getattr(h.vouches, col)), col

@@ -548,3 +548,32 @@ def test_lock_conflicts_match_intent_lock_manager():
                             torch.tensor([SE.LOCK_INTENT[q[2].value] for q in reqs], dtype=u8))
     for k, (r, a, it) in enumerate(reqs):
         assert got[k].item() == len(mgr._check_contention(f"/r{r}", f"a{a}", it))
+
+
+def test_bond_fused_host_twin_matches_creation_order():
+    """Host twin of the fused K03/K04 kernel: σ_eff bit-identical to the
+    creation-order CSR path, exposure equal to the dense-tile pair."""
+    import random as _r
+
+    from agent_hypervisor_amd.ops import liability as LI
+
+    rng = _r.Random(3)
+    S = 300
+    offs, vr, ve, bd, ac, ex = [0], [], [], [], [], []
+    for _ in range(S):
+        for _ in range(rng.randint(0, 30)):
+            a, b = rng.sample(range(16), 2)
+            vr.append(a), ve.append(b), bd.append(rng.uniform(0, 0.4))
+            ac.append(int(rng.random() < 0.9)), ex.append(rng.choice([-1, 50, 150]))
+        offs.append(len(vr))
+    vb = LI.VouchBatch(torch.tensor(offs, dtype=torch.int32), torch.tensor(vr, dtype=torch.uint8),
+                       torch.tensor(ve, dtype=torch.uint8), torch.tensor(bd, dtype=torch.float64),
+                       torch.tensor(ac, dtype=torch.uint8), torch.tensor(ex, dtype=torch.int64),
+                       torch.zeros(len(vr), dtype=torch.int64))
+    sigma = torch.rand((S, 16), dtype=torch.float64)
+    omega = torch.rand(S, dtype=torch.float64)
+    se, expo, bi = LI.bond_fused(vb, sigma, omega, 100, bonded_in=True)
+    assert torch.equal(se, LI.sigma_eff_exact(vb, sigma, omega, 100))
+    t_se, t_ex, t_bi = LI.bond_tiles(LI.build_tiles(vb, 100), sigma, omega)
+    torch.testing.assert_close(expo, t_ex, rtol=0, atol=1e-12)
+    torch.testing.assert_close(bi, t_bi, rtol=0, atol=1e-12)
