@@ -185,53 +185,19 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   t.saga_state[slot] = saga_st;
   t.step_state[slot] = step_st;
 
-  // ---- terminate transition ------------------------------------------------------
+  // ---- terminate: everything except the Merkle root ---------------------------------
+  // (commit timestamp, bond release K07, GC, archive and the counters read nothing the
+  // capture stage produces, so they are settled here: across the SHA rounds only the
+  // slot, the delta-hash row and one packed word stay live — no register spill)
   if ((session_op_allowed_from(OP_TERMINATE) >> state) & 1u) {
     state = SS_TERMINATING;
     t.sess_terminated_us[slot] = now + a.deltas + 3;
   } else if (status == PIPE_OK) {
     status = PIPE_BAD_TERMINATE;
   }
-  // ---- D × capture: canonical JSON + SHA-256 Merkle chain (K08) -------------------
-  SessionIdent sid;
-  sid.str_id = -1;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) sid.uuid[k] = u[k];
-  const StrRef did = pool_ref(a.pool, a.agent_did[agent]);  // resolved once per session
-  Digest prev, mid;
-  uint32_t* hrow = t.delta_hash + slot * a.dmax * 8;
-  const bool share_block0 = did.n >= kMidstateMinDid;  // every delta's block 0 is the same bytes
-  for (int d = 0; d < a.deltas; ++d) {
-    uint32_t h[8];
-    const int mode = !share_block0 ? MID_OFF : (d == 0 ? MID_CAPTURE : MID_RESUME);
-    emit_delta_and_hash(sink, a.pool, did, a.changes + d * a.nch, static_cast<uint32_t>(a.nch), -1,
-                        static_cast<uint32_t>(d + 1), d > 0, prev, sid, now + d + 1, h, mid, mode);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      prev.v[k] = h[k];
-      hrow[d * 8 + k] = h[k];
-    }
-  }
-  t.delta_count[slot] = a.deltas;
-
-  // ---- terminate: Merkle root (K09) → commit → release bonds (K07) → GC → archive --
-  // Merkle root: leaves re-read from this session's delta_hash row (written by this
-  // same lane above); interior levels in the sink's digest scratch (LDS on the device).
-  uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (a.deltas > 0) {
-    merkle_root_levels(
-        sink, static_cast<uint32_t>(a.deltas),
-        [&](uint32_t d, uint32_t h[8]) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) h[k] = hrow[d * 8 + k];
-        },
-        root);
-  }
   const bool committed = a.audit && a.deltas > 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t.merkle_root[slot * 8 + k] = committed ? root[k] : 0u;
-  t.committed_at_us[slot] = committed ? now + a.deltas + 3 : 0;
   const int64_t t_term = now + a.deltas + 3;
+  t.committed_at_us[slot] = committed ? t_term : 0;
   int32_t released = 0;
   if (a.vouch_count) {
     const int64_t e0 = slot * a.vouch_stride;
@@ -254,6 +220,7 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   if ((session_op_allowed_from(OP_ARCHIVE) >> state) & 1u) state = SS_ARCHIVED;
   t.sess_state[slot] = state;
   t.status[slot] = status;
+  t.delta_count[slot] = a.deltas;
   PipeCounters c;
   c.v[0] = 1;
   c.v[1] = status == PIPE_OK ? 1u : 0u;
@@ -261,6 +228,43 @@ AHV_HD PipeCounters pipeline_session(const PipelineArgs& a, int64_t i, Sink& sin
   c.v[3] = static_cast<uint32_t>(a.deltas);
   c.v[4] = committed ? 1u : 0u;
   c.v[5] = state == SS_ARCHIVED ? 1u : 0u;
+
+  // ---- D × capture: canonical JSON + SHA-256 Merkle chain (K08) -------------------
+  SessionIdent sid;
+  sid.str_id = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sid.uuid[k] = u[k];
+  const StrRef did = pool_ref(a.pool, a.agent_did[agent]);  // resolved once per session
+  Digest prev, mid;
+  uint32_t* hrow = t.delta_hash + slot * a.dmax * 8;
+  const bool share_block0 = did.n >= kMidstateMinDid;  // every delta's block 0 is the same bytes
+  for (int d = 0; d < a.deltas; ++d) {
+    uint32_t h[8];
+    const int mode = !share_block0 ? MID_OFF : (d == 0 ? MID_CAPTURE : MID_RESUME);
+    emit_delta_and_hash(sink, a.pool, did, a.changes + d * a.nch, static_cast<uint32_t>(a.nch), -1,
+                        static_cast<uint32_t>(d + 1), d > 0, prev, sid, now + d + 1, h, mid, mode);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      prev.v[k] = h[k];
+      hrow[d * 8 + k] = h[k];
+    }
+  }
+
+  // ---- terminate: Merkle root (K09) → commitment -------------------------------------
+  // Leaves re-read from this session's delta_hash row (written by this same lane
+  // above); interior levels in the sink's digest scratch (LDS on the device).
+  uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (a.deltas > 0) {
+    merkle_root_levels(
+        sink, static_cast<uint32_t>(a.deltas),
+        [&](uint32_t d, uint32_t h[8]) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) h[k] = hrow[d * 8 + k];
+        },
+        root);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t.merkle_root[slot * 8 + k] = committed ? root[k] : 0u;
   return c;
 }
 
