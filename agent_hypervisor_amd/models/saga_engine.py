@@ -81,6 +81,10 @@ class SagaBatchEngine:
         self.stats = z(4, i64)
         self._spread = SpreadCounters(4, self.device)
         self.now_us = 0
+        # device time base read by every launch (graph replays stamp the time
+        # written before them) and persistent outcome buffers (load_outcomes)
+        self.now_dev = z(1, i64)
+        self._persist: Optional[SagaOutcomes] = None
         self._graph = None
         self._graph_outcomes = None
         self._prep_src = None
@@ -117,7 +121,24 @@ class SagaBatchEngine:
         for f in ("saga_state", "saga_completed_us", "failed_step", "comp_failed", "tick"):
             d[f] = getattr(self, f).data_ptr()
         d["stats"] = self._spread.buf.data_ptr()
+        d["now_dev"] = self.now_dev.data_ptr()
         return d
+
+    def load_outcomes(self, o: SagaOutcomes) -> SagaOutcomes:
+        """Copy ``o`` ([S, K] u8 tables, any device) into this engine's persistent
+        outcome buffers and return their handle: a step loop captured on the
+        handle replays against whatever was loaded last (no recapture)."""
+        if self._persist is None:
+            z = lambda: torch.zeros((self.S, self.K), dtype=u8, device=self.device)  # noqa: E731
+            self._persist = SagaOutcomes(z(), z(), z(), z(), z())
+            self._prepared(self._persist)
+        prep = self._prepared(self._persist)
+        for f in o.__dataclass_fields__:
+            src = getattr(o, f)
+            if tuple(src.shape) != (self.S, self.K):
+                raise ValueError(f"outcome table {f} must be [{self.S}, {self.K}]")
+            prep[f].copy_(src.to(self.device, u8).t(), non_blocking=True)
+        return self._persist
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -128,6 +149,7 @@ class SagaBatchEngine:
         (completed, escalated, failed, compensated steps) of this batch."""
         self.now_us = int(now_us if now_us is not None else _clock.now_us())
         a = self._args(outcomes, self.now_us)
+        self.now_dev.fill_(self.now_us)
         self._spread.begin()
         if self.device.type == "cuda":
             C.saga_fused(a, self._stream())
@@ -158,10 +180,11 @@ class SagaBatchEngine:
         on GPU when ``graph`` (captured on first use for these outcome tables)."""
         self.now_us = int(now_us if now_us is not None else _clock.now_us())
         a = self._args(outcomes, self.now_us)
+        self.now_dev.fill_(self.now_us)  # outside any capture: replays read it
         if self.device.type != "cuda" or not graph:
             self._loop(a)
             return self.stats
-        if self._graph is None or self._graph_outcomes is not outcomes or self._graph_now != self.now_us:
+        if self._graph is None or self._graph_outcomes is not outcomes:
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side):
@@ -171,7 +194,7 @@ class SagaBatchEngine:
             self._graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._graph):
                 self._loop(a)
-            self._graph_outcomes, self._graph_now = outcomes, self.now_us
+            self._graph_outcomes = outcomes
         self._graph.replay()
         return self.stats
 

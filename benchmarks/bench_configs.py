@@ -232,6 +232,59 @@ def config4(ctx: Ctx, args):
     ctx.emit(config="config4", mode="hipgraph_step_loop", launches_per_batch=2 * K + 3, sagas=S,
              ms_per_batch=el / args.steps * 1e3, batch_p50_ms=statistics.median(lat) * 1e3,
              sagas_per_s=S * ctx.world * args.steps / el)
+    # real (stub) coroutines: SagaOrchestrator.execute_sagas awaits every executor /
+    # compensator on the host (asyncio) and replays the captured step loop on the
+    # device over the gathered outcomes (agent_hypervisor_amd.models.saga_runner)
+    import asyncio
+    import random as _random
+
+    from hypervisor.saga.orchestrator import SagaOrchestrator
+
+    Sc = min(S, args.coroutine_sagas)
+    rng = _random.Random(ctx.rank)
+
+    def build():
+        orch = SagaOrchestrator()
+        orch.DEFAULT_RETRY_DELAY_SECONDS = 0.0
+        ids, ex = [], {}
+        for i in range(Sc):
+            sg = orch.create_saga(f"session-{i}")
+            ids.append(sg.saga_id)
+            for k in range(K):
+                st = orch.add_step(sg.saga_id, f"a{k}", "did:mesh:agent", "/exec",
+                                   "/undo" if rng.random() >= 0.05 else None, max_retries=1)
+                fail = rng.random() < 0.03
+
+                async def run(fail=fail):
+                    if fail:
+                        raise RuntimeError("executor failed")
+                    return True
+
+                ex[st.step_id] = run
+        return orch, ids, ex
+
+    async def compensator(step):
+        return True
+
+    times = []
+    for _ in range(args.warmup + args.steps):
+        orch, ids, ex = build()
+        t0 = time.perf_counter()
+        asyncio.run(orch.execute_sagas(ids, ex, compensator, device=str(ctx.dev)))
+        ctx.sync()
+        times.append(time.perf_counter() - t0)
+    el = sum(times[args.warmup:])
+    orch, ids, ex = build()  # the host orchestrator on the same workload, for reference
+    t0 = time.perf_counter()
+    asyncio.run(orch.execute_sagas(ids, ex, compensator))
+    host_ms = (time.perf_counter() - t0) * 1e3
+    from agent_hypervisor_amd.models.saga_runner import runner_for
+
+    st = runner_for(ctx.dev).last_stats
+    ctx.emit(config="config4", mode="coroutines+device_fsm_graph", sagas=Sc, steps_per_saga=K,
+             ms_per_batch=el / args.steps * 1e3, sagas_per_s=Sc * ctx.world * args.steps / el,
+             completed=st[0], escalated=st[1], compensated_steps=st[3], host_orchestrator_ms=host_ms,
+             note="outcomes from awaited stub coroutines (3% failing executors, 5% steps without Undo_API)")
 
 
 # ------------------------------------------------------------------ config 5
@@ -309,6 +362,7 @@ def main():
     ap.add_argument("--agents", type=int, default=0)
     ap.add_argument("--edges", type=int, default=0)
     ap.add_argument("--deltas", type=int, default=0)
+    ap.add_argument("--coroutine-sagas", type=int, default=4096, help="config4: sagas in the coroutine mode")
     ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
     ap.add_argument("--owner-reduce", action="store_true", help="config3: reduce-scatter exposure to agent owners")
     args = ap.parse_args()

@@ -100,19 +100,28 @@ void bond_tiles_host(const BondTileArgs& a) {
 // Operand layouts of v_mfma_f64_16x16x4_f64 (as in bond_tiles_mfma_kernel):
 // lane l = 16·r + c supplies A[i=c][k=r] and B[k=r][j=c]; it receives
 // D[row=r+4q][col=c] in register q.  A wave owns 16 consecutive sessions (their
-// edges are one contiguous CSR range).  Edges are read 64 at a time, one per
-// lane, fully coalesced (liveness, voucher and vouchee packed into one word);
-// the next 64 are loaded before the current ones are consumed.  For each chunk of
-// 4 edges, lane (r, c) fetches edge 4u+r of the batch with a cross-lane shuffle:
-// A is its bond if the edge lies in session c's CSR range [off_c, off_c+1) — each
-// lane tests its own session, no search — and B is whether the edge's vouchee
+// edges are one contiguous CSR range) and walks it 64 edges at a time.
+//
+// Load: lane 16·r + c reads edge base + 4c + r — the 64 lanes cover 64
+// consecutive edges, so the loads stay fully coalesced — packing liveness,
+// voucher and vouchee into one word.  Chunk u (edges base+4u … base+4u+3) needs,
+// in every lane of row r, edge 4u + r, which lane 16·r + u holds: one DPP
+// row_newbcast:u per 32-bit value hands it to the whole row (VALU, no LDS).
+// Then A is the edge's bond if it lies in session c's CSR range [off_c, off_c+1)
+// — each lane tests its own session, no search — and B is whether its vouchee
 // (voucher) is c.  Two MFMAs per chunk accumulate Σbonded per (session, vouchee)
-// and per (session, voucher).  In-chunk sums are MFMA-ordered, so results agree
-// with the creation-order reference to ulp level (the CSR kernel stays the
-// bit-exact path).
+// and per (session, voucher).  The next 64 edges are loaded before the current
+// ones are consumed.  In-chunk sums are MFMA-ordered, so results agree with the
+// creation-order reference to ulp level (the CSR kernel stays the bit-exact path).
 
 constexpr int kFusedWaves = 4;      // waves per block
 constexpr int kFusedSessions = 16;  // sessions per wave (A rows)
+
+struct FusedLane {
+  int32_t base;   // first edge of the batch
+  int32_t off_c, off_c1;
+  uint32_t c, r;
+};
 
 __device__ __forceinline__ void fused_load(const BondFusedArgs& a, int32_t g, int32_t e1, uint32_t& meta, double& bond) {
   meta = 0u;
@@ -124,51 +133,70 @@ __device__ __forceinline__ void fused_load(const BondFusedArgs& a, int32_t g, in
   }
 }
 
+template <int U>
+__device__ __forceinline__ void fused_chunk(const FusedLane& L, uint32_t meta, uint32_t b_lo, uint32_t b_hi,
+                                            f64x4& acc_in, f64x4& acc_out) {
+  constexpr int kBcast = 0x150 + U;  // row_newbcast:U
+  const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(meta), kBcast, 0xF, 0xF, false));
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(b_lo), kBcast, 0xF, 0xF, false));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(b_hi), kBcast, 0xF, 0xF, false));
+  const double b = __hiloint2double(static_cast<int>(hi), static_cast<int>(lo));
+  const int32_t g = L.base + 4 * U + static_cast<int32_t>(L.r);
+  const double av = ((m >> 16) && g >= L.off_c && g < L.off_c1) ? b : 0.0;
+  const double bi = (m & 0xffu) == L.c ? 1.0 : 0.0;
+  const double bo = ((m >> 8) & 0xffu) == L.c ? 1.0 : 0.0;
+  acc_in = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bi, acc_in, 0, 0, 0);
+  acc_out = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bo, acc_out, 0, 0, 0);
+}
+
+template <int U0>
+__device__ __forceinline__ void fused_quad(const FusedLane& L, uint32_t meta, uint32_t lo, uint32_t hi, f64x4& ai,
+                                           f64x4& ao) {
+  fused_chunk<U0>(L, meta, lo, hi, ai, ao);
+  fused_chunk<U0 + 1>(L, meta, lo, hi, ai, ao);
+  fused_chunk<U0 + 2>(L, meta, lo, hi, ai, ao);
+  fused_chunk<U0 + 3>(L, meta, lo, hi, ai, ao);
+}
+
 __global__ __launch_bounds__(64 * kFusedWaves) void bond_fused_mfma_kernel(BondFusedArgs a) {
   const int wave = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
-  const int r = l >> 4, c = l & 15;
   const int64_t s0 = (static_cast<int64_t>(blockIdx.x) * kFusedWaves + wave) * kFusedSessions;
   if (s0 >= a.sessions) return;  // wave-uniform
   const int64_t s_end = s0 + kFusedSessions < a.sessions ? s0 + kFusedSessions : a.sessions;
   const int32_t e0 = a.offsets[s0], e1 = a.offsets[s_end];
-  const int64_t sc = s0 + c;
-  const int32_t off_c = sc < s_end ? a.offsets[sc] : e1;
-  const int32_t off_c1 = sc < s_end ? a.offsets[sc + 1] : e1;
+  FusedLane L;
+  L.r = static_cast<uint32_t>(l >> 4);
+  L.c = static_cast<uint32_t>(l & 15);
+  const int64_t sc = s0 + L.c;
+  L.off_c = sc < s_end ? a.offsets[sc] : e1;
+  L.off_c1 = sc < s_end ? a.offsets[sc + 1] : e1;
+  const int32_t my = static_cast<int32_t>(4 * L.c + L.r);  // this lane's edge within a batch
   f64x4 acc_in = {0.0, 0.0, 0.0, 0.0};
   f64x4 acc_out = {0.0, 0.0, 0.0, 0.0};
   uint32_t meta;
   double bond;
-  fused_load(a, e0 + l, e1, meta, bond);
+  fused_load(a, e0 + my, e1, meta, bond);
   for (int32_t base = e0; base < e1; base += 64) {
     uint32_t meta_n;
     double bond_n;
-    fused_load(a, base + 64 + l, e1, meta_n, bond_n);  // next batch in flight
-    // chunks of this batch, rounded up to a multiple of 4 (lanes past e1 carry
-    // meta = 0, bond = 0: padding chunks add exact zeros)
-    const int chunks = (e1 - base) >= 64 ? 16 : ((e1 - base + 15) >> 4) << 2;  // wave-uniform
-    for (int u0 = 0; u0 < chunks; u0 += 4) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int src = 4 * (u0 + j) + r;
-        const uint32_t m = __shfl(meta, src, 64);
-        const double b = __shfl(bond, src, 64);
-        const int32_t g = base + src;
-        const double av = ((m >> 16) && g >= off_c && g < off_c1) ? b : 0.0;
-        const double bi = (m & 0xffu) == static_cast<uint32_t>(c) ? 1.0 : 0.0;
-        const double bo = ((m >> 8) & 0xffu) == static_cast<uint32_t>(c) ? 1.0 : 0.0;
-        acc_in = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bi, acc_in, 0, 0, 0);
-        acc_out = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bo, acc_out, 0, 0, 0);
-      }
-    }
+    fused_load(a, base + 64 + my, e1, meta_n, bond_n);  // next batch in flight
+    L.base = base;
+    const uint32_t lo = static_cast<uint32_t>(__double2loint(bond));
+    const uint32_t hi = static_cast<uint32_t>(__double2hiint(bond));
+    const int32_t rem = e1 - base;  // wave-uniform; lanes past e1 carry zeros
+    fused_quad<0>(L, meta, lo, hi, acc_in, acc_out);
+    if (rem > 16) fused_quad<4>(L, meta, lo, hi, acc_in, acc_out);
+    if (rem > 32) fused_quad<8>(L, meta, lo, hi, acc_in, acc_out);
+    if (rem > 48) fused_quad<12>(L, meta, lo, hi, acc_in, acc_out);
     meta = meta_n;
     bond = bond_n;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int64_t s = s0 + r + 4 * q;
+    const int64_t s = s0 + L.r + 4 * q;
     if (s >= s_end) continue;
-    const int64_t o = s * kTile + c;  // 64 consecutive doubles per q across the wave
+    const int64_t o = s * kTile + L.c;  // 64 consecutive doubles per q across the wave
     const double bonded = acc_in[q];
     if (a.bonded_in) a.bonded_in[o] = bonded;
     a.sigma_eff[o] = sigma_eff_combine(score_or_zero(a.sigma[o]), a.omega[s], bonded);

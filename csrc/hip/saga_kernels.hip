@@ -38,7 +38,8 @@ __device__ __forceinline__ void add_counters(const SagaBatchArgs& a, SagaCounter
 }
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void saga_fused_kernel(SagaBatchArgs a) {
+__global__ __launch_bounds__(kBlock) void saga_fused_kernel(SagaBatchArgs a0) {
+  const SagaBatchArgs a = saga_with_now(a0);
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const bool active = s < a.sagas;
   SagaCounters c{0, 0, 0, 0};
@@ -48,7 +49,8 @@ __global__ __launch_bounds__(kBlock) void saga_fused_kernel(SagaBatchArgs a) {
 
 // One instantiation per step count: the chain's state lives in registers.
 template <int K>
-__global__ __launch_bounds__(kBlock) void saga_fused_regs_kernel(SagaBatchArgs a) {
+__global__ __launch_bounds__(kBlock) void saga_fused_regs_kernel(SagaBatchArgs a0) {
+  const SagaBatchArgs a = saga_with_now(a0);
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const bool active = s < a.sagas;
   SagaCounters c{0, 0, 0, 0};
@@ -57,7 +59,8 @@ __global__ __launch_bounds__(kBlock) void saga_fused_regs_kernel(SagaBatchArgs a
 }
 
 // phase 0 init, 1 execute step k, 2 decide, 3 compensate step k, 4 finish (+counters)
-__global__ __launch_bounds__(kBlock) void saga_phase_kernel(SagaBatchArgs a, int phase, int k) {
+__global__ __launch_bounds__(kBlock) void saga_phase_kernel(SagaBatchArgs a0, int phase, int k) {
+  const SagaBatchArgs a = saga_with_now(a0);
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const bool active = s < a.sagas;
   SagaCounters c{0, 0, 0, 0};
@@ -97,7 +100,8 @@ void launch_saga_fused(const SagaBatchArgs& a, hipStream_t st) {
   check_hip(hipGetLastError(), "saga_fused_kernel");
 }
 
-void saga_fused_host(const SagaBatchArgs& a) {
+void saga_fused_host(const SagaBatchArgs& a0) {
+  const SagaBatchArgs a = saga_with_now(a0);
   check_args(a);
   for (int64_t s = 0; s < a.sagas; ++s) {
     const SagaCounters c = saga_run_chain_fused(a, s);
@@ -118,7 +122,8 @@ void launch_saga_phase(const SagaBatchArgs& a, int phase, int k, hipStream_t st)
   check_hip(hipGetLastError(), "saga_phase_kernel");
 }
 
-void saga_phase_host(const SagaBatchArgs& a, int phase, int k) {
+void saga_phase_host(const SagaBatchArgs& a0, int phase, int k) {
+  const SagaBatchArgs a = saga_with_now(a0);
   check_args(a);
   if (phase < 0 || phase > 4 || k < 0 || k >= a.steps) throw std::invalid_argument("bad saga phase/step");
   for (int64_t s = 0; s < a.sagas; ++s) {

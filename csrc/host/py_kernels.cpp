@@ -268,6 +268,7 @@ static SagaBatchArgs to_saga(const py::dict& d) {
   P(step_error, uint8_t); P(started_us, int64_t); P(completed_us, int64_t); P(saga_state, uint8_t);
   P(saga_completed_us, int64_t); P(failed_step, int32_t); P(comp_failed, int32_t); P(tick, int32_t);
   P(stats, unsigned long long);
+  a.now_dev = d.contains("now_dev") ? ptr<const int64_t>(d, "now_dev") : nullptr;
   return a;
 }
 #undef P

@@ -64,7 +64,15 @@ struct SagaBatchArgs {
   int32_t* comp_failed;   // compensation failures
   int32_t* tick;          // transition counter (per-step mode keeps it across launches)
   unsigned long long* stats;  // [4] completed, escalated, failed, compensated steps (or null)
+  // Device-resident time base (int64[1]) or null: when set it overrides now_us, so
+  // a captured step-loop graph stamps each replay with the time written before it.
+  const int64_t* now_dev;
 };
+
+AHV_HD SagaBatchArgs saga_with_now(SagaBatchArgs a) {
+  if (a.now_dev) a.now_us = *a.now_dev;
+  return a;
+}
 
 // Per-step tables are step-major, [K][S]: lane s of a wave touches element
 // k*S + s, so every per-step access of a wave is one contiguous (coalesced)

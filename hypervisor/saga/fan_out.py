@@ -108,6 +108,34 @@ class FanOutOrchestrator:
         timeout_seconds: int = 300,
     ) -> FanOutGroup:
         g = self._get_group(group_id)
+        await self.run_branches(g, executors, timeout_seconds)
+        g.policy_satisfied = g.check_policy()
+        g.resolved = True
+        if not g.policy_satisfied:
+            g.compensation_needed = [b.step.step_id for b in g.branches if b.succeeded and b.step]
+        return g
+
+    async def execute_groups(
+        self,
+        group_ids: list[str],
+        executors: dict[str, Callable[..., Any]],
+        timeout_seconds: int = 300,
+        device: Optional[str] = None,
+    ) -> list[FanOutGroup]:
+        """:meth:`execute` for many groups at once (all branches concurrent).
+        With ``device`` every group's policy and compensation list come from one
+        K15 launch over the gathered branch outcomes."""
+        groups = [self._get_group(i) for i in group_ids]
+        if device is not None:
+            from agent_hypervisor_amd.models.saga_runner import execute_fanout_groups
+
+            return await execute_fanout_groups(self, groups, executors, timeout_seconds, device)
+        await asyncio.gather(*(self.execute(g.group_id, executors, timeout_seconds) for g in groups))
+        return groups
+
+    async def run_branches(self, g: FanOutGroup, executors: dict[str, Callable[..., Any]],
+                           timeout_seconds: int) -> None:
+        """Every branch of ``g`` concurrently under one overall timeout."""
         parity = _cfg.parity_mode()
 
         async def run(b: FanOutBranch) -> None:
@@ -137,11 +165,6 @@ class FanOutOrchestrator:
             asyncio.gather(*(run(b) for b in g.branches), return_exceptions=True),
             timeout=timeout_seconds,
         )
-        g.policy_satisfied = g.check_policy()
-        g.resolved = True
-        if not g.policy_satisfied:
-            g.compensation_needed = [b.step.step_id for b in g.branches if b.succeeded and b.step]
-        return g
 
     @staticmethod
     def _fail(b: FanOutBranch, msg: str) -> None:

@@ -138,6 +138,45 @@ class SagaOrchestrator:
             saga.transition(SagaState.COMPLETED)
         return failed
 
+    async def execute_sagas(
+        self,
+        saga_ids: list[str],
+        executors: dict[str, Callable[..., Any]],
+        compensator: Optional[Callable[[SagaStep], Any]] = None,
+        compensate: bool = True,
+        device: Optional[str] = None,
+    ) -> list[Saga]:
+        """Run many sagas to completion: each saga executes its steps in order
+        (``execute_step`` semantics, ``executors[step_id]``); on the first step
+        that exhausts its attempts it is compensated (``compensate``) or marked
+        FAILED, otherwise COMPLETED.  Sagas run concurrently.
+
+        With ``device`` the coroutines are still awaited here, but the state
+        machine runs as one replay of the hipGraph-captured K13/K14 step loop
+        (:mod:`agent_hypervisor_amd.models.saga_runner`) and its states are
+        written back into these Saga objects."""
+        sagas = [self._get_saga(i) for i in saga_ids]
+        if device is not None:
+            from agent_hypervisor_amd.models.saga_runner import runner_for
+
+            await runner_for(device).run(self, sagas, executors, compensator, compensate)
+            return sagas
+
+        async def one(saga: Saga) -> None:
+            for step in saga.steps:
+                try:
+                    await self.execute_step(saga.saga_id, step.step_id, executors[step.step_id])
+                except Exception:
+                    if compensate:
+                        await self.compensate(saga.saga_id, compensator)
+                    else:
+                        saga.transition(SagaState.FAILED)
+                    return
+            saga.transition(SagaState.COMPLETED)
+
+        await asyncio.gather(*(one(s) for s in sagas))
+        return sagas
+
     def get_saga(self, saga_id: str) -> Optional[Saga]:
         return self._sagas.get(saga_id)
 

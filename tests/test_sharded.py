@@ -102,6 +102,7 @@ def _worker(rank: int, world: int, port: int, store: str, q) -> None:
         if rank == 0:
             ref = asyncio.run(scenario(ShardedHypervisor(device=store, single=True)))
             q.put((got, ref, owners))
+        dist.barrier()  # followers stay up while rank 0 builds the single-rank reference
     finally:
         dist.destroy_process_group()
 
