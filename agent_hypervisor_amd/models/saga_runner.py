@@ -92,11 +92,11 @@ class SagaBatchRunner:
     async def _run_group(self, orch, sagas, K, executors, compensator, compensate) -> list[int]:
         S = len(sagas)
         delay = float(orch.DEFAULT_RETRY_DELAY_SECONDS)
-        fa = torch.zeros((S, K), dtype=u8)
-        fk = torch.zeros((S, K), dtype=u8)
-        cf = torch.zeros((S, K), dtype=u8)
-        hu = torch.tensor([[1 if st.undo_api else 0 for st in sg.steps] for sg in sagas], dtype=u8)
-        mr = torch.tensor([[min(int(st.max_retries), 254) for st in sg.steps] for sg in sagas], dtype=u8)
+        # outcome tables filled element-wise on the host: flat bytearrays (row s·K + k),
+        # turned into tensors once
+        fa, fk, cf = bytearray(S * K), bytearray(S * K), bytearray(S * K)
+        hu = bytearray(1 if st.undo_api else 0 for sg in sagas for st in sg.steps)
+        mr = bytearray(min(int(st.max_retries), 254) for sg in sagas for st in sg.steps)
         results: dict[tuple[int, int], Any] = {}
         errors: dict[tuple[int, int], str] = {}
         comp_results: dict[tuple[int, int], Any] = {}
@@ -123,20 +123,22 @@ class SagaBatchRunner:
             errors[(s, k)] = err
             return NEVER, kind
 
-        alive = list(range(S))
-        failed_at = {}
-        for k in range(K):  # forward: step k of every still-running saga, concurrently
-            outs = await asyncio.gather(*(attempts(s, k) for s in alive))
-            nxt = []
-            for s, (nf, kind) in zip(alive, outs):
-                fa[s, k], fk[s, k] = nf, kind
+        failed_at: dict[int, int] = {}
+
+        async def forward(s: int) -> None:  # the saga's steps in order, until one fails
+            for k in range(K):
+                nf, kind = await attempts(s, k)
+                fa[s * K + k], fk[s * K + k] = nf, kind
                 if nf == NEVER:
                     failed_at[s] = k
-                else:
-                    nxt.append(s)
-            alive = nxt
+                    return
+
+        await asyncio.gather(*(forward(s) for s in range(S)))  # sagas run concurrently
         if compensate and failed_at:
-            async def comp(s: int, k: int):
+            if compensator is None:
+                raise ValueError("compensate=True needs a compensator")
+
+            async def comp(s: int, k: int) -> int:
                 st = sagas[s].steps[k]
                 try:
                     res = await await_with_timeout(compensator(st), st.timeout_seconds)
@@ -149,16 +151,16 @@ class SagaBatchRunner:
                 comp_results[(s, k)] = res
                 return 0
 
-            if compensator is None:
-                raise ValueError("compensate=True needs a compensator")
-            for k in range(K - 1, -1, -1):  # reverse order within each saga, concurrent across sagas
-                todo = [s for s, f in failed_at.items() if k < f and hu[s, k]]
-                outs = await asyncio.gather(*(comp(s, k) for s in todo))
-                for s, c in zip(todo, outs):
-                    cf[s, k] = c
+            async def backward(s: int, f: int) -> None:  # committed steps in reverse order
+                for k in range(f - 1, -1, -1):
+                    if hu[s * K + k]:
+                        cf[s * K + k] = await comp(s, k)
+
+            await asyncio.gather(*(backward(s, f) for s, f in failed_at.items()))
         # device FSM: one replay of the captured step loop over the gathered outcomes
         eng = self.engine(S, K, compensate)
-        handle = eng.load_outcomes(SagaOutcomes(fa, fk, cf, hu, mr))
+        tab = lambda b: torch.frombuffer(b, dtype=u8).view(S, K)  # noqa: E731
+        handle = eng.load_outcomes(SagaOutcomes(tab(fa), tab(fk), tab(cf), tab(hu), tab(mr)))
         stats = eng.run_step_loop(handle, now_us=_clock.now_us(), graph=True)
         self._write_back(eng, sagas, results, errors, comp_results, comp_errors)
         return [int(x) for x in stats.cpu().tolist()]

@@ -181,7 +181,8 @@ def slash(
     clip_cap: int = 64,
 ) -> SlashOutcome:
     """K06: slash ``target[s]`` in every session (cascade ≤ 2), mutating ``vb``
-    (bonds released) and ``scores`` in place, like SlashingEngine.slash.
+    (bonds released) and ``scores`` in place, like SlashingEngine.slash.  A
+    target ≥ 16 (e.g. 255) leaves that session untouched (storms over a subset).
 
     At most ``clip_cap`` clip *records* are kept per session (``clip_count`` holds
     the true count; :attr:`SlashOutcome.truncated` flags sessions whose records

@@ -290,66 +290,144 @@ def config4(ctx: Ctx, args):
 # ------------------------------------------------------------------ config 5
 
 
+class AuditArena:
+    """Resident audit chains of ``S`` sessions with distinct payloads (config 5).
+
+    A template chain — D deltas captured through the scalar DeltaEngine, plus one
+    "slash" delta whose content hash is a 256-character placeholder — is stamped
+    per session on the device: session index digits into the DID, session id,
+    paths and content hashes, per-session microseconds into the timestamps.
+    Deltas 0..D-1 of every session live in one HBM arena; the slash delta of each
+    *touched* session is written after the slash into a tail region (the hex of
+    that session's post-slash score row), so the re-chain depends on the slash."""
+
+    PH, MICRO, HEXPH = b"@@@@@@@", b"999999", b"x" * 256
+
+    def __init__(self, S: int, D: int, dev) -> None:
+        from datetime import datetime, timezone
+
+        from hypervisor import _clock
+        from hypervisor.audit.delta import DeltaEngine, VFSChange
+
+        prev = _clock._override
+        _clock.set_clock(lambda: datetime(2026, 3, 1, 12, 0, 0, 999999, tzinfo=timezone.utc))
+        try:
+            de = DeltaEngine("session:@@@@@@@")
+            for k in range(D):
+                de.capture("did:mesh:agent-@@@@@@@", [VFSChange(f"/s@@@@@@@/f{k}", "add", f"h{k}-@@@@@@@")])
+            de.capture("did:mesh:agent-@@@@@@@", [VFSChange("/s@@@@@@@/slash", "modify", "x" * 256)])
+        finally:
+            _clock.set_clock(prev)
+        chain = A.pack_chains([de.deltas[:D]])
+        last = A.pack_chains([de.deltas[D:]])
+        self.S, self.D, self.dev = S, D, dev
+        tb, lb = bytes(chain["bytes"].tolist()), bytes(last["bytes"].tolist())
+        self.L, self.Ls = len(tb), len(lb)
+        self.t_pre_off, self.t_pre_len = chain["pre_off"].to(dev), chain["pre_len"].to(dev)
+        self.t_suf_off, self.t_suf_len = chain["suf_off"].to(dev), chain["suf_len"].to(dev)
+        self.s_pre_off, self.s_pre_len = int(last["pre_off"][0]), int(last["pre_len"][0])
+        self.s_suf_off, self.s_suf_len = int(last["suf_off"][0]), int(last["suf_len"][0])
+        find = lambda buf, pat: [i for i in range(len(buf) - len(pat) + 1) if buf[i:i + len(pat)] == pat]  # noqa: E731
+        self.ph, self.micro = find(tb, self.PH), find(tb, self.MICRO)
+        self.s_ph, self.s_micro, self.s_hex = find(lb, self.PH), find(lb, self.MICRO), find(lb, self.HEXPH)
+        assert len(self.s_hex) == 1 and self.ph and self.micro
+        # resident arena: S chains, then S slash-delta slots (a storm touches ≤ S sessions)
+        self.tail = S * self.L
+        self.bytes = torch.empty(self.tail + S * self.Ls, dtype=u8, device=dev)
+        body = self.bytes[: self.tail].view(S, self.L)
+        body.copy_(torch.frombuffer(bytearray(tb), dtype=u8).to(dev).expand(S, self.L))
+        self._tmpl_slash = torch.frombuffer(bytearray(lb), dtype=u8).to(dev)
+        idx = torch.arange(S, device=dev)
+        self._stamp(body, idx, self.ph, self.micro)
+
+    @staticmethod
+    def _digits(idx: torch.Tensor, n: int) -> torch.Tensor:
+        p = 10 ** torch.arange(n - 1, -1, -1, device=idx.device)
+        return ((idx[:, None] // p) % 10 + 48).to(u8)
+
+    def _stamp(self, rows: torch.Tensor, idx: torch.Tensor, ph, micro) -> None:
+        # microseconds 1..999999: a zero field would drop out of isoformat()
+        d7, d6 = self._digits(idx, 7), self._digits(idx % 999_999 + 1, 6)
+        for p in ph:
+            rows[:, p:p + 7] = d7
+        for p in micro:
+            rows[:, p:p + 6] = d6
+
+    def write_slash_deltas(self, touched: torch.Tensor, score_rows: torch.Tensor) -> None:
+        """Slash delta of each touched session (slot i of the tail): the template
+        stamped with the session, content hash = hex of its post-slash scores."""
+        T = touched.numel()
+        rows = self.bytes[self.tail: self.tail + T * self.Ls].view(T, self.Ls)
+        rows.copy_(self._tmpl_slash.expand(T, self.Ls))
+        self._stamp(rows, touched, self.s_ph, self.s_micro)
+        raw = score_rows.contiguous().view(torch.uint8).reshape(T, 128)
+        hexd = torch.tensor(list(b"0123456789abcdef"), dtype=u8, device=raw.device)
+        h = torch.stack([hexd[(raw >> 4).long()], hexd[(raw & 15).long()]], dim=2).reshape(T, 256)
+        p = self.s_hex[0]
+        rows[:, p:p + 256] = h
+
+    def packed(self, touched: torch.Tensor) -> dict:
+        """chain_hash arguments for the touched sessions' chains (D + 1 deltas)."""
+        T, D, dev = touched.numel(), self.D, self.dev
+        base = touched.to(i64)[:, None] * self.L
+        slot = self.tail + torch.arange(T, device=dev, dtype=i64)[:, None] * self.Ls
+        cat = lambda x, y: torch.cat([x, y], dim=1).reshape(-1).contiguous()  # noqa: E731
+        full = lambda v, dt: torch.full((T, 1), v, dtype=dt, device=dev)  # noqa: E731
+        return {
+            "bytes": self.bytes,
+            "chain_offsets": (torch.arange(T + 1, device=dev, dtype=i64) * (D + 1)).to(i32),
+            "pre_off": cat(base + self.t_pre_off[None, :], slot + self.s_pre_off),
+            "pre_len": cat(self.t_pre_len[None, :].expand(T, D), full(self.s_pre_len, i32)),
+            "suf_off": cat(base + self.t_suf_off[None, :], slot + self.s_suf_off),
+            "suf_len": cat(self.t_suf_len[None, :].expand(T, D), full(self.s_suf_len, i32)),
+        }
+
+
 def config5(ctx: Ctx, args):
     E_total = args.edges or 10_000_000
     per = 16
     S = E_total // per
     vb0 = random_vouch_batch(S, per, ctx.dev, seed=5)
     g = torch.Generator().manual_seed(9)
-    tgt = torch.randint(0, 16, (S,), generator=g, dtype=u8).to(ctx.dev)
+    # the storm hits a random subset of the sessions; the others keep target 255 (no slash)
+    tgt = torch.full((S,), 255, dtype=u8)
+    hit = torch.randperm(S, generator=g)[: max(1, int(S * args.storm_fraction))]
+    tgt[hit] = torch.randint(0, 16, (hit.numel(),), generator=g, dtype=u8)
+    tgt = tgt.to(ctx.dev)
     omega = torch.full((S,), 0.95, dtype=f64, device=ctx.dev)
     scores0 = torch.rand((S, 16), generator=g, dtype=f64).to(ctx.dev)
-    # audit chains of the same sessions (3 deltas each) for the re-chain
     D = args.deltas or 3
-    from hypervisor.audit.delta import DeltaEngine, VFSChange
-
-    proto = DeltaEngine("session:slash-storm")
-    for k in range(D):
-        proto.capture("did:mesh:agent", [VFSChange(f"/f{k}", "add", f"h{k}")])
-    one = A.pack_chains([proto.deltas])
-    # every session re-chains the same-shaped payloads (tiled arena → S chains)
-    chains_n = S
-    Lb = one["bytes"].numel()
-    packed = {
-        "bytes": one["bytes"].to(ctx.dev),
-        "chain_offsets": (torch.arange(chains_n + 1, dtype=i64) * D).to(i32).to(ctx.dev),
-        "pre_off": one["pre_off"].repeat(chains_n).to(ctx.dev),
-        "pre_len": one["pre_len"].repeat(chains_n).to(ctx.dev),
-        "suf_off": one["suf_off"].repeat(chains_n).to(ctx.dev),
-        "suf_len": one["suf_len"].repeat(chains_n).to(ctx.dev),
-    }
-    leaves_offs = packed["chain_offsets"]
-    # P03: the audit stage (re-chain + Merkle: SHA-issue-bound, fills the GPU) and the
-    # liability stage (slash cascade + σ_eff: latency-bound CSR walks) are
-    # independent, so they run on two streams and share the CUs
-    side = torch.cuda.Stream(ctx.dev) if ctx.dev.type == "cuda" else None
-
-    def audit_stage():
-        digests = A.chain_hashes(packed)
-        A.merkle_roots(leaves_offs, digests)
+    arena = AuditArena(S, D, ctx.dev)
+    last = {}
 
     def step():
-        main = torch.cuda.current_stream(ctx.dev) if side is not None else None
-        if side is not None:
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                audit_stage()
-        # fresh storm state: the slash mutates only `active`, `released_us` and the
-        # scores, so only those are reset (the CSR topology and bonds are shared)
+        # fresh storm state: the slash mutates only `active`, `released_us` and the scores
         vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, vb0.active.clone(),
                            vb0.expiry_us, vb0.released_us.clone())
         out = LI.slash(vb, tgt, omega, scores0.clone(), 1, clip_cap=per)  # ≤ one clip per edge
         se = LI.sigma_eff_exact(vb, out.scores, omega, 1)  # NaN (absent) reads as 0.0
-        if side is None:
-            audit_stage()
-        else:
-            main.wait_stream(side)
+        # re-chain exactly the sessions the slash touched, after it (data dependency):
+        # each gets a slash delta carrying its post-slash scores, then its whole
+        # chain is re-hashed (K08) and its Merkle root recomputed (K09)
+        touched = torch.nonzero(out.clip_count > 0).flatten()
+        arena.write_slash_deltas(touched, out.scores[touched])
+        packed = arena.packed(touched)
+        digests = A.chain_hashes(packed)
+        roots = A.merkle_roots(packed["chain_offsets"], digests)
+        last.update(T=touched.numel(), roots=roots)
         return se
 
     el, lat = ctx.timed(step, args.steps, args.warmup)
-    ctx.emit(config="config5", what="slash cascade + sigma_eff + re-chain + merkle", bond_edges=S * per,
-             sessions=S, deltas_rechained=S * D, arena_bytes=Lb, ms_per_storm=el / args.steps * 1e3,
-             storm_p50_ms=statistics.median(lat) * 1e3, bond_updates_per_s=S * per * ctx.world * args.steps / el)
+    T = int(last["T"])
+    rechain_bytes = T * (arena.L + arena.Ls) + T * (D + 1) * 32 * 2 + T * 16 * 8
+    slash_bytes = S * per * (1 + 1 + 1 + 8 + 8) + S * 16 * 8 * 3 + S * 4
+    ctx.emit(config="config5", what="slash storm on a session subset + sigma_eff + re-chain/merkle of the "
+                                    "touched sessions", bond_edges=S * per, sessions=S,
+             sessions_slashed=int(hit.numel()), sessions_touched=T, deltas_rechained=T * (D + 1),
+             arena_bytes_resident=int(arena.bytes.numel()), distinct_payloads=True,
+             hbm_bytes_est=dict(slash_sigma=slash_bytes, rechain=rechain_bytes),
+             ms_per_storm=el / args.steps * 1e3, storm_p50_ms=statistics.median(lat) * 1e3,
+             bond_updates_per_s=S * per * ctx.world * args.steps / el)
 
 
 def main():
@@ -362,6 +440,7 @@ def main():
     ap.add_argument("--agents", type=int, default=0)
     ap.add_argument("--edges", type=int, default=0)
     ap.add_argument("--deltas", type=int, default=0)
+    ap.add_argument("--storm-fraction", type=float, default=0.1, help="config5: share of sessions slashed")
     ap.add_argument("--coroutine-sagas", type=int, default=4096, help="config4: sagas in the coroutine mode")
     ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
     ap.add_argument("--owner-reduce", action="store_true", help="config3: reduce-scatter exposure to agent owners")

@@ -491,6 +491,10 @@ AHV_HD bool has_live_voucher(const Edges& ed, int32_t b, int32_t e, int who) {
 // slots through a pointer — scratch memory on the device, ~2 µs per step.)
 template <class Edges>
 AHV_HD void slash_session_t(const SlashArgs& a, int64_t s, const Edges& ed, double* sc, int ss) {
+  if (a.target[s] >= kTile) {  // no slash in this session (storm subsets)
+    a.clip_count[s] = 0;
+    return;
+  }
   const int32_t b = a.offsets[s], e = a.offsets[s + 1];
   const double omega = a.omega[s];
   const int32_t base = a.clip_offsets[s];
@@ -652,6 +656,10 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
   const int gl0 = gw * kSlashGroup;              // first wave lane of the group
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kSlashGroupsPerBlock + g;
   if (s >= a.sessions) return;
+  if (a.target[s] >= kTile) {  // group-uniform: no slash in this session
+    if (j == 0) a.clip_count[s] = 0;
+    return;
+  }
   const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
   if (n > kGroupEdges) {
     if (j == 0) slash_session(a, s);
