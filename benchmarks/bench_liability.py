@@ -84,6 +84,17 @@ def main() -> None:
             def fused():
                 return LI.bond_fused(vb, sigma, omega, 0, members=members, agent_exposure=ax)
             res["fused"] = (time_us(fused, a.iters), (fused()[0] - ref).abs().max().item())
+        if "admit" in only or not a.only:  # K05: 4 vouch requests per session against the resident edges
+            g2 = torch.Generator(device=dev).manual_seed(3)
+            R = 4 * S
+            r_off = (torch.arange(S + 1, device=dev) * 4).to(torch.int32)
+            rv = torch.randint(0, 16, (R,), device=dev, generator=g2).to(torch.uint8)
+            re_ = torch.randint(0, 16, (R,), device=dev, generator=g2).to(torch.uint8)
+            rs = torch.rand(R, dtype=torch.float64, device=dev, generator=g2) * 0.7 + 0.3
+            rp = torch.full((R,), 0.1, dtype=torch.float64, device=dev)
+            us = time_us(lambda: LI.vouch_admit(vb, r_off, rv, re_, rs, rp, 0), a.iters)
+            print(json.dumps(dict(variant="vouch_admit", sessions=S, edges=E, requests=R, us=round(us, 2),
+                                  requests_per_us=round(R / us, 1))), flush=True)
         for k, (us, err) in res.items():
             print(json.dumps(dict(variant=k, sessions=S, edges=E, us=round(us, 2),
                                   edges_per_us=round(E / us, 1), max_abs_err_vs_csr=err,

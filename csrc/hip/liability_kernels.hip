@@ -395,10 +395,22 @@ AHV_HD void adj_set(uint64_t w[4], int v, int e) {
   else w[3] |= bit;
 }
 
-AHV_HD void vouch_admit_session(const VouchAdmitArgs& a, int64_t s) {
+// Per-session admission, O(E + R·16): one pass over the live edges builds the
+// adjacency bits and each voucher's running exposure (creation order); every
+// request then reads its voucher's running sum and, when admitted, adds its bond
+// to it — the same additions in the same order as rescanning edges and earlier
+// admitted requests, so the exposure test is bit-identical to the reference's.
+// `Ed` supplies edge k (global arrays or an LDS stage); `exp` is 16 doubles.
+template <class Ed>
+AHV_HD void vouch_admit_body(const VouchAdmitArgs& a, int64_t s, const Ed& ed, double* exp, int xs) {
   uint64_t adj[4] = {0, 0, 0, 0};
-  for (int32_t k = a.e_offsets[s]; k < a.e_offsets[s + 1]; ++k)
-    if (live_edge(a.e_active, a.e_expiry, k, a.now_us)) adj_set(adj, a.e_voucher[k], a.e_vouchee[k]);
+  for (int u = 0; u < kTile; ++u) exp[u * xs] = 0.0;
+  for (int32_t k = a.e_offsets[s]; k < a.e_offsets[s + 1]; ++k) {
+    if (!ed.live(k)) continue;
+    const int v = ed.voucher(k);
+    adj_set(adj, v, ed.vouchee(k));
+    exp[v * xs] += ed.bonded(k);
+  }
   for (int32_t q = a.r_offsets[s]; q < a.r_offsets[s + 1]; ++q) {
     const int v = a.r_voucher[q], e = a.r_vouchee[q];
     const double sig = a.r_sigma[q];
@@ -423,27 +435,75 @@ AHV_HD void vouch_admit_session(const VouchAdmitArgs& a, int64_t s) {
         double pct = a.r_pct[q];
         pct = pct < 0.0 ? 0.0 : (pct > 1.0 ? 1.0 : pct);
         bonded = sig * pct;
-        double cur = 0.0;  // exposure in creation order: existing live edges, then admitted requests
-        for (int32_t k = a.e_offsets[s]; k < a.e_offsets[s + 1]; ++k)
-          if (a.e_voucher[k] == v && live_edge(a.e_active, a.e_expiry, k, a.now_us)) cur += a.e_bonded[k];
-        for (int32_t p = a.r_offsets[s]; p < q; ++p)
-          if (a.code[p] == 0 && a.r_voucher[p] == v) cur += a.r_bonded[p];
-        if (cur + bonded > sig * a.max_exposure) code = 4;
+        if (exp[v * xs] + bonded > sig * a.max_exposure) code = 4;
       }
     }
     a.code[q] = code;
     a.r_bonded[q] = code == 0 ? bonded : 0.0;
-    if (code == 0) adj_set(adj, v, e);
+    if (code == 0) {
+      adj_set(adj, v, e);
+      exp[v * xs] += bonded;
+    }
   }
 }
-__global__ void vouch_admit_kernel(VouchAdmitArgs a) {
-  for (int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; s < a.sessions;
-       s += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    vouch_admit_session(a, s);
+
+struct AdmitGlobalEdges {
+  const VouchAdmitArgs* a;
+  AHV_HD bool live(int32_t k) const { return live_edge(a->e_active, a->e_expiry, k, a->now_us); }
+  AHV_HD int voucher(int32_t k) const { return a->e_voucher[k]; }
+  AHV_HD int vouchee(int32_t k) const { return a->e_vouchee[k]; }
+  AHV_HD double bonded(int32_t k) const { return a->e_bonded[k]; }
+};
+
+AHV_HD void vouch_admit_session(const VouchAdmitArgs& a, int64_t s) {
+  double exp[kTile];
+  vouch_admit_body(a, s, AdmitGlobalEdges{&a}, exp, 1);
+}
+
+// Device: 64 sessions per block (one lane each).  The block's contiguous edge
+// range is staged in LDS with coalesced loads — voucher·16 + vouchee with 0xff
+// for a dead edge, and the bond — and every lane keeps its 16 running exposures
+// in an LDS row (dynamic voucher index: LDS, not scratch).  Ranges larger than
+// the stage read global memory.
+constexpr int kAdmitSessions = 64;
+constexpr int kAdmitLdsEdges = 1024;
+constexpr int kAdmitExpStride = kAdmitSessions + 1;  // exp[v] of lane t at v·65 + t: consecutive lanes, distinct banks
+
+struct AdmitLdsEdges {
+  int32_t e0;
+  const uint8_t* key;
+  const double* bd;
+  __device__ bool live(int32_t k) const { return key[k - e0] != 0xff; }
+  __device__ int voucher(int32_t k) const { return key[k - e0] >> 4; }
+  __device__ int vouchee(int32_t k) const { return key[k - e0] & 15; }
+  __device__ double bonded(int32_t k) const { return bd[k - e0]; }
+};
+
+__global__ __launch_bounds__(kAdmitSessions) void vouch_admit_kernel(VouchAdmitArgs a) {
+  __shared__ uint8_t s_key[kAdmitLdsEdges];
+  __shared__ double s_bd[kAdmitLdsEdges];
+  __shared__ double s_exp[kTile * kAdmitExpStride];
+  const int t = threadIdx.x;
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * kAdmitSessions;
+  const int64_t s1 = s0 + kAdmitSessions < a.sessions ? s0 + kAdmitSessions : a.sessions;
+  const int64_t s = s0 + t;
+  const int32_t e0 = a.e_offsets[s0], e1 = a.e_offsets[s1];
+  double* exp = s_exp + t;
+  if (e1 - e0 > kAdmitLdsEdges) {  // block-uniform
+    if (s < s1) vouch_admit_body(a, s, AdmitGlobalEdges{&a}, exp, kAdmitExpStride);
+    return;
+  }
+  for (int32_t k = e0 + t; k < e1; k += kAdmitSessions) {
+    const bool live = live_edge(a.e_active, a.e_expiry, k, a.now_us);
+    s_key[k - e0] = live ? static_cast<uint8_t>((a.e_voucher[k] << 4) | a.e_vouchee[k]) : 0xffu;
+    s_bd[k - e0] = a.e_bonded[k];
+  }
+  __syncthreads();
+  if (s < s1) vouch_admit_body(a, s, AdmitLdsEdges{e0, s_key, s_bd}, exp, kAdmitExpStride);
 }
 void launch_vouch_admit(const VouchAdmitArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
-  hipLaunchKernelGGL(vouch_admit_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(vouch_admit_kernel, grid1(a.sessions, kAdmitSessions), dim3(kAdmitSessions), 0, st, a);
   check_hip(hipGetLastError(), "vouch_admit_kernel");
 }
 void vouch_admit_host(const VouchAdmitArgs& a) { for (int64_t s = 0; s < a.sessions; ++s) vouch_admit_session(a, s); }

@@ -196,6 +196,24 @@ def test_liability_kernels_large_sessions(cuda_device):
     scores[scores < 0.1] = float("nan")
     _check(lambda *t: LI.slash(mk(*t[:-3]), t[-3], t[-2], t[-1], 100), *[getattr(vb, f) for f in fields],
            tgt, omega, scores)
+    # storm subsets: target 255 leaves a session untouched
+    tgt2 = tgt.clone()
+    tgt2[::3] = 255
+    _check(lambda *t: LI.slash(mk(*t[:-3]), t[-3], t[-2], t[-1], 100), *[getattr(vb, f) for f in fields],
+           tgt2, omega, scores)
+    # admission past the 1024-edge LDS stage (global-memory fallback) mixed with staged blocks
+    rng = random.Random(9)
+    r_off, rv, re_, rs, rp = [0], [], [], [], []
+    for _ in range(S):
+        for _ in range(rng.randint(0, 20)):
+            rv.append(rng.randrange(16))
+            re_.append(rng.randrange(16))
+            rs.append(rng.uniform(0.3, 1.0))
+            rp.append(rng.choice([0.05, 0.1, 0.5]))
+        r_off.append(len(rv))
+    _check(lambda *t: LI.vouch_admit(mk(*t[: len(fields)]), *t[len(fields):], 100),
+           *[getattr(vb, f) for f in fields], torch.tensor(r_off, dtype=i32), torch.tensor(rv, dtype=u8),
+           torch.tensor(re_, dtype=u8), torch.tensor(rs, dtype=f64), torch.tensor(rp, dtype=f64))
 
 
 def test_audit_kernels(cuda_device):
