@@ -78,6 +78,12 @@ class ShardedHypervisor:
         self._vouch_seq = 0
         self._vouch_meta: dict[str, tuple[int, str]] = {}  # vouch id → (global seq, session) on the owner
         self._step_owner: dict[str, str] = {}  # step id → saga id (replicated)
+        # live membership: global ranks still serving; after a failover the control and
+        # data collectives move to sub-groups of the survivors (global rank ids stay)
+        self.members = list(range(self.world))
+        self.data_group = None  # default group (RCCL on MI355X) until a failover
+        self.heartbeat = None
+        self.failovers: list[dict] = []
 
     # -- control plane ---------------------------------------------------------
     def _bcast(self, obj: Any, src: int) -> Any:
@@ -90,9 +96,13 @@ class ShardedHypervisor:
     def _gather(self, obj: Any) -> list:
         if self.world == 1:
             return [obj]
-        out: list = [None] * self.world
+        out: list = [None] * len(self.members)
         dist.all_gather_object(out, obj, group=self.group)
         return out
+
+    def _all_reduce(self, t: torch.Tensor, op) -> None:
+        if self.world > 1:
+            dist.all_reduce(t, op=op, group=self.data_group)
 
     async def _on(self, owner: int, fn: Callable[[], Any]) -> Any:
         """Run ``fn`` on the owner rank; every rank returns its result or raises its exception."""
@@ -113,7 +123,9 @@ class ShardedHypervisor:
     def owner(self, session_id: str) -> int:
         r = self.directory.owner(session_id)
         if r is None:  # liability sessions that are not hypervisor sessions (e.g. "s1")
-            return stable_rank(session_id, self.world)
+            r = stable_rank(session_id, self.world)
+            if r not in self.members:
+                r = self.members[stable_rank(session_id, len(self.members))]
         return r
 
     def _owner_strict(self, session_id: str) -> int:
@@ -270,8 +282,7 @@ class ShardedHypervisor:
             sum(1 for m in sessions for _ in m.saga.sagas),
         ]
         t = torch.tensor(vals, dtype=torch.int64, device=_tensor_device() if self.world > 1 else "cpu")
-        if self.world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        self._all_reduce(t, dist.ReduceOp.SUM)
         keys = ("total_sessions", "active_sessions", "total_participants", "active_sagas", "total_vouches",
                 "total_sagas")
         return dict(zip(keys, (int(x) for x in t.tolist())))
@@ -290,8 +301,7 @@ class ShardedHypervisor:
                         best, best_sid, best_ring = key, sid, int(p.ring)
                     break
         t = torch.tensor([best], dtype=torch.int64, device=_tensor_device() if self.world > 1 else "cpu")
-        if self.world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        self._all_reduce(t, dist.ReduceOp.MIN)
         key = int(t.item())
         if key >= big:
             return None
@@ -327,8 +337,7 @@ class ShardedHypervisor:
             if k is not None and v.is_live:
                 x[k] += v.bonded_amount
         x = x.to(dev)
-        if self.world > 1:
-            dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        self._all_reduce(x, dist.ReduceOp.SUM)
         return x
 
     def list_sessions(self, state: Optional[str] = None) -> list[dict]:
@@ -341,6 +350,71 @@ class ShardedHypervisor:
                               {"session_id": sid, "state": st, "participant_count": m.sso.participant_count,
                                "rank": self.rank}))
         return [d for _, d in sorted((x for part in self._gather(local) for x in part), key=lambda x: x[0])]
+
+    # -- resilience: heartbeat, checkpoint, failover -----------------------
+    def start_heartbeat(self, interval_s: float = 0.5):
+        """Stamp this rank's liveness in the rendezvous store every ``interval_s``."""
+        from agent_hypervisor_amd.parallel.resilience import Heartbeat
+
+        if self.world > 1 and self.heartbeat is None:
+            self.heartbeat = Heartbeat(interval_s).start()
+        return self.heartbeat
+
+    def dead_ranks(self, timeout_s: float) -> list[int]:
+        """Members whose heartbeat is older than ``timeout_s`` (local, no collective)."""
+        if self.heartbeat is None:
+            return []
+        return [r for r in self.heartbeat.dead_ranks(timeout_s) if r in self.members]
+
+    def checkpoint(self, root: str) -> str:
+        """Each rank persists its own sessions (and its share of the vouch
+        ordering) under ``root/rank<r>``; collective over the members."""
+        import json
+        import os
+
+        from agent_hypervisor_amd.runtime.checkpoint import save_hypervisor
+
+        d = save_hypervisor(self.local, os.path.join(root, f"rank{self.rank}"))
+        with open(os.path.join(d, "sharded.json"), "w") as f:
+            json.dump({"rank": self.rank, "vouch_meta": self._vouch_meta}, f)
+        if self.world > 1:
+            dist.barrier(group=self.group)
+        return d
+
+    async def failover(self, failed: list[int], root: str) -> list[tuple[str, int, int]]:
+        """Survivors (every remaining member calls this) re-home the failed
+        ranks' sessions (least-loaded first), re-hydrate the ones assigned here
+        from the failed ranks' checkpoints — audit chains re-verified on load — and
+        move the control/data collectives to sub-groups of the survivors."""
+        import json
+        import os
+
+        from agent_hypervisor_amd.parallel.resilience import apply_failover, failover_plan, rehydrate
+
+        failed = sorted(set(failed) & set(self.members))
+        if not failed:
+            return []
+        if self.rank in failed:
+            raise RuntimeError("a failed rank cannot take part in its own failover")
+        moves = failover_plan(self.directory, failed)
+        apply_failover(self.directory, moves, failed)
+        for f in failed:
+            src = os.path.join(root, f"rank{f}")
+            mine = [(s, a, b) for s, a, b in moves if a == f and b == self.rank]
+            if mine:
+                rehydrate(src, mine, self.rank, hv=self.local)
+            meta = os.path.join(src, "sharded.json")
+            if os.path.exists(meta):
+                with open(meta) as fh:
+                    vm = json.load(fh)["vouch_meta"]
+                moved = {s for s, _, b in mine}
+                self._vouch_meta.update({k: tuple(v) for k, v in vm.items() if v[1] in moved})
+        self.members = [r for r in self.members if r not in failed]
+        # only the survivors synchronise on these groups (the failed ranks never call in)
+        self.group = dist.new_group(ranks=self.members, backend="gloo", use_local_synchronization=True)
+        self.data_group = dist.new_group(ranks=self.members, use_local_synchronization=True)
+        self.failovers.append({"failed": failed, "moves": len(moves)})
+        return moves
 
     def invalidate_agents(self, agent_dids: list[str]) -> list[str]:
         """X08: broadcast Nexus cache invalidations from rank 0 to every rank."""
