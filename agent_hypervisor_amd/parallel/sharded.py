@@ -366,6 +366,23 @@ class ShardedHypervisor:
             return []
         return [r for r in self.heartbeat.dead_ranks(timeout_s) if r in self.members]
 
+    def agree_failed(self, suspects: list[int]) -> list[int]:
+        """One failure verdict for all survivors: the lowest member not suspected
+        publishes its suspect list in the rendezvous store under the next failover
+        epoch and every survivor adopts it (local heartbeat views can differ by a
+        beat)."""
+        import json
+
+        from agent_hypervisor_amd.parallel.resilience import _store
+
+        st = _store()
+        key = f"ahv/failover/{len(self.failovers)}"
+        coord = min(r for r in self.members if r not in suspects)
+        if self.rank == coord:
+            st.set(key, json.dumps(sorted(suspects)))
+        st.wait([key])
+        return json.loads(st.get(key).decode())
+
     def checkpoint(self, root: str) -> str:
         """Each rank persists its own sessions (and its share of the vouch
         ordering) under ``root/rank<r>``; collective over the members."""

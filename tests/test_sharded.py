@@ -133,6 +133,7 @@ def _rest_worker(rank: int, world: int, port: int, q) -> None:
         shv = ShardedHypervisor()
         if rank != 0:
             asyncio.run(serve_followers(shv))
+            dist.barrier()  # leave together: teardown while a peer still runs can abort gloo
             return
         from fastapi.testclient import TestClient
 
@@ -158,6 +159,7 @@ def _rest_worker(rank: int, world: int, port: int, q) -> None:
             }
         driver.stop()
         q.put(out)
+        dist.barrier()
     finally:
         dist.destroy_process_group()
 
@@ -195,8 +197,16 @@ def test_failover_never_places_on_dead_rank():
 
 
 def _failover_worker(rank: int, world: int, port: int, root: str, q) -> None:
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), AHV_STORE="host")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(AHV_STORE="host")
+    log = open(os.path.join(root, f"progress{rank}.log"), "a", buffering=1)
+
+    def mark(what):
+        import time as _t
+
+        log.write(f"{_t.time():.3f} {what}\n")
+
+    # file rendezvous: no TCP port to race other concurrently running tests for
+    dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
     from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
     from hypervisor import SessionConfig
     from hypervisor.audit.delta import VFSChange
@@ -218,23 +228,30 @@ def _failover_worker(rank: int, world: int, port: int, root: str, q) -> None:
         await shv.add_step(gid, "a", "did:agent-1", "/a", undo_api="/u")
         return sids, gid
 
+    mark("init")
     sids, gid = asyncio.run(build())
+    mark("built")
     before = {s: asyncio.run(shv.get_session(s)) for s in sids}
     roots = {s: asyncio.run(shv.merkle_root(s)) for s in sids}
     stats0 = shv.stats()
     liab0 = shv.agent_liability("did:agent-0")
     shv.checkpoint(root)
+    mark("checkpointed")
     if rank == world - 1:  # this rank dies: stop beating and leave without tearing down
         shv.heartbeat.stop()
         os._exit(0)
     import time
 
-    deadline = time.time() + 30
+    deadline = time.time() + 60
     dead = []
     while time.time() < deadline and not dead:
         time.sleep(0.2)
-        dead = shv.dead_ranks(1.0)
-    moves = asyncio.run(shv.failover(dead, root))
+        dead = shv.dead_ranks(3.0)  # 15 missed beats: robust to a loaded test machine
+    mark(f"suspects {dead}")
+    verdict = shv.agree_failed(dead)
+    mark(f"verdict {verdict}")
+    moves = asyncio.run(shv.failover(verdict, root))
+    mark("failed over")
 
     async def after():
         out = {s: await shv.get_session(s) for s in sids}
@@ -245,6 +262,7 @@ def _failover_worker(rank: int, world: int, port: int, root: str, q) -> None:
         return out, r, new, saga
 
     out, r2, new, saga = asyncio.run(after())
+    mark("served")
     res = dict(dead=dead, moves=len(moves), members=shv.members, stats0=stats0, stats1=shv.stats(),
                same_sessions=all(
                    {k: v for k, v in out[s].items() if k != "rank"} == {k: v for k, v in before[s].items()
@@ -254,6 +272,8 @@ def _failover_worker(rank: int, world: int, port: int, root: str, q) -> None:
                root_changed=asyncio.run(shv.merkle_root(sids[-1])) != roots[sids[-1]])
     if rank == 0:
         q.put(res)
+        q.close()
+        q.join_thread()  # flush the queue's feeder thread before the hard exit
     dist.barrier(group=shv.group)
     os._exit(0)  # the default group still names the dead rank: skip its teardown
 
@@ -268,7 +288,15 @@ def test_failover_rehydrates_dead_rank(tmp_path):
     procs = [ctx.Process(target=_failover_worker, args=(r, 3, port, str(tmp_path), q)) for r in range(3)]
     for p in procs:
         p.start()
-    res = q.get(timeout=240)
+    try:
+        res = q.get(timeout=150)
+    except Exception:
+        for r in range(3):
+            pth = tmp_path / f"progress{r}.log"
+            print(r, pth.read_text() if pth.exists() else "-")
+        for p in procs:
+            p.kill()
+        raise
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
