@@ -276,6 +276,13 @@ def main() -> None:
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     totals = last.cpu().tolist()
+    # X09: job-wide step-latency histogram (log2 µs bins), summed over ranks outside the timed loop
+    from agent_hypervisor_amd.parallel.collectives import reduce_histogram
+
+    hist = torch.zeros(32, dtype=torch.int64)
+    for x in lat:
+        hist[min(31, max(0, int(x * 1e6).bit_length() - 1))] += 1
+    hist = reduce_histogram(hist.to(dev)).cpu().tolist()
 
     scalar_p50 = scalar_mean = device_p50 = device_mean = None
     if rank == 0 and not args.no_scalar:
@@ -317,6 +324,7 @@ def main() -> None:
             "scalar_mean_us": round(scalar_mean, 2) if scalar_mean is not None else None,
             "scalar_vs_baseline_p50": round(BASELINE_P50_US / scalar_p50, 2) if scalar_p50 else None,
             "last_step_counters": dict(zip(["sessions", "ok", "participants", "deltas", "commits", "archived"], totals)),
+            "step_latency_hist_log2_us": {str(1 << b): c for b, c in enumerate(hist) if c},
             "rccl_ranks": world if (multi and dev.type == "cuda") else 0,
             "collective_backend": dist.get_backend() if multi else None,
             "collectives_per_step": {

@@ -604,6 +604,40 @@ class DeviceLiabilityLedger(LiabilityLedger):
         self.log.add(agent=a, type=_LEDGER_CODE[LedgerEntryType(entry_type)], severity=float(severity))
         return e
 
+    def partials(self, agent_dids: Sequence[str]) -> dict[str, torch.Tensor]:
+        """Per-agent ledger partials on the device (one K22 launch over the log):
+        raw (unclamped) risk, slash / quarantine / clean / fault counts, fault
+        severity sum and entry count — the additive state the sharded ledger
+        all-reduces (X03).  Agents without entries get zeros."""
+        self.log.flush()
+        n, A = self.log.n, len(self._agent_row)
+        dev = self.device
+        rows = torch.tensor([self._agent_row.get(a, -1) for a in agent_dids], dtype=i64).to(dev)
+        z = {k: torch.zeros(len(agent_dids), dtype=f64 if k in ("raw", "fault_sum") else i64, device=dev)
+             for k in ("raw", "slash", "quarantine", "clean", "fault_sum", "fault_n", "total")}
+        if n == 0 or A == 0:
+            return z
+        agent = self.log.view("agent")
+        order = torch.sort(agent, stable=True).indices
+        offs = torch.zeros(A + 1, dtype=i64, device=dev)
+        offs[1:] = torch.bincount(agent.to(i64), minlength=A).cumsum(0)
+        types = self.log.view("type")[order].contiguous()
+        sev = self.log.view("severity")[order].contiguous()
+        out = LG.risk_profiles(offs.to(i32), types, sev)
+        fault = (self.log.view("type") == LG.LEDGER_CODE["fault_attributed"])
+        fault_n = torch.bincount(agent.to(i64), weights=fault.to(f64), minlength=A).round().to(i64)
+        have = rows >= 0
+        r = rows.clamp(min=0)
+        pick = lambda t, dt: torch.where(have, t[r].to(dt), torch.zeros((), dtype=dt, device=dev))  # noqa: E731
+        z["raw"] = pick(out["raw_risk"], f64)
+        z["slash"] = pick(out["slash_count"], i64)
+        z["quarantine"] = pick(out["quarantine_count"], i64)
+        z["clean"] = pick(out["clean_count"], i64)
+        z["fault_n"] = pick(fault_n, i64)
+        z["fault_sum"] = pick(out["fault_avg"], f64) * z["fault_n"].to(f64)
+        z["total"] = pick(offs[1:] - offs[:-1], i64)
+        return z
+
     def compute_risk_profiles(self, agent_dids: Sequence[str]) -> list[AgentRiskProfile]:
         """Risk profiles of many agents from one K22 launch over the whole log."""
         self.log.flush()

@@ -304,3 +304,46 @@ def test_failover_rehydrates_dead_rank(tmp_path):
     assert res["same_sessions"] and res["same_roots"] and res["liab_same"]
     assert res["stats1"]["total_sessions"] == res["stats0"]["total_sessions"] + 1
     assert res["new_owner"] in (0, 1) and res["saga_steps"] == 1 and res["root_changed"]
+
+
+def _ledger_worker(rank: int, world: int, root: str, device, q) -> None:
+    dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
+    try:
+        import random as _r
+
+        from agent_hypervisor_amd.parallel.sharded_ledger import ShardedLedger
+        from hypervisor.liability.ledger import LedgerEntryType, LiabilityLedger
+
+        rng = _r.Random(5)
+        led = ShardedLedger(device=device)
+        ref = LiabilityLedger()
+        agents = [f"did:l{i}" for i in range(25)]
+        for k in range(500):
+            e = (rng.choice(agents), rng.choice(list(LedgerEntryType)), f"session-{rng.randrange(40)}",
+                 rng.choice([0.0, 0.3, 0.5, 0.9, 1.0, rng.random()]))
+            led.record(*e)
+            ref.record(*e)
+        ask = agents + ["did:nobody"]
+        got = led.compute_risk_profiles(ask)
+        if rank == 0:
+            q.put((got, ref.compute_risk_profiles(ask), len(led.local.get_agent_history(agents[0]))))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,device", [(2, None), (3, "cpu")])
+def test_sharded_ledger_matches_single(tmp_path, world, device):
+    """X03: ledger entries live on their session's owner; profiles combined with
+    the fixed-point risk all-reduce equal one ledger's (host and device ledgers)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ledger_worker, args=(r, world, str(tmp_path), device, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, want, local_n = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == want
+    assert 0 < local_n < want[0].total_entries  # the entries really are spread over ranks
