@@ -57,7 +57,7 @@ if __name__ == "__main__" and (len(sys.argv) <= 3 or sys.argv[3] != "breakdown")
     asyncio.run(main())
 
 
-async def breakdown(dev: str = "cuda", iters: int = 1000) -> dict:
+async def breakdown(dev: str = "cuda", iters: int = 1000, idle_us: int = 0) -> dict:
     """Median wall time of each API call of the reference pipeline."""
     import collections
 
@@ -87,6 +87,11 @@ async def breakdown(dev: str = "cuda", iters: int = 1000) -> dict:
         t = tick("add_step", t)
         await s.saga.execute_step(saga.saga_id, step.step_id, executor=lambda: asyncio.sleep(0))
         t = tick("execute_step", t)
+        if idle_us:  # let the hash-engine wave drain first: terminate then measures its own work
+            end = time.perf_counter_ns() + idle_us * 1000
+            while time.perf_counter_ns() < end:
+                pass
+            t = tick("idle", t)
         await hv.terminate_session(sid)
         t = tick("terminate", t)
         if it < 200:
@@ -95,4 +100,5 @@ async def breakdown(dev: str = "cuda", iters: int = 1000) -> dict:
 
 
 if __name__ == "__main__" and len(sys.argv) > 3 and sys.argv[3] == "breakdown":
-    print(json.dumps(asyncio.run(breakdown(sys.argv[1], int(sys.argv[2])))), flush=True)
+    idle = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    print(json.dumps(asyncio.run(breakdown(sys.argv[1], int(sys.argv[2]), idle))), flush=True)

@@ -163,3 +163,6 @@ def test_dashboard_page_and_live_summary(client):
     assert s["liability"]["top_exposure"][0]["agent_did"] == "did:hi"
     assert s["events"]["recent"][0]["event_type"] in {"saga.created", "liability.vouch_created"}
     assert s["engine"] is None
+    assert s["sessions"][0]["session_id"] == sid and s["agents"][0]["agent_did"] == "did:a"
+    assert s["liability"]["vouches"][0]["voucher_did"] == "did:hi" and s["sagas"]["rows"][0]["state"] == "running"
+    assert s["overview"]["state_authority"] in ("host", "device")
