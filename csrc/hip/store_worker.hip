@@ -56,6 +56,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
                                                            int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks) {
   __shared__ uint64_t inl[kInlineWords];
   __shared__ uint32_t lds1[kLdsWords];      // wave 1: capture message staging
+  __shared__ uint32_t kw1[64 * kKwStride];  // wave 1: per-lane K+W schedule rows
   __shared__ uint32_t lds0[kLdsWords / 4];  // wave 0: staging for its own (rare) in-place hashing
   __shared__ HashJob jobs[kJobs];
   __shared__ uint32_t q_head, q_done, stop, bye;
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
 
   if (wave == 1) {
     // ------------------------------------------------------------ hash engine
-    const Lanes L{lane, 64, lds1};
+    const Lanes L{lane, 64, lds1, kw1};
     uint32_t done = 0;
     for (;;) {
       const uint32_t head = lds_acquire(&q_head);

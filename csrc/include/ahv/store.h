@@ -182,11 +182,13 @@ struct Tables {
 // `lds` is a word buffer in LDS on the device (a thread-local array on the host)
 // used to stage audit payloads as big-endian SHA message words.
 constexpr int kLdsWords = 4096;  // 16 KiB: payloads up to 16 KiB − 72 B hash from LDS
+constexpr int kKwStride = 65;    // words per schedule row: odd stride, the 64 lanes' rows hit distinct banks
 
 struct Lanes {
   int lane;
   int n;
   uint32_t* lds;
+  uint32_t* kw = nullptr;  // [n][kKwStride] per-lane K+W schedule rows (hash-engine wave), or null
   AHV_HD bool leader() const { return lane == 0; }
   // Lanes of ONE wave exchange data through LDS / global memory: a wave-level
   // barrier with wavefront-scope fences (the worker runs two waves with
@@ -465,6 +467,67 @@ AHV_HD int64_t stage_message(const Lanes& L, uint8_t* src, uint64_t n, int64_t h
 AHV_HD void sha256_lds_blocks(const uint32_t* w, int64_t nblk, uint32_t out[8]) {
   sha256_init(out);
   for (int64_t b = 0; b < nblk; ++b) sha256_compress(out, w + 16 * b);
+}
+
+// Message schedule of one block with the round constants folded in: kw[t] =
+// K[t] + W[t] for t < 64 (the half of a compression that does not depend on the
+// chaining state).
+AHV_HD void sha256_expand_kw(const uint32_t* blk, uint32_t* kw) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    w[i] = blk[i];
+    kw[i] = w[i] + sha256_k(i);
+  }
+#pragma unroll
+  for (int i = 16; i < 64; ++i) {
+    const uint32_t x = w[(i + 1) & 15];
+    const uint32_t y = w[(i + 14) & 15];
+    const uint32_t s0 = xor3(rotr32(x, 7), rotr32(x, 18), x >> 3);
+    const uint32_t s1 = xor3(rotr32(y, 17), rotr32(y, 19), y >> 10);
+    const uint32_t wi = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
+    w[i & 15] = wi;
+    kw[i] = wi + sha256_k(i);
+  }
+}
+
+// The 64 rounds of a compression over a precomputed K+W row.
+AHV_HD void sha256_rounds_kw(uint32_t st[8], const uint32_t* kw) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+  uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    const uint32_t t1 = h + S1 + sha_ch(e, f, g) + kw[i];
+    const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+    const uint32_t t2 = S0 + sha_maj(a, b, c);
+    h = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = t1 + t2;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// SHA-256 of `nblk` staged blocks by one wave: the lanes expand up to L.n block
+// schedules at once (one block per lane, SIMT), then the leader runs only the
+// rounds — the serial part shrinks by the schedule's third.  Without schedule
+// rows (host twin) the plain serial form.  The digest is valid on the leader.
+AHV_HD void sha256_lds_blocks_par(const Lanes& L, const uint32_t* w, int64_t nblk, uint32_t out[8]) {
+  if (L.kw == nullptr || L.n < 2) {
+    if (L.leader()) sha256_lds_blocks(w, nblk, out);
+    return;
+  }
+  if (L.leader()) sha256_init(out);
+  for (int64_t b0 = 0; b0 < nblk; b0 += L.n) {
+    const int64_t b = b0 + L.lane;
+    if (b < nblk) sha256_expand_kw(w + 16 * b, L.kw + kKwStride * L.lane);
+    L.sync();
+    if (L.leader()) {
+      const int64_t m = nblk - b0 < L.n ? nblk - b0 : L.n;
+      for (int64_t j = 0; j < m; ++j) sha256_rounds_kw(out, L.kw + kKwStride * j);
+    }
+    L.sync();
+  }
 }
 
 // ------------------------------------------------------------- session ops
@@ -1255,10 +1318,10 @@ AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, ui
   uint8_t* p = t.payload + j.off;
   const uint32_t* parent = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
   const int64_t nblk = stage_message(L, p, static_cast<uint64_t>(j.len), j.hole, parent);
-  if (!L.leader()) return;
   uint32_t h[8];
-  if (nblk >= 0) sha256_lds_blocks(L.lds, nblk, h);
-  else sha256_fine(p, static_cast<uint64_t>(j.len), h);  // record larger than the LDS window
+  if (nblk >= 0) sha256_lds_blocks_par(L, L.lds, nblk, h);  // wave-wide: schedules on all lanes
+  if (!L.leader()) return;
+  if (nblk < 0) sha256_fine(p, static_cast<uint64_t>(j.len), h);  // record larger than the LDS window
   store8(t.d_hash + 8 * j.d, h);
   store8(t.s_head + 8 * j.s, h);
   for (int k = 0; k < 8; ++k) out64(r + 2 + k, h[k]);
