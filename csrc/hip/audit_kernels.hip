@@ -84,10 +84,10 @@ void hash_many_host(const HashManyArgs& a) { for (int64_t i = 0; i < a.n; ++i) h
 namespace {
 template <class Sink>
 AHV_HD void chain_emit(Sink& s, const ChainHashArgs& a, int32_t i, bool have, const Digest& prev) {
-  emit_span_prefetch<8>(s, a.bytes + a.pre_off[i], static_cast<uint32_t>(a.pre_len[i]));
+  emit_span_prefetch<16>(s, a.bytes + a.pre_off[i], static_cast<uint32_t>(a.pre_len[i]));
   if (have) emit_hex_digest_quoted(s, prev.v);
   else emit_lit(s, canon::K_NULL);
-  emit_span_prefetch<8>(s, a.bytes + a.suf_off[i], static_cast<uint32_t>(a.suf_len[i]));
+  emit_span_prefetch<16>(s, a.bytes + a.suf_off[i], static_cast<uint32_t>(a.suf_len[i]));
 }
 
 template <class Sink>
