@@ -180,6 +180,36 @@ class GovernanceEngine:
         self._last_specs = None
         self._change_cache: dict = {}
         self._spread = SpreadCounters(6, self.device)
+        self._batches: list[PipelineBatch] = []  # host-cursor batches, newest last (for lookup)
+        self.sessions_run = 0
+
+    # -- lookup ------------------------------------------------------------------
+    def lookup(self, session_id: str) -> Optional[tuple[PipelineBatch, int]]:
+        """(batch, index) of a pipeline session by its id, or None.
+
+        One device compare over the resident ``sess_uuid`` column; the slot is
+        then attributed to the newest batch that wrote it (the session table is
+        a ring, so an overwritten session is no longer found)."""
+        if not session_id.startswith("session:"):
+            return None
+        h = session_id[len("session:"):].replace("-", "")
+        if len(h) != 32:
+            return None
+        try:
+            words = [int(h[8 * k: 8 * k + 8], 16) for k in range(4)]
+        except ValueError:
+            return None
+        w = torch.tensor(words, dtype=torch.int64).to(torch.int32).to(self.device)
+        hit = torch.nonzero((self.sessions.sess_uuid == w).all(dim=1)).flatten()
+        if hit.numel() == 0:
+            return None
+        slot = int(hit[0])
+        cap = self.sessions.capacity
+        for b in reversed(self._batches):
+            i = (slot - b.slot_base) % cap
+            if i < b.n:
+                return b, i
+        return None
 
     # -- agents ----------------------------------------------------------------
     def register_agents(self, dids: Sequence[str], sigmas) -> torch.Tensor:
@@ -292,7 +322,17 @@ class GovernanceEngine:
             self._spread.add_into(stats)
         self._next_slot = (slot_base + n) % cap
         self._id_counter = id_base + 3 * n
-        return PipelineBatch(self, slot_base, n, id_base, now, deltas, list(specs), agents)
+        self.sessions_run += n
+        batch = PipelineBatch(self, slot_base, n, id_base, now, deltas, list(specs), agents)
+        # keep only the batches whose rows can still be live (the table is a ring)
+        live, covered = [], n
+        for b in reversed(self._batches):
+            if covered >= cap:  # every row of b (and of anything older) was overwritten
+                break
+            live.append(b)
+            covered += b.n
+        self._batches = live[::-1] + [batch]
+        return batch
 
     def stage_vouches(self, slots, voucher, vouchee, bonded, expiry_us=None) -> torch.Tensor:
         """Record vouch edges of the sessions in ``slots`` (participant-local

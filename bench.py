@@ -129,7 +129,11 @@ def main() -> None:
         dev = torch.device("cpu")
     if multi:
         if dev.type == "cuda":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            # RCCL's internal streams at high priority: the collectives' workgroups are
+            # dispatched ahead of the pipeline kernel's queued waves instead of behind them
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, pg_options=opts)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
@@ -175,7 +179,7 @@ def main() -> None:
             "cur": torch.zeros(1, dtype=torch.int64, device=dev),
             "factor": torch.ones(A, dtype=torch.float64, device=dev),
             "work": None,
-            "stream": torch.cuda.Stream(dev) if dev.type == "cuda" else None,
+            "stream": torch.cuda.Stream(dev, priority=-1) if dev.type == "cuda" else None,
             "gen": torch.Generator(device=dev).manual_seed(99 + rank),
         }
         x01_bytes = A * 8
@@ -200,18 +204,21 @@ def main() -> None:
         if works[b] is not None:
             works[b].wait()
         st = bufs[b]
+        side = liab["stream"] if liab is not None else None
+        if side is not None:
+            # the liability stage reads nothing the pipeline writes: order it after
+            # the previous step only, so its kernels run beside this step's pipeline
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                liability_step()
         st.zero_()
         agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
         eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
         works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if multi else None
-        if liab is not None:
-            if liab["stream"] is not None:
-                liab["stream"].wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.stream(liab["stream"]):
-                    liability_step()
-                torch.cuda.current_stream(dev).wait_stream(liab["stream"])
-            else:
-                liability_step()
+        if side is not None:
+            torch.cuda.current_stream(dev).wait_stream(side)
+        elif liab is not None:
+            liability_step()
         return st
 
     def drain():

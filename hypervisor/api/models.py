@@ -246,6 +246,7 @@ class StatsResponse(BaseModel):
     active_sagas: int
     total_vouches: int
     event_count: int
+    batched_sessions: int = 0  # sessions run by the batched device pipeline (readable by id)
 
 
 # ------------------------------------------------- MI355X batch extension
@@ -267,3 +268,4 @@ class PipelineBatchResponse(BaseModel):
     elapsed_ms: float
     sessions_per_second: float
     sample_merkle_root: Optional[str] = None
+    sample_session_id: Optional[str] = None

@@ -120,6 +120,7 @@ async def get_stats(request: Request) -> StatsResponse:
         active_sagas=sum(len(m.saga.active_sagas) for m in sessions),
         total_vouches=len(hv.vouching.records()),
         event_count=st.bus.event_count,
+        batched_sessions=hv._device_engine.sessions_run if hv._device_engine is not None else 0,
     )
 
 
@@ -374,6 +375,7 @@ async def run_pipeline_batch(req: PipelineBatchRequest, request: Request) -> Pip
         elapsed_ms=dt * 1e3,
         sessions_per_second=req.sessions / dt if dt > 0 else 0.0,
         sample_merkle_root=batch.merkle_root_hex(0) if req.deltas > 0 else None,
+        sample_session_id=batch.session_id(0) if req.sessions > 0 else None,
     )
 
 

@@ -118,6 +118,7 @@ class Hypervisor:
         self.demote_on_slash = demote_on_slash
         self._sessions: dict[str, ManagedSession] = {}
         self._device_engine = None
+        self._batch_views: dict[str, ManagedSession] = {}
 
     # -- events --------------------------------------------------------------
     def _emit(self, etype, session_id=None, agent_did=None, **payload) -> None:
@@ -270,7 +271,26 @@ class Hypervisor:
         return root
 
     def get_session(self, session_id: str) -> Optional[ManagedSession]:
-        return self._sessions.get(session_id)
+        m = self._sessions.get(session_id)
+        if m is None and self._device_engine is not None:
+            m = self._batch_session(session_id)
+        return m
+
+    def _batch_session(self, session_id: str) -> Optional[ManagedSession]:
+        """Host view of a session the batched device pipeline ran (read back
+        from the resident session table on demand; a small LRU of views)."""
+        views = self._batch_views
+        m = views.pop(session_id, None)
+        if m is None:
+            hit = self._device_engine.lookup(session_id)
+            if hit is None:
+                return None
+            batch, i = hit
+            m = batch.materialize(i)
+        views[session_id] = m
+        while len(views) > 1024:
+            views.pop(next(iter(views)))
+        return m
 
     # -- behaviour verification --------------------------------------------------
     async def verify_behavior(

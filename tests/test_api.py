@@ -146,6 +146,31 @@ def test_pipeline_batch_endpoint_cpu(client, monkeypatch):
     assert r.status_code == 200, r.text
     body = r.json()
     assert body["completed"] == 256 and body["device"] == "cpu" and len(body["sample_merkle_root"]) == 64
+    # batched sessions are first-class: readable by id through the API and the façade
+    sid = body["sample_session_id"]
+    d = client.get(f"/api/v1/sessions/{sid}")
+    assert d.status_code == 200, d.text
+    assert d.json()["state"] == "archived" and d.json()["participant_count"] == 1
+    m = hv.get_session(sid)
+    assert m.delta_engine.verify_chain() and m.delta_engine.compute_merkle_root() == body["sample_merkle_root"]
+    assert client.get("/api/v1/stats").json()["batched_sessions"] == 256
+    assert client.get("/api/v1/sessions/session:00000000-0000-4000-8000-000000000000").status_code == 404
+
+
+def test_batch_lookup_survives_ring_reuse():
+    from agent_hypervisor_amd.models.engine import GovernanceEngine
+    from hypervisor import Hypervisor
+
+    hv = Hypervisor()
+    hv._device_engine = GovernanceEngine(device="cpu", session_capacity=64, agent_capacity=64, seed=3)
+    b1 = hv.pipeline_batch(40, now_us=1767225600000000)
+    first, last = b1.session_id(0), b1.session_id(39)
+    b2 = hv.pipeline_batch(40, now_us=1767225601000000)  # wraps: overwrites b1's first 16 rows
+    assert hv.get_session(first) is None
+    m = hv.get_session(last)
+    assert m is not None and m.delta_engine.compute_merkle_root() == b1.merkle_root_hex(39)
+    assert hv.get_session(b2.session_id(39)).sso.session_id == b2.session_id(39)
+    assert hv.get_session("not-a-session") is None
 
 
 def test_dashboard_page_and_live_summary(client):
