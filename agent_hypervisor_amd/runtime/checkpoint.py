@@ -266,6 +266,11 @@ def _session_record(m) -> dict:
         "vfs": {
             "files": dict(sso.vfs._files),
             "permissions": {k: sorted(v) for k, v in sso.vfs._permissions.items()},
+            "edits": [
+                {"path": e.path, "operation": e.operation, "agent_did": e.agent_did, "timestamp": _iso(e.timestamp),
+                 "content_hash": e.content_hash, "previous_hash": e.previous_hash}
+                for e in sso.vfs.edit_log
+            ],
         },
         "reversibility": [
             {"action_id": e.action_id, "execute_api": e.execute_api, "undo_api": e.undo_api,
@@ -318,6 +323,35 @@ def save_hypervisor(hv, d: str) -> str:
     return final
 
 
+def _restore_vfs(vfs, rec: dict) -> None:
+    from hypervisor.session.sso import VFSEdit
+
+    vfs._files = dict(rec["files"])
+    vfs._permissions = {k: set(v) for k, v in rec["permissions"].items()}
+    vfs._edit_log = [
+        VFSEdit(e["path"], e["operation"], e["agent_did"], timestamp=_dt(e["timestamp"]),
+                content_hash=e["content_hash"], previous_hash=e["previous_hash"])
+        for e in rec.get("edits", ())  # checkpoints written before round 2 carry no edit log
+    ]
+
+
+def _verify_restored(sessions: list, commitments: dict) -> None:
+    """One batched audit pass over everything restored (K10 chains, K09 roots vs
+    commitments, K11 VFS contents vs their edit log), on the GPU when the batch
+    is large enough to pay for a launch (``AHV_VERIFY_DEVICE`` overrides)."""
+    from hypervisor.audit.batch_verify import verify_audit
+
+    rep = verify_audit(sessions, commitments, device=os.environ.get("AHV_VERIFY_DEVICE") or None)
+    if rep.bad_chains:
+        raise CheckpointError(f"session {rep.bad_chains[0]}: audit chain fails verification "
+                              f"({len(rep.bad_chains)} chain(s) in total)")
+    if rep.bad_roots:
+        raise CheckpointError(f"session {rep.bad_roots[0]}: Merkle root differs from its commitment")
+    if rep.bad_files:
+        sid, path = rep.bad_files[0]
+        raise CheckpointError(f"session {sid}: VFS file {path} does not match its logged content hash")
+
+
 def _delta_from_record(rec: dict):
     from hypervisor.audit.delta import SemanticDelta, VFSChange
 
@@ -364,6 +398,7 @@ def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
         records = [r for r in records if r["session_id"] in only]
     if getattr(hv, "_store", None) is not None:
         return _load_device(hv, d, records, verify, only)
+    restored: list = []
     for r in records:
         cfg = dict(r["config"])
         cfg["consistency_mode"] = ConsistencyMode(cfg["consistency_mode"])
@@ -376,8 +411,7 @@ def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
             sso._participants[p["agent_did"]] = SessionParticipant(
                 agent_did=p["agent_did"], ring=ExecutionRing(p["ring"]), sigma_raw=p["sigma_raw"],
                 sigma_eff=p["sigma_eff"], joined_at=_dt(p["joined_at"]), is_active=p["is_active"])
-        sso.vfs._files = dict(r["vfs"]["files"])
-        sso.vfs._permissions = {k: set(v) for k, v in r["vfs"]["permissions"].items()}
+        _restore_vfs(sso.vfs, r["vfs"])
         m = ManagedSession(sso)
         for e in r["reversibility"]:
             m.reversibility.register(ActionDescriptor(
@@ -399,9 +433,8 @@ def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
             m.saga._sagas[saga.saga_id] = saga
         m.delta_engine._deltas = [_delta_from_record(x) for x in r["audit"]]
         m.delta_engine._turn_counter = r["turn_count"]
-        if verify and not m.delta_engine.verify_chain():
-            raise CheckpointError(f"session {sso.session_id}: audit chain fails verification")
         hv._sessions[sso.session_id] = m
+        restored.append(m)
     with open(os.path.join(d, "liability.json")) as f:
         for v in json.load(f):
             if only is not None and v["session_id"] not in only:
@@ -421,12 +454,8 @@ def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
                                    committed_at=_dt(c["committed_at"]), blockchain_tx_id=c["blockchain_tx_id"],
                                    committed_to=c["committed_to"])
             hv.commitment._commitments[rec.session_id] = rec
-            if verify:
-                m = hv.get_session(rec.session_id)
-                de = m.delta_engine if m is not None else None
-                complete = de is not None and de.deltas and len(de.deltas) == de.turn_count  # nothing pruned by GC
-                if complete and de.compute_merkle_root() != rec.merkle_root:
-                    raise CheckpointError(f"session {rec.session_id}: Merkle root differs from its commitment")
+    if verify:
+        _verify_restored(restored, {sid: c.merkle_root for sid, c in hv.commitment._commitments.items()})
     return hv
 
 
@@ -562,8 +591,7 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
                 compensation_method=e["compensation_method"]))
             if not e["undo_api_healthy"]:
                 m.reversibility.mark_undo_unhealthy(e["action_id"])
-        sso.vfs._files = dict(r["vfs"]["files"])
-        sso.vfs._permissions = {k: set(v) for k, v in r["vfs"]["permissions"].items()}
+        _restore_vfs(sso.vfs, r["vfs"])
         hv._sessions[sso.session_id] = m
         sess_list.append(m)
     # vouch bonds: edges in creation order, linked per liability session
@@ -603,13 +631,6 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
                 session_id=sid, merkle_root=c["merkle_root"], participant_dids=c["participant_dids"],
                 delta_count=c["delta_count"], committed_at=_dt(c["committed_at"]),
                 blockchain_tx_id=c["blockchain_tx_id"], committed_to=c["committed_to"])
-    if verify:
-        for m in sess_list:
-            de = m.delta_engine
-            if not de.verify_chain():  # K10 on the device over the restored records
-                raise CheckpointError(f"session {m.sso.session_id}: audit chain fails verification")
-            c = commits.get(m.sso.session_id)
-            complete = de.deltas and len(de.deltas) == de.turn_count
-            if c is not None and complete and de.compute_merkle_root() != c["merkle_root"]:
-                raise CheckpointError(f"session {m.sso.session_id}: Merkle root differs from its commitment")
+    if verify:  # K10/K09/K11 over every restored session in one batched pass
+        _verify_restored(sess_list, {sid: c["merkle_root"] for sid, c in commits.items()})
     return hv

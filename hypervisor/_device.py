@@ -542,6 +542,17 @@ class DeviceVouchingEngine(VouchingEngine):
             return self._store.liability_id(self._tenant, session_id)
         return self._store.liability_lookup(self._tenant, session_id)
 
+    def vouch_batch(self, requests: list, device: Optional[str] = None) -> list:
+        """The edges already live in the device table: every request is one
+        admission command to the worker (the same K05 body), queued in order."""
+        out: list = []
+        for r in requests:
+            try:
+                out.append(self.vouch(*r))
+            except VouchingError as e:
+                out.append(e)
+        return out
+
     def vouch(self, voucher_did: str, vouchee_did: str, session_id: str, voucher_sigma: float,
               bond_pct: Optional[float] = None, expiry: Optional[datetime] = None) -> DeviceVouchRecord:
         st = self._store

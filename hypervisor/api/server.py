@@ -348,6 +348,23 @@ async def get_event_stats(request: Request) -> EventStatsResponse:
     return EventStatsResponse(total_events=bus.event_count, by_type=bus.type_counts())
 
 
+# ------------------------------------------------------------- audit
+
+
+@router.get("/api/v1/audit/verify", tags=["Audit"])
+async def verify_audit(
+    request: Request,
+    session_id: Optional[list[str]] = Query(None, description="Sessions to audit (default: all)"),
+    device: Optional[str] = Query(None, description="cuda | cpu (default: GPU for large batches)"),
+) -> dict[str, Any]:
+    """Batched audit: delta chains (K10), committed roots (K09), VFS contents (K11)."""
+    hv = _state(request).hv
+    try:
+        return hv.verify_audit(session_id, device=device).to_dict()
+    except ValueError as e:
+        raise HTTPException(status_code=404, detail=str(e)) from e
+
+
 # ------------------------------------------------- MI355X batched engine
 
 

@@ -359,6 +359,21 @@ class Hypervisor:
                 return m, s
         return None, None
 
+    def verify_audit(self, session_ids: Optional[list[str]] = None, device: Optional[str] = None,
+                     checkpoints=()):
+        """Batched audit of many sessions at once: every delta chain (K10), every
+        committed Merkle root (K09), every VFS file against its edit log (K11) and
+        the goal hashes of the given ``CheckpointManager`` s (K12) — see
+        :mod:`hypervisor.audit.batch_verify`.  ``device`` defaults to the GPU for
+        large batches (and to the store's device for a device-backed hypervisor)."""
+        from hypervisor.audit.batch_verify import verify_audit
+
+        sessions = self.sessions if session_ids is None else [self._get_session(s) for s in session_ids]
+        roots = {c.session_id: c.merkle_root for c in self.commitment.all_commitments()}
+        if device is None and self._store is not None and self._store.device.type == "cuda":
+            device = str(self._store.device)
+        return verify_audit(sessions, roots, device=device, checkpoints=checkpoints)
+
     @property
     def active_sessions(self) -> list[ManagedSession]:
         return [m for m in self._sessions.values() if m.sso.state.value not in ("archived", "terminating")]

@@ -131,6 +131,107 @@ class VouchingEngine:
         self._by_session.setdefault(session_id, []).append(rec)
         return rec
 
+    def vouch_batch(self, requests: list, device: Optional[str] = None) -> list:
+        """Admit many vouch requests at once; returns, per request, the new
+        :class:`VouchRecord` or the :class:`VouchingError` that ``vouch`` would
+        have raised — exactly as if ``vouch(*req)`` were called in list order.
+
+        ``requests``: tuples ``(voucher_did, vouchee_did, session_id,
+        voucher_sigma[, bond_pct[, expiry]])``.  Sessions are independent, so
+        every session's requests are admitted in one K05 launch (adjacency
+        bit-matrix cycle closure + running per-voucher exposure, fp64 in the
+        reference's addition order) over the session's live edges.  Sessions with
+        more than 16 distinct agents, and parity mode (the reference's diamond
+        "cycles"), take the scalar path."""
+        import torch
+
+        from agent_hypervisor_amd.ops import liability as LI
+        from hypervisor._clock import to_us
+
+        reqs = [tuple(r) + (None,) * (6 - len(r)) for r in requests]
+        out: list = [None] * len(reqs)
+        now = _now()
+        by_sess: dict[str, list[int]] = {}
+        for i, r in enumerate(reqs):
+            by_sess.setdefault(r[2], []).append(i)
+        batched: list[tuple[str, list[int], list, dict]] = []
+        for sid, idx in by_sess.items():
+            live = list(self._live(sid))
+            local: dict[str, int] = {}
+            for v in live:
+                local.setdefault(v.voucher_did, len(local))
+                local.setdefault(v.vouchee_did, len(local))
+            for i in idx:
+                local.setdefault(reqs[i][0], len(local))
+                local.setdefault(reqs[i][1], len(local))
+            stale = any(reqs[i][5] is not None and reqs[i][5] < now for i in idx)  # born expired: not live later
+            if _cfg.parity_mode() or len(local) > 16 or stale:
+                for i in idx:  # scalar path, in order
+                    try:
+                        out[i] = self.vouch(*reqs[i])
+                    except VouchingError as e:
+                        out[i] = e
+                continue
+            batched.append((sid, idx, live, local))
+        if not batched:
+            return out
+        dev = torch.device(device) if device else torch.device("cpu")
+        e_off, e_vr, e_ve, e_bd, r_off, r_vr, r_ve, r_sg, r_pc = [0], [], [], [], [0], [], [], [], []
+        for sid, idx, live, local in batched:
+            for v in live:  # every edge passed is live now: active, expiry -1
+                e_vr.append(local[v.voucher_did])
+                e_ve.append(local[v.vouchee_did])
+                e_bd.append(v.bonded_amount)
+            e_off.append(len(e_vr))
+            for i in idx:
+                r = reqs[i]
+                r_vr.append(local[r[0]])
+                r_ve.append(local[r[1]])
+                r_sg.append(float(r[3]))
+                r_pc.append(self.DEFAULT_BOND_PCT if r[4] is None else float(r[4]))
+            r_off.append(len(r_vr))
+        t = lambda x, dt: torch.tensor(x, dtype=dt).to(dev)  # noqa: E731
+        u8, i32, i64, f64 = torch.uint8, torch.int32, torch.int64, torch.float64
+        E = len(e_vr)
+        vb = LI.VouchBatch(t(e_off, i32), t(e_vr, u8), t(e_ve, u8), t(e_bd, f64), torch.ones(E, dtype=u8, device=dev),
+                           torch.full((E,), -1, dtype=i64, device=dev), torch.full((E,), -1, dtype=i64, device=dev))
+        code, bonded = LI.vouch_admit(vb, t(r_off, i32), t(r_vr, u8), t(r_ve, u8), t(r_sg, f64), t(r_pc, f64),
+                                      to_us(now), self.max_exposure)
+        code, bonded = code.cpu().tolist(), bonded.cpu().tolist()
+        q = 0
+        for sid, idx, _live, _local in batched:
+            for i in idx:
+                vr, ve, _s, sig, pct, expiry = reqs[i]
+                c = code[q]
+                q += 1
+                if c == 0:
+                    p = self.DEFAULT_BOND_PCT if pct is None else pct
+                    rec = VouchRecord(vouch_id=_C.uuid4("vouch:"), voucher_did=vr, vouchee_did=ve, session_id=sid,
+                                      bonded_sigma_pct=max(0.0, min(1.0, p)), bonded_amount=bonded[q - 1],
+                                      expiry=expiry)
+                    self._vouches[rec.vouch_id] = rec
+                    self._by_session.setdefault(sid, []).append(rec)
+                    out[i] = rec
+                else:
+                    out[i] = self._admit_error(c, vr, ve, sid, sig, pct)
+        return out
+
+    def _admit_error(self, code: int, voucher_did, vouchee_did, session_id, sigma, pct) -> VouchingError:
+        """The error ``vouch`` raises for a K05 rejection code (message rebuilt on the host)."""
+        if code == 1:
+            return VouchingError("Cannot vouch for yourself")
+        if code == 2:
+            return VouchingError(f"Voucher σ ({sigma:.2f}) below minimum ({self.MIN_VOUCHER_SCORE:.2f})")
+        if code == 3:
+            return VouchingError(f"Circular vouching detected: {vouchee_did} already vouches for "
+                                 f"{voucher_did} in session {session_id}")
+        p = max(0.0, min(1.0, self.DEFAULT_BOND_PCT if pct is None else pct))
+        return VouchingError(
+            f"Voucher {voucher_did} would exceed max exposure ({self.max_exposure:.0%} of σ). "
+            f"Current: {self.get_total_exposure(voucher_did, session_id):.3f}, requested: {sigma * p:.3f}, "
+            f"limit: {sigma * self.max_exposure:.3f}"
+        )
+
     def compute_sigma_eff(
         self,
         vouchee_did: str,

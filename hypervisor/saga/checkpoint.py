@@ -96,6 +96,42 @@ class CheckpointManager:
         done = {c.step_id for c in self.get_saga_checkpoints(saga_id)}
         return [s for s in steps if s not in done]
 
+    # -- persistence / audit (K12) ----------------------------------------------
+    def verify(self, device: Optional[str] = None) -> list[str]:
+        """Ids of checkpoints whose goal hash does not match sha256(goal:step)[:16],
+        every checkpoint re-hashed in one batched K12 launch."""
+        from hypervisor.audit.batch_verify import verify_audit
+
+        return verify_audit((), device=device, checkpoints=[self]).bad_checkpoints
+
+    def export_records(self) -> list[dict]:
+        return [
+            {"checkpoint_id": c.checkpoint_id, "saga_id": c.saga_id, "step_id": c.step_id,
+             "goal_description": c.goal_description, "goal_hash": c.goal_hash,
+             "achieved_at": c.achieved_at.isoformat(), "state_snapshot": c.state_snapshot,
+             "is_valid": c.is_valid, "invalidated_reason": c.invalidated_reason}
+            for cps in self._checkpoints.values() for c in cps
+        ]
+
+    @classmethod
+    def from_records(cls, records: list[dict], verify: bool = True, device: Optional[str] = None) -> "CheckpointManager":
+        """Rebuild a manager from :meth:`export_records`; with ``verify`` every goal
+        hash is re-derived (K12) and a mismatch raises ``ValueError``."""
+        mgr = cls()
+        for r in records:
+            c = SemanticCheckpoint(
+                checkpoint_id=r["checkpoint_id"], saga_id=r["saga_id"], step_id=r["step_id"],
+                goal_description=r["goal_description"], goal_hash=r["goal_hash"],
+                achieved_at=datetime.fromisoformat(r["achieved_at"]), state_snapshot=dict(r["state_snapshot"]),
+                is_valid=r["is_valid"], invalidated_reason=r["invalidated_reason"])
+            mgr._checkpoints.setdefault(c.saga_id, []).append(c)
+            mgr._by_goal_hash[cls._key(c.saga_id, c.goal_hash)] = c
+        if verify:
+            bad = mgr.verify(device)
+            if bad:
+                raise ValueError(f"checkpoint {bad[0]}: goal hash does not match its goal ({len(bad)} bad)")
+        return mgr
+
     @property
     def total_checkpoints(self) -> int:
         return sum(len(v) for v in self._checkpoints.values())

@@ -105,6 +105,11 @@ def _worker(rank: int, world: int, port: int, store: str, q) -> None:
         dist.barrier()  # followers stay up while rank 0 builds the single-rank reference
     finally:
         dist.destroy_process_group()
+    # hard exit once the result is flushed: gloo's background threads can abort
+    # the interpreter's own teardown ("terminate called without an active exception")
+    q.close()
+    q.join_thread()
+    os._exit(0)
 
 
 @pytest.mark.parametrize("world,store", [(2, "host"), (4, "host"), (2, "cpu")])
