@@ -507,7 +507,7 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
             ("s_minsig", float(config.min_sigma_eff)), ("s_creator", st.agent_id(r["creator_did"])),
             ("s_created", us(r["created_at"])), ("s_terminated", us(r["terminated_at"])),
             ("s_pcount", len(r["participants"])), ("s_pactive", sum(1 for p in r["participants"] if p["is_active"])),
-            ("s_dcount", len(r["audit"])), ("s_released", 0), ("s_retained", 0),
+            ("s_dcount", len(r["audit"])), ("s_released", 0), ("s_retained", 0), ("s_proot_n", 0),
         ):
             put(col, s, v)
         if len(r["participants"]) > P:

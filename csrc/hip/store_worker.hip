@@ -53,13 +53,14 @@ __device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
 
 __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
                                                            uint64_t* res, uint8_t* bulk, uint64_t* alive,
-                                                           int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks) {
+                                                           int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks,
+                                                           int speculate) {
   __shared__ uint64_t inl[kInlineWords];
   __shared__ uint32_t lds1[kLdsWords];      // wave 1: capture message staging
   __shared__ uint32_t kw1[64 * kKwStride];  // wave 1: per-lane K+W schedule rows
   __shared__ uint32_t lds0[kLdsWords / 4];  // wave 0: staging for its own (rare) in-place hashing
   __shared__ HashJob jobs[kJobs];
-  __shared__ uint32_t q_head, q_done, stop, bye;
+  __shared__ uint32_t q_head, q_done, stop, bye, spec_s;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   if (threadIdx.x == 0) {
@@ -67,6 +68,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     q_done = 0;
     stop = 0;
     bye = 0;
+    spec_s = 0;  // session + 1 whose provisional Merkle root wave 1 is computing (0: none)
   }
   __syncthreads();  // the only workgroup barrier: both waves pass it once
 
@@ -89,7 +91,21 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         out64(r, j.seq + 1);
       }
       ++done;
-      if (lane == 0) lds_release(&q_done, done);
+      // Idle next?  Then compute the chain's provisional Merkle root now, so a
+      // terminate / compute_merkle_root that follows finds it ready.  `spec_s`
+      // is raised before q_done: a drained command wave sees it and, for the
+      // same session, waits for the (abortable, few-µs) tree instead of
+      // recomputing it; every other command runs alongside.
+      const bool idle = speculate && __shfl(static_cast<int>(lds_acquire(&q_head) == done), 0) != 0;  // wave-uniform
+      if (lane == 0) {
+        if (idle) lds_release(&spec_s, static_cast<uint32_t>(j.s) + 1u);
+        lds_release(&q_done, done);
+      }
+      if (idle) {
+        const int64_t n = static_cast<int64_t>(t.d_turn[j.d]);
+        merkle_provisional(L, t, j.s, j.d, n, lds1, [&] { return lds_acquire(&q_head) != done; });
+        if (lane == 0) lds_release(&spec_s, 0u);  // the s_proot rows precede this release
+      }
     }
     if (lane == 0) lds_release(&bye, 1u);
     return;
@@ -123,6 +139,10 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     c.inl = inl;
     if (needs_drain(c.op)) {
       while (lds_acquire(&q_done) != queued) __builtin_amdgcn_s_sleep(1);
+    }
+    if (c.op == OP_SESS_CLOSE || c.op == OP_DELTA_MERKLE) {  // wait for the tree in flight
+      const uint32_t want = static_cast<uint32_t>(c.a[0]) + 1u;
+      while (lds_acquire(&spec_s) == want) __builtin_amdgcn_s_sleep(1);
     }
     if (c.op == OP_DELTA_CAPTURE) {
       while (queued - lds_acquire(&q_done) >= static_cast<uint32_t>(kJobs)) __builtin_amdgcn_s_sleep(1);
@@ -164,8 +184,9 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
 // Host-callable launcher (one workgroup: command wave + hash-engine wave).
 extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64_t* ring, int64_t nslots,
                                        uint64_t* res, uint8_t* bulk, uint64_t* alive, int64_t* tail,
-                                       uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream) {
+                                       uint64_t idle_ticks, uint64_t max_ticks, int speculate,
+                                       hipStream_t stream) {
   hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(128), 0, stream, *t, ring, nslots, res, bulk,
-                     alive, tail, idle_ticks, max_ticks);
+                     alive, tail, idle_ticks, max_ticks, speculate);
   return static_cast<int>(hipGetLastError());
 }

@@ -20,6 +20,7 @@
 #include <immintrin.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -31,7 +32,7 @@ namespace py = pybind11;
 
 extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64_t* ring, int64_t nslots,
                                        uint64_t* res, uint8_t* bulk, uint64_t* alive, int64_t* tail,
-                                       uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
+                                       uint64_t idle_ticks, uint64_t max_ticks, int speculate, hipStream_t stream);
 
 namespace ahv {
 namespace host {
@@ -83,6 +84,8 @@ class Store {
       hip_check(hipDeviceSynchronize(), "store init sync");
       hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "store stream");
       idle_ticks_ = static_cast<uint64_t>(idle_us) * 100;   // s_memrealtime: 100 MHz
+      const char* sp = std::getenv("AHV_STORE_SPECULATE");  // provisional Merkle roots on the idle hash engine
+      speculate_ = (sp == nullptr || std::atoi(sp) != 0) ? 1 : 0;
       max_ticks_ = static_cast<uint64_t>(max_ms) * 100000;
     } else {
       ring_ = static_cast<uint64_t*>(std::calloc(ring_bytes / 8, 8));
@@ -180,7 +183,7 @@ class Store {
   void ensure_worker() {
     if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) != 0) return;
     __atomic_store_n(alive_, 1ull, __ATOMIC_RELEASE);
-    const int rc = ahv_store_launch_worker(&t_, ring_, nslots_, res_, bulk_, alive_, tail_, idle_ticks_, max_ticks_,
+    const int rc = ahv_store_launch_worker(&t_, ring_, nslots_, res_, bulk_, alive_, tail_, idle_ticks_, max_ticks_, speculate_,
                                            stream_);
     if (rc != 0) {
       __atomic_store_n(alive_, 0ull, __ATOMIC_RELEASE);
@@ -393,6 +396,7 @@ class Store {
   int64_t* tail_ = nullptr;
   hipStream_t stream_ = nullptr;
   uint64_t idle_ticks_ = 0, max_ticks_ = 0;
+  int speculate_ = 1;
   uint64_t next_ = 0;
   uint64_t posted_ = 0;
   uint64_t launches_ = 0;

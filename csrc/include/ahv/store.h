@@ -125,6 +125,9 @@ constexpr uint64_t JOIN_ROWS = 5;  // participant row table exhausted
   X(s_uuid, uint32_t, S4)          \
   X(s_head, uint32_t, S8)          \
   X(s_root, uint32_t, S8)          \
+  X(s_proot, uint32_t, S8)         \
+  X(s_proot_n, int32_t, S)         \
+  X(s_proot_last, int32_t, S)      \
   X(p_agent, int32_t, SP)          \
   X(p_ring, uint8_t, SP)           \
   X(p_active, uint8_t, SP)         \
@@ -491,18 +494,33 @@ AHV_HD void sha256_expand_kw(const uint32_t* blk, uint32_t* kw) {
   }
 }
 
-// The 64 rounds of a compression over a precomputed K+W row.
+// 3-input add: one v_add3_u32.  LLVM forms it in sha256_compress but not in
+// the K+W round loop below (~2.5 extra VALU per round on the single-lane,
+// issue-bound serial path), so it is spelled out there.
+AHV_HD uint32_t add3u(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return a + b + c;
+#endif
+}
+
+// The 64 rounds of a compression over a precomputed K+W row.  h + kw[i] does
+// not depend on the previous round (h is e from three rounds back), so the
+// round's critical path is Σ1 → add3 → add.
 AHV_HD void sha256_rounds_kw(uint32_t st[8], const uint32_t* kw) {
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
   uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
     const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
-    const uint32_t t1 = h + S1 + sha_ch(e, f, g) + kw[i];
+    const uint32_t t1 = add3u(h + kw[i], S1, sha_ch(e, f, g));
     const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
-    const uint32_t t2 = S0 + sha_maj(a, b, c);
+    const uint32_t na = add3u(t1, S0, sha_maj(a, b, c));
     h = g; g = f; f = e; e = d + t1;
-    d = c; c = b; b = a; a = t1 + t2;
+    d = c; c = b; b = a; a = na;
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
@@ -528,6 +546,68 @@ AHV_HD void sha256_lds_blocks_par(const Lanes& L, const uint32_t* w, int64_t nbl
     }
     L.sync();
   }
+}
+
+// Provisional Merkle root (hash-engine wave, while it would otherwise idle):
+// after the capture of delta `d` of session `s` — the chain's n-th, n ≤ 64 —
+// the root of the n leaves is computed ahead of time into s_proot, tagged with
+// (n, d).  Terminate / compute_merkle_root use it when their leaf list is
+// exactly that chain (same count, same last delta) and skip the tree.  The
+// leaves come from walking d_prev back from d; the levels run SIMT: lanes
+// 2i, 2i+1 expand the schedules of node i's two hex blocks (K+W rows), lane i
+// then runs only the rounds, plus the constant 128-byte padding block (its
+// schedule folds at compile time).  `abort()` is polled between levels (a new
+// capture is queued: its digest comes first); returns false when abandoned or
+// when the chain is not the expected one.  `lv`: 8·64 words of LDS.
+template <class Abort>
+AHV_HD bool merkle_provisional(const Lanes& L, const Tables& t, int64_t s, int64_t d, int64_t n, uint32_t* lv,
+                               const Abort& abort) {
+  if (n < 1 || n > 64 || L.kw == nullptr) return false;
+  int ok = 1;
+  if (L.leader()) {
+    int64_t k = d;
+    for (int64_t i = n - 1; i >= 0; --i) {
+      if (k < 0 || k >= t.cap.D || t.d_sess[k] != s || t.d_turn[k] != i + 1) {
+        ok = 0;
+        break;
+      }
+      load8(t.d_hash + 8 * k, lv + 8 * i);
+      k = t.d_prev[k];
+    }
+  }
+  if (!bcast(L, ok)) return false;
+  L.sync();
+  int64_t m = n;
+  while (m > 1) {
+    const int64_t half = (m + 1) / 2;
+    if (L.lane < 2 * half) {
+      const int64_t node = L.lane >> 1;
+      int64_t child = 2 * node + (L.lane & 1);
+      if (child >= m) child = 2 * node;  // odd level: the last node pairs with itself
+      uint32_t blk[16];
+      digest_to_hex_words(lv + 8 * child, blk);
+      sha256_expand_kw(blk, L.kw + kKwStride * L.lane);
+    }
+    L.sync();
+    uint32_t o[8];
+    if (L.lane < half) {
+      sha256_init(o);
+      sha256_rounds_kw(o, L.kw + kKwStride * (2 * L.lane));
+      sha256_rounds_kw(o, L.kw + kKwStride * (2 * L.lane + 1));
+      sha256_compress_pad_only(o, 128u);
+    }
+    L.sync();
+    if (L.lane < half) store8(lv + 8 * L.lane, o);
+    L.sync();
+    m = half;
+    if (m > 1 && bcast(L, abort() ? 1 : 0)) return false;
+  }
+  if (L.leader()) {
+    store8(t.s_proot + 8 * s, lv);
+    t.s_proot_last[s] = static_cast<int32_t>(d);
+    t.s_proot_n[s] = static_cast<int32_t>(n);
+  }
+  return true;
 }
 
 // ------------------------------------------------------------- session ops
@@ -557,6 +637,7 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       t.s_commit_n[s] = 0;
       t.s_released[s] = 0;
       t.s_retained[s] = 0;
+      t.s_proot_n[s] = 0;  // no provisional Merkle root (a reused slot must not inherit one)
       t.s_uuid[4 * s + 0] = static_cast<uint32_t>(c.a[7] >> 32);
       t.s_uuid[4 * s + 1] = static_cast<uint32_t>(c.a[7]);
       t.s_uuid[4 * s + 2] = static_cast<uint32_t>(c.a[8] >> 32);
@@ -1314,13 +1395,27 @@ AHV_HD bool capture_begin(const Lanes& L, const Tables& t, const Cmd& c, uint64_
 // the parent's quoted digest spliced in, then the serial SHA-256 on lane 0;
 // writes the digest row, the chain head and the result words r[1..9] (not the
 // sequence word).
+AHV_HD uint64_t engine_clock() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_s_memrealtime();  // 100 MHz
+#else
+  return 0;
+#endif
+}
+
 AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, uint64_t* r) {
+  const uint64_t c0 = engine_clock();
   uint8_t* p = t.payload + j.off;
   const uint32_t* parent = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
   const int64_t nblk = stage_message(L, p, static_cast<uint64_t>(j.len), j.hole, parent);
+  const uint64_t c1 = engine_clock();
   uint32_t h[8];
   if (nblk >= 0) sha256_lds_blocks_par(L, L.lds, nblk, h);  // wave-wide: schedules on all lanes
   if (!L.leader()) return;
+  // engine telemetry in the result slot: stage / hash ticks (10 ns) and blocks
+  out64(r + 10, c1 - c0);
+  out64(r + 11, engine_clock() - c1);
+  out64(r + 12, static_cast<uint64_t>(nblk));
   if (nblk < 0) sha256_fine(p, static_cast<uint64_t>(j.len), h);  // record larger than the LDS window
   store8(t.d_hash + 8 * j.d, h);
   store8(t.s_head + 8 * j.s, h);
@@ -1364,10 +1459,16 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
         return;
       }
       const bool want_root = n > 0 && (!close || c.a[6]);
-      if (want_root) merkle_inplace(L, lv, n);  // K09
+      // the hash engine's provisional root, when it covers exactly these leaves
+      const IndexList il = index_list(t, c, static_cast<uint64_t>(n), c.a[2]);
+      const bool have = want_root && bcast(L, L.leader() ? static_cast<int>(t.s_proot_n[s] == n &&
+                                                                            t.s_proot_last[s] == il[n - 1])
+                                                         : 0) != 0;
+      if (want_root && !have) merkle_inplace(L, lv, n);  // K09
       if (!L.leader()) return;
       uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (want_root) load8(lv, root);
+      if (have) load8(t.s_proot + 8 * s, root);
+      else if (want_root) load8(lv, root);
       for (int k = 0; k < 8; ++k) out64(r + 3 + k, root[k]);
       out64(r + 2, want_root ? 1u : 0u);
       if (close) {

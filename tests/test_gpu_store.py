@@ -16,6 +16,7 @@ from tests.test_store import (
     _run_suites,
     check_lifecycle_errors,
     check_liability_parity,
+    check_merkle_roots_track_chain,
     check_pipeline_parity,
     check_saga_compensation,
 )
@@ -25,6 +26,10 @@ pytestmark = pytest.mark.gpu
 
 def test_pipeline_parity_on_device(cuda_device):
     check_pipeline_parity("cuda")
+
+
+def test_merkle_roots_track_chain_on_device(cuda_device):
+    check_merkle_roots_track_chain("cuda")
 
 
 def test_liability_parity_on_device(cuda_device):

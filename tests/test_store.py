@@ -65,6 +65,45 @@ def check_pipeline_parity(device: str) -> None:
     asyncio.run(run())
 
 
+def check_merkle_roots_track_chain(device: str) -> None:
+    """compute_merkle_root / terminate after every capture (immediately, and after
+    the hash engine has gone idle and precomputed its provisional root), with two
+    sessions' captures interleaved and chains past the 64-leaf speculation limit:
+    every root equals the host Merkle root of the digests so far."""
+    import time
+
+    async def run():
+        hv = Hypervisor(device=device)
+        a = await hv.create_session(SessionConfig(), creator_did="did:mesh:admin")
+        b = await hv.create_session(SessionConfig(), creator_did="did:mesh:admin")
+        for m in (a, b):
+            await hv.join_session(m.sso.session_id, "did:mesh:x", sigma_raw=0.8)
+            await hv.activate_session(m.sso.session_id)
+        for i in range(70):
+            for m in (a, b) if i % 3 else (b, a):
+                m.delta_engine.capture("did:mesh:x", [VFSChange(path=f"/p{i}", operation="add", content_hash=f"c{i}")])
+            if i % 5 == 0:
+                time.sleep(0.0005)  # let the engine idle: the provisional root is ready
+            m = a if i % 2 else b
+            want = C.merkle_root([d.delta_hash for d in m.delta_engine.deltas])
+            assert m.delta_engine.compute_merkle_root() == want, (i, device)
+        for m in (a, b):
+            want = C.merkle_root([d.delta_hash for d in m.delta_engine.deltas])
+            assert await hv.terminate_session(m.sso.session_id) == want
+        for n in range(1, 6):  # short chains terminated right after the last capture
+            m = await hv.create_session(SessionConfig(), creator_did="did:mesh:admin")
+            await hv.join_session(m.sso.session_id, "did:mesh:x", sigma_raw=0.8)
+            await hv.activate_session(m.sso.session_id)
+            for i in range(n):
+                m.delta_engine.capture("did:mesh:x", [VFSChange(path=f"/q{i}", operation="add", content_hash=None)])
+            if n % 2:
+                time.sleep(0.0005)
+            want = C.merkle_root([d.delta_hash for d in m.delta_engine.deltas])
+            assert await hv.terminate_session(m.sso.session_id) == want
+
+    asyncio.run(run())
+
+
 def check_liability_parity(device: str) -> None:
     """Vouch / σ_eff / exposure / slash cascade on the store == the host engines."""
 
@@ -149,6 +188,10 @@ def check_saga_compensation(device: str) -> None:
 
 def test_pipeline_parity_cpu_twin():
     check_pipeline_parity("cpu")
+
+
+def test_merkle_roots_track_chain_cpu_twin():
+    check_merkle_roots_track_chain("cpu")
 
 
 def test_liability_parity_cpu_twin():
