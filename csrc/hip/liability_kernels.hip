@@ -321,9 +321,22 @@ __global__ __launch_bounds__(kSigmaSessions * kTile) void sigma_eff_csr_kernel(V
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * kSigmaSessions;
   const int64_t s1 = s0 + kSigmaSessions < a.sessions ? s0 + kSigmaSessions : a.sessions;
   const int64_t i = s0 * kTile + threadIdx.x;  // (session, vouchee) element
+  // Everything this thread reads that does not depend on the block's edge range
+  // is requested up front, so the σ / ω / own-range loads overlap the range
+  // lookup and the edge staging (two dependent memory round trips, not three).
+  const bool mine = i < s1 * kTile;
+  const int64_t si = mine ? i / kTile : s0;
+  double sig = 0.0, om = 0.0;
+  int32_t kb = 0, ke = 0;
+  if (mine) {
+    sig = a.sigma[i];
+    om = a.omega[si];
+    kb = a.offsets[si];
+    ke = a.offsets[si + 1];
+  }
   const int32_t e0 = a.offsets[s0], e1 = a.offsets[s1];
   if (e1 - e0 > kSigmaLdsEdges) {  // uniform per block: element form from global memory
-    if (i < s1 * kTile) sigma_eff_csr_elem(a, i);
+    if (mine) sigma_eff_csr_elem(a, i);
     return;
   }
   for (int32_t k = e0 + threadIdx.x; k < e1; k += kSigmaSessions * kTile) {
@@ -333,15 +346,14 @@ __global__ __launch_bounds__(kSigmaSessions * kTile) void sigma_eff_csr_kernel(V
     s_bd[j] = a.bonded[k];
   }
   __syncthreads();
-  if (i < s1 * kTile) {
-    const int64_t s = i / kTile;
+  if (mine) {
     const uint32_t e = static_cast<uint32_t>(i % kTile);
     double contrib = 0.0;
-    for (int32_t k = a.offsets[s] - e0; k < a.offsets[s + 1] - e0; ++k) {
+    for (int32_t k = kb - e0; k < ke - e0; ++k) {
       const int32_t j = pad_edge(k);
       if (s_ve[j] == e) contrib += s_bd[j];
     }
-    a.sigma_eff[i] = sigma_eff_combine(score_or_zero(a.sigma[i]), a.omega[s], contrib);
+    a.sigma_eff[i] = sigma_eff_combine(score_or_zero(sig), om, contrib);
   }
 }
 void launch_sigma_eff_csr(const VouchCsrArgs& a, hipStream_t st) {
@@ -716,11 +728,14 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
   const int gl0 = gw * kSlashGroup;              // first wave lane of the group
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kSlashGroupsPerBlock + g;
   if (s >= a.sessions) return;
-  if (a.target[s] >= kTile) {  // group-uniform: no slash in this session
+  // target and edge range in one memory round trip (the range is 8 bytes per
+  // session; the score row, 128 bytes, is only read for slashed sessions)
+  const uint8_t tgt = a.target[s];
+  const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
+  if (tgt >= kTile) {  // group-uniform: no slash in this session
     if (j == 0) a.clip_count[s] = 0;
     return;
   }
-  const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
   if (n > kGroupEdges) {
     if (j == 0) slash_session(a, s);
     return;
@@ -746,7 +761,7 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
   static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
   int32_t next0 = 0, end0 = 0, next1 = 0, end1 = 0;
   int sp = 0;
-  int who = a.target[s], who_depth = 0;
+  int who = tgt, who_depth = 0;
   bool pending = true;
   for (;;) {
     if (pending) {

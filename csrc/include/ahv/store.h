@@ -421,50 +421,59 @@ AHV_HD void merkle_inplace(const Lanes& L, uint32_t* lv, int64_t n) {
   }
 }
 
-// Stage `n` payload bytes at `src` (64-byte aligned) into L.lds as big-endian
-// SHA-256 message words, splice the quoted hex of `head` into a 66-byte hole at
-// byte `hole` (also written back to `src`, so the stored record is complete),
-// and append the SHA padding.  Returns the number of 64-byte blocks, or -1 when
-// the message does not fit the LDS buffer.  All lanes participate.
-AHV_HD int64_t stage_message(const Lanes& L, uint8_t* src, uint64_t n, int64_t hole, const uint32_t* head) {
+// Stage `n` payload bytes at `src` (64-byte aligned) into `w` as big-endian
+// SHA-256 message words and append the SHA padding.  Returns the number of
+// 64-byte blocks, or -1 when the message needs more than `cap` words.  All
+// lanes participate (lane-strided loads of the host-written arena).
+AHV_HD int64_t stage_words(const Lanes& L, const uint8_t* src, uint64_t n, uint32_t* w, int64_t cap) {
   const uint64_t nblk = (n + 9 + 63) / 64;
-  if (nblk * 16 > static_cast<uint64_t>(kLdsWords)) return -1;
+  if (static_cast<int64_t>(nblk * 16) > cap) return -1;
   const uint64_t nw = nblk * 16;
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
   for (uint64_t i = L.lane; i < nw; i += L.n) {
-    uint32_t w = 0;
+    uint32_t x = 0;
     const uint64_t b = 4 * i;
     if (b + 4 <= n) {
-      w = bswap32(ld32f(s32 + i));
+      x = bswap32(ld32f(s32 + i));
     } else if (b < n) {
       const uint32_t raw = bswap32(ld32f(s32 + i));
       const uint32_t keep = static_cast<uint32_t>(n - b);  // 1..3 leading bytes
-      w = raw & (0xffffffffu << (8 * (4 - keep)));
+      x = raw & (0xffffffffu << (8 * (4 - keep)));
     }
-    if (b <= n && n < b + 4) w |= 0x80u << (8 * (3 - (n - b)));  // padding marker
-    if (i == nw - 2) w |= static_cast<uint32_t>((n * 8) >> 32);
-    if (i == nw - 1) w |= static_cast<uint32_t>(n * 8);
-    L.lds[i] = w;
+    if (b <= n && n < b + 4) x |= 0x80u << (8 * (3 - (n - b)));  // padding marker
+    if (i == nw - 2) x |= static_cast<uint32_t>((n * 8) >> 32);
+    if (i == nw - 1) x |= static_cast<uint32_t>(n * 8);
+    w[i] = x;
   }
   L.sync();
-  if (hole >= 0) {
-    // 66 bytes: '"', 64 lowercase hex digits of head (big-endian word order), '"'
-    for (int k = L.lane; k < 66; k += L.n) {
-      uint32_t ch;
-      if (k == 0 || k == 65) {
-        ch = 0x22u;
-      } else {
-        const int nib = k - 1;
-        ch = hex_nibble((head[nib >> 3] >> (28 - 4 * (nib & 7))) & 15u);
-      }
-      const uint64_t b = static_cast<uint64_t>(hole) + k;
-      src[b] = static_cast<uint8_t>(ch);
-      uint8_t* lb = reinterpret_cast<uint8_t*>(L.lds);
-      lb[(b & ~uint64_t(3)) | (3 - (b & 3))] = static_cast<uint8_t>(ch);
-    }
-    L.sync();
-  }
   return static_cast<int64_t>(nblk);
+}
+
+// Splice the quoted hex of `head` ('"', 64 lowercase hex digits, '"' = 66
+// bytes) into the staged words `w` at byte `hole`, and into the arena record
+// `src` so the stored record is complete.  All lanes participate.
+AHV_HD void splice_parent(const Lanes& L, uint8_t* src, uint32_t* w, int64_t hole, const uint32_t* head) {
+  for (int k = L.lane; k < 66; k += L.n) {
+    uint32_t ch;
+    if (k == 0 || k == 65) {
+      ch = 0x22u;
+    } else {
+      const int nib = k - 1;
+      ch = hex_nibble((head[nib >> 3] >> (28 - 4 * (nib & 7))) & 15u);
+    }
+    const uint64_t b = static_cast<uint64_t>(hole) + k;
+    src[b] = static_cast<uint8_t>(ch);
+    uint8_t* lb = reinterpret_cast<uint8_t*>(w);
+    lb[(b & ~uint64_t(3)) | (3 - (b & 3))] = static_cast<uint8_t>(ch);
+  }
+  L.sync();
+}
+
+// stage_words + splice_parent into L.lds (the whole window).
+AHV_HD int64_t stage_message(const Lanes& L, uint8_t* src, uint64_t n, int64_t hole, const uint32_t* head) {
+  const int64_t nblk = stage_words(L, src, n, L.lds, kLdsWords);
+  if (nblk >= 0 && hole >= 0) splice_parent(L, src, L.lds, hole, head);
+  return nblk;
 }
 
 AHV_HD void sha256_lds_blocks(const uint32_t* w, int64_t nblk, uint32_t out[8]) {
@@ -513,10 +522,19 @@ AHV_HD uint32_t add3u(uint32_t a, uint32_t b, uint32_t c) {
 AHV_HD void sha256_rounds_kw(uint32_t st[8], const uint32_t* kw) {
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
   uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
+  // K+W words are read 8 rounds ahead through a small register ring: the LDS
+  // latency hides behind the rounds without holding all 64 words live (the
+  // worker kernel sits at the VGPR limit, where the compiler otherwise waits on
+  // every read).
+  uint32_t q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = kw[i];
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
+    const uint32_t kwi = q[i & 7];
+    if (i + 8 < 64) q[i & 7] = kw[i + 8];
     const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
-    const uint32_t t1 = add3u(h + kw[i], S1, sha_ch(e, f, g));
+    const uint32_t t1 = add3u(h + kwi, S1, sha_ch(e, f, g));
     const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
     const uint32_t na = add3u(t1, S0, sha_maj(a, b, c));
     h = g; g = f; f = e; e = d + t1;
