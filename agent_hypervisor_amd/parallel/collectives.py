@@ -233,15 +233,17 @@ def merge_slash_fixed(
     pi = pair_ids.to(torch.int32)
     pf = pair_factors.to(torch.float64)
     if _ready():
+        # one collective: the three fixed-capacity buffers travel as one byte row
         c = _comm()
         w = c.get_world_size()
-        gb = [torch.empty_like(bl) for _ in range(w)]
-        gi = [torch.empty_like(pi) for _ in range(w)]
-        gf = [torch.empty_like(pf) for _ in range(w)]
-        c.all_gather(gb, bl)
-        c.all_gather(gi, pi)
-        c.all_gather(gf, pf)
-        bl, pi, pf = torch.cat(gb), torch.cat(gi), torch.cat(gf)
+        nb, ni = bl.numel() * 4, pi.numel() * 4
+        row = torch.cat([bl.contiguous().view(torch.uint8), pi.contiguous().view(torch.uint8),
+                         pf.contiguous().view(torch.uint8)])
+        rows = [torch.empty_like(row) for _ in range(w)]
+        c.all_gather(rows, row)
+        bl = torch.cat([r[:nb] for r in rows]).view(torch.int32)
+        pi = torch.cat([r[nb:nb + ni] for r in rows]).view(torch.int32)
+        pf = torch.cat([r[nb + ni:] for r in rows]).view(torch.float64)
     if factor is None:
         factor = torch.ones_like(sigma)
     launch("x02_apply", {"npairs": int(pi.numel()), "nbl": int(bl.numel()), "floor": float(floor)},

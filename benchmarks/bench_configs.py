@@ -404,7 +404,7 @@ def config5(ctx: Ctx, args):
         # fresh storm state: the slash mutates only `active`, `released_us` and the scores
         vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, vb0.active.clone(),
                            vb0.expiry_us, vb0.released_us.clone())
-        out = LI.slash(vb, tgt, omega, scores0.clone(), 1, clip_cap=per)  # ≤ one clip per edge
+        out = LI.slash(vb, tgt, omega, scores0.clone(), 1, clip_cap=per, zero_records=False)  # ≤ 1 clip per edge
         se = LI.sigma_eff_exact(vb, out.scores, omega, 1)  # NaN (absent) reads as 0.0
         # re-chain exactly the sessions the slash touched, after it (data dependency):
         # each gets a slash delta carrying its post-slash scores, then its whole
