@@ -58,7 +58,8 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   __shared__ uint64_t inl[kInlineWords];
   __shared__ uint32_t lds1[kLdsWords];      // wave 1: capture message staging
   __shared__ uint32_t kw1[64 * kKwStride];  // wave 1: per-lane K+W schedule rows
-  __shared__ uint32_t lds0[kLdsWords / 4];  // wave 0: staging for its own (rare) in-place hashing
+  __shared__ uint32_t lds0[kLdsWords / 4];  // wave 0: staging for its own hashing (capture prefixes)
+  __shared__ uint32_t kw0[64 * kKwStride];  // wave 0: K+W schedule rows
   __shared__ HashJob jobs[kJobs];
   __shared__ uint32_t q_head, q_done, stop, bye, spec_s;
   const int wave = threadIdx.x >> 6;
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       // is raised before q_done: a drained command wave sees it and, for the
       // same session, waits for the (abortable, few-µs) tree instead of
       // recomputing it; every other command runs alongside.
-      const bool idle = speculate && __shfl(static_cast<int>(lds_acquire(&q_head) == done), 0) != 0;  // wave-uniform
+      const bool idle = (speculate & 1) && __shfl(static_cast<int>(lds_acquire(&q_head) == done), 0) != 0;  // wave-uniform
       if (lane == 0) {
         if (idle) lds_release(&spec_s, static_cast<uint32_t>(j.s) + 1u);
         lds_release(&q_done, done);
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   }
 
   // ------------------------------------------------------------ command wave
-  const Lanes L{lane, 64, lds0};
+  const Lanes L{lane, 64, lds0, kw0};
   uint64_t next = static_cast<uint64_t>(__hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
   uint32_t queued = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -154,6 +155,24 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     if (c.op == OP_FLUSH) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     L.sync();
     if (rc == EXEC_DEFERRED) {
+      // A capture with a parent: while the hash engine works through the queue,
+      // compress the record's blocks that precede the parent hole here — unless
+      // the next command is already waiting (then wave 1 does all of it).
+      const int64_t jhole = bcast(L, job.hole);
+      if ((speculate & 2) && jhole >= 64 && lds_acquire(&q_done) != queued) {
+        const uint64_t* nslot = ring + ((next + 1) % static_cast<uint64_t>(nslots)) * kSlotWords;
+        if (__shfl(ld_sys(nslot + lane), 0) != next + 2) {
+          HashJob jb;
+          jb.off = bcast(L, job.off);
+          jb.hole = jhole;
+          uint32_t mid[8];
+          const int32_t pb = capture_prefix(L, t, jb, lds0, kLdsWords / 4, 4, mid);
+          if (lane == 0 && pb > 0) {
+            job.mid_blocks = pb;
+            for (int k = 0; k < 8; ++k) job.mid[k] = mid[k];
+          }
+        }
+      }
       if (lane == 0) {
         jobs[queued % kJobs] = job;
         lds_release(&q_head, queued + 1);  // the capture's global row writes precede this release

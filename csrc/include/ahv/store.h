@@ -210,7 +210,9 @@ struct Lanes {
 struct HashJob {
   uint64_t seq;
   int64_t s, d, off, len, hole;
-  int64_t prev;  // parent delta index (-1 for turn 1)
+  int64_t prev;        // parent delta index (-1 for turn 1)
+  int32_t mid_blocks;  // leading blocks already compressed into `mid` (0: none)
+  uint32_t mid[8];     // SHA-256 state after those blocks (they precede the parent hole)
 };
 
 enum ExecResult : int { EXEC_STOP = 0, EXEC_DONE = 1, EXEC_DEFERRED = 2 };
@@ -548,12 +550,27 @@ AHV_HD void sha256_rounds_kw(uint32_t st[8], const uint32_t* kw) {
 // schedules at once (one block per lane, SIMT), then the leader runs only the
 // rounds — the serial part shrinks by the schedule's third.  Without schedule
 // rows (host twin) the plain serial form.  The digest is valid on the leader.
-AHV_HD void sha256_lds_blocks_par(const Lanes& L, const uint32_t* w, int64_t nblk, uint32_t out[8]) {
+// With `from` the compression resumes from that state (blocks `w` follow it).
+AHV_HD void sha256_lds_blocks_par(const Lanes& L, const uint32_t* w, int64_t nblk, uint32_t out[8],
+                                  const uint32_t* from = nullptr) {
   if (L.kw == nullptr || L.n < 2) {
-    if (L.leader()) sha256_lds_blocks(w, nblk, out);
+    if (L.leader()) {
+      if (from) {
+        for (int k = 0; k < 8; ++k) out[k] = from[k];
+        for (int64_t b = 0; b < nblk; ++b) sha256_compress(out, w + 16 * b);
+      } else {
+        sha256_lds_blocks(w, nblk, out);
+      }
+    }
     return;
   }
-  if (L.leader()) sha256_init(out);
+  if (L.leader()) {
+    if (from) {
+      for (int k = 0; k < 8; ++k) out[k] = from[k];
+    } else {
+      sha256_init(out);
+    }
+  }
   for (int64_t b0 = 0; b0 < nblk; b0 += L.n) {
     const int64_t b = b0 + L.lane;
     if (b < nblk) sha256_expand_kw(w + 16 * b, L.kw + kKwStride * L.lane);
@@ -564,6 +581,25 @@ AHV_HD void sha256_lds_blocks_par(const Lanes& L, const uint32_t* w, int64_t nbl
     }
     L.sync();
   }
+}
+
+// Midstate of the blocks of a captured record that lie entirely before its
+// `"parent_hash": ` hole — they do not depend on the parent digest (sort_keys
+// puts agent_did, changes and delta_id first), so the command
+// wave compresses them while the hash engine is still busy with the parent.
+// At most `max_blocks`; returns the count (0: nothing to do).  Valid on the leader.
+AHV_HD int32_t capture_prefix(const Lanes& L, const Tables& t, const HashJob& j, uint32_t* w, int64_t cap_words,
+                              int32_t max_blocks, uint32_t mid[8]) {
+  if (j.hole < 64) return 0;
+  int64_t pb = j.hole / 64;
+  if (pb > max_blocks) pb = max_blocks;
+  if (pb * 16 > cap_words) return 0;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(t.payload + j.off);
+  for (int64_t i = L.lane; i < pb * 16; i += L.n) w[i] = bswap32(ld32f(s32 + i));
+  L.sync();
+  sha256_lds_blocks_par(L, w, pb, mid);
+  L.sync();
+  return static_cast<int32_t>(pb);
 }
 
 // Provisional Merkle root (hash-engine wave, while it would otherwise idle):
@@ -1428,7 +1464,9 @@ AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, ui
   const int64_t nblk = stage_message(L, p, static_cast<uint64_t>(j.len), j.hole, parent);
   const uint64_t c1 = engine_clock();
   uint32_t h[8];
-  if (nblk >= 0) sha256_lds_blocks_par(L, L.lds, nblk, h);  // wave-wide: schedules on all lanes
+  // blocks before the parent hole may already be compressed (by the command wave)
+  const int64_t skip = nblk >= 0 && j.mid_blocks > 0 && j.mid_blocks < nblk ? j.mid_blocks : 0;
+  if (nblk >= 0) sha256_lds_blocks_par(L, L.lds + 16 * skip, nblk - skip, h, skip ? j.mid : nullptr);
   if (!L.leader()) return;
   // engine telemetry in the result slot: stage / hash ticks (10 ns) and blocks
   out64(r + 10, c1 - c0);
@@ -1622,7 +1660,10 @@ AHV_HD int store_exec(const Lanes& L, const Tables& t, const Cmd& c, uint64_t se
     const bool ok = bcast(L, capture_begin(L, t, c, seq, r, j) ? 1 : 0) != 0;
     if (!ok) return EXEC_DONE;
     if (defer) {
-      if (L.leader()) *defer = j;
+      if (L.leader()) {
+        j.mid_blocks = 0;
+        *defer = j;
+      }
       return EXEC_DEFERRED;
     }
     // host twin / single-wave: hash now (all lanes need the job)
@@ -1634,6 +1675,7 @@ AHV_HD int store_exec(const Lanes& L, const Tables& t, const Cmd& c, uint64_t se
     jb.len = bcast(L, j.len);
     jb.hole = bcast(L, j.hole);
     jb.prev = bcast(L, j.prev);
+    jb.mid_blocks = 0;
     capture_finish(L, t, jb, r);
     return EXEC_DONE;
   }
