@@ -118,7 +118,7 @@ class Hypervisor:
         self.demote_on_slash = demote_on_slash
         self._sessions: dict[str, ManagedSession] = {}
         self._device_engine = None
-        self._batch_views: dict[str, ManagedSession] = {}
+        self._batch_views: dict = {}  # session id → (batch, host view), a small LRU
 
     # -- events --------------------------------------------------------------
     def _emit(self, etype, session_id=None, agent_did=None, **payload) -> None:
@@ -279,15 +279,15 @@ class Hypervisor:
     def _batch_session(self, session_id: str) -> Optional[ManagedSession]:
         """Host view of a session the batched device pipeline ran (read back
         from the resident session table on demand; a small LRU of views)."""
+        hit = self._device_engine.lookup(session_id)  # the row may have been reused since
+        if hit is None:
+            self._batch_views.pop(session_id, None)
+            return None
+        batch, i = hit
         views = self._batch_views
-        m = views.pop(session_id, None)
-        if m is None:
-            hit = self._device_engine.lookup(session_id)
-            if hit is None:
-                return None
-            batch, i = hit
-            m = batch.materialize(i)
-        views[session_id] = m
+        cached = views.pop(session_id, None)
+        m = cached[1] if cached is not None and cached[0] is batch else batch.materialize(i)
+        views[session_id] = (batch, m)
         while len(views) > 1024:
             views.pop(next(iter(views)))
         return m
