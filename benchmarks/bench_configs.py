@@ -412,7 +412,7 @@ def config5(ctx: Ctx, args):
         touched = torch.nonzero(out.clip_count > 0).flatten()
         arena.write_slash_deltas(touched, out.scores[touched])
         packed = arena.packed(touched)
-        digests = A.chain_hashes(packed)
+        digests = A.chain_hashes(packed, midstate=not args.no_midstate)
         roots = A.merkle_roots(packed["chain_offsets"], digests)
         last.update(T=touched.numel(), roots=roots)
         return se
@@ -442,6 +442,7 @@ def main():
     ap.add_argument("--deltas", type=int, default=0)
     ap.add_argument("--storm-fraction", type=float, default=0.1, help="config5: share of sessions slashed")
     ap.add_argument("--coroutine-sagas", type=int, default=4096, help="config4: sagas in the coroutine mode")
+    ap.add_argument("--no-midstate", action="store_true", help="config5: single-phase K08 re-chain (A/B)")
     ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
     ap.add_argument("--owner-reduce", action="store_true", help="config3: reduce-scatter exposure to agent owners")
     args = ap.parse_args()

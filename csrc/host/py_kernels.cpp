@@ -258,6 +258,8 @@ static ChainHashArgs to_chain_hash(const py::dict& d) {
   V(chains, int64_t); P(chain_offsets, const int32_t); P(bytes, const uint8_t); P(pre_off, const int64_t);
   P(pre_len, const int32_t); P(suf_off, const int64_t); P(suf_len, const int32_t);
   P(seed_parent, const uint32_t); P(has_seed, const uint8_t); P(digest, uint32_t);
+  a.mid = d.contains("mid") ? ptr<uint32_t>(d, "mid") : nullptr;
+  a.deltas = d.contains("deltas") ? d["deltas"].cast<int64_t>() : 0;
   return a;
 }
 static SagaBatchArgs to_saga(const py::dict& d) {

@@ -96,6 +96,16 @@ struct HostSink {
   AHV_HD void hash_mid(Emit&& emit, uint32_t out[8], Mid&, int) {
     hash(emit, out);
   }
+  // Resume from a midstate taken after `base_bytes` (multiple of 64) that the
+  // emitter does not replay (see WordWindowSink::hash_from).
+  template <class Emit>
+  AHV_HD void hash_from(Emit&& emit, const uint32_t st_in[8], uint32_t base_bytes, uint32_t out[8]) {
+    h.init();
+    for (int k = 0; k < 8; ++k) h.st[k] = st_in[k];
+    h.total = base_bytes;
+    emit(*this);
+    h.final(out);
+  }
   AHV_HD void stash(int j, const uint32_t d[8]) {
     for (int k = 0; k < 8; ++k) scratch[j][k] = d[k];
   }

@@ -344,6 +344,10 @@ struct ChainHashArgs {
   const uint32_t* seed_parent;   // [chains, 8] or null
   const uint8_t* has_seed;       // [chains] or null
   uint32_t* digest;              // [D, 8] out
+  // K08 midstate split (null = single phase): [D, 8] scratch for the state after
+  // each delta's whole prefix blocks, computed in parallel over all `deltas`.
+  uint32_t* mid;
+  int64_t deltas;
 };
 void launch_chain_hash(const ChainHashArgs&, hipStream_t);
 void chain_hash_host(const ChainHashArgs&);

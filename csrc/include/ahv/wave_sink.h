@@ -134,6 +134,26 @@ struct WordWindowSink {
       sha256_init(st);
       lo = 0;
     }
+    run(emit, st, 0u, out, mid, mode);
+  }
+
+  // Resume from an arbitrary midstate `st_in` taken after `base_bytes` (a
+  // multiple of 64, per lane) of message that the emitter does NOT replay: the
+  // emitter produces only the remaining bytes; the bit length counts both.
+  template <class Emit>
+  __device__ __forceinline__ void hash_from(Emit&& emit, const uint32_t st_in[8], uint32_t base_bytes,
+                                            uint32_t out[8]) {
+    uint32_t st[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st[k] = st_in[k];
+    lo = 0;
+    Digest unused;
+    run(emit, st, base_bytes, out, unused, MID_OFF);
+  }
+
+  template <class Emit>
+  __device__ __forceinline__ void run(Emit&& emit, uint32_t st[8], uint32_t base_bytes, uint32_t out[8],
+                                      Digest& mid, int mode) {
     int32_t total = 0;  // padded length in words, known after the first pass
     bool first = true;
     while (first || __any(lo < total)) {
@@ -150,7 +170,7 @@ struct WordWindowSink {
       // supplies the zero bytes up to the length words)
       put(0x80000000u, 1);
       store_at(sh ? addr : trash, __builtin_amdgcn_alignbit(prev, 0u, sh));
-      const uint64_t bits = static_cast<uint64_t>(L) * 8u;
+      const uint64_t bits = (static_cast<uint64_t>(L) + base_bytes) * 8u;
       store(total - 2 - lo, static_cast<uint32_t>(bits >> 32));
       store(total - 1 - lo, static_cast<uint32_t>(bits));
 #pragma nounroll

@@ -254,6 +254,8 @@ def test_audit_kernels(cuda_device):
     hc = A.chain_hashes(packed)
     hd = A.chain_hashes({k: v.cuda() for k, v in packed.items()})
     assert torch.equal(hc, hd.cpu())
+    hs = A.chain_hashes({k: v.cuda() for k, v in packed.items()}, midstate=False)
+    assert torch.equal(hc, hs.cpu())
     assert A.digests_to_hex(hc) == [d.delta_hash for c in chains for d in c]
     d, o = A.pack_bytes(pays)
     _check(lambda *t: A.verify_chains(*t), d, o, A.hex_to_digests(hexes), A.hex_to_digests(parent),

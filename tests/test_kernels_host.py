@@ -266,6 +266,28 @@ def test_chain_hashes_rederive_delta_engine_chains():
     assert A.digests_to_hex(got2) == [d.delta_hash for t in tails for d in t]
 
 
+def test_chain_hashes_midstate_split_every_prefix_length():
+    """K08 midstate split: prefixes of 2-6 whole blocks at every arena alignment give
+    the same digests as the single-phase pass and the scalar DeltaEngine."""
+    from hypervisor.audit.delta import DeltaEngine, VFSChange
+
+    rng = random.Random(5)
+    chains = []
+    for s in range(40):
+        de = DeltaEngine(f"session:{s}")
+        for t in range(rng.randint(1, 5)):
+            did = "did:" + "x" * rng.randint(1, 200)  # prefixes of 2-6 whole blocks, odd offsets
+            de.capture(did, [VFSChange(f"/p{t}", "add", "h" * rng.randint(0, 90))])
+        chains.append(de.deltas)
+    packed = A.pack_chains(chains)
+    want = [d.delta_hash for c in chains for d in c]
+    assert {int(x) % 4 for x in packed["pre_off"]} == {0, 1, 2, 3}
+    assert len({int(x) // 64 for x in packed["pre_len"]}) >= 4
+    split = A.chain_hashes(packed)
+    assert torch.equal(split, A.chain_hashes(packed, midstate=False))
+    assert A.digests_to_hex(split) == want
+
+
 def test_merkle_roots_match_delta_engine():
     engines = _delta_engines()
     leaves, offs = [], [0]
