@@ -10,6 +10,7 @@ local index, and its vouch edges in creation order as CSR arrays
 from __future__ import annotations
 
 from dataclasses import dataclass
+from typing import Optional
 
 import torch
 
@@ -165,6 +166,7 @@ class SlashOutcome:
     clip_depth: torch.Tensor  # u8 [S, cap]
     clip_before: torch.Tensor  # f64 [S, cap]
     clip_after: torch.Tensor  # f64 [S, cap]
+    sigma_eff: Optional[torch.Tensor] = None  # f64 [S,16] post-slash σ_eff (fused K03), or None
 
     @property
     def truncated(self) -> torch.Tensor:
@@ -180,6 +182,7 @@ def slash(
     now_us: int,
     clip_cap: int = 64,
     zero_records: bool = True,
+    with_sigma_eff: bool = False,
 ) -> SlashOutcome:
     """K06: slash ``target[s]`` in every session (cascade ≤ 2), mutating ``vb``
     (bonds released) and ``scores`` in place, like SlashingEngine.slash.  A
@@ -192,7 +195,12 @@ def slash(
 
     ``zero_records=False`` leaves record slots past ``clip_count[s]`` undefined
     instead of zero-filling S × clip_cap records first (18 bytes each: 180 MB
-    for a 625 k-session storm with cap 16 — more HBM traffic than the slash)."""
+    for a 625 k-session storm with cap 16 — more HBM traffic than the slash).
+
+    ``with_sigma_eff=True`` fuses K03 into the same pass: :attr:`SlashOutcome.sigma_eff`
+    is then every session's σ_eff over its post-slash live bonds with risk weight
+    ``omega`` — equal, bit for bit, to ``sigma_eff_exact(vb, scores, omega, now_us)``
+    run after the slash — without a second read of the bond graph."""
     S = vb.sessions
     dev = vb.device
     offs = (torch.arange(S, dtype=i32, device=dev) * clip_cap).contiguous()
@@ -205,6 +213,10 @@ def slash(
         clip_before=alloc((S, clip_cap), dtype=f64, device=dev),
         clip_after=alloc((S, clip_cap), dtype=f64, device=dev),
     )
+    fused = {}
+    if with_sigma_eff:
+        out.sigma_eff = torch.empty((S, TILE), dtype=f64, device=dev)
+        fused = dict(bonded=vb.bonded, sigma_eff=out.sigma_eff)
     launch(
         "slash",
         {"sessions": S, "now_us": int(now_us), "clip_cap": int(clip_cap)},
@@ -212,8 +224,8 @@ def slash(
              expiry_us=vb.expiry_us, released_us=vb.released_us, target=target, omega=omega, scores=scores,
              clip_offsets=offs, clip_count=out.clip_count, clip_voucher=out.clip_voucher,
              clip_depth=out.clip_depth, clip_before=out.clip_before, clip_after=out.clip_after,
-             clip_walk=torch.empty(max(int(vb.voucher.numel()), 1), dtype=u8, device=dev)),
-        dict(target=u8, omega=f64, scores=f64),
+             clip_walk=torch.empty(max(int(vb.voucher.numel()), 1), dtype=u8, device=dev), **fused),
+        dict(target=u8, omega=f64, scores=f64, bonded=f64),
     )
     return out
 

@@ -404,8 +404,10 @@ def config5(ctx: Ctx, args):
         # fresh storm state: the slash mutates only `active`, `released_us` and the scores
         vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, vb0.active.clone(),
                            vb0.expiry_us, vb0.released_us.clone())
-        out = LI.slash(vb, tgt, omega, scores0.clone(), 1, clip_cap=per, zero_records=False)  # ≤ 1 clip per edge
-        se = LI.sigma_eff_exact(vb, out.scores, omega, 1)  # NaN (absent) reads as 0.0
+        # ≤ 1 clip per edge; σ_eff over the post-slash bonds fused into the same pass (K06+K03)
+        out = LI.slash(vb, tgt, omega, scores0.clone(), 1, clip_cap=per, zero_records=False,
+                       with_sigma_eff=not args.unfused)
+        se = out.sigma_eff if not args.unfused else LI.sigma_eff_exact(vb, out.scores, omega, 1)
         # re-chain exactly the sessions the slash touched, after it (data dependency):
         # each gets a slash delta carrying its post-slash scores, then its whole
         # chain is re-hashed (K08) and its Merkle root recomputed (K09)
@@ -442,6 +444,7 @@ def main():
     ap.add_argument("--deltas", type=int, default=0)
     ap.add_argument("--storm-fraction", type=float, default=0.1, help="config5: share of sessions slashed")
     ap.add_argument("--coroutine-sagas", type=int, default=4096, help="config4: sagas in the coroutine mode")
+    ap.add_argument("--unfused", action="store_true", help="config5: separate slash and sigma_eff passes (A/B)")
     ap.add_argument("--no-midstate", action="store_true", help="config5: single-phase K08 re-chain (A/B)")
     ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
     ap.add_argument("--owner-reduce", action="store_true", help="config3: reduce-scatter exposure to agent owners")

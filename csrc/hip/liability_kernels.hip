@@ -633,6 +633,18 @@ AHV_HD void slash_session(const SlashArgs& a, int64_t s) {
   slash_session_t(a, s, GlobalEdges{&a}, a.scores + s * kTile, 1);
 }
 
+// Fused K03 tail: σ_eff of vouchee j of session s over the post-slash live bonds
+// (creation order — the sigma_eff_csr_elem sum).
+AHV_HD double slash_sigma_eff(const SlashArgs& a, int64_t s, int j) {
+  double contrib = 0.0;
+  for (int32_t k = a.offsets[s]; k < a.offsets[s + 1]; ++k)
+    if (a.vouchee[k] == j && live_edge(a.active, a.expiry_us, k, a.now_us)) contrib += a.bonded[k];
+  return sigma_eff_combine(score_or_zero(a.scores[s * kTile + j]), a.omega[s], contrib);
+}
+AHV_HD void slash_sigma_row(const SlashArgs& a, int64_t s) {
+  for (int j = 0; j < kTile; ++j) a.sigma_eff[s * kTile + j] = slash_sigma_eff(a, s, j);
+}
+
 // Device: a workgroup of 64 sessions stages its contiguous edge range
 // (voucher, vouchee, live) and its 64×16 score rows in LDS with coalesced loads,
 // runs the cascades out of LDS (one lane per session), and writes the scores
@@ -705,6 +717,12 @@ __global__ __launch_bounds__(64) void slash_kernel(SlashArgs a) {
   for (int64_t j = threadIdx.x; j < nsc; j += 64) a.scores[s0 * kTile + j] = s_sc[(j / kTile) * kScorePad + j % kTile];
 }
 
+// σ_eff tail of the per-lane form (AHV_SLASH_PER_LANE), one thread per (session, vouchee).
+__global__ void slash_sigma_kernel(SlashArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.sessions * kTile) a.sigma_eff[i] = slash_sigma_eff(a, i / kTile, static_cast<int>(i % kTile));
+}
+
 // Group-cooperative form: 16 lanes per session (4 sessions per wave, 16 per
 // 256-thread block).  Lane j holds edges j, j+16, j+32, j+48 of its session in
 // registers (voucher, vouchee, live) and the session's score σ[j]; "which live
@@ -720,6 +738,29 @@ constexpr int kGroupChunks = 4;
 constexpr int kGroupEdges = kSlashGroup * kGroupChunks;  // 64
 constexpr int kSlashGroupsPerBlock = 16;
 
+// σ_eff of the lane's vouchee j over the group's live edges, summed in edge
+// (= creation) order: edge c·16 + k sits in lane k of chunk c; its vouchee (−1
+// when dead) and bond arrive by lane shuffle, so all 16 lanes walk the same
+// sequence and each adds the bonds of its own vouchee — the additions, in the
+// order, of sigma_eff_csr_elem.
+__device__ __forceinline__ double group_sigma_eff(const int (&ve)[kGroupChunks], const bool (&lv)[kGroupChunks],
+                                                  const double (&bd)[kGroupChunks], int32_t n, int j, int gl0,
+                                                  double sc, double omega) {
+  double contrib = 0.0;
+#pragma unroll
+  for (int c = 0; c < kGroupChunks; ++c) {
+    if (!__any(c * kSlashGroup < n)) break;
+    const int vk_own = lv[c] ? ve[c] : -1;
+#pragma unroll
+    for (int k = 0; k < kSlashGroup; ++k) {
+      const int vk = __shfl(vk_own, gl0 + k, kWaveLanes);
+      const double bk = __shfl(bd[c], gl0 + k, kWaveLanes);
+      if (vk == j) contrib += bk;
+    }
+  }
+  return sigma_eff_combine(score_or_zero(sc), omega, contrib);
+}
+
 __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_group_kernel(SlashArgs a) {
   __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
   const int g = threadIdx.x / kSlashGroup;       // group in block
@@ -732,12 +773,16 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
   // session; the score row, 128 bytes, is only read for slashed sessions)
   const uint8_t tgt = a.target[s];
   const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
-  if (tgt >= kTile) {  // group-uniform: no slash in this session
+  const bool fused = a.sigma_eff != nullptr;
+  if (tgt >= kTile && !fused) {  // group-uniform: no slash in this session
     if (j == 0) a.clip_count[s] = 0;
     return;
   }
   if (n > kGroupEdges) {
-    if (j == 0) slash_session(a, s);
+    if (j == 0) {
+      slash_session(a, s);
+      if (fused) slash_sigma_row(a, s);
+    }
     return;
   }
   auto group_bits = [&](bool p) -> uint32_t {
@@ -745,16 +790,23 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
   };
   int vr[kGroupChunks], ve[kGroupChunks];
   bool lv[kGroupChunks];
+  double bd[kGroupChunks];
 #pragma unroll
   for (int c = 0; c < kGroupChunks; ++c) {
     const int32_t i = c * kSlashGroup + j;
     const bool in = i < n;
-    vr[c] = in ? a.voucher[b + i] : 0;
+    vr[c] = in && tgt < kTile ? a.voucher[b + i] : 0;
     ve[c] = in ? a.vouchee[b + i] : -1;
     lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
+    bd[c] = in && fused ? a.bonded[b + i] : 0.0;
   }
   double sc = a.scores[s * kTile + j];
   const double omega = a.omega[s];
+  if (tgt >= kTile) {  // fused, no slash here: σ_eff only
+    if (j == 0) a.clip_count[s] = 0;
+    a.sigma_eff[s * kTile + j] = group_sigma_eff(ve, lv, bd, n, j, gl0, sc, omega);
+    return;
+  }
   const int32_t base = a.clip_offsets[s];
   uint8_t* cl = s_cl[g];
   int32_t nclip = 0;
@@ -829,6 +881,7 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
   }
   a.scores[s * kTile + j] = sc;
   if (j == 0) a.clip_count[s] = nclip;
+  if (fused) a.sigma_eff[s * kTile + j] = group_sigma_eff(ve, lv, bd, n, j, gl0, sc, omega);
 }
 
 void launch_slash(const SlashArgs& a, hipStream_t st) {
@@ -837,13 +890,21 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
     const char* e = std::getenv("AHV_SLASH_PER_LANE");
     return e && std::atoi(e) == 1;
   }();
-  if (per_lane) hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
-  else
+  if (per_lane) {
+    hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
+    if (a.sigma_eff) hipLaunchKernelGGL(slash_sigma_kernel, grid1(a.sessions * kTile), dim3(kBlock), 0, st, a);
+  } else {
     hipLaunchKernelGGL(slash_group_kernel, grid1(a.sessions, kSlashGroupsPerBlock),
                        dim3(kSlashGroup * kSlashGroupsPerBlock), 0, st, a);
+  }
   check_hip(hipGetLastError(), "slash_kernel");
 }
-void slash_host(const SlashArgs& a) { for (int64_t s = 0; s < a.sessions; ++s) slash_session(a, s); }
+void slash_host(const SlashArgs& a) {
+  for (int64_t s = 0; s < a.sessions; ++s) {
+    slash_session(a, s);
+    if (a.sigma_eff) slash_sigma_row(a, s);
+  }
+}
 
 
 void kernels_liability(std::vector<KernelEntry>& out) {

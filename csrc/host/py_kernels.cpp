@@ -220,6 +220,8 @@ static SlashArgs to_slash(const py::dict& d) {
   P(target, const uint8_t); P(omega, const double); P(scores, double); P(clip_offsets, int32_t);
   P(clip_count, int32_t); P(clip_voucher, uint8_t); P(clip_depth, uint8_t); P(clip_before, double);
   P(clip_after, double); V(clip_cap, int32_t); P(clip_walk, uint8_t);
+  a.bonded = d.contains("bonded") ? ptr<const double>(d, "bonded") : nullptr;
+  a.sigma_eff = d.contains("sigma_eff") ? ptr<double>(d, "sigma_eff") : nullptr;
   return a;
 }
 static HashManyArgs to_hash_many(const py::dict& d) {

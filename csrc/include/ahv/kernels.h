@@ -285,6 +285,10 @@ struct SlashArgs {
   int32_t clip_cap;         // records per session (records beyond it are dropped, not the cascade)
   uint8_t* clip_walk;       // [E] scratch: the cascade walk's (voucher | cascade<<7) per clip, uncapped —
                             // a session has at most (its edge count) clips, indexed from its first edge
+  // Fused K03 (null = slash only): σ_eff of every session over its post-slash live
+  // bonds, in the same pass — bit-identical to slash followed by sigma_eff_csr.
+  const double* bonded;     // [E]
+  double* sigma_eff;        // [S,16] out
 };
 void launch_slash(const SlashArgs&, hipStream_t);
 void slash_host(const SlashArgs&);

@@ -201,6 +201,18 @@ def test_liability_kernels_large_sessions(cuda_device):
     tgt2[::3] = 255
     _check(lambda *t: LI.slash(mk(*t[:-3]), t[-3], t[-2], t[-1], 100), *[getattr(vb, f) for f in fields],
            tgt2, omega, scores)
+    # fused K06+K03 (σ_eff in the slash pass): device == host twin == unfused, bit for bit,
+    # across the 16-lane group form, the > 64-edge fallback and untouched sessions
+    vd = vb.to("cuda")
+    fd = LI.slash(vd, tgt2.cuda(), omega.cuda(), scores.cuda(), 100, with_sigma_eff=True)
+    vh = LI.VouchBatch(*[getattr(vb, f).clone() for f in fields])
+    fh = LI.slash(vh, tgt2, omega, scores.clone(), 100, with_sigma_eff=True)
+    vs = LI.VouchBatch(*[getattr(vb, f).clone() for f in fields])
+    sh = LI.slash(vs, tgt2, omega, scores.clone(), 100)
+    assert torch.equal(fh.sigma_eff, LI.sigma_eff_exact(vs, sh.scores, omega, 100))
+    assert torch.equal(fd.sigma_eff.cpu(), fh.sigma_eff)
+    torch.testing.assert_close(fd.scores.cpu(), fh.scores, rtol=0, atol=0, equal_nan=True)  # NaN = absent
+    assert torch.equal(vd.active.cpu(), vh.active)
     # admission past the 1024-edge LDS stage (global-memory fallback) mixed with staged blocks
     rng = random.Random(9)
     r_off, rv, re_, rs, rp = [0], [], [], [], []
@@ -256,6 +268,18 @@ def test_audit_kernels(cuda_device):
     assert torch.equal(hc, hd.cpu())
     hs = A.chain_hashes({k: v.cuda() for k, v in packed.items()}, midstate=False)
     assert torch.equal(hc, hs.cpu())
+    # midstate split with prefixes of 2-8 whole blocks (more than one 4-block LDS
+    # staging round) at every byte alignment of the arena
+    long_chains = []
+    for s in range(700):
+        de = DeltaEngine(f"session:{s}")
+        for t in range(rng.randint(1, 6)):
+            de.capture("did:" + "x" * rng.randint(1, 330), [VFSChange(f"/p{t}", "add", "h" * rng.randint(0, 90))])
+        long_chains.append(de.deltas)
+    lp = A.pack_chains(long_chains)
+    assert {int(x) % 4 for x in lp["pre_off"]} == {0, 1, 2, 3} and int(lp["pre_len"].max()) >= 7 * 64
+    ld = A.chain_hashes({k: v.cuda() for k, v in lp.items()})
+    assert A.digests_to_hex(ld.cpu()) == [d.delta_hash for c in long_chains for d in c]
     assert A.digests_to_hex(hc) == [d.delta_hash for c in chains for d in c]
     d, o = A.pack_bytes(pays)
     _check(lambda *t: A.verify_chains(*t), d, o, A.hex_to_digests(hexes), A.hex_to_digests(parent),

@@ -212,6 +212,41 @@ def test_slash_cascade_matches_slashing_engine(clip_cap):
     assert vb.active.tolist() == vb2.active.tolist()
 
 
+def test_fused_slash_sigma_eff_matches_engines():
+    """K06+K03 fused: σ_eff over the post-slash bonds equals, bit for bit, the
+    separate sigma_eff pass and VouchingEngine.compute_sigma_eff after
+    SlashingEngine.slash; storm subsets (target 255) get σ_eff too."""
+    from hypervisor.liability.slashing import SlashingEngine
+
+    ve, sids, parts, sigmas = _random_vouch_world(n_sessions=50, seed=15, expiry=False)
+    now_us = _clock.to_us(T0)
+    vb = LI.from_engine(ve, sids, parts)
+    vb_sep = LI.from_engine(ve, sids, parts)
+    S = len(sids)
+    rng = random.Random(16)
+    targets = [rng.randrange(len(p)) if s % 3 else 255 for s, p in enumerate(parts)]
+    omega = torch.tensor([rng.choice([0.3, 0.9]) for _ in range(S)], dtype=f64)
+    scores = torch.full((S, 16), float("nan"), dtype=f64)
+    py_scores = []
+    for s, p in enumerate(parts):
+        d = {}
+        for k, did in enumerate(p):
+            d[did] = sigmas[s][did]
+            scores[s, k] = sigmas[s][did]
+        py_scores.append(d)
+    tgt = torch.tensor(targets, dtype=u8)
+    fused = LI.slash(vb, tgt, omega, scores.clone(), now_us, with_sigma_eff=True)
+    sep = LI.slash(vb_sep, tgt, omega, scores.clone(), now_us)
+    assert torch.equal(fused.sigma_eff, LI.sigma_eff_exact(vb_sep, sep.scores, omega, now_us))
+    se = SlashingEngine(ve)
+    for s, (sid, p) in enumerate(zip(sids, parts)):
+        if targets[s] != 255:
+            se.slash(p[targets[s]], sid, 0.5, omega[s].item(), "t", py_scores[s])
+        for k, did in enumerate(p):
+            want = ve.compute_sigma_eff(did, sid, py_scores[s][did], omega[s].item())
+            assert fused.sigma_eff[s, k].item() == want
+
+
 def test_release_bonds_matches_release_session_bonds():
     ve, sids, parts, _ = _random_vouch_world(n_sessions=20, seed=7)
     now_us = _clock.to_us(T0)
