@@ -156,78 +156,31 @@ AHV_HD void chain_hash_elem(const ChainHashArgs& a, int64_t c, Sink& sink) {
 }
 }  // namespace
 
-// Phase 1 on the device: one wave per 64 deltas.  Lane-per-delta word loads would
-// touch 64 cache lines per instruction (deltas sit a payload apart); instead the
-// wave stages 4 blocks of every delta's prefix in LDS at a time, one coalesced
-// 256-byte row load per delta (its base address read from the owning lane with
-// a scalar readlane), then each lane compresses its own delta's blocks from LDS,
-// funnel-shifting to the span's byte offset.
-constexpr int kPrefixChunkWords = 64;                   // 4 SHA blocks per staging round
-constexpr int kPrefixRow = kPrefixChunkWords + 2;       // +1 funnel word, +1 pad (bank spread)
-
-__global__ __launch_bounds__(kWaveLanes) void chain_prefix_kernel(ChainHashArgs a) {
-  __shared__ uint32_t raw[kWaveLanes * kPrefixRow];
-  const int lane = threadIdx.x;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
-  const bool mine = i < a.deltas;
-  const int64_t off = mine ? a.pre_off[i] : 0;
-  const int32_t nb = mine ? (a.pre_len[i] >> 6) : 0;
-  const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.bytes + off) & 3u) * 8u;
-  // word index of the span start from the arena's aligned base, and the words its
-  // whole blocks occupy (one more when unaligned: never past the prefix)
-  const int64_t skew = static_cast<int64_t>(reinterpret_cast<uintptr_t>(a.bytes) & 3u);
-  const uint32_t* base = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a.bytes) - skew);
-  const int64_t wbase = (off + skew) >> 2;
-  const int32_t need = nb * 16 + (sh ? 1 : 0);
-  uint32_t st[8];
-  sha256_init(st);
-  int32_t maxnb = nb;
-  for (int o = 32; o; o >>= 1) {
-    const int32_t t = __shfl_xor(maxnb, o, kWaveLanes);
-    maxnb = t > maxnb ? t : maxnb;
-  }
-  for (int32_t q = 0; q * 4 < maxnb; ++q) {
-    const int32_t c0 = q * kPrefixChunkWords;
-    for (int d = 0; d < kWaveLanes; ++d) {
-      // delta d's row: its span start and length from lane d (scalar readlanes)
-      const int64_t wd = static_cast<int64_t>(
-          (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(wbase >> 32), d))) << 32) |
-          static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(wbase & 0xffffffff), d)));
-      const int32_t nd = __builtin_amdgcn_readlane(need, d);
-      const int32_t k = c0 + lane;
-      raw[d * kPrefixRow + lane] = k < nd ? base[wd + k] : 0u;
-      if (lane == 0) raw[d * kPrefixRow + kPrefixChunkWords] = c0 + kPrefixChunkWords < nd ? base[wd + c0 + kPrefixChunkWords] : 0u;
-    }
-    __syncthreads();
-    const uint32_t* row = raw + lane * kPrefixRow;
-#pragma nounroll
-    for (int b = 0; b < 4; ++b) {
-      if (q * 4 + b < nb) {
-        uint32_t blk[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) blk[k] = bswap_word(funnel32(row[16 * b + k], row[16 * b + k + 1], sh));
-        sha256_compress(st, blk);
-      }
-    }
-    __syncthreads();
-  }
-  if (mine)
-    for (int k = 0; k < 8; ++k) a.mid[i * 8 + k] = st[k];
+// Phase 1 on the device: one lane per delta, 256-thread blocks.  (Staging every
+// delta's prefix rows in LDS with coalesced 256-byte loads measured slower —
+// 56 → 92 µs for 160 k deltas: the kernel is bound by the SHA rounds of its
+// longest lanes, not by the scattered word loads, which mostly hit L2.)
+__global__ __launch_bounds__(256) void chain_prefix_kernel(ChainHashArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.deltas) chain_prefix_elem(a, i);
 }
 
 // One wave per 64 chains; lanes whose chains are shorter idle (masked) while
-// the wave finishes its longest chain.
+// the wave finishes its longest chain.  (A 4-block window — one emission pass
+// for a governance delta's ≈ 225-byte post-midstate remainder — measured no
+// faster than 3 blocks: the walk is bound by its SHA rounds and load latency.)
+constexpr int kChainWin = 3;
 __global__ __launch_bounds__(kWaveLanes, 3) void chain_hash_kernel(ChainHashArgs a) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * kWaveLanes + threadIdx.x;
-  WordWindowSink<3> sink;
-  sink.g_win = win_lds<3>();
+  WordWindowSink<kChainWin> sink;
+  sink.g_win = win_lds<kChainWin>();
   sink.lane = threadIdx.x;
   if (c < a.chains) chain_hash_elem(a, c, sink);
 }
 void launch_chain_hash(const ChainHashArgs& a, hipStream_t st) {
   if (a.chains <= 0) return;
   if (a.mid && a.deltas > 0) {
-    hipLaunchKernelGGL(chain_prefix_kernel, grid1(a.deltas, kWaveLanes), dim3(kWaveLanes), 0, st, a);
+    hipLaunchKernelGGL(chain_prefix_kernel, grid1(a.deltas, 256), dim3(256), 0, st, a);
     check_hip(hipGetLastError(), "chain_prefix_kernel");
   }
   hipLaunchKernelGGL(chain_hash_kernel, grid1(a.chains, kWaveLanes), dim3(kWaveLanes), 0, st, a);

@@ -7,7 +7,7 @@ export TMPDIR=/tmp AHV_SKIP_AUTOBUILD=1
 OUT=gpurun_out/r2t
 mkdir -p $OUT
 C5="python3 benchmarks/bench_configs.py config5 --steps 10 --warmup 2"
-timeout -k 10 200 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_config5_arena.py -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 &&
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 &&
 timeout -k 10 200 $C5 > $OUT/c5_new.log 2>&1 &&
 timeout -k 10 200 $C5 --no-midstate > $OUT/c5_nomid.log 2>&1 &&
 timeout -k 10 200 $C5 --unfused > $OUT/c5_unfused.log 2>&1 &&
