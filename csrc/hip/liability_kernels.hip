@@ -201,7 +201,10 @@ __global__ __launch_bounds__(64 * kFusedWaves) void bond_fused_mfma_kernel(BondF
     if (a.bonded_in) a.bonded_in[o] = bonded;
     a.sigma_eff[o] = sigma_eff_combine(score_or_zero(a.sigma[o]), a.omega[s], bonded);
     a.exposure[o] = acc_out[q];
-    if (a.members) unsafeAtomicAdd(a.agent_exposure + a.members[o], acc_out[q]);
+    // X01 input: only members that vouch for someone carry exposure (≈ 60 % of a
+    // 16-member row with 8 edges is zero) — adding +0.0 to a non-negative sum is a
+    // no-op, so those fp64 atomics are skipped
+    if (a.members && acc_out[q] != 0.0) unsafeAtomicAdd(a.agent_exposure + a.members[o], acc_out[q]);
   }
 }
 
