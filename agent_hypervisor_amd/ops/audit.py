@@ -159,21 +159,29 @@ def pack_chains(chains, device="cpu") -> dict:
 
 
 def chain_hashes(packed: dict, seed_parent: Optional[torch.Tensor] = None,
-                 has_seed: Optional[torch.Tensor] = None, midstate: bool = True) -> torch.Tensor:
+                 has_seed: Optional[torch.Tensor] = None, midstate: bool = True,
+                 uniform_len: int = 0) -> torch.Tensor:
     """K08: re-derive every delta hash of every chain (parent links recomputed
     from the chain itself) → int32 [D, 8].
 
     ``midstate=True`` splits the work in two launches: every delta's whole
     prefix blocks (the chain-independent bytes before ``"parent_hash"``) are
     compressed in parallel, one lane per delta; the serial per-chain pass then
-    resumes from those midstates."""
+    resumes from those midstates.
+
+    ``uniform_len`` (> 0) promises that every chain holds exactly that many
+    deltas; phase 1 then assigns a wave the same turn of 64 chains (payloads of
+    one shape) instead of consecutive deltas of a few chains."""
     D = packed["pre_off"].numel()
     dev = packed["bytes"].device
+    chains = packed["chain_offsets"].numel() - 1
+    if uniform_len and (uniform_len < 0 or chains * uniform_len != D):
+        raise ValueError(f"uniform_len={uniform_len} does not match {chains} chains of {D} deltas")
     out = torch.empty((D, 8), dtype=i32, device=dev)
     mid = torch.empty((D, 8), dtype=i32, device=dev) if midstate and D else None
     launch(
         "chain_hash",
-        {"chains": packed["chain_offsets"].numel() - 1, "deltas": D},
+        {"chains": packed["chain_offsets"].numel() - 1, "deltas": D, "uniform_len": int(uniform_len)},
         dict(packed, seed_parent=seed_parent, has_seed=has_seed, digest=out, mid=mid),
         dict(bytes=u8, chain_offsets=i32, pre_off=i64, pre_len=i32, suf_off=i64, suf_len=i32,
              seed_parent=i32, has_seed=u8, mid=i32),

@@ -160,9 +160,15 @@ AHV_HD void chain_hash_elem(const ChainHashArgs& a, int64_t c, Sink& sink) {
 // delta's prefix rows in LDS with coalesced 256-byte loads measured slower —
 // 56 → 92 µs for 160 k deltas: the kernel is bound by the SHA rounds of its
 // longest lanes, not by the scattered word loads, which mostly hit L2.)
+AHV_HD int64_t prefix_lane_delta(const ChainHashArgs& a, int64_t i) {
+  if (a.uniform_len <= 0) return i;
+  const int64_t c = a.deltas / a.uniform_len;  // chains
+  return (i % c) * a.uniform_len + i / c;
+}
+
 __global__ __launch_bounds__(256) void chain_prefix_kernel(ChainHashArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < a.deltas) chain_prefix_elem(a, i);
+  if (i < a.deltas) chain_prefix_elem(a, prefix_lane_delta(a, i));
 }
 
 // One wave per 64 chains; lanes whose chains are shorter idle (masked) while
@@ -188,7 +194,7 @@ void launch_chain_hash(const ChainHashArgs& a, hipStream_t st) {
 }
 void chain_hash_host(const ChainHashArgs& a) {
   if (a.mid)
-    for (int64_t i = 0; i < a.deltas; ++i) chain_prefix_elem(a, i);
+    for (int64_t i = 0; i < a.deltas; ++i) chain_prefix_elem(a, prefix_lane_delta(a, i));
   HostSink sink;
   for (int64_t c = 0; c < a.chains; ++c) chain_hash_elem(a, c, sink);
 }

@@ -262,6 +262,7 @@ static ChainHashArgs to_chain_hash(const py::dict& d) {
   P(seed_parent, const uint32_t); P(has_seed, const uint8_t); P(digest, uint32_t);
   a.mid = d.contains("mid") ? ptr<uint32_t>(d, "mid") : nullptr;
   a.deltas = d.contains("deltas") ? d["deltas"].cast<int64_t>() : 0;
+  a.uniform_len = d.contains("uniform_len") ? d["uniform_len"].cast<int32_t>() : 0;
   return a;
 }
 static SagaBatchArgs to_saga(const py::dict& d) {

@@ -352,6 +352,11 @@ struct ChainHashArgs {
   // each delta's whole prefix blocks, computed in parallel over all `deltas`.
   uint32_t* mid;
   int64_t deltas;
+  // > 0: every chain has exactly this many deltas.  Phase 1 then gives a wave
+  // the same turn of 64 chains (lane i → delta (i mod C)·len + i div C), so the
+  // lanes of a wave hash prefixes of the same shape instead of idling behind the
+  // longest turn of their chain.
+  int32_t uniform_len;
 };
 void launch_chain_hash(const ChainHashArgs&, hipStream_t);
 void chain_hash_host(const ChainHashArgs&);

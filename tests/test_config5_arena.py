@@ -8,6 +8,7 @@ import os
 import sys
 from datetime import datetime, timezone
 
+import pytest
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -26,6 +27,8 @@ def test_arena_chains_match_scalar_delta_engine():
     arena.write_slash_deltas(touched, scores)
     packed = arena.packed(touched)
     dig = A.digests_to_hex(A.chain_hashes(packed))
+    # equal-length chains: the turn-major phase-1 lane order gives the same digests
+    assert A.digests_to_hex(A.chain_hashes(packed, uniform_len=D + 1)) == dig
     for i, s in enumerate(touched.tolist()):
         tag = f"{s:07d}"
         _clock.set_clock(lambda s=s: datetime(2026, 3, 1, 12, 0, 0, s % 999_999 + 1, tzinfo=timezone.utc))
@@ -38,3 +41,18 @@ def test_arena_chains_match_scalar_delta_engine():
         roots = A.merkle_roots(packed["chain_offsets"], A.chain_hashes(packed))
         assert A.digests_to_hex(roots[i:i + 1])[0] == de.compute_merkle_root()
     _clock.set_clock(None)
+
+
+@pytest.mark.gpu
+def test_arena_chains_gfx950_turn_major(cuda_device):
+    """Device K08 over the arena, turn-major phase 1 (``uniform_len``) and
+    consecutive lanes, against the host twin."""
+    S, D = 3000, 3
+    arena = AuditArena(S, D, torch.device("cuda"))
+    touched = torch.arange(0, S, 7, device="cuda")
+    scores = torch.rand((touched.numel(), 16), dtype=torch.float64, device="cuda")
+    arena.write_slash_deltas(touched, scores)
+    packed = arena.packed(touched)
+    want = A.chain_hashes({k: v.cpu() for k, v in packed.items()})
+    assert torch.equal(A.chain_hashes(packed, uniform_len=D + 1).cpu(), want)
+    assert torch.equal(A.chain_hashes(packed).cpu(), want)
