@@ -173,13 +173,28 @@ class SagaBatchRunner:
                             eng.step_error.to(torch.int64), eng.started_us, eng.completed_us]).cpu().tolist()
         sg_cols = torch.stack([eng.saga_state.to(torch.int64), eng.saga_completed_us,
                                eng.comp_failed.to(torch.int64)]).cpu().tolist()
-        ts = lambda us: _clock.from_us(us) if us else None  # noqa: E731
+        # Per-batch lookup tables: enum members by code, and one datetime per distinct
+        # device timestamp (the step loop stamps from one time base, so few distinct
+        # values) — this loop touches every step of the batch.
+        step_enum = [StepState(n) for n in STEP_NAMES]
+        saga_enum = [SagaState(n) for n in SAGA_NAMES]
+        stamps: dict[int, Any] = {0: None}
+
+        def ts(us: int):
+            d = stamps.get(us)
+            if d is None and us:
+                d = stamps[us] = _clock.from_us(us)
+            return d
+
+        st_state, st_retry, st_err, st_start, st_done = cols
         for s, sg in enumerate(sagas):
+            row_state, row_retry, row_err = st_state[s], st_retry[s], st_err[s]
+            row_start, row_done = st_start[s], st_done[s]
             for k, st in enumerate(sg.steps):
-                st.state = StepState(STEP_NAMES[cols[0][s][k]])
-                st.retry_count = cols[1][s][k]
-                st.started_at, st.completed_at = ts(cols[3][s][k]), ts(cols[4][s][k])
-                code = cols[2][s][k]
+                st.state = step_enum[row_state[k]]
+                st.retry_count = row_retry[k]
+                st.started_at, st.completed_at = ts(row_start[k]), ts(row_done[k])
+                code = row_err[k]
                 if code == ERR_NONE:
                     st.error = None
                 elif code in (ERR_EXEC, ERR_TIMEOUT):
@@ -188,16 +203,15 @@ class SagaBatchRunner:
                     st.error = "No Undo_API available"
                 elif code in (ERR_COMP, ERR_COMP_TIMEOUT):
                     st.error = comp_errors.get((s, k))
-                if (s, k) in results:
-                    st.execute_result = results[(s, k)]
+                r = results.get((s, k), results)  # the dict itself marks "absent"
+                if r is not results:
+                    st.execute_result = r
                 if (s, k) in comp_results:
                     st.compensation_result = comp_results[(s, k)]
-            sg.state = SagaState(SAGA_NAMES[sg_cols[0][s]])
+            sg.state = saga_enum[sg_cols[0][s]]
             sg.completed_at = ts(sg_cols[1][s])
             if sg.state is SagaState.ESCALATED:
                 sg.error = f"{sg_cols[2][s]} step(s) failed compensation — Joint Liability slashing triggered"
-
-
 _RUNNERS: dict[str, SagaBatchRunner] = {}
 
 
