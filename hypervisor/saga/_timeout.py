@@ -10,6 +10,12 @@ that cancellation into ``asyncio.TimeoutError``.
 Behaviour kept from ``wait_for`` where callers can observe it: a non-awaitable
 raises the same ``TypeError`` message, ``timeout=None`` waits forever, and
 ``timeout <= 0`` delegates to ``wait_for`` itself.
+
+A coroutine is driven by hand up to its first suspension before any timer is
+armed: one that completes without suspending (a synchronous executor, a cache
+hit) costs no loop timer at all.  The deadline is still taken when the await
+starts, so a coroutine that first suspends late times out exactly when the eager
+timer would have fired.
 """
 
 from __future__ import annotations
@@ -30,6 +36,8 @@ async def await_with_timeout(aw, timeout):
         return await asyncio.wait_for(aw, timeout)
     loop = asyncio.get_running_loop()
     task = asyncio.current_task(loop)
+    if type(aw) is CoroutineType:
+        return await _Deadline(aw, loop, loop.time() + timeout, task)
     state = [False]
 
     def _expire() -> None:
@@ -45,3 +53,51 @@ async def await_with_timeout(aw, timeout):
         raise
     finally:
         handle.cancel()
+
+
+class _Deadline:
+    """Awaitable that delegates to ``coro`` like ``yield from`` and arms the
+    cancelling timer (due at ``when``) only once ``coro`` first suspends."""
+
+    __slots__ = ("coro", "loop", "when", "task")
+
+    def __init__(self, coro, loop, when, task) -> None:
+        self.coro, self.loop, self.when, self.task = coro, loop, when, task
+
+    def __await__(self):
+        coro = self.coro
+        try:
+            y = coro.send(None)
+        except StopIteration as e:  # finished without suspending: no timer needed
+            return e.value
+        expired = [False]
+        task = self.task
+
+        def _expire() -> None:
+            expired[0] = True
+            task.cancel()
+
+        handle = self.loop.call_at(self.when, _expire)
+        try:
+            while True:
+                try:
+                    v = yield y
+                except GeneratorExit:
+                    coro.close()
+                    raise
+                except BaseException as exc:  # thrown in by the task (cancellation)
+                    try:
+                        y = coro.throw(exc)
+                    except StopIteration as e:
+                        return e.value
+                else:
+                    try:
+                        y = coro.send(v)
+                    except StopIteration as e:
+                        return e.value
+        except asyncio.CancelledError:
+            if expired[0]:
+                raise asyncio.TimeoutError() from None
+            raise
+        finally:
+            handle.cancel()
