@@ -28,6 +28,7 @@ are attached from the host side.  Sagas are batched by step count.
 from __future__ import annotations
 
 import asyncio
+from types import CoroutineType
 from typing import Any, Callable, Optional, Sequence
 
 import torch
@@ -46,7 +47,7 @@ from agent_hypervisor_amd.models.saga_engine import (
     SagaOutcomes,
 )
 from hypervisor import _clock
-from hypervisor.saga._timeout import await_with_timeout
+from hypervisor.saga._timeout import await_with_timeout, resume_with_deadline
 
 u8 = torch.uint8
 _KIND_EXC, _KIND_TIMEOUT = 1, 2
@@ -102,14 +103,29 @@ class SagaBatchRunner:
         comp_results: dict[tuple[int, int], Any] = {}
         comp_errors: dict[tuple[int, int], str] = {}
 
+        loop = asyncio.get_running_loop()
+
         async def attempts(s: int, k: int):
             st = sagas[s].steps[k]
             n = 1 + int(st.max_retries)
             fn = executors[st.step_id]
+            tmo = st.timeout_seconds
             kind, err = 0, None
             for at in range(n):
                 try:
-                    res = await await_with_timeout(fn(), st.timeout_seconds)
+                    c = fn()
+                    if type(c) is CoroutineType and tmo is not None and tmo > 0:
+                        # started inline: a coroutine that finishes without suspending
+                        # needs no deadline timer (await_with_timeout semantics otherwise)
+                        when = loop.time() + tmo
+                        try:
+                            y = c.send(None)
+                        except StopIteration as e:
+                            res = e.value
+                        else:
+                            res = await resume_with_deadline(c, y, when)
+                    else:
+                        res = await await_with_timeout(c, tmo)
                 except asyncio.TimeoutError:
                     kind = _KIND_TIMEOUT
                     err = f"Step {st.step_id} timed out after {st.timeout_seconds}s (attempt {at + 1}/{n})"

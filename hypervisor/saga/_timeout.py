@@ -55,21 +55,34 @@ async def await_with_timeout(aw, timeout):
         handle.cancel()
 
 
+def resume_with_deadline(coro, first, when):
+    """Awaitable continuing ``coro`` — already started by the caller with
+    ``coro.send(None)``, which yielded ``first`` — under a deadline at loop time
+    ``when`` (batch runners start coroutines inline and only pay for the timer
+    when one actually suspends)."""
+    loop = asyncio.get_running_loop()
+    return _Deadline(coro, loop, when, asyncio.current_task(loop), first, True)
+
+
 class _Deadline:
     """Awaitable that delegates to ``coro`` like ``yield from`` and arms the
     cancelling timer (due at ``when``) only once ``coro`` first suspends."""
 
-    __slots__ = ("coro", "loop", "when", "task")
+    __slots__ = ("coro", "loop", "when", "task", "first", "started")
 
-    def __init__(self, coro, loop, when, task) -> None:
+    def __init__(self, coro, loop, when, task, first=None, started=False) -> None:
         self.coro, self.loop, self.when, self.task = coro, loop, when, task
+        self.first, self.started = first, started
 
     def __await__(self):
         coro = self.coro
-        try:
-            y = coro.send(None)
-        except StopIteration as e:  # finished without suspending: no timer needed
-            return e.value
+        if self.started:
+            y = self.first
+        else:
+            try:
+                y = coro.send(None)
+            except StopIteration as e:  # finished without suspending: no timer needed
+                return e.value
         expired = [False]
         task = self.task
 
