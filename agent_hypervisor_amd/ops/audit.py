@@ -41,6 +41,41 @@ def sha256_many(data: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def render_rows(out: torch.Tensor, template: torch.Tensor, ids: torch.Tensor, stamps: Sequence = (),
+                hex_field: Optional[tuple] = None, check: bool = True) -> None:
+    """Render audit payload rows in place: row ``ids[r]`` of ``out`` (u8, rows of
+    ``template.numel()`` bytes) becomes ``template`` with
+
+    * each stamp ``(pos, width, mod, add)``: the decimal of ``ids[r] % mod + add``
+      (``mod`` 0 = no modulus), zero-padded to ``width`` digits at ``pos``;
+    * ``hex_field = (pos, src, nbytes)``: lowercase hex of the first ``nbytes``
+      bytes of row ``ids[r]`` of ``src`` (any dtype, viewed as bytes) at ``pos``.
+
+    One launch for every byte of every row (the per-session payload variation
+    of re-hashed audit records, written next to the resident arena).
+    ``check=False`` skips the bounds check of ``ids`` (a device sync) when the
+    caller guarantees ``0 <= ids < out.numel() // len(template)`` (and the hex
+    source has that many rows)."""
+    L = template.numel()
+    rows = ids.numel()
+    if check and rows:
+        hi, lo = int(ids.max()), int(ids.min())
+        limit = out.numel() // L if hex_field is None else min(out.numel() // L, hex_field[1].shape[0])
+        if lo < 0 or hi >= limit:
+            raise ValueError(f"render_rows: row ids in [{lo}, {hi}] outside [0, {limit})")
+    hp, src, nb, stride = -1, None, 0, 0
+    if hex_field is not None:
+        hp, hsrc, nb = hex_field
+        src = hsrc.contiguous().view(torch.uint8).reshape(hsrc.shape[0], -1)
+        stride = src.shape[1]
+        if nb > stride:
+            raise ValueError("hex field longer than its source rows")
+    launch("render_rows",
+           {"rows": rows, "len": L, "stamps": [tuple(int(x) for x in st) for st in stamps], "hex_pos": int(hp),
+            "hex_bytes": int(nb), "hex_stride": int(stride)},
+           dict(tmpl=template, out=out, ids=ids, hex_src=src), dict(tmpl=u8, out=u8, ids=i64, hex_src=u8))
+
+
 def content_hashes(contents: Sequence[str], device="cpu") -> list[str]:
     """K11: sha256(content.encode()).hexdigest() for many VFS contents."""
     data, offs = pack_bytes([c.encode() for c in contents], device)

@@ -74,6 +74,49 @@ void launch_hash_many(const HashManyArgs& a, hipStream_t st) {
 }
 void hash_many_host(const HashManyArgs& a) { for (int64_t i = 0; i < a.n; ++i) hash_many_elem(a, i); }
 
+// ------------------------------------------------------- payload rendering
+// One thread per output byte: template byte, or a stamp digit, or a hex nibble.
+
+AHV_HD void render_byte(const RenderArgs& a, int64_t idx) {
+  const int64_t r = idx / a.len;
+  const int32_t j = static_cast<int32_t>(idx - r * a.len);
+  const int64_t id = a.ids[r];
+  uint32_t c = a.tmpl[j];
+  for (int k = 0; k < a.nstamp; ++k) {
+    const int32_t p = j - a.stamp_pos[k];
+    if (p >= 0 && p < a.stamp_width[k]) {
+      int64_t v = (a.stamp_mod[k] > 0 ? id % a.stamp_mod[k] : id) + a.stamp_add[k];
+      for (int32_t q = a.stamp_width[k] - 1; q > p; --q) v /= 10;
+      c = static_cast<uint32_t>('0' + v % 10);
+    }
+  }
+  if (a.hex_pos >= 0) {
+    const int32_t p = j - a.hex_pos;
+    if (p >= 0 && p < 2 * a.hex_bytes) {
+      const uint32_t b = a.hex_src[id * a.hex_stride + (p >> 1)];
+      c = hex_nibble((p & 1) ? (b & 15u) : (b >> 4));
+    }
+  }
+  a.out[id * a.len + j] = static_cast<uint8_t>(c);
+}
+__global__ void render_rows_kernel(RenderArgs a) {
+  const int64_t n = a.rows * a.len;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    render_byte(a, i);
+}
+void launch_render_rows(const RenderArgs& a, hipStream_t st) {
+  const int64_t n = a.rows * a.len;
+  if (n <= 0) return;
+  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(render_rows_kernel, dim3(static_cast<uint32_t>(blocks < 65536 ? blocks : 65536)), dim3(kBlock),
+                     0, st, a);
+  check_hip(hipGetLastError(), "render_rows_kernel");
+}
+void render_rows_host(const RenderArgs& a) {
+  for (int64_t i = 0; i < a.rows * a.len; ++i) render_byte(a, i);
+}
+
 // ------------------------------------------------------------------ K08
 // The message is virtual: prefix bytes, then the parent field text, then the
 // suffix bytes.  The device assembles each message a 32-bit word at a time in
@@ -304,6 +347,7 @@ void verify_host(const VerifyArgs& a) {
 void kernels_audit(std::vector<KernelEntry>& out) {
   out.push_back({"chain_hash_kernel", reinterpret_cast<const void*>(&chain_hash_kernel)});
   out.push_back({"chain_prefix_kernel", reinterpret_cast<const void*>(&chain_prefix_kernel)});
+  out.push_back({"render_rows_kernel", reinterpret_cast<const void*>(&render_rows_kernel)});
   out.push_back({"merkle_kernel", reinterpret_cast<const void*>(&merkle_kernel)});
   out.push_back({"hash_many_kernel", reinterpret_cast<const void*>(&hash_many_kernel)});
   out.push_back({"verify_delta_kernel", reinterpret_cast<const void*>(&verify_delta_kernel)});

@@ -224,6 +224,25 @@ static SlashArgs to_slash(const py::dict& d) {
   a.sigma_eff = d.contains("sigma_eff") ? ptr<double>(d, "sigma_eff") : nullptr;
   return a;
 }
+static RenderArgs to_render(const py::dict& d) {
+  RenderArgs a{};
+  V(rows, int64_t); V(len, int32_t); P(tmpl, const uint8_t); P(out, uint8_t); P(ids, const int64_t);
+  const auto stamps = d["stamps"].cast<std::vector<std::tuple<int32_t, int32_t, int64_t, int64_t>>>();
+  if (stamps.size() > static_cast<size_t>(kRenderMaxStamps)) throw py::value_error("render_rows: too many stamp fields");
+  a.nstamp = static_cast<int32_t>(stamps.size());
+  for (size_t k = 0; k < stamps.size(); ++k) {
+    const auto& [pos, width, mod, add] = stamps[k];
+    if (pos < 0 || width <= 0 || width > 18 || pos + width > a.len) throw py::value_error("render_rows: bad stamp field");
+    a.stamp_pos[k] = pos;
+    a.stamp_width[k] = width;
+    a.stamp_mod[k] = mod;
+    a.stamp_add[k] = add;
+  }
+  V(hex_pos, int32_t); V(hex_bytes, int32_t); P(hex_src, const uint8_t); V(hex_stride, int64_t);
+  if (a.hex_pos >= 0 && (a.hex_src == nullptr || a.hex_pos + 2 * a.hex_bytes > a.len))
+    throw py::value_error("render_rows: bad hex field");
+  return a;
+}
 static HashManyArgs to_hash_many(const py::dict& d) {
   HashManyArgs a{};
   V(n, int64_t); P(bytes, const uint8_t); P(offsets, const int64_t); P(digest, uint32_t);
@@ -319,6 +338,7 @@ void register_kernels(py::module_& m) {
   bind_pair(m, "vouch_admit", to_vouch_admit, launch_vouch_admit, vouch_admit_host);
   bind_pair(m, "slash", to_slash, launch_slash, slash_host);
   bind_pair(m, "hash_many", to_hash_many, launch_hash_many, hash_many_host);
+  bind_pair(m, "render_rows", to_render, launch_render_rows, render_rows_host);
   bind_pair(m, "merkle", to_merkle, launch_merkle, merkle_host);
   bind_pair(m, "verify", to_verify, launch_verify, verify_host);
   bind_pair(m, "vclock", to_vclock, launch_vclock, vclock_host);

@@ -295,6 +295,30 @@ void slash_host(const SlashArgs&);
 
 // ------------------------------------------------------------------ audit
 
+// Payload rendering for re-hashed audit records: row r of `rows` is the template
+// with decimal stamp fields (value = ids[r] mod m + add, zero-padded to the field
+// width; m = 0: no modulus) and one lowercase-hex field (the `hex_bytes` bytes of
+// source row ids[r]) written in place, at out + ids[r]·len.
+constexpr int kRenderMaxStamps = 8;
+struct RenderArgs {
+  int64_t rows;
+  int32_t len;
+  const uint8_t* tmpl;      // [len]
+  uint8_t* out;             // row ids[r] at out + ids[r]·len
+  const int64_t* ids;       // [rows]
+  int32_t nstamp;
+  int32_t stamp_pos[kRenderMaxStamps];
+  int32_t stamp_width[kRenderMaxStamps];
+  int64_t stamp_mod[kRenderMaxStamps];
+  int64_t stamp_add[kRenderMaxStamps];
+  int32_t hex_pos;          // -1: none
+  int32_t hex_bytes;
+  const uint8_t* hex_src;   // source row ids[r] at hex_src + ids[r]·hex_stride
+  int64_t hex_stride;
+};
+void launch_render_rows(const RenderArgs&, hipStream_t);
+void render_rows_host(const RenderArgs&);
+
 // K11 / K12 — SHA-256 of variable-length messages (offsets into a byte arena)
 struct HashManyArgs {
   int64_t n;

@@ -23,8 +23,9 @@ def test_arena_chains_match_scalar_delta_engine():
     S, D = 40, 3
     arena = AuditArena(S, D, torch.device("cpu"))
     touched = torch.tensor([0, 7, 13, 39])
-    scores = torch.rand((4, 16), dtype=torch.float64, generator=torch.Generator().manual_seed(1))
-    arena.write_slash_deltas(touched, scores)
+    scores_all = torch.rand((S, 16), dtype=torch.float64, generator=torch.Generator().manual_seed(1))
+    scores = scores_all[touched]
+    arena.write_slash_deltas(touched, scores_all)
     packed = arena.packed(touched)
     dig = A.digests_to_hex(A.chain_hashes(packed))
     # equal-length chains: the turn-major phase-1 lane order gives the same digests
@@ -50,9 +51,12 @@ def test_arena_chains_gfx950_turn_major(cuda_device):
     S, D = 3000, 3
     arena = AuditArena(S, D, torch.device("cuda"))
     touched = torch.arange(0, S, 7, device="cuda")
-    scores = torch.rand((touched.numel(), 16), dtype=torch.float64, device="cuda")
+    scores = torch.rand((S, 16), dtype=torch.float64, device="cuda")
     arena.write_slash_deltas(touched, scores)
+    host = AuditArena(S, D, torch.device("cpu"))
+    host.write_slash_deltas(touched.cpu(), scores.cpu())
+    assert torch.equal(arena.bytes.cpu(), host.bytes)  # render_rows: device == host twin
     packed = arena.packed(touched)
-    want = A.chain_hashes({k: v.cpu() for k, v in packed.items()})
+    want = A.chain_hashes(host.packed(touched.cpu()))
     assert torch.equal(A.chain_hashes(packed, uniform_len=D + 1).cpu(), want)
     assert torch.equal(A.chain_hashes(packed).cpu(), want)

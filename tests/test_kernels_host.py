@@ -634,3 +634,23 @@ def test_bond_fused_host_twin_matches_creation_order():
     t_se, t_ex, t_bi = LI.bond_tiles(LI.build_tiles(vb, 100), sigma, omega)
     torch.testing.assert_close(expo, t_ex, rtol=0, atol=1e-12)
     torch.testing.assert_close(bi, t_bi, rtol=0, atol=1e-12)
+
+
+def test_render_rows_stamps_and_hex():
+    tmpl = torch.frombuffer(bytearray(b'{"id": "#######", "us": "......", "h": "' + b"?" * 8 + b'"}'), dtype=u8)
+    L = tmpl.numel()
+    out = torch.zeros(5 * L, dtype=u8)
+    src = torch.arange(5 * 4, dtype=torch.int32).reshape(5, 4)  # 16 bytes per row
+    ids = torch.tensor([4, 0, 2], dtype=torch.int64)
+    p_id, p_us, p_h = bytes(tmpl.tolist()).index(b"#"), bytes(tmpl.tolist()).index(b"."), bytes(tmpl.tolist()).index(b"?")
+    A.render_rows(out, tmpl, ids, stamps=[(p_id, 7, 0, 0), (p_us, 6, 3, 998)], hex_field=(p_h, src, 4))
+    rows = out.view(5, L)
+    for i in ids.tolist():
+        want = bytearray(tmpl.tolist())
+        want[p_id:p_id + 7] = f"{i:07d}".encode()
+        want[p_us:p_us + 6] = f"{i % 3 + 998:06d}".encode()
+        want[p_h:p_h + 8] = src[i].contiguous().view(u8)[:4].numpy().tobytes().hex().encode()
+        assert bytes(rows[i].tolist()) == bytes(want)
+    assert int(rows[1].sum()) == 0 and int(rows[3].sum()) == 0  # rows not listed stay untouched
+    with pytest.raises(ValueError):
+        A.render_rows(out, tmpl, torch.tensor([5]), stamps=[(p_id, 7, 0, 0)])
