@@ -55,7 +55,11 @@ def test_arena_chains_gfx950_turn_major(cuda_device):
     arena.write_slash_deltas(touched, scores)
     host = AuditArena(S, D, torch.device("cpu"))
     host.write_slash_deltas(touched.cpu(), scores.cpu())
-    assert torch.equal(arena.bytes.cpu(), host.bytes)  # render_rows: device == host twin
+    # render_rows: device == host twin (body rows, and the rendered tail slots)
+    dev_b, host_b = arena.bytes.cpu(), host.bytes
+    assert torch.equal(dev_b[: arena.tail], host_b[: host.tail])
+    slots = lambda b: b[arena.tail:].view(S, arena.Ls)[touched.cpu()]  # noqa: E731
+    assert torch.equal(slots(dev_b), slots(host_b))
     packed = arena.packed(touched)
     want = A.chain_hashes(host.packed(touched.cpu()))
     assert torch.equal(A.chain_hashes(packed, uniform_len=D + 1).cpu(), want)
