@@ -75,19 +75,21 @@ void launch_hash_many(const HashManyArgs& a, hipStream_t st) {
 void hash_many_host(const HashManyArgs& a) { for (int64_t i = 0; i < a.n; ++i) hash_many_elem(a, i); }
 
 // ------------------------------------------------------- payload rendering
-// One thread per output byte: template byte, or a stamp digit, or a hex nibble.
+// One workgroup per row, threads over its bytes: template byte, or a stamp digit
+// (only the stamp's own bytes do the division), or a hex nibble.
 
-AHV_HD void render_byte(const RenderArgs& a, int64_t idx) {
-  const int64_t r = idx / a.len;
-  const int32_t j = static_cast<int32_t>(idx - r * a.len);
-  const int64_t id = a.ids[r];
+AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, int32_t j) {
+  constexpr uint64_t kPow10[19] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                                   100000000ull, 1000000000ull, 10000000000ull, 100000000000ull,
+                                   1000000000000ull, 10000000000000ull, 100000000000000ull,
+                                   1000000000000000ull, 10000000000000000ull, 100000000000000000ull,
+                                   1000000000000000000ull};
   uint32_t c = a.tmpl[j];
   for (int k = 0; k < a.nstamp; ++k) {
     const int32_t p = j - a.stamp_pos[k];
     if (p >= 0 && p < a.stamp_width[k]) {
-      int64_t v = (a.stamp_mod[k] > 0 ? id % a.stamp_mod[k] : id) + a.stamp_add[k];
-      for (int32_t q = a.stamp_width[k] - 1; q > p; --q) v /= 10;
-      c = static_cast<uint32_t>('0' + v % 10);
+      const uint64_t v = static_cast<uint64_t>((a.stamp_mod[k] > 0 ? id % a.stamp_mod[k] : id) + a.stamp_add[k]);
+      c = static_cast<uint32_t>('0' + (v / kPow10[a.stamp_width[k] - 1 - p]) % 10u);
     }
   }
   if (a.hex_pos >= 0) {
@@ -97,24 +99,25 @@ AHV_HD void render_byte(const RenderArgs& a, int64_t idx) {
       c = hex_nibble((p & 1) ? (b & 15u) : (b >> 4));
     }
   }
-  a.out[id * a.len + j] = static_cast<uint8_t>(c);
+  return c;
 }
-__global__ void render_rows_kernel(RenderArgs a) {
-  const int64_t n = a.rows * a.len;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    render_byte(a, i);
+__global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
+  for (int64_t r = blockIdx.x; r < a.rows; r += gridDim.x) {
+    const int64_t id = a.ids[r];
+    uint8_t* row = a.out + id * a.len;
+    for (int32_t j = threadIdx.x; j < a.len; j += kBlock) row[j] = static_cast<uint8_t>(render_char(a, id, j));
+  }
 }
 void launch_render_rows(const RenderArgs& a, hipStream_t st) {
-  const int64_t n = a.rows * a.len;
-  if (n <= 0) return;
-  const int64_t blocks = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(render_rows_kernel, dim3(static_cast<uint32_t>(blocks < 65536 ? blocks : 65536)), dim3(kBlock),
-                     0, st, a);
+  if (a.rows <= 0 || a.len <= 0) return;
+  const int64_t blocks = a.rows < 65536 ? a.rows : 65536;
+  hipLaunchKernelGGL(render_rows_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
   check_hip(hipGetLastError(), "render_rows_kernel");
 }
 void render_rows_host(const RenderArgs& a) {
-  for (int64_t i = 0; i < a.rows * a.len; ++i) render_byte(a, i);
+  for (int64_t r = 0; r < a.rows; ++r)
+    for (int32_t j = 0; j < a.len; ++j)
+      a.out[a.ids[r] * a.len + j] = static_cast<uint8_t>(render_char(a, a.ids[r], j));
 }
 
 // ------------------------------------------------------------------ K08
