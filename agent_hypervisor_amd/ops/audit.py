@@ -42,9 +42,9 @@ def sha256_many(data: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
 
 
 def render_rows(out: torch.Tensor, template: torch.Tensor, ids: torch.Tensor, stamps: Sequence = (),
-                hex_field: Optional[tuple] = None, check: bool = True) -> None:
-    """Render audit payload rows in place: row ``ids[r]`` of ``out`` (u8, rows of
-    ``template.numel()`` bytes) becomes ``template`` with
+                hex_field: Optional[tuple] = None, check: bool = True, pitch: Optional[int] = None) -> None:
+    """Render audit payload rows in place: row ``ids[r]`` of ``out`` (u8, rows
+    ``pitch`` bytes apart, default ``template.numel()``) becomes ``template`` with
 
     * each stamp ``(pos, width, mod, add)``: the decimal of ``ids[r] % mod + add``
       (``mod`` 0 = no modulus), zero-padded to ``width`` digits at ``pos``;
@@ -57,10 +57,15 @@ def render_rows(out: torch.Tensor, template: torch.Tensor, ids: torch.Tensor, st
     caller guarantees ``0 <= ids < out.numel() // len(template)`` (and the hex
     source has that many rows)."""
     L = template.numel()
+    P = L if pitch is None else int(pitch)
+    if P < L:
+        raise ValueError("render_rows: pitch shorter than the template")
     rows = ids.numel()
     if check and rows:
         hi, lo = int(ids.max()), int(ids.min())
-        limit = out.numel() // L if hex_field is None else min(out.numel() // L, hex_field[1].shape[0])
+        limit = (out.numel() - L) // P + 1 if out.numel() >= L else 0
+        if hex_field is not None:
+            limit = min(limit, hex_field[1].shape[0])
         if lo < 0 or hi >= limit:
             raise ValueError(f"render_rows: row ids in [{lo}, {hi}] outside [0, {limit})")
     hp, src, nb, stride = -1, None, 0, 0
@@ -71,7 +76,7 @@ def render_rows(out: torch.Tensor, template: torch.Tensor, ids: torch.Tensor, st
         if nb > stride:
             raise ValueError("hex field longer than its source rows")
     launch("render_rows",
-           {"rows": rows, "len": L, "stamps": [tuple(int(x) for x in st) for st in stamps], "hex_pos": int(hp),
+           {"rows": rows, "len": L, "pitch": P, "stamps": [tuple(int(x) for x in st) for st in stamps], "hex_pos": int(hp),
             "hex_bytes": int(nb), "hex_stride": int(stride)},
            dict(tmpl=template, out=out, ids=ids, hex_src=src), dict(tmpl=u8, out=u8, ids=i64, hex_src=u8))
 

@@ -330,9 +330,11 @@ class AuditArena:
         self.ph, self.micro = find(tb, self.PH), find(tb, self.MICRO)
         self.s_ph, self.s_micro, self.s_hex = find(lb, self.PH), find(lb, self.MICRO), find(lb, self.HEXPH)
         assert len(self.s_hex) == 1 and self.ph and self.micro
-        # resident arena: S chains, then one slash-delta slot per session
-        self.tail = S * self.L
-        self.bytes = torch.empty(self.tail + S * self.Ls, dtype=u8, device=dev)
+        # resident arena: S chains, then one slash-delta slot per session (slots
+        # 16-byte aligned so the render kernel writes whole words)
+        self.tail = (S * self.L + 255) // 256 * 256
+        self.pitch = (self.Ls + 15) // 16 * 16
+        self.bytes = torch.empty(self.tail + S * self.pitch, dtype=u8, device=dev)
         body = self.bytes[: self.tail].view(S, self.L)
         body.copy_(torch.frombuffer(bytearray(tb), dtype=u8).to(dev).expand(S, self.L))
         self._tmpl_slash = torch.frombuffer(bytearray(lb), dtype=u8).to(dev)
@@ -342,7 +344,7 @@ class AuditArena:
         s64 = idx.to(i64)[:, None]
         cat = lambda x, y: torch.cat([x, y], dim=1).contiguous()  # noqa: E731
         col = lambda v, dt: torch.full((S, 1), v, dtype=dt, device=dev)  # noqa: E731
-        slot = self.tail + s64 * self.Ls
+        slot = self.tail + s64 * self.pitch
         self.pre_off = cat(s64 * self.L + chain["pre_off"].to(dev)[None, :], slot + int(last["pre_off"][0]))
         self.suf_off = cat(s64 * self.L + chain["suf_off"].to(dev)[None, :], slot + int(last["suf_off"][0]))
         self.pre_len = cat(chain["pre_len"].to(dev)[None, :].expand(S, D), col(int(last["pre_len"][0]), i32))
@@ -368,7 +370,7 @@ class AuditArena:
         (row ``touched[r]`` of ``scores`` [S, 16]).  ``touched`` ⊂ [0, S)."""
         A.render_rows(self.bytes[self.tail:], self._tmpl_slash, touched.to(i64),
                       stamps=[(p, 7, 0, 0) for p in self.s_ph] + [(p, 6, 999_999, 1) for p in self.s_micro],
-                      hex_field=(self.s_hex[0], scores, 128), check=False)
+                      hex_field=(self.s_hex[0], scores, 128), check=False, pitch=self.pitch)
 
     def packed(self, touched: torch.Tensor) -> dict:
         """chain_hash arguments for the touched sessions' chains (D + 1 deltas)."""

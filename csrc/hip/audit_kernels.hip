@@ -101,11 +101,27 @@ AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, int32_t j) {
   }
   return c;
 }
+// Rows are written a 32-bit word (4 chars) per thread when the rows are word
+// aligned and the pitch leaves room for the last partial word: single-byte
+// stores would be partial-line writes (read-modify-write in the memory system).
 __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
+  const bool words = ((reinterpret_cast<uintptr_t>(a.out) | static_cast<uintptr_t>(a.pitch)) & 3u) == 0 &&
+                     a.pitch >= ((a.len + 3) & ~3);
   for (int64_t r = blockIdx.x; r < a.rows; r += gridDim.x) {
     const int64_t id = a.ids[r];
-    uint8_t* row = a.out + id * a.len;
-    for (int32_t j = threadIdx.x; j < a.len; j += kBlock) row[j] = static_cast<uint8_t>(render_char(a, id, j));
+    uint8_t* row = a.out + id * a.pitch;
+    if (words) {
+      for (int32_t w = threadIdx.x; 4 * w < a.len; w += kBlock) {
+        uint32_t v = 0;
+        for (int b = 0; b < 4; ++b) {
+          const int32_t j = 4 * w + b;
+          if (j < a.len) v |= render_char(a, id, j) << (8 * b);
+        }
+        reinterpret_cast<uint32_t*>(row)[w] = v;
+      }
+    } else {
+      for (int32_t j = threadIdx.x; j < a.len; j += kBlock) row[j] = static_cast<uint8_t>(render_char(a, id, j));
+    }
   }
 }
 void launch_render_rows(const RenderArgs& a, hipStream_t st) {
@@ -117,7 +133,7 @@ void launch_render_rows(const RenderArgs& a, hipStream_t st) {
 void render_rows_host(const RenderArgs& a) {
   for (int64_t r = 0; r < a.rows; ++r)
     for (int32_t j = 0; j < a.len; ++j)
-      a.out[a.ids[r] * a.len + j] = static_cast<uint8_t>(render_char(a, a.ids[r], j));
+      a.out[a.ids[r] * a.pitch + j] = static_cast<uint8_t>(render_char(a, a.ids[r], j));
 }
 
 // ------------------------------------------------------------------ K08

@@ -226,7 +226,9 @@ static SlashArgs to_slash(const py::dict& d) {
 }
 static RenderArgs to_render(const py::dict& d) {
   RenderArgs a{};
-  V(rows, int64_t); V(len, int32_t); P(tmpl, const uint8_t); P(out, uint8_t); P(ids, const int64_t);
+  V(rows, int64_t); V(len, int32_t); V(pitch, int64_t); P(tmpl, const uint8_t); P(out, uint8_t);
+  P(ids, const int64_t);
+  if (a.pitch < a.len) throw py::value_error("render_rows: pitch < len");
   const auto stamps = d["stamps"].cast<std::vector<std::tuple<int32_t, int32_t, int64_t, int64_t>>>();
   if (stamps.size() > static_cast<size_t>(kRenderMaxStamps)) throw py::value_error("render_rows: too many stamp fields");
   a.nstamp = static_cast<int32_t>(stamps.size());

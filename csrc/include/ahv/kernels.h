@@ -303,8 +303,9 @@ constexpr int kRenderMaxStamps = 8;
 struct RenderArgs {
   int64_t rows;
   int32_t len;
+  int64_t pitch;            // bytes between rows of `out` (≥ len)
   const uint8_t* tmpl;      // [len]
-  uint8_t* out;             // row ids[r] at out + ids[r]·len
+  uint8_t* out;             // row ids[r] at out + ids[r]·pitch
   const int64_t* ids;       // [rows]
   int32_t nstamp;
   int32_t stamp_pos[kRenderMaxStamps];

@@ -58,9 +58,27 @@ def test_arena_chains_gfx950_turn_major(cuda_device):
     # render_rows: device == host twin (body rows, and the rendered tail slots)
     dev_b, host_b = arena.bytes.cpu(), host.bytes
     assert torch.equal(dev_b[: arena.tail], host_b[: host.tail])
-    slots = lambda b: b[arena.tail:].view(S, arena.Ls)[touched.cpu()]  # noqa: E731
+    slots = lambda b: b[arena.tail:].view(S, arena.pitch)[touched.cpu(), : arena.Ls]  # noqa: E731
     assert torch.equal(slots(dev_b), slots(host_b))
     packed = arena.packed(touched)
     want = A.chain_hashes(host.packed(touched.cpu()))
     assert torch.equal(A.chain_hashes(packed, uniform_len=D + 1).cpu(), want)
     assert torch.equal(A.chain_hashes(packed).cpu(), want)
+
+
+@pytest.mark.gpu
+def test_render_rows_gfx950_word_and_byte_paths(cuda_device):
+    """render_rows on the device: the aligned word path (pitch multiple of 4) and
+    the byte path (odd pitch) both equal the host twin."""
+    g = torch.Generator().manual_seed(3)
+    tmpl = torch.randint(32, 127, (101,), dtype=torch.uint8, generator=g)
+    src = torch.randint(0, 256, (500, 24), dtype=torch.uint8, generator=g)
+    ids = torch.randperm(500, generator=g)[:300].to(torch.int64)
+    for pitch in (104, 101):
+        outs = []
+        for dev in ("cpu", "cuda"):
+            out = torch.zeros(500 * pitch, dtype=torch.uint8, device=dev)
+            A.render_rows(out, tmpl.to(dev), ids.to(dev), stamps=[(3, 7, 0, 0), (20, 6, 999_999, 1)],
+                          hex_field=(40, src.to(dev), 24), pitch=pitch)
+            outs.append(out.cpu())
+        assert torch.equal(outs[0], outs[1]), pitch
