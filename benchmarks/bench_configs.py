@@ -335,7 +335,7 @@ class AuditArena:
         self.tail = (S * self.L + 255) // 256 * 256
         self.pitch = (self.Ls + 15) // 16 * 16
         self.bytes = torch.empty(self.tail + S * self.pitch, dtype=u8, device=dev)
-        body = self.bytes[: self.tail].view(S, self.L)
+        body = self.bytes[: S * self.L].view(S, self.L)
         body.copy_(torch.frombuffer(bytearray(tb), dtype=u8).to(dev).expand(S, self.L))
         self._tmpl_slash = torch.frombuffer(bytearray(lb), dtype=u8).to(dev)
         idx = torch.arange(S, device=dev)

@@ -57,7 +57,7 @@ def test_arena_chains_gfx950_turn_major(cuda_device):
     host.write_slash_deltas(touched.cpu(), scores.cpu())
     # render_rows: device == host twin (body rows, and the rendered tail slots)
     dev_b, host_b = arena.bytes.cpu(), host.bytes
-    assert torch.equal(dev_b[: arena.tail], host_b[: host.tail])
+    assert torch.equal(dev_b[: S * arena.L], host_b[: S * host.L])
     slots = lambda b: b[arena.tail:].view(S, arena.pitch)[touched.cpu(), : arena.Ls]  # noqa: E731
     assert torch.equal(slots(dev_b), slots(host_b))
     packed = arena.packed(touched)
