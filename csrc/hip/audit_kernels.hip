@@ -78,7 +78,13 @@ void hash_many_host(const HashManyArgs& a) { for (int64_t i = 0; i < a.n; ++i) h
 // One workgroup per row, threads over its bytes: template byte, or a stamp digit
 // (only the stamp's own bytes do the division), or a hex nibble.
 
-AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, int32_t j) {
+// Stamp values of one row (uniform across the row's workgroup: computed once).
+AHV_HD void render_stamp_values(const RenderArgs& a, int64_t id, uint64_t sv[kRenderMaxStamps]) {
+  for (int k = 0; k < a.nstamp; ++k)
+    sv[k] = static_cast<uint64_t>((a.stamp_mod[k] > 0 ? id % a.stamp_mod[k] : id) + a.stamp_add[k]);
+}
+
+AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, const uint64_t sv[kRenderMaxStamps], int32_t j) {
   constexpr uint64_t kPow10[19] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
                                    100000000ull, 1000000000ull, 10000000000ull, 100000000000ull,
                                    1000000000000ull, 10000000000000ull, 100000000000000ull,
@@ -88,8 +94,13 @@ AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, int32_t j) {
   for (int k = 0; k < a.nstamp; ++k) {
     const int32_t p = j - a.stamp_pos[k];
     if (p >= 0 && p < a.stamp_width[k]) {
-      const uint64_t v = static_cast<uint64_t>((a.stamp_mod[k] > 0 ? id % a.stamp_mod[k] : id) + a.stamp_add[k]);
-      c = static_cast<uint32_t>('0' + (v / kPow10[a.stamp_width[k] - 1 - p]) % 10u);
+      const uint64_t v = sv[k], d = kPow10[a.stamp_width[k] - 1 - p];
+      uint32_t digit;
+      if ((v >> 32) == 0)  // 32-bit division whenever the value fits (stamps are short ids)
+        digit = d > 0xffffffffull ? 0u : (static_cast<uint32_t>(v) / static_cast<uint32_t>(d)) % 10u;
+      else
+        digit = static_cast<uint32_t>((v / d) % 10u);
+      c = '0' + digit;
     }
   }
   if (a.hex_pos >= 0) {
@@ -101,26 +112,29 @@ AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, int32_t j) {
   }
   return c;
 }
+
 // Rows are written a 32-bit word (4 chars) per thread when the rows are word
-// aligned and the pitch leaves room for the last partial word: single-byte
-// stores would be partial-line writes (read-modify-write in the memory system).
+// aligned and the pitch leaves room for the last partial word.
 __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
   const bool words = ((reinterpret_cast<uintptr_t>(a.out) | static_cast<uintptr_t>(a.pitch)) & 3u) == 0 &&
                      a.pitch >= ((a.len + 3) & ~3);
   for (int64_t r = blockIdx.x; r < a.rows; r += gridDim.x) {
     const int64_t id = a.ids[r];
+    uint64_t sv[kRenderMaxStamps];
+    render_stamp_values(a, id, sv);
     uint8_t* row = a.out + id * a.pitch;
     if (words) {
       for (int32_t w = threadIdx.x; 4 * w < a.len; w += kBlock) {
         uint32_t v = 0;
+#pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int32_t j = 4 * w + b;
-          if (j < a.len) v |= render_char(a, id, j) << (8 * b);
+          if (j < a.len) v |= render_char(a, id, sv, j) << (8 * b);
         }
         reinterpret_cast<uint32_t*>(row)[w] = v;
       }
     } else {
-      for (int32_t j = threadIdx.x; j < a.len; j += kBlock) row[j] = static_cast<uint8_t>(render_char(a, id, j));
+      for (int32_t j = threadIdx.x; j < a.len; j += kBlock) row[j] = static_cast<uint8_t>(render_char(a, id, sv, j));
     }
   }
 }
@@ -131,9 +145,12 @@ void launch_render_rows(const RenderArgs& a, hipStream_t st) {
   check_hip(hipGetLastError(), "render_rows_kernel");
 }
 void render_rows_host(const RenderArgs& a) {
-  for (int64_t r = 0; r < a.rows; ++r)
+  for (int64_t r = 0; r < a.rows; ++r) {
+    uint64_t sv[kRenderMaxStamps];
+    render_stamp_values(a, a.ids[r], sv);
     for (int32_t j = 0; j < a.len; ++j)
-      a.out[a.ids[r] * a.pitch + j] = static_cast<uint8_t>(render_char(a, a.ids[r], j));
+      a.out[a.ids[r] * a.pitch + j] = static_cast<uint8_t>(render_char(a, a.ids[r], sv, j));
+  }
 }
 
 // ------------------------------------------------------------------ K08
