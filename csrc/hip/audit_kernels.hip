@@ -80,8 +80,16 @@ void hash_many_host(const HashManyArgs& a) { for (int64_t i = 0; i < a.n; ++i) h
 
 // Stamp values of one row (uniform across the row's workgroup: computed once).
 AHV_HD void render_stamp_values(const RenderArgs& a, int64_t id, uint64_t sv[kRenderMaxStamps]) {
-  for (int k = 0; k < a.nstamp; ++k)
-    sv[k] = static_cast<uint64_t>((a.stamp_mod[k] > 0 ? id % a.stamp_mod[k] : id) + a.stamp_add[k]);
+  for (int k = 0; k < a.nstamp; ++k) {
+    const int64_t m = a.stamp_mod[k];
+    int64_t v = id;
+    if (m > 0) {  // 32-bit remainder when both fit (64-bit division is a long software sequence)
+      v = (id >= 0 && id <= 0x7fffffff && m <= 0x7fffffff)
+              ? static_cast<int64_t>(static_cast<uint32_t>(id) % static_cast<uint32_t>(m))
+              : id % m;
+    }
+    sv[k] = static_cast<uint64_t>(v + a.stamp_add[k]);
+  }
 }
 
 AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, const uint64_t sv[kRenderMaxStamps], int32_t j) {
@@ -115,16 +123,20 @@ AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, const uint64_t sv[k
 
 // Rows are written a 32-bit word (4 chars) per thread when the rows are word
 // aligned and the pitch leaves room for the last partial word.
+// One wave per row (4 rows per 256-thread workgroup).
+constexpr int kRenderRowsPerBlock = kBlock / 64;
 __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
   const bool words = ((reinterpret_cast<uintptr_t>(a.out) | static_cast<uintptr_t>(a.pitch)) & 3u) == 0 &&
                      a.pitch >= ((a.len + 3) & ~3);
-  for (int64_t r = blockIdx.x; r < a.rows; r += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * kRenderRowsPerBlock + (threadIdx.x >> 6); r < a.rows;
+       r += static_cast<int64_t>(gridDim.x) * kRenderRowsPerBlock) {
     const int64_t id = a.ids[r];
     uint64_t sv[kRenderMaxStamps];
     render_stamp_values(a, id, sv);
     uint8_t* row = a.out + id * a.pitch;
     if (words) {
-      for (int32_t w = threadIdx.x; 4 * w < a.len; w += kBlock) {
+      for (int32_t w = lane; 4 * w < a.len; w += 64) {
         uint32_t v = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -134,13 +146,14 @@ __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
         reinterpret_cast<uint32_t*>(row)[w] = v;
       }
     } else {
-      for (int32_t j = threadIdx.x; j < a.len; j += kBlock) row[j] = static_cast<uint8_t>(render_char(a, id, sv, j));
+      for (int32_t j = lane; j < a.len; j += 64) row[j] = static_cast<uint8_t>(render_char(a, id, sv, j));
     }
   }
 }
 void launch_render_rows(const RenderArgs& a, hipStream_t st) {
   if (a.rows <= 0 || a.len <= 0) return;
-  const int64_t blocks = a.rows < 65536 ? a.rows : 65536;
+  const int64_t need = (a.rows + kRenderRowsPerBlock - 1) / kRenderRowsPerBlock;
+  const int64_t blocks = need < 65536 ? need : 65536;
   hipLaunchKernelGGL(render_rows_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
   check_hip(hipGetLastError(), "render_rows_kernel");
 }
