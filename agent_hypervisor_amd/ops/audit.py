@@ -200,7 +200,7 @@ def pack_chains(chains, device="cpu") -> dict:
 
 def chain_hashes(packed: dict, seed_parent: Optional[torch.Tensor] = None,
                  has_seed: Optional[torch.Tensor] = None, midstate: bool = True,
-                 uniform_len: int = 0) -> torch.Tensor:
+                 uniform_len: int = 0, sel: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K08: re-derive every delta hash of every chain (parent links recomputed
     from the chain itself) → int32 [D, 8].
 
@@ -211,10 +211,20 @@ def chain_hashes(packed: dict, seed_parent: Optional[torch.Tensor] = None,
 
     ``uniform_len`` (> 0) promises that every chain holds exactly that many
     deltas; phase 1 then assigns a wave the same turn of 64 chains (payloads of
-    one shape) instead of consecutive deltas of a few chains."""
-    D = packed["pre_off"].numel()
+    one shape) instead of consecutive deltas of a few chains.
+
+    ``sel`` (int64 [chains], with ``uniform_len``) reads chain c's spans from
+    rows ``sel[c]·len …`` of the span tables in ``packed`` — resident
+    per-session tables — instead of gathering them per call; ``chain_offsets``
+    must then be the uniform ``c·len``.  Digests come back in chain order."""
     dev = packed["bytes"].device
     chains = packed["chain_offsets"].numel() - 1
+    if sel is not None:
+        if uniform_len <= 0 or sel.numel() != chains:
+            raise ValueError("sel needs uniform_len and one row per chain")
+        D = chains * uniform_len
+    else:
+        D = packed["pre_off"].numel()
     if uniform_len and (uniform_len < 0 or chains * uniform_len != D):
         raise ValueError(f"uniform_len={uniform_len} does not match {chains} chains of {D} deltas")
     out = torch.empty((D, 8), dtype=i32, device=dev)
@@ -222,9 +232,9 @@ def chain_hashes(packed: dict, seed_parent: Optional[torch.Tensor] = None,
     launch(
         "chain_hash",
         {"chains": packed["chain_offsets"].numel() - 1, "deltas": D, "uniform_len": int(uniform_len)},
-        dict(packed, seed_parent=seed_parent, has_seed=has_seed, digest=out, mid=mid),
+        dict(packed, seed_parent=seed_parent, has_seed=has_seed, digest=out, mid=mid, sel=sel),
         dict(bytes=u8, chain_offsets=i32, pre_off=i64, pre_len=i32, suf_off=i64, suf_len=i32,
-             seed_parent=i32, has_seed=u8, mid=i32),
+             seed_parent=i32, has_seed=u8, mid=i32, sel=i64),
     )
     return out
 

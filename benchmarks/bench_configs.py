@@ -373,7 +373,8 @@ class AuditArena:
                       hex_field=(self.s_hex[0], scores, 128), check=False, pitch=self.pitch)
 
     def packed(self, touched: torch.Tensor) -> dict:
-        """chain_hash arguments for the touched sessions' chains (D + 1 deltas)."""
+        """chain_hash arguments for the touched sessions' chains (D + 1 deltas),
+        gathered from the resident span table (tests / the host path)."""
         T = touched.numel()
         g = lambda t: t.index_select(0, touched).reshape(-1)  # noqa: E731
         return {
@@ -382,6 +383,18 @@ class AuditArena:
             "pre_off": g(self.pre_off), "pre_len": g(self.pre_len),
             "suf_off": g(self.suf_off), "suf_len": g(self.suf_len),
         }
+
+    def resident(self, touched: torch.Tensor) -> tuple[dict, torch.Tensor]:
+        """(chain_hash arguments over the resident span table, sel): the kernels
+        read chain c's spans at row touched[c] — no per-storm gather."""
+        T = touched.numel()
+        flat = lambda t: t.reshape(-1)  # noqa: E731
+        return {
+            "bytes": self.bytes,
+            "chain_offsets": self.chain_offsets[: T + 1],
+            "pre_off": flat(self.pre_off), "pre_len": flat(self.pre_len),
+            "suf_off": flat(self.suf_off), "suf_len": flat(self.suf_len),
+        }, touched
 
 
 def config5(ctx: Ctx, args):
@@ -417,8 +430,8 @@ def config5(ctx: Ctx, args):
         # chain is re-hashed (K08) and its Merkle root recomputed (K09)
         touched = torch.nonzero(out.clip_count > 0).flatten()
         arena.write_slash_deltas(touched, out.scores)
-        packed = arena.packed(touched)
-        digests = A.chain_hashes(packed, midstate=not args.no_midstate, uniform_len=D + 1)
+        packed, sel = arena.resident(touched)
+        digests = A.chain_hashes(packed, midstate=not args.no_midstate, uniform_len=D + 1, sel=sel)
         roots = A.merkle_roots(packed["chain_offsets"], digests)
         last.update(T=touched.numel(), roots=roots)
         return se

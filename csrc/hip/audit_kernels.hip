@@ -92,13 +92,14 @@ AHV_HD void render_stamp_values(const RenderArgs& a, int64_t id, uint64_t sv[kRe
   }
 }
 
-AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, const uint64_t sv[kRenderMaxStamps], int32_t j) {
+AHV_HD uint32_t render_char(const RenderArgs& a, const uint8_t* tmpl, int64_t id, const uint64_t sv[kRenderMaxStamps],
+                            int32_t j) {
   constexpr uint64_t kPow10[19] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
                                    100000000ull, 1000000000ull, 10000000000ull, 100000000000ull,
                                    1000000000000ull, 10000000000000ull, 100000000000000ull,
                                    1000000000000000ull, 10000000000000000ull, 100000000000000000ull,
                                    1000000000000000000ull};
-  uint32_t c = a.tmpl[j];
+  uint32_t c = tmpl[j];
   for (int k = 0; k < a.nstamp; ++k) {
     const int32_t p = j - a.stamp_pos[k];
     if (p >= 0 && p < a.stamp_width[k]) {
@@ -123,12 +124,22 @@ AHV_HD uint32_t render_char(const RenderArgs& a, int64_t id, const uint64_t sv[k
 
 // Rows are written a 32-bit word (4 chars) per thread when the rows are word
 // aligned and the pitch leaves room for the last partial word.
-// One wave per row (4 rows per 256-thread workgroup).
+// One wave per row (4 rows per 256-thread workgroup); the template is staged in
+// LDS once per workgroup, so the only global reads per row are its id and hex
+// source bytes (a wave's rows are latency-bound otherwise: dependent byte loads).
 constexpr int kRenderRowsPerBlock = kBlock / 64;
+constexpr int kRenderLdsTmpl = 4096;
 __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
+  __shared__ uint8_t s_tmpl[kRenderLdsTmpl];
   const bool words = ((reinterpret_cast<uintptr_t>(a.out) | static_cast<uintptr_t>(a.pitch)) & 3u) == 0 &&
                      a.pitch >= ((a.len + 3) & ~3);
   const int lane = threadIdx.x & 63;
+  const bool staged = a.len <= kRenderLdsTmpl;  // uniform
+  if (staged) {
+    for (int32_t j = threadIdx.x; j < a.len; j += kBlock) s_tmpl[j] = a.tmpl[j];
+    __syncthreads();
+  }
+  const uint8_t* tmpl = staged ? s_tmpl : a.tmpl;
   for (int64_t r = static_cast<int64_t>(blockIdx.x) * kRenderRowsPerBlock + (threadIdx.x >> 6); r < a.rows;
        r += static_cast<int64_t>(gridDim.x) * kRenderRowsPerBlock) {
     const int64_t id = a.ids[r];
@@ -141,12 +152,12 @@ __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int32_t j = 4 * w + b;
-          if (j < a.len) v |= render_char(a, id, sv, j) << (8 * b);
+          if (j < a.len) v |= render_char(a, tmpl, id, sv, j) << (8 * b);
         }
         reinterpret_cast<uint32_t*>(row)[w] = v;
       }
     } else {
-      for (int32_t j = lane; j < a.len; j += 64) row[j] = static_cast<uint8_t>(render_char(a, id, sv, j));
+      for (int32_t j = lane; j < a.len; j += 64) row[j] = static_cast<uint8_t>(render_char(a, tmpl, id, sv, j));
     }
   }
 }
@@ -162,7 +173,7 @@ void render_rows_host(const RenderArgs& a) {
     uint64_t sv[kRenderMaxStamps];
     render_stamp_values(a, a.ids[r], sv);
     for (int32_t j = 0; j < a.len; ++j)
-      a.out[a.ids[r] * a.pitch + j] = static_cast<uint8_t>(render_char(a, a.ids[r], sv, j));
+      a.out[a.ids[r] * a.pitch + j] = static_cast<uint8_t>(render_char(a, a.tmpl, a.ids[r], sv, j));
   }
 }
 
@@ -190,11 +201,19 @@ AHV_HD uint32_t funnel32(uint32_t lo, uint32_t hi, uint32_t sh) {
 #endif
 }
 
+// Span-table row of packed delta i (see ChainHashArgs::sel).
+AHV_HD int64_t span_row(const ChainHashArgs& a, int64_t i) {
+  if (!a.sel) return i;
+  const int64_t c = i / a.uniform_len;
+  return a.sel[c] * a.uniform_len + (i - c * a.uniform_len);
+}
+
 AHV_HD void chain_prefix_elem(const ChainHashArgs& a, int64_t i) {
   uint32_t st[8];
   sha256_init(st);
-  const uint8_t* p = a.bytes + a.pre_off[i];
-  const int32_t nb = a.pre_len[i] >> 6;
+  const int64_t sr = span_row(a, i);
+  const uint8_t* p = a.bytes + a.pre_off[sr];
+  const int32_t nb = a.pre_len[sr] >> 6;
   const uintptr_t ad = reinterpret_cast<uintptr_t>(p);
   const uint32_t* w = reinterpret_cast<const uint32_t*>(ad & ~static_cast<uintptr_t>(3));
   const uint32_t sh = static_cast<uint32_t>(ad & 3u) * 8u;
@@ -215,10 +234,11 @@ AHV_HD void chain_prefix_elem(const ChainHashArgs& a, int64_t i) {
 
 template <class Sink>
 AHV_HD void chain_emit(Sink& s, const ChainHashArgs& a, int32_t i, uint32_t skip, bool have, const Digest& prev) {
-  emit_span_prefetch<16>(s, a.bytes + a.pre_off[i] + skip, static_cast<uint32_t>(a.pre_len[i]) - skip);
+  const int64_t sr = span_row(a, i);
+  emit_span_prefetch<16>(s, a.bytes + a.pre_off[sr] + skip, static_cast<uint32_t>(a.pre_len[sr]) - skip);
   if (have) emit_hex_digest_quoted(s, prev.v);
   else emit_lit(s, canon::K_NULL);
-  emit_span_prefetch<16>(s, a.bytes + a.suf_off[i], static_cast<uint32_t>(a.suf_len[i]));
+  emit_span_prefetch<16>(s, a.bytes + a.suf_off[sr], static_cast<uint32_t>(a.suf_len[sr]));
 }
 
 template <class Sink>
@@ -232,7 +252,7 @@ AHV_HD void chain_hash_elem(const ChainHashArgs& a, int64_t c, Sink& sink) {
     const bool hv = have;
     const Digest pv = prev;
     if (a.mid) {
-      const uint32_t skip = static_cast<uint32_t>(a.pre_len[i]) & ~63u;
+      const uint32_t skip = static_cast<uint32_t>(a.pre_len[span_row(a, i)]) & ~63u;
       uint32_t st[8];
       for (int k = 0; k < 8; ++k) st[k] = a.mid[static_cast<int64_t>(i) * 8 + k];
       sink.hash_from([&](Sink& k) { chain_emit(k, a, i, skip, hv, pv); }, st, skip, h);

@@ -284,6 +284,8 @@ static ChainHashArgs to_chain_hash(const py::dict& d) {
   a.mid = d.contains("mid") ? ptr<uint32_t>(d, "mid") : nullptr;
   a.deltas = d.contains("deltas") ? d["deltas"].cast<int64_t>() : 0;
   a.uniform_len = d.contains("uniform_len") ? d["uniform_len"].cast<int32_t>() : 0;
+  a.sel = d.contains("sel") ? ptr<const int64_t>(d, "sel") : nullptr;
+  if (a.sel && a.uniform_len <= 0) throw py::value_error("chain_hash: sel needs uniform_len");
   return a;
 }
 static SagaBatchArgs to_saga(const py::dict& d) {

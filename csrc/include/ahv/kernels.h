@@ -382,6 +382,10 @@ struct ChainHashArgs {
   // lanes of a wave hash prefixes of the same shape instead of idling behind the
   // longest turn of their chain.
   int32_t uniform_len;
+  // With uniform_len > 0: chain c's span rows are sel[c]·len … sel[c]·len + len − 1
+  // of the span tables (resident per-session tables, no gather), or null (rows
+  // in packed order).  Digests and midstates stay in packed order.
+  const int64_t* sel;
 };
 void launch_chain_hash(const ChainHashArgs&, hipStream_t);
 void chain_hash_host(const ChainHashArgs&);

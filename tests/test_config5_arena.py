@@ -30,6 +30,8 @@ def test_arena_chains_match_scalar_delta_engine():
     dig = A.digests_to_hex(A.chain_hashes(packed))
     # equal-length chains: the turn-major phase-1 lane order gives the same digests
     assert A.digests_to_hex(A.chain_hashes(packed, uniform_len=D + 1)) == dig
+    res, sel = arena.resident(touched)
+    assert A.digests_to_hex(A.chain_hashes(res, uniform_len=D + 1, sel=sel)) == dig
     for i, s in enumerate(touched.tolist()):
         tag = f"{s:07d}"
         _clock.set_clock(lambda s=s: datetime(2026, 3, 1, 12, 0, 0, s % 999_999 + 1, tzinfo=timezone.utc))
@@ -63,6 +65,9 @@ def test_arena_chains_gfx950_turn_major(cuda_device):
     packed = arena.packed(touched)
     want = A.chain_hashes(host.packed(touched.cpu()))
     assert torch.equal(A.chain_hashes(packed, uniform_len=D + 1).cpu(), want)
+    res, sel = arena.resident(touched)  # spans read in place through sel
+    assert torch.equal(A.chain_hashes(res, uniform_len=D + 1, sel=sel).cpu(), want)
+    assert torch.equal(A.chain_hashes(res, uniform_len=D + 1, sel=sel, midstate=False).cpu(), want)
     assert torch.equal(A.chain_hashes(packed).cpu(), want)
 
 
