@@ -161,11 +161,86 @@ __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
     }
   }
 }
+// Fast path (word-aligned rows, len ≤ 2 KiB): each wave assembles its row in LDS
+// — template words copied, then only the stamp digits (one lane per digit) and
+// the hex field (one lane per source byte pair, 4 chars) overwritten — and
+// streams the finished row out with word stores.  Per-byte ALU work only where
+// the row differs from the template.
+constexpr int kRenderFastLen = 2048;
+__global__ __launch_bounds__(kBlock) void render_rows_fast_kernel(RenderArgs a) {
+  __shared__ uint32_t s_tmpl[kRenderFastLen / 4];
+  __shared__ uint32_t s_row[kRenderRowsPerBlock][kRenderFastLen / 4];
+  constexpr uint32_t kPow10[10] = {1u, 10u, 100u, 1000u, 10000u, 100000u, 1000000u, 10000000u, 100000000u,
+                                   1000000000u};
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int32_t nw = (a.len + 3) >> 2;
+  uint8_t* tb = reinterpret_cast<uint8_t*>(s_tmpl);
+  for (int32_t j = threadIdx.x; j < 4 * nw; j += kBlock) tb[j] = j < a.len ? a.tmpl[j] : uint8_t(0);
+  __syncthreads();
+  uint32_t* row = s_row[wave];
+  uint8_t* rb = reinterpret_cast<uint8_t*>(row);
+  // the row-group loop runs the same number of times in every wave of the block
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * kRenderRowsPerBlock; base < a.rows;
+       base += static_cast<int64_t>(gridDim.x) * kRenderRowsPerBlock) {
+    const int64_t r = base + wave;
+    const bool act = r < a.rows;
+    const int64_t id = act ? a.ids[r] : 0;
+    if (act)
+      for (int32_t w = lane; w < nw; w += 64) row[w] = s_tmpl[w];
+    __syncthreads();
+    if (act) {
+      uint64_t sv[kRenderMaxStamps];
+      render_stamp_values(a, id, sv);
+      for (int k = 0; k < a.nstamp; ++k) {
+        const int32_t wd = a.stamp_width[k];
+        if (lane < wd) {
+          const int32_t e = wd - 1 - lane;  // power of ten of this digit
+          const uint64_t v = sv[k];
+          uint32_t digit;
+          if ((v >> 32) == 0) digit = e > 9 ? 0u : (static_cast<uint32_t>(v) / kPow10[e]) % 10u;
+          else {
+            uint64_t d = 1;
+            for (int q = 0; q < e; ++q) d *= 10u;
+            digit = static_cast<uint32_t>((v / d) % 10u);
+          }
+          rb[a.stamp_pos[k] + lane] = static_cast<uint8_t>('0' + digit);
+        }
+      }
+      if (a.hex_pos >= 0) {
+        const uint8_t* src = a.hex_src + id * a.hex_stride;
+        for (int32_t q = lane; 2 * q < a.hex_bytes; q += 64) {
+          const uint32_t b0 = src[2 * q];
+          const bool two = 2 * q + 1 < a.hex_bytes;
+          const uint32_t b1 = two ? src[2 * q + 1] : 0u;
+          uint8_t* o = rb + a.hex_pos + 4 * q;
+          o[0] = static_cast<uint8_t>(hex_nibble(b0 >> 4));
+          o[1] = static_cast<uint8_t>(hex_nibble(b0 & 15u));
+          if (two) {
+            o[2] = static_cast<uint8_t>(hex_nibble(b1 >> 4));
+            o[3] = static_cast<uint8_t>(hex_nibble(b1 & 15u));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (act) {
+      uint32_t* dst = reinterpret_cast<uint32_t*>(a.out + id * a.pitch);
+      for (int32_t w = lane; w < nw; w += 64) dst[w] = row[w];
+    }
+    __syncthreads();
+  }
+}
+
 void launch_render_rows(const RenderArgs& a, hipStream_t st) {
   if (a.rows <= 0 || a.len <= 0) return;
   const int64_t need = (a.rows + kRenderRowsPerBlock - 1) / kRenderRowsPerBlock;
   const int64_t blocks = need < 65536 ? need : 65536;
-  hipLaunchKernelGGL(render_rows_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
+  const bool fast = ((reinterpret_cast<uintptr_t>(a.out) | static_cast<uintptr_t>(a.pitch)) & 3u) == 0 &&
+                    a.pitch >= ((a.len + 3) & ~3) && a.len <= kRenderFastLen;
+  if (fast)
+    hipLaunchKernelGGL(render_rows_fast_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL(render_rows_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
   check_hip(hipGetLastError(), "render_rows_kernel");
 }
 void render_rows_host(const RenderArgs& a) {
@@ -417,6 +492,7 @@ void kernels_audit(std::vector<KernelEntry>& out) {
   out.push_back({"chain_hash_kernel", reinterpret_cast<const void*>(&chain_hash_kernel)});
   out.push_back({"chain_prefix_kernel", reinterpret_cast<const void*>(&chain_prefix_kernel)});
   out.push_back({"render_rows_kernel", reinterpret_cast<const void*>(&render_rows_kernel)});
+  out.push_back({"render_rows_fast_kernel", reinterpret_cast<const void*>(&render_rows_fast_kernel)});
   out.push_back({"merkle_kernel", reinterpret_cast<const void*>(&merkle_kernel)});
   out.push_back({"hash_many_kernel", reinterpret_cast<const void*>(&hash_many_kernel)});
   out.push_back({"verify_delta_kernel", reinterpret_cast<const void*>(&verify_delta_kernel)});
