@@ -107,6 +107,8 @@ def main() -> None:
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from a captured hipGraph (device cursor + RCCL counters)")
     ap.add_argument("--no-liability", action="store_true", help="skip the X01/X02 liability stage")
+    ap.add_argument("--join-liability", action="store_true",
+                    help="join the liability side stream with the pipeline stream every step (A/B)")
     ap.add_argument("--bond-degree", type=int, default=4, help="resident vouch edges per agent")
     ap.add_argument("--slash-k", type=int, default=1024, help="vouchees slashed per step (X02 stage)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
@@ -184,6 +186,8 @@ def main() -> None:
         }
         x01_bytes = A * 8
         x02_bytes = k * 4 + cap * 12  # per rank: blacklist ids (i32) + (id i32, factor f64) pairs
+        if liab["stream"] is not None:  # the stage's buffers were initialised on the main stream
+            liab["stream"].wait_stream(torch.cuda.current_stream(dev))
 
     def liability_step():
         L = liab
@@ -206,9 +210,13 @@ def main() -> None:
         st = bufs[b]
         side = liab["stream"] if liab is not None else None
         if side is not None:
-            # the liability stage reads nothing the pipeline writes: order it after
-            # the previous step only, so its kernels run beside this step's pipeline
-            side.wait_stream(torch.cuda.current_stream(dev))
+            # The liability stage reads and writes nothing the pipeline touches, and
+            # its own steps are ordered by its stream, so it runs beside the pipeline
+            # with no cross-stream joins (each join is a barrier packet the main
+            # queue processes between pipeline launches); the timed region's final
+            # synchronize covers both streams.  --join-liability restores per-step joins.
+            if args.join_liability:
+                side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 liability_step()
         st.zero_()
@@ -216,7 +224,8 @@ def main() -> None:
         eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
         works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if multi else None
         if side is not None:
-            torch.cuda.current_stream(dev).wait_stream(side)
+            if args.join_liability:
+                torch.cuda.current_stream(dev).wait_stream(side)
         elif liab is not None:
             liability_step()
         return st
