@@ -277,10 +277,24 @@ AHV_HD uint32_t funnel32(uint32_t lo, uint32_t hi, uint32_t sh) {
 }
 
 // Span-table row of packed delta i (see ChainHashArgs::sel).
+// (i / d, i % d) with 32-bit division when both fit (64-bit integer division is a
+// long software sequence on the device)
+AHV_HD void divmod_idx(int64_t i, int64_t d, int64_t& q, int64_t& r) {
+  if (i >= 0 && i <= 0x7fffffff && d > 0 && d <= 0x7fffffff) {
+    const uint32_t qq = static_cast<uint32_t>(i) / static_cast<uint32_t>(d);
+    q = qq;
+    r = i - static_cast<int64_t>(qq) * d;
+  } else {
+    q = i / d;
+    r = i - q * d;
+  }
+}
+
 AHV_HD int64_t span_row(const ChainHashArgs& a, int64_t i) {
   if (!a.sel) return i;
-  const int64_t c = i / a.uniform_len;
-  return a.sel[c] * a.uniform_len + (i - c * a.uniform_len);
+  int64_t c, k;
+  divmod_idx(i, a.uniform_len, c, k);
+  return a.sel[c] * a.uniform_len + k;
 }
 
 AHV_HD void chain_prefix_elem(const ChainHashArgs& a, int64_t i) {
@@ -308,8 +322,7 @@ AHV_HD void chain_prefix_elem(const ChainHashArgs& a, int64_t i) {
 }
 
 template <class Sink>
-AHV_HD void chain_emit(Sink& s, const ChainHashArgs& a, int32_t i, uint32_t skip, bool have, const Digest& prev) {
-  const int64_t sr = span_row(a, i);
+AHV_HD void chain_emit(Sink& s, const ChainHashArgs& a, int64_t sr, uint32_t skip, bool have, const Digest& prev) {
   emit_span_prefetch<16>(s, a.bytes + a.pre_off[sr] + skip, static_cast<uint32_t>(a.pre_len[sr]) - skip);
   if (have) emit_hex_digest_quoted(s, prev.v);
   else emit_lit(s, canon::K_NULL);
@@ -326,13 +339,15 @@ AHV_HD void chain_hash_elem(const ChainHashArgs& a, int64_t c, Sink& sink) {
     uint32_t h[8];
     const bool hv = have;
     const Digest pv = prev;
+    // span-table row of delta i (chain c's rows start at sel[c]·len)
+    const int64_t sr = a.sel ? a.sel[c] * a.uniform_len + (i - a.chain_offsets[c]) : i;
     if (a.mid) {
-      const uint32_t skip = static_cast<uint32_t>(a.pre_len[span_row(a, i)]) & ~63u;
+      const uint32_t skip = static_cast<uint32_t>(a.pre_len[sr]) & ~63u;
       uint32_t st[8];
       for (int k = 0; k < 8; ++k) st[k] = a.mid[static_cast<int64_t>(i) * 8 + k];
-      sink.hash_from([&](Sink& k) { chain_emit(k, a, i, skip, hv, pv); }, st, skip, h);
+      sink.hash_from([&](Sink& k) { chain_emit(k, a, sr, skip, hv, pv); }, st, skip, h);
     } else {
-      sink.hash([&](Sink& k) { chain_emit(k, a, i, 0u, hv, pv); }, h);
+      sink.hash([&](Sink& k) { chain_emit(k, a, sr, 0u, hv, pv); }, h);
     }
     for (int k = 0; k < 8; ++k) {
       a.digest[static_cast<int64_t>(i) * 8 + k] = h[k];
@@ -349,8 +364,10 @@ AHV_HD void chain_hash_elem(const ChainHashArgs& a, int64_t c, Sink& sink) {
 // longest lanes, not by the scattered word loads, which mostly hit L2.)
 AHV_HD int64_t prefix_lane_delta(const ChainHashArgs& a, int64_t i) {
   if (a.uniform_len <= 0) return i;
-  const int64_t c = a.deltas / a.uniform_len;  // chains
-  return (i % c) * a.uniform_len + i / c;
+  const int64_t c = a.deltas / a.uniform_len;  // chains (wave-uniform)
+  int64_t turn, chain;
+  divmod_idx(i, c, turn, chain);
+  return chain * a.uniform_len + turn;
 }
 
 __global__ __launch_bounds__(256) void chain_prefix_kernel(ChainHashArgs a) {
