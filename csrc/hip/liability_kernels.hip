@@ -764,54 +764,18 @@ __device__ __forceinline__ double group_sigma_eff(const int (&ve)[kGroupChunks],
   return sigma_eff_combine(score_or_zero(sc), omega, contrib);
 }
 
-// Per-session inputs of the group form, loaded one session ahead (see below).
-struct GroupHead {
-  uint8_t tgt;
-  int32_t b, n;
-};
-struct GroupBody {
-  int vr[kGroupChunks], ve[kGroupChunks];
-  bool lv[kGroupChunks];
-  double bd[kGroupChunks];
-  double sc, omega;
-};
-
-__device__ __forceinline__ GroupHead group_head(const SlashArgs& a, int64_t s) {
-  GroupHead h{kTile, 0, 0};
-  if (s < a.sessions) {
-    h.tgt = a.target[s];
-    h.b = a.offsets[s];
-    h.n = a.offsets[s + 1] - h.b;
-  }
-  return h;
-}
-
-// Edges (lane j holds edges j, j+16, j+32, j+48), the lane's score and ω — nothing
-// for a session that needs no work here (untouched without fused σ_eff) or that
-// takes the one-lane fallback (> kGroupEdges edges).
-__device__ __forceinline__ GroupBody group_body(const SlashArgs& a, int64_t s, const GroupHead& h, int j) {
-  GroupBody d;
-  const bool fused = a.sigma_eff != nullptr;
-  const bool load = s < a.sessions && h.n <= kGroupEdges && (h.tgt < kTile || fused);
-#pragma unroll
-  for (int c = 0; c < kGroupChunks; ++c) {
-    const int32_t i = c * kSlashGroup + j;
-    const bool in = load && i < h.n;
-    d.vr[c] = in && h.tgt < kTile ? a.voucher[h.b + i] : 0;
-    d.ve[c] = in ? a.vouchee[h.b + i] : -1;
-    d.lv[c] = in && live_edge(a.active, a.expiry_us, h.b + i, a.now_us);
-    d.bd[c] = in && fused ? a.bonded[h.b + i] : 0.0;
-  }
-  d.sc = load ? a.scores[s * kTile + j] : 0.0;
-  d.omega = load ? a.omega[s] : 0.0;
-  return d;
-}
-
-// One session on its 16-lane group: the slash cascade and, when fused, σ_eff.
-__device__ __forceinline__ void slash_group_session(const SlashArgs& a, int64_t s, const GroupHead& h,
-                                                    GroupBody& d, uint8_t* cl, int j, int gl0) {
-  const uint8_t tgt = h.tgt;
-  const int32_t b = h.b, n = h.n;
+__global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_group_kernel(SlashArgs a) {
+  __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
+  const int g = threadIdx.x / kSlashGroup;       // group in block
+  const int j = threadIdx.x % kSlashGroup;       // lane in group
+  const int gw = (threadIdx.x % kWaveLanes) / kSlashGroup;  // group in wave
+  const int gl0 = gw * kSlashGroup;              // first wave lane of the group
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kSlashGroupsPerBlock + g;
+  if (s >= a.sessions) return;
+  // target and edge range in one memory round trip (the range is 8 bytes per
+  // session; the score row, 128 bytes, is only read for slashed sessions)
+  const uint8_t tgt = a.target[s];
+  const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
   const bool fused = a.sigma_eff != nullptr;
   if (tgt >= kTile && !fused) {  // group-uniform: no slash in this session
     if (j == 0) a.clip_count[s] = 0;
@@ -827,14 +791,27 @@ __device__ __forceinline__ void slash_group_session(const SlashArgs& a, int64_t 
   auto group_bits = [&](bool p) -> uint32_t {
     return static_cast<uint32_t>((__ballot(p) >> gl0) & 0xffffu);
   };
-  double sc = d.sc;
-  const double omega = d.omega;
+  int vr[kGroupChunks], ve[kGroupChunks];
+  bool lv[kGroupChunks];
+  double bd[kGroupChunks];
+#pragma unroll
+  for (int c = 0; c < kGroupChunks; ++c) {
+    const int32_t i = c * kSlashGroup + j;
+    const bool in = i < n;
+    vr[c] = in && tgt < kTile ? a.voucher[b + i] : 0;
+    ve[c] = in ? a.vouchee[b + i] : -1;
+    lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
+    bd[c] = in && fused ? a.bonded[b + i] : 0.0;
+  }
+  double sc = a.scores[s * kTile + j];
+  const double omega = a.omega[s];
   if (tgt >= kTile) {  // fused, no slash here: σ_eff only
     if (j == 0) a.clip_count[s] = 0;
-    a.sigma_eff[s * kTile + j] = group_sigma_eff(d.ve, d.lv, d.bd, n, j, gl0, sc, omega);
+    a.sigma_eff[s * kTile + j] = group_sigma_eff(ve, lv, bd, n, j, gl0, sc, omega);
     return;
   }
   const int32_t base = a.clip_offsets[s];
+  uint8_t* cl = s_cl[g];
   int32_t nclip = 0;
   static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
   int32_t next0 = 0, end0 = 0, next1 = 0, end1 = 0;
@@ -848,11 +825,11 @@ __device__ __forceinline__ void slash_group_session(const SlashArgs& a, int64_t 
       const int32_t first = nclip;
 #pragma unroll
       for (int c = 0; c < kGroupChunks; ++c) {
-        uint32_t m = group_bits(d.ve[c] == who && d.lv[c]);
+        uint32_t m = group_bits(ve[c] == who && lv[c]);
         while (m) {
           const int k = __builtin_ctz(m);
           m &= m - 1;
-          const int v = __shfl(d.vr[c], gl0 + k, kWaveLanes);
+          const int v = __shfl(vr[c], gl0 + k, kWaveLanes);
           const double x = __shfl(sc, gl0 + v, kWaveLanes);
           const double before = x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
           const double after = clip_sigma(before, omega);
@@ -867,7 +844,7 @@ __device__ __forceinline__ void slash_group_session(const SlashArgs& a, int64_t 
             }
           }
           if (j == k) {
-            d.lv[c] = false;
+            lv[c] = false;
             a.active[b + c * kSlashGroup + k] = 0;
             a.released_us[b + c * kSlashGroup + k] = a.now_us;
           }
@@ -893,12 +870,12 @@ __device__ __forceinline__ void slash_group_session(const SlashArgs& a, int64_t 
     }
     if (depth == 0) next0 = nx + 1;
     else next1 = nx + 1;
-    const int c8 = cl[nx];  // every clip is cached (≤ kGroupEdges edges ≥ clips); written by lane 0 of this wave
+    const int c8 = cl[nx];  // every clip is cached: a group's session has ≤ kGroupEdges edges ≥ clips  // the LDS write by the group's lane 0 is visible: same wave
     const int v = c8 & 0x7f;
     if (!(c8 & 0x80)) continue;
     bool any_live = false;
 #pragma unroll
-    for (int c = 0; c < kGroupChunks; ++c) any_live = any_live || group_bits(d.ve[c] == v && d.lv[c]) != 0u;
+    for (int c = 0; c < kGroupChunks; ++c) any_live = any_live || group_bits(ve[c] == v && lv[c]) != 0u;
     if (any_live) {
       who = v;
       who_depth = depth + 1;
@@ -907,39 +884,7 @@ __device__ __forceinline__ void slash_group_session(const SlashArgs& a, int64_t 
   }
   a.scores[s * kTile + j] = sc;
   if (j == 0) a.clip_count[s] = nclip;
-  if (fused) a.sigma_eff[s * kTile + j] = group_sigma_eff(d.ve, d.lv, d.bd, n, j, gl0, sc, omega);
-}
-
-// Each group works through kSlashSessionsPerGroup sessions (grid-strided) with a
-// software pipeline: while session i is processed, the edges of session i+1 and
-// the head (target, edge range) of session i+2 are already in flight, so a wave
-// pays the two dependent memory round trips of a CSR session once per group
-// instead of once per session.
-constexpr int kSlashSessionsPerGroup = 4;
-
-__global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_group_kernel(SlashArgs a) {
-  __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
-  const int g = threadIdx.x / kSlashGroup;       // group in block
-  const int j = threadIdx.x % kSlashGroup;       // lane in group
-  const int gw = (threadIdx.x % kWaveLanes) / kSlashGroup;  // group in wave
-  const int gl0 = gw * kSlashGroup;              // first wave lane of the group
-  const int64_t step = static_cast<int64_t>(gridDim.x) * kSlashGroupsPerBlock;
-  int64_t s0 = static_cast<int64_t>(blockIdx.x) * kSlashGroupsPerBlock + g;
-  GroupHead h0 = group_head(a, s0);
-  GroupBody d0 = group_body(a, s0, h0, j);
-  int64_t s1 = s0 + step;
-  GroupHead h1 = group_head(a, s1);
-  while (s0 < a.sessions) {
-    GroupBody d1 = group_body(a, s1, h1, j);
-    const int64_t s2 = s1 + step;
-    const GroupHead h2 = group_head(a, s2);
-    slash_group_session(a, s0, h0, d0, s_cl[g], j, gl0);
-    s0 = s1;
-    h0 = h1;
-    d0 = d1;
-    s1 = s2;
-    h1 = h2;
-  }
+  if (fused) a.sigma_eff[s * kTile + j] = group_sigma_eff(ve, lv, bd, n, j, gl0, sc, omega);
 }
 
 void launch_slash(const SlashArgs& a, hipStream_t st) {
@@ -952,7 +897,7 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
     if (a.sigma_eff) hipLaunchKernelGGL(slash_sigma_kernel, grid1(a.sessions * kTile), dim3(kBlock), 0, st, a);
   } else {
-    hipLaunchKernelGGL(slash_group_kernel, grid1(a.sessions, kSlashGroupsPerBlock * kSlashSessionsPerGroup),
+    hipLaunchKernelGGL(slash_group_kernel, grid1(a.sessions, kSlashGroupsPerBlock),
                        dim3(kSlashGroup * kSlashGroupsPerBlock), 0, st, a);
   }
   check_hip(hipGetLastError(), "slash_kernel");
