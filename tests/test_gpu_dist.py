@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -19,17 +18,16 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+# --standalone: the rendezvous binds a port the OS picks at bind time (a port probed
+# here and bound later by torchrun can be taken in between: EADDRINUSE)
+_LAUNCH = ["-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+           "--nproc-per-node", "1"]
 
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_bench_rccl_path_one_rank(cuda_device, graph):
     env = dict(os.environ, AHV_BENCH_FORCE_DIST="1", AHV_SKIP_AUTOBUILD="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+    cmd = [sys.executable, *_LAUNCH, os.path.join(ROOT, "bench.py"),
            "--gpus", "1", "--sessions", "65536", "--agents", "65536", "--steps", "3", "--warmup", "1",
            "--no-scalar"] + (["--graph"] if graph else [])
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
@@ -43,9 +41,7 @@ def test_sharded_hypervisor_rccl_one_rank(cuda_device):
     """The sharded front-end's collectives (X01/X04/X05 on RCCL, control on gloo)
     with the device store, under torch.distributed.run — the 8-GPU code path."""
     env = dict(os.environ, AHV_SKIP_AUTOBUILD="1", PYTHONPATH=ROOT)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(ROOT, "scripts", "sharded_rccl_check.py")]
+    cmd = [sys.executable, *_LAUNCH, os.path.join(ROOT, "scripts", "sharded_rccl_check.py")]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
