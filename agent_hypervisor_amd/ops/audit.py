@@ -200,7 +200,7 @@ def pack_chains(chains, device="cpu") -> dict:
 
 def chain_hashes(packed: dict, seed_parent: Optional[torch.Tensor] = None,
                  has_seed: Optional[torch.Tensor] = None, midstate: bool = True,
-                 uniform_len: int = 0, sel: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 uniform_len: int = 0, sel: Optional[torch.Tensor] = None, check: bool = True) -> torch.Tensor:
     """K08: re-derive every delta hash of every chain (parent links recomputed
     from the chain itself) → int32 [D, 8].
 
@@ -216,12 +216,17 @@ def chain_hashes(packed: dict, seed_parent: Optional[torch.Tensor] = None,
     ``sel`` (int64 [chains], with ``uniform_len``) reads chain c's spans from
     rows ``sel[c]·len …`` of the span tables in ``packed`` — resident
     per-session tables — instead of gathering them per call; ``chain_offsets``
-    must then be the uniform ``c·len``.  Digests come back in chain order."""
+    must then be the uniform ``c·len``.  Digests come back in chain order.
+    ``check=False`` skips the range check of ``sel`` (a device sync) when the
+    caller guarantees every row exists."""
     dev = packed["bytes"].device
     chains = packed["chain_offsets"].numel() - 1
     if sel is not None:
         if uniform_len <= 0 or sel.numel() != chains:
             raise ValueError("sel needs uniform_len and one row per chain")
+        rows = min(packed[k].numel() for k in ("pre_off", "pre_len", "suf_off", "suf_len")) // uniform_len
+        if check and chains and not (0 <= int(sel.min()) and int(sel.max()) < rows):
+            raise ValueError(f"sel rows outside the span tables' {rows} rows")
         D = chains * uniform_len
     else:
         D = packed["pre_off"].numel()

@@ -32,6 +32,8 @@ def test_arena_chains_match_scalar_delta_engine():
     assert A.digests_to_hex(A.chain_hashes(packed, uniform_len=D + 1)) == dig
     res, sel = arena.resident(touched)
     assert A.digests_to_hex(A.chain_hashes(res, uniform_len=D + 1, sel=sel)) == dig
+    with pytest.raises(ValueError):
+        A.chain_hashes(res, uniform_len=D + 1, sel=torch.tensor([0, 7, 13, S]))
     for i, s in enumerate(touched.tolist()):
         tag = f"{s:07d}"
         _clock.set_clock(lambda s=s: datetime(2026, 3, 1, 12, 0, 0, s % 999_999 + 1, tzinfo=timezone.utc))
