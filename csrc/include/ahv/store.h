@@ -1493,7 +1493,17 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
         return;
       }
       const bool close = c.op == OP_SESS_CLOSE;
-      const uint8_t st0 = bcast(L, L.leader() ? t.s_state[s] : uint8_t(0));
+      // the row words this command reads, requested together (one memory round
+      // trip for the lone command wave instead of one per check)
+      uint8_t st_raw = 0;
+      int64_t dcount_raw = 0, proot_n_raw = 0, proot_last_raw = 0;
+      if (L.leader()) {
+        st_raw = t.s_state[s];
+        dcount_raw = static_cast<int64_t>(t.s_dcount[s]);
+        proot_n_raw = static_cast<int64_t>(t.s_proot_n[s]);
+        proot_last_raw = static_cast<int64_t>(t.s_proot_last[s]);
+      }
+      const uint8_t st0 = bcast(L, st_raw);
       if (close && !((session_op_allowed_from(OP_TERMINATE) >> st0) & 1u)) {
         if (L.leader()) {
           out64(r + 2, st0);
@@ -1501,7 +1511,7 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
         }
         return;
       }
-      if (n != bcast(L, L.leader() ? static_cast<int64_t>(t.s_dcount[s]) : int64_t(0))) {
+      if (n != bcast(L, dcount_raw)) {
         if (L.leader()) out64(r + 1, ST_BAD_ARG);
         return;
       }
@@ -1517,8 +1527,8 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
       const bool want_root = n > 0 && (!close || c.a[6]);
       // the hash engine's provisional root, when it covers exactly these leaves
       const IndexList il = index_list(t, c, static_cast<uint64_t>(n), c.a[2]);
-      const bool have = want_root && bcast(L, L.leader() ? static_cast<int>(t.s_proot_n[s] == n &&
-                                                                            t.s_proot_last[s] == il[n - 1])
+      const bool have = want_root && bcast(L, L.leader() ? static_cast<int>(proot_n_raw == n &&
+                                                                            proot_last_raw == il[n - 1])
                                                          : 0) != 0;
       if (want_root && !have) merkle_inplace(L, lv, n);  // K09
       if (!L.leader()) return;

@@ -259,7 +259,11 @@ class Hypervisor:
         root = _hex(r[2:10]) if r[1] else None
         if root:
             self.commitment.register(sso)
-        self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de, delta_count=de.turn_count)
+        # the device counted the deltas past retention (r[12]); with none expired the
+        # host GC has nothing to prune and needs no walk over the delta views
+        expired = int(r[12])
+        self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de if expired else None,
+                        delta_count=de.turn_count if expired else n)
         if self.event_bus is not None:
             from hypervisor.observability.event_bus import EventType
 
