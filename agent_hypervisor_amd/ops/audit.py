@@ -93,20 +93,14 @@ def goal_hashes(goals: Sequence[str], step_ids: Sequence[str], device="cpu") -> 
     return [h[:16] for h in digests_to_hex(sha256_many(data, offs))]
 
 
-def merkle_roots(offsets: torch.Tensor, leaves: torch.Tensor, uniform_len: int = 0) -> torch.Tensor:
-    """K09: Merkle root of each chain of leaf digests (zeros for empty chains).
-
-    ``uniform_len`` (1..64) promises every chain has exactly that many leaves
-    (``offsets`` = c·len): the device then reduces all chains level-synchronously,
-    one lane per interior node, instead of one lane per chain."""
+def merkle_roots(offsets: torch.Tensor, leaves: torch.Tensor) -> torch.Tensor:
+    """K09: Merkle root of each chain of leaf digests (zeros for empty chains)."""
     chains = offsets.numel() - 1
-    if uniform_len and not (0 < uniform_len <= 64 and chains * uniform_len == leaves.shape[0]):
-        raise ValueError(f"uniform_len={uniform_len} does not match {chains} chains of {leaves.shape[0]} leaves")
     root = torch.empty((chains, 8), dtype=i32, device=leaves.device)
     scratch = torch.empty_like(leaves)
     launch(
         "merkle",
-        {"chains": chains, "uniform_len": int(uniform_len)},
+        {"chains": chains},
         dict(offsets=offsets, leaves=leaves, scratch=scratch, root=root),
         dict(offsets=i32, leaves=i32),
     )

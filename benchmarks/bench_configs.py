@@ -432,7 +432,7 @@ def config5(ctx: Ctx, args):
         arena.write_slash_deltas(touched, out.scores)
         packed, sel = arena.resident(touched)
         digests = A.chain_hashes(packed, midstate=not args.no_midstate, uniform_len=D + 1, sel=sel, check=False)
-        roots = A.merkle_roots(packed["chain_offsets"], digests, uniform_len=D + 1)
+        roots = A.merkle_roots(packed["chain_offsets"], digests)
         last.update(T=touched.numel(), roots=roots)
         return se
 

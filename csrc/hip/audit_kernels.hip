@@ -445,59 +445,8 @@ __global__ __launch_bounds__(kWaveLanes) void merkle_kernel(MerkleArgs a) {
        c += static_cast<int64_t>(gridDim.x) * blockDim.x)
     merkle_elem(a, c);
 }
-// Many chains of one length (≤ 64 leaves): a 256-thread workgroup owns
-// G = 256 / ⌈len/2⌉ chains, stages their leaves in LDS and reduces them level by
-// level, one lane per interior node (odd levels pair their last node with itself,
-// as the reference) — every node of a level in parallel instead of one lane
-// walking a whole chain.  Nodes are written back in place after a barrier.
-constexpr int kMerkleUniThreads = 256;
-constexpr int kMerkleUniDigests = 2 * kMerkleUniThreads;  // G·len ≤ 512
-
-__global__ __launch_bounds__(kMerkleUniThreads) void merkle_uniform_kernel(MerkleArgs a) {
-  __shared__ uint32_t buf[kMerkleUniDigests * 8];
-  const int len = a.uniform_len;
-  const int half0 = (len + 1) >> 1;
-  const int G = kMerkleUniThreads / half0;
-  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * G;
-  const int gc = c0 + G <= a.chains ? G : static_cast<int>(a.chains - c0);  // chains in this block
-  const int64_t w0 = c0 * len * 8;
-  for (int w = threadIdx.x; w < gc * len * 8; w += kMerkleUniThreads) buf[w] = a.leaves[w0 + w];
-  __syncthreads();
-  for (int m = len; m > 1; m = (m + 1) >> 1) {
-    const int half = (m + 1) >> 1;
-    const int ch = threadIdx.x / half, j = threadIdx.x - ch * half;
-    uint32_t o[8];
-    const bool act = ch < gc;
-    if (act) {
-      uint32_t l[8], r[8];
-      const int li = 2 * j, ri = 2 * j + 1 < m ? 2 * j + 1 : 2 * j;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        l[k] = buf[(ch * len + li) * 8 + k];
-        r[k] = buf[(ch * len + ri) * 8 + k];
-      }
-      merkle_node(l, r, o);
-    }
-    __syncthreads();
-    if (act)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) buf[(ch * len + j) * 8 + k] = o[k];
-    __syncthreads();
-  }
-  for (int w = threadIdx.x; w < gc * 8; w += kMerkleUniThreads) {
-    const int ch = w >> 3, k = w & 7;
-    a.root[(c0 + ch) * 8 + k] = buf[ch * len * 8 + k];
-  }
-}
-
 void launch_merkle(const MerkleArgs& a, hipStream_t st) {
   if (a.chains <= 0) return;
-  if (a.uniform_len > 0) {
-    const int G = kMerkleUniThreads / ((a.uniform_len + 1) >> 1);
-    hipLaunchKernelGGL(merkle_uniform_kernel, grid1(a.chains, G), dim3(kMerkleUniThreads), 0, st, a);
-    check_hip(hipGetLastError(), "merkle_uniform_kernel");
-    return;
-  }
   hipLaunchKernelGGL(merkle_kernel, grid1(a.chains, 64), dim3(64), 0, st, a);
   check_hip(hipGetLastError(), "merkle_kernel");
 }
@@ -562,7 +511,6 @@ void kernels_audit(std::vector<KernelEntry>& out) {
   out.push_back({"render_rows_kernel", reinterpret_cast<const void*>(&render_rows_kernel)});
   out.push_back({"render_rows_fast_kernel", reinterpret_cast<const void*>(&render_rows_fast_kernel)});
   out.push_back({"merkle_kernel", reinterpret_cast<const void*>(&merkle_kernel)});
-  out.push_back({"merkle_uniform_kernel", reinterpret_cast<const void*>(&merkle_uniform_kernel)});
   out.push_back({"hash_many_kernel", reinterpret_cast<const void*>(&hash_many_kernel)});
   out.push_back({"verify_delta_kernel", reinterpret_cast<const void*>(&verify_delta_kernel)});
 }

@@ -254,8 +254,6 @@ static MerkleArgs to_merkle(const py::dict& d) {
   MerkleArgs a{};
   V(chains, int64_t); P(offsets, const int32_t); P(leaves, const uint32_t); P(scratch, uint32_t);
   P(root, uint32_t);
-  a.uniform_len = d.contains("uniform_len") ? d["uniform_len"].cast<int32_t>() : 0;
-  if (a.uniform_len < 0 || a.uniform_len > 64) throw py::value_error("merkle: uniform_len must be 0..64");
   return a;
 }
 static VerifyArgs to_verify(const py::dict& d) {

@@ -337,9 +337,6 @@ struct MerkleArgs {
   const uint32_t* leaves;  // [L, 8]
   uint32_t* scratch;       // [L, 8] level buffer
   uint32_t* root;          // [chains, 8] (zeros for empty chains)
-  // 1..64: every chain has exactly this many leaves (offsets = c·len); the device
-  // then reduces the chains level-synchronously in LDS, one lane per node
-  int32_t uniform_len;
 };
 void launch_merkle(const MerkleArgs&, hipStream_t);
 void merkle_host(const MerkleArgs&);

@@ -49,36 +49,3 @@ def test_tree_on_gfx950_matches_host(cuda_device, n):
     got = merkle_tree_root(lv.to(cuda_device))
     torch.cuda.synchronize()
     assert _hex(got.cpu().tolist()) == want
-
-
-def _uniform_batch(chains: int, length: int, seed: int):
-    g = torch.Generator().manual_seed(seed)
-    leaves = torch.randint(-2**31, 2**31 - 1, (chains * length, 8), dtype=torch.int32, generator=g)
-    offs = (torch.arange(chains + 1) * length).to(torch.int32)
-    return offs, leaves
-
-
-def test_uniform_len_validated_and_host_equal():
-    from agent_hypervisor_amd.ops.audit import merkle_roots
-
-    offs, leaves = _uniform_batch(7, 5, 1)
-    assert torch.equal(merkle_roots(offs, leaves, uniform_len=5), merkle_roots(offs, leaves))
-    with pytest.raises(ValueError):
-        merkle_roots(offs, leaves, uniform_len=4)
-    with pytest.raises(ValueError):
-        merkle_roots(offs, leaves, uniform_len=65)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("length", [1, 2, 3, 4, 5, 7, 8, 9, 16, 33, 64])
-def test_uniform_level_kernel_on_gfx950(cuda_device, length):
-    """Level-synchronous K09 over many equal-length chains (LDS, one lane per node)
-    == the per-chain kernel == the host twin, with a ragged last workgroup."""
-    from agent_hypervisor_amd.ops.audit import merkle_roots
-
-    chains = 1000 + length  # not a multiple of the chains per workgroup
-    offs, leaves = _uniform_batch(chains, length, length)
-    want = merkle_roots(offs, leaves)
-    got = merkle_roots(offs.cuda(), leaves.cuda(), uniform_len=length).cpu()
-    assert torch.equal(got, want)
-    assert torch.equal(merkle_roots(offs.cuda(), leaves.cuda()).cpu(), want)
