@@ -167,6 +167,13 @@ __global__ __launch_bounds__(kBlock) void render_rows_kernel(RenderArgs a) {
 // streams the finished row out with word stores.  Per-byte ALU work only where
 // the row differs from the template.
 constexpr int kRenderFastLen = 2048;
+
+// Wave-scope LDS hand-off: release/acquire fences plus the wave barrier.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __global__ __launch_bounds__(kBlock) void render_rows_fast_kernel(RenderArgs a) {
   __shared__ uint32_t s_tmpl[kRenderFastLen / 4];
   __shared__ uint32_t s_row[kRenderRowsPerBlock][kRenderFastLen / 4];
@@ -179,7 +186,6 @@ __global__ __launch_bounds__(kBlock) void render_rows_fast_kernel(RenderArgs a) 
   __syncthreads();
   uint32_t* row = s_row[wave];
   uint8_t* rb = reinterpret_cast<uint8_t*>(row);
-  // the row-group loop runs the same number of times in every wave of the block
   for (int64_t base = static_cast<int64_t>(blockIdx.x) * kRenderRowsPerBlock; base < a.rows;
        base += static_cast<int64_t>(gridDim.x) * kRenderRowsPerBlock) {
     const int64_t r = base + wave;
@@ -187,7 +193,9 @@ __global__ __launch_bounds__(kBlock) void render_rows_fast_kernel(RenderArgs a) 
     const int64_t id = act ? a.ids[r] : 0;
     if (act)
       for (int32_t w = lane; w < nw; w += 64) row[w] = s_tmpl[w];
-    __syncthreads();
+    // each wave owns its row: a wave barrier orders the LDS phases (a wave's LDS
+    // instructions execute in order; the barrier keeps the compiler from moving them)
+    wave_lds_sync();
     if (act) {
       uint64_t sv[kRenderMaxStamps];
       render_stamp_values(a, id, sv);
@@ -222,12 +230,12 @@ __global__ __launch_bounds__(kBlock) void render_rows_fast_kernel(RenderArgs a) 
         }
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     if (act) {
       uint32_t* dst = reinterpret_cast<uint32_t*>(a.out + id * a.pitch);
       for (int32_t w = lane; w < nw; w += 64) dst[w] = row[w];
     }
-    __syncthreads();
+    wave_lds_sync();
   }
 }
 
