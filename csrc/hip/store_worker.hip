@@ -166,11 +166,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
           jb.off = bcast(L, job.off);
           jb.hole = jhole;
           uint32_t mid[8];
-          // stop between blocks as soon as the next command has arrived (it is
-          // answered first; the hash engine finishes the remaining blocks)
-          const int32_t pb = capture_prefix(L, t, jb, lds0, kLdsWords / 4, 4, mid, [&]() -> bool {
-            return (speculate & 4) == 0 && __shfl(ld_sys(nslot + lane), 0) == next + 2;
-          });
+          const int32_t pb = capture_prefix(L, t, jb, lds0, kLdsWords / 4, 4, mid);
           if (lane == 0 && pb > 0) {
             job.mid_blocks = pb;
             for (int k = 0; k < 8; ++k) job.mid[k] = mid[k];

@@ -85,13 +85,10 @@ class Store {
       hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "store stream");
       idle_ticks_ = static_cast<uint64_t>(idle_us) * 100;   // s_memrealtime: 100 MHz
       // worker feature bits: 1 = provisional Merkle roots on the idle hash engine,
-      // 2 = capture prefix midstates on the command wave, 4 = never cut a prefix
-      // short for a waiting command (A/B of the per-block stop)
+      // 2 = capture prefix midstates on the command wave
       const char* sp = std::getenv("AHV_STORE_SPECULATE");
       const char* pf = std::getenv("AHV_STORE_PREFIX");
-      const char* ns = std::getenv("AHV_STORE_PREFIX_NOSTOP");
-      speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
-                   ((ns != nullptr && std::atoi(ns) != 0) ? 4 : 0);
+      speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0);
       max_ticks_ = static_cast<uint64_t>(max_ms) * 100000;
     } else {
       ring_ = static_cast<uint64_t*>(std::calloc(ring_bytes / 8, 8));

@@ -588,14 +588,8 @@ AHV_HD void sha256_lds_blocks_par(const Lanes& L, const uint32_t* w, int64_t nbl
 // puts agent_did, changes and delta_id first), so the command
 // wave compresses them while the hash engine is still busy with the parent.
 // At most `max_blocks`; returns the count (0: nothing to do).  Valid on the leader.
-// `stop()` (wave-uniform) is polled between blocks: when another command is
-// waiting, the blocks done so far are handed over (the job resumes from them).
-struct NeverStop {
-  AHV_HD bool operator()() const { return false; }
-};
-template <class Stop = NeverStop>
 AHV_HD int32_t capture_prefix(const Lanes& L, const Tables& t, const HashJob& j, uint32_t* w, int64_t cap_words,
-                              int32_t max_blocks, uint32_t mid[8], const Stop& stop = Stop{}) {
+                              int32_t max_blocks, uint32_t mid[8]) {
   if (j.hole < 64) return 0;
   int64_t pb = j.hole / 64;
   if (pb > max_blocks) pb = max_blocks;
@@ -603,14 +597,9 @@ AHV_HD int32_t capture_prefix(const Lanes& L, const Tables& t, const HashJob& j,
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(t.payload + j.off);
   for (int64_t i = L.lane; i < pb * 16; i += L.n) w[i] = bswap32(ld32f(s32 + i));
   L.sync();
-  int32_t done = 0;
-  for (int64_t b = 0; b < pb; ++b) {
-    sha256_lds_blocks_par(L, w + 16 * b, 1, mid, b ? mid : nullptr);
-    L.sync();
-    ++done;
-    if (b + 1 < pb && stop()) break;
-  }
-  return done;
+  sha256_lds_blocks_par(L, w, pb, mid);
+  L.sync();
+  return static_cast<int32_t>(pb);
 }
 
 // Provisional Merkle root (hash-engine wave, while it would otherwise idle):
