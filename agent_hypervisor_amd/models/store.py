@@ -14,10 +14,9 @@ CPU tensors — the host twin the CPU suite and the reference oracle run against
 
 One store per (process, device) is shared by every ``Hypervisor`` on it
 (:func:`shared_store`): the reference benchmark builds a fresh ``Hypervisor()``
-per pipeline, which must not allocate tables each time.  Rows are recycled ring
-style when a table wraps; the default capacities (``AHV_STORE_*``) size one GPU
-for ~65 k live sessions — raise them for resident populations (a session row is
-≈1.1 KB with 32 participant rows; 288 GB holds >10⁸).
+per pipeline, which must not allocate tables each time.  Rows are recycled
+only once no API object refers to them (never while live); full tables grow by
+doubling up to ``AHV_STORE_MAX_*`` (defaults sized for 288 GB of HBM3E).
 """
 
 from __future__ import annotations
@@ -79,14 +78,74 @@ def default_caps() -> dict:
     }
 
 
+def default_max_caps() -> dict:
+    """Growth ceilings (``AHV_STORE_MAX_*``): sized for one 288 GB MI355X — a session
+    row with 32 participant rows is ≈1.4 KB, a delta row 72 B + its ≈300 B record."""
+    return {
+        "S": _env_int("AHV_STORE_MAX_SESSIONS", 1 << 25),
+        "D": _env_int("AHV_STORE_MAX_DELTAS", 1 << 28),
+        "E": _env_int("AHV_STORE_MAX_VOUCHES", 1 << 28),
+        "V": _env_int("AHV_STORE_MAX_LIABILITY_SESSIONS", 1 << 25),
+        "G": _env_int("AHV_STORE_MAX_SAGAS", 1 << 25),
+        "T": _env_int("AHV_STORE_MAX_STEPS", 1 << 26),
+        "B": _env_int("AHV_STORE_MAX_PAYLOAD", 1 << 37),
+    }
+
+
+_KIND = {"S": 0, "G": 1, "T": 2, "E": 3, "D": 4, "V": 5}  # csrc/include/ahv/store.h RowKind
+_EXT_OF = {"S": ("S", "S4", "S8", "SP"), "D": ("D", "D8"), "E": ("E",), "V": ("V",), "G": ("G",), "T": ("T",)}
+_FILL_NEG = ("v_head", "v_tail", "s_dlast", "d_prev", "e_next", "d_sess", "e_vsess", "t_saga")
+_FILL_FREE = ("s_state", "g_state", "t_state")  # kFree8
+
+
+def _fill(name: str) -> int:
+    return -1 if name in _FILL_NEG else (255 if name in _FILL_FREE else 0)
+
+
+def _extents(c: dict) -> dict:
+    return {
+        "S": c["S"], "S4": c["S"] * 4, "S8": c["S"] * 8, "SP": c["S"] * c["P"],
+        "D": c["D"], "D8": c["D"] * 8, "E": c["E"], "V": c["V"], "G": c["G"], "T": c["T"], "SCR": c["X"],
+    }
+
+
 class StoreError(RuntimeError):
     """A store command failed for a reason the API layer does not map to a user error."""
 
 
-class GovernanceStore:
-    """Device tables + command transport + host-side allocators/interners."""
+class _Rows:
+    """Host allocator of one table: LIFO free list of reclaimed rows + high-water mark."""
 
-    def __init__(self, device: str = "cuda", caps: Optional[dict] = None, idle_us: Optional[int] = None) -> None:
+    __slots__ = ("cap", "hw", "free")
+
+    def __init__(self, cap: int) -> None:
+        self.cap = cap
+        self.hw = 0
+        self.free: list[int] = []
+
+    @property
+    def live(self) -> int:
+        return self.hw - len(self.free)
+
+
+class GovernanceStore:
+    """Device tables + command transport + host-side allocators/interners.
+
+    Row lifecycle: every session / saga / step / vouch-edge / delta row is handed
+    out by a host allocator and is *live* while an API object refers to it (the
+    view objects of :mod:`hypervisor._device` own their rows; dropping the last
+    reference queues the row in ``_pending`` from ``__del__``).  Queued rows are
+    reclaimed in batches: one ``OP_FREE_ROWS`` command marks them free on the
+    device (after the hash engine has drained), then they return to the free
+    list.  Creates on the device refuse a row that is not free, so a live row is
+    never overwritten.  A full table grows (capacity doubles, rows keep their
+    index) up to ``AHV_STORE_MAX_*``, then allocation raises :class:`StoreError`.
+    """
+
+    RECLAIM_BATCH = 256
+
+    def __init__(self, device: str = "cuda", caps: Optional[dict] = None, idle_us: Optional[int] = None,
+                 max_caps: Optional[dict] = None) -> None:
         dev = torch.device(device)
         if dev.type == "cuda":
             if not torch.cuda.is_available():
@@ -97,16 +156,15 @@ class GovernanceStore:
             raise ValueError(f"unsupported store device {dev}")
         self.device = dev
         self.caps = dict(default_caps(), **(caps or {}))
+        self.max_caps = dict(default_max_caps(), **(max_caps or {}))
+        for k, v in self.caps.items():
+            if k in self.max_caps and self.max_caps[k] < v:
+                self.max_caps[k] = v
         c = self.caps
-        ext = {
-            "S": c["S"], "S4": c["S"] * 4, "S8": c["S"] * 8, "SP": c["S"] * c["P"],
-            "D": c["D"], "D8": c["D"] * 8, "E": c["E"], "V": c["V"], "G": c["G"], "T": c["T"], "SCR": c["X"],
-        }
+        ext = _extents(c)
         self.tables: dict[str, torch.Tensor] = {}
         for name, ctype, kind in C.STORE_COLUMNS:
-            fill = -1 if name in ("v_head", "v_tail", "s_dlast", "d_prev", "e_next") else 0
-            self.tables[name] = torch.full((ext[kind],), fill, dtype=_DTYPES[ctype], device=dev)
-        self.tables["s_state"].fill_(255)
+            self.tables[name] = torch.full((ext[kind],), _fill(name), dtype=_DTYPES[ctype], device=dev)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         ptrs = {k: v.data_ptr() for k, v in self.tables.items()}
@@ -115,25 +173,133 @@ class GovernanceStore:
             idle_us=idle_us if idle_us is not None else _env_int("AHV_STORE_IDLE_US", 500),
         )
         self._lock = threading.RLock()
+        self._closed = False
         self.agents = Interner()  # DID → dense agent id
-        self.keys = Interner()  # (tenant, session id) liability keys → dense liability-session id
-        self._next = {"S": 0, "E": 0, "G": 0, "T": 0}
+        self._rows = {k: _Rows(c[k]) for k in ("S", "G", "T", "E", "V")}
+        self._pending: dict[str, list] = {k: [] for k in ("S", "G", "T", "E", "V", "D")}
+        self._tenant_v: dict[int, dict[str, int]] = {}  # tenant → liability session id → V row
         self._tenants = 0
+        self.grows = {k: 0 for k in ("S", "G", "T", "E", "V", "D", "B")}
         self.seed = int.from_bytes(os.urandom(8), "little") >> 1
 
     # -- allocation ----------------------------------------------------------
     def alloc(self, kind: str) -> int:
-        """Next row of table ``kind`` (S sessions, E vouch edges, G sagas, T steps)."""
-        i = self._next[kind]
-        cap = self.caps[kind]
-        if kind == "E" and i >= cap:
-            raise StoreError(f"vouch table full ({cap} edges); raise AHV_STORE_VOUCHES")
-        self._next[kind] = i + 1
-        return i % cap
+        """A free row of table ``kind`` (S sessions, E vouch edges, G sagas, T steps, V liability sessions)."""
+        rows = self._rows[kind]
+        if len(self._pending[kind]) >= self.RECLAIM_BATCH:
+            self.reclaim(kind)
+        if rows.free:
+            return rows.free.pop()
+        if rows.hw < rows.cap:
+            i = rows.hw
+            rows.hw = i + 1
+            return i
+        if self._room(kind):
+            return self.alloc(kind)
+        self._grow(kind)
+        return self.alloc(kind)
+
+    def _room(self, kind: str) -> bool:
+        """Table ``kind`` is full: reclaim queued rows, then (once) collect unreachable
+        API views — chains of delta views are reference cycles only the cyclic
+        collector frees — before the caller grows the table."""
+        import gc
+
+        if self._pending[kind] and self.reclaim(kind):
+            return True
+        gc.collect()
+        return bool(self._pending[kind]) and self.reclaim(kind) > 0
+
+    def release(self, kind: str, row: int) -> None:
+        """Queue a row whose last API reference is gone (safe to call from ``__del__``)."""
+        self._pending[kind].append(row)
+
+    def release_many(self, kind: str, rows) -> None:
+        self._pending[kind].extend(rows)
+
+    def reclaim(self, kind: Optional[str] = None) -> int:
+        """Return queued rows to the free lists (one OP_FREE_ROWS per table); returns the count."""
+        total = 0
+        with self._lock:
+            for k in ([kind] if kind else list(self._pending)):
+                pend = self._pending[k]
+                n = len(pend)
+                if not n:
+                    continue
+                rows = pend[:n]
+                del pend[:n]  # rows queued meanwhile (GC during this call) stay queued
+                if self._closed:
+                    continue
+                if k == "D":
+                    self._c.free_deltas(rows)
+                else:
+                    self._c.free_rows(_KIND[k], rows)
+                    self._rows[k].free.extend(rows)
+                total += n
+        return total
+
+    def live_rows(self) -> dict:
+        out = {k: r.live for k, r in self._rows.items()}
+        out["D"] = self._c.delta_live
+        return out
+
+    def _grow(self, kind: str) -> None:
+        """Double table ``kind`` (rows keep their indices), up to its ``AHV_STORE_MAX_*``."""
+        cur, mx = self.caps[kind], self.max_caps[kind]
+        if cur >= mx:
+            raise StoreError(
+                f"store table {kind} full ({cur} live rows; ceiling AHV_STORE_MAX_* = {mx}): refusing to reuse live rows")
+        new = min(mx, 2 * cur)
+        with self._lock:
+            self.drain()
+            self._c.quiesce()
+            caps = dict(self.caps, **{kind: new})
+            ext = _extents(caps)
+            grown = set(_EXT_OF[kind])
+            for name, ctype, ek in C.STORE_COLUMNS:
+                if ek not in grown:
+                    continue
+                old = self.tables[name]
+                t = torch.full((ext[ek],), _fill(name), dtype=old.dtype, device=self.device)
+                t[: old.numel()].copy_(old)
+                self.tables[name] = t
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.caps = caps
+            if kind in self._rows:
+                self._rows[kind].cap = new
+            self._c.rebind({k: v.data_ptr() for k, v in self.tables.items()}, dict(caps))
+            self.grows[kind] += 1
+
+    def _grow_payload(self) -> None:
+        cur, mx = self._c.payload_cap, self.max_caps["B"]
+        if cur >= mx:
+            raise StoreError(f"audit payload arena full ({cur} bytes; ceiling AHV_STORE_MAX_PAYLOAD)")
+        with self._lock:
+            self.drain()
+            self._c.grow_payload(min(mx, 2 * cur))
+            self.caps["B"] = self._c.payload_cap
+            self.grows["B"] += 1
+
+    def _make_room(self, code: int, tries: int) -> None:
+        """capture / restore_delta reported a full table (-2 deltas, -3 arena)."""
+        if tries == 0 and self._room("D"):
+            return
+        if code == -2:
+            self._grow("D")
+        else:
+            self._grow_payload()
 
     def new_tenant(self) -> int:
         self._tenants += 1
         return self._tenants
+
+    def release_tenant(self, tenant: int, edges) -> None:
+        """A vouching engine is gone: its edge rows and liability-session rows are reclaimable."""
+        self._pending["E"].extend(edges)
+        vs = self._tenant_v.pop(tenant, None)
+        if vs:
+            self._pending["V"].extend(vs.values())
 
     def agent_id(self, did: str) -> int:
         return self.agents.intern(did)
@@ -142,13 +308,17 @@ class GovernanceStore:
         return self.agents.str(agent_id)
 
     def liability_id(self, tenant: int, session_id: str) -> int:
-        v = self.keys.intern(f"{tenant}\x00{session_id}")
-        if v >= self.caps["V"]:
-            raise StoreError(f"liability-session table full ({self.caps['V']}); raise AHV_STORE_LIABILITY_SESSIONS")
+        d = self._tenant_v.get(tenant)
+        if d is None:
+            d = self._tenant_v[tenant] = {}
+        v = d.get(session_id)
+        if v is None:
+            v = d[session_id] = self.alloc("V")
         return v
 
     def liability_lookup(self, tenant: int, session_id: str) -> int:
-        return self.keys.lookup(f"{tenant}\x00{session_id}")
+        d = self._tenant_v.get(tenant)
+        return -1 if d is None else d.get(session_id, -1)
 
     # -- transport -----------------------------------------------------------
     def post(self, op: int, args: list, inline: Optional[bytes] = None) -> int:
@@ -170,7 +340,34 @@ class GovernanceStore:
         return self._c.payload(off, n)
 
     def capture(self, slot: int, turn: int, ts_us: int, delta) -> tuple:
-        return self._c.capture(slot, turn, ts_us, delta)
+        if len(self._pending["D"]) >= self.RECLAIM_BATCH:
+            self.reclaim("D")
+        r = self._c.capture(slot, turn, ts_us, delta)
+        tries = 0
+        while r[0] <= -2:
+            self._make_room(r[0], tries)
+            tries += 1
+            r = self._c.capture(slot, turn, ts_us, delta)
+        return r
+
+    def capture_bytes(self, slot: int, turn: int, ts_us: int, raw: bytes, null_at: int) -> tuple:
+        r = self._c.capture_bytes(slot, turn, ts_us, raw, null_at)
+        tries = 0
+        while r[0] <= -2:
+            self._make_room(r[0], tries)
+            tries += 1
+            r = self._c.capture_bytes(slot, turn, ts_us, raw, null_at)
+        return r
+
+    def restore_delta(self, data: bytes) -> tuple:
+        """(delta row, arena offset) for a checkpointed record."""
+        r = self._c.restore_delta(data)
+        tries = 0
+        while r[0] <= -2:
+            self._make_room(r[0], tries)
+            tries += 1
+            r = self._c.restore_delta(data)
+        return r
 
     def drain(self) -> None:
         self._c.drain()
@@ -184,6 +381,7 @@ class GovernanceStore:
         self.call(OP_ACQUIRE, [], 1)
 
     def close(self) -> None:
+        self._closed = True
         self._c.close()
 
     @property
@@ -191,7 +389,11 @@ class GovernanceStore:
         return self._c.gpu
 
     def info(self) -> dict:
-        return dict(self._c.info())
+        d = dict(self._c.info())
+        d["live_rows"] = self.live_rows()
+        d["caps"] = dict(self.caps)
+        d["grows"] = dict(self.grows)
+        return d
 
     def write_rows(self, rows: dict) -> None:
         """Scatter host values into table rows: ``{column: (indices, values)}``.
@@ -218,18 +420,42 @@ class GovernanceStore:
             torch.cuda.synchronize(self.device)
             self.acquire()
 
-    def payload_append(self, data: bytes) -> int:
-        return self._c.payload_append(data)
-
-    def alloc_delta(self) -> int:
-        return self._c.alloc_delta()
-
     def column(self, name: str) -> torch.Tensor:
-        """A table column (flushes pending device writes first)."""
+        """A table column as the worker last wrote it (flushes pending device writes
+        first).  Growth replaces the tensors: fetch a column again after creating rows."""
         self.drain()
         if self.device.type == "cuda":
             self.flush()
         return self.tables[name]
+
+    # -- batched reads ----------------------------------------------------------
+    def read_sessions(self, slots, parts: bool = False):
+        """Header rows (and participant rows) of many sessions, O(1) commands:
+        ``(hdr uint64[n, STORE_HDR_WORDS], parts uint64[n, P, 5] | None)``.  Header
+        layout: ``exec_read_many`` in ``csrc/include/ahv/store.h``."""
+        import numpy as np
+
+        slots = list(slots)
+        n = len(slots)
+        H = C.STORE_HDR_WORDS
+        P = self.caps["P"]
+        per = 8 * H + (40 * P if parts else 0)
+        chunk = max(1, min(self._c.bulk_cap // per, self._c.staging_cap // 8))
+        hdr = np.zeros((n, H), dtype=np.uint64)
+        prt = np.zeros((n, P, 5), dtype=np.uint64) if parts else None
+        for i in range(0, n, chunk):
+            part = slots[i: i + chunk]
+            k = len(part)
+            cnt, off, inl = self.index_args(part)
+            r = self.call(OP_SESS_READ_MANY, [cnt, off, 0, int(parts)], 1, inl)
+            if r[0]:
+                raise StoreError(f"OP_SESS_READ_MANY failed with status {r[0]}")
+            raw = self.bulk(0, 8 * H * k + (40 * P * k if parts else 0))
+            words = np.frombuffer(raw, dtype=np.uint64)
+            hdr[i: i + k] = words[: H * k].reshape(k, H)
+            if parts:
+                prt[i: i + k] = words[H * k:].reshape(k, P, 5)
+        return hdr, prt
 
     # -- index lists -----------------------------------------------------------
     def index_args(self, idx: list) -> tuple:

@@ -520,15 +520,15 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
             put("p_sraw", row, float(p["sigma_raw"]))
             put("p_seff", row, float(p["sigma_eff"]))
             put("p_joined", row, us(p["joined_at"]))
-        de = _device.DeviceDeltaEngine(st, s, r["session_id"])
+        de = _device.DeviceDeltaEngine(st, s, r["session_id"], sso)
         prev_idx, prev_view = -1, None
         for rec in r["audit"]:
             payload = rec["payload"].encode()
             if hashlib.sha256(payload).hexdigest() != rec["delta_hash"]:
                 raise CheckpointError(f"session {r['session_id']}: stored hash does not match its payload")
             p = json.loads(payload)
-            didx = st.alloc_delta()
-            off = st.payload_append(payload)
+            didx, off = st.restore_delta(payload)
+            de._rows.append(didx)
             ts = datetime.fromisoformat(p["timestamp"])
             from hypervisor.audit.delta import VFSChange
 
@@ -617,7 +617,7 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
         put("v_tail", vs, e)
         rec = _device.DeviceVouchRecord(st, e, v["vouch_id"], v["voucher_did"], v["vouchee_did"], v["session_id"],
                                         v["bonded_sigma_pct"], v["bonded_amount"], _dt(v["created_at"]),
-                                        _dt(v["expiry"]))
+                                        _dt(v["expiry"]), owner=ve)
         ve._by_id[rec.vouch_id] = rec
         ve._by_edge[e] = rec
         ve._order.append(rec)

@@ -20,6 +20,7 @@
 #include <immintrin.h>
 
 #include <chrono>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -51,6 +52,74 @@ struct ResultGone : std::exception {
 void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
+
+// Allocator of the audit payload arena: 64-byte granules, exact-fit free lists
+// per granule count (records are a few hundred bytes, so a handful of classes
+// see nearly all traffic), a best-fit map for large records, a bump pointer, and
+// splitting of larger free blocks when both run dry.  A record's bytes are
+// reclaimed together with its delta row (free_deltas), never overwritten while
+// the row is live.
+class ArenaAlloc {
+ public:
+  static constexpr int64_t kGran = 64;
+  static constexpr int64_t kClasses = 256;
+
+  void reset(int64_t cap) {
+    cap_ = cap;
+    head_ = 0;
+    live_ = 0;
+    for (auto& v : cls_) v.clear();
+    big_.clear();
+  }
+  void grow(int64_t cap) { cap_ = cap; }
+  static int64_t granules(int64_t bytes) { return bytes <= 0 ? 1 : (bytes + kGran - 1) / kGran; }
+
+  // Offset of a block of `bytes`, or -1 when the arena is full.
+  int64_t alloc(int64_t bytes) {
+    const int64_t g = granules(bytes);
+    int64_t off = -1;
+    if (g < kClasses && !cls_[g].empty()) {
+      off = cls_[g].back();
+      cls_[g].pop_back();
+    } else if (head_ + g * kGran <= cap_) {
+      off = head_;
+      head_ += g * kGran;
+    } else {
+      for (int64_t k = g + 1; k < kClasses && off < 0; ++k) {
+        if (cls_[k].empty()) continue;
+        off = cls_[k].back();
+        cls_[k].pop_back();
+        put(off + g * kGran, k - g);
+      }
+      if (off < 0) {
+        auto it = big_.lower_bound(g);
+        if (it == big_.end()) return -1;
+        const int64_t k = it->first;
+        off = it->second;
+        big_.erase(it);
+        if (k > g) put(off + g * kGran, k - g);
+      }
+    }
+    live_ += g * kGran;
+    return off;
+  }
+  void free(int64_t off, int64_t bytes) {
+    const int64_t g = granules(bytes);
+    put(off, g);
+    live_ -= g * kGran;
+  }
+  int64_t live() const { return live_; }
+  int64_t head() const { return head_; }
+
+ private:
+  void put(int64_t off, int64_t g) {
+    if (g < kClasses) cls_[g].push_back(off);
+    else big_.emplace(g, off);
+  }
+  std::vector<int64_t> cls_[kClasses];
+  std::multimap<int64_t, int64_t> big_;
+  int64_t head_ = 0, cap_ = 0, live_ = 0;
+};
 
 class Store {
  public:
@@ -103,6 +172,9 @@ class Store {
     *alive_ = 0;
     t_.payload = payload_;
     t_.staging = staging_;
+    arena_.reset(t_.cap.B);
+    d_off_.assign(static_cast<size_t>(t_.cap.D), -1);
+    d_len_.assign(static_cast<size_t>(t_.cap.D), 0);
   }
 
   ~Store() {
@@ -133,6 +205,12 @@ class Store {
   void close() {
     if (closed_) return;
     closed_ = true;
+    quiesce();
+  }
+
+  // Every posted command has completed and no worker wave is resident (its
+  // table writes are visible to other kernels); the next post relaunches it.
+  void quiesce() {
     if (gpu_ && launches_ > 0) {
       if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) != 0) {
         const uint64_t q = post_raw(OP_STOP, nullptr, 0, nullptr, 0);
@@ -140,6 +218,42 @@ class Store {
       }
       hip_check(hipStreamSynchronize(stream_), "store worker drain");
     }
+  }
+
+  // New table pointers / capacities (table growth).  The caller quiesced the
+  // worker and copied the old rows into the new tensors.
+  void rebind(const py::dict& ptrs, const py::dict& caps) {
+    quiesce();
+    auto cap = [&](const char* k) { return caps[k].cast<int64_t>(); };
+    const int64_t oldB = t_.cap.B;
+    t_.cap = Caps{cap("S"), cap("P"), cap("D"), cap("E"), cap("V"), cap("G"), cap("T"), cap("X"), oldB};
+#define AHV_PTR(name, type, ext) t_.name = reinterpret_cast<type*>(ptrs[#name].cast<uintptr_t>());
+    AHV_STORE_COLUMNS(AHV_PTR)
+#undef AHV_PTR
+    d_off_.resize(static_cast<size_t>(t_.cap.D), -1);
+    d_len_.resize(static_cast<size_t>(t_.cap.D), 0);
+  }
+
+  // Double (at least) the payload arena, keeping every record at its offset.
+  void grow_payload(int64_t new_bytes) {
+    if (new_bytes <= t_.cap.B) return;
+    quiesce();
+    uint8_t* p = nullptr;
+    if (gpu_) {
+      hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&p), static_cast<size_t>(new_bytes),
+                                      hipDeviceMallocFinegrained),
+                "store payload arena (grow)");
+      hip_check(hipMemcpy(p, payload_, static_cast<size_t>(arena_.head()), hipMemcpyDeviceToDevice), "arena copy");
+      hip_check(hipDeviceSynchronize(), "arena grow sync");
+      (void)hipFree(payload_);
+    } else {
+      p = static_cast<uint8_t*>(std::realloc(payload_, static_cast<size_t>(new_bytes)));
+      if (!p) throw std::bad_alloc();
+    }
+    payload_ = p;
+    t_.payload = p;
+    t_.cap.B = new_bytes;
+    arena_.grow(new_bytes);
   }
 
   // ------------------------------------------------------------ transport
@@ -320,13 +434,21 @@ class Store {
     return capture_rendered(slot, turn, ts_us, buf, static_cast<size_t>(null_at));
   }
 
+  // Returns (-2, ...) when the delta table is full and (-3, ...) when the payload
+  // arena is: the Python layer reclaims / grows and retries.  Nothing is
+  // recycled while it is live.
   py::tuple capture_rendered(int64_t slot, int64_t turn, int64_t ts_us, const std::string& buf, size_t at) {
     const bool hole = turn > 1;
     const size_t len = hole ? buf.size() - 4 + 66 : buf.size();
-    if (static_cast<int64_t>(len) > t_.cap.B) throw std::length_error("audit payload larger than the arena");
-    if (payload_head_ + static_cast<int64_t>(len) > t_.cap.B) payload_head_ = 0;  // ring: oldest records recycled
-    const int64_t off = payload_head_;
-    payload_head_ += static_cast<int64_t>((len + 63) & ~size_t(63));
+    const int64_t didx = take_delta_row();
+    if (didx < 0) return py::make_tuple(-2, -1, static_cast<int64_t>(len), -1);
+    const int64_t off = arena_.alloc(static_cast<int64_t>(len));
+    if (off < 0) {
+      dfree_.push_back(static_cast<int32_t>(didx));
+      return py::make_tuple(-3, -1, static_cast<int64_t>(len), -1);
+    }
+    d_off_[static_cast<size_t>(didx)] = off;
+    d_len_[static_cast<size_t>(didx)] = static_cast<int64_t>(len);
     uint8_t* dst = payload_ + off;
     if (hole) {
       std::memcpy(dst, buf.data(), at);
@@ -335,8 +457,6 @@ class Store {
       std::memcpy(dst, buf.data(), buf.size());
     }
     if (gpu_) _mm_sfence();
-    const int64_t didx = delta_head_;
-    delta_head_ = (delta_head_ + 1) % t_.cap.D;
     uint64_t a[7] = {static_cast<uint64_t>(slot), static_cast<uint64_t>(didx), static_cast<uint64_t>(turn),
                      static_cast<uint64_t>(ts_us), static_cast<uint64_t>(off), static_cast<uint64_t>(len),
                      hole ? static_cast<uint64_t>(at) : ~0ull};
@@ -346,22 +466,69 @@ class Store {
 
   // Append a complete record to the payload arena (checkpoint restore); returns
   // its offset.  The device re-hashes restored records before they are trusted.
-  int64_t payload_append(const py::bytes& b) {
+  // Checkpoint restore: a delta row plus its record in the arena (the caller
+  // writes the row's columns).  Returns (delta index, offset); -2 / -3 as capture.
+  py::tuple restore_delta(const py::bytes& b) {
     std::string_view v = b;
     const int64_t len = static_cast<int64_t>(v.size());
-    if (len > t_.cap.B) throw std::length_error("audit payload larger than the arena");
-    if (payload_head_ + len > t_.cap.B) payload_head_ = 0;
-    const int64_t off = payload_head_;
-    payload_head_ += (len + 63) & ~int64_t(63);
+    const int64_t didx = take_delta_row();
+    if (didx < 0) return py::make_tuple(-2, -1);
+    const int64_t off = arena_.alloc(len);
+    if (off < 0) {
+      dfree_.push_back(static_cast<int32_t>(didx));
+      return py::make_tuple(-3, -1);
+    }
+    d_off_[static_cast<size_t>(didx)] = off;
+    d_len_[static_cast<size_t>(didx)] = len;
     std::memcpy(payload_ + off, v.data(), v.size());
     if (gpu_) _mm_sfence();
-    return off;
+    return py::make_tuple(didx, off);
   }
 
-  int64_t alloc_delta() {
-    const int64_t d = delta_head_;
-    delta_head_ = (delta_head_ + 1) % t_.cap.D;
-    return d;
+  // Reclaim delta rows (and their arena records) no API object refers to any
+  // more: OP_FREE_ROWS marks them free on the device after the hash engine has
+  // drained, then the rows and bytes return to the host free lists.
+  void free_deltas(const std::vector<int32_t>& rows) {
+    if (rows.empty()) return;
+    for (int32_t d : rows)
+      if (d < 0 || d >= t_.cap.D || d_off_[static_cast<size_t>(d)] < 0)
+        throw std::invalid_argument("free_deltas: row " + std::to_string(d) + " is not allocated");
+    free_rows_cmd(RK_D, rows);
+    for (int32_t d : rows) {
+      arena_.free(d_off_[static_cast<size_t>(d)], d_len_[static_cast<size_t>(d)]);
+      d_off_[static_cast<size_t>(d)] = -1;
+      d_len_[static_cast<size_t>(d)] = 0;
+      dfree_.push_back(d);
+    }
+  }
+
+  // OP_FREE_ROWS for any table; waits for completion.
+  void free_rows_cmd(uint64_t kind, const std::vector<int32_t>& rows) {
+    const size_t per = static_cast<size_t>(staging_cap_ / 8);  // one staged list per command
+    for (size_t i = 0; i < rows.size(); i += per) {
+      const size_t n = std::min(per, rows.size() - i);
+      uint64_t a[3] = {kind, static_cast<uint64_t>(n), 0};
+      const uint8_t* raw = reinterpret_cast<const uint8_t*>(rows.data() + i);
+      uint64_t q;
+      if (n <= static_cast<size_t>(2 * kInlineWords)) {
+        q = post_raw(OP_FREE_ROWS, a, 3, raw, 4 * n);
+      } else {
+        a[2] = static_cast<uint64_t>(stage_raw(raw, 4 * n));
+        q = post_raw(OP_FREE_ROWS, a, 3, nullptr, 0);
+      }
+      const uint64_t* r = wait(q);
+      if (r[1] != ST_OK) throw std::runtime_error("OP_FREE_ROWS failed with status " + std::to_string(r[1]));
+    }
+  }
+
+  int64_t take_delta_row() {
+    if (!dfree_.empty()) {
+      const int32_t d = dfree_.back();
+      dfree_.pop_back();
+      return d;
+    }
+    if (dhw_ < t_.cap.D) return dhw_++;
+    return -1;
   }
 
   py::dict info() const {
@@ -371,15 +538,19 @@ class Store {
     d["posted"] = posted_;
     d["launches"] = launches_;
     d["nslots"] = nslots_;
-    d["payload_head"] = payload_head_;
-    d["delta_head"] = delta_head_;
+    d["payload_live"] = arena_.live();
+    d["payload_head"] = arena_.head();
+    d["payload_cap"] = t_.cap.B;
+    d["delta_rows"] = dhw_ - static_cast<int64_t>(dfree_.size());
+    d["delta_hw"] = dhw_;
+    d["delta_cap"] = t_.cap.D;
     return d;
   }
 
-  int64_t delta_head() const { return delta_head_; }
-  void set_delta_head(int64_t v) { delta_head_ = v; }
-  int64_t payload_head() const { return payload_head_; }
-  void set_payload_head(int64_t v) { payload_head_ = v; }
+  int64_t delta_live() const { return dhw_ - static_cast<int64_t>(dfree_.size()); }
+  int64_t payload_cap() const { return t_.cap.B; }
+  int64_t bulk_cap() const { return bulk_cap_; }
+  int64_t staging_cap() const { return staging_cap_; }
   void set_timeout(int s) { timeout_s_ = s; }
   bool gpu() const { return gpu_; }
 
@@ -404,8 +575,10 @@ class Store {
   uint64_t posted_ = 0;
   uint64_t launches_ = 0;
   size_t stage_head_ = 0;
-  int64_t payload_head_ = 0;
-  int64_t delta_head_ = 0;
+  ArenaAlloc arena_;
+  std::vector<int64_t> d_off_, d_len_;  // arena record of each delta row (-1: row free)
+  std::vector<int32_t> dfree_;          // reclaimed delta rows
+  int64_t dhw_ = 0;                      // delta rows ever handed out (high-water mark)
   int timeout_s_ = 30;
   bool closed_ = false;
 };
@@ -416,7 +589,7 @@ void register_store(py::module_& m) {
   py::class_<Store>(m, "Store", "Device-authoritative governance state store (gfx950 worker or CPU twin)")
       .def(py::init<int, const py::dict&, const py::dict&, int64_t, int64_t, int64_t, int64_t, int64_t>(),
            py::arg("device"), py::arg("ptrs"), py::arg("caps"), py::arg("nslots") = 256,
-           py::arg("staging_bytes") = 1 << 22, py::arg("bulk_bytes") = 1 << 22, py::arg("idle_us") = 500,
+           py::arg("staging_bytes") = 1 << 22, py::arg("bulk_bytes") = 1 << 24, py::arg("idle_us") = 500,
            py::arg("max_ms") = 2000)
       .def("post", &Store::post, py::arg("op"), py::arg("args"), py::arg("inline") = py::none())
       .def("call", &Store::call, py::arg("op"), py::arg("args"), py::arg("nres") = 4, py::arg("inline") = py::none())
@@ -427,17 +600,23 @@ void register_store(py::module_& m) {
       .def("payload", &Store::payload)
       .def("capture", &Store::capture)
       .def("capture_bytes", &Store::capture_bytes)
-      .def("payload_append", &Store::payload_append)
-      .def("alloc_delta", &Store::alloc_delta)
+      .def("restore_delta", &Store::restore_delta)
+      .def("free_deltas", &Store::free_deltas)
+      .def("free_rows", &Store::free_rows_cmd)
+      .def("quiesce", &Store::quiesce)
+      .def("rebind", &Store::rebind)
+      .def("grow_payload", &Store::grow_payload)
       .def("close", &Store::close)
       .def("info", &Store::info)
       .def("set_timeout", &Store::set_timeout)
-      .def_property("delta_head", &Store::delta_head, &Store::set_delta_head)
-      .def_property("payload_head", &Store::payload_head, &Store::set_payload_head)
+      .def_property_readonly("delta_live", &Store::delta_live)
+      .def_property_readonly("payload_cap", &Store::payload_cap)
+      .def_property_readonly("bulk_cap", &Store::bulk_cap)
+      .def_property_readonly("staging_cap", &Store::staging_cap)
       .def_property_readonly("gpu", &Store::gpu);
   py::dict ops;
 #define AHV_OP(n) ops[#n] = static_cast<int>(ahv::store::n);
-  AHV_OP(OP_NOP) AHV_OP(OP_STOP) AHV_OP(OP_FLUSH) AHV_OP(OP_ACQUIRE) AHV_OP(OP_SESS_CREATE) AHV_OP(OP_SESS_JOIN)
+  AHV_OP(OP_NOP) AHV_OP(OP_STOP) AHV_OP(OP_FLUSH) AHV_OP(OP_ACQUIRE) AHV_OP(OP_FREE_ROWS) AHV_OP(OP_SESS_READ_MANY) AHV_OP(OP_V_RETIRE) AHV_OP(OP_SESS_CREATE) AHV_OP(OP_SESS_JOIN)
   AHV_OP(OP_SESS_LEAVE) AHV_OP(OP_SESS_ACTIVATE) AHV_OP(OP_SESS_TERMINATE) AHV_OP(OP_SESS_ARCHIVE)
   AHV_OP(OP_SESS_UPDATE_RING) AHV_OP(OP_SESS_SET_MODE) AHV_OP(OP_SESS_READ) AHV_OP(OP_SESS_SET_SIGMA)
   AHV_OP(OP_SESS_CLOSE) AHV_OP(OP_SESS_HANDSHAKE) AHV_OP(OP_DELTA_CAPTURE) AHV_OP(OP_DELTA_MERKLE)
@@ -448,6 +627,7 @@ void register_store(py::module_& m) {
   AHV_OP(OP_SAGA_READ) AHV_OP(OP_SAGA_PLAN)
 #undef AHV_OP
   m.attr("STORE_OPS") = ops;
+  m.attr("STORE_HDR_WORDS") = static_cast<int>(ahv::store::kHdrWords);
   py::list cols;
 #define AHV_COL(name, type, ext) cols.append(py::make_tuple(#name, #type, #ext));
   AHV_STORE_COLUMNS(AHV_COL)

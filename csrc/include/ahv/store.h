@@ -45,6 +45,7 @@ enum Op : uint32_t {
   OP_STOP = 1,
   OP_FLUSH = 2,    // release: make table writes visible to other agents (torch, kernels)
   OP_ACQUIRE = 3,  // acquire: see rows other kernels wrote (batched pipeline)
+  OP_FREE_ROWS = 4,  // return rows to the free state (host allocator reclaim; drains the hash engine)
 
   OP_SESS_CREATE = 10,
   OP_SESS_JOIN = 11,
@@ -58,6 +59,7 @@ enum Op : uint32_t {
   OP_SESS_SET_SIGMA = 19,
   OP_SESS_CLOSE = 20,  // Hypervisor.terminate_session: terminate+root+commit+release+GC+archive
   OP_SESS_HANDSHAKE = 21,
+  OP_SESS_READ_MANY = 22,  // headers (+ participant rows) of many sessions in one command
 
   OP_DELTA_CAPTURE = 30,
   OP_DELTA_MERKLE = 31,
@@ -72,6 +74,7 @@ enum Op : uint32_t {
   OP_VOUCH_LIST = 45,
   OP_EDGE_READ = 46,
   OP_SLASH = 47,
+  OP_V_RETIRE = 48,  // unlink a liability session's edge list and free its rows (after close)
 
   OP_SAGA_CREATE = 60,
   OP_STEP_ADD = 61,
@@ -98,6 +101,13 @@ enum VouchCode : uint64_t { V_OK = 0, V_SELF = 1, V_LOW_SIGMA = 2, V_CYCLE = 3, 
 
 // Join codes extend semantics.h JoinCode.
 constexpr uint64_t JOIN_ROWS = 5;  // participant row table exhausted
+
+// Row lifecycle.  A row is FREE until a create command claims it and FREE again
+// after the host allocator reclaims it (OP_FREE_ROWS); creates refuse a row that
+// is not free (ST_BAD_STATE), so an allocator bug can never overwrite live state.
+// Markers: s_state / g_state / t_state = kFree8, d_sess / e_vsess = -1.
+constexpr uint8_t kFree8 = 255;
+enum RowKind : uint64_t { RK_S = 0, RK_G = 1, RK_T = 2, RK_E = 3, RK_D = 4, RK_V = 5 };
 
 // --------------------------------------------------------------- tables
 
@@ -669,12 +679,17 @@ AHV_HD bool merkle_provisional(const Lanes& L, const Tables& t, int64_t s, int64
 AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
   if (!L.leader()) return;
   const int64_t s = static_cast<int64_t>(c.a[0]);
-  if (s < 0 || s >= t.cap.S) {
+  if (s < 0 || s >= t.cap.S || (c.op != OP_SESS_CREATE && c.op != OP_SESS_READ && t.s_state[s] == kFree8)) {
     if (L.leader()) out64(r + 1, ST_BAD_ARG);
     return;
   }
   switch (c.op) {
     case OP_SESS_CREATE: {
+      if (t.s_state[s] != kFree8) {  // the row still holds a session: never overwrite it
+        out64(r + 2, t.s_state[s]);
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
       t.s_state[s] = SS_HANDSHAKING;  // create + begin_handshake (Hypervisor.create_session)
       t.s_mode[s] = static_cast<uint8_t>(c.a[3]);
       t.s_audit[s] = static_cast<uint8_t>(c.a[6]);
@@ -1091,6 +1106,10 @@ AHV_HD void exec_vouch(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
         out64(r + 1, ST_BAD_ARG);
         return;
       }
+      if (t.e_vsess[e] != -1) {  // edge row in use
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
       if (vr == ve) {
         out64(r + 1, V_SELF);
         return;
@@ -1182,10 +1201,13 @@ AHV_HD void exec_vouch(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
     }
     case OP_VOUCH_LIST: {
       // a0 vsess, a1 filter (0 all, 1 live by vouchee a2, 2 live by voucher a2, 3 live), a3 now,
-      // a4 bulk offset, a5 bulk capacity (edges).  Rows: [edge, voucher, vouchee, flags|released?]
+      // a4 bulk offset, a5 bulk capacity (edges), a6 matches to skip (paging).
+      // Rows: [edge, voucher, vouchee, active, bonded, pct, expiry, released];
+      // r[2] = total matches (the host pages until it has them all).
       const int32_t v = static_cast<int32_t>(c.a[0]);
       const int64_t now = static_cast<int64_t>(c.a[3]);
       const int32_t who = static_cast<int32_t>(c.a[2]);
+      const int64_t skip = static_cast<int64_t>(c.a[6]);
       uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[4]);
       int64_t n = 0;
       if (v >= 0 && v < t.cap.V) {
@@ -1199,8 +1221,8 @@ AHV_HD void exec_vouch(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
             default: break;
           }
           if (!keep) continue;
-          if (n < static_cast<int64_t>(c.a[5])) {
-            uint64_t* row = b + 8 * n;
+          if (n >= skip && n - skip < static_cast<int64_t>(c.a[5])) {
+            uint64_t* row = b + 8 * (n - skip);
             out64(row + 0, static_cast<uint64_t>(static_cast<int64_t>(e)));
             out64(row + 1, static_cast<uint64_t>(static_cast<int64_t>(t.e_voucher[e])));
             out64(row + 2, static_cast<uint64_t>(static_cast<int64_t>(t.e_vouchee[e])));
@@ -1214,7 +1236,7 @@ AHV_HD void exec_vouch(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
         }
       }
       out64(r + 2, static_cast<uint64_t>(n));
-      out64(r + 1, n > static_cast<int64_t>(c.a[5]) ? ST_SCRATCH : ST_OK);
+      out64(r + 1, ST_OK);
       return;
     }
     case OP_EDGE_READ: {
@@ -1277,9 +1299,161 @@ AHV_HD void exec_vouch(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
       out64(r + 1, ST_OK);
       return;
     }
+    case OP_V_RETIRE: {
+      // a0 vsess, a1 bulk offset, a2 capacity (edges).  Every edge of the list —
+      // all released by the close that precedes this — is reported as
+      // [edge, active, released µs] and returned to the free state; the list is
+      // emptied (later vouches in the same session start a new list).  Nothing
+      // changes when the list is longer than the capacity (ST_SCRATCH + count).
+      const int32_t v = static_cast<int32_t>(c.a[0]);
+      if (v < 0 || v >= t.cap.V) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      int64_t n = 0;
+      for (int32_t e = t.v_head[v]; e >= 0; e = t.e_next[e]) ++n;
+      out64(r + 2, static_cast<uint64_t>(n));
+      if (n > static_cast<int64_t>(c.a[2])) {
+        out64(r + 1, ST_SCRATCH);
+        return;
+      }
+      uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[1]);
+      int64_t k = 0;
+      for (int32_t e = t.v_head[v]; e >= 0;) {
+        const int32_t nx = t.e_next[e];
+        out64(b + 3 * k + 0, static_cast<uint64_t>(static_cast<int64_t>(e)));
+        out64(b + 3 * k + 1, uint64_t(t.e_active[e]));
+        out64(b + 3 * k + 2, static_cast<uint64_t>(t.e_released[e]));
+        t.e_active[e] = 0;
+        t.e_vsess[e] = -1;
+        t.e_next[e] = -1;
+        ++k;
+        e = nx;
+      }
+      t.v_head[v] = -1;
+      t.v_tail[v] = -1;
+      out64(r + 1, ST_OK);
+      return;
+    }
     default:
       break;
   }
+}
+
+// OP_FREE_ROWS: a0 kind (RowKind), a1 n, a2 staging offset of the row list.
+// The host reclaims a row only once no API object refers to it any more; the
+// command marks it free so the next create may claim it.  Runs after the hash
+// engine has drained (needs_drain), so no queued capture still writes a freed
+// delta row or the chain head of a freed session.
+AHV_HD void exec_free_rows(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r) {
+  const uint64_t kind = c.a[0];
+  const uint64_t n = c.a[1];
+  const IndexList idx = index_list(t, c, n, c.a[2]);
+  int bad = 0;
+  for (uint64_t i = L.lane; i < n; i += L.n) {
+    const int64_t x = idx[i];
+    switch (kind) {
+      case RK_S:
+        if (x < 0 || x >= t.cap.S) { bad = 1; break; }
+        t.s_state[x] = kFree8;
+        t.s_proot_n[x] = 0;
+        t.s_dlast[x] = -1;
+        t.s_dcount[x] = 0;
+        break;
+      case RK_G:
+        if (x < 0 || x >= t.cap.G) { bad = 1; break; }
+        t.g_state[x] = kFree8;
+        break;
+      case RK_T:
+        if (x < 0 || x >= t.cap.T) { bad = 1; break; }
+        t.t_state[x] = kFree8;
+        t.t_saga[x] = -1;
+        break;
+      case RK_E:
+        if (x < 0 || x >= t.cap.E) { bad = 1; break; }
+        t.e_active[x] = 0;
+        t.e_vsess[x] = -1;
+        t.e_next[x] = -1;
+        break;
+      case RK_D:
+        if (x < 0 || x >= t.cap.D) { bad = 1; break; }
+        t.d_sess[x] = -1;
+        t.d_turn[x] = 0;
+        t.d_prev[x] = -1;
+        break;
+      case RK_V:
+        if (x < 0 || x >= t.cap.V) { bad = 1; break; }
+        t.v_head[x] = -1;
+        t.v_tail[x] = -1;
+        break;
+      default:
+        bad = 1;
+    }
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  bad = __any(bad) ? 1 : 0;
+#endif
+  L.sync();
+  if (L.leader()) out64(r + 1, bad ? ST_BAD_ARG : ST_OK);
+}
+
+// OP_SESS_READ_MANY: a0 n, a1 staging offset of the slot list, a2 bulk offset,
+// a3 participant rows too (1) or headers only (0).  One lane per session.
+// Header row (kHdrWords u64): [state | mode<<8 | audit<<16, pcount | pactive<<32,
+// created, terminated, dcount | commit_n<<32, maxpart, minsig bits, committed,
+// creator, released | retained<<32, uuid (2 words), root (4 words), head (4 words)].
+// With participants, session i's rows follow all headers at stride cap.P × 5 words
+// (the OP_SESS_READ participant layout).
+constexpr int kHdrWords = 20;
+
+AHV_HD void exec_read_many(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {
+  const uint64_t n = c.a[0];
+  const IndexList idx = index_list(t, c, n, c.a[1]);
+  uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[2]);
+  const bool parts = c.a[3] != 0;
+  uint64_t* pb = b + kHdrWords * n;
+  int bad = 0;
+  for (uint64_t i = L.lane; i < n; i += L.n) {
+    const int64_t s = idx[i];
+    uint64_t* h = b + kHdrWords * i;
+    if (s < 0 || s >= t.cap.S) {
+      bad = 1;
+      continue;
+    }
+    out64(h + 0, uint64_t(t.s_state[s]) | (uint64_t(t.s_mode[s]) << 8) | (uint64_t(t.s_audit[s]) << 16));
+    out64(h + 1, uint64_t(static_cast<uint32_t>(t.s_pcount[s])) | (uint64_t(static_cast<uint32_t>(t.s_pactive[s])) << 32));
+    out64(h + 2, static_cast<uint64_t>(t.s_created[s]));
+    out64(h + 3, static_cast<uint64_t>(t.s_terminated[s]));
+    out64(h + 4, uint64_t(static_cast<uint32_t>(t.s_dcount[s])) | (uint64_t(static_cast<uint32_t>(t.s_commit_n[s])) << 32));
+    out64(h + 5, static_cast<uint64_t>(static_cast<int64_t>(t.s_maxpart[s])));
+    out64(h + 6, dbits(t.s_minsig[s]));
+    out64(h + 7, static_cast<uint64_t>(t.s_committed[s]));
+    out64(h + 8, static_cast<uint64_t>(static_cast<int64_t>(t.s_creator[s])));
+    out64(h + 9, uint64_t(static_cast<uint32_t>(t.s_released[s])) | (uint64_t(static_cast<uint32_t>(t.s_retained[s])) << 32));
+    for (int k = 0; k < 2; ++k)
+      out64(h + 10 + k, (uint64_t(t.s_uuid[4 * s + 2 * k]) << 32) | uint64_t(t.s_uuid[4 * s + 2 * k + 1]));
+    for (int k = 0; k < 4; ++k) {
+      out64(h + 12 + k, (uint64_t(t.s_root[8 * s + 2 * k]) << 32) | uint64_t(t.s_root[8 * s + 2 * k + 1]));
+      out64(h + 16 + k, (uint64_t(t.s_head[8 * s + 2 * k]) << 32) | uint64_t(t.s_head[8 * s + 2 * k + 1]));
+    }
+    if (parts) {
+      uint64_t* p = pb + 5 * t.cap.P * i;
+      const int32_t np = t.s_pcount[s];
+      for (int32_t k = 0; k < np; ++k) {
+        const int64_t row = s * t.cap.P + k;
+        out64(p + 5 * k + 0, static_cast<uint64_t>(static_cast<int64_t>(t.p_agent[row])));
+        out64(p + 5 * k + 1, uint64_t(t.p_ring[row]) | (uint64_t(t.p_active[row]) << 8));
+        out64(p + 5 * k + 2, dbits(t.p_sraw[row]));
+        out64(p + 5 * k + 3, dbits(t.p_seff[row]));
+        out64(p + 5 * k + 4, static_cast<uint64_t>(t.p_joined[row]));
+      }
+    }
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  bad = __any(bad) ? 1 : 0;
+#endif
+  L.sync();
+  if (L.leader()) out64(r + 1, bad ? ST_BAD_ARG : ST_OK);
 }
 
 // ------------------------------------------------------------- saga ops
@@ -1293,6 +1467,11 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
         out64(r + 1, ST_BAD_ARG);
         return;
       }
+      if (t.g_state[g] != kFree8) {
+        out64(r + 2, t.g_state[g]);
+        out64(r + 1, ST_BAD_STATE);
+        return;
+      }
       t.g_state[g] = SG_RUNNING;
       t.g_created[g] = static_cast<int64_t>(c.a[1]);
       t.g_completed[g] = 0;
@@ -1304,6 +1483,11 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       const int64_t g = static_cast<int64_t>(c.a[0]), st = static_cast<int64_t>(c.a[1]);
       if (g < 0 || g >= t.cap.G || st < 0 || st >= t.cap.T) {
         out64(r + 1, ST_BAD_ARG);
+        return;
+      }
+      if (t.t_state[st] != kFree8 || t.g_state[g] == kFree8) {
+        out64(r + 2, t.t_state[st]);
+        out64(r + 1, ST_BAD_STATE);
         return;
       }
       t.t_saga[st] = static_cast<int32_t>(g);
@@ -1420,6 +1604,7 @@ AHV_HD bool capture_begin(const Lanes& L, const Tables& t, const Cmd& c, uint64_
   const int64_t hole = static_cast<int64_t>(c.a[6]);
   bool ok = !(s < 0 || s >= t.cap.S || d < 0 || d >= t.cap.D || turn != t.s_dcount[s] + 1 ||
               c.a[4] + c.a[5] > static_cast<uint64_t>(t.cap.B));
+  if (ok && (t.d_sess[d] != -1 || t.s_state[s] == kFree8)) ok = false;  // delta row in use / no session
   const int32_t prev = ok ? t.s_dlast[s] : -1;
   if (ok && hole >= 0 && prev < 0) ok = false;
   if (ok && hole >= 0 && (hole + 66 > static_cast<int64_t>(c.a[5]))) ok = false;
@@ -1689,7 +1874,11 @@ AHV_HD int store_exec(const Lanes& L, const Tables& t, const Cmd& c, uint64_t se
     capture_finish(L, t, jb, r);
     return EXEC_DONE;
   }
-  if (c.op >= 10 && c.op < 30 && c.op != OP_SESS_CLOSE) {
+  if (c.op == OP_SESS_READ_MANY) {
+    exec_read_many(L, t, c, r, bulk);
+  } else if (c.op == OP_FREE_ROWS) {
+    exec_free_rows(L, t, c, r);
+  } else if (c.op >= 10 && c.op < 30 && c.op != OP_SESS_CLOSE) {
     exec_sess(L, t, c, r, bulk);
   } else if ((c.op >= 30 && c.op < 40) || c.op == OP_SESS_CLOSE) {
     exec_delta(L, t, c, r, bulk);

@@ -121,13 +121,14 @@ class DeviceSession(SharedSessionObject):
         self.vfs = SessionVFS(self.session_id, namespace=self.vfs_namespace)
         self._vfs_snapshots: dict[str, Any] = {}
         self.slot = store.alloc("S") if slot is None else slot
+        self._cseq = -1
         if create:
             u = self.session_id.rsplit(":", 1)[-1].replace("-", "")
             try:
                 hi, lo = int(u[:16], 16), int(u[16:32], 16)
             except ValueError:
                 hi = lo = 0
-            store.post(
+            self._cseq = store.post(
                 _st.OP_SESS_CREATE,
                 [
                     self.slot, store.agent_id(creator_did), to_us(_now()), _MODE[config.consistency_mode],
@@ -135,6 +136,24 @@ class DeviceSession(SharedSessionObject):
                     _i64(hi), _i64(lo), 0 if handshake else 1,
                 ],
             )
+
+    def __del__(self) -> None:
+        # the row stays allocated while this view (or a delta engine / saga built
+        # on it) exists; afterwards the store may reclaim it
+        try:
+            self._store.release("S", self.slot)
+        except Exception:
+            pass
+
+    def _created(self) -> None:
+        """Raise if the device refused the create (the slot was not free)."""
+        q = self._cseq
+        if q >= 0:
+            self._cseq = -1
+            r = self._store.result(q, 2)
+            if r is not None and r[0]:
+                raise _st.StoreError(f"device refused to create session {self.session_id} in row {self.slot} "
+                                     f"(row state {r[1]}): allocator invariant violated")
 
     # -- device reads -----------------------------------------------------------
     def _read(self, with_parts: bool = False):
@@ -208,6 +227,8 @@ class DeviceSession(SharedSessionObject):
             raise _lifecycle(r[1], SessionState.CREATED)
 
     def activate(self) -> None:
+        if self._cseq >= 0:
+            self._created()
         r = self._store.call(_st.OP_SESS_ACTIVATE, [self.slot], 2)
         if r[0] == _st.ST_BAD_STATE:
             raise _lifecycle(r[1], SessionState.HANDSHAKING)
@@ -216,6 +237,8 @@ class DeviceSession(SharedSessionObject):
         _check(r, "activate")
 
     def _join(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> int:
+        if self._cseq >= 0:
+            self._created()
         r = self._store.call(
             _st.OP_SESS_JOIN,
             [self.slot, self._store.agent_id(agent_did), dbits(sigma_raw), dbits(sigma_eff), flags, ring,
@@ -377,12 +400,21 @@ def _host_digest(d) -> str:
 class DeviceDeltaEngine(DeltaEngine):
     """Audit chain of one device session: the device links, hashes and roots it."""
 
-    def __init__(self, store: GovernanceStore, slot: int, session_id: str) -> None:
+    def __init__(self, store: GovernanceStore, slot: int, session_id: str, owner: Optional[DeviceSession] = None) -> None:
         self._store = store
         self.slot = slot
         self.session_id = session_id
+        self._owner = owner  # keeps the session row allocated while the chain is reachable
         self._deltas: list[DeviceDelta] = []
+        self._rows: list[int] = []  # every delta row this chain owns (pruned views included)
         self._turn_counter = 0
+
+    def __del__(self) -> None:
+        try:
+            if self._rows:
+                self._store.release_many("D", self._rows)
+        except Exception:
+            pass
 
     def capture(self, agent_did: str, changes: list[VFSChange], delta_id: Optional[str] = None) -> DeviceDelta:
         turn = self._turn_counter + 1
@@ -393,7 +425,8 @@ class DeviceDeltaEngine(DeltaEngine):
         if didx < 0:  # field types the native renderer defers to json.dumps
             raw = _payload_json(_NullParent(d)).encode()
             at = raw.index(b'"parent_hash": null') + len(b'"parent_hash": ')
-            didx, off, ln, seq = self._store._c.capture_bytes(self.slot, turn, to_us(ts), raw, at)
+            didx, off, ln, seq = self._store.capture_bytes(self.slot, turn, to_us(ts), raw, at)
+        self._rows.append(didx)
         d.__dict__.update(_didx=didx, _poff=off, _plen=ln, _seq=seq)
         self._turn_counter = turn
         self._deltas.append(d)
@@ -491,15 +524,22 @@ class DeviceVouchRecord(VouchRecord):
     """A vouch edge view: identity on the host, bond state on the device."""
 
     def __init__(self, store: GovernanceStore, edge: int, vouch_id, voucher_did, vouchee_did, session_id, pct,
-                 bonded, created_at, expiry) -> None:
+                 bonded, created_at, expiry, owner=None) -> None:
         self.__dict__.update(
             _store=store, edge=edge, vouch_id=vouch_id, voucher_did=voucher_did, vouchee_did=vouchee_did,
             session_id=session_id, bonded_sigma_pct=pct, bonded_amount=bonded, created_at=created_at,
-            expiry=expiry,
+            expiry=expiry, _owner=owner, _frozen=None,
         )
 
     def _row(self):
+        f = self._frozen
+        if f is not None:  # retired edge: its final state was read back when its row was freed
+            return f
         return self._store.call(_st.OP_EDGE_READ, [self.edge], 3)
+
+    def _freeze(self, active: int, released_us: int) -> None:
+        self.__dict__["_frozen"] = (0, int(active), _u64(released_us))
+        self.__dict__["edge"] = -1
 
     @property
     def is_active(self) -> bool:  # type: ignore[override]
@@ -508,7 +548,8 @@ class DeviceVouchRecord(VouchRecord):
     @is_active.setter
     def is_active(self, v: bool) -> None:
         if not v:
-            self._store.call(_st.OP_RELEASE_BOND, [self.edge, to_us(_now())], 1)
+            if self._frozen is None:
+                self._store.call(_st.OP_RELEASE_BOND, [self.edge, to_us(_now())], 1)
         elif not self.is_active:
             raise ValueError("a released bond cannot be re-activated")
 
@@ -529,13 +570,45 @@ class DeviceVouchRecord(VouchRecord):
 class DeviceVouchingEngine(VouchingEngine):
     """Bond edges in the device vouch table, linked per (hypervisor, session)."""
 
+    LIST_PAGE: Optional[int] = None  # edges per listing page (default: what the bulk buffer holds)
+
     def __init__(self, store: GovernanceStore, tenant: int, max_exposure: Optional[float] = None) -> None:
         self._store = store
         self._tenant = tenant
         self.max_exposure = max_exposure or self.DEFAULT_MAX_EXPOSURE
         self._by_id: dict[str, DeviceVouchRecord] = {}
-        self._by_edge: dict[int, DeviceVouchRecord] = {}
+        self._by_edge: dict[int, DeviceVouchRecord] = {}  # edges still linked on the device
         self._order: list[DeviceVouchRecord] = []
+
+    def __del__(self) -> None:
+        try:
+            self._store.release_tenant(self._tenant, list(self._by_edge))
+        except Exception:
+            pass
+
+    def retire_session(self, session_id: str) -> int:
+        """After a session's bonds were released (terminate), freeze each edge's
+        final state into its record and return the edge rows to the store
+        (OP_V_RETIRE); later vouches in the session start a new list."""
+        st = self._store
+        v = self._v(session_id)
+        if v < 0:
+            return 0
+        cap = st._c.bulk_cap // 24
+        r = st.call(_st.OP_V_RETIRE, [v, 0, cap], 2)
+        if r[0]:
+            return 0  # longer than one bulk page: the rows stay linked until the engine is dropped
+        n = r[1]
+        raw = st.bulk(0, 24 * n)
+        edges = []
+        for k in range(n):
+            e, act, rel = struct.unpack_from("<qQq", raw, 24 * k)
+            rec = self._by_edge.pop(e, None)
+            if rec is not None:
+                rec._freeze(act, rel)
+            edges.append(e)
+        st._rows["E"].free.extend(edges)  # already free on the device (V_RETIRE)
+        return n
 
     def _v(self, session_id: str, create: bool = False) -> int:
         if create:
@@ -567,6 +640,8 @@ class DeviceVouchingEngine(VouchingEngine):
             6,
         )
         code = r[0]
+        if code:  # rejected (or refused): the row was not linked and is still free on the device
+            st._rows["E"].free.append(edge)
         if code == 1:
             raise VouchingError("Cannot vouch for yourself")
         if code == 2:
@@ -587,7 +662,7 @@ class DeviceVouchingEngine(VouchingEngine):
             )
         _check(r, "vouch")
         rec = DeviceVouchRecord(st, edge, _C.uuid4("vouch:"), voucher_did, vouchee_did, session_id,
-                                bitsd(r[4]), bitsd(r[2]), now, expiry)
+                                bitsd(r[4]), bitsd(r[2]), now, expiry, owner=self)
         self._by_id[rec.vouch_id] = rec
         self._by_edge[edge] = rec
         self._order.append(rec)
@@ -606,23 +681,30 @@ class DeviceVouchingEngine(VouchingEngine):
         return bitsd(r[1])
 
     def _list(self, session_id: str, flt: int, who: Optional[str]) -> list[DeviceVouchRecord]:
+        """Edges of a session's device list matching ``flt`` (live by vouchee / by
+        voucher / all live), in creation order; paged through the bulk buffer."""
         v = self._v(session_id)
         if v < 0:
             return []
-        cap = 4096
-        r = self._store.call(
-            _st.OP_VOUCH_LIST,
-            [v, flt, self._store.agent_id(who) if who is not None else -1, to_us(_now()), 0, cap], 2,
-        )
-        n = r[1]
-        if n > cap:
-            raise _st.StoreError(f"{n} vouch edges exceed the listing buffer")
-        raw = self._store.bulk(0, 64 * n)
-        return [self._by_edge[struct.unpack_from("<q", raw, 64 * k)[0]] for k in range(n)]
+        st = self._store
+        cap = self.LIST_PAGE or st._c.bulk_cap // 64
+        who_id = st.agent_id(who) if who is not None else -1
+        now = to_us(_now())
+        out: list[DeviceVouchRecord] = []
+        skip = 0
+        while True:
+            r = st.call(_st.OP_VOUCH_LIST, [v, flt, who_id, now, 0, cap, skip], 2)
+            n = r[1]
+            k = min(n - skip, cap)
+            raw = st.bulk(0, 64 * k)
+            out.extend(self._by_edge[struct.unpack_from("<q", raw, 64 * i)[0]] for i in range(k))
+            skip += k
+            if skip >= n:
+                return out
 
     def records(self, session_id: Optional[str] = None) -> list[DeviceVouchRecord]:
-        if session_id is not None:
-            return self._list(session_id, 0, None)
+        if session_id is not None:  # identities are host-side; retired edges included
+            return [r for r in self._order if r.session_id == session_id]
         return list(self._order)
 
     def get_vouchers_for(self, agent_did: str, session_id: str) -> list[DeviceVouchRecord]:
@@ -775,6 +857,12 @@ class DeviceSagaStep(SagaStep):
         for k, v in kw.items():
             self.__dict__[k] = v
 
+    def __del__(self) -> None:
+        try:
+            self._store.release("T", self.slot)
+        except Exception:
+            pass
+
     def _row(self):
         return self._store.call(_st.OP_STEP_READ, [self.slot], 5)
 
@@ -837,6 +925,12 @@ class DeviceSaga(Saga):
 
     def __init__(self, store: GovernanceStore, slot: int, saga_id: str, session_id: str) -> None:
         self.__dict__.update(_store=store, slot=slot, saga_id=saga_id, session_id=session_id, steps=[], error=None)
+
+    def __del__(self) -> None:
+        try:
+            self._store.release("G", self.slot)
+        except Exception:
+            pass
 
     def _hdr(self):
         return self._store.call(_st.OP_SAGA_READ, [self.slot, 0, 0, 0], 5)
@@ -998,7 +1092,7 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
 
 def session_views(store: GovernanceStore, sso: DeviceSession):
     """(delta engine, saga orchestrator) for a device session."""
-    return DeviceDeltaEngine(store, sso.slot, sso.session_id), DeviceSagaOrchestrator(store)
+    return DeviceDeltaEngine(store, sso.slot, sso.session_id, sso), DeviceSagaOrchestrator(store)
 
 
 __all__ = [

@@ -88,10 +88,11 @@ class Hypervisor:
         event_bus: Optional[Any] = None,
         demote_on_slash: bool = False,
         device: Optional[str] = None,
+        store: Optional[Any] = None,
     ) -> None:
         from hypervisor.config import store_mode
 
-        mode = store_mode(device)
+        mode = store_mode(device) if store is None else str(store.device)
         self._store = None
         if mode == "host":
             self.vouching = VouchingEngine(max_exposure=max_exposure)
@@ -101,7 +102,7 @@ class Hypervisor:
             from agent_hypervisor_amd.models.store import shared_store
             from hypervisor import _device
 
-            self._store = shared_store(mode)
+            self._store = store if store is not None else shared_store(mode)
             self._tenant = self._store.new_tenant()
             self.vouching = _device.DeviceVouchingEngine(self._store, self._tenant, max_exposure)
             self.slashing = _device.DeviceSlashingEngine(self.vouching)
@@ -257,6 +258,8 @@ class Hypervisor:
             raise _lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
         _check(r, "terminate")
         root = _hex(r[2:10]) if r[1] else None
+        if v >= 0:  # every bond of the session is released now: freeze the records, reuse the edge rows
+            self.vouching.retire_session(session_id)
         if root:
             self.commitment.register(sso)
         # the device counted the deltas past retention (r[12]); with none expired the
