@@ -457,6 +457,24 @@ class GovernanceStore:
                 prt[i: i + k] = words[H * k:].reshape(k, P, 5)
         return hdr, prt
 
+    def gather(self, cols: dict) -> dict:
+        """``{column: row indices}`` → ``{column: numpy array}``: a device gather of
+        every requested column after one release of the worker's writes (O(1)
+        store commands however many rows)."""
+        import numpy as np
+
+        if not any(len(v) for v in cols.values()):
+            return {k: np.zeros(0, dtype=np.int64) for k in cols}
+        self.drain()
+        if self.device.type == "cuda":
+            self.flush()
+        out = {}
+        for name, idx in cols.items():
+            t = self.tables[name]
+            ix = torch.as_tensor(list(idx), dtype=torch.int64).to(self.device, non_blocking=True)
+            out[name] = t.index_select(0, ix).cpu().numpy()
+        return out
+
     # -- index lists -----------------------------------------------------------
     def index_args(self, idx: list) -> tuple:
         """(count, staging offset, inline bytes) for an int32 index list argument."""

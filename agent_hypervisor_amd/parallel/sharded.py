@@ -275,11 +275,13 @@ class ShardedHypervisor:
     def stats(self) -> dict:
         """X04: session / participant / saga / vouch totals summed over ranks."""
         hv = self.local
-        sessions = hv.sessions
+        snaps = hv.snapshots()  # one batched device read
+        sagas = hv.saga_summaries()
         vals = [
-            len(sessions), len(hv.active_sessions), sum(m.sso.participant_count for m in sessions),
-            sum(len(m.saga.active_sagas) for m in sessions), len(hv.vouching.records()),
-            sum(1 for m in sessions for _ in m.saga.sagas),
+            len(snaps), sum(1 for x in snaps if x.state.value not in ("archived", "terminating")),
+            sum(x.participant_count for x in snaps),
+            sum(1 for g in sagas if g["state"] in ("running", "compensating")), len(hv.vouching.records()),
+            len(sagas),
         ]
         t = torch.tensor(vals, dtype=torch.int64, device=_tensor_device() if self.world > 1 else "cpu")
         self._all_reduce(t, dist.ReduceOp.SUM)
@@ -292,9 +294,9 @@ class ShardedHypervisor:
         active participant (reference: first match in ``_sessions`` order)."""
         big = 1 << 62
         best, best_sid, best_ring = big, None, None
-        for m in self.local.sessions:  # local creation order
-            sid = m.sso.session_id
-            for p in m.sso.participants:
+        for x in self.local.snapshots(parts=True):  # local creation order, one batched read
+            sid = x.session_id
+            for p in x.participants:
                 if p.agent_did == agent_did and p.is_active:
                     key = (self._session_seq[sid] << 8) | int(p.ring)
                     if key < best:
@@ -342,12 +344,12 @@ class ShardedHypervisor:
 
     def list_sessions(self, state: Optional[str] = None) -> list[dict]:
         local = []
-        for m in self.local.sessions:
-            sid = m.sso.session_id
-            st = m.sso.state.value
+        for x in self.local.snapshots():
+            sid = x.session_id
+            st = x.state.value
             if state is None or st == state:
                 local.append((self._session_seq.get(sid, 1 << 62),
-                              {"session_id": sid, "state": st, "participant_count": m.sso.participant_count,
+                              {"session_id": sid, "state": st, "participant_count": x.participant_count,
                                "rank": self.rank}))
         return [d for _, d in sorted((x for part in self._gather(local) for x in part), key=lambda x: x[0])]
 

@@ -57,6 +57,7 @@ from hypervisor.saga.state_machine import (
     StepState,
 )
 from hypervisor.session import SessionLifecycleError, SessionParticipantError, SharedSessionObject
+from hypervisor.session.snapshot import SessionSnapshot
 from hypervisor.session.sso import SessionVFS
 
 _STATES = list(SessionState)
@@ -831,10 +832,13 @@ class DeviceCommitmentEngine(CommitmentEngine):
     @property
     def _commitments_view(self) -> dict[str, CommitmentRecord]:
         out = {}
-        for sid, sso in self._device.items():
-            rec = self._record(sso)
-            if rec is not None:
-                out[sid] = rec
+        ssos = list(self._device.values())
+        for sso, x in zip(ssos, snapshots(self._store, ssos, parts=True)):  # one batched read
+            if x.committed_at is not None:
+                out[sso.session_id] = CommitmentRecord(
+                    session_id=sso.session_id, merkle_root=x.merkle_root,
+                    participant_dids=[p.agent_did for p in x.participants], delta_count=x.commit_count,
+                    committed_at=x.committed_at)
         out.update(self._commitments)
         return out
 
@@ -1090,6 +1094,57 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         return failed
 
 
+def snapshots(store: GovernanceStore, ssos: list, parts: bool = False) -> list[SessionSnapshot]:
+    """Snapshots of many device sessions with O(1) store commands (OP_SESS_READ_MANY)."""
+    if not ssos:
+        return []
+    hdr, prt = store.read_sessions([x.slot for x in ssos], parts=parts)
+    out = []
+    for i, sso in enumerate(ssos):
+        h = hdr[i]
+        s = SessionSnapshot()
+        w0 = int(h[0])
+        s.session_id = sso.session_id
+        s.state = _STATES[w0 & 0xFF]
+        s.consistency_mode = _MODES[(w0 >> 8) & 0xFF]
+        w1 = int(h[1])
+        pc = w1 & 0xFFFFFFFF
+        s.participant_count = (w1 >> 32) & 0xFFFFFFFF
+        s.created_at = from_us(_i64(int(h[2])))
+        te = _i64(int(h[3]))
+        s.terminated_at = from_us(te) if te else None
+        s.delta_count = int(h[4]) & 0xFFFFFFFF
+        s.creator_did = sso.creator_did
+        c = _i64(int(h[7]))
+        s.committed_at = from_us(c) if c else None
+        s.commit_count = (int(h[4]) >> 32) & 0xFFFFFFFF
+        s.merkle_root = "".join(f"{int(w):016x}" for w in h[12:16]) if c else None
+        if parts:
+            plist = []
+            for k in range(pc):
+                a, fl, sr, se, j = (int(x) for x in prt[i, k])
+                if (fl >> 8) & 0xFF:
+                    plist.append(SessionParticipant(
+                        agent_did=store.did(_i64(a)), ring=_RINGS[fl & 0xFF], sigma_raw=bitsd(sr), sigma_eff=bitsd(se),
+                        joined_at=from_us(_i64(j)), is_active=True))
+            s.participants = plist
+        else:
+            s.participants = None
+        out.append(s)
+    return out
+
+
+def saga_rows(store: GovernanceStore, sagas: list) -> dict:
+    """States / timestamps of many device sagas and their steps: one column gather
+    per field (O(1) store commands).  ``{"g_state": [...], "steps": {col: [...]}}``
+    in saga order, steps flattened in saga-then-step order."""
+    gi = [g.slot for g in sagas]
+    ti = [st.slot for g in sagas for st in g.steps]
+    out = store.gather({"g_state": gi, "g_created": gi, "g_completed": gi,
+                        "t_state": ti, "t_retry": ti, "t_started": ti, "t_completed": ti})
+    return out
+
+
 def session_views(store: GovernanceStore, sso: DeviceSession):
     """(delta engine, saga orchestrator) for a device session."""
     return DeviceDeltaEngine(store, sso.slot, sso.session_id, sso), DeviceSagaOrchestrator(store)
@@ -1098,4 +1153,5 @@ def session_views(store: GovernanceStore, sso: DeviceSession):
 __all__ = [
     "DeviceSession", "DeviceDelta", "DeviceDeltaEngine", "DeviceVouchRecord", "DeviceVouchingEngine",
     "DeviceSlashingEngine", "DeviceCommitmentEngine", "DeviceSaga", "DeviceSagaStep", "DeviceSagaOrchestrator",
+    "SessionSnapshot", "snapshots", "saga_rows",
 ]

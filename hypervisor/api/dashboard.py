@@ -27,40 +27,39 @@ def summary(st, limit: int = 200) -> dict[str, Any]:
     """Every tab's data from the live hypervisor (capped at ``limit`` rows each)."""
     hv, bus = st.hv, st.bus
     sessions = hv.sessions
+    snaps = hv.snapshots(sessions, parts=True)  # one batched device read
     rings: Counter = Counter()
     states: Counter = Counter()
     session_rows, agent_rows = [], []
-    for m in sessions:
-        sso = m.sso
-        states[sso.state.value] += 1
-        for p in sso.participants:
+    for m, x in zip(sessions, snaps):
+        states[x.state.value] += 1
+        for p in x.participants:
             rings[p.ring.name] += 1
             if len(agent_rows) < limit:
-                agent_rows.append({"agent_did": p.agent_did, "session_id": sso.session_id, "ring": int(p.ring),
+                agent_rows.append({"agent_did": p.agent_did, "session_id": x.session_id, "ring": int(p.ring),
                                    "ring_name": p.ring.name, "sigma_raw": round(p.sigma_raw, 4),
                                    "sigma_eff": round(p.sigma_eff, 4), "active": bool(p.is_active)})
         if len(session_rows) < limit:
             de = m.delta_engine
-            session_rows.append({"session_id": sso.session_id, "state": sso.state.value,
-                                 "participants": sso.participant_count, "created_at": _iso(sso.created_at),
+            session_rows.append({"session_id": x.session_id, "state": x.state.value,
+                                 "participants": x.participant_count, "created_at": _iso(x.created_at),
                                  "deltas": de.turn_count if de is not None else 0,
-                                 "merkle_root": getattr(hv.commitment.get_commitment(sso.session_id),
-                                                        "merkle_root", None)})
+                                 "merkle_root": x.merkle_root if x.committed_at is not None else
+                                 getattr(hv.commitment.get_commitment(x.session_id), "merkle_root", None)})
     sagas: Counter = Counter()
     steps: Counter = Counter()
     saga_rows = []
-    for m in sessions:
-        for g in m.saga.sagas:
-            sagas[g.state.value] += 1
-            for s_ in g.steps:
-                steps[s_.state.value] += 1
-            if len(saga_rows) < limit:
-                saga_rows.append({
-                    "saga_id": g.saga_id, "session_id": g.session_id, "state": g.state.value, "error": g.error,
-                    "created_at": _iso(g.created_at), "completed_at": _iso(g.completed_at),
-                    "steps": [{"action_id": x.action_id, "agent_did": x.agent_did, "state": x.state.value,
-                               "retry_count": x.retry_count, "error": x.error, "started_at": _iso(x.started_at),
-                               "completed_at": _iso(x.completed_at)} for x in g.steps]})
+    for g in hv.saga_summaries(sessions):  # one column gather per field
+        sagas[g["state"]] += 1
+        for s_ in g["steps"]:
+            steps[s_["state"]] += 1
+        if len(saga_rows) < limit:
+            saga_rows.append({
+                "saga_id": g["saga_id"], "session_id": g["session_id"], "state": g["state"], "error": g["error"],
+                "created_at": _iso(g["created_at"]), "completed_at": _iso(g["completed_at"]),
+                "steps": [{"action_id": x["action_id"], "agent_did": x["agent_did"], "state": x["state"],
+                           "retry_count": x["retry_count"], "error": x["error"], "started_at": _iso(x["started_at"]),
+                           "completed_at": _iso(x["completed_at"])} for x in g["steps"]]})
     exposure: Counter = Counter()
     vouch_rows = []
     for v in hv.vouching.records():
@@ -92,8 +91,8 @@ def summary(st, limit: int = 200) -> dict[str, Any]:
     return {
         "overview": {
             "sessions": len(sessions),
-            "active_sessions": len(hv.active_sessions),
-            "participants": sum(m.sso.participant_count for m in sessions),
+            "active_sessions": sum(1 for x in snaps if x.state.value not in ("archived", "terminating")),
+            "participants": sum(x.participant_count for x in snaps),
             "vouches": len(hv.vouching.records()),
             "slashes": len(hv.slashing.history),
             "commitments": hv.commitment.commitment_count,

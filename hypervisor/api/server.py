@@ -111,13 +111,14 @@ async def health_check() -> dict[str, str]:
 async def get_stats(request: Request) -> StatsResponse:
     st = _state(request)
     hv = st.hv
-    sessions = hv.sessions
+    snaps = hv.snapshots()  # one batched device read for all sessions
+    sagas = hv.saga_summaries()
     return StatsResponse(
         version=__version__,
-        total_sessions=len(sessions),
-        active_sessions=len(hv.active_sessions),
-        total_participants=sum(m.sso.participant_count for m in sessions),
-        active_sagas=sum(len(m.saga.active_sagas) for m in sessions),
+        total_sessions=len(snaps),
+        active_sessions=sum(1 for x in snaps if x.state.value not in ("archived", "terminating")),
+        total_participants=sum(x.participant_count for x in snaps),
+        active_sagas=sum(1 for g in sagas if g["state"] in ("running", "compensating")),
         total_vouches=len(hv.vouching.records()),
         event_count=st.bus.event_count,
         batched_sessions=hv._device_engine.sessions_run if hv._device_engine is not None else 0,
@@ -139,7 +140,7 @@ async def create_session(req: CreateSessionRequest, request: Request) -> CreateS
 async def list_sessions(
     request: Request, state: Optional[str] = Query(None, description="Filter by session state")
 ) -> list[SessionListItem]:
-    return [SessionListItem.of(m.sso) for m in _state(request).hv.sessions if not state or m.sso.state.value == state]
+    return [SessionListItem.of(x) for x in _state(request).hv.snapshots() if not state or x.state.value == state]
 
 
 @router.get("/api/v1/sessions/{session_id}", response_model=SessionDetailResponse, tags=["Sessions"])
@@ -198,11 +199,11 @@ async def get_ring_distribution(session_id: str, request: Request) -> RingDistri
 
 @router.get("/api/v1/agents/{agent_did}/ring", response_model=AgentRingResponse, tags=["Rings"])
 async def get_agent_ring(agent_did: str, request: Request) -> AgentRingResponse:
-    for m in _state(request).hv.sessions:
-        for p in m.sso.participants:
+    for x in _state(request).hv.snapshots(parts=True):
+        for p in x.participants:
             if p.agent_did == agent_did and p.is_active:
                 return AgentRingResponse(agent_did=agent_did, ring=p.ring.value, ring_name=p.ring.name,
-                                         session_id=m.sso.session_id)
+                                         session_id=x.session_id)
     raise HTTPException(status_code=404, detail=f"Agent {agent_did} not found in any session")
 
 

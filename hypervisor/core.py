@@ -383,7 +383,60 @@ class Hypervisor:
 
     @property
     def active_sessions(self) -> list[ManagedSession]:
-        return [m for m in self._sessions.values() if m.sso.state.value not in ("archived", "terminating")]
+        ms = list(self._sessions.values())
+        snaps = self.snapshots(ms)
+        return [m for m, sn in zip(ms, snaps) if sn.state.value not in ("archived", "terminating")]
+
+    def snapshots(self, managed: Optional[list] = None, parts: bool = False) -> list:
+        """:class:`~hypervisor.session.snapshot.SessionSnapshot` of each session (all by
+        default, creation order); device-backed: O(1) store commands for any count."""
+        ms = list(self._sessions.values()) if managed is None else list(managed)
+        if self._store is not None:
+            from hypervisor import _device
+
+            return _device.snapshots(self._store, [m.sso for m in ms], parts)
+        from hypervisor.session.snapshot import SessionSnapshot
+
+        return [SessionSnapshot.of(m.sso, parts) for m in ms]
+
+    def saga_summaries(self, managed: Optional[list] = None) -> list[dict]:
+        """Every saga of the given sessions with its step rows, as plain dicts
+        (``state`` values, timestamps, retry counts); device-backed: one column
+        gather per field."""
+        from hypervisor._clock import from_us
+        from hypervisor.saga.state_machine import SagaState, StepState
+
+        ms = list(self._sessions.values()) if managed is None else list(managed)
+        sagas = [g for m in ms for g in m.saga.sagas]
+        out = []
+        if self._store is not None and sagas:
+            from hypervisor import _device
+
+            rows = _device.saga_rows(self._store, sagas)
+            gst, sst = list(SagaState), list(StepState)
+            k = 0
+            for i, g in enumerate(sagas):
+                steps = []
+                for x in g.steps:
+                    t0, t1 = int(rows["t_started"][k]), int(rows["t_completed"][k])
+                    steps.append({"step_id": x.step_id, "action_id": x.action_id, "agent_did": x.agent_did,
+                                  "state": sst[int(rows["t_state"][k]) & 0xFF].value,
+                                  "retry_count": int(rows["t_retry"][k]), "error": x.error,
+                                  "started_at": from_us(t0) if t0 else None, "completed_at": from_us(t1) if t1 else None})
+                    k += 1
+                c1 = int(rows["g_completed"][i])
+                out.append({"saga_id": g.saga_id, "session_id": g.session_id,
+                            "state": gst[int(rows["g_state"][i]) & 0xFF].value, "error": g.error,
+                            "created_at": from_us(int(rows["g_created"][i])),
+                            "completed_at": from_us(c1) if c1 else None, "steps": steps})
+            return out
+        for g in sagas:
+            out.append({"saga_id": g.saga_id, "session_id": g.session_id, "state": g.state.value, "error": g.error,
+                        "created_at": g.created_at, "completed_at": g.completed_at,
+                        "steps": [{"step_id": x.step_id, "action_id": x.action_id, "agent_did": x.agent_did,
+                                   "state": x.state.value, "retry_count": x.retry_count, "error": x.error,
+                                   "started_at": x.started_at, "completed_at": x.completed_at} for x in g.steps]})
+        return out
 
     def _get_session(self, session_id: str) -> ManagedSession:
         m = self._sessions.get(session_id)
