@@ -180,6 +180,8 @@ class GovernanceStore:
         self._tenant_v: dict[int, dict[str, int]] = {}  # tenant → liability session id → V row
         self._tenants = 0
         self.grows = {k: 0 for k in ("S", "G", "T", "E", "V", "D", "B")}
+        self._waiters: list = []  # (seq, nres, future) of suspended asyncio calls
+        self._polling = False
         self.seed = int.from_bytes(os.urandom(8), "little") >> 1
 
     # -- allocation ----------------------------------------------------------
@@ -368,6 +370,55 @@ class GovernanceStore:
             tries += 1
             r = self._c.restore_delta(data)
         return r
+
+    # -- asyncio API -------------------------------------------------------------
+    SPIN_NS = 150_000  # spin this long for a result when the event loop has nothing else to run
+
+    async def result_async(self, seq: int, nres: int = 4) -> tuple:
+        """The results of ``seq`` without blocking the event loop: when other tasks
+        are ready (many sessions in flight) the caller suspends at once and a
+        loop-driven poller resumes it; otherwise it spins briefly first (a lone
+        pipeline's round trip is a few µs, cheaper than a suspension)."""
+        import asyncio
+
+        loop = asyncio.get_running_loop()
+        ready = getattr(loop, "_ready", None)
+        spin = 0 if ready else self.SPIN_NS
+        r = self._c.try_result(seq, nres, spin)
+        if r is not None:
+            return r
+        fut = loop.create_future()
+        self._waiters.append((seq, nres, fut))
+        if not self._polling:
+            self._polling = True
+            loop.call_soon(self._poll, loop)
+        return await fut
+
+    def _poll(self, loop) -> None:
+        ws = self._waiters
+        self._waiters = []
+        keep = []
+        for w in ws:
+            try:
+                r = self._c.try_result(w[0], w[1], 0)
+            except Exception as e:  # noqa: BLE001 - delivered to the awaiting call
+                if not w[2].done():
+                    w[2].set_exception(e)
+                continue
+            if r is None:
+                keep.append(w)
+            elif not w[2].done():
+                w[2].set_result(r)
+        if self._waiters:
+            keep.extend(self._waiters)
+        self._waiters = keep
+        if keep:
+            loop.call_soon(self._poll, loop)
+        else:
+            self._polling = False
+
+    async def call_async(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
+        return await self.result_async(self._c.post(op, args, inline), nres)
 
     def drain(self) -> None:
         self._c.drain()

@@ -214,7 +214,7 @@ def merge_slash_sparse(
 
 def merge_slash_fixed(
     sigma: torch.Tensor, blacklist_ids: torch.Tensor, pair_ids: torch.Tensor, pair_factors: torch.Tensor,
-    floor: float = 0.05, factor: Optional[torch.Tensor] = None,
+    floor: float = 0.05, factor: Optional[torch.Tensor] = None, blacklist_codes: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """X02 for a slash stage inside a timed step: fixed-capacity buffers (unused
     entries id −1 / factor 1, the ``slash_clip`` kernel's output) are all-gathered
@@ -226,30 +226,47 @@ def merge_slash_fixed(
 
     Product order across duplicate (agent, factor) pairs is not fixed, so σ may
     differ from :func:`merge_slash_sparse` in the last bit where an agent is
-    clipped more than once in one step."""
+    clipped more than once in one step.
+
+    ``blacklist_codes`` (int32, per blacklist entry; default all 2) carries the
+    blacklist-then-clip convention of :func:`merge_slash_effects`: 1 = the agent
+    was clipped after its blacklist on its rank (ends at the floor), 2 = zero;
+    the larger code wins across ranks."""
     from agent_hypervisor_amd.ops._launch import launch
 
     bl = blacklist_ids.to(torch.int32)
     pi = pair_ids.to(torch.int32)
     pf = pair_factors.to(torch.float64)
+    bc = None if blacklist_codes is None else blacklist_codes.to(device=bl.device, dtype=torch.int32)
+    if bc is not None and bc.numel() != bl.numel():
+        raise ValueError("blacklist_codes must have one entry per blacklist id")
     if _ready():
-        # one collective: the three fixed-capacity buffers travel as one byte row
+        # one collective: the fixed-capacity buffers travel as one byte row
         c = _comm()
         w = c.get_world_size()
         nb, ni = bl.numel() * 4, pi.numel() * 4
-        row = torch.cat([bl.contiguous().view(torch.uint8), pi.contiguous().view(torch.uint8),
-                         pf.contiguous().view(torch.uint8)])
+        parts = [bl.contiguous().view(torch.uint8), pi.contiguous().view(torch.uint8),
+                 pf.contiguous().view(torch.uint8)]
+        if bc is not None:
+            parts.append(bc.contiguous().view(torch.uint8))
+        row = torch.cat(parts)
         rows = [torch.empty_like(row) for _ in range(w)]
         c.all_gather(rows, row)
+        nf = pf.numel() * 8
         bl = torch.cat([r[:nb] for r in rows]).view(torch.int32)
         pi = torch.cat([r[nb:nb + ni] for r in rows]).view(torch.int32)
-        pf = torch.cat([r[nb + ni:] for r in rows]).view(torch.float64)
+        pf = torch.cat([r[nb + ni:nb + ni + nf] for r in rows]).view(torch.float64)
+        if bc is not None:
+            bc = torch.cat([r[nb + ni + nf:] for r in rows]).view(torch.int32)
     if factor is None:
         factor = torch.ones_like(sigma)
-    launch("x02_apply", {"npairs": int(pi.numel()), "nbl": int(bl.numel()), "floor": float(floor)},
-           {"pair_id": pi, "pair_f": pf, "bl": bl, "factor": factor, "sigma": sigma},
-           {"pair_id": torch.int32, "pair_f": torch.float64, "bl": torch.int32, "factor": torch.float64,
-            "sigma": torch.float64})
+    tensors = {"pair_id": pi, "pair_f": pf, "bl": bl, "factor": factor, "sigma": sigma}
+    dtypes = {"pair_id": torch.int32, "pair_f": torch.float64, "bl": torch.int32, "factor": torch.float64,
+              "sigma": torch.float64}
+    if bc is not None:
+        tensors["bl_code"] = bc
+        dtypes["bl_code"] = torch.int32
+    launch("x02_apply", {"npairs": int(pi.numel()), "nbl": int(bl.numel()), "floor": float(floor)}, tensors, dtypes)
     return sigma
 
 

@@ -114,10 +114,32 @@ def _staging_dir(d: str) -> str:
     return tempfile.mkdtemp(prefix="." + os.path.basename(os.path.abspath(d)) + ".tmp-", dir=parent)
 
 
+def recover(d: str) -> str:
+    """The checkpoint directory to load for ``d``: ``d`` itself, or — when a crash
+    hit :func:`_publish` between its two renames — the previous checkpoint left
+    at ``d.old-*`` (moved back into place).  Staging directories are never
+    loaded."""
+    import glob
+
+    d = os.path.abspath(d)
+    if os.path.exists(os.path.join(d, "manifest.json")):
+        return d
+    olds = sorted(glob.glob(d + ".old-*"), key=os.path.getmtime, reverse=True)
+    for o in olds:
+        if os.path.exists(os.path.join(o, "manifest.json")):
+            if not os.path.exists(d):
+                os.replace(o, d)
+                return d
+            return o
+    return d
+
+
 def _publish(tmp: str, d: str) -> str:
     """Replace ``d`` by the complete checkpoint in ``tmp``.  A crash before this
     point leaves the previous checkpoint intact; the swap itself is two renames
-    (the old directory is removed only after the new one is in place)."""
+    (the old directory is removed only after the new one is in place), and a
+    crash between them leaves the old one at ``d.old-*``, which :func:`recover`
+    (called by every loader) moves back."""
     import shutil
 
     d = os.path.abspath(d)
@@ -182,6 +204,8 @@ def load_engine(d: str, device: Optional[str] = None, verify: bool = True):
     from safetensors.torch import load_file
 
     from agent_hypervisor_amd.models.engine import GovernanceEngine
+
+    d = recover(d)
     from agent_hypervisor_amd.models.tables import SessionTable
 
     read_manifest(d, "engine")
@@ -296,9 +320,20 @@ def _session_record(m) -> dict:
     }
 
 
-def save_hypervisor(hv, d: str) -> str:
-    """Write the hypervisor's state as a checkpoint directory (atomically replaced)."""
+def save_hypervisor(hv, d: str, extra_files: Optional[dict] = None) -> str:
+    """Write the hypervisor's state as a checkpoint directory (atomically replaced).
+
+    ``extra_files`` (name → text) are written into the same staging directory and
+    listed in the manifest, so they are published together with the state (the
+    sharded façade keeps its routing metadata there)."""
     final, d = d, _staging_dir(d)
+    extra = dict(extra_files or {})
+    for name, text in extra.items():
+        if os.path.basename(name) != name or name in ("sessions.jsonl", "liability.json", "commitments.json",
+                                                       "manifest.json"):
+            raise ValueError(f"invalid extra checkpoint file name {name!r}")
+        with open(os.path.join(d, name), "w") as f:
+            f.write(text)
     with open(os.path.join(d, "sessions.jsonl"), "w") as f:
         for m in hv.sessions:
             f.write(json.dumps(_session_record(m), sort_keys=True) + "\n")
@@ -317,7 +352,7 @@ def save_hypervisor(hv, d: str) -> str:
              "blockchain_tx_id": c.blockchain_tx_id, "committed_to": c.committed_to}
             for c in hv.commitment.all_commitments()
         ], f)
-    _write_manifest(d, "hypervisor", ["sessions.jsonl", "liability.json", "commitments.json"],
+    _write_manifest(d, "hypervisor", ["sessions.jsonl", "liability.json", "commitments.json", *sorted(extra)],
                     {"sessions": len(hv.sessions)})
     _publish(d, final)
     return final
@@ -368,12 +403,32 @@ def _delta_from_record(rec: dict):
     return d
 
 
+def checkpoint_session_keys(d: str) -> list[str]:
+    """Every session id a hypervisor checkpoint holds state for: its sessions and
+    the liability-only session ids of its vouch records (failover re-homes both)."""
+    d = recover(d)
+    read_manifest(d, "hypervisor")
+    keys = []
+    with open(os.path.join(d, "sessions.jsonl")) as f:
+        for line in f:
+            if line.strip():
+                keys.append(json.loads(line)["session_id"])
+    seen = set(keys)
+    with open(os.path.join(d, "liability.json")) as f:
+        for v in json.load(f):
+            if v["session_id"] not in seen:
+                seen.add(v["session_id"])
+                keys.append(v["session_id"])
+    return keys
+
+
 def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
     """Resume a :class:`hypervisor.Hypervisor` from ``d`` (into ``hv`` if given).
 
     ``sessions``: restore only these session ids (with their vouch bonds and
     commitments) — failover re-homes a dead rank's sessions onto survivors this
     way (:func:`agent_hypervisor_amd.parallel.resilience.rehydrate`)."""
+    d = recover(d)
     from hypervisor.audit.commitment import CommitmentRecord
     from hypervisor.core import Hypervisor, ManagedSession
     from hypervisor.liability.vouching import VouchRecord

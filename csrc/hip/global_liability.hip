@@ -112,6 +112,8 @@ struct X02Args {
   const int32_t* bl;         // [nbl] (−1 = unused)
   double* factor;            // [A] all ones between calls
   double* sigma;             // [A]
+  const int32_t* bl_code;    // [nbl] merge code per blacklist entry (null: all 2), see below
+  int32_t phase;             // x02_blacklist_kernel pass: 1 floors code-1 entries, 2 zeroes code-2 entries
 };
 
 __device__ void atomic_mul(double* p, double f) {
@@ -143,9 +145,19 @@ __global__ __launch_bounds__(256) void x02_apply_kernel(X02Args a) {
   }
 }
 
+// Blacklist codes (the exact merge's convention, collectives.merge_slash_effects):
+// 2 = blacklisted → σ 0; 1 = blacklisted and then clipped on its rank → the floor.
+// Across ranks the larger code wins (MAX): pass 1 floors the code-1 agents, pass 2
+// zeroes the code-2 agents afterwards.
+__host__ __device__ __forceinline__ int32_t x02_code(const X02Args& a, int64_t i) { return a.bl_code ? a.bl_code[i] : 2; }
+
 __global__ __launch_bounds__(256) void x02_blacklist_kernel(X02Args a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < a.nbl && a.bl[i] >= 0) a.sigma[a.bl[i]] = 0.0;
+  if (i < a.nbl && a.bl[i] >= 0) {
+    const int32_t c = x02_code(a, i);
+    if (a.phase == 1 && c == 1) a.sigma[a.bl[i]] = a.floor;
+    if (a.phase == 2 && c >= 2) a.sigma[a.bl[i]] = 0.0;
+  }
 }
 
 int grid_for(int64_t n) {
@@ -180,7 +192,8 @@ ClipArgs to_clip(const py::dict& d) {
 X02Args to_x02(const py::dict& d) {
   return X02Args{d["npairs"].cast<int64_t>(), d["nbl"].cast<int64_t>(), d["floor"].cast<double>(),
                  P<const int32_t>(d, "pair_id"), P<const double>(d, "pair_f"), P<const int32_t>(d, "bl"),
-                 P<double>(d, "factor"), P<double>(d, "sigma")};
+                 P<double>(d, "factor"), P<double>(d, "sigma"),
+                 d.contains("bl_code") ? P<const int32_t>(d, "bl_code") : nullptr, 0};
 }
 
 }  // namespace
@@ -222,7 +235,13 @@ void register_global_liability(py::module_& m) {
         const int gb = static_cast<int>((std::max<int64_t>(a.nbl, 1) + 255) / 256);
         hipLaunchKernelGGL(x02_mul_kernel, dim3(gp), dim3(256), 0, st, a);
         hipLaunchKernelGGL(x02_apply_kernel, dim3(gp), dim3(256), 0, st, a);
-        hipLaunchKernelGGL(x02_blacklist_kernel, dim3(gb), dim3(256), 0, st, a);
+        X02Args b = a;
+        if (a.bl_code) {
+          b.phase = 1;
+          hipLaunchKernelGGL(x02_blacklist_kernel, dim3(gb), dim3(256), 0, st, b);
+        }
+        b.phase = 2;
+        hipLaunchKernelGGL(x02_blacklist_kernel, dim3(gb), dim3(256), 0, st, b);
         check_hip(hipGetLastError(), "x02_apply");
       },
       py::arg("args"), py::arg("stream"));
@@ -240,8 +259,13 @@ void register_global_liability(py::module_& m) {
         a.sigma[id] = v < a.floor ? a.floor : v;
       }
     }
-    for (int64_t i = 0; i < a.nbl; ++i)
-      if (a.bl[i] >= 0) a.sigma[a.bl[i]] = 0.0;
+    for (int phase = 1; phase <= 2; ++phase)
+      for (int64_t i = 0; i < a.nbl; ++i) {
+        if (a.bl[i] < 0) continue;
+        const int32_t c = x02_code(a, i);
+        if (phase == 1 && c == 1) a.sigma[a.bl[i]] = a.floor;
+        if (phase == 2 && c >= 2) a.sigma[a.bl[i]] = 0.0;
+      }
   });
   m.def("slash_clip_host", [](const py::dict& d) {
     const ClipArgs a = to_clip(d);

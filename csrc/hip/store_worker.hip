@@ -51,6 +51,113 @@ __device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ------------------------------------------------------- batched hash engine
+//
+// When several captures are queued, the hash engine takes the longest prefix of
+// the queue whose jobs belong to distinct sessions (so every job's parent digest
+// is already final — the queue is in command order) and hashes it one job per
+// lane: up to 64 independent chains advance together instead of one lane doing
+// all the rounds while 63 wait.  Each lane stages its own record into a private
+// LDS window as big-endian message words (all its loads issued back to back),
+// splices the parent's quoted digest in, compresses its blocks and completes its
+// capture's result slot.  Windows are kBatchStride = 16·16+1 words apart, so
+// when the 64 lanes read word k of their current block they hit 64 different
+// banks.  Records longer than kBatchBlocks blocks end the batch (the single-job
+// path takes them).
+constexpr int kBatchBlocks = 16;
+constexpr int kBatchStride = kBatchBlocks * 16 + 1;
+
+__device__ __forceinline__ int64_t job_blocks(const HashJob& j) { return (j.len + 9 + 63) / 64; }
+
+// Number of jobs from jobs[done % kJobs ...] the batch takes (≤ avail, ≤ 64);
+// wave-uniform.  `sess` is 64 words of LDS scratch.
+__device__ int batch_size(const HashJob* jobs, uint32_t done, uint32_t avail, int32_t* sess, int lane) {
+  const bool mine = static_cast<uint32_t>(lane) < avail;
+  const HashJob* j = &jobs[(done + lane) % kJobs];
+  const int32_t s = mine ? static_cast<int32_t>(j->s) : -1;
+  sess[lane] = s;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  bool ok = mine && job_blocks(*j) <= kBatchBlocks;
+  for (int k = 0; ok && k < lane; ++k) ok = sess[k] != s;
+  const uint64_t bad = __ballot(!ok);
+  return bad ? __builtin_ctzll(bad) : 64;
+}
+
+// Lane `lane` < n hashes job jobs[(done + lane) % kJobs] and completes it.
+__device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, int n, uint32_t* win,
+                           uint32_t* kwrows, uint64_t* res, int64_t nslots, int lane) {
+  if (lane >= n) return;
+  const HashJob j = jobs[(done + lane) % kJobs];
+  uint32_t* w = win + kBatchStride * lane;
+  const uint64_t len = static_cast<uint64_t>(j.len);
+  const int64_t nblk = job_blocks(j);
+  const int64_t nw = nblk * 16;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(t.payload + j.off);
+  // stage: independent system-scope loads of the host-written record, all in flight together
+  for (int64_t i = 0; i < nw; ++i) {
+    const uint64_t b = 4 * static_cast<uint64_t>(i);
+    uint32_t x = 0;
+    if (b + 4 <= len) {
+      x = bswap32(ld32f(s32 + i));
+    } else if (b < len) {
+      x = bswap32(ld32f(s32 + i)) & (0xffffffffu << (8 * (4 - static_cast<uint32_t>(len - b))));
+    }
+    if (b <= len && len < b + 4) x |= 0x80u << (8 * (3 - (len - b)));
+    if (i == nw - 2) x |= static_cast<uint32_t>((len * 8) >> 32);
+    if (i == nw - 1) x |= static_cast<uint32_t>(len * 8);
+    w[i] = x;
+  }
+  // parent digest: the previous delta of the chain (final: earlier in the queue,
+  // hashed by an earlier batch) or the session's chain head for turn 1
+  if (j.hole >= 0) {
+    const uint32_t* head = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
+    uint32_t hd[8];
+    load8(head, hd);
+    uint8_t* src = t.payload + j.off;
+    uint8_t* lb = reinterpret_cast<uint8_t*>(w);
+    auto put = [&](int k, uint32_t ch) {
+      const uint64_t b = static_cast<uint64_t>(j.hole) + k;
+      src[b] = static_cast<uint8_t>(ch);  // the stored record is completed too
+      lb[(b & ~uint64_t(3)) | (3 - (b & 3))] = static_cast<uint8_t>(ch);
+    };
+    put(0, 0x22u);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) put(1 + 8 * q + e, hex_nibble((hd[q] >> (28 - 4 * e)) & 15u));
+    }
+    put(65, 0x22u);
+  }
+  uint32_t h[8];
+  const int64_t skip = j.mid_blocks > 0 && j.mid_blocks < nblk ? j.mid_blocks : 0;
+  if (skip) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = j.mid[k];
+  } else {
+    sha256_init(h);
+  }
+  // per block: message schedule (+K) into the lane's K+W row, then the rounds
+  // (the split form keeps the round state in registers; see sha256_rounds_kw)
+  uint32_t* kw = kwrows + kKwStride * lane;
+  for (int64_t b = skip; b < nblk; ++b) {
+    sha256_expand_kw(w + 16 * b, kw);
+    sha256_rounds_kw(h, kw);
+  }
+  store8(t.d_hash + 8 * j.d, h);
+  store8(t.s_head + 8 * j.s, h);
+  uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out64(r + 2 + k, h[k]);
+  out64(r + 10, 0);
+  out64(r + 11, 0);
+  out64(r + 12, static_cast<uint64_t>(nblk) | (static_cast<uint64_t>(n) << 32));  // blocks | batch size
+  out64(r + 1, ST_OK);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // digest rows + result words before the sequence word
+  out64(r, j.seq + 1);
+}
+
 __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
                                                            uint64_t* res, uint8_t* bulk, uint64_t* alive,
                                                            int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks,
@@ -61,6 +168,8 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   __shared__ uint32_t lds0[kLdsWords / 4];  // wave 0: staging for its own hashing (capture prefixes)
   __shared__ uint32_t kw0[64 * kKwStride];  // wave 0: K+W schedule rows
   __shared__ HashJob jobs[kJobs];
+  __shared__ uint32_t batch_win[64 * kBatchStride];  // wave 1: per-lane record windows (batched hashing)
+  __shared__ int32_t batch_sess[64];
   __shared__ uint32_t q_head, q_done, stop, bye, spec_s;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -83,6 +192,17 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         if (lds_acquire(&stop)) break;
         __builtin_amdgcn_s_sleep(1);
         continue;
+      }
+      if ((speculate & 4) && head - done >= 2) {
+        // several captures queued: hash the distinct-session prefix one job per lane
+        const int nb = batch_size(jobs, done, head - done, batch_sess, lane);
+        if (nb >= 2) {
+          hash_batch(t, jobs, done, nb, batch_win, kw1, res, nslots, lane);
+          done += static_cast<uint32_t>(nb);
+          L.sync();
+          if (lane == 0) lds_release(&q_done, done);
+          continue;
+        }
       }
       const HashJob j = jobs[done % kJobs];
       uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;

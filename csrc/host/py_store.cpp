@@ -21,6 +21,8 @@
 
 #include <chrono>
 #include <map>
+#include <unordered_map>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -154,10 +156,13 @@ class Store {
       hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "store stream");
       idle_ticks_ = static_cast<uint64_t>(idle_us) * 100;   // s_memrealtime: 100 MHz
       // worker feature bits: 1 = provisional Merkle roots on the idle hash engine,
-      // 2 = capture prefix midstates on the command wave
+      // 2 = capture prefix midstates on the command wave,
       const char* sp = std::getenv("AHV_STORE_SPECULATE");
       const char* pf = std::getenv("AHV_STORE_PREFIX");
-      speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0);
+      // 4 = batched hashing: queued captures of distinct sessions hashed one per lane
+      const char* bt = std::getenv("AHV_STORE_BATCH");
+      speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
+                   ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0);
       max_ticks_ = static_cast<uint64_t>(max_ms) * 100000;
     } else {
       ring_ = static_cast<uint64_t*>(std::calloc(ring_bytes / 8, 8));
@@ -263,8 +268,21 @@ class Store {
     if (inl_bytes > static_cast<size_t>(kInlineWords) * 8) throw std::invalid_argument("inline payload too large");
     const uint64_t q = next_++;
     const uint64_t idx = q % static_cast<uint64_t>(nslots_);
-    // the slot's previous occupant must have completed
-    if (q >= static_cast<uint64_t>(nslots_)) wait(q - static_cast<uint64_t>(nslots_));
+    // the slot's previous occupant must have completed; if an asyncio waiter
+    // has not collected its results yet, they are kept aside first
+    if (q >= static_cast<uint64_t>(nslots_)) {
+      const uint64_t p = q - static_cast<uint64_t>(nslots_);
+      const uint64_t* pr = wait(p);
+      if (!watched_.empty()) {
+        auto it = watched_.find(p);
+        if (it != watched_.end()) {
+          std::array<uint64_t, kSaveWords> a;
+          for (int k = 0; k < kSaveWords; ++k) a[k] = pr[k];
+          saved_[p] = a;
+          watched_.erase(it);
+        }
+      }
+    }
     uint64_t w[kSlotWords];
     std::memset(w, 0, sizeof w);
     w[1] = op;
@@ -349,6 +367,47 @@ class Store {
   py::tuple call(uint32_t op, const std::vector<int64_t>& args, int nres, const py::object& inl) {
     const uint64_t q = post(op, args, inl);
     const uint64_t* r = wait(q);
+    py::tuple out(nres);
+    for (int k = 0; k < nres; ++k) out[k] = py::int_(static_cast<int64_t>(r[1 + k]));
+    return out;
+  }
+
+  // Non-blocking form for the asyncio API: the results of `q` if it completed
+  // within `spin_ns` (0: just look), else None.  A worker that idled out
+  // between the post and now is relaunched.
+  py::object try_result(uint64_t q, int nres, int64_t spin_ns) {
+    if (nres > kSaveWords - 1) throw std::invalid_argument("try_result: at most 15 result words");
+    if (!saved_.empty()) {
+      auto it = saved_.find(q);
+      if (it != saved_.end()) {
+        py::tuple out(nres);
+        for (int k = 0; k < nres; ++k) out[k] = py::int_(static_cast<int64_t>(it->second[1 + k]));
+        saved_.erase(it);
+        return out;
+      }
+    }
+    const uint64_t idx = q % static_cast<uint64_t>(nslots_);
+    volatile uint64_t* r = res_ + idx * kResWords;
+    if (q >= next_) throw std::out_of_range("store: sequence number not posted");
+    if (r[0] < q + 1 && gpu_) {
+      auto t0 = std::chrono::steady_clock::now();
+      uint32_t spins = 0;
+      while (r[0] < q + 1) {
+        if ((++spins & 255u) == 0) {
+          if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) == 0) ensure_worker();
+          if (std::chrono::steady_clock::now() - t0 >= std::chrono::nanoseconds(spin_ns)) break;
+        }
+        _mm_pause();
+      }
+      if (r[0] < q + 1) {
+        if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) == 0) ensure_worker();
+        watched_[q] = 1;  // keep the results if the slot is recycled before they are collected
+        return py::none();
+      }
+    }
+    if (!watched_.empty()) watched_.erase(q);
+    if (r[0] >= q + 1 + static_cast<uint64_t>(nslots_)) throw ResultGone();
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
     py::tuple out(nres);
     for (int k = 0; k < nres; ++k) out[k] = py::int_(static_cast<int64_t>(r[1 + k]));
     return out;
@@ -576,6 +635,9 @@ class Store {
   uint64_t launches_ = 0;
   size_t stage_head_ = 0;
   ArenaAlloc arena_;
+  static constexpr int kSaveWords = 16;
+  std::unordered_map<uint64_t, int> watched_;                             // seqs with a pending async waiter
+  std::unordered_map<uint64_t, std::array<uint64_t, kSaveWords>> saved_;  // their results, once recycled
   std::vector<int64_t> d_off_, d_len_;  // arena record of each delta row (-1: row free)
   std::vector<int32_t> dfree_;          // reclaimed delta rows
   int64_t dhw_ = 0;                      // delta rows ever handed out (high-water mark)
@@ -588,12 +650,13 @@ class Store {
 void register_store(py::module_& m) {
   py::class_<Store>(m, "Store", "Device-authoritative governance state store (gfx950 worker or CPU twin)")
       .def(py::init<int, const py::dict&, const py::dict&, int64_t, int64_t, int64_t, int64_t, int64_t>(),
-           py::arg("device"), py::arg("ptrs"), py::arg("caps"), py::arg("nslots") = 256,
+           py::arg("device"), py::arg("ptrs"), py::arg("caps"), py::arg("nslots") = 4096,
            py::arg("staging_bytes") = 1 << 22, py::arg("bulk_bytes") = 1 << 24, py::arg("idle_us") = 500,
            py::arg("max_ms") = 2000)
       .def("post", &Store::post, py::arg("op"), py::arg("args"), py::arg("inline") = py::none())
       .def("call", &Store::call, py::arg("op"), py::arg("args"), py::arg("nres") = 4, py::arg("inline") = py::none())
       .def("result", &Store::result, py::arg("seq"), py::arg("nres") = 4)
+      .def("try_result", &Store::try_result, py::arg("seq"), py::arg("nres") = 4, py::arg("spin_ns") = 0)
       .def("drain", &Store::drain)
       .def("stage", &Store::stage)
       .def("bulk", &Store::bulk)

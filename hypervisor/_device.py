@@ -230,22 +230,39 @@ class DeviceSession(SharedSessionObject):
     def activate(self) -> None:
         if self._cseq >= 0:
             self._created()
-        r = self._store.call(_st.OP_SESS_ACTIVATE, [self.slot], 2)
+        self._activated(self._store.call(_st.OP_SESS_ACTIVATE, [self.slot], 2))
+
+    async def activate_async(self) -> None:
+        if self._cseq >= 0:
+            self._created()
+        self._activated(await self._store.call_async(_st.OP_SESS_ACTIVATE, [self.slot], 2))
+
+    @staticmethod
+    def _activated(r: tuple) -> None:
         if r[0] == _st.ST_BAD_STATE:
             raise _lifecycle(r[1], SessionState.HANDSHAKING)
         if r[0] == 3:
             raise SessionLifecycleError("Cannot activate session with no participants")
         _check(r, "activate")
 
-    def _join(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> int:
+    def _join_args(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> list:
         if self._cseq >= 0:
             self._created()
-        r = self._store.call(
-            _st.OP_SESS_JOIN,
-            [self.slot, self._store.agent_id(agent_did), dbits(sigma_raw), dbits(sigma_eff), flags, ring,
-             to_us(_now())],
-            6,
-        )
+        return [self.slot, self._store.agent_id(agent_did), dbits(sigma_raw), dbits(sigma_eff), flags, ring,
+                to_us(_now())]
+
+    def _join(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> int:
+        r = self._store.call(_st.OP_SESS_JOIN, self._join_args(agent_did, sigma_raw, sigma_eff, flags, ring), 6)
+        return self._joined(r, agent_did, sigma_eff)
+
+    async def join_gated_async(self, agent_did: str, sigma_raw: float, sigma_eff: float,
+                               trustworthy: bool) -> ExecutionRing:
+        """:meth:`join_gated` without blocking the event loop on the device round trip."""
+        args = self._join_args(agent_did, sigma_raw, sigma_eff, 1 if trustworthy else 0, 0)
+        r = await self._store.call_async(_st.OP_SESS_JOIN, args, 6)
+        return _RINGS[self._joined(r, agent_did, sigma_eff)]
+
+    def _joined(self, r: tuple, agent_did: str, sigma_eff: float) -> int:
         code = r[0]
         if code == 0:
             return r[1]
@@ -907,6 +924,15 @@ class DeviceSagaStep(SagaStep):
     def transition(self, new_state: StepState, retry: int = -1) -> None:
         to = _STEPS.index(StepState(new_state))
         r = self._store.call(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], 2)
+        self._transitioned(r, new_state)
+
+    async def transition_async(self, new_state: StepState, retry: int = -1) -> None:
+        to = _STEPS.index(StepState(new_state))
+        r = await self._store.call_async(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], 2)
+        self._transitioned(r, new_state)
+
+    @staticmethod
+    def _transitioned(r: tuple, new_state) -> None:
         if r[0]:
             frm = _STEPS[r[1]]
             allowed = STEP_TRANSITIONS.get(frm, ())
@@ -1014,9 +1040,9 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         self._store = store
         self._sagas: dict[str, DeviceSaga] = {}
 
-    def create_saga(self, session_id: str) -> DeviceSaga:
+    def create_saga(self, session_id: str, saga_id: Optional[str] = None) -> DeviceSaga:
         slot = self._store.alloc("G")
-        saga = DeviceSaga(self._store, slot, _C.uuid4("saga:"), session_id)
+        saga = DeviceSaga(self._store, slot, saga_id or _C.uuid4("saga:"), session_id)
         self._store.post(_st.OP_SAGA_CREATE, [slot, to_us(_now())])
         self._sagas[saga.saga_id] = saga
         return saga
@@ -1039,7 +1065,7 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         attempts = 1 + step.max_retries
         last: Optional[Exception] = None
         for attempt in range(attempts):
-            step.transition(StepState.EXECUTING, retry=attempt)
+            await step.transition_async(StepState.EXECUTING, retry=attempt)
             try:
                 result = await await_with_timeout(executor(), step.timeout_seconds)
             except asyncio.TimeoutError:
@@ -1051,7 +1077,7 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                 last = e
             else:
                 step.execute_result = result
-                step.transition(StepState.COMMITTED)
+                await step.transition_async(StepState.COMMITTED)
                 return result
             step.error = str(last)
             step.transition(StepState.FAILED)

@@ -130,14 +130,19 @@ class Hypervisor:
             bus.emit(HypervisorEvent(event_type=etype, session_id=session_id, agent_did=agent_did, payload=payload))
 
     # -- lifecycle -------------------------------------------------------------
-    async def create_session(self, config: SessionConfig, creator_did: str) -> ManagedSession:
+    async def create_session(self, config: SessionConfig, creator_did: str,
+                             session_id: Optional[str] = None) -> ManagedSession:
+        """``session_id``: an explicit id (extension: the sharded façade mints ids
+        that route to the owner rank); default ``session:{uuid4}``."""
+        if session_id is not None and session_id in self._sessions:
+            raise ValueError(f"Session {session_id} already exists")
         if self._store is not None:
             from hypervisor import _device
 
-            sso = _device.DeviceSession(self._store, config, creator_did)  # created in HANDSHAKING
+            sso = _device.DeviceSession(self._store, config, creator_did, session_id=session_id)  # HANDSHAKING
             managed = ManagedSession(sso, *_device.session_views(self._store, sso))
         else:
-            sso = SharedSessionObject(config=config, creator_did=creator_did)
+            sso = SharedSessionObject(config=config, creator_did=creator_did, session_id=session_id)
             sso.begin_handshake()
             managed = ManagedSession(sso)
         self._sessions[sso.session_id] = managed
@@ -185,7 +190,7 @@ class Hypervisor:
                 sigma_eff = min(sigma_raw, self.nexus.resolve_sigma(agent_did, history=agent_history))
 
         if self._store is not None:  # ring gate (K01) + admission on the device
-            ring = managed.sso.join_gated(agent_did, sigma_raw, sigma_eff, verification.is_trustworthy)
+            ring = await managed.sso.join_gated_async(agent_did, sigma_raw, sigma_eff, verification.is_trustworthy)
         else:
             ring = self.ring_enforcer.compute_ring(sigma_eff)
             if not verification.is_trustworthy:
@@ -199,7 +204,11 @@ class Hypervisor:
         return ring
 
     async def activate_session(self, session_id: str) -> None:
-        self._get_session(session_id).sso.activate()
+        sso = self._get_session(session_id).sso
+        if self._store is not None:
+            await sso.activate_async()
+        else:
+            sso.activate()
         if self.event_bus is not None:
             from hypervisor.observability.event_bus import EventType
 
@@ -208,7 +217,7 @@ class Hypervisor:
     async def terminate_session(self, session_id: str) -> Optional[str]:
         managed = self._get_session(session_id)
         if self._store is not None:
-            return self._terminate_device(session_id, managed)
+            return await self._terminate_device(session_id, managed)
         sso = managed.sso
         sso.terminate()
         de = managed.delta_engine
@@ -235,7 +244,7 @@ class Hypervisor:
             self._emit(EventType.SESSION_ARCHIVED, session_id)
         return root
 
-    def _terminate_device(self, session_id: str, managed: ManagedSession) -> Optional[str]:
+    async def _terminate_device(self, session_id: str, managed: ManagedSession) -> Optional[str]:
         """One device command: terminate → Merkle root (K09) → commit → release the
         session's bonds (K07) → GC retention count → archive."""
         from datetime import timedelta
@@ -250,7 +259,7 @@ class Hypervisor:
         v = st.liability_lookup(self._tenant, session_id)
         cutoff = now - timedelta(days=self.gc.policy.delta_retention_days)
         n, off, inl = st.index_args(de._indices())
-        r = st.call(
+        r = await st.call_async(
             _st.OP_SESS_CLOSE,
             [sso.slot, n, off, to_us(now), v, to_us(cutoff), int(bool(sso.config.enable_audit))], 13, inl,
         )

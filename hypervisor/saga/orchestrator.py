@@ -47,8 +47,9 @@ class SagaOrchestrator:
     def __init__(self) -> None:
         self._sagas: dict[str, Saga] = {}
 
-    def create_saga(self, session_id: str) -> Saga:
-        saga = Saga(saga_id=_uuid4("saga:"), session_id=session_id)
+    def create_saga(self, session_id: str, saga_id: Optional[str] = None) -> Saga:
+        """``saga_id``: an explicit id (the sharded façade mints ids that route to the owner rank)."""
+        saga = Saga(saga_id=saga_id or _uuid4("saga:"), session_id=session_id)
         self._sagas[saga.saga_id] = saga
         return saga
 

@@ -21,17 +21,27 @@ def main() -> None:
     from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
     from tests.test_sharded import scenario
 
-    shv = ShardedHypervisor(device="cuda")
-    got = asyncio.run(scenario(shv))
-    x = shv.exposure_vector({f"did:agent-{a}": a for a in range(5)}, 5)  # X01 dense over RCCL
+    async def run():
+        shv = await ShardedHypervisor(device="cuda", policy="round_robin").start()
+        if dist.get_rank() != 0:
+            await shv.serve_forever()
+            return None
+        got = await scenario(shv)
+        x = await shv.exposure_vector([f"did:agent-{a}" for a in range(5)])  # X01: K04 over store edges + RCCL
+        counters = dict(shv.counters)
+        await shv.shutdown()
+        ref = await scenario(await ShardedHypervisor(device="cuda", single=True).start())
+        return got, ref, x, counters, shv.local._store.is_gpu
+
+    res = asyncio.run(run())
     ok = True
     if dist.get_rank() == 0:
-        ref = asyncio.run(scenario(ShardedHypervisor(device="cuda", single=True)))
+        got, ref, x, counters, gpu = res
         bad = [k for k in ref if got[k] != ref[k]]
         ok = not bad
         print(json.dumps({"ok": ok, "mismatch": bad, "world": dist.get_world_size(),
-                          "backend": dist.get_backend(), "exposure": x.cpu().tolist(),
-                          "store_gpu": shv.local._store.is_gpu}), flush=True)
+                          "backend": dist.get_backend(), "exposure": x, "counters": counters,
+                          "store_gpu": gpu}), flush=True)
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
 

@@ -197,3 +197,30 @@ def test_group_is_thread_local():
     finally:
         X.set_thread_group(None)
     assert seen == [1]
+
+
+def test_merge_slash_fixed_floored_codes_match_sparse():
+    """Blacklist-then-clip (code 1 → floor) on one rank, plain blacklist (code 2 → 0)
+    on another: the fixed-capacity path with codes equals the exact sparse merge."""
+    world = 3
+    sigma, per_rank = _slash_inputs(world, seed=11)
+    cap = 16
+
+    def body(rank):
+        ids, f, bl = per_rank[rank]
+        floored = bl[: max(1, bl.numel() // 2)] if rank != 1 else bl[:0]
+        pi = torch.full((cap,), -1, dtype=torch.int32)
+        pf = torch.ones(cap, dtype=torch.float64)
+        pi[: ids.numel()] = ids
+        pf[: f.numel()] = f
+        b = torch.full((4,), -1, dtype=torch.int32)
+        b[: bl.numel()] = bl
+        codes = torch.full((4,), 2, dtype=torch.int32)
+        codes[: bl.numel()] = torch.where(torch.isin(bl, floored), 1, 2).to(torch.int32)
+        fixed = X.merge_slash_fixed(sigma.clone(), b, pi, pf, blacklist_codes=codes)
+        return fixed, X.merge_slash_sparse(sigma, bl, ids, f, floored_ids=floored)
+
+    outs = run_ranks(world, body)
+    for fixed, sparse in outs:
+        torch.testing.assert_close(fixed, sparse, rtol=0, atol=0)
+    assert any(bool((o[1] == 0.05).any()) for o in outs)  # the floor case is exercised

@@ -1,7 +1,9 @@
-"""Sharded Hypervisor (one process per GPU): every route's answer on 2/4 ranks
-equals the single-rank answer for the same workload (gloo on CPU; the same code
-runs with RCCL on MI355X, tests/test_gpu_dist.py).  Also: the rank-0 REST
-front-end with followers, and failover never placing on a dead rank."""
+"""Sharded Hypervisor (one process per GPU, rank-local serving): every route's
+answer on 2/4 ranks equals the single-rank answer for the same workload (gloo on
+CPU; the same code runs with RCCL on MI355X, tests/test_gpu_dist.py).  Rank 0
+drives the workload; per-session calls run on their owner (forwarded when rank 0
+is not the owner) while the other ranks serve; views combine every rank.  Also:
+the REST front-end, and failover re-homing sessions and liability-only bonds."""
 
 from __future__ import annotations
 
@@ -43,7 +45,7 @@ async def scenario(shv) -> dict:
             await shv.activate_session(sid)
         for d in range(k % 3):
             await shv.capture(sid, agents[k % 5], [VFSChange(path=f"/f{d}", operation="add", content_hash=f"h{d}")])
-    # liability: session-scoped vouches, one slash cascade
+    # liability: session-scoped vouches, one slash cascade, bonds on a liability-only session
     errors = []
     for k, sid in enumerate(sids[:4]):
         await shv.vouch(agents[k % 5], agents[(k + 1) % 5], sid, 0.9, bond_pct=0.3)
@@ -52,6 +54,7 @@ async def scenario(shv) -> dict:
             await shv.vouch(agents[(k + 1) % 5], agents[k % 5], sid, 0.9)  # cycle → rejected on the owner
         except Exception as e:  # noqa: BLE001
             errors.append(type(e).__name__)
+    await shv.vouch(agents[3], agents[4], "liability-only", 0.95, bond_pct=0.1)
     scores = {a: 0.7 for a in agents}
     sl = await shv.slash(agents[1], sids[0], 0.7, 0.95, "drift", scores)
     # sagas, routed by id
@@ -59,27 +62,28 @@ async def scenario(shv) -> dict:
     st1 = await shv.add_step(gid, "a", agents[1], "/a", undo_api="/u")
     st2 = await shv.add_step(gid, "b", agents[2], "/b")
     for st in (st1, st2):
-        await shv.execute_step(gid, st, lambda: asyncio.sleep(0))
-    failed = await shv.compensate(gid, lambda step: asyncio.sleep(0))
+        await shv.execute_step(gid, st, "noop")
+    failed = await shv.compensate(gid, "noop")
     saga = await shv.get_saga(gid)
     roots = [await shv.terminate_session(s) is not None for s in sids[3:]]
     out = {
         "rings": rings,
         "errors": errors,
-        "slash": (sl["clips"], sorted(scores.items())),
+        "slash": ([tuple(c) for c in sl["clips"]], sorted(scores.items())),
         "saga": ([s["state"] for s in saga["steps"]], saga["state"], len(failed)),
         "roots": roots,
-        "stats": shv.stats(),
+        "stats": await shv.stats(),
         "agent_ring": [],
         "liability": [],
-        "sessions": [(idx[d["session_id"]], d["state"], d["participant_count"]) for d in shv.list_sessions()],
+        "sessions": [(idx[d["session_id"]], d["state"], d["participant_count"]) for d in await shv.list_sessions()],
         "sigma": await shv.compute_sigma_eff(agents[2], sids[2], 0.5, 0.65),
         "exposure": await shv.get_total_exposure(agents[2], sids[2]),
+        "exposure_vector": await shv.exposure_vector(agents + ["did:nobody"]),
     }
     for a in agents + ["did:nobody"]:
-        r = shv.agent_ring(a)
+        r = await shv.agent_ring(a)
         out["agent_ring"].append(None if r is None else (r["ring"], idx[r["session_id"]]))
-        lia = shv.agent_liability(a)
+        lia = await shv.agent_liability(a)
         out["liability"].append((
             [(v["voucher_did"], v["vouchee_did"], v["bonded_amount"], v["is_active"]) for v in lia["vouches_given"]],
             [(v["voucher_did"], v["vouchee_did"]) for v in lia["vouches_received"]],
@@ -96,13 +100,22 @@ def _worker(rank: int, world: int, port: int, store: str, q) -> None:
     try:
         from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
 
-        shv = ShardedHypervisor(device=store)
-        got = asyncio.run(scenario(shv))
-        owners = shv.directory.load
+        async def main():
+            shv = await ShardedHypervisor(device=store, policy="round_robin").start()
+            if rank != 0:
+                await shv.serve_forever()
+                return None
+            got = await scenario(shv)
+            load = await shv.load()
+            counters = dict(shv.counters)
+            await shv.shutdown()
+            ref = await scenario(await ShardedHypervisor(device=store, single=True).start())
+            return got, ref, load, counters
+
+        res = asyncio.run(main())
         if rank == 0:
-            ref = asyncio.run(scenario(ShardedHypervisor(device=store, single=True)))
-            q.put((got, ref, owners))
-        dist.barrier()  # followers stay up while rank 0 builds the single-rank reference
+            q.put(res)
+        dist.barrier()
     finally:
         dist.destroy_process_group()
     # hard exit once the result is flushed: gloo's background threads can abort
@@ -120,11 +133,12 @@ def test_routes_match_single_rank(world, store):
     procs = [ctx.Process(target=_worker, args=(r, world, port, store, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got, ref, owners = q.get(timeout=240)
+    got, ref, load, counters = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert owners == [6 // world + (1 if r < 6 % world else 0) for r in range(world)]
+    assert load == [6 // world + (1 if r < 6 % world else 0) for r in range(world)]
+    assert counters["forwarded"] > 0 and counters["local"] > 0  # round-robin placement: both paths ran
     for key in ref:
         assert got[key] == ref[key], key
 
@@ -135,16 +149,21 @@ def _rest_worker(rank: int, world: int, port: int, q) -> None:
     try:
         from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor, serve_followers
 
-        shv = ShardedHypervisor()
+        shv = ShardedHypervisor(policy="round_robin")
         if rank != 0:
-            asyncio.run(serve_followers(shv))
+            async def follow():
+                await shv.start()
+                await serve_followers(shv)
+                await shv.close()
+
+            asyncio.run(follow())
             dist.barrier()  # leave together: teardown while a peer still runs can abort gloo
             return
         from fastapi.testclient import TestClient
 
         from hypervisor.api.sharded import create_sharded_app
 
-        app, driver = create_sharded_app(shv)
+        app = create_sharded_app(shv)
         with TestClient(app) as c:
             sids = [c.post("/api/v1/sessions", json={"creator_did": "did:admin"}).json()["session_id"]
                     for _ in range(3)]
@@ -159,10 +178,9 @@ def _rest_worker(rank: int, world: int, port: int, q) -> None:
                 "liability": c.get("/api/v1/agents/did:v/liability").json(),
                 "session": c.get(f"/api/v1/sessions/{sids[2]}").json(),
                 "missing": c.get("/api/v1/sessions/session:nope").status_code,
-                "owners": [shv.directory.owner(s) for s in sids],
+                "owners": [shv.owner(s) for s in sids],
                 "sids": sids,
             }
-        driver.stop()
         q.put(out)
         dist.barrier()
     finally:
@@ -216,7 +234,7 @@ def _failover_worker(rank: int, world: int, port: int, root: str, q) -> None:
     from hypervisor import SessionConfig
     from hypervisor.audit.delta import VFSChange
 
-    shv = ShardedHypervisor(device="host")
+    shv = ShardedHypervisor(device="host", policy="round_robin")
     shv.start_heartbeat(0.2)
 
     async def build():
@@ -229,52 +247,84 @@ def _failover_worker(rank: int, world: int, port: int, root: str, q) -> None:
             await shv.capture(sid, "did:agent-0", [VFSChange(path=f"/f{k}", operation="add", content_hash=f"h{k}")])
             sids.append(sid)
         await shv.vouch("did:agent-0", "did:agent-1", sids[2], 0.9, bond_pct=0.2)
+        # liability-only sessions (no hypervisor session): one homed on each rank
+        lonly = []
+        for r in range(world):
+            k = next(f"lia-{r}-{i}" for i in range(1000) if shv.owner(f"lia-{r}-{i}") == r)
+            await shv.vouch("did:agent-2", "did:agent-3", k, 0.8, bond_pct=0.25)
+            lonly.append(k)
         gid = await shv.create_saga(sids[2])
         await shv.add_step(gid, "a", "did:agent-1", "/a", undo_api="/u")
-        return sids, gid
+        return sids, gid, lonly
 
-    mark("init")
-    sids, gid = asyncio.run(build())
-    mark("built")
-    before = {s: asyncio.run(shv.get_session(s)) for s in sids}
-    roots = {s: asyncio.run(shv.merkle_root(s)) for s in sids}
-    stats0 = shv.stats()
-    liab0 = shv.agent_liability("did:agent-0")
-    shv.checkpoint(root)
-    mark("checkpointed")
-    if rank == world - 1:  # this rank dies: stop beating and leave without tearing down
-        shv.heartbeat.stop()
-        os._exit(0)
-    import time
+    async def main():
+        await shv.start()
+        mark("started")
+        if rank == 0:
+            sids, gid, lonly = await build()
+            before = {s: await shv.get_session(s) for s in sids}
+            roots = {s: await shv.merkle_root(s) for s in sids}
+            expo = {k: await shv.get_total_exposure("did:agent-2", k) for k in lonly}
+            ctx = dict(sids=sids, gid=gid, lonly=lonly, before=before, roots=roots, expo=expo,
+                       stats0=await shv.stats(), liab0=await shv.agent_liability("did:agent-0"))
+        else:
+            ctx = None
+        return ctx
 
-    deadline = time.time() + 60
-    dead = []
-    while time.time() < deadline and not dead:
-        time.sleep(0.2)
-        dead = shv.dead_ranks(3.0)  # 15 missed beats: robust to a loaded test machine
-    mark(f"suspects {dead}")
-    verdict = shv.agree_failed(dead)
-    mark(f"verdict {verdict}")
-    moves = asyncio.run(shv.failover(verdict, root))
-    mark("failed over")
-
-    async def after():
-        out = {s: await shv.get_session(s) for s in sids}
-        r = {s: await shv.merkle_root(s) for s in sids}
+    async def phase2(ctx):
+        out = {s: await shv.get_session(s) for s in ctx["sids"]}
+        r = {s: await shv.merkle_root(s) for s in ctx["sids"]}
         new = await shv.create_session(SessionConfig(), "did:admin-new")
-        await shv.capture(sids[-1], "did:agent-1", [VFSChange(path="/g", operation="add", content_hash="g")])
-        saga = await shv.get_saga(gid)
-        return out, r, new, saga
+        await shv.capture(ctx["sids"][-1], "did:agent-1", [VFSChange(path="/g", operation="add", content_hash="g")])
+        saga = await shv.get_saga(ctx["gid"])
+        expo = {k: await shv.get_total_exposure("did:agent-2", k) for k in ctx["lonly"]}
+        return out, r, new, saga, expo
 
-    out, r2, new, saga = asyncio.run(after())
-    mark("served")
-    res = dict(dead=dead, moves=len(moves), members=shv.members, stats0=stats0, stats1=shv.stats(),
-               same_sessions=all(
-                   {k: v for k, v in out[s].items() if k != "rank"} == {k: v for k, v in before[s].items()
-                                                                        if k != "rank"} for s in sids),
-               same_roots=r2 == roots, new_owner=shv.directory.owner(new),
-               liab_same=shv.agent_liability("did:agent-0") == liab0, saga_steps=len(saga["steps"]),
-               root_changed=asyncio.run(shv.merkle_root(sids[-1])) != roots[sids[-1]])
+    async def run_all():
+        ctx = await main()
+        # rank 0 built the workload (the others served it); a store key, not a collective,
+        # says so — the views rank 0 ran used the collectives meanwhile
+        from agent_hypervisor_amd.parallel.resilience import _store
+
+        st = _store()
+        if rank == 0:
+            st.set("test/built", "1")
+        else:
+            await asyncio.get_running_loop().run_in_executor(None, st.wait, ["test/built"])
+        shv.checkpoint(root)
+        mark("checkpointed")
+        if rank == world - 1:  # this rank dies: stop beating and leave without tearing down
+            shv.heartbeat.stop()
+            os._exit(0)
+        import time
+
+        deadline = time.time() + 60
+        dead = []
+        while time.time() < deadline and not dead:
+            await asyncio.sleep(0.2)
+            dead = shv.dead_ranks(3.0)  # 15 missed beats: robust to a loaded test machine
+        mark(f"suspects {dead}")
+        verdict = shv.agree_failed(dead)
+        mark(f"verdict {verdict}")
+        moves = await shv.failover(verdict, root)
+        mark("failed over")
+        if rank != 0:
+            await shv.serve_forever()
+            return None
+        out, r2, new, saga, expo2 = await phase2(ctx)
+        mark("served")
+        res = dict(dead=dead, moves=len(moves), members=shv.members, stats0=ctx["stats0"], stats1=await shv.stats(),
+                   same_sessions=all(
+                       {k: v for k, v in out[s].items() if k != "rank"} == {k: v for k, v in ctx["before"][s].items()
+                                                                            if k != "rank"} for s in ctx["sids"]),
+                   same_roots=r2 == ctx["roots"], new_owner=shv.owner(new),
+                   liab_same=await shv.agent_liability("did:agent-0") == ctx["liab0"], saga_steps=len(saga["steps"]),
+                   root_changed=await shv.merkle_root(ctx["sids"][-1]) != ctx["roots"][ctx["sids"][-1]],
+                   lonly_same=expo2 == ctx["expo"] and all(v > 0 for v in expo2.values()))
+        await shv.shutdown()
+        return res
+
+    res = asyncio.run(run_all())
     if rank == 0:
         q.put(res)
         q.close()
@@ -285,8 +335,9 @@ def _failover_worker(rank: int, world: int, port: int, root: str, q) -> None:
 
 def test_failover_rehydrates_dead_rank(tmp_path):
     """3 gloo ranks; rank 2 checkpoints and dies.  The survivors detect it from
-    the heartbeats, re-home its sessions, re-hydrate them from its checkpoint
-    (chains re-verified) and keep serving every route on survivor sub-groups."""
+    the heartbeats, agree on it, re-home its sessions *and* its liability-only
+    bonds, re-hydrate them from its checkpoint (chains re-verified)
+    and keep serving every route on survivor sub-groups."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -306,9 +357,34 @@ def test_failover_rehydrates_dead_rank(tmp_path):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res["dead"] == [2] and res["members"] == [0, 1] and res["moves"] >= 2
-    assert res["same_sessions"] and res["same_roots"] and res["liab_same"]
+    assert res["same_sessions"] and res["same_roots"] and res["liab_same"] and res["lonly_same"]
     assert res["stats1"]["total_sessions"] == res["stats0"]["total_sessions"] + 1
     assert res["new_owner"] in (0, 1) and res["saga_steps"] == 1 and res["root_changed"]
+
+
+def _agree_worker(rank: int, world: int, root: str, q) -> None:
+    dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
+    from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
+
+    shv = ShardedHypervisor(device="host")
+    # ranks hold different suspect lists (heartbeat views a beat apart)
+    verdict = shv.agree_failed([3] if rank % 2 else [2, 3])
+    q.put((rank, verdict))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_agree_failed_first_proposal_wins(tmp_path):
+    """ranks with different suspect lists adopt one verdict."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 4, str(tmp_path), q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(4))
+    for p in procs:
+        p.join(timeout=60)
+    assert len({tuple(v) for v in got.values()}) == 1 and got[0] in ([3], [2, 3])
 
 
 def _ledger_worker(rank: int, world: int, root: str, device, q) -> None:
