@@ -94,7 +94,7 @@ def default_max_caps() -> dict:
 
 _KIND = {"S": 0, "G": 1, "T": 2, "E": 3, "D": 4, "V": 5}  # csrc/include/ahv/store.h RowKind
 _EXT_OF = {"S": ("S", "S4", "S8", "SP"), "D": ("D", "D8"), "E": ("E",), "V": ("V",), "G": ("G",), "T": ("T",)}
-_FILL_NEG = ("v_head", "v_tail", "s_dlast", "d_prev", "e_next", "d_sess", "e_vsess", "t_saga")
+_FILL_NEG = ("v_head", "v_tail", "s_dlast", "d_prev", "e_next", "d_sess", "e_vsess", "t_saga", "d_hole")
 _FILL_FREE = ("s_state", "g_state", "t_state")  # kFree8
 
 

@@ -38,3 +38,84 @@ def exposure_by_agent(store, agent_ids: list[int], edges: list[int], now: int | 
     keep = live & (slot >= 0) & (voucher >= 0)
     out.index_add_(0, slot[keep], bonded[keep])
     return out
+
+
+def verify_store_chains(store, chains: list[list[int]]) -> tuple[torch.Tensor, torch.Tensor]:
+    """K10 over the store's resident audit rows: ``chains`` are lists of delta rows
+    (each a session's chain in turn order).  Returns ``(row_ok u8 [Σ], chain_ok u8
+    [len(chains)])`` on the store device.  Only the int32 row lists travel to the
+    device; the records are re-hashed from the payload arena where they live."""
+    from agent_hypervisor_amd._native import C
+    from agent_hypervisor_amd.ops._launch import launch
+
+    dev = store.device
+    rows = [d for ch in chains for d in ch]
+    first = [1 if k == 0 else 0 for ch in chains for k in range(len(ch))]
+    n = len(rows)
+    chain_ok = torch.ones(len(chains), dtype=torch.uint8, device=dev)
+    if not n:
+        return torch.zeros(0, dtype=torch.uint8, device=dev), chain_ok
+    store.drain()
+    if dev.type == "cuda":
+        store.flush()  # the worker's row writes are visible to this kernel
+    t = store.tables
+    rows_t = torch.tensor(rows, dtype=torch.int32).to(dev)
+    first_t = torch.tensor(first, dtype=torch.uint8).to(dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    launch("store_verify",
+           {"n": n, "payload": store._c.payload_ptr, "payload_cap": int(store._c.payload_cap),
+            "cap_d": int(store.caps["D"])},
+           {"rows": rows_t, "first": first_t, "d_off": t["d_off"], "d_len": t["d_len"], "d_prev": t["d_prev"],
+            "d_hole": t["d_hole"], "d_sess": t["d_sess"], "d_turn": t["d_turn"], "d_hash": t["d_hash"], "ok": ok},
+           {"rows": torch.int32, "first": torch.uint8, "ok": torch.uint8})
+    lens = torch.tensor([len(ch) for ch in chains], dtype=torch.int64).to(dev)
+    cid = torch.repeat_interleave(torch.arange(len(chains), device=dev), lens)
+    chain_ok.scatter_reduce_(0, cid, ok, reduce="amin")
+    return ok, chain_ok
+
+
+def store_roots(store, chains: list[list[int]]) -> torch.Tensor:
+    """K09 over resident rows: the Merkle root of each chain's d_hash leaves (int32
+    [C, 8]; zeros for an empty chain), gathered on the device."""
+    from agent_hypervisor_amd.ops import audit as A
+
+    dev = store.device
+    rows = [d for ch in chains for d in ch]
+    offs = [0]
+    for ch in chains:
+        offs.append(offs[-1] + len(ch))
+    if not rows:
+        return torch.zeros(len(chains), 8, dtype=torch.int32, device=dev)
+    leaves = store.column("d_hash").view(-1, 8).index_select(0, torch.tensor(rows, dtype=torch.int64).to(dev))
+    return A.merkle_roots(torch.tensor(offs, dtype=torch.int32).to(dev), leaves.contiguous())
+
+
+def sigma_batch(store, vsess: list[int], agents: list[int], sigma=None, omega=None, mode: int = 0,
+                now: int | None = None) -> torch.Tensor:
+    """K03 (mode 0: σ_eff of vouchee ``agents[i]`` with (σ, ω)) or K04 (mode 1:
+    exposure of voucher ``agents[i]``) for many requests over the store's resident
+    vouch lists — one lane per request, each sum in creation order, so every value
+    is bit-identical to the scalar command.  fp64 [n] on the store device."""
+    from agent_hypervisor_amd.ops._launch import launch
+
+    dev = store.device
+    n = len(vsess)
+    out = torch.zeros(n, dtype=torch.float64, device=dev)
+    if not n:
+        return out
+    store.drain()
+    if dev.type == "cuda":
+        store.flush()
+    t = store.tables
+    f64 = torch.float64
+    sig = torch.as_tensor(sigma if sigma is not None else [0.0] * n, dtype=f64).to(dev)
+    om = torch.as_tensor(omega if omega is not None else [0.0] * n, dtype=f64).to(dev)
+    launch("store_sigma",
+           {"n": n, "mode": int(mode), "now_us": int(now if now is not None else now_us()),
+            "cap_v": int(store.caps["V"])},
+           {"vsess": torch.tensor(vsess, dtype=torch.int32).to(dev), "agent": torch.tensor(agents, dtype=torch.int32).to(dev),
+            "sigma": sig, "omega": om, "v_head": t["v_head"], "e_next": t["e_next"], "e_voucher": t["e_voucher"],
+            "e_vouchee": t["e_vouchee"], "e_active": t["e_active"], "e_expiry": t["e_expiry"],
+            "e_bonded": t["e_bonded"], "out": out},
+           {"sigma": f64, "omega": f64, "out": f64})
+    return out

@@ -595,8 +595,10 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
             if p["parent_hash"] != (prev_view.device_hash() if prev_view is not None else None):
                 view.parent_hash = p["parent_hash"]  # keep what the record says; verify will flag it
             words = [int(rec["delta_hash"][8 * k: 8 * k + 8], 16) for k in range(8)]
+            hole = payload.find(b'"parent_hash": "')
+            hole = hole + len(b'"parent_hash": ') if hole >= 0 and p["parent_hash"] is not None else -1
             for col, v in (("d_sess", s), ("d_turn", int(p["turn_id"])), ("d_prev", prev_idx), ("d_ts", to_us(ts)),
-                           ("d_off", off), ("d_len", len(payload))):
+                           ("d_off", off), ("d_len", len(payload)), ("d_hole", hole)):
                 put(col, didx, v)
             for k, w in enumerate(words):
                 put("d_hash", 8 * didx + k, w)

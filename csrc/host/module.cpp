@@ -17,6 +17,7 @@ void register_comm(py::module_& m);
 void register_store(py::module_& m);
 void register_global_liability(py::module_& m);
 void register_merkle_tree(py::module_& m);
+void register_store_views(py::module_& m);
 }  // namespace host
 }  // namespace ahv
 
@@ -30,4 +31,5 @@ PYBIND11_MODULE(_C, m) {
   ahv::host::register_store(m);
   ahv::host::register_global_liability(m);
   ahv::host::register_merkle_tree(m);
+  ahv::host::register_store_views(m);
 }

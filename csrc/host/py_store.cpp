@@ -609,6 +609,7 @@ class Store {
   int64_t delta_live() const { return dhw_ - static_cast<int64_t>(dfree_.size()); }
   int64_t payload_cap() const { return t_.cap.B; }
   int64_t bulk_cap() const { return bulk_cap_; }
+  uintptr_t payload_ptr() const { return reinterpret_cast<uintptr_t>(payload_); }
   int64_t staging_cap() const { return staging_cap_; }
   void set_timeout(int s) { timeout_s_ = s; }
   bool gpu() const { return gpu_; }
@@ -675,6 +676,7 @@ void register_store(py::module_& m) {
       .def_property_readonly("delta_live", &Store::delta_live)
       .def_property_readonly("payload_cap", &Store::payload_cap)
       .def_property_readonly("bulk_cap", &Store::bulk_cap)
+      .def_property_readonly("payload_ptr", &Store::payload_ptr)
       .def_property_readonly("staging_cap", &Store::staging_cap)
       .def_property_readonly("gpu", &Store::gpu);
   py::dict ops;

@@ -150,6 +150,7 @@ enum RowKind : uint64_t { RK_S = 0, RK_G = 1, RK_T = 2, RK_E = 3, RK_D = 4, RK_V
   X(d_ts, int64_t, D)              \
   X(d_off, int64_t, D)             \
   X(d_len, int32_t, D)             \
+  X(d_hole, int32_t, D)            \
   X(d_hash, uint32_t, D8)          \
   X(e_voucher, int32_t, E)         \
   X(e_vouchee, int32_t, E)         \
@@ -1380,6 +1381,7 @@ AHV_HD void exec_free_rows(const Lanes& L, const Tables& t, const Cmd& c, uint64
         t.d_sess[x] = -1;
         t.d_turn[x] = 0;
         t.d_prev[x] = -1;
+        t.d_hole[x] = -1;
         break;
       case RK_V:
         if (x < 0 || x >= t.cap.V) { bad = 1; break; }
@@ -1618,6 +1620,7 @@ AHV_HD bool capture_begin(const Lanes& L, const Tables& t, const Cmd& c, uint64_
   t.d_ts[d] = static_cast<int64_t>(c.a[3]);
   t.d_off[d] = static_cast<int64_t>(c.a[4]);
   t.d_len[d] = static_cast<int32_t>(c.a[5]);
+  t.d_hole[d] = static_cast<int32_t>(hole);  // offset of the quoted parent digest (-1: null parent)
   t.s_dlast[s] = static_cast<int32_t>(d);
   t.s_dcount[s] = turn;
   j.seq = seq;

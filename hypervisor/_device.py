@@ -698,6 +698,27 @@ class DeviceVouchingEngine(VouchingEngine):
         )
         return bitsd(r[1])
 
+    def compute_sigma_eff_batch(self, requests: list) -> list[float]:
+        """σ_eff for many ``(vouchee_did, session_id, vouchee_sigma, risk_weight)``
+        at once: one device launch over the resident vouch lists (K03), each value
+        bit-identical to :meth:`compute_sigma_eff`."""
+        from agent_hypervisor_amd.ops.store_views import sigma_batch
+
+        st = self._store
+        vs = [self._v(s) for _, s, _, _ in requests]
+        ag = [st.agents.lookup(d) for d, _, _, _ in requests]
+        out = sigma_batch(st, vs, ag, [float(x) for _, _, x, _ in requests], [float(w) for *_, w in requests], 0)
+        return [float(x) for x in out.cpu().tolist()]
+
+    def get_total_exposure_batch(self, requests: list) -> list[float]:
+        """Exposure for many ``(voucher_did, session_id)`` at once (K04 over the
+        resident vouch lists; bit-identical to :meth:`get_total_exposure`)."""
+        from agent_hypervisor_amd.ops.store_views import sigma_batch
+
+        st = self._store
+        out = sigma_batch(st, [self._v(s) for _, s in requests], [st.agents.lookup(d) for d, _ in requests], mode=1)
+        return [float(x) for x in out.cpu().tolist()]
+
     def _list(self, session_id: str, flt: int, who: Optional[str]) -> list[DeviceVouchRecord]:
         """Edges of a session's device list matching ``flt`` (live by vouchee / by
         voucher / all live), in creation order; paged through the bulk buffer."""

@@ -19,6 +19,14 @@ K11    SHA-256 of every VFS file's current content vs the content hash of
 K12    every semantic checkpoint's goal hash vs sha256(goal:step)[:16]
 =====  ==================================================================
 
+Sessions whose audit chain lives in a device store (``store=``) are verified
+where their rows live: K10 re-hashes the canonical-JSON records in the store's
+payload arena and checks each row's digest and parent link, K09 recomputes the
+roots from the resident digests — no record is re-rendered on the host or
+copied to the device (:mod:`agent_hypervisor_amd.ops.store_views`).  Other
+sessions (host engines, or ``source="views"``) are re-rendered from their
+delta views, which also catches edits made to those Python objects.
+
 Nothing is mutated (the reference's self-"repairing" verify, Q02, is not
 reproduced here even in parity mode: this is an auditor).
 """
@@ -98,6 +106,7 @@ def verify_audit(
     commitments: Optional[dict] = None,
     device: Optional[str] = None,
     checkpoints: Iterable = (),
+    store=None,
 ) -> AuditReport:
     """Verify the audit state of ``sessions`` (``ManagedSession`` objects).
 
@@ -115,10 +124,15 @@ def verify_audit(
     payloads, stored, parent, has_parent, chain_offs, chain_sid = [], [], [], [], [0], []
     root_rows, root_expect, root_sid = [], [], []
     files, file_expect, file_key = [], [], []
+    resident = []  # device-store sessions: verified where their rows live
     for m in sessions:
         sid = m.sso.session_id
         de = m.delta_engine
         ds = de.deltas
+        if store is not None and getattr(de, "_store", None) is store:
+            if ds:
+                resident.append((sid, [d._didx for d in ds], len(ds) == de.turn_count))
+            ds = ()
         if ds:
             first = len(payloads)
             for d in ds:
@@ -154,6 +168,20 @@ def verify_audit(
     dev = _pick_device(device, len(payloads) + len(files) + len(goals))
     rep = AuditReport(device=str(dev), sessions=len(sessions), deltas=len(payloads),
                       roots_checked=len(root_sid), files=len(files), checkpoints=len(goals))
+    if resident:  # K10 + K09 over the store's rows and arena records (nothing re-rendered or uploaded)
+        from agent_hypervisor_amd.ops.store_views import store_roots, verify_store_chains
+
+        _, cok = verify_store_chains(store, [rows for _, rows, _ in resident])
+        rep.bad_chains.extend(resident[i][0] for i in torch.nonzero(cok == 0).flatten().tolist())
+        rep.deltas += sum(len(rows) for _, rows, _ in resident)
+        rc = [(sid, rows) for sid, rows, complete in resident if complete and commitments.get(sid) is not None]
+        if rc:
+            roots = store_roots(store, [rows for _, rows in rc])
+            want = A.hex_to_digests([_hex64(commitments[sid]) for sid, _ in rc], store.device)
+            bad = (roots != want).any(dim=1)
+            rep.bad_roots.extend(rc[i][0] for i in torch.nonzero(bad).flatten().tolist())
+            rep.roots_checked += len(rc)
+        rep.device = str(store.device) if not payloads else rep.device
     # -- K10: payload digests + parent links, every chain in one launch -----------
     if payloads:
         data, offs = A.pack_bytes(payloads, dev)

@@ -376,19 +376,25 @@ class Hypervisor:
         return None, None
 
     def verify_audit(self, session_ids: Optional[list[str]] = None, device: Optional[str] = None,
-                     checkpoints=()):
+                     checkpoints=(), source: str = "store"):
         """Batched audit of many sessions at once: every delta chain (K10), every
         committed Merkle root (K09), every VFS file against its edit log (K11) and
         the goal hashes of the given ``CheckpointManager`` s (K12) — see
         :mod:`hypervisor.audit.batch_verify`.  ``device`` defaults to the GPU for
-        large batches (and to the store's device for a device-backed hypervisor)."""
+        large batches (and to the store's device for a device-backed hypervisor).
+
+        ``source``: ``"store"`` (default) verifies a device-backed session's audit
+        where it lives — the records in the store's payload arena and the resident
+        digests, nothing re-rendered or uploaded; ``"views"`` re-renders the
+        Python delta views instead (which also flags edits made to those objects)."""
         from hypervisor.audit.batch_verify import verify_audit
 
         sessions = self.sessions if session_ids is None else [self._get_session(s) for s in session_ids]
         roots = {c.session_id: c.merkle_root for c in self.commitment.all_commitments()}
         if device is None and self._store is not None and self._store.device.type == "cuda":
             device = str(self._store.device)
-        return verify_audit(sessions, roots, device=device, checkpoints=checkpoints)
+        store = self._store if source == "store" else None
+        return verify_audit(sessions, roots, device=device, checkpoints=checkpoints, store=store)
 
     @property
     def active_sessions(self) -> list[ManagedSession]:
