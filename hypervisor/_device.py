@@ -358,8 +358,19 @@ class DeviceDelta(SemanticDelta):
         self.__dict__.update(
             delta_id=delta_id, turn_id=turn_id, session_id=session_id, agent_did=agent_did, timestamp=timestamp,
             changes=changes, _engine=engine, _prev=prev, _dev_hash=None, _hash_override=None,
-            _parent_override=None, _didx=-1, _poff=-1, _plen=0, _seq=-1,
+            _parent_override=None, _didx=-1, _poff=-1, _plen=0, _seq=-1, _dirty=False,
         )
+
+    _FIELDS = frozenset(("delta_id", "turn_id", "session_id", "agent_did", "timestamp", "changes"))
+
+    def __setattr__(self, k, v) -> None:
+        # an edit of a hashed field after capture: the view no longer shows what
+        # the device holds, so audits of this chain re-render the views
+        if k in DeviceDelta._FIELDS:
+            self.__dict__[k] = v
+            self.__dict__["_dirty"] = True
+        else:
+            object.__setattr__(self, k, v)
 
     def device_hash(self) -> str:
         """The digest the device computed for this delta (K08)."""
@@ -376,6 +387,7 @@ class DeviceDelta(SemanticDelta):
     @delta_hash.setter
     def delta_hash(self, v: str) -> None:
         self.__dict__["_hash_override"] = v
+        self.__dict__["_dirty"] = True
 
     @property
     def parent_hash(self) -> Optional[str]:  # type: ignore[override]
@@ -388,6 +400,7 @@ class DeviceDelta(SemanticDelta):
     @parent_hash.setter
     def parent_hash(self, v: Optional[str]) -> None:
         self.__dict__["_parent_override"] = _NULL if v is None else v
+        self.__dict__["_dirty"] = True
 
     def compute_hash(self) -> str:
         self.delta_hash = _host_digest(self)

@@ -19,8 +19,8 @@ K11    SHA-256 of every VFS file's current content vs the content hash of
 K12    every semantic checkpoint's goal hash vs sha256(goal:step)[:16]
 =====  ==================================================================
 
-Sessions whose audit chain lives in a device store (``store=``) are verified
-where their rows live: K10 re-hashes the canonical-JSON records in the store's
+Sessions whose audit chain lives in a device store (``store=``) — and whose
+delta views were not edited after capture — are verified where their rows live: K10 re-hashes the canonical-JSON records in the store's
 payload arena and checks each row's digest and parent link, K09 recomputes the
 roots from the resident digests — no record is re-rendered on the host or
 copied to the device (:mod:`agent_hypervisor_amd.ops.store_views`).  Other
@@ -129,7 +129,8 @@ def verify_audit(
         sid = m.sso.session_id
         de = m.delta_engine
         ds = de.deltas
-        if store is not None and getattr(de, "_store", None) is store:
+        if store is not None and getattr(de, "_store", None) is store and not any(
+                d.__dict__.get("_dirty") for d in ds):  # views edited after capture: re-render them below
             if ds:
                 resident.append((sid, [d._didx for d in ds], len(ds) == de.turn_count))
             ds = ()
