@@ -175,6 +175,7 @@ class GovernanceStore:
         self._lock = threading.RLock()
         self._closed = False
         self.agents = Interner()  # DID → dense agent id
+        self.pool = Interner()  # strings the batched pipeline renders (DIDs, change fields)
         self._rows = {k: _Rows(c[k]) for k in ("S", "G", "T", "E", "V")}
         self._pending: dict[str, list] = {k: [] for k in ("S", "G", "T", "E", "V", "D")}
         self._tenant_v: dict[int, dict[str, int]] = {}  # tenant → liability session id → V row
@@ -211,6 +212,42 @@ class GovernanceStore:
             return True
         gc.collect()
         return bool(self._pending[kind]) and self.reclaim(kind) > 0
+
+    def alloc_many(self, kind: str, n: int) -> list:
+        """``n`` free rows of table ``kind`` (reclaimed rows first, then fresh ones;
+        the table grows as needed)."""
+        rows = self._rows[kind]
+        out: list = []
+        if len(self._pending[kind]) >= self.RECLAIM_BATCH:
+            self.reclaim(kind)
+        while len(out) < n:
+            need = n - len(out)
+            if rows.free:
+                k = min(need, len(rows.free))
+                out.extend(rows.free[-k:])
+                del rows.free[-k:]
+                continue
+            room = rows.cap - rows.hw
+            if room > 0:
+                k = min(need, room)
+                out.extend(range(rows.hw, rows.hw + k))
+                rows.hw += k
+                continue
+            if not self._room(kind):
+                self._grow(kind)
+        return out
+
+    def reserve_deltas(self, caps: list) -> tuple:
+        """Delta rows + arena reservations of ``caps`` bytes each (batched pipeline):
+        ``(rows int32 bytes, offsets int64 bytes)``."""
+        raw = struct.pack(f"<{len(caps)}i", *caps)
+        tries = 0
+        while True:
+            r = self._c.reserve_deltas(raw)
+            if r[1] is not None:
+                return r
+            self._make_room(r[0], tries)
+            tries += 1
 
     def release(self, kind: str, row: int) -> None:
         """Queue a row whose last API reference is gone (safe to call from ``__del__``)."""
@@ -522,7 +559,7 @@ class GovernanceStore:
         out = {}
         for name, idx in cols.items():
             t = self.tables[name]
-            ix = torch.as_tensor(list(idx), dtype=torch.int64).to(self.device, non_blocking=True)
+            ix = torch.from_numpy(np.asarray(idx, dtype=np.int64)).to(self.device)
             out[name] = t.index_select(0, ix).cpu().numpy()
         return out
 

@@ -1,0 +1,388 @@
+"""Batched, heterogeneous governance pipelines written straight into the store.
+
+:meth:`hypervisor.Hypervisor.run_pipelines` runs the reference pipeline
+(``benchmarks/bench_hypervisor.py:217-239``) for many sessions in three gfx950
+launches over the *store's* tables (``csrc/hip/store_pipeline.hip``) plus the K09
+root kernel — and the sessions it creates are ordinary device sessions of the
+public API: ``hv.get_session(sid)`` returns a ``ManagedSession`` whose views read
+the same rows, ``verify_audit`` / ``terminate_session`` / snapshots work on them,
+and their rows are reclaimed like any other once unreferenced.
+
+Heterogeneity (:class:`PipelineSpec`, one per session or one shared): any number
+of joins with per-agent σ (ring gate + admission in order — reference
+``core.py:106-185``), per-delta agents and change lists, saga steps with
+pre-resolved outcomes — ``failures`` attempts fail before one succeeds; with more
+failures than ``1 + max_retries`` attempts the step fails and the saga stops —
+and reverse-order compensation (``saga/orchestrator.py:77-198``).  Executors are
+not run: the outcomes are inputs (a batch replays decided work at device speed).
+
+Sessions are registered lazily: the hypervisor holds a small placeholder per
+session and builds the Python views only when one is first used, so a batch of
+10⁵ sessions costs a few µs of host work per session, not a view graph each.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from agent_hypervisor_amd._native import C
+
+REFERENCE_JOINS = (("did:mesh:a", 0.8),)
+REFERENCE_DELTAS = tuple(("did:mesh:a", ((f"/f{i}", "add", f"h{i}"),)) for i in range(3))
+REFERENCE_STEPS = (("action", "did:mesh:a", "/api/action", None, 0, 0),)
+
+_STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
+           5: "terminate_refused", 6: "record_overflow"}
+
+
+@dataclass(frozen=True)
+class PipelineSpec:
+    """One session's pipeline.
+
+    ``joins``: ``(agent_did, sigma_raw)`` in order.  ``deltas``: ``(agent_did,
+    changes)`` with changes ``(path, operation, content_hash[, previous_hash])``.
+    ``steps``: ``(action_id, agent_did, execute_api, undo_api, max_retries,
+    failures)``.  ``config``: a :class:`hypervisor.SessionConfig` (default one)."""
+
+    joins: Sequence[tuple] = REFERENCE_JOINS
+    deltas: Sequence[tuple] = REFERENCE_DELTAS
+    steps: Sequence[tuple] = REFERENCE_STEPS
+    activate: bool = True
+    terminate: bool = True
+    compensate: bool = True
+    config: Optional[object] = None
+    creator_did: str = "did:mesh:admin"
+
+
+@dataclass
+class PipelineRun:
+    """What one :meth:`Hypervisor.run_pipelines` call produced."""
+
+    session_ids: list
+    status: np.ndarray        # per session, 0 = every stage admitted (see status_name)
+    join_rings: np.ndarray    # per join, in spec order
+    join_codes: np.ndarray
+    roots: dict = field(default_factory=dict)  # session id → committed Merkle root (hex)
+    device_seconds: float = 0.0
+
+    def status_name(self, i: int) -> str:
+        return _STATUS.get(int(self.status[i]), str(int(self.status[i])))
+
+    @property
+    def ok(self) -> int:
+        return int((self.status == 0).sum())
+
+
+class _Batch:
+    """Host metadata of one batch: what a lazy session needs to build its views."""
+
+    __slots__ = ("store", "specs", "shared", "ids", "slots", "t0", "doff", "drows", "dlen", "dhash",
+                 "delta_off", "gslots", "step_off", "tslots", "__weakref__")
+
+
+def _spec(b: _Batch, i: int) -> PipelineSpec:
+    return b.specs if b.shared else b.specs[i]
+
+
+def _escaped_len(pool, cache: dict, s: Optional[str]) -> int:
+    if s is None:
+        return 4
+    n = cache.get(s)
+    if n is None:
+        n = cache[s] = len(pool.escaped(pool.intern(s))) + 2
+    return n
+
+
+_FIXED = 14 + 14 + 16 + 7 + 1 + 17 + 16 + 46 + 15 + 34 + 13 + 1  # literals, session id, timestamp
+
+
+def _delta_cap(pool, cache, did: str, changes, turn: int) -> int:
+    n = _FIXED + 2 * len(str(turn)) + (66 if turn > 1 else 4) + _escaped_len(pool, cache, did)
+    for k, c in enumerate(changes):
+        n += 17 + 15 + 10 + 19 + 1 + (2 if k else 0)
+        n += _escaped_len(pool, cache, c[2]) + _escaped_len(pool, cache, c[1]) + _escaped_len(pool, cache, c[0])
+        n += _escaped_len(pool, cache, c[3] if len(c) > 3 else None)
+    return (n + 8 + 63) & ~63
+
+
+def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
+    """Build the batch arrays, run the store pipeline, register lazy sessions."""
+    import time
+
+    from hypervisor._clock import now_us
+    from hypervisor.models import ConsistencyMode, SessionConfig
+
+    st = hv._store
+    if st is None:
+        raise RuntimeError("run_pipelines needs a device-backed Hypervisor (device='cuda' or 'cpu')")
+    shared = isinstance(specs, PipelineSpec)
+    if shared:
+        if n is None:
+            raise ValueError("run_pipelines(spec) needs n")
+    else:
+        specs = list(specs)
+        n = len(specs)
+    dev = st.device
+    pool = st.pool
+    cache: dict = {}
+    ids, words = C.uuid4_many(n, "session:")
+    slots = np.asarray(st.alloc_many("S", n), dtype=np.int32)
+    t0 = now_us()
+
+    def per_session(fn, dtype):
+        if shared:
+            return np.full(n, fn(specs), dtype=dtype)
+        return np.asarray([fn(s) for s in specs], dtype=dtype)
+
+    def cfg(s):
+        return s.config or SessionConfig()
+
+    creator = per_session(lambda s: st.agent_id(s.creator_did), np.int32)
+    maxpart = per_session(lambda s: int(cfg(s).max_participants), np.int32)
+    minsig = per_session(lambda s: float(cfg(s).min_sigma_eff), np.float64)
+    flags = per_session(lambda s: (1 if cfg(s).enable_audit else 0)
+                        | (2 if ConsistencyMode(cfg(s).consistency_mode) is ConsistencyMode.STRONG else 0)
+                        | (4 if s.activate else 0) | (8 if s.terminate else 0) | (16 if s.compensate else 0), np.uint8)
+
+    def table(get_rows, width_fn):
+        """Concatenate per-session row lists: (offsets [n+1], rows)."""
+        if shared:
+            rows = list(get_rows(specs))
+            k = len(rows)
+            return np.arange(0, (n + 1) * k, k, dtype=np.int32), rows, k
+        off, out = [0], []
+        for s in specs:
+            r = list(get_rows(s))
+            out.extend(r)
+            off.append(len(out))
+        return np.asarray(off, dtype=np.int32), out, None
+
+    join_off, joins, jk = table(lambda s: s.joins, None)
+    j_agent = np.asarray([st.agent_id(d) for d, _ in joins], dtype=np.int32)
+    j_sigma = np.asarray([float(x) for _, x in joins], dtype=np.float64)
+    if shared:
+        j_agent, j_sigma = np.tile(j_agent, n), np.tile(j_sigma, n)
+
+    delta_off, deltas, dk = table(lambda s: s.deltas, None)
+    d_pool = [pool.intern(did) for did, _ in deltas]
+    ch_off, ch_rows = [0], []
+    caps = []
+    for k, (did, chs) in enumerate(deltas):
+        for c in chs:
+            ch_rows.append([pool.intern(c[0]), pool.intern(c[1]),
+                            pool.intern(c[2]) if c[2] is not None else -1,
+                            pool.intern(c[3]) if len(c) > 3 and c[3] is not None else -1])
+        ch_off.append(len(ch_rows))
+    if shared:
+        per = len(deltas)
+        caps = [_delta_cap(pool, cache, did, chs, t + 1) for t, (did, chs) in enumerate(deltas)] * n
+        nch = [ch_off[k + 1] - ch_off[k] for k in range(per)]
+        d_pool = d_pool * n
+        base = np.asarray(ch_off[:-1], dtype=np.int32)
+        per_ch = ch_off[-1]
+        ch_off_all = (np.tile(base, n) + np.repeat(np.arange(n, dtype=np.int32) * per_ch, per)).tolist() + [per_ch * n]
+        ch_rows = np.tile(np.asarray(ch_rows or [[0, 0, 0, 0]], dtype=np.int32), (n, 1)) if ch_rows else []
+        del nch
+    else:
+        turn_of = []
+        for i in range(n):
+            turn_of.extend(range(1, delta_off[i + 1] - delta_off[i] + 1))
+        caps = [_delta_cap(pool, cache, did, chs, t) for (did, chs), t in zip(deltas, turn_of)]
+        ch_off_all = ch_off
+    nd = len(caps)
+    drows, doff = st.reserve_deltas(caps)
+    dsess = np.repeat(np.arange(n, dtype=np.int32), np.diff(delta_off))
+
+    step_off, steps, sk = table(lambda s: s.steps, None)
+    has_saga = np.diff(step_off) > 0
+    gslots = np.full(n, -1, dtype=np.int32)
+    ng = int(has_saga.sum())
+    if ng:
+        gslots[has_saga] = st.alloc_many("G", ng)
+    nsteps = int(step_off[-1])
+    tslots = np.asarray(st.alloc_many("T", nsteps), dtype=np.int32) if nsteps else np.zeros(0, dtype=np.int32)
+    if shared:
+        s_undo = np.tile(np.asarray([1 if x[3] else 0 for x in steps], dtype=np.uint8), n)
+        s_retry = np.tile(np.asarray([int(x[4]) for x in steps], dtype=np.int32), n)
+        s_fail = np.tile(np.asarray([min(255, int(x[5])) for x in steps], dtype=np.uint8), n)
+    else:
+        s_undo = np.asarray([1 if x[3] else 0 for x in steps], dtype=np.uint8)
+        s_retry = np.asarray([int(x[4]) for x in steps], dtype=np.int32)
+        s_fail = np.asarray([min(255, int(x[5])) for x in steps], dtype=np.uint8)
+
+    def T(a, dtype=None):
+        arr = np.array(a if dtype is None else np.asarray(a, dtype=dtype), copy=True, order="C")
+        return torch.from_numpy(arr).to(dev)
+
+    pb, po, pl = pool.device_view(dev)
+    tens = {
+        "slot": T(slots), "uuid": T(np.frombuffer(words, dtype=np.int32).reshape(n, 4)),
+        "t0": T(np.full(n, t0, dtype=np.int64)), "creator": T(creator), "maxpart": T(maxpart), "minsig": T(minsig),
+        "flags": T(flags), "join_off": T(join_off), "join_agent": T(j_agent), "join_sigma": T(j_sigma),
+        "join_ring": torch.zeros(max(1, len(j_agent)), dtype=torch.uint8, device=dev),
+        "join_code": torch.zeros(max(1, len(j_agent)), dtype=torch.uint8, device=dev),
+        "delta_off": T(delta_off), "drow": T(np.frombuffer(drows, dtype=np.int32)), "dagent_pool": T(d_pool, np.int32),
+        "dch_off": T(ch_off_all, np.int32),
+        "changes": T(ch_rows if len(ch_rows) else np.zeros((1, 4), np.int32), np.int32),
+        "doff": T(np.frombuffer(doff, dtype=np.int64)), "dcap": T(caps, np.int32), "dsess": T(dsess),
+        "gslot": T(gslots), "step_off": T(step_off), "tslot": T(tslots if nsteps else np.zeros(1, np.int32)),
+        "step_undo": T(s_undo if nsteps else np.zeros(1, np.uint8)),
+        "step_retries": T(s_retry if nsteps else np.zeros(1, np.int32)),
+        "step_fail": T(s_fail if nsteps else np.zeros(1, np.uint8)),
+        "status": torch.zeros(n, dtype=torch.int32, device=dev),
+        "pool_bytes": pb, "pool_off": po, "pool_len": pl,
+    }
+    args = {k: v.data_ptr() for k, v in tens.items()}
+    args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
+    cuda = dev.type == "cuda"
+    t_dev = time.perf_counter()
+    if cuda:
+        st.drain()
+        st.flush()  # the worker's row writes (frees) are visible to the batch kernels
+        stream = torch.cuda.current_stream(dev)
+        st._c.run_pipeline(args, stream.cuda_stream)
+    else:
+        st._c.run_pipeline(args, 0)
+    # K09: roots of the committed chains over the digests just written → s_root
+    status = tens["status"]
+    roots = {}
+    committed = [i for i in range(n) if (int(flags[i]) & 9) == 9 and delta_off[i + 1] > delta_off[i]] \
+        if not shared else (list(range(n)) if (int(flags[0]) & 9) == 9 and delta_off[1] > 0 else [])
+    drow_np = np.frombuffer(drows, dtype=np.int32)
+    if committed:
+        from agent_hypervisor_amd.ops import audit as A
+
+        cix = torch.as_tensor(committed, dtype=torch.int64).to(dev)
+        if shared:
+            k = int(delta_off[1])
+            leaves_idx = tens["drow"].view(n, k).index_select(0, cix).reshape(-1).to(torch.int64)
+            offs = torch.arange(0, (len(committed) + 1) * k, k, dtype=torch.int32, device=dev)
+        else:
+            lens = [int(delta_off[i + 1] - delta_off[i]) for i in committed]
+            leaves_idx = torch.as_tensor(np.concatenate([drow_np[delta_off[i]:delta_off[i + 1]] for i in committed]),
+                                         dtype=torch.int64).to(dev)
+            offs = torch.as_tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32).to(dev)
+        hashes = st.tables["d_hash"].view(-1, 8)
+        r = A.merkle_roots(offs, hashes.index_select(0, leaves_idx).contiguous())
+        sl = tens["slot"].index_select(0, cix).to(torch.int64)
+        ok = st.tables["s_committed"].index_select(0, sl) != 0  # terminated with audit: committed
+        st.tables["s_root"].view(-1, 8)[sl] = torch.where(ok[:, None], r, torch.zeros_like(r))
+    if cuda:
+        torch.cuda.synchronize(dev)
+        st.acquire()  # the worker sees the batch's rows
+    dev_s = time.perf_counter() - t_dev
+    # results the lazy views need, in one copy each
+    status_np = status.cpu().numpy()
+    dlen = tens["dcap"]  # replaced below by the rendered lengths
+    hidx = (drow_np.astype(np.int64)[:, None] * 8 + np.arange(8, dtype=np.int64)[None, :]).reshape(-1)
+    gath = st.gather({"d_len": drow_np, "d_hash": hidx}) \
+        if nd else {"d_len": np.zeros(0, np.int32), "d_hash": np.zeros(0, np.int32)}
+    dlen = gath["d_len"].astype(np.int64)
+    dhash = gath["d_hash"].astype(np.uint32).reshape(-1, 8) if nd else np.zeros((0, 8), np.uint32)
+    committed_ids: set = set()
+    if committed:
+        cs = slots[np.asarray(committed, dtype=np.int64)].astype(np.int64)
+        gg = st.gather({"s_root": (cs[:, None] * 8 + np.arange(8, dtype=np.int64)[None, :]).reshape(-1),
+                        "s_committed": cs})
+        rr = gg["s_root"].astype(np.uint32).reshape(-1, 8)
+        hexes = [bytes(x).hex() for x in rr.byteswap()] if len(rr) else []  # 8 BE words → 64 hex digits
+        for j, i in enumerate(committed):
+            if gg["s_committed"][j] != 0:
+                roots[ids[i]] = hexes[j]
+                committed_ids.add(ids[i])
+    b = _Batch()
+    b.store, b.specs, b.shared, b.ids, b.slots, b.t0 = st, specs, shared, ids, slots, t0
+    b.doff, b.drows, b.dlen, b.dhash = np.frombuffer(doff, dtype=np.int64), drow_np, dlen, dhash
+    b.delta_off, b.gslots, b.step_off, b.tslots = delta_off, gslots, step_off, tslots
+    register_lazy(hv, b, status_np, committed_ids)
+    run_ = PipelineRun(session_ids=ids, status=status_np,
+                       join_rings=tens["join_ring"].cpu().numpy()[: len(j_agent)],
+                       join_codes=tens["join_code"].cpu().numpy()[: len(j_agent)], roots=roots, device_seconds=dev_s)
+    return run_
+
+
+# ------------------------------------------------------------------ lazy sessions
+
+
+class _RowRef:
+    """The identity of a lazy session's row (what batched reads need)."""
+
+    __slots__ = ("slot", "session_id", "creator_did")
+
+    def __init__(self, slot: int, session_id: str, creator_did: str) -> None:
+        self.slot, self.session_id, self.creator_did = slot, session_id, creator_did
+
+
+def register_lazy(hv, b: _Batch, status: np.ndarray, committed: set) -> None:
+    from hypervisor.core import LazyManagedSession
+
+    sessions = hv._sessions
+    reg = hv.commitment
+    for i, sid in enumerate(b.ids):
+        if status[i] == 1:  # row refused: nothing was written, the row stays with its owner
+            continue
+        m = LazyManagedSession(b, i)
+        sessions[sid] = m
+        if sid in committed:
+            reg.register(m)  # resolved to its row when a commitment view asks
+
+
+def materialize(m) -> None:
+    """Build the device views of lazy session ``m`` (they take over its rows)."""
+    from hypervisor import _device
+    from hypervisor._clock import from_us
+    from hypervisor.audit.delta import VFSChange
+    from hypervisor.models import SessionConfig
+
+    b, i = m._batch, m._index
+    st = b.store
+    sp = _spec(b, i)
+    sid = b.ids[i]
+    slot = int(b.slots[i])
+    sso = _device.DeviceSession(st, sp.config or SessionConfig(), sp.creator_did, session_id=sid, slot=slot,
+                                create=False)
+    de = _device.DeviceDeltaEngine(st, slot, sid, sso)
+    d0, d1 = int(b.delta_off[i]), int(b.delta_off[i + 1])
+    prev = None
+    specs_d = sp.deltas
+    for k in range(d1 - d0):
+        did, chs = specs_d[k]
+        g = d0 + k
+        ts = from_us(int(b.t0) + 1 + k)
+        changes = [VFSChange(path=c[0], operation=c[1], content_hash=c[2],
+                             previous_hash=c[3] if len(c) > 3 else None) for c in chs]
+        d = _device.DeviceDelta(de, f"delta:{k + 1}", k + 1, sid, did, ts, changes, prev)
+        h = "".join(f"{int(w):08x}" for w in b.dhash[g])
+        d.__dict__.update(_didx=int(b.drows[g]), _poff=int(b.doff[g]), _plen=int(b.dlen[g]), _seq=-1, _dev_hash=h)
+        de._deltas.append(d)
+        de._rows.append(int(b.drows[g]))
+        prev = d
+    de._turn_counter = d1 - d0
+    orch = _device.DeviceSagaOrchestrator(st)
+    g = int(b.gslots[i])
+    if g >= 0:
+        saga = _device.DeviceSaga(st, g, C.uuid4("saga:"), sid)
+        for k in range(int(b.step_off[i]), int(b.step_off[i + 1])):
+            a = sp.steps[k - int(b.step_off[i])]
+            step = _device.DeviceSagaStep(st, int(b.tslots[k]), step_id=C.uuid4("step:"), action_id=a[0],
+                                          agent_did=a[1], execute_api=a[2], undo_api=a[3], timeout_seconds=300,
+                                          max_retries=int(a[4]))
+            saga.steps.append(step)
+        orch._sagas[saga.saga_id] = saga
+    return sso, de, orch
+
+
+def release_unmaterialized(b: _Batch, i: int) -> None:
+    """A lazy session that never built its views is gone: its rows go back."""
+    st = b.store
+    st.release("S", int(b.slots[i]))
+    d0, d1 = int(b.delta_off[i]), int(b.delta_off[i + 1])
+    if d1 > d0:
+        st.release_many("D", [int(x) for x in b.drows[d0:d1]])
+    if int(b.gslots[i]) >= 0:
+        st.release("G", int(b.gslots[i]))
+        st.release_many("T", [int(x) for x in b.tslots[int(b.step_off[i]):int(b.step_off[i + 1])]])

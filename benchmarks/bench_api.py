@@ -67,16 +67,63 @@ def api_throughput(device: str, n: int = 10_000, rounds: int = 3, warm: int = 50
             "rounds": [round(r, 1) for r in rates], "roots_ok": roots_ok}
 
 
+def batch_api_throughput(device: str, n: int = 100_000, rounds: int = 3, hetero: bool = False,
+                         seed: int = 5) -> dict:
+    """Sessions/s of :meth:`Hypervisor.run_pipelines` — the public batched API over
+    the device store: every session is a complete pipeline written into store rows
+    (create → join → activate → 3 audit deltas → saga step → terminate with its
+    Merkle root committed) and an ordinary session of the hypervisor afterwards.
+    ``hetero``: a randomized mix (1–5 joins with per-agent σ, 0–4 deltas of 0–3
+    changes, 0–3 steps with retries/failures/compensation) instead of the template."""
+    import random
+
+    from agent_hypervisor_amd.models.store_pipeline import PipelineSpec
+    from hypervisor import Hypervisor
+
+    if hetero:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_store_pipeline import random_spec
+
+        rng = random.Random(seed)
+        specs = [random_spec(rng) for _ in range(n)]
+    else:
+        specs = PipelineSpec()
+
+    async def one():
+        hv = Hypervisor(device=device)
+        return await hv.run_pipelines(specs, None if hetero else n)
+
+    asyncio.run(one())  # warm-up (allocations, kernel load)
+    rates, dev = [], []
+    ok = True
+    for _ in range(rounds):
+        gc.collect()
+        t0 = time.perf_counter()
+        run = asyncio.run(one())
+        dt = time.perf_counter() - t0
+        rates.append(n / dt)
+        dev.append(run.device_seconds)
+        ok = ok and (hetero or (run.ok == n and len(run.roots) == n))
+    return {"device": device, "sessions": n, "hetero": hetero, "sessions_per_s": round(statistics.median(rates), 1),
+            "rounds": [round(r, 1) for r in rates], "device_ms": [round(1000 * x, 2) for x in dev], "ok": ok}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--n", type=int, default=10_000)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--host", action="store_true", help="also run the host engines for comparison")
+    ap.add_argument("--batch", type=int, default=0, help="also time run_pipelines over this many sessions")
     args = ap.parse_args()
-    out = {"device": api_throughput(args.device, args.n, args.rounds)}
-    if args.host:
-        out["host"] = api_throughput("host", args.n, args.rounds)
+    out = {}
+    if args.n:
+        out["device"] = api_throughput(args.device, args.n, args.rounds)
+        if args.host:
+            out["host"] = api_throughput("host", args.n, args.rounds)
+    if args.batch:
+        out["batch"] = batch_api_throughput(args.device, args.batch, args.rounds)
+        out["batch_hetero"] = batch_api_throughput(args.device, args.batch, args.rounds, hetero=True)
     print(json.dumps(out), flush=True)
 
 

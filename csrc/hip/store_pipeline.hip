@@ -1,0 +1,482 @@
+// Batched governance pipeline over the *store's* tables (one device state).
+//
+// `Hypervisor.run_pipelines` runs the reference pipeline (benchmarks/
+// bench_hypervisor.py:217-239) — generalised to heterogeneous sessions: several
+// joins per session with per-agent σ (reference core.py:106-185), per-delta
+// change lists, and saga steps with pre-resolved outcomes, retries and reverse-
+// order compensation (saga/orchestrator.py:77-198) — for thousands of sessions
+// at once, writing ordinary store rows: afterwards every session is a normal
+// device session of the public API (views, reads, verify, terminate all work on
+// it), unlike the standalone engine tables of models/engine.py.
+//
+// Three launches, all over rows the host allocator handed out (free rows; a row
+// that is not free is refused and reported, never overwritten):
+//
+//   store_pipe_rows_kernel    lane per session: create (+ handshake), joins
+//                             through the K01 ring gate and join admission,
+//                             activate, saga/step FSM (K13) with retries and
+//                             compensation (K14), terminate → commit → GC →
+//                             archive bookkeeping, chain links of its delta rows
+//   store_pipe_render_kernel  lane per delta: the canonical-JSON record (the
+//                             shared emitters of ahv/delta_emit.h) written into
+//                             the payload arena, parent digest left as a hole
+//   store_pipe_chain_kernel   lane per session: the serial SHA-256 chain (K08):
+//                             each record's parent hole filled with the previous
+//                             digest, then compressed; digests and chain head
+//
+// The Merkle roots (K09) of the committed chains then come from the K09 kernel
+// over the resident digests (agent_hypervisor_amd/ops/store_pipeline.py).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <algorithm>
+
+#include "ahv/delta_emit.h"
+#include "ahv/launch.h"
+#include "ahv/semantics.h"
+#include "ahv/store.h"
+
+namespace py = pybind11;
+
+namespace ahv {
+namespace {
+
+using store::Tables;
+using store::kFree8;
+
+// Per-batch specification (host-built int32/int64/fp64 arrays on the device).
+struct StorePipeArgs {
+  Tables t;
+  int64_t n;                    // sessions
+  StrPool pool;                 // escaped strings: DIDs, change fields
+  const int32_t* slot;          // [n] session rows
+  const uint32_t* uuid;         // [n, 4] session id words
+  const int64_t* t0;            // [n] base timestamp (µs) of each session
+  const int32_t* creator;       // [n] creator agent id
+  const int32_t* maxpart;       // [n]
+  const double* minsig;         // [n]
+  const uint8_t* flags;         // [n] bit0 audit, bit1 strong mode, bit2 activate, bit3 terminate, bit4 compensate
+  const int32_t* join_off;      // [n+1]
+  const int32_t* join_agent;    // [J] agent ids
+  const double* join_sigma;     // [J] σ_raw (= σ_eff: no Nexus in batches)
+  uint8_t* join_ring;           // [J] out: assigned ring
+  uint8_t* join_code;           // [J] out: JoinCode (0 = admitted)
+  const int32_t* delta_off;     // [n+1]
+  const int32_t* drow;          // [Dn] delta rows
+  const int32_t* dagent_pool;   // [Dn] pool id of the delta's agent DID
+  const int32_t* dch_off;       // [Dn+1] change ranges
+  const ChangeIds* changes;     // [C]
+  const int64_t* doff;          // [Dn] arena offsets (64-aligned)
+  const int32_t* dcap;          // [Dn] bytes reserved at doff
+  const int32_t* gslot;         // [n] saga row (-1: no saga)
+  const int32_t* step_off;      // [n+1]
+  const int32_t* tslot;         // [T] step rows
+  const uint8_t* step_undo;     // [T]
+  const int32_t* step_retries;  // [T] max_retries
+  const uint8_t* step_fail;     // [T] attempts that fail before success (≥ 1 + retries: the step fails)
+  int64_t gc_retention_us;
+  int32_t* status;              // [n] out: 0 ok, else first refused stage (StorePipeStatus)
+};
+
+enum StorePipeStatus : int32_t {
+  SP_OK = 0,
+  SP_ROW_IN_USE = 1,
+  SP_JOIN = 2,        // at least one join refused (its code in join_code)
+  SP_ACTIVATE = 3,
+  SP_STEP_FAILED = 4, // a step failed (after its retries)
+  SP_TERMINATE = 5,
+  SP_RENDER = 6,      // a record did not fit its reservation
+};
+
+// Event times of session i: created/joins/activate at t0, delta k at t0+1+k,
+// step attempt a of step j at t0+D+1+2·(A_j+a) / +1, terminate after the last.
+AHV_HD int64_t sp_delta_ts(const StorePipeArgs& a, int64_t i, int32_t k) { return a.t0[i] + 1 + k; }
+
+AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
+  const Tables& t = a.t;
+  const int64_t s = a.slot[i];
+  if (s < 0 || s >= t.cap.S || t.s_state[s] != kFree8) {
+    a.status[i] = SP_ROW_IN_USE;
+    return;
+  }
+  int32_t status = SP_OK;
+  const int64_t t0 = a.t0[i];
+  const uint8_t fl = a.flags[i];
+  // create + begin_handshake (OP_SESS_CREATE)
+  uint8_t st = SS_HANDSHAKING;
+  t.s_mode[s] = (fl & 2u) ? 1 : 0;
+  t.s_audit[s] = fl & 1u;
+  t.s_maxpart[s] = a.maxpart[i];
+  t.s_minsig[s] = a.minsig[i];
+  t.s_creator[s] = a.creator[i];
+  t.s_created[s] = t0;
+  t.s_terminated[s] = 0;
+  t.s_committed[s] = 0;
+  t.s_commit_n[s] = 0;
+  t.s_released[s] = 0;
+  t.s_retained[s] = 0;
+  t.s_proot_n[s] = 0;
+  for (int k = 0; k < 4; ++k) t.s_uuid[4 * s + k] = a.uuid[4 * i + k];
+  for (int k = 0; k < 8; ++k) {
+    t.s_head[8 * s + k] = 0;
+    t.s_root[8 * s + k] = 0;
+  }
+  // joins, in order: K01 ring gate + admission (OP_SESS_JOIN semantics)
+  int32_t pc = 0, active = 0;
+  const int64_t base = s * t.cap.P;
+  for (int32_t j = a.join_off[i]; j < a.join_off[i + 1]; ++j) {
+    const int32_t agent = a.join_agent[j];
+    const double sg = a.join_sigma[j];
+    const uint8_t ring = ring_from_sigma(sg, false);
+    bool dup = false;
+    for (int32_t k = 0; k < pc; ++k) dup = dup || t.p_agent[base + k] == agent;
+    uint8_t code = join_check(st, dup, active, a.maxpart[i], sg, a.minsig[i], ring);
+    if (code == JOIN_OK && pc >= t.cap.P) code = static_cast<uint8_t>(store::JOIN_ROWS);
+    a.join_ring[j] = ring;
+    a.join_code[j] = code;
+    if (code == JOIN_OK) {
+      const int64_t row = base + pc;
+      t.p_agent[row] = agent;
+      t.p_ring[row] = ring;
+      t.p_active[row] = 1;
+      t.p_sraw[row] = sg;
+      t.p_seff[row] = sg;
+      t.p_joined[row] = t0;
+      ++pc;
+      ++active;
+    } else if (status == SP_OK) {
+      status = SP_JOIN;
+    }
+  }
+  t.s_pcount[s] = pc;
+  t.s_pactive[s] = active;
+  if (fl & 4u) {  // activate: HANDSHAKING with ≥ 1 participant row
+    if (st == SS_HANDSHAKING && pc > 0) st = SS_ACTIVE;
+    else if (status == SP_OK) status = SP_ACTIVATE;
+  }
+  // delta rows: chain links (records and digests come from the render/chain kernels)
+  const int32_t d0 = a.delta_off[i], d1 = a.delta_off[i + 1];
+  const int32_t nd = d1 - d0;
+  t.s_dcount[s] = nd;
+  t.s_dlast[s] = nd > 0 ? a.drow[d1 - 1] : -1;
+  int64_t tnext = t0 + 1 + nd;
+  // saga: steps executed in order with their pre-resolved outcomes (K13), retries
+  // reset to PENDING between attempts as the reference does (orchestrator.py:124/134)
+  const int32_t g = a.gslot[i];
+  if (g >= 0) {
+    t.g_state[g] = SG_RUNNING;
+    t.g_created[g] = t0;
+    t.g_completed[g] = 0;
+    t.g_nsteps[g] = a.step_off[i + 1] - a.step_off[i];
+    bool failed = false;
+    for (int32_t k = a.step_off[i]; k < a.step_off[i + 1]; ++k) {
+      const int32_t ts = a.tslot[k];
+      t.t_saga[ts] = g;
+      t.t_state[ts] = ST_PENDING;
+      t.t_undo[ts] = a.step_undo[k];
+      t.t_maxretry[ts] = a.step_retries[k];
+      t.t_retry[ts] = 0;
+      t.t_started[ts] = 0;
+      t.t_completed[ts] = 0;
+      if (failed) continue;  // the caller stops at the first failed step
+      const int32_t attempts = 1 + a.step_retries[k];
+      for (int32_t at = 0; at < attempts; ++at) {
+        t.t_retry[ts] = at;
+        t.t_state[ts] = ST_EXECUTING;
+        t.t_started[ts] = tnext++;
+        if (at >= a.step_fail[k]) {
+          t.t_state[ts] = ST_COMMITTED;
+          t.t_completed[ts] = tnext++;
+          break;
+        }
+        t.t_state[ts] = ST_FAILED;
+        t.t_completed[ts] = tnext++;
+        if (at < attempts - 1) t.t_state[ts] = ST_PENDING;
+      }
+      if (t.t_state[ts] == ST_FAILED) {
+        failed = true;
+        if (status == SP_OK) status = SP_STEP_FAILED;
+      }
+    }
+    if (failed && (fl & 16u)) {  // compensate: committed steps in reverse (K14)
+      t.g_state[g] = SG_COMPENSATING;
+      int32_t comp_failed = 0;
+      for (int32_t k = a.step_off[i + 1] - 1; k >= a.step_off[i]; --k) {
+        const int32_t ts = a.tslot[k];
+        if (t.t_state[ts] != ST_COMMITTED) continue;
+        if (!a.step_undo[k]) {
+          t.t_state[ts] = ST_COMPENSATION_FAILED;  // "No Undo_API available" (set directly, no stamp)
+          ++comp_failed;
+          continue;
+        }
+        t.t_state[ts] = ST_COMPENSATING;
+        t.t_state[ts] = ST_COMPENSATED;
+        t.t_completed[ts] = tnext++;
+      }
+      t.g_state[g] = comp_failed ? SG_ESCALATED : SG_COMPLETED;
+      t.g_completed[g] = tnext++;
+    }
+  }
+  // terminate → Merkle root (K09, afterwards) → commit → bond release → GC → archive
+  if (fl & 8u) {
+    if ((session_op_allowed_from(OP_TERMINATE) >> st) & 1u) {
+      const int64_t tt = tnext++;
+      t.s_terminated[s] = tt;
+      if ((fl & 1u) && nd > 0) {
+        t.s_committed[s] = tt;
+        t.s_commit_n[s] = nd;
+      }
+      int32_t retained = 0;
+      for (int32_t k = 0; k < nd; ++k) retained += sp_delta_ts(a, i, k) >= tt - a.gc_retention_us ? 1 : 0;
+      t.s_retained[s] = retained;
+      t.s_released[s] = 0;  // batched sessions post no bonds
+      st = SS_ARCHIVED;
+    } else if (status == SP_OK) {
+      status = SP_TERMINATE;
+    }
+  }
+  t.s_state[s] = st;
+  a.status[i] = status;
+}
+
+// Bytes of one record, written straight to the arena a word at a time (records
+// start 64-byte aligned).  Big-endian chunks from the emitters → little-endian
+// memory words.
+struct ArenaSink {
+  uint32_t* dst;
+  uint32_t cap_w;
+  uint32_t nw = 0;   // whole words written
+  uint32_t acc = 0;  // pending bytes in memory order
+  uint32_t nb = 0;   // pending byte count
+  AHV_HD bool seg(uint32_t) { return true; }
+  AHV_HD bool any(bool b) const { return b; }
+  template <class T>
+  AHV_HD void launder(T&) const {}
+  AHV_HD uint32_t pos() const { return 4 * nw + nb; }
+  AHV_HD void byte(uint32_t b) {
+    acc |= (b & 0xffu) << (8 * nb);
+    if (++nb == 4) {
+      if (nw < cap_w) dst[nw] = acc;
+      ++nw;
+      acc = 0;
+      nb = 0;
+    }
+  }
+  AHV_HD void put(uint32_t v, uint32_t n) {
+    for (uint32_t j = 0; j < n; ++j) byte(v >> (24 - 8 * j));
+  }
+  AHV_HD void put4(uint32_t v) {
+    if (nb == 0) {  // aligned: one store
+      if (nw < cap_w) dst[nw] = bswap32(v);
+      ++nw;
+      return;
+    }
+    put(v, 4);
+  }
+  AHV_HD void flush() {
+    if (nb) {
+      if (nw < cap_w) dst[nw] = acc;
+      ++nw;
+      acc = 0;
+      nb = 0;
+    }
+  }
+};
+
+// Lane per delta g (session `i`, turn k+1): render the record; the parent digest
+// is rendered as 66 placeholder bytes whose offset is recorded (d_hole).
+AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
+  const Tables& t = a.t;
+  const int32_t k = g - a.delta_off[i];
+  const int32_t d = a.drow[g];
+  const int64_t s = a.slot[i];
+  ArenaSink snk;
+  snk.dst = reinterpret_cast<uint32_t*>(t.payload + a.doff[g]);
+  snk.cap_w = static_cast<uint32_t>(a.dcap[g]) / 4;
+  const ChangeIds* ch = a.changes + a.dch_off[g];
+  const uint32_t nch = static_cast<uint32_t>(a.dch_off[g + 1] - a.dch_off[g]);
+  const uint32_t turn = static_cast<uint32_t>(k + 1);
+  emit_lit(snk, canon::K_OPEN_AGENT);
+  emit_str_ref(snk, pool_ref(a.pool, a.dagent_pool[g]));
+  emit_lit(snk, canon::K_CHANGES);
+  for (uint32_t c = 0; c < nch; ++c) {
+    if (c) emit_lit(snk, canon::K_CH_SEP);
+    emit_lit(snk, canon::K_CH_OPEN);
+    emit_pool_str(snk, a.pool, ch[c].content_hash);
+    emit_lit(snk, canon::K_CH_OP);
+    emit_pool_str(snk, a.pool, ch[c].op);
+    emit_lit(snk, canon::K_CH_PATH);
+    emit_pool_str(snk, a.pool, ch[c].path);
+    emit_lit(snk, canon::K_CH_PREV);
+    emit_pool_str(snk, a.pool, ch[c].previous_hash);
+    emit_lit(snk, canon::K_CH_CLOSE);
+  }
+  emit_lit(snk, canon::K_DELTA_ID);
+  emit_lit(snk, canon::K_DELTA_PFX);
+  emit_uint(snk, turn);
+  emit_char(snk, 0x22u);
+  emit_lit(snk, canon::K_PARENT);
+  int32_t hole = -1;
+  if (turn > 1) {
+    hole = static_cast<int32_t>(snk.pos());
+    for (int b = 0; b < 66; ++b) snk.byte(0x22u);  // placeholder: the chain kernel writes the quoted digest
+  } else {
+    emit_lit(snk, canon::K_NULL);
+  }
+  emit_lit(snk, canon::K_SESSION);
+  emit_session_uuid_quoted(snk, a.uuid + 4 * i);
+  emit_lit(snk, canon::K_TS);
+  emit_iso_quoted(snk, sp_delta_ts(a, i, k));
+  emit_lit(snk, canon::K_TURN);
+  emit_uint(snk, turn);
+  emit_lit(snk, canon::K_CLOSE);
+  const uint32_t len = snk.pos();
+  snk.flush();
+  t.d_sess[d] = static_cast<int32_t>(s);
+  t.d_turn[d] = static_cast<int32_t>(turn);
+  t.d_prev[d] = k > 0 ? a.drow[g - 1] : -1;
+  t.d_ts[d] = sp_delta_ts(a, i, k);
+  t.d_off[d] = a.doff[g];
+  t.d_len[d] = static_cast<int32_t>(len);
+  t.d_hole[d] = hole;
+  if (len > static_cast<uint32_t>(a.dcap[g])) a.status[i] = SP_RENDER;
+}
+
+// Lane per session: the SHA-256 chain over its records (K08).
+AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
+  const Tables& t = a.t;
+  const int64_t s = a.slot[i];
+  uint32_t prev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int32_t g = a.delta_off[i]; g < a.delta_off[i + 1]; ++g) {
+    const int32_t d = a.drow[g];
+    uint8_t* rec = t.payload + t.d_off[d];
+    const uint64_t len = static_cast<uint64_t>(t.d_len[d]);
+    const int32_t hole = t.d_hole[d];
+    if (hole >= 0) {  // '"' + hex(prev) + '"' into the record
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rec[hole + 1 + 8 * q + e] = static_cast<uint8_t>(hex_nibble((prev[q] >> (28 - 4 * e)) & 15u));
+      }
+    }
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(rec);
+    uint32_t h[8];
+    sha256_init(h);
+    const uint64_t nblk = (len + 9 + 63) / 64;
+    for (uint64_t b = 0; b < nblk; ++b) {
+      uint32_t blk[16];
+#pragma unroll
+      for (int w = 0; w < 16; ++w) {
+        const uint64_t o = 64 * b + 4 * w;
+        uint32_t x = 0;
+        if (o + 4 <= len) {
+          x = bswap32(w32[o / 4]);
+        } else if (o < len) {
+          x = bswap32(w32[o / 4]) & (0xffffffffu << (8 * (4 - (len - o))));
+        }
+        if (o <= len && len < o + 4) x |= 0x80u << (8 * (3 - (len - o)));
+        if (b == nblk - 1 && w == 14) x |= static_cast<uint32_t>((len * 8) >> 32);
+        if (b == nblk - 1 && w == 15) x |= static_cast<uint32_t>(len * 8);
+        blk[w] = x;
+      }
+      sha256_compress(h, blk);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      t.d_hash[8 * static_cast<int64_t>(d) + k] = h[k];
+      prev[k] = h[k];
+    }
+  }
+  if (a.delta_off[i + 1] > a.delta_off[i]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t.s_head[8 * s + k] = prev[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void store_pipe_rows_kernel(StorePipeArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.n) sp_rows(a, i);
+}
+
+// lane per delta; `dsess` maps a delta to its session
+__global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd) {
+  const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g < nd) {
+    const int64_t i = dsess[g];
+    if (a.status[i] != SP_ROW_IN_USE) sp_render(a, i, static_cast<int32_t>(g));
+  }
+}
+
+__global__ __launch_bounds__(64) void store_pipe_chain_kernel(StorePipeArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.n && a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
+}
+
+template <class T>
+T* P(const py::dict& d, const char* k) {
+  return reinterpret_cast<T*>(d[k].cast<uintptr_t>());
+}
+
+StorePipeArgs to_args(const Tables& t, const py::dict& d) {
+  StorePipeArgs a{};
+  a.t = t;
+  a.n = d["n"].cast<int64_t>();
+  a.pool = StrPool{P<const uint8_t>(d, "pool_bytes"), P<const int64_t>(d, "pool_off"), P<const int32_t>(d, "pool_len")};
+  a.slot = P<const int32_t>(d, "slot");
+  a.uuid = P<const uint32_t>(d, "uuid");
+  a.t0 = P<const int64_t>(d, "t0");
+  a.creator = P<const int32_t>(d, "creator");
+  a.maxpart = P<const int32_t>(d, "maxpart");
+  a.minsig = P<const double>(d, "minsig");
+  a.flags = P<const uint8_t>(d, "flags");
+  a.join_off = P<const int32_t>(d, "join_off");
+  a.join_agent = P<const int32_t>(d, "join_agent");
+  a.join_sigma = P<const double>(d, "join_sigma");
+  a.join_ring = P<uint8_t>(d, "join_ring");
+  a.join_code = P<uint8_t>(d, "join_code");
+  a.delta_off = P<const int32_t>(d, "delta_off");
+  a.drow = P<const int32_t>(d, "drow");
+  a.dagent_pool = P<const int32_t>(d, "dagent_pool");
+  a.dch_off = P<const int32_t>(d, "dch_off");
+  a.changes = P<const ChangeIds>(d, "changes");
+  a.doff = P<const int64_t>(d, "doff");
+  a.dcap = P<const int32_t>(d, "dcap");
+  a.gslot = P<const int32_t>(d, "gslot");
+  a.step_off = P<const int32_t>(d, "step_off");
+  a.tslot = P<const int32_t>(d, "tslot");
+  a.step_undo = P<const uint8_t>(d, "step_undo");
+  a.step_retries = P<const int32_t>(d, "step_retries");
+  a.step_fail = P<const uint8_t>(d, "step_fail");
+  a.gc_retention_us = d["gc_retention_us"].cast<int64_t>();
+  a.status = P<int32_t>(d, "status");
+  return a;
+}
+
+}  // namespace
+
+// Launch the three kernels on `stream` (device) or run the twin (host tables).
+void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t stream) {
+  const StorePipeArgs a = to_args(t, d);
+  const int32_t* dsess = P<const int32_t>(d, "dsess");
+  const int64_t nd = d["nd"].cast<int64_t>();
+  if (!gpu) {
+    for (int64_t i = 0; i < a.n; ++i) sp_rows(a, i);
+    for (int64_t g = 0; g < nd; ++g)
+      if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_render(a, dsess[g], static_cast<int32_t>(g));
+    for (int64_t i = 0; i < a.n; ++i)
+      if (a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
+    return;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  py::gil_scoped_release nogil;
+  if (a.n > 0) {
+    hipLaunchKernelGGL(store_pipe_rows_kernel, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, st, a);
+    if (nd > 0)
+      hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
+                         a, dsess, nd);
+    hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
+  }
+  check_hip(hipGetLastError(), "store_pipeline");
+}
+
+}  // namespace ahv

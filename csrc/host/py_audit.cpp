@@ -467,6 +467,38 @@ static py::object uuid4(const std::string& prefix) {
   return py::reinterpret_steal<py::object>(s);
 }
 
+// uuid4_many(n, prefix) -> ([prefix + uuid4] * n, bytes of n×4 native u32 words):
+// the words are the uuid's 32 hex digits as four big-endian 8-digit numbers
+// (the layout of the store's s_uuid rows and of the device renderer).
+static py::tuple uuid4_many(int64_t n, const std::string& prefix) {
+  if (n < 0) throw py::value_error("n must be >= 0");
+  py::list ids(n);
+  std::string words(static_cast<size_t>(n) * 16, '\0');
+  uint32_t* w = reinterpret_cast<uint32_t*>(words.data());
+  const size_t pl = prefix.size();
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t hi = g_rng.next(), lo = g_rng.next();
+    hi = (hi & 0xffffffffffff0fffull) | 0x0000000000004000ull;
+    lo = (lo & 0x3fffffffffffffffull) | 0x8000000000000000ull;
+    PyObject* s = PyUnicode_New(static_cast<Py_ssize_t>(pl + 36), 127);
+    if (!s) throw py::error_already_set();
+    char* o = reinterpret_cast<char*>(PyUnicode_1BYTE_DATA(s));
+    std::memcpy(o, prefix.data(), pl);
+    o += pl;
+    put_hex(o, hi >> 32, 8); o[8] = '-';
+    put_hex(o + 9, (hi >> 16) & 0xffff, 4); o[13] = '-';
+    put_hex(o + 14, hi & 0xffff, 4); o[18] = '-';
+    put_hex(o + 19, lo >> 48, 4); o[23] = '-';
+    put_hex(o + 24, lo & 0xffffffffffffull, 12);
+    PyList_SET_ITEM(ids.ptr(), static_cast<Py_ssize_t>(i), s);
+    w[4 * i + 0] = static_cast<uint32_t>(hi >> 32);
+    w[4 * i + 1] = static_cast<uint32_t>(hi);
+    w[4 * i + 2] = static_cast<uint32_t>(lo >> 32);
+    w[4 * i + 3] = static_cast<uint32_t>(lo);
+  }
+  return py::make_tuple(ids, py::bytes(words));
+}
+
 // hex_id(prefix, nchars) -> prefix + nchars random lowercase hex digits
 // (the reference's f"{prefix}{uuid.uuid4().hex[:n]}" id pattern).
 static py::object hex_id(const std::string& prefix, int nchars) {
@@ -495,6 +527,8 @@ void register_audit(py::module_& m) {
   m.def("sha256_hex", &sha256_hex, "SHA-256 hex digest of str (UTF-8) or bytes");
   m.def("uuid4", &uuid4, py::arg("prefix") = std::string(), "prefix + random uuid4 string");
   m.def("hex_id", &hex_id, py::arg("prefix"), py::arg("nchars"), "prefix + random hex digits");
+  m.def("uuid4_many", &uuid4_many, py::arg("n"), py::arg("prefix") = std::string(),
+        "n uuid4 strings and their 4 u32 words each");
 }
 
 }  // namespace host

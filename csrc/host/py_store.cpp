@@ -38,6 +38,8 @@ extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64
                                        uint64_t idle_ticks, uint64_t max_ticks, int speculate, hipStream_t stream);
 
 namespace ahv {
+void store_pipeline_run(const store::Tables& t, bool gpu, const pybind11::dict& d, uintptr_t stream);
+
 namespace host {
 
 bool render_delta(PyObject* d, std::string& out, size_t* null_parent_at);
@@ -544,6 +546,43 @@ class Store {
     return py::make_tuple(didx, off);
   }
 
+  // Delta rows + arena reservations for a batch of records (the batched store
+  // pipeline renders into them): `caps` = int32 bytes per record.  Returns
+  // (int32 rows bytes, int64 offsets bytes), or (code, None) with code -2 (delta
+  // table full) / -3 (arena full) after releasing what it took.
+  py::tuple reserve_deltas(const py::bytes& caps) {
+    std::string_view v = caps;
+    const size_t n = v.size() / 4;
+    const int32_t* c = reinterpret_cast<const int32_t*>(v.data());
+    std::string rows(n * 4, '\0'), offs(n * 8, '\0');
+    int32_t* r = reinterpret_cast<int32_t*>(rows.data());
+    int64_t* o = reinterpret_cast<int64_t*>(offs.data());
+    for (size_t i = 0; i < n; ++i) {
+      const int64_t d = take_delta_row();
+      const int64_t off = d < 0 ? -1 : arena_.alloc(c[i]);
+      if (d < 0 || off < 0) {
+        if (d >= 0) dfree_.push_back(static_cast<int32_t>(d));
+        for (size_t k = 0; k < i; ++k) {
+          arena_.free(o[k], c[k]);
+          d_off_[static_cast<size_t>(r[k])] = -1;
+          d_len_[static_cast<size_t>(r[k])] = 0;
+          dfree_.push_back(r[k]);
+        }
+        return py::make_tuple(d < 0 ? -2 : -3, py::none());
+      }
+      r[i] = static_cast<int32_t>(d);
+      o[i] = off;
+      d_off_[static_cast<size_t>(d)] = off;
+      d_len_[static_cast<size_t>(d)] = c[i];  // the reservation is what a free returns
+    }
+    return py::make_tuple(py::bytes(rows), py::bytes(offs));
+  }
+
+  // The batched store pipeline (csrc/hip/store_pipeline.hip) over this store's
+  // tables on `stream`; the caller released the worker's writes (OP_FLUSH)
+  // before and has it acquire the new rows (OP_ACQUIRE) after the stream drains.
+  void run_pipeline(const py::dict& d, uintptr_t stream) { store_pipeline_run(t_, gpu_, d, stream); }
+
   // Reclaim delta rows (and their arena records) no API object refers to any
   // more: OP_FREE_ROWS marks them free on the device after the hash engine has
   // drained, then the rows and bytes return to the host free lists.
@@ -666,6 +705,8 @@ void register_store(py::module_& m) {
       .def("capture_bytes", &Store::capture_bytes)
       .def("restore_delta", &Store::restore_delta)
       .def("free_deltas", &Store::free_deltas)
+      .def("reserve_deltas", &Store::reserve_deltas)
+      .def("run_pipeline", &Store::run_pipeline)
       .def("free_rows", &Store::free_rows_cmd)
       .def("quiesce", &Store::quiesce)
       .def("rebind", &Store::rebind)

@@ -857,23 +857,31 @@ class DeviceCommitmentEngine(CommitmentEngine):
         self._store = store
         self._device: dict[str, DeviceSession] = {}
 
-    def _record(self, sso: DeviceSession) -> Optional[CommitmentRecord]:
-        r, parts = sso._read(True)
-        if not r[11]:
+    def _record(self, sso) -> Optional[CommitmentRecord]:
+        x = snapshots(self._store, [sso], parts=True)[0]
+        if x.committed_at is None:
             return None
         return CommitmentRecord(
-            session_id=sso.session_id, merkle_root=_hex(r[20:28]),
-            participant_dids=[self._store.did(p[0]) for p in parts if p[2]],
-            delta_count=r[12], committed_at=from_us(r[11]),
+            session_id=sso.session_id, merkle_root=x.merkle_root,
+            participant_dids=[p.agent_did for p in x.participants], delta_count=x.commit_count,
+            committed_at=x.committed_at,
         )
 
-    def register(self, sso: DeviceSession) -> None:
-        self._device[sso.session_id] = sso
+    def register(self, sso) -> None:
+        """A committed device session (or a lazy batched one: its row is used)."""
+        sid = sso.session_id if hasattr(sso, "session_id") else sso.row.session_id
+        self._device[sid] = sso
+
+    @staticmethod
+    def _row(x):
+        from hypervisor.core import LazyManagedSession
+
+        return x.row if isinstance(x, LazyManagedSession) else x
 
     def get_commitment(self, session_id: str) -> Optional[CommitmentRecord]:
         sso = self._device.get(session_id)
         if sso is not None:
-            return self._record(sso)
+            return self._record(self._row(sso))
         return super().get_commitment(session_id)
 
     def verify(self, session_id: str, expected_root: str) -> bool:
@@ -883,7 +891,7 @@ class DeviceCommitmentEngine(CommitmentEngine):
     @property
     def _commitments_view(self) -> dict[str, CommitmentRecord]:
         out = {}
-        ssos = list(self._device.values())
+        ssos = [self._row(x) for x in self._device.values()]
         for sso, x in zip(ssos, snapshots(self._store, ssos, parts=True)):  # one batched read
             if x.committed_at is not None:
                 out[sso.session_id] = CommitmentRecord(

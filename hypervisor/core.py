@@ -77,6 +77,48 @@ class ManagedSession:
         self.saga = saga if saga is not None else SagaOrchestrator()
 
 
+class LazyManagedSession(ManagedSession):
+    """A session a batched pipeline wrote into the device store
+    (:meth:`Hypervisor.run_pipelines`): its Python views are built on first use
+    and then own its rows; if it is dropped before that, its rows are released."""
+
+    __slots__ = ("_batch", "_index", "_built")
+
+    def __init__(self, batch, index: int) -> None:  # noqa: D107 - views come later
+        self._batch = batch
+        self._index = index
+        self._built = False
+
+    @property
+    def row(self):
+        """Identity of the session row (slot, id, creator) without building views."""
+        from agent_hypervisor_amd.models.store_pipeline import _RowRef, _spec
+
+        if self._built:
+            return self.sso
+        b, i = self._batch, self._index
+        return _RowRef(int(b.slots[i]), b.ids[i], _spec(b, i).creator_did)
+
+    def __getattr__(self, name):
+        if name in ("sso", "reversibility", "delta_engine", "saga") and not self._built:
+            from agent_hypervisor_amd.models.store_pipeline import materialize
+
+            sso, de, orch = materialize(self)
+            object.__setattr__(self, "_built", True)
+            ManagedSession.__init__(self, sso, de, orch)
+            return getattr(self, name)
+        raise AttributeError(name)
+
+    def __del__(self) -> None:
+        try:
+            if not self._built:
+                from agent_hypervisor_amd.models.store_pipeline import release_unmaterialized
+
+                release_unmaterialized(self._batch, self._index)
+        except Exception:
+            pass
+
+
 class Hypervisor:
     def __init__(
         self,
@@ -286,6 +328,17 @@ class Hypervisor:
             self._emit(EventType.SESSION_ARCHIVED, session_id)
         return root
 
+    async def run_pipelines(self, specs, n: Optional[int] = None):
+        """Run governance pipelines for many sessions at once on the device store
+        (create → joins → activate → audit deltas → saga steps → terminate): one
+        :class:`~agent_hypervisor_amd.models.store_pipeline.PipelineSpec` per
+        session, or one spec and ``n``.  The sessions are ordinary sessions of this
+        hypervisor afterwards (views built on first use).  Returns a
+        :class:`~agent_hypervisor_amd.models.store_pipeline.PipelineRun`."""
+        from agent_hypervisor_amd.models import store_pipeline
+
+        return store_pipeline.run(self, specs, n)
+
     def get_session(self, session_id: str) -> Optional[ManagedSession]:
         m = self._sessions.get(session_id)
         if m is None and self._device_engine is not None:
@@ -404,12 +457,14 @@ class Hypervisor:
 
     def snapshots(self, managed: Optional[list] = None, parts: bool = False) -> list:
         """:class:`~hypervisor.session.snapshot.SessionSnapshot` of each session (all by
-        default, creation order); device-backed: O(1) store commands for any count."""
+        default, creation order); device-backed: O(1) store commands for any count
+        (batched-pipeline sessions are read without building their views)."""
         ms = list(self._sessions.values()) if managed is None else list(managed)
         if self._store is not None:
             from hypervisor import _device
 
-            return _device.snapshots(self._store, [m.sso for m in ms], parts)
+            rows = [m.row if isinstance(m, LazyManagedSession) else m.sso for m in ms]
+            return _device.snapshots(self._store, rows, parts)
         from hypervisor.session.snapshot import SessionSnapshot
 
         return [SessionSnapshot.of(m.sso, parts) for m in ms]

@@ -1,0 +1,170 @@
+"""Heterogeneous batched pipelines over the device store (``Hypervisor.run_pipelines``).
+
+A randomized batch — several joins per session with per-agent σ (some refused:
+capacity, σ floor, duplicates), per-delta agents and change lists, saga steps
+that succeed, retry or fail, compensation with and without undo APIs, sessions
+left unactivated / unterminated — must equal the scalar public API run session
+by session over the same ids and timestamps, byte for byte: Merkle roots, delta
+digests, session and step states, ring assignments (reference ``core.py:106-185``,
+``saga/orchestrator.py:77-198``).  The batch's sessions are ordinary sessions
+afterwards (views, verify, snapshots).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import random
+
+import pytest
+
+from agent_hypervisor_amd.models.store import GovernanceStore
+from agent_hypervisor_amd.models.store_pipeline import PipelineSpec
+from hypervisor import Hypervisor, SessionConfig
+from hypervisor import _clock
+from hypervisor.audit.delta import VFSChange
+from hypervisor.saga.orchestrator import SagaOrchestrator
+
+AGENTS = [f"did:mesh:agent-{k}" for k in range(9)] + ["did:mesh:ünïcode\"quoted\\"]
+
+
+def random_spec(rng: random.Random) -> PipelineSpec:
+    joins = [(rng.choice(AGENTS), rng.choice([0.3, 0.55, 0.61, 0.7, 0.96, rng.random()]))
+             for _ in range(rng.randrange(0, 6))]
+    deltas = []
+    for _ in range(rng.randrange(0, 5)):
+        chs = [(f"/p{rng.randrange(50)}", rng.choice(["add", "update", "delete"]),
+                rng.choice([None, f"h{rng.randrange(1000)}", "x" * rng.randrange(1, 90)]))
+               for _ in range(rng.randrange(0, 4))]
+        deltas.append((rng.choice(AGENTS), tuple(chs)))
+    steps = [(f"act{k}", rng.choice(AGENTS), f"/api/{k}", rng.choice([None, f"/undo/{k}"]),
+              rng.randrange(0, 3), rng.choice([0, 0, 0, 1, 2, 5])) for k in range(rng.randrange(0, 4))]
+    cfg = SessionConfig(max_participants=rng.choice([2, 3, 10]), min_sigma_eff=rng.choice([0.5, 0.6, 0.9]),
+                        enable_audit=rng.random() < 0.9)
+    return PipelineSpec(joins=tuple(joins), deltas=tuple(deltas), steps=tuple(steps),
+                        activate=rng.random() < 0.9, terminate=rng.random() < 0.85,
+                        compensate=rng.random() < 0.7, config=cfg, creator_did=rng.choice(AGENTS))
+
+
+async def scalar(hv, sid: str, sp: PipelineSpec, t0: int) -> dict:
+    """The same pipeline through the per-call public API (clock pinned to the batch's times)."""
+    out = {"rings": [], "root": None}
+    _clock.set_clock(lambda: _clock.from_us(t0))
+    m = await hv.create_session(sp.config or SessionConfig(), sp.creator_did, session_id=sid)
+    for did, sg in sp.joins:
+        try:
+            out["rings"].append(int(await hv.join_session(sid, did, sigma_raw=sg)))
+        except Exception:  # noqa: BLE001 - a refused join
+            out["rings"].append(None)
+    if sp.activate:
+        try:
+            await hv.activate_session(sid)
+        except Exception:  # noqa: BLE001
+            pass
+    for k, (did, chs) in enumerate(sp.deltas):
+        _clock.set_clock(lambda k=k: _clock.from_us(t0 + 1 + k))
+        m.delta_engine.capture(did, [VFSChange(path=c[0], operation=c[1], content_hash=c[2]) for c in chs])
+    if sp.steps:
+        saga = m.saga.create_saga(sid)
+        steps = [m.saga.add_step(saga.saga_id, a[0], a[1], a[2], undo_api=a[3], max_retries=a[4]) for a in sp.steps]
+        failed = False
+        for st_, a in zip(steps, sp.steps):
+            calls = {"n": 0}
+
+            async def ex(calls=calls, fails=a[5]):
+                calls["n"] += 1
+                if calls["n"] <= fails:
+                    raise RuntimeError("planned failure")
+                return "ok"
+
+            try:
+                await m.saga.execute_step(saga.saga_id, st_.step_id, ex)
+            except RuntimeError:
+                failed = True
+                break
+        if failed and sp.compensate:
+            async def comp(step):
+                return "undone"
+
+            await m.saga.compensate(saga.saga_id, comp)
+        out["steps"] = [s.state.value for s in steps]
+        out["saga"] = saga.state.value
+    if sp.terminate:
+        try:
+            out["root"] = await hv.terminate_session(sid)
+        except Exception:  # noqa: BLE001
+            pass
+    _clock.set_clock(None)
+    out["state"] = m.sso.state.value
+    out["parts"] = [(p.agent_did, int(p.ring)) for p in m.sso.participants]
+    out["digests"] = [d.delta_hash for d in m.delta_engine.deltas]
+    return out
+
+
+def batched(m) -> dict:
+    out = {"state": m.sso.state.value, "parts": [(p.agent_did, int(p.ring)) for p in m.sso.participants],
+           "digests": [d.delta_hash for d in m.delta_engine.deltas]}
+    if m.saga.sagas:
+        g = m.saga.sagas[0]
+        out["steps"] = [s.state.value for s in g.steps]
+        out["saga"] = g.state.value
+    return out
+
+
+def check_randomized(device: str, n: int, seed: int = 3) -> None:
+    rng = random.Random(seed)
+    specs = [random_spec(rng) for _ in range(n)]
+    st = GovernanceStore(device, caps={"S": max(64, n), "D": max(256, 4 * n), "G": max(64, n), "T": max(64, 3 * n)})
+    hv = Hypervisor(store=st)
+    old_delay = SagaOrchestrator.DEFAULT_RETRY_DELAY_SECONDS
+    SagaOrchestrator.DEFAULT_RETRY_DELAY_SECONDS = 0.0
+    try:
+        run = asyncio.run(hv.run_pipelines(specs))
+        assert run.status.shape == (n,)
+        t0 = int(hv._sessions[run.session_ids[0]]._batch.t0)
+        ref = Hypervisor(device="host")
+        check = range(n) if n <= 2000 else rng.sample(range(n), 2000)
+        jpos = [0]
+        for sp in specs:
+            jpos.append(jpos[-1] + len(sp.joins))
+        for i in check:
+            sid = run.session_ids[i]
+            want = asyncio.run(scalar(ref, sid, specs[i], t0))
+            got = batched(hv.get_session(sid))
+            for k in ("state", "parts", "digests", "steps", "saga"):
+                assert got.get(k) == want.get(k), (i, k, specs[i])
+            codes = run.join_codes[jpos[i]:jpos[i + 1]].tolist()
+            rings = run.join_rings[jpos[i]:jpos[i + 1]].tolist()
+            assert [r if c == 0 else None for r, c in zip(rings, codes)] == want["rings"], (i, specs[i])
+            assert run.roots.get(sid) == want["root"], (i, specs[i])
+        rep = hv.verify_audit()
+        assert rep.ok and rep.deltas == sum(len(s.deltas) for s in specs)
+    finally:
+        SagaOrchestrator.DEFAULT_RETRY_DELAY_SECONDS = old_delay
+        _clock.set_clock(None)
+    st.close()
+
+
+def test_randomized_batch_equals_scalar_api_cpu_twin():
+    check_randomized("cpu", 400)
+
+
+def test_reference_template_batch_and_reuse_cpu_twin():
+    st = GovernanceStore("cpu", caps={"S": 64, "D": 256, "G": 64, "T": 64},
+                         max_caps={"S": 64, "D": 256, "G": 64, "T": 64})
+    for _ in range(5):  # rows of dropped (never materialized) batches come back: the table never grows
+        hv = Hypervisor(store=st)
+        run = asyncio.run(hv.run_pipelines(PipelineSpec(), 60))
+        assert run.ok == 60 and len(run.roots) == 60
+        snaps = hv.snapshots()
+        assert all(x.state.value == "archived" and x.participant_count == 1 for x in snaps)
+        del hv, run, snaps
+        import gc
+
+        gc.collect()
+    assert st.grows == {k: 0 for k in st.grows}
+    st.close()
+
+
+@pytest.mark.gpu
+def test_randomized_batch_equals_scalar_api_gpu():
+    check_randomized("cuda", 100_000)

@@ -61,7 +61,8 @@ def check_verify_in_place(device: str, n: int) -> None:
         st.stage = st_stage
     assert rep.ok and rep.deltas == sum(m.delta_engine.turn_count for m in ms)
     assert rep.roots_checked == n // 2
-    assert sum(staged) == 0 and posted <= 4  # drain + flush: row lists only, no records
+    # only int32 row lists cross (the commitment view's slot list); a record is ~300 B per delta
+    assert sum(staged) <= 4 * n and posted <= 8
     # tamper one resident digest: its chain (digest) and the link of its successor fail
     victim = ms[3].delta_engine.deltas[1]
     idx = [8 * victim._didx + k for k in range(8)]
