@@ -27,6 +27,7 @@ import struct
 import threading
 from typing import Optional
 
+import numpy as np
 import torch
 
 from agent_hypervisor_amd._native import C
@@ -240,7 +241,7 @@ class GovernanceStore:
     def reserve_deltas(self, caps: list) -> tuple:
         """Delta rows + arena reservations of ``caps`` bytes each (batched pipeline):
         ``(rows int32 bytes, offsets int64 bytes)``."""
-        raw = struct.pack(f"<{len(caps)}i", *caps)
+        raw = np.ascontiguousarray(caps, dtype="<i4").tobytes()
         tries = 0
         while True:
             r = self._c.reserve_deltas(raw)

@@ -78,10 +78,52 @@ class PipelineRun:
 
 
 class _Batch:
-    """Host metadata of one batch: what a lazy session needs to build its views."""
+    """Host metadata of one batch: what a lazy session needs to build its views.
+
+    Row ownership: a session that builds its views hands its rows to them
+    (``built``); the rows of sessions dropped unbuilt are returned in bulk — a
+    dropped session only appends its index to ``dead`` and every ``_FLUSH`` of
+    them (and whatever is left when the batch itself goes) are released with one
+    vectorized gather per table."""
 
     __slots__ = ("store", "specs", "shared", "ids", "slots", "t0", "doff", "drows", "dlen", "dhash",
-                 "delta_off", "gslots", "step_off", "tslots", "__weakref__")
+                 "delta_off", "gslots", "step_off", "tslots", "status", "built", "released", "dead",
+                 "__weakref__")
+
+    _FLUSH = 8192
+
+    def drop(self, i: int) -> None:
+        self.dead.append(i)
+        if len(self.dead) >= self._FLUSH:
+            self.release(np.asarray(self.dead, dtype=np.int64))
+            self.dead = []
+
+    def release(self, idx: np.ndarray) -> None:
+        """Return the rows of unbuilt sessions ``idx`` to the store (once each)."""
+        idx = idx[~self.built[idx] & ~self.released[idx]]
+        if not len(idx):
+            return
+        self.released[idx] = True
+        st = self.store
+        n = len(self.slots)
+        sel = np.zeros(n, dtype=bool)
+        sel[idx] = True
+        refused = self.status == 1  # the device kept the row from us: not ours to free
+        st.release_many("S", self.slots[sel & ~refused].tolist())
+        nd = np.diff(self.delta_off)
+        if nd.any():
+            st.release_many("D", self.drows[np.repeat(sel, nd)].tolist())
+        g = self.gslots[sel]
+        g = g[g >= 0]
+        if len(g):
+            st.release_many("G", g.tolist())
+            st.release_many("T", self.tslots[np.repeat(sel, np.diff(self.step_off))].tolist())
+
+    def __del__(self) -> None:
+        try:
+            self.release(np.arange(len(self.slots), dtype=np.int64))
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
 
 def _spec(b: _Batch, i: int) -> PipelineSpec:
@@ -179,14 +221,13 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         ch_off.append(len(ch_rows))
     if shared:
         per = len(deltas)
-        caps = [_delta_cap(pool, cache, did, chs, t + 1) for t, (did, chs) in enumerate(deltas)] * n
-        nch = [ch_off[k + 1] - ch_off[k] for k in range(per)]
-        d_pool = d_pool * n
+        caps = np.tile(np.asarray([_delta_cap(pool, cache, did, chs, t + 1) for t, (did, chs) in enumerate(deltas)],
+                                  dtype=np.int32), n)
+        d_pool = np.tile(np.asarray(d_pool, dtype=np.int32), n)
         base = np.asarray(ch_off[:-1], dtype=np.int32)
         per_ch = ch_off[-1]
-        ch_off_all = (np.tile(base, n) + np.repeat(np.arange(n, dtype=np.int32) * per_ch, per)).tolist() + [per_ch * n]
+        ch_off_all = np.append(np.tile(base, n) + np.repeat(np.arange(n, dtype=np.int32) * per_ch, per), per_ch * n)
         ch_rows = np.tile(np.asarray(ch_rows or [[0, 0, 0, 0]], dtype=np.int32), (n, 1)) if ch_rows else []
-        del nch
     else:
         turn_of = []
         for i in range(n):
@@ -289,15 +330,16 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         gg = st.gather({"s_root": (cs[:, None] * 8 + np.arange(8, dtype=np.int64)[None, :]).reshape(-1),
                         "s_committed": cs})
         rr = gg["s_root"].astype(np.uint32).reshape(-1, 8)
-        hexes = [bytes(x).hex() for x in rr.byteswap()] if len(rr) else []  # 8 BE words → 64 hex digits
-        for j, i in enumerate(committed):
-            if gg["s_committed"][j] != 0:
-                roots[ids[i]] = hexes[j]
-                committed_ids.add(ids[i])
+        flat = rr.byteswap().tobytes().hex()  # 8 BE words → 64 hex digits per root
+        for j in np.flatnonzero(gg["s_committed"]).tolist():
+            sid = ids[committed[j]]
+            roots[sid] = flat[64 * j:64 * j + 64]
+            committed_ids.add(sid)
     b = _Batch()
     b.store, b.specs, b.shared, b.ids, b.slots, b.t0 = st, specs, shared, ids, slots, t0
     b.doff, b.drows, b.dlen, b.dhash = np.frombuffer(doff, dtype=np.int64), drow_np, dlen, dhash
     b.delta_off, b.gslots, b.step_off, b.tslots = delta_off, gslots, step_off, tslots
+    b.status, b.built, b.released, b.dead = status_np, np.zeros(n, dtype=bool), np.zeros(n, dtype=bool), []
     register_lazy(hv, b, status_np, committed_ids)
     run_ = PipelineRun(session_ids=ids, status=status_np,
                        join_rings=tens["join_ring"].cpu().numpy()[: len(j_agent)],
@@ -321,14 +363,14 @@ def register_lazy(hv, b: _Batch, status: np.ndarray, committed: set) -> None:
     from hypervisor.core import LazyManagedSession
 
     sessions = hv._sessions
-    reg = hv.commitment
+    lazy = {}
     for i, sid in enumerate(b.ids):
         if status[i] == 1:  # row refused: nothing was written, the row stays with its owner
             continue
-        m = LazyManagedSession(b, i)
-        sessions[sid] = m
-        if sid in committed:
-            reg.register(m)  # resolved to its row when a commitment view asks
+        lazy[sid] = LazyManagedSession(b, i)
+    sessions.update(lazy)
+    if committed:  # resolved to their rows when a commitment view asks
+        hv.commitment.register_many({sid: lazy[sid] for sid in committed if sid in lazy})
 
 
 def materialize(m) -> None:
@@ -376,13 +418,3 @@ def materialize(m) -> None:
     return sso, de, orch
 
 
-def release_unmaterialized(b: _Batch, i: int) -> None:
-    """A lazy session that never built its views is gone: its rows go back."""
-    st = b.store
-    st.release("S", int(b.slots[i]))
-    d0, d1 = int(b.delta_off[i]), int(b.delta_off[i + 1])
-    if d1 > d0:
-        st.release_many("D", [int(x) for x in b.drows[d0:d1]])
-    if int(b.gslots[i]) >= 0:
-        st.release("G", int(b.gslots[i]))
-        st.release_many("T", [int(x) for x in b.tslots[int(b.step_off[i]):int(b.step_off[i + 1])]])

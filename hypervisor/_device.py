@@ -872,6 +872,10 @@ class DeviceCommitmentEngine(CommitmentEngine):
         sid = sso.session_id if hasattr(sso, "session_id") else sso.row.session_id
         self._device[sid] = sso
 
+    def register_many(self, lazy: dict) -> None:
+        """Session id → lazy batched session, for a whole batch at once."""
+        self._device.update(lazy)
+
     @staticmethod
     def _row(x):
         from hypervisor.core import LazyManagedSession

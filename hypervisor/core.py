@@ -105,6 +105,7 @@ class LazyManagedSession(ManagedSession):
 
             sso, de, orch = materialize(self)
             object.__setattr__(self, "_built", True)
+            self._batch.built[self._index] = True
             ManagedSession.__init__(self, sso, de, orch)
             return getattr(self, name)
         raise AttributeError(name)
@@ -112,10 +113,8 @@ class LazyManagedSession(ManagedSession):
     def __del__(self) -> None:
         try:
             if not self._built:
-                from agent_hypervisor_amd.models.store_pipeline import release_unmaterialized
-
-                release_unmaterialized(self._batch, self._index)
-        except Exception:
+                self._batch.drop(self._index)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 
 

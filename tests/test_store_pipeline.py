@@ -168,3 +168,33 @@ def test_reference_template_batch_and_reuse_cpu_twin():
 @pytest.mark.gpu
 def test_randomized_batch_equals_scalar_api_gpu():
     check_randomized("cuda", 100_000)
+
+
+def test_lazy_rows_released_in_bulk_and_materialized_rows_kept(monkeypatch):
+    import gc
+
+    from agent_hypervisor_amd.models import store_pipeline as SP
+
+    monkeypatch.setattr(SP._Batch, "_FLUSH", 7)
+    st = GovernanceStore("cpu", caps={"S": 128, "D": 512, "G": 128, "T": 128})
+    base = {k: st.live_rows()[k] for k in ("S", "G", "T", "D")}
+    hv = Hypervisor(store=st)
+    run = asyncio.run(hv.run_pipelines(PipelineSpec(), 40))
+    keep = [hv.get_session(sid) for sid in run.session_ids[:5]]
+    assert all(len(m.delta_engine.deltas) == 3 for m in keep)  # materialized: they own their rows
+    for sid in run.session_ids[5:25]:  # dropped one by one: released every _FLUSH
+        hv._sessions.pop(sid)
+        hv.commitment._device.pop(sid, None)
+    gc.collect()
+    st.reclaim()
+    assert st.live_rows()["S"] == base["S"] + 40 - 14  # two flushes of 7; 6 wait for the batch
+    del hv, run
+    gc.collect()
+    st.reclaim()
+    assert st.live_rows()["S"] == base["S"] + 5 and st.live_rows()["G"] == base["G"] + 5
+    assert [m.sso.session_id for m in keep] and all(m.delta_engine.deltas[2].delta_id == "delta:3" for m in keep)
+    del keep
+    gc.collect()
+    st.reclaim()
+    assert {k: st.live_rows()[k] for k in ("S", "G", "T", "D")} == base
+    st.close()
