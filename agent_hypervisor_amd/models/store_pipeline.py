@@ -66,8 +66,19 @@ class PipelineRun:
     status: np.ndarray        # per session, 0 = every stage admitted (see status_name)
     join_rings: np.ndarray    # per join, in spec order
     join_codes: np.ndarray
-    roots: dict = field(default_factory=dict)  # session id → committed Merkle root (hex)
     device_seconds: float = 0.0
+    _roots: tuple = field(default=(), repr=False)  # (committed session indices, their roots as one hex string)
+
+    @property
+    def roots(self) -> dict:
+        """Session id → committed Merkle root (64 hex digits), built on first access."""
+        r = self.__dict__.get("_roots_dict")
+        if r is None:
+            idx, flat = self._roots or ((), "")
+            ids = self.session_ids
+            r = self.__dict__["_roots_dict"] = {ids[i]: flat[64 * j:64 * j + 64]
+                                                for j, i in enumerate(list(idx))}
+        return r
 
     def status_name(self, i: int) -> str:
         return _STATUS.get(int(self.status[i]), str(int(self.status[i])))
@@ -88,9 +99,54 @@ class _Batch:
 
     __slots__ = ("store", "specs", "shared", "ids", "slots", "t0", "doff", "drows", "dlen", "dhash",
                  "delta_off", "gslots", "step_off", "tslots", "status", "built", "released", "dead",
-                 "__weakref__")
+                 "index", "views", "committed", "__weakref__")
 
     _FLUSH = 8192
+
+    # -- the session table's view of the batch (hypervisor.session.table) --------
+    def view(self, i: int):
+        """The ManagedSession of session ``i`` (built on first use; it then owns the rows)."""
+        m = self.views.get(i)
+        if m is None:
+            from hypervisor.core import ManagedSession
+
+            m = self.views[i] = ManagedSession(*materialize(self, i))
+            self.built[i] = True
+        return m
+
+    def forget(self, i: int):
+        """Session ``i`` left the hypervisor: its view (if built) or its rows go."""
+        m = self.views.pop(i, None)
+        if m is None:
+            self.drop(i)
+        return m
+
+    def entries(self):
+        from hypervisor.core import LazyManagedSession
+
+        views = self.views
+        for i in self.index.values():
+            m = views.get(i)
+            yield m if m is not None else LazyManagedSession(self, i)
+
+    def rowref(self, i: int):
+        m = self.views.get(i)
+        if m is not None:
+            return m.sso
+        return _RowRef(int(self.slots[i]), self.ids[i], _spec(self, i).creator_did)
+
+    def rows(self, committed: bool = False) -> tuple:
+        """(slots, session ids, creator DIDs) of the batch's sessions (or of its
+        committed ones) in order — what a batched snapshot read needs."""
+        idx = np.fromiter(self.index.values(), dtype=np.int64, count=len(self.index))
+        if committed:
+            idx = idx[self.committed[idx]]
+        ids = self.ids
+        if self.shared:
+            creators = [self.specs.creator_did] * len(idx)
+        else:
+            creators = [self.specs[i].creator_did for i in idx.tolist()]
+        return self.slots[idx], [ids[i] for i in idx.tolist()], creators
 
     def drop(self, i: int) -> None:
         self.dead.append(i)
@@ -290,7 +346,6 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         st._c.run_pipeline(args, 0)
     # K09: roots of the committed chains over the digests just written → s_root
     status = tens["status"]
-    roots = {}
     committed = [i for i in range(n) if (int(flags[i]) & 9) == 9 and delta_off[i + 1] > delta_off[i]] \
         if not shared else (list(range(n)) if (int(flags[0]) & 9) == 9 and delta_off[1] > 0 else [])
     drow_np = np.frombuffer(drows, dtype=np.int32)
@@ -324,26 +379,27 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         if nd else {"d_len": np.zeros(0, np.int32), "d_hash": np.zeros(0, np.int32)}
     dlen = gath["d_len"].astype(np.int64)
     dhash = gath["d_hash"].astype(np.uint32).reshape(-1, 8) if nd else np.zeros((0, 8), np.uint32)
-    committed_ids: set = set()
+    cidx = np.zeros(0, dtype=np.int64)
+    flat = ""
     if committed:
-        cs = slots[np.asarray(committed, dtype=np.int64)].astype(np.int64)
+        call = np.asarray(committed, dtype=np.int64)
+        cs = slots[call].astype(np.int64)
         gg = st.gather({"s_root": (cs[:, None] * 8 + np.arange(8, dtype=np.int64)[None, :]).reshape(-1),
                         "s_committed": cs})
-        rr = gg["s_root"].astype(np.uint32).reshape(-1, 8)
+        keep = np.flatnonzero(gg["s_committed"])
+        cidx = call[keep]
+        rr = gg["s_root"].astype(np.uint32).reshape(-1, 8)[keep]
         flat = rr.byteswap().tobytes().hex()  # 8 BE words → 64 hex digits per root
-        for j in np.flatnonzero(gg["s_committed"]).tolist():
-            sid = ids[committed[j]]
-            roots[sid] = flat[64 * j:64 * j + 64]
-            committed_ids.add(sid)
     b = _Batch()
     b.store, b.specs, b.shared, b.ids, b.slots, b.t0 = st, specs, shared, ids, slots, t0
     b.doff, b.drows, b.dlen, b.dhash = np.frombuffer(doff, dtype=np.int64), drow_np, dlen, dhash
     b.delta_off, b.gslots, b.step_off, b.tslots = delta_off, gslots, step_off, tslots
     b.status, b.built, b.released, b.dead = status_np, np.zeros(n, dtype=bool), np.zeros(n, dtype=bool), []
-    register_lazy(hv, b, status_np, committed_ids)
+    register_lazy(hv, b, status_np, cidx)
     run_ = PipelineRun(session_ids=ids, status=status_np,
                        join_rings=tens["join_ring"].cpu().numpy()[: len(j_agent)],
-                       join_codes=tens["join_code"].cpu().numpy()[: len(j_agent)], roots=roots, device_seconds=dev_s)
+                       join_codes=tens["join_code"].cpu().numpy()[: len(j_agent)], device_seconds=dev_s)
+    run_._roots = (cidx, flat)
     return run_
 
 
@@ -359,28 +415,28 @@ class _RowRef:
         self.slot, self.session_id, self.creator_did = slot, session_id, creator_did
 
 
-def register_lazy(hv, b: _Batch, status: np.ndarray, committed: set) -> None:
-    from hypervisor.core import LazyManagedSession
+def register_lazy(hv, b: _Batch, status: np.ndarray, committed: np.ndarray) -> None:
+    """Make the batch's sessions sessions of ``hv`` (no per-session objects);
+    ``committed``: indices of the sessions whose roots the device committed."""
+    ok = np.flatnonzero(status != 1)  # 1: row refused — nothing was written, the row stays with its owner
+    ids = b.ids if len(ok) == len(b.ids) else [b.ids[i] for i in ok.tolist()]
+    b.index = dict(zip(ids, ok.tolist()))
+    b.views = {}
+    b.committed = np.zeros(len(b.ids), dtype=bool)
+    if len(committed):
+        b.committed[committed] = True
+        hv.commitment.register_batch(b)
+    hv._sessions.add_batch(b, ids)
 
-    sessions = hv._sessions
-    lazy = {}
-    for i, sid in enumerate(b.ids):
-        if status[i] == 1:  # row refused: nothing was written, the row stays with its owner
-            continue
-        lazy[sid] = LazyManagedSession(b, i)
-    sessions.update(lazy)
-    if committed:  # resolved to their rows when a commitment view asks
-        hv.commitment.register_many({sid: lazy[sid] for sid in committed if sid in lazy})
 
-
-def materialize(m) -> None:
-    """Build the device views of lazy session ``m`` (they take over its rows)."""
+def materialize(b: _Batch, i: int) -> tuple:
+    """Build the device views (session, delta engine, saga orchestrator) of batch
+    session ``i`` (they take over its rows)."""
     from hypervisor import _device
     from hypervisor._clock import from_us
     from hypervisor.audit.delta import VFSChange
     from hypervisor.models import SessionConfig
 
-    b, i = m._batch, m._index
     st = b.store
     sp = _spec(b, i)
     sid = b.ids[i]

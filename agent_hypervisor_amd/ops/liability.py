@@ -9,6 +9,7 @@ local index, and its vouch edges in creation order as CSR arrays
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -88,16 +89,63 @@ def bond_tiles(tiles: torch.Tensor, sigma: torch.Tensor, omega: torch.Tensor,
     return tuple(out)
 
 
+@dataclass
+class AgentIndex:
+    """Resident agent-major index of a batch's voucher slots: agent ``a``'s
+    entries ``index[offsets[a]:offsets[a+1]]`` are the flat (session·16 + local)
+    positions where ``a`` vouches for someone, in session order.  Members that
+    vouch for nobody always carry exposure 0 and are left out."""
+
+    offsets: torch.Tensor  # i64 [A+1]
+    index: torch.Tensor    # i32 [P]
+
+    @property
+    def agents(self) -> int:
+        return self.offsets.numel() - 1
+
+
+def agent_index(vb: VouchBatch, members: torch.Tensor, agents: int) -> AgentIndex:
+    """Build the :class:`AgentIndex` of ``members`` (int64 [S,16] global ids) — once
+    per bond graph (it depends on who vouches, not on which bonds are live)."""
+    dev = vb.device
+    counts = (vb.offsets[1:] - vb.offsets[:-1]).to(i64)
+    sess = torch.repeat_interleave(torch.arange(vb.sessions, device=dev, dtype=i64), counts)
+    pos = torch.unique(sess * TILE + vb.voucher.to(i64))  # sorted: session order
+    ag = members.reshape(-1).to(i64)[pos]
+    order = torch.argsort(ag, stable=True)
+    offs = torch.zeros(agents + 1, dtype=i64, device=dev)
+    offs[1:] = torch.cumsum(torch.bincount(ag, minlength=agents), 0)
+    return AgentIndex(offs, pos[order].to(i32).contiguous())
+
+
+def agent_gather(idx: AgentIndex, rows: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[a] = Σ rows.flat[i] over agent a's entries, in session order — a
+    segmented reduction (no atomics, deterministic; ``agent_exposure`` kernel)."""
+    if out.dtype != f64 or out.numel() != idx.agents:
+        raise ValueError("out must be fp64 [agents]")
+    launch("agent_exposure", {"agents": idx.agents, "now_us": 0},
+           {"offsets": idx.offsets, "bonded": rows.reshape(-1), "active": None, "expiry": None, "out": out,
+            "index": idx.index},
+           {"offsets": i64, "bonded": f64, "index": i32, "out": f64})
+    return out
+
+
 def bond_fused(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us: int,
                members: "torch.Tensor | None" = None, agent_exposure: "torch.Tensor | None" = None,
-               bonded_in: bool = False):
+               bonded_in: bool = False, agent_idx: Optional[AgentIndex] = None):
     """K03/K04 straight from the CSR edges on fp64 MFMA (no dense tile):
     (σ_eff [S,16], exposure [S,16], bonded_in [S,16] or None).
 
     Same outputs as ``build_tiles`` + ``bond_tiles`` at a fraction of the HBM
-    traffic; sums agree with the creation-order reference to ulp level.  With
-    ``members``/``agent_exposure`` the exposure is also scattered into the
-    agent-indexed vector (X01 input) by the same kernel."""
+    traffic; sums agree with the creation-order reference to ulp level.
+
+    Agent-indexed exposure (X01 input), two forms:
+
+    * ``agent_idx`` (an :class:`AgentIndex`): ``agent_exposure`` is *written*
+      with each agent's exposure summed over its sessions in session order by a
+      segmented reduction after the MFMA pass — no atomics, deterministic;
+    * ``members``: the MFMA kernel *adds* each member's exposure into
+      ``agent_exposure`` with fp64 atomics (order across sessions unspecified)."""
     S = vb.sessions
     dev = vb.device
     se = torch.empty((S, TILE), dtype=f64, device=dev)
@@ -105,19 +153,34 @@ def bond_fused(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us:
     bi = torch.empty((S, TILE), dtype=f64, device=dev) if bonded_in else None
     if members is not None and (agent_exposure is None or tuple(members.shape) != (S, TILE)):
         raise ValueError("members must be int64 [S, 16] and come with agent_exposure")
+    if agent_idx is not None and (agent_exposure is None or members is not None):
+        raise ValueError("agent_idx needs agent_exposure (and no members)")
     launch("bond_fused", {"sessions": S, "now_us": int(now_us)},
            dict(offsets=vb.offsets, voucher=vb.voucher, vouchee=vb.vouchee, bonded=vb.bonded, active=vb.active,
                 expiry_us=vb.expiry_us, sigma=sigma, omega=omega, sigma_eff=se, exposure=ex, bonded_in=bi,
                 members=members, agent_exposure=agent_exposure if members is not None else None),
            dict(_CSR_DT, exposure=f64, bonded_in=f64, members=torch.int64, agent_exposure=f64))
+    if agent_idx is not None:
+        agent_gather(agent_idx, ex, agent_exposure)
     return se, ex, bi
 
 
-def sigma_eff_exact(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us: int) -> torch.Tensor:
-    """K03 creation-order path: bit-identical to VouchingEngine.compute_sigma_eff."""
+SIGMA_KERNEL = os.environ.get("AHV_SIGMA_KERNEL", "stream")
+
+
+def sigma_eff_exact(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us: int,
+                    kernel: Optional[str] = None) -> torch.Tensor:
+    """K03 creation-order path: bit-identical to VouchingEngine.compute_sigma_eff.
+
+    ``kernel``: ``"stream"`` (default; register/DPP streaming form, every load of
+    a wave's 16 sessions in flight at once) or ``"csr"`` (LDS-staged form) — the
+    same additions in the same order, so the results are identical."""
+    k = kernel or SIGMA_KERNEL
+    if k not in ("stream", "csr"):
+        raise ValueError(f"unknown sigma_eff kernel {k!r}")
     out = torch.empty((vb.sessions, TILE), dtype=f64, device=vb.device)
     s, t = vb._csr(now_us, tiles=None, sigma=sigma, omega=omega, sigma_eff=out, released=None)
-    launch("sigma_eff_csr", s, t, _CSR_DT)
+    launch("sigma_eff_" + ("stream" if k == "stream" else "csr"), s, t, _CSR_DT)
     return out
 
 
@@ -183,6 +246,7 @@ def slash(
     clip_cap: int = 64,
     zero_records: bool = True,
     with_sigma_eff: bool = False,
+    mode: Optional[str] = None,
 ) -> SlashOutcome:
     """K06: slash ``target[s]`` in every session (cascade ≤ 2), mutating ``vb``
     (bonds released) and ``scores`` in place, like SlashingEngine.slash.  A
@@ -200,7 +264,11 @@ def slash(
     ``with_sigma_eff=True`` fuses K03 into the same pass: :attr:`SlashOutcome.sigma_eff`
     is then every session's σ_eff over its post-slash live bonds with risk weight
     ``omega`` — equal, bit for bit, to ``sigma_eff_exact(vb, scores, omega, now_us)``
-    run after the slash — without a second read of the bond graph."""
+    run after the slash — without a second read of the bond graph.
+
+    ``mode`` picks the device form (all give identical results): ``"split"``
+    (default: cascade over the slashed sessions only, then the streaming σ_eff
+    pass), ``"group"`` (one 16-lane pass per session doing both) or ``"lane"``."""
     S = vb.sessions
     dev = vb.device
     offs = (torch.arange(S, dtype=i32, device=dev) * clip_cap).contiguous()
@@ -219,7 +287,8 @@ def slash(
         fused = dict(bonded=vb.bonded, sigma_eff=out.sigma_eff)
     launch(
         "slash",
-        {"sessions": S, "now_us": int(now_us), "clip_cap": int(clip_cap)},
+        {"sessions": S, "now_us": int(now_us), "clip_cap": int(clip_cap),
+         "mode": {None: -1, "split": 0, "group": 1, "lane": 2}[mode]},
         dict(offsets=vb.offsets, voucher=vb.voucher, vouchee=vb.vouchee, active=vb.active,
              expiry_us=vb.expiry_us, released_us=vb.released_us, target=target, omega=omega, scores=scores,
              clip_offsets=offs, clip_count=out.clip_count, clip_voucher=out.clip_voucher,

@@ -8,7 +8,16 @@
   one-hot products: σ_eff + exposure + agent scatter, no tile).
 
 ``*_ns`` variants skip the agent-indexed exposure scatter (fp64 atomics into the
-[A] vector), the like-for-like comparison with ``csr``.
+[A] vector), the like-for-like comparison with ``csr``;
+* ``stream`` — sigma_eff_stream (K03 exact, register/DPP streaming form — the
+  default ``sigma_eff_exact`` kernel since round 3);
+* ``fused_gather`` — bond_fused + the AgentIndex segmented reduction (X01 input
+  with no atomics, deterministic) instead of the in-kernel atomic scatter;
+* ``exposure`` — ResidentBonds.exposure, the headline's K04 agent form
+  (``--agents`` agents × ``--bond-degree`` edges, segmented LDS reduction);
+* ``slash_split`` / ``slash_group`` — config5's storm (``--slash-sessions``
+  sessions × 16 edges, 10 % slashed, σ_eff fused) in the round-3 split form and
+  the round-2 single group pass.
 
 Prints one JSON line per (variant, S) with µs per call (CUDA events, median of
 ``--iters``).  rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE runs of this script give
@@ -52,9 +61,46 @@ def main() -> None:
     ap.add_argument("--agents", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="comma list of variants (profiling)")
+    ap.add_argument("--bond-degree", type=int, default=4)
+    ap.add_argument("--slash-sessions", type=int, default=625_000)
     a = ap.parse_args()
     dev = torch.device("cuda")
-    only = set(a.only.split(",")) if a.only else {"tiles", "tiles_ns", "csr", "fused", "fused_ns"}
+    only = set(a.only.split(",")) if a.only else {"tiles", "tiles_ns", "csr", "stream", "fused", "fused_ns",
+                                                  "fused_gather", "exposure", "slash_split", "slash_group"}
+    if "exposure" in only:
+        from agent_hypervisor_amd.ops.global_liability import ResidentBonds
+
+        rb = ResidentBonds(a.agents, a.bond_degree, dev, seed=4242)
+        out = torch.empty(a.agents, dtype=torch.float64, device=dev)
+        us = time_us(lambda: rb.exposure(out), a.iters)
+        print(json.dumps(dict(variant="exposure", agents=a.agents, edges=rb.edges, us=round(us, 2),
+                              edges_per_us=round(rb.edges / us, 1),
+                              hbm_gbps=round((rb.edges * 17 + a.agents * 16) / us / 1e3, 1))), flush=True)
+        del rb
+    for mode in ("split", "group"):
+        if "slash_" + mode not in only:
+            continue
+        S5 = a.slash_sessions
+        vb0 = random_vouch_batch(S5, 16, dev, seed=5)
+        g5 = torch.Generator().manual_seed(9)
+        tgt = torch.full((S5,), 255, dtype=torch.uint8)
+        hit = torch.randperm(S5, generator=g5)[: S5 // 10]
+        tgt[hit] = torch.randint(0, 16, (hit.numel(),), generator=g5, dtype=torch.uint8)
+        tgt = tgt.to(dev)
+        om5 = torch.full((S5,), 0.95, dtype=torch.float64, device=dev)
+        sc0 = torch.rand((S5, 16), generator=g5, dtype=torch.float64).to(dev)
+        n_it = a.iters + 3
+        fresh = [(vb0.active.clone(), vb0.released_us.clone(), sc0.clone()) for _ in range(n_it)]
+
+        def storm():
+            act, rel, sc = fresh.pop()
+            vb5 = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, act, vb0.expiry_us, rel)
+            return LI.slash(vb5, tgt, om5, sc, 1, clip_cap=16, zero_records=False, with_sigma_eff=True, mode=mode)
+
+        us = time_us(storm, a.iters)
+        print(json.dumps(dict(variant="slash_" + mode, sessions=S5, edges=S5 * 16, slashed=S5 // 10,
+                              us=round(us, 2), edges_per_us=round(S5 * 16 / us, 1))), flush=True)
+        del fresh, vb0
     for S in a.sessions:
         vb = random_vouch_batch(S, a.edges_per_session, dev, seed=1)
         g = torch.Generator(device=dev).manual_seed(2)
@@ -79,7 +125,16 @@ def main() -> None:
                 return LI.bond_fused(vb, sigma, omega, 0)
             res["fused_ns"] = (time_us(fused_ns, a.iters), (fused_ns()[0] - ref).abs().max().item())
         if "csr" in only:
-            res["csr"] = (time_us(lambda: LI.sigma_eff_exact(vb, sigma, omega, 0), a.iters), 0.0)
+            res["csr"] = (time_us(lambda: LI.sigma_eff_exact(vb, sigma, omega, 0, kernel="csr"), a.iters), 0.0)
+        if "stream" in only:
+            res["stream"] = (time_us(lambda: LI.sigma_eff_exact(vb, sigma, omega, 0, kernel="stream"), a.iters),
+                             (LI.sigma_eff_exact(vb, sigma, omega, 0, kernel="stream") - ref).abs().max().item())
+        if "fused_gather" in only:
+            aidx = LI.agent_index(vb, members, a.agents)
+
+            def fused_gather():
+                return LI.bond_fused(vb, sigma, omega, 0, agent_exposure=ax, agent_idx=aidx)
+            res["fused_gather"] = (time_us(fused_gather, a.iters), (fused_gather()[0] - ref).abs().max().item())
         if "fused" in only:
             def fused():
                 return LI.bond_fused(vb, sigma, omega, 0, members=members, agent_exposure=ax)
@@ -98,8 +153,8 @@ def main() -> None:
         for k, (us, err) in res.items():
             print(json.dumps(dict(variant=k, sessions=S, edges=E, us=round(us, 2),
                                   edges_per_us=round(E / us, 1), max_abs_err_vs_csr=err,
-                                  outputs={"csr": "sigma_eff"}.get(k, "sigma_eff+exposure" + (
-                                      "" if k.endswith("_ns") else "+agent_scatter")))),
+                                  outputs={"csr": "sigma_eff", "stream": "sigma_eff"}.get(k, "sigma_eff+exposure" + (
+                                      "" if k.endswith("_ns") else "+agent_vector")))),
                   flush=True)
 
 

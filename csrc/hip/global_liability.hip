@@ -4,10 +4,17 @@
 //   agent_exposure  (K04, global form) — exposure[a] = Σ live bonded amounts of
 //                   the edges agent a vouches with (reference vouching.py:157-166
 //                   summed over every session the rank owns).  Edges are stored
-//                   CSR by voucher in creation order; one lane per agent walks its
-//                   row sequentially, so each partial is the exact creation-order
-//                   fp64 sum.  The [A] fp64 vector is then all-reduced over ranks
-//                   (X01: 8 MB for 1 M agents, RCCL over xGMI).
+//                   CSR by voucher in creation order — a resident voucher-sorted
+//                   layout, so the agent sums are a segmented reduction with no
+//                   atomics: a wave owns 64 consecutive rows, stages their edge
+//                   range (live bond or +0.0) in LDS with coalesced loads — every
+//                   chunk requested before the first is stored — and each lane
+//                   then adds its row in creation order (the exact fp64 sum;
+//                   adding +0.0 for a dead edge leaves a +0.0-started sum
+//                   unchanged).  The [A] vector is then all-reduced over ranks
+//                   (X01: 8 MB for 1 M agents, RCCL over xGMI).  The same kernel
+//                   gathers an agent's per-session exposure rows through an index
+//                   (X01 input of the fused MFMA pass, ops.liability.bond_fused).
 //   slash_clip      (K06 stage) — for a storm of k slashed vouchees: every live
 //                   incoming edge (CSR by vouchee) is released and its voucher
 //                   gets a clip factor (1 − ω) (reference slashing.py:89-99).  Each
@@ -36,23 +43,60 @@ struct ExposureArgs {
   int64_t agents;
   int64_t now_us;
   const int64_t* offsets;  // [A+1] CSR by voucher
-  const double* bonded;    // [E]
-  const uint8_t* active;   // [E]
-  const int64_t* expiry;   // [E] (-1 = never)
+  const double* bonded;    // [V] values (bond amounts, or per-session exposure rows)
+  const uint8_t* active;   // [V] (null: every entry live)
+  const int64_t* expiry;   // [V] (-1 = never; null: no expiry)
   double* out;             // [A]
+  const int32_t* index;    // [E] value index of entry e (null: e itself)
 };
+
+AHV_HD double exposure_value(const ExposureArgs& a, int64_t e) {
+  const int64_t v = a.index ? a.index[e] : e;
+  const bool live = (!a.active || a.active[v]) && (!a.expiry || a.expiry[v] < 0 || a.now_us <= a.expiry[v]);
+  return live ? a.bonded[v] : 0.0;
+}
 
 AHV_HD double exposure_row(const ExposureArgs& a, int64_t r) {
   double s = 0.0;
-  for (int64_t e = a.offsets[r]; e < a.offsets[r + 1]; ++e)
-    if (a.active[e] && (a.expiry[e] < 0 || a.now_us <= a.expiry[e])) s += a.bonded[e];
+  for (int64_t e = a.offsets[r]; e < a.offsets[r + 1]; ++e) s += exposure_value(a, e);
   return s;
 }
 
-__global__ __launch_bounds__(256) void agent_exposure_kernel(ExposureArgs a) {
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; r < a.agents; r += stride)
-    a.out[r] = exposure_row(a, r);
+constexpr int kSegWaves = 4;
+constexpr int kSegChunks = 8;                      // staged chunks of 64 entries per wave
+constexpr int kSegLds = kSegChunks * 64;           // 512 entries (4 KB) per wave
+
+__global__ __launch_bounds__(64 * kSegWaves) void agent_exposure_kernel(ExposureArgs a) {
+  __shared__ double s_v[kSegWaves][kSegLds];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t r0 = (static_cast<int64_t>(blockIdx.x) * kSegWaves + w) * 64;
+  const int64_t r = r0 + l;
+  const int64_t lo = a.offsets[r < a.agents ? r : a.agents];
+  const int64_t hi = a.offsets[r + 1 < a.agents ? r + 1 : a.agents];
+  const int64_t E0 = __shfl(lo, 0), E1 = __shfl(hi, 63);  // the wave's contiguous edge range
+  const int64_t n = E1 - E0;
+  double* v = s_v[w];
+  const bool staged = n <= kSegLds;                   // wave-uniform
+  if (staged) {
+    double x[kSegChunks];
+#pragma unroll
+    for (int c = 0; c < kSegChunks; ++c) {           // all loads first, then the LDS stores
+      const int64_t i = c * 64 + l;
+      x[c] = i < n ? exposure_value(a, E0 + i) : 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < kSegChunks; ++c)
+      if (c * 64 < n) v[c * 64 + l] = x[c];
+  }
+  __syncthreads();
+  if (r >= a.agents) return;
+  double s = 0.0;
+  if (staged) {
+    for (int64_t k = lo - E0; k < hi - E0; ++k) s += v[k];
+  } else {  // a wave whose 64 rows hold more than 512 entries: walk them in place
+    for (int64_t e = lo; e < hi; ++e) s += exposure_value(a, e);
+  }
+  a.out[r] = s;
 }
 
 struct ClipArgs {
@@ -175,10 +219,15 @@ T* P(const py::dict& d, const char* k) {
   return reinterpret_cast<T*>(d[k].cast<uintptr_t>());
 }
 
+template <class T>
+T* Popt(const py::dict& d, const char* k) {
+  return d.contains(k) && !d[k].is_none() ? P<T>(d, k) : nullptr;
+}
+
 ExposureArgs to_exposure(const py::dict& d) {
   return ExposureArgs{d["agents"].cast<int64_t>(), d["now_us"].cast<int64_t>(), P<const int64_t>(d, "offsets"),
-                      P<const double>(d, "bonded"), P<const uint8_t>(d, "active"), P<const int64_t>(d, "expiry"),
-                      P<double>(d, "out")};
+                      P<const double>(d, "bonded"), Popt<const uint8_t>(d, "active"),
+                      Popt<const int64_t>(d, "expiry"), P<double>(d, "out"), Popt<const int32_t>(d, "index")};
 }
 
 ClipArgs to_clip(const py::dict& d) {
@@ -206,7 +255,9 @@ void register_global_liability(py::module_& m) {
       [](const py::dict& d, uintptr_t stream) {
         const ExposureArgs a = to_exposure(d);
         py::gil_scoped_release nogil;
-        hipLaunchKernelGGL(agent_exposure_kernel, dim3(grid_for(a.agents)), dim3(256), 0,
+        if (a.agents <= 0) return;
+        const int64_t blocks = (a.agents + 64 * kSegWaves - 1) / (64 * kSegWaves);
+        hipLaunchKernelGGL(agent_exposure_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(64 * kSegWaves), 0,
                            reinterpret_cast<hipStream_t>(stream), a);
         check_hip(hipGetLastError(), "agent_exposure");
       },

@@ -368,6 +368,93 @@ void sigma_eff_csr_host(const VouchCsrArgs& a) {
   for (int64_t i = 0; i < a.sessions * kTile; ++i) sigma_eff_csr_elem(a, i);
 }
 
+
+// Streaming form (the default K03 exact path): a 16-lane group per session (lane
+// j = vouchee j), a wave = 4 consecutive sessions, kStreamSlices such slices per
+// wave, and every load of every slice — edge range, σ, ω, then the first 16
+// edges, one per lane — issued before the first sum, so a wave keeps ~4 KB in
+// flight instead of one dependent round trip at a time (the LDS-staged form
+// above spends half its waves' time on the offsets round trip).  The sum needs
+// no LDS: DPP row_newbcast:u hands edge u of each 16-lane row (= the group) to
+// every lane of the row, so each lane walks its session's edges in creation
+// order and adds the live bonds of its own vouchee — the additions, in the
+// order, of sigma_eff_csr_elem.  Sessions with more than 16 edges walk further
+// chunks in-line (loads on demand).
+constexpr int kStreamSlices = 4;
+constexpr int kStreamWaves = 4;
+constexpr int kStreamSessions = 4 * kStreamSlices * kStreamWaves;  // per 256-thread block
+
+__device__ __forceinline__ uint32_t row_bcast(uint32_t x, int u) {
+  // dpp_ctrl row_newbcast:u = 0x150 + u (must be an immediate: unrolled callers)
+  switch (u) {
+#define AHV_RB(U) case U: return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x150 + U, 0xF, 0xF, false));
+    AHV_RB(0) AHV_RB(1) AHV_RB(2) AHV_RB(3) AHV_RB(4) AHV_RB(5) AHV_RB(6) AHV_RB(7)
+    AHV_RB(8) AHV_RB(9) AHV_RB(10) AHV_RB(11) AHV_RB(12) AHV_RB(13) AHV_RB(14) AHV_RB(15)
+#undef AHV_RB
+    default: return 0u;
+  }
+}
+
+// Creation-order sum over one 16-edge chunk: `key` = the lane's edge vouchee, or
+// 0xff when the edge is dead or absent; (lo, hi) = its bond's words.
+__device__ __forceinline__ double chunk_sum(uint32_t key, uint32_t lo, uint32_t hi, uint32_t j, double acc) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const uint32_t k = row_bcast(key, u);
+    const double b = __hiloint2double(static_cast<int>(row_bcast(hi, u)), static_cast<int>(row_bcast(lo, u)));
+    const double t = acc + b;
+    acc = k == j ? t : acc;
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void stream_edge(const VouchCsrArgs& a, int32_t e, int32_t end, uint32_t& key, double& bd) {
+  key = 0xffu;
+  bd = 0.0;
+  if (e < end) {
+    bd = a.bonded[e];
+    key = live_edge(a.active, a.expiry_us, e, a.now_us) ? a.vouchee[e] : 0xffu;
+  }
+}
+
+__global__ __launch_bounds__(64 * kStreamWaves) void sigma_stream_kernel(VouchCsrArgs a) {
+  const int l = threadIdx.x & 63;
+  const uint32_t j = static_cast<uint32_t>(l & 15);
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * kStreamSessions + (threadIdx.x >> 6) * 4 * kStreamSlices;
+  int32_t lo[kStreamSlices], hi[kStreamSlices];
+  double sig[kStreamSlices], om[kStreamSlices], bd[kStreamSlices];
+  uint32_t key[kStreamSlices];
+#pragma unroll
+  for (int q = 0; q < kStreamSlices; ++q) {
+    const int64_t s = s0 + 4 * q + (l >> 4);
+    const bool in = s < a.sessions;
+    lo[q] = in ? a.offsets[s] : 0;
+    hi[q] = in ? a.offsets[s + 1] : 0;
+    sig[q] = in ? a.sigma[s * kTile + j] : 0.0;
+    om[q] = in ? a.omega[s] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < kStreamSlices; ++q) stream_edge(a, lo[q] + static_cast<int32_t>(j), hi[q], key[q], bd[q]);
+#pragma unroll
+  for (int q = 0; q < kStreamSlices; ++q) {
+    double acc = chunk_sum(key[q], static_cast<uint32_t>(__double2loint(bd[q])),
+                           static_cast<uint32_t>(__double2hiint(bd[q])), j, 0.0);
+    for (int32_t c = lo[q] + 16; c < hi[q]; c += 16) {  // group-uniform: > 16 edges
+      uint32_t k2;
+      double b2;
+      stream_edge(a, c + static_cast<int32_t>(j), hi[q], k2, b2);
+      acc = chunk_sum(k2, static_cast<uint32_t>(__double2loint(b2)), static_cast<uint32_t>(__double2hiint(b2)), j, acc);
+    }
+    const int64_t s = s0 + 4 * q + (l >> 4);
+    if (s < a.sessions) a.sigma_eff[s * kTile + j] = sigma_eff_combine(score_or_zero(sig[q]), om[q], acc);
+  }
+}
+void launch_sigma_eff_stream(const VouchCsrArgs& a, hipStream_t st) {
+  if (a.sessions <= 0) return;
+  hipLaunchKernelGGL(sigma_stream_kernel, grid1(a.sessions, kStreamSessions), dim3(64 * kStreamWaves), 0, st, a);
+  check_hip(hipGetLastError(), "sigma_stream_kernel");
+}
+
 // ------------------------------------------------------------------ K07
 
 AHV_HD void release_elem(const VouchCsrArgs& a, int64_t s) {
@@ -764,54 +851,20 @@ __device__ __forceinline__ double group_sigma_eff(const int (&ve)[kGroupChunks],
   return sigma_eff_combine(score_or_zero(sc), omega, contrib);
 }
 
-__global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_group_kernel(SlashArgs a) {
-  __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
-  const int g = threadIdx.x / kSlashGroup;       // group in block
-  const int j = threadIdx.x % kSlashGroup;       // lane in group
-  const int gw = (threadIdx.x % kWaveLanes) / kSlashGroup;  // group in wave
-  const int gl0 = gw * kSlashGroup;              // first wave lane of the group
-  const int64_t s = static_cast<int64_t>(blockIdx.x) * kSlashGroupsPerBlock + g;
-  if (s >= a.sessions) return;
-  // target and edge range in one memory round trip (the range is 8 bytes per
-  // session; the score row, 128 bytes, is only read for slashed sessions)
-  const uint8_t tgt = a.target[s];
-  const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
-  const bool fused = a.sigma_eff != nullptr;
-  if (tgt >= kTile && !fused) {  // group-uniform: no slash in this session
-    if (j == 0) a.clip_count[s] = 0;
-    return;
-  }
-  if (n > kGroupEdges) {
-    if (j == 0) {
-      slash_session(a, s);
-      if (fused) slash_sigma_row(a, s);
-    }
-    return;
-  }
+// The cascade of one slashed session on its 16-lane group (the edges already in
+// registers: lane j holds edges j, j+16, j+32, j+48): ballots pick the live
+// edges vouching for `who` in creation order, clips read the voucher and its σ by
+// lane shuffle, the walk reads the group's clip list from LDS (`cl`).  Writes the
+// session's scores row, clip records and count; returns the lane's final σ and
+// leaves the released edges dead in `lv`.
+__device__ __forceinline__ double group_cascade(const SlashArgs& a, int64_t s, int tgt, int32_t b, int j, int gl0,
+                                                uint8_t* cl, const int (&vr)[kGroupChunks],
+                                                const int (&ve)[kGroupChunks], bool (&lv)[kGroupChunks], double sc,
+                                                double omega) {
   auto group_bits = [&](bool p) -> uint32_t {
     return static_cast<uint32_t>((__ballot(p) >> gl0) & 0xffffu);
   };
-  int vr[kGroupChunks], ve[kGroupChunks];
-  bool lv[kGroupChunks];
-  double bd[kGroupChunks];
-#pragma unroll
-  for (int c = 0; c < kGroupChunks; ++c) {
-    const int32_t i = c * kSlashGroup + j;
-    const bool in = i < n;
-    vr[c] = in && tgt < kTile ? a.voucher[b + i] : 0;
-    ve[c] = in ? a.vouchee[b + i] : -1;
-    lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
-    bd[c] = in && fused ? a.bonded[b + i] : 0.0;
-  }
-  double sc = a.scores[s * kTile + j];
-  const double omega = a.omega[s];
-  if (tgt >= kTile) {  // fused, no slash here: σ_eff only
-    if (j == 0) a.clip_count[s] = 0;
-    a.sigma_eff[s * kTile + j] = group_sigma_eff(ve, lv, bd, n, j, gl0, sc, omega);
-    return;
-  }
   const int32_t base = a.clip_offsets[s];
-  uint8_t* cl = s_cl[g];
   int32_t nclip = 0;
   static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
   int32_t next0 = 0, end0 = 0, next1 = 0, end1 = 0;
@@ -884,7 +937,112 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
   }
   a.scores[s * kTile + j] = sc;
   if (j == 0) a.clip_count[s] = nclip;
+  return sc;
+}
+
+__global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_group_kernel(SlashArgs a) {
+  __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
+  const int g = threadIdx.x / kSlashGroup;       // group in block
+  const int j = threadIdx.x % kSlashGroup;       // lane in group
+  const int gw = (threadIdx.x % kWaveLanes) / kSlashGroup;  // group in wave
+  const int gl0 = gw * kSlashGroup;              // first wave lane of the group
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kSlashGroupsPerBlock + g;
+  if (s >= a.sessions) return;
+  // target and edge range in one memory round trip (the range is 8 bytes per
+  // session; the score row, 128 bytes, is only read for slashed sessions)
+  const uint8_t tgt = a.target[s];
+  const int32_t b = a.offsets[s], e = a.offsets[s + 1], n = e - b;
+  const bool fused = a.sigma_eff != nullptr;
+  if (tgt >= kTile && !fused) {  // group-uniform: no slash in this session
+    if (j == 0) a.clip_count[s] = 0;
+    return;
+  }
+  if (n > kGroupEdges) {
+    if (j == 0) {
+      slash_session(a, s);
+      if (fused) slash_sigma_row(a, s);
+    }
+    return;
+  }
+  int vr[kGroupChunks], ve[kGroupChunks];
+  bool lv[kGroupChunks];
+  double bd[kGroupChunks];
+#pragma unroll
+  for (int c = 0; c < kGroupChunks; ++c) {
+    const int32_t i = c * kSlashGroup + j;
+    const bool in = i < n;
+    vr[c] = in && tgt < kTile ? a.voucher[b + i] : 0;
+    ve[c] = in ? a.vouchee[b + i] : -1;
+    lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
+    bd[c] = in && fused ? a.bonded[b + i] : 0.0;
+  }
+  double sc = a.scores[s * kTile + j];
+  const double omega = a.omega[s];
+  if (tgt >= kTile) {  // fused, no slash here: σ_eff only
+    if (j == 0) a.clip_count[s] = 0;
+    a.sigma_eff[s * kTile + j] = group_sigma_eff(ve, lv, bd, n, j, gl0, sc, omega);
+    return;
+  }
+  sc = group_cascade(a, s, tgt, b, j, gl0, s_cl[g], vr, ve, lv, sc, omega);
   if (fused) a.sigma_eff[s * kTile + j] = group_sigma_eff(ve, lv, bd, n, j, gl0, sc, omega);
+}
+
+// Split form (default): the cascade runs over the slashed sessions only and the
+// σ_eff of every session is the streaming K03 pass afterwards.  A 256-thread
+// block scans a window of 256 sessions' targets (one coalesced byte per
+// thread), compacts the slashed ones into an LDS list (wave ballots + a 4-entry
+// prefix), writes clip_count 0 for the rest, and its 16 groups take the list
+// round-robin: a group loads its session's edges and score row into registers
+// (lane j: edges j, j+16, j+32, j+48 — all four chunks requested at once), then
+// runs the cascade out of registers, shuffles and its LDS clip list.  A storm
+// over 10 % of the sessions launches one wave per 64 sessions instead of one
+// per 4, and σ_eff no longer waits behind the cascades in the same waves.
+constexpr int kCascWindow = 256;
+
+__global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a) {
+  __shared__ int32_t s_list[kCascWindow];
+  __shared__ int32_t s_wcount[kCascWindow / kWaveLanes];
+  __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
+  const int t = threadIdx.x;
+  const int w = t / kWaveLanes, l = t % kWaveLanes;
+  const int64_t s_me = static_cast<int64_t>(blockIdx.x) * kCascWindow + t;
+  const uint8_t tg = s_me < a.sessions ? a.target[s_me] : 0xff;
+  const bool hit = tg < kTile;
+  if (s_me < a.sessions && !hit) a.clip_count[s_me] = 0;
+  const uint64_t m = __ballot(hit);
+  if (l == 0) s_wcount[w] = __popcll(m);
+  __syncthreads();
+  int pre = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < kCascWindow / kWaveLanes; ++k) {
+    pre += k < w ? s_wcount[k] : 0;
+    total += s_wcount[k];
+  }
+  if (hit) s_list[pre + __popcll(m & ((1ull << l) - 1ull))] = t;
+  __syncthreads();
+  const int g = t / kSlashGroup, j = t % kSlashGroup;
+  const int gl0 = (t % kWaveLanes) / kSlashGroup * kSlashGroup;
+  for (int idx = g; idx < total; idx += kSlashGroupsPerBlock) {  // group-uniform
+    const int64_t s = static_cast<int64_t>(blockIdx.x) * kCascWindow + s_list[idx];
+    const int tgt = a.target[s];
+    const int32_t b = a.offsets[s], n = a.offsets[s + 1] - b;
+    if (n > kGroupEdges) {  // beyond the registers: the one-lane global-memory form
+      if (j == 0) slash_session(a, s);
+      continue;
+    }
+    int vr[kGroupChunks], ve[kGroupChunks];
+    bool lv[kGroupChunks];
+#pragma unroll
+    for (int c = 0; c < kGroupChunks; ++c) {
+      const int32_t i = c * kSlashGroup + j;
+      const bool in = i < n;
+      vr[c] = in ? a.voucher[b + i] : 0;
+      ve[c] = in ? a.vouchee[b + i] : -1;
+      lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
+    }
+    const double sc = a.scores[s * kTile + j];
+    group_cascade(a, s, tgt, b, j, gl0, s_cl[g], vr, ve, lv, sc, a.omega[s]);
+  }
 }
 
 void launch_slash(const SlashArgs& a, hipStream_t st) {
@@ -893,12 +1051,24 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
     const char* e = std::getenv("AHV_SLASH_PER_LANE");
     return e && std::atoi(e) == 1;
   }();
-  if (per_lane) {
+  static const bool fused_group = [] {  // A/B: the round-2 single pass (cascade + σ_eff per group)
+    const char* e = std::getenv("AHV_SLASH_FUSED");
+    return e && std::atoi(e) == 1;
+  }();
+  const int mode = a.mode >= 0 ? a.mode : (per_lane ? 2 : fused_group ? 1 : 0);
+  if (mode == 2) {
     hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
     if (a.sigma_eff) hipLaunchKernelGGL(slash_sigma_kernel, grid1(a.sessions * kTile), dim3(kBlock), 0, st, a);
-  } else {
+  } else if (mode == 1) {
     hipLaunchKernelGGL(slash_group_kernel, grid1(a.sessions, kSlashGroupsPerBlock),
                        dim3(kSlashGroup * kSlashGroupsPerBlock), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(slash_cascade_kernel, grid1(a.sessions, kCascWindow), dim3(kCascWindow), 0, st, a);
+    if (a.sigma_eff) {  // K03 over the post-slash scores and bonds
+      const VouchCsrArgs v{a.sessions, a.now_us, a.offsets, a.voucher, a.vouchee, a.bonded, a.active,
+                           a.expiry_us, a.released_us, nullptr, a.scores, a.omega, a.sigma_eff, nullptr};
+      launch_sigma_eff_stream(v, st);
+    }
   }
   check_hip(hipGetLastError(), "slash_kernel");
 }
@@ -912,6 +1082,8 @@ void slash_host(const SlashArgs& a) {
 
 void kernels_liability(std::vector<KernelEntry>& out) {
   out.push_back({"slash_group_kernel", reinterpret_cast<const void*>(&slash_group_kernel)});
+  out.push_back({"slash_cascade_kernel", reinterpret_cast<const void*>(&slash_cascade_kernel)});
+  out.push_back({"sigma_stream_kernel", reinterpret_cast<const void*>(&sigma_stream_kernel)});
   out.push_back({"slash_kernel", reinterpret_cast<const void*>(&slash_kernel)});
   out.push_back({"sigma_eff_csr_kernel", reinterpret_cast<const void*>(&sigma_eff_csr_kernel)});
   out.push_back({"build_tiles_kernel", reinterpret_cast<const void*>(&build_tiles_kernel)});

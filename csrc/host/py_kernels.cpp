@@ -222,6 +222,8 @@ static SlashArgs to_slash(const py::dict& d) {
   P(clip_after, double); V(clip_cap, int32_t); P(clip_walk, uint8_t);
   a.bonded = d.contains("bonded") ? ptr<const double>(d, "bonded") : nullptr;
   a.sigma_eff = d.contains("sigma_eff") ? ptr<double>(d, "sigma_eff") : nullptr;
+  a.mode = d.contains("mode") ? val<int32_t>(d, "mode") : -1;
+  if (a.mode < -1 || a.mode > 2) throw py::value_error("slash: mode must be -1, 0, 1 or 2");
   return a;
 }
 static RenderArgs to_render(const py::dict& d) {
@@ -338,6 +340,7 @@ void register_kernels(py::module_& m) {
   bind_pair(m, "bond_fused", to_bond_fused, launch_bond_fused, bond_fused_host);
   bind_pair(m, "build_tiles", to_vouch_csr, launch_build_tiles, build_tiles_host);
   bind_pair(m, "sigma_eff_csr", to_vouch_csr, launch_sigma_eff_csr, sigma_eff_csr_host);
+  bind_pair(m, "sigma_eff_stream", to_vouch_csr, launch_sigma_eff_stream, sigma_eff_csr_host);
   bind_pair(m, "release_bonds", to_vouch_csr, launch_release, release_host);
   bind_pair(m, "vouch_admit", to_vouch_admit, launch_vouch_admit, vouch_admit_host);
   bind_pair(m, "slash", to_slash, launch_slash, slash_host);

@@ -209,6 +209,7 @@ struct VouchCsrArgs {
 void launch_build_tiles(const VouchCsrArgs&, hipStream_t);
 void build_tiles_host(const VouchCsrArgs&);
 void launch_sigma_eff_csr(const VouchCsrArgs&, hipStream_t);
+void launch_sigma_eff_stream(const VouchCsrArgs&, hipStream_t);  // same results, streaming form
 void sigma_eff_csr_host(const VouchCsrArgs&);
 void launch_release(const VouchCsrArgs&, hipStream_t);
 void release_host(const VouchCsrArgs&);
@@ -289,6 +290,10 @@ struct SlashArgs {
   // bonds, in the same pass — bit-identical to slash followed by sigma_eff_csr.
   const double* bonded;     // [E]
   double* sigma_eff;        // [S,16] out
+  // Device form: 0 = split (cascade over the slashed sessions, then streaming
+  // K03), 1 = one group pass per session (cascade + σ_eff), 2 = one lane per
+  // session; −1 = AHV_SLASH_FUSED / AHV_SLASH_PER_LANE, else split.
+  int32_t mode = -1;
 };
 void launch_slash(const SlashArgs&, hipStream_t);
 void slash_host(const SlashArgs&);

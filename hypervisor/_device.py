@@ -856,6 +856,7 @@ class DeviceCommitmentEngine(CommitmentEngine):
         super().__init__()
         self._store = store
         self._device: dict[str, DeviceSession] = {}
+        self._batches: list = []  # batched pipelines (store_pipeline._Batch) with committed sessions
 
     def _record(self, sso) -> Optional[CommitmentRecord]:
         x = snapshots(self._store, [sso], parts=True)[0]
@@ -868,13 +869,13 @@ class DeviceCommitmentEngine(CommitmentEngine):
         )
 
     def register(self, sso) -> None:
-        """A committed device session (or a lazy batched one: its row is used)."""
-        sid = sso.session_id if hasattr(sso, "session_id") else sso.row.session_id
-        self._device[sid] = sso
+        """A committed device session."""
+        self._device[sso.session_id] = sso
 
-    def register_many(self, lazy: dict) -> None:
-        """Session id → lazy batched session, for a whole batch at once."""
-        self._device.update(lazy)
+    def register_batch(self, batch) -> None:
+        """The committed sessions of a batched pipeline (``batch.committed``), read
+        from their rows on demand."""
+        self._batches.append(batch)
 
     @staticmethod
     def _row(x):
@@ -886,6 +887,10 @@ class DeviceCommitmentEngine(CommitmentEngine):
         sso = self._device.get(session_id)
         if sso is not None:
             return self._record(self._row(sso))
+        for b in self._batches:
+            i = b.index.get(session_id)
+            if i is not None:
+                return self._record(b.rowref(i)) if b.committed[i] else None
         return super().get_commitment(session_id)
 
     def verify(self, session_id: str, expected_root: str) -> bool:
@@ -896,10 +901,13 @@ class DeviceCommitmentEngine(CommitmentEngine):
     def _commitments_view(self) -> dict[str, CommitmentRecord]:
         out = {}
         ssos = [self._row(x) for x in self._device.values()]
-        for sso, x in zip(ssos, snapshots(self._store, ssos, parts=True)):  # one batched read
+        snaps = snapshots(self._store, ssos, parts=True)  # one batched read per source
+        for b in self._batches:
+            snaps.extend(snapshots_rows(self._store, *b.rows(committed=True), parts=True))
+        for x in snaps:
             if x.committed_at is not None:
-                out[sso.session_id] = CommitmentRecord(
-                    session_id=sso.session_id, merkle_root=x.merkle_root,
+                out[x.session_id] = CommitmentRecord(
+                    session_id=x.session_id, merkle_root=x.merkle_root,
                     participant_dids=[p.agent_did for p in x.participants], delta_count=x.commit_count,
                     committed_at=x.committed_at)
         out.update(self._commitments)
@@ -1170,13 +1178,22 @@ def snapshots(store: GovernanceStore, ssos: list, parts: bool = False) -> list[S
     """Snapshots of many device sessions with O(1) store commands (OP_SESS_READ_MANY)."""
     if not ssos:
         return []
-    hdr, prt = store.read_sessions([x.slot for x in ssos], parts=parts)
+    return snapshots_rows(store, [x.slot for x in ssos], [x.session_id for x in ssos],
+                          [x.creator_did for x in ssos], parts)
+
+
+def snapshots_rows(store: GovernanceStore, slots, ids: list, creators: list,
+                   parts: bool = False) -> list[SessionSnapshot]:
+    """:func:`snapshots` from row arrays (slot, session id, creator DID per row)."""
+    if not len(ids):
+        return []
+    hdr, prt = store.read_sessions(slots, parts=parts)
     out = []
-    for i, sso in enumerate(ssos):
+    for i, sid in enumerate(ids):
         h = hdr[i]
         s = SessionSnapshot()
         w0 = int(h[0])
-        s.session_id = sso.session_id
+        s.session_id = sid
         s.state = _STATES[w0 & 0xFF]
         s.consistency_mode = _MODES[(w0 >> 8) & 0xFF]
         w1 = int(h[1])
@@ -1186,7 +1203,7 @@ def snapshots(store: GovernanceStore, ssos: list, parts: bool = False) -> list[S
         te = _i64(int(h[3]))
         s.terminated_at = from_us(te) if te else None
         s.delta_count = int(h[4]) & 0xFFFFFFFF
-        s.creator_did = sso.creator_did
+        s.creator_did = creators[i]
         c = _i64(int(h[7]))
         s.committed_at = from_us(c) if c else None
         s.commit_count = (int(h[4]) >> 32) & 0xFFFFFFFF

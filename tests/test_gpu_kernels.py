@@ -386,3 +386,85 @@ def test_spread_fold(cuda_device):
     torch.cuda.synchronize()
     assert out.cpu().tolist() == rows.sum(0).tolist()
     assert int(sc.buf.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("S,lo,hi", [(4099, 0, 40), (300, 0, 90), (7, 0, 3)])
+def test_slash_forms_and_sigma_kernels_agree(cuda_device, S, lo, hi):
+    """Round-3 split slash (cascade over the slashed sessions only + streaming
+    K03) == the round-2 group pass == the per-lane form == the host twin, bit for
+    bit (scores, releases, clip records, σ_eff), on storms over a session subset
+    with ragged, multi-chunk (> 16) and > 64-edge sessions; both K03 device
+    kernels (stream, csr) equal the host twin."""
+    vb = _vouch_batch(S, 31 + S, lo=lo, hi=hi)
+    fields = list(vb.__dataclass_fields__)
+    g = torch.Generator().manual_seed(S)
+    sigma = torch.rand((S, 16), dtype=f64, generator=g)
+    sigma[sigma < 0.05] = float("nan")
+    omega = torch.rand(S, dtype=f64, generator=g)
+    host = LI.sigma_eff_exact(vb, sigma, omega, 100)
+    vd = vb.to("cuda")
+    for k in ("stream", "csr"):
+        assert torch.equal(LI.sigma_eff_exact(vd, sigma.cuda(), omega.cuda(), 100, kernel=k).cpu(), host), k
+    tgt = torch.randint(0, 16, (S,), dtype=u8, generator=g)
+    tgt[torch.rand(S, generator=g) < 0.6] = 255
+    scores = torch.rand((S, 16), dtype=f64, generator=g)
+    scores[scores < 0.1] = float("nan")
+    vh = LI.VouchBatch(*[getattr(vb, f).clone() for f in fields])
+    want = LI.slash(vh, tgt, omega, scores.clone(), 100, clip_cap=64, with_sigma_eff=True)
+    for mode in ("split", "group", "lane"):
+        for fused in (True, False):
+            v = vb.to("cuda")
+            got = LI.slash(v, tgt.cuda(), omega.cuda(), scores.cuda(), 100, clip_cap=64, with_sigma_eff=fused,
+                           mode=mode)
+            torch.cuda.synchronize()
+            assert torch.equal(got.clip_count.cpu(), want.clip_count), mode
+            assert torch.equal(got.scores.cpu().nan_to_num(7.0), want.scores.nan_to_num(7.0)), mode
+            assert torch.equal(v.active.cpu(), vh.active) and torch.equal(v.released_us.cpu(), vh.released_us)
+            n = want.clip_count.clamp(max=64)
+            for s in torch.nonzero(n).flatten().tolist()[:400]:
+                k = int(n[s])
+                for f in ("clip_voucher", "clip_depth", "clip_before", "clip_after"):
+                    assert torch.equal(getattr(got, f)[s, :k].cpu(), getattr(want, f)[s, :k]), (mode, f, s)
+            if fused:
+                assert torch.equal(got.sigma_eff.cpu(), want.sigma_eff), mode
+
+
+@pytest.mark.parametrize("degree_hi", [6, 40])
+def test_agent_exposure_segmented_and_gather(cuda_device, degree_hi):
+    """K04 agent form: the segmented LDS reduction (and its > 512-entries-per-wave
+    in-place walk) == the host twin bit for bit; the AgentIndex gather of the
+    fused MFMA rows == a session-order sum of the host rows (no atomics)."""
+    from agent_hypervisor_amd.ops.global_liability import ResidentBonds
+
+    A = 20_000
+    rb = ResidentBonds(A, 4, "cpu", seed=3)
+    rng = torch.Generator().manual_seed(degree_hi)
+    deg = torch.randint(0, degree_hi, (A,), generator=rng)
+    E = int(deg.sum())
+    rb.offsets = torch.zeros(A + 1, dtype=i64)
+    rb.offsets[1:] = torch.cumsum(deg, 0)
+    rb.bonded = torch.rand(E, dtype=f64, generator=rng)
+    rb.active = (torch.rand(E, generator=rng) < 0.8).to(u8)
+    rb.expiry = torch.where(torch.rand(E, generator=rng) < 0.2, 50, -1).to(i64)
+    rb.agents, rb.edges = A, E
+    host = rb.exposure(torch.empty(A, dtype=f64), now_us=100)
+    for f in ("offsets", "bonded", "active", "expiry"):
+        setattr(rb, f, getattr(rb, f).cuda())
+    dev = rb.exposure(torch.empty(A, dtype=f64, device="cuda"), now_us=100)
+    assert torch.equal(dev.cpu(), host)
+    S = 3000
+    vb = _vouch_batch(S, 5, lo=0, hi=20)
+    sigma = torch.rand((S, 16), dtype=f64, generator=rng)
+    omega = torch.rand(S, dtype=f64, generator=rng)
+    members = torch.randint(0, 500, (S, 16), generator=rng)
+    idx = LI.agent_index(vb, members, 500)
+    _, h_ex, _ = LI.bond_fused(vb, sigma, omega, 100)
+    hx = LI.agent_gather(idx, h_ex, torch.empty(500, dtype=f64))
+    vd = vb.to("cuda")
+    didx = LI.agent_index(vd, members.cuda(), 500)
+    assert torch.equal(didx.offsets.cpu(), idx.offsets) and torch.equal(didx.index.cpu(), idx.index)
+    dx = torch.empty(500, dtype=f64, device="cuda")
+    _, d_ex, _ = LI.bond_fused(vd, sigma.cuda(), omega.cuda(), 100, agent_exposure=dx, agent_idx=didx)
+    assert torch.equal(LI.agent_gather(didx, d_ex, torch.empty(500, dtype=f64, device="cuda")).cpu(),
+                       LI.agent_gather(idx, d_ex.cpu(), torch.empty(500, dtype=f64)))
+    torch.testing.assert_close(dx.cpu(), hx, rtol=1e-12, atol=1e-12)

@@ -654,3 +654,40 @@ def test_render_rows_stamps_and_hex():
     assert int(rows[1].sum()) == 0 and int(rows[3].sum()) == 0  # rows not listed stay untouched
     with pytest.raises(ValueError):
         A.render_rows(out, tmpl, torch.tensor([5]), stamps=[(p_id, 7, 0, 0)])
+
+
+def test_agent_gather_is_session_order_sum_of_voucher_rows():
+    """X01 input without atomics: AgentIndex lists each agent's voucher slots in
+    session order, and the segmented reduction adds their exposure rows in that
+    order (members that vouch for nobody carry 0 and are skipped)."""
+    import random
+
+    rng = random.Random(4)
+    S, A = 200, 60
+    offs, vr, ve = [0], [], []
+    for _ in range(S):
+        for _ in range(rng.randint(0, 12)):
+            a, b = rng.sample(range(16), 2)
+            vr.append(a)
+            ve.append(b)
+        offs.append(len(vr))
+    E = len(vr)
+    vb = LI.VouchBatch(torch.tensor(offs, dtype=torch.int32), torch.tensor(vr, dtype=torch.uint8),
+                       torch.tensor(ve, dtype=torch.uint8), torch.rand(E, dtype=torch.float64),
+                       torch.ones(E, dtype=torch.uint8), torch.full((E,), -1, dtype=torch.int64),
+                       torch.zeros(E, dtype=torch.int64))
+    members = torch.randint(0, A, (S, 16), generator=torch.Generator().manual_seed(2))
+    sigma = torch.rand((S, 16), dtype=torch.float64)
+    omega = torch.rand(S, dtype=torch.float64)
+    idx = LI.agent_index(vb, members, A)
+    out = torch.empty(A, dtype=torch.float64)
+    _, ex, _ = LI.bond_fused(vb, sigma, omega, 0, agent_exposure=out, agent_idx=idx)
+    want = [0.0] * A
+    for s in range(S):
+        vouchers = sorted({vr[k] for k in range(offs[s], offs[s + 1])})
+        for j in vouchers:
+            want[int(members[s, j])] += float(ex[s, j])
+    assert out.tolist() == want
+    legacy = torch.zeros(A, dtype=torch.float64)  # the atomic form adds every member's row
+    LI.bond_fused(vb, sigma, omega, 0, members=members, agent_exposure=legacy)
+    torch.testing.assert_close(legacy, out, rtol=1e-12, atol=1e-15)

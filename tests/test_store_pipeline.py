@@ -120,7 +120,7 @@ def check_randomized(device: str, n: int, seed: int = 3) -> None:
     try:
         run = asyncio.run(hv.run_pipelines(specs))
         assert run.status.shape == (n,)
-        t0 = int(hv._sessions[run.session_ids[0]]._batch.t0)
+        t0 = int(hv._sessions.batch_of(run.session_ids[0]).t0)
         ref = Hypervisor(device="host")
         check = range(n) if n <= 2000 else rng.sample(range(n), 2000)
         jpos = [0]
@@ -184,7 +184,6 @@ def test_lazy_rows_released_in_bulk_and_materialized_rows_kept(monkeypatch):
     assert all(len(m.delta_engine.deltas) == 3 for m in keep)  # materialized: they own their rows
     for sid in run.session_ids[5:25]:  # dropped one by one: released every _FLUSH
         hv._sessions.pop(sid)
-        hv.commitment._device.pop(sid, None)
     gc.collect()
     st.reclaim()
     assert st.live_rows()["S"] == base["S"] + 40 - 14  # two flushes of 7; 6 wait for the batch
