@@ -5,20 +5,20 @@ fan-out policy (K15).
 :meth:`hypervisor.saga.fan_out.FanOutOrchestrator.execute_groups` with a
 ``device`` land here.  The split of work:
 
-* **host** — awaits the user's executor / compensator coroutines, concurrently
-  across sagas (``asyncio.gather``), step by step in each saga's order: step k
-  runs only in sagas whose steps < k committed, compensations walk committed
-  steps in reverse — exactly the calls the reference orchestrator makes
-  (saga/orchestrator.py:77-198).  Each step's outcome is reduced to the FSM's
-  inputs: failing attempts before success (255 = never), the last failure's
-  kind (exception / timeout), the compensation outcome, Undo_API presence and
-  max_retries;
-* **device** — one replay of the hipGraph-captured step loop (init, K ×
-  execute, decide, K × compensate, finish; :class:`SagaBatchEngine`) turns
-  those tables into every step/saga state, retry count, error code, transition
-  timestamp and the batch counters.  The graph is captured once per (sagas,
-  steps) shape and replayed for every later batch: outcomes are loaded into
-  persistent buffers and the time base is a device scalar.
+* **device** — the saga state machine (K13/K14 phase kernels of
+  :class:`SagaBatchEngine`) decides what runs: after the execute phase of step
+  k it reports which sagas committed step k (those, and only those, run step
+  k+1); after the decide phase, which committed steps of which sagas are
+  compensated, round by round in reverse step order.  Every state, retry count,
+  error code, transition timestamp and the batch counters are device state;
+* **host** — awaits exactly the executor / compensator coroutines the device
+  asked for, all sagas of a round at once: a coroutine that finishes without
+  suspending (the common case) is driven inline, the rest run concurrently
+  under ``asyncio.gather`` with the reference's deadline, retry and delay
+  semantics (saga/orchestrator.py:77-198).  Each step's outcome is reduced to
+  the FSM's inputs — failing attempts before success (255 = never), the last
+  failure's kind (exception / timeout), the compensation outcome — and uploaded
+  as one row per round.
 
 The resulting states are written back into the orchestrator's ``Saga`` /
 ``SagaStep`` objects; host-only payloads (executor results, exception texts)
@@ -51,6 +51,37 @@ from hypervisor.saga._timeout import await_with_timeout, resume_with_deadline
 
 u8 = torch.uint8
 _KIND_EXC, _KIND_TIMEOUT = 1, 2
+_ST_COMMITTED = STEP_NAMES.index("committed")
+_SG_RUNNING, _SG_COMPENSATING = SAGA_NAMES.index("running"), SAGA_NAMES.index("compensating")
+
+
+class _Resume:
+    """Awaitable continuing a coroutine already started with ``send(None)``."""
+
+    __slots__ = ("coro", "first")
+
+    def __init__(self, coro, first) -> None:
+        self.coro, self.first = coro, first
+
+    def __await__(self):
+        coro, y = self.coro, self.first
+        while True:
+            try:
+                x = yield y
+            except BaseException as e:  # noqa: BLE001 - thrown into the coroutine (cancellation)
+                try:
+                    y = coro.throw(e)
+                except StopIteration as stop:
+                    return stop.value
+            else:
+                try:
+                    y = coro.send(x)
+                except StopIteration as stop:
+                    return stop.value
+
+
+def _resume(coro, first):
+    return _Resume(coro, first)
 
 
 class SagaBatchRunner:
@@ -93,39 +124,64 @@ class SagaBatchRunner:
     async def _run_group(self, orch, sagas, K, executors, compensator, compensate) -> list[int]:
         S = len(sagas)
         delay = float(orch.DEFAULT_RETRY_DELAY_SECONDS)
-        # outcome tables filled element-wise on the host: flat bytearrays (row s·K + k),
-        # turned into tensors once
-        fa, fk, cf = bytearray(S * K), bytearray(S * K), bytearray(S * K)
-        hu = bytearray(1 if st.undo_api else 0 for sg in sagas for st in sg.steps)
-        mr = bytearray(min(int(st.max_retries), 254) for sg in sagas for st in sg.steps)
+        rows = [sg.steps for sg in sagas]
+        hu = bytearray(1 if st.undo_api else 0 for row in rows for st in row)
+        mr = bytearray(min(int(st.max_retries), 254) for row in rows for st in row)
         results: dict[tuple[int, int], Any] = {}
         errors: dict[tuple[int, int], str] = {}
         comp_results: dict[tuple[int, int], Any] = {}
         comp_errors: dict[tuple[int, int], str] = {}
-
         loop = asyncio.get_running_loop()
 
-        async def attempts(s: int, k: int):
-            st = sagas[s].steps[k]
+        # device state machine, driven phase by phase: the outcome rows of step k
+        # are uploaded just before its execute phase, and after it the device
+        # says which sagas run step k+1
+        eng = self.engine(S, K, compensate)
+        zero = bytearray(S * K)
+        tab = lambda b: torch.frombuffer(b, dtype=u8).view(S, K)  # noqa: E731
+        handle = eng.load_outcomes(SagaOutcomes(tab(zero), tab(zero), tab(zero), tab(hu), tab(mr)))
+        prep = eng._prepared(handle)  # [K, S] rows the phase kernels read
+        now = _clock.now_us()
+        args = eng._args(handle, now)
+        eng.now_dev.fill_(now)
+        eng._spread.begin()
+        eng._phase(args, 0)
+
+        def upload(name: str, k: int, row: bytearray) -> None:
+            prep[name][k].copy_(torch.frombuffer(row, dtype=u8))
+
+        async def attempts(s: int, k: int, fa_row: bytearray, fk_row: bytearray, at0: int = 0,
+                           started=None, first=None) -> None:
+            """Attempts ``at0``… of step k of saga s with full await semantics
+            (suspending executors, deadlines, retry delays).  ``started``: the
+            (coroutine, first yield) of attempt ``at0``, already begun inline;
+            ``first``: what the executor returned for attempt ``at0`` when that
+            was not a coroutine."""
+            st = rows[s][k]
             n = 1 + int(st.max_retries)
             fn = executors[st.step_id]
             tmo = st.timeout_seconds
             kind, err = 0, None
-            for at in range(n):
+            for at in range(at0, n):
                 try:
-                    c = fn()
-                    if type(c) is CoroutineType and tmo is not None and tmo > 0:
-                        # started inline: a coroutine that finishes without suspending
-                        # needs no deadline timer (await_with_timeout semantics otherwise)
-                        when = loop.time() + tmo
-                        try:
-                            y = c.send(None)
-                        except StopIteration as e:
-                            res = e.value
-                        else:
-                            res = await resume_with_deadline(c, y, when)
+                    if started is not None:
+                        c, y = started
+                        started = None
+                        res = await (resume_with_deadline(c, y, loop.time() + tmo) if tmo is not None and tmo > 0
+                                     else _resume(c, y))
                     else:
-                        res = await await_with_timeout(c, tmo)
+                        c = fn() if first is None else first
+                        first = None
+                        if type(c) is CoroutineType and tmo is not None and tmo > 0:
+                            when = loop.time() + tmo
+                            try:
+                                y = c.send(None)
+                            except StopIteration as e:
+                                res = e.value
+                            else:
+                                res = await resume_with_deadline(c, y, when)
+                        else:
+                            res = await await_with_timeout(c, tmo)
                 except asyncio.TimeoutError:
                     kind = _KIND_TIMEOUT
                     err = f"Step {st.step_id} timed out after {st.timeout_seconds}s (attempt {at + 1}/{n})"
@@ -133,51 +189,84 @@ class SagaBatchRunner:
                     kind, err = _KIND_EXC, str(e)
                 else:
                     results[(s, k)] = res
-                    return at, 0
+                    fa_row[s] = at
+                    return
                 if at < n - 1:
                     await asyncio.sleep(delay * (at + 1))
             errors[(s, k)] = err
-            return NEVER, kind
+            fa_row[s], fk_row[s] = NEVER, kind
 
-        failed_at: dict[int, int] = {}
+        def inline(s: int, k: int, fa_row: bytearray, fk_row: bytearray):
+            """Run step k of saga s here if its executor never suspends (the
+            common case); returns None when done, else the coroutine finishing it."""
+            st = rows[s][k]
+            n = 1 + int(st.max_retries)
+            fn = executors[st.step_id]
+            err = None
+            for at in range(n):
+                try:
+                    c = fn()
+                    if type(c) is not CoroutineType:  # other awaitables (or none): the full path
+                        return attempts(s, k, fa_row, fk_row, at, first=c)
+                    try:
+                        y = c.send(None)
+                    except StopIteration as e:
+                        results[(s, k)] = e.value
+                        fa_row[s] = at
+                        return None
+                    return attempts(s, k, fa_row, fk_row, at, (c, y))
+                except Exception as e:  # raised before suspending: a failed attempt
+                    err = str(e)
+                if at < n - 1 and delay > 0:
+                    return attempts(s, k, fa_row, fk_row, at + 1)  # the retry waits its delay
+            errors[(s, k)] = err
+            fa_row[s], fk_row[s] = NEVER, _KIND_EXC
+            return None
 
-        async def forward(s: int) -> None:  # the saga's steps in order, until one fails
-            for k in range(K):
-                nf, kind = await attempts(s, k)
-                fa[s * K + k], fk[s * K + k] = nf, kind
-                if nf == NEVER:
-                    failed_at[s] = k
-                    return
-
-        await asyncio.gather(*(forward(s) for s in range(S)))  # sagas run concurrently
-        if compensate and failed_at:
+        runnable = list(range(S))
+        for k in range(K):
+            fa_row, fk_row = bytearray(S), bytearray(S)
+            slow = [c for c in (inline(s, k, fa_row, fk_row) for s in runnable) if c is not None]
+            if slow:
+                await asyncio.gather(*slow)  # suspending executors: concurrently, across sagas
+            upload("fail_attempts", k, fa_row)
+            upload("fail_kind", k, fk_row)
+            eng._phase(args, 1, k)
+            if k + 1 < K:  # the device picks the sagas whose step k committed
+                runnable = torch.nonzero((eng._step_state[k] == _ST_COMMITTED)
+                                         & (eng.saga_state == _SG_RUNNING)).flatten().tolist()
+                if not runnable:
+                    break
+        eng._phase(args, 2)
+        if compensate and bool((eng.saga_state == _SG_COMPENSATING).any()):
             if compensator is None:
                 raise ValueError("compensate=True needs a compensator")
+            has_undo = prep["has_undo"]
 
-            async def comp(s: int, k: int) -> int:
-                st = sagas[s].steps[k]
+            async def comp(s: int, k: int, cf_row: bytearray) -> None:
+                st = rows[s][k]
                 try:
                     res = await await_with_timeout(compensator(st), st.timeout_seconds)
                 except asyncio.TimeoutError:
                     comp_errors[(s, k)] = f"Compensation timed out after {st.timeout_seconds}s"
-                    return _KIND_TIMEOUT
+                    cf_row[s] = _KIND_TIMEOUT
+                    return
                 except Exception as e:
                     comp_errors[(s, k)] = f"Compensation failed: {e}"
-                    return _KIND_EXC
+                    cf_row[s] = _KIND_EXC
+                    return
                 comp_results[(s, k)] = res
-                return 0
 
-            async def backward(s: int, f: int) -> None:  # committed steps in reverse order
-                for k in range(f - 1, -1, -1):
-                    if hu[s * K + k]:
-                        cf[s * K + k] = await comp(s, k)
-
-            await asyncio.gather(*(backward(s, f) for s, f in failed_at.items()))
-        # device FSM: one replay of the captured step loop over the gathered outcomes
-        eng = self.engine(S, K, compensate)
-        tab = lambda b: torch.frombuffer(b, dtype=u8).view(S, K)  # noqa: E731
-        handle = eng.load_outcomes(SagaOutcomes(tab(fa), tab(fk), tab(cf), tab(hu), tab(mr)))
-        stats = eng.run_step_loop(handle, now_us=_clock.now_us(), graph=True)
+            for k in range(K - 1, -1, -1):  # committed steps in reverse order, all sagas at once
+                todo = torch.nonzero((eng.saga_state == _SG_COMPENSATING) & (eng._step_state[k] == _ST_COMMITTED)
+                                     & (has_undo[k] != 0)).flatten().tolist()
+                if todo:
+                    cf_row = bytearray(S)
+                    await asyncio.gather(*(comp(s, k, cf_row) for s in todo))
+                    upload("comp_fail", k, cf_row)
+                eng._phase(args, 3, k)  # also fails the committed steps without an Undo_API
+        eng._phase(args, 4)
+        stats = eng._spread.copy_into(eng.stats)
         self._write_back(eng, sagas, results, errors, comp_results, comp_errors)
         return [int(x) for x in stats.cpu().tolist()]
 

@@ -12,6 +12,7 @@
 // path agrees to within an ulp-level tolerance while `sigma_eff_csr` (one lane
 // per vouchee, creation order) is the bit-exact path.
 #include <cstdlib>
+#include <string>
 
 #include "ahv/kernels.h"
 #include "ahv/launch.h"
@@ -380,9 +381,7 @@ void sigma_eff_csr_host(const VouchCsrArgs& a) {
 // order and adds the live bonds of its own vouchee — the additions, in the
 // order, of sigma_eff_csr_elem.  Sessions with more than 16 edges walk further
 // chunks in-line (loads on demand).
-constexpr int kStreamSlices = 4;
 constexpr int kStreamWaves = 4;
-constexpr int kStreamSessions = 4 * kStreamSlices * kStreamWaves;  // per 256-thread block
 
 __device__ __forceinline__ uint32_t row_bcast(uint32_t x, int u) {
   // dpp_ctrl row_newbcast:u = 0x150 + u (must be an immediate: unrolled callers)
@@ -417,7 +416,9 @@ __device__ __forceinline__ void stream_edge(const VouchCsrArgs& a, int32_t e, in
   }
 }
 
+template <int kStreamSlices>
 __global__ __launch_bounds__(64 * kStreamWaves) void sigma_stream_kernel(VouchCsrArgs a) {
+  constexpr int kStreamSessions = 4 * kStreamSlices * kStreamWaves;  // per 256-thread block
   const int l = threadIdx.x & 63;
   const uint32_t j = static_cast<uint32_t>(l & 15);
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * kStreamSessions + (threadIdx.x >> 6) * 4 * kStreamSlices;
@@ -449,9 +450,20 @@ __global__ __launch_bounds__(64 * kStreamWaves) void sigma_stream_kernel(VouchCs
     if (s < a.sessions) a.sigma_eff[s * kTile + j] = sigma_eff_combine(score_or_zero(sig[q]), om[q], acc);
   }
 }
+template <int K>
+void launch_stream_k(const VouchCsrArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(sigma_stream_kernel<K>, grid1(a.sessions, 4 * K * kStreamWaves), dim3(64 * kStreamWaves), 0, st, a);
+}
 void launch_sigma_eff_stream(const VouchCsrArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
-  hipLaunchKernelGGL(sigma_stream_kernel, grid1(a.sessions, kStreamSessions), dim3(64 * kStreamWaves), 0, st, a);
+  static const int slices = [] {  // sessions per wave / 4 (A/B: AHV_STREAM_SLICES = 1, 2, 4)
+    const char* e = std::getenv("AHV_STREAM_SLICES");
+    const int k = e ? std::atoi(e) : 2;
+    return k == 1 || k == 4 ? k : 2;
+  }();
+  if (slices == 1) launch_stream_k<1>(a, st);
+  else if (slices == 4) launch_stream_k<4>(a, st);
+  else launch_stream_k<2>(a, st);
   check_hip(hipGetLastError(), "sigma_stream_kernel");
 }
 
@@ -989,26 +1001,39 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
 
 // Split form (default): the cascade runs over the slashed sessions only and the
 // σ_eff of every session is the streaming K03 pass afterwards.  A 256-thread
-// block scans a window of 256 sessions' targets (one coalesced byte per
-// thread), compacts the slashed ones into an LDS list (wave ballots + a 4-entry
-// prefix), writes clip_count 0 for the rest, and its 16 groups take the list
-// round-robin: a group loads its session's edges and score row into registers
-// (lane j: edges j, j+16, j+32, j+48 — all four chunks requested at once), then
-// runs the cascade out of registers, shuffles and its LDS clip list.  A storm
-// over 10 % of the sessions launches one wave per 64 sessions instead of one
-// per 4, and σ_eff no longer waits behind the cascades in the same waves.
+// block owns a window of 256 sessions:
+//   1. one coalesced round trip reads the window's targets and edge offsets
+//      (offsets into LDS); the rest get clip_count 0; wave ballots + a 4-entry
+//      prefix compact the slashed sessions into an LDS list;
+//   2. one round trip stages up to kCascStage listed sessions at once — thread
+//      (entry q, lane j) loads edges j, j+16, j+32, j+48 of entry q (voucher,
+//      vouchee, liveness), its σ[j] and ω — every load issued before the first
+//      LDS store;
+//   3. the 16 groups run the staged cascades (≤ 2 each) out of LDS, registers
+//      and lane shuffles — no global load on the cascade's critical path.
+// A storm over 10 % of the sessions launches one wave per 64 sessions instead
+// of one per 4, and σ_eff no longer waits behind cascades in the same waves.
 constexpr int kCascWindow = 256;
+constexpr int kCascStage = 32;  // listed sessions staged per round (two per group)
 
 __global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a) {
   __shared__ int32_t s_list[kCascWindow];
+  __shared__ int32_t s_off[kCascWindow + 1];
   __shared__ int32_t s_wcount[kCascWindow / kWaveLanes];
+  __shared__ uint8_t s_vr[kCascStage][kGroupEdges], s_ve[kCascStage][kGroupEdges], s_lv[kCascStage][kGroupEdges];
+  __shared__ double s_sc[kCascStage][kTile];
+  __shared__ double s_om[kCascStage];
   __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
   const int t = threadIdx.x;
   const int w = t / kWaveLanes, l = t % kWaveLanes;
-  const int64_t s_me = static_cast<int64_t>(blockIdx.x) * kCascWindow + t;
-  const uint8_t tg = s_me < a.sessions ? a.target[s_me] : 0xff;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kCascWindow;
+  const int64_t s_me = w0 + t;
+  const bool in_range = s_me < a.sessions;
+  const uint8_t tg = in_range ? a.target[s_me] : 0xff;
+  s_off[t] = a.offsets[in_range ? s_me : a.sessions];
+  if (t == kCascWindow - 1) s_off[kCascWindow] = a.offsets[s_me + 1 < a.sessions ? s_me + 1 : a.sessions];
   const bool hit = tg < kTile;
-  if (s_me < a.sessions && !hit) a.clip_count[s_me] = 0;
+  if (in_range && !hit) a.clip_count[s_me] = 0;
   const uint64_t m = __ballot(hit);
   if (l == 0) s_wcount[w] = __popcll(m);
   __syncthreads();
@@ -1022,26 +1047,63 @@ __global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a)
   __syncthreads();
   const int g = t / kSlashGroup, j = t % kSlashGroup;
   const int gl0 = (t % kWaveLanes) / kSlashGroup * kSlashGroup;
-  for (int idx = g; idx < total; idx += kSlashGroupsPerBlock) {  // group-uniform
-    const int64_t s = static_cast<int64_t>(blockIdx.x) * kCascWindow + s_list[idx];
-    const int tgt = a.target[s];
-    const int32_t b = a.offsets[s], n = a.offsets[s + 1] - b;
-    if (n > kGroupEdges) {  // beyond the registers: the one-lane global-memory form
-      if (j == 0) slash_session(a, s);
-      continue;
-    }
-    int vr[kGroupChunks], ve[kGroupChunks];
-    bool lv[kGroupChunks];
+  constexpr int kPasses = kCascStage / kSlashGroupsPerBlock;  // entries staged per thread
+  for (int base = 0; base < total; base += kCascStage) {  // block-uniform
+    const int m_here = total - base < kCascStage ? total - base : kCascStage;
+    // 2. stage: all loads of both passes first
+    uint8_t vr[kPasses][kGroupChunks], ve[kPasses][kGroupChunks], lv[kPasses][kGroupChunks];
+    double sc[kPasses], om[kPasses];
 #pragma unroll
-    for (int c = 0; c < kGroupChunks; ++c) {
-      const int32_t i = c * kSlashGroup + j;
-      const bool in = i < n;
-      vr[c] = in ? a.voucher[b + i] : 0;
-      ve[c] = in ? a.vouchee[b + i] : -1;
-      lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
+    for (int p = 0; p < kPasses; ++p) {
+      const int q = p * kSlashGroupsPerBlock + g;
+      const int ls = q < m_here ? s_list[base + q] : 0;
+      const int32_t b = s_off[ls], n = q < m_here ? s_off[ls + 1] - b : 0;
+      const bool small = n <= kGroupEdges;
+#pragma unroll
+      for (int c = 0; c < kGroupChunks; ++c) {
+        const int32_t i = c * kSlashGroup + j;
+        const bool in = small && i < n;
+        vr[p][c] = in ? a.voucher[b + i] : 0;
+        ve[p][c] = in ? a.vouchee[b + i] : 0xff;
+        lv[p][c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us) ? 1 : 0;
+      }
+      sc[p] = q < m_here && small ? a.scores[(w0 + ls) * kTile + j] : 0.0;
+      om[p] = q < m_here ? a.omega[w0 + ls] : 0.0;
     }
-    const double sc = a.scores[s * kTile + j];
-    group_cascade(a, s, tgt, b, j, gl0, s_cl[g], vr, ve, lv, sc, a.omega[s]);
+#pragma unroll
+    for (int p = 0; p < kPasses; ++p) {
+      const int q = p * kSlashGroupsPerBlock + g;
+#pragma unroll
+      for (int c = 0; c < kGroupChunks; ++c) {
+        s_vr[q][c * kSlashGroup + j] = vr[p][c];
+        s_ve[q][c * kSlashGroup + j] = ve[p][c];
+        s_lv[q][c * kSlashGroup + j] = lv[p][c];
+      }
+      s_sc[q][j] = sc[p];
+      if (j == 0) s_om[q] = om[p];
+    }
+    __syncthreads();
+    // 3. cascades out of LDS/registers (group-uniform loop)
+    for (int q = g; q < m_here; q += kSlashGroupsPerBlock) {
+      const int ls = s_list[base + q];
+      const int64_t s = w0 + ls;
+      const int32_t b = s_off[ls], n = s_off[ls + 1] - b;
+      if (n > kGroupEdges) {  // beyond the staging rows: the one-lane global-memory form
+        if (j == 0) slash_session(a, s);
+        continue;
+      }
+      int rvr[kGroupChunks], rve[kGroupChunks];
+      bool rlv[kGroupChunks];
+#pragma unroll
+      for (int c = 0; c < kGroupChunks; ++c) {
+        const int i = c * kSlashGroup + j;
+        rvr[c] = s_vr[q][i];
+        rve[c] = i < n ? static_cast<int>(s_ve[q][i]) : -1;
+        rlv[c] = s_lv[q][i] != 0;
+      }
+      group_cascade(a, s, a.target[s], b, j, gl0, s_cl[g], rvr, rve, rlv, s_sc[q][j], s_om[q]);
+    }
+    __syncthreads();  // the next round overwrites the staging rows
   }
 }
 
@@ -1065,9 +1127,14 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
   } else {
     hipLaunchKernelGGL(slash_cascade_kernel, grid1(a.sessions, kCascWindow), dim3(kCascWindow), 0, st, a);
     if (a.sigma_eff) {  // K03 over the post-slash scores and bonds
+      static const bool csr = [] {  // A/B: AHV_SLASH_SIGMA=csr runs the LDS-staged K03 form
+        const char* e = std::getenv("AHV_SLASH_SIGMA");
+        return e && std::string(e) == "csr";
+      }();
       const VouchCsrArgs v{a.sessions, a.now_us, a.offsets, a.voucher, a.vouchee, a.bonded, a.active,
                            a.expiry_us, a.released_us, nullptr, a.scores, a.omega, a.sigma_eff, nullptr};
-      launch_sigma_eff_stream(v, st);
+      if (csr) launch_sigma_eff_csr(v, st);
+      else launch_sigma_eff_stream(v, st);
     }
   }
   check_hip(hipGetLastError(), "slash_kernel");
@@ -1083,7 +1150,7 @@ void slash_host(const SlashArgs& a) {
 void kernels_liability(std::vector<KernelEntry>& out) {
   out.push_back({"slash_group_kernel", reinterpret_cast<const void*>(&slash_group_kernel)});
   out.push_back({"slash_cascade_kernel", reinterpret_cast<const void*>(&slash_cascade_kernel)});
-  out.push_back({"sigma_stream_kernel", reinterpret_cast<const void*>(&sigma_stream_kernel)});
+  out.push_back({"sigma_stream_kernel<2>", reinterpret_cast<const void*>(&sigma_stream_kernel<2>)});
   out.push_back({"slash_kernel", reinterpret_cast<const void*>(&slash_kernel)});
   out.push_back({"sigma_eff_csr_kernel", reinterpret_cast<const void*>(&sigma_eff_csr_kernel)});
   out.push_back({"build_tiles_kernel", reinterpret_cast<const void*>(&build_tiles_kernel)});

@@ -151,3 +151,56 @@ def test_fanout_groups_device_matches_host(device):
                  [(b.succeeded, b.error, b.result) for b in g.branches]) for g in map(fo.get_group, gids)]
 
     assert view(host, hg) == view(dev, dg)
+
+
+@pytest.mark.parametrize("delay", [0.0, 0.001])
+def test_device_runner_mixed_executor_kinds_match_host(delay):
+    """Executors that are plain functions (returning a non-awaitable: a failed
+    attempt, as in the reference), futures, coroutines that raise before
+    suspending, and retry delays — the device-decided rounds call each executor
+    exactly as often as the host orchestrator does."""
+    calls_h, calls_d = {}, {}
+
+    def build(orch, calls):
+        ids, ex = [], {}
+        loop_kinds = ["coro", "raise_now", "plain", "future", "suspend"]
+        for i in range(25):
+            sg = orch.create_saga(f"s{i}")
+            ids.append(sg.saga_id)
+            for k in range(3):
+                kind = loop_kinds[(i + k) % len(loop_kinds)]
+                st = orch.add_step(sg.saga_id, f"a{i}.{k}", "did:x", "/e", "/u", timeout_seconds=1, max_retries=1)
+                key = (i, k)
+
+                def mk(kind=kind, key=key):
+                    def fn():
+                        calls[key] = calls.get(key, 0) + 1
+                        if kind == "plain":
+                            return "not awaitable"
+                        if kind == "future":
+                            f = asyncio.get_running_loop().create_future()
+                            f.set_result(key)
+                            return f
+
+                        async def co():
+                            if kind == "raise_now" and calls[key] == 1:
+                                raise RuntimeError("first attempt fails")
+                            if kind == "suspend":
+                                await asyncio.sleep(0)
+                            return key
+                        return co()
+                    return fn
+                ex[st.step_id] = mk()
+        return ids, ex
+
+    async def comp(step):
+        return "undone"
+
+    host, dev = SagaOrchestrator(), SagaOrchestrator()
+    host.DEFAULT_RETRY_DELAY_SECONDS = dev.DEFAULT_RETRY_DELAY_SECONDS = delay
+    h_ids, h_ex = build(host, calls_h)
+    d_ids, d_ex = build(dev, calls_d)
+    asyncio.run(host.execute_sagas(h_ids, h_ex, comp))
+    asyncio.run(dev.execute_sagas(d_ids, d_ex, comp, device="cpu"))
+    assert _view(host, h_ids) == _view(dev, d_ids)
+    assert calls_h == calls_d
