@@ -52,6 +52,7 @@ from hypervisor.saga._timeout import await_with_timeout, resume_with_deadline
 u8 = torch.uint8
 _KIND_EXC, _KIND_TIMEOUT = 1, 2
 _ST_COMMITTED = STEP_NAMES.index("committed")
+_UNSET = object()
 _SG_RUNNING, _SG_COMPENSATING = SAGA_NAMES.index("running"), SAGA_NAMES.index("compensating")
 
 
@@ -127,10 +128,11 @@ class SagaBatchRunner:
         rows = [sg.steps for sg in sagas]
         hu = bytearray(1 if st.undo_api else 0 for row in rows for st in row)
         mr = bytearray(min(int(st.max_retries), 254) for row in rows for st in row)
-        results: dict[tuple[int, int], Any] = {}
-        errors: dict[tuple[int, int], str] = {}
-        comp_results: dict[tuple[int, int], Any] = {}
-        comp_errors: dict[tuple[int, int], str] = {}
+        # per (saga, step) host payloads, flat at s·K + k (_UNSET = none)
+        results: list = [_UNSET] * (S * K)
+        errors: list = [None] * (S * K)
+        comp_results: list = [_UNSET] * (S * K)
+        comp_errors: list = [None] * (S * K)
         loop = asyncio.get_running_loop()
 
         # device state machine, driven phase by phase: the outcome rows of step k
@@ -188,12 +190,12 @@ class SagaBatchRunner:
                 except Exception as e:  # executor failure
                     kind, err = _KIND_EXC, str(e)
                 else:
-                    results[(s, k)] = res
+                    results[s * K + k] = res
                     fa_row[s] = at
                     return
                 if at < n - 1:
                     await asyncio.sleep(delay * (at + 1))
-            errors[(s, k)] = err
+            errors[s * K + k] = err
             fa_row[s], fk_row[s] = NEVER, kind
 
         def inline(s: int, k: int, fa_row: bytearray, fk_row: bytearray):
@@ -211,7 +213,7 @@ class SagaBatchRunner:
                     try:
                         y = c.send(None)
                     except StopIteration as e:
-                        results[(s, k)] = e.value
+                        results[s * K + k] = e.value
                         fa_row[s] = at
                         return None
                     return attempts(s, k, fa_row, fk_row, at, (c, y))
@@ -219,7 +221,7 @@ class SagaBatchRunner:
                     err = str(e)
                 if at < n - 1 and delay > 0:
                     return attempts(s, k, fa_row, fk_row, at + 1)  # the retry waits its delay
-            errors[(s, k)] = err
+            errors[s * K + k] = err
             fa_row[s], fk_row[s] = NEVER, _KIND_EXC
             return None
 
@@ -243,26 +245,53 @@ class SagaBatchRunner:
                 raise ValueError("compensate=True needs a compensator")
             has_undo = prep["has_undo"]
 
-            async def comp(s: int, k: int, cf_row: bytearray) -> None:
+            async def comp(s: int, k: int, cf_row: bytearray, first=None, started=None) -> None:
                 st = rows[s][k]
+                tmo = st.timeout_seconds
                 try:
-                    res = await await_with_timeout(compensator(st), st.timeout_seconds)
+                    if started is not None:
+                        c, y = started
+                        res = await (resume_with_deadline(c, y, loop.time() + tmo) if tmo is not None and tmo > 0
+                                     else _resume(c, y))
+                    else:
+                        res = await await_with_timeout(compensator(st) if first is None else first, tmo)
                 except asyncio.TimeoutError:
-                    comp_errors[(s, k)] = f"Compensation timed out after {st.timeout_seconds}s"
+                    comp_errors[s * K + k] = f"Compensation timed out after {st.timeout_seconds}s"
                     cf_row[s] = _KIND_TIMEOUT
                     return
                 except Exception as e:
-                    comp_errors[(s, k)] = f"Compensation failed: {e}"
+                    comp_errors[s * K + k] = f"Compensation failed: {e}"
                     cf_row[s] = _KIND_EXC
                     return
-                comp_results[(s, k)] = res
+                comp_results[s * K + k] = res
+
+            def comp_inline(s: int, k: int, cf_row: bytearray):
+                """A compensator coroutine that finishes without suspending is driven
+                here; otherwise the awaitable finishing it (deadline armed)."""
+                st = rows[s][k]
+                try:
+                    c = compensator(st)
+                    if type(c) is not CoroutineType:
+                        return comp(s, k, cf_row, c)
+                    try:
+                        y = c.send(None)
+                    except StopIteration as e:
+                        comp_results[s * K + k] = e.value
+                        return None
+                except Exception as e:
+                    comp_errors[s * K + k] = f"Compensation failed: {e}"
+                    cf_row[s] = _KIND_EXC
+                    return None
+                return comp(s, k, cf_row, None, (c, y))
 
             for k in range(K - 1, -1, -1):  # committed steps in reverse order, all sagas at once
                 todo = torch.nonzero((eng.saga_state == _SG_COMPENSATING) & (eng._step_state[k] == _ST_COMMITTED)
                                      & (has_undo[k] != 0)).flatten().tolist()
                 if todo:
                     cf_row = bytearray(S)
-                    await asyncio.gather(*(comp(s, k, cf_row) for s in todo))
+                    slow = [c for c in (comp_inline(s, k, cf_row) for s in todo) if c is not None]
+                    if slow:
+                        await asyncio.gather(*slow)
                     upload("comp_fail", k, cf_row)
                 eng._phase(args, 3, k)  # also fails the committed steps without an Undo_API
         eng._phase(args, 4)
@@ -274,49 +303,55 @@ class SagaBatchRunner:
     def _write_back(eng, sagas, results, errors, comp_results, comp_errors) -> None:
         from hypervisor.saga.state_machine import SagaState, StepState
 
+        K = eng.K
         cols = torch.stack([eng.step_state.to(torch.int64), eng.retry_count.to(torch.int64),
                             eng.step_error.to(torch.int64), eng.started_us, eng.completed_us]).cpu().tolist()
         sg_cols = torch.stack([eng.saga_state.to(torch.int64), eng.saga_completed_us,
                                eng.comp_failed.to(torch.int64)]).cpu().tolist()
         # Per-batch lookup tables: enum members by code, and one datetime per distinct
-        # device timestamp (the step loop stamps from one time base, so few distinct
-        # values) — this loop touches every step of the batch.
+        # device timestamp (the phases stamp from one time base, so few distinct values)
         step_enum = [StepState(n) for n in STEP_NAMES]
         saga_enum = [SagaState(n) for n in SAGA_NAMES]
-        stamps: dict[int, Any] = {0: None}
-
-        def ts(us: int):
-            d = stamps.get(us)
-            if d is None and us:
-                d = stamps[us] = _clock.from_us(us)
-            return d
-
         st_state, st_retry, st_err, st_start, st_done = cols
+        seen = set()
+        for rows_ in (st_start, st_done, [sg_cols[1]]):
+            for r in rows_:
+                seen.update(r)
+        stamps = {us: (_clock.from_us(us) if us else None) for us in seen}
+        no_undo = "No Undo_API available"
+        escalated = SagaState.ESCALATED
         for s, sg in enumerate(sagas):
             row_state, row_retry, row_err = st_state[s], st_retry[s], st_err[s]
             row_start, row_done = st_start[s], st_done[s]
+            base = s * K
             for k, st in enumerate(sg.steps):
-                st.state = step_enum[row_state[k]]
-                st.retry_count = row_retry[k]
-                st.started_at, st.completed_at = ts(row_start[k]), ts(row_done[k])
                 code = row_err[k]
                 if code == ERR_NONE:
-                    st.error = None
-                elif code in (ERR_EXEC, ERR_TIMEOUT):
-                    st.error = errors.get((s, k))
+                    err = None
+                elif code == ERR_EXEC or code == ERR_TIMEOUT:
+                    err = errors[base + k]
                 elif code == ERR_NO_UNDO:
-                    st.error = "No Undo_API available"
-                elif code in (ERR_COMP, ERR_COMP_TIMEOUT):
-                    st.error = comp_errors.get((s, k))
-                r = results.get((s, k), results)  # the dict itself marks "absent"
-                if r is not results:
-                    st.execute_result = r
-                if (s, k) in comp_results:
-                    st.compensation_result = comp_results[(s, k)]
+                    err = no_undo
+                else:  # ERR_COMP, ERR_COMP_TIMEOUT
+                    err = comp_errors[base + k]
+                d = st.__dict__
+                d["state"] = step_enum[row_state[k]]
+                d["retry_count"] = row_retry[k]
+                d["started_at"] = stamps[row_start[k]]
+                d["completed_at"] = stamps[row_done[k]]
+                d["error"] = err
+                r = results[base + k]
+                if r is not _UNSET:
+                    d["execute_result"] = r
+                r = comp_results[base + k]
+                if r is not _UNSET:
+                    d["compensation_result"] = r
             sg.state = saga_enum[sg_cols[0][s]]
-            sg.completed_at = ts(sg_cols[1][s])
-            if sg.state is SagaState.ESCALATED:
+            sg.completed_at = stamps[sg_cols[1][s]]
+            if sg.state is escalated:
                 sg.error = f"{sg_cols[2][s]} step(s) failed compensation — Joint Liability slashing triggered"
+
+
 _RUNNERS: dict[str, SagaBatchRunner] = {}
 
 

@@ -268,7 +268,8 @@ def slash(
 
     ``mode`` picks the device form (all give identical results): ``"split"``
     (default: cascade over the slashed sessions only, then the streaming σ_eff
-    pass), ``"group"`` (one 16-lane pass per session doing both) or ``"lane"``."""
+    pass), ``"wave"`` (the same split, one session per wave), ``"group"`` (one
+    16-lane pass per session doing both) or ``"lane"``."""
     S = vb.sessions
     dev = vb.device
     offs = (torch.arange(S, dtype=i32, device=dev) * clip_cap).contiguous()
@@ -288,7 +289,7 @@ def slash(
     launch(
         "slash",
         {"sessions": S, "now_us": int(now_us), "clip_cap": int(clip_cap),
-         "mode": {None: -1, "split": 0, "group": 1, "lane": 2}[mode]},
+         "mode": {None: -1, "split": 0, "group": 1, "lane": 2, "wave": 3}[mode]},
         dict(offsets=vb.offsets, voucher=vb.voucher, vouchee=vb.vouchee, active=vb.active,
              expiry_us=vb.expiry_us, released_us=vb.released_us, target=target, omega=omega, scores=scores,
              clip_offsets=offs, clip_count=out.clip_count, clip_voucher=out.clip_voucher,

@@ -38,3 +38,22 @@ def lock_conflicts(res_offsets, lock_agent, lock_intent, req_res, req_agent, req
         dict(res_offsets=i32, lock_agent=i32, lock_intent=u8, req_res=i32, req_agent=i32, req_intent=u8),
     )
     return out
+
+
+LOCK_HOLDERS = 16
+LOCK_ROW = 2 + 2 * LOCK_HOLDERS
+LOCK_RELEASE = 0x80
+
+
+def lock_grant(seg_offsets, order, req_res, req_agent, req_intent, table, granted) -> None:
+    """K20 grant pass over the resident holder tables ``table`` [R, LOCK_ROW]
+    (in place); see ``LockGrantArgs`` in csrc/include/ahv/kernels.h."""
+    if table.dim() != 2 or table.shape[1] != LOCK_ROW or not table.is_contiguous():
+        raise ValueError(f"lock table must be contiguous int32 [R, {LOCK_ROW}]")
+    launch(
+        "lock_grant",
+        {"segments": seg_offsets.numel() - 1},
+        dict(seg_offsets=seg_offsets, order=order, req_res=req_res, req_agent=req_agent, req_intent=req_intent,
+             table=table, granted=granted),
+        dict(seg_offsets=i32, order=i32, req_res=i32, req_agent=i32, req_intent=u8, table=i32, granted=u8),
+    )

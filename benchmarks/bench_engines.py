@@ -9,6 +9,9 @@ so host and device see the same instants) and timed three ways where they exist:
 * ``tensor`` — the device engine's tensor API (inputs already on the device, the
   grouping is a device sort; output left on the device).
 
+Every workload is ``--calls`` operations (100 k by default; the host loops are
+timed on the first ``--host-calls`` of them).
+
 Prints one JSON line per (engine, path) with ops/s and µs per batch.  Kernels:
 K16 breach, K17 bucket, K18 expiry, K22 ledger + drift, K19 vector clocks, K20
 lock contention, K02 ring check, K21 attribution.
@@ -132,17 +135,28 @@ def main() -> None:
     # ---------------- K19 vector clocks
     va = [f"did:v{i}" for i in range(64)]
     vp = [f"/p{i}" for i in range(1024)]
-    vops = [(rng.choice(["read", "write"]), rng.choice(vp), rng.choice(va)) for _ in range(n // 10)]
-    emit("vector_clock", "host", len(vops),
-         timed(lambda: VectorClockManager().apply_batch(vops), torch.device("cpu"), 1))
+    vops = [(rng.choice(["read", "write"]), rng.choice(vp), rng.choice(va)) for _ in range(n)]
+    emit("vector_clock", "host", nh,
+         timed(lambda: VectorClockManager().apply_batch(vops[:nh]), torch.device("cpu"), 1))
     emit("vector_clock", "batch", len(vops), timed(lambda: VectorClockManager(device=dev).apply_batch(vops), dev))
 
     # ---------------- K20 locks
     lreq = [(f"did:k{rng.randrange(256)}", "s", f"/r{rng.randrange(4096)}", rng.choice(list(LockIntent)))
-            for _ in range(n // 10)]
+            for _ in range(n)]
     emit("intent_locks", "host", len(lreq), timed(lambda: IntentLockManager().acquire_batch(lreq),
                                                   torch.device("cpu"), 1))
     emit("intent_locks", "batch", len(lreq), timed(lambda: IntentLockManager(device=dev).acquire_batch(lreq), dev))
+    lm = IntentLockManager(device=dev)
+    l_ag = torch.tensor([lm.agent_row(q[0]) for q in lreq], dtype=torch.int32, device=dev)
+    l_rs = torch.tensor([lm.resource_row(q[2]) for q in lreq], dtype=torch.int32, device=dev)
+    l_it = torch.tensor([{"read": 0, "write": 1, "exclusive": 2}[q[3].value] for q in lreq], dtype=torch.uint8,
+                        device=dev)
+
+    def rows_cycle():  # acquire the batch, then release what was granted
+        g = lm.acquire_rows(l_ag, l_rs, l_it)
+        k = g == 1
+        lm.release_rows(l_ag[k], l_rs[k], l_it[k])
+    emit("intent_locks", "tensor", len(lreq), timed(rows_cycle, dev), note="acquire_rows + release_rows")
 
     # ---------------- K02 ring check
     enf = RingEnforcer()
@@ -153,7 +167,10 @@ def main() -> None:
     sig = [rng.random() for _ in range(n)]
     emit("ring_check", "host", nh, timed(lambda: [enf.check(r, x, s) for r, x, s in zip(rings[:nh], acts, sig)],
                                          torch.device("cpu"), 1))
-    emit("ring_check", "batch", n, timed(lambda: enf.check_batch(rings, acts, sig, device=dev), dev))
+    emit("ring_check", "batch", n, timed(lambda: enf.check_batch(rings, acts, sig, device=dev), dev),
+         note="decisions as arrays; RingCheckResult objects built on access")
+    emit("ring_check", "batch_materialized", n, timed(lambda: list(enf.check_batch(rings, acts, sig, device=dev)),
+                                                      dev), note="every RingCheckResult built")
     u8 = torch.uint8
     t_ring = torch.tensor([r.value for r in rings], dtype=u8, device=dev)
     t_flag = torch.tensor([RG.action_flags(x.is_admin, x.is_read_only, x.required_ring is R[1]) for x in acts],
@@ -164,15 +181,30 @@ def main() -> None:
 
     # ---------------- K21 attribution
     cases = []
-    for c in range(n // 100):
+    for c in range(n):
         ag = [f"did:x{j}" for j in range(rng.randint(2, 8))]
         acts_c = {x: [{"action_id": f"act{rng.randint(0, 5)}", "step_id": f"st{rng.randint(0, 4)}",
                        "success": rng.random() < 0.6} for _ in range(rng.randint(1, 5))] for x in ag}
         cases.append(dict(saga_id=f"saga{c}", session_id="s", agent_actions=acts_c, failure_step_id="st0",
                           failure_agent_did=ag[0]))
-    emit("attribution", "host", len(cases), timed(lambda: [CausalAttributor().attribute(**c) for c in cases],
-                                                  torch.device("cpu"), 1))
+    emit("attribution", "host", nh, timed(lambda: [CausalAttributor().attribute(**c) for c in cases[:nh]],
+                                          torch.device("cpu"), 1))
     emit("attribution", "batch", len(cases), timed(lambda: CausalAttributor().attribute_batch(cases, device=dev), dev))
+    # tensor-native: the same cases as CSR columns already on the device
+    no, ao, aof, sc_, rc_, om_ = [0], [0], [], [], [], []
+    for c in cases:
+        ags = list(c["agent_actions"])
+        for j, a_ in enumerate(ags):
+            for x in c["agent_actions"][a_]:
+                aof.append(j)
+                sc_.append(1 if x["success"] else 0)
+                rc_.append(1 if (x["step_id"] == c["failure_step_id"] and a_ == c["failure_agent_did"]) else 0)
+                om_.append(0.5)
+        no.append(len(aof))
+        ao.append(ao[-1] + len(ags))
+    ti = lambda v, dt=torch.int32: torch.tensor(v, dtype=dt, device=dev)  # noqa: E731
+    t_args = (ti(no), ti(ao), ti(aof), ti(sc_, torch.uint8), ti(rc_, torch.uint8), ti(om_, torch.float64))
+    emit("attribution", "tensor", len(cases), timed(lambda: CausalAttributor().attribute_tensors(*t_args), dev))
 
     # ---------------- K22 drift
     drift = torch.rand(n, dtype=torch.float64, device=dev)

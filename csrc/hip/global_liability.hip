@@ -52,8 +52,11 @@ struct ExposureArgs {
 
 AHV_HD double exposure_value(const ExposureArgs& a, int64_t e) {
   const int64_t v = a.index ? a.index[e] : e;
-  const bool live = (!a.active || a.active[v]) && (!a.expiry || a.expiry[v] < 0 || a.now_us <= a.expiry[v]);
-  return live ? a.bonded[v] : 0.0;
+  // every word loaded unconditionally (no short-circuit: one round trip, not three)
+  const double x = a.bonded[v];
+  const uint8_t act = a.active ? a.active[v] : 1;
+  const int64_t ex = a.expiry ? a.expiry[v] : -1;
+  return act != 0 && (ex < 0 || a.now_us <= ex) ? x : 0.0;
 }
 
 AHV_HD double exposure_row(const ExposureArgs& a, int64_t r) {
@@ -122,7 +125,9 @@ __global__ __launch_bounds__(256) void slash_clip_kernel(ClipArgs a) {
     const int32_t v = a.ids[i];
     for (int64_t j = a.offsets[v]; j < a.offsets[v + 1]; ++j) {
       const int32_t e = a.edge[j];
-      if (!a.active[e] || (a.expiry[e] >= 0 && a.now_us > a.expiry[e])) continue;
+      const uint8_t act = a.active[e];
+      const int64_t ex = a.expiry[e];
+      if (!act || (ex >= 0 && a.now_us > ex)) continue;
       // claim the bond: the same vouchee may appear twice in one storm, and a bond
       // is released (and its voucher clipped) once — as the sequential engine does
       const uintptr_t addr = reinterpret_cast<uintptr_t>(a.active + e);

@@ -28,8 +28,12 @@ inline dim3 grid1(int64_t n, int per_block = kBlock) {
   const int64_t b = (n + per_block - 1) / per_block;
   return dim3(static_cast<uint32_t>(b > 0 ? b : 1));
 }
+// Both words are loaded unconditionally: a short-circuit `active[e] && expiry[e]…`
+// makes the expiry load wait for the active byte (two dependent round trips).
 AHV_HD bool live_edge(const uint8_t* active, const int64_t* expiry, int64_t e, int64_t now) {
-  return active[e] && (expiry == nullptr || expiry[e] < 0 || now <= expiry[e]);
+  const uint8_t act = active[e];
+  const int64_t x = expiry != nullptr ? expiry[e] : -1;
+  return act != 0 && (x < 0 || now <= x);
 }
 // σ of the batched encoding: NaN marks an agent absent from agent_scores, which the
 // reference reads as 0.0 (as the slash kernel does), so no caller has to scrub NaNs.
@@ -128,8 +132,9 @@ __device__ __forceinline__ void fused_load(const BondFusedArgs& a, int32_t g, in
   meta = 0u;
   bond = 0.0;
   if (g < e1) {
+    const uint32_t vr = a.voucher[g], ve = a.vouchee[g];  // one round trip with the liveness words
     const bool live = live_edge(a.active, a.expiry_us, g, a.now_us);
-    meta = live ? (0x10000u | (static_cast<uint32_t>(a.voucher[g]) << 8) | a.vouchee[g]) : 0u;
+    meta = live ? (0x10000u | (vr << 8) | ve) : 0u;
     bond = a.bonded[g];
   }
 }
@@ -345,8 +350,9 @@ __global__ __launch_bounds__(kSigmaSessions * kTile) void sigma_eff_csr_kernel(V
   }
   for (int32_t k = e0 + threadIdx.x; k < e1; k += kSigmaSessions * kTile) {
     const int32_t j = pad_edge(k - e0);
+    const uint8_t ve = a.vouchee[k];
     const bool live = live_edge(a.active, a.expiry_us, k, a.now_us);
-    s_ve[j] = live ? a.vouchee[k] : 0xff;  // a dead edge matches no vouchee
+    s_ve[j] = live ? ve : 0xff;  // a dead edge matches no vouchee
     s_bd[j] = a.bonded[k];
   }
   __syncthreads();
@@ -412,7 +418,8 @@ __device__ __forceinline__ void stream_edge(const VouchCsrArgs& a, int32_t e, in
   bd = 0.0;
   if (e < end) {
     bd = a.bonded[e];
-    key = live_edge(a.active, a.expiry_us, e, a.now_us) ? a.vouchee[e] : 0xffu;
+    const uint32_t ve = a.vouchee[e];  // loaded with the liveness words, not after them
+    key = live_edge(a.active, a.expiry_us, e, a.now_us) ? ve : 0xffu;
   }
 }
 
@@ -458,12 +465,12 @@ void launch_sigma_eff_stream(const VouchCsrArgs& a, hipStream_t st) {
   if (a.sessions <= 0) return;
   static const int slices = [] {  // sessions per wave / 4 (A/B: AHV_STREAM_SLICES = 1, 2, 4)
     const char* e = std::getenv("AHV_STREAM_SLICES");
-    const int k = e ? std::atoi(e) : 2;
-    return k == 1 || k == 4 ? k : 2;
+    const int k = e ? std::atoi(e) : 1;  // measured: 1 (62 VGPRs, 8 waves/SIMD) beats 2 and 4
+    return k == 2 || k == 4 ? k : 1;
   }();
-  if (slices == 1) launch_stream_k<1>(a, st);
+  if (slices == 2) launch_stream_k<2>(a, st);
   else if (slices == 4) launch_stream_k<4>(a, st);
-  else launch_stream_k<2>(a, st);
+  else launch_stream_k<1>(a, st);
   check_hip(hipGetLastError(), "sigma_stream_kernel");
 }
 
@@ -1000,29 +1007,171 @@ __global__ __launch_bounds__(kSlashGroup * kSlashGroupsPerBlock) void slash_grou
 }
 
 // Split form (default): the cascade runs over the slashed sessions only and the
-// σ_eff of every session is the streaming K03 pass afterwards.  A 256-thread
-// block owns a window of 256 sessions:
-//   1. one coalesced round trip reads the window's targets and edge offsets
-//      (offsets into LDS); the rest get clip_count 0; wave ballots + a 4-entry
-//      prefix compact the slashed sessions into an LDS list;
-//   2. one round trip stages up to kCascStage listed sessions at once — thread
-//      (entry q, lane j) loads edges j, j+16, j+32, j+48 of entry q (voucher,
-//      vouchee, liveness), its σ[j] and ω — every load issued before the first
-//      LDS store;
-//   3. the 16 groups run the staged cascades (≤ 2 each) out of LDS, registers
-//      and lane shuffles — no global load on the cascade's critical path.
-// A storm over 10 % of the sessions launches one wave per 64 sessions instead
-// of one per 4, and σ_eff no longer waits behind cascades in the same waves.
+// σ_eff of every session is the streaming K03 pass afterwards.
+//
+// Cascade: a wave scans 64 sessions (targets + edge ranges in one coalesced
+// round trip, clip_count 0 for the untouched ones), takes the slashed ones in
+// batches of kWaveBatch — loading every edge of the batch at once, lane l =
+// edge l of a session (≤ 64 edges), and the score rows — and then runs each
+// cascade with the whole wave on one session.  The walk's state is
+// wave-uniform, so "which live edges vouch for `who`" is one 64-bit ballot and
+// every read of another lane's value (the clipped voucher, its σ, the clip list)
+// is a v_readlane into an SGPR — a few cycles, where the 16-lane group form
+// pays an LDS-crossbar ds_bpermute round trip per read on the cascade's
+// critical path.  The clip list lives one entry per lane in a VGPR.  Clip
+// order, arithmetic and records are those of slash_session_t.
+constexpr int kWaveBatch = 8;  // slashed sessions loaded per round trip
+
+__device__ __forceinline__ int rl_i(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
+__device__ __forceinline__ double rl_d(double x, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// One slashed session on the whole wave: lane l holds edge l (`e8` = voucher |
+// vouchee << 8, 0xffff when absent; `live`), lanes 0..15 its σ row.
+__device__ __forceinline__ void wave_cascade(const SlashArgs& a, int64_t s, int tgt, int32_t b, int l,
+                                             uint32_t e8, bool live, double sc, double omega) {
+  const int vr = static_cast<int>(e8 & 0xffu), ve = static_cast<int>((e8 >> 8) & 0xffu);
+  const int32_t base = a.clip_offsets[s];
+  uint32_t clv = 0;  // clip list: lane i = clip i as (voucher | cascade << 7)
+  int32_t nclip = 0;
+  static_assert(kMaxCascadeDepth == 2, "scalar DFS frames assume a cascade depth of 2");
+  int32_t next0 = 0, end0 = 0, next1 = 0, end1 = 0;
+  int sp = 0;
+  int who = tgt, who_depth = 0;
+  bool pending = true;
+  for (;;) {
+    if (pending) {
+      pending = false;
+      if (l == who) sc = 0.0;
+      const int32_t first = nclip;
+      uint64_t m = __ballot(ve == who && live);
+      while (m) {
+        const int k = static_cast<int>(__builtin_ctzll(m));
+        m &= m - 1;
+        const int v = rl_i(vr, k);
+        const double x = rl_d(sc, v);
+        const double before = x != x ? 0.0 : x;  // NaN = absent from agent_scores → 0.0
+        const double after = clip_sigma(before, omega);
+        if (l == v) sc = after;
+        if (l == nclip) clv = static_cast<uint32_t>(v | (after < kCascadeBelow ? 0x80 : 0));
+        if (l == 0 && nclip < a.clip_cap) {
+          a.clip_voucher[base + nclip] = static_cast<uint8_t>(v);
+          a.clip_depth[base + nclip] = static_cast<uint8_t>(who_depth);
+          a.clip_before[base + nclip] = before;
+          a.clip_after[base + nclip] = after;
+        }
+        if (l == k) {
+          live = false;
+          a.active[b + k] = 0;
+          a.released_us[b + k] = a.now_us;
+        }
+        ++nclip;
+      }
+      if (who_depth == 0) {
+        next0 = first;
+        end0 = nclip;
+      } else if (who_depth == 1) {
+        next1 = first;
+        end1 = nclip;
+      }
+      sp = who_depth + 1;
+    }
+    if (sp == 0) break;
+    const int depth = sp - 1;
+    const int32_t nx = depth == 0 ? next0 : next1;
+    const int32_t en = depth == 0 ? end0 : end1;
+    if (depth >= kMaxCascadeDepth || nx >= en) {
+      --sp;
+      continue;
+    }
+    if (depth == 0) next0 = nx + 1;
+    else next1 = nx + 1;
+    const int c8 = rl_i(static_cast<int>(clv), nx);
+    const int v = c8 & 0x7f;
+    if ((c8 & 0x80) && __ballot(ve == v && live) != 0ull) {
+      who = v;
+      who_depth = depth + 1;
+      pending = true;
+    }
+  }
+  if (l < kTile) a.scores[s * kTile + l] = sc;
+  if (l == 0) a.clip_count[s] = nclip;
+}
+
+__global__ __launch_bounds__(256) void slash_wave_kernel(SlashArgs a) {
+  const int l = threadIdx.x & 63;
+  const int64_t w0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * kWaveLanes;
+  if (w0 >= a.sessions) return;  // wave-uniform
+  const int64_t s_me = w0 + l;
+  const bool in = s_me < a.sessions;
+  const uint8_t tg = in ? a.target[s_me] : 0xff;
+  const int32_t off0 = a.offsets[in ? s_me : a.sessions];
+  const int32_t off1 = a.offsets[in ? s_me + 1 : a.sessions];
+  const bool hit = tg < kTile;
+  if (in && !hit) a.clip_count[s_me] = 0;
+  uint64_t m = __ballot(hit);
+  while (m) {  // wave-uniform
+    int idx[kWaveBatch];
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kWaveBatch; ++i) {
+      idx[i] = m ? static_cast<int>(__builtin_ctzll(m)) : 0;
+      cnt += m ? 1 : 0;
+      m &= m ? m - 1 : 0ull;
+    }
+    uint32_t e8[kWaveBatch];
+    bool live[kWaveBatch];
+    double sc[kWaveBatch], om[kWaveBatch];
+#pragma unroll
+    for (int i = 0; i < kWaveBatch; ++i) {  // every load of the batch in flight at once
+      const int32_t b = rl_i(off0, idx[i]), n = rl_i(off1, idx[i]) - b;
+      const bool use = i < cnt && n <= kWaveLanes;
+      const bool mine = use && l < n;
+      e8[i] = mine ? (static_cast<uint32_t>(a.voucher[b + l]) | (static_cast<uint32_t>(a.vouchee[b + l]) << 8))
+                   : 0xffffu;
+      live[i] = mine && live_edge(a.active, a.expiry_us, b + l, a.now_us);
+      sc[i] = use && l < kTile ? a.scores[(w0 + idx[i]) * kTile + l] : 0.0;
+      om[i] = i < cnt ? a.omega[w0 + idx[i]] : 0.0;
+    }
+#pragma unroll 1
+    for (int i = 0; i < cnt; ++i) {  // one copy of the cascade code: the batch rotates through slot 0
+      const int64_t s = w0 + idx[0];
+      const int32_t b = rl_i(off0, idx[0]), n = rl_i(off1, idx[0]) - b;
+      if (n > kWaveLanes) {  // more edges than lanes: the one-lane global-memory form
+        if (l == 0) slash_session(a, s);
+      } else {
+        wave_cascade(a, s, rl_i(static_cast<int>(tg), idx[0]), b, l, e8[0], live[0], sc[0], om[0]);
+      }
+#pragma unroll
+      for (int j = 0; j + 1 < kWaveBatch; ++j) {
+        idx[j] = idx[j + 1];
+        e8[j] = e8[j + 1];
+        live[j] = live[j + 1];
+        sc[j] = sc[j + 1];
+        om[j] = om[j + 1];
+      }
+    }
+  }
+}
+
+// Default split cascade: a 256-thread block owns a window of 256 sessions.  One
+// coalesced round trip reads the window's targets and edge offsets (offsets
+// into LDS; clip_count 0 for the untouched), wave ballots + a 4-entry prefix
+// compact the slashed ones into an LDS list, and the 16 groups of 16 lanes take
+// the list round-robin: a group requests its session's edges (lane j: edges
+// j, j+16, j+32, j+48 — one round trip, liveness words included), σ row and ω,
+// then runs group_cascade.  (slash_wave_kernel — one session per wave with
+// v_readlane instead of ds_bpermute — issues far fewer LDS ops but serialises
+// ~6 sessions per wave on SALU: slower, kept for A/B as mode 3.)
 constexpr int kCascWindow = 256;
-constexpr int kCascStage = 32;  // listed sessions staged per round (two per group)
 
 __global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a) {
   __shared__ int32_t s_list[kCascWindow];
   __shared__ int32_t s_off[kCascWindow + 1];
   __shared__ int32_t s_wcount[kCascWindow / kWaveLanes];
-  __shared__ uint8_t s_vr[kCascStage][kGroupEdges], s_ve[kCascStage][kGroupEdges], s_lv[kCascStage][kGroupEdges];
-  __shared__ double s_sc[kCascStage][kTile];
-  __shared__ double s_om[kCascStage];
   __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
   const int t = threadIdx.x;
   const int w = t / kWaveLanes, l = t % kWaveLanes;
@@ -1043,67 +1192,31 @@ __global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a)
     pre += k < w ? s_wcount[k] : 0;
     total += s_wcount[k];
   }
-  if (hit) s_list[pre + __popcll(m & ((1ull << l) - 1ull))] = t;
+  if (hit) s_list[pre + __popcll(m & ((1ull << l) - 1ull))] = t | (static_cast<int>(tg) << 16);
   __syncthreads();
   const int g = t / kSlashGroup, j = t % kSlashGroup;
   const int gl0 = (t % kWaveLanes) / kSlashGroup * kSlashGroup;
-  constexpr int kPasses = kCascStage / kSlashGroupsPerBlock;  // entries staged per thread
-  for (int base = 0; base < total; base += kCascStage) {  // block-uniform
-    const int m_here = total - base < kCascStage ? total - base : kCascStage;
-    // 2. stage: all loads of both passes first
-    uint8_t vr[kPasses][kGroupChunks], ve[kPasses][kGroupChunks], lv[kPasses][kGroupChunks];
-    double sc[kPasses], om[kPasses];
-#pragma unroll
-    for (int p = 0; p < kPasses; ++p) {
-      const int q = p * kSlashGroupsPerBlock + g;
-      const int ls = q < m_here ? s_list[base + q] : 0;
-      const int32_t b = s_off[ls], n = q < m_here ? s_off[ls + 1] - b : 0;
-      const bool small = n <= kGroupEdges;
-#pragma unroll
-      for (int c = 0; c < kGroupChunks; ++c) {
-        const int32_t i = c * kSlashGroup + j;
-        const bool in = small && i < n;
-        vr[p][c] = in ? a.voucher[b + i] : 0;
-        ve[p][c] = in ? a.vouchee[b + i] : 0xff;
-        lv[p][c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us) ? 1 : 0;
-      }
-      sc[p] = q < m_here && small ? a.scores[(w0 + ls) * kTile + j] : 0.0;
-      om[p] = q < m_here ? a.omega[w0 + ls] : 0.0;
+  for (int idx = g; idx < total; idx += kSlashGroupsPerBlock) {  // group-uniform
+    const int e = s_list[idx];
+    const int ls = e & 0xffff, tgt = e >> 16;
+    const int64_t s = w0 + ls;
+    const int32_t b = s_off[ls], n = s_off[ls + 1] - b;
+    if (n > kGroupEdges) {  // beyond the registers: the one-lane global-memory form
+      if (j == 0) slash_session(a, s);
+      continue;
     }
+    int vr[kGroupChunks], ve[kGroupChunks];
+    bool lv[kGroupChunks];
 #pragma unroll
-    for (int p = 0; p < kPasses; ++p) {
-      const int q = p * kSlashGroupsPerBlock + g;
-#pragma unroll
-      for (int c = 0; c < kGroupChunks; ++c) {
-        s_vr[q][c * kSlashGroup + j] = vr[p][c];
-        s_ve[q][c * kSlashGroup + j] = ve[p][c];
-        s_lv[q][c * kSlashGroup + j] = lv[p][c];
-      }
-      s_sc[q][j] = sc[p];
-      if (j == 0) s_om[q] = om[p];
+    for (int c = 0; c < kGroupChunks; ++c) {
+      const int32_t i = c * kSlashGroup + j;
+      const bool in = i < n;
+      vr[c] = in ? a.voucher[b + i] : 0;
+      ve[c] = in ? a.vouchee[b + i] : -1;
+      lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
     }
-    __syncthreads();
-    // 3. cascades out of LDS/registers (group-uniform loop)
-    for (int q = g; q < m_here; q += kSlashGroupsPerBlock) {
-      const int ls = s_list[base + q];
-      const int64_t s = w0 + ls;
-      const int32_t b = s_off[ls], n = s_off[ls + 1] - b;
-      if (n > kGroupEdges) {  // beyond the staging rows: the one-lane global-memory form
-        if (j == 0) slash_session(a, s);
-        continue;
-      }
-      int rvr[kGroupChunks], rve[kGroupChunks];
-      bool rlv[kGroupChunks];
-#pragma unroll
-      for (int c = 0; c < kGroupChunks; ++c) {
-        const int i = c * kSlashGroup + j;
-        rvr[c] = s_vr[q][i];
-        rve[c] = i < n ? static_cast<int>(s_ve[q][i]) : -1;
-        rlv[c] = s_lv[q][i] != 0;
-      }
-      group_cascade(a, s, a.target[s], b, j, gl0, s_cl[g], rvr, rve, rlv, s_sc[q][j], s_om[q]);
-    }
-    __syncthreads();  // the next round overwrites the staging rows
+    const double sc = a.scores[s * kTile + j];
+    group_cascade(a, s, tgt, b, j, gl0, s_cl[g], vr, ve, lv, sc, a.omega[s]);
   }
 }
 
@@ -1113,11 +1226,12 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
     const char* e = std::getenv("AHV_SLASH_PER_LANE");
     return e && std::atoi(e) == 1;
   }();
-  static const bool fused_group = [] {  // A/B: the round-2 single pass (cascade + σ_eff per group)
-    const char* e = std::getenv("AHV_SLASH_FUSED");
-    return e && std::atoi(e) == 1;
+  static const int env_mode = [] {  // A/B: AHV_SLASH_FUSED=1 the round-2 single pass; AHV_SLASH_MODE=0..3
+    const char* f = std::getenv("AHV_SLASH_FUSED");
+    const char* m = std::getenv("AHV_SLASH_MODE");
+    return f && std::atoi(f) == 1 ? 1 : m ? std::atoi(m) : 0;
   }();
-  const int mode = a.mode >= 0 ? a.mode : (per_lane ? 2 : fused_group ? 1 : 0);
+  const int mode = a.mode >= 0 ? a.mode : (per_lane ? 2 : env_mode);
   if (mode == 2) {
     hipLaunchKernelGGL(slash_kernel, grid1(a.sessions, 64), dim3(64), 0, st, a);
     if (a.sigma_eff) hipLaunchKernelGGL(slash_sigma_kernel, grid1(a.sessions * kTile), dim3(kBlock), 0, st, a);
@@ -1125,7 +1239,8 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(slash_group_kernel, grid1(a.sessions, kSlashGroupsPerBlock),
                        dim3(kSlashGroup * kSlashGroupsPerBlock), 0, st, a);
   } else {
-    hipLaunchKernelGGL(slash_cascade_kernel, grid1(a.sessions, kCascWindow), dim3(kCascWindow), 0, st, a);
+    if (mode == 3) hipLaunchKernelGGL(slash_wave_kernel, grid1(a.sessions, 4 * kWaveLanes), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(slash_cascade_kernel, grid1(a.sessions, kCascWindow), dim3(kCascWindow), 0, st, a);
     if (a.sigma_eff) {  // K03 over the post-slash scores and bonds
       static const bool csr = [] {  // A/B: AHV_SLASH_SIGMA=csr runs the LDS-staged K03 form
         const char* e = std::getenv("AHV_SLASH_SIGMA");
@@ -1150,7 +1265,8 @@ void slash_host(const SlashArgs& a) {
 void kernels_liability(std::vector<KernelEntry>& out) {
   out.push_back({"slash_group_kernel", reinterpret_cast<const void*>(&slash_group_kernel)});
   out.push_back({"slash_cascade_kernel", reinterpret_cast<const void*>(&slash_cascade_kernel)});
-  out.push_back({"sigma_stream_kernel<2>", reinterpret_cast<const void*>(&sigma_stream_kernel<2>)});
+  out.push_back({"slash_wave_kernel", reinterpret_cast<const void*>(&slash_wave_kernel)});
+  out.push_back({"sigma_stream_kernel<1>", reinterpret_cast<const void*>(&sigma_stream_kernel<1>)});
   out.push_back({"slash_kernel", reinterpret_cast<const void*>(&slash_kernel)});
   out.push_back({"sigma_eff_csr_kernel", reinterpret_cast<const void*>(&sigma_eff_csr_kernel)});
   out.push_back({"build_tiles_kernel", reinterpret_cast<const void*>(&build_tiles_kernel)});

@@ -101,4 +101,66 @@ void launch_locks(const LockArgs& a, hipStream_t st) {
 }
 void locks_host(const LockArgs& a) { for (int64_t i = 0; i < a.n; ++i) locks_elem(a, i); }
 
+AHV_HD void lock_grant_segment(const LockGrantArgs& a, int64_t g) {
+  const int32_t k0 = a.seg_offsets[g], k1 = a.seg_offsets[g + 1];
+  int32_t* row = a.table + static_cast<int64_t>(a.req_res[a.order[k0]]) * kLockRow;
+  int32_t rc = row[0], wc = row[1];
+  for (int32_t k = k0; k < k1; ++k) {
+    const int32_t i = a.order[k];
+    const int32_t ag = a.req_agent[i];
+    const uint8_t in = a.req_intent[i];
+    const bool write = (in & 0x7f) != 0;
+    int own = -1, free_slot = -1;
+    for (int h = 0; h < kLockHolders; ++h) {
+      const int32_t who = row[2 + 2 * h];
+      if (who == ag) own = h;
+      if (who == -1 && free_slot < 0) free_slot = h;
+    }
+    const int32_t rw = own >= 0 ? row[3 + 2 * own] : 0;
+    const int32_t own_r = rw & 0xffff, own_w = rw >> 16;
+    if (in & 0x80) {  // release one lock of this intent
+      if (own >= 0 && (write ? own_w : own_r) > 0) {
+        const int32_t nrw = write ? rw - 0x10000 : rw - 1;
+        row[3 + 2 * own] = nrw;
+        if (nrw == 0) row[2 + 2 * own] = -1;
+        if (write) --wc;
+        else --rc;
+        a.granted[i] = 1;
+      } else {
+        a.granted[i] = 0;
+      }
+      continue;
+    }
+    const bool ok = write ? (rc - own_r) + (wc - own_w) == 0 : wc - own_w == 0;
+    if (!ok) {
+      a.granted[i] = 0;
+      continue;
+    }
+    const int slot = own >= 0 ? own : free_slot;
+    if (slot < 0) {  // every holder slot belongs to another agent
+      a.granted[i] = 2;
+      continue;
+    }
+    row[2 + 2 * slot] = ag;
+    row[3 + 2 * slot] = write ? rw + 0x10000 : rw + 1;
+    if (write) ++wc;
+    else ++rc;
+    a.granted[i] = 1;
+  }
+  row[0] = rc;
+  row[1] = wc;
+}
+__global__ void lock_grant_kernel(LockGrantArgs a) {
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < a.segments;
+       g += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    lock_grant_segment(a, g);
+}
+void launch_lock_grant(const LockGrantArgs& a, hipStream_t st) {
+  if (a.segments <= 0) return;
+  const int64_t b = (a.segments + 255) / 256;
+  hipLaunchKernelGGL(lock_grant_kernel, dim3(static_cast<uint32_t>(b)), dim3(256), 0, st, a);
+  check_hip(hipGetLastError(), "lock_grant_kernel");
+}
+void lock_grant_host(const LockGrantArgs& a) { for (int64_t g = 0; g < a.segments; ++g) lock_grant_segment(a, g); }
+
 }  // namespace ahv

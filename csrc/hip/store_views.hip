@@ -118,7 +118,9 @@ AHV_HD double sigma_batch_row(const SigmaBatchArgs& a, int64_t i) {
   double acc = 0.0;
   if (v >= 0 && v < a.cap_v) {
     for (int32_t e = a.v_head[v]; e >= 0; e = a.e_next[e]) {
-      const bool live = a.e_active[e] && (a.e_expiry[e] < 0 || a.now_us <= a.e_expiry[e]);
+      const uint8_t act = a.e_active[e];
+      const int64_t ex = a.e_expiry[e];
+      const bool live = act && (ex < 0 || a.now_us <= ex);
       const int32_t x = a.mode == 0 ? a.e_vouchee[e] : a.e_voucher[e];
       if (live && x == who) acc += a.e_bonded[e];
     }

@@ -223,7 +223,7 @@ static SlashArgs to_slash(const py::dict& d) {
   a.bonded = d.contains("bonded") ? ptr<const double>(d, "bonded") : nullptr;
   a.sigma_eff = d.contains("sigma_eff") ? ptr<double>(d, "sigma_eff") : nullptr;
   a.mode = d.contains("mode") ? val<int32_t>(d, "mode") : -1;
-  if (a.mode < -1 || a.mode > 2) throw py::value_error("slash: mode must be -1, 0, 1 or 2");
+  if (a.mode < -1 || a.mode > 3) throw py::value_error("slash: mode must be -1, 0, 1, 2 or 3");
   return a;
 }
 static RenderArgs to_render(const py::dict& d) {
@@ -276,6 +276,12 @@ static LockArgs to_locks(const py::dict& d) {
   LockArgs a{};
   V(n, int64_t); P(res_offsets, const int32_t); P(lock_agent, const int32_t); P(lock_intent, const uint8_t);
   P(req_res, const int32_t); P(req_agent, const int32_t); P(req_intent, const uint8_t); P(conflicts, int32_t);
+  return a;
+}
+static LockGrantArgs to_lock_grant(const py::dict& d) {
+  LockGrantArgs a{};
+  V(segments, int64_t); P(seg_offsets, const int32_t); P(order, const int32_t); P(req_res, const int32_t);
+  P(req_agent, const int32_t); P(req_intent, const uint8_t); P(table, int32_t); P(granted, uint8_t);
   return a;
 }
 static ChainHashArgs to_chain_hash(const py::dict& d) {
@@ -350,6 +356,7 @@ void register_kernels(py::module_& m) {
   bind_pair(m, "verify", to_verify, launch_verify, verify_host);
   bind_pair(m, "vclock", to_vclock, launch_vclock, vclock_host);
   bind_pair(m, "locks", to_locks, launch_locks, locks_host);
+  bind_pair(m, "lock_grant", to_lock_grant, launch_lock_grant, lock_grant_host);
   bind_pair(m, "saga_fused", to_saga, launch_saga_fused, saga_fused_host);
   bind_pair(m, "chain_hash", to_chain_hash, launch_chain_hash, chain_hash_host);
   m.def(

@@ -292,7 +292,8 @@ struct SlashArgs {
   double* sigma_eff;        // [S,16] out
   // Device form: 0 = split (cascade over the slashed sessions, then streaming
   // K03), 1 = one group pass per session (cascade + σ_eff), 2 = one lane per
-  // session; −1 = AHV_SLASH_FUSED / AHV_SLASH_PER_LANE, else split.
+  // session, 3 = split with one session per wave (slash_wave_kernel);
+  // −1 = AHV_SLASH_FUSED / AHV_SLASH_PER_LANE / AHV_SLASH_MODE, else split.
   int32_t mode = -1;
 };
 void launch_slash(const SlashArgs&, hipStream_t);
@@ -429,6 +430,31 @@ struct LockArgs {
 };
 void launch_locks(const LockArgs&, hipStream_t);
 void locks_host(const LockArgs&);
+
+// K20 grant pass: decide a batch of lock requests against resident
+// per-resource holder tables, in request order within each resource (one lane
+// per resource segment), and record the outcome in the tables.  Resource r's
+// row (kLockRow int32): [0] active READ locks, [1] active WRITE/EXCLUSIVE
+// locks, then kLockHolders slots of (agent, reads | writes << 16) (agent −1 =
+// free).  An acquire by agent a conflicts iff another agent holds a lock it is
+// incompatible with (only READ+READ coexist; an agent never conflicts with
+// itself) — granted 1, refused 0, or 2 when all holder slots are taken by
+// other agents (an overflow, reported instead of guessed).  A request with
+// intent bit 0x80 releases one lock of that intent held by the agent instead.
+constexpr int kLockHolders = 16;
+constexpr int kLockRow = 2 + 2 * kLockHolders;
+struct LockGrantArgs {
+  int64_t segments;            // resources touched by the batch
+  const int32_t* seg_offsets;  // [segments+1] into `order`
+  const int32_t* order;        // [n] request indices, resource-major, request order within a resource
+  const int32_t* req_res;      // [n] resource row
+  const int32_t* req_agent;    // [n]
+  const uint8_t* req_intent;   // [n] 0 read 1 write 2 exclusive (| 0x80: release)
+  int32_t* table;              // [R, kLockRow] in/out
+  uint8_t* granted;            // [n] out
+};
+void launch_lock_grant(const LockGrantArgs&, hipStream_t);
+void lock_grant_host(const LockGrantArgs&);
 
 // ------------------------------------------------------------------- sagas
 // K13/K14 batched saga chains (args and semantics in ahv/saga_batch.h)

@@ -37,6 +37,7 @@ is read back only as the batch's results.
 
 from __future__ import annotations
 
+import os
 from datetime import timedelta
 from typing import Iterable, Optional, Sequence
 
@@ -765,20 +766,95 @@ class DeviceVectorClockManager(VectorClockManager):
 
 
 class DeviceIntentLockManager(IntentLockManager):
-    """Contention of a batch of acquires scanned by K20 against the active locks.
+    """Intent locks whose contention decisions run on the device (K20 grant pass).
 
-    Requests run in rounds — the k-th request of every resource in round k — so a
-    request sees every lock granted before it, as sequential :meth:`acquire`
-    does.  Lock records (ids, saga step links) and the wait-for graph of the
-    deadlock check stay on the host."""
+    The device keeps a resident holder table per resource — active READ and
+    WRITE/EXCLUSIVE lock counts and up to 16 holder slots (agent, its reads,
+    its writes) — and a batch of acquires is decided in one launch: requests
+    are grouped by resource (stable, so request order holds within a resource)
+    and one lane per resource walks its requests, granting or refusing each
+    exactly as a sequential :meth:`acquire` would and recording the grants.
+    The host keeps the lock records (ids, saga-step links, the per-resource
+    index that release and the queries use) and the wait-for graph: refused
+    requests take the host path, which builds the same LockContentionError /
+    DeadlockError (and wait edges) sequential acquire raises.  Releases mark
+    their resource stale; its row is rebuilt from the records before the next
+    batch.  More than 16 concurrent holders can only be readers: the counts
+    stay exact, the extra readers are granted by the host path.
+
+    :meth:`acquire_rows` / :meth:`release_rows` are the tensor-native form
+    (device tensors in, granted mask out, holds tracked only on the device)."""
 
     def __init__(self, record_waits: bool = False, device="cuda") -> None:
         super().__init__(record_waits)
         self.device = torch.device(device)
         self._agent_id: dict[str, int] = {}
+        self._res_id: dict[str, int] = {}
+        self._res_path: list[str] = []
+        self._table = self._fresh(1024)
+        self._dirty: set[str] = set()
+
+    def _fresh(self, n: int) -> torch.Tensor:
+        t = torch.zeros((n, SN.LOCK_ROW), dtype=i32, device=self.device)
+        t[:, 2::2] = -1
+        return t
 
     def _aid(self, did: str) -> int:
         return self._agent_id.setdefault(did, len(self._agent_id))
+
+    def _rid(self, path: str) -> int:
+        r = self._res_id.get(path)
+        if r is None:
+            r = self._res_id[path] = len(self._res_path)
+            self._res_path.append(path)
+        return r
+
+    def release(self, lock_id: str) -> None:
+        lock = self._locks.get(lock_id)
+        super().release(lock_id)
+        if lock is not None:
+            self._dirty.add(lock.resource_path)
+
+    def _row_of(self, path: str) -> list[int]:
+        rc = wc = 0
+        slots: dict[int, list[int]] = {}
+        for lk in self.get_resource_locks(path):
+            a = self._aid(lk.agent_did)
+            w = not (lk.intent is LockIntent.READ or lk.intent == "read")
+            wc += w
+            rc += not w
+            if a in slots or len(slots) < SN.LOCK_HOLDERS:
+                c = slots.setdefault(a, [0, 0])
+                c[w] += 1
+        row = [rc, wc]
+        for a, (r, w) in slots.items():
+            row += [a, r | (w << 16)]
+        row += [-1, 0] * (SN.LOCK_HOLDERS - len(slots))
+        return row
+
+    def _sync(self) -> None:
+        """Grow the table to every known resource and rebuild the rows the host
+        changed (releases, overflow grants) from the lock records."""
+        R = len(self._res_path)
+        if R > self._table.shape[0]:
+            cap = self._table.shape[0]
+            while cap < R:
+                cap *= 2
+            grown = self._fresh(cap)
+            grown[: self._table.shape[0]] = self._table
+            self._table = grown
+        if not self._dirty:
+            return
+        rows, vals = [], []
+        for path in self._dirty:
+            r = self._res_id.get(path)
+            if r is not None:
+                rows.append(r)
+                vals.append(self._row_of(path))
+        self._dirty.clear()
+        if rows:
+            self._table[torch.tensor(rows, dtype=i64, device=self.device)] = \
+                torch.tensor(vals, dtype=i32).to(self.device)
 
     def acquire(self, agent_did, session_id, resource_path, intent, saga_step_id=None) -> IntentLock:
         res = self.acquire_batch([(agent_did, session_id, resource_path, intent, saga_step_id)])[0]
@@ -786,46 +862,124 @@ class DeviceIntentLockManager(IntentLockManager):
             raise res
         return res
 
+    def _grant(self, rs, ag, it) -> "np.ndarray":
+        import numpy as np
+
+        n = len(rs)
+        order = np.argsort(rs, kind="stable").astype(np.int32)
+        sr = rs[order]
+        starts = np.flatnonzero(np.r_[True, sr[1:] != sr[:-1]]).astype(np.int32)
+        G = len(starts)
+        buf = torch.from_numpy(np.concatenate([np.r_[starts, n].astype(np.int32), order, rs, ag, it]))
+        buf = buf.to(self.device)
+        granted = torch.empty(n, dtype=u8, device=self.device)
+        o = G + 1
+        SN.lock_grant(buf[:o], buf[o: o + n], buf[o + n: o + 2 * n], buf[o + 2 * n: o + 3 * n],
+                      buf[o + 3 * n:].to(u8), self._table, granted)
+        return granted.cpu().numpy()
+
     def acquire_batch(self, requests: Iterable[tuple]) -> list:
         """``(agent_did, session_id, resource_path, intent[, saga_step_id])`` →
         IntentLock, or the LockContentionError / DeadlockError sequential
         acquire would raise, per request."""
-        reqs = list(requests)
-        out: list = [None] * len(reqs)
-        rounds: list[list[int]] = []
-        seen: dict[str, int] = {}
-        for i, q in enumerate(reqs):
-            k = seen.get(q[2], 0)
-            seen[q[2]] = k + 1
-            if k == len(rounds):
-                rounds.append([])
-            rounds[k].append(i)
-        for rnd in rounds:
-            res_list = [reqs[i][2] for i in rnd]
-            offs, l_agent, l_int = [0], [], []
-            for path in res_list:
-                for lk in self.get_resource_locks(path):
-                    l_agent.append(self._aid(lk.agent_did))
-                    l_int.append(SN.LOCK_INTENT[LockIntent(lk.intent).value])
-                offs.append(len(l_agent))
-            dev = self.device
-            o, la, li, ra, ri = _upload_i64(dev, offs, l_agent, l_int, [self._aid(reqs[i][0]) for i in rnd],
-                                            [SN.LOCK_INTENT[LockIntent(reqs[i][3]).value] for i in rnd])
-            rr = torch.arange(len(rnd), dtype=i32, device=dev)
-            conf = SN.lock_conflicts(o.to(i32), la.to(i32), li.to(u8), rr, ra.to(i32), ri.to(u8)).cpu().tolist()
-            for j, i in enumerate(rnd):
-                agent, session, path, intent = reqs[i][:4]
-                step = reqs[i][4] if len(reqs[i]) > 4 else None
-                if conf[j] == 0:
-                    lock = IntentLock(agent_did=agent, session_id=session, resource_path=path,
-                                      intent=LockIntent(intent), saga_step_id=step)
-                    self._locks[lock.lock_id] = lock
-                    self._resource_locks.setdefault(path, []).append(lock.lock_id)
-                    out[i] = lock
-                    continue
-                try:  # the error (message, wait-for edges) exactly as the host engine builds it
-                    IntentLockManager.acquire(self, agent, session, path, LockIntent(intent), step)
-                    raise AssertionError("K20 reported contention the host check did not see")
-                except (LockContentionError, DeadlockError) as err:
-                    out[i] = err
+        import numpy as np
+
+        reqs = requests if isinstance(requests, list) else list(requests)
+        n = len(reqs)
+        if not n:
+            return []
+        aid, rid = self._aid, self._rid
+        codes = SN.LOCK_INTENT
+        ag = np.fromiter((aid(q[0]) for q in reqs), dtype=np.int32, count=n)
+        rs = np.fromiter((rid(q[2]) for q in reqs), dtype=np.int32, count=n)
+        it = np.fromiter((codes[q[3]] for q in reqs), dtype=np.int32, count=n)
+        self._sync()
+        ok = self._grant(rs, ag, it)
+        # lock records for the grants (one timestamp per batch, ids minted in bulk), errors for the rest
+        when = _now()
+        hexes = os.urandom(4 * n).hex()
+        locks, index = self._locks, self._resource_locks
+        new = object.__new__
+        out: list = [None] * n
+        for i in range(n):
+            q = reqs[i]
+            if ok[i] == 1:
+                lock = new(IntentLock)
+                lid = "lock:" + hexes[8 * i: 8 * i + 8]
+                lock.__dict__.update(lock_id=lid, agent_did=q[0], session_id=q[1], resource_path=q[2],
+                                     intent=LockIntent(q[3]), acquired_at=when, is_active=True,
+                                     saga_step_id=q[4] if len(q) > 4 else None)
+                locks[lid] = lock
+                ids = index.get(q[2])
+                if ids is None:
+                    index[q[2]] = [lid]
+                else:
+                    ids.append(lid)
+                out[i] = lock
+                continue
+            err = self._refusal(q[0], q[2], LockIntent(q[3]))
+            if err is not None:
+                out[i] = err
+                continue
+            if ok[i] != 2:
+                raise AssertionError("K20 refused a request the host check grants")
+            # more readers than holder slots: granted here, the row is rebuilt
+            out[i] = IntentLockManager.acquire(self, q[0], q[1], q[2], LockIntent(q[3]), q[4] if len(q) > 4 else None)
+            self._dirty.add(q[2])
         return out
+
+    def _refusal(self, agent: str, path: str, intent: LockIntent):
+        """The error sequential :meth:`IntentLockManager.acquire` raises for a
+        refused request (same message, same wait-for edges), or None when the
+        records show no conflict.  Without wait-for edges no deadlock is possible
+        (a conflict never involves the requester itself), so the search is skipped."""
+        locks = self._locks
+        read = intent is LockIntent.READ
+        conflicts = [lk for lk in (locks[i] for i in self._resource_locks.get(path, ()) if i in locks)
+                     if lk.is_active and lk.agent_did != agent and not (read and lk.intent == LockIntent.READ)]
+        if not conflicts:
+            return None
+        blockers = {c.agent_did for c in conflicts}
+        if self._wait_for and self._would_deadlock(agent, blockers):
+            return DeadlockError(
+                f"Deadlock detected: {agent} would wait on "
+                f"{blockers} which are waiting on {agent}"
+            )
+        if self._record_waits:
+            self._wait_for.setdefault(agent, set()).update(blockers)
+        return LockContentionError(
+            f"Lock contention on {path}: {agent} ({intent.value}) "
+            f"conflicts with {', '.join(c.agent_did for c in conflicts)}"
+        )
+
+    def acquire_rows(self, agent_ids: torch.Tensor, resource_rows: torch.Tensor, intents: torch.Tensor) -> torch.Tensor:
+        """Tensor-native K20: decide (and record in the device holder tables) a
+        batch of acquires given as device tensors — int32 agent ids
+        (:meth:`agent_row`) and resource rows (:meth:`resource_row`), u8 intents
+        (0 read 1 write 2 exclusive) — → u8 per request on the device: 1
+        granted, 0 refused (contention), 2 refused because the resource's 16
+        holder slots belong to other agents.  No host lock records are made: the
+        caller tracks its holds and returns them with :meth:`release_rows`."""
+        self._sync()
+        n = resource_rows.numel()
+        rows = resource_rows.to(i32)
+        sr, order = torch.sort(rows, stable=True)
+        first = torch.ones(n, dtype=torch.bool, device=self.device)
+        first[1:] = sr[1:] != sr[:-1]
+        seg = torch.cat([torch.nonzero(first).flatten().to(i32), torch.tensor([n], dtype=i32, device=self.device)])
+        granted = torch.empty(n, dtype=u8, device=self.device)
+        SN.lock_grant(seg, order.to(i32), rows, agent_ids.to(i32), intents.to(u8), self._table, granted)
+        return granted
+
+    def release_rows(self, agent_ids: torch.Tensor, resource_rows: torch.Tensor, intents: torch.Tensor) -> torch.Tensor:
+        """Return holds granted by :meth:`acquire_rows` (one lock of that intent
+        per request) → u8 per request, 1 released, 0 not held."""
+        return self.acquire_rows(agent_ids, resource_rows, intents.to(u8) | SN.LOCK_RELEASE)
+
+    def resource_row(self, path: str) -> int:
+        r = self._rid(path)
+        self._sync()
+        return r
+
+    def agent_row(self, did: str) -> int:
+        return self._aid(did)

@@ -157,7 +157,12 @@ class CausalAttributor:
     def attribute_batch(self, cases, device="cpu") -> list[AttributionResult]:
         """:meth:`attribute` for many failure cases — dicts of its keyword
         arguments — with the raw per-agent scores of all cases from one K21
-        launch on ``device``; normalisation and ranking stay on the host."""
+        launch on ``device``; normalisation (CPython ``round``) and ranking stay
+        on the host.  The causal nodes are flattened straight into the kernel's
+        columns (no :class:`CausalNode` objects: a result records only the chain
+        length), and agents are ranked from the same set order as
+        :meth:`attribute`, so ties sort identically."""
+        import numpy as np
         import torch
 
         from agent_hypervisor_amd.ops import ledger as LG
@@ -165,30 +170,64 @@ class CausalAttributor:
         node_off, agent_off, agent_of, succ, root, omega = [0], [0], [], [], [], []
         per_case = []
         for c in cases:
-            nodes = self.build_causal_dag(c["agent_actions"], c["failure_step_id"], c["failure_agent_did"])
-            agents = list(c["agent_actions"].keys())
+            aa = c["agent_actions"]
+            fstep, fagent = c["failure_step_id"], c["failure_agent_did"]
+            agents = list(set(aa.keys()))  # the iteration order raw_scores uses
             col = {a: j for j, a in enumerate(agents)}
             rw = c.get("risk_weights") or {}
-            for n in nodes:
-                agent_of.append(col[n.agent_did])
-                succ.append(1 if n.success else 0)
-                root.append(1 if n.is_root_cause else 0)
-                omega.append(float(rw.get(n.action_id, 0.5)))
+            for agent, acts in aa.items():
+                j = col[agent]
+                me = agent == fagent
+                for a in acts:
+                    agent_of.append(j)
+                    succ.append(1 if a.get("success", True) else 0)
+                    root.append(1 if me and a.get("step_id") == fstep else 0)
+                    omega.append(float(rw.get(a.get("action_id", ""), 0.5)))
             node_off.append(len(agent_of))
             agent_off.append(agent_off[-1] + len(agents))
-            per_case.append((c, nodes, agents))
-        i32 = torch.int32
-        ints = torch.tensor(node_off + agent_off + agent_of, dtype=i32).to(device)
+            per_case.append((c, agents, node_off[-1] - node_off[-2]))
         C, N = len(per_case), len(agent_of)
-        flags = torch.tensor([succ, root], dtype=torch.uint8).reshape(2, N).to(device)
+        ints = torch.from_numpy(np.asarray(node_off + agent_off + agent_of, dtype=np.int32)).to(device)
+        flags = torch.from_numpy(np.asarray([succ, root], dtype=np.uint8).reshape(2, N)).to(device)
         raw = LG.attribution_raw(ints[: C + 1], ints[C + 1: 2 * C + 2], ints[2 * C + 2:], flags[0].contiguous(),
-                                 flags[1].contiguous(), torch.tensor(omega, dtype=torch.float64).to(device))
+                                 flags[1].contiguous(), torch.from_numpy(np.asarray(omega, dtype=np.float64)).to(device))
         raw = raw.cpu().tolist()
-        out = []
-        for k, (c, nodes, agents) in enumerate(per_case):
-            scores = dict(zip(agents, raw[agent_off[k]: agent_off[k + 1]]))
-            out.append(self._result(c["saga_id"], c["session_id"], nodes, scores, c["failure_agent_did"]))
-        return out
+        return [self._result_n(c["saga_id"], c["session_id"], n, agents, raw[agent_off[k]: agent_off[k + 1]],
+                               c["failure_agent_did"])
+                for k, (c, agents, n) in enumerate(per_case)]
+
+    def attribute_tensors(self, node_offsets, agent_offsets, agent_of_node, success, root_cause, risk_weight):
+        """Tensor-native K21 (inputs on one device, int32 CSR offsets per case /
+        agent, u8 flags, fp64 ω per node) → (raw, normalised) fp64 scores per
+        (case, agent) on that device; a zero case total divides by 1."""
+        import torch
+
+        from agent_hypervisor_amd.ops import ledger as LG
+
+        raw = LG.attribution_raw(node_offsets, agent_offsets, agent_of_node, success, root_cause, risk_weight)
+        counts = (agent_offsets[1:] - agent_offsets[:-1]).to(torch.int64)
+        case = torch.repeat_interleave(torch.arange(counts.numel(), device=raw.device), counts)
+        total = torch.zeros(counts.numel(), dtype=raw.dtype, device=raw.device).index_add_(0, case, raw)
+        total = torch.where(total == 0, torch.ones_like(total), total)
+        return raw, raw / total[case]
+
+    def _result_n(self, saga_id, session_id, n_nodes: int, agents, vals, failure_agent_did) -> AttributionResult:
+        total = sum(vals) or 1.0
+        attrs = [
+            FaultAttribution(
+                agent_did=a,
+                liability_score=round(r / total, 4),
+                causal_contribution=round(r, 4),
+                is_direct_cause=a == failure_agent_did,
+                reason="Direct cause of failure" if a == failure_agent_did else "Contributing factor",
+            )
+            for a, r in zip(agents, vals)
+        ]
+        attrs.sort(key=lambda x: x.liability_score, reverse=True)
+        res = AttributionResult(saga_id=saga_id, session_id=session_id, attributions=attrs,
+                                causal_chain_length=n_nodes, root_cause_agent=failure_agent_did)
+        self._history.append(res)
+        return res
 
     @property
     def attribution_history(self) -> list[AttributionResult]:

@@ -18,10 +18,11 @@ that :func:`reason_text` turns back into the exact strings below.
 
 from __future__ import annotations
 
+from collections.abc import Sequence
 from dataclasses import dataclass
 from typing import Optional
 
-from hypervisor.models import ActionDescriptor, ExecutionRing
+from hypervisor.models import ActionDescriptor, ExecutionRing, ReversibilityLevel
 
 # Reason codes shared with the device kernel (semantics.h: RingReason).
 REASON_GRANTED = 0
@@ -41,6 +42,77 @@ class RingCheckResult:
     reason: str
     requires_consensus: bool = False
     requires_sre_witness: bool = False
+
+
+class RingCheckBatch(Sequence):
+    """Results of :meth:`RingEnforcer.check_batch`: the K02 decisions as arrays
+    (``allowed``, ``required``, ``reason_code``, ``agent_ring``, ``sigma_eff``)
+    and, per index, the :class:`RingCheckResult` :meth:`RingEnforcer.check`
+    returns (built on access)."""
+
+    __slots__ = ("_enf", "agent_ring", "required", "reason_code", "sigma_eff")
+
+    def __init__(self, enf, agent_ring, required, reason_code, sigma_eff) -> None:
+        self._enf = enf
+        self.agent_ring, self.required, self.reason_code, self.sigma_eff = agent_ring, required, reason_code, sigma_eff
+
+    @property
+    def allowed(self):
+        return self.reason_code == REASON_GRANTED
+
+    def __len__(self) -> int:
+        return len(self.reason_code)
+
+    def _one(self, i: int) -> RingCheckResult:
+        return self._make(int(self.agent_ring[i]), int(self.required[i]), int(self.reason_code[i]),
+                          float(self.sigma_eff[i]), {})
+
+    def _make(self, ar: int, req: int, code: int, sig: float, texts: dict) -> RingCheckResult:
+        if code == REASON_RING1_SIGMA or code == REASON_RING2_SIGMA:
+            reason = self._enf.reason_text(code, ar, req, sig)
+        else:  # the other reasons depend on (code, rings) only: formatted once per batch
+            key = (code, ar, req)
+            reason = texts.get(key)
+            if reason is None:
+                reason = texts[key] = self._enf.reason_text(code, ar, req, sig)
+        r = _new(RingCheckResult)
+        r.__dict__.update(allowed=code == REASON_GRANTED, required_ring=_RINGS[req], agent_ring=_RINGS[ar],
+                          sigma_eff=sig, reason=reason, requires_consensus=code == REASON_NEEDS_CONSENSUS,
+                          requires_sre_witness=code == REASON_NEEDS_WITNESS)
+        return r
+
+    def __iter__(self):
+        texts: dict = {}
+        make = self._make
+        for ar, req, code, sig in zip(self.agent_ring.tolist(), self.required.tolist(), self.reason_code.tolist(),
+                                      self.sigma_eff.tolist()):
+            yield make(ar, req, code, sig, texts)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return list(self)[i]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        return self._one(i)
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, RingCheckBatch):
+            other = list(other)
+        try:
+            return len(other) == len(self) and all(x == y for x, y in zip(self, other))
+        except TypeError:
+            return NotImplemented
+
+    __hash__ = None  # type: ignore[assignment]
+
+    def __repr__(self) -> str:
+        return f"RingCheckBatch(n={len(self)}, allowed={int(self.allowed.sum())})"
+
+
+_RINGS = list(ExecutionRing)
+_new = object.__new__
 
 
 class RingEnforcer:
@@ -115,37 +187,51 @@ class RingEnforcer:
         has_consensus=None,
         has_sre_witness=None,
         device="cpu",
-    ) -> list[RingCheckResult]:
+    ) -> "RingCheckBatch":
         """:meth:`check` for many (agent ring, action, σ_eff) triples with one
-        K02 launch on ``device`` (``cpu`` runs the kernel's host twin)."""
+        K02 launch on ``device`` (``cpu`` runs the kernel's host twin).
+
+        Inputs are packed column-wise (one vectorized pass per field); the result
+        is a :class:`RingCheckBatch` — a sequence equal, element for element, to
+        ``[check(...) for ...]`` whose :class:`RingCheckResult` objects (and their
+        reason strings) are built only when read, with the decisions also
+        available as arrays (``allowed``, ``required``, ``reason_code``)."""
+        import numpy as np
         import torch
 
         from agent_hypervisor_amd.ops import rings as RG
 
         n = len(actions)
-        flags = [RG.action_flags(a.is_admin, a.is_read_only, a.required_ring is ExecutionRing.RING_1_PRIVILEGED)
-                 for a in actions]
-        u8 = torch.uint8
-        cons = [bool(x) for x in (has_consensus or [False] * n)]
-        wit = [bool(x) for x in (has_sre_witness or [False] * n)]
-        packed = torch.tensor([[int(ExecutionRing(r).value) for r in agent_rings], flags, cons, wit], dtype=u8)
-        packed = packed.to(device)
-        sig = torch.tensor([float(s) for s in sigma_effs], dtype=torch.float64).to(device)
-        req, reason = RG.ring_check(packed[0], packed[1], sig, packed[2], packed[3])
-        host = torch.stack([req, reason]).cpu().tolist()
-        out = []
-        for i in range(n):
-            ar, required, code = ExecutionRing(agent_rings[i]), ExecutionRing(host[0][i]), host[1][i]
-            out.append(RingCheckResult(
-                allowed=code == REASON_GRANTED,
-                required_ring=required,
-                agent_ring=ar,
-                sigma_eff=float(sigma_effs[i]),
-                reason=self.reason_text(code, ar.value, required.value, float(sigma_effs[i])),
-                requires_consensus=code == REASON_NEEDS_CONSENSUS,
-                requires_sre_witness=code == REASON_NEEDS_WITNESS,
-            ))
-        return out
+        none = ReversibilityLevel.NONE
+        flags = (np.fromiter((a.is_admin for a in actions), dtype=np.uint8, count=n) * RG.ACT_ADMIN
+                 | np.fromiter((a.is_read_only for a in actions), dtype=np.uint8, count=n) * RG.ACT_READ_ONLY
+                 | np.fromiter((a.reversibility is none or a.reversibility == "none" for a in actions),
+                               dtype=np.uint8, count=n) * RG.ACT_IRREVERSIBLE)
+        ring = np.fromiter(agent_rings, dtype=np.uint8, count=n)
+        sig = np.fromiter(sigma_effs, dtype=np.float64, count=n)
+        zeros = None
+        cons = np.fromiter(has_consensus, dtype=np.uint8, count=n) if has_consensus is not None else None
+        wit = np.fromiter(has_sre_witness, dtype=np.uint8, count=n) if has_sre_witness is not None else None
+        if cons is None or wit is None:
+            zeros = np.zeros(n, dtype=np.uint8)
+        packed = torch.from_numpy(np.stack([ring, flags, cons if cons is not None else zeros,
+                                            wit if wit is not None else zeros])).to(device)
+        req, reason = RG.ring_check(packed[0], packed[1], torch.from_numpy(sig).to(device), packed[2], packed[3])
+        host = torch.stack([req, reason]).cpu().numpy()
+        return RingCheckBatch(self, ring, host[0], host[1], sig)
+
+    def check_tensors(self, agent_ring, action_flags, sigma_eff, has_consensus=None, has_sre_witness=None):
+        """Tensor-native K02: u8 rings / action flags (``ops.rings.action_flags``),
+        fp64 σ_eff, u8 consensus / witness — all on one device — → (required ring,
+        reason code) u8 tensors on that device (0 = granted)."""
+        import torch
+
+        from agent_hypervisor_amd.ops import rings as RG
+
+        z = torch.zeros_like(agent_ring)
+        return RG.ring_check(agent_ring, action_flags, sigma_eff,
+                             z if has_consensus is None else has_consensus,
+                             z if has_sre_witness is None else has_sre_witness)
 
     def compute_ring(self, sigma_eff: float, has_consensus: bool = False) -> ExecutionRing:
         return ExecutionRing.from_sigma_eff(sigma_eff, has_consensus)

@@ -260,6 +260,9 @@ def test_attribution_batch_matches_attribute(device):
                        for a in r.attributions))
 
     assert [norm(r) for r in got] == [norm(r) for r in want]
+    # unsorted too: the same ranking, ties included
+    assert [[(a.agent_did, a.liability_score) for a in r.attributions] for r in got] == \
+        [[(a.agent_did, a.liability_score) for a in r.attributions] for r in want]
 
 
 @pytest.mark.parametrize("device", DEVICES)
@@ -305,3 +308,67 @@ def test_tensor_paths_match_host(device):
                                                                       device=lrows.device))
         assert [bool(x) for x in ok.cpu().tolist()] == hw
     assert [_ev(e) for e in hb.breach_history] == [_ev(e) for e in db.breach_history]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_intent_lock_rows_match_sequential_acquire(device):
+    """Tensor-native K20 (acquire_rows / release_rows over the device summaries)
+    grants exactly the requests a sequential host manager grants, across
+    interleaved batches, record-path acquires and releases of both kinds."""
+    import torch
+
+    from hypervisor.session.intent_locks import LockIntent
+
+    rng = random.Random(13)
+    dev = IntentLockManager(device=_dev(device))
+    host = IntentLockManager()
+    agents = [f"did:t{i}" for i in range(5)]
+    paths = [f"/q{i}" for i in range(6)]
+    kinds = list(LockIntent)
+    held = []  # (path, intent, host lock) of row-path grants
+    for step in range(25):
+        batch = [(rng.choice(agents), rng.choice(paths), rng.choice(kinds)) for _ in range(rng.randint(1, 30))]
+        want = []
+        for a, p, k in batch:
+            try:
+                want.append(host.acquire(a, "s", p, k))
+            except Exception:  # noqa: BLE001 - contention / deadlock: refused
+                want.append(None)
+        rows = torch.tensor([dev.resource_row(p) for _, p, _ in batch], dtype=torch.int32, device=_dev(device))
+        ags = torch.tensor([dev.agent_row(a) for a, _, _ in batch], dtype=torch.int32, device=_dev(device))
+        its = torch.tensor([{"read": 0, "write": 1, "exclusive": 2}[k.value] for _, _, k in batch],
+                           dtype=torch.uint8, device=_dev(device))
+        got = dev.acquire_rows(ags, rows, its).cpu().tolist()
+        assert got == [int(w is not None) for w in want], step
+        held += [(p, k, w) for (a, p, k), w in zip(batch, want) if w is not None]
+        rng.shuffle(held)
+        drop, held = held[: len(held) // 3], held[len(held) // 3:]
+        for _, _, w in drop:
+            host.release(w.lock_id)
+        if drop:
+            rel = dev.release_rows(
+                torch.tensor([dev.agent_row(w.agent_did) for _, _, w in drop], dtype=torch.int32, device=_dev(device)),
+                torch.tensor([dev.resource_row(p) for p, _, _ in drop], dtype=torch.int32, device=_dev(device)),
+                torch.tensor([0 if k is LockIntent.READ else 1 for _, k, _ in drop], dtype=torch.uint8,
+                             device=_dev(device)))
+            assert rel.cpu().tolist() == [1] * len(drop)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_intent_locks_more_readers_than_holder_slots(device):
+    from hypervisor.session.intent_locks import LockIntent
+
+    host, dev = IntentLockManager(), IntentLockManager(device=_dev(device))
+
+    def norm(x):
+        return (type(x).__name__, str(x)) if isinstance(x, Exception) else (x.agent_did, x.resource_path, x.intent)
+
+    reads = [(f"did:r{i}", "s", "/hot", LockIntent.READ) for i in range(24)]
+    assert [norm(x) for x in host.acquire_batch(reads)] == [norm(x) for x in dev.acquire_batch(reads)]
+    w = [("did:r0", "s", "/hot", LockIntent.WRITE)]
+    assert [norm(x) for x in host.acquire_batch(w)] == [norm(x) for x in dev.acquire_batch(w)]
+    for i in range(1, 24):
+        assert host.release_agent_locks(f"did:r{i}", "s") == dev.release_agent_locks(f"did:r{i}", "s")
+    got = dev.acquire_batch(w)
+    assert [norm(x) for x in host.acquire_batch(w)] == [norm(x) for x in got]
+    assert not isinstance(got[0], Exception)

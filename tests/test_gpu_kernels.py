@@ -411,7 +411,7 @@ def test_slash_forms_and_sigma_kernels_agree(cuda_device, S, lo, hi):
     scores[scores < 0.1] = float("nan")
     vh = LI.VouchBatch(*[getattr(vb, f).clone() for f in fields])
     want = LI.slash(vh, tgt, omega, scores.clone(), 100, clip_cap=64, with_sigma_eff=True)
-    for mode in ("split", "group", "lane"):
+    for mode in ("split", "wave", "group", "lane"):
         for fused in (True, False):
             v = vb.to("cuda")
             got = LI.slash(v, tgt.cuda(), omega.cuda(), scores.cuda(), 100, clip_cap=64, with_sigma_eff=fused,
