@@ -207,6 +207,38 @@ def _delta_cap(pool, cache, did: str, changes, turn: int) -> int:
     return (n + 8 + 63) & ~63
 
 
+def _pack_deltas(pool, cache, deltas) -> tuple:
+    """Heterogeneous batches: (agent pool ids, change offsets, change rows, the
+    turn-independent part of each delta's record-size bound), one pass, with
+    each distinct DID and change tuple interned / measured once."""
+    did_cache: dict = {}
+    ch_cache: dict = {}
+    intern = pool.intern
+    d_pool = []
+    base = np.empty(len(deltas), dtype=np.int64)
+    ch_off, ch_rows = [0], []
+    for k, (did, chs) in enumerate(deltas):
+        d = did_cache.get(did)
+        if d is None:
+            d = did_cache[did] = (intern(did), _FIXED + _escaped_len(pool, cache, did))
+        d_pool.append(d[0])
+        n = d[1]
+        for j, c in enumerate(chs):
+            e = ch_cache.get(c)
+            if e is None:
+                prev = c[3] if len(c) > 3 else None
+                e = ch_cache[c] = ([intern(c[0]), intern(c[1]), intern(c[2]) if c[2] is not None else -1,
+                                    intern(prev) if prev is not None else -1],
+                                   17 + 15 + 10 + 19 + 1 + _escaped_len(pool, cache, c[2])
+                                   + _escaped_len(pool, cache, c[1]) + _escaped_len(pool, cache, c[0])
+                                   + _escaped_len(pool, cache, prev))
+            ch_rows.append(e[0])
+            n += e[1] + (2 if j else 0)
+        ch_off.append(len(ch_rows))
+        base[k] = n
+    return d_pool, ch_off, ch_rows, base
+
+
 def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
     """Build the batch arrays, run the store pipeline, register lazy sessions."""
     import time
@@ -239,12 +271,34 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
     def cfg(s):
         return s.config or SessionConfig()
 
-    creator = per_session(lambda s: st.agent_id(s.creator_did), np.int32)
-    maxpart = per_session(lambda s: int(cfg(s).max_participants), np.int32)
-    minsig = per_session(lambda s: float(cfg(s).min_sigma_eff), np.float64)
-    flags = per_session(lambda s: (1 if cfg(s).enable_audit else 0)
-                        | (2 if ConsistencyMode(cfg(s).consistency_mode) is ConsistencyMode.STRONG else 0)
-                        | (4 if s.activate else 0) | (8 if s.terminate else 0) | (16 if s.compensate else 0), np.uint8)
+    cfg_cache: dict = {}
+
+    def cfg_row(s):  # (max_participants, min_sigma_eff, audit | strong) per distinct config object
+        c = s.config
+        r = cfg_cache.get(id(c))
+        if r is None:
+            cc = c or SessionConfig()
+            r = cfg_cache[id(c)] = (int(cc.max_participants), float(cc.min_sigma_eff),
+                                    (1 if cc.enable_audit else 0)
+                                    | (2 if ConsistencyMode(cc.consistency_mode) is ConsistencyMode.STRONG else 0), c)
+        return r
+
+    if shared:
+        creator = per_session(lambda s: st.agent_id(s.creator_did), np.int32)
+        mp, ms, cf, _ = cfg_row(specs)
+        maxpart = np.full(n, mp, dtype=np.int32)
+        minsig = np.full(n, ms, dtype=np.float64)
+        flags = np.full(n, cf | (4 if specs.activate else 0) | (8 if specs.terminate else 0)
+                        | (16 if specs.compensate else 0), dtype=np.uint8)
+    else:
+        aid = st.agent_id
+        rows_ = [cfg_row(s) for s in specs]
+        creator = np.fromiter((aid(s.creator_did) for s in specs), dtype=np.int32, count=n)
+        maxpart = np.fromiter((r[0] for r in rows_), dtype=np.int32, count=n)
+        minsig = np.fromiter((r[1] for r in rows_), dtype=np.float64, count=n)
+        flags = np.fromiter((r[2] | (4 if s.activate else 0) | (8 if s.terminate else 0)
+                             | (16 if s.compensate else 0) for r, s in zip(rows_, specs)), dtype=np.uint8, count=n)
+        del rows_
 
     def table(get_rows, width_fn):
         """Concatenate per-session row lists: (offsets [n+1], rows)."""
@@ -266,15 +320,18 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         j_agent, j_sigma = np.tile(j_agent, n), np.tile(j_sigma, n)
 
     delta_off, deltas, dk = table(lambda s: s.deltas, None)
-    d_pool = [pool.intern(did) for did, _ in deltas]
-    ch_off, ch_rows = [0], []
+    if not shared:  # one pass with per-string / per-change caches (batches repeat them)
+        d_pool, ch_off, ch_rows, base_caps = _pack_deltas(pool, cache, deltas)
+    else:
+        d_pool = [pool.intern(did) for did, _ in deltas]
+        ch_off, ch_rows = [0], []
+        for k, (did, chs) in enumerate(deltas):
+            for c in chs:
+                ch_rows.append([pool.intern(c[0]), pool.intern(c[1]),
+                                pool.intern(c[2]) if c[2] is not None else -1,
+                                pool.intern(c[3]) if len(c) > 3 and c[3] is not None else -1])
+            ch_off.append(len(ch_rows))
     caps = []
-    for k, (did, chs) in enumerate(deltas):
-        for c in chs:
-            ch_rows.append([pool.intern(c[0]), pool.intern(c[1]),
-                            pool.intern(c[2]) if c[2] is not None else -1,
-                            pool.intern(c[3]) if len(c) > 3 and c[3] is not None else -1])
-        ch_off.append(len(ch_rows))
     if shared:
         per = len(deltas)
         caps = np.tile(np.asarray([_delta_cap(pool, cache, did, chs, t + 1) for t, (did, chs) in enumerate(deltas)],
@@ -285,10 +342,11 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         ch_off_all = np.append(np.tile(base, n) + np.repeat(np.arange(n, dtype=np.int32) * per_ch, per), per_ch * n)
         ch_rows = np.tile(np.asarray(ch_rows or [[0, 0, 0, 0]], dtype=np.int32), (n, 1)) if ch_rows else []
     else:
-        turn_of = []
-        for i in range(n):
-            turn_of.extend(range(1, delta_off[i + 1] - delta_off[i] + 1))
-        caps = [_delta_cap(pool, cache, did, chs, t) for (did, chs), t in zip(deltas, turn_of)]
+        cnt = np.diff(delta_off)
+        turn = np.arange(len(deltas), dtype=np.int64) - np.repeat(delta_off[:-1].astype(np.int64), cnt) + 1
+        digits = np.char.str_len(turn.astype(str)) if len(turn) else np.zeros(0, np.int64)
+        raw = base_caps + 2 * digits + np.where(turn > 1, 66, 4)
+        caps = ((raw + 8 + 63) & ~63).astype(np.int32)
         ch_off_all = ch_off
     nd = len(caps)
     drows, doff = st.reserve_deltas(caps)

@@ -299,12 +299,20 @@ def main() -> None:
         pg = PipelineGraph(eng, S, buf, deltas=args.deltas, stats=stats,
                            refresh_agents=lambda: buf.random_(0, args.agents), reduce=reduce)
 
-        def step():  # noqa: F811 - graph-replay form of the same step
+        def step():  # noqa: F811 - graph-replay form of the same step (liability stage included)
+            side = liab["stream"] if liab is not None else None
+            if side is not None:
+                with torch.cuda.stream(side):
+                    liability_step()
             pg.step()
+            if side is None and liab is not None:
+                liability_step()
             return stats
 
-        def drain():  # noqa: F811 - the graph's collective is in-stream
-            pass
+        def drain():  # noqa: F811 - the graph's collective is in-stream; the liability X01 is not
+            if liab is not None and liab["work"] is not None:
+                liab["work"].wait()
+                liab["work"] = None
 
     for _ in range(args.warmup):
         step()
@@ -381,6 +389,7 @@ def main() -> None:
                 "deltas_per_session": args.deltas,
             },
             "batch_p50_ms": round(statistics.median(lat) * 1000.0, 4),
+            "pipeline_launch": "hipgraph" if args.graph else "stream",
             "vs_baseline_note": "batched GPU throughput / single-threaded Python reference rate (not like-for-like)",
             "device_p50_us": round(device_p50, 2) if device_p50 is not None else None,
             "device_mean_us": round(device_mean, 2) if device_mean is not None else None,

@@ -450,6 +450,31 @@ def config5(ctx: Ctx, args):
              bond_updates_per_s=S * per * ctx.world * args.steps / el)
 
 
+# ------------------------------------------------------------------ config 2 (public API)
+
+
+def config2_api(ctx: Ctx, args):
+    """BASELINE config 2 through the public API: 10⁴–10⁵ concurrent sessions, each
+    a full governance pipeline (joins with σ ring gates, audit deltas, saga steps,
+    terminate with its Merkle root committed) written into the device store by
+    ``Hypervisor.run_pipelines`` — once with the reference template, once with a
+    randomized spec per session (heterogeneous) — and the per-call pipeline under
+    ``asyncio.gather`` for comparison (benchmarks/bench_api.py)."""
+    from benchmarks.bench_api import api_throughput, batch_api_throughput
+
+    n = args.sessions or 100_000
+    dev = str(ctx.dev)
+    t = batch_api_throughput(dev, n, max(1, args.steps // 3))
+    h = batch_api_throughput(dev, n, max(1, args.steps // 5), hetero=True)
+    g = api_throughput(dev, min(n, 10_000), 1)
+    ctx.emit(config="config2_api", what="public API: batched store pipelines (template / heterogeneous) and "
+                                        "per-call asyncio.gather", sessions=n,
+             template_sessions_per_s=t["sessions_per_s"], template_device_ms=t["device_ms"],
+             hetero_sessions_per_s=h["sessions_per_s"], hetero_device_ms=h["device_ms"],
+             gather_pipelines_per_s=g["pipelines_per_s"], gather_concurrent=g["concurrent_pipelines"],
+             ok=bool(t["ok"] and h["ok"] and g["roots_ok"]))
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("configs", nargs="*", default=["config2", "config3", "config4", "config5"])
@@ -469,7 +494,8 @@ def main():
     args = ap.parse_args()
     ctx = Ctx(args.device)
     for c in args.configs:
-        {"config2": config2, "config3": config3, "config4": config4, "config5": config5}[c](ctx, args)
+        {"config2": config2, "config2_api": config2_api, "config3": config3, "config4": config4,
+         "config5": config5}[c](ctx, args)
     if ctx.world > 1:
         dist.destroy_process_group()
 

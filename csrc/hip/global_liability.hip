@@ -119,28 +119,77 @@ struct ClipArgs {
   unsigned long long* cursor;  // [1] pairs written (may exceed cap: overflow is counted, not written)
 };
 
+// Each lane owns one slashed vouchee and walks its in-edges kClipUnroll at a
+// time: the edge ids, then their liveness words, are requested for the whole
+// group at once (two round trips per group instead of two per edge); the claim
+// (atomicAnd on the active byte) keeps the release-once semantics, and the
+// wave's released edges take their pair slots with one cursor atomic per wave
+// (ballot + mbcnt prefix) instead of one per edge.
+constexpr int kClipUnroll = 8;
+
 __global__ __launch_bounds__(256) void slash_clip_kernel(ClipArgs a) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.k; i += stride) {
-    const int32_t v = a.ids[i];
-    for (int64_t j = a.offsets[v]; j < a.offsets[v + 1]; ++j) {
-      const int32_t e = a.edge[j];
-      const uint8_t act = a.active[e];
-      const int64_t ex = a.expiry[e];
-      if (!act || (ex >= 0 && a.now_us > ex)) continue;
-      // claim the bond: the same vouchee may appear twice in one storm, and a bond
-      // is released (and its voucher clipped) once — as the sequential engine does
-      const uintptr_t addr = reinterpret_cast<uintptr_t>(a.active + e);
-      unsigned int* word = reinterpret_cast<unsigned int*>(addr & ~uintptr_t(3));
-      const unsigned int shift = static_cast<unsigned int>(addr & 3u) * 8u;
-      const unsigned int old = atomicAnd(word, ~(0xffu << shift));
-      if (((old >> shift) & 0xffu) == 0u) continue;
-      a.released[e] = a.now_us;
-      const unsigned long long slot = atomicAdd(a.cursor, 1ull);
-      if (slot < static_cast<unsigned long long>(a.cap)) {
-        a.pair_id[slot] = a.src[j];
-        a.pair_factor[slot] = 1.0 - a.omega;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (int64_t i0 = base - threadIdx.x % 64; i0 < a.k; i0 += stride) {  // wave-uniform trip count
+    const int64_t i = i0 + threadIdx.x % 64;
+    const bool mine = i < a.k;
+    const int32_t v = mine ? a.ids[i] : 0;
+    int64_t j = mine ? a.offsets[v] : 0;
+    const int64_t j1 = mine ? a.offsets[v + 1] : 0;
+    while (__any(j < j1)) {
+      int32_t e[kClipUnroll], src[kClipUnroll];
+#pragma unroll
+      for (int u = 0; u < kClipUnroll; ++u) {
+        const bool in = j + u < j1;
+        e[u] = in ? a.edge[j + u] : -1;
+        src[u] = in ? a.src[j + u] : -1;
       }
+      bool take[kClipUnroll];
+#pragma unroll
+      for (int u = 0; u < kClipUnroll; ++u) {
+        take[u] = false;
+        if (e[u] < 0) continue;
+        const uint8_t act = a.active[e[u]];
+        const int64_t ex = a.expiry[e[u]];
+        take[u] = act && !(ex >= 0 && a.now_us > ex);
+      }
+#pragma unroll
+      for (int u = 0; u < kClipUnroll; ++u) {
+        if (!take[u]) continue;
+        // claim the bond: the same vouchee may appear twice in one storm, and a bond
+        // is released (and its voucher clipped) once — as the sequential engine does
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(a.active + e[u]);
+        unsigned int* word = reinterpret_cast<unsigned int*>(addr & ~uintptr_t(3));
+        const unsigned int shift = static_cast<unsigned int>(addr & 3u) * 8u;
+        const unsigned int old = atomicAnd(word, ~(0xffu << shift));
+        take[u] = ((old >> shift) & 0xffu) != 0u;
+        if (take[u]) a.released[e[u]] = a.now_us;
+      }
+      int mine_n = 0;
+#pragma unroll
+      for (int u = 0; u < kClipUnroll; ++u) mine_n += take[u] ? 1 : 0;
+      // wave-aggregated slots: prefix over lanes of their release counts
+      int pre = mine_n;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(pre, d, 64);
+        if ((threadIdx.x % 64) >= d) pre += y;
+      }
+      const int total = __shfl(pre, 63, 64);
+      unsigned long long slot0 = 0;
+      if ((threadIdx.x % 64) == 63 && total > 0) slot0 = atomicAdd(a.cursor, static_cast<unsigned long long>(total));
+      slot0 = __shfl(slot0, 63, 64);
+      unsigned long long slot = slot0 + static_cast<unsigned long long>(pre - mine_n);
+#pragma unroll
+      for (int u = 0; u < kClipUnroll; ++u) {
+        if (!take[u]) continue;
+        if (slot < static_cast<unsigned long long>(a.cap)) {
+          a.pair_id[slot] = src[u];
+          a.pair_factor[slot] = 1.0 - a.omega;
+        }
+        ++slot;
+      }
+      j += kClipUnroll;
     }
   }
 }

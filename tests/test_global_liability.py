@@ -63,3 +63,41 @@ def test_global_liability_cpu_twin():
 @pytest.mark.gpu
 def test_global_liability_gfx950(cuda_device):
     _run("cuda")
+
+
+def _run_storm(dev: str) -> None:
+    """A larger storm: duplicate ids, in-degrees past the 8-edge unroll, a pair
+    buffer smaller than the releases (the cursor still counts every one)."""
+    g = torch.Generator().manual_seed(11)
+    b = ResidentBonds(5000, 12, dev, seed=9)
+    b.active[::5] = 0
+    active_before = b.active.cpu().clone()
+    ids = torch.randint(0, 5000, (1500,), generator=g, dtype=torch.int32)
+    ids[::10] = ids[1::10]  # duplicates within the storm
+    vr, ve = b.voucher.tolist(), b.vouchee.tolist()
+    hit = set(ids.tolist())
+    want = sorted(vr[e] for e in range(b.edges) if ve[e] in hit and active_before[e])
+    for cap in (4 * len(want), len(want) // 3):
+        bb = ResidentBonds(5000, 12, dev, seed=9)
+        bb.active[::5] = 0
+        pid = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        pf = torch.ones(cap, dtype=torch.float64, device=dev)
+        cur = torch.zeros(1, dtype=torch.int64, device=dev)
+        bb.slash_clip(ids.to(dev), 0.9, pid, pf, cur)
+        assert int(cur.item()) == len(want)
+        got = sorted(x for x in pid.cpu().tolist() if x >= 0)
+        if cap >= len(want):
+            assert got == want
+        else:
+            assert len(got) == cap and not (set(got) - set(want))
+        act = bb.active.cpu()
+        assert all(int(act[e]) == 0 for e in range(bb.edges) if ve[e] in hit)
+
+
+def test_slash_clip_storm_cpu_twin():
+    _run_storm("cpu")
+
+
+@pytest.mark.gpu
+def test_slash_clip_storm_gfx950(cuda_device):
+    _run_storm("cuda")
