@@ -207,36 +207,13 @@ def _delta_cap(pool, cache, did: str, changes, turn: int) -> int:
     return (n + 8 + 63) & ~63
 
 
-def _pack_deltas(pool, cache, deltas) -> tuple:
-    """Heterogeneous batches: (agent pool ids, change offsets, change rows, the
-    turn-independent part of each delta's record-size bound), one pass, with
-    each distinct DID and change tuple interned / measured once."""
-    did_cache: dict = {}
-    ch_cache: dict = {}
-    intern = pool.intern
-    d_pool = []
-    base = np.empty(len(deltas), dtype=np.int64)
-    ch_off, ch_rows = [0], []
-    for k, (did, chs) in enumerate(deltas):
-        d = did_cache.get(did)
-        if d is None:
-            d = did_cache[did] = (intern(did), _FIXED + _escaped_len(pool, cache, did))
-        d_pool.append(d[0])
-        n = d[1]
-        for j, c in enumerate(chs):
-            e = ch_cache.get(c)
-            if e is None:
-                prev = c[3] if len(c) > 3 else None
-                e = ch_cache[c] = ([intern(c[0]), intern(c[1]), intern(c[2]) if c[2] is not None else -1,
-                                    intern(prev) if prev is not None else -1],
-                                   17 + 15 + 10 + 19 + 1 + _escaped_len(pool, cache, c[2])
-                                   + _escaped_len(pool, cache, c[1]) + _escaped_len(pool, cache, c[0])
-                                   + _escaped_len(pool, cache, prev))
-            ch_rows.append(e[0])
-            n += e[1] + (2 if j else 0)
-        ch_off.append(len(ch_rows))
-        base[k] = n
-    return d_pool, ch_off, ch_rows, base
+class _CfgHolder:
+    """A spec-shaped holder of one config (cfg_row caches by the config object)."""
+
+    __slots__ = ("config",)
+
+    def __init__(self, config) -> None:
+        self.config = config
 
 
 def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
@@ -290,50 +267,22 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         minsig = np.full(n, ms, dtype=np.float64)
         flags = np.full(n, cf | (4 if specs.activate else 0) | (8 if specs.terminate else 0)
                         | (16 if specs.compensate else 0), dtype=np.uint8)
-    else:
-        aid = st.agent_id
-        rows_ = [cfg_row(s) for s in specs]
-        creator = np.fromiter((aid(s.creator_did) for s in specs), dtype=np.int32, count=n)
-        maxpart = np.fromiter((r[0] for r in rows_), dtype=np.int32, count=n)
-        minsig = np.fromiter((r[1] for r in rows_), dtype=np.float64, count=n)
-        flags = np.fromiter((r[2] | (4 if s.activate else 0) | (8 if s.terminate else 0)
-                             | (16 if s.compensate else 0) for r, s in zip(rows_, specs)), dtype=np.uint8, count=n)
-        del rows_
-
-    def table(get_rows, width_fn):
-        """Concatenate per-session row lists: (offsets [n+1], rows)."""
-        if shared:
-            rows = list(get_rows(specs))
-            k = len(rows)
-            return np.arange(0, (n + 1) * k, k, dtype=np.int32), rows, k
-        off, out = [0], []
-        for s in specs:
-            r = list(get_rows(s))
-            out.extend(r)
-            off.append(len(out))
-        return np.asarray(off, dtype=np.int32), out, None
-
-    join_off, joins, jk = table(lambda s: s.joins, None)
-    j_agent = np.asarray([st.agent_id(d) for d, _ in joins], dtype=np.int32)
-    j_sigma = np.asarray([float(x) for _, x in joins], dtype=np.float64)
-    if shared:
-        j_agent, j_sigma = np.tile(j_agent, n), np.tile(j_sigma, n)
-
-    delta_off, deltas, dk = table(lambda s: s.deltas, None)
-    if not shared:  # one pass with per-string / per-change caches (batches repeat them)
-        d_pool, ch_off, ch_rows, base_caps = _pack_deltas(pool, cache, deltas)
-    else:
+        joins = list(specs.joins)
+        j_agent = np.tile(np.asarray([st.agent_id(d) for d, _ in joins], dtype=np.int32), n)
+        j_sigma = np.tile(np.asarray([float(x) for _, x in joins], dtype=np.float64), n)
+        k = len(joins)
+        join_off = np.arange(0, (n + 1) * k, k, dtype=np.int32) if k else np.zeros(n + 1, dtype=np.int32)
+        deltas = list(specs.deltas)
+        per = len(deltas)
+        delta_off = np.arange(0, (n + 1) * per, per, dtype=np.int32) if per else np.zeros(n + 1, dtype=np.int32)
         d_pool = [pool.intern(did) for did, _ in deltas]
         ch_off, ch_rows = [0], []
-        for k, (did, chs) in enumerate(deltas):
+        for did, chs in deltas:
             for c in chs:
                 ch_rows.append([pool.intern(c[0]), pool.intern(c[1]),
                                 pool.intern(c[2]) if c[2] is not None else -1,
                                 pool.intern(c[3]) if len(c) > 3 and c[3] is not None else -1])
             ch_off.append(len(ch_rows))
-    caps = []
-    if shared:
-        per = len(deltas)
         caps = np.tile(np.asarray([_delta_cap(pool, cache, did, chs, t + 1) for t, (did, chs) in enumerate(deltas)],
                                   dtype=np.int32), n)
         d_pool = np.tile(np.asarray(d_pool, dtype=np.int32), n)
@@ -341,18 +290,33 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         per_ch = ch_off[-1]
         ch_off_all = np.append(np.tile(base, n) + np.repeat(np.arange(n, dtype=np.int32) * per_ch, per), per_ch * n)
         ch_rows = np.tile(np.asarray(ch_rows or [[0, 0, 0, 0]], dtype=np.int32), (n, 1)) if ch_rows else []
-    else:
+        steps = list(specs.steps)
+        ks = len(steps)
+        step_off = np.arange(0, (n + 1) * ks, ks, dtype=np.int32) if ks else np.zeros(n + 1, dtype=np.int32)
+        s_undo = np.tile(np.asarray([1 if x[3] else 0 for x in steps], dtype=np.uint8), n)
+        s_retry = np.tile(np.asarray([int(x[4]) for x in steps], dtype=np.int32), n)
+        s_fail = np.tile(np.asarray([min(255, int(x[5])) for x in steps], dtype=np.uint8), n)
+    else:  # one spec per session: flattened natively (csrc/host/py_runtime.cpp pack_specs)
+        packed = C.pack_specs(specs, st.agents._pool, pool._pool, lambda c: cfg_row(_CfgHolder(c))[:3], _FIXED)
+        col = lambda k, dt: np.frombuffer(packed[k], dtype=dt)  # noqa: E731
+        creator, maxpart, minsig, flags = col("creator", np.int32), col("maxpart", np.int32), \
+            col("minsig", np.float64), col("flags", np.uint8)
+        join_off, j_agent, j_sigma = col("join_off", np.int32), col("join_agent", np.int32), \
+            col("join_sigma", np.float64)
+        delta_off, d_pool, base_caps = col("delta_off", np.int32), col("d_pool", np.int32), col("base_caps", np.int64)
+        ch_off_all = col("ch_off", np.int32)
+        ch_rows = col("ch_rows", np.int32).reshape(-1, 4)
+        step_off, s_undo, s_retry, s_fail = col("step_off", np.int32), col("s_undo", np.uint8), \
+            col("s_retry", np.int32), col("s_fail", np.uint8)
+        nd_ = len(d_pool)
         cnt = np.diff(delta_off)
-        turn = np.arange(len(deltas), dtype=np.int64) - np.repeat(delta_off[:-1].astype(np.int64), cnt) + 1
-        digits = np.char.str_len(turn.astype(str)) if len(turn) else np.zeros(0, np.int64)
-        raw = base_caps + 2 * digits + np.where(turn > 1, 66, 4)
-        caps = ((raw + 8 + 63) & ~63).astype(np.int32)
-        ch_off_all = ch_off
+        turn = np.arange(nd_, dtype=np.int64) - np.repeat(delta_off[:-1].astype(np.int64), cnt) + 1
+        digits = np.char.str_len(turn.astype(str)) if nd_ else np.zeros(0, np.int64)
+        caps = ((base_caps + 2 * digits + np.where(turn > 1, 66, 4) + 8 + 63) & ~63).astype(np.int32)
     nd = len(caps)
     drows, doff = st.reserve_deltas(caps)
     dsess = np.repeat(np.arange(n, dtype=np.int32), np.diff(delta_off))
 
-    step_off, steps, sk = table(lambda s: s.steps, None)
     has_saga = np.diff(step_off) > 0
     gslots = np.full(n, -1, dtype=np.int32)
     ng = int(has_saga.sum())
@@ -360,14 +324,6 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
         gslots[has_saga] = st.alloc_many("G", ng)
     nsteps = int(step_off[-1])
     tslots = np.asarray(st.alloc_many("T", nsteps), dtype=np.int32) if nsteps else np.zeros(0, dtype=np.int32)
-    if shared:
-        s_undo = np.tile(np.asarray([1 if x[3] else 0 for x in steps], dtype=np.uint8), n)
-        s_retry = np.tile(np.asarray([int(x[4]) for x in steps], dtype=np.int32), n)
-        s_fail = np.tile(np.asarray([min(255, int(x[5])) for x in steps], dtype=np.uint8), n)
-    else:
-        s_undo = np.asarray([1 if x[3] else 0 for x in steps], dtype=np.uint8)
-        s_retry = np.asarray([int(x[4]) for x in steps], dtype=np.int32)
-        s_fail = np.asarray([min(255, int(x[5])) for x in steps], dtype=np.uint8)
 
     def T(a, dtype=None):
         arr = np.array(a if dtype is None else np.asarray(a, dtype=dtype), copy=True, order="C")

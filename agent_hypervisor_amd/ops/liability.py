@@ -166,6 +166,7 @@ def bond_fused(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us:
 
 
 SIGMA_KERNEL = os.environ.get("AHV_SIGMA_KERNEL", "stream")
+_CLIP_OFFS: dict = {}
 
 
 def sigma_eff_exact(vb: VouchBatch, sigma: torch.Tensor, omega: torch.Tensor, now_us: int,
@@ -230,6 +231,7 @@ class SlashOutcome:
     clip_before: torch.Tensor  # f64 [S, cap]
     clip_after: torch.Tensor  # f64 [S, cap]
     sigma_eff: Optional[torch.Tensor] = None  # f64 [S,16] post-slash σ_eff (fused K03), or None
+    touched: Optional[torch.Tensor] = None  # i64 [T] sessions with ≥ 1 clip (with_touched), or None
 
     @property
     def truncated(self) -> torch.Tensor:
@@ -247,6 +249,7 @@ def slash(
     zero_records: bool = True,
     with_sigma_eff: bool = False,
     mode: Optional[str] = None,
+    with_touched: bool = False,
 ) -> SlashOutcome:
     """K06: slash ``target[s]`` in every session (cascade ≤ 2), mutating ``vb``
     (bonds released) and ``scores`` in place, like SlashingEngine.slash.  A
@@ -269,10 +272,20 @@ def slash(
     ``mode`` picks the device form (all give identical results): ``"split"``
     (default: cascade over the slashed sessions only, then the streaming σ_eff
     pass), ``"wave"`` (the same split, one session per wave), ``"group"`` (one
-    16-lane pass per session doing both) or ``"lane"``."""
+    16-lane pass per session doing both) or ``"lane"``.
+
+    ``with_touched=True`` also returns :attr:`SlashOutcome.touched`: the sessions
+    with at least one clip, in session order (int64) — compacted on the device
+    (the split cascade writes per-window segments; two small kernels place them),
+    which costs one 8-byte read of the count instead of a ``torch.nonzero``."""
     S = vb.sessions
     dev = vb.device
-    offs = (torch.arange(S, dtype=i32, device=dev) * clip_cap).contiguous()
+    key = (S, int(clip_cap), str(dev))
+    offs = _CLIP_OFFS.get(key)
+    if offs is None:  # read-only record offsets s·cap, made once per shape (not a launch per storm)
+        if len(_CLIP_OFFS) >= 8:
+            _CLIP_OFFS.pop(next(iter(_CLIP_OFFS)))
+        offs = _CLIP_OFFS[key] = (torch.arange(S, dtype=i32, device=dev) * clip_cap).contiguous()
     alloc = torch.zeros if zero_records else torch.empty
     out = SlashOutcome(
         scores=scores,
@@ -286,6 +299,14 @@ def slash(
     if with_sigma_eff:
         out.sigma_eff = torch.empty((S, TILE), dtype=f64, device=dev)
         fused = dict(bonded=vb.bonded, sigma_eff=out.sigma_eff)
+    if with_touched:
+        nb = (S + 255) // 256
+        tt = dict(touched_tmp=torch.empty(max(S, 1), dtype=i32, device=dev),
+                  touched_blocks=torch.empty(nb, dtype=i32, device=dev),
+                  touched_offsets=torch.empty(nb, dtype=i32, device=dev),
+                  touched=torch.empty(max(S, 1), dtype=i64, device=dev),
+                  touched_total=torch.zeros(1, dtype=i64, device=dev))
+        fused.update(tt)
     launch(
         "slash",
         {"sessions": S, "now_us": int(now_us), "clip_cap": int(clip_cap),
@@ -297,6 +318,8 @@ def slash(
              clip_walk=torch.empty(max(int(vb.voucher.numel()), 1), dtype=u8, device=dev), **fused),
         dict(target=u8, omega=f64, scores=f64, bonded=f64),
     )
+    if with_touched:
+        out.touched = fused["touched"][: int(fused["touched_total"].item())]
     return out
 
 

@@ -423,12 +423,14 @@ def config5(ctx: Ctx, args):
         active, released, scores = fresh.pop()
         vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, active, vb0.expiry_us, released)
         # ≤ 1 clip per edge; σ_eff over the post-slash bonds fused into the same pass (K06+K03)
-        out = LI.slash(vb, tgt, omega, scores, 1, clip_cap=per, zero_records=False, with_sigma_eff=not args.unfused)
+        out = LI.slash(vb, tgt, omega, scores, 1, clip_cap=per, zero_records=False, with_sigma_eff=not args.unfused,
+                       with_touched=True)
         se = out.sigma_eff if not args.unfused else LI.sigma_eff_exact(vb, out.scores, omega, 1)
         # re-chain exactly the sessions the slash touched, after it (data dependency):
         # each gets a slash delta carrying its post-slash scores, then its whole
-        # chain is re-hashed (K08) and its Merkle root recomputed (K09)
-        touched = torch.nonzero(out.clip_count > 0).flatten()
+        # chain is re-hashed (K08) and its Merkle root recomputed (K09); the touched
+        # list comes compacted from the cascade kernel (one 8-byte count read)
+        touched = out.touched
         arena.write_slash_deltas(touched, out.scores)
         packed, sel = arena.resident(touched)
         digests = A.chain_hashes(packed, midstate=not args.no_midstate, uniform_len=D + 1, sel=sel, check=False)

@@ -879,7 +879,7 @@ __device__ __forceinline__ double group_sigma_eff(const int (&ve)[kGroupChunks],
 __device__ __forceinline__ double group_cascade(const SlashArgs& a, int64_t s, int tgt, int32_t b, int j, int gl0,
                                                 uint8_t* cl, const int (&vr)[kGroupChunks],
                                                 const int (&ve)[kGroupChunks], bool (&lv)[kGroupChunks], double sc,
-                                                double omega) {
+                                                double omega, int32_t* nclip_out = nullptr) {
   auto group_bits = [&](bool p) -> uint32_t {
     return static_cast<uint32_t>((__ballot(p) >> gl0) & 0xffffu);
   };
@@ -956,6 +956,7 @@ __device__ __forceinline__ double group_cascade(const SlashArgs& a, int64_t s, i
   }
   a.scores[s * kTile + j] = sc;
   if (j == 0) a.clip_count[s] = nclip;
+  if (nclip_out) *nclip_out = nclip;
   return sc;
 }
 
@@ -1173,6 +1174,7 @@ __global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a)
   __shared__ int32_t s_off[kCascWindow + 1];
   __shared__ int32_t s_wcount[kCascWindow / kWaveLanes];
   __shared__ uint8_t s_cl[kSlashGroupsPerBlock][kGroupEdges];
+  __shared__ int32_t s_nclip[kCascWindow];
   const int t = threadIdx.x;
   const int w = t / kWaveLanes, l = t % kWaveLanes;
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kCascWindow;
@@ -1202,7 +1204,10 @@ __global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a)
     const int64_t s = w0 + ls;
     const int32_t b = s_off[ls], n = s_off[ls + 1] - b;
     if (n > kGroupEdges) {  // beyond the registers: the one-lane global-memory form
-      if (j == 0) slash_session(a, s);
+      if (j == 0) {
+        slash_session(a, s);
+        s_nclip[ls] = a.clip_count[s];  // this thread's own write
+      }
       continue;
     }
     int vr[kGroupChunks], ve[kGroupChunks];
@@ -1216,8 +1221,81 @@ __global__ __launch_bounds__(kCascWindow) void slash_cascade_kernel(SlashArgs a)
       lv[c] = in && live_edge(a.active, a.expiry_us, b + i, a.now_us);
     }
     const double sc = a.scores[s * kTile + j];
-    group_cascade(a, s, tgt, b, j, gl0, s_cl[g], vr, ve, lv, sc, a.omega[s]);
+    int32_t nclip = 0;
+    group_cascade(a, s, tgt, b, j, gl0, s_cl[g], vr, ve, lv, sc, a.omega[s], &nclip);
+    if (j == 0) s_nclip[ls] = nclip;
   }
+  if (a.touched_tmp == nullptr) return;  // block-uniform
+  // touched sessions (≥ 1 clip) of the window, in session order: per-wave ballots
+  // + prefix into a window-local segment; touched_compact places the segments
+  __syncthreads();
+  const bool touched = hit && s_nclip[t] > 0;
+  const uint64_t tm = __ballot(touched);
+  if (l == 0) s_wcount[w] = __popcll(tm);
+  __syncthreads();
+  int tpre = 0, ttotal = 0;
+#pragma unroll
+  for (int k = 0; k < kCascWindow / kWaveLanes; ++k) {
+    tpre += k < w ? s_wcount[k] : 0;
+    ttotal += s_wcount[k];
+  }
+  if (touched) a.touched_tmp[w0 + tpre + __popcll(tm & ((1ull << l) - 1ull))] = static_cast<int32_t>(s_me);
+  if (t == 0) a.touched_blocks[blockIdx.x] = ttotal;
+}
+
+// Window segments of the touched list from clip_count (the non-split forms).
+__global__ __launch_bounds__(kCascWindow) void touched_flags_kernel(SlashArgs a) {
+  __shared__ int32_t s_wcount[kCascWindow / kWaveLanes];
+  const int t = threadIdx.x, w = t / kWaveLanes, l = t % kWaveLanes;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kCascWindow, s_me = w0 + t;
+  const bool touched = s_me < a.sessions && a.clip_count[s_me] > 0;
+  const uint64_t tm = __ballot(touched);
+  if (l == 0) s_wcount[w] = __popcll(tm);
+  __syncthreads();
+  int tpre = 0, ttotal = 0;
+#pragma unroll
+  for (int k = 0; k < kCascWindow / kWaveLanes; ++k) {
+    tpre += k < w ? s_wcount[k] : 0;
+    ttotal += s_wcount[k];
+  }
+  if (touched) a.touched_tmp[w0 + tpre + __popcll(tm & ((1ull << l) - 1ull))] = static_cast<int32_t>(s_me);
+  if (t == 0) a.touched_blocks[blockIdx.x] = ttotal;
+}
+
+// touched_compact: exclusive prefix of the per-window counts (one workgroup),
+// then every window copies its segment to its offset — the touched list in
+// session order without a device-wide sort or a host round trip per window.
+__global__ __launch_bounds__(1024) void touched_scan_kernel(const int32_t* counts, int64_t nblocks, int32_t* offsets,
+                                                            int64_t* total) {
+  __shared__ int32_t s_sum[1024];
+  __shared__ int32_t s_run;
+  const int t = threadIdx.x;
+  if (t == 0) s_run = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nblocks; base += 1024) {
+    const int32_t c = base + t < nblocks ? counts[base + t] : 0;
+    s_sum[t] = c;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // Hillis–Steele inclusive scan
+      const int32_t y = t >= d ? s_sum[t - d] : 0;
+      __syncthreads();
+      s_sum[t] += y;
+      __syncthreads();
+    }
+    if (base + t < nblocks) offsets[base + t] = s_run + s_sum[t] - c;
+    __syncthreads();
+    if (t == 0) s_run += s_sum[1023];
+    __syncthreads();
+  }
+  if (t == 0) *total = s_run;
+}
+
+__global__ __launch_bounds__(kCascWindow) void touched_copy_kernel(const int32_t* counts, const int32_t* offsets,
+                                                                   const int32_t* tmp, int64_t* out) {
+  const int64_t blk = blockIdx.x;
+  const int32_t c = counts[blk];
+  if (static_cast<int32_t>(threadIdx.x) < c)
+    out[offsets[blk] + threadIdx.x] = tmp[blk * kCascWindow + threadIdx.x];
 }
 
 void launch_slash(const SlashArgs& a, hipStream_t st) {
@@ -1241,6 +1319,7 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
   } else {
     if (mode == 3) hipLaunchKernelGGL(slash_wave_kernel, grid1(a.sessions, 4 * kWaveLanes), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(slash_cascade_kernel, grid1(a.sessions, kCascWindow), dim3(kCascWindow), 0, st, a);
+
     if (a.sigma_eff) {  // K03 over the post-slash scores and bonds
       static const bool csr = [] {  // A/B: AHV_SLASH_SIGMA=csr runs the LDS-staged K03 form
         const char* e = std::getenv("AHV_SLASH_SIGMA");
@@ -1252,12 +1331,26 @@ void launch_slash(const SlashArgs& a, hipStream_t st) {
       else launch_sigma_eff_stream(v, st);
     }
   }
+  if (a.touched_tmp != nullptr) {  // the touched list (split mode: segments written by the cascade)
+    const int64_t nb = (a.sessions + kCascWindow - 1) / kCascWindow;
+    if (mode != 0) hipLaunchKernelGGL(touched_flags_kernel, dim3(static_cast<uint32_t>(nb)), dim3(kCascWindow), 0, st, a);
+    hipLaunchKernelGGL(touched_scan_kernel, dim3(1), dim3(1024), 0, st, a.touched_blocks, nb, a.touched_offsets,
+                       a.touched_total);
+    hipLaunchKernelGGL(touched_copy_kernel, dim3(static_cast<uint32_t>(nb)), dim3(kCascWindow), 0, st,
+                       a.touched_blocks, a.touched_offsets, a.touched_tmp, a.touched);
+  }
   check_hip(hipGetLastError(), "slash_kernel");
 }
 void slash_host(const SlashArgs& a) {
   for (int64_t s = 0; s < a.sessions; ++s) {
     slash_session(a, s);
     if (a.sigma_eff) slash_sigma_row(a, s);
+  }
+  if (a.touched != nullptr) {
+    int64_t n = 0;
+    for (int64_t s = 0; s < a.sessions; ++s)
+      if (a.clip_count[s] > 0) a.touched[n++] = s;
+    *a.touched_total = n;
   }
 }
 

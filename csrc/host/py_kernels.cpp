@@ -223,6 +223,10 @@ static SlashArgs to_slash(const py::dict& d) {
   a.bonded = d.contains("bonded") ? ptr<const double>(d, "bonded") : nullptr;
   a.sigma_eff = d.contains("sigma_eff") ? ptr<double>(d, "sigma_eff") : nullptr;
   a.mode = d.contains("mode") ? val<int32_t>(d, "mode") : -1;
+  if (d.contains("touched") && !d["touched"].is_none()) {
+    P(touched_tmp, int32_t); P(touched_blocks, int32_t); P(touched_offsets, int32_t); P(touched, int64_t);
+    P(touched_total, int64_t);
+  }
   if (a.mode < -1 || a.mode > 3) throw py::value_error("slash: mode must be -1, 0, 1, 2 or 3");
   return a;
 }

@@ -95,6 +95,7 @@ class StringPool {
     return raw_[static_cast<size_t>(id)];
   }
 
+  int32_t esc_len(int32_t id) const { return lengths_[static_cast<size_t>(id)]; }
   size_t size() const { return raw_.size(); }
   size_t nbytes() const { return bytes_.size(); }
 
@@ -139,6 +140,140 @@ static py::str uuid_str(uint64_t seed, uint64_t counter, const std::string& pref
   return py::str(s);
 }
 
+
+// ------------------------------------------------------------------ spec packing
+// Hypervisor.run_pipelines with one PipelineSpec per session: flatten the specs
+// into the batch kernels' columns natively (models/store_pipeline.py documents
+// the columns).  Strings go through the two pools (agents: DIDs of creators and
+// joins; pool: every string a record renders); each distinct config object is
+// read once (None: `cfg_of(None) -> (max_participants, min_sigma_eff,
+// audit|strong flags)` of the default SessionConfig).  The turn-independent part of each delta's record-size
+// bound is computed here from the pool's escaped lengths (+2 quotes, 4 = null).
+
+static std::string utf8_of(const py::handle& o) {
+  Py_ssize_t n = 0;
+  const char* c = PyUnicode_AsUTF8AndSize(o.ptr(), &n);
+  if (c != nullptr) return std::string(c, static_cast<size_t>(n));
+  PyErr_Clear();  // lone surrogates: the pools hold their surrogatepass UTF-8
+  py::bytes b = py::reinterpret_steal<py::bytes>(PyUnicode_AsEncodedString(o.ptr(), "utf-8", "surrogatepass"));
+  if (!b) throw py::error_already_set();
+  return std::string(b);
+}
+
+template <class T>
+static py::bytes as_bytes(const std::vector<T>& v) {
+  return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(T));
+}
+
+static std::tuple<int32_t, double, uint8_t> config_row(const py::handle& c) {
+  static const py::str kMode("consistency_mode"), kMax("max_participants"), kMin("min_sigma_eff"),
+      kAudit("enable_audit");
+  const std::string mode = utf8_of(c.attr(kMode));
+  if (mode != "strong" && mode != "eventual") throw py::value_error("'" + mode + "' is not a valid ConsistencyMode");
+  const int audit = PyObject_IsTrue(c.attr(kAudit).ptr());
+  if (audit < 0) throw py::error_already_set();
+  return {py::int_(c.attr(kMax)).cast<int32_t>(), py::float_(c.attr(kMin)).cast<double>(),
+          static_cast<uint8_t>((audit ? 1 : 0) | (mode == "strong" ? 2 : 0))};
+}
+
+static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool& pool, const py::object& cfg_of,
+                           int64_t fixed) {
+  const size_t n = specs.size();
+  std::vector<int32_t> creator(n), maxpart(n), join_off{0}, join_agent, delta_off{0}, d_pool, ch_off{0}, ch_rows,
+      step_off{0}, s_retry;
+  std::vector<double> minsig(n), join_sigma;
+  std::vector<uint8_t> flags(n), s_undo, s_fail;
+  std::vector<int64_t> base_caps;
+  std::unordered_map<PyObject*, std::tuple<int32_t, double, uint8_t>> cfg_cache;
+  std::unordered_map<PyObject*, int32_t> str_cache;  // per-call: the same str object interned once
+  auto intern = [&](StringPool& p, const py::handle& o) -> int32_t {
+    auto it = str_cache.find(o.ptr());
+    if (&p == &pool && it != str_cache.end()) return it->second;
+    const int32_t id = p.intern(utf8_of(o));
+    if (&p == &pool) str_cache.emplace(o.ptr(), id);
+    return id;
+  };
+  auto esc = [&](const py::handle& o) -> int64_t {  // escaped length with quotes, "null" for None
+    return o.is_none() ? 4 : pool.esc_len(intern(pool, o)) + 2;
+  };
+  static const py::str kJoins("joins"), kDeltas("deltas"), kSteps("steps"), kAct("activate"), kTerm("terminate"),
+      kComp("compensate"), kCfg("config"), kCreator("creator_did");
+  for (size_t i = 0; i < n; ++i) {
+    py::handle sp = specs[i];
+    py::object cfg = sp.attr(kCfg);
+    auto ci = cfg_cache.find(cfg.ptr());
+    if (ci == cfg_cache.end()) {
+      if (cfg.is_none()) {  // the default SessionConfig, resolved by the caller
+        py::tuple r = cfg_of(cfg);
+        ci = cfg_cache.emplace(cfg.ptr(), std::make_tuple(r[0].cast<int32_t>(), r[1].cast<double>(),
+                                                          r[2].cast<uint8_t>())).first;
+      } else {
+        ci = cfg_cache.emplace(cfg.ptr(), config_row(cfg)).first;
+      }
+    }
+    maxpart[i] = std::get<0>(ci->second);
+    minsig[i] = std::get<1>(ci->second);
+    flags[i] = static_cast<uint8_t>(std::get<2>(ci->second) | (PyObject_IsTrue(sp.attr(kAct).ptr()) ? 4 : 0) |
+                                    (PyObject_IsTrue(sp.attr(kTerm).ptr()) ? 8 : 0) |
+                                    (PyObject_IsTrue(sp.attr(kComp).ptr()) ? 16 : 0));
+    creator[i] = intern(agents, sp.attr(kCreator));
+    for (py::handle j : sp.attr(kJoins)) {
+      py::sequence t = py::reinterpret_borrow<py::sequence>(j);
+      join_agent.push_back(intern(agents, t[0]));
+      join_sigma.push_back(py::float_(t[1]).cast<double>());
+    }
+    join_off.push_back(static_cast<int32_t>(join_agent.size()));
+    for (py::handle d : sp.attr(kDeltas)) {
+      py::sequence t = py::reinterpret_borrow<py::sequence>(d);
+      py::object did = t[0];
+      d_pool.push_back(intern(pool, did));
+      int64_t cap = fixed + esc(did);
+      int k = 0;
+      for (py::handle c : py::reinterpret_borrow<py::sequence>(t[1])) {
+        py::sequence ct = py::reinterpret_borrow<py::sequence>(c);
+        const size_t cn = py::len(ct);
+        py::object path = ct[0], op = ct[1], h = ct[2];
+        py::object prev = cn > 3 ? py::object(ct[3]) : py::object(py::none());
+        ch_rows.push_back(intern(pool, path));
+        ch_rows.push_back(intern(pool, op));
+        ch_rows.push_back(h.is_none() ? -1 : intern(pool, h));
+        ch_rows.push_back(prev.is_none() ? -1 : intern(pool, prev));
+        cap += 17 + 15 + 10 + 19 + 1 + (k ? 2 : 0) + esc(h) + esc(op) + esc(path) + esc(prev);
+        ++k;
+      }
+      ch_off.push_back(static_cast<int32_t>(ch_rows.size() / 4));
+      base_caps.push_back(cap);
+    }
+    delta_off.push_back(static_cast<int32_t>(d_pool.size()));
+    for (py::handle st : sp.attr(kSteps)) {
+      py::sequence t = py::reinterpret_borrow<py::sequence>(st);
+      s_undo.push_back(PyObject_IsTrue(py::object(t[3]).ptr()) ? 1 : 0);
+      s_retry.push_back(py::int_(t[4]).cast<int32_t>());
+      const int64_t f = py::int_(t[5]).cast<int64_t>();
+      s_fail.push_back(static_cast<uint8_t>(f < 255 ? f : 255));
+    }
+    step_off.push_back(static_cast<int32_t>(s_undo.size()));
+  }
+  py::dict out;
+  out["creator"] = as_bytes(creator);
+  out["maxpart"] = as_bytes(maxpart);
+  out["minsig"] = as_bytes(minsig);
+  out["flags"] = as_bytes(flags);
+  out["join_off"] = as_bytes(join_off);
+  out["join_agent"] = as_bytes(join_agent);
+  out["join_sigma"] = as_bytes(join_sigma);
+  out["delta_off"] = as_bytes(delta_off);
+  out["d_pool"] = as_bytes(d_pool);
+  out["base_caps"] = as_bytes(base_caps);
+  out["ch_off"] = as_bytes(ch_off);
+  out["ch_rows"] = as_bytes(ch_rows);
+  out["step_off"] = as_bytes(step_off);
+  out["s_undo"] = as_bytes(s_undo);
+  out["s_retry"] = as_bytes(s_retry);
+  out["s_fail"] = as_bytes(s_fail);
+  return out;
+}
+
 void register_runtime(py::module_& m) {
   py::class_<StringPool>(m, "StringPool", "Host string interner feeding the device string pool")
       .def(py::init<>())
@@ -153,6 +288,8 @@ void register_runtime(py::module_& m) {
       .def("lengths_view", &StringPool::lengths_view)
       .def_property_readonly("nbytes", &StringPool::nbytes)
       .def("__len__", &StringPool::size);
+  m.def("pack_specs", &pack_specs, py::arg("specs"), py::arg("agents"), py::arg("pool"), py::arg("cfg_of"),
+        py::arg("fixed"), "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py)");
   m.def("iso_from_us", &iso_from_us, "datetime.isoformat() text of an epoch-µs UTC instant");
   m.def("uuid_from_counter", &uuid_str, py::arg("seed"), py::arg("counter"), py::arg("prefix") = std::string(),
         "uuid4 string minted by the device id generator for (seed, counter)");

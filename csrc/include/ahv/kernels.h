@@ -295,6 +295,13 @@ struct SlashArgs {
   // session, 3 = split with one session per wave (slash_wave_kernel);
   // −1 = AHV_SLASH_FUSED / AHV_SLASH_PER_LANE / AHV_SLASH_MODE, else split.
   int32_t mode = -1;
+  // Touched list (split mode; null = not wanted): the sessions with ≥ 1 clip, in
+  // session order, written to `touched` [S] with their count in `touched_total`.
+  int32_t* touched_tmp = nullptr;      // [S] window-local segments
+  int32_t* touched_blocks = nullptr;   // [ceil(S/256)] per-window counts
+  int32_t* touched_offsets = nullptr;  // [ceil(S/256)]
+  int64_t* touched = nullptr;          // [S] out
+  int64_t* touched_total = nullptr;    // [1] out
 };
 void launch_slash(const SlashArgs&, hipStream_t);
 void slash_host(const SlashArgs&);

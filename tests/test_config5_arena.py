@@ -89,3 +89,22 @@ def test_render_rows_gfx950_word_and_byte_paths(cuda_device):
                           hex_field=(40, src.to(dev), 24), pitch=pitch)
             outs.append(out.cpu())
         assert torch.equal(outs[0], outs[1]), pitch
+
+
+@pytest.mark.gpu
+def test_render_rows_gfx950_long_rows_and_wide_hex(cuda_device):
+    """Rows longer than 64 words, several stamps, a hex field of 128 and of 300
+    source bytes at an odd position: device == host twin."""
+    g = torch.Generator().manual_seed(4)
+    tmpl = torch.randint(32, 127, (1500,), dtype=torch.uint8, generator=g)
+    src = torch.randint(0, 256, (400, 300), dtype=torch.uint8, generator=g)
+    ids = torch.randperm(400, generator=g)[:257].to(torch.int64)
+    for hb, pos in ((128, 401), (300, 777)):
+        outs = []
+        for dev in ("cpu", "cuda"):
+            out = torch.zeros(400 * 1504, dtype=torch.uint8, device=dev)
+            A.render_rows(out, tmpl.to(dev), ids.to(dev),
+                          stamps=[(3, 7, 0, 0), (20, 6, 999_999, 1), (1490, 9, 0, 12345), (64, 18, 0, 0)],
+                          hex_field=(pos, src.to(dev), hb), pitch=1504)
+            outs.append(out.cpu())
+        assert torch.equal(outs[0], outs[1]), hb

@@ -415,8 +415,9 @@ def test_slash_forms_and_sigma_kernels_agree(cuda_device, S, lo, hi):
         for fused in (True, False):
             v = vb.to("cuda")
             got = LI.slash(v, tgt.cuda(), omega.cuda(), scores.cuda(), 100, clip_cap=64, with_sigma_eff=fused,
-                           mode=mode)
+                           mode=mode, with_touched=True)
             torch.cuda.synchronize()
+            assert torch.equal(got.touched.cpu(), torch.nonzero(want.clip_count > 0).flatten()), mode
             assert torch.equal(got.clip_count.cpu(), want.clip_count), mode
             assert torch.equal(got.scores.cpu().nan_to_num(7.0), want.scores.nan_to_num(7.0)), mode
             assert torch.equal(v.active.cpu(), vh.active) and torch.equal(v.released_us.cpu(), vh.released_us)

@@ -691,3 +691,27 @@ def test_agent_gather_is_session_order_sum_of_voucher_rows():
     legacy = torch.zeros(A, dtype=torch.float64)  # the atomic form adds every member's row
     LI.bond_fused(vb, sigma, omega, 0, members=members, agent_exposure=legacy)
     torch.testing.assert_close(legacy, out, rtol=1e-12, atol=1e-15)
+
+
+def test_slash_touched_list_is_sessions_with_clips():
+    import random
+
+    rng = random.Random(21)
+    S = 300
+    offs, vr, ve = [0], [], []
+    for _ in range(S):
+        for _ in range(rng.randint(0, 20)):
+            a, b = rng.sample(range(16), 2)
+            vr.append(a)
+            ve.append(b)
+        offs.append(len(vr))
+    E = len(vr)
+    vb = LI.VouchBatch(torch.tensor(offs, dtype=torch.int32), torch.tensor(vr, dtype=torch.uint8),
+                       torch.tensor(ve, dtype=torch.uint8), torch.rand(E, dtype=torch.float64),
+                       torch.ones(E, dtype=torch.uint8), torch.full((E,), -1, dtype=torch.int64),
+                       torch.zeros(E, dtype=torch.int64))
+    tgt = torch.randint(0, 16, (S,), dtype=torch.uint8)
+    tgt[torch.rand(S) < 0.7] = 255
+    out = LI.slash(vb, tgt, torch.full((S,), 0.9, dtype=torch.float64), torch.rand((S, 16), dtype=torch.float64),
+                   5, with_touched=True)
+    assert torch.equal(out.touched, torch.nonzero(out.clip_count > 0).flatten())
