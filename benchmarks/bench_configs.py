@@ -165,7 +165,8 @@ def config3(ctx: Ctx, args):
     exposure = [torch.zeros(A_, dtype=f64, device=ctx.dev) for _ in range(2)]
     comm = [AS.OverlappedCollective(ctx.dev) for _ in range(2)]
     owned = {}
-    exchange = (lambda t: owned.__setitem__("view", AS.reduce_to_owners(t))) if args.owner_reduce \
+    owner_reduce = not args.allreduce_exposure
+    exchange = (lambda t: owned.__setitem__("view", AS.reduce_to_owners(t))) if owner_reduce \
         else X.allreduce_exposure
     it = [0]
     # P03: the liability stage (tile build + fp64 MFMA σ_eff/exposure) does not
@@ -202,7 +203,7 @@ def config3(ctx: Ctx, args):
 
     el, lat = ctx.timed(step, args.steps, args.warmup)
     ctx.emit(config="config3", liability="tiles" if args.tiles else "fused",
-             what="pipeline+sigma_eff/exposure+" + ("reduce_scatter to owners" if args.owner_reduce
+             what="pipeline+sigma_eff/exposure+" + ("reduce_scatter to owners" if owner_reduce
                                                                           else "all_reduce[A]") + " (overlapped)",
              agents=A_,
              sessions_global=args.sessions or 100_000, sessions_per_rank=S, exposure_bytes=A_ * 8,
@@ -492,7 +493,9 @@ def main():
     ap.add_argument("--unfused", action="store_true", help="config5: separate slash and sigma_eff passes (A/B)")
     ap.add_argument("--no-midstate", action="store_true", help="config5: single-phase K08 re-chain (A/B)")
     ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
-    ap.add_argument("--owner-reduce", action="store_true", help="config3: reduce-scatter exposure to agent owners")
+    ap.add_argument("--allreduce-exposure", action="store_true",
+                    help="config3: all-reduce the full exposure vector on every rank instead of the default "
+                         "reduce-scatter to agent owners (P02)")
     args = ap.parse_args()
     ctx = Ctx(args.device)
     for c in args.configs:

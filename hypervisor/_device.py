@@ -221,6 +221,12 @@ class DeviceSession(SharedSessionObject):
     def participant_count(self) -> int:
         return self._store.call(_st.OP_SESS_READ, [self.slot, 0], 5)[4]
 
+    def snapshot(self, parts: bool = True):
+        """Every field of the session row (and its participants) in one batched
+        read — the form for callers that need several fields at once (each
+        property above is its own device round trip)."""
+        return snapshots(self._store, [self], parts)[0]
+
     # -- lifecycle ---------------------------------------------------------------
     def begin_handshake(self) -> None:
         r = self._store.call(_st.OP_SESS_HANDSHAKE, [self.slot], 2)

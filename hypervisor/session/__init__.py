@@ -80,6 +80,13 @@ class SharedSessionObject:
         return n
 
     # -- lifecycle --------------------------------------------------------
+    def snapshot(self, parts: bool = True):
+        """A :class:`hypervisor.session.snapshot.SessionSnapshot` of this session
+        (the device session reads it in one round trip)."""
+        from hypervisor.session.snapshot import SessionSnapshot
+
+        return SessionSnapshot.of(self, parts)
+
     def _assert_state(self, *allowed: SessionState) -> None:
         if self.state not in allowed:
             raise SessionLifecycleError(

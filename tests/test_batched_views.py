@@ -99,3 +99,27 @@ def test_views_match_host_engines():
 @pytest.mark.gpu
 def test_views_issue_constant_commands_gpu():
     check_views_constant_commands("cuda")
+
+
+def test_session_snapshot_one_read_matches_properties():
+    import asyncio
+
+    from agent_hypervisor_amd.models.store import GovernanceStore
+    from hypervisor import Hypervisor, SessionConfig
+
+    for hv in (Hypervisor(device="host"), Hypervisor(store=GovernanceStore("cpu", caps={"S": 64}))):
+        async def go():
+            m = await hv.create_session(SessionConfig(), "did:c")
+            await hv.join_session(m.sso.session_id, "did:a", sigma_raw=0.8)
+            await hv.activate_session(m.sso.session_id)
+            return m
+        m = asyncio.run(go())
+        sso = m.sso
+        store = getattr(hv, "_store", None)
+        before = store.info()["posted"] if store is not None else 0
+        snap = sso.snapshot()
+        if store is not None:
+            assert store.info()["posted"] - before <= 1
+        assert snap.state == sso.state and snap.participant_count == sso.participant_count
+        assert [p.agent_did for p in snap.participants] == [p.agent_did for p in sso.participants]
+        assert snap.created_at == sso.created_at and snap.session_id == sso.session_id
