@@ -99,7 +99,61 @@ class _Batch:
 
     __slots__ = ("store", "specs", "shared", "ids", "slots", "t0", "doff", "drows", "dlen", "dhash",
                  "delta_off", "gslots", "step_off", "tslots", "status", "built", "released", "dead",
-                 "index", "views", "committed", "__weakref__")
+                 "index", "views", "committed", "_saga_ids", "_step_ids", "__weakref__")
+
+    def saga_ids(self) -> tuple:
+        """(saga id per session or None, step id per step row): minted once, in
+        bulk, the first time a view or a summary needs them."""
+        if self._saga_ids is None:
+            has = self.gslots >= 0
+            ng = int(has.sum())
+            sg, _ = C.uuid4_many(ng, "saga:") if ng else ([], b"")
+            it = iter(sg)
+            self._saga_ids = [next(it) if h else None for h in has.tolist()]
+            nt = int(self.step_off[-1])
+            self._step_ids = C.uuid4_many(nt, "step:")[0] if nt else []
+        return self._saga_ids, self._step_ids
+
+    def saga_summaries(self, rows: dict, idx) -> list:
+        """Summary dicts (Hypervisor.saga_summaries form) of the sagas of unbuilt
+        sessions ``idx``, from gathered ``rows`` (g_* per saga, t_* per step)."""
+        from hypervisor._clock import from_us
+        from hypervisor.saga.state_machine import SagaState, StepState
+
+        gids, tids = self.saga_ids()
+        gst, sst = list(SagaState), list(StepState)
+        out, gk, tk = [], 0, 0
+        for i in idx:
+            if self.gslots[i] < 0:
+                continue
+            sp = _spec(self, i)
+            s0, s1 = int(self.step_off[i]), int(self.step_off[i + 1])
+            steps = []
+            for k in range(s0, s1):
+                a = sp.steps[k - s0]
+                t0, t1 = int(rows["t_started"][tk]), int(rows["t_completed"][tk])
+                steps.append({"step_id": tids[k], "action_id": a[0], "agent_did": a[1],
+                              "state": sst[int(rows["t_state"][tk]) & 0xFF].value,
+                              "retry_count": int(rows["t_retry"][tk]), "error": None,
+                              "started_at": from_us(t0) if t0 else None, "completed_at": from_us(t1) if t1 else None})
+                tk += 1
+            c1 = int(rows["g_completed"][gk])
+            out.append({"saga_id": gids[i], "session_id": self.ids[i],
+                        "state": gst[int(rows["g_state"][gk]) & 0xFF].value, "error": None,
+                        "created_at": from_us(int(rows["g_created"][gk])),
+                        "completed_at": from_us(c1) if c1 else None, "steps": steps})
+            gk += 1
+        return out
+
+    def saga_row_slots(self, idx) -> tuple:
+        """(saga rows, step rows) of the unbuilt sessions ``idx`` in summary order."""
+        gi, ti = [], []
+        for i in idx:
+            g = int(self.gslots[i])
+            if g >= 0:
+                gi.append(g)
+                ti.extend(self.tslots[int(self.step_off[i]):int(self.step_off[i + 1])].tolist())
+        return gi, ti
 
     _FLUSH = 8192
 
@@ -409,6 +463,7 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
     b.doff, b.drows, b.dlen, b.dhash = np.frombuffer(doff, dtype=np.int64), drow_np, dlen, dhash
     b.delta_off, b.gslots, b.step_off, b.tslots = delta_off, gslots, step_off, tslots
     b.status, b.built, b.released, b.dead = status_np, np.zeros(n, dtype=bool), np.zeros(n, dtype=bool), []
+    b._saga_ids = b._step_ids = None
     register_lazy(hv, b, status_np, cidx)
     run_ = PipelineRun(session_ids=ids, status=status_np,
                        join_rings=tens["join_ring"].cpu().numpy()[: len(j_agent)],
@@ -477,10 +532,11 @@ def materialize(b: _Batch, i: int) -> tuple:
     orch = _device.DeviceSagaOrchestrator(st)
     g = int(b.gslots[i])
     if g >= 0:
-        saga = _device.DeviceSaga(st, g, C.uuid4("saga:"), sid)
+        gids, tids = b.saga_ids()
+        saga = _device.DeviceSaga(st, g, gids[i], sid)
         for k in range(int(b.step_off[i]), int(b.step_off[i + 1])):
             a = sp.steps[k - int(b.step_off[i])]
-            step = _device.DeviceSagaStep(st, int(b.tslots[k]), step_id=C.uuid4("step:"), action_id=a[0],
+            step = _device.DeviceSagaStep(st, int(b.tslots[k]), step_id=tids[k], action_id=a[0],
                                           agent_did=a[1], execute_api=a[2], undo_api=a[3], timeout_seconds=300,
                                           max_retries=int(a[4]))
             saga.steps.append(step)

@@ -25,9 +25,11 @@ def _iso(t) -> Any:
 
 def summary(st, limit: int = 200) -> dict[str, Any]:
     """Every tab's data from the live hypervisor (capped at ``limit`` rows each)."""
+    from hypervisor.core import LazyManagedSession
+
     hv, bus = st.hv, st.bus
-    sessions = hv.sessions
-    snaps = hv.snapshots(sessions, parts=True)  # one batched device read
+    sessions = hv.sessions  # batched-pipeline sessions come as row proxies: nothing is built for the summary
+    snaps = hv.snapshots(parts=True)  # one batched device read per segment, same order as hv.sessions
     rings: Counter = Counter()
     states: Counter = Counter()
     session_rows, agent_rows = [], []
@@ -40,16 +42,20 @@ def summary(st, limit: int = 200) -> dict[str, Any]:
                                    "ring_name": p.ring.name, "sigma_raw": round(p.sigma_raw, 4),
                                    "sigma_eff": round(p.sigma_eff, 4), "active": bool(p.is_active)})
         if len(session_rows) < limit:
-            de = m.delta_engine
+            if isinstance(m, LazyManagedSession):
+                turns = x.delta_count
+            else:
+                de = m.delta_engine
+                turns = de.turn_count if de is not None else 0
             session_rows.append({"session_id": x.session_id, "state": x.state.value,
                                  "participants": x.participant_count, "created_at": _iso(x.created_at),
-                                 "deltas": de.turn_count if de is not None else 0,
+                                 "deltas": turns,
                                  "merkle_root": x.merkle_root if x.committed_at is not None else
                                  getattr(hv.commitment.get_commitment(x.session_id), "merkle_root", None)})
     sagas: Counter = Counter()
     steps: Counter = Counter()
     saga_rows = []
-    for g in hv.saga_summaries(sessions):  # one column gather per field
+    for g in hv.saga_summaries():  # one column gather per field (batches from their rows)
         sagas[g["state"]] += 1
         for s_ in g["steps"]:
             steps[s_["state"]] += 1

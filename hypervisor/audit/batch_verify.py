@@ -125,7 +125,18 @@ def verify_audit(
     root_rows, root_expect, root_sid = [], [], []
     files, file_expect, file_key = [], [], []
     resident = []  # device-store sessions: verified where their rows live
+    from hypervisor.core import LazyManagedSession
+
     for m in sessions:
+        if isinstance(m, LazyManagedSession):
+            b, i = m._batch, m._index
+            built = b.views.get(i)
+            if built is None and store is not None and b.store is store:
+                d0, d1 = int(b.delta_off[i]), int(b.delta_off[i + 1])  # rows straight from the batch
+                if d1 > d0:
+                    resident.append((b.ids[i], b.drows[d0:d1].tolist(), True))
+                continue
+            m = built if built is not None else b.view(i)
         sid = m.sso.session_id
         de = m.delta_engine
         ds = de.deltas

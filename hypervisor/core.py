@@ -405,8 +405,10 @@ class Hypervisor:
         return list(self._sessions.values())
 
     def find_saga(self, saga_id: str):
-        """(managed session, saga) owning ``saga_id``, or (None, None)."""
-        for m in self._sessions.values():
+        """(managed session, saga) owning ``saga_id``, or (None, None).  Saga ids are
+        minted by the views, so batched sessions whose views were never built are
+        not searched (and not built)."""
+        for m in self._sessions.built_values():
             s = m.saga.get_saga(saga_id)
             if s is not None:
                 return m, s
@@ -468,6 +470,21 @@ class Hypervisor:
         from hypervisor._clock import from_us
         from hypervisor.saga.state_machine import SagaState, StepState
 
+        if managed is None and self._store is not None:  # batches: from their rows, no views built
+            out = []
+            for kind, seg in self._sessions.segments():
+                if kind == "own":
+                    out.extend(self.saga_summaries(seg))
+                    continue
+                built = [seg.views[i] for i in sorted(seg.views)]
+                out.extend(self.saga_summaries(built))
+                rest = [i for i in seg.index.values() if i not in seg.views]
+                gi, ti = seg.saga_row_slots(rest)
+                if gi:
+                    rows = self._store.gather({"g_state": gi, "g_created": gi, "g_completed": gi, "t_state": ti,
+                                               "t_retry": ti, "t_started": ti, "t_completed": ti})
+                    out.extend(seg.saga_summaries(rows, rest))
+            return out
         ms = list(self._sessions.values()) if managed is None else list(managed)
         sagas = [g for m in ms for g in m.saga.sagas]
         out = []

@@ -95,6 +95,19 @@ class SessionTable:
             else:
                 yield from seg.entries()
 
+    def built_values(self):
+        """The sessions that have Python views (ordinary ones and batched ones
+        already used) — what a search for an id the views minted needs."""
+        own = self._own
+        for seg in self._segs:
+            if isinstance(seg, list):
+                for sid in seg:
+                    m = own.get(sid)
+                    if m is not None:
+                        yield m
+            else:
+                yield from (seg.views[i] for i in sorted(seg.views))
+
     def items(self):
         for sid, m in zip(self, self.values()):
             yield sid, m

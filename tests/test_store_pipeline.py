@@ -197,3 +197,56 @@ def test_lazy_rows_released_in_bulk_and_materialized_rows_kept(monkeypatch):
     st.reclaim()
     assert {k: st.live_rows()[k] for k in ("S", "G", "T", "D")} == base
     st.close()
+
+
+def test_batch_sessions_verify_and_search_without_building_views():
+    st = GovernanceStore("cpu", caps={"S": 256, "D": 1024, "G": 256, "T": 256})
+    hv = Hypervisor(store=st)
+    run = asyncio.run(hv.run_pipelines(PipelineSpec(), 100))
+    b = hv._sessions.batch_of(run.session_ids[0])
+    rep = hv.verify_audit()
+    assert rep.ok and rep.deltas == 300 and rep.roots_checked == 100
+    assert hv.find_saga("saga:none") == (None, None)
+    assert not b.views  # nothing was materialized
+    m = hv.get_session(run.session_ids[7])
+    sg = m.saga.sagas[0]
+    assert hv.find_saga(sg.saga_id)[1] is sg and len(b.views) == 1
+    st.write_rows({"d_hash": ([8 * int(b.drows[3 * 9 + 1])], [0x0BADBEEF])})  # corrupt session 9's 2nd digest
+    rep = hv.verify_audit()
+    assert rep.bad_chains == [run.session_ids[9]] and rep.bad_roots == [run.session_ids[9]]
+    st.close()
+
+
+def test_batch_saga_summaries_without_views_match_built_views():
+    st = GovernanceStore("cpu", caps={"S": 256, "D": 1024, "G": 256, "T": 256})
+    hv = Hypervisor(store=st)
+    rng = random.Random(3)
+    specs = [random_spec(rng) for _ in range(60)]
+    run = asyncio.run(hv.run_pipelines(specs))
+    lazy = hv.saga_summaries()
+    b = hv._sessions.batch_of(run.session_ids[0])
+    assert not b.views
+    built = hv.saga_summaries([hv.get_session(sid) for sid in run.session_ids if hv.get_session(sid) is not None])
+    assert len(b.views) == 60
+    key = lambda d: d["session_id"]  # noqa: E731
+    assert sorted(lazy, key=key) == sorted(built, key=key)
+    st.close()
+
+
+def test_dashboard_and_stats_over_batches_build_no_views():
+    from fastapi.testclient import TestClient
+
+    from hypervisor.api.server import create_app
+
+    st = GovernanceStore("cpu", caps={"S": 1024, "D": 4096, "G": 1024, "T": 1024})
+    hv = Hypervisor(store=st)
+    run = asyncio.run(hv.run_pipelines(PipelineSpec(), 500))
+    b = hv._sessions.batch_of(run.session_ids[0])
+    app = create_app(hv)
+    with TestClient(app) as c:
+        s = c.get("/api/v1/stats").json()
+        assert s["total_sessions"] == 500
+        d = c.get("/api/v1/dashboard/summary").json()
+    assert not b.views
+    assert d["overview"]["sessions"] == 500
+    st.close()
