@@ -360,7 +360,7 @@ def main() -> None:
             device_p50, device_mean = scalar_pipeline_p50(args.scalar_iters, "cuda")
 
     api = None
-    if rank == 0 and not args.no_api and dev.type == "cuda":
+    if rank == 0 and world == 1 and not args.no_api and dev.type == "cuda":  # 1-GPU runs (the N>1 scaling runs skip it)
         api = api_section(args, scalar_p50)
 
     if rank == 0:
