@@ -49,3 +49,18 @@ def test_dashboard_example_workload_feeds_every_tab():
     assert o["sessions"] == 8 and o["vouches"] > 0 and o["slashes"] > 0 and o["commitments"] == 4
     assert len(s["rings"]) >= 2 and "escalated" in s["sagas"]["by_state"]
     assert s["events"]["recent"]
+
+
+def test_batch_pipelines_example(capsys, monkeypatch):
+    import asyncio
+
+    import torch
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)  # the CPU twin here
+    spec = importlib.util.spec_from_file_location("ahv_batch_example",
+                                                  os.path.join(ROOT, "examples", "batch_pipelines.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    asyncio.run(mod.main())
+    out = capsys.readouterr().out
+    assert "template: 20000 sessions ok" in out and "verify_audit: ok=True" in out
