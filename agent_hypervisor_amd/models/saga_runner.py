@@ -56,6 +56,18 @@ _UNSET = object()
 _SG_RUNNING, _SG_COMPENSATING = SAGA_NAMES.index("running"), SAGA_NAMES.index("compensating")
 
 
+class _Setter:
+    """``obj[name] = v`` as ``setattr`` (the write-back's slow path)."""
+
+    __slots__ = ("obj",)
+
+    def __init__(self, obj) -> None:
+        self.obj = obj
+
+    def __setitem__(self, name: str, value) -> None:
+        setattr(self.obj, name, value)
+
+
 class _Resume:
     """Awaitable continuing a coroutine already started with ``send(None)``."""
 
@@ -301,7 +313,7 @@ class SagaBatchRunner:
 
     @staticmethod
     def _write_back(eng, sagas, results, errors, comp_results, comp_errors) -> None:
-        from hypervisor.saga.state_machine import SagaState, StepState
+        from hypervisor.saga.state_machine import SagaState, SagaStep, StepState
 
         K = eng.K
         cols = torch.stack([eng.step_state.to(torch.int64), eng.retry_count.to(torch.int64),
@@ -334,7 +346,9 @@ class SagaBatchRunner:
                     err = no_undo
                 else:  # ERR_COMP, ERR_COMP_TIMEOUT
                     err = comp_errors[base + k]
-                d = st.__dict__
+                # plain SagaSteps take the fields in one dict update; views with
+                # properties (device-store steps) through their setters
+                d = st.__dict__ if type(st) is SagaStep else _Setter(st)
                 d["state"] = step_enum[row_state[k]]
                 d["retry_count"] = row_retry[k]
                 d["started_at"] = stamps[row_start[k]]

@@ -954,6 +954,7 @@ class DeviceSagaStep(SagaStep):
     @state.setter
     def state(self, s: StepState) -> None:  # direct write outside the FSM (reference retry reset / no-undo path)
         self._store.call(_st.OP_STEP_SET, [self.slot, _STEPS.index(StepState(s)), -1], 1)
+        self.__dict__["_hint"] = StepState(s)
 
     @property
     def retry_count(self) -> int:  # type: ignore[override]
@@ -984,12 +985,33 @@ class DeviceSagaStep(SagaStep):
     def transition(self, new_state: StepState, retry: int = -1) -> None:
         to = _STEPS.index(StepState(new_state))
         r = self._store.call(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], 2)
+        self.__dict__["_hint"] = None
         self._transitioned(r, new_state)
+        self.__dict__["_hint"] = StepState(new_state)
 
     async def transition_async(self, new_state: StepState, retry: int = -1) -> None:
         to = _STEPS.index(StepState(new_state))
+        self.__dict__["_hint"] = None
         r = await self._store.call_async(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], 2)
         self._transitioned(r, new_state)
+        self.__dict__["_hint"] = StepState(new_state)
+
+    def post_transition(self, new_state: StepState, retry: int = -1) -> int:
+        """Post a transition without waiting (its result is read later with
+        :meth:`check_posted`); the worker applies commands in order."""
+        to = _STEPS.index(StepState(new_state))
+        self.__dict__["_hint"] = None
+        return self._store.post(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry])
+
+    async def check_posted(self, seq: int, new_state: StepState) -> None:
+        self._transitioned(await self._store.result_async(seq, 2), new_state)
+        self.__dict__["_hint"] = StepState(new_state)
+
+    def can_speculate(self, new_state: StepState) -> bool:
+        """True when this process's last known state of the step allows
+        ``new_state`` (every transition of a device step goes through this object)."""
+        h = self.__dict__.get("_hint")
+        return h is not None and StepState(new_state) in STEP_TRANSITIONS.get(h, ())
 
     @staticmethod
     def _transitioned(r: tuple, new_state) -> None:
@@ -1100,6 +1122,13 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         self._store = store
         self._sagas: dict[str, DeviceSaga] = {}
 
+    async def execute_sagas(self, saga_ids, executors, compensator=None, compensate: bool = True,
+                            device: Optional[str] = None) -> list:
+        """The sagas' state machines already live in the store's rows: every step
+        runs through the store worker's FSM (``device`` is accepted for API
+        symmetry — there is no separate batch engine to replay into)."""
+        return await SagaOrchestrator.execute_sagas(self, saga_ids, executors, compensator, compensate, None)
+
     def create_saga(self, session_id: str, saga_id: Optional[str] = None) -> DeviceSaga:
         slot = self._store.alloc("G")
         saga = DeviceSaga(self._store, slot, saga_id or _C.uuid4("saga:"), session_id)
@@ -1116,6 +1145,7 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
             execute_api=execute_api, undo_api=undo_api, timeout_seconds=timeout_seconds, max_retries=max_retries,
         )
         self._store.post(_st.OP_STEP_ADD, [saga.slot, slot, int(bool(undo_api)), int(max_retries)])
+        step.__dict__["_hint"] = StepState.PENDING
         saga.steps.append(step)
         return step
 
@@ -1125,7 +1155,12 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         attempts = 1 + step.max_retries
         last: Optional[Exception] = None
         for attempt in range(attempts):
-            await step.transition_async(StepState.EXECUTING, retry=attempt)
+            # the EXECUTING transition is posted and the executor starts at once when this
+            # process knows the step's state allows it (its result is checked right after)
+            seq = step.post_transition(StepState.EXECUTING, retry=attempt) \
+                if step.can_speculate(StepState.EXECUTING) else None
+            if seq is None:
+                await step.transition_async(StepState.EXECUTING, retry=attempt)
             try:
                 result = await await_with_timeout(executor(), step.timeout_seconds)
             except asyncio.TimeoutError:
@@ -1137,8 +1172,12 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                 last = e
             else:
                 step.execute_result = result
+                if seq is not None:
+                    await step.check_posted(seq, StepState.EXECUTING)
                 await step.transition_async(StepState.COMMITTED)
                 return result
+            if seq is not None:
+                await step.check_posted(seq, StepState.EXECUTING)
             step.error = str(last)
             step.transition(StepState.FAILED)
             if attempt < attempts - 1:

@@ -204,3 +204,44 @@ def test_device_runner_mixed_executor_kinds_match_host(delay):
     asyncio.run(dev.execute_sagas(d_ids, d_ex, comp, device="cpu"))
     assert _view(host, h_ids) == _view(dev, d_ids)
     assert calls_h == calls_d
+
+
+def test_device_runner_writes_back_through_device_store_steps():
+    """execute_sagas(device=...) on a device-store hypervisor's orchestrator: the
+    states land in the store's step rows (the views' setters), as the host
+    orchestrator's would."""
+    from agent_hypervisor_amd.models.store import GovernanceStore
+    from hypervisor import Hypervisor, SessionConfig
+
+    st = GovernanceStore("cpu", caps={"S": 64, "G": 64, "T": 256})
+    hv = Hypervisor(store=st)
+
+    async def go():
+        m = await hv.create_session(SessionConfig(), "did:c")
+        orch = m.saga
+        ids, ex = [], {}
+        for i in range(6):
+            sg = orch.create_saga(m.sso.session_id)
+            ids.append(sg.saga_id)
+            for k in range(3):
+                step = orch.add_step(sg.saga_id, f"a{i}.{k}", "did:x", "/e", "/u", max_retries=0)
+                fail = (i + k) % 4 == 0
+
+                async def run(fail=fail):
+                    if fail:
+                        raise RuntimeError("no")
+                    return "ok"
+                ex[step.step_id] = run
+
+        async def comp(step):
+            return "undone"
+        await orch.execute_sagas(ids, ex, comp, device="cpu")
+        return orch, ids
+
+    orch, ids = asyncio.run(go())
+    states = [(orch.get_saga(i).state.value, [s_.state.value for s_ in orch.get_saga(i).steps]) for i in ids]
+    assert any(s == "completed" for s, _ in states) and any("failed" in ss for _, ss in states)
+    # the values read back come from the device rows
+    row = orch.get_saga(ids[1]).steps[0]
+    assert row.state.value == states[1][1][0] and "state" not in row.__dict__
+    st.close()
