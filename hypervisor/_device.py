@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import os
 import struct
 from datetime import datetime, timedelta
 from typing import Any, Callable, Optional
@@ -930,6 +931,9 @@ class DeviceCommitmentEngine(CommitmentEngine):
 # ------------------------------------------------------------------ sagas
 
 
+_SPECULATE = os.environ.get("AHV_STEP_SPECULATE", "1") != "0"  # A/B switch for the posted EXECUTING transition
+
+
 class DeviceSagaStep(SagaStep):
     """Step view: FSM state, timestamps and retry counter live in the device step table."""
 
@@ -1011,7 +1015,7 @@ class DeviceSagaStep(SagaStep):
         """True when this process's last known state of the step allows
         ``new_state`` (every transition of a device step goes through this object)."""
         h = self.__dict__.get("_hint")
-        return h is not None and StepState(new_state) in STEP_TRANSITIONS.get(h, ())
+        return _SPECULATE and h is not None and StepState(new_state) in STEP_TRANSITIONS.get(h, ())
 
     @staticmethod
     def _transitioned(r: tuple, new_state) -> None:
