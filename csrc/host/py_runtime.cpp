@@ -9,6 +9,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -274,6 +277,102 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   return out;
 }
 
+
+// ------------------------------------------------------------------ attribution packing
+// CausalAttributor.attribute_batch: the K21 columns of many failure cases, read
+// natively from their dicts.  Per case the agents are listed in the iteration
+// order of set(agent_actions) — the order the scalar engine ranks ties in — and
+// each node's (agent column, success, root cause, ω) is taken exactly as
+// build_causal_dag / raw_scores read it.
+
+static py::tuple pack_attribution(const py::list& cases) {
+  std::vector<int32_t> node_off{0}, agent_off{0}, agent_of;
+  std::vector<uint8_t> succ, root;
+  std::vector<double> omega;
+  py::list agents_per_case(cases.size());
+  static const py::str kAA("agent_actions"), kFS("failure_step_id"), kFA("failure_agent_did"), kRW("risk_weights"),
+      kSucc("success"), kStep("step_id"), kAct("action_id");
+  size_t ci = 0;
+  for (py::handle c : cases) {
+    py::dict cd = py::reinterpret_borrow<py::dict>(c);
+    py::dict aa = py::reinterpret_borrow<py::dict>(cd[kAA]);
+    py::object fstep = cd[kFS], fagent = cd[kFA];
+    py::object rwo = cd.contains(kRW) ? py::object(cd[kRW]) : py::object(py::none());
+    const bool has_rw = !rwo.is_none() && PyObject_IsTrue(rwo.ptr());
+    // set(agent_actions.keys()) exactly: a set built from the dict itself is presized
+    // and iterates in a different order than one built from the keys view
+    py::object kview = aa.attr("keys")();
+    py::set keys = py::reinterpret_steal<py::set>(PySet_New(kview.ptr()));
+    if (!keys) throw py::error_already_set();
+    py::list agents;
+    std::unordered_map<PyObject*, int32_t> col;
+    int32_t j = 0;
+    for (py::handle k : keys) {  // set iteration order
+      agents.append(k);
+      col.emplace(k.ptr(), j++);
+    }
+    for (auto kv : aa) {
+      py::handle agent = kv.first;
+      auto it = col.find(agent.ptr());
+      int32_t aj;
+      if (it != col.end()) {
+        aj = it->second;
+      } else {  // equal key, different object: fall back to equality
+        aj = -1;
+        int32_t q = 0;
+        for (py::handle k : agents) {
+          if (k.equal(agent)) { aj = q; break; }
+          ++q;
+        }
+      }
+      const bool me = agent.equal(fagent);
+      for (py::handle a : kv.second) {
+        py::dict ad = py::reinterpret_borrow<py::dict>(a);
+        agent_of.push_back(aj);
+        py::object s = ad.contains(kSucc) ? py::object(ad[kSucc]) : py::object(py::bool_(true));
+        const int t = PyObject_IsTrue(s.ptr());
+        if (t < 0) throw py::error_already_set();
+        succ.push_back(t ? 1 : 0);
+        root.push_back(me && ad.contains(kStep) && py::object(ad[kStep]).equal(fstep) ? 1 : 0);
+        double w = 0.5;
+        if (has_rw) {
+          py::object aid = ad.contains(kAct) ? py::object(ad[kAct]) : py::object(py::str(""));
+          PyObject* v = PyDict_Check(rwo.ptr()) ? PyDict_GetItemWithError(rwo.ptr(), aid.ptr()) : nullptr;
+          if (v == nullptr && PyErr_Occurred()) throw py::error_already_set();
+          if (v != nullptr) w = py::reinterpret_borrow<py::object>(v).cast<double>();
+          else if (!PyDict_Check(rwo.ptr())) w = py::float_(rwo.attr("get")(aid, 0.5)).cast<double>();
+        }
+        omega.push_back(w);
+      }
+    }
+    node_off.push_back(static_cast<int32_t>(agent_of.size()));
+    agent_off.push_back(agent_off.back() + static_cast<int32_t>(py::len(agents)));
+    agents_per_case[ci++] = agents;
+  }
+  return py::make_tuple(as_bytes(node_off), as_bytes(agent_off), as_bytes(agent_of), as_bytes(succ), as_bytes(root),
+                        as_bytes(omega), agents_per_case);
+}
+
+// Python's round(x, n) (correctly rounded decimal, half-even on the exact binary
+// value) for many values at once: printf's %.*f rounds the exact value in the
+// default rounding mode, and strtod reads the decimal back.
+static py::list round_many(const std::vector<double>& xs, int n) {
+  py::list out(xs.size());
+  char buf[512];
+  for (size_t i = 0; i < xs.size(); ++i) {
+    const double x = xs[i];
+    if (!std::isfinite(x) || std::fabs(x) >= 1e300) {
+      out[i] = py::float_(x);
+      continue;
+    }
+    std::snprintf(buf, sizeof buf, "%.*f", n, x);
+    double y = std::strtod(buf, nullptr);
+    if (y == 0.0) y = std::copysign(0.0, x);  // round(-0.00001, 4) is -0.0
+    out[i] = py::float_(y);
+  }
+  return out;
+}
+
 void register_runtime(py::module_& m) {
   py::class_<StringPool>(m, "StringPool", "Host string interner feeding the device string pool")
       .def(py::init<>())
@@ -288,6 +387,9 @@ void register_runtime(py::module_& m) {
       .def("lengths_view", &StringPool::lengths_view)
       .def_property_readonly("nbytes", &StringPool::nbytes)
       .def("__len__", &StringPool::size);
+  m.def("pack_attribution", &pack_attribution, py::arg("cases"),
+        "K21 columns + per-case agent lists (set order) of CausalAttributor.attribute_batch cases");
+  m.def("round_many", &round_many, py::arg("xs"), py::arg("ndigits"), "[round(x, ndigits) for x in xs]");
   m.def("pack_specs", &pack_specs, py::arg("specs"), py::arg("agents"), py::arg("pool"), py::arg("cfg_of"),
         py::arg("fixed"), "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py)");
   m.def("iso_from_us", &iso_from_us, "datetime.isoformat() text of an epoch-µs UTC instant");

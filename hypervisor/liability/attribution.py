@@ -70,6 +70,20 @@ class AttributionResult:
         return 0.0
 
 
+_DIRECT, _CONTRIB = "Direct cause of failure", "Contributing factor"
+
+
+def _fault(agent, share: float, contrib: float, direct: bool) -> FaultAttribution:
+    f = object.__new__(FaultAttribution)
+    f.__dict__.update(agent_did=agent, liability_score=share, causal_contribution=contrib, is_direct_cause=direct,
+                      reason=_DIRECT if direct else _CONTRIB)
+    return f
+
+
+def _by_score(x: FaultAttribution) -> float:
+    return x.liability_score
+
+
 class CausalAttributor:
     DIRECT_CAUSE_WEIGHT = 0.5
     ENABLING_WEIGHT = 0.3
@@ -157,44 +171,46 @@ class CausalAttributor:
     def attribute_batch(self, cases, device="cpu") -> list[AttributionResult]:
         """:meth:`attribute` for many failure cases — dicts of its keyword
         arguments — with the raw per-agent scores of all cases from one K21
-        launch on ``device``; normalisation (CPython ``round``) and ranking stay
-        on the host.  The causal nodes are flattened straight into the kernel's
-        columns (no :class:`CausalNode` objects: a result records only the chain
-        length), and agents are ranked from the same set order as
-        :meth:`attribute`, so ties sort identically."""
+        launch on ``device``.  The cases' dicts are read into the kernel's columns
+        natively (``_C.pack_attribution``; no :class:`CausalNode` objects — a
+        result records only the chain length), the scores are rounded natively
+        with CPython ``round``'s exact result (``_C.round_many``), and agents are
+        ranked from the same set order as :meth:`attribute`, so ties sort
+        identically."""
         import numpy as np
         import torch
 
         from agent_hypervisor_amd.ops import ledger as LG
 
-        node_off, agent_off, agent_of, succ, root, omega = [0], [0], [], [], [], []
-        per_case = []
-        for c in cases:
-            aa = c["agent_actions"]
-            fstep, fagent = c["failure_step_id"], c["failure_agent_did"]
-            agents = list(set(aa.keys()))  # the iteration order raw_scores uses
-            col = {a: j for j, a in enumerate(agents)}
-            rw = c.get("risk_weights") or {}
-            for agent, acts in aa.items():
-                j = col[agent]
-                me = agent == fagent
-                for a in acts:
-                    agent_of.append(j)
-                    succ.append(1 if a.get("success", True) else 0)
-                    root.append(1 if me and a.get("step_id") == fstep else 0)
-                    omega.append(float(rw.get(a.get("action_id", ""), 0.5)))
-            node_off.append(len(agent_of))
-            agent_off.append(agent_off[-1] + len(agents))
-            per_case.append((c, agents, node_off[-1] - node_off[-2]))
-        C, N = len(per_case), len(agent_of)
-        ints = torch.from_numpy(np.asarray(node_off + agent_off + agent_of, dtype=np.int32)).to(device)
-        flags = torch.from_numpy(np.asarray([succ, root], dtype=np.uint8).reshape(2, N)).to(device)
+        cases = cases if isinstance(cases, list) else list(cases)
+        no, ao, aof, sc, rc, om, agents_of = _C.pack_attribution(cases)  # columns read natively
+        node_off = np.frombuffer(no, dtype=np.int32)
+        agent_off = np.frombuffer(ao, dtype=np.int32)
+        C, N = len(cases), len(aof) // 4
+        ints = torch.from_numpy(np.concatenate([node_off, agent_off, np.frombuffer(aof, dtype=np.int32)])).to(device)
+        flags = torch.from_numpy(np.concatenate([np.frombuffer(sc, dtype=np.uint8),
+                                                 np.frombuffer(rc, dtype=np.uint8)]).reshape(2, N)).to(device)
         raw = LG.attribution_raw(ints[: C + 1], ints[C + 1: 2 * C + 2], ints[2 * C + 2:], flags[0].contiguous(),
-                                 flags[1].contiguous(), torch.from_numpy(np.asarray(omega, dtype=np.float64)).to(device))
+                                 flags[1].contiguous(), torch.from_numpy(np.frombuffer(om, dtype=np.float64).copy())
+                                 .to(device))
         raw = raw.cpu().tolist()
-        return [self._result_n(c["saga_id"], c["session_id"], n, agents, raw[agent_off[k]: agent_off[k + 1]],
-                               c["failure_agent_did"])
-                for k, (c, agents, n) in enumerate(per_case)]
+        # normalisation in case order, CPython rounding done natively for all cases at once
+        off = agent_off.tolist()
+        totals = [sum(raw[off[k]: off[k + 1]]) or 1.0 for k in range(C)]
+        share = C and _C.round_many([r / totals[k] for k in range(C) for r in raw[off[k]: off[k + 1]]], 4)
+        contrib = C and _C.round_many(raw, 4)
+        nodes = (node_off[1:] - node_off[:-1]).tolist()
+        out = []
+        for k, c in enumerate(cases):
+            fa = c["failure_agent_did"]
+            lo, hi = off[k], off[k + 1]
+            attrs = [_fault(a, share[q], contrib[q], a == fa) for a, q in zip(agents_of[k], range(lo, hi))]
+            attrs.sort(key=_by_score, reverse=True)
+            res = AttributionResult(saga_id=c["saga_id"], session_id=c["session_id"], attributions=attrs,
+                                    causal_chain_length=nodes[k], root_cause_agent=fa)
+            self._history.append(res)
+            out.append(res)
+        return out
 
     def attribute_tensors(self, node_offsets, agent_offsets, agent_of_node, success, root_cause, risk_weight):
         """Tensor-native K21 (inputs on one device, int32 CSR offsets per case /
