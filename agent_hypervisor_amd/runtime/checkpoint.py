@@ -565,13 +565,16 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
             ("s_dcount", len(r["audit"])), ("s_released", 0), ("s_retained", 0), ("s_proot_n", 0),
         ):
             put(col, s, v)
+        c = commits.get(r["session_id"])
+        commit_dids = set(c["participant_dids"]) if c is not None else ()
         if len(r["participants"]) > P:
             raise CheckpointError(f"session {r['session_id']}: more participants than the store's row width {P}")
         for k, p in enumerate(r["participants"]):
             row = s * P + k
             put("p_agent", row, st.agent_id(p["agent_did"]))
             put("p_ring", row, int(p["ring"]))
-            put("p_active", row, int(bool(p["is_active"])))
+            # P_ACTIVE | P_COMMITTED (store.h): members of the committed participant list
+            put("p_active", row, int(bool(p["is_active"])) | (2 if p["agent_did"] in commit_dids else 0))
             put("p_sraw", row, float(p["sigma_raw"]))
             put("p_seff", row, float(p["sigma_eff"]))
             put("p_joined", row, us(p["joined_at"]))

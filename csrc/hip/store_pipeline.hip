@@ -225,6 +225,7 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
       if ((fl & 1u) && nd > 0) {
         t.s_committed[s] = tt;
         t.s_commit_n[s] = nd;
+        for (int32_t k = 0; k < pc; ++k) t.p_active[base + k] = store::P_ACTIVE | store::P_COMMITTED;
       }
       int32_t retained = 0;
       for (int32_t k = 0; k < nd; ++k) retained += sp_delta_ts(a, i, k) >= tt - a.gc_retention_us ? 1 : 0;

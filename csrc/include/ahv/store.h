@@ -382,6 +382,20 @@ AHV_HD bool edge_live(const Tables& t, int32_t e, int64_t now) {
   return t.e_active[e] && (t.e_expiry[e] < 0 || now <= t.e_expiry[e]);
 }
 
+// p_active bits: P_ACTIVE — the participant is in the session now (SSO leave
+// clears it); P_COMMITTED — it was active when the session's Merkle root was
+// committed (the commitment record's participant_dids, reference core.py:209-214:
+// the list is taken at terminate, so a later leave must not change it).
+constexpr uint8_t P_ACTIVE = 1u;
+constexpr uint8_t P_COMMITTED = 2u;
+
+AHV_HD void mark_committed_participants(const Tables& t, int64_t s) {
+  const int32_t n = t.s_pcount[s];
+  const int64_t base = s * t.cap.P;
+  for (int32_t k = 0; k < n; ++k)
+    if (t.p_active[base + k] & P_ACTIVE) t.p_active[base + k] = P_ACTIVE | P_COMMITTED;
+}
+
 // Participant row of `agent` in session `s` (all rows, active or not), or -1.
 AHV_HD int32_t find_part(const Tables& t, int64_t s, int32_t agent) {
   const int32_t n = t.s_pcount[s];
@@ -769,8 +783,8 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
         return;
       }
       const int64_t row = s * t.cap.P + k;
-      if (t.p_active[row]) {
-        t.p_active[row] = 0;
+      if (t.p_active[row] & P_ACTIVE) {  // a commit-time membership bit (P_COMMITTED) stays
+        t.p_active[row] = static_cast<uint8_t>(t.p_active[row] & ~P_ACTIVE);
         t.s_pactive[s] -= 1;
       }
       out64(r + 1, ST_OK);
@@ -1733,6 +1747,7 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
           store8(t.s_root + 8 * s, root);
           t.s_committed[s] = now;
           t.s_commit_n[s] = static_cast<int32_t>(n);
+          mark_committed_participants(t, s);
         }
         const int32_t rel = release_vsess(t, static_cast<int32_t>(static_cast<int64_t>(c.a[4])), now);  // K07
         t.s_released[s] = rel;

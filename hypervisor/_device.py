@@ -165,7 +165,7 @@ class DeviceSession(SharedSessionObject):
             raw = self._store.bulk(0, 40 * r[3])
             for k in range(r[3]):
                 a, fl, sr, se, j = struct.unpack_from("<qQddq", raw, 40 * k)
-                parts.append((a, fl & 0xFF, (fl >> 8) & 0xFF, sr, se, j))
+                parts.append((a, fl & 0xFF, (fl >> 8) & 1, sr, se, j))  # bit 8 P_ACTIVE, bit 9 P_COMMITTED
         return r, parts
 
     def _participant(self, row) -> SessionParticipant:
@@ -871,7 +871,7 @@ class DeviceCommitmentEngine(CommitmentEngine):
             return None
         return CommitmentRecord(
             session_id=sso.session_id, merkle_root=x.merkle_root,
-            participant_dids=[p.agent_did for p in x.participants], delta_count=x.commit_count,
+            participant_dids=x.commit_dids, delta_count=x.commit_count,
             committed_at=x.committed_at,
         )
 
@@ -915,7 +915,7 @@ class DeviceCommitmentEngine(CommitmentEngine):
             if x.committed_at is not None:
                 out[x.session_id] = CommitmentRecord(
                     session_id=x.session_id, merkle_root=x.merkle_root,
-                    participant_dids=[p.agent_did for p in x.participants], delta_count=x.commit_count,
+                    participant_dids=x.commit_dids, delta_count=x.commit_count,
                     committed_at=x.committed_at)
         out.update(self._commitments)
         return out
@@ -1258,16 +1258,19 @@ def snapshots_rows(store: GovernanceStore, slots, ids: list, creators: list,
         s.commit_count = (int(h[4]) >> 32) & 0xFFFFFFFF
         s.merkle_root = "".join(f"{int(w):016x}" for w in h[12:16]) if c else None
         if parts:
-            plist = []
+            plist, committed = [], []
             for k in range(pc):
                 a, fl, sr, se, j = (int(x) for x in prt[i, k])
-                if (fl >> 8) & 0xFF:
+                if (fl >> 9) & 1:  # P_COMMITTED: active when the root was committed
+                    committed.append(store.did(_i64(a)))
+                if (fl >> 8) & 1:  # P_ACTIVE
                     plist.append(SessionParticipant(
                         agent_did=store.did(_i64(a)), ring=_RINGS[fl & 0xFF], sigma_raw=bitsd(sr), sigma_eff=bitsd(se),
                         joined_at=from_us(_i64(j)), is_active=True))
             s.participants = plist
+            s.commit_dids = committed
         else:
-            s.participants = None
+            s.participants = s.commit_dids = None
         out.append(s)
     return out
 

@@ -14,7 +14,8 @@ class SessionSnapshot:
     the list / aggregate views need, without a device round trip per field."""
 
     __slots__ = ("session_id", "state", "consistency_mode", "participant_count", "created_at", "terminated_at",
-                 "delta_count", "participants", "creator_did", "committed_at", "commit_count", "merkle_root")
+                 "delta_count", "participants", "creator_did", "committed_at", "commit_count", "merkle_root",
+                 "commit_dids")
 
     @classmethod
     def of(cls, sso, parts: bool = False) -> "SessionSnapshot":
@@ -29,5 +30,5 @@ class SessionSnapshot:
         s.creator_did = sso.creator_did
         s.delta_count = None
         s.participants = list(sso.participants) if parts else None
-        s.committed_at = s.commit_count = s.merkle_root = None  # host: ask the CommitmentEngine
+        s.committed_at = s.commit_count = s.merkle_root = s.commit_dids = None  # host: ask the CommitmentEngine
         return s

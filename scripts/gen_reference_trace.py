@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Record the reference implementation's results for the golden trace.
+
+Runs ``tests/golden_trace.py``'s operation script under the REFERENCE package
+(``/root/reference/src``, read-only; imported in a child interpreter whose
+``sys.path`` does not contain this repository) with its ``datetime.now`` pinned to
+the trace clock and ``uuid.uuid4`` seeded (so a re-recording is identical), and writes ``tests/fixtures/reference_trace.json``:
+``{"seed", "ops", "sids", "results"}``.
+
+    python scripts/gen_reference_trace.py [--check]
+
+``--check`` compares a fresh recording with the committed fixture instead of
+writing it (``tests/test_reference_trace.py`` runs this when the reference is
+mounted, so the fixture stays pinned to the reference's behaviour).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_SRC = "/root/reference/src"
+FIXTURE = os.path.join(ROOT, "tests", "fixtures", "reference_trace.json")
+SEED = 2026
+
+_CHILD = r"""
+import asyncio, datetime as _dt, importlib.util, json, sys
+spec = importlib.util.spec_from_file_location("golden_trace", sys.argv[1])
+gt = importlib.util.module_from_spec(spec); spec.loader.exec_module(gt)
+import random, uuid
+_urng = random.Random(int(sys.argv[3]))
+uuid.uuid4 = lambda: uuid.UUID(int=_urng.getrandbits(128), version=4)  # reproducible ids across recordings
+import hypervisor  # the reference package (only REF_SRC is on sys.path)
+assert hypervisor.__file__.startswith(sys.argv[2]), hypervisor.__file__
+cur = [gt.BASE_US]
+class PinnedDatetime(_dt.datetime):
+    @classmethod
+    def now(cls, tz=None):
+        t = gt.at(cur[0])
+        return t if tz is not None else t.replace(tzinfo=None)
+    @classmethod
+    def utcnow(cls):
+        return gt.at(cur[0]).replace(tzinfo=None)
+def pin():
+    for name, mod in list(sys.modules.items()):
+        if name.split(".")[0] == "hypervisor" and getattr(mod, "datetime", None) is _dt.datetime:
+            mod.datetime = PinnedDatetime
+import pkgutil
+for m in pkgutil.walk_packages(hypervisor.__path__, "hypervisor."):
+    try:
+        importlib.import_module(m.name)
+    except Exception:
+        pass
+pin()
+def set_now(us):
+    cur[0] = us
+seed = int(sys.argv[3])
+ops = gt.make_ops(seed)
+out = asyncio.run(gt.run_ops(ops, set_now))
+json.dump({"seed": seed, "ops": ops, "sids": out["sids"], "results": out["results"]}, sys.stdout)
+"""
+
+
+def record(seed: int = SEED) -> dict:
+    env = {k: v for k, v in os.environ.items() if k not in ("PYTHONPATH",)}
+    env.update(PYTHONPATH=REF_SRC, PYTHONDONTWRITEBYTECODE="1")
+    p = subprocess.run([sys.executable, "-c", "import importlib; " + _CHILD, os.path.join(ROOT, "tests", "golden_trace.py"),
+                        REF_SRC, str(seed)], capture_output=True, text=True, env=env, cwd="/tmp", timeout=600)
+    if p.returncode != 0:
+        raise RuntimeError(p.stderr[-4000:])
+    return json.loads(p.stdout)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--check", action="store_true")
+    args = ap.parse_args()
+    rec = record()
+    if args.check:
+        with open(FIXTURE) as f:
+            old = json.load(f)
+        same = old == json.loads(json.dumps(rec))
+        print("fixture matches the reference" if same else "fixture DIFFERS from the reference")
+        return 0 if same else 1
+    os.makedirs(os.path.dirname(FIXTURE), exist_ok=True)
+    with open(FIXTURE, "w") as f:
+        json.dump(rec, f, separators=(",", ":"))
+        f.write("\n")
+    errs = sum(1 for r in rec["results"] if "error" in r)
+    print(f"wrote {FIXTURE}: {len(rec['ops'])} ops, {errs} reference errors recorded")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
