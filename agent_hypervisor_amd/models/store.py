@@ -361,8 +361,13 @@ class GovernanceStore:
         return -1 if d is None else d.get(session_id, -1)
 
     # -- transport -----------------------------------------------------------
-    def post(self, op: int, args: list, inline: Optional[bytes] = None) -> int:
-        return self._c.post(op, args, inline)
+    def post(self, op: int, args: list, inline: Optional[bytes] = None, keep: bool = False) -> int:
+        """Post a command; ``keep``: its results survive the recycling of its result
+        slot until they are read (for results awaited after other sessions' posts)."""
+        q = self._c.post(op, args, inline)
+        if keep:
+            self._c.keep(q)
+        return q
 
     def call(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
         return self._c.call(op, args, nres, inline)

@@ -51,6 +51,9 @@ def api_throughput(device: str, n: int = 10_000, rounds: int = 3, warm: int = 50
     async def batch(k):
         return await asyncio.gather(*[reference_pipeline(device) for _ in range(k)])
 
+    from hypervisor.config import tune_gc
+
+    old = tune_gc()  # the serving process's collector thresholds (AHV_GC_THRESHOLD), same for both paths
     asyncio.run(batch(warm))
     rates = []
     roots_ok = True
@@ -63,6 +66,7 @@ def api_throughput(device: str, n: int = 10_000, rounds: int = 3, warm: int = 50
         roots_ok = roots_ok and all(r is not None and len(r) == 64 for r in roots)
         # every pipeline computes the same chain shape but distinct ids → distinct roots
         roots_ok = roots_ok and len(set(roots)) == n
+    gc.set_threshold(*old)
     return {"device": device, "concurrent_pipelines": n, "pipelines_per_s": round(statistics.median(rates), 1),
             "rounds": [round(r, 1) for r in rates], "roots_ok": roots_ok}
 

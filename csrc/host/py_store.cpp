@@ -374,6 +374,15 @@ class Store {
     return out;
   }
 
+  // Keep the results of `q` even if its slot is recycled before they are read
+  // (a posted command whose result is awaited later, after an unbounded number
+  // of other sessions' posts — e.g. the saga step's posted EXECUTING transition
+  // under thousands of concurrent pipelines).  Consumed by try_result/result.
+  void keep(uint64_t q) {
+    if (q >= next_) throw std::out_of_range("store: sequence number not posted");
+    if (q + static_cast<uint64_t>(nslots_) >= next_) watched_[q] = 1;
+  }
+
   // Non-blocking form for the asyncio API: the results of `q` if it completed
   // within `spin_ns` (0: just look), else None.  A worker that idled out
   // between the post and now is relaunched.
@@ -694,6 +703,7 @@ void register_store(py::module_& m) {
            py::arg("staging_bytes") = 1 << 22, py::arg("bulk_bytes") = 1 << 24, py::arg("idle_us") = 500,
            py::arg("max_ms") = 2000)
       .def("post", &Store::post, py::arg("op"), py::arg("args"), py::arg("inline") = py::none())
+      .def("keep", &Store::keep, py::arg("seq"))
       .def("call", &Store::call, py::arg("op"), py::arg("args"), py::arg("nres") = 4, py::arg("inline") = py::none())
       .def("result", &Store::result, py::arg("seq"), py::arg("nres") = 4)
       .def("try_result", &Store::try_result, py::arg("seq"), py::arg("nres") = 4, py::arg("spin_ns") = 0)

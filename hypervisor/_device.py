@@ -1005,7 +1005,7 @@ class DeviceSagaStep(SagaStep):
         :meth:`check_posted`); the worker applies commands in order."""
         to = _STEPS.index(StepState(new_state))
         self.__dict__["_hint"] = None
-        return self._store.post(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry])
+        return self._store.post(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], keep=True)
 
     async def check_posted(self, seq: int, new_state: StepState) -> None:
         self._transitioned(await self._store.result_async(seq, 2), new_state)

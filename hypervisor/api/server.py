@@ -407,6 +407,9 @@ def create_app(hypervisor: Optional[Hypervisor] = None, event_bus: Optional[Hype
     async def lifespan(application: FastAPI):
         if getattr(application.state, "hv", None) is None:
             application.state.hv = ApiState(bus=event_bus or HypervisorEventBus(), hv=hypervisor)
+        from hypervisor.config import tune_gc
+
+        tune_gc()  # a serving process: collector thresholds for many in-flight sessions
         yield
         application.state.hv = None
 

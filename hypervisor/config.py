@@ -25,6 +25,9 @@ vouch_capacity              AHV_VOUCH_CAPACITY    device vouch-edge rows per ran
 use_hip_graphs              AHV_HIP_GRAPHS    capture steady-state launches in hipGraphs
 collective_epoch            AHV_COLLECTIVE_EPOCH  pipeline steps between cross-rank
                                      liability/commitment flushes
+gc_threshold                AHV_GC_THRESHOLD  ``gen0,gen1,gen2`` collector thresholds that
+                                     :func:`tune_gc` installs for a serving process
+                                     (the REST app and the API benches call it)
 ==========================  =======  ===============================================
 """
 
@@ -57,6 +60,7 @@ class HypervisorRuntimeConfig:
     vouch_capacity: int = 1 << 22
     use_hip_graphs: bool = True
     collective_epoch: int = 1
+    gc_threshold: str = "50000,50,1000"
 
     @classmethod
     def from_env(cls) -> "HypervisorRuntimeConfig":
@@ -70,6 +74,7 @@ class HypervisorRuntimeConfig:
             vouch_capacity=_env_int("AHV_VOUCH_CAPACITY", 1 << 22),
             use_hip_graphs=_env_bool("AHV_HIP_GRAPHS", True),
             collective_epoch=_env_int("AHV_COLLECTIVE_EPOCH", 1),
+            gc_threshold=os.environ.get("AHV_GC_THRESHOLD", "50000,50,1000"),
         )
 
     def as_dict(self) -> dict:
@@ -94,6 +99,25 @@ def store_mode(device=None) -> str:
         except Exception:
             return "host"
     return d
+
+
+def tune_gc() -> tuple:
+    """Install the serving process's cyclic-GC thresholds (``AHV_GC_THRESHOLD``;
+    ``off`` leaves the interpreter's defaults) and return the previous ones.
+
+    Thousands of in-flight sessions keep hundreds of thousands of objects alive;
+    with CPython's default gen-0 threshold (700 allocations) the collector re-walks
+    them continuously, which measured 2.4-2.9x of the per-call API's throughput
+    under 10^4 concurrent pipelines (host engines and device store alike).  Nothing
+    in the governance engines relies on prompt cycle collection.
+    """
+    import gc
+
+    old = gc.get_threshold()
+    spec = (RUNTIME.gc_threshold or "").strip().lower()
+    if spec and spec != "off":
+        gc.set_threshold(*(int(x) for x in spec.split(",")))
+    return old
 
 
 def set_parity_mode(on: bool) -> None:
