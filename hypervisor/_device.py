@@ -79,8 +79,15 @@ def _i64(v: int) -> int:
     return v - (1 << 64) if v >= 1 << 63 else v
 
 
+_PACK8 = struct.Struct(">8I").pack
+
+
 def _hex(words) -> str:
-    return "".join(f"{int(w) & 0xFFFFFFFF:08x}" for w in words)
+    """Hex of eight 32-bit digest words (one struct pack: ~10x the per-word format)."""
+    try:
+        return _PACK8(*words).hex()
+    except struct.error:  # not eight words in range
+        return "".join(f"{int(w) & 0xFFFFFFFF:08x}" for w in words)
 
 
 def _words(hexstr: str) -> list[int]:

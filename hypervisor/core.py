@@ -51,7 +51,7 @@ from hypervisor.audit.delta import DeltaEngine
 from hypervisor.audit.gc import EphemeralGC, RetentionPolicy
 from hypervisor.liability.slashing import SlashingEngine
 from hypervisor.liability.vouching import VouchingEngine
-from hypervisor.models import ActionDescriptor, ConsistencyMode, ExecutionRing, SessionConfig
+from hypervisor.models import ActionDescriptor, ConsistencyMode, ExecutionRing, SessionConfig, SessionState
 from hypervisor.reversibility.registry import ReversibilityRegistry
 from hypervisor.rings.classifier import ActionClassifier
 from hypervisor.rings.enforcer import RingEnforcer
@@ -273,26 +273,21 @@ class Hypervisor:
     async def _terminate_device(self, session_id: str, managed: ManagedSession) -> Optional[str]:
         """One device command: terminate → Merkle root (K09) → commit → release the
         session's bonds (K07) → GC retention count → archive."""
-        from datetime import timedelta
-
-        from agent_hypervisor_amd.models import store as _st
-        from hypervisor._clock import now as _now, to_us
-        from hypervisor._device import _check, _hex, _lifecycle
-        from hypervisor.models import SessionState
+        from hypervisor import _device as _d  # loaded with the device store (device mode only)
 
         sso, de, st = managed.sso, managed.delta_engine, self._store
-        now = _now()
+        now_us = _d.to_us(_d._now())
         v = st.liability_lookup(self._tenant, session_id)
-        cutoff = now - timedelta(days=self.gc.policy.delta_retention_days)
+        cutoff = now_us - int(self.gc.policy.delta_retention_days * 86_400_000_000)
         n, off, inl = st.index_args(de._indices())
         r = await st.call_async(
-            _st.OP_SESS_CLOSE,
-            [sso.slot, n, off, to_us(now), v, to_us(cutoff), int(bool(sso.config.enable_audit))], 13, inl,
+            _d._st.OP_SESS_CLOSE, [sso.slot, n, off, now_us, v, cutoff, int(bool(sso.config.enable_audit))], 13, inl,
         )
-        if r[0] == _st.ST_BAD_STATE:
-            raise _lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
-        _check(r, "terminate")
-        root = _hex(r[2:10]) if r[1] else None
+        if r[0]:
+            if r[0] == _d._st.ST_BAD_STATE:
+                raise _d._lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
+            _d._check(r, "terminate")
+        root = _d._hex(r[2:10]) if r[1] else None
         if v >= 0:  # every bond of the session is released now: freeze the records, reuse the edge rows
             self.vouching.retire_session(session_id)
         if root:
