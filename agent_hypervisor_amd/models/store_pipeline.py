@@ -236,6 +236,37 @@ class _Batch:
             pass
 
 
+def mixed_specs(n: int, seed: int = 5, distinct: int = 4096, agents: int = 64, prefix: str = "did:mesh:m") -> list:
+    """``n`` heterogeneous pipelines (a pool of ``distinct`` random specs, dealt
+    out in a seeded order): 1–5 joins with per-agent σ (some refused by the gate
+    or by capacity), 0–4 audit deltas of 0–3 changes by varying agents, 0–3 saga
+    steps with retries, failures and compensation, varied configs, and sessions
+    that never activate or terminate.  The mix ``bench.py --mix hetero`` times."""
+    import random
+
+    from hypervisor.models import SessionConfig
+
+    rng = random.Random(seed)
+    dids = [f"{prefix}{k}" for k in range(agents)]
+    sigmas = [0.3, 0.55, 0.61, 0.7, 0.8, 0.96]
+    pool = []
+    for _ in range(distinct):
+        joins = tuple((rng.choice(dids), rng.choice(sigmas + [rng.random()])) for _ in range(rng.randint(1, 5)))
+        deltas = tuple((rng.choice(dids), tuple((f"/p{rng.randrange(50)}", rng.choice(["add", "update", "delete"]),
+                                                 rng.choice([None, f"h{rng.randrange(1000)}"]))
+                                                for _ in range(rng.randrange(0, 4))))
+                       for _ in range(rng.randrange(0, 5)))
+        steps = tuple((f"act{k}", rng.choice(dids), f"/api/{k}", rng.choice([None, f"/undo/{k}"]),
+                       rng.randrange(0, 3), rng.choice([0, 0, 0, 1, 2, 5])) for k in range(rng.randrange(0, 4)))
+        cfg = SessionConfig(max_participants=rng.choice([2, 3, 10]), min_sigma_eff=rng.choice([0.5, 0.6, 0.9]),
+                            enable_audit=rng.random() < 0.9)
+        pool.append(PipelineSpec(joins=joins, deltas=deltas, steps=steps, activate=rng.random() < 0.95,
+                                 terminate=rng.random() < 0.9, compensate=rng.random() < 0.7, config=cfg,
+                                 creator_did=rng.choice(dids)))
+    order = np.random.default_rng(seed).integers(0, distinct, size=n)
+    return [pool[i] for i in order.tolist()]
+
+
 def _spec(b: _Batch, i: int) -> PipelineSpec:
     return b.specs if b.shared else b.specs[i]
 
@@ -272,8 +303,25 @@ class _CfgHolder:
 
 def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
     """Build the batch arrays, run the store pipeline, register lazy sessions."""
-    import time
+    return finish(hv, launch(prepare(hv, specs, n)))
 
+
+class Prepared:
+    """A packed batch: its store rows (allocated), device argument arrays and the
+    host-side metadata :func:`finish` needs.  :func:`launch` runs it; a benchmark
+    may re-run the same batch after :meth:`reset` (the rows freed in place)."""
+
+    def reset(self) -> None:
+        """Free the batch's session / saga / step rows in place (on the stream), so
+        :func:`launch` can run the whole pipeline over them again."""
+        t = self.store.tables
+        for col, ix in (("s_state", self.tens["slot"]), ("g_state", self.g_live), ("t_state", self.t_live)):
+            if ix is not None and ix.numel():
+                t[col].index_fill_(0, ix.to(torch.int64), 255)  # kFree8
+
+
+def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
+    """Pack ``specs`` into device arrays over freshly allocated store rows."""
     from hypervisor._clock import now_us
     from hypervisor.models import ConsistencyMode, SessionConfig
 
@@ -403,44 +451,85 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
     }
     args = {k: v.data_ptr() for k, v in tens.items()}
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
-    cuda = dev.type == "cuda"
-    t_dev = time.perf_counter()
-    if cuda:
-        st.drain()
-        st.flush()  # the worker's row writes (frees) are visible to the batch kernels
-        stream = torch.cuda.current_stream(dev)
-        st._c.run_pipeline(args, stream.cuda_stream)
-    else:
-        st._c.run_pipeline(args, 0)
-    # K09: roots of the committed chains over the digests just written → s_root
-    status = tens["status"]
     committed = [i for i in range(n) if (int(flags[i]) & 9) == 9 and delta_off[i + 1] > delta_off[i]] \
         if not shared else (list(range(n)) if (int(flags[0]) & 9) == 9 and delta_off[1] > 0 else [])
-    drow_np = np.frombuffer(drows, dtype=np.int32)
-    if committed:
-        from agent_hypervisor_amd.ops import audit as A
+    p = Prepared()
+    p.store, p.specs, p.shared, p.n, p.nd, p.ids, p.slots, p.t0 = st, specs, shared, n, nd, ids, slots, t0
+    p.tens, p.args, p.flags, p.committed, p.j_agent = tens, args, flags, committed, j_agent
+    p.drows, p.doff, p.delta_off, p.gslots, p.step_off, p.tslots = drows, doff, delta_off, gslots, step_off, tslots
+    p.g_live = tens["gslot"][tens["gslot"] >= 0] if ng else None
+    p.t_live = tens["tslot"] if nsteps else None
+    p.device_seconds = 0.0
+    return p
 
+
+def _k09_plan(p: "Prepared") -> Optional[tuple]:
+    """(committed session indices, leaf delta rows, chain offsets, committed slots)
+    on the device, built once per batch."""
+    plan = p.__dict__.get("_k09")
+    if plan is None and p.committed:
+        st, tens, n, delta_off, committed = p.store, p.tens, p.n, p.delta_off, p.committed
+        dev = st.device
         cix = torch.as_tensor(committed, dtype=torch.int64).to(dev)
-        if shared:
+        if p.shared:
             k = int(delta_off[1])
             leaves_idx = tens["drow"].view(n, k).index_select(0, cix).reshape(-1).to(torch.int64)
             offs = torch.arange(0, (len(committed) + 1) * k, k, dtype=torch.int32, device=dev)
         else:
-            lens = [int(delta_off[i + 1] - delta_off[i]) for i in committed]
-            leaves_idx = torch.as_tensor(np.concatenate([drow_np[delta_off[i]:delta_off[i + 1]] for i in committed]),
-                                         dtype=torch.int64).to(dev)
+            c = np.asarray(committed, dtype=np.int64)
+            lo, hi = delta_off[c].astype(np.int64), delta_off[c + 1].astype(np.int64)
+            lens = hi - lo
+            # the committed chains' delta rows, concatenated (vectorized segment gather)
+            seg = np.repeat(lo - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
+            drow_np = np.frombuffer(p.drows, dtype=np.int32)
+            leaves_idx = torch.as_tensor(drow_np[seg], dtype=torch.int64).to(dev)
             offs = torch.as_tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32).to(dev)
-        hashes = st.tables["d_hash"].view(-1, 8)
-        r = A.merkle_roots(offs, hashes.index_select(0, leaves_idx).contiguous())
-        sl = tens["slot"].index_select(0, cix).to(torch.int64)
+        plan = p.__dict__["_k09"] = (cix, leaves_idx, offs, tens["slot"].index_select(0, cix).to(torch.int64))
+    return plan
+
+
+def launch(p: "Prepared", sync: bool = True) -> "Prepared":
+    """Run a prepared batch: rows / render / chain kernels, then K09 roots of the
+    committed chains into ``s_root`` (stream-ordered; ``sync``: wait for them and
+    let the store worker see the rows)."""
+    import time
+
+    st = p.store
+    dev = st.device
+    cuda = dev.type == "cuda"
+    t_dev = time.perf_counter()
+    if cuda:
+        if sync:
+            st.drain()
+            st.flush()  # the worker's row writes (frees) are visible to the batch kernels
+        st._c.run_pipeline(p.args, torch.cuda.current_stream(dev).cuda_stream)
+    else:
+        st._c.run_pipeline(p.args, 0)
+    # K09: roots of the committed chains over the digests just written → s_root
+    plan = _k09_plan(p)
+    if plan is not None:
+        from agent_hypervisor_amd.ops import audit as A
+
+        _, leaves_idx, offs, sl = plan
+        r = A.merkle_roots(offs, st.tables["d_hash"].view(-1, 8).index_select(0, leaves_idx))
         ok = st.tables["s_committed"].index_select(0, sl) != 0  # terminated with audit: committed
         st.tables["s_root"].view(-1, 8)[sl] = torch.where(ok[:, None], r, torch.zeros_like(r))
-    if cuda:
+    if cuda and sync:
         torch.cuda.synchronize(dev)
         st.acquire()  # the worker sees the batch's rows
-    dev_s = time.perf_counter() - t_dev
+    p.device_seconds = time.perf_counter() - t_dev
+    return p
+
+
+def finish(hv, p: "Prepared") -> PipelineRun:
+    """Read back what the lazy views need and register the batch's sessions."""
+    st, tens, n, nd, shared = p.store, p.tens, p.n, p.nd, p.shared
+    specs, ids, slots, t0, committed = p.specs, p.ids, p.slots, p.t0, p.committed
+    doff, delta_off, gslots, step_off, tslots = p.doff, p.delta_off, p.gslots, p.step_off, p.tslots
+    drow_np = np.frombuffer(p.drows, dtype=np.int32)
+    j_agent = p.j_agent
     # results the lazy views need, in one copy each
-    status_np = status.cpu().numpy()
+    status_np = tens["status"].cpu().numpy()
     dlen = tens["dcap"]  # replaced below by the rendered lengths
     hidx = (drow_np.astype(np.int64)[:, None] * 8 + np.arange(8, dtype=np.int64)[None, :]).reshape(-1)
     gath = st.gather({"d_len": drow_np, "d_hash": hidx}) \
@@ -467,7 +556,7 @@ def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
     register_lazy(hv, b, status_np, cidx)
     run_ = PipelineRun(session_ids=ids, status=status_np,
                        join_rings=tens["join_ring"].cpu().numpy()[: len(j_agent)],
-                       join_codes=tens["join_code"].cpu().numpy()[: len(j_agent)], device_seconds=dev_s)
+                       join_codes=tens["join_code"].cpu().numpy()[: len(j_agent)], device_seconds=p.device_seconds)
     run_._roots = (cidx, flat)
     return run_
 

@@ -156,6 +156,10 @@ def main() -> None:
                     help="join the liability side stream with the pipeline stream every step (A/B)")
     ap.add_argument("--bond-degree", type=int, default=4, help="resident vouch edges per agent")
     ap.add_argument("--slash-k", type=int, default=1024, help="vouchees slashed per step (X02 stage)")
+    ap.add_argument("--mix", choices=("template", "hetero"), default="template",
+                    help="template: the reference pipeline for every session (headline kernel); hetero: a "
+                         "heterogeneous mix (store_pipeline.mixed_specs) through the public batched API's kernels "
+                         "over store rows (rows / render / chain + K09 roots, rows freed and rebuilt every step)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                     help="cpu runs the host twin of the kernel over gloo (multi-process CPU rehearsal)")
     args = ap.parse_args()
@@ -247,6 +251,33 @@ def main() -> None:
         L["bonds"].slash_clip(L["ids"], 0.95, L["pid"], L["pf"], L["cur"])  # K06 stage
         merge_slash_fixed(L["sigma"], L["ids"], L["pid"], L["pf"], factor=L["factor"])  # X02
 
+    hetero = None
+    if args.mix == "hetero":
+        # The public batched API's kernels over the device store (Hypervisor.run_pipelines):
+        # the batch is packed once (host), then every step frees its rows in place and
+        # runs the whole pipeline over them again (create, joins, activate, rendered
+        # and SHA-chained deltas, sagas with retries/compensation, terminate, K09 roots).
+        from agent_hypervisor_amd.models import store_pipeline as SP
+        from hypervisor import Hypervisor
+
+        os.environ.setdefault("AHV_STORE_SESSIONS", str(1 << 21))
+        hv = Hypervisor(device="cuda" if dev.type == "cuda" else "cpu")
+        hp = SP.prepare(hv, SP.mixed_specs(S, seed=11 + rank))
+        SP.launch(hp)  # first run (also builds the K09 plan)
+        status0 = hp.tens["status"].clone()
+        hetero = {"hv": hv, "p": hp, "status0": status0,
+                  "deltas": int(hp.nd), "committed": len(hp.committed), "ok": int((status0 == 0).sum())}
+
+    def run_batch(st, agents):
+        if hetero is None:
+            eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
+            return
+        hp = hetero["p"]
+        hp.reset()
+        SP.launch(hp, sync=False)
+        st[0] = S
+        st[1] = (hp.tens["status"] == 0).sum()
+
     def step():
         b = it[0] & 1
         it[0] += 1
@@ -266,7 +297,7 @@ def main() -> None:
                 liability_step()
         st.zero_()
         agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
-        eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
+        run_batch(st, agents)
         works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if multi else None
         if side is not None:
             if args.join_liability:
@@ -284,6 +315,8 @@ def main() -> None:
             liab["work"].wait()
             liab["work"] = None
 
+    if args.graph and hetero is not None:
+        raise SystemExit("--graph captures the template pipeline; --mix hetero runs on the stream")
     if args.graph:
         from agent_hypervisor_amd.runtime.graphs import PipelineGraph
 
@@ -345,6 +378,9 @@ def main() -> None:
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     totals = last.cpu().tolist()
+    if hetero is not None:  # every re-run produced exactly the first run's per-session outcomes
+        sync()
+        assert torch.equal(hetero["p"].tens["status"], hetero["status0"]), "hetero batch outcomes changed between runs"
     # X09: job-wide step-latency histogram (log2 µs bins), summed over ranks outside the timed loop
     from agent_hypervisor_amd.parallel.collectives import reduce_histogram
 
@@ -380,13 +416,13 @@ def main() -> None:
             "dtype": "fp64",
             "data": "synthetic",
             "config": {
-                "model": "full_governance_pipeline",
+                "model": "full_governance_pipeline" if hetero is None else "heterogeneous_governance_pipeline",
                 "global_batch": S * world,
-                "seq_len": args.deltas,
+                "seq_len": args.deltas if hetero is None else round(hetero["deltas"] / S, 3),
                 "parallelism": f"dp{world}",
                 "sessions_per_gpu": S,
                 "agents_per_gpu": args.agents,
-                "deltas_per_session": args.deltas,
+                "deltas_per_session": args.deltas if hetero is None else round(hetero["deltas"] / S, 3),
             },
             "batch_p50_ms": round(statistics.median(lat) * 1000.0, 4),
             "pipeline_launch": "hipgraph" if args.graph else "stream",
@@ -408,6 +444,11 @@ def main() -> None:
                 "x01_exposure_allreduce_bytes": x01_bytes if liab is not None else 0,
                 "x02_slash_allgather_bytes_per_rank": x02_bytes if liab is not None else 0,
             },
+            "mix": args.mix,
+            "hetero": None if hetero is None else {
+                "sessions": S, "deltas": hetero["deltas"], "committed_roots": hetero["committed"],
+                "sessions_all_stages_admitted": hetero["ok"], "spec_pool": 4096,
+                "path": "store_pipeline rows/render/chain kernels + K09 over store rows"},
             "liability_stage": None if liab is None else {
                 "agents": args.agents, "resident_edges": liab["bonds"].edges, "slash_k": args.slash_k,
                 "bond_graph_bytes": liab["bonds"].nbytes, "in_timed_region": True,

@@ -204,3 +204,23 @@ def test_bench_ranks_over_gloo(world):
     assert out["config"]["global_batch"] == 256 * world
     assert out["last_step_counters"]["sessions"] == 256 * world and out["last_step_counters"]["ok"] == 256 * world
     assert out["value"] > 0 and out["steps"] == 3 and out["warmup"] == 1
+
+
+@pytest.mark.slow
+def test_bench_hetero_mix_over_gloo():
+    """``bench.py --mix hetero`` at 2 ranks on the CPU twin: each rank re-runs its
+    packed heterogeneous batch every step over freed store rows, and the outcomes of
+    every re-run equal the first run's (asserted inside bench.py)."""
+    port = _free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="1", AHV_SKIP_AUTOBUILD="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--device", "cpu", "--mix", "hetero", "--sessions", "1500", "--agents", "2048",
+           "--steps", "2", "--warmup", "1", "--no-scalar"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["mix"] == "hetero" and out["config"]["model"] == "heterogeneous_governance_pipeline"
+    assert out["last_step_counters"]["sessions"] == 3000 and 0 < out["last_step_counters"]["ok"] < 3000
+    h = out["hetero"]
+    assert h["sessions"] == 1500 and h["deltas"] > 1500 and 0 < h["committed_roots"] <= 1500

@@ -46,3 +46,15 @@ def test_sharded_hypervisor_rccl_one_rank(cuda_device):
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert out["ok"] and out["backend"] == "nccl" and out["store_gpu"]
+
+
+def test_bench_hetero_mix_gfx950(cuda_device):
+    """``bench.py --mix hetero`` on the GPU: the public batched API's kernels over
+    store rows, re-run every step; outcomes identical across re-runs."""
+    env = dict(os.environ, AHV_SKIP_AUTOBUILD="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mix", "hetero", "--sessions", "65536",
+           "--agents", "65536", "--steps", "3", "--warmup", "1", "--no-scalar", "--no-api"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["mix"] == "hetero" and out["last_step_counters"]["sessions"] == 65536 and out["value"] > 0
