@@ -449,6 +449,25 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         "status": torch.zeros(n, dtype=torch.int32, device=dev),
         "pool_bytes": pb, "pool_off": po, "pool_len": pl,
     }
+    # lane orders that balance the waves: sessions by descending chain work (SHA
+    # blocks of their records), deltas by descending record size (stable sorts)
+    # The render pass also compresses each record's parent-independent blocks (all
+    # of a turn-1 record); the chain pass hashes the rest, ≈ the 4 blocks from the
+    # parent hole on.  Work estimates: render ∝ record bytes (+ the whole record
+    # again at turn 1, ~the part before the hole otherwise); chain ∝ later deltas.
+    cnt_d = np.diff(delta_off).astype(np.int64)
+    turn1 = np.zeros(nd, dtype=bool)
+    if nd:
+        turn1[delta_off[:-1][cnt_d > 0]] = True
+    capl = caps.astype(np.int64)
+    cs = np.concatenate([[0], np.cumsum(np.where(turn1, 0, 4))])
+    work = cs[delta_off[1:]] - cs[delta_off[:-1]]
+    tens["chain_order"] = T(np.argsort(-work, kind="stable").astype(np.int32))
+    if nd:
+        tens["render_order"] = T(np.argsort(-(capl + np.where(turn1, capl, np.maximum(capl - 260, 0))),
+                                            kind="stable").astype(np.int32))
+    tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
+    tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
     args = {k: v.data_ptr() for k, v in tens.items()}
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
     committed = [i for i in range(n) if (int(flags[i]) & 9) == 9 and delta_off[i + 1] > delta_off[i]] \

@@ -76,6 +76,10 @@ struct StorePipeArgs {
   const uint8_t* step_fail;     // [T] attempts that fail before success (≥ 1 + retries: the step fails)
   int64_t gc_retention_us;
   int32_t* status;              // [n] out: 0 ok, else first refused stage (StorePipeStatus)
+  uint32_t* mid;                // [Dn, 8] SHA-256 state after a record's parent-independent blocks, or null
+  int32_t* mid_blocks;          // [Dn] blocks `mid` covers (all of them for a turn-1 record: its digest)
+  const int32_t* chain_order;   // [n] sessions by descending SHA work (chain kernel lane order), or null
+  const int32_t* render_order;  // [Dn] deltas by descending record size (render kernel lane order), or null
 };
 
 enum StorePipeStatus : int32_t {
@@ -286,6 +290,25 @@ struct ArenaSink {
 
 // Lane per delta g (session `i`, turn k+1): render the record; the parent digest
 // is rendered as 66 placeholder bytes whose offset is recorded (d_hole).
+// Block `b` of the SHA-256 message of a `len`-byte record at w32 (big-endian
+// words, 0x80 terminator and bit length in the last of its `nblk` blocks).
+AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t b, uint32_t blk[16]) {
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const uint64_t o = 64 * b + 4 * w;
+    uint32_t x = 0;
+    if (o + 4 <= len) {
+      x = bswap32(w32[o / 4]);
+    } else if (o < len) {
+      x = bswap32(w32[o / 4]) & (0xffffffffu << (8 * (4 - (len - o))));
+    }
+    if (o <= len && len < o + 4) x |= 0x80u << (8 * (3 - (len - o)));
+    if (b == nblk - 1 && w == 14) x |= static_cast<uint32_t>((len * 8) >> 32);
+    if (b == nblk - 1 && w == 15) x |= static_cast<uint32_t>(len * 8);
+    blk[w] = x;
+  }
+}
+
 AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   const Tables& t = a.t;
   const int32_t k = g - a.delta_off[i];
@@ -340,7 +363,30 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   t.d_off[d] = a.doff[g];
   t.d_len[d] = static_cast<int32_t>(len);
   t.d_hole[d] = hole;
-  if (len > static_cast<uint32_t>(a.dcap[g])) a.status[i] = SP_RENDER;
+  if (len > static_cast<uint32_t>(a.dcap[g])) {
+    a.status[i] = SP_RENDER;
+    if (a.mid) a.mid_blocks[g] = 0;
+    return;
+  }
+  if (a.mid) {
+    // K08 split: the blocks before the parent hole (sort_keys puts agent_did,
+    // changes and delta_id first) — or the whole record of turn 1 — do not depend
+    // on the chain, so they are compressed here, one lane per record, and the
+    // serial chain pass resumes from this state.
+    const uint64_t nblk = (static_cast<uint64_t>(len) + 9 + 63) / 64;
+    const uint64_t pb = hole >= 0 ? static_cast<uint64_t>(hole) / 64 : nblk;
+    uint32_t h[8];
+    sha256_init(h);
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(t.payload + a.doff[g]);
+    for (uint64_t b = 0; b < pb; ++b) {
+      uint32_t blk[16];
+      sp_block(w32, len, nblk, b, blk);
+      sha256_compress(h, blk);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a.mid[8 * static_cast<int64_t>(g) + k] = h[k];
+    a.mid_blocks[g] = static_cast<int32_t>(pb);
+  }
 }
 
 // Lane per session: the SHA-256 chain over its records (K08).
@@ -362,24 +408,17 @@ AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
     }
     const uint32_t* w32 = reinterpret_cast<const uint32_t*>(rec);
     uint32_t h[8];
-    sha256_init(h);
     const uint64_t nblk = (len + 9 + 63) / 64;
-    for (uint64_t b = 0; b < nblk; ++b) {
-      uint32_t blk[16];
+    const uint64_t pb = a.mid ? static_cast<uint64_t>(a.mid_blocks[g]) : 0;  // compressed by the render pass
+    if (pb > 0) {
 #pragma unroll
-      for (int w = 0; w < 16; ++w) {
-        const uint64_t o = 64 * b + 4 * w;
-        uint32_t x = 0;
-        if (o + 4 <= len) {
-          x = bswap32(w32[o / 4]);
-        } else if (o < len) {
-          x = bswap32(w32[o / 4]) & (0xffffffffu << (8 * (4 - (len - o))));
-        }
-        if (o <= len && len < o + 4) x |= 0x80u << (8 * (3 - (len - o)));
-        if (b == nblk - 1 && w == 14) x |= static_cast<uint32_t>((len * 8) >> 32);
-        if (b == nblk - 1 && w == 15) x |= static_cast<uint32_t>(len * 8);
-        blk[w] = x;
-      }
+      for (int k = 0; k < 8; ++k) h[k] = a.mid[8 * static_cast<int64_t>(g) + k];
+    } else {
+      sha256_init(h);
+    }
+    for (uint64_t b = pb; b < nblk; ++b) {
+      uint32_t blk[16];
+      sp_block(w32, len, nblk, b, blk);
       sha256_compress(h, blk);
     }
 #pragma unroll
@@ -401,16 +440,23 @@ __global__ __launch_bounds__(256) void store_pipe_rows_kernel(StorePipeArgs a) {
 
 // lane per delta; `dsess` maps a delta to its session
 __global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd) {
-  const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (g < nd) {
+  const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (x < nd) {
+    const int64_t g = a.render_order ? a.render_order[x] : x;  // records of similar size per wave
     const int64_t i = dsess[g];
     if (a.status[i] != SP_ROW_IN_USE) sp_render(a, i, static_cast<int32_t>(g));
   }
 }
 
+// A lane's chain is serial and its length varies per session (0..k deltas of
+// varying size): lanes take sessions in descending-work order (chain_order), so
+// the 64 chains of a wave are about equally long and the wave does not idle most
+// lanes while its longest chain finishes.
 __global__ __launch_bounds__(64) void store_pipe_chain_kernel(StorePipeArgs a) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < a.n && a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
+  const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (x >= a.n) return;
+  const int64_t i = a.chain_order ? a.chain_order[x] : x;
+  if (a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
 }
 
 template <class T>
@@ -450,6 +496,10 @@ StorePipeArgs to_args(const Tables& t, const py::dict& d) {
   a.step_fail = P<const uint8_t>(d, "step_fail");
   a.gc_retention_us = d["gc_retention_us"].cast<int64_t>();
   a.status = P<int32_t>(d, "status");
+  a.chain_order = d.contains("chain_order") ? P<const int32_t>(d, "chain_order") : nullptr;
+  a.mid = d.contains("mid") ? P<uint32_t>(d, "mid") : nullptr;
+  a.mid_blocks = d.contains("mid_blocks") ? P<int32_t>(d, "mid_blocks") : nullptr;
+  a.render_order = d.contains("render_order") ? P<const int32_t>(d, "render_order") : nullptr;
   return a;
 }
 
