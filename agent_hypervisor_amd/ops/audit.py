@@ -93,17 +93,32 @@ def goal_hashes(goals: Sequence[str], step_ids: Sequence[str], device="cpu") -> 
     return [h[:16] for h in digests_to_hex(sha256_many(data, offs))]
 
 
-def merkle_roots(offsets: torch.Tensor, leaves: torch.Tensor) -> torch.Tensor:
-    """K09: Merkle root of each chain of leaf digests (zeros for empty chains)."""
+def merkle_roots(offsets: torch.Tensor, leaves: torch.Tensor, leaf_idx: Optional[torch.Tensor] = None,
+                 root_out: Optional[torch.Tensor] = None, root_row: Optional[torch.Tensor] = None,
+                 gate: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K09: Merkle root of each chain of leaf digests (zeros for empty chains).
+
+    Fused forms: ``leaf_idx`` (int64) — leaf i of the concatenated chains is row
+    ``leaf_idx[i]`` of ``leaves`` (a resident digest table: no gathered copy);
+    ``root_out`` + ``root_row`` (int64) — root c is written to row ``root_row[c]``
+    of ``root_out`` (e.g. the store's ``s_root``), zeros where ``gate[row] == 0``."""
     chains = offsets.numel() - 1
-    root = torch.empty((chains, 8), dtype=i32, device=leaves.device)
-    scratch = torch.empty_like(leaves)
-    launch(
-        "merkle",
-        {"chains": chains},
-        dict(offsets=offsets, leaves=leaves, scratch=scratch, root=root),
-        dict(offsets=i32, leaves=i32),
-    )
+    nleaf = leaf_idx.numel() if leaf_idx is not None else leaves.shape[0]
+    root = root_out if root_out is not None else torch.empty((chains, 8), dtype=i32, device=leaves.device)
+    scratch = torch.empty((max(1, nleaf), 8), dtype=i32, device=leaves.device)
+    tensors = dict(offsets=offsets, leaves=leaves, scratch=scratch, root=root)
+    dtypes = dict(offsets=i32, leaves=i32)
+    if leaf_idx is not None:
+        if offsets.device.type == "cpu" and nleaf and int(leaf_idx.max()) >= leaves.shape[0]:
+            raise IndexError("merkle_roots: leaf_idx out of range")
+        tensors["leaf_idx"], dtypes["leaf_idx"] = leaf_idx, torch.int64
+    if root_row is not None:
+        if root_out is None:
+            raise ValueError("merkle_roots: root_row needs root_out")
+        tensors["root_row"], dtypes["root_row"] = root_row, torch.int64
+        if gate is not None:
+            tensors["gate"], dtypes["gate"] = gate, torch.int64
+    launch("merkle", {"chains": chains}, tensors, dtypes)
     return root
 
 

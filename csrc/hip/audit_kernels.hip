@@ -435,8 +435,9 @@ struct GlobalStash {
 
 AHV_HD void merkle_elem(const MerkleArgs& a, int64_t c) {
   const int32_t b = a.offsets[c], e = a.offsets[c + 1];
-  uint32_t* root = a.root + c * 8;
-  if (e <= b) {
+  const int64_t row = a.root_row ? a.root_row[c] : c;
+  uint32_t* root = a.root + row * 8;
+  if (e <= b || (a.root_row && a.gate && a.gate[row] == 0)) {
     for (int k = 0; k < 8; ++k) root[k] = 0;
     return;
   }
@@ -445,7 +446,9 @@ AHV_HD void merkle_elem(const MerkleArgs& a, int64_t c) {
   merkle_root_levels(
       gs, static_cast<uint32_t>(e - b),
       [&](uint32_t i, uint32_t h[8]) {
-        for (int k = 0; k < 8; ++k) h[k] = a.leaves[(static_cast<int64_t>(b) + i) * 8 + k];
+        const int64_t li = static_cast<int64_t>(b) + i;
+        const int64_t src = a.leaf_idx ? a.leaf_idx[li] : li;  // the leaf gather, fused
+        for (int k = 0; k < 8; ++k) h[k] = a.leaves[src * 8 + k];
       },
       r);
   for (int k = 0; k < 8; ++k) root[k] = r[k];

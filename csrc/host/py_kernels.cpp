@@ -260,6 +260,9 @@ static MerkleArgs to_merkle(const py::dict& d) {
   MerkleArgs a{};
   V(chains, int64_t); P(offsets, const int32_t); P(leaves, const uint32_t); P(scratch, uint32_t);
   P(root, uint32_t);
+  if (d.contains("leaf_idx")) P(leaf_idx, const int64_t);
+  if (d.contains("root_row")) P(root_row, const int64_t);
+  if (d.contains("gate")) P(gate, const int64_t);
   return a;
 }
 static VerifyArgs to_verify(const py::dict& d) {

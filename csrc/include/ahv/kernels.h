@@ -350,6 +350,10 @@ struct MerkleArgs {
   const uint32_t* leaves;  // [L, 8]
   uint32_t* scratch;       // [L, 8] level buffer
   uint32_t* root;          // [chains, 8] (zeros for empty chains)
+  // optional fusions (null = off)
+  const int64_t* leaf_idx;  // [L] leaf i of the concatenated list is leaves row leaf_idx[i] (gather fused)
+  const int64_t* root_row;  // [chains] root c is written to root row root_row[c] (scatter fused)
+  const int64_t* gate;      // with root_row: a zero gate[root_row[c]] writes a zero root (uncommitted)
 };
 void launch_merkle(const MerkleArgs&, hipStream_t);
 void merkle_host(const MerkleArgs&);
