@@ -20,12 +20,17 @@
 //   store_pipe_render_kernel  lane per delta: the canonical-JSON record (the
 //                             shared emitters of ahv/delta_emit.h) written into
 //                             the payload arena, parent digest left as a hole
+//   store_pipe_prefix_kernel  lane per delta: SHA-256 of the record's blocks
+//                             before the parent hole (all of a turn-1 record)
 //   store_pipe_chain_kernel   lane per session: the serial SHA-256 chain (K08):
 //                             each record's parent hole filled with the previous
-//                             digest, then compressed; digests and chain head
+//                             digest, then compressed from the prefix midstate;
+//                             digests and chain head
 //
-// The Merkle roots (K09) of the committed chains then come from the K09 kernel
-// over the resident digests (agent_hypervisor_amd/ops/store_pipeline.py).
+// Lanes take records / sessions in descending-work order (render_order,
+// chain_order) so a wave's lanes finish together.  The Merkle roots (K09) of
+// the committed chains then come from the K09 kernel reading the resident
+// digests in place and writing s_root (agent_hypervisor_amd/models/store_pipeline.py).
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
@@ -363,30 +368,37 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   t.d_off[d] = a.doff[g];
   t.d_len[d] = static_cast<int32_t>(len);
   t.d_hole[d] = hole;
-  if (len > static_cast<uint32_t>(a.dcap[g])) {
-    a.status[i] = SP_RENDER;
-    if (a.mid) a.mid_blocks[g] = 0;
+  if (len > static_cast<uint32_t>(a.dcap[g])) a.status[i] = SP_RENDER;
+}
+
+// K08 split (its own pass, lane per record): the blocks before the parent hole
+// (sort_keys puts agent_did, changes and delta_id first) — or the whole record
+// of turn 1 — do not depend on the chain, so they are compressed here in
+// parallel over records, and the serial chain pass resumes from this state.
+// Kept out of the render pass: the SHA rounds are uniform control flow, the
+// rendering is not (its lanes diverge on string lengths and field kinds).
+AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g) {
+  const Tables& t = a.t;
+  const int32_t d = a.drow[g];
+  const uint32_t len = static_cast<uint32_t>(t.d_len[d]);
+  if (len > static_cast<uint32_t>(a.dcap[g])) {  // overflowed its reservation (SP_RENDER)
+    a.mid_blocks[g] = 0;
     return;
   }
-  if (a.mid) {
-    // K08 split: the blocks before the parent hole (sort_keys puts agent_did,
-    // changes and delta_id first) — or the whole record of turn 1 — do not depend
-    // on the chain, so they are compressed here, one lane per record, and the
-    // serial chain pass resumes from this state.
-    const uint64_t nblk = (static_cast<uint64_t>(len) + 9 + 63) / 64;
-    const uint64_t pb = hole >= 0 ? static_cast<uint64_t>(hole) / 64 : nblk;
-    uint32_t h[8];
-    sha256_init(h);
-    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(t.payload + a.doff[g]);
-    for (uint64_t b = 0; b < pb; ++b) {
-      uint32_t blk[16];
-      sp_block(w32, len, nblk, b, blk);
-      sha256_compress(h, blk);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a.mid[8 * static_cast<int64_t>(g) + k] = h[k];
-    a.mid_blocks[g] = static_cast<int32_t>(pb);
+  const int32_t hole = t.d_hole[d];
+  const uint64_t nblk = (static_cast<uint64_t>(len) + 9 + 63) / 64;
+  const uint64_t pb = hole >= 0 ? static_cast<uint64_t>(hole) / 64 : nblk;
+  uint32_t h[8];
+  sha256_init(h);
+  const uint32_t* w32 = reinterpret_cast<const uint32_t*>(t.payload + a.doff[g]);
+  for (uint64_t b = 0; b < pb; ++b) {
+    uint32_t blk[16];
+    sp_block(w32, len, nblk, b, blk);
+    sha256_compress(h, blk);
   }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a.mid[8 * g + k] = h[k];
+  a.mid_blocks[g] = static_cast<int32_t>(pb);
 }
 
 // Lane per session: the SHA-256 chain over its records (K08).
@@ -436,6 +448,16 @@ AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
 __global__ __launch_bounds__(256) void store_pipe_rows_kernel(StorePipeArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < a.n) sp_rows(a, i);
+}
+
+// lane per record (records in render_order: similar sizes per wave)
+__global__ __launch_bounds__(256) void store_pipe_prefix_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd) {
+  const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (x < nd) {
+    const int64_t g = a.render_order ? a.render_order[x] : x;
+    if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix(a, g);
+    else a.mid_blocks[g] = 0;
+  }
 }
 
 // lane per delta; `dsess` maps a delta to its session
@@ -505,7 +527,7 @@ StorePipeArgs to_args(const Tables& t, const py::dict& d) {
 
 }  // namespace
 
-// Launch the three kernels on `stream` (device) or run the twin (host tables).
+// Launch the kernels (rows, render, prefix, chain) on `stream` (device) or run the twin (host tables).
 void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t stream) {
   const StorePipeArgs a = to_args(t, d);
   const int32_t* dsess = P<const int32_t>(d, "dsess");
@@ -514,6 +536,11 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
     for (int64_t i = 0; i < a.n; ++i) sp_rows(a, i);
     for (int64_t g = 0; g < nd; ++g)
       if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_render(a, dsess[g], static_cast<int32_t>(g));
+    if (a.mid)
+      for (int64_t g = 0; g < nd; ++g) {
+        if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix(a, g);
+        else a.mid_blocks[g] = 0;
+      }
     for (int64_t i = 0; i < a.n; ++i)
       if (a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
     return;
@@ -522,9 +549,13 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
   py::gil_scoped_release nogil;
   if (a.n > 0) {
     hipLaunchKernelGGL(store_pipe_rows_kernel, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, st, a);
-    if (nd > 0)
+    if (nd > 0) {
       hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                          a, dsess, nd);
+      if (a.mid)
+        hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
+                           a, dsess, nd);
+    }
     hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
   }
   check_hip(hipGetLastError(), "store_pipeline");
