@@ -35,6 +35,14 @@ REFERENCE_JOINS = (("did:mesh:a", 0.8),)
 REFERENCE_DELTAS = tuple(("did:mesh:a", ((f"/f{i}", "add", f"h{i}"),)) for i in range(3))
 REFERENCE_STEPS = (("action", "did:mesh:a", "/api/action", None, 0, 0),)
 
+# A/B switches of the batch kernels' work layout (AHV_SP_ORDER bit0 chain lanes by work,
+# bit1 render lanes by record size; AHV_SP_PREFIX=render|kernel: where the records'
+# parent-independent SHA blocks are compressed)
+import os as _os  # noqa: E402
+
+_SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "1"))
+_SP_PREFIX_IN_RENDER = 0 if _os.environ.get("AHV_SP_PREFIX", "render") == "kernel" else 1
+
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
            5: "terminate_refused", 6: "record_overflow"}
 
@@ -462,13 +470,15 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
     capl = caps.astype(np.int64)
     cs = np.concatenate([[0], np.cumsum(np.where(turn1, 0, 4))])
     work = cs[delta_off[1:]] - cs[delta_off[:-1]]
-    tens["chain_order"] = T(np.argsort(-work, kind="stable").astype(np.int32))
-    if nd:
+    if _SP_ORDER & 1:
+        tens["chain_order"] = T(np.argsort(-work, kind="stable").astype(np.int32))
+    if nd and _SP_ORDER & 2:
         tens["render_order"] = T(np.argsort(-(capl + np.where(turn1, capl, np.maximum(capl - 260, 0))),
                                             kind="stable").astype(np.int32))
     tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
     tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
     args = {k: v.data_ptr() for k, v in tens.items()}
+    args.update(prefix_in_render=_SP_PREFIX_IN_RENDER)
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
     committed = [i for i in range(n) if (int(flags[i]) & 9) == 9 and delta_off[i + 1] > delta_off[i]] \
         if not shared else (list(range(n)) if (int(flags[0]) & 9) == 9 and delta_off[1] > 0 else [])

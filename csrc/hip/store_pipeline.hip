@@ -83,6 +83,7 @@ struct StorePipeArgs {
   int32_t* status;              // [n] out: 0 ok, else first refused stage (StorePipeStatus)
   uint32_t* mid;                // [Dn, 8] SHA-256 state after a record's parent-independent blocks, or null
   int32_t* mid_blocks;          // [Dn] blocks `mid` covers (all of them for a turn-1 record: its digest)
+  int32_t prefix_in_render;     // 1: the render lane compresses its record's prefix; 0: store_pipe_prefix_kernel
   const int32_t* chain_order;   // [n] sessions by descending SHA work (chain kernel lane order), or null
   const int32_t* render_order;  // [Dn] deltas by descending record size (render kernel lane order), or null
 };
@@ -314,6 +315,8 @@ AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t 
   }
 }
 
+AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g);
+
 AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   const Tables& t = a.t;
   const int32_t k = g - a.delta_off[i];
@@ -369,9 +372,10 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   t.d_len[d] = static_cast<int32_t>(len);
   t.d_hole[d] = hole;
   if (len > static_cast<uint32_t>(a.dcap[g])) a.status[i] = SP_RENDER;
+  if (a.mid && a.prefix_in_render) sp_prefix(a, g);  // the record is still hot in this lane's cache lines
 }
 
-// K08 split (its own pass, lane per record): the blocks before the parent hole
+// K08 split (lane per record; in the render pass or its own pass): the blocks before the parent hole
 // (sort_keys puts agent_did, changes and delta_id first) — or the whole record
 // of turn 1 — do not depend on the chain, so they are compressed here in
 // parallel over records, and the serial chain pass resumes from this state.
@@ -521,6 +525,7 @@ StorePipeArgs to_args(const Tables& t, const py::dict& d) {
   a.chain_order = d.contains("chain_order") ? P<const int32_t>(d, "chain_order") : nullptr;
   a.mid = d.contains("mid") ? P<uint32_t>(d, "mid") : nullptr;
   a.mid_blocks = d.contains("mid_blocks") ? P<int32_t>(d, "mid_blocks") : nullptr;
+  a.prefix_in_render = d.contains("prefix_in_render") ? d["prefix_in_render"].cast<int32_t>() : 1;
   a.render_order = d.contains("render_order") ? P<const int32_t>(d, "render_order") : nullptr;
   return a;
 }
@@ -536,7 +541,7 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
     for (int64_t i = 0; i < a.n; ++i) sp_rows(a, i);
     for (int64_t g = 0; g < nd; ++g)
       if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_render(a, dsess[g], static_cast<int32_t>(g));
-    if (a.mid)
+    if (a.mid && !a.prefix_in_render)
       for (int64_t g = 0; g < nd; ++g) {
         if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix(a, g);
         else a.mid_blocks[g] = 0;
@@ -552,7 +557,7 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
     if (nd > 0) {
       hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                          a, dsess, nd);
-      if (a.mid)
+      if (a.mid && !a.prefix_in_render)
         hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                            a, dsess, nd);
     }
