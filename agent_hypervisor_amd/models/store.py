@@ -369,6 +369,10 @@ class GovernanceStore:
             self._c.keep(q)
         return q
 
+    def discard(self, seq: int) -> None:
+        """Forget a kept result (``post(..., keep=True)``) that will never be read."""
+        self._c.discard(seq)
+
     def call(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
         return self._c.call(op, args, nres, inline)
 

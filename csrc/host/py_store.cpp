@@ -383,6 +383,12 @@ class Store {
     if (q + static_cast<uint64_t>(nslots_) >= next_) watched_[q] = 1;
   }
 
+  // Drop a kept result that will never be read (its awaiting call was cancelled).
+  void discard(uint64_t q) {
+    watched_.erase(q);
+    saved_.erase(q);
+  }
+
   // Non-blocking form for the asyncio API: the results of `q` if it completed
   // within `spin_ns` (0: just look), else None.  A worker that idled out
   // between the post and now is relaunched.
@@ -651,6 +657,7 @@ class Store {
     d["delta_rows"] = dhw_ - static_cast<int64_t>(dfree_.size());
     d["delta_hw"] = dhw_;
     d["delta_cap"] = t_.cap.D;
+    d["kept"] = static_cast<int64_t>(watched_.size() + saved_.size());  // posted results awaiting their reader
     return d;
   }
 
@@ -704,6 +711,7 @@ void register_store(py::module_& m) {
            py::arg("max_ms") = 2000)
       .def("post", &Store::post, py::arg("op"), py::arg("args"), py::arg("inline") = py::none())
       .def("keep", &Store::keep, py::arg("seq"))
+      .def("discard", &Store::discard, py::arg("seq"))
       .def("call", &Store::call, py::arg("op"), py::arg("args"), py::arg("nres") = 4, py::arg("inline") = py::none())
       .def("result", &Store::result, py::arg("seq"), py::arg("nres") = 4)
       .def("try_result", &Store::try_result, py::arg("seq"), py::arg("nres") = 4, py::arg("spin_ns") = 0)

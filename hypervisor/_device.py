@@ -1174,6 +1174,10 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                 await step.transition_async(StepState.EXECUTING, retry=attempt)
             try:
                 result = await await_with_timeout(executor(), step.timeout_seconds)
+            except asyncio.CancelledError:
+                if seq is not None:  # the posted transition's kept result will never be read
+                    self._store.discard(seq)
+                raise
             except asyncio.TimeoutError:
                 last = SagaTimeoutError(
                     f"Step {step_id} timed out after {step.timeout_seconds}s "

@@ -35,3 +35,31 @@ def test_concurrent_pipelines_cpu_twin():
 def test_concurrent_pipelines_gfx950():
     roots = _gather("cuda", 5000)
     assert len(roots) == 5000 and len(set(roots)) == 5000 and all(len(r) == 64 for r in roots)
+
+
+def test_cancelled_step_discards_its_kept_result():
+    """A cancelled executor leaves no kept result behind in the store."""
+    from hypervisor import Hypervisor, SessionConfig
+
+    async def go():
+        hv = Hypervisor(device="cpu")
+        m = await hv.create_session(SessionConfig(), "did:admin")
+        sid = m.sso.session_id
+        await hv.join_session(sid, "did:a", sigma_raw=0.8)
+        g = m.saga.create_saga(sid)
+        st = m.saga.add_step(g.saga_id, "a", "did:a", "/x")
+        st2 = m.saga.add_step(g.saga_id, "b", "did:a", "/y")
+        await m.saga.execute_step(g.saga_id, st.step_id, executor=lambda: asyncio.sleep(0))  # state known: speculates
+        t = asyncio.ensure_future(m.saga.execute_step(g.saga_id, st2.step_id, executor=lambda: asyncio.sleep(10)))
+        await asyncio.sleep(0.01)
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        return hv._store.info()
+
+    info = _run(go())
+    assert info.get("kept", 0) == 0, info
+
+
+def _run(coro):
+    return asyncio.run(coro)
