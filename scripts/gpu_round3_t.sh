@@ -9,7 +9,7 @@ run() {  # $1 name, $2 counters
   timeout -s KILL 120 rocprofv3 --pmc $2 --kernel-include-regex store_pipe --output-format csv -d $OUT/$1 -o pmc -- python3 bench.py --mix hetero --sessions 262144 --steps 2 --warmup 1 --no-scalar --no-api --no-liability > $OUT/$1.log 2>&1 || return 1
   python3 scripts/pmc_summary.py $(find $OUT/$1 -name "*counter_collection.csv" | head -1) > $OUT/$1.md || return 1
 }
-run issue "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" &&
-run stall "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_WAIT_ANY" &&
-run mem "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" &&
+run issue "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" &&
+run stall "SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_INT" &&
+run mem "TCC_HIT_sum TCC_MISS_sum" &&
 echo done
