@@ -441,21 +441,36 @@ class GovernanceStore:
             loop.call_soon(self._poll, loop)
         return await fut
 
+    POLL_MISSES = 16  # consecutive pending waiters after which a poll pass stops scanning
+
     def _poll(self, loop) -> None:
+        """Deliver completed results to their waiters.  Waiters are in post (= seq)
+        order and the worker completes commands in order (only deferred captures
+        finish after later commands), so a pass stops after ``POLL_MISSES``
+        consecutive pending ones: with thousands of sessions in flight a pass costs
+        O(completed), not O(waiting)."""
         ws = self._waiters
         self._waiters = []
         keep = []
-        for w in ws:
+        misses = 0
+        try_result = self._c.try_result
+        for i, w in enumerate(ws):
             try:
-                r = self._c.try_result(w[0], w[1], 0)
+                r = try_result(w[0], w[1], 0)
             except Exception as e:  # noqa: BLE001 - delivered to the awaiting call
                 if not w[2].done():
                     w[2].set_exception(e)
                 continue
             if r is None:
                 keep.append(w)
-            elif not w[2].done():
-                w[2].set_result(r)
+                misses += 1
+                if misses >= self.POLL_MISSES:
+                    keep.extend(ws[i + 1:])
+                    break
+            else:
+                misses = 0
+                if not w[2].done():
+                    w[2].set_result(r)
         if self._waiters:
             keep.extend(self._waiters)
         self._waiters = keep
