@@ -36,11 +36,11 @@ REFERENCE_DELTAS = tuple(("did:mesh:a", ((f"/f{i}", "add", f"h{i}"),)) for i in 
 REFERENCE_STEPS = (("action", "did:mesh:a", "/api/action", None, 0, 0),)
 
 # A/B switches of the batch kernels' work layout (AHV_SP_ORDER bit0 chain lanes by work,
-# bit1 render lanes by record size; AHV_SP_PREFIX=render|kernel: where the records'
+# bit1 render lanes by record shape with co-located arena space; AHV_SP_PREFIX=render|kernel: where the records'
 # parent-independent SHA blocks are compressed)
 import os as _os  # noqa: E402
 
-_SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "1"))
+_SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "3"))
 _SP_PREFIX_IN_RENDER = 0 if _os.environ.get("AHV_SP_PREFIX", "render") == "kernel" else 1
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
@@ -424,7 +424,27 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         digits = np.char.str_len(turn.astype(str)) if nd_ else np.zeros(0, np.int64)
         caps = ((base_caps + 2 * digits + np.where(turn > 1, 66, 4) + 8 + 63) & ~63).astype(np.int32)
     nd = len(caps)
-    drows, doff = st.reserve_deltas(caps)
+    # Lane orders that balance the waves.  Render: records grouped by shape (turn 1 —
+    # whole record hashed — first, then by change count and size), with their arena
+    # space reserved in that same order so a wave's 64 records stay adjacent in the
+    # arena.  Chain: sessions by descending serial work (later deltas).
+    cnt_d = np.diff(delta_off).astype(np.int64)
+    turn1 = np.zeros(nd, dtype=bool)
+    if nd:
+        turn1[delta_off[:-1][cnt_d > 0]] = True
+    capl = caps.astype(np.int64)
+    render_order = None
+    if nd and _SP_ORDER & 2:
+        nch = np.diff(np.asarray(ch_off_all, dtype=np.int64))
+        render_order = np.lexsort((-capl, -nch, ~turn1)).astype(np.int32)
+        rows_s, offs_s = st.reserve_deltas(caps[render_order])
+        dr = np.empty(nd, dtype=np.int32)
+        do = np.empty(nd, dtype=np.int64)
+        dr[render_order] = np.frombuffer(rows_s, dtype=np.int32)
+        do[render_order] = np.frombuffer(offs_s, dtype=np.int64)
+        drows, doff = dr.tobytes(), do.tobytes()
+    else:
+        drows, doff = st.reserve_deltas(caps)
     dsess = np.repeat(np.arange(n, dtype=np.int32), np.diff(delta_off))
 
     has_saga = np.diff(step_off) > 0
@@ -461,20 +481,13 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
     # blocks of their records), deltas by descending record size (stable sorts)
     # The render pass also compresses each record's parent-independent blocks (all
     # of a turn-1 record); the chain pass hashes the rest, ≈ the 4 blocks from the
-    # parent hole on.  Work estimates: render ∝ record bytes (+ the whole record
-    # again at turn 1, ~the part before the hole otherwise); chain ∝ later deltas.
-    cnt_d = np.diff(delta_off).astype(np.int64)
-    turn1 = np.zeros(nd, dtype=bool)
-    if nd:
-        turn1[delta_off[:-1][cnt_d > 0]] = True
-    capl = caps.astype(np.int64)
+    # parent hole on: chain work ∝ a session's later deltas.
     cs = np.concatenate([[0], np.cumsum(np.where(turn1, 0, 4))])
     work = cs[delta_off[1:]] - cs[delta_off[:-1]]
     if _SP_ORDER & 1:
         tens["chain_order"] = T(np.argsort(-work, kind="stable").astype(np.int32))
-    if nd and _SP_ORDER & 2:
-        tens["render_order"] = T(np.argsort(-(capl + np.where(turn1, capl, np.maximum(capl - 260, 0))),
-                                            kind="stable").astype(np.int32))
+    if render_order is not None:
+        tens["render_order"] = T(render_order)
     tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
     tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
     args = {k: v.data_ptr() for k, v in tens.items()}
