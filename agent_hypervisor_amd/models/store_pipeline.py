@@ -40,7 +40,7 @@ REFERENCE_STEPS = (("action", "did:mesh:a", "/api/action", None, 0, 0),)
 # parent-independent SHA blocks are compressed)
 import os as _os  # noqa: E402
 
-_SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "3"))
+_SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "1"))
 _SP_PREFIX_IN_RENDER = 0 if _os.environ.get("AHV_SP_PREFIX", "render") == "kernel" else 1
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
