@@ -48,12 +48,12 @@ ST_OK, ST_BAD_STATE, ST_NOT_FOUND, ST_BAD_ARG, ST_SCRATCH = 0, 1, 2, 90, 91
 
 _u64 = struct.Struct("<Q")
 _d = struct.Struct("<d")
+_i64_of_d = struct.Struct("<q").unpack
 
 
 def dbits(x: float) -> int:
     """fp64 bit pattern as a signed int64 (store argument encoding)."""
-    v = _u64.unpack(_d.pack(float(x)))[0]
-    return v - (1 << 64) if v >= 1 << 63 else v
+    return _i64_of_d(_d.pack(x))[0]
 
 
 def bitsd(v: int) -> float:

@@ -8,6 +8,7 @@ be handed the same instant as an int64 microsecond count (:func:`now_us`).
 from __future__ import annotations
 
 from datetime import datetime, timezone
+from time import time_ns as _time_ns
 from typing import Callable, Optional
 
 UTC = timezone.utc
@@ -43,4 +44,8 @@ def from_us(us: int) -> datetime:
 
 
 def now_us() -> int:
-    return to_us(now())
+    """``to_us(now())`` — without building a datetime when no clock is pinned
+    (the device store's commands take integer µs; same CLOCK_REALTIME source)."""
+    if _override is None:
+        return _time_ns() // 1000
+    return to_us(_override())

@@ -40,7 +40,7 @@ from agent_hypervisor_amd._native import C as _C
 from agent_hypervisor_amd.models import store as _st
 from agent_hypervisor_amd.models.store import GovernanceStore, bitsd, dbits
 from hypervisor import config as _cfg
-from hypervisor._clock import from_us, now as _now, to_us
+from hypervisor._clock import from_us, now as _now, now_us as _now_us, to_us
 from hypervisor.audit.commitment import CommitmentEngine, CommitmentRecord
 from hypervisor.audit.delta import DeltaEngine, SemanticDelta, VFSChange, _payload_json
 from hypervisor.liability.slashing import SlashingEngine, SlashResult, VoucherClip
@@ -63,6 +63,7 @@ from hypervisor.session.sso import SessionVFS
 
 _STATES = list(SessionState)
 _STEPS = list(StepState)
+_STEP_IDX = {**{x: i for i, x in enumerate(_STEPS)}, **{x.value: i for i, x in enumerate(_STEPS)}}
 _SAGAS = list(SagaState)
 _RINGS = list(ExecutionRing)
 _MODE = {ConsistencyMode.EVENTUAL: 0, ConsistencyMode.STRONG: 1}
@@ -98,6 +99,18 @@ def _lifecycle(state_code: int, *allowed: SessionState) -> SessionLifecycleError
     st = _STATES[state_code] if state_code < len(_STATES) else state_code
     val = st.value if isinstance(st, SessionState) else str(st)
     return SessionLifecycleError(f"Operation not allowed in state {val}. Allowed: {[s.value for s in allowed]}")
+
+
+_STORE_BY_MODE: dict = {}
+
+
+def _shared_store(mode: str) -> GovernanceStore:
+    """The process-wide store of a ``Hypervisor(device=...)`` mode string (cached per
+    string: one dict lookup per Hypervisor instead of a torch.device parse)."""
+    st = _STORE_BY_MODE.get(mode)
+    if st is None or getattr(st, "_closed", False):
+        st = _STORE_BY_MODE[mode] = _st.shared_store(mode)
+    return st
 
 
 def _check(res: tuple, what: str) -> tuple:
@@ -140,7 +153,7 @@ class DeviceSession(SharedSessionObject):
             self._cseq = store.post(
                 _st.OP_SESS_CREATE,
                 [
-                    self.slot, store.agent_id(creator_did), to_us(_now()), _MODE[config.consistency_mode],
+                    self.slot, store.agent_id(creator_did), _now_us(), _MODE[config.consistency_mode],
                     int(config.max_participants), dbits(config.min_sigma_eff), int(bool(config.enable_audit)),
                     _i64(hi), _i64(lo), 0 if handshake else 1,
                 ],
@@ -263,7 +276,7 @@ class DeviceSession(SharedSessionObject):
         if self._cseq >= 0:
             self._created()
         return [self.slot, self._store.agent_id(agent_did), dbits(sigma_raw), dbits(sigma_eff), flags, ring,
-                to_us(_now())]
+                _now_us()]
 
     def _join(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> int:
         r = self._store.call(_st.OP_SESS_JOIN, self._join_args(agent_did, sigma_raw, sigma_eff, flags, ring), 6)
@@ -325,7 +338,7 @@ class DeviceSession(SharedSessionObject):
         self._store.post(_st.OP_SESS_SET_MODE, [self.slot, _MODE[ConsistencyMode(mode)]])
 
     def terminate(self) -> None:
-        r = self._store.call(_st.OP_SESS_TERMINATE, [self.slot, to_us(_now())], 2)
+        r = self._store.call(_st.OP_SESS_TERMINATE, [self.slot, _now_us()], 2)
         if r[0]:
             raise _lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
 
@@ -594,7 +607,7 @@ class DeviceVouchRecord(VouchRecord):
     def is_active(self, v: bool) -> None:
         if not v:
             if self._frozen is None:
-                self._store.call(_st.OP_RELEASE_BOND, [self.edge, to_us(_now())], 1)
+                self._store.call(_st.OP_RELEASE_BOND, [self.edge, _now_us()], 1)
         elif not self.is_active:
             raise ValueError("a released bond cannot be re-activated")
 
@@ -721,7 +734,7 @@ class DeviceVouchingEngine(VouchingEngine):
         v = self._v(session_id)
         r = self._store.call(
             _st.OP_SIGMA_EFF,
-            [v, self._store.agent_id(vouchee_did), dbits(vouchee_sigma), dbits(risk_weight), to_us(_now())], 2,
+            [v, self._store.agent_id(vouchee_did), dbits(vouchee_sigma), dbits(risk_weight), _now_us()], 2,
         )
         return bitsd(r[1])
 
@@ -755,7 +768,7 @@ class DeviceVouchingEngine(VouchingEngine):
         st = self._store
         cap = self.LIST_PAGE or st._c.bulk_cap // 64
         who_id = st.agent_id(who) if who is not None else -1
-        now = to_us(_now())
+        now = _now_us()
         out: list[DeviceVouchRecord] = []
         skip = 0
         while True:
@@ -783,20 +796,20 @@ class DeviceVouchingEngine(VouchingEngine):
         v = self._v(session_id)
         if v < 0:
             return 0
-        r = self._store.call(_st.OP_EXPOSURE, [v, self._store.agent_id(voucher_did), to_us(_now())], 2)
+        r = self._store.call(_st.OP_EXPOSURE, [v, self._store.agent_id(voucher_did), _now_us()], 2)
         return bitsd(r[1])
 
     def release_bond(self, vouch_id: str) -> None:
         rec = self._by_id.get(vouch_id)
         if rec is None:
             raise VouchingError(f"Vouch {vouch_id} not found")
-        self._store.call(_st.OP_RELEASE_BOND, [rec.edge, to_us(_now())], 1)
+        self._store.call(_st.OP_RELEASE_BOND, [rec.edge, _now_us()], 1)
 
     def release_session_bonds(self, session_id: str) -> int:
         v = self._v(session_id)
         if v < 0:
             return 0
-        return self._store.call(_st.OP_RELEASE_SESSION, [v, to_us(_now())], 2)[1]
+        return self._store.call(_st.OP_RELEASE_SESSION, [v, _now_us()], 2)[1]
 
     def _creates_cycle(self, voucher_did: str, vouchee_did: str, session_id: str) -> bool:
         raise NotImplementedError("the cycle check runs inside the device vouch command (K05)")
@@ -826,7 +839,7 @@ class DeviceSlashingEngine(SlashingEngine):
         scores_off = 8 * out_cap
         r = st.call(
             _st.OP_SLASH,
-            [v, st.agent_id(vouchee_did), dbits(vouchee_sigma), dbits(risk_weight), to_us(_now()), len(pairs), off,
+            [v, st.agent_id(vouchee_did), dbits(vouchee_sigma), dbits(risk_weight), _now_us(), len(pairs), off,
              0, out_cap, scores_off, cascade_depth],
             3,
         )
@@ -994,35 +1007,38 @@ class DeviceSagaStep(SagaStep):
         pass
 
     def transition(self, new_state: StepState, retry: int = -1) -> None:
-        to = _STEPS.index(StepState(new_state))
-        r = self._store.call(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], 2)
+        to = _STEP_IDX[new_state] if new_state in _STEP_IDX else _STEPS.index(StepState(new_state))
+        r = self._store.call(_st.OP_STEP_TRANSITION, [self.slot, to, _now_us(), retry], 2)
         self.__dict__["_hint"] = None
         self._transitioned(r, new_state)
-        self.__dict__["_hint"] = StepState(new_state)
+        self.__dict__["_hint"] = _STEPS[_STEP_IDX[new_state]] if new_state in _STEP_IDX else StepState(new_state)
 
     async def transition_async(self, new_state: StepState, retry: int = -1) -> None:
-        to = _STEPS.index(StepState(new_state))
+        to = _STEP_IDX[new_state] if new_state in _STEP_IDX else _STEPS.index(StepState(new_state))
         self.__dict__["_hint"] = None
-        r = await self._store.call_async(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], 2)
+        r = await self._store.call_async(_st.OP_STEP_TRANSITION, [self.slot, to, _now_us(), retry], 2)
         self._transitioned(r, new_state)
-        self.__dict__["_hint"] = StepState(new_state)
+        self.__dict__["_hint"] = _STEPS[_STEP_IDX[new_state]] if new_state in _STEP_IDX else StepState(new_state)
 
     def post_transition(self, new_state: StepState, retry: int = -1) -> int:
         """Post a transition without waiting (its result is read later with
         :meth:`check_posted`); the worker applies commands in order."""
-        to = _STEPS.index(StepState(new_state))
+        to = _STEP_IDX[new_state] if new_state in _STEP_IDX else _STEPS.index(StepState(new_state))
         self.__dict__["_hint"] = None
-        return self._store.post(_st.OP_STEP_TRANSITION, [self.slot, to, to_us(_now()), retry], keep=True)
+        return self._store.post(_st.OP_STEP_TRANSITION, [self.slot, to, _now_us(), retry], keep=True)
 
     async def check_posted(self, seq: int, new_state: StepState) -> None:
         self._transitioned(await self._store.result_async(seq, 2), new_state)
-        self.__dict__["_hint"] = StepState(new_state)
+        self.__dict__["_hint"] = _STEPS[_STEP_IDX[new_state]] if new_state in _STEP_IDX else StepState(new_state)
 
     def can_speculate(self, new_state: StepState) -> bool:
         """True when this process's last known state of the step allows
         ``new_state`` (every transition of a device step goes through this object)."""
         h = self.__dict__.get("_hint")
-        return _SPECULATE and h is not None and StepState(new_state) in STEP_TRANSITIONS.get(h, ())
+        if not _SPECULATE or h is None:
+            return False
+        to = _STEPS[_STEP_IDX[new_state]] if new_state in _STEP_IDX else StepState(new_state)
+        return to in STEP_TRANSITIONS.get(h, ())
 
     @staticmethod
     def _transitioned(r: tuple, new_state) -> None:
@@ -1085,7 +1101,7 @@ class DeviceSaga(Saga):
 
     def transition(self, new_state: SagaState) -> None:
         to = _SAGAS.index(SagaState(new_state))
-        r = self._store.call(_st.OP_SAGA_TRANSITION, [self.slot, to, to_us(_now())], 2)
+        r = self._store.call(_st.OP_SAGA_TRANSITION, [self.slot, to, _now_us()], 2)
         if r[0]:
             frm = _SAGAS[r[1]]
             allowed = SAGA_TRANSITIONS.get(frm, ())
@@ -1143,7 +1159,7 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
     def create_saga(self, session_id: str, saga_id: Optional[str] = None) -> DeviceSaga:
         slot = self._store.alloc("G")
         saga = DeviceSaga(self._store, slot, saga_id or _C.uuid4("saga:"), session_id)
-        self._store.post(_st.OP_SAGA_CREATE, [slot, to_us(_now())])
+        self._store.post(_st.OP_SAGA_CREATE, [slot, _now_us()])
         self._sagas[saga.saga_id] = saga
         return saga
 

@@ -47,6 +47,7 @@ import logging
 from typing import Any, Optional
 
 from hypervisor.audit.commitment import CommitmentEngine
+from hypervisor.config import store_mode as _store_mode
 from hypervisor.audit.delta import DeltaEngine
 from hypervisor.audit.gc import EphemeralGC, RetentionPolicy
 from hypervisor.liability.slashing import SlashingEngine
@@ -57,6 +58,7 @@ from hypervisor.rings.classifier import ActionClassifier
 from hypervisor.rings.enforcer import RingEnforcer
 from hypervisor.saga.orchestrator import SagaOrchestrator
 from hypervisor.session import SharedSessionObject
+from hypervisor.session.table import SessionTable
 from hypervisor.verification.history import TransactionHistoryVerifier
 
 logger = logging.getLogger(__name__)
@@ -101,6 +103,20 @@ class LazyManagedSession(ManagedSession):
         return getattr(self._batch.view(self._index), name)
 
 
+_DEVICE_MOD = None
+
+
+def _device_mod():
+    """``hypervisor._device`` (imported on first use: host-only processes never load
+    torch or the device store)."""
+    global _DEVICE_MOD
+    if _DEVICE_MOD is None:
+        from hypervisor import _device
+
+        _DEVICE_MOD = _device
+    return _DEVICE_MOD
+
+
 class Hypervisor:
     def __init__(
         self,
@@ -114,19 +130,15 @@ class Hypervisor:
         device: Optional[str] = None,
         store: Optional[Any] = None,
     ) -> None:
-        from hypervisor.config import store_mode
-
-        mode = store_mode(device) if store is None else str(store.device)
+        mode = _store_mode(device) if store is None else str(store.device)
         self._store = None
         if mode == "host":
             self.vouching = VouchingEngine(max_exposure=max_exposure)
             self.slashing = SlashingEngine(self.vouching)
             self.commitment = CommitmentEngine()
         else:
-            from agent_hypervisor_amd.models.store import shared_store
-            from hypervisor import _device
-
-            self._store = store if store is not None else shared_store(mode)
+            _device = _device_mod()
+            self._store = store if store is not None else _device._shared_store(mode)
             self._tenant = self._store.new_tenant()
             self.vouching = _device.DeviceVouchingEngine(self._store, self._tenant, max_exposure)
             self.slashing = _device.DeviceSlashingEngine(self.vouching)
@@ -141,8 +153,6 @@ class Hypervisor:
         self.iatp = iatp
         self.event_bus = event_bus
         self.demote_on_slash = demote_on_slash
-        from hypervisor.session.table import SessionTable
-
         self._sessions = SessionTable()
         self._device_engine = None
         self._batch_views: dict = {}  # session id → (batch, host view), a small LRU
@@ -163,8 +173,7 @@ class Hypervisor:
         if session_id is not None and session_id in self._sessions:
             raise ValueError(f"Session {session_id} already exists")
         if self._store is not None:
-            from hypervisor import _device
-
+            _device = _device_mod()
             sso = _device.DeviceSession(self._store, config, creator_did, session_id=session_id)  # HANDSHAKING
             managed = ManagedSession(sso, *_device.session_views(self._store, sso))
         else:
@@ -273,8 +282,7 @@ class Hypervisor:
     async def _terminate_device(self, session_id: str, managed: ManagedSession) -> Optional[str]:
         """One device command: terminate → Merkle root (K09) → commit → release the
         session's bonds (K07) → GC retention count → archive."""
-        from hypervisor import _device as _d  # loaded with the device store (device mode only)
-
+        _d = _device_mod()
         sso, de, st = managed.sso, managed.delta_engine, self._store
         now_us = _d.to_us(_d._now())
         v = st.liability_lookup(self._tenant, session_id)
