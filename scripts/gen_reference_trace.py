@@ -24,8 +24,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_SRC = "/root/reference/src"
-FIXTURE = os.path.join(ROOT, "tests", "fixtures", "reference_trace.json")
-SEED = 2026
+FIXTURES = {  # seed → (fixture, sessions, operations)
+    2026: (os.path.join(ROOT, "tests", "fixtures", "reference_trace.json"), 32, 1200),
+    7: (os.path.join(ROOT, "tests", "fixtures", "reference_trace_s7.json"), 48, 2400),
+}
+FIXTURE, SEED = FIXTURES[2026][0], 2026
 
 _CHILD = r"""
 import asyncio, datetime as _dt, importlib.util, json, sys
@@ -59,7 +62,7 @@ pin()
 def set_now(us):
     cur[0] = us
 seed = int(sys.argv[3])
-ops = gt.make_ops(seed)
+ops = gt.make_ops(seed, int(sys.argv[4]), int(sys.argv[5]))
 out = asyncio.run(gt.run_ops(ops, set_now))
 json.dump({"seed": seed, "ops": ops, "sids": out["sids"], "results": out["results"]}, sys.stdout)
 """
@@ -68,8 +71,10 @@ json.dump({"seed": seed, "ops": ops, "sids": out["sids"], "results": out["result
 def record(seed: int = SEED) -> dict:
     env = {k: v for k, v in os.environ.items() if k not in ("PYTHONPATH",)}
     env.update(PYTHONPATH=REF_SRC, PYTHONDONTWRITEBYTECODE="1")
+    _, sessions, nops = FIXTURES[seed]
     p = subprocess.run([sys.executable, "-c", "import importlib; " + _CHILD, os.path.join(ROOT, "tests", "golden_trace.py"),
-                        REF_SRC, str(seed)], capture_output=True, text=True, env=env, cwd="/tmp", timeout=600)
+                        REF_SRC, str(seed), str(sessions), str(nops)], capture_output=True, text=True, env=env,
+                       cwd="/tmp", timeout=600)
     if p.returncode != 0:
         raise RuntimeError(p.stderr[-4000:])
     return json.loads(p.stdout)
@@ -79,20 +84,23 @@ def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--check", action="store_true")
     args = ap.parse_args()
-    rec = record()
-    if args.check:
-        with open(FIXTURE) as f:
-            old = json.load(f)
-        same = old == json.loads(json.dumps(rec))
-        print("fixture matches the reference" if same else "fixture DIFFERS from the reference")
-        return 0 if same else 1
-    os.makedirs(os.path.dirname(FIXTURE), exist_ok=True)
-    with open(FIXTURE, "w") as f:
-        json.dump(rec, f, separators=(",", ":"))
-        f.write("\n")
-    errs = sum(1 for r in rec["results"] if "error" in r)
-    print(f"wrote {FIXTURE}: {len(rec['ops'])} ops, {errs} reference errors recorded")
-    return 0
+    bad = 0
+    for seed, (fixture, _, _) in FIXTURES.items():
+        rec = record(seed)
+        if args.check:
+            with open(fixture) as f:
+                old = json.load(f)
+            same = old == json.loads(json.dumps(rec))
+            print(f"{os.path.basename(fixture)}: " + ("matches the reference" if same else "DIFFERS from the reference"))
+            bad += 0 if same else 1
+            continue
+        os.makedirs(os.path.dirname(fixture), exist_ok=True)
+        with open(fixture, "w") as f:
+            json.dump(rec, f, separators=(",", ":"))
+            f.write("\n")
+        errs = sum(1 for r in rec["results"] if "msg" in r)
+        print(f"wrote {fixture}: {len(rec['ops'])} ops, {errs} reference errors recorded")
+    return 1 if bad else 0
 
 
 if __name__ == "__main__":

@@ -22,33 +22,36 @@ sys.path.insert(0, HERE)
 
 import golden_trace  # noqa: E402
 
-FIXTURE = os.path.join(HERE, "fixtures", "reference_trace.json")
+FIXTURES = ["reference_trace.json", "reference_trace_s7.json"]  # seeds 2026 (1,297 ops) and 7 (2,545 ops)
 
 
-def _fixture() -> dict:
-    with open(FIXTURE) as f:
+def _fixture(name: str = FIXTURES[0]) -> dict:
+    with open(os.path.join(HERE, "fixtures", name)) as f:
         return json.load(f)
 
 
-def _check(device: str) -> None:
-    fx = _fixture()
+def _check(device: str, name: str) -> None:
+    fx = _fixture(name)
     assert len(fx["ops"]) >= 1000 and len(fx["results"]) == len(fx["ops"])
     bad = golden_trace.replay(fx, device)
     msg = "\n".join(f"#{i} {op}\n  reference: {exp}\n  this repo: {got}" for i, op, exp, got in bad[:8])
     assert not bad, f"{len(bad)} of {len(fx['ops'])} results differ from the reference:\n{msg}"
 
 
-def test_reference_trace_host_engines():
-    _check("host")
+@pytest.mark.parametrize("name", FIXTURES)
+def test_reference_trace_host_engines(name):
+    _check("host", name)
 
 
-def test_reference_trace_cpu_twin_store():
-    _check("cpu")
+@pytest.mark.parametrize("name", FIXTURES)
+def test_reference_trace_cpu_twin_store(name):
+    _check("cpu", name)
 
 
 @pytest.mark.gpu
-def test_reference_trace_gfx950_store():
-    _check("cuda")
+@pytest.mark.parametrize("name", FIXTURES)
+def test_reference_trace_gfx950_store(name):
+    _check("cuda", name)
 
 
 @pytest.mark.slow
