@@ -41,7 +41,8 @@ REFERENCE_STEPS = (("action", "did:mesh:a", "/api/action", None, 0, 0),)
 import os as _os  # noqa: E402
 
 _SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "1"))
-_SP_PREFIX_IN_RENDER = 0 if _os.environ.get("AHV_SP_PREFIX", "render") == "kernel" else 1
+_SP_PREFIX = _os.environ.get("AHV_SP_PREFIX", "render")  # render | kernel | chain (no split: the chain lane hashes all)
+_SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX == "kernel" else 1
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
            5: "terminate_refused", 6: "record_overflow"}
@@ -482,14 +483,15 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
     # The render pass also compresses each record's parent-independent blocks (all
     # of a turn-1 record); the chain pass hashes the rest, ≈ the 4 blocks from the
     # parent hole on: chain work ∝ a session's later deltas.
-    cs = np.concatenate([[0], np.cumsum(np.where(turn1, 0, 4))])
+    cs = np.concatenate([[0], np.cumsum((capl + 9 + 63) // 64 if _SP_PREFIX == "chain" else np.where(turn1, 0, 4))])
     work = cs[delta_off[1:]] - cs[delta_off[:-1]]
     if _SP_ORDER & 1:
         tens["chain_order"] = T(np.argsort(-work, kind="stable").astype(np.int32))
     if render_order is not None:
         tens["render_order"] = T(render_order)
-    tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
-    tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
+    if _SP_PREFIX != "chain":
+        tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
+        tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
     args = {k: v.data_ptr() for k, v in tens.items()}
     args.update(prefix_in_render=_SP_PREFIX_IN_RENDER)
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
