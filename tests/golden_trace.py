@@ -120,10 +120,26 @@ def make_ops(seed: int = 2026, n_sessions: int = 32, n_ops: int = 1200) -> list:
                         rng.random() < 0.3, rng.random() < 0.3])
         elif r < 0.95:
             ops.append(["verify_chain", k])
-        elif r < 0.97:
+        elif r < 0.96:
             ops.append(["root", k])
-        else:
+        elif r < 0.97:
             ops.append(["state", k])
+        else:  # participant / VFS-snapshot / permission / hypervisor-view operations
+            q = rng.random()
+            if q < 0.2:
+                ops.append(["update_ring", k, did, rng.randrange(4)])
+            elif q < 0.35:
+                ops.append(["get_participant", k, did])
+            elif q < 0.5:
+                ops.append(["snapshot", k])
+            elif q < 0.65:
+                ops.append(["restore", k, rng.randrange(4), did])
+            elif q < 0.8:
+                ops.append(["perm", k, rng.choice(files), sorted(rng.sample(DIDS, rng.randrange(1, 3))), did])
+            elif q < 0.9:
+                ops.append(["views"])
+            else:
+                ops.append(["edits", k, did])
     for k in range(n_sessions):
         ops.append(["terminate", k])
         ops.append(["state", k])
@@ -177,6 +193,7 @@ async def run_ops(ops: list, set_now: Callable[[int], None], hv_kwargs: Optional
     sagas: list = []  # (managed session, saga, [steps])
     res: list = []
     calls: dict[tuple, int] = {}
+    snaps: dict[int, list] = {}
 
     def action(spec: list) -> Any:
         aid, rev, ro, admin, undo = spec
@@ -325,6 +342,37 @@ async def run_ops(ops: list, set_now: Callable[[int], None], hv_kwargs: Optional
                        "participants": participants(m),
                        "commit": (lambda c: None if c is None else [c.merkle_root, c.participant_dids, c.delta_count])(
                            hv.commitment.get_commitment(sids[op[1]]))}
+            elif kind == "update_ring":
+                _, k, did, ring = op
+                sessions[k].sso.update_ring(did, ExecutionRing(ring))
+                out = {"participants": participants(sessions[k])}
+            elif kind == "get_participant":
+                p_ = sessions[op[1]].sso.get_participant(op[2])
+                out = {"p": [p_.agent_did, _v(p_.ring), p_.sigma_raw, p_.sigma_eff, p_.is_active]}
+            elif kind == "snapshot":
+                snap = sessions[op[1]].sso.create_vfs_snapshot()
+                snaps.setdefault(op[1], []).append(snap)
+                out = {"snap": snap, "n": sessions[op[1]].sso.vfs.snapshot_count}
+            elif kind == "restore":
+                _, k, j, did = op
+                lst = snaps.get(k, [])
+                sessions[k].sso.restore_vfs_snapshot(lst[j % len(lst)] if lst else "snap:missing", did)
+                vfs = sessions[k].sso.vfs
+                out = {"files": sorted(vfs.list_files()), "contents": [vfs.read(f) for f in sorted(vfs.list_files())]}
+            elif kind == "perm":
+                _, k, path, allowed, did = op
+                e = sessions[k].sso.vfs.set_permissions(path, set(allowed), did)
+                out = {"op": _v(getattr(e, "operation", None)),
+                       "perms": sorted(sessions[k].sso.vfs.get_permissions(path) or [])}
+            elif kind == "views":
+                out = {"active": sorted(sids.index(m.sso.session_id) for m in hv.active_sessions),
+                       "known": [hv.get_session(x) is not None for x in sids]}
+            elif kind == "edits":
+                vfs = sessions[op[1]].sso.vfs
+                log = vfs.edit_log
+                mine = vfs.edits_by_agent(op[2])
+                out = {"n": len(log), "last": [log[-1].operation, log[-1].agent_did] if log else None,
+                       "mine": len(mine), "count": vfs.file_count}
             elif kind == "gc_history":
                 out = {"gc": [[sids.index(h.session_id) if h.session_id in sids else -1, h.retained_deltas,
                                h.purged_vfs_files, h.purged_caches] for h in hv.gc.history]}
