@@ -420,6 +420,9 @@ class GovernanceStore:
 
     # -- asyncio API -------------------------------------------------------------
     SPIN_NS = 150_000  # spin this long for a result when the event loop has nothing else to run
+    # ... and this long when other tasks are ready: a suspension + wake-up costs more
+    # CPU than a short spin when the round trip is a few µs (AHV_STORE_SPIN_BUSY_NS)
+    SPIN_BUSY_NS = _env_int("AHV_STORE_SPIN_BUSY_NS", 0)
 
     async def result_async(self, seq: int, nres: int = 4) -> tuple:
         """The results of ``seq`` without blocking the event loop: when other tasks
@@ -430,7 +433,7 @@ class GovernanceStore:
 
         loop = asyncio.get_running_loop()
         ready = getattr(loop, "_ready", None)
-        spin = 0 if ready else self.SPIN_NS
+        spin = self.SPIN_BUSY_NS if ready else self.SPIN_NS
         r = self._c.try_result(seq, nres, spin)
         if r is not None:
             return r
