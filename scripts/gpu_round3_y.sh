@@ -3,9 +3,9 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp AHV_SKIP_AUTOBUILD=1
-OUT=gpurun_out/r3y
+OUT=gpurun_out/r3y2
 mkdir -p $OUT
-for ns in 0 4000 10000 0 4000 10000; do
+for ns in 10000 20000 40000 80000 20000 40000; do
   AHV_STORE_SPIN_BUSY_NS=$ns timeout -k 10 200 python -u -c "
 import sys, json; sys.path.insert(0, '.'); sys.path.insert(0, 'benchmarks')
 from bench_api import api_throughput
