@@ -422,7 +422,7 @@ class GovernanceStore:
     SPIN_NS = 150_000  # spin this long for a result when the event loop has nothing else to run
     # ... and this long when other tasks are ready: a suspension + wake-up costs more
     # CPU than a short spin when the round trip is a few µs (AHV_STORE_SPIN_BUSY_NS)
-    SPIN_BUSY_NS = _env_int("AHV_STORE_SPIN_BUSY_NS", 0)
+    SPIN_BUSY_NS = _env_int("AHV_STORE_SPIN_BUSY_NS", 15_000)
 
     async def result_async(self, seq: int, nres: int = 4) -> tuple:
         """The results of ``seq`` without blocking the event loop: when other tasks
