@@ -9,7 +9,7 @@
 // device session of the public API (views, reads, verify, terminate all work on
 // it), unlike the standalone engine tables of models/engine.py.
 //
-// Three launches, all over rows the host allocator handed out (free rows; a row
+// Four launches, all over rows the host allocator handed out (free rows; a row
 // that is not free is refused and reported, never overwritten):
 //
 //   store_pipe_rows_kernel    lane per session: create (+ handshake), joins
