@@ -186,13 +186,28 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     // ------------------------------------------------------------ hash engine
     const Lanes L{lane, 64, lds1, kw1};
     uint32_t done = 0;
+    uint64_t ebusy = static_cast<uint64_t>(__hip_atomic_load(tail + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    uint64_t ejobs = static_cast<uint64_t>(__hip_atomic_load(tail + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    uint64_t e_start = 0;
+    uint32_t e_done0 = 0;
     for (;;) {
       const uint32_t head = lds_acquire(&q_head);
+      if (e_start) {  // telemetry: the previous pass's busy ticks and jobs (host-visible)
+        ebusy += __builtin_amdgcn_s_memrealtime() - e_start;
+        ejobs += done - e_done0;
+        e_start = 0;
+        if (lane == 0) {
+          __hip_atomic_store(tail + 3, static_cast<int64_t>(ebusy), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(tail + 4, static_cast<int64_t>(ejobs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
       if (head == done) {
         if (lds_acquire(&stop)) break;
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
+      e_start = __builtin_amdgcn_s_memrealtime();
+      e_done0 = done;
       if ((speculate & 4) && head - done >= 2) {
         // several captures queued: hash the distinct-session prefix one job per lane
         const int nb = batch_size(jobs, done, head - done, batch_sess, lane);
@@ -238,6 +253,9 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   uint32_t queued = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t last = t0;
+  // telemetry accumulates across relaunches (tail[1..4] persist in pinned memory)
+  uint64_t busy = static_cast<uint64_t>(__hip_atomic_load(tail + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  uint64_t ncmd = static_cast<uint64_t>(__hip_atomic_load(tail + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
   for (;;) {
     const uint64_t* slot = ring + (next % static_cast<uint64_t>(nslots)) * kSlotWords;
     const uint64_t w = ld_sys(slot + lane);
@@ -251,6 +269,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     uint64_t x = (lane == 0 || lane == 2) ? 0ull : w;
     for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
     if (x != __shfl(w, 2)) continue;  // torn read of a slot still being written: poll again
+    const uint64_t c_start = __builtin_amdgcn_s_memrealtime();
     Cmd c;
     c.op = static_cast<uint32_t>(__shfl(w, 1));
 #pragma unroll
@@ -305,6 +324,14 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     ++next;
     last = __builtin_amdgcn_s_memrealtime();
+    // utilisation telemetry (host-visible, pinned): busy ticks of the command wave
+    // (decode → result written; waits for the hash engine included) and commands
+    busy += last - c_start;
+    ++ncmd;
+    if (lane == 0) {
+      __hip_atomic_store(tail + 1, static_cast<int64_t>(busy), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(tail + 2, static_cast<int64_t>(ncmd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (rc == EXEC_STOP) break;
   }
   // drain the hash engine, stop it, wait for its goodbye, then release the queue

@@ -153,7 +153,7 @@ class Store {
       hip_check(hipHostMalloc(reinterpret_cast<void**>(&alive_), 64, hipHostMallocCoherent), "store ctl");
       hip_check(hipHostMalloc(reinterpret_cast<void**>(&tail_), 64, hipHostMallocCoherent), "store tail");
       hip_check(hipMemset(ring_, 0, ring_bytes), "memset ring");
-      *tail_ = 0;
+      std::memset(tail_, 0, 64);  // [0] next sequence, [1..4] worker telemetry
       hip_check(hipDeviceSynchronize(), "store init sync");
       hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "store stream");
       idle_ticks_ = static_cast<uint64_t>(idle_us) * 100;   // s_memrealtime: 100 MHz
@@ -658,6 +658,12 @@ class Store {
     d["delta_hw"] = dhw_;
     d["delta_cap"] = t_.cap.D;
     d["kept"] = static_cast<int64_t>(watched_.size() + saved_.size());  // posted results awaiting their reader
+    if (gpu_) {  // worker utilisation telemetry (store_worker.hip; s_memrealtime ticks are 10 ns)
+      d["worker_busy_us"] = static_cast<double>(__atomic_load_n(tail_ + 1, __ATOMIC_RELAXED)) / 100.0;
+      d["worker_commands"] = __atomic_load_n(tail_ + 2, __ATOMIC_RELAXED);
+      d["engine_busy_us"] = static_cast<double>(__atomic_load_n(tail_ + 3, __ATOMIC_RELAXED)) / 100.0;
+      d["engine_jobs"] = __atomic_load_n(tail_ + 4, __ATOMIC_RELAXED);
+    }
     return d;
   }
 

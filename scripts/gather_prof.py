@@ -13,7 +13,21 @@ sys.path.insert(0, "benchmarks")
 from bench_api import api_throughput, reference_pipeline  # noqa: E402
 
 dev = sys.argv[1] if len(sys.argv) > 1 else "cuda"
-print(json.dumps(api_throughput(dev, 10_000, rounds=3)), flush=True)
+import time  # noqa: E402
+
+from agent_hypervisor_amd.models.store import shared_store  # noqa: E402
+
+st = shared_store(dev)
+i0, t0 = st.info(), time.perf_counter()
+res = api_throughput(dev, 10_000, rounds=3)
+i1, wall = st.info(), time.perf_counter() - t0
+if "worker_busy_us" in i1:  # store worker utilisation over the whole measurement (warm-up included)
+    res["worker_busy_frac"] = round((i1["worker_busy_us"] - i0["worker_busy_us"]) / (wall * 1e6), 4)
+    res["engine_busy_frac"] = round((i1["engine_busy_us"] - i0["engine_busy_us"]) / (wall * 1e6), 4)
+    res["commands"] = i1["worker_commands"] - i0["worker_commands"]
+    res["us_per_command_busy"] = round((i1["worker_busy_us"] - i0["worker_busy_us"]) / max(1, res["commands"]), 3)
+    res["wall_s"] = round(wall, 3)
+print(json.dumps(res), flush=True)
 print(json.dumps(api_throughput("host", 10_000, rounds=3)), flush=True)
 
 
