@@ -184,6 +184,7 @@ class GovernanceStore:
         self.grows = {k: 0 for k in ("S", "G", "T", "E", "V", "D", "B")}
         self._waiters: list = []  # (seq, nres, future) of suspended asyncio calls
         self._polling = False
+        self._deferred: list = []  # (seq, nres, check) of speculative posts not verified yet
         self.seed = int.from_bytes(os.urandom(8), "little") >> 1
 
     # -- allocation ----------------------------------------------------------
@@ -369,11 +370,54 @@ class GovernanceStore:
             self._c.keep(q)
         return q
 
+    # -- speculation: commands whose outcome the host already knows -------------
+    DEFERRED_MAX = 512  # unverified speculative posts before a blocking verification
+
+    def post_checked(self, op: int, args: list, nres: int, check, inline: Optional[bytes] = None) -> int:
+        """Post a command whose result the caller has predicted (from the same
+        semantics.h predicates over state only it mutates) without waiting for it;
+        ``check(result)`` returns None when the device agreed, else the exception to
+        raise.  Results are verified by :meth:`verify_deferred` — before every later
+        store call and whenever the list grows long — so a disagreement (an internal
+        invariant violation) surfaces at the next interaction with the store."""
+        q = self._c.post(op, args, inline)
+        self._c.keep(q)
+        self.defer(q, nres, check)
+        return q
+
+    def defer(self, seq: int, nres: int, check) -> None:
+        """Verify a kept post (``post(..., keep=True)``) later instead of awaiting it."""
+        self._deferred.append((seq, nres, check))
+        if len(self._deferred) >= self.DEFERRED_MAX:
+            self.verify_deferred(block=True)
+
+    def verify_deferred(self, block: bool = False) -> None:
+        """Check speculatively posted commands whose results are in (all of them with
+        ``block``); raises the first disagreement."""
+        ds = self._deferred
+        if not ds:
+            return
+        self._deferred = []
+        pending, err = [], None
+        for i, (q, nres, check) in enumerate(ds):
+            r = self._c.try_result(q, nres, 1_000_000_000 if block else 0)
+            if r is None:
+                pending.append((q, nres, check))
+                continue
+            e = check(r)
+            if e is not None and err is None:
+                err = e
+        self._deferred = pending + self._deferred
+        if err is not None:
+            raise err
+
     def discard(self, seq: int) -> None:
         """Forget a kept result (``post(..., keep=True)``) that will never be read."""
         self._c.discard(seq)
 
     def call(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
+        if self._deferred:
+            self.verify_deferred()
         return self._c.call(op, args, nres, inline)
 
     def result(self, seq: int, nres: int = 4) -> tuple:
@@ -483,6 +527,8 @@ class GovernanceStore:
             self._polling = False
 
     async def call_async(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
+        if self._deferred:
+            self.verify_deferred()
         return await self.result_async(self._c.post(op, args, inline), nres)
 
     def drain(self) -> None:

@@ -390,6 +390,20 @@ void register_runtime(py::module_& m) {
   m.def("pack_attribution", &pack_attribution, py::arg("cases"),
         "K21 columns + per-case agent lists (set order) of CausalAttributor.attribute_batch cases");
   m.def("round_many", &round_many, py::arg("xs"), py::arg("ndigits"), "[round(x, ndigits) for x in xs]");
+  // The store's join decision (OP_SESS_JOIN: K01 ring gate + join_check) from the
+  // same semantics.h predicates, for hosts that know the session row's state.
+  m.def(
+      "join_predict",
+      [](int state, bool duplicate, int active, int max_participants, double sigma_eff, double min_sigma,
+         bool trustworthy) {
+        uint8_t ring = ring_from_sigma(sigma_eff, false);
+        if (!trustworthy) ring = RING3;
+        const uint8_t code = join_check(static_cast<uint8_t>(state), duplicate, active, max_participants, sigma_eff,
+                                        min_sigma, ring);
+        return py::make_tuple(static_cast<int>(code), static_cast<int>(ring));
+      },
+      py::arg("state"), py::arg("duplicate"), py::arg("active"), py::arg("max_participants"), py::arg("sigma_eff"),
+      py::arg("min_sigma"), py::arg("trustworthy"), "(JoinCode, ring) the device join would produce");
   m.def("pack_specs", &pack_specs, py::arg("specs"), py::arg("agents"), py::arg("pool"), py::arg("cfg_of"),
         py::arg("fixed"), "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py)");
   m.def("iso_from_us", &iso_from_us, "datetime.isoformat() text of an epoch-µs UTC instant");

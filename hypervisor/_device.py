@@ -62,6 +62,11 @@ from hypervisor.session.snapshot import SessionSnapshot
 from hypervisor.session.sso import SessionVFS
 
 _STATES = list(SessionState)
+_S_CREATED, _S_HANDSHAKING, _S_ACTIVE = (_STATES.index(x) for x in (SessionState.CREATED, SessionState.HANDSHAKING,
+                                                                   SessionState.ACTIVE))
+# A/B switch: joins / activations / step transitions whose outcome the host already knows
+# are posted without waiting for the device (verified later; GovernanceStore.post_checked)
+_SPEC_LIFECYCLE = os.environ.get("AHV_SPEC_LIFECYCLE", "1") != "0"
 _STEPS = list(StepState)
 _STEP_IDX = {**{x: i for i, x in enumerate(_STEPS)}, **{x.value: i for i, x in enumerate(_STEPS)}}
 _SAGAS = list(SagaState)
@@ -144,6 +149,17 @@ class DeviceSession(SharedSessionObject):
         self._vfs_snapshots: dict[str, Any] = {}
         self.slot = store.alloc("S") if slot is None else slot
         self._cseq = -1
+        # Host mirror of the row's admission state (state code, agent id → active for every
+        # participant row), valid while every change to the row goes through this object:
+        # then join / activate outcomes are known before the device confirms them and are
+        # posted without waiting (verified later, GovernanceStore.post_checked).  None: unknown.
+        self._m_state: Optional[int] = None
+        self._m_rows: Optional[dict] = None
+        self._m_active = 0
+        if create and _SPEC_LIFECYCLE:
+            self._m_state = _S_HANDSHAKING if handshake else _S_CREATED
+            self._m_rows = {}
+            self._m_cfg = (int(config.max_participants), float(config.min_sigma_eff))  # what the row holds
         if create:
             u = self.session_id.rsplit(":", 1)[-1].replace("-", "")
             try:
@@ -253,16 +269,37 @@ class DeviceSession(SharedSessionObject):
         r = self._store.call(_st.OP_SESS_HANDSHAKE, [self.slot], 2)
         if r[0]:
             raise _lifecycle(r[1], SessionState.CREATED)
+        if self._m_state is not None:
+            self._m_state = _S_HANDSHAKING
+
+    def _activate_known_ok(self) -> bool:
+        return self._m_state == _S_HANDSHAKING and bool(self._m_rows)
+
+    def _activate_speculated(self) -> None:
+        """The row is HANDSHAKING with ≥ 1 participant row: the device will accept."""
+        slot = self.slot
+        self._store.post_checked(_st.OP_SESS_ACTIVATE, [slot], 2,
+                                 lambda r: None if r[0] == 0 else _st.StoreError(
+                                     f"speculated activate of row {slot} refused by the device (status {r[0]})"))
+        self._m_state = _S_ACTIVE
 
     def activate(self) -> None:
         if self._cseq >= 0:
             self._created()
+        if self._activate_known_ok():
+            return self._activate_speculated()
         self._activated(self._store.call(_st.OP_SESS_ACTIVATE, [self.slot], 2))
+        if self._m_state is not None:
+            self._m_state = _S_ACTIVE
 
     async def activate_async(self) -> None:
         if self._cseq >= 0:
             self._created()
+        if self._activate_known_ok():
+            return self._activate_speculated()
         self._activated(await self._store.call_async(_st.OP_SESS_ACTIVATE, [self.slot], 2))
+        if self._m_state is not None:
+            self._m_state = _S_ACTIVE
 
     @staticmethod
     def _activated(r: tuple) -> None:
@@ -279,15 +316,50 @@ class DeviceSession(SharedSessionObject):
                 _now_us()]
 
     def _join(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> int:
-        r = self._store.call(_st.OP_SESS_JOIN, self._join_args(agent_did, sigma_raw, sigma_eff, flags, ring), 6)
-        return self._joined(r, agent_did, sigma_eff)
+        args = self._join_args(agent_did, sigma_raw, sigma_eff, flags, ring)
+        if not flags & 2:
+            got = self._join_speculated(args, sigma_eff, bool(flags & 1))
+            if got is not None:
+                return got
+        r = self._store.call(_st.OP_SESS_JOIN, args, 6)
+        return self._mirror_join(args[1], self._joined(r, agent_did, sigma_eff))
+
+    def _join_speculated(self, args: list, sigma_eff: float, trustworthy: bool) -> Optional[int]:
+        """The ring of a join the device will certainly admit (posted without waiting),
+        or None: the outcome is not known here (refusals always take the awaited path,
+        so the device's own error reaches the caller)."""
+        rows = self._m_rows
+        if self._m_state is None or rows is None or len(rows) >= self._store.caps["P"]:
+            return None
+        aid = args[1]
+        maxpart, minsig = self._m_cfg
+        code, ring = _C.join_predict(self._m_state, aid in rows, self._m_active, maxpart, float(sigma_eff), minsig,
+                                     trustworthy)
+        if code:
+            return None
+        slot = self.slot
+        self._store.post_checked(_st.OP_SESS_JOIN, args, 6,
+                                 lambda r: None if r[0] == 0 and r[1] == ring else _st.StoreError(
+                                     f"speculated join to row {slot} diverged from the device (status {r[0]})"))
+        rows[aid] = True
+        self._m_active += 1
+        return ring
+
+    def _mirror_join(self, aid: int, ring: int) -> int:
+        if self._m_rows is not None:
+            self._m_rows[aid] = True
+            self._m_active += 1
+        return ring
 
     async def join_gated_async(self, agent_did: str, sigma_raw: float, sigma_eff: float,
                                trustworthy: bool) -> ExecutionRing:
         """:meth:`join_gated` without blocking the event loop on the device round trip."""
         args = self._join_args(agent_did, sigma_raw, sigma_eff, 1 if trustworthy else 0, 0)
+        got = self._join_speculated(args, sigma_eff, trustworthy)
+        if got is not None:
+            return _RINGS[got]
         r = await self._store.call_async(_st.OP_SESS_JOIN, args, 6)
-        return _RINGS[self._joined(r, agent_did, sigma_eff)]
+        return _RINGS[self._mirror_join(args[1], self._joined(r, agent_did, sigma_eff))]
 
     def _joined(self, r: tuple, agent_did: str, sigma_eff: float) -> int:
         code = r[0]
@@ -313,9 +385,14 @@ class DeviceSession(SharedSessionObject):
         return _RINGS[self._join(agent_did, sigma_raw, sigma_eff, 1 if trustworthy else 0, 0)]
 
     def leave(self, agent_did: str) -> None:
-        r = self._store.call(_st.OP_SESS_LEAVE, [self.slot, self._store.agent_id(agent_did)], 1)
+        aid = self._store.agent_id(agent_did)
+        r = self._store.call(_st.OP_SESS_LEAVE, [self.slot, aid], 1)
         if r[0]:
             raise SessionParticipantError(f"Agent {agent_did} not in session")
+        rows = self._m_rows
+        if rows is not None and rows.get(aid):
+            rows[aid] = False
+            self._m_active -= 1
 
     def get_participant(self, agent_did: str) -> SessionParticipant:
         p = self._participants.get(agent_did)
@@ -337,12 +414,19 @@ class DeviceSession(SharedSessionObject):
     def force_consistency_mode(self, mode: ConsistencyMode) -> None:
         self._store.post(_st.OP_SESS_SET_MODE, [self.slot, _MODE[ConsistencyMode(mode)]])
 
+    def _m_forget(self) -> None:
+        """The row leaves the states joins/activation can change: stop mirroring it."""
+        self._m_state = None
+        self._m_rows = None
+
     def terminate(self) -> None:
+        self._m_forget()
         r = self._store.call(_st.OP_SESS_TERMINATE, [self.slot, _now_us()], 2)
         if r[0]:
             raise _lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
 
     def archive(self) -> None:
+        self._m_forget()
         r = self._store.call(_st.OP_SESS_ARCHIVE, [self.slot], 2)
         if r[0]:
             raise _lifecycle(r[1], SessionState.TERMINATING)
@@ -954,6 +1038,16 @@ class DeviceCommitmentEngine(CommitmentEngine):
 _SPECULATE = os.environ.get("AHV_STEP_SPECULATE", "1") != "0"  # A/B switch for the posted EXECUTING transition
 
 
+def _transition_check(slot: int, state: StepState):
+    def check(r: tuple):
+        if r[0] == 0:
+            return None
+        return _st.StoreError(f"speculated {state.value} transition of step row {slot} refused by the device "
+                              f"(from state {_STEPS[r[1]].value if r[1] < len(_STEPS) else r[1]})")
+
+    return check
+
+
 class DeviceSagaStep(SagaStep):
     """Step view: FSM state, timestamps and retry counter live in the device step table."""
 
@@ -1203,6 +1297,16 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                 last = e
             else:
                 step.execute_result = result
+                if seq is not None and _SPEC_LIFECYCLE:
+                    # EXECUTING was known-valid when posted, and COMMITTED is allowed from
+                    # EXECUTING: neither needs the device's answer before returning —
+                    # both are verified with the store's next interaction
+                    st = self._store
+                    st.defer(seq, 2, _transition_check(step.slot, StepState.EXECUTING))
+                    cseq = step.post_transition(StepState.COMMITTED)
+                    st.defer(cseq, 2, _transition_check(step.slot, StepState.COMMITTED))
+                    step.__dict__["_hint"] = StepState.COMMITTED
+                    return result
                 if seq is not None:
                     await step.check_posted(seq, StepState.EXECUTING)
                 await step.transition_async(StepState.COMMITTED)

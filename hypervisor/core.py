@@ -284,7 +284,8 @@ class Hypervisor:
         session's bonds (K07) → GC retention count → archive."""
         _d = _device_mod()
         sso, de, st = managed.sso, managed.delta_engine, self._store
-        now_us = _d.to_us(_d._now())
+        sso._m_forget()  # the row leaves the mirrored states (terminate → archive)
+        now_us = _d._now_us()
         v = st.liability_lookup(self._tenant, session_id)
         cutoff = now_us - int(self.gc.policy.delta_retention_days * 86_400_000_000)
         n, off, inl = st.index_args(de._indices())

@@ -55,6 +55,7 @@ def test_cancelled_step_discards_its_kept_result():
         t.cancel()
         with pytest.raises(asyncio.CancelledError):
             await t
+        hv._store.verify_deferred(block=True)  # speculated posts verified: only leaks would remain kept
         return hv._store.info()
 
     info = _run(go())
