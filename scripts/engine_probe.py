@@ -29,7 +29,8 @@ async def main(n: int) -> dict:
         for k, d in enumerate(ds):
             r = hv._store.result(d._seq, 13)
             if r is not None:
-                rows[k].append((r[10], r[11], r[12] & 0xFFFFFFFF, r[12] >> 32))
+                # result tuple k = result word k+1: words 10/11 stage/hash ticks, 12 blocks | batch << 32
+                rows[k].append((r[9], r[10], r[11] & 0xFFFFFFFF, r[11] >> 32))
     out = {}
     for k, v in rows.items():
         if v:
