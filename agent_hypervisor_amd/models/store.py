@@ -398,12 +398,18 @@ class GovernanceStore:
         if not ds:
             return
         self._deferred = []
-        pending, err = [], None
+        pending, err, misses = [], None, 0
+        try_result = self._c.try_result
         for i, (q, nres, check) in enumerate(ds):
-            r = self._c.try_result(q, nres, 1_000_000_000 if block else 0)
+            r = try_result(q, nres, 1_000_000_000 if block else 0)
             if r is None:
                 pending.append((q, nres, check))
+                misses += 1
+                if misses >= self.POLL_MISSES:  # results complete in post order: the rest are pending too
+                    pending.extend(ds[i + 1:])
+                    break
                 continue
+            misses = 0
             e = check(r)
             if e is not None and err is None:
                 err = e
