@@ -42,4 +42,5 @@ async def main(n: int) -> dict:
     return out
 
 
-print(json.dumps(asyncio.run(main(int(sys.argv[1]) if len(sys.argv) > 1 else 500))), flush=True)
+if __name__ == "__main__":
+    print(json.dumps(asyncio.run(main(int(sys.argv[1]) if len(sys.argv) > 1 else 500))), flush=True)
