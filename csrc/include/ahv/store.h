@@ -101,6 +101,8 @@ enum VouchCode : uint64_t { V_OK = 0, V_SELF = 1, V_LOW_SIGMA = 2, V_CYCLE = 3, 
 
 // Join codes extend semantics.h JoinCode.
 constexpr uint64_t JOIN_ROWS = 5;  // participant row table exhausted
+constexpr uint64_t JOIN_NOT_MINE = 6;  // the row holds another session (creation stamp differs)
+constexpr uint64_t ACT_NOT_MINE = 4;   // activate: the row holds another session
 
 // Row lifecycle.  A row is FREE until a create command claims it and FREE again
 // after the host allocator reclaims it (OP_FREE_ROWS); creates refuse a row that
@@ -746,7 +748,14 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       return;
     }
     case OP_SESS_JOIN: {
-      // a1 agent, a2 σ_raw, a3 σ_eff, a4 flags (bit0 trustworthy, bit1 explicit ring), a5 ring, a6 now
+      // a1 agent, a2 σ_raw, a3 σ_eff, a4 flags (bit0 trustworthy, bit1 explicit ring), a5 ring, a6 now,
+      // a7 creation stamp the host sent with its create (0: unchecked) — a host that posts
+      // before it has seen its create's result: a row holding another session (the create
+      // was refused) refuses the join instead of being changed (JOIN_NOT_MINE)
+      if (c.a[7] && t.s_created[s] != static_cast<int64_t>(c.a[7])) {
+        out64(r + 1, JOIN_NOT_MINE);
+        return;
+      }
       const int32_t agent = static_cast<int32_t>(c.a[1]);
       const double sraw = bitsd(c.a[2]);
       const double seff = bitsd(c.a[3]);
@@ -812,6 +821,10 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       out64(r + 1, ST_OK);
       return;
     case OP_SESS_ACTIVATE: {
+      if (c.a[1] && t.s_created[s] != static_cast<int64_t>(c.a[1])) {  // a1: creation stamp (see OP_SESS_JOIN)
+        out64(r + 1, ACT_NOT_MINE);
+        return;
+      }
       const uint8_t st = t.s_state[s];
       out64(r + 2, st);
       if (st != SS_HANDSHAKING) {

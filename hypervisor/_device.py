@@ -160,20 +160,28 @@ class DeviceSession(SharedSessionObject):
             self._m_state = _S_HANDSHAKING if handshake else _S_CREATED
             self._m_rows = {}
             self._m_cfg = (int(config.max_participants), float(config.min_sigma_eff))  # what the row holds
+        self._stamp = 0  # creation stamp this object sent (0: not created here)
         if create:
             u = self.session_id.rsplit(":", 1)[-1].replace("-", "")
             try:
                 hi, lo = int(u[:16], 16), int(u[16:32], 16)
             except ValueError:
                 hi = lo = 0
-            self._cseq = store.post(
-                _st.OP_SESS_CREATE,
-                [
-                    self.slot, store.agent_id(creator_did), _now_us(), _MODE[config.consistency_mode],
-                    int(config.max_participants), dbits(config.min_sigma_eff), int(bool(config.enable_audit)),
-                    _i64(hi), _i64(lo), 0 if handshake else 1,
-                ],
-            )
+            stamp = _now_us()
+            args = [
+                self.slot, store.agent_id(creator_did), stamp, _MODE[config.consistency_mode],
+                int(config.max_participants), dbits(config.min_sigma_eff), int(bool(config.enable_audit)),
+                _i64(hi), _i64(lo), 0 if handshake else 1,
+            ]
+            if self._m_state is not None and stamp:
+                # posted and verified later: the join / activate that follow carry the stamp,
+                # so a row holding another session (a refused create) refuses them on the device
+                self._stamp = stamp
+                slot = self.slot
+                store.post_checked(_st.OP_SESS_CREATE, args, 2, lambda r: None if r[0] == 0 else _st.StoreError(
+                    f"device refused to create session in row {slot} (row state {r[1]}): allocator invariant violated"))
+            else:
+                self._cseq = store.post(_st.OP_SESS_CREATE, args)
 
     def __del__(self) -> None:
         # the row stays allocated while this view (or a delta engine / saga built
@@ -278,7 +286,7 @@ class DeviceSession(SharedSessionObject):
     def _activate_speculated(self) -> None:
         """The row is HANDSHAKING with ≥ 1 participant row: the device will accept."""
         slot = self.slot
-        self._store.post_checked(_st.OP_SESS_ACTIVATE, [slot], 2,
+        self._store.post_checked(_st.OP_SESS_ACTIVATE, [slot, self._stamp], 2,
                                  lambda r: None if r[0] == 0 else _st.StoreError(
                                      f"speculated activate of row {slot} refused by the device (status {r[0]})"))
         self._m_state = _S_ACTIVE
@@ -288,7 +296,7 @@ class DeviceSession(SharedSessionObject):
             self._created()
         if self._activate_known_ok():
             return self._activate_speculated()
-        self._activated(self._store.call(_st.OP_SESS_ACTIVATE, [self.slot], 2))
+        self._activated(self._store.call(_st.OP_SESS_ACTIVATE, [self.slot, self._stamp], 2))
         if self._m_state is not None:
             self._m_state = _S_ACTIVE
 
@@ -297,7 +305,7 @@ class DeviceSession(SharedSessionObject):
             self._created()
         if self._activate_known_ok():
             return self._activate_speculated()
-        self._activated(await self._store.call_async(_st.OP_SESS_ACTIVATE, [self.slot], 2))
+        self._activated(await self._store.call_async(_st.OP_SESS_ACTIVATE, [self.slot, self._stamp], 2))
         if self._m_state is not None:
             self._m_state = _S_ACTIVE
 
@@ -307,13 +315,15 @@ class DeviceSession(SharedSessionObject):
             raise _lifecycle(r[1], SessionState.HANDSHAKING)
         if r[0] == 3:
             raise SessionLifecycleError("Cannot activate session with no participants")
+        if r[0] == 4:
+            raise _st.StoreError("activate: the row holds another session (its create was refused)")
         _check(r, "activate")
 
     def _join_args(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> list:
         if self._cseq >= 0:
             self._created()
         return [self.slot, self._store.agent_id(agent_did), dbits(sigma_raw), dbits(sigma_eff), flags, ring,
-                _now_us()]
+                _now_us(), self._stamp]
 
     def _join(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> int:
         args = self._join_args(agent_did, sigma_raw, sigma_eff, flags, ring)
@@ -373,6 +383,8 @@ class DeviceSession(SharedSessionObject):
             raise SessionParticipantError(f"Session at capacity ({self.config.max_participants})")
         if code == 4:
             raise SessionParticipantError(f"σ_eff {sigma_eff:.2f} below minimum {bitsd(r[5]):.2f}")
+        if code == 6:
+            raise _st.StoreError("join: the row holds another session (its create was refused)")
         raise _st.StoreError(f"join failed with status {code}")
 
     def join(self, agent_did: str, sigma_raw: float = 0.0, sigma_eff: float = 0.0,

@@ -82,3 +82,27 @@ def test_speculation_off_gives_the_same_results(monkeypatch):
     monkeypatch.setattr(_device, "_SPEC_LIFECYCLE", False)
     off = _run(pipeline())
     assert on == off
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+def test_refused_create_never_lets_a_speculated_join_touch_the_live_row(dev):
+    """An allocator bug that hands out a live row: the create is refused, and the join
+    posted before its result carries the creation stamp, so the device refuses it too —
+    the live session's participants are untouched; the divergence surfaces as StoreError."""
+    from hypervisor import _device
+
+    async def go():
+        hv = Hypervisor(device=dev)
+        st = hv._store
+        a = await hv.create_session(SessionConfig(), "did:admin")
+        await hv.join_session(a.sso.session_id, "did:a", sigma_raw=0.8)
+        st.verify_deferred(block=True)
+        b = _device.DeviceSession(st, SessionConfig(), "did:admin", session_id="session:intruder", slot=a.sso.slot)
+        b._join_speculated(b._join_args("did:x", 0.9, 0.9, 1, 0), 0.9, True)  # predicted admissible
+        with pytest.raises(StoreError):
+            st.verify_deferred(block=True)
+        st.verify_deferred(block=True)  # the remaining checks drained
+        b._store = None  # b never owned the row: its finaliser must not release it
+        return [p.agent_did for p in a.sso.participants]
+
+    assert _run(go()) == ["did:a"]
