@@ -296,11 +296,12 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     if (rc == EXEC_DEFERRED) {
       // A capture with a parent: while the hash engine works through the queue,
       // compress the record's blocks that precede the parent hole here — unless
-      // the next command is already waiting (then wave 1 does all of it).
+      // the next command is already waiting and feature bit 8 is off (then wave 1
+      // does all of it).
       const int64_t jhole = bcast(L, job.hole);
       if ((speculate & 2) && jhole >= 64 && lds_acquire(&q_done) != queued) {
         const uint64_t* nslot = ring + ((next + 1) % static_cast<uint64_t>(nslots)) * kSlotWords;
-        if (__shfl(ld_sys(nslot + lane), 0) != next + 2) {
+        if ((speculate & 8) || __shfl(ld_sys(nslot + lane), 0) != next + 2) {
           HashJob jb;
           jb.off = bcast(L, job.off);
           jb.hole = jhole;
