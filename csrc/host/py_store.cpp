@@ -163,12 +163,13 @@ class Store {
       const char* pf = std::getenv("AHV_STORE_PREFIX");
       // 4 = batched hashing: queued captures of distinct sessions hashed one per lane
       const char* bt = std::getenv("AHV_STORE_BATCH");
-      // 8 = compute the capture prefix even when the next command is already waiting (the
-      //     commands that follow a capture are mostly posted without a waiter: delaying
-      //     them costs nothing, while the hash engine's chain is the latency path)
+      // 8 = compute the capture prefix even when the next command is already waiting (off by
+      //     default: it shortens the engine's later captures but the command wave's SHA work
+      //     slows the engine's current one — both waves issue on one CU; p50 measured equal or
+      //     slightly worse, profiles/r3/prefix_always_ab_r3aj.*)
       const char* pw = std::getenv("AHV_STORE_PREFIX_ALWAYS");
       speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
-                   ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) | ((pw == nullptr || std::atoi(pw) != 0) ? 8 : 0);
+                   ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) | ((pw != nullptr && std::atoi(pw) != 0) ? 8 : 0);
       max_ticks_ = static_cast<uint64_t>(max_ms) * 100000;
     } else {
       ring_ = static_cast<uint64_t*>(std::calloc(ring_bytes / 8, 8));
