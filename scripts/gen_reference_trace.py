@@ -4,7 +4,8 @@
 Runs ``tests/golden_trace.py``'s operation script under the REFERENCE package
 (``/root/reference/src``, read-only; imported in a child interpreter whose
 ``sys.path`` does not contain this repository) with its ``datetime.now`` pinned to
-the trace clock and ``uuid.uuid4`` seeded (so a re-recording is identical), and writes ``tests/fixtures/reference_trace.json``:
+the trace clock and ``uuid.uuid4`` seeded (so a re-recording is identical), and writes one
+fixture per seed (``tests/fixtures/reference_trace.json``, ``reference_trace_s7.json``):
 ``{"seed", "ops", "sids", "results"}``.
 
     python scripts/gen_reference_trace.py [--check]

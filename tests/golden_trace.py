@@ -2,12 +2,13 @@
 
 The reference package (``/root/reference/src/hypervisor``) is not present on the GPU
 box, so its 326 tests can only be run here against the CPU twin store.  This module
-closes that gap: a seeded script of ~1,000 public-API operations (session lifecycle,
-joins with boundary σ values and action manifests, VFS writes, audit captures and
+closes that gap: seeded scripts of 1,300–2,500 public-API operations (session lifecycle,
+joins with boundary σ values and action manifests, VFS writes / snapshots / permissions,
+participant ring updates, audit captures and
 Merkle roots, sagas with failing/retrying executors and compensation, vouch / σ_eff /
 exposure / slash with cascades and bond expiry, ring checks, GC) is executed once by
 the REFERENCE implementation on the CPU and every observable result is recorded in
-``tests/fixtures/reference_trace.json`` (``scripts/gen_reference_trace.py``).  The
+``tests/fixtures/reference_trace*.json`` (``scripts/gen_reference_trace.py``).  The
 replay (:func:`replay`) runs the same operations through THIS package with any store
 (``host`` engines, the ``cpu`` twin, or ``cuda`` — the gfx950 store worker) and the
 results must match the reference's record exactly: states, rings, error types and
