@@ -115,18 +115,20 @@ class StoreError(RuntimeError):
 
 
 class _Rows:
-    """Host allocator of one table: LIFO free list of reclaimed rows + high-water mark."""
+    """Host allocator of one table: LIFO free list of reclaimed rows (single rows as
+    ints, bulk-reclaimed rows as int32 array chunks) + high-water mark."""
 
-    __slots__ = ("cap", "hw", "free")
+    __slots__ = ("cap", "hw", "free", "free_arr")
 
     def __init__(self, cap: int) -> None:
         self.cap = cap
         self.hw = 0
         self.free: list[int] = []
+        self.free_arr: list[np.ndarray] = []
 
     @property
     def live(self) -> int:
-        return self.hw - len(self.free)
+        return self.hw - len(self.free) - sum(len(a) for a in self.free_arr)
 
 
 class GovernanceStore:
@@ -179,6 +181,7 @@ class GovernanceStore:
         self.pool = Interner()  # strings the batched pipeline renders (DIDs, change fields)
         self._rows = {k: _Rows(c[k]) for k in ("S", "G", "T", "E", "V")}
         self._pending: dict[str, list] = {k: [] for k in ("S", "G", "T", "E", "V", "D")}
+        self._pending_arr: dict[str, list] = {k: [] for k in ("S", "G", "T", "E", "V", "D")}  # int32 chunks
         self._tenant_v: dict[int, dict[str, int]] = {}  # tenant → liability session id → V row
         self._tenants = 0
         self.grows = {k: 0 for k in ("S", "G", "T", "E", "V", "D", "B")}
@@ -191,8 +194,10 @@ class GovernanceStore:
     def alloc(self, kind: str) -> int:
         """A free row of table ``kind`` (S sessions, E vouch edges, G sagas, T steps, V liability sessions)."""
         rows = self._rows[kind]
-        if len(self._pending[kind]) >= self.RECLAIM_BATCH:
+        if self._npend(kind) >= self.RECLAIM_BATCH:
             self.reclaim(kind)
+        if not rows.free and rows.free_arr:
+            rows.free.extend(rows.free_arr.pop().tolist())
         if rows.free:
             return rows.free.pop()
         if rows.hw < rows.cap:
@@ -210,34 +215,52 @@ class GovernanceStore:
         collector frees — before the caller grows the table."""
         import gc
 
-        if self._pending[kind] and self.reclaim(kind):
+        if self._npend(kind) and self.reclaim(kind):
             return True
         gc.collect()
-        return bool(self._pending[kind]) and self.reclaim(kind) > 0
+        return bool(self._npend(kind)) and self.reclaim(kind) > 0
 
-    def alloc_many(self, kind: str, n: int) -> list:
-        """``n`` free rows of table ``kind`` (reclaimed rows first, then fresh ones;
-        the table grows as needed)."""
+    def _npend(self, kind: str) -> int:
+        return len(self._pending[kind]) + sum(len(a) for a in self._pending_arr[kind])
+
+    def alloc_many(self, kind: str, n: int) -> np.ndarray:
+        """``n`` free rows of table ``kind`` as int32 (reclaimed rows first, then fresh
+        ones; the table grows as needed)."""
         rows = self._rows[kind]
         out: list = []
-        if len(self._pending[kind]) >= self.RECLAIM_BATCH:
+        got = 0
+        if self._npend(kind) >= self.RECLAIM_BATCH:
             self.reclaim(kind)
-        while len(out) < n:
-            need = n - len(out)
+        while got < n:
+            need = n - got
+            if rows.free_arr:
+                a = rows.free_arr[-1]
+                k = min(need, len(a))
+                out.append(a[len(a) - k:])
+                if k == len(a):
+                    rows.free_arr.pop()
+                else:
+                    rows.free_arr[-1] = a[:len(a) - k]
+                got += k
+                continue
             if rows.free:
                 k = min(need, len(rows.free))
-                out.extend(rows.free[-k:])
+                out.append(np.asarray(rows.free[-k:], dtype=np.int32))
                 del rows.free[-k:]
+                got += k
                 continue
             room = rows.cap - rows.hw
             if room > 0:
                 k = min(need, room)
-                out.extend(range(rows.hw, rows.hw + k))
+                out.append(np.arange(rows.hw, rows.hw + k, dtype=np.int32))
                 rows.hw += k
+                got += k
                 continue
             if not self._room(kind):
                 self._grow(kind)
-        return out
+        if not out:
+            return np.zeros(0, dtype=np.int32)
+        return out[0] if len(out) == 1 else np.concatenate(out)
 
     def reserve_deltas(self, caps: list) -> tuple:
         """Delta rows + arena reservations of ``caps`` bytes each (batched pipeline):
@@ -256,27 +279,36 @@ class GovernanceStore:
         self._pending[kind].append(row)
 
     def release_many(self, kind: str, rows) -> None:
-        self._pending[kind].extend(rows)
+        """Queue many rows: an int sequence, or an int32 array (kept as one chunk: no
+        per-row Python objects on the batched paths)."""
+        if isinstance(rows, np.ndarray):
+            if len(rows):
+                self._pending_arr[kind].append(np.ascontiguousarray(rows, dtype=np.int32))
+        else:
+            self._pending[kind].extend(rows)
 
     def reclaim(self, kind: Optional[str] = None) -> int:
         """Return queued rows to the free lists (one OP_FREE_ROWS per table); returns the count."""
         total = 0
         with self._lock:
             for k in ([kind] if kind else list(self._pending)):
-                pend = self._pending[k]
-                n = len(pend)
-                if not n:
+                pend, arrs = self._pending[k], self._pending_arr[k]
+                n, na = len(pend), len(arrs)
+                if not n and not na:
                     continue
-                rows = pend[:n]
+                parts = [np.asarray(pend[:n], dtype=np.int32)] if n else []
+                parts += arrs[:na]
                 del pend[:n]  # rows queued meanwhile (GC during this call) stay queued
+                del arrs[:na]
+                rows = parts[0] if len(parts) == 1 else np.concatenate(parts)
                 if self._closed:
                     continue
                 if k == "D":
-                    self._c.free_deltas(rows)
+                    self._c.free_deltas_arr(rows)
                 else:
-                    self._c.free_rows(_KIND[k], rows)
-                    self._rows[k].free.extend(rows)
-                total += n
+                    self._c.free_rows_arr(_KIND[k], rows)
+                    self._rows[k].free_arr.append(rows)
+                total += len(rows)
         return total
 
     def live_rows(self) -> dict:
@@ -439,7 +471,7 @@ class GovernanceStore:
         return self._c.payload(off, n)
 
     def capture(self, slot: int, turn: int, ts_us: int, delta) -> tuple:
-        if len(self._pending["D"]) >= self.RECLAIM_BATCH:
+        if self._npend("D") >= self.RECLAIM_BATCH:
             self.reclaim("D")
         r = self._c.capture(slot, turn, ts_us, delta)
         tries = 0

@@ -228,15 +228,15 @@ class _Batch:
         sel = np.zeros(n, dtype=bool)
         sel[idx] = True
         refused = self.status == 1  # the device kept the row from us: not ours to free
-        st.release_many("S", self.slots[sel & ~refused].tolist())
+        st.release_many("S", self.slots[sel & ~refused])
         nd = np.diff(self.delta_off)
         if nd.any():
-            st.release_many("D", self.drows[np.repeat(sel, nd)].tolist())
+            st.release_many("D", self.drows[np.repeat(sel, nd)])
         g = self.gslots[sel]
         g = g[g >= 0]
         if len(g):
-            st.release_many("G", g.tolist())
-            st.release_many("T", self.tslots[np.repeat(sel, np.diff(self.step_off))].tolist())
+            st.release_many("G", g)
+            st.release_many("T", self.tslots[np.repeat(sel, np.diff(self.step_off))])
 
     def __del__(self) -> None:
         try:

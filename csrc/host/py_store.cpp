@@ -15,6 +15,7 @@
 // agent_hypervisor_amd/models/store.py) passed in by data pointer.
 #include <Python.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
@@ -734,6 +735,14 @@ void register_store(py::module_& m) {
       .def("capture_bytes", &Store::capture_bytes)
       .def("restore_delta", &Store::restore_delta)
       .def("free_deltas", &Store::free_deltas)
+      .def("free_deltas_arr",
+           [](Store& st, py::array_t<int32_t, py::array::c_style | py::array::forcecast> a) {
+             st.free_deltas(std::vector<int32_t>(a.data(), a.data() + a.size()));
+           })
+      .def("free_rows_arr",
+           [](Store& st, uint64_t kind, py::array_t<int32_t, py::array::c_style | py::array::forcecast> a) {
+             st.free_rows_cmd(kind, std::vector<int32_t>(a.data(), a.data() + a.size()));
+           })
       .def("reserve_deltas", &Store::reserve_deltas)
       .def("run_pipeline", &Store::run_pipeline)
       .def("free_rows", &Store::free_rows_cmd)
