@@ -305,16 +305,23 @@ struct ArenaSink {
       nb = 0;
     }
   }
+  // The top n ≤ 4 bytes of v appended after the nb pending bytes with one funnel
+  // shift (at most one word completes), not n byte steps: n and nb differ per
+  // lane, and a per-byte loop made every lane of a wave run the longest one.
   AHV_HD void put(uint32_t v, uint32_t n) {
-    for (uint32_t j = 0; j < n; ++j) byte(v >> (24 - 8 * j));
-  }
-  AHV_HD void put4(uint32_t v) {
-    if (nb == 0) {  // aligned
-      word(bswap32(v));
-      return;
+    const uint32_t m = n >= 4 ? 0xffffffffu : (1u << (8 * n)) - 1u;
+    const uint64_t x = static_cast<uint64_t>(acc) | (static_cast<uint64_t>(bswap32(v) & m) << (8 * nb));
+    const uint32_t tot = nb + n;
+    if (tot >= 4) {
+      word(static_cast<uint32_t>(x));
+      acc = static_cast<uint32_t>(x >> 32);
+      nb = tot - 4;
+    } else {
+      acc = static_cast<uint32_t>(x);
+      nb = tot;
     }
-    put(v, 4);
   }
+  AHV_HD void put4(uint32_t v) { put(v, 4); }
   AHV_HD void flush() {
     if (nb) {
       word(acc);
@@ -412,7 +419,8 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   int32_t hole = -1;
   if (turn > 1) {
     hole = static_cast<int32_t>(snk.pos());
-    for (int b = 0; b < 66; ++b) snk.byte(0x22u);  // placeholder: the chain kernel writes the quoted digest
+    for (int b = 0; b < 16; ++b) snk.put4(0x22222222u);  // 66-byte placeholder: the chain kernel
+    snk.put(0x22220000u, 2);                              // writes the quoted digest into it
   } else {
     emit_lit(snk, canon::K_NULL);
   }
