@@ -221,7 +221,9 @@ class GovernanceStore:
         return bool(self._npend(kind)) and self.reclaim(kind) > 0
 
     def _npend(self, kind: str) -> int:
-        return len(self._pending[kind]) + sum(len(a) for a in self._pending_arr[kind])
+        n = len(self._pending[kind])
+        arrs = self._pending_arr[kind]
+        return n + sum(len(a) for a in arrs) if arrs else n  # per-call paths: no generator
 
     def alloc_many(self, kind: str, n: int) -> np.ndarray:
         """``n`` free rows of table ``kind`` as int32 (reclaimed rows first, then fresh
