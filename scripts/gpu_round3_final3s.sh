@@ -1,0 +1,13 @@
+#!/bin/bash
+# Short round-end check after the render-sink change: every GPU test and smoke().
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp AHV_SKIP_AUTOBUILD=1
+OUT=gpurun_out/r3final3s
+mkdir -p $OUT
+echo "[r3final3s] $(date +%T) tests"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.log; exit 1; }
+echo "[r3final3s] $(date +%T) smoke"
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/tests.log
+echo "[r3final3s] $(date +%T) done"
