@@ -114,23 +114,6 @@ class StoreError(RuntimeError):
     """A store command failed for a reason the API layer does not map to a user error."""
 
 
-class _Rows:
-    """Host allocator of one table: LIFO free list of reclaimed rows (single rows as
-    ints, bulk-reclaimed rows as int32 array chunks) + high-water mark."""
-
-    __slots__ = ("cap", "hw", "free", "free_arr")
-
-    def __init__(self, cap: int) -> None:
-        self.cap = cap
-        self.hw = 0
-        self.free: list[int] = []
-        self.free_arr: list[np.ndarray] = []
-
-    @property
-    def live(self) -> int:
-        return self.hw - len(self.free) - sum(len(a) for a in self.free_arr)
-
-
 class GovernanceStore:
     """Device tables + command transport + host-side allocators/interners.
 
@@ -179,9 +162,9 @@ class GovernanceStore:
         self._closed = False
         self.agents = Interner()  # DID → dense agent id
         self.pool = Interner()  # strings the batched pipeline renders (DIDs, change fields)
-        self._rows = {k: _Rows(c[k]) for k in ("S", "G", "T", "E", "V")}
-        self._pending: dict[str, list] = {k: [] for k in ("S", "G", "T", "E", "V", "D")}
-        self._pending_arr: dict[str, list] = {k: [] for k in ("S", "G", "T", "E", "V", "D")}  # int32 chunks
+        # row allocators live in the native store (Store.alloc_row / release_row / reclaim_pool)
+        self._alloc_row = self._c.alloc_row
+        self._release_row = self._c.release_row
         self._tenant_v: dict[int, dict[str, int]] = {}  # tenant → liability session id → V row
         self._tenants = 0
         self.grows = {k: 0 for k in ("S", "G", "T", "E", "V", "D", "B")}
@@ -189,80 +172,31 @@ class GovernanceStore:
         self._polling = False
         self._deferred: list = []  # (seq, nres, check) of speculative posts not verified yet
         self.seed = int.from_bytes(os.urandom(8), "little") >> 1
+        self._stamp_seq = 0
 
     # -- allocation ----------------------------------------------------------
     def alloc(self, kind: str) -> int:
-        """A free row of table ``kind`` (S sessions, E vouch edges, G sagas, T steps, V liability sessions)."""
-        rows = self._rows[kind]
-        if self._npend(kind) >= self.RECLAIM_BATCH:
-            self.reclaim(kind)
-        if not rows.free and rows.free_arr:
-            rows.free.extend(rows.free_arr.pop().tolist())
-        if rows.free:
-            return rows.free.pop()
-        if rows.hw < rows.cap:
-            i = rows.hw
-            rows.hw = i + 1
-            return i
-        if self._room(kind):
-            return self.alloc(kind)
-        self._grow(kind)
-        return self.alloc(kind)
-
-    def _room(self, kind: str) -> bool:
-        """Table ``kind`` is full: reclaim queued rows, then (once) collect unreachable
-        API views — chains of delta views are reference cycles only the cyclic
-        collector frees — before the caller grows the table."""
-        import gc
-
-        if self._npend(kind) and self.reclaim(kind):
-            return True
-        gc.collect()
-        return bool(self._npend(kind)) and self.reclaim(kind) > 0
-
-    def _npend(self, kind: str) -> int:
-        n = len(self._pending[kind])
-        arrs = self._pending_arr[kind]
-        return n + sum(len(a) for a in arrs) if arrs else n  # per-call paths: no generator
+        """A free row of table ``kind`` (S sessions, E vouch edges, G sagas, T steps,
+        V liability sessions): reclaimed rows first, then fresh ones; a full table
+        grows (rows keep their index) up to its ``AHV_STORE_MAX_*`` ceiling."""
+        k = _KIND[kind]
+        r = self._alloc_row(k)
+        while r < 0:
+            self._grow(kind)
+            r = self._alloc_row(k)
+        return r
 
     def alloc_many(self, kind: str, n: int) -> np.ndarray:
         """``n`` free rows of table ``kind`` as int32 (reclaimed rows first, then fresh
         ones; the table grows as needed)."""
-        rows = self._rows[kind]
-        out: list = []
-        got = 0
-        if self._npend(kind) >= self.RECLAIM_BATCH:
-            self.reclaim(kind)
-        while got < n:
-            need = n - got
-            if rows.free_arr:
-                a = rows.free_arr[-1]
-                k = min(need, len(a))
-                out.append(a[len(a) - k:])
-                if k == len(a):
-                    rows.free_arr.pop()
-                else:
-                    rows.free_arr[-1] = a[:len(a) - k]
-                got += k
-                continue
-            if rows.free:
-                k = min(need, len(rows.free))
-                out.append(np.asarray(rows.free[-k:], dtype=np.int32))
-                del rows.free[-k:]
-                got += k
-                continue
-            room = rows.cap - rows.hw
-            if room > 0:
-                k = min(need, room)
-                out.append(np.arange(rows.hw, rows.hw + k, dtype=np.int32))
-                rows.hw += k
-                got += k
-                continue
-            if not self._room(kind):
-                self._grow(kind)
-        if not out:
+        if n <= 0:
             return np.zeros(0, dtype=np.int32)
-        return out[0] if len(out) == 1 else np.concatenate(out)
+        k = _KIND[kind]
+        out = self._c.alloc_rows(k, n)
+        while out is None:
+            self._grow(kind)
+            out = self._c.alloc_rows(k, n)
+        return out
 
     def reserve_deltas(self, caps: list) -> tuple:
         """Delta rows + arena reservations of ``caps`` bytes each (batched pipeline):
@@ -278,45 +212,29 @@ class GovernanceStore:
 
     def release(self, kind: str, row: int) -> None:
         """Queue a row whose last API reference is gone (safe to call from ``__del__``)."""
-        self._pending[kind].append(row)
+        self._release_row(_KIND[kind], row)
 
     def release_many(self, kind: str, rows) -> None:
-        """Queue many rows: an int sequence, or an int32 array (kept as one chunk: no
-        per-row Python objects on the batched paths)."""
-        if isinstance(rows, np.ndarray):
-            if len(rows):
-                self._pending_arr[kind].append(np.ascontiguousarray(rows, dtype=np.int32))
-        else:
-            self._pending[kind].extend(rows)
+        """Queue many rows: an int sequence or an int32 array (one native call)."""
+        if len(rows):
+            self._c.release_rows(_KIND[kind], np.ascontiguousarray(rows, dtype=np.int32))
+
+    def _npend(self, kind: str) -> int:
+        return self._c.npend(_KIND[kind])
 
     def reclaim(self, kind: Optional[str] = None) -> int:
         """Return queued rows to the free lists (one OP_FREE_ROWS per table); returns the count."""
+        if self._closed:
+            return 0
         total = 0
         with self._lock:
-            for k in ([kind] if kind else list(self._pending)):
-                pend, arrs = self._pending[k], self._pending_arr[k]
-                n, na = len(pend), len(arrs)
-                if not n and not na:
-                    continue
-                parts = [np.asarray(pend[:n], dtype=np.int32)] if n else []
-                parts += arrs[:na]
-                del pend[:n]  # rows queued meanwhile (GC during this call) stay queued
-                del arrs[:na]
-                rows = parts[0] if len(parts) == 1 else np.concatenate(parts)
-                if self._closed:
-                    continue
-                if k == "D":
-                    self._c.free_deltas_arr(rows)
-                else:
-                    self._c.free_rows_arr(_KIND[k], rows)
-                    self._rows[k].free_arr.append(rows)
-                total += len(rows)
+            for k in ([kind] if kind else list(_KIND)):
+                total += self._c.reclaim_pool(_KIND[k])
         return total
 
     def live_rows(self) -> dict:
-        out = {k: r.live for k, r in self._rows.items()}
-        out["D"] = self._c.delta_live
-        return out
+        """Rows held by API objects (allocated, not released), per table."""
+        return {k: self._c.live_rows(v) for k, v in _KIND.items()}
 
     def _grow(self, kind: str) -> None:
         """Double table ``kind`` (rows keep their indices), up to its ``AHV_STORE_MAX_*``."""
@@ -341,8 +259,6 @@ class GovernanceStore:
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             self.caps = caps
-            if kind in self._rows:
-                self._rows[kind].cap = new
             self._c.rebind({k: v.data_ptr() for k, v in self.tables.items()}, dict(caps))
             self.grows[kind] += 1
 
@@ -358,7 +274,7 @@ class GovernanceStore:
 
     def _make_room(self, code: int, tries: int) -> None:
         """capture / restore_delta reported a full table (-2 deltas, -3 arena)."""
-        if tries == 0 and self._room("D"):
+        if tries == 0 and self.reclaim("D"):
             return
         if code == -2:
             self._grow("D")
@@ -371,10 +287,16 @@ class GovernanceStore:
 
     def release_tenant(self, tenant: int, edges) -> None:
         """A vouching engine is gone: its edge rows and liability-session rows are reclaimable."""
-        self._pending["E"].extend(edges)
+        self.release_many("E", list(edges))
         vs = self._tenant_v.pop(tenant, None)
         if vs:
-            self._pending["V"].extend(vs.values())
+            self.release_many("V", list(vs.values()))
+
+    def next_stamp(self) -> int:
+        """A creation stamp for a session whose id is not a uuid: a per-store serial
+        with the top bit set (never a uuid4's low half, whose variant bits are 10)."""
+        self._stamp_seq += 1
+        return (1 << 63) | (0x3FFFFFFF << 32) | (self._stamp_seq & 0xFFFFFFFF)
 
     def agent_id(self, did: str) -> int:
         return self.agents.intern(did)
@@ -407,45 +329,57 @@ class GovernanceStore:
     # -- speculation: commands whose outcome the host already knows -------------
     DEFERRED_MAX = 512  # unverified speculative posts before a blocking verification
 
-    def post_checked(self, op: int, args: list, nres: int, check, inline: Optional[bytes] = None) -> int:
+    def post_checked(self, op: int, args: list, nres: int, check, inline: Optional[bytes] = None,
+                     owner=None) -> int:
         """Post a command whose result the caller has predicted (from the same
         semantics.h predicates over state only it mutates) without waiting for it;
-        ``check(result)`` returns None when the device agreed, else the exception to
-        raise.  Results are verified by :meth:`verify_deferred` — before every later
-        store call and whenever the list grows long — so a disagreement (an internal
-        invariant violation) surfaces at the next interaction with the store."""
+        ``check(result)`` returns None when the device agreed, else the exception
+        the prediction's owner gets.  Results are verified by :meth:`verify_deferred`
+        (before every later store call and whenever the list grows long).
+
+        ``owner``: the API object the prediction belongs to (a device session).  A
+        disagreement — an internal invariant violation — is handed to it
+        (``owner._spec_failed(exc)``) and raised on *its* next operation; it never
+        surfaces in a call made by another session or tenant sharing the store."""
         q = self._c.post(op, args, inline)
         self._c.keep(q)
-        self.defer(q, nres, check)
+        self.defer(q, nres, check, owner)
         return q
 
-    def defer(self, seq: int, nres: int, check) -> None:
+    def defer(self, seq: int, nres: int, check, owner=None) -> None:
         """Verify a kept post (``post(..., keep=True)``) later instead of awaiting it."""
-        self._deferred.append((seq, nres, check))
+        self._deferred.append((seq, nres, check, owner))
         if len(self._deferred) >= self.DEFERRED_MAX:
             self.verify_deferred(block=True)
 
     def verify_deferred(self, block: bool = False) -> None:
         """Check speculatively posted commands whose results are in (all of them with
-        ``block``); raises the first disagreement."""
+        ``block``).  A disagreement goes to the prediction's owner; only an
+        unowned prediction raises here."""
+        if block:
+            self._c.check_frees(True)  # row reclaims posted without waiting (native allocator)
         ds = self._deferred
         if not ds:
             return
         self._deferred = []
         pending, err, misses = [], None, 0
         try_result = self._c.try_result
-        for i, (q, nres, check) in enumerate(ds):
-            r = try_result(q, nres, 1_000_000_000 if block else 0)
+        for i, d in enumerate(ds):
+            r = try_result(d[0], d[1], 1_000_000_000 if block else 0)
             if r is None:
-                pending.append((q, nres, check))
+                pending.append(d)
                 misses += 1
                 if misses >= self.POLL_MISSES:  # results complete in post order: the rest are pending too
                     pending.extend(ds[i + 1:])
                     break
                 continue
             misses = 0
-            e = check(r)
-            if e is not None and err is None:
+            e = d[2](r)
+            if e is None:
+                continue
+            if d[3] is not None:
+                d[3]._spec_failed(e)
+            elif err is None:
                 err = e
         self._deferred = pending + self._deferred
         if err is not None:
@@ -473,8 +407,8 @@ class GovernanceStore:
         return self._c.payload(off, n)
 
     def capture(self, slot: int, turn: int, ts_us: int, delta) -> tuple:
-        if self._npend("D") >= self.RECLAIM_BATCH:
-            self.reclaim("D")
+        if self._c.npend(4) >= self.RECLAIM_BATCH:
+            self._c.reclaim_pool(4)
         r = self._c.capture(slot, turn, ts_us, delta)
         tries = 0
         while r[0] <= -2:

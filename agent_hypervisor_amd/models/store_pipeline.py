@@ -663,7 +663,7 @@ def materialize(b: _Batch, i: int) -> tuple:
         de._rows.append(int(b.drows[g]))
         prev = d
     de._turn_counter = d1 - d0
-    orch = _device.DeviceSagaOrchestrator(st)
+    orch = _device.DeviceSagaOrchestrator(st, sso)
     g = int(b.gslots[i])
     if g >= 0:
         gids, tids = b.saga_ids()

@@ -164,12 +164,12 @@ class RpcEndpoint:
 
     # -- client side ------------------------------------------------------------
     async def _conn(self, rank: int):
-        c = self._conns.get(rank)
+        c = self._live(rank)
         if c is not None:
             return c
         lock = self._conn_lock.setdefault(rank, asyncio.Lock())
         async with lock:
-            c = self._conns.get(rank)
+            c = self._live(rank)
             if c is not None:
                 return c
             path = self.peers.get(rank)
@@ -177,12 +177,31 @@ class RpcEndpoint:
                 raise ConnectionError(f"no RPC address for rank {rank}")
             reader, writer = await asyncio.open_unix_connection(path)
             pend: dict[int, asyncio.Future] = {}
-            task = asyncio.get_running_loop().create_task(self._reader(rank, reader, pend))
+            task = asyncio.get_running_loop().create_task(self._reader(rank, reader, writer, pend))
             c = (writer, pend, task)
             self._conns[rank] = c
             return c
 
-    async def _reader(self, rank: int, reader: asyncio.StreamReader, pend: dict) -> None:
+    def _live(self, rank: int):
+        """The open connection to ``rank`` or None; a connection whose writer is
+        closing is forgotten here (its reader fails its pending calls), so the
+        next :meth:`call` reconnects instead of writing into a dead socket."""
+        c = self._conns.get(rank)
+        if c is not None and c[0].is_closing():
+            self._forget(rank, c)
+            return None
+        return c
+
+    def _forget(self, rank: int, c: tuple) -> None:
+        if self._conns.get(rank) is c:
+            del self._conns[rank]
+        c[0].close()
+        for f in c[1].values():
+            if not f.done():
+                f.set_exception(ConnectionError(f"rank {rank}: connection lost"))
+        c[1].clear()
+
+    async def _reader(self, rank: int, reader: asyncio.StreamReader, writer, pend: dict) -> None:
         try:
             while True:
                 msg = json.loads(await _read_frame(reader))
@@ -196,10 +215,19 @@ class RpcEndpoint:
                         f.set_exception(e)
                 else:
                     f.set_result(msg.get("ok"))
-        except (asyncio.IncompleteReadError, ConnectionError, asyncio.CancelledError, ValueError):
+        except (asyncio.IncompleteReadError, ConnectionError, asyncio.CancelledError, ValueError, OSError):
+            pass
+        # the connection is dead: fail what waits on it and drop it (if it is still the
+        # registered one), so later calls reconnect rather than reuse a closed writer
+        c = self._conns.get(rank)
+        if c is not None and c[0] is writer:
+            self._forget(rank, c)
+        else:
+            writer.close()
             for f in pend.values():
                 if not f.done():
                     f.set_exception(ConnectionError(f"rank {rank}: connection lost"))
+            pend.clear()
 
     async def connect(self, rank: int) -> None:
         """Open the connection to ``rank`` now (so :meth:`send` can write at once)."""
@@ -207,10 +235,15 @@ class RpcEndpoint:
 
     def send(self, rank: int, name: str, *args, **kwargs) -> "asyncio.Future":
         """Write a call to an already connected peer *now* (no await before the bytes
-        leave) and return the future of its result."""
-        writer, pend, _ = self._conns[rank]
-        rid = next(self._ids)
+        leave) and return the future of its result.  A peer whose connection is gone
+        yields an already-failed future (never one that stays unresolved)."""
         fut = asyncio.get_running_loop().create_future()
+        c = self._live(rank)
+        if c is None:
+            fut.set_exception(ConnectionError(f"rank {rank}: not connected"))
+            return fut
+        writer, pend, _ = c
+        rid = next(self._ids)
         pend[rid] = fut
         writer.write(_frame({"id": rid, "m": name, "a": list(args), "k": kwargs}))
         self.counters["rpc_out"] += 1
@@ -224,5 +257,9 @@ class RpcEndpoint:
         pend[rid] = fut
         writer.write(_frame({"id": rid, "m": name, "a": list(args), "k": kwargs}))
         self.counters["rpc_out"] += 1
-        await writer.drain()
+        try:
+            await writer.drain()
+        except (ConnectionError, OSError) as e:
+            pend.pop(rid, None)
+            raise ConnectionError(f"rank {rank}: connection lost") from e
         return await fut

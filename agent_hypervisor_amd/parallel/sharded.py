@@ -215,13 +215,20 @@ class ShardedHypervisor:
             h = (h + 1) % self.world
         return h
 
+    _MINT_TRIES = 1 << 16  # P(no hit) for one live rank of 8 after this many draws: (7/8)^65536
+
     def _mint(self, prefix: str, target: int) -> str:
+        """A fresh ``prefix{uuid4}`` whose owner is ``target`` (a live rank: an id can
+        only hash to a live rank, so a dead or unknown target is refused up front)."""
         from agent_hypervisor_amd._native import C
 
-        while True:
+        if target not in self._live:
+            raise ValueError(f"rank {target} is not a live member {sorted(self._live)}")
+        for _ in range(self._MINT_TRIES):
             k = C.uuid4(prefix)
             if self.owner(k) == target:
                 return k
+        raise RuntimeError(f"could not mint an id owned by rank {target}")
 
     async def _route(self, key: str, name: str, *args, **kwargs) -> Any:
         o = self.owner(key)

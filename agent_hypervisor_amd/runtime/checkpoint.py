@@ -117,21 +117,28 @@ def _staging_dir(d: str) -> str:
 def recover(d: str) -> str:
     """The checkpoint directory to load for ``d``: ``d`` itself, or — when a crash
     hit :func:`_publish` between its two renames — the previous checkpoint left
-    at ``d.old-*`` (moved back into place).  Staging directories are never
-    loaded."""
+    at ``d.old-*``.  Loaders only *pick* the path and never rename anything:
+    several survivors of a failover load the same dead rank's directory at the
+    same time, and a rename race among them would abort the loser.  Rolling the
+    old directory back into place is the writer's job (:func:`_publish` of the
+    next checkpoint replaces it).  Staging directories are never loaded."""
     import glob
 
     d = os.path.abspath(d)
     if os.path.exists(os.path.join(d, "manifest.json")):
         return d
-    olds = sorted(glob.glob(d + ".old-*"), key=os.path.getmtime, reverse=True)
+    olds = sorted(glob.glob(d + ".old-*"), key=_mtime, reverse=True)
     for o in olds:
         if os.path.exists(os.path.join(o, "manifest.json")):
-            if not os.path.exists(d):
-                os.replace(o, d)
-                return d
             return o
     return d
+
+
+def _mtime(p: str) -> float:
+    try:
+        return os.path.getmtime(p)
+    except FileNotFoundError:  # removed by a concurrent publish
+        return 0.0
 
 
 def _publish(tmp: str, d: str) -> str:
@@ -142,14 +149,17 @@ def _publish(tmp: str, d: str) -> str:
     (called by every loader) moves back."""
     import shutil
 
+    import glob
+
     d = os.path.abspath(d)
+    stale = [o for o in glob.glob(d + ".old-*")]  # left by an earlier crash mid-publish
     old = None
     if os.path.exists(d):
         old = d + ".old-" + os.path.basename(tmp)
         os.replace(d, old)
     os.replace(tmp, d)
-    if old is not None:
-        shutil.rmtree(old, ignore_errors=True)
+    for o in ([old] if old is not None else []) + stale:
+        shutil.rmtree(o, ignore_errors=True)
     return d
 
 
@@ -619,7 +629,7 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
             for k, w in enumerate(_device._words(c["merkle_root"])):
                 put("s_root", 8 * s + k, w)
             hv.commitment.register(sso)
-        saga_orch = _device.DeviceSagaOrchestrator(st)
+        saga_orch = _device.DeviceSagaOrchestrator(st, sso)
         for g in r["sagas"]:
             gslot = st.alloc("G")
             saga = _device.DeviceSaga(st, gslot, g["saga_id"], g["session_id"])

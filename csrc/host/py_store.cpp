@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
 
+#include <algorithm>
 #include <chrono>
 #include <map>
 #include <unordered_map>
@@ -186,6 +187,11 @@ class Store {
     t_.payload = payload_;
     t_.staging = staging_;
     arena_.reset(t_.cap.B);
+    pools_[0].cap = t_.cap.S;
+    pools_[1].cap = t_.cap.G;
+    pools_[2].cap = t_.cap.T;
+    pools_[3].cap = t_.cap.E;
+    pools_[4].cap = t_.cap.V;
     d_off_.assign(static_cast<size_t>(t_.cap.D), -1);
     d_len_.assign(static_cast<size_t>(t_.cap.D), 0);
   }
@@ -245,6 +251,11 @@ class Store {
 #undef AHV_PTR
     d_off_.resize(static_cast<size_t>(t_.cap.D), -1);
     d_len_.resize(static_cast<size_t>(t_.cap.D), 0);
+    pools_[0].cap = t_.cap.S;
+    pools_[1].cap = t_.cap.G;
+    pools_[2].cap = t_.cap.T;
+    pools_[3].cap = t_.cap.E;
+    pools_[4].cap = t_.cap.V;
   }
 
   // Double (at least) the payload arena, keeping every record at its offset.
@@ -640,6 +651,162 @@ class Store {
     }
   }
 
+  // ------------------------------------------------------------ row allocator
+  //
+  // Free lists of the session / saga / step / vouch-edge / liability-session
+  // tables (RowKind S G T E V; delta rows have their own, with their arena
+  // records).  A row is *live* from alloc_row until its last API view releases
+  // it (release_row, cheap enough for a finaliser); released rows queue in
+  // `pend` and are reclaimed in small batches — OP_FREE_ROWS marks them free on
+  // the device, then they return to the free list.  The host does not wait for
+  // that command: every later command that could reuse a row executes after it
+  // (the worker runs commands in order, and batched kernels drain the worker
+  // first), so the rows are handed out again at once; the command's status is
+  // checked when the next reclaim of any table runs.  Delta rows are different:
+  // their arena bytes are rewritten by the host at the next capture's post, so
+  // they wait for the FREE_ROWS (which drains the hash engine) to complete.
+  struct RowPool {
+    int64_t cap = 0, hw = 0;
+    std::vector<int32_t> free, pend;
+  };
+
+  static size_t pool_index(uint64_t kind) {
+    switch (kind) {
+      case RK_S: return 0;
+      case RK_G: return 1;
+      case RK_T: return 2;
+      case RK_E: return 3;
+      case RK_V: return 4;
+      default: throw std::invalid_argument("row kind has no row pool: " + std::to_string(kind));
+    }
+  }
+  RowPool& pool(uint64_t kind) { return pools_[pool_index(kind)]; }
+
+  void set_row_cap(uint64_t kind, int64_t cap) { pool(kind).cap = cap; }
+
+  // Queued rows that trigger a reclaim: 256, or an eighth of a small table.
+  static size_t reclaim_at(const RowPool& p) {
+    return static_cast<size_t>(std::max<int64_t>(8, std::min<int64_t>(256, p.cap >> 3)));
+  }
+
+  // A free row of `kind`, or -1 when the table is full (the caller grows it).
+  int64_t alloc_row(uint64_t kind) {
+    RowPool& p = pool(kind);
+    if (p.pend.size() >= reclaim_at(p)) reclaim_pool(kind);
+    if (p.free.empty() && p.hw >= p.cap && !p.pend.empty()) reclaim_pool(kind);
+    if (!p.free.empty()) {
+      const int32_t r = p.free.back();
+      p.free.pop_back();
+      return r;
+    }
+    if (p.hw < p.cap) return p.hw++;
+    return -1;
+  }
+
+  // `n` free rows of `kind` (int32), or None when the table cannot hold them (nothing taken).
+  py::object alloc_rows(uint64_t kind, int64_t n) {
+    RowPool& p = pool(kind);
+    if (!p.pend.empty()) reclaim_pool(kind);
+    if (static_cast<int64_t>(p.free.size()) + (p.cap - p.hw) < n) return py::none();
+    py::array_t<int32_t> out(n);
+    int32_t* o = out.mutable_data();
+    int64_t k = 0;
+    while (k < n && !p.free.empty()) {
+      o[k++] = p.free.back();
+      p.free.pop_back();
+    }
+    while (k < n) o[k++] = static_cast<int32_t>(p.hw++);
+    return std::move(out);
+  }
+
+  void release_row(uint64_t kind, int64_t row) {
+    if (kind == RK_D) {
+      dpend_.push_back(static_cast<int32_t>(row));
+      return;
+    }
+    pool(kind).pend.push_back(static_cast<int32_t>(row));
+  }
+
+  // A row that was allocated but never written on the device (a refused vouch):
+  // straight back to the free list.
+  void return_row(uint64_t kind, int64_t row) { pool(kind).free.push_back(static_cast<int32_t>(row)); }
+
+  void release_rows(uint64_t kind, py::array_t<int32_t, py::array::c_style | py::array::forcecast> a) {
+    std::vector<int32_t>& v = kind == RK_D ? dpend_ : pool(kind).pend;
+    v.insert(v.end(), a.data(), a.data() + a.size());
+  }
+
+  // Return the queued rows of `kind` to its free list; returns their count.
+  int64_t reclaim_pool(uint64_t kind) {
+    if (kind == RK_D) {
+      if (dpend_.empty()) return 0;
+      std::vector<int32_t> rows;
+      rows.swap(dpend_);
+      free_deltas(rows);
+      return static_cast<int64_t>(rows.size());
+    }
+    RowPool& p = pool(kind);
+    if (p.pend.empty()) return 0;
+    check_frees();
+    std::vector<int32_t> rows;
+    rows.swap(p.pend);
+    post_frees(kind, rows);
+    p.free.insert(p.free.end(), rows.begin(), rows.end());
+    return static_cast<int64_t>(rows.size());
+  }
+
+  int64_t npend(uint64_t kind) const {
+    return static_cast<int64_t>(kind == RK_D ? dpend_.size() : pools_[pool_index(kind)].pend.size());
+  }
+  int64_t live_rows(uint64_t kind) const {
+    if (kind == RK_D) return delta_live() - static_cast<int64_t>(dpend_.size());
+    const RowPool& p = pools_[pool_index(kind)];
+    return p.hw - static_cast<int64_t>(p.free.size() + p.pend.size());
+  }
+
+  // OP_FREE_ROWS without waiting; statuses are checked by check_frees.
+  void post_frees(uint64_t kind, const std::vector<int32_t>& rows) {
+    const size_t per = static_cast<size_t>(staging_cap_ / 8);
+    for (size_t i = 0; i < rows.size(); i += per) {
+      const size_t n = std::min(per, rows.size() - i);
+      uint64_t a[3] = {kind, static_cast<uint64_t>(n), 0};
+      const uint8_t* raw = reinterpret_cast<const uint8_t*>(rows.data() + i);
+      uint64_t q;
+      if (n <= static_cast<size_t>(2 * kInlineWords)) {
+        q = post_raw(OP_FREE_ROWS, a, 3, raw, 4 * n);
+      } else {
+        a[2] = static_cast<uint64_t>(stage_raw(raw, 4 * n));
+        q = post_raw(OP_FREE_ROWS, a, 3, nullptr, 0);
+      }
+      keep(q);
+      frees_.push_back(q);
+    }
+  }
+
+  // Statuses of the FREE_ROWS posted so far whose results are in (`block`: all).
+  void check_frees(bool block = false) {
+    size_t k = 0;
+    for (; k < frees_.size(); ++k) {
+      const uint64_t q = frees_[k];
+      uint64_t st;
+      auto it = saved_.find(q);
+      if (it != saved_.end()) {
+        st = it->second[1];
+        saved_.erase(it);
+      } else {
+        volatile uint64_t* r = res_ + (q % static_cast<uint64_t>(nslots_)) * kResWords;
+        if (r[0] < q + 1 && !block) break;
+        st = wait(q)[1];
+        watched_.erase(q);
+      }
+      if (st != ST_OK) {
+        frees_.erase(frees_.begin(), frees_.begin() + static_cast<std::ptrdiff_t>(k + 1));
+        throw std::runtime_error("OP_FREE_ROWS failed with status " + std::to_string(st));
+      }
+    }
+    frees_.erase(frees_.begin(), frees_.begin() + static_cast<std::ptrdiff_t>(k));
+  }
+
   int64_t take_delta_row() {
     if (!dfree_.empty()) {
       const int32_t d = dfree_.back();
@@ -708,6 +875,9 @@ class Store {
   std::unordered_map<uint64_t, std::array<uint64_t, kSaveWords>> saved_;  // their results, once recycled
   std::vector<int64_t> d_off_, d_len_;  // arena record of each delta row (-1: row free)
   std::vector<int32_t> dfree_;          // reclaimed delta rows
+  std::vector<int32_t> dpend_;          // delta rows released by their views, not reclaimed yet
+  RowPool pools_[5];                    // S G T E V row allocators
+  std::vector<uint64_t> frees_;         // FREE_ROWS posted without waiting, status unchecked
   int64_t dhw_ = 0;                      // delta rows ever handed out (high-water mark)
   int timeout_s_ = 30;
   bool closed_ = false;
@@ -744,6 +914,16 @@ void register_store(py::module_& m) {
              st.free_rows_cmd(kind, std::vector<int32_t>(a.data(), a.data() + a.size()));
            })
       .def("reserve_deltas", &Store::reserve_deltas)
+      .def("alloc_row", &Store::alloc_row)
+      .def("alloc_rows", &Store::alloc_rows)
+      .def("release_row", &Store::release_row)
+      .def("release_rows", &Store::release_rows)
+      .def("return_row", &Store::return_row)
+      .def("reclaim_pool", &Store::reclaim_pool)
+      .def("check_frees", &Store::check_frees, py::arg("block") = false)
+      .def("npend", &Store::npend)
+      .def("live_rows", &Store::live_rows)
+      .def("set_row_cap", &Store::set_row_cap)
       .def("run_pipeline", &Store::run_pipeline)
       .def("free_rows", &Store::free_rows_cmd)
       .def("quiesce", &Store::quiesce)

@@ -399,6 +399,12 @@ AHV_HD void mark_committed_participants(const Tables& t, int64_t s) {
 }
 
 // Participant row of `agent` in session `s` (all rows, active or not), or -1.
+// Creation stamp of row s: the low 64 bits of the id words its create wrote (a
+// uuid4's low half always has the variant bits set, so it is never 0).
+AHV_HD uint64_t row_stamp(const Tables& t, int64_t s) {
+  return (static_cast<uint64_t>(t.s_uuid[4 * s + 2]) << 32) | t.s_uuid[4 * s + 3];
+}
+
 AHV_HD int32_t find_part(const Tables& t, int64_t s, int32_t agent) {
   const int32_t n = t.s_pcount[s];
   const int64_t base = s * t.cap.P;
@@ -751,8 +757,10 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       // a1 agent, a2 σ_raw, a3 σ_eff, a4 flags (bit0 trustworthy, bit1 explicit ring), a5 ring, a6 now,
       // a7 creation stamp the host sent with its create (0: unchecked) — a host that posts
       // before it has seen its create's result: a row holding another session (the create
-      // was refused) refuses the join instead of being changed (JOIN_NOT_MINE)
-      if (c.a[7] && t.s_created[s] != static_cast<int64_t>(c.a[7])) {
+      // was refused) refuses the join instead of being changed (JOIN_NOT_MINE).  The stamp
+      // is the low 64 bits of the session's id words (row_stamp), not a clock value: two
+      // creates in the same microsecond (or under a pinned clock) still differ.
+      if (c.a[7] && row_stamp(t, s) != c.a[7]) {
         out64(r + 1, JOIN_NOT_MINE);
         return;
       }
@@ -821,7 +829,7 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       out64(r + 1, ST_OK);
       return;
     case OP_SESS_ACTIVATE: {
-      if (c.a[1] && t.s_created[s] != static_cast<int64_t>(c.a[1])) {  // a1: creation stamp (see OP_SESS_JOIN)
+      if (c.a[1] && row_stamp(t, s) != c.a[1]) {  // a1: creation stamp (see OP_SESS_JOIN)
         out64(r + 1, ACT_NOT_MINE);
         return;
       }

@@ -161,25 +161,31 @@ class DeviceSession(SharedSessionObject):
             self._m_rows = {}
             self._m_cfg = (int(config.max_participants), float(config.min_sigma_eff))  # what the row holds
         self._stamp = 0  # creation stamp this object sent (0: not created here)
+        self._poisoned: Optional[Exception] = None  # a speculated post of this session the device refused
         if create:
             u = self.session_id.rsplit(":", 1)[-1].replace("-", "")
             try:
                 hi, lo = int(u[:16], 16), int(u[16:32], 16)
             except ValueError:
                 hi = lo = 0
-            stamp = _now_us()
+            if len(u) != 32 or not lo:  # not a uuid id: a per-store serial stands in for its id words
+                hi, lo = 0, store.next_stamp()
+            # the creation stamp later posts carry is the row's id words (row_stamp in
+            # store.h), not a clock value: creates in one µs / under a pinned clock differ
+            stamp = lo
             args = [
-                self.slot, store.agent_id(creator_did), stamp, _MODE[config.consistency_mode],
+                self.slot, store.agent_id(creator_did), _now_us(), _MODE[config.consistency_mode],
                 int(config.max_participants), dbits(config.min_sigma_eff), int(bool(config.enable_audit)),
                 _i64(hi), _i64(lo), 0 if handshake else 1,
             ]
             if self._m_state is not None and stamp:
                 # posted and verified later: the join / activate that follow carry the stamp,
                 # so a row holding another session (a refused create) refuses them on the device
-                self._stamp = stamp
+                self._stamp = _i64(stamp)
                 slot = self.slot
                 store.post_checked(_st.OP_SESS_CREATE, args, 2, lambda r: None if r[0] == 0 else _st.StoreError(
-                    f"device refused to create session in row {slot} (row state {r[1]}): allocator invariant violated"))
+                    f"device refused to create session in row {slot} (row state {r[1]}): allocator invariant violated"),
+                    owner=self)
             else:
                 self._cseq = store.post(_st.OP_SESS_CREATE, args)
 
@@ -190,6 +196,23 @@ class DeviceSession(SharedSessionObject):
             self._store.release("S", self.slot)
         except Exception:
             pass
+
+    # -- speculation failures (GovernanceStore.post_checked) -----------------------
+    def _spec_failed(self, exc: Exception) -> None:
+        """The device disagreed with a prediction this session posted: from now on
+        every operation of this session raises it (the first one is kept)."""
+        if self._poisoned is None:
+            self._poisoned = exc
+        self._m_forget()  # the mirror is wrong: nothing more is speculated for this row
+
+    def _guard(self) -> None:
+        """Raise this session's speculation failure, if any (after checking the
+        predictions whose results are in)."""
+        st = self._store
+        if st._deferred:
+            st.verify_deferred()
+        if self._poisoned is not None:
+            raise self._poisoned
 
     def _created(self) -> None:
         """Raise if the device refused the create (the slot was not free)."""
@@ -288,10 +311,12 @@ class DeviceSession(SharedSessionObject):
         slot = self.slot
         self._store.post_checked(_st.OP_SESS_ACTIVATE, [slot, self._stamp], 2,
                                  lambda r: None if r[0] == 0 else _st.StoreError(
-                                     f"speculated activate of row {slot} refused by the device (status {r[0]})"))
+                                     f"speculated activate of row {slot} refused by the device (status {r[0]})"),
+                                 owner=self)
         self._m_state = _S_ACTIVE
 
     def activate(self) -> None:
+        self._guard()
         if self._cseq >= 0:
             self._created()
         if self._activate_known_ok():
@@ -301,6 +326,7 @@ class DeviceSession(SharedSessionObject):
             self._m_state = _S_ACTIVE
 
     async def activate_async(self) -> None:
+        self._guard()
         if self._cseq >= 0:
             self._created()
         if self._activate_known_ok():
@@ -320,6 +346,7 @@ class DeviceSession(SharedSessionObject):
         _check(r, "activate")
 
     def _join_args(self, agent_did: str, sigma_raw: float, sigma_eff: float, flags: int, ring: int) -> list:
+        self._guard()
         if self._cseq >= 0:
             self._created()
         return [self.slot, self._store.agent_id(agent_did), dbits(sigma_raw), dbits(sigma_eff), flags, ring,
@@ -350,7 +377,8 @@ class DeviceSession(SharedSessionObject):
         slot = self.slot
         self._store.post_checked(_st.OP_SESS_JOIN, args, 6,
                                  lambda r: None if r[0] == 0 and r[1] == ring else _st.StoreError(
-                                     f"speculated join to row {slot} diverged from the device (status {r[0]})"))
+                                     f"speculated join to row {slot} diverged from the device (status {r[0]})"),
+                                 owner=self)
         rows[aid] = True
         self._m_active += 1
         return ring
@@ -397,6 +425,7 @@ class DeviceSession(SharedSessionObject):
         return _RINGS[self._join(agent_did, sigma_raw, sigma_eff, 1 if trustworthy else 0, 0)]
 
     def leave(self, agent_did: str) -> None:
+        self._guard()
         aid = self._store.agent_id(agent_did)
         r = self._store.call(_st.OP_SESS_LEAVE, [self.slot, aid], 1)
         if r[0]:
@@ -432,12 +461,14 @@ class DeviceSession(SharedSessionObject):
         self._m_rows = None
 
     def terminate(self) -> None:
+        self._guard()
         self._m_forget()
         r = self._store.call(_st.OP_SESS_TERMINATE, [self.slot, _now_us()], 2)
         if r[0]:
             raise _lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
 
     def archive(self) -> None:
+        self._guard()
         self._m_forget()
         r = self._store.call(_st.OP_SESS_ARCHIVE, [self.slot], 2)
         if r[0]:
@@ -474,13 +505,18 @@ class DeviceSession(SharedSessionObject):
 
 
 class DeviceDelta(SemanticDelta):
-    """A captured delta whose digest and parent link are held by the device chain."""
+    """A captured delta whose digest and parent link are held by the device chain.
+
+    It refers to the store, not to its engine: the engine lists its deltas, and a
+    back-reference would make every chain a reference cycle that only the cyclic
+    collector frees — the rows of a dropped session would then wait for a
+    ``gc.collect()`` instead of being released when the last reference goes."""
 
     def __init__(self, engine: "DeviceDeltaEngine", delta_id, turn_id, session_id, agent_did, timestamp, changes,
                  prev: Optional["DeviceDelta"]) -> None:
         self.__dict__.update(
             delta_id=delta_id, turn_id=turn_id, session_id=session_id, agent_did=agent_did, timestamp=timestamp,
-            changes=changes, _engine=engine, _prev=prev, _dev_hash=None, _hash_override=None,
+            changes=changes, _store=engine._store, _prev=prev, _dev_hash=None, _hash_override=None,
             _parent_override=None, _didx=-1, _poff=-1, _plen=0, _seq=-1, _dirty=False,
         )
 
@@ -499,7 +535,7 @@ class DeviceDelta(SemanticDelta):
         """The digest the device computed for this delta (K08)."""
         h = self.__dict__["_dev_hash"]
         if h is None:
-            h = self._engine._resolve(self)
+            h = _resolve(self._store, self)
         return h
 
     @property
@@ -531,7 +567,7 @@ class DeviceDelta(SemanticDelta):
 
     def record(self) -> bytes:
         """The device-held canonical-JSON record (exact hashed bytes)."""
-        return self._engine._store.payload(self._poff, self._plen)
+        return self._store.payload(self._poff, self._plen)
 
     def __repr__(self) -> str:
         return f"DeviceDelta(delta_id={self.delta_id!r}, turn_id={self.turn_id}, session_id={self.session_id!r})"
@@ -587,17 +623,7 @@ class DeviceDeltaEngine(DeltaEngine):
         return d
 
     def _resolve(self, d: DeviceDelta) -> str:
-        r = self._store.result(d._seq, 9)
-        if r is None:  # result slot recycled: read the arena row
-            n, off, inl = self._store.index_args([d._didx])
-            self._store.call(_st.OP_DELTA_READ, [n, off, 0], 1, inl)
-            raw = self._store.bulk(0, 96)
-            r = (0,) + struct.unpack_from("<8Q", raw, 32)
-        if r[0]:
-            raise _st.StoreError(f"device capture of {d.delta_id} failed with status {r[0]}")
-        h = _hex(r[1:9])
-        d.__dict__["_dev_hash"] = h
-        return h
+        return _resolve(self._store, d)
 
     def _indices(self) -> list[int]:
         return [d._didx for d in self._deltas]
@@ -659,6 +685,21 @@ class DeviceDeltaEngine(DeltaEngine):
         n = len(self._deltas) - len(keep)
         self._deltas = keep
         return n
+
+
+def _resolve(store: GovernanceStore, d: DeviceDelta) -> str:
+    """The device digest of a captured delta (its capture result, or its arena row)."""
+    r = store.result(d._seq, 9)
+    if r is None:  # result slot recycled: read the arena row
+        n, off, inl = store.index_args([d._didx])
+        store.call(_st.OP_DELTA_READ, [n, off, 0], 1, inl)
+        raw = store.bulk(0, 96)
+        r = (0,) + struct.unpack_from("<8Q", raw, 32)
+    if r[0]:
+        raise _st.StoreError(f"device capture of {d.delta_id} failed with status {r[0]}")
+    h = _hex(r[1:9])
+    d.__dict__["_dev_hash"] = h
+    return h
 
 
 class _NullParent:
@@ -761,7 +802,8 @@ class DeviceVouchingEngine(VouchingEngine):
             if rec is not None:
                 rec._freeze(act, rel)
             edges.append(e)
-        st._rows["E"].free.extend(edges)  # already free on the device (V_RETIRE)
+        for e in edges:  # already free on the device (V_RETIRE)
+            st._c.return_row(3, e)
         return n
 
     def _v(self, session_id: str, create: bool = False) -> int:
@@ -795,7 +837,7 @@ class DeviceVouchingEngine(VouchingEngine):
         )
         code = r[0]
         if code:  # rejected (or refused): the row was not linked and is still free on the device
-            st._rows["E"].free.append(edge)
+            st._c.return_row(3, edge)  # RK_E
         if code == 1:
             raise VouchingError("Cannot vouch for yourself")
         if code == 2:
@@ -1251,9 +1293,15 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
     loop; every state change they cause is a device command.
     """
 
-    def __init__(self, store: GovernanceStore) -> None:
+    def __init__(self, store: GovernanceStore, owner: Optional[DeviceSession] = None) -> None:
         self._store = store
         self._sagas: dict[str, DeviceSaga] = {}
+        self._owner = owner  # the session whose speculated step transitions these are
+
+    def _guard(self) -> None:
+        o = self._owner
+        if o is not None:
+            o._guard()
 
     async def execute_sagas(self, saga_ids, executors, compensator=None, compensate: bool = True,
                             device: Optional[str] = None) -> list:
@@ -1283,6 +1331,7 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         return step
 
     async def execute_step(self, saga_id: str, step_id: str, executor: Callable[..., Any]) -> Any:
+        self._guard()
         saga = self._get_saga(saga_id)
         step = self._get_step(saga, step_id)
         attempts = 1 + step.max_retries
@@ -1314,9 +1363,9 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                     # EXECUTING: neither needs the device's answer before returning —
                     # both are verified with the store's next interaction
                     st = self._store
-                    st.defer(seq, 2, _transition_check(step.slot, StepState.EXECUTING))
+                    st.defer(seq, 2, _transition_check(step.slot, StepState.EXECUTING), self._owner)
                     cseq = step.post_transition(StepState.COMMITTED)
-                    st.defer(cseq, 2, _transition_check(step.slot, StepState.COMMITTED))
+                    st.defer(cseq, 2, _transition_check(step.slot, StepState.COMMITTED), self._owner)
                     step.__dict__["_hint"] = StepState.COMMITTED
                     return result
                 if seq is not None:
@@ -1336,6 +1385,7 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         raise SagaStateError("Step execution failed with no error captured")
 
     async def compensate(self, saga_id: str, compensator: Callable[[SagaStep], Any]) -> list[SagaStep]:
+        self._guard()
         saga = self._get_saga(saga_id)
         saga.transition(SagaState.COMPENSATING)
         failed: list[SagaStep] = []
@@ -1431,7 +1481,7 @@ def saga_rows(store: GovernanceStore, sagas: list) -> dict:
 
 def session_views(store: GovernanceStore, sso: DeviceSession):
     """(delta engine, saga orchestrator) for a device session."""
-    return DeviceDeltaEngine(store, sso.slot, sso.session_id, sso), DeviceSagaOrchestrator(store)
+    return DeviceDeltaEngine(store, sso.slot, sso.session_id, sso), DeviceSagaOrchestrator(store, sso)
 
 
 __all__ = [

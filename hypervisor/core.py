@@ -284,6 +284,9 @@ class Hypervisor:
         session's bonds (K07) → GC retention count → archive."""
         _d = _device_mod()
         sso, de, st = managed.sso, managed.delta_engine, self._store
+        guard = getattr(sso, "_guard", None)
+        if guard is not None:  # a speculation of this session the device refused raises here
+            guard()
         sso._m_forget()  # the row leaves the mirrored states (terminate → archive)
         now_us = _d._now_us()
         v = st.liability_lookup(self._tenant, session_id)
@@ -292,6 +295,12 @@ class Hypervisor:
         r = await st.call_async(
             _d._st.OP_SESS_CLOSE, [sso.slot, n, off, now_us, v, cutoff, int(bool(sso.config.enable_audit))], 13, inl,
         )
+        if guard is not None and st._deferred:
+            # every post before the close has completed now: a prediction of this
+            # session that the device refused is this terminate's error
+            st.verify_deferred()
+            if sso._poisoned is not None:
+                raise sso._poisoned
         if r[0]:
             if r[0] == _d._st.ST_BAD_STATE:
                 raise _d._lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)

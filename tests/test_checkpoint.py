@@ -173,3 +173,29 @@ async def test_failed_save_keeps_previous_checkpoint(tmp_path, monkeypatch):
     assert ck.read_manifest(d, "hypervisor") == before
     restored = ck.load_hypervisor(d, hv=Hypervisor(device="host"))
     assert [x.sso.session_id for x in restored.sessions] == [m.sso.session_id]
+
+
+async def test_loaders_never_rename_after_crash_mid_publish(tmp_path):
+    """after a crash between _publish's two renames, every loader reads the
+    previous checkpoint from ``d.old-*`` in place (concurrent failover loaders must not
+    race on a rename); the next save publishes normally and removes the leftover."""
+    import concurrent.futures
+    import os
+
+    from agent_hypervisor_amd.runtime import checkpoint as ck
+    from hypervisor import Hypervisor, SessionConfig
+
+    hv = Hypervisor(device="host")
+    m = await hv.create_session(SessionConfig(), "did:admin")
+    d = str(tmp_path / "rank1")
+    ck.save_hypervisor(hv, d)
+    old = d + ".old-crashed"
+    os.replace(d, old)  # the crash: d moved aside, the new checkpoint never renamed in
+    with concurrent.futures.ThreadPoolExecutor(4) as ex:
+        keys = list(ex.map(lambda _: ck.checkpoint_session_keys(d), range(8)))
+    assert all(k == [m.sso.session_id] for k in keys)
+    assert os.path.isdir(old) and not os.path.exists(d)  # nothing renamed by the loaders
+    restored = ck.load_hypervisor(d, hv=Hypervisor(device="host"))
+    assert [x.sso.session_id for x in restored.sessions] == [m.sso.session_id]
+    ck.save_hypervisor(hv, d)
+    assert os.path.exists(os.path.join(d, "manifest.json")) and not os.path.exists(old)
