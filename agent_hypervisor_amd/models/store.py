@@ -173,6 +173,7 @@ class GovernanceStore:
         self._deferred: list = []  # (seq, nres, check) of speculative posts not verified yet
         self.seed = int.from_bytes(os.urandom(8), "little") >> 1
         self._stamp_seq = 0
+        self._id_ctr = 0  # device id generator counters handed out (reserve_ids)
 
     # -- allocation ----------------------------------------------------------
     def alloc(self, kind: str) -> int:
@@ -291,6 +292,13 @@ class GovernanceStore:
         vs = self._tenant_v.pop(tenant, None)
         if vs:
             self.release_many("V", list(vs.values()))
+
+    def reserve_ids(self, n: int) -> int:
+        """A range of ``n`` counters of the store's device id generator
+        (``uuid4_words(seed, counter)``, batched pipelines); returns its base."""
+        b = self._id_ctr
+        self._id_ctr = b + n
+        return b
 
     def next_stamp(self) -> int:
         """A creation stamp for a session whose id is not a uuid: a per-store serial

@@ -1,40 +1,28 @@
-"""Launcher for the batched governance pipeline kernel (``csrc/hip/pipeline.hip``).
+"""Launcher for the batched template pipeline over a store's rows
+(``csrc/hip/store_template.hip``, body ``csrc/include/ahv/store_template.h``).
 
-``run(args)`` validates that every tensor argument lives on one device and then
-launches the gfx950 kernel on the current HIP stream — or, for CPU tensors, runs
-the host twin (the same ``pipeline_session`` body instantiated for the CPU; used
-by the CPU test-suite and as the reference in GPU equivalence tests).  There is
-no silent fallback: a CUDA tensor always takes the kernel path.
+``run(store, args, tensors)`` launches the gfx950 kernel on the current HIP
+stream for a device store, or runs the host twin (the same ``template_session``
+body instantiated for the CPU) for a CPU store — no silent fallback: a device
+store always takes the kernel path.  The launch goes through the fault-injection
+hooks (:mod:`agent_hypervisor_amd.utils.faults`) under the name ``"pipeline"``;
+``tensors`` names the outputs an injected ``corrupt`` fault may flip.
 """
 
 from __future__ import annotations
 
 import torch
 
-from agent_hypervisor_amd._native import C
 from agent_hypervisor_amd.utils import faults as _faults
 
 
-def run(scalars: dict, tensors: dict[str, torch.Tensor | None]) -> None:
-    devs = {t.device for t in tensors.values() if t is not None}
-    if len(devs) != 1:
-        raise ValueError(f"pipeline tensors span devices {devs}")
-    (dev,) = devs
-    args = dict(scalars)
-    for k, t in tensors.items():
-        if t is None:
-            args[k] = None
-            continue
-        if not t.is_contiguous():
-            raise ValueError(f"pipeline argument {k} must be contiguous")
-        args[k] = t.data_ptr()
+def run(store, args: dict, tensors: dict[str, torch.Tensor] | None = None) -> None:
     if _faults.active() and not _faults.before_launch("pipeline"):
         return  # injected fault: launch dropped
+    dev = store.device
     if dev.type == "cuda":
-        C.pipeline(args, torch.cuda.current_stream(dev).cuda_stream)
-    elif dev.type == "cpu":
-        C.pipeline_host(args)
+        store._c.run_template(args, torch.cuda.current_stream(dev).cuda_stream)
     else:
-        raise ValueError(f"unsupported device {dev}")
+        store._c.run_template(args, 0)
     if _faults.active():
-        _faults.after_launch("pipeline", tensors)
+        _faults.after_launch("pipeline", tensors or {})

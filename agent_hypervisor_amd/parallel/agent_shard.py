@@ -27,7 +27,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from agent_hypervisor_amd.models.tables import SessionTable
+from agent_hypervisor_amd.models.engine import EngineSessions as SessionTable
 
 
 def _world_rank() -> tuple[int, int]:

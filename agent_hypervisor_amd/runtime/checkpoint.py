@@ -167,94 +167,104 @@ def _publish(tmp: str, d: str) -> str:
 
 
 def save_engine(engine, d: str) -> str:
-    """Write an engine checkpoint into directory ``d`` (created)."""
+    """Write an engine checkpoint into directory ``d``: its store's columns over the
+    ring's rows (columnar, safetensors), the ring's arena region (the exact hashed
+    record bytes), the two interners' strings in id order and the engine counters."""
     from safetensors.torch import save_file
-
-    from agent_hypervisor_amd.models.tables import SessionTable
 
     final, d = d, _staging_dir(d)
     engine.synchronize()
-    tensors = {f"sessions.{k}": getattr(engine.sessions, k).detach().cpu().contiguous() for k in SessionTable.COLUMNS}
+    st = engine.store
+    cap, dmax = engine.sessions.capacity, engine.dmax
+    ext = {"S": cap, "S4": 4 * cap, "S8": 8 * cap, "SP": cap * st.caps["P"], "G": cap, "T": cap,
+           "D": cap * dmax, "D8": 8 * cap * dmax}
+    from agent_hypervisor_amd._native import C
+
+    tensors = {f"store.{name}": st.tables[name][: ext[kind]].detach().cpu().contiguous()
+               for name, _, kind in C.STORE_COLUMNS if kind in ext}
+    tensors["engine.status"] = engine._status.cpu().contiguous()
     n = engine.agents.count
-    tensors["agents.sigma"] = engine.agents.sigma[:n].cpu().contiguous()
-    tensors["agents.did"] = engine.agents.did[:n].cpu().contiguous()
-    v = engine.vouches
-    if v.allocated:
-        tensors["vouches.count"] = v.count.cpu().contiguous()
-        for f in v.COLUMNS:
-            tensors[f"vouches.{f}"] = getattr(v, f).cpu().contiguous()
+    for k in ("sigma", "did", "store_id"):
+        tensors[f"agents.{k}"] = getattr(engine.agents, k)[:n].cpu().contiguous()
     save_file(tensors, os.path.join(d, "tables.safetensors"), metadata={"format": FORMAT, "version": str(VERSION)})
+    end = engine._off_base + cap * dmax * engine._rec_bytes if engine._rec_bytes else 0
+    with open(os.path.join(d, "arena.bin"), "wb") as f:
+        f.write(st.payload(0, end) if end else b"")
     with open(os.path.join(d, "interner.json"), "w") as f:
-        json.dump([engine.interner.str(i) for i in range(len(engine.interner))], f)
+        json.dump({"pool": [st.pool.str(i) for i in range(len(st.pool))],
+                   "agents": [st.agents.str(i) for i in range(len(st.agents))]}, f)
     meta = {
-        "session_capacity": engine.sessions.capacity,
-        "dmax": engine.sessions.dmax,
-        "agent_capacity": engine.agents.capacity,
-        "agent_count": n,
-        "vouch_stride": v.stride,
-        "vouch_slab": v.allocated,
-        "gc_retention_us": engine.gc_retention_us,
-        "seed": engine.seed,
-        "creator_id": engine.creator_id,
-        "next_slot": engine._next_slot,
-        "id_counter": engine._id_counter,
-        "last_specs": engine._last_specs,
+        "session_capacity": cap, "dmax": dmax, "participant_rows": st.caps["P"],
+        "agent_capacity": engine.agents.capacity, "agent_count": n, "max_did": engine.agents.max_did,
+        "gc_retention_us": engine.gc_retention_us, "seed": engine.seed, "creator_id": engine.creator_id,
+        "next_slot": engine._next_slot, "id_counter": engine._id_counter, "last_specs": engine._last_specs,
+        "rec_bytes": engine._rec_bytes, "off_base": engine._off_base, "arena_bytes": end,
+        "sessions_run": engine.sessions_run,
     }
     with open(os.path.join(d, "engine.json"), "w") as f:
         json.dump(meta, f, indent=2)
-    _write_manifest(d, "engine", ["tables.safetensors", "interner.json", "engine.json"])
+    _write_manifest(d, "engine", ["tables.safetensors", "arena.bin", "interner.json", "engine.json"])
     _publish(d, final)
     return final
 
 
 def load_engine(d: str, device: Optional[str] = None, verify: bool = True):
-    """Resume a :class:`GovernanceEngine` from ``d``; with ``verify`` the Merkle
-    root of every archived session is recomputed on ``device`` from its stored
-    delta digests (K09) and compared with the stored root."""
+    """Resume a :class:`GovernanceEngine` from ``d``; with ``verify`` every archived
+    session's chain is re-hashed from its arena records (K10) and its Merkle root
+    recomputed from its digests (K09) on ``device``, both compared with the stored
+    values."""
     from safetensors.torch import load_file
 
     from agent_hypervisor_amd.models.engine import GovernanceEngine
 
     d = recover(d)
-    from agent_hypervisor_amd.models.tables import SessionTable
-
     read_manifest(d, "engine")
     with open(os.path.join(d, "engine.json")) as f:
         meta = json.load(f)
     with open(os.path.join(d, "interner.json")) as f:
         strings = json.load(f)
     eng = GovernanceEngine(device=device, session_capacity=meta["session_capacity"],
-                           agent_capacity=meta["agent_capacity"], vouch_stride=meta.get("vouch_stride", 16),
-                           dmax=meta["dmax"], seed=meta["seed"], creator_did=strings[meta["creator_id"]])
-    ids = eng.interner.intern_many(strings)
-    if ids != list(range(len(strings))):
-        raise CheckpointError("interner ids do not reproduce (pool was not empty?)")
+                           agent_capacity=meta["agent_capacity"], dmax=meta["dmax"], seed=meta["seed"],
+                           creator_did=strings["agents"][meta["creator_id"]],
+                           participant_rows=meta["participant_rows"])
+    st = eng.store
+    if st.pool.intern_many(strings["pool"]) != list(range(len(strings["pool"]))) or \
+            st.agents.intern_many(strings["agents"]) != list(range(len(strings["agents"]))):
+        raise CheckpointError("interner ids do not reproduce")
     t = load_file(os.path.join(d, "tables.safetensors"))
-    for k in SessionTable.COLUMNS:
-        getattr(eng.sessions, k).copy_(t[f"sessions.{k}"])
+    for key, v in t.items():
+        grp, name = key.split(".", 1)
+        if grp == "store":
+            st.tables[name][: v.numel()].copy_(v.to(st.device))
     n = meta["agent_count"]
-    eng.agents.sigma[:n].copy_(t["agents.sigma"])
-    eng.agents.did[:n].copy_(t["agents.did"])
-    eng.agents.count = n
-    if meta.get("vouch_slab"):
-        v = eng.vouches
-        v._alloc()
-        v.count.copy_(t["vouches.count"])
-        for f_ in v.COLUMNS:
-            getattr(v, f_).copy_(t[f"vouches.{f_}"])
+    for k in ("sigma", "did", "store_id"):
+        getattr(eng.agents, k)[:n].copy_(t[f"agents.{k}"])
+    eng.agents.count, eng.agents.max_did = n, meta["max_did"]
+    eng._status.copy_(t["engine.status"])
+    end = meta["arena_bytes"]
+    if end:
+        st._c.grow_payload(end)
+        st.caps["B"] = st._c.payload_cap
+        with open(os.path.join(d, "arena.bin"), "rb") as f:
+            st._c.write_payload(0, f.read())
+    eng._rec_bytes, eng._off_base = meta["rec_bytes"], meta["off_base"]
     eng.gc_retention_us = meta.get("gc_retention_us", eng.gc_retention_us)
     eng._next_slot, eng._id_counter = meta["next_slot"], meta["id_counter"]
+    eng.sessions_run = meta.get("sessions_run", 0)
     eng._last_specs = [tuple(x) for x in meta["last_specs"]] if meta["last_specs"] else None
     if verify:
         bad = verify_engine_audit(eng)
         if bad:
-            raise CheckpointError(f"{bad} archived session(s) fail Merkle re-verification")
+            raise CheckpointError(f"{bad} archived session(s) fail audit re-verification (chain or Merkle root)")
     return eng
 
 
 def verify_engine_audit(eng) -> int:
-    """Recompute Merkle roots of archived sessions from their delta digests; returns mismatches."""
+    """Re-verify archived sessions: every chain re-hashed from its arena records
+    (K10, parent links included) and every Merkle root recomputed from the
+    digests (K09).  Returns the number of sessions that fail either check."""
     from agent_hypervisor_amd.ops import audit as A
+    from agent_hypervisor_amd.ops.store_views import verify_store_chains
 
     t = eng.sessions
     rows = torch.nonzero((t.sess_state == 4) & (t.delta_count > 0)).flatten()
@@ -268,7 +278,13 @@ def verify_engine_audit(eng) -> int:
     mask = torch.arange(dmax, device=rows.device)[None, :] < counts[:, None]
     leaves = t.delta_hash[rows][mask].contiguous()
     roots = A.merkle_roots(offs.to(torch.int32), leaves)
-    return int((roots != t.merkle_root[rows]).any(dim=1).sum())
+    bad = (roots != t.merkle_root[rows]).any(dim=1)
+    if eng._rec_bytes:  # chains from the records (engine checkpoints written before round 4 have none)
+        r = rows.cpu().tolist()
+        c = counts.cpu().tolist()
+        _, ok = verify_store_chains(eng.store, [[s * dmax + k for k in range(n)] for s, n in zip(r, c)])
+        bad = bad | (ok.to(bad.device) == 0)
+    return int(bad.sum())
 
 
 # ------------------------------------------------------- hypervisor (scalar)

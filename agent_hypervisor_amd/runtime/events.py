@@ -1,6 +1,6 @@
 """Device event ring buffer.
 
-The batched pipeline kernel appends compact lifecycle records — one 64-bit
+The batched pipeline kernel (``store_template_kernel``) appends compact lifecycle records — one 64-bit
 atomic per wave reserves the wave's slots — into SoA tensors owned here.  The
 host drains them on its own cadence into :class:`HypervisorEventBus` events
 (the same event types the scalar facade publishes), so kernels can emit events
@@ -89,8 +89,8 @@ class DeviceEventRing:
                 w = t.sess_uuid[slot].cpu().tolist()
                 h = "".join(f"{x & 0xFFFFFFFF:08x}" for x in w)
                 sid = sid_cache[slot] = f"session:{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:]}"
-            a = int(snap["agent"][j])
-            did = engine.interner.str(int(engine.agents.did[a])) if a >= 0 else None
+            a = int(snap["agent"][j])  # store agent id (participant rows)
+            did = engine.store.did(a) if a >= 0 else None
             et = EVENT_FROM_CODE[int(snap["type"][j])]
             payload = {"ring": int(snap["aux"][j])} if et.value == "ring.assigned" else {}
             ev = HypervisorEvent(event_type=et, timestamp=_clock.from_us(int(snap["ts_us"][j])), session_id=sid,

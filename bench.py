@@ -9,9 +9,14 @@ reference pipeline (bench_hypervisor.py:217-239) for one session: create → joi
 release, GC, archive).
 
 Each timed step runs that pipeline for ``--sessions`` new sessions per GPU in one
-gfx950 launch (device-resident tables, device-minted ids, synthetic agents with
-random-init σ), then a cross-rank RCCL all-reduce of the step's governance
-counters (collective X04) — weak scaling, sessions sharded data-parallel.
+gfx950 launch over the device store's rows (``store_template_kernel``: session,
+participant, delta rows with their canonical-JSON records in the payload arena,
+saga and step rows — the same rows the per-call API writes, so every session is
+an ordinary store session; rows allocated once and freed in place every step;
+device-minted ids, synthetic agents with random-init σ), then a cross-rank RCCL
+all-reduce of the step's governance counters (collective X04) — weak scaling,
+sessions sharded data-parallel.  (``--graph`` replays the older standalone
+engine-table kernel from a captured hipGraph.)
 
 Cross-session liability propagation runs inside the same timed step, on a side
 stream overlapping the pipeline kernel (``--no-liability`` turns it off): over a
@@ -161,6 +166,9 @@ def main() -> None:
                     help="template: the reference pipeline for every session (headline kernel); hetero: a "
                          "heterogeneous mix (store_pipeline.mixed_specs) through the public batched API's kernels "
                          "over store rows (rows / render / chain + K09 roots, rows freed and rebuilt every step)")
+    ap.add_argument("--participant-rows", type=int, default=16,
+                    help="participant rows per session row of the headline store (SessionConfig.max_participants "
+                         "of the template is 10; a join past the row width is refused)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                     help="cpu runs the host twin of the kernel over gloo (multi-process CPU rehearsal)")
     args = ap.parse_args()
@@ -193,15 +201,37 @@ def main() -> None:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    from agent_hypervisor_amd.models.engine import GovernanceEngine
     from agent_hypervisor_amd.parallel.collectives import allreduce_stats  # noqa: F401 (graph mode)
 
     S = args.sessions
-    eng = GovernanceEngine(
-        device=str(dev), session_capacity=2 * S, agent_capacity=args.agents, seed=0x5EED0000 + rank
-    )
-    eng.register_synthetic_agents(args.agents, seed=1000 + rank, prefix=f"did:mesh:r{rank}-agent-")
     g = torch.Generator(device=dev).manual_seed(77 + rank)
+    tmpl = None
+    eng = None
+    if args.graph:
+        from agent_hypervisor_amd.models.engine import GovernanceEngine
+
+        eng = GovernanceEngine(
+            device=str(dev), session_capacity=2 * S, agent_capacity=args.agents, seed=0x5EED0000 + rank
+        )
+        eng.register_synthetic_agents(args.agents, seed=1000 + rank, prefix=f"did:mesh:r{rank}-agent-")
+    elif args.mix == "template":
+        # The headline step writes the device store's rows (one device state): the
+        # template pipeline kernel over rows allocated once and freed in place every
+        # step — every session is an ordinary store session (session, participant,
+        # delta rows + canonical-JSON records in the payload arena, saga and step rows).
+        from agent_hypervisor_amd.models import store_template as TT
+        from agent_hypervisor_amd.models.store import GovernanceStore
+
+        nd = max(1, S * args.deltas)
+        caps = {"S": S, "G": S, "T": S, "D": nd, "P": args.participant_rows, "E": 1 << 12, "V": 1 << 12, "X": 1 << 22,
+                "B": nd * 384 + (1 << 20)}
+        tstore = GovernanceStore(str(dev), caps=caps, max_caps={k: v for k, v in caps.items() if k not in ("P", "X")})
+        tagents = TT.AgentSet.synthetic(tstore, args.agents, seed=1000 + rank, prefix=f"did:mesh:r{rank}-agent-")
+        tmpl = TT.TemplatePipeline(tstore, S, tagents, deltas=args.deltas, seed=0x5EED0000 + rank)
+        first = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
+        tmpl.launch(first, sync=True)  # first run over the freshly allocated rows (checks them)
+        if not bool((tmpl.tens["status"] == 0).all()):
+            raise SystemExit("template pipeline: rows refused on the first run")
     stats = torch.zeros(6, dtype=torch.int64, device=dev)
 
     # X04 counters: double-buffered so step i's all-reduce (RCCL, on its own
@@ -270,6 +300,10 @@ def main() -> None:
                   "deltas": int(hp.nd), "committed": len(hp.committed), "ok": int((status0 == 0).sum())}
 
     def run_batch(st, agents):
+        if tmpl is not None:
+            tmpl.reset()
+            tmpl.launch(agents, stats=st, sync=False)
+            return
         if hetero is None:
             eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
             return
@@ -400,6 +434,9 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_api and dev.type == "cuda":  # 1-GPU runs (the N>1 scaling runs skip it)
         api = api_section(args, scalar_p50)
 
+    if tmpl is not None:  # the rows the timed steps wrote are ordinary store sessions: spot-check one
+        sync()
+        assert bool((tmpl.tens["status"] == 0).all()), "template pipeline refused sessions"
     if rank == 0:
         total_sessions = S * world * args.steps
         value = total_sessions / elapsed
@@ -446,6 +483,7 @@ def main() -> None:
                 "x02_slash_allgather_bytes_per_rank": x02_bytes if liab is not None else 0,
             },
             "mix": args.mix,
+            "state": "governance_tables (--graph)" if eng is not None else "store rows",
             "hetero": None if hetero is None else {
                 "sessions": S, "deltas": hetero["deltas"], "committed_roots": hetero["committed"],
                 "sessions_all_stages_admitted": hetero["ok"], "spec_pool": 4096,

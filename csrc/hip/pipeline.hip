@@ -1,16 +1,6 @@
-// Batched governance pipeline kernel (gfx950) and its host twin.
-//
-// Geometry: one wave (64 lanes) per workgroup, one session per lane, a
-// 3-block LDS message window per wave (ahv/wave_sink.h: 12.5 KiB for 3
-// blocks → 12 waves per CU, 3 per SIMD).  The SHA rounds are pure VALU
-// (v_alignbit / v_bitop3 / v_add3); a wave alone issues a VALU op every 4
-// cycles against the SIMD's 2, so ≥2 waves per SIMD keep the issue slots busy
-// (measured SHA-256 ceiling: scripts/exp/sha_sol.hip).  A launch of n sessions is
-// ⌈n/64⌉ workgroups: the 256 CUs are saturated from ~200k sessions per batch.
-// There is no inter-workgroup data reuse, so no XCD remapping is needed.
-//
-// Batch counters (collective X04 input) are reduced across the wave with DPP
-// shuffles and added with one 64-bit atomic per counter per wave.
+// Support kernels of the batched pipeline (csrc/hip/store_template.hip): the
+// device time base and cursor of hipGraph-captured steps (N07/N09) and the fold
+// of spread batch counters (X04 input).
 #include <cstdlib>
 
 #include "ahv/launch.h"
@@ -18,76 +8,6 @@
 #include "ahv/wave_sink.h"
 
 namespace ahv {
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWaveLanes);
-  return v;
-}
-
-// (64 threads, ≥MinWaves waves per SIMD).  The LDS window caps residency (8.4 KiB
-// for 2 blocks → 4 waves per SIMD; 12.5 KiB for 3 blocks → 3), so MinWaves
-// matches it: the VGPR budget is 128 or 168 registers.  Both shapes are
-// instantiated; AHV_PIPE_WIN=2|3 selects one for A/B runs.
-template <int MinWaves, int WinBlocks>
-__global__ __launch_bounds__(kWaveLanes, MinWaves) void governance_pipeline_kernel(PipelineArgs a) {
-  const uint32_t lane = threadIdx.x;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
-  PipeCounters c{};
-  if (i < a.n) {
-    WordWindowSink<WinBlocks> sink;
-    sink.g_win = win_lds<WinBlocks>();
-    sink.lane = lane;
-    c = pipeline_session(a, i, sink);
-  }
-  if (a.stats) {
-#pragma unroll
-    for (int k = 0; k < kPipeStats; ++k) {
-      const uint32_t s = wave_sum(c.v[k]);
-      if (lane == 0 && s)
-        atomicAdd(a.stats + (blockIdx.x % kStatSpread) * kPipeStats + k, static_cast<unsigned long long>(s));
-    }
-  }
-  if (a.ev.cursor) {
-    // one 64-bit atomic reserves the whole wave's records; lanes write at their
-    // exclusive prefix offset
-    const uint32_t nev = i < a.n ? pipeline_event_count(a, i, c) : 0u;
-    uint32_t incl = nev;
-#pragma unroll
-    for (int off = 1; off < kWaveLanes; off <<= 1) {
-      const uint32_t y = __shfl_up(incl, off, kWaveLanes);
-      if (lane >= static_cast<uint32_t>(off)) incl += y;
-    }
-    const uint32_t total = __shfl(incl, kWaveLanes - 1, kWaveLanes);
-    const int seg = static_cast<int>(blockIdx.x % kStatSpread);
-    unsigned long long base = 0;
-    if (lane == 0 && total) base = atomicAdd(a.ev.cursor + seg, static_cast<unsigned long long>(total));
-    base = __shfl(base, 0, kWaveLanes);
-    if (i < a.n) {
-      const unsigned long long first = base + (incl - nev);
-      pipeline_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
-        event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
-      });
-    }
-  }
-}
-
-static int pipeline_window() {
-  static const int w = [] {
-    const char* e = std::getenv("AHV_PIPE_WIN");
-    return e && std::atoi(e) == 2 ? 2 : 3;
-  }();
-  return w;
-}
-
-void launch_pipeline(const PipelineArgs& a, hipStream_t stream) {
-  if (a.n <= 0) return;
-  const int64_t blocks = (a.n + kWaveLanes - 1) / kWaveLanes;
-  const dim3 grid(static_cast<uint32_t>(blocks)), block(kWaveLanes);
-  if (pipeline_window() == 2) hipLaunchKernelGGL((governance_pipeline_kernel<4, 2>), grid, block, 0, stream, a);
-  else hipLaunchKernelGGL((governance_pipeline_kernel<3, 3>), grid, block, 0, stream, a);
-  check_hip(hipGetLastError(), "governance_pipeline_kernel launch");
-}
 
 // ---------------------------------------------------------- cursor kernels
 // wall_clock64() is the constant-rate counter (hipDeviceAttributeWallClockRate);
@@ -165,29 +85,6 @@ int64_t device_wall_clock_rate_khz(int device) {
   int rate = 0;
   check_hip(hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, device), "wall clock rate");
   return rate;
-}
-
-void pipeline_host(const PipelineArgs& a) {
-  HostSink sink;
-  for (int64_t i = 0; i < a.n; ++i) {
-    const PipeCounters c = pipeline_session(a, i, sink);
-    if (a.stats)
-      for (int k = 0; k < kPipeStats; ++k) a.stats[k] += c.v[k];
-    if (a.ev.cursor) {
-      const int seg = static_cast<int>((i / kWaveLanes) % kStatSpread);  // the device's workgroup mapping
-      const unsigned long long first = a.ev.cursor[seg];
-      a.ev.cursor[seg] += pipeline_event_count(a, i, c);
-      pipeline_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
-        event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
-      });
-    }
-  }
-}
-
-
-void kernels_pipeline(std::vector<KernelEntry>& out) {
-  out.push_back({"governance_pipeline_kernel<3,3>", reinterpret_cast<const void*>(&governance_pipeline_kernel<3, 3>)});
-  out.push_back({"governance_pipeline_kernel<4,2>", reinterpret_cast<const void*>(&governance_pipeline_kernel<4, 2>)});
 }
 
 }  // namespace ahv

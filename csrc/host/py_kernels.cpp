@@ -31,79 +31,6 @@ static T val(const py::dict& d, const char* k) {
   return d[k].cast<T>();
 }
 
-static PipelineArgs pipeline_args(const py::dict& d) {
-  PipelineArgs a{};
-  a.n = val<int64_t>(d, "n");
-  a.slot_base = val<int64_t>(d, "slot_base");
-  a.capacity = val<int64_t>(d, "capacity");
-  a.deltas = val<int32_t>(d, "deltas");
-  a.nch = val<int32_t>(d, "nch");
-  a.dmax = val<int32_t>(d, "dmax");
-  a.max_participants = val<int32_t>(d, "max_participants");
-  a.min_sigma_eff = val<double>(d, "min_sigma_eff");
-  a.now_us = val<int64_t>(d, "now_us");
-  a.seed = val<uint64_t>(d, "seed");
-  a.id_base = val<uint64_t>(d, "id_base");
-  a.creator_id = val<int32_t>(d, "creator_id");
-  a.audit = val<int32_t>(d, "audit");
-  if (a.deltas < 0 || a.deltas > kMaxDeltasPipeline) throw py::value_error("deltas out of range");
-  if (a.nch < 1 || a.nch > kMaxChanges) throw py::value_error("nch out of range");
-  if (a.dmax < a.deltas) throw py::value_error("dmax < deltas");
-  if (a.max_participants > kMaxParticipants) throw py::value_error("max_participants > 16");
-  if (a.capacity <= 0 || a.n > a.capacity) throw py::value_error("batch larger than table capacity");
-  a.session_agent = ptr<const int32_t>(d, "session_agent");
-  a.agent_sigma = ptr<const double>(d, "agent_sigma");
-  a.agent_did = ptr<const int32_t>(d, "agent_did");
-  a.changes = ptr<const ChangeIds>(d, "changes");
-  a.vouch_count = ptr<int32_t>(d, "vouch_count");
-  a.vouch_stride = d.contains("vouch_stride") ? val<int32_t>(d, "vouch_stride") : 0;
-  a.vouch_active = ptr<uint8_t>(d, "vouch_active");
-  a.vouch_released_us = ptr<int64_t>(d, "vouch_released_us");
-  a.gc_retention_us = d.contains("gc_retention_us") ? val<int64_t>(d, "gc_retention_us") : (int64_t(90) * 86400 * 1000000);
-  if (a.vouch_count && (a.vouch_stride <= 0 || !a.vouch_active || !a.vouch_released_us))
-    throw py::value_error("vouch slab needs stride, active and released_us");
-  a.pool.bytes = ptr<const uint8_t>(d, "pool_bytes");
-  a.pool.off = ptr<const int64_t>(d, "pool_off");
-  a.pool.len = ptr<const int32_t>(d, "pool_len");
-  a.stats = ptr<unsigned long long>(d, "stats");
-  a.cursor = d.contains("cursor") ? ptr<const int64_t>(d, "cursor") : nullptr;
-  if (d.contains("ev_cursor") && !d["ev_cursor"].is_none()) {
-    a.ev.type = ptr<uint8_t>(d, "ev_type");
-    a.ev.slot = ptr<int32_t>(d, "ev_slot");
-    a.ev.agent = ptr<int32_t>(d, "ev_agent");
-    a.ev.ts_us = ptr<int64_t>(d, "ev_ts_us");
-    a.ev.aux = ptr<int32_t>(d, "ev_aux");
-    a.ev.cursor = ptr<unsigned long long>(d, "ev_cursor");
-    a.ev.capacity = val<int64_t>(d, "ev_capacity");
-  }
-  SessionTables& t = a.t;
-  t.sess_uuid = ptr<uint32_t>(d, "sess_uuid");
-  t.sess_state = ptr<uint8_t>(d, "sess_state");
-  t.sess_mode = ptr<uint8_t>(d, "sess_mode");
-  t.sess_creator = ptr<int32_t>(d, "sess_creator");
-  t.sess_created_us = ptr<int64_t>(d, "sess_created_us");
-  t.sess_terminated_us = ptr<int64_t>(d, "sess_terminated_us");
-  t.part_count = ptr<int32_t>(d, "part_count");
-  t.part_agent = ptr<int32_t>(d, "part_agent");
-  t.part_ring = ptr<uint8_t>(d, "part_ring");
-  t.part_sigma_raw = ptr<double>(d, "part_sigma_raw");
-  t.part_sigma_eff = ptr<double>(d, "part_sigma_eff");
-  t.part_joined_us = ptr<int64_t>(d, "part_joined_us");
-  t.delta_hash = ptr<uint32_t>(d, "delta_hash");
-  t.delta_count = ptr<int32_t>(d, "delta_count");
-  t.merkle_root = ptr<uint32_t>(d, "merkle_root");
-  t.saga_uuid = ptr<uint32_t>(d, "saga_uuid");
-  t.step_uuid = ptr<uint32_t>(d, "step_uuid");
-  t.saga_state = ptr<uint8_t>(d, "saga_state");
-  t.step_state = ptr<uint8_t>(d, "step_state");
-  t.step_started_us = ptr<int64_t>(d, "step_started_us");
-  t.step_completed_us = ptr<int64_t>(d, "step_completed_us");
-  t.committed_at_us = ptr<int64_t>(d, "committed_at_us");
-  t.gc_retained = ptr<int32_t>(d, "gc_retained");
-  t.bonds_released = ptr<int32_t>(d, "bonds_released");
-  t.status = ptr<int32_t>(d, "status");
-  return a;
-}
 
 // ---------------------------------------------------------------------------
 // Generic binding: every kernel gets `<name>(args: dict, stream: int)` (device)
@@ -383,23 +310,6 @@ void register_kernels(py::module_& m) {
       },
       py::arg("args"), py::arg("phase"), py::arg("k"));
   m.def(
-      "pipeline",
-      [](const py::dict& d, uintptr_t stream) {
-        PipelineArgs a = pipeline_args(d);
-        py::gil_scoped_release nogil;
-        launch_pipeline(a, reinterpret_cast<hipStream_t>(stream));
-      },
-      py::arg("args"), py::arg("stream"),
-      "Launch the batched governance pipeline kernel on `stream`.");
-  m.def(
-      "pipeline_host",
-      [](const py::dict& d) {
-        PipelineArgs a = pipeline_args(d);
-        py::gil_scoped_release nogil;
-        pipeline_host(a);
-      },
-      py::arg("args"), "Run the same per-session pipeline body on the CPU (host twin).");
-  m.def(
       "spread_fold",
       [](uintptr_t spread, uintptr_t out, int k, bool accumulate, uintptr_t stream) {
         launch_spread_fold(reinterpret_cast<unsigned long long*>(spread), reinterpret_cast<unsigned long long*>(out), k,
@@ -425,8 +335,8 @@ void register_kernels(py::module_& m) {
       "kernel_attributes",
       []() {
         std::vector<KernelEntry> ks;
-        kernels_pipeline(ks);
         kernels_audit(ks);
+        kernels_store_template(ks);
         kernels_liability(ks);
         kernels_saga(ks);
         kernels_merkle_tree(ks);

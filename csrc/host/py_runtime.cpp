@@ -143,6 +143,28 @@ static py::str uuid_str(uint64_t seed, uint64_t counter, const std::string& pref
   return py::str(s);
 }
 
+// uuid_from_counter for n consecutive counters (the session ids a template batch
+// minted on the device, formatted on demand for lazy registration).
+static py::list uuids_from_counters(uint64_t seed, uint64_t base, int64_t n, const std::string& prefix) {
+  if (n < 0) throw py::value_error("n must be >= 0");
+  py::list out(n);
+  const size_t pl = prefix.size();
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t u[4];
+    uuid4_words(seed, base + static_cast<uint64_t>(i), u);
+    PyObject* s = PyUnicode_New(static_cast<Py_ssize_t>(pl + 36), 127);
+    if (!s) throw py::error_already_set();
+    char* o = reinterpret_cast<char*>(PyUnicode_1BYTE_DATA(s));
+    std::memcpy(o, prefix.data(), pl);
+    o += pl;
+    for (int k = 0, j = 0; k < 32; ++k) {
+      if (k == 8 || k == 12 || k == 16 || k == 20) o[j++] = '-';
+      o[j++] = static_cast<char>(hex_nibble((u[k >> 3] >> (28 - 4 * (k & 7))) & 15u));
+    }
+    PyList_SET_ITEM(out.ptr(), static_cast<Py_ssize_t>(i), s);
+  }
+  return out;
+}
 
 // ------------------------------------------------------------------ spec packing
 // Hypervisor.run_pipelines with one PipelineSpec per session: flatten the specs
@@ -407,6 +429,8 @@ void register_runtime(py::module_& m) {
   m.def("pack_specs", &pack_specs, py::arg("specs"), py::arg("agents"), py::arg("pool"), py::arg("cfg_of"),
         py::arg("fixed"), "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py)");
   m.def("iso_from_us", &iso_from_us, "datetime.isoformat() text of an epoch-µs UTC instant");
+  m.def("uuids_from_counters", &uuids_from_counters, py::arg("seed"), py::arg("base"), py::arg("n"),
+        py::arg("prefix") = std::string(), "uuid_from_counter(seed, base + i, prefix) for i < n");
   m.def("uuid_from_counter", &uuid_str, py::arg("seed"), py::arg("counter"), py::arg("prefix") = std::string(),
         "uuid4 string minted by the device id generator for (seed, counter)");
 }

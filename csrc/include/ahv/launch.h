@@ -15,10 +15,6 @@ inline void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-struct PipelineArgs;
-void launch_pipeline(const PipelineArgs& a, hipStream_t stream);
-void pipeline_host(const PipelineArgs& a);
-
 // Fold [kStatSpread, k] spread counters into out[k] and re-zero them (one wave).
 void launch_spread_fold(unsigned long long* spread, unsigned long long* out, int k, bool accumulate, hipStream_t s);
 
@@ -36,10 +32,10 @@ struct KernelEntry {
   const char* name;
   const void* fn;
 };
-void kernels_pipeline(std::vector<KernelEntry>& out);
 void kernels_audit(std::vector<KernelEntry>& out);
 void kernels_liability(std::vector<KernelEntry>& out);
 void kernels_saga(std::vector<KernelEntry>& out);
 void kernels_merkle_tree(std::vector<KernelEntry>& out);
+void kernels_store_template(std::vector<KernelEntry>& out);
 
 }  // namespace ahv

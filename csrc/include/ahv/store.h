@@ -498,16 +498,17 @@ AHV_HD void splice_parent(const Lanes& L, uint8_t* src, uint32_t* w, int64_t hol
     }
     const uint64_t b = static_cast<uint64_t>(hole) + k;
     src[b] = static_cast<uint8_t>(ch);
-    uint8_t* lb = reinterpret_cast<uint8_t*>(w);
-    lb[(b & ~uint64_t(3)) | (3 - (b & 3))] = static_cast<uint8_t>(ch);
+    if (w) reinterpret_cast<uint8_t*>(w)[(b & ~uint64_t(3)) | (3 - (b & 3))] = static_cast<uint8_t>(ch);
   }
   L.sync();
 }
 
-// stage_words + splice_parent into L.lds (the whole window).
+// stage_words + splice_parent into L.lds (the whole window).  A record larger
+// than the window (-1) is hashed from the arena, so the parent is spliced there
+// only — before the caller's sha256_fine reads it.
 AHV_HD int64_t stage_message(const Lanes& L, uint8_t* src, uint64_t n, int64_t hole, const uint32_t* head) {
   const int64_t nblk = stage_words(L, src, n, L.lds, kLdsWords);
-  if (nblk >= 0 && hole >= 0) splice_parent(L, src, L.lds, hole, head);
+  if (hole >= 0) splice_parent(L, src, nblk >= 0 ? L.lds : nullptr, hole, head);
   return nblk;
 }
 
@@ -906,6 +907,7 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       return;
     }
     default:
+      out64(r + 1, ST_BAD_OP);  // an unassigned code in the session range
       break;
   }
 }
@@ -1372,6 +1374,7 @@ AHV_HD void exec_vouch(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
       return;
     }
     default:
+      out64(r + 1, ST_BAD_OP);
       break;
   }
 }
@@ -1541,6 +1544,10 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
     case OP_STEP_TRANSITION: {
       // a0 step, a1 to-state, a2 now, a3 retry count (≥0 sets retry_count first)
       const int64_t st = static_cast<int64_t>(c.a[0]);
+      if (st < 0 || st >= t.cap.T) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
       const uint8_t to = static_cast<uint8_t>(c.a[1]);
       const uint8_t from = t.t_state[st];
       if (static_cast<int64_t>(c.a[3]) >= 0) t.t_retry[st] = static_cast<int32_t>(c.a[3]);
@@ -1558,6 +1565,10 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
     case OP_STEP_SET: {
       // direct write outside the FSM (reference orchestrator.py:124/134 retry reset, :167 no-undo)
       const int64_t st = static_cast<int64_t>(c.a[0]);
+      if (st < 0 || st >= t.cap.T) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
       t.t_state[st] = static_cast<uint8_t>(c.a[1]);
       if (static_cast<int64_t>(c.a[2]) >= 0) t.t_retry[st] = static_cast<int32_t>(c.a[2]);
       out64(r + 1, ST_OK);
@@ -1565,6 +1576,10 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
     }
     case OP_SAGA_TRANSITION: {
       const int64_t g = static_cast<int64_t>(c.a[0]);
+      if (g < 0 || g >= t.cap.G) {
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
       const uint8_t to = static_cast<uint8_t>(c.a[1]);
       const uint8_t from = t.g_state[g];
       out64(r + 2, from);
@@ -1598,6 +1613,12 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       const uint64_t n = c.a[1];
       const IndexList idx = index_list(t, c, n, c.a[2]);
       uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[3]);
+      bool bad = g < 0 || g >= t.cap.G;
+      for (uint64_t k = 0; k < n && !bad; ++k) bad = idx[k] < 0 || idx[k] >= t.cap.T;
+      if (bad) {  // row indices come from API objects: validated like every other row argument
+        out64(r + 1, ST_BAD_ARG);
+        return;
+      }
       out64(r + 2, t.g_state[g]);
       out64(r + 3, static_cast<uint64_t>(t.g_created[g]));
       out64(r + 4, static_cast<uint64_t>(t.g_completed[g]));
@@ -1623,6 +1644,7 @@ AHV_HD void exec_saga(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       return;
     }
     default:
+      out64(r + 1, ST_BAD_OP);
       break;
   }
 }
@@ -1846,6 +1868,12 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
       const IndexList idx = index_list(t, c, n, c.a[1]);
       uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[2]);
       for (uint64_t k = 0; k < n; ++k) {
+        if (idx[k] < 0 || idx[k] >= t.cap.D) {
+          out64(r + 1, ST_BAD_ARG);
+          return;
+        }
+      }
+      for (uint64_t k = 0; k < n; ++k) {
         const int32_t d = idx[k];
         out64(b + 12 * k + 0, static_cast<uint64_t>(static_cast<int64_t>(t.d_turn[d])));
         out64(b + 12 * k + 1, static_cast<uint64_t>(static_cast<int64_t>(t.d_prev[d])));
@@ -1857,6 +1885,7 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
       return;
     }
     default:
+      if (L.leader()) out64(r + 1, ST_BAD_OP);
       break;
   }
 }

@@ -140,26 +140,25 @@ async def demo_integrations() -> None:
 
 
 async def demo_engine() -> None:
-    banner("6. MI355X batch engine: the full pipeline for many sessions in one launch")
+    banner("6. MI355X batched pipeline: the full pipeline for many sessions in one launch")
     import torch
 
-    from agent_hypervisor_amd.models.engine import GovernanceEngine
+    from hypervisor import Hypervisor
 
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     n = 65536 if dev == "cuda" else 2048
-    eng = GovernanceEngine(device=dev, session_capacity=n, agent_capacity=n)
-    eng.register_synthetic_agents(n, seed=1)
-    stats = torch.zeros(6, dtype=torch.int64, device=dev)
+    hv = Hypervisor(device=dev)
+    hv.pipeline_batch(64)  # warm-up (agent registration, kernel load)
     import time
 
     t0 = time.perf_counter()
-    batch = eng.run_pipeline(n, stats=stats)
-    eng.synchronize()
+    run = hv.pipeline_batch(n)
     dt = time.perf_counter() - t0
-    say(f"{n} sessions on {dev} in {dt * 1e3:.2f} ms; counters {stats.tolist()}")
-    m = batch.materialize(0)
-    say(f"session 0 {batch.session_id(0)} root {batch.merkle_root_hex(0)[:16]}… host re-verify "
-        f"chain={m.delta_engine.verify_chain()} root-match={m.delta_engine.compute_merkle_root() == batch.merkle_root_hex(0)}")
+    say(f"{n} sessions on {dev} in {dt * 1e3:.2f} ms ({run.ok} completed), written as ordinary store sessions")
+    sid = run.session_ids[0]
+    m = hv.get_session(sid)
+    say(f"session {sid} root {run.roots[sid][:16]}… via the API: state={m.sso.state.value} "
+        f"chain={m.delta_engine.verify_chain()} root-match={m.delta_engine.compute_merkle_root() == run.roots[sid]}")
 
 
 DEMOS = {

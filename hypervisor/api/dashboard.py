@@ -83,16 +83,9 @@ def summary(st, limit: int = 200) -> dict[str, Any]:
     ring_events = [e.to_dict() for e in bus.query(limit=limit) if e.event_type.value.startswith("ring.")][::-1]
     events = [e.to_dict() for e in bus.query(limit=limit)][::-1]
     engine = None
-    if hv._device_engine is not None:
-        eng = hv._device_engine
-        t = eng.sessions
-        engine = {
-            "device": str(eng.device),
-            "session_capacity": t.capacity,
-            "agents": eng.agents.count,
-            "archived_rows": int((t.sess_state == 4).sum().item()),
-            "table_bytes": t.nbytes() if hasattr(t, "nbytes") else None,
-        }
+    if getattr(hv, "batched_sessions", 0):  # sessions written by batched device launches (store rows)
+        engine = {"device": str(hv._store.device), "batched_sessions": hv.batched_sessions,
+                  "live_rows": hv._store.live_rows()}
     store = getattr(hv, "_store", None)
     return {
         "overview": {

@@ -121,7 +121,7 @@ async def get_stats(request: Request) -> StatsResponse:
         active_sagas=sum(1 for g in sagas if g["state"] in ("running", "compensating")),
         total_vouches=len(hv.vouching.records()),
         event_count=st.bus.event_count,
-        batched_sessions=hv._device_engine.sessions_run if hv._device_engine is not None else 0,
+        batched_sessions=hv.batched_sessions,
     )
 
 
@@ -373,27 +373,20 @@ async def verify_audit(
 async def run_pipeline_batch(req: PipelineBatchRequest, request: Request) -> PipelineBatchResponse:
     hv = _state(request).hv
     try:
-        eng = hv.device_engine
-        if eng.agents.count == 0:
-            eng.register_synthetic_agents(max(req.sessions, 1024), seed=req.seed)
-        if req.sessions > eng.sessions.capacity:
-            raise ValueError(f"batch of {req.sessions} exceeds session capacity {eng.sessions.capacity}")
         t0 = time.perf_counter()
-        batch = eng.run_pipeline(req.sessions, deltas=req.deltas)
-        status = batch.status()
-        eng.synchronize()
+        run = hv.pipeline_batch(req.sessions, deltas=req.deltas)
         dt = time.perf_counter() - t0
     except Exception as e:  # noqa: BLE001
         raise HTTPException(status_code=400, detail=str(e)) from e
-    ok = int((status == 0).sum().item())
+    sid = run.session_ids[0] if req.sessions > 0 else None
     return PipelineBatchResponse(
         sessions=req.sessions,
-        completed=ok,
-        device=str(eng.device),
+        completed=run.ok,
+        device=str(hv._store.device),
         elapsed_ms=dt * 1e3,
         sessions_per_second=req.sessions / dt if dt > 0 else 0.0,
-        sample_merkle_root=batch.merkle_root_hex(0) if req.deltas > 0 else None,
-        sample_session_id=batch.session_id(0) if req.sessions > 0 else None,
+        sample_merkle_root=run.roots.get(sid) if sid is not None else None,
+        sample_session_id=sid,
     )
 
 

@@ -27,8 +27,9 @@ reference the participant's own σ/ring are left unchanged unless
 
 Additions: an optional ``event_bus`` that receives lifecycle events (the
 reference never emitted, Q03); an optional ``declared_history`` for join (Q23);
-and :meth:`Hypervisor.pipeline_batch`, which runs the same governance pipeline
-for thousands of sessions at once on the MI355X device engine.
+and :meth:`Hypervisor.pipeline_batch` / :meth:`Hypervisor.run_pipelines`, which
+run the pipeline for thousands of sessions in one device launch over the same
+store rows the per-call API uses (one device state).
 
 Device-authoritative mode (``Hypervisor(device="cuda")``, the default when a HIP
 device is visible; ``AHV_STORE``): sessions, participants, the audit chain,
@@ -154,8 +155,7 @@ class Hypervisor:
         self.event_bus = event_bus
         self.demote_on_slash = demote_on_slash
         self._sessions = SessionTable()
-        self._device_engine = None
-        self._batch_views: dict = {}  # session id → (batch, host view), a small LRU
+        self.batched_sessions = 0  # sessions written by pipeline_batch / run_pipelines (ordinary sessions)
 
     # -- events --------------------------------------------------------------
     def _emit(self, etype, session_id=None, agent_did=None, **payload) -> None:
@@ -337,26 +337,7 @@ class Hypervisor:
         return store_pipeline.run(self, specs, n)
 
     def get_session(self, session_id: str) -> Optional[ManagedSession]:
-        m = self._sessions.get(session_id)
-        if m is None and self._device_engine is not None:
-            m = self._batch_session(session_id)
-        return m
-
-    def _batch_session(self, session_id: str) -> Optional[ManagedSession]:
-        """Host view of a session the batched device pipeline ran (read back
-        from the resident session table on demand; a small LRU of views)."""
-        hit = self._device_engine.lookup(session_id)  # the row may have been reused since
-        if hit is None:
-            self._batch_views.pop(session_id, None)
-            return None
-        batch, i = hit
-        views = self._batch_views
-        cached = views.pop(session_id, None)
-        m = cached[1] if cached is not None and cached[0] is batch else batch.materialize(i)
-        views[session_id] = (batch, m)
-        while len(views) > 1024:
-            views.pop(next(iter(views)))
-        return m
+        return self._sessions.get(session_id)
 
     # -- behaviour verification --------------------------------------------------
     async def verify_behavior(
@@ -536,24 +517,16 @@ class Hypervisor:
             raise ValueError(f"Session {session_id} not found")
         return m
 
-    # -- MI355X batched engine --------------------------------------------------------
-    @property
-    def device_engine(self):
-        """Lazily-created :class:`agent_hypervisor_amd.models.GovernanceEngine`."""
-        if self._device_engine is None:
-            from agent_hypervisor_amd.models.engine import GovernanceEngine
-
-            self._device_engine = GovernanceEngine()
-        return self._device_engine
-
+    # -- MI355X batched pipeline ------------------------------------------------------
     def pipeline_batch(self, n_sessions: int, **kwargs):
-        """Run the full governance pipeline for ``n_sessions`` sessions on device.
+        """Run the reference pipeline for ``n_sessions`` new sessions in one device
+        launch, written into this hypervisor's store (one device state: they are
+        ordinary sessions afterwards — ``get_session``, terminate, ``verify_audit``,
+        checkpoints).  See :func:`agent_hypervisor_amd.models.store_template.run`
+        (``agents``, ``session_agent``, ``deltas``, ``changes``, ``now_us``,
+        ``config``); returns a :class:`~agent_hypervisor_amd.models.store_pipeline.PipelineRun`."""
+        from agent_hypervisor_amd.models import store_template
 
-        See :meth:`agent_hypervisor_amd.models.engine.GovernanceEngine.run_pipeline`.
-        With no agents registered yet, a synthetic population (random-init σ) the
-        size of the batch is registered first.
-        """
-        eng = self.device_engine
-        if eng.agents.count == 0:
-            eng.register_synthetic_agents(min(max(n_sessions, 1), eng.agents.capacity))
-        return eng.run_pipeline(n_sessions, **kwargs)
+        run = store_template.run(self, n_sessions, **kwargs)
+        self.batched_sessions += n_sessions
+        return run

@@ -138,39 +138,47 @@ def test_events_are_recorded_and_filterable(client):
     assert stats["total_events"] == len(ev) and stats["by_type"]["session.created"] == 1
 
 
-def test_pipeline_batch_endpoint_cpu(client, monkeypatch):
-    from agent_hypervisor_amd.models.engine import GovernanceEngine
-
-    hv = client.app.state.hv.hv
-    hv._device_engine = GovernanceEngine(device="cpu", session_capacity=4096, agent_capacity=4096)
-    r = client.post("/api/v1/engine/pipeline", json={"sessions": 256, "deltas": 3})
-    assert r.status_code == 200, r.text
-    body = r.json()
-    assert body["completed"] == 256 and body["device"] == "cpu" and len(body["sample_merkle_root"]) == 64
-    # batched sessions are first-class: readable by id through the API and the façade
-    sid = body["sample_session_id"]
-    d = client.get(f"/api/v1/sessions/{sid}")
-    assert d.status_code == 200, d.text
-    assert d.json()["state"] == "archived" and d.json()["participant_count"] == 1
-    m = hv.get_session(sid)
-    assert m.delta_engine.verify_chain() and m.delta_engine.compute_merkle_root() == body["sample_merkle_root"]
-    assert client.get("/api/v1/stats").json()["batched_sessions"] == 256
-    assert client.get("/api/v1/sessions/session:00000000-0000-4000-8000-000000000000").status_code == 404
-
-
-def test_batch_lookup_survives_ring_reuse():
-    from agent_hypervisor_amd.models.engine import GovernanceEngine
+def test_pipeline_batch_endpoint_cpu():
+    """The batched pipeline endpoint writes the hypervisor's own store rows: the
+    sessions are ordinary sessions, readable by id through the API and the façade."""
     from hypervisor import Hypervisor
 
-    hv = Hypervisor()
-    hv._device_engine = GovernanceEngine(device="cpu", session_capacity=64, agent_capacity=64, seed=3)
+    hv = Hypervisor(device="cpu")
+    with TestClient(create_app(hv)) as client:
+        r = client.post("/api/v1/engine/pipeline", json={"sessions": 256, "deltas": 3})
+        assert r.status_code == 200, r.text
+        body = r.json()
+        assert body["completed"] == 256 and body["device"] == "cpu" and len(body["sample_merkle_root"]) == 64
+        sid = body["sample_session_id"]
+        d = client.get(f"/api/v1/sessions/{sid}")
+        assert d.status_code == 200, d.text
+        assert d.json()["state"] == "archived" and d.json()["participant_count"] == 1
+        m = hv.get_session(sid)
+        assert m.delta_engine.verify_chain() and m.delta_engine.compute_merkle_root() == body["sample_merkle_root"]
+        assert client.get("/api/v1/stats").json()["batched_sessions"] == 256
+        assert client.get("/api/v1/sessions/session:00000000-0000-4000-8000-000000000000").status_code == 404
+        # later calls see the same rows: terminating an archived batch session is the reference's error
+        assert client.post(f"/api/v1/sessions/{sid}/terminate").status_code == 400
+
+
+def test_pipeline_batch_endpoint_on_host_engines_is_refused():
+    from hypervisor import Hypervisor
+
+    with TestClient(create_app(Hypervisor(device="host"))) as client:
+        r = client.post("/api/v1/engine/pipeline", json={"sessions": 4, "deltas": 3})
+        assert r.status_code == 400 and "device-backed" in r.json()["detail"]
+
+
+def test_batches_stay_addressable():
+    from hypervisor import Hypervisor
+
+    hv = Hypervisor(device="cpu")
     b1 = hv.pipeline_batch(40, now_us=1767225600000000)
-    first, last = b1.session_id(0), b1.session_id(39)
-    b2 = hv.pipeline_batch(40, now_us=1767225601000000)  # wraps: overwrites b1's first 16 rows
-    assert hv.get_session(first) is None
-    m = hv.get_session(last)
-    assert m is not None and m.delta_engine.compute_merkle_root() == b1.merkle_root_hex(39)
-    assert hv.get_session(b2.session_id(39)).sso.session_id == b2.session_id(39)
+    b2 = hv.pipeline_batch(40, now_us=1767225601000000)  # store rows: nothing is overwritten
+    for b in (b1, b2):
+        for sid in (b.session_ids[0], b.session_ids[39]):
+            m = hv.get_session(sid)
+            assert m is not None and m.delta_engine.compute_merkle_root() == b.roots[sid]
     assert hv.get_session("not-a-session") is None
 
 

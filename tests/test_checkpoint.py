@@ -123,7 +123,7 @@ def test_engine_round_trip_and_resume(tmp_path):
     b = eng.run_pipeline(100, deltas=3)
     d = save_engine(eng, str(tmp_path / "eng"))
     eng2 = load_engine(d, device="cpu")
-    assert eng2.interner.str(eng2.creator_id) == "did:mesh:admin" and eng2.agents.count == 300
+    assert eng2.store.did(eng2.creator_id) == "did:mesh:admin" and eng2.agents.count == 300
     for k in ("merkle_root", "delta_hash", "sess_uuid", "part_sigma_eff"):
         assert torch.equal(getattr(eng.sessions, k), getattr(eng2.sessions, k))
     # continuing on the restored engine produces exactly what the original would
@@ -144,10 +144,28 @@ def test_engine_tamper_detected_by_merkle_reverify(tmp_path):
     d = save_engine(eng, str(tmp_path / "eng"))
     p = os.path.join(d, "tables.safetensors")
     t = load_file(p)
-    t["sessions.delta_hash"][5, 1, 0] ^= 1
+    t["store.d_hash"][(5 * eng.dmax + 1) * 8] ^= 1  # delta 1 of session row 5
     save_file(t, p)
-    ck._write_manifest(d, "engine", ["tables.safetensors", "interner.json", "engine.json"])
-    with pytest.raises(CheckpointError, match="Merkle"):
+    ck._write_manifest(d, "engine", ["tables.safetensors", "arena.bin", "interner.json", "engine.json"])
+    with pytest.raises(CheckpointError, match="re-verification"):
+        load_engine(d, device="cpu")
+
+
+def test_engine_record_tamper_detected_by_chain_reverify(tmp_path):
+    """A record edited in the checkpoint's arena no longer hashes to its digest (K10)."""
+    from agent_hypervisor_amd.runtime import checkpoint as ck
+
+    eng = GovernanceEngine(device="cpu", session_capacity=32, agent_capacity=32, seed=4)
+    eng.register_synthetic_agents(8)
+    eng.run_pipeline(16, deltas=3)
+    d = save_engine(eng, str(tmp_path / "eng"))
+    p = os.path.join(d, "arena.bin")
+    raw = bytearray(open(p, "rb").read())
+    off = eng._off_base + (3 * eng.dmax + 2) * eng._rec_bytes  # session row 3, delta 2
+    raw[off + 20] ^= 0x01
+    open(p, "wb").write(bytes(raw))
+    ck._write_manifest(d, "engine", ["tables.safetensors", "arena.bin", "interner.json", "engine.json"])
+    with pytest.raises(CheckpointError, match="re-verification"):
         load_engine(d, device="cpu")
 
 

@@ -57,7 +57,7 @@ def test_corrupted_pipeline_root_fails_checkpoint_verification(tmp_path):
         eng.run_pipeline(64)
     assert f.hits == 1
     d = save_engine(eng, str(tmp_path / "e"))
-    with pytest.raises(CheckpointError, match="Merkle"):
+    with pytest.raises(CheckpointError, match="re-verification"):
         load_engine(d, device="cpu")
 
 
