@@ -34,11 +34,12 @@ Also reported (not the headline value):
   gfx950 store worker (hypervisor/_device.py, csrc/hip/store_worker.hip);
 * ``scalar_p50_us`` — the same harness on the pure host engines (CPU only);
 * ``batch_p50_ms`` — p50 wall time of one synchronised pipeline step;
-* ``api_ops_per_s`` / ``api`` — public-API throughput after the timed region
-  (rank 0, 1 GPU runs): the batched API ``Hypervisor.run_pipelines`` over 10⁵
-  reference pipelines (10 API operations each) written into the device store,
-  a randomized-spec batch, and 10⁴ concurrent per-call pipelines under
-  ``asyncio.gather`` on the device and on the host engines (``--no-api`` skips).
+* ``api`` — public-API throughput after the timed region (rank 0, 1 GPU runs),
+  in reference pipelines per second: the batched API ``Hypervisor.run_pipelines``
+  over 10⁵ pipelines written into the device store (wall clock incl. host-side
+  registration), a randomized-spec batch, and 10⁴ concurrent per-call pipelines
+  under ``asyncio.gather`` on the device and on the host engines (``--no-api``
+  skips).
 
 ``vs_baseline`` divides the batched GPU throughput by the reference's
 single-threaded Python pipeline rate — a capability ratio, not a like-for-like
@@ -104,9 +105,6 @@ def scalar_pipeline_p50(iters: int = 2000, device: str = "host") -> tuple[float,
     return statistics.median(times) / 1000.0, statistics.mean(times) / 1000.0
 
 
-API_OPS_PER_PIPELINE = 10  # create, join, activate, 3 captures, saga create, add_step, execute, terminate
-
-
 def api_section(args, scalar_p50) -> dict:
     """Public-API throughput on this GPU (outside the timed step; rank 0).
 
@@ -118,7 +116,7 @@ def api_section(args, scalar_p50) -> dict:
     * ``gather``: ``--api-concurrent`` per-call pipelines under one asyncio.gather
       through ``Hypervisor(device="cuda")`` (reference bench_hypervisor.py:217-239),
       and the same harness on the host engines.
-    ``api_ops_per_s`` = batch pipelines/s × 10 API operations per pipeline."""
+    All rates are whole reference pipelines per second."""
     from benchmarks.bench_api import api_throughput, batch_api_throughput
 
     b = batch_api_throughput("cuda", args.api_sessions, 3)
@@ -128,8 +126,6 @@ def api_section(args, scalar_p50) -> dict:
     host_scalar = 1e6 / scalar_p50 if scalar_p50 else None
     rate = b["sessions_per_s"]
     return {
-        "api_ops_per_s": round(rate * API_OPS_PER_PIPELINE, 1),
-        "ops_per_pipeline": API_OPS_PER_PIPELINE,
         "batch_pipelines_per_s": rate, "batch_sessions": args.api_sessions, "batch_ok": b["ok"],
         "batch_device_ms": b["device_ms"],
         "batch_hetero_sessions_per_s": bh["sessions_per_s"], "batch_hetero_sessions": bh["sessions"],
@@ -152,7 +148,7 @@ def main() -> None:
     ap.add_argument("--deltas", type=int, default=3)
     ap.add_argument("--scalar-iters", type=int, default=2000)
     ap.add_argument("--no-scalar", action="store_true")
-    ap.add_argument("--no-api", action="store_true", help="skip the public-API throughput section (api_ops_per_s)")
+    ap.add_argument("--no-api", action="store_true", help="skip the public-API throughput section")
     ap.add_argument("--api-sessions", type=int, default=100_000, help="sessions per batched API call")
     ap.add_argument("--api-concurrent", type=int, default=10_000, help="concurrent per-call pipelines (gather)")
     ap.add_argument("--graph", action="store_true",
@@ -471,7 +467,8 @@ def main() -> None:
             "scalar_p50_us": round(scalar_p50, 2) if scalar_p50 is not None else None,
             "scalar_mean_us": round(scalar_mean, 2) if scalar_mean is not None else None,
             "scalar_vs_baseline_p50": round(BASELINE_P50_US / scalar_p50, 2) if scalar_p50 else None,
-            "api_ops_per_s": api["api_ops_per_s"] if api else None,
+            "api_batch_pipelines_per_s": api["batch_pipelines_per_s"] if api else None,
+            "api_gather_pipelines_per_s": api["gather_pipelines_per_s"] if api else None,
             "api": api,
             "last_step_counters": dict(zip(["sessions", "ok", "participants", "deltas", "commits", "archived"], totals)),
             "step_latency_hist_log2_us": {str(1 << b): c for b, c in enumerate(hist) if c},

@@ -243,3 +243,35 @@ def test_reference_oracle_through_cpu_twin_store():
            "-p", "no:cacheprovider", "-c", os.devnull, "--rootdir", "/tmp"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd="/tmp")
     assert p.returncode == 0 and "326 passed" in p.stdout, p.stdout[-3000:]
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_records_larger_than_the_hash_window_chain_correctly(dev):
+    """A record past the worker's 16 KiB LDS window is hashed from the arena: the
+    parent digest must be spliced there first (found by the store program fuzz in
+    csrc/tests/host_selftest.cpp)."""
+    import hashlib
+
+    async def go():
+        hv = Hypervisor(device=dev)
+        s = await hv.create_session(config=SessionConfig(enable_audit=True), creator_did="did:mesh:admin")
+        sid = s.sso.session_id
+        await hv.join_session(sid, "did:mesh:a", sigma_raw=0.8)
+        await hv.activate_session(sid)
+        sizes = [10, 20000, 40, 17000]
+        ds = [s.delta_engine.capture("did:mesh:a", [VFSChange(path=f"/f{i}", operation="add",
+                                                              content_hash="x" * n)])
+              for i, n in enumerate(sizes)]
+        parent = None
+        for d in ds:
+            raw = d.record()
+            assert len(raw) > 16384 or d.delta_hash
+            assert d.parent_hash == parent
+            assert d.delta_hash == hashlib.sha256(raw).hexdigest()
+            parent = d.delta_hash
+        assert s.delta_engine.verify_chain()
+        assert hv.verify_audit([sid]).ok
+        root = await hv.terminate_session(sid)
+        assert root == C.merkle_root([d.delta_hash for d in ds])
+
+    asyncio.run(go())
