@@ -44,6 +44,9 @@ _DTYPES = {
     "double": torch.float64,
 }
 
+_NP_OF = {torch.uint8: np.dtype(np.uint8), torch.int32: np.dtype(np.int32), torch.int64: np.dtype(np.int64),
+          torch.float64: np.dtype(np.float64)}
+
 ST_OK, ST_BAD_STATE, ST_NOT_FOUND, ST_BAD_ARG, ST_SCRATCH = 0, 1, 2, 90, 91
 
 _u64 = struct.Struct("<Q")
@@ -560,6 +563,29 @@ class GovernanceStore:
                 vals = [v - (1 << 32) if v >= 1 << 31 else v for v in vals]
             t[torch.tensor(idx, dtype=torch.int64, device=self.device)] = torch.tensor(vals, dtype=t.dtype).to(
                 self.device)
+        if cuda:
+            torch.cuda.synchronize(self.device)
+            self.acquire()
+
+    def write_columns(self, cols: dict) -> None:
+        """Vectorized :meth:`write_rows`: ``{column: (int64 element indices, values)}``
+        with numpy / torch arrays (one ``index_copy_`` per column; indices must be
+        distinct).  Checkpoint restore writes whole tables this way."""
+        self.drain()
+        cuda = self.device.type == "cuda"
+        if cuda:
+            self.flush()
+        for col, (idx, vals) in cols.items():
+            if len(idx) == 0:
+                continue
+            t = self.tables[col]
+            ix = torch.as_tensor(np.ascontiguousarray(idx, dtype=np.int64)).to(self.device)
+            want = _NP_OF[t.dtype]
+            a = np.ascontiguousarray(vals)
+            if a.dtype != want:  # same-width integers are bit patterns (uint32 words); else convert
+                same = a.dtype.itemsize == want.itemsize and a.dtype.kind in "iu" and want.kind in "iu"
+                a = a.view(want) if same else a.astype(want)
+            t.index_copy_(0, ix, torch.from_numpy(a).to(self.device))
         if cuda:
             torch.cuda.synchronize(self.device)
             self.acquire()

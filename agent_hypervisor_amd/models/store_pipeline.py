@@ -108,19 +108,35 @@ class _Batch:
 
     __slots__ = ("store", "specs", "shared", "ids", "slots", "t0", "doff", "drows", "dlen", "dhash",
                  "delta_off", "gslots", "step_off", "tslots", "status", "built", "released", "dead",
-                 "index", "views", "committed", "_saga_ids", "_step_ids", "__weakref__")
+                 "index", "views", "committed", "_saga_ids", "_step_ids", "id_seed", "gid_base", "tid_base",
+                 "__weakref__")
+
+    def reserve_saga_ids(self) -> None:
+        """Give the batch's saga / step ids fixed counters of the store's id
+        generator: ids are formatted only when first needed (uuid4 words of
+        (seed, counter)), and a checkpoint that saves the counters restores the
+        same ids whether or not they were formatted before."""
+        st = self.store
+        self.id_seed = st.seed
+        self.gid_base = st.reserve_ids(len(self.gslots))
+        self.tid_base = st.reserve_ids(int(self.step_off[-1]))
 
     def saga_ids(self) -> tuple:
-        """(saga id per session or None, step id per step row): minted once, in
+        """(saga id per session or None, step id per step row): formatted once, in
         bulk, the first time a view or a summary needs them."""
         if self._saga_ids is None:
             has = self.gslots >= 0
-            ng = int(has.sum())
-            sg, _ = C.uuid4_many(ng, "saga:") if ng else ([], b"")
-            it = iter(sg)
-            self._saga_ids = [next(it) if h else None for h in has.tolist()]
             nt = int(self.step_off[-1])
-            self._step_ids = C.uuid4_many(nt, "step:")[0] if nt else []
+            if getattr(self, "id_seed", None) is not None:
+                allg = C.uuids_from_counters(self.id_seed, self.gid_base, len(self.gslots), "saga:")
+                self._saga_ids = [g if h else None for g, h in zip(allg, has.tolist())]
+                self._step_ids = C.uuids_from_counters(self.id_seed, self.tid_base, nt, "step:") if nt else []
+            else:
+                ng = int(has.sum())
+                sg, _ = C.uuid4_many(ng, "saga:") if ng else ([], b"")
+                it = iter(sg)
+                self._saga_ids = [next(it) if h else None for h in has.tolist()]
+                self._step_ids = C.uuid4_many(nt, "step:")[0] if nt else []
         return self._saga_ids, self._step_ids
 
     def saga_summaries(self, rows: dict, idx) -> list:
@@ -598,6 +614,7 @@ def finish(hv, p: "Prepared") -> PipelineRun:
     b.delta_off, b.gslots, b.step_off, b.tslots = delta_off, gslots, step_off, tslots
     b.status, b.built, b.released, b.dead = status_np, np.zeros(n, dtype=bool), np.zeros(n, dtype=bool), []
     b._saga_ids = b._step_ids = None
+    b.reserve_saga_ids()
     register_lazy(hv, b, status_np, cidx)
     run_ = PipelineRun(session_ids=ids, status=status_np,
                        join_rings=tens["join_ring"].cpu().numpy()[: len(j_agent)],

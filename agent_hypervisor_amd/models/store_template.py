@@ -294,6 +294,7 @@ def run(hv, n: int, agents: Optional[AgentSet] = None, session_agent=None, delta
     b.step_off = np.arange(n + 1, dtype=np.int32)
     b.status, b.built, b.released, b.dead = status, np.zeros(n, dtype=bool), np.zeros(n, dtype=bool), []
     b._saga_ids = b._step_ids = None
+    b.reserve_saga_ids()
     SP.register_lazy(hv, b, status, committed)
     out = SP.PipelineRun(session_ids=ids, status=status, join_rings=np.zeros(0, np.uint8),
                          join_codes=np.zeros(0, np.uint8))

@@ -5,13 +5,23 @@ recovery that does not exist).  Two checkpoint kinds share one layout — a
 directory with a versioned ``manifest.json`` listing every file with its
 SHA-256:
 
-engine checkpoint (device tables of a :class:`GovernanceEngine`)
-    ``tables.safetensors``  every SoA column (sessions, agents, vouch edges),
-                            columnar, loaded with a loader that executes nothing
-    ``interner.json``       the string pool in id order (ids are positions)
-    ``engine.json``         counters, seed, capacities, change specs
+engine checkpoint (the private store of a :class:`GovernanceEngine`)
+    ``tables.safetensors``  the store columns over the engine's ring rows and
+                            the agent table, loaded with a loader that executes
+                            nothing
+    ``arena.bin``           the ring's region of the payload arena (the exact
+                            hashed record bytes)
+    ``interner.json``       the string pool and agent DIDs in id order
+    ``engine.json``         counters, seed, capacities, ring geometry
 
-hypervisor checkpoint (the scalar :class:`hypervisor.Hypervisor` state)
+hypervisor checkpoint of a device-backed :class:`hypervisor.Hypervisor`
+    (``layout: columnar``, version 2): the store's live rows column by column,
+    the payload-arena records and the few host-side fields — see
+    :mod:`agent_hypervisor_amd.runtime.store_checkpoint`.  Saved with no store
+    command per session, restored with bulk row writes, lazily built views and
+    a multi-threaded K10/K09 re-verification.
+
+hypervisor checkpoint (host engines, ``device="host"``)
     ``sessions.jsonl``      one record per session: config, lifecycle, VFS
                             files/ACLs, reversibility entries, sagas (full step
                             state), and the audit log as *canonical-JSON delta
@@ -36,7 +46,7 @@ from typing import Any, Optional
 import torch
 
 FORMAT = "ahv-checkpoint"
-VERSION = 1
+VERSION = 2  # 2: columnar device-hypervisor layout
 
 
 class CheckpointError(Exception):
@@ -54,12 +64,16 @@ def _sha(path: str) -> str:
     return h.hexdigest()
 
 
-def _write_manifest(d: str, kind: str, files: list[str], extra: Optional[dict] = None) -> None:
+def _write_manifest(d: str, kind: str, files: list[str], extra: Optional[dict] = None,
+                    digests: Optional[dict] = None) -> None:
+    """``digests``: precomputed entries — ``"k10"`` marks a file of audit records
+    whose every byte the loader re-verifies against manifest-protected digests."""
+    digests = digests or {}
     man = {
         "format": FORMAT,
         "version": VERSION,
         "kind": kind,
-        "files": {f: _sha(os.path.join(d, f)) for f in files},
+        "files": {f: digests[f] if f in digests else _sha(os.path.join(d, f)) for f in files},
         **(extra or {}),
     }
     tmp = os.path.join(d, "manifest.json.tmp")
@@ -84,6 +98,8 @@ def read_manifest(d: str, kind: str) -> dict:
         fp = os.path.join(d, f)
         if not os.path.exists(fp):
             raise CheckpointError(f"{d}: missing {f}")
+        if digest == "k10":  # verified record by record by the loader (store_checkpoint.load_store)
+            continue
         if _sha(fp) != digest:
             raise CheckpointError(f"{d}: {f} is corrupt (sha256 mismatch)")
     return man
@@ -354,12 +370,19 @@ def save_hypervisor(hv, d: str, extra_files: Optional[dict] = None) -> str:
     sharded façade keeps its routing metadata there)."""
     final, d = d, _staging_dir(d)
     extra = dict(extra_files or {})
+    from agent_hypervisor_amd.runtime import store_checkpoint as SC
+
     for name, text in extra.items():
         if os.path.basename(name) != name or name in ("sessions.jsonl", "liability.json", "commitments.json",
-                                                       "manifest.json"):
+                                                       "manifest.json", *SC.FILES):
             raise ValueError(f"invalid extra checkpoint file name {name!r}")
         with open(os.path.join(d, name), "w") as f:
             f.write(text)
+    if getattr(hv, "_store", None) is not None and os.environ.get("AHV_CHECKPOINT_LAYOUT", SC.LAYOUT) == SC.LAYOUT:
+        man = SC.save_store(hv, d)  # columnar: no store command per session
+        _write_manifest(d, "hypervisor", [*SC.FILES, *sorted(extra)], man, {"arena.bin": "k10"})
+        _publish(d, final)
+        return final
     with open(os.path.join(d, "sessions.jsonl"), "w") as f:
         for m in hv.sessions:
             f.write(json.dumps(_session_record(m), sort_keys=True) + "\n")
@@ -433,7 +456,11 @@ def checkpoint_session_keys(d: str) -> list[str]:
     """Every session id a hypervisor checkpoint holds state for: its sessions and
     the liability-only session ids of its vouch records (failover re-homes both)."""
     d = recover(d)
-    read_manifest(d, "hypervisor")
+    man = read_manifest(d, "hypervisor")
+    if man.get("layout") == "columnar":
+        from agent_hypervisor_amd.runtime import store_checkpoint as SC
+
+        return SC.session_keys(d)
     keys = []
     with open(os.path.join(d, "sessions.jsonl")) as f:
         for line in f:
@@ -470,15 +497,28 @@ def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
     from hypervisor.saga.state_machine import Saga, SagaState, SagaStep, StepState
     from hypervisor.session import SharedSessionObject
 
-    read_manifest(d, "hypervisor")
+    man = read_manifest(d, "hypervisor")
     hv = hv or Hypervisor()
-    with open(os.path.join(d, "sessions.jsonl")) as f:
-        records = [json.loads(line) for line in f if line.strip()]
     only = set(sessions) if sessions is not None else None
-    if only is not None:
-        records = [r for r in records if r["session_id"] in only]
-    if getattr(hv, "_store", None) is not None:
-        return _load_device(hv, d, records, verify, only)
+    vouches = commits = None
+    if man.get("layout") == "columnar":
+        from agent_hypervisor_amd.runtime import store_checkpoint as SC
+
+        if getattr(hv, "_store", None) is not None:
+            return SC.load_store(hv, d, verify, only)
+        records, vouches, commits = SC.to_records(d, only)  # into the host engines
+    else:
+        with open(os.path.join(d, "sessions.jsonl")) as f:
+            records = [json.loads(line) for line in f if line.strip()]
+        if only is not None:
+            records = [r for r in records if r["session_id"] in only]
+        if getattr(hv, "_store", None) is not None:
+            return _load_device(hv, d, records, verify, only)
+    if vouches is None:
+        with open(os.path.join(d, "liability.json")) as f:
+            vouches = json.load(f)
+        with open(os.path.join(d, "commitments.json")) as f:
+            commits = json.load(f)
     restored: list = []
     for r in records:
         cfg = dict(r["config"])
@@ -516,25 +556,23 @@ def load_hypervisor(d: str, hv=None, verify: bool = True, sessions=None):
         m.delta_engine._turn_counter = r["turn_count"]
         hv._sessions[sso.session_id] = m
         restored.append(m)
-    with open(os.path.join(d, "liability.json")) as f:
-        for v in json.load(f):
-            if only is not None and v["session_id"] not in only:
-                continue
-            rec = VouchRecord(vouch_id=v["vouch_id"], voucher_did=v["voucher_did"], vouchee_did=v["vouchee_did"],
-                              session_id=v["session_id"], bonded_sigma_pct=v["bonded_sigma_pct"],
-                              bonded_amount=v["bonded_amount"], created_at=_dt(v["created_at"]),
-                              expiry=_dt(v["expiry"]), is_active=v["is_active"], released_at=_dt(v["released_at"]))
-            hv.vouching._vouches[rec.vouch_id] = rec
-            hv.vouching._by_session.setdefault(rec.session_id, []).append(rec)
-    with open(os.path.join(d, "commitments.json")) as f:
-        for c in json.load(f):
-            if only is not None and c["session_id"] not in only:
-                continue
-            rec = CommitmentRecord(session_id=c["session_id"], merkle_root=c["merkle_root"],
-                                   participant_dids=c["participant_dids"], delta_count=c["delta_count"],
-                                   committed_at=_dt(c["committed_at"]), blockchain_tx_id=c["blockchain_tx_id"],
-                                   committed_to=c["committed_to"])
-            hv.commitment._commitments[rec.session_id] = rec
+    for v in vouches:
+        if only is not None and v["session_id"] not in only:
+            continue
+        rec = VouchRecord(vouch_id=v["vouch_id"], voucher_did=v["voucher_did"], vouchee_did=v["vouchee_did"],
+                          session_id=v["session_id"], bonded_sigma_pct=v["bonded_sigma_pct"],
+                          bonded_amount=v["bonded_amount"], created_at=_dt(v["created_at"]),
+                          expiry=_dt(v["expiry"]), is_active=v["is_active"], released_at=_dt(v["released_at"]))
+        hv.vouching._vouches[rec.vouch_id] = rec
+        hv.vouching._by_session.setdefault(rec.session_id, []).append(rec)
+    for c in commits:
+        if only is not None and c["session_id"] not in only:
+            continue
+        rec = CommitmentRecord(session_id=c["session_id"], merkle_root=c["merkle_root"],
+                               participant_dids=c["participant_dids"], delta_count=c["delta_count"],
+                               committed_at=_dt(c["committed_at"]), blockchain_tx_id=c["blockchain_tx_id"],
+                               committed_to=c["committed_to"])
+        hv.commitment._commitments[rec.session_id] = rec
     if verify:
         _verify_restored(restored, {sid: c.merkle_root for sid, c in hv.commitment._commitments.items()})
     return hv

@@ -12,11 +12,13 @@
 // path and the batched gfx950 kernels hash with the same code.
 #include <Python.h>
 #include <datetime.h>
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ahv/canon_json.h"
@@ -518,7 +520,103 @@ static py::object hex_id(const std::string& prefix, int nchars) {
   return py::reinterpret_steal<py::object>(s);
 }
 
+// verify_chain_records(blob, rec_off, rec_len, hole, digest, sess_off, root, commit_n, threads)
+//   -> (bad_chain bytes[N], bad_root bytes[N])
+// K10 + K09 over audit records held in host memory (checkpoint restore, before
+// they are written back): session i owns records [sess_off[i], sess_off[i+1]) in
+// chain order.  A chain is good when every record hashes to its digest and
+// record k > 0 quotes record k-1's digest at its parent hole (record 0: no hole);
+// a committed session (commit_n > 0) needs root == the Merkle root of its first
+// commit_n digests.  Sessions are split over `threads` host threads (SHA-NI).
+static py::tuple verify_chain_records(py::buffer blob, py::array_t<int64_t, py::array::c_style | py::array::forcecast> off,
+                                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> len,
+                                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> hole,
+                                      py::array_t<uint32_t, py::array::c_style | py::array::forcecast> dig,
+                                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> soff,
+                                      py::array_t<uint32_t, py::array::c_style | py::array::forcecast> root,
+                                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> commit_n,
+                                      int threads) {
+  const py::buffer_info bi = blob.request();
+  const uint8_t* b = static_cast<const uint8_t*>(bi.ptr);
+  const int64_t bn = static_cast<int64_t>(bi.size * bi.itemsize);
+  const int64_t nrec = off.size();
+  const int64_t ns = soff.size() - 1;
+  if (len.size() != nrec || hole.size() != nrec || dig.size() != 8 * nrec || ns < 0 || root.size() != 8 * ns ||
+      commit_n.size() != ns)
+    throw py::value_error("verify_chain_records: inconsistent array sizes");
+  const int64_t* po = off.data();
+  const int64_t* pl = len.data();
+  const int32_t* ph = hole.data();
+  const uint32_t* pd = dig.data();
+  const int64_t* so = soff.data();
+  const uint32_t* pr = root.data();
+  const int32_t* pc = commit_n.data();
+  if (ns > 0 && (so[0] < 0 || so[ns] > nrec)) throw py::value_error("verify_chain_records: session offsets out of range");
+  for (int64_t i = 0; i < ns; ++i)
+    if (so[i + 1] < so[i]) throw py::value_error("verify_chain_records: session offsets decrease");
+  std::string bad_chain(static_cast<size_t>(ns), '\0'), bad_root(static_cast<size_t>(ns), '\0');
+  auto work = [&](int64_t s0, int64_t s1) {
+    std::vector<uint32_t> level;
+    for (int64_t s = s0; s < s1; ++s) {
+      bool ok = true;
+      for (int64_t r = so[s]; r < so[s + 1] && ok; ++r) {
+        const int64_t k = r - so[s];
+        if (po[r] < 0 || pl[r] < 0 || po[r] + pl[r] > bn) { ok = false; break; }
+        const uint8_t* rec = b + po[r];
+        uint32_t h[8];
+        sha256_bytes(rec, static_cast<size_t>(pl[r]), h);
+        ok = std::memcmp(h, pd + 8 * r, 32) == 0;
+        if (!ok) break;
+        if (k == 0) {
+          ok = ph[r] < 0;
+        } else {
+          const int64_t at = ph[r];
+          if (at < 0 || at + 66 > pl[r]) { ok = false; break; }
+          uint8_t q[64];
+          hex_bytes(pd + 8 * (r - 1), q);
+          ok = rec[at] == '"' && rec[at + 65] == '"' && std::memcmp(rec + at + 1, q, 64) == 0;
+        }
+      }
+      bad_chain[static_cast<size_t>(s)] = ok ? 0 : 1;
+      const int64_t m0 = pc[s];
+      if (m0 > 0) {
+        if (m0 > so[s + 1] - so[s]) { bad_root[static_cast<size_t>(s)] = 1; continue; }
+        level.assign(pd + 8 * so[s], pd + 8 * (so[s] + m0));
+        size_t m = static_cast<size_t>(m0);
+        while (m > 1) {
+          const size_t half = (m + 1) / 2;
+          for (size_t i = 0; i < half; ++i) {
+            const uint32_t* l = &level[16 * i];
+            const uint32_t* rr = (2 * i + 1 < m) ? &level[16 * i + 8] : l;
+            uint32_t o[8];
+            merkle_node_host(l, rr, o);
+            std::memcpy(&level[8 * i], o, sizeof o);
+          }
+          m = half;
+        }
+        bad_root[static_cast<size_t>(s)] = std::memcmp(level.data(), pr + 8 * s, 32) == 0 ? 0 : 1;
+      }
+    }
+  };
+  {
+    py::gil_scoped_release nogil;
+    const int nt = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(threads, (ns + 1023) / 1024)));
+    std::vector<std::thread> pool;
+    const int64_t per = (ns + nt - 1) / std::max(nt, 1);
+    for (int t = 1; t < nt; ++t) {
+      const int64_t a = std::min(ns, t * per), z = std::min(ns, (t + 1) * per);
+      if (a < z) pool.emplace_back(work, a, z);
+    }
+    work(0, std::min(ns, per));
+    for (auto& th : pool) th.join();
+  }
+  return py::make_tuple(py::bytes(bad_chain), py::bytes(bad_root));
+}
+
 void register_audit(py::module_& m) {
+  m.def("verify_chain_records", &verify_chain_records, py::arg("blob"), py::arg("rec_off"), py::arg("rec_len"),
+        py::arg("hole"), py::arg("digest"), py::arg("sess_off"), py::arg("root"), py::arg("commit_n"),
+        py::arg("threads") = 8, "K10 chains + K09 roots over host-held audit records (checkpoint restore)");
   m.def("delta_payload", &delta_payload, "Canonical JSON payload bytes of a SemanticDelta");
   m.def("delta_hash", &delta_hash, "SHA-256 hex of the canonical SemanticDelta payload");
   m.def("merkle_root", &merkle_root, "Merkle root over hex leaf hashes (reference semantics)");

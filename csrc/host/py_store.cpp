@@ -103,11 +103,28 @@ class Store : public StoreCore {
     write_payload_raw(off, v.data(), v.size());
   }
 
-  void write_records(I64Array offs, I64Array lens, const py::bytes& blob) {
+  void write_records(I64Array offs, I64Array lens, py::buffer blob) {
     if (lens.size() != offs.size()) throw std::invalid_argument("write_records: offs and lens differ in length");
-    std::string_view v = blob;
+    const py::buffer_info bi = blob.request();
     py::gil_scoped_release nogil;
-    write_records_raw(offs.data(), lens.data(), offs.size(), reinterpret_cast<const uint8_t*>(v.data()), v.size());
+    write_records_raw(offs.data(), lens.data(), offs.size(), static_cast<const uint8_t*>(bi.ptr),
+                      static_cast<size_t>(bi.size * bi.itemsize));
+  }
+
+  // The records at `offs` / `lens`, concatenated (checkpoint save; no store command).
+  py::bytes payload_gather(I64Array offs, I64Array lens) {
+    if (lens.size() != offs.size()) throw std::invalid_argument("payload_gather: offs and lens differ in length");
+    int64_t total = 0;
+    for (py::ssize_t i = 0; i < lens.size(); ++i) total += std::max<int64_t>(lens.data()[i], 0);
+    PyObject* out = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(total));
+    if (!out) throw py::error_already_set();
+    py::bytes res = py::reinterpret_steal<py::bytes>(out);
+    uint8_t* dst = reinterpret_cast<uint8_t*>(PyBytes_AS_STRING(out));
+    {
+      py::gil_scoped_release nogil;
+      gather_records_raw(offs.data(), lens.data(), offs.size(), dst);
+    }
+    return res;
   }
 
   // DeltaEngine.capture: render the canonical payload around a null parent
@@ -215,6 +232,7 @@ void register_store(py::module_& m) {
       .def("payload", &Store::payload)
       .def("write_payload", &Store::write_payload)
       .def("write_records", &Store::write_records)
+      .def("payload_gather", &Store::payload_gather, py::arg("offs"), py::arg("lens"))
       .def("capture", &Store::capture)
       .def("capture_bytes", &Store::capture_bytes)
       .def("restore_delta", &Store::restore_delta)

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -488,6 +489,30 @@ class StoreCore {
       pos += l[i];
     }
     if (gpu_) _mm_sfence();
+  }
+
+  // The records at arena offsets `o` / lengths `l`, concatenated into `dst`
+  // (checkpoint save).  On the GPU the used span is copied to the host once.
+  void gather_records_raw(const int64_t* o, const int64_t* l, int64_t n, uint8_t* dst) const {
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      if (o[i] < 0 || l[i] < 0 || o[i] + l[i] > t_.cap.B) throw std::out_of_range("gather_records: record out of range");
+      lo = std::min(lo, o[i]);
+      hi = std::max(hi, o[i] + l[i]);
+    }
+    if (n == 0 || hi <= lo) return;
+    std::vector<uint8_t> tmp;
+    const uint8_t* base = payload_ + lo;
+    if (gpu_) {
+      tmp.resize(static_cast<size_t>(hi - lo));
+      hip_check(hipMemcpy(tmp.data(), payload_ + lo, tmp.size(), hipMemcpyDeviceToHost), "payload gather");
+      base = tmp.data();
+    }
+    size_t pos = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      std::memcpy(dst + pos, base + (o[i] - lo), static_cast<size_t>(l[i]));
+      pos += static_cast<size_t>(l[i]);
+    }
   }
 
   // Same, for a payload the caller rendered (`at`: offset of the parent's `null`).

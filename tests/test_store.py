@@ -217,7 +217,8 @@ def test_default_mode_is_host_without_gpu():
 
 def _run_suites(store: str, files: list[str]) -> None:
     env = dict(os.environ, AHV_STORE=store, PYTHONDONTWRITEBYTECODE="1")
-    p = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", *files],
+    marks = ["-m", "not gpu"] if store == "cpu" else []
+    p = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", *marks, *files],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
 
