@@ -40,6 +40,62 @@ def exposure_by_agent(store, agent_ids: list[int], edges: list[int], now: int | 
     return out
 
 
+def session_rows(hv) -> tuple:
+    """(session rows int64 [n] in the hypervisor's session order, ``sid_of(i)``) —
+    from the session table's segments, no store command and no view built."""
+    import numpy as np
+
+    parts, getters = [], []
+    for kind, seg in hv._sessions.segments():
+        if kind == "own":
+            parts.append(np.fromiter((m.sso.slot for m in seg), dtype=np.int64, count=len(seg)))
+            getters.append(lambda k, seg=seg: seg[k].sso.session_id)
+        else:
+            idx = np.fromiter(seg.index.values(), dtype=np.int64, count=len(seg.index))
+            parts.append(seg.slots[idx].astype(np.int64))
+            getters.append(lambda k, seg=seg, idx=idx: seg.ids[int(idx[k])])
+    if not parts:
+        return np.zeros(0, dtype=np.int64), lambda i: None
+    bounds = np.cumsum([0] + [len(x) for x in parts])
+
+    def sid_of(i: int):
+        j = int(np.searchsorted(bounds, i, side="right")) - 1
+        return getters[j](i - int(bounds[j]))
+
+    return np.concatenate(parts), sid_of
+
+
+def first_active_ring(store, slots, agent_id: int):
+    """X05 on the device: among the session rows ``slots`` (session order), the
+    earliest-created one (first in order on ties) where store agent ``agent_id``
+    holds an active participant row; returns ``(index into slots, created µs,
+    ring)`` or None.  One pass of gathers over the participant columns."""
+    import numpy as np
+
+    st = store
+    st.drain()
+    if st.device.type == "cuda":
+        st.flush()
+    dev = st.device
+    P = st.caps["P"]
+    rows = torch.from_numpy(np.ascontiguousarray(slots, dtype=np.int64)).to(dev)
+    agent = st.tables["p_agent"].view(-1, P).index_select(0, rows)
+    active = st.tables["p_active"].view(-1, P).index_select(0, rows)
+    pc = st.tables["s_pcount"].index_select(0, rows).to(torch.int64)
+    k = torch.arange(P, device=dev)
+    m = (agent == agent_id) & ((active & 1) != 0) & (k[None, :] < pc[:, None])
+    has = m.any(dim=1)
+    if not bool(has.any()):
+        return None
+    created = st.tables["s_created"].index_select(0, rows)
+    big = torch.iinfo(torch.int64).max
+    key = torch.where(has, created, torch.full_like(created, big))
+    i = int(torch.argmin(key))  # first minimal index: session order breaks ties
+    col = int(torch.argmax(m[i].to(torch.int32)))
+    ring = int(st.tables["p_ring"].view(-1, P)[rows[i], col])
+    return i, int(created[i]), ring
+
+
 def verify_store_chains(store, chains: list[list[int]]) -> tuple[torch.Tensor, torch.Tensor]:
     """K10 over the store's resident audit rows: ``chains`` are lists of delta rows
     (each a session's chain in turn order).  Returns ``(row_ok u8 [Σ], chain_ok u8

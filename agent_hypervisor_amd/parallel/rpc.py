@@ -44,11 +44,12 @@ def _error_classes() -> dict:
     from hypervisor.saga.orchestrator import SagaTimeoutError
     from hypervisor.saga.state_machine import SagaStateError
     from hypervisor.session import SessionLifecycleError, SessionParticipantError
+    from hypervisor.session.sso import VFSPermissionError
 
     return {c.__name__: c for c in (
         ValueError, KeyError, TypeError, LookupError, RuntimeError, TimeoutError, PermissionError,
         FileNotFoundError, VouchingError, SagaStateError, SagaTimeoutError, SessionLifecycleError,
-        SessionParticipantError,
+        SessionParticipantError, VFSPermissionError,
     )}
 
 

@@ -33,7 +33,22 @@ sessions it owns) and serves requests *independently*:
   dense per-agent exposure                 X01: K04 over each rank's store edge
                                            columns → [A] fp64 all-reduce
   ``GET /api/v1/sessions``                 per-rank snapshots, merged by creation
+  ``GET /api/v1/events`` (:328-343)        each rank's event bus, merged by
+                                           (timestamp, rank, sequence)
+  ``GET /api/v1/events/stats`` (:346)      per-type counts summed over ranks
   =======================================  ======================================
+
+  A view never stalls a rank's serving: its local part (batched device reads)
+  runs on the event loop, its blocking collective on a dedicated communication
+  thread (:attr:`ShardedHypervisor._comm`), so forwarded per-session calls keep
+  completing on every rank while a view is in flight.  X05 (agent ring) is one
+  device MIN over the store's participant columns of the rank's sessions (O(1)
+  store commands); the agent-liability view gathers bond state from the edge
+  columns in one read.
+* **The rest of the per-session surface** routes the same way: ring
+  distribution, saga and vouch listings, and the session object's operations —
+  leave, ring updates, consistency mode, VFS write/read/delete/permissions and
+  snapshot/restore (:meth:`ShardedHypervisor.sso`).
 
 Failure handling: heartbeats, one agreed failure verdict (the first
 proposer's list wins), checkpoints per rank, and failover — the dead rank's
@@ -46,6 +61,7 @@ from __future__ import annotations
 import asyncio
 import json
 import os
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import asdict
 from datetime import datetime
 from typing import Any, Callable, Optional
@@ -116,13 +132,59 @@ async def _noop_comp(step):
     return None
 
 
+async def _api_executor():
+    return {"status": "executed_via_api"}  # what the reference REST step execution runs
+
+
 # per-session methods served for other ranks (the RPC whitelist)
 _SERVED = (
     "create_session", "join_session", "activate_session", "terminate_session", "verify_behavior", "get_session",
     "capture", "merkle_root", "vouch", "compute_sigma_eff", "get_total_exposure", "release_session_bonds",
     "slash", "create_saga", "add_step", "execute_step", "compensate", "get_saga",
+    "ring_distribution", "list_sagas", "list_vouches", "sso",
     "_view", "_view_enter", "_stop",
 )
+
+
+def _edit(e) -> Optional[dict]:
+    return None if e is None else {"path": e.path, "operation": e.operation, "agent_did": e.agent_did,
+                                   "timestamp": e.timestamp.isoformat() if e.timestamp else None,
+                                   "content_hash": e.content_hash, "previous_hash": e.previous_hash}
+
+
+def _participant(p) -> dict:
+    return {"agent_did": p.agent_did, "ring": int(p.ring), "sigma_raw": p.sigma_raw, "sigma_eff": p.sigma_eff,
+            "joined_at": p.joined_at.isoformat() if p.joined_at else None, "is_active": p.is_active}
+
+
+def _perms(p) -> Optional[list]:
+    return None if p is None else sorted(p)
+
+
+def _sso_ops() -> dict:
+    from hypervisor.models import ExecutionRing
+
+    # SharedSessionObject operations (reference session/__init__.py:115-175 and its VFS),
+    # run on the owner; arguments and results are JSON values
+    return {
+        "leave": lambda s, did: s.leave(did),
+        "update_ring": lambda s, did, ring: s.update_ring(did, ExecutionRing(ring)),
+        "force_consistency_mode": lambda s, mode: s.force_consistency_mode(ConsistencyMode(mode)),
+        "get_participant": lambda s, did: _participant(s.get_participant(did)),
+        "vfs_write": lambda s, path, content, did: _edit(s.vfs.write(path, content, did)),
+        "vfs_read": lambda s, path, did=None: s.vfs.read(path, did),
+        "vfs_delete": lambda s, path, did: _edit(s.vfs.delete(path, did)),
+        "vfs_list": lambda s: s.vfs.list_files(),
+        "vfs_set_permissions": lambda s, path, agents, did: _edit(s.vfs.set_permissions(path, set(agents), did)),
+        "vfs_get_permissions": lambda s, path: _perms(s.vfs.get_permissions(path)),
+        "vfs_snapshot": lambda s, snapshot_id=None: s.create_vfs_snapshot(snapshot_id),
+        "vfs_restore": lambda s, snapshot_id, did: s.restore_vfs_snapshot(snapshot_id, did),
+        "vfs_list_snapshots": lambda s: s.vfs.list_snapshots(),
+        "vfs_delete_snapshot": lambda s, snapshot_id: s.vfs.delete_snapshot(snapshot_id),
+    }
+
+
+_SSO: dict = {}
 
 
 class ShardedHypervisor:
@@ -138,13 +200,19 @@ class ShardedHypervisor:
         self.rank = 0 if single or not dist.is_initialized() else dist.get_rank()
         self.world = 1 if single or not dist.is_initialized() else dist.get_world_size()
         self.policy = policy
+        if "event_bus" not in hv_kwargs:  # each rank publishes its own sessions' events
+            from hypervisor.observability.event_bus import HypervisorEventBus
+
+            hv_kwargs["event_bus"] = HypervisorEventBus()
         self.local = Hypervisor(device=device, **hv_kwargs)
+        self.bus = self.local.event_bus
+        self._comm: Optional[ThreadPoolExecutor] = None  # the communication thread of the views
         self.members = list(range(self.world))
         self._live = frozenset(self.members)
         self.group = None if self.world == 1 else control_group()
         self.data_group = None  # default group (RCCL on MI355X) until a failover
         self.rpc = None
-        self.executors: dict[str, Callable[..., Any]] = {"noop": _noop}
+        self.executors: dict[str, Callable[..., Any]] = {"noop": _noop, "api": _api_executor}
         self.compensators: dict[str, Callable[..., Any]] = {"noop": _noop_comp}
         self.counters = {"local": 0, "forwarded": 0, "collectives": 0, "views": 0}
         self._rr = 0
@@ -192,6 +260,9 @@ class ShardedHypervisor:
         if self.rpc is not None:
             await self.rpc.close()
             self.rpc = None
+        if self._comm is not None:
+            self._comm.shutdown(wait=True)
+            self._comm = None
 
     async def _handle(self, name: str, args: list, kwargs: dict) -> Any:
         if name == "_stop":
@@ -200,7 +271,7 @@ class ShardedHypervisor:
         if name == "_view":
             return await self._view(*args)
         if name == "_view_enter":
-            return self._collective(*args)
+            return await self._enter(*args)
         return await getattr(self, "_local_" + name)(*args, **kwargs)
 
     # -- placement ---------------------------------------------------------------------
@@ -239,9 +310,11 @@ class ShardedHypervisor:
         return await self.rpc.call(o, name, *args, **kwargs)
 
     # -- lifecycle ---------------------------------------------------------------------
-    async def create_session(self, config: SessionConfig, creator_did: str, rank: Optional[int] = None) -> str:
+    async def create_session(self, config: SessionConfig, creator_did: str, rank: Optional[int] = None,
+                             detail: bool = False):
         """Create a session on ``rank`` (default: this rank with policy ``local``,
-        the next live rank with ``round_robin``); returns its id."""
+        the next live rank with ``round_robin``); returns its id (``detail``: the
+        REST route's CreateSessionResponse fields)."""
         if rank is None:
             if self.policy == "local":
                 rank = self.rank
@@ -249,11 +322,15 @@ class ShardedHypervisor:
                 rank = self.members[self._rr % len(self.members)]
                 self._rr += 1
         sid = self._mint("session:", rank)
-        return await self._route(sid, "create_session", _cfg_out(config), creator_did, sid)
+        return await self._route(sid, "create_session", _cfg_out(config), creator_did, sid, detail)
 
-    async def _local_create_session(self, cfg: dict, creator_did: str, sid: str) -> str:
+    async def _local_create_session(self, cfg: dict, creator_did: str, sid: str, detail: bool = False):
         m = await self.local.create_session(_cfg_in(cfg), creator_did, session_id=sid)
-        return m.sso.session_id
+        if not detail:
+            return m.sso.session_id
+        x = m.sso
+        return {"session_id": x.session_id, "state": x.state.value, "consistency_mode": x.consistency_mode.value,
+                "created_at": x.created_at.isoformat()}
 
     async def join_session(self, session_id: str, agent_did: str, sigma_raw: float = 0.0, **kw):
         from hypervisor.models import ExecutionRing
@@ -295,13 +372,25 @@ class ShardedHypervisor:
         return None if r is None else {"drift_score": r.drift_score, "severity": r.severity.value,
                                        "passed": r.passed, "should_slash": r.should_slash}
 
-    async def get_session(self, session_id: str) -> dict:
-        return await self._route(session_id, "get_session", session_id)
+    async def get_session(self, session_id: str, detail: bool = False) -> dict:
+        """Session summary (``detail``: the REST route's SessionDetailResponse fields)."""
+        return await self._route(session_id, "get_session", session_id, detail)
 
-    async def _local_get_session(self, session_id: str) -> dict:
+    async def _local_get_session(self, session_id: str, detail: bool = False) -> dict:
         m = self.local.get_session(session_id)
         if m is None:
             raise ValueError(f"Session {session_id} not found")
+        if detail:
+            from hypervisor.api.models import ParticipantInfo
+
+            sso = m.sso
+            return {"session_id": sso.session_id, "state": sso.state.value,
+                    "consistency_mode": sso.consistency_mode.value, "creator_did": sso.creator_did,
+                    "participant_count": sso.participant_count,
+                    "participants": [ParticipantInfo.of(p).model_dump() for p in sso.participants],
+                    "created_at": sso.created_at.isoformat(),
+                    "terminated_at": sso.terminated_at.isoformat() if sso.terminated_at else None,
+                    "sagas": [g.to_dict() for g in m.saga.sagas]}
         x = self.local.snapshots([m], parts=True)[0]
         return {
             "session_id": x.session_id, "state": x.state.value, "consistency_mode": x.consistency_mode.value,
@@ -329,15 +418,22 @@ class ShardedHypervisor:
 
     # -- liability (session-scoped → the owner's device) ---------------------------------
     async def vouch(self, voucher_did: str, vouchee_did: str, session_id: str, voucher_sigma: float,
-                    bond_pct: Optional[float] = None, expiry: Optional[datetime] = None) -> dict:
+                    bond_pct: Optional[float] = None, expiry: Optional[datetime] = None, emit: bool = False) -> dict:
+        """``emit``: publish the REST route's ``vouch.created`` event on the owner."""
         return await self._route(session_id, "vouch", voucher_did, vouchee_did, session_id, voucher_sigma, bond_pct,
-                                 expiry.isoformat() if expiry is not None else None)
+                                 expiry.isoformat() if expiry is not None else None, emit)
 
-    async def _local_vouch(self, voucher_did, vouchee_did, session_id, voucher_sigma, bond_pct=None, expiry=None):
+    async def _local_vouch(self, voucher_did, vouchee_did, session_id, voucher_sigma, bond_pct=None, expiry=None,
+                           emit: bool = False):
         exp = datetime.fromisoformat(expiry) if expiry else None
         v = self.local.vouching.vouch(voucher_did, vouchee_did, session_id, voucher_sigma, bond_pct, exp)
         self._vouch_seq += 1
         self._vouch_key[v.vouch_id] = (_us(v.created_at), self.rank, self._vouch_seq)
+        if emit:  # the REST route's event (reference api/server.py vouch handler)
+            from hypervisor.observability.event_bus import EventType
+
+            self.local._emit(EventType.VOUCH_CREATED, session_id, voucher_did, vouch_id=v.vouch_id,
+                             vouchee_did=vouchee_did, bonded_amount=v.bonded_amount)
         return _vouch_dict(v)
 
     async def compute_sigma_eff(self, vouchee_did: str, session_id: str, sigma: float, risk_weight: float) -> float:
@@ -374,14 +470,22 @@ class ShardedHypervisor:
                 "clips": [[c.voucher_did, c.sigma_before, c.sigma_after] for c in res.voucher_clips]}
 
     # -- sagas (ids route to their session's owner) ---------------------------------------
-    async def create_saga(self, session_id: str) -> str:
+    async def create_saga(self, session_id: str, emit: bool = False):
+        """Returns the saga id (``emit``: the REST route's form — its event is
+        published on the owner and the CreateSagaResponse fields returned)."""
         gid = self._mint("saga:", self.owner(session_id))
-        return await self._route(session_id, "create_saga", session_id, gid)
+        return await self._route(session_id, "create_saga", session_id, gid, emit)
 
-    async def _local_create_saga(self, session_id: str, gid: str) -> str:
-        self.local._get_session(session_id).saga.create_saga(session_id, saga_id=gid)
+    async def _local_create_saga(self, session_id: str, gid: str, emit: bool = False):
+        g = self.local._get_session(session_id).saga.create_saga(session_id, saga_id=gid)
         self._sagas[gid] = session_id
-        return gid
+        if not emit:
+            return gid
+        from hypervisor.observability.event_bus import EventType
+
+        self.local._emit(EventType.SAGA_CREATED, session_id, saga_id=gid)
+        return {"saga_id": gid, "session_id": g.session_id, "state": g.state.value,
+                "created_at": g.created_at.isoformat()}
 
     def _saga_session(self, saga_id: str) -> str:
         sid = self._sagas.get(saga_id)
@@ -392,15 +496,24 @@ class ShardedHypervisor:
         return sid
 
     async def add_step(self, saga_id: str, action_id: str, agent_did: str, execute_api: str,
-                       undo_api: Optional[str] = None, timeout_seconds: int = 300, max_retries: int = 0) -> str:
+                       undo_api: Optional[str] = None, timeout_seconds: int = 300, max_retries: int = 0,
+                       detail: bool = False):
+        """Returns the step id (``detail``: the REST route's AddStepResponse fields;
+        a refused step then raises RuntimeError — the route's 400)."""
         return await self._route(saga_id, "add_step", saga_id, action_id, agent_did, execute_api, undo_api,
-                                 timeout_seconds, max_retries)
+                                 timeout_seconds, max_retries, detail)
 
     async def _local_add_step(self, saga_id, action_id, agent_did, execute_api, undo_api=None, timeout_seconds=300,
-                              max_retries=0) -> str:
+                              max_retries=0, detail: bool = False):
         orch = self.local._get_session(self._saga_session(saga_id)).saga
-        return orch.add_step(saga_id, action_id, agent_did, execute_api, undo_api, timeout_seconds,
-                             max_retries).step_id
+        if not detail:
+            return orch.add_step(saga_id, action_id, agent_did, execute_api, undo_api, timeout_seconds,
+                                 max_retries).step_id
+        try:
+            st = orch.add_step(saga_id, action_id, agent_did, execute_api, undo_api, timeout_seconds, max_retries)
+        except Exception as e:  # noqa: BLE001 - the single-rank route answers 400
+            raise RuntimeError(str(e)) from e
+        return {"step_id": st.step_id, "saga_id": saga_id, "action_id": st.action_id, "state": st.state.value}
 
     def register_executor(self, name: str, fn: Callable[..., Any]) -> None:
         """Make an executor callable by name from any rank (register on every rank)."""
@@ -409,20 +522,40 @@ class ShardedHypervisor:
     def register_compensator(self, name: str, fn: Callable[..., Any]) -> None:
         self.compensators[name] = fn
 
-    async def execute_step(self, saga_id: str, step_id: str, executor: Any = "noop") -> Any:
-        """``executor``: a registered name (any rank) or a callable (owner rank only)."""
+    async def execute_step(self, saga_id: str, step_id: str, executor: Any = "noop", rest: bool = False) -> Any:
+        """``executor``: a registered name (any rank) or a callable (owner rank only).
+        ``rest``: the REST route's form — failures are reported, not raised, as
+        ``{"state", "error"}``, with the route's step event published on the owner."""
         if callable(executor):
             if self.owner(saga_id) != self.rank:
                 raise TypeError("executors cross ranks by name: register_executor() on every rank")
             self.counters["local"] += 1
             return await self._exec_step(saga_id, step_id, executor)
-        return await self._route(saga_id, "execute_step", saga_id, step_id, executor)
+        return await self._route(saga_id, "execute_step", saga_id, step_id, executor, rest)
 
-    async def _local_execute_step(self, saga_id: str, step_id: str, executor: str = "noop") -> Any:
+    async def _local_execute_step(self, saga_id: str, step_id: str, executor: str = "noop", rest: bool = False) -> Any:
         fn = self.executors.get(executor)
         if fn is None:
             raise KeyError(f"executor {executor!r} is not registered on rank {self.rank}")
-        return await self._exec_step(saga_id, step_id, fn)
+        if not rest:
+            return await self._exec_step(saga_id, step_id, fn)
+        from hypervisor.observability.event_bus import EventType
+
+        sid = self._saga_session(saga_id)
+        orch = self.local._get_session(sid).saga
+        saga = orch.get_saga(saga_id)
+        if saga is None or not any(x.step_id == step_id for x in saga.steps):
+            raise ValueError(f"Saga {saga_id} or step {step_id} not found")
+        try:
+            await orch.execute_step(saga_id, step_id, executor=fn)
+        except Exception as e:  # noqa: BLE001 - the single-rank route answers 400
+            raise RuntimeError(str(e)) from e
+        for x in saga.steps:
+            if x.step_id == step_id:
+                et = EventType.SAGA_STEP_COMMITTED if x.state.value == "committed" else EventType.SAGA_STEP_FAILED
+                self.local._emit(et, saga.session_id, x.agent_did, saga_id=saga_id, step_id=step_id)
+                return {"state": x.state.value, "error": x.error}
+        raise ValueError(f"Saga {saga_id} or step {step_id} not found")
 
     async def _exec_step(self, saga_id, step_id, fn):
         orch = self.local._get_session(self._saga_session(saga_id)).saga
@@ -446,12 +579,96 @@ class ShardedHypervisor:
         orch = self.local._get_session(self._saga_session(saga_id)).saga
         return [s.step_id for s in await orch.compensate(saga_id, fn)]
 
-    async def get_saga(self, saga_id: str) -> dict:
-        return await self._route(saga_id, "get_saga", saga_id)
+    async def get_saga(self, saga_id: str, detail: bool = False) -> dict:
+        """``saga.to_dict()`` (``detail``: the REST route's SagaDetailResponse fields)."""
+        return await self._route(saga_id, "get_saga", saga_id, detail)
 
-    async def _local_get_saga(self, saga_id: str) -> dict:
+    async def _local_get_saga(self, saga_id: str, detail: bool = False) -> dict:
         orch = self.local._get_session(self._saga_session(saga_id)).saga
+        if detail:
+            from hypervisor.api.models import SagaDetailResponse
+
+            return SagaDetailResponse.of(orch.get_saga(saga_id)).model_dump()
         return orch.get_saga(saga_id).to_dict()
+
+    # -- the rest of the per-session surface (reference api/server.py:192-309) ------------
+    async def ring_distribution(self, session_id: str) -> dict:
+        """``GET /sessions/{id}/rings``: ring name → participant DIDs."""
+        return await self._route(session_id, "ring_distribution", session_id)
+
+    async def _local_ring_distribution(self, session_id: str) -> dict:
+        out: dict = {}
+        for p in self.local._get_session(session_id).sso.participants:
+            out.setdefault(p.ring.name, []).append(p.agent_did)
+        return out
+
+    def check_ring(self, agent_ring: int, action: dict, sigma_eff: float, has_consensus: bool = False,
+                   has_sre_witness: bool = False) -> dict:
+        """``POST /rings/check``: stateless, answered by the calling rank."""
+        from hypervisor.models import ActionDescriptor, ExecutionRing
+
+        r = self.local.ring_enforcer.check(agent_ring=ExecutionRing(agent_ring), action=ActionDescriptor(**action),
+                                           sigma_eff=sigma_eff, has_consensus=has_consensus,
+                                           has_sre_witness=has_sre_witness)
+        return {"allowed": r.allowed, "required_ring": r.required_ring.value, "agent_ring": r.agent_ring.value,
+                "sigma_eff": r.sigma_eff, "reason": r.reason, "requires_consensus": r.requires_consensus,
+                "requires_sre_witness": r.requires_sre_witness}
+
+    async def list_sagas(self, session_id: str) -> list:
+        """``GET /sessions/{id}/sagas`` (SagaDetailResponse rows)."""
+        return await self._route(session_id, "list_sagas", session_id)
+
+    async def _local_list_sagas(self, session_id: str) -> list:
+        from hypervisor.api.models import SagaDetailResponse
+
+        return [SagaDetailResponse.of(g).model_dump() for g in self.local._get_session(session_id).saga.sagas]
+
+    async def list_vouches(self, session_id: str) -> list:
+        """``GET /sessions/{id}/vouches`` (VouchResponse rows, creation order)."""
+        return await self._route(session_id, "list_vouches", session_id)
+
+    async def _local_list_vouches(self, session_id: str) -> list:
+        from hypervisor.api.models import VouchResponse
+
+        self.local._get_session(session_id)  # unknown session: 404 like the single-rank route
+        return [VouchResponse.of(v).model_dump() for v in self.local.vouching.records(session_id)]
+
+    async def sso(self, session_id: str, op: str, *args) -> Any:
+        """A SharedSessionObject operation on the session's owner: ``leave``,
+        ``update_ring``, ``force_consistency_mode``, ``get_participant``,
+        ``vfs_write`` / ``vfs_read`` / ``vfs_delete`` / ``vfs_list``,
+        ``vfs_set_permissions`` / ``vfs_get_permissions``, ``vfs_snapshot`` /
+        ``vfs_restore`` / ``vfs_list_snapshots`` / ``vfs_delete_snapshot``."""
+        return await self._route(session_id, "sso", session_id, op, *args)
+
+    async def _local_sso(self, session_id: str, op: str, *args) -> Any:
+        if not _SSO:
+            _SSO.update(_sso_ops())
+        fn = _SSO.get(op)
+        if fn is None:
+            raise ValueError(f"unknown session operation {op!r}")
+        return fn(self.local._get_session(session_id).sso, *args)
+
+    async def leave_session(self, session_id: str, agent_did: str) -> None:
+        await self.sso(session_id, "leave", agent_did)
+
+    async def update_ring(self, session_id: str, agent_did: str, ring: int) -> None:
+        await self.sso(session_id, "update_ring", agent_did, int(ring))
+
+    async def vfs_write(self, session_id: str, path: str, content: str, agent_did: str) -> dict:
+        return await self.sso(session_id, "vfs_write", path, content, agent_did)
+
+    async def vfs_read(self, session_id: str, path: str, agent_did: Optional[str] = None) -> Optional[str]:
+        return await self.sso(session_id, "vfs_read", path, agent_did)
+
+    async def vfs_delete(self, session_id: str, path: str, agent_did: str) -> dict:
+        return await self.sso(session_id, "vfs_delete", path, agent_did)
+
+    async def vfs_snapshot(self, session_id: str, snapshot_id: Optional[str] = None) -> str:
+        return await self.sso(session_id, "vfs_snapshot", snapshot_id)
+
+    async def vfs_restore(self, session_id: str, snapshot_id: str, agent_did: str) -> None:
+        await self.sso(session_id, "vfs_restore", snapshot_id, agent_did)
 
     # -- agent-global views ----------------------------------------------------------------
     async def stats(self) -> dict:
@@ -477,6 +694,21 @@ class ShardedHypervisor:
     async def list_sessions(self, state: Optional[str] = None) -> list[dict]:
         return await self._view("list_sessions", state)
 
+    async def events(self, event_type: Optional[str] = None, session_id: Optional[str] = None,
+                     agent_did: Optional[str] = None, limit: Optional[int] = None) -> list[dict]:
+        """``GET /events``: every rank's bus filtered, merged by (timestamp, rank,
+        sequence); ``limit`` keeps the latest ones (reference event_bus.py:158-175)."""
+        return await self._view("events", event_type, session_id, agent_did, limit)
+
+    async def event_stats(self) -> dict:
+        """``GET /events/stats``: total and per-type counts over every rank."""
+        return await self._view("event_stats")
+
+    async def hold(self, seconds: float) -> int:
+        """Diagnostics view: every rank keeps its collective open ``seconds`` (what a
+        slow view looks like); per-session calls keep being served meanwhile."""
+        return await self._view("hold", float(seconds))
+
     async def load(self) -> list[int]:
         """Sessions per rank."""
         return await self._view("load")
@@ -494,15 +726,42 @@ class ShardedHypervisor:
             others = [r for r in self.members if r != self.rank]
             for r in others:
                 await self.rpc.connect(r)
-            # the enter messages are written before this rank blocks in the collective
+            # every rank enters; this rank's collective runs on its communication thread
             peers = [self.rpc.send(r, "_view_enter", name, *args) for r in others]
-            mine = self._collective(name, *args)
+            mine = await self._enter(name, *args)
             parts = [mine] + list(await asyncio.gather(*peers))
         return self._combine(name, args, parts)
 
+    async def _enter(self, name: str, *args) -> Any:
+        """This rank's part of a view: the local reads on the event loop (the store
+        is not shared across threads), the blocking collective on the
+        communication thread — the loop keeps serving per-session calls while the
+        collective waits for the other ranks — then the JSON answer."""
+        part, t, op, wait_s = self._local_part(name, *args)
+        if t is not None and (self.world > 1 or wait_s):
+            if self._comm is None:
+                self._comm = ThreadPoolExecutor(max_workers=1, thread_name_prefix="ahv-comm")
+            await asyncio.get_running_loop().run_in_executor(self._comm, self._blocking_collective, t, op, wait_s)
+        return self._finish(name, args, part, t)
+
+    def _blocking_collective(self, t: torch.Tensor, op, wait_s: float) -> None:
+        if wait_s:
+            import time
+
+            time.sleep(wait_s)
+        self._all_reduce(t, op)
+
     def _collective(self, name: str, *args) -> Any:
-        """This rank's part of a view (runs its collectives); JSON-serialisable."""
+        """Synchronous form of :meth:`_enter` (one-rank façades)."""
+        part, t, op, _ = self._local_part(name, *args)
+        if t is not None:
+            self._all_reduce(t, op)
+        return self._finish(name, args, part, t)
+
+    def _local_part(self, name: str, *args) -> tuple:
+        """(local data, tensor to all-reduce or None, reduce op, hold seconds)."""
         hv = self.local
+        dev = _tensor_device()
         if name == "stats":
             snaps = hv.snapshots()  # one batched device read
             sagas = hv.saga_summaries()
@@ -510,48 +769,133 @@ class ShardedHypervisor:
                     sum(x.participant_count for x in snaps),
                     sum(1 for g in sagas if g["state"] in ("running", "compensating")),
                     len(hv.vouching.records()), len(sagas)]
-            t = torch.tensor(vals, dtype=torch.int64, device=_tensor_device())
-            self._all_reduce(t, dist.ReduceOp.SUM)
-            return [int(x) for x in t.tolist()]
+            return None, torch.tensor(vals, dtype=torch.int64, device=dev), dist.ReduceOp.SUM, 0.0
         if name == "agent_ring":
             (agent_did,) = args
-            big = (1 << 62) - 1
-            best, sid = big, None
-            for x in hv.snapshots(parts=True):
-                for p in x.participants:
-                    if p.agent_did == agent_did and p.is_active:
-                        key = ((_us(x.created_at) - _EPOCH_US) << 12) | (self.rank << 4) | int(p.ring)
-                        if key < best:
-                            best, sid = key, x.session_id
-                        break
-            t = torch.tensor([best], dtype=torch.int64, device=_tensor_device())
-            self._all_reduce(t, dist.ReduceOp.MIN)
-            g = int(t.item())
-            return [g, sid if g == best and g < big else None]
+            best, sid = self._local_first_ring(agent_did)
+            return (best, sid), torch.tensor([best], dtype=torch.int64, device=dev), dist.ReduceOp.MIN, 0.0
         if name == "agent_liability":
             (agent_did,) = args
-            out = []
-            for v in hv.vouching.records():
-                if v.voucher_did == agent_did or v.vouchee_did == agent_did:
-                    key = self._vouch_key.get(v.vouch_id, (_us(v.created_at), self.rank, 1 << 40))
-                    out.append([list(key), _vouch_dict(v)])
-            return out
+            return self._local_liability(agent_did), None, None, 0.0
         if name == "exposure_vector":
             (dids,) = args
-            x = self._local_exposure(dids)
-            self._all_reduce(x, dist.ReduceOp.SUM)
-            return x.cpu().tolist()
+            return None, self._local_exposure(dids), dist.ReduceOp.SUM, 0.0
         if name == "list_sessions":
             (state,) = args
             return [[_us(x.created_at), self.rank, i,
-                     {"session_id": x.session_id, "state": x.state.value, "participant_count": x.participant_count,
+                     {"session_id": x.session_id, "state": x.state.value, "consistency_mode": x.consistency_mode.value,
+                      "participant_count": x.participant_count, "created_at": x.created_at.isoformat(),
                       "rank": self.rank}]
-                    for i, x in enumerate(hv.snapshots()) if state is None or x.state.value == state]
+                    for i, x in enumerate(hv.snapshots()) if state is None or x.state.value == state], None, None, 0.0
         if name == "load":
-            return len(hv.sessions)
+            return len(hv.sessions), None, None, 0.0
+        if name == "events":
+            et, sid, did, limit = args
+            from hypervisor.observability.event_bus import EventType
+
+            bus = self.bus
+            if bus is None:
+                return [], None, None, 0.0
+            evs = bus.query(event_type=EventType(et) if et else None, session_id=sid, agent_did=did)
+            seq = {id(e): k for k, e in enumerate(bus.all_events)} if evs else {}
+            if limit is not None:
+                evs = evs[-int(limit):] if int(limit) > 0 else []
+            return [[_us(e.timestamp), self.rank, seq[id(e)],
+                     {"event_id": e.event_id, "event_type": e.event_type.value, "timestamp": e.timestamp.isoformat(),
+                      "session_id": e.session_id, "agent_did": e.agent_did, "causal_trace_id": e.causal_trace_id,
+                      "payload": e.payload}] for e in evs], None, None, 0.0
+        if name == "event_stats":
+            bus = self.bus
+            return ({"total_events": bus.event_count if bus else 0, "by_type": bus.type_counts() if bus else {}},
+                    None, None, 0.0)
+        if name == "hold":
+            (secs,) = args
+            return None, torch.zeros(1, dtype=torch.int64, device=dev), dist.ReduceOp.SUM, float(secs)
         raise ValueError(f"unknown view {name!r}")
 
+    def _finish(self, name: str, args, part, t) -> Any:
+        if name in ("stats",):
+            return [int(x) for x in t.tolist()]
+        if name == "agent_ring":
+            best, sid = part
+            g = int(t.item())
+            return [g, sid if g == best and g < _NO_RING else None]
+        if name == "exposure_vector":
+            return t.cpu().tolist()
+        if name == "hold":
+            return self.world
+        return part
+
+    def _local_first_ring(self, agent_did: str) -> tuple:
+        """X05 on this rank: the key ((created − epoch) << 12 | rank << 4 | ring) of the
+        earliest-created session (session order on ties) where the agent is an
+        active participant, and that session's id.  Device-backed: one MIN over
+        the store's participant columns of the rank's session rows."""
+        hv = self.local
+        st = hv._store
+        if st is None:  # host engines: the snapshots in creation order
+            return self._earliest(agent_did)
+        from agent_hypervisor_amd.ops.store_views import first_active_ring, session_rows
+
+        slots, sid_of = session_rows(hv)
+        a = st.agents.lookup(agent_did)
+        if a < 0 or not len(slots):
+            return _NO_RING, None
+        hit = first_active_ring(st, slots, a)
+        if hit is None:
+            return _NO_RING, None
+        i, created, ring = hit
+        return ((created - _EPOCH_US) << 12) | (self.rank << 4) | ring, sid_of(i)
+
+    def _earliest(self, agent_did: str) -> tuple:
+        """(key, session id) by a walk over the snapshots (creation order: the first
+        match wins ties)."""
+        best, sid = _NO_RING, None
+        for x in self.local.snapshots(parts=True):
+            for p in x.participants:
+                if p.agent_did == agent_did and p.is_active:
+                    key = ((_us(x.created_at) - _EPOCH_US) << 12) | (self.rank << 4) | int(p.ring)
+                    if key < best:
+                        best, sid = key, x.session_id
+                    break
+        return best, sid
+
+    def _local_liability(self, agent_did: str) -> list:
+        """This rank's vouch records naming the agent, each with its global order
+        key; bond state for all of them from one gather of the edge columns."""
+        hv = self.local
+        recs = [v for v in hv.vouching.records() if v.voucher_did == agent_did or v.vouchee_did == agent_did]
+        st = hv._store
+        state = {}
+        if st is not None:
+            live = [v.edge for v in recs if getattr(v, "edge", -1) >= 0]
+            if live:
+                g = st.gather({"e_active": live})
+                state = {e: bool(a) for e, a in zip(live, g["e_active"].tolist())}
+        out = []
+        for v in recs:
+            key = self._vouch_key.get(v.vouch_id, (_us(v.created_at), self.rank, 1 << 40))
+            d = _vouch_dict(v, state.get(getattr(v, "edge", -1)) if st is not None else None)
+            out.append([list(key), d])
+        return out
+
     def _combine(self, name: str, args, parts: list) -> Any:
+        if name == "events":
+            limit = args[3]
+            rows = sorted((tuple(p[:3]), p[3]) for part in parts for p in part)
+            out = [d for _, d in rows]
+            if limit is not None:
+                out = out[-int(limit):] if int(limit) > 0 else []
+            return out
+        if name == "event_stats":
+            total, by = 0, {}
+            for p in parts:
+                total += p["total_events"]
+                for k, v in p["by_type"].items():
+                    by[k] = by.get(k, 0) + v
+            return {"total_events": total, "by_type": by}
+        if name == "hold":
+            return parts[0]
         if name == "stats":
             keys = ("total_sessions", "active_sessions", "total_participants", "active_sagas", "total_vouches",
                     "total_sagas")
@@ -690,11 +1034,15 @@ class ShardedHypervisor:
         return moves
 
 
-def _vouch_dict(v) -> dict:
+_NO_RING = (1 << 62) - 1
+
+
+def _vouch_dict(v, active: Optional[bool] = None) -> dict:
+    """``active``: the bond state already gathered from the edge columns (None: ask the record)."""
     return {
         "vouch_id": v.vouch_id, "voucher_did": v.voucher_did, "vouchee_did": v.vouchee_did,
         "session_id": v.session_id, "bonded_sigma_pct": v.bonded_sigma_pct, "bonded_amount": v.bonded_amount,
-        "is_active": bool(v.is_active), "is_expired": bool(v.is_expired),
+        "is_active": bool(v.is_active) if active is None else active, "is_expired": bool(v.is_expired),
     }
 
 
