@@ -95,8 +95,8 @@ class EngineSessions:
         t, P = store.tables, store.caps["P"]
         for name, (col, shape) in self._MAP.items():
             x = t[col]
-            if shape == "P":
-                x = x[: capacity * P].view(capacity, P)
+            if shape == "P":  # participant-major columns (store.h prow): [P][S] → a [cap, P] view
+                x = x[: P * store.caps["S"]].view(P, store.caps["S"])[:, :capacity].t()
             elif shape is not None:
                 x = x[: capacity * shape].view(capacity, shape)
             else:

@@ -253,12 +253,16 @@ class GovernanceStore:
             caps = dict(self.caps, **{kind: new})
             ext = _extents(caps)
             grown = set(_EXT_OF[kind])
+            P = self.caps["P"]
             for name, ctype, ek in C.STORE_COLUMNS:
                 if ek not in grown:
                     continue
                 old = self.tables[name]
                 t = torch.full((ext[ek],), _fill(name), dtype=old.dtype, device=self.device)
-                t[: old.numel()].copy_(old)
+                if ek == "SP":  # participant-major [P][S]: each participant plane keeps its rows
+                    t.view(P, new)[:, :cur].copy_(old.view(P, cur))
+                else:
+                    t[: old.numel()].copy_(old)
                 self.tables[name] = t
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)

@@ -79,8 +79,8 @@ def first_active_ring(store, slots, agent_id: int):
     dev = st.device
     P = st.caps["P"]
     rows = torch.from_numpy(np.ascontiguousarray(slots, dtype=np.int64)).to(dev)
-    agent = st.tables["p_agent"].view(-1, P).index_select(0, rows)
-    active = st.tables["p_active"].view(-1, P).index_select(0, rows)
+    agent = st.tables["p_agent"].view(P, -1).index_select(1, rows).t()  # participant-major columns
+    active = st.tables["p_active"].view(P, -1).index_select(1, rows).t()
     pc = st.tables["s_pcount"].index_select(0, rows).to(torch.int64)
     k = torch.arange(P, device=dev)
     m = (agent == agent_id) & ((active & 1) != 0) & (k[None, :] < pc[:, None])
@@ -92,7 +92,7 @@ def first_active_ring(store, slots, agent_id: int):
     key = torch.where(has, created, torch.full_like(created, big))
     i = int(torch.argmin(key))  # first minimal index: session order breaks ties
     col = int(torch.argmax(m[i].to(torch.int32)))
-    ring = int(st.tables["p_ring"].view(-1, P)[rows[i], col])
+    ring = int(st.tables["p_ring"].view(P, -1)[col, rows[i]])
     return i, int(created[i]), ring
 
 

@@ -634,7 +634,7 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
         if len(r["participants"]) > P:
             raise CheckpointError(f"session {r['session_id']}: more participants than the store's row width {P}")
         for k, p in enumerate(r["participants"]):
-            row = s * P + k
+            row = ("P", s, k)  # participant-major row k·S + s, resolved once every row is allocated
             put("p_agent", row, st.agent_id(p["agent_did"]))
             put("p_ring", row, int(p["ring"]))
             # P_ACTIVE | P_COMMITTED (store.h): members of the committed participant list
@@ -745,6 +745,13 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
         ve._by_id[rec.vouch_id] = rec
         ve._by_edge[e] = rec
         ve._order.append(rec)
+    # participant rows: the store's final session capacity fixes their index (store.h prow)
+    S_cap = st.caps["S"]
+
+    def _row(i):
+        return i[2] * S_cap + i[1] if isinstance(i, tuple) else i
+
+    rows = {col: ([_row(i) for i in ix], vs) for col, (ix, vs) in rows.items()}
     # later writes to one index win (e_next of an edge that gained a successor)
     st.write_rows(rows)
     for sid, c in commits.items():

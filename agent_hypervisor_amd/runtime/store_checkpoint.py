@@ -516,9 +516,10 @@ def save_store(hv, d: str) -> dict:
         T[f"S.{name}"] = _take(st, name, slots)
     for name, w in S_WIDE.items():
         T[f"S.{name}"] = _take(st, name, slots, w)
-    P = st.caps["P"]
+    P, S_cap = st.caps["P"], st.caps["S"]
     pcnt = T["S.s_pcount"].numpy().astype(np.int64)
-    prow = _ragged(slots * P, pcnt)
+    kpos = np.arange(int(pcnt.sum()), dtype=np.int64) - np.repeat(np.concatenate([[0], np.cumsum(pcnt)[:-1]]), pcnt)
+    prow = kpos * S_cap + np.repeat(slots, pcnt)  # participant-major columns (store.h prow)
     for name in P_COLS:
         T[f"P.{name}"] = _take(st, name, prow)
     # -- delta chains: walk d_prev back from s_dlast (chain order, every live row) --
@@ -758,7 +759,7 @@ def load_store(hv, d: str, verify: bool = True, only=None):
     W["s_dlast"] = (slots, last.astype(np.int32))
     W["s_proot_n"] = (slots, np.zeros(n, np.int32))
     kpos = np.arange(len(pi), dtype=np.int64) - np.repeat(np.concatenate([[0], np.cumsum(pcnt)[:-1]]), pcnt)
-    prow = np.repeat(slots * P, pcnt) + kpos
+    prow = kpos * st.caps["S"] + np.repeat(slots, pcnt)  # participant-major (store.h prow), S after the allocs
     for name in P_COLS:
         v = Pc[f"P.{name}"]
         if name == "p_agent":

@@ -133,19 +133,18 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
   }
   // joins, in order: K01 ring gate + admission (OP_SESS_JOIN semantics)
   int32_t pc = 0, active = 0;
-  const int64_t base = s * t.cap.P;
   for (int32_t j = a.join_off[i]; j < a.join_off[i + 1]; ++j) {
     const int32_t agent = a.join_agent[j];
     const double sg = a.join_sigma[j];
     const uint8_t ring = ring_from_sigma(sg, false);
     bool dup = false;
-    for (int32_t k = 0; k < pc; ++k) dup = dup || t.p_agent[base + k] == agent;
+    for (int32_t k = 0; k < pc; ++k) dup = dup || t.p_agent[store::prow(t, s, k)] == agent;
     uint8_t code = join_check(st, dup, active, a.maxpart[i], sg, a.minsig[i], ring);
     if (code == JOIN_OK && pc >= t.cap.P) code = static_cast<uint8_t>(store::JOIN_ROWS);
     a.join_ring[j] = ring;
     a.join_code[j] = code;
     if (code == JOIN_OK) {
-      const int64_t row = base + pc;
+      const int64_t row = store::prow(t, s, pc);
       t.p_agent[row] = agent;
       t.p_ring[row] = ring;
       t.p_active[row] = 1;
@@ -235,7 +234,7 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
       if ((fl & 1u) && nd > 0) {
         t.s_committed[s] = tt;
         t.s_commit_n[s] = nd;
-        for (int32_t k = 0; k < pc; ++k) t.p_active[base + k] = store::P_ACTIVE | store::P_COMMITTED;
+        for (int32_t k = 0; k < pc; ++k) t.p_active[store::prow(t, s, k)] = store::P_ACTIVE | store::P_COMMITTED;
       }
       int32_t retained = 0;
       for (int32_t k = 0; k < nd; ++k) retained += sp_delta_ts(a, i, k) >= tt - a.gc_retention_us ? 1 : 0;

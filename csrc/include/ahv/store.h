@@ -114,7 +114,8 @@ enum RowKind : uint64_t { RK_S = 0, RK_G = 1, RK_T = 2, RK_E = 3, RK_D = 4, RK_V
 // --------------------------------------------------------------- tables
 
 // X-macro: (name, element type, extent) where extent names a capacity:
-// S sessions, SP session×participant rows, S8/S4 session×digest/uuid words,
+// S sessions, SP participant rows (participant-major: row k·S + s, see prow),
+// S8/S4 session×digest/uuid words,
 // D deltas, D8 delta×digest words, E vouch edges, V liability sessions,
 // G sagas, T steps, SCR scratch bytes (cap X).
 #define AHV_STORE_COLUMNS(X)       \
@@ -391,11 +392,17 @@ AHV_HD bool edge_live(const Tables& t, int32_t e, int64_t now) {
 constexpr uint8_t P_ACTIVE = 1u;
 constexpr uint8_t P_COMMITTED = 2u;
 
+// Participant row k of session s.  The participant columns are participant-major
+// ([k][session]): the k-th rows of consecutive sessions are adjacent, so the
+// batched pipelines' first-participant writes from 64 lanes are contiguous.
+AHV_HD int64_t prow(const Tables& t, int64_t s, int64_t k) { return k * t.cap.S + s; }
+
 AHV_HD void mark_committed_participants(const Tables& t, int64_t s) {
   const int32_t n = t.s_pcount[s];
-  const int64_t base = s * t.cap.P;
-  for (int32_t k = 0; k < n; ++k)
-    if (t.p_active[base + k] & P_ACTIVE) t.p_active[base + k] = P_ACTIVE | P_COMMITTED;
+  for (int32_t k = 0; k < n; ++k) {
+    const int64_t row = prow(t, s, k);
+    if (t.p_active[row] & P_ACTIVE) t.p_active[row] = P_ACTIVE | P_COMMITTED;
+  }
 }
 
 // Participant row of `agent` in session `s` (all rows, active or not), or -1.
@@ -407,9 +414,8 @@ AHV_HD uint64_t row_stamp(const Tables& t, int64_t s) {
 
 AHV_HD int32_t find_part(const Tables& t, int64_t s, int32_t agent) {
   const int32_t n = t.s_pcount[s];
-  const int64_t base = s * t.cap.P;
   for (int32_t k = 0; k < n; ++k)
-    if (t.p_agent[base + k] == agent) return k;
+    if (t.p_agent[prow(t, s, k)] == agent) return k;
   return -1;
 }
 
@@ -776,7 +782,7 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
       uint64_t code = join_check(st, dup, active, t.s_maxpart[s], seff, t.s_minsig[s], ring);
       if (code == JOIN_OK && t.s_pcount[s] >= t.cap.P) code = JOIN_ROWS;
       if (code == JOIN_OK) {
-        const int64_t row = s * t.cap.P + t.s_pcount[s];
+        const int64_t row = prow(t, s, t.s_pcount[s]);
         t.p_agent[row] = agent;
         t.p_ring[row] = ring;
         t.p_active[row] = 1;
@@ -800,7 +806,7 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
         out64(r + 1, ST_NOT_FOUND);
         return;
       }
-      const int64_t row = s * t.cap.P + k;
+      const int64_t row = prow(t, s, k);
       if (t.p_active[row] & P_ACTIVE) {  // a commit-time membership bit (P_COMMITTED) stays
         t.p_active[row] = static_cast<uint8_t>(t.p_active[row] & ~P_ACTIVE);
         t.s_pactive[s] -= 1;
@@ -815,7 +821,7 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
         out64(r + 1, ST_NOT_FOUND);
         return;
       }
-      const int64_t row = s * t.cap.P + k;
+      const int64_t row = prow(t, s, k);
       if (c.op == OP_SESS_UPDATE_RING) {
         t.p_ring[row] = static_cast<uint8_t>(c.a[2]);
       } else {
@@ -895,7 +901,7 @@ AHV_HD void exec_sess(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r
         uint64_t* b = reinterpret_cast<uint64_t*>(bulk + c.a[1]);
         const int32_t n = t.s_pcount[s];
         for (int32_t k = 0; k < n; ++k) {
-          const int64_t row = s * t.cap.P + k;
+          const int64_t row = prow(t, s, k);
           out64(b + 5 * k + 0, static_cast<uint64_t>(static_cast<int64_t>(t.p_agent[row])));
           out64(b + 5 * k + 1, uint64_t(t.p_ring[row]) | (uint64_t(t.p_active[row]) << 8));
           out64(b + 5 * k + 2, dbits(t.p_sraw[row]));
@@ -1480,7 +1486,7 @@ AHV_HD void exec_read_many(const Lanes& L, const Tables& t, const Cmd& c, uint64
       uint64_t* p = pb + 5 * t.cap.P * i;
       const int32_t np = t.s_pcount[s];
       for (int32_t k = 0; k < np; ++k) {
-        const int64_t row = s * t.cap.P + k;
+        const int64_t row = prow(t, s, k);
         out64(p + 5 * k + 0, static_cast<uint64_t>(static_cast<int64_t>(t.p_agent[row])));
         out64(p + 5 * k + 1, uint64_t(t.p_ring[row]) | (uint64_t(t.p_active[row]) << 8));
         out64(p + 5 * k + 2, dbits(t.p_sraw[row]));

@@ -180,14 +180,14 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
   const uint8_t ring = ring_from_sigma(sg, false);
   uint8_t code = join_check(st, false, 0, a.maxpart, sg, a.minsig, ring);
   if (code == JOIN_OK && t.cap.P < 1) code = static_cast<uint8_t>(store::JOIN_ROWS);
-  const int64_t prow = s * t.cap.P;
+  const int64_t prow0 = store::prow(t, s, 0);
   int32_t pc = 0;
   if (code == JOIN_OK) {
-    t.p_agent[prow] = a.agent_id[ag];
-    t.p_ring[prow] = ring;
-    t.p_sraw[prow] = sg;
-    t.p_seff[prow] = sg;
-    t.p_joined[prow] = t0;
+    t.p_agent[prow0] = a.agent_id[ag];
+    t.p_ring[prow0] = ring;
+    t.p_sraw[prow0] = sg;
+    t.p_seff[prow0] = sg;
+    t.p_joined[prow0] = t0;
     pc = 1;
   } else {
     status = TP_JOIN;
@@ -229,13 +229,13 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
     int32_t retained = 0;
     for (int32_t k = 0; k < D; ++k) retained += (t0 + 1 + k >= tt - a.gc_retention_us) ? 1 : 0;
     t.s_retained[s] = retained;
-    if (committed && pc) t.p_active[prow] = store::P_ACTIVE | store::P_COMMITTED;
-    else if (pc) t.p_active[prow] = store::P_ACTIVE;
+    if (committed && pc) t.p_active[prow0] = store::P_ACTIVE | store::P_COMMITTED;
+    else if (pc) t.p_active[prow0] = store::P_ACTIVE;
     st = SS_ARCHIVED;
   } else {
     t.s_terminated[s] = 0;
     t.s_retained[s] = 0;
-    if (pc) t.p_active[prow] = store::P_ACTIVE;
+    if (pc) t.p_active[prow0] = store::P_ACTIVE;
     if (status == TP_OK) status = TP_TERMINATE;
   }
   t.s_committed[s] = committed ? tt : 0;
@@ -332,7 +332,7 @@ AHV_HD void template_events(const TemplateArgs& a, int64_t i, const PipeCounters
   const int32_t agent = a.agent_id[a.session_agent[i]];
   const int64_t t0 = t.s_created[s];
   const int64_t te = t.s_terminated[s];
-  const int64_t prow = s * t.cap.P;
+  const int64_t prow = store::prow(t, s, 0);
   uint32_t k = 0;
   put(k++, s, EventRec{EV_SESSION_CREATED, -1, t0, 0});
   if (c.v[2]) {

@@ -356,14 +356,22 @@ struct HostCols {
     if (e == "SCR") return c.X;
     throw std::logic_error("unknown extent " + e);
   }
-  void grow_col(const std::string& n, size_t es, int64_t ext) {
+  void grow_col(const std::string& n, size_t es, int64_t ext, bool sp, const sto::Caps& c) {
     std::vector<uint8_t> v(static_cast<size_t>(ext) * es, ones(n) ? 0xFF : 0);
     auto it = col.find(n);
-    if (it != col.end()) std::memcpy(v.data(), it->second.data(), std::min(v.size(), it->second.size()));
+    if (it != col.end()) {
+      if (sp) {  // participant-major [P][S] (store.h prow): each participant plane keeps its rows
+        for (int64_t k = 0; k < c.P; ++k)
+          std::memcpy(v.data() + static_cast<size_t>(k * c.S) * es, it->second.data() + static_cast<size_t>(k * cap.S) * es,
+                      static_cast<size_t>(cap.S) * es);
+      } else {
+        std::memcpy(v.data(), it->second.data(), std::min(v.size(), it->second.size()));
+      }
+    }
     col[n] = std::move(v);
   }
   void resize(const sto::Caps& c) {
-#define AHV_COL(name, type, ext) grow_col(#name, sizeof(type), extent(c, #ext));
+#define AHV_COL(name, type, ext) grow_col(#name, sizeof(type), extent(c, #ext), std::string(#ext) == "SP", c);
     AHV_STORE_COLUMNS(AHV_COL)
 #undef AHV_COL
     cap = c;
