@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 ``--pmc`` CSV output (``pmc_counter_collection.csv``) into a
+"""Summarise rocprofv3 ``--pmc`` output (``pmc_counter_collection.csv`` or the rocpd
+``*_results.db``) into a
 markdown table: one row per kernel, each counter summed over its instances
 (SE/XCD dimensions) per dispatch, then averaged over the kernel's dispatches.
 
@@ -13,13 +14,24 @@ import csv
 import sys
 
 
+def _rows(path: str):
+    """(dispatch id, kernel name, counter, value) from the CSV or the rocpd SQLite database."""
+    if path.endswith(".db"):
+        import sqlite3
+
+        c = sqlite3.connect(path)
+        yield from c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection")
+        return
+    for r in csv.DictReader(open(path)):
+        yield r["Dispatch_Id"], r["Kernel_Name"], r["Counter_Name"], r["Counter_Value"]
+
+
 def summarise(path: str) -> str:
     per_dispatch: dict = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
-    for r in csv.DictReader(open(path)):
-        d = r["Dispatch_Id"]
-        names[d] = r["Kernel_Name"]
-        per_dispatch[d][r["Counter_Name"]] += float(r["Counter_Value"])
+    for d, k, cn, v in _rows(path):
+        names[d] = k
+        per_dispatch[d][cn] += float(v)
     by_kernel: dict = collections.defaultdict(list)
     for d, ctr in per_dispatch.items():
         by_kernel[names[d]].append(ctr)
