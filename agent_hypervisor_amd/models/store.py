@@ -421,24 +421,28 @@ class GovernanceStore:
     def payload(self, off: int, n: int) -> bytes:
         return self._c.payload(off, n)
 
-    def capture(self, slot: int, turn: int, ts_us: int, delta) -> tuple:
+    def capture(self, slot: int, turn: int, ts_us: int, delta, parent: Optional[str] = None) -> tuple:
+        """(delta row, arena offset, length, sequence, predicted digest): the last is
+        the device's digest computed on the host (``parent``: the previous capture's
+        predicted digest; None for turn 1 or when unknown → no prediction)."""
         if self._c.npend(4) >= self.RECLAIM_BATCH:
             self._c.reclaim_pool(4)
-        r = self._c.capture(slot, turn, ts_us, delta)
+        r = self._c.capture(slot, turn, ts_us, delta, parent)
         tries = 0
         while r[0] <= -2:
             self._make_room(r[0], tries)
             tries += 1
-            r = self._c.capture(slot, turn, ts_us, delta)
+            r = self._c.capture(slot, turn, ts_us, delta, parent)
         return r
 
-    def capture_bytes(self, slot: int, turn: int, ts_us: int, raw: bytes, null_at: int) -> tuple:
-        r = self._c.capture_bytes(slot, turn, ts_us, raw, null_at)
+    def capture_bytes(self, slot: int, turn: int, ts_us: int, raw: bytes, null_at: int,
+                      parent: Optional[str] = None) -> tuple:
+        r = self._c.capture_bytes(slot, turn, ts_us, raw, null_at, parent)
         tries = 0
         while r[0] <= -2:
             self._make_room(r[0], tries)
             tries += 1
-            r = self._c.capture_bytes(slot, turn, ts_us, raw, null_at)
+            r = self._c.capture_bytes(slot, turn, ts_us, raw, null_at, parent)
         return r
 
     def restore_delta(self, data: bytes) -> tuple:

@@ -14,8 +14,10 @@
 //            (the chain is inherently serial: ≈2.4 µs per 64-byte block on one
 //            lane, scripts/exp/doorbell2.hip) and completes the capture's result.
 //
-// Commands that read audit state (Merkle root, verify, terminate, reads, FLUSH,
-// NOP = host drain) wait until wave 1 has drained (`needs_drain`).
+// Commands that read audit state wholesale (FLUSH, FREE_ROWS, NOP = host drain,
+// delta reads) wait until wave 1 has drained (`needs_drain`); those that read one
+// session's (Merkle root, verify, terminate, header read) wait only for that
+// session's queued captures (`session_drain`).
 //
 // Measured transport (scripts/exp/doorbell2.hip): one host→device→host round
 // trip of a 512-byte command ≈3.1 µs p50, vs ≈12 µs for a kernel launch + sync.
@@ -279,6 +281,18 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     c.inl = inl;
     if (needs_drain(c.op)) {
       while (lds_acquire(&q_done) != queued) __builtin_amdgcn_s_sleep(1);
+      if (c.op == OP_FREE_ROWS) {  // no provisional tree still writing a row about to be freed
+        while (lds_acquire(&spec_s) != 0u) __builtin_amdgcn_s_sleep(1);
+      }
+    } else if (session_drain(c.op)) {
+      // only this session's captures: lane k checks queued job done+k (≤ kJobs pending)
+      const int64_t s = static_cast<int64_t>(c.a[0]);
+      for (;;) {
+        const uint32_t d0 = lds_acquire(&q_done);
+        const bool mine = static_cast<uint32_t>(lane) < queued - d0 && jobs[(d0 + lane) % kJobs].s == s;
+        if (__ballot(mine) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
     if (c.op == OP_SESS_CLOSE || c.op == OP_DELTA_MERKLE) {  // wait for the tree in flight
       const uint32_t want = static_cast<uint32_t>(c.a[0]) + 1u;

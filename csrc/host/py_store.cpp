@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "ahv/host_sha.h"
 #include "ahv/store_host.h"
 
 namespace py = pybind11;
@@ -129,21 +130,86 @@ class Store : public StoreCore {
 
   // DeltaEngine.capture: render the canonical payload around a null parent
   // (py_audit.cpp), then place it (StoreCore::capture_rendered).
-  // Returns (delta index, payload offset, payload length, sequence).
-  py::tuple capture(int64_t slot, int64_t turn, int64_t ts_us, py::handle delta) {
+  // Returns (delta index, payload offset, payload length, sequence, predicted
+  // digest): the digest the device will compute, hashed here with SHA-NI over
+  // the same bytes (turn 1: the record as rendered; later turns: with `parent`,
+  // the previous capture's predicted hex digest, spliced in quoted) — None when
+  // the parent is not known.  The caller verifies it against the device later.
+  py::tuple capture(int64_t slot, int64_t turn, int64_t ts_us, py::handle delta, const py::object& parent) {
     thread_local std::string buf;
     size_t at = 0;
-    if (!render_delta(delta.ptr(), buf, &at)) return py::make_tuple(-1, -1, -1, -1);
+    if (!render_delta(delta.ptr(), buf, &at)) return py::make_tuple(-1, -1, -1, -1, py::none());
     const Placed p = capture_rendered(slot, turn, ts_us, buf, at);
-    return py::make_tuple(p.didx, p.off, p.len, p.seq);
+    return py::make_tuple(p.didx, p.off, p.len, p.seq, p.didx >= 0 ? predict(buf, at, turn, parent) : py::none());
   }
 
-  py::tuple capture_bytes(int64_t slot, int64_t turn, int64_t ts_us, const py::bytes& payload, int64_t null_at) {
+  py::tuple capture_bytes(int64_t slot, int64_t turn, int64_t ts_us, const py::bytes& payload, int64_t null_at,
+                          const py::object& parent) {
     std::string buf = payload;
     if (null_at < 0 || static_cast<size_t>(null_at) + 4 > buf.size() || buf.compare(null_at, 4, "null") != 0)
       throw std::invalid_argument("capture_bytes: null_at does not point at the parent's null");
     const Placed p = capture_rendered(slot, turn, ts_us, buf, static_cast<size_t>(null_at));
-    return py::make_tuple(p.didx, p.off, p.len, p.seq);
+    return py::make_tuple(p.didx, p.off, p.len, p.seq,
+                          p.didx >= 0 ? predict(buf, static_cast<size_t>(null_at), turn, parent) : py::none());
+  }
+
+  static py::object predict(const std::string& buf, size_t at, int64_t turn, const py::object& parent) {
+    uint32_t h[8];
+    if (turn <= 1) {
+      host::sha256_bytes(reinterpret_cast<const uint8_t*>(buf.data()), buf.size(), h);
+    } else {
+      if (parent.is_none() || !PyUnicode_Check(parent.ptr())) return py::none();
+      Py_ssize_t n = 0;
+      const char* ph = PyUnicode_AsUTF8AndSize(parent.ptr(), &n);
+      if (ph == nullptr || n != 64) {
+        PyErr_Clear();
+        return py::none();
+      }
+      thread_local std::string rec;
+      rec.assign(buf.data(), at);
+      rec.push_back('"');
+      rec.append(ph, 64);
+      rec.push_back('"');
+      rec.append(buf.data() + at + 4, buf.size() - at - 4);
+      host::sha256_bytes(reinterpret_cast<const uint8_t*>(rec.data()), rec.size(), h);
+    }
+    PyObject* out = PyUnicode_New(64, 127);
+    if (out == nullptr) throw py::error_already_set();
+    host::hex_bytes(h, PyUnicode_1BYTE_DATA(out));
+    return py::reinterpret_steal<py::object>(out);
+  }
+
+  // Reference Merkle root over predicted hex digests (SHA-NI), or None when one
+  // is missing or not canonical hex.
+  static py::object merkle_predict(const py::list& leaves) {
+    const size_t n = leaves.size();
+    if (n == 0) return py::none();
+    std::vector<uint32_t> level(8 * n);
+    for (size_t i = 0; i < n; ++i) {
+      PyObject* o = leaves[i].ptr();
+      if (!PyUnicode_Check(o) || PyUnicode_GET_LENGTH(o) != 64 || PyUnicode_KIND(o) != PyUnicode_1BYTE_KIND)
+        return py::none();
+      const uint8_t* c = PyUnicode_1BYTE_DATA(o);
+      for (int w = 0; w < 8; ++w) {
+        uint32_t x = 0;
+        for (int k = 0; k < 8; ++k) {
+          const uint8_t ch = c[8 * w + k];
+          uint32_t v;
+          if (ch >= '0' && ch <= '9') v = ch - '0';
+          else if (ch >= 'a' && ch <= 'f') v = ch - 'a' + 10;
+          else return py::none();
+          x = (x << 4) | v;
+        }
+        level[8 * i + w] = x;
+      }
+    }
+    if (n == 1) return leaves[0];
+    uint32_t root[8];
+    host::merkle_root_host(level.data(), n, root);
+    PyObject* out = PyUnicode_New(64, 127);
+    if (out == nullptr) throw py::error_already_set();
+    host::hex_bytes(root, PyUnicode_1BYTE_DATA(out));
+    return py::reinterpret_steal<py::object>(out);
   }
 
   py::tuple restore_delta(const py::bytes& b) {
@@ -233,8 +299,11 @@ void register_store(py::module_& m) {
       .def("write_payload", &Store::write_payload)
       .def("write_records", &Store::write_records)
       .def("payload_gather", &Store::payload_gather, py::arg("offs"), py::arg("lens"))
-      .def("capture", &Store::capture)
-      .def("capture_bytes", &Store::capture_bytes)
+      .def("capture", &Store::capture, py::arg("slot"), py::arg("turn"), py::arg("ts_us"), py::arg("delta"),
+           py::arg("parent") = py::none())
+      .def("capture_bytes", &Store::capture_bytes, py::arg("slot"), py::arg("turn"), py::arg("ts_us"),
+           py::arg("payload"), py::arg("null_at"), py::arg("parent") = py::none())
+      .def_static("merkle_predict", &Store::merkle_predict)
       .def("restore_delta", &Store::restore_delta)
       .def("free_deltas", &Store::free_deltas)
       .def("free_deltas_arr", [](Store& st, I32Array a) { st.free_deltas(std::vector<int32_t>(a.data(), a.data() + a.size())); })

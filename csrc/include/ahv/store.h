@@ -235,6 +235,11 @@ enum ExecResult : int { EXEC_STOP = 0, EXEC_DONE = 1, EXEC_DEFERRED = 2 };
 // (delta digests, chain heads) or that publish table state wholesale; the
 // command wave drains the hash queue before executing them.
 AHV_HD bool needs_drain(uint32_t op);
+// Commands that read the audit state of ONE session (a0): the command wave waits
+// only until no queued capture of that session is pending — captures of other
+// sessions keep hashing alongside (many pipelines in flight never serialise on
+// the engine).
+AHV_HD bool session_drain(uint32_t op);
 
 // Result / bulk-output stores.  On the device these land in pinned host memory,
 // so they are system-scope stores (vector stores that bypass the caches).
@@ -1898,10 +1903,24 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
 
 // ------------------------------------------------------------- dispatch
 
+AHV_HD bool session_drain(uint32_t op) {
+  switch (op) {
+    case OP_SESS_CLOSE:
+    case OP_DELTA_MERKLE:
+    case OP_DELTA_VERIFY:
+    case OP_SESS_READ:
+      return true;
+    default:
+      return false;
+  }
+}
+
 AHV_HD bool needs_drain(uint32_t op) {
   if (op == OP_DELTA_CAPTURE) return false;
   if (op >= 40 && op < 80) return false;  // liability and saga rows: no audit state
+  if (session_drain(op)) return false;
   switch (op) {
+    case OP_SESS_CREATE:  // claims a FREE row: no queued capture refers to it (FREE_ROWS drained)
     case OP_SESS_JOIN:
     case OP_SESS_LEAVE:
     case OP_SESS_ACTIVATE:

@@ -142,8 +142,19 @@ class StoreCore {
     const size_t res_bytes = static_cast<size_t>(nslots_) * store::kResWords * 8;
     if (gpu_) {
       hip_check(hipSetDevice(device_), "hipSetDevice");
-      hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&ring_), ring_bytes, hipDeviceMallocFinegrained),
-                "store ring");
+      // The command ring: fine-grained device memory by default, written through
+      // the BAR with 32-byte stores, so the worker's slot reads stay in HBM.
+      // AHV_STORE_RING=host puts it in pinned host memory (cached host stores,
+      // but every worker read crosses PCIe: measured 2.47 us vs 1.77 us per NOP
+      // of worker throughput, profiles/r4/worker_probe_r4h_*.json).
+      const char* rm = std::getenv("AHV_STORE_RING");
+      ring_host_ = rm != nullptr && std::string(rm) == "host";
+      if (ring_host_) {
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&ring_), ring_bytes, hipHostMallocCoherent), "store ring");
+      } else {
+        hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&ring_), ring_bytes, hipDeviceMallocFinegrained),
+                  "store ring");
+      }
       hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&staging_), static_cast<size_t>(staging_cap_),
                                       hipDeviceMallocFinegrained),
                 "store staging");
@@ -155,7 +166,8 @@ class StoreCore {
                 "store bulk");
       hip_check(hipHostMalloc(reinterpret_cast<void**>(&alive_), 64, hipHostMallocCoherent), "store ctl");
       hip_check(hipHostMalloc(reinterpret_cast<void**>(&tail_), 64, hipHostMallocCoherent), "store tail");
-      hip_check(hipMemset(ring_, 0, ring_bytes), "memset ring");
+      if (ring_host_) std::memset(ring_, 0, ring_bytes);
+      else hip_check(hipMemset(ring_, 0, ring_bytes), "memset ring");
       std::memset(tail_, 0, 64);  // [0] next sequence, [1..4] worker telemetry
       hip_check(hipDeviceSynchronize(), "store init sync");
       hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "store stream");
@@ -202,7 +214,8 @@ class StoreCore {
     } catch (...) {
     }
     if (gpu_) {
-      (void)hipFree(ring_);
+      if (ring_host_) (void)hipHostFree(ring_);
+      else (void)hipFree(ring_);
       (void)hipFree(staging_);
       (void)hipFree(payload_);
       (void)hipHostFree(res_);
@@ -323,13 +336,36 @@ class StoreCore {
       r[0] = q + 1;
       return q;
     }
-    volatile uint64_t* slot = ring_ + idx * kSlotWords;
-    for (int k = 1; k < kSlotWords; ++k) slot[k] = w[k];
-    _mm_sfence();
-    slot[0] = q + 1;
-    _mm_sfence();
+    uint64_t* slot = ring_ + idx * kSlotWords;
+    if (ring_host_) {
+      // cached stores; x86 keeps them in order, and the worker rejects a torn read
+      // through the checksum, so the sequence word goes last
+      std::memcpy(slot + 1, w + 1, 8 * (kSlotWords - 1));
+      __atomic_store_n(slot, q + 1, __ATOMIC_RELEASE);
+    } else if (__builtin_cpu_supports("avx2")) {
+      write_slot_bar(slot, w, q + 1);
+    } else {
+      volatile uint64_t* v = slot;
+      for (int k = 1; k < kSlotWords; ++k) v[k] = w[k];
+      _mm_sfence();
+      v[0] = q + 1;
+      _mm_sfence();
+    }
     ensure_worker();
     return q;
+  }
+
+  // A slot in device memory through the BAR: 32-byte stores (16 PCIe writes for
+  // the 512-byte slot instead of 63), the sequence word last.
+  __attribute__((target("avx2"))) static void write_slot_bar(uint64_t* slot, const uint64_t* w, uint64_t seq) {
+    uint64_t first[4] = {0, w[1], w[2], w[3]};  // word 0 (sequence) stays "not ready" until the end
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(slot), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(first)));
+    for (int k = 4; k < store::kSlotWords; k += 4)
+      _mm256_storeu_si256(reinterpret_cast<__m256i*>(slot + k),
+                          _mm256_loadu_si256(reinterpret_cast<const __m256i*>(w + k)));
+    _mm_sfence();
+    *reinterpret_cast<volatile uint64_t*>(slot) = seq;
+    _mm_sfence();
   }
 
   void ensure_worker() {
@@ -837,6 +873,7 @@ class StoreCore {
   int64_t bulk_cap_;
   Tables t_{};
   uint64_t* ring_ = nullptr;
+  bool ring_host_ = false;  // command ring in pinned host memory (else fine-grained device memory)
   uint8_t* staging_ = nullptr;
   uint8_t* payload_ = nullptr;
   uint64_t* res_ = nullptr;

@@ -67,6 +67,10 @@ _S_CREATED, _S_HANDSHAKING, _S_ACTIVE = (_STATES.index(x) for x in (SessionState
 # A/B switch: joins / activations / step transitions whose outcome the host already knows
 # are posted without waiting for the device (verified later; GovernanceStore.post_checked)
 _SPEC_LIFECYCLE = os.environ.get("AHV_SPEC_LIFECYCLE", "1") != "0"
+# ... and a terminate whose Merkle root the host predicted from its SHA-NI digest
+# predictions (K08/K09 on the host beside the device; the device's own root is what
+# it commits, and it must equal the prediction)
+_SPEC_TERMINATE = os.environ.get("AHV_SPEC_TERMINATE", "1") != "0"
 _STEPS = list(StepState)
 _STEP_IDX = {**{x: i for i, x in enumerate(_STEPS)}, **{x.value: i for i, x in enumerate(_STEPS)}}
 _SAGAS = list(SagaState)
@@ -517,7 +521,7 @@ class DeviceDelta(SemanticDelta):
         self.__dict__.update(
             delta_id=delta_id, turn_id=turn_id, session_id=session_id, agent_did=agent_did, timestamp=timestamp,
             changes=changes, _store=engine._store, _prev=prev, _dev_hash=None, _hash_override=None,
-            _parent_override=None, _didx=-1, _poff=-1, _plen=0, _seq=-1, _dirty=False,
+            _parent_override=None, _didx=-1, _poff=-1, _plen=0, _seq=-1, _dirty=False, _pred=None, _tsu=0,
         )
 
     _FIELDS = frozenset(("delta_id", "turn_id", "session_id", "agent_did", "timestamp", "changes"))
@@ -611,13 +615,17 @@ class DeviceDeltaEngine(DeltaEngine):
         ts = _now()
         prev = self._deltas[-1] if self._deltas else None
         d = DeviceDelta(self, delta_id or f"delta:{turn}", turn, self.session_id, agent_did, ts, changes, prev)
-        didx, off, ln, seq = self._store.capture(self.slot, turn, to_us(ts), d)
+        # the device's digest, predicted on the host from the same bytes and the
+        # previous prediction (terminate then needs no wait for the hash engine)
+        parent = prev.__dict__["_pred"] if prev is not None else None
+        tsu = to_us(ts)
+        didx, off, ln, seq, pred = self._store.capture(self.slot, turn, tsu, d, parent)
         if didx < 0:  # field types the native renderer defers to json.dumps
             raw = _payload_json(_NullParent(d)).encode()
             at = raw.index(b'"parent_hash": null') + len(b'"parent_hash": ')
-            didx, off, ln, seq = self._store.capture_bytes(self.slot, turn, to_us(ts), raw, at)
+            didx, off, ln, seq, pred = self._store.capture_bytes(self.slot, turn, tsu, raw, at, parent)
         self._rows.append(didx)
-        d.__dict__.update(_didx=didx, _poff=off, _plen=ln, _seq=seq)
+        d.__dict__.update(_didx=didx, _poff=off, _plen=ln, _seq=seq, _pred=pred, _tsu=tsu)
         self._turn_counter = turn
         self._deltas.append(d)
         return d
@@ -685,6 +693,48 @@ class DeviceDeltaEngine(DeltaEngine):
         n = len(self._deltas) - len(keep)
         self._deltas = keep
         return n
+
+
+def close_prediction(sso, de: "DeviceDeltaEngine", vsess: int, audit: bool, cutoff_us: int):
+    """(root, expired) the device's OP_SESS_CLOSE of this session will produce, when
+    the host knows it: the row is mirrored in a state terminate accepts, the session
+    holds no liability rows (their release is awaited), and every delta of the chain
+    was captured here with a predicted digest.  None otherwise (the caller awaits)."""
+    if not _SPEC_TERMINATE or vsess >= 0 or sso._poisoned is not None:
+        return None
+    if sso._m_state != _S_ACTIVE and sso._m_state != _S_HANDSHAKING:
+        return None
+    ds = de._deltas
+    if len(ds) != de._turn_counter:
+        return None
+    preds = [d.__dict__["_pred"] for d in ds]
+    if None in preds:
+        return None
+    root = None
+    if audit and preds:
+        root = de._store._c.merkle_predict(preds)
+        if root is None:
+            return None
+    expired = 0
+    for d in ds:
+        if d.__dict__["_tsu"] < cutoff_us:
+            expired += 1
+    return root, expired
+
+
+def close_check(slot: int, root: Optional[str], expired: int):
+    """The deferred check of a speculated close: the device's status, root and GC count."""
+
+    def check(r):
+        if r[0]:
+            return _st.StoreError(f"speculated terminate of row {slot} refused by the device (status {r[0]})")
+        if root is not None and (not r[1] or _hex(r[2:10]) != root):
+            return _st.StoreError(f"device Merkle root of row {slot} differs from the host prediction")
+        if int(r[11]) != expired:
+            return _st.StoreError(f"device GC count of row {slot} differs from the host prediction")
+        return None
+
+    return check
 
 
 def _resolve(store: GovernanceStore, d: DeviceDelta) -> str:

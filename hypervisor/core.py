@@ -287,14 +287,22 @@ class Hypervisor:
         guard = getattr(sso, "_guard", None)
         if guard is not None:  # a speculation of this session the device refused raises here
             guard()
-        sso._m_forget()  # the row leaves the mirrored states (terminate → archive)
         now_us = _d._now_us()
         v = st.liability_lookup(self._tenant, session_id)
         cutoff = now_us - int(self.gc.policy.delta_retention_days * 86_400_000_000)
         n, off, inl = st.index_args(de._indices())
-        r = await st.call_async(
-            _d._st.OP_SESS_CLOSE, [sso.slot, n, off, now_us, v, cutoff, int(bool(sso.config.enable_audit))], 13, inl,
-        )
+        audit = bool(sso.config.enable_audit)
+        args = [sso.slot, n, off, now_us, v, cutoff, int(audit)]
+        spec = _d.close_prediction(sso, de, v, audit, cutoff) if guard is not None else None
+        sso._m_forget()  # the row leaves the mirrored states (terminate → archive)
+        if spec is not None:
+            # the host knows the outcome (root from its digest predictions): post the
+            # close without waiting for the hash engine; the device's answer is
+            # checked later and a disagreement goes to this session (post_checked)
+            root, expired = spec
+            st.post_checked(_d._st.OP_SESS_CLOSE, args, 12, _d.close_check(sso.slot, root, expired), inl, owner=sso)
+            return self._terminated(session_id, sso, de, root, expired, n)
+        r = await st.call_async(_d._st.OP_SESS_CLOSE, args, 13, inl)
         if guard is not None and st._deferred:
             # every post before the close has completed now: a prediction of this
             # session that the device refused is this terminate's error
@@ -308,11 +316,14 @@ class Hypervisor:
         root = _d._hex(r[2:10]) if r[1] else None
         if v >= 0:  # every bond of the session is released now: freeze the records, reuse the edge rows
             self.vouching.retire_session(session_id)
+        return self._terminated(session_id, sso, de, root, int(r[11]), n)
+
+    def _terminated(self, session_id: str, sso, de, root: Optional[str], expired: int, n: int) -> Optional[str]:
+        """Host bookkeeping after a device close: commitment, GC, events."""
         if root:
             self.commitment.register(sso)
-        # the device counted the deltas past retention (r[12]); with none expired the
-        # host GC has nothing to prune and needs no walk over the delta views
-        expired = int(r[12])
+        # the device counted the deltas past retention (result word 12); with none
+        # expired the host GC has nothing to prune and needs no walk over the views
         self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de if expired else None,
                         delta_count=de.turn_count if expired else n)
         if self.event_bus is not None:
