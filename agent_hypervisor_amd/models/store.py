@@ -361,6 +361,21 @@ class GovernanceStore:
         self.defer(q, nres, check, owner)
         return q
 
+    def post_expect(self, op: int, args: list, want: tuple, token: tuple, inline: Optional[bytes] = None) -> int:
+        """The fast form of :meth:`post_checked`: the prediction is the leading result
+        words ``want`` (None = any value), checked natively in post order; a mismatch
+        hands ``token`` = (owner, make_error, arg) to :meth:`verify_deferred`, which
+        raises ``make_error(arg, result)`` in the owner's next call (or here, unowned)."""
+        return self._c.post_expect(op, args, inline, want, token)
+
+    def expect(self, seq: int, want: tuple, token: tuple) -> None:
+        """:meth:`post_expect` for a command already posted."""
+        self._c.expect(seq, want, token)
+
+    def pending_checks(self) -> int:
+        """Speculated posts not verified yet."""
+        return len(self._deferred) + self._c.n_expects()
+
     def defer(self, seq: int, nres: int, check, owner=None) -> None:
         """Verify a kept post (``post(..., keep=True)``) later instead of awaiting it."""
         self._deferred.append((seq, nres, check, owner))
@@ -373,11 +388,22 @@ class GovernanceStore:
         unowned prediction raises here."""
         if block:
             self._c.check_frees(True)  # row reclaims posted without waiting (native allocator)
+        bad = self._c.verify_expects(block)
+        err = None
+        if bad is not None:
+            for (owner, make, arg), r in bad:
+                e = make(arg, r)
+                if owner is not None:
+                    owner._spec_failed(e)
+                elif err is None:
+                    err = e
         ds = self._deferred
         if not ds:
+            if err is not None:
+                raise err
             return
         self._deferred = []
-        pending, err, misses = [], None, 0
+        pending, misses = [], 0
         try_result = self._c.try_result
         for i, d in enumerate(ds):
             r = try_result(d[0], d[1], 1_000_000_000 if block else 0)
@@ -405,8 +431,7 @@ class GovernanceStore:
         self._c.discard(seq)
 
     def call(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
-        if self._deferred:
-            self.verify_deferred()
+        self.verify_deferred()
         return self._c.call(op, args, nres, inline)
 
     def result(self, seq: int, nres: int = 4) -> tuple:
@@ -520,8 +545,7 @@ class GovernanceStore:
             self._polling = False
 
     async def call_async(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
-        if self._deferred:
-            self.verify_deferred()
+        self.verify_deferred()
         return await self.result_async(self._c.post(op, args, inline), nres)
 
     def drain(self) -> None:

@@ -6,6 +6,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
+#include <deque>
+
 #include "ahv/host_sha.h"
 #include "ahv/store_host.h"
 
@@ -83,6 +86,78 @@ class Store : public StoreCore {
     }
     return words(r, nres);
   }
+
+  // ---- speculation: posted commands whose results the caller predicted ----
+  //
+  // An expectation is the leading result words a kept post must produce (None:
+  // any value).  They are checked here, in post order, without a Python call per
+  // result; only a mismatch hands its token (and the device's words) back to the
+  // caller, which turns it into the prediction owner's error.
+  struct Expect {
+    uint64_t seq;
+    uint32_t mask;
+    uint64_t want[kSaveWords - 1];
+    py::object token;
+  };
+  std::deque<Expect> expects_;
+  py::list expect_bad_;  // mismatches found by an automatic blocking pass
+  static constexpr size_t kExpectMax = 512;  // pending expectations before a blocking pass
+
+  void expect(uint64_t q, const py::tuple& want, py::object token) {
+    keep(q);
+    Expect e;
+    e.seq = q;
+    e.mask = 0;
+    const size_t n = std::min<size_t>(want.size(), kSaveWords - 1);
+    for (size_t k = 0; k < n; ++k) {
+      py::handle w = want[k];
+      if (w.is_none()) continue;
+      e.mask |= 1u << k;
+      e.want[k] = static_cast<uint64_t>(w.cast<int64_t>());
+    }
+    e.token = std::move(token);
+    expects_.push_back(std::move(e));
+    if (expects_.size() >= kExpectMax) {
+      py::object bad = verify_expects(true);
+      if (!bad.is_none())
+        for (auto b : py::reinterpret_borrow<py::list>(bad)) expect_bad_.append(b);
+    }
+  }
+
+  uint64_t post_expect(uint32_t op, const std::vector<int64_t>& args, const py::object& inl, const py::tuple& want,
+                       py::object token) {
+    const uint64_t q = post(op, args, inl);
+    expect(q, want, std::move(token));
+    return q;
+  }
+
+  // Check the expectations whose results are in (all of them with `block`);
+  // returns [(token, result words)] for the mismatches, or None.
+  py::object verify_expects(bool block) {
+    if (expects_.empty() && expect_bad_.size() == 0) return py::none();
+    py::list bad = expect_bad_;
+    expect_bad_ = py::list();
+    while (!expects_.empty()) {
+      Expect& e = expects_.front();
+      uint64_t r[kSaveWords];
+      if (!try_result_raw(e.seq, 0, r)) {
+        if (!block) break;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!try_result_raw(e.seq, 1000000, r)) {
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+            throw std::runtime_error("store: speculated command " + std::to_string(e.seq) + " never completed");
+        }
+      }
+      bool ok = true;
+      for (int k = 0; k < kSaveWords - 1 && ok; ++k)
+        if ((e.mask >> k) & 1u) ok = r[1 + k] == e.want[k];
+      if (!ok) bad.append(py::make_tuple(e.token, words(r, kSaveWords - 1)));
+      expects_.pop_front();
+    }
+    return bad.size() ? py::object(bad) : py::object(py::none());
+  }
+
+  size_t n_expects() const { return expects_.size(); }
 
   int64_t stage(const py::bytes& b) {
     std::string_view v = b;
@@ -288,6 +363,11 @@ void register_store(py::module_& m) {
            py::arg("max_ms") = 2000)
       .def("post", &Store::post, py::arg("op"), py::arg("args"), py::arg("inline") = py::none())
       .def("keep", &Store::keep, py::arg("seq"))
+      .def("expect", &Store::expect, py::arg("seq"), py::arg("want"), py::arg("token"))
+      .def("post_expect", &Store::post_expect, py::arg("op"), py::arg("args"), py::arg("inline"), py::arg("want"),
+           py::arg("token"))
+      .def("verify_expects", &Store::verify_expects, py::arg("block") = false)
+      .def("n_expects", &Store::n_expects)
       .def("discard", &Store::discard, py::arg("seq"))
       .def("call", &Store::call, py::arg("op"), py::arg("args"), py::arg("nres") = 4, py::arg("inline") = py::none())
       .def("result", &Store::result, py::arg("seq"), py::arg("nres") = 4)

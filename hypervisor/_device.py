@@ -187,9 +187,7 @@ class DeviceSession(SharedSessionObject):
                 # so a row holding another session (a refused create) refuses them on the device
                 self._stamp = _i64(stamp)
                 slot = self.slot
-                store.post_checked(_st.OP_SESS_CREATE, args, 2, lambda r: None if r[0] == 0 else _st.StoreError(
-                    f"device refused to create session in row {slot} (row state {r[1]}): allocator invariant violated"),
-                    owner=self)
+                store.post_expect(_st.OP_SESS_CREATE, args, _OK, (self, _create_refused, slot))
             else:
                 self._cseq = store.post(_st.OP_SESS_CREATE, args)
 
@@ -212,9 +210,7 @@ class DeviceSession(SharedSessionObject):
     def _guard(self) -> None:
         """Raise this session's speculation failure, if any (after checking the
         predictions whose results are in)."""
-        st = self._store
-        if st._deferred:
-            st.verify_deferred()
+        self._store.verify_deferred()
         if self._poisoned is not None:
             raise self._poisoned
 
@@ -313,10 +309,7 @@ class DeviceSession(SharedSessionObject):
     def _activate_speculated(self) -> None:
         """The row is HANDSHAKING with ≥ 1 participant row: the device will accept."""
         slot = self.slot
-        self._store.post_checked(_st.OP_SESS_ACTIVATE, [slot, self._stamp], 2,
-                                 lambda r: None if r[0] == 0 else _st.StoreError(
-                                     f"speculated activate of row {slot} refused by the device (status {r[0]})"),
-                                 owner=self)
+        self._store.post_expect(_st.OP_SESS_ACTIVATE, [slot, self._stamp], _OK, (self, _activate_refused, slot))
         self._m_state = _S_ACTIVE
 
     def activate(self) -> None:
@@ -379,10 +372,7 @@ class DeviceSession(SharedSessionObject):
         if code:
             return None
         slot = self.slot
-        self._store.post_checked(_st.OP_SESS_JOIN, args, 6,
-                                 lambda r: None if r[0] == 0 and r[1] == ring else _st.StoreError(
-                                     f"speculated join to row {slot} diverged from the device (status {r[0]})"),
-                                 owner=self)
+        self._store.post_expect(_st.OP_SESS_JOIN, args, (0, int(ring)), (self, _join_diverged, slot))
         rows[aid] = True
         self._m_active += 1
         return ring
@@ -722,19 +712,34 @@ def close_prediction(sso, de: "DeviceDeltaEngine", vsess: int, audit: bool, cuto
     return root, expired
 
 
-def close_check(slot: int, root: Optional[str], expired: int):
-    """The deferred check of a speculated close: the device's status, root and GC count."""
+def close_expect(root: Optional[str], expired: int) -> tuple:
+    """The result words a speculated close must produce: status 0, the root flag and
+    words (when a root is predicted), any release count, the GC count."""
+    if root is None:
+        return (0, None, None, None, None, None, None, None, None, None, None, expired)
+    return (0, 1, *struct.unpack(">8I", bytes.fromhex(root)), None, expired)
 
-    def check(r):
-        if r[0]:
-            return _st.StoreError(f"speculated terminate of row {slot} refused by the device (status {r[0]})")
-        if root is not None and (not r[1] or _hex(r[2:10]) != root):
-            return _st.StoreError(f"device Merkle root of row {slot} differs from the host prediction")
-        if int(r[11]) != expired:
-            return _st.StoreError(f"device GC count of row {slot} differs from the host prediction")
-        return None
 
-    return check
+def _close_diverged(slot: int, r: tuple) -> Exception:
+    if r[0]:
+        return _st.StoreError(f"speculated terminate of row {slot} refused by the device (status {r[0]})")
+    return _st.StoreError(f"device Merkle root / GC count of row {slot} differs from the host prediction")
+
+
+def _create_refused(slot: int, r: tuple) -> Exception:
+    return _st.StoreError(f"device refused to create session in row {slot} (row state {r[1]}): "
+                          "allocator invariant violated")
+
+
+def _activate_refused(slot: int, r: tuple) -> Exception:
+    return _st.StoreError(f"speculated activate of row {slot} refused by the device (status {r[0]})")
+
+
+def _join_diverged(slot: int, r: tuple) -> Exception:
+    return _st.StoreError(f"speculated join to row {slot} diverged from the device (status {r[0]})")
+
+
+_OK = (0,)  # a speculated post's expected result: status 0
 
 
 def _resolve(store: GovernanceStore, d: DeviceDelta) -> str:
@@ -1142,6 +1147,12 @@ class DeviceCommitmentEngine(CommitmentEngine):
 _SPECULATE = os.environ.get("AHV_STEP_SPECULATE", "1") != "0"  # A/B switch for the posted EXECUTING transition
 
 
+def _transition_refused(arg, r: tuple) -> Exception:
+    slot, state = arg
+    return _st.StoreError(f"speculated {state.value} transition of step row {slot} refused by the device "
+                          f"(from state {_STEPS[r[1]].value if r[1] < len(_STEPS) else r[1]})")
+
+
 def _transition_check(slot: int, state: StepState):
     def check(r: tuple):
         if r[0] == 0:
@@ -1413,9 +1424,9 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                     # EXECUTING: neither needs the device's answer before returning —
                     # both are verified with the store's next interaction
                     st = self._store
-                    st.defer(seq, 2, _transition_check(step.slot, StepState.EXECUTING), self._owner)
+                    st.expect(seq, _OK, (self._owner, _transition_refused, (step.slot, StepState.EXECUTING)))
                     cseq = step.post_transition(StepState.COMMITTED)
-                    st.defer(cseq, 2, _transition_check(step.slot, StepState.COMMITTED), self._owner)
+                    st.expect(cseq, _OK, (self._owner, _transition_refused, (step.slot, StepState.COMMITTED)))
                     step.__dict__["_hint"] = StepState.COMMITTED
                     return result
                 if seq is not None:

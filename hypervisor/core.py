@@ -300,10 +300,11 @@ class Hypervisor:
             # close without waiting for the hash engine; the device's answer is
             # checked later and a disagreement goes to this session (post_checked)
             root, expired = spec
-            st.post_checked(_d._st.OP_SESS_CLOSE, args, 12, _d.close_check(sso.slot, root, expired), inl, owner=sso)
+            st.post_expect(_d._st.OP_SESS_CLOSE, args, _d.close_expect(root, expired), (sso, _d._close_diverged, sso.slot),
+                           inl)
             return self._terminated(session_id, sso, de, root, expired, n)
         r = await st.call_async(_d._st.OP_SESS_CLOSE, args, 13, inl)
-        if guard is not None and st._deferred:
+        if guard is not None:
             # every post before the close has completed now: a prediction of this
             # session that the device refused is this terminate's error
             st.verify_deferred()

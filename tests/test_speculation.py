@@ -33,7 +33,7 @@ def test_known_outcomes_are_posted_without_waiting(dev):
         m = await hv.create_session(SessionConfig(max_participants=2), "did:admin")
         sid = m.sso.session_id
         ring = await hv.join_session(sid, "did:a", sigma_raw=0.8)
-        assert len(st._deferred) >= 1  # the join was speculated
+        assert st.pending_checks() >= 1  # the join was speculated
         await hv.activate_session(sid)
         g = m.saga.create_saga(sid)
         s1 = m.saga.add_step(g.saga_id, "a", "did:a", "/x")
@@ -257,8 +257,8 @@ def test_terminate_root_is_predicted_and_equals_the_devices(dev):
         hv = Hypervisor(device=dev)
         st = hv._store
         posted = []
-        real = st.post_checked
-        st.post_checked = lambda op, *a, **k: (posted.append(op), real(op, *a, **k))[1]
+        real = st.post_expect
+        st.post_expect = lambda op, *a, **k: (posted.append(op), real(op, *a, **k))[1]
         for n in range(1, 10):
             m = await hv.create_session(SessionConfig(enable_audit=True), "did:admin")
             sid = m.sso.session_id
