@@ -220,6 +220,10 @@ class GovernanceStore:
 
     def release_many(self, kind: str, rows) -> None:
         """Queue many rows: an int sequence or an int32 array (one native call)."""
+        if type(rows) is list:
+            if len(rows) <= 64:
+                self._c.release_list(_KIND[kind], rows)
+                return
         if len(rows):
             self._c.release_rows(_KIND[kind], np.ascontiguousarray(rows, dtype=np.int32))
 

@@ -35,14 +35,15 @@ REFERENCE_JOINS = (("did:mesh:a", 0.8),)
 REFERENCE_DELTAS = tuple(("did:mesh:a", ((f"/f{i}", "add", f"h{i}"),)) for i in range(3))
 REFERENCE_STEPS = (("action", "did:mesh:a", "/api/action", None, 0, 0),)
 
-# A/B switches of the batch kernels' work layout (AHV_SP_ORDER bit0 chain lanes by work,
-# bit1 render lanes by record shape with co-located arena space; AHV_SP_PREFIX=render|kernel: where the records'
-# parent-independent SHA blocks are compressed)
+# A/B switches of the batch kernels' work layout (AHV_SP_ORDER bit0 chain lanes by work, bit1
+# render lanes by record shape with co-located arena space, bit2 K09 lanes by chain length;
+# AHV_SP_PREFIX: where the records' parent-independent SHA blocks are compressed)
 import os as _os  # noqa: E402
 
 _SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "1"))
-_SP_PREFIX = _os.environ.get("AHV_SP_PREFIX", "render")  # render | kernel | chain (no split: the chain lane hashes all)
-_SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX == "kernel" else 1
+# render | kernel | sorted (its own kernel, lanes grouped by SHA work) | chain (no split: the chain lane hashes all)
+_SP_PREFIX = _os.environ.get("AHV_SP_PREFIX", "render")
+_SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX in ("kernel", "sorted") else 1
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
            5: "terminate_refused", 6: "record_overflow"}
@@ -505,11 +506,16 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         tens["chain_order"] = T(np.argsort(-work, kind="stable").astype(np.int32))
     if render_order is not None:
         tens["render_order"] = T(render_order)
+    if _SP_PREFIX == "sorted" and nd:
+        # prefix SHA lanes grouped by work: turn-1 records (hashed whole) first, then by
+        # reserved size (∝ the blocks before the parent hole), so a wave's lanes finish together
+        tens["prefix_order"] = T(np.lexsort((-capl, ~turn1)).astype(np.int32))
     if _SP_PREFIX != "chain":
         tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
         tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
     args = {k: v.data_ptr() for k, v in tens.items()}
-    args.update(prefix_in_render=_SP_PREFIX_IN_RENDER)
+    args.update(prefix_in_render=_SP_PREFIX_IN_RENDER,
+                max_nch=int(np.diff(np.asarray(ch_off_all, dtype=np.int64)).max()) if nd else 0)
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
     committed = [i for i in range(n) if (int(flags[i]) & 9) == 9 and delta_off[i + 1] > delta_off[i]] \
         if not shared else (list(range(n)) if (int(flags[0]) & 9) == 9 and delta_off[1] > 0 else [])
@@ -539,6 +545,10 @@ def _k09_plan(p: "Prepared") -> Optional[tuple]:
             c = np.asarray(committed, dtype=np.int64)
             lo, hi = delta_off[c].astype(np.int64), delta_off[c + 1].astype(np.int64)
             lens = hi - lo
+            if _SP_ORDER & 4:  # K09 lanes by chain length: a wave's trees have equal depth
+                o = np.argsort(-lens, kind="stable")
+                c, lo, hi, lens = c[o], lo[o], hi[o], lens[o]
+                cix = torch.as_tensor(c, dtype=torch.int64).to(dev)
             # the committed chains' delta rows, concatenated (vectorized segment gather)
             seg = np.repeat(lo - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
             drow_np = np.frombuffer(p.drows, dtype=np.int32)

@@ -35,6 +35,8 @@
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 #include "ahv/delta_emit.h"
 #include "ahv/launch.h"
@@ -86,6 +88,9 @@ struct StorePipeArgs {
   int32_t prefix_in_render;     // 1: the render lane compresses its record's prefix; 0: store_pipe_prefix_kernel
   const int32_t* chain_order;   // [n] sessions by descending SHA work (chain kernel lane order), or null
   const int32_t* render_order;  // [Dn] deltas by descending record size (render kernel lane order), or null
+  const int32_t* prefix_order;  // [Dn] deltas grouped by prefix SHA work (prefix kernel lane order), or null
+  int32_t max_nch;              // most changes of any record
+  int32_t wide_only;            // lane renderer: only records with more than coop::kCoopChanges changes
 };
 
 enum StorePipeStatus : int32_t {
@@ -526,7 +531,9 @@ __global__ __launch_bounds__(256) void store_pipe_rows_kernel(StorePipeArgs a) {
 __global__ __launch_bounds__(256) void store_pipe_prefix_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd) {
   const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (x < nd) {
-    const int64_t g = a.render_order ? a.render_order[x] : x;
+    // lanes of a wave hash records with the same number of parent-independent blocks
+    // (prefix_order: turn-1 records, whole record, first, then by reserved size)
+    const int64_t g = a.prefix_order ? a.prefix_order[x] : a.render_order ? a.render_order[x] : x;
     if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix(a, g);
     else a.mid_blocks[g] = 0;
   }
@@ -538,7 +545,8 @@ __global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a,
   if (x < nd) {
     const int64_t g = a.render_order ? a.render_order[x] : x;  // records of similar size per wave
     const int64_t i = dsess[g];
-    if (a.status[i] != SP_ROW_IN_USE) sp_render(a, i, static_cast<int32_t>(g));
+    if (a.status[i] != SP_ROW_IN_USE && (!a.wide_only || a.dch_off[g + 1] - a.dch_off[g] > 4))
+      sp_render(a, i, static_cast<int32_t>(g));
   }
 }
 
@@ -551,6 +559,315 @@ __global__ __launch_bounds__(64) void store_pipe_chain_kernel(StorePipeArgs a) {
   if (x >= a.n) return;
   const int64_t i = a.chain_order ? a.chain_order[x] : x;
   if (a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
+}
+
+// ------------------------------------------------- wave-cooperative renderer
+//
+// store_pipe_render_kernel gives each lane a whole record: its emission branches
+// on field kinds, null values and string lengths, so the wave runs every lane's
+// path and half its lanes idle (r3 PMC: 48 % lane utilisation).  Here 16 lanes
+// render one record:
+//
+//   1. layout — the record is a fixed schema of 18 + 18·nch pieces (literals,
+//      quotes, pool string bodies, "null", the 66-byte parent placeholder and the
+//      generated turn / session-uuid / timestamp text); lane j resolves pieces
+//      j, j+16, … to (source, length) in LDS — a handful of uniform selects — and
+//      the group prefix-sums the lengths (one 16-lane shuffle scan);
+//   2. assembly — lane j builds output words j, j+16, … : each word is 1–2
+//      funnel-shifted reads of the piece(s) covering its 4 bytes, found by a short
+//      forward walk over the piece offsets; the 16 lanes store 64 contiguous bytes
+//      per instruction.
+//
+// A wave renders its 64 records (in render_order: similar shapes together) 64/G
+// at a time; store_pipe_prefix_kernel then compresses each record's parent-
+// independent blocks one record per lane (uniform SHA control flow).
+// Same bytes as sp_render (the CPU twin), checked by the batch tests' digests.
+namespace coop {
+
+constexpr int kCoopChanges = 4;      // records with more changes take the lane renderer
+constexpr int kMaxPieces = 18 + 18 * kCoopChanges;
+constexpr int kGenBytes = 128;       // generated text: turn digits, "session:…", "…timestamp…"
+
+enum Lit : int {
+  L_OPEN_AGENT, L_CHANGES, L_CH_OPEN, L_CH_OP, L_CH_PATH, L_CH_PREV, L_CH_CLOSE, L_CH_SEP, L_DELTA_ID,
+  L_DELTA_PFX, L_PARENT, L_SESSION, L_TS, L_TURN, L_CLOSE, L_NULL, L_QUOTE, L_HOLE, L_COUNT
+};
+
+struct Lits {
+  uint8_t b[352] = {};
+  uint16_t off[L_COUNT] = {};
+  uint16_t len[L_COUNT] = {};
+  template <size_t N>
+  constexpr void add(size_t& p, int i, const char (&v)[N]) {
+    off[i] = static_cast<uint16_t>(p);
+    len[i] = static_cast<uint16_t>(N - 1);
+    for (size_t k = 0; k + 1 < N; ++k) b[p++] = static_cast<uint8_t>(v[k]);
+    p = (p + 3) & ~size_t(3);
+  }
+  constexpr Lits() {
+    size_t p = 0;
+    add(p, L_OPEN_AGENT, canon::K_OPEN_AGENT);
+    add(p, L_CHANGES, canon::K_CHANGES);
+    add(p, L_CH_OPEN, canon::K_CH_OPEN);
+    add(p, L_CH_OP, canon::K_CH_OP);
+    add(p, L_CH_PATH, canon::K_CH_PATH);
+    add(p, L_CH_PREV, canon::K_CH_PREV);
+    add(p, L_CH_CLOSE, canon::K_CH_CLOSE);
+    add(p, L_CH_SEP, canon::K_CH_SEP);
+    add(p, L_DELTA_ID, canon::K_DELTA_ID);
+    add(p, L_DELTA_PFX, canon::K_DELTA_PFX);
+    add(p, L_PARENT, canon::K_PARENT);
+    add(p, L_SESSION, canon::K_SESSION);
+    add(p, L_TS, canon::K_TS);
+    add(p, L_TURN, canon::K_TURN);
+    add(p, L_CLOSE, canon::K_CLOSE);
+    add(p, L_NULL, canon::K_NULL);
+    add(p, L_QUOTE, "\"");
+    off[L_HOLE] = static_cast<uint16_t>(p);  // the parent placeholder: 66 quote bytes
+    len[L_HOLE] = 66;
+    for (int k = 0; k < 66; ++k) b[p++] = 0x22;
+  }
+};
+
+// in global memory (a constexpr device object indexed at run time would be
+// copied into per-lane scratch)
+__device__ Lits kLits = Lits();
+
+// Generated text of one record, in LDS: [0,16) turn digits, [16,64) the quoted
+// session id, [64,128) the quoted timestamp.
+struct GenSink {
+  uint8_t* p;
+  uint32_t n;
+  __device__ bool seg(uint32_t) { return true; }
+  __device__ bool any(bool b) const { return b; }
+  template <class T>
+  __device__ void launder(T&) const {}
+  __device__ void put(uint32_t v, uint32_t k) {
+    for (uint32_t j = 0; j < k; ++j) p[n++] = static_cast<uint8_t>(v >> (24 - 8 * j));
+  }
+  __device__ void put4(uint32_t v) { put(v, 4); }
+};
+
+struct Group {  // one record's layout (LDS)
+  const uint8_t* src[kMaxPieces];
+  uint32_t off[kMaxPieces + 1];
+  uint32_t len[kMaxPieces];
+  uint8_t gen[kGenBytes];
+};
+
+__device__ __forceinline__ uint32_t lit_len(int i) { return kLits.len[i]; }
+__device__ __forceinline__ const uint8_t* lit_src(int i) { return kLits.b + kLits.off[i]; }
+
+// Piece q of record g: (source, length).  `nch` changes; str triple = ( '"', body, '"' )
+// or ( -, "null", - ).
+__device__ __forceinline__ void piece(const StorePipeArgs& a, int64_t g, uint32_t nch, uint32_t turn, const Group& G, int q,
+                      const uint8_t*& src, uint32_t& len) {
+  int lit = -1;
+  int32_t sid = -2;  // pool id of a string triple's value (-1 null)
+  int part = 0;      // 0 open quote, 1 body, 2 close quote
+  const int tail = 5 + 18 * static_cast<int>(nch);
+  if (q < 5) {
+    switch (q) {
+      case 0: lit = L_OPEN_AGENT; break;
+      case 4: lit = L_CHANGES; break;
+      default: sid = a.dagent_pool[g]; part = q - 1; break;
+    }
+  } else if (q < tail) {
+    const int c = (q - 5) / 18;
+    const int k = (q - 5) - 18 * c;
+    const ChangeIds ch = a.changes[a.dch_off[g] + c];
+    switch (k) {
+      case 0: lit = c ? L_CH_SEP : -2; break;
+      case 1: lit = L_CH_OPEN; break;
+      case 5: lit = L_CH_OP; break;
+      case 9: lit = L_CH_PATH; break;
+      case 13: lit = L_CH_PREV; break;
+      case 17: lit = L_CH_CLOSE; break;
+      default: {
+        const int f = (k - 2) / 4;  // 0 content_hash, 1 op, 2 path, 3 previous_hash
+        part = (k - 2) - 4 * f;
+        sid = f == 0 ? ch.content_hash : f == 1 ? ch.op : f == 2 ? ch.path : ch.previous_hash;
+        break;
+      }
+    }
+  } else {
+    const uint32_t td = canon::dec_digits(turn);
+    switch (q - tail) {
+      case 0: lit = L_DELTA_ID; break;
+      case 1: lit = L_DELTA_PFX; break;
+      case 2: case 11: src = G.gen; len = td; return;
+      case 3: lit = L_QUOTE; break;
+      case 4: lit = L_PARENT; break;
+      case 5: lit = turn > 1 ? L_HOLE : L_NULL; break;
+      case 6: lit = L_SESSION; break;
+      case 7: src = G.gen + 16; len = 46; return;
+      case 8: lit = L_TS; break;
+      case 9: src = G.gen + 64; len = G.off[kMaxPieces]; return;  // its length, stashed by the generator
+      case 10: lit = L_TURN; break;
+      case 12: lit = L_CLOSE; break;
+      default: lit = -2; break;
+    }
+  }
+  if (lit == -2) {  // an empty slot
+    src = kLits.b;
+    len = 0;
+    return;
+  }
+  if (lit >= 0) {
+    src = lit_src(lit);
+    len = lit_len(lit);
+    return;
+  }
+  if (sid < 0) {  // null: ( -, "null", - )
+    src = part == 1 ? lit_src(L_NULL) : kLits.b;
+    len = part == 1 ? 4u : 0u;
+    return;
+  }
+  if (part == 1) {
+    src = a.pool.bytes + a.pool.off[sid];
+    len = static_cast<uint32_t>(a.pool.len[sid]);
+  } else {
+    src = lit_src(L_QUOTE);
+    len = 1;
+  }
+}
+
+// `t` ≤ 4 bytes at `p` (any alignment) as a little-endian word (bytes past `t` zero);
+// reads only the aligned words that hold them.
+__device__ __forceinline__ uint32_t read_bytes(const uint8_t* p, uint32_t t) {
+  const uintptr_t ad = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(ad & ~uintptr_t(3));
+  const uint32_t sh = static_cast<uint32_t>(ad & 3u);
+  const uint32_t lo = w[0];
+  const uint32_t hi = sh + t > 4u ? w[1] : 0u;
+  const uint32_t x = __builtin_amdgcn_alignbit(hi, lo, 8u * sh);
+  return t >= 4u ? x : (x & ((1u << (8u * t)) - 1u));
+}
+
+}  // namespace coop
+
+// G lanes per record (16, 8 or 4; AHV_SP_COOP_G), one wave per workgroup: the
+// wave's 64 records take 64/G rounds of 64/G… records at a time.
+template <int kGroup>
+__global__ __launch_bounds__(64) void store_pipe_render_coop_kernel(StorePipeArgs a, const int32_t* dsess,
+                                                                    int64_t nd) {
+  using namespace coop;
+  constexpr int kNG = 64 / kGroup;  // groups per wave
+  __shared__ Group groups[kNG];
+  const int lane = static_cast<int>(threadIdx.x);
+  const int gl = lane & (kGroup - 1);  // lane within the group
+  const int gq = lane / kGroup;        // group within the wave
+  Group& G = groups[gq];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 64;  // this wave's 64 records
+  const Tables& t = a.t;
+  for (int it = 0; it < 64 / kNG; ++it) {
+    const int64_t x = base + kNG * it + gq;
+    const bool live = x < nd;
+    const int64_t g = live ? (a.render_order ? a.render_order[x] : x) : 0;
+    const int64_t i = live ? dsess[g] : 0;
+    bool on = live && a.status[i] != SP_ROW_IN_USE;
+    const int32_t k = on ? static_cast<int32_t>(g - a.delta_off[i]) : 0;
+    const uint32_t turn = static_cast<uint32_t>(k + 1);
+    uint32_t nch = on ? static_cast<uint32_t>(a.dch_off[g + 1] - a.dch_off[g]) : 0u;
+    if (on && nch > static_cast<uint32_t>(kCoopChanges)) {  // rare: the lane renderer's (wide_only pass)
+      on = false;
+      nch = 0;
+    }
+    const int np = 18 + 18 * static_cast<int>(nch);
+    // generated text (three lanes of the group, in parallel)
+    if (on && gl < 3) {
+      GenSink gs{G.gen, 0};
+      if (gl == 0) {
+        emit_uint(gs, turn);
+      } else if (gl == 1) {
+        gs.n = 16;
+        emit_session_uuid_quoted(gs, a.uuid + 4 * i);
+      } else {
+        gs.n = 64;
+        emit_iso_quoted(gs, sp_delta_ts(a, i, k));
+        G.off[kMaxPieces] = gs.n - 64;  // the timestamp's length (read by piece 9 of the tail)
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // layout: lane gl resolves pieces gl, gl+16, …; sums its own contiguous chunk after
+    uint32_t mine = 0;
+    if (on) {
+      for (int q = gl; q < np; q += kGroup) {
+        const uint8_t* sp;
+        uint32_t ln;
+        piece(a, g, nch, turn, G, q, sp, ln);
+        G.src[q] = sp;
+        G.len[q] = ln;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const int per = (np + kGroup - 1) / kGroup;
+    const int q0 = gl * per;
+    const int q1 = q0 + per < np ? q0 + per : np;
+    if (on)
+      for (int q = q0; q < q1; ++q) mine += G.len[q];
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < kGroup; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, kGroup);
+      if (gl >= o) incl += y;
+    }
+    const uint32_t L = __shfl(incl, kGroup - 1, kGroup);
+    if (on) {
+      uint32_t run = incl - mine;
+      for (int q = q0; q < q1; ++q) {
+        G.off[q] = run;
+        run += G.len[q];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // assembly: output word w = gl + 16·j (64 contiguous bytes per group store)
+    const int32_t d = on ? a.drow[g] : 0;
+    const uint32_t cap = on ? static_cast<uint32_t>(a.dcap[g]) : 0u;
+    const uint32_t lim = L < cap ? L : cap;  // an overflowing record keeps what fits (SP_RENDER)
+    uint32_t* dst = reinterpret_cast<uint32_t*>(t.payload + (on ? a.doff[g] : 0));
+    int p = 0;
+    for (uint32_t w = static_cast<uint32_t>(gl); on && 4 * w < lim; w += kGroup) {
+      uint32_t pos = 4 * w;
+      const uint32_t end = pos + 4 < L ? pos + 4 : L;
+      while (p < np - 1 && G.off[p] + G.len[p] <= pos) ++p;
+      uint32_t out = 0;
+      uint32_t sh = 0;
+      while (pos < end) {
+        const uint32_t in = pos - G.off[p];
+        const uint32_t rem = G.len[p] - in;
+        const uint32_t take = rem < end - pos ? rem : end - pos;
+        out |= read_bytes(G.src[p] + in, take) << sh;
+        sh += 8 * take;
+        pos += take;
+        if (pos < end) {
+          ++p;
+          while (p < np - 1 && G.len[p] == 0) ++p;
+        }
+      }
+      if (4 * w + 4 <= cap) dst[w] = out;
+    }
+    if (on && gl == 0) {
+      t.d_sess[d] = static_cast<int32_t>(a.slot[i]);
+      t.d_turn[d] = static_cast<int32_t>(turn);
+      t.d_prev[d] = k > 0 ? a.drow[g - 1] : -1;
+      t.d_ts[d] = sp_delta_ts(a, i, k);
+      t.d_off[d] = a.doff[g];
+      t.d_len[d] = static_cast<int32_t>(L);
+      t.d_hole[d] = turn > 1 ? static_cast<int32_t>(G.off[5 + 18 * static_cast<int>(nch) + 5]) : -1;
+      if (L > cap) a.status[i] = SP_RENDER;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();  // the group's LDS layout is rewritten next iteration
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  // (the parent-independent blocks: store_pipe_prefix_kernel, one record per lane)
 }
 
 template <class T>
@@ -595,7 +912,23 @@ StorePipeArgs to_args(const Tables& t, const py::dict& d) {
   a.mid_blocks = d.contains("mid_blocks") ? P<int32_t>(d, "mid_blocks") : nullptr;
   a.prefix_in_render = d.contains("prefix_in_render") ? d["prefix_in_render"].cast<int32_t>() : 1;
   a.render_order = d.contains("render_order") ? P<const int32_t>(d, "render_order") : nullptr;
+  a.prefix_order = d.contains("prefix_order") ? P<const int32_t>(d, "prefix_order") : nullptr;
+  a.max_nch = d.contains("max_nch") ? d["max_nch"].cast<int32_t>() : 1 << 30;
+  a.wide_only = 0;
   return a;
+}
+
+// AHV_SP_RENDER=coop: the wave-cooperative renderer with AHV_SP_COOP_G lanes per
+// record (16, 8 or 4); default: the lane-per-record renderer (0).
+static int render_coop() {
+  static const int v = [] {
+    const char* e = std::getenv("AHV_SP_RENDER");
+    if (e == nullptr || std::string(e) != "coop") return 0;
+    const char* g = std::getenv("AHV_SP_COOP_G");
+    const int n = g ? std::atoi(g) : 16;
+    return n == 8 || n == 4 ? n : 16;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -623,9 +956,25 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
   if (a.n > 0) {
     hipLaunchKernelGGL(store_pipe_rows_kernel, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, st, a);
     if (nd > 0) {
-      hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
-                         a, dsess, nd);
-      if (a.mid && !a.prefix_in_render)
+      const int cg = render_coop();
+      const dim3 cgrid(static_cast<unsigned>((nd + 63) / 64));
+      if (cg == 16)
+        hipLaunchKernelGGL(store_pipe_render_coop_kernel<16>, cgrid, dim3(64), 0, st, a, dsess, nd);
+      else if (cg == 8)
+        hipLaunchKernelGGL(store_pipe_render_coop_kernel<8>, cgrid, dim3(64), 0, st, a, dsess, nd);
+      else if (cg == 4)
+        hipLaunchKernelGGL(store_pipe_render_coop_kernel<4>, cgrid, dim3(64), 0, st, a, dsess, nd);
+      if (cg && a.max_nch > coop::kCoopChanges) {  // records past the cooperative layout: one lane each
+        StorePipeArgs w = a;
+        w.wide_only = 1;
+        w.prefix_in_render = 0;
+        hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
+                           w, dsess, nd);
+      }
+      if (!cg)
+        hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
+                           a, dsess, nd);
+      if (a.mid && (cg || !a.prefix_in_render))
         hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                            a, dsess, nd);
     }

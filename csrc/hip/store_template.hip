@@ -115,6 +115,17 @@ static int template_ab() {
   return v;
 }
 
+// Small batches (n ≤ AHV_TEMPLATE_SMALL sessions, default 65,536: fewer waves than
+// the chip has SIMDs, so each wave runs alone and latency is all that counts) use a
+// 6-block window: a whole record in one emission pass instead of two.
+static int64_t template_small() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("AHV_TEMPLATE_SMALL");
+    return e ? std::atoll(e) : int64_t(65536);
+  }();
+  return v;
+}
+
 // Occupancy variant (AHV_TEMPLATE_WAVES = 2 or 3 waves per SIMD).
 static int template_waves() {
   static const int v = [] {
@@ -263,7 +274,9 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
   }
   py::gil_scoped_release nogil;
   const dim3 grid(static_cast<uint32_t>((a.n + kWaveLanes - 1) / kWaveLanes)), block(kWaveLanes);
-  if (template_waves() == 2)  // 231 VGPRs, no scratch
+  if (a.n <= template_small())  // latency-bound: one pass per record
+    hipLaunchKernelGGL((store_template_kernel<1, 6>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
+  else if (template_waves() == 2)  // 231 VGPRs, no scratch
     hipLaunchKernelGGL((store_template_kernel<2, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else  // 168 VGPRs (3 waves/SIMD) with a small spill
     hipLaunchKernelGGL((store_template_kernel<3, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
@@ -273,6 +286,7 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
 void kernels_store_template(std::vector<KernelEntry>& out) {
   out.push_back({"store_template_kernel<3,3>", reinterpret_cast<const void*>(&store_template_kernel<3, 3>)});
   out.push_back({"store_template_kernel<2,3>", reinterpret_cast<const void*>(&store_template_kernel<2, 3>)});
+  out.push_back({"store_template_kernel<1,6>", reinterpret_cast<const void*>(&store_template_kernel<1, 6>)});
 }
 
 }  // namespace ahv

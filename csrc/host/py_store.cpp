@@ -318,6 +318,11 @@ class Store : public StoreCore {
 
   void release_rows(uint64_t kind, I32Array a) { release_rows_raw(kind, a.data(), a.size()); }
 
+  // A short Python list of rows (a chain's delta rows from a finaliser): no array.
+  void release_list(uint64_t kind, const py::list& rows) {
+    for (auto r : rows) release_row(kind, r.cast<int64_t>());
+  }
+
   py::dict info() const {
     py::dict d;
     d["gpu"] = gpu_;
@@ -395,6 +400,7 @@ void register_store(py::module_& m) {
       .def("alloc_rows", &Store::alloc_rows)
       .def("release_row", &Store::release_row)
       .def("release_rows", &Store::release_rows)
+      .def("release_list", &Store::release_list)
       .def("return_row", &Store::return_row)
       .def("reclaim_pool", &Store::reclaim_pool)
       .def("check_frees", &Store::check_frees, py::arg("block") = false)

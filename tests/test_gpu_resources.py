@@ -5,7 +5,8 @@ footprint fails here instead of showing up as a slower profile.
 
 * template pipeline over store rows: 3-block LDS window = (48 + 1 trash) rows ×
   64 lanes × 4 B; the 2-waves/SIMD variant holds everything in ≤ 256 VGPRs with no
-  scratch, the 3-waves variant stays within 168 VGPRs (a small spill);
+  scratch, the 3-waves variant stays within 168 VGPRs (a small spill); the small-batch
+  variant holds a whole record ((96 + 1) rows) with no scratch;
 * K08 chain re-hash: same window, no scratch;
 * slash (16-lane groups), σ_eff (16 threads per session), tile build: no scratch.
 """
@@ -29,6 +30,8 @@ def test_hot_kernels_fit_their_budgets(cuda_device):
     assert p2["lds_bytes"] == p3["lds_bytes"] == (48 + 1) * 64 * 4
     assert p2["vgprs"] <= 256 and p2["scratch_bytes"] == 0, p2
     assert p3["vgprs"] <= 168 and p3["scratch_bytes"] <= 128, p3
+    p6 = a["store_template_kernel<1,6>"]
+    assert p6["lds_bytes"] == (96 + 1) * 64 * 4 and p6["scratch_bytes"] == 0, p6
     ch = a["chain_hash_kernel"]
     assert ch["lds_bytes"] == (48 + 1) * 64 * 4 and ch["scratch_bytes"] == 0, ch
     for name in ("slash_group_kernel", "sigma_eff_csr_kernel", "build_tiles_kernel", "bond_tiles_mfma_kernel",
