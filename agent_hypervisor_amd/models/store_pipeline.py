@@ -40,9 +40,9 @@ REFERENCE_STEPS = (("action", "did:mesh:a", "/api/action", None, 0, 0),)
 # AHV_SP_PREFIX: where the records' parent-independent SHA blocks are compressed)
 import os as _os  # noqa: E402
 
-_SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "1"))
+_SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "5"))
 # render | kernel | sorted (its own kernel, lanes grouped by SHA work) | chain (no split: the chain lane hashes all)
-_SP_PREFIX = _os.environ.get("AHV_SP_PREFIX", "render")
+_SP_PREFIX = _os.environ.get("AHV_SP_PREFIX", "sorted")
 _SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX in ("kernel", "sorted") else 1
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
