@@ -370,6 +370,7 @@ class GovernanceEngine:
         stats: Optional[torch.Tensor] = None,
         cursor: Optional[torch.Tensor] = None,
         events=None,
+        fold: bool = True,
     ) -> PipelineBatch:
         """Run the full governance pipeline for ``n`` new sessions (asynchronously
         on the current stream).
@@ -385,6 +386,9 @@ class GovernanceEngine:
         counters — the graph-capturable form used by
         :class:`agent_hypervisor_amd.runtime.graphs.PipelineGraph`, which also
         advances the cursor on the device.  The host counters are not touched.
+
+        ``fold=False``: leave the batch counters in the engine's spread rows
+        (``_spread``); the caller folds them (the graph's fused epilogue does).
         """
         if stats is not None and (stats.dtype != torch.int64 or stats.numel() != 6 or stats.device != self.device):
             raise ValueError("stats must be an int64[6] tensor on the engine device")
@@ -425,15 +429,15 @@ class GovernanceEngine:
             "cursor": cursor.data_ptr() if cursor is not None else None,
         }
         if cursor is not None:
-            if cursor.dtype != torch.int64 or cursor.numel() != 3 or cursor.device != self.device:
-                raise ValueError("cursor must be an int64[3] tensor on the engine device")
+            if cursor.dtype != torch.int64 or cursor.numel() not in (3, 4) or cursor.device != self.device:
+                raise ValueError("cursor must be an int64[3] (or [4]) tensor on the engine device")
         if events is not None:  # DeviceEventRing (N08): lifecycle records appended by the kernel
             ev_scalars, ev_tensors = events.kernel_args()
             args.update(ev_scalars)
             args.update({k: v.data_ptr() for k, v in ev_tensors.items()})
         _pipeline_op.run(st, args, {"merkle_root": self.sessions.merkle_root, "delta_hash": self.sessions.delta_hash,
                                     "status": self._status})
-        if stats is not None:
+        if stats is not None and fold:
             self._spread.add_into(stats)
         self._keep = (agents, ch)
         if cursor is not None:

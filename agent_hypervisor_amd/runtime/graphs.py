@@ -71,8 +71,15 @@ class PipelineGraph:
 
     ``agents`` is the (device) int32 buffer of joining agent ids read by every
     replay; ``refresh_agents`` (optional, capturable) rewrites it each step.
-    ``stats`` (int64[6]) is zeroed and accumulated each step; ``reduce`` is an
-    optional capturable collective applied to it (e.g. ``comm.all_reduce``).
+    ``stats`` (int64[6]) receives each step's batch counters; ``reduce`` is an
+    optional capturable collective applied to it (e.g. ``comm.all_reduce``);
+    ``tail`` an optional capturable op run after the batch (e.g. config2's σ_eff
+    and ring re-gate), so the whole step is one graph launch.
+
+    On the GPU the step is two nodes besides the hooks: the pipeline kernel and one
+    epilogue kernel that folds the counters, advances the cursor and stamps the
+    next step's time base (``fused=False``: the separate zero / clock / fold /
+    advance nodes).
     """
 
     def __init__(
@@ -85,6 +92,8 @@ class PipelineGraph:
         refresh_agents: Optional[Callable[[], None]] = None,
         reduce: Optional[Callable[[torch.Tensor], object]] = None,
         use_graph: Optional[bool] = None,
+        tail: Optional[Callable[[], None]] = None,
+        fused: bool = True,
     ) -> None:
         if n > engine.sessions.capacity:
             raise ValueError(f"batch of {n} exceeds session capacity {engine.sessions.capacity}")
@@ -92,11 +101,14 @@ class PipelineGraph:
             raise ValueError("agents must be an int32 tensor of n ids on the engine device")
         self.engine, self.n, self.deltas = engine, n, deltas
         self.agents, self.stats = agents, stats
-        self._refresh, self._reduce = refresh_agents, reduce
+        self._refresh, self._reduce, self._tail = refresh_agents, reduce, tail
         dev = engine.device
+        self._fused = fused and dev.type == "cuda"
         self.clock = DeviceClock.calibrate(dev)
-        self.cursor = torch.tensor([engine._next_slot, engine._id_counter, _clock.now_us()], dtype=torch.int64,
-                                   device=dev)
+        now = _clock.now_us()
+        # [slot_base, id_base, now_us] (+ [3]: the last batch's now_us, fused epilogue)
+        self.cursor = torch.tensor([engine._next_slot, engine._id_counter, now] + ([now] if self._fused else []),
+                                   dtype=torch.int64, device=dev)
         self.steps = 0
         self.use_graph = (dev.type == "cuda") if use_graph is None else use_graph
         self.graph = None
@@ -105,14 +117,32 @@ class PipelineGraph:
 
     # -- the captured body ----------------------------------------------------------
     def _body(self) -> None:
-        if self.stats is not None:
-            self.stats.zero_()
-        self.clock.stamp(self.cursor)
-        if self._refresh is not None:
-            self._refresh()
-        self.engine.run_pipeline(self.n, agents=self.agents, deltas=self.deltas, stats=self.stats,
-                                 cursor=self.cursor)
-        advance(self.cursor, self.n, self.engine.sessions.capacity)
+        if self._fused:
+            # the cursor's time base was stamped by the previous step's epilogue
+            # (or at construction): pipeline kernel + one epilogue node
+            if self._refresh is not None:
+                self._refresh()
+            eng = self.engine
+            eng.run_pipeline(self.n, agents=self.agents, deltas=self.deltas, stats=self.stats, cursor=self.cursor,
+                             fold=False)
+            c = self.clock
+            spread = eng._spread.buf if self.stats is not None else None
+            C.pipeline_epilogue(spread.data_ptr() if spread is not None else 0,
+                                self.stats.data_ptr() if spread is not None else 0,
+                                self.stats.numel() if spread is not None else 0, self.cursor.data_ptr(), self.n,
+                                eng.sessions.capacity, c.base_us, c.base_clk, c.rate_khz,
+                                torch.cuda.current_stream(self.cursor.device).cuda_stream)
+        else:
+            if self.stats is not None:
+                self.stats.zero_()
+            self.clock.stamp(self.cursor)
+            if self._refresh is not None:
+                self._refresh()
+            self.engine.run_pipeline(self.n, agents=self.agents, deltas=self.deltas, stats=self.stats,
+                                     cursor=self.cursor)
+            advance(self.cursor, self.n, self.engine.sessions.capacity)
+        if self._tail is not None:
+            self._tail()
         if self._reduce is not None and self.stats is not None:
             self._reduce(self.stats)
 
@@ -153,7 +183,9 @@ class PipelineGraph:
         if self.steps == 0:
             raise RuntimeError("no step has run yet")
         self.engine.synchronize()
-        slot, idb, now = (int(x) for x in self.cursor.cpu().tolist())
+        cur = [int(x) for x in self.cursor.cpu().tolist()]
+        slot, idb = cur[0], cur[1]
+        now = cur[3] if self._fused else cur[2]  # the epilogue already stamped the next step's time base
         cap = self.engine.sessions.capacity
         return PipelineBatch(self.engine, (slot - self.n) % cap, self.n, idb - 3 * self.n, now, self.deltas,
                              list(self.engine._last_specs or []), self.agents)

@@ -123,19 +123,23 @@ def config2(ctx: Ctx, args):
     eng.register_synthetic_agents(max(S, 1024), seed=2)
     agents = torch.randint(0, max(S, 1024), (S,), dtype=i32, device=ctx.dev)
     stats = torch.zeros(6, dtype=i64, device=ctx.dev)
-    pg = PipelineGraph(eng, S, agents, stats=stats)
     g = torch.Generator(device="cpu").manual_seed(3)
     tiles = (torch.rand((S, 16, 16), generator=g, dtype=f64) * 0.05).to(ctx.dev)
     sigma = torch.rand((S, 16), generator=g, dtype=f64).to(ctx.dev)
     omega = torch.full((S,), 0.5, dtype=f64, device=ctx.dev)
 
-    # (Running the σ_eff + ring-gate stage on a second stream beside the pipeline
-    # measured slower — 0.154 vs 0.136 ms — the cross-stream event waits cost more
-    # than the ~15 µs stage they would hide; one stream it is.)
-    def step():
-        pg.step()
+    def liability_tail():
         se, expo, _ = LI.bond_tiles(tiles, sigma, omega)
         R.ring_gate(se.reshape(-1))
+
+    # (Running the σ_eff + ring-gate stage on a second stream beside the pipeline
+    # measured slower — 0.154 vs 0.136 ms — the cross-stream event waits cost more
+    # than the ~15 µs stage they would hide; one stream it is, captured with the
+    # pipeline in one graph: pipeline kernel, epilogue, σ_eff tiles, ring gate.)
+    pg = PipelineGraph(eng, S, agents, stats=stats, tail=liability_tail, fused=not args.unfused_graph)
+
+    def step():
+        pg.step()
 
     el, lat = ctx.timed(step, args.steps, args.warmup)
     ctx.emit(config="config2", what="pipeline+sigma_eff(MFMA)+ring_gate", sessions_per_step=S,
@@ -491,6 +495,8 @@ def main():
     ap.add_argument("--storm-fraction", type=float, default=0.1, help="config5: share of sessions slashed")
     ap.add_argument("--coroutine-sagas", type=int, default=4096, help="config4: sagas in the coroutine mode")
     ap.add_argument("--unfused", action="store_true", help="config5: separate slash and sigma_eff passes (A/B)")
+    ap.add_argument("--unfused-graph", action="store_true",
+                    help="config2: separate zero/clock/fold/advance graph nodes instead of the fused epilogue (A/B)")
     ap.add_argument("--no-midstate", action="store_true", help="config5: single-phase K08 re-chain (A/B)")
     ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
     ap.add_argument("--allreduce-exposure", action="store_true",

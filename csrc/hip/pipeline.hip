@@ -49,6 +49,48 @@ __global__ __launch_bounds__(kWaveLanes) void spread_fold_kernel(unsigned long l
   }
 }
 
+// The captured step's epilogue in one launch (N07/N09/X04): fold the batch's spread
+// counters into out[] (copied: no zero-fill node before the batch), advance the
+// cursor's slot/id bases past it, and stamp the next step's time base from the
+// device wall clock — three single-wave nodes (fill, fold, advance) plus the next
+// step's clock node become one.  `cursor` is int64[4]: [3] keeps the time base
+// of the batch that just ran.
+__global__ __launch_bounds__(kWaveLanes) void pipeline_epilogue_kernel(unsigned long long* spread,
+                                                                       unsigned long long* out, int k, int64_t* cursor,
+                                                                       int64_t n, int64_t capacity, int64_t base_us,
+                                                                       int64_t base_clk, int64_t rate_khz) {
+  const int lane = threadIdx.x;
+  if (spread != nullptr) {
+    unsigned long long v[kMaxFold];
+#pragma unroll
+    for (int j = 0; j < kMaxFold; ++j) v[j] = j < k ? spread[lane * k + j] : 0ull;
+#pragma unroll
+    for (int j = 0; j < kMaxFold; ++j) {
+      if (j >= k) break;
+      spread[lane * k + j] = 0;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v[j] += __shfl_xor(v[j], off, kWaveLanes);
+      if (lane == 0) out[j] = v[j];
+    }
+  }
+  if (lane == 0) {
+    cursor[0] = (cursor[0] + n) % capacity;
+    cursor[1] += 3 * n;
+    const int64_t ticks = static_cast<int64_t>(wall_clock64()) - base_clk;
+    cursor[3] = cursor[2];  // the time base the finished batch used (PipelineGraph.last_batch)
+    cursor[2] = base_us + ticks * 1000 / rate_khz;
+  }
+}
+
+void launch_pipeline_epilogue(unsigned long long* spread, unsigned long long* out, int k, int64_t* cursor, int64_t n,
+                              int64_t capacity, int64_t base_us, int64_t base_clk, int64_t rate_khz, hipStream_t s) {
+  if (spread != nullptr && (k <= 0 || k > kMaxFold)) throw std::invalid_argument("pipeline epilogue: k out of range");
+  if (capacity <= 0 || rate_khz <= 0) throw std::invalid_argument("pipeline epilogue: bad capacity / clock rate");
+  hipLaunchKernelGGL(pipeline_epilogue_kernel, dim3(1), dim3(kWaveLanes), 0, s, spread, out, k, cursor, n, capacity,
+                     base_us, base_clk, rate_khz);
+  check_hip(hipGetLastError(), "pipeline_epilogue_kernel");
+}
+
 void launch_spread_fold(unsigned long long* spread, unsigned long long* out, int k, bool accumulate, hipStream_t s) {
   if (k <= 0 || k > kMaxFold) throw std::invalid_argument("spread fold: k out of range");
   hipLaunchKernelGGL(spread_fold_kernel, dim3(1), dim3(kWaveLanes), 0, s, spread, out, k, accumulate ? 1 : 0);

@@ -332,6 +332,15 @@ void register_kernels(py::module_& m) {
       },
       "Advance cursor slot/id bases by one batch of `n` sessions on `stream`.");
   m.def(
+      "pipeline_epilogue",
+      [](uintptr_t spread, uintptr_t out, int k, uintptr_t cursor, int64_t n, int64_t capacity, int64_t base_us,
+         int64_t base_clk, int64_t rate_khz, uintptr_t stream) {
+        launch_pipeline_epilogue(reinterpret_cast<unsigned long long*>(spread), reinterpret_cast<unsigned long long*>(out),
+                                 k, reinterpret_cast<int64_t*>(cursor), n, capacity, base_us, base_clk, rate_khz,
+                                 reinterpret_cast<hipStream_t>(stream));
+      },
+      "Captured step epilogue: fold spread counters into out (copy), advance the cursor, stamp the next time base.");
+  m.def(
       "kernel_attributes",
       []() {
         std::vector<KernelEntry> ks;

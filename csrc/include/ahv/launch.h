@@ -22,6 +22,8 @@ void launch_spread_fold(unsigned long long* spread, unsigned long long* out, int
 // cursor = int64[3] {slot_base, id_base, now_us}.
 void launch_pipeline_clock(int64_t* cursor, int64_t base_us, int64_t base_clk, int64_t rate_khz, hipStream_t s);
 void launch_pipeline_advance(int64_t* cursor, int64_t n, int64_t capacity, hipStream_t s);
+void launch_pipeline_epilogue(unsigned long long* spread, unsigned long long* out, int k, int64_t* cursor, int64_t n,
+                              int64_t capacity, int64_t base_us, int64_t base_clk, int64_t rate_khz, hipStream_t s);
 int64_t device_wall_clock(int device);  // one synchronous sample of wall_clock64()
 int64_t device_wall_clock_rate_khz(int device);
 

@@ -170,6 +170,30 @@ def test_randomized_batch_equals_scalar_api_gpu():
     check_randomized("cuda", 100_000)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", [
+    {"AHV_SP_RENDER": "coop", "AHV_SP_COOP_G": "16"},
+    {"AHV_SP_RENDER": "coop", "AHV_SP_COOP_G": "4"},
+    {"AHV_SP_PREFIX": "render", "AHV_SP_ORDER": "1"},
+    {"AHV_SP_ORDER": "7"},
+])
+def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
+    """The A/B layouts of the batch kernels (cooperative renderer with 16 / 4 lanes per
+    record, prefix SHA inside the render pass, render lanes by record shape) produce
+    the same records, digests and roots as the scalar API (a fresh process each: the
+    switches are read once)."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, **layout)
+    code = ("import sys; sys.path.insert(0, 'tests'); import test_store_pipeline as t; "
+            "t.check_randomized('cuda', 20_000)")
+    r = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
 def test_lazy_rows_released_in_bulk_and_materialized_rows_kept(monkeypatch):
     import gc
 
