@@ -136,15 +136,25 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
     t.s_head[8 * s + k] = 0;
     t.s_root[8 * s + k] = 0;
   }
-  // joins, in order: K01 ring gate + admission (OP_SESS_JOIN semantics)
+  // joins, in order: K01 ring gate + admission (OP_SESS_JOIN semantics).  The
+  // duplicate check compares the session's earlier admitted joins (a bit mask over
+  // its first 64 joins, in registers) instead of reading back the participant rows
+  // just stored: a read after a store waits out a full memory round trip.
   int32_t pc = 0, active = 0;
-  for (int32_t j = a.join_off[i]; j < a.join_off[i + 1]; ++j) {
+  const int32_t j0 = a.join_off[i], j1 = a.join_off[i + 1];
+  const int32_t maxpart = a.maxpart[i];
+  const double minsig = a.minsig[i];
+  uint64_t admitted = 0;
+  for (int32_t j = j0; j < j1; ++j) {
     const int32_t agent = a.join_agent[j];
     const double sg = a.join_sigma[j];
     const uint8_t ring = ring_from_sigma(sg, false);
     bool dup = false;
-    for (int32_t k = 0; k < pc; ++k) dup = dup || t.p_agent[store::prow(t, s, k)] == agent;
-    uint8_t code = join_check(st, dup, active, a.maxpart[i], sg, a.minsig[i], ring);
+    for (int32_t q = j0; q < j; ++q) {
+      const bool adm = q - j0 < 64 ? ((admitted >> (q - j0)) & 1u) != 0 : a.join_code[q] == JOIN_OK;
+      dup = dup || (adm && a.join_agent[q] == agent);
+    }
+    uint8_t code = join_check(st, dup, active, maxpart, sg, minsig, ring);
     if (code == JOIN_OK && pc >= t.cap.P) code = static_cast<uint8_t>(store::JOIN_ROWS);
     a.join_ring[j] = ring;
     a.join_code[j] = code;
@@ -156,6 +166,7 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
       t.p_sraw[row] = sg;
       t.p_seff[row] = sg;
       t.p_joined[row] = t0;
+      if (j - j0 < 64) admitted |= uint64_t(1) << (j - j0);
       ++pc;
       ++active;
     } else if (status == SP_OK) {
@@ -175,56 +186,63 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
   t.s_dlast[s] = nd > 0 ? a.drow[d1 - 1] : -1;
   int64_t tnext = t0 + 1 + nd;
   // saga: steps executed in order with their pre-resolved outcomes (K13), retries
-  // reset to PENDING between attempts as the reference does (orchestrator.py:124/134)
+  // reset to PENDING between attempts as the reference does (orchestrator.py:124/134).
+  // Each step's state is settled in registers and stored once; the committed steps
+  // (first 64) are a bit mask for the compensation pass.
   const int32_t g = a.gslot[i];
   if (g >= 0) {
+    const int32_t k0 = a.step_off[i], k1 = a.step_off[i + 1];
     t.g_state[g] = SG_RUNNING;
     t.g_created[g] = t0;
     t.g_completed[g] = 0;
-    t.g_nsteps[g] = a.step_off[i + 1] - a.step_off[i];
+    t.g_nsteps[g] = k1 - k0;
     bool failed = false;
-    for (int32_t k = a.step_off[i]; k < a.step_off[i + 1]; ++k) {
+    uint64_t committed = 0;
+    for (int32_t k = k0; k < k1; ++k) {
       const int32_t ts = a.tslot[k];
+      uint8_t sst = ST_PENDING;
+      int32_t rt = 0;
+      int64_t started = 0, completed = 0;
+      if (!failed) {  // the caller stops at the first failed step
+        const int32_t attempts = 1 + a.step_retries[k];
+        const int32_t fails = a.step_fail[k];
+        for (int32_t at = 0; at < attempts; ++at) {
+          rt = at;
+          started = tnext++;
+          if (at >= fails) {
+            sst = ST_COMMITTED;
+            completed = tnext++;
+            break;
+          }
+          completed = tnext++;
+          sst = at < attempts - 1 ? ST_PENDING : ST_FAILED;
+        }
+        if (sst == ST_FAILED) {
+          failed = true;
+          if (status == SP_OK) status = SP_STEP_FAILED;
+        }
+      }
       t.t_saga[ts] = g;
-      t.t_state[ts] = ST_PENDING;
+      t.t_state[ts] = sst;
       t.t_undo[ts] = a.step_undo[k];
       t.t_maxretry[ts] = a.step_retries[k];
-      t.t_retry[ts] = 0;
-      t.t_started[ts] = 0;
-      t.t_completed[ts] = 0;
-      if (failed) continue;  // the caller stops at the first failed step
-      const int32_t attempts = 1 + a.step_retries[k];
-      for (int32_t at = 0; at < attempts; ++at) {
-        t.t_retry[ts] = at;
-        t.t_state[ts] = ST_EXECUTING;
-        t.t_started[ts] = tnext++;
-        if (at >= a.step_fail[k]) {
-          t.t_state[ts] = ST_COMMITTED;
-          t.t_completed[ts] = tnext++;
-          break;
-        }
-        t.t_state[ts] = ST_FAILED;
-        t.t_completed[ts] = tnext++;
-        if (at < attempts - 1) t.t_state[ts] = ST_PENDING;
-      }
-      if (t.t_state[ts] == ST_FAILED) {
-        failed = true;
-        if (status == SP_OK) status = SP_STEP_FAILED;
-      }
+      t.t_retry[ts] = rt;
+      t.t_started[ts] = started;
+      t.t_completed[ts] = completed;
+      if (sst == ST_COMMITTED && k - k0 < 64) committed |= uint64_t(1) << (k - k0);
     }
     if (failed && (fl & 16u)) {  // compensate: committed steps in reverse (K14)
-      t.g_state[g] = SG_COMPENSATING;
       int32_t comp_failed = 0;
-      for (int32_t k = a.step_off[i + 1] - 1; k >= a.step_off[i]; --k) {
+      for (int32_t k = k1 - 1; k >= k0; --k) {
         const int32_t ts = a.tslot[k];
-        if (t.t_state[ts] != ST_COMMITTED) continue;
+        const bool was = k - k0 < 64 ? ((committed >> (k - k0)) & 1u) != 0 : t.t_state[ts] == ST_COMMITTED;
+        if (!was) continue;
         if (!a.step_undo[k]) {
           t.t_state[ts] = ST_COMPENSATION_FAILED;  // "No Undo_API available" (set directly, no stamp)
           ++comp_failed;
           continue;
         }
-        t.t_state[ts] = ST_COMPENSATING;
-        t.t_state[ts] = ST_COMPENSATED;
+        t.t_state[ts] = ST_COMPENSATED;  // COMPENSATING → COMPENSATED
         t.t_completed[ts] = tnext++;
       }
       t.g_state[g] = comp_failed ? SG_ESCALATED : SG_COMPLETED;
