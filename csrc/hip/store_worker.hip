@@ -268,15 +268,19 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    uint64_t x = (lane == 0 || lane == 2) ? 0ull : w;
+    // the host writes only the words in use (count in w[1]'s high half); the rest of
+    // the slot still holds an older command and reads as zero
+    const uint32_t nwr = static_cast<uint32_t>(__shfl(w, 1) >> 32) & 0x7fu;
+    const uint64_t v = static_cast<uint32_t>(lane) < (nwr ? nwr : 64u) ? w : 0ull;
+    uint64_t x = (lane == 0 || lane == 2) ? 0ull : v;
     for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
-    if (x != __shfl(w, 2)) continue;  // torn read of a slot still being written: poll again
+    if (x != __shfl(v, 2)) continue;  // torn read of a slot still being written: poll again
     const uint64_t c_start = __builtin_amdgcn_s_memrealtime();
     Cmd c;
-    c.op = static_cast<uint32_t>(__shfl(w, 1));
+    c.op = static_cast<uint32_t>(__shfl(v, 1));
 #pragma unroll
-    for (int k = 0; k < kArgs; ++k) c.a[k] = __shfl(w, 3 + k);
-    if (lane >= 16) inl[lane - 16] = w;
+    for (int k = 0; k < kArgs; ++k) c.a[k] = __shfl(v, 3 + k);
+    if (lane >= 16) inl[lane - 16] = v;
     L.sync();
     c.inl = inl;
     if (needs_drain(c.op)) {

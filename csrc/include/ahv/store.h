@@ -22,9 +22,10 @@
 // semantics for both.  Strings never reach the device: DIDs and session ids are
 // interned ids, error texts are formatted on the host from returned codes.
 //
-// Slot layout:  w[0] seq (written last), w[1] op, w[2] checksum (xor of w[1],
-// w[3..63]), w[3..15] = a[0..12] scalar args, w[16..63] = 384 inline payload
-// bytes (index lists, score pairs).  Larger variable data lives in the staging
+// Slot layout:  w[0] seq (written last), w[1] op | words-in-use << 32, w[2]
+// checksum (xor of w[1], w[3..63]), w[3..15] = a[0..12] scalar args, w[16..63] =
+// 384 inline payload bytes (index lists, score pairs).  Only the words in use are
+// written; the worker reads the others as zero.  Larger variable data lives in the staging
 // area (fine-grained device memory), addressed by (offset, length) args.
 #pragma once
 

@@ -315,7 +315,10 @@ class StoreCore {
     }
     uint64_t w[kSlotWords];
     std::memset(w, 0, sizeof w);
-    w[1] = op;
+    // words in use (header, arguments, inline payload): only these cross the BAR;
+    // the worker reads the count from w[1]'s high half and treats the rest as zero
+    const uint32_t nw = inl_bytes ? 16u + static_cast<uint32_t>((inl_bytes + 7) / 8) : 3u + static_cast<uint32_t>(nargs);
+    w[1] = op | (static_cast<uint64_t>(nw) << 32);
     for (size_t k = 0; k < nargs; ++k) w[3 + k] = args[k];
     if (inl_bytes) std::memcpy(w + 16, inl, inl_bytes);
     uint64_t x = w[1];
@@ -340,13 +343,13 @@ class StoreCore {
     if (ring_host_) {
       // cached stores; x86 keeps them in order, and the worker rejects a torn read
       // through the checksum, so the sequence word goes last
-      std::memcpy(slot + 1, w + 1, 8 * (kSlotWords - 1));
+      std::memcpy(slot + 1, w + 1, 8 * (nw - 1));
       __atomic_store_n(slot, q + 1, __ATOMIC_RELEASE);
     } else if (__builtin_cpu_supports("avx2")) {
-      write_slot_bar(slot, w, q + 1);
+      write_slot_bar(slot, w, q + 1, nw);
     } else {
       volatile uint64_t* v = slot;
-      for (int k = 1; k < kSlotWords; ++k) v[k] = w[k];
+      for (uint32_t k = 1; k < nw; ++k) v[k] = w[k];
       _mm_sfence();
       v[0] = q + 1;
       _mm_sfence();
@@ -355,12 +358,14 @@ class StoreCore {
     return q;
   }
 
-  // A slot in device memory through the BAR: 32-byte stores (16 PCIe writes for
-  // the 512-byte slot instead of 63), the sequence word last.
-  __attribute__((target("avx2"))) static void write_slot_bar(uint64_t* slot, const uint64_t* w, uint64_t seq) {
+  // A slot in device memory through the BAR: 32-byte stores of the `nw` words in
+  // use (a typical command is 3–4 PCIe writes, not the 16 of the whole 512-byte
+  // slot), the sequence word last.
+  __attribute__((target("avx2"))) static void write_slot_bar(uint64_t* slot, const uint64_t* w, uint64_t seq,
+                                                             uint32_t nw) {
     uint64_t first[4] = {0, w[1], w[2], w[3]};  // word 0 (sequence) stays "not ready" until the end
     _mm256_storeu_si256(reinterpret_cast<__m256i*>(slot), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(first)));
-    for (int k = 4; k < store::kSlotWords; k += 4)
+    for (uint32_t k = 4; k < nw; k += 4)
       _mm256_storeu_si256(reinterpret_cast<__m256i*>(slot + k),
                           _mm256_loadu_si256(reinterpret_cast<const __m256i*>(w + k)));
     _mm_sfence();
@@ -437,6 +442,13 @@ class StoreCore {
     const uint64_t idx = q % static_cast<uint64_t>(nslots_);
     volatile uint64_t* r = res_ + idx * store::kResWords;
     if (q >= next_) throw std::out_of_range("store: sequence number not posted");
+    if (r[0] < q + 1 && gpu_ && spin_ns <= 0) {
+      // just look: no spin (a 256-pause spin before the first clock check cost ≈3 µs
+      // on every speculation check and asyncio poll of a command still in flight)
+      if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) == 0) ensure_worker();
+      watched_[q] = 1;
+      return false;
+    }
     if (r[0] < q + 1 && gpu_) {
       auto t0 = std::chrono::steady_clock::now();
       uint32_t spins = 0;
