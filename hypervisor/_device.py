@@ -73,6 +73,7 @@ _SPEC_LIFECYCLE = os.environ.get("AHV_SPEC_LIFECYCLE", "1") != "0"
 _SPEC_TERMINATE = os.environ.get("AHV_SPEC_TERMINATE", "1") != "0"
 _STEPS = list(StepState)
 _STEP_IDX = {**{x: i for i, x in enumerate(_STEPS)}, **{x.value: i for i, x in enumerate(_STEPS)}}
+_COMMITTED_IDX = _STEP_IDX[StepState.COMMITTED]
 _SAGAS = list(SagaState)
 _RINGS = list(ExecutionRing)
 _MODE = {ConsistencyMode.EVENTUAL: 0, ConsistencyMode.STRONG: 1}
@@ -1424,9 +1425,10 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                     # EXECUTING: neither needs the device's answer before returning —
                     # both are verified with the store's next interaction
                     st = self._store
-                    st.expect(seq, _OK, (self._owner, _transition_refused, (step.slot, StepState.EXECUTING)))
-                    cseq = step.post_transition(StepState.COMMITTED)
-                    st.expect(cseq, _OK, (self._owner, _transition_refused, (step.slot, StepState.COMMITTED)))
+                    slot = step.slot
+                    st.expect(seq, _OK, (self._owner, _transition_refused, (slot, StepState.EXECUTING)))
+                    st._c.post_expect(_st.OP_STEP_TRANSITION, [slot, _COMMITTED_IDX, _now_us(), -1], None, _OK,
+                                      (self._owner, _transition_refused, (slot, StepState.COMMITTED)))
                     step.__dict__["_hint"] = StepState.COMMITTED
                     return result
                 if seq is not None:
