@@ -359,17 +359,18 @@ class StoreCore {
   }
 
   // A slot in device memory through the BAR: 32-byte stores of the `nw` words in
-  // use (a typical command is 3–4 PCIe writes, not the 16 of the whole 512-byte
-  // slot), the sequence word last.
+  // use (a typical command is 1–4 PCIe writes, not the 16 of the whole 512-byte
+  // slot): the argument / payload chunks, then the first chunk with the sequence
+  // word, then one fence.  Write-combined stores may reach the device in any
+  // order; a worker that sees the sequence word before the rest rejects the read
+  // through the checksum and polls again (store_worker.hip).
   __attribute__((target("avx2"))) static void write_slot_bar(uint64_t* slot, const uint64_t* w, uint64_t seq,
                                                              uint32_t nw) {
-    uint64_t first[4] = {0, w[1], w[2], w[3]};  // word 0 (sequence) stays "not ready" until the end
-    _mm256_storeu_si256(reinterpret_cast<__m256i*>(slot), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(first)));
     for (uint32_t k = 4; k < nw; k += 4)
       _mm256_storeu_si256(reinterpret_cast<__m256i*>(slot + k),
                           _mm256_loadu_si256(reinterpret_cast<const __m256i*>(w + k)));
-    _mm_sfence();
-    *reinterpret_cast<volatile uint64_t*>(slot) = seq;
+    const uint64_t first[4] = {seq, w[1], w[2], w[3]};
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(slot), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(first)));
     _mm_sfence();
   }
 
