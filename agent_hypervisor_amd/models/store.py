@@ -454,9 +454,7 @@ class GovernanceStore:
         """(delta row, arena offset, length, sequence, predicted digest): the last is
         the device's digest computed on the host (``parent``: the previous capture's
         predicted digest; None for turn 1 or when unknown → no prediction)."""
-        if self._c.npend(4) >= self.RECLAIM_BATCH:
-            self._c.reclaim_pool(4)
-        r = self._c.capture(slot, turn, ts_us, delta, parent)
+        r = self._c.capture(slot, turn, ts_us, delta, parent)  # reclaims released delta rows natively
         tries = 0
         while r[0] <= -2:
             self._make_room(r[0], tries)

@@ -211,6 +211,7 @@ class Store : public StoreCore {
   // the previous capture's predicted hex digest, spliced in quoted) — None when
   // the parent is not known.  The caller verifies it against the device later.
   py::tuple capture(int64_t slot, int64_t turn, int64_t ts_us, py::handle delta, const py::object& parent) {
+    if (npend(store::RK_D) >= kReclaimDeltas) reclaim_pool(store::RK_D);  // released delta rows back in bulk
     thread_local std::string buf;
     size_t at = 0;
     if (!render_delta(delta.ptr(), buf, &at)) return py::make_tuple(-1, -1, -1, -1, py::none());
@@ -218,8 +219,11 @@ class Store : public StoreCore {
     return py::make_tuple(p.didx, p.off, p.len, p.seq, p.didx >= 0 ? predict(buf, at, turn, parent) : py::none());
   }
 
+  static constexpr int64_t kReclaimDeltas = 256;  // == GovernanceStore.RECLAIM_BATCH
+
   py::tuple capture_bytes(int64_t slot, int64_t turn, int64_t ts_us, const py::bytes& payload, int64_t null_at,
                           const py::object& parent) {
+    if (npend(store::RK_D) >= kReclaimDeltas) reclaim_pool(store::RK_D);
     std::string buf = payload;
     if (null_at < 0 || static_cast<size_t>(null_at) + 4 > buf.size() || buf.compare(null_at, 4, "null") != 0)
       throw std::invalid_argument("capture_bytes: null_at does not point at the parent's null");
@@ -328,6 +332,8 @@ class Store : public StoreCore {
     d["gpu"] = gpu_;
     d["device"] = device_;
     d["posted"] = posted_;
+    d["ring_waits"] = ring_waits();
+    d["ring_wait_us"] = static_cast<double>(ring_wait_ns()) / 1e3;
     d["launches"] = launches_;
     d["nslots"] = nslots_;
     d["payload_live"] = payload_live();

@@ -302,7 +302,18 @@ class StoreCore {
     // has not collected its results yet, they are kept aside first
     if (q >= static_cast<uint64_t>(nslots_)) {
       const uint64_t p = q - static_cast<uint64_t>(nslots_);
-      const uint64_t* pr = wait(p);
+      const uint64_t* pr;
+      if (gpu_ && *reinterpret_cast<volatile uint64_t*>(res_ + (p % static_cast<uint64_t>(nslots_)) * store::kResWords) <
+                      p + 1) {
+        // the ring is full: the worker is a whole ring behind (telemetry: host back-pressure)
+        const auto t0 = std::chrono::steady_clock::now();
+        pr = wait(p);
+        ring_wait_ns_ += static_cast<uint64_t>(
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+        ++ring_waits_;
+      } else {
+        pr = wait(p);
+      }
       if (!watched_.empty()) {
         auto it = watched_.find(p);
         if (it != watched_.end()) {
@@ -855,6 +866,8 @@ class StoreCore {
   bool gpu() const { return gpu_; }
   int device() const { return device_; }
   uint64_t posted() const { return posted_; }
+  uint64_t ring_waits() const { return ring_waits_; }
+  uint64_t ring_wait_ns() const { return ring_wait_ns_; }
   uint64_t launches() const { return launches_; }
   int64_t nslots() const { return nslots_; }
   size_t kept() const { return watched_.size() + saved_.size(); }
@@ -898,6 +911,8 @@ class StoreCore {
   int speculate_ = 1;
   uint64_t next_ = 0;
   uint64_t posted_ = 0;
+  uint64_t ring_waits_ = 0;    // posts that found the ring full (waited for the worker)
+  uint64_t ring_wait_ns_ = 0;  // host time spent in those waits
   uint64_t launches_ = 0;
   size_t stage_head_ = 0;
   ArenaAlloc arena_;

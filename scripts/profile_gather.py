@@ -52,6 +52,7 @@ def main() -> None:
             "engine_busy_us_per_pipeline": round(d.get("engine_busy_us", 0) / n, 2),
             "commands_per_pipeline": round(d.get("posted", 0) / n, 3),
             "engine_jobs_per_pipeline": round(d.get("engine_jobs", 0) / n, 3),
+            "ring_wait_us_per_pipeline": round(d.get("ring_wait_us", 0) / n, 2),
         }), flush=True)
     pr = cProfile.Profile()
     pr.enable()
