@@ -25,7 +25,6 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -586,11 +585,7 @@ class StoreCore {
     const size_t len = hole ? buf.size() - 4 + 66 : buf.size();
     const int64_t didx = take_delta_row();
     if (didx < 0) return Placed{-2, -1, static_cast<int64_t>(len), -1};
-    int64_t off = arena_.alloc(static_cast<int64_t>(len));
-    if (off < 0 && !dfree_q_.empty()) {  // arena bytes still held by posted frees: wait for them first
-      settle_delta_frees(true);
-      off = arena_.alloc(static_cast<int64_t>(len));
-    }
+    const int64_t off = arena_.alloc(static_cast<int64_t>(len));
     if (off < 0) {
       dfree_.push_back(static_cast<int32_t>(didx));
       return Placed{-3, -1, static_cast<int64_t>(len), -1};
@@ -618,7 +613,6 @@ class StoreCore {
     const int64_t len = static_cast<int64_t>(n);
     const int64_t didx = take_delta_row();
     if (didx < 0) return {-2, -1};
-    if (!dfree_q_.empty()) settle_delta_frees(true);
     const int64_t off = arena_.alloc(len);
     if (off < 0) {
       dfree_.push_back(static_cast<int32_t>(didx));
@@ -635,7 +629,6 @@ class StoreCore {
   // pipelines render into them): `caps[i]` bytes each.  Fills rows/offs and returns
   // 0, or -2 (delta table full) / -3 (arena full) after releasing what it took.
   int reserve_deltas_raw(const int32_t* c, size_t n, int32_t* r, int64_t* o) {
-    if (!dfree_q_.empty()) settle_delta_frees(true);  // a batch reservation sees every freed row
     for (size_t i = 0; i < n; ++i) {
       const int64_t d = take_delta_row();
       const int64_t off = d < 0 ? -1 : arena_.alloc(c[i]);
@@ -671,49 +664,6 @@ class StoreCore {
       d_off_[static_cast<size_t>(d)] = -1;
       d_len_[static_cast<size_t>(d)] = 0;
       dfree_.push_back(d);
-    }
-  }
-
-  // Delta rows freed without waiting (the capture path's batched reclaim): OP_FREE_ROWS
-  // drains the hash engine on the device, which under a steady stream of captures
-  // takes a whole engine backlog (≈1.5 ms) — the host posts it and goes on; the rows
-  // and their arena bytes return to the free lists only once its result is in
-  // (settle_delta_frees), so no record is overwritten before the engine hashed it.
-  void free_deltas_async(std::vector<int32_t> rows) {
-    using namespace store;
-    if (rows.empty()) return;
-    for (int32_t d : rows)
-      if (d < 0 || d >= t_.cap.D || d_off_[static_cast<size_t>(d)] < 0)
-        throw std::invalid_argument("free_deltas: row " + std::to_string(d) + " is not allocated");
-    const size_t per = static_cast<size_t>(2 * kInlineWords);
-    for (size_t i = 0; i < rows.size(); i += per) {
-      const size_t n = std::min(per, rows.size() - i);
-      uint64_t a[3] = {RK_D, static_cast<uint64_t>(n), 0};
-      const uint64_t q = post_raw(OP_FREE_ROWS, a, 3, reinterpret_cast<const uint8_t*>(rows.data() + i), 4 * n);
-      keep(q);
-      dfree_q_.emplace_back(q, std::vector<int32_t>(rows.begin() + static_cast<std::ptrdiff_t>(i),
-                                                    rows.begin() + static_cast<std::ptrdiff_t>(i + n)));
-    }
-  }
-
-  // Return the rows of completed asynchronous delta frees (all of them with `block`).
-  void settle_delta_frees(bool block) {
-    while (!dfree_q_.empty()) {
-      const uint64_t q = dfree_q_.front().first;
-      uint64_t r[kSaveWords];
-      if (!try_result_raw(q, 0, r)) {
-        if (!block) return;
-        wait(q);
-        if (!try_result_raw(q, 0, r)) throw std::runtime_error("store: delta free " + std::to_string(q) + " lost");
-      }
-      if (r[1] != store::ST_OK) throw std::runtime_error("OP_FREE_ROWS failed with status " + std::to_string(r[1]));
-      for (int32_t d : dfree_q_.front().second) {
-        arena_.free(d_off_[static_cast<size_t>(d)], d_len_[static_cast<size_t>(d)]);
-        d_off_[static_cast<size_t>(d)] = -1;
-        d_len_[static_cast<size_t>(d)] = 0;
-        dfree_.push_back(d);
-      }
-      dfree_q_.pop_front();
     }
   }
 
@@ -826,10 +776,8 @@ class StoreCore {
       if (dpend_.empty()) return 0;
       std::vector<int32_t> rows;
       rows.swap(dpend_);
-      const int64_t n = static_cast<int64_t>(rows.size());
-      free_deltas_async(std::move(rows));
-      settle_delta_frees(false);
-      return n;
+      free_deltas(rows);
+      return static_cast<int64_t>(rows.size());
     }
     RowPool& p = pool(kind);
     if (p.pend.empty()) return 0;
@@ -895,7 +843,6 @@ class StoreCore {
   }
 
   int64_t take_delta_row() {
-    if (dfree_.empty() && !dfree_q_.empty()) settle_delta_frees(dhw_ >= t_.cap.D);  // wait only when full
     if (!dfree_.empty()) {
       const int32_t d = dfree_.back();
       dfree_.pop_back();
@@ -963,7 +910,6 @@ class StoreCore {
   uint64_t idle_ticks_ = 0, max_ticks_ = 0;
   int speculate_ = 1;
   uint64_t next_ = 0;
-  std::deque<std::pair<uint64_t, std::vector<int32_t>>> dfree_q_;  // posted, unconfirmed delta frees
   uint64_t posted_ = 0;
   uint64_t ring_waits_ = 0;    // posts that found the ring full (waited for the worker)
   uint64_t ring_wait_ns_ = 0;  // host time spent in those waits
