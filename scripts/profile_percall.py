@@ -69,6 +69,19 @@ def main() -> None:
 
     st = _device._shared_store(dev)
     tel0 = list(st._c.tail)[:5] if hasattr(st._c, "tail") else None
+    import gc
+
+    gc_t = {"n": [0, 0, 0], "ns": [0, 0, 0], "t0": 0}
+
+    def on_gc(phase, info):  # time spent in the cyclic collector, per generation
+        if phase == "start":
+            gc_t["t0"] = time.perf_counter_ns()
+        else:
+            g = info.get("generation", 0)
+            gc_t["n"][g] += 1
+            gc_t["ns"][g] += time.perf_counter_ns() - gc_t["t0"]
+
+    gc.callbacks.append(on_gc)
     info0 = st.info()
     c0 = time.process_time()
     w0 = time.perf_counter()
@@ -76,6 +89,8 @@ def main() -> None:
     wall = time.perf_counter() - w0
     cpu = time.process_time() - c0
     info1 = st.info()
+    gc.callbacks.remove(on_gc)
+    srt = sorted(lat)
     pr = cProfile.Profile()
     pr.enable()
     asyncio.run(run(300))
@@ -87,6 +102,8 @@ def main() -> None:
         "device": dev, "iters": iters, "p50_us": statistics.median(lat) / 1e3, "mean_us": statistics.mean(lat) / 1e3,
         "host_cpu_us_per_pipeline": cpu / iters * 1e6, "wall_us_per_pipeline": wall / iters * 1e6,
         "terminate_wait_p50_us": statistics.median(waits[-iters:]) / 1e3 if waits else None,
+        "p90_us": srt[int(0.9 * len(srt))] / 1e3, "p99_us": srt[int(0.99 * len(srt))] / 1e3, "max_us": srt[-1] / 1e3,
+        "gc_collections": gc_t["n"], "gc_us_per_pipeline": sum(gc_t["ns"]) / iters / 1e3,
         "commands_per_pipeline": (info1.get("posted", 0) - info0.get("posted", 0)) / iters,
         "store_info_delta": {k: info1[k] - info0[k] for k in info1 if isinstance(info1.get(k), (int, float))
                              and isinstance(info0.get(k), (int, float))},
