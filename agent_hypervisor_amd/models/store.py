@@ -131,7 +131,7 @@ class GovernanceStore:
     index) up to ``AHV_STORE_MAX_*``, then allocation raises :class:`StoreError`.
     """
 
-    RECLAIM_BATCH = 256
+    RECLAIM_BATCH = 4096  # released delta rows per reclaim (native: py_store.cpp kReclaimDeltas)
 
     def __init__(self, device: str = "cuda", caps: Optional[dict] = None, idle_us: Optional[int] = None,
                  max_caps: Optional[dict] = None) -> None:

@@ -219,7 +219,13 @@ class Store : public StoreCore {
     return py::make_tuple(p.didx, p.off, p.len, p.seq, p.didx >= 0 ? predict(buf, at, turn, parent) : py::none());
   }
 
-  static constexpr int64_t kReclaimDeltas = 256;  // == GovernanceStore.RECLAIM_BATCH
+  // Released delta rows reclaimed per batch.  The reclaim's OP_FREE_ROWS waits for the
+  // hash engine to drain (its records must be hashed before their arena bytes are
+  // reused), which under a steady capture stream is the engine's whole backlog
+  // (≈1.5 ms): batches of 4,096 rows pay it once per ≈1,400 pipelines instead of once
+  // per ≈85 (256 rows: a +19 µs mean on the per-call path, profiles/r4/
+  // percall_outliers_r4y_before_async_reclaim.txt).
+  static constexpr int64_t kReclaimDeltas = 4096;  // == GovernanceStore.RECLAIM_BATCH
 
   py::tuple capture_bytes(int64_t slot, int64_t turn, int64_t ts_us, const py::bytes& payload, int64_t null_at,
                           const py::object& parent) {
