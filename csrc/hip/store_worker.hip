@@ -42,6 +42,7 @@ namespace ahv {
 namespace store {
 
 constexpr int kJobs = 64;  // LDS capture-job ring
+constexpr uint64_t kFreeScan = 8192;  // session / delta rows a FREE_ROWS checks against the queue (longer: full drain)
 
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -51,6 +52,23 @@ __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
 }
 __device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Publication of a result slot: its words are system-scope stores to pinned host
+// memory, and the host only needs them to land before the sequence word.  With
+// feature bit 32 (`light`) the command wave's per-command publication is a wait
+// for the wave's outstanding stores (vmcnt 0) instead of a system-scope release,
+// whose L2 write-back of every dirty table line is paid on each command; table
+// rows still reach other agents through the full releases of the wholesale
+// commands (FLUSH, the host's drain NOP, FREE_ROWS — needs_drain) and of the
+// kernel's exit.  Captures (hash engine, payload bytes) keep the full release.
+__device__ __forceinline__ void publish_fence(bool light) {
+  if (light) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt/lgkmcnt unconstrained
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // and no compiler motion of the seq store above it
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
 }
 
 // ------------------------------------------------------- batched hash engine
@@ -89,7 +107,7 @@ __device__ int batch_size(const HashJob* jobs, uint32_t done, uint32_t avail, in
 
 // Lane `lane` < n hashes job jobs[(done + lane) % kJobs] and completes it.
 __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, int n, uint32_t* win,
-                           uint32_t* kwrows, uint64_t* res, int64_t nslots, int lane) {
+                           uint32_t* kwrows, uint64_t* res, int64_t nslots, int lane, bool light) {
   if (lane >= n) return;
   const HashJob j = jobs[(done + lane) % kJobs];
   uint32_t* w = win + kBatchStride * lane;
@@ -156,7 +174,7 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
   out64(r + 11, 0);
   out64(r + 12, static_cast<uint64_t>(nblk) | (static_cast<uint64_t>(n) << 32));  // blocks | batch size
   out64(r + 1, ST_OK);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // digest rows + result words before the sequence word
+  publish_fence(light);  // digest rows + result words before the sequence word
   out64(r, j.seq + 1);
 }
 
@@ -214,7 +232,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         // several captures queued: hash the distinct-session prefix one job per lane
         const int nb = batch_size(jobs, done, head - done, batch_sess, lane);
         if (nb >= 2) {
-          hash_batch(t, jobs, done, nb, batch_win, kw1, res, nslots, lane);
+          hash_batch(t, jobs, done, nb, batch_win, kw1, res, nslots, lane, false);
           done += static_cast<uint32_t>(nb);
           L.sync();
           if (lane == 0) lds_release(&q_done, done);
@@ -225,7 +243,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;
       capture_finish(L, t, j, r);
       if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // digest row + result words before the sequence word
+        publish_fence(false);  // digest row + result words before the sequence word
         out64(r, j.seq + 1);
       }
       ++done;
@@ -283,7 +301,46 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     if (lane >= 16) inl[lane - 16] = v;
     L.sync();
     c.inl = inl;
-    if (needs_drain(c.op)) {
+    // OP_FREE_ROWS of saga / step / vouch-edge / liability rows: the hash engine
+    // never touches those tables, so nothing to wait for.  Of session rows: only
+    // the queued captures (and a provisional tree) of the sessions being freed —
+    // not the engine's whole backlog, which stalled every command behind it for
+    // milliseconds once per few hundred released sessions.  Long lists and delta
+    // rows (their digests are what the engine writes) still drain it fully.
+    const bool free_rows = c.op == OP_FREE_ROWS;
+    const bool free_light = (speculate & 16) && free_rows && ((c.a[0] != RK_S && c.a[0] != RK_D) || c.a[1] <= kFreeScan);
+    if (free_light && (c.a[0] == RK_S || c.a[0] == RK_D)) {
+      // lanes stride over the freed rows (independent loads); each row is compared
+      // with the pending jobs' sessions (S) or delta rows (D: a queued job reads its
+      // record from the arena and writes its digest row), snapshotted into this
+      // wave's scratch.  A provisional tree in flight blocks freeing its session, and
+      // any delta rows (it reads its chain's digests).
+      const bool drows = c.a[0] == RK_D;
+      const IndexList idx = index_list(t, c, c.a[1], c.a[2]);
+      const int64_t n = static_cast<int64_t>(c.a[1]);
+      int32_t* pend = reinterpret_cast<int32_t*>(lds0);
+      for (;;) {
+        const uint32_t d0 = __shfl(lds_acquire(&q_done), 0);
+        const uint32_t np = queued - d0;  // ≤ kJobs
+        // spec_s is raised before q_done is released: read after q_done, it shows any
+        // tree started on a job this snapshot already counts as done
+        const int32_t sp = static_cast<int32_t>(__shfl(lds_acquire(&spec_s), 0)) - 1;
+        if (static_cast<uint32_t>(lane) < np) {
+          const HashJob& jb = jobs[(d0 + lane) % kJobs];
+          pend[lane] = static_cast<int32_t>(drows ? jb.d : jb.s);
+        }
+        L.sync();
+        bool hit = drows && sp >= 0;
+        for (int64_t i = lane; i < n && !hit; i += 64) {
+          const int32_t x = idx[i];
+          hit = x == sp;
+          for (uint32_t k = 0; k < np && !hit; ++k) hit = pend[k] == x;
+        }
+        L.sync();  // every lane has read `pend` before the next snapshot
+        if (__ballot(hit) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    } else if (!free_light && needs_drain(c.op)) {
       while (lds_acquire(&q_done) != queued) __builtin_amdgcn_s_sleep(1);
       if (c.op == OP_FREE_ROWS) {  // no provisional tree still writing a row about to be freed
         while (lds_acquire(&spec_s) != 0u) __builtin_amdgcn_s_sleep(1);
@@ -337,7 +394,8 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       }
       ++queued;
     } else if (lane == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      // (captures complete payload bytes the host may read by DMA: full release)
+      publish_fence((speculate & 32) != 0 && !needs_drain(c.op) && c.op != OP_DELTA_CAPTURE);
       out64(r, next + 1);
     }
     if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -183,8 +183,16 @@ class StoreCore {
       //     slows the engine's current one — both waves issue on one CU; p50 measured equal or
       //     slightly worse, profiles/r3/prefix_always_ab_r3aj.*)
       const char* pw = std::getenv("AHV_STORE_PREFIX_ALWAYS");
+      // 16 = FREE_ROWS waits only for the queued captures of the rows it frees (S, D) or
+      //      not at all (G, T, E, V), instead of draining the hash engine
+      const char* nf = std::getenv("AHV_STORE_NARROW_FREE");
+      // 32 = results published with a wait for the worker's stores, not a system release
+      //      (wholesale commands keep the full release; see publish_fence)
+      const char* lp = std::getenv("AHV_STORE_LIGHT_PUBLISH");
       speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
-                   ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) | ((pw != nullptr && std::atoi(pw) != 0) ? 8 : 0);
+                   ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) | ((pw != nullptr && std::atoi(pw) != 0) ? 8 : 0) |
+                   ((nf == nullptr || std::atoi(nf) != 0) ? 16 : 0) |
+                   ((lp != nullptr && std::atoi(lp) != 0) ? 32 : 0);
       max_ticks_ = static_cast<uint64_t>(max_ms) * 100000;
     } else {
       ring_ = static_cast<uint64_t*>(std::calloc(ring_bytes / 8, 8));

@@ -71,12 +71,14 @@ async def one():
 async def run(n):
     out = []
     for _ in range(n):
-        g0 = dict(st.grows); l0 = st._c.info()["launches"]; n0, ns0 = _gc["n"], _gc["ns"]
+        i0 = st._c.info(); g0 = dict(st.grows); l0 = i0["launches"]; n0, ns0 = _gc["n"], _gc["ns"]
+        lag0 = i0["posted"] - i0.get("worker_commands", i0["posted"])  # commands the worker has not run yet
         a = time.perf_counter_ns(); t = await one(); tot = time.perf_counter_ns() - a
         ev = {k: st.grows[k] - g0[k] for k in g0 if st.grows[k] != g0[k]}
         l1 = st._c.info()["launches"]
         if l1 != l0: ev["worker_launches"] = l1 - l0
         if _gc["n"] != n0: ev["gc2"] = (_gc["n"] - n0, round((_gc["ns"] - ns0) / 1e3, 1))
+        ev["lag_before"] = lag0
         out.append((tot, t, ev))
     return out
 asyncio.run(run(300))
@@ -84,6 +86,9 @@ res = asyncio.run(run(int(sys.argv[2]) if len(sys.argv) > 2 else 2000))
 res.sort(key=lambda x: -x[0])
 tots = sorted(r[0] for r in res)
 print("p50", tots[len(tots)//2]/1e3, "p99", tots[int(.99*len(tots))]/1e3, "mean", sum(tots)/len(tots)/1e3)
+lags = sorted(r[2]["lag_before"] for r in res)
+print("worker lag before a pipeline (commands): p50", lags[len(lags) // 2], "p90", lags[int(.9 * len(lags))],
+      "p99", lags[int(.99 * len(lags))], "max", lags[-1])
 print("slow calls (>1 ms): count, max us", SLOW)
 print("gen2 collections", _gc["n"], "total ms", round(_gc["ns"] / 1e6, 2), "worker launches", st._c.info()["launches"])
 for tot, t, g in res[:12]:
