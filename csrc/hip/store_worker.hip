@@ -56,7 +56,7 @@ __device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
 
 // Publication of a result slot: its words are system-scope stores to pinned host
 // memory, and the host only needs them to land before the sequence word.  With
-// feature bit 32 (`light`) the command wave's per-command publication is a wait
+// feature bit 32 (`light`, default on; AHV_STORE_LIGHT_PUBLISH=0 turns it off) the command wave's per-command publication is a wait
 // for the wave's outstanding stores (vmcnt 0) instead of a system-scope release,
 // whose L2 write-back of every dirty table line is paid on each command; table
 // rows still reach other agents through the full releases of the wholesale
@@ -276,9 +276,20 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   // telemetry accumulates across relaunches (tail[1..4] persist in pinned memory)
   uint64_t busy = static_cast<uint64_t>(__hip_atomic_load(tail + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
   uint64_t ncmd = static_cast<uint64_t>(__hip_atomic_load(tail + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  // feature bit 64 (default on; AHV_STORE_SLOT_PREFETCH=0 off): the next slot is loaded while the current command executes, so
+  // a worker running behind the host does not pay a fine-grained read round trip
+  // between commands (a stale or torn prefetch is simply re-polled)
+  uint64_t pre = 0;
+  bool have_pre = false;
   for (;;) {
     const uint64_t* slot = ring + (next % static_cast<uint64_t>(nslots)) * kSlotWords;
-    const uint64_t w = ld_sys(slot + lane);
+    uint64_t w;
+    if (have_pre) {
+      w = pre;
+      have_pre = false;
+    } else {
+      w = ld_sys(slot + lane);
+    }
     const uint64_t seq = __shfl(w, 0);
     if (seq != next + 1) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -301,6 +312,10 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     if (lane >= 16) inl[lane - 16] = v;
     L.sync();
     c.inl = inl;
+    if (speculate & 64) {
+      pre = ld_sys(ring + ((next + 1) % static_cast<uint64_t>(nslots)) * kSlotWords + lane);
+      have_pre = true;
+    }
     // OP_FREE_ROWS of saga / step / vouch-edge / liability rows: the hash engine
     // never touches those tables, so nothing to wait for.  Of session rows: only
     // the queued captures (and a provisional tree) of the sessions being freed —

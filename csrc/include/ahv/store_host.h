@@ -189,10 +189,13 @@ class StoreCore {
       // 32 = results published with a wait for the worker's stores, not a system release
       //      (wholesale commands keep the full release; see publish_fence)
       const char* lp = std::getenv("AHV_STORE_LIGHT_PUBLISH");
+      // 64 = prefetch the next command slot while the current command executes
+      const char* pf2 = std::getenv("AHV_STORE_SLOT_PREFETCH");
       speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
                    ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) | ((pw != nullptr && std::atoi(pw) != 0) ? 8 : 0) |
                    ((nf == nullptr || std::atoi(nf) != 0) ? 16 : 0) |
-                   ((lp != nullptr && std::atoi(lp) != 0) ? 32 : 0);
+                   ((lp == nullptr || std::atoi(lp) != 0) ? 32 : 0) |
+                   ((pf2 == nullptr || std::atoi(pf2) != 0) ? 64 : 0);
       max_ticks_ = static_cast<uint64_t>(max_ms) * 100000;
     } else {
       ring_ = static_cast<uint64_t*>(std::calloc(ring_bytes / 8, 8));
