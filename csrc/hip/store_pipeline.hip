@@ -496,29 +496,6 @@ AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g) {
   a.mid_blocks[g] = static_cast<int32_t>(pb);
 }
 
-// The 64 lowercase hex chars of digest `h` written at byte `p0` of a record as 16–17
-// aligned word stores (lanes of a wave write different records, so each store
-// instruction touches up to 64 cache lines: 17 word stores instead of 64 byte
-// stores).  Word k of the aligned span holds chars 4k−sh … 4k+3−sh (sh = p0 mod 4),
-// a byte-funnel of hex words k−1 and k; the edge words keep their bytes outside
-// the 64 chars (the placeholder's quotes and what precedes them).
-AHV_HD uint32_t sp_funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
-  return static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8u * sh));
-}
-
-AHV_HD void sp_put_hex(uint8_t* rec, int64_t p0, const uint32_t h[8]) {
-  uint32_t hx[16];
-  digest_to_hex_words(h, hx);  // big-endian: first char in the top byte
-  const uint32_t sh = static_cast<uint32_t>(p0 & 3);
-  uint32_t* w = reinterpret_cast<uint32_t*>(rec + (p0 - static_cast<int64_t>(sh)));  // reservations are 64-byte aligned
-  const uint32_t lo_mask = sh ? (0xffffffffu >> (32u - 8u * sh)) : 0u;  // memory bytes j < sh
-  const uint32_t first = bswap32(sp_funnel(0u, hx[0], sh));
-  w[0] = (w[0] & lo_mask) | (first & ~lo_mask);
-#pragma unroll
-  for (int k = 1; k < 16; ++k) w[k] = bswap32(sp_funnel(hx[k - 1], hx[k], sh));
-  if (sh) w[16] = (bswap32(sp_funnel(hx[15], 0u, sh)) & lo_mask) | (w[16] & ~lo_mask);
-}
-
 // Lane per session: the SHA-256 chain over its records (K08).
 AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
   const Tables& t = a.t;
@@ -529,7 +506,13 @@ AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
     uint8_t* rec = t.payload + t.d_off[d];
     const uint64_t len = static_cast<uint64_t>(t.d_len[d]);
     const int32_t hole = t.d_hole[d];
-    if (hole >= 0) sp_put_hex(rec, hole + 1, prev);  // hex(prev) between the placeholder's quotes
+    if (hole >= 0) {  // '"' + hex(prev) + '"' into the record
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rec[hole + 1 + 8 * q + e] = static_cast<uint8_t>(hex_nibble((prev[q] >> (28 - 4 * e)) & 15u));
+      }
+    }
     const uint32_t* w32 = reinterpret_cast<const uint32_t*>(rec);
     uint32_t h[8];
     const uint64_t nblk = (len + 9 + 63) / 64;
