@@ -126,7 +126,7 @@ static int64_t template_small() {
   return v;
 }
 
-// Occupancy variant (AHV_TEMPLATE_WAVES = 2 or 3 waves per SIMD).
+// Occupancy variant (AHV_TEMPLATE_WAVES = 2, 3 or 4 waves per SIMD; 4 uses a 2-block window).
 static int template_waves() {
   static const int v = [] {
     const char* e = std::getenv("AHV_TEMPLATE_WAVES");
@@ -278,6 +278,8 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
     hipLaunchKernelGGL((store_template_kernel<1, 6>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else if (template_waves() == 2)  // 231 VGPRs, no scratch
     hipLaunchKernelGGL((store_template_kernel<2, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
+  else if (template_waves() == 4)  // 2-block window (8.5 KiB LDS): 4 waves per SIMD, one more emission pass
+    hipLaunchKernelGGL((store_template_kernel<4, 2>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else  // 168 VGPRs (3 waves/SIMD) with a small spill
     hipLaunchKernelGGL((store_template_kernel<3, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   check_hip(hipGetLastError(), "store_template_kernel launch");
@@ -287,6 +289,7 @@ void kernels_store_template(std::vector<KernelEntry>& out) {
   out.push_back({"store_template_kernel<3,3>", reinterpret_cast<const void*>(&store_template_kernel<3, 3>)});
   out.push_back({"store_template_kernel<2,3>", reinterpret_cast<const void*>(&store_template_kernel<2, 3>)});
   out.push_back({"store_template_kernel<1,6>", reinterpret_cast<const void*>(&store_template_kernel<1, 6>)});
+  out.push_back({"store_template_kernel<4,2>", reinterpret_cast<const void*>(&store_template_kernel<4, 2>)});
 }
 
 }  // namespace ahv
