@@ -313,9 +313,11 @@ class GovernanceStore:
 
     def next_stamp(self) -> int:
         """A creation stamp for a session whose id is not a uuid: a per-store serial
-        with the top bit set (never a uuid4's low half, whose variant bits are 10)."""
+        with the top two bits 11.  A uuid4's low half always carries the RFC 4122
+        variant bits 10 there, so no uuid session can share a stamp with one of
+        these; the word is never zero (the serial starts at 1)."""
         self._stamp_seq += 1
-        return (1 << 63) | (0x3FFFFFFF << 32) | (self._stamp_seq & 0xFFFFFFFF)
+        return (3 << 62) | (self._stamp_seq & ((1 << 62) - 1))
 
     def agent_id(self, did: str) -> int:
         return self.agents.intern(did)

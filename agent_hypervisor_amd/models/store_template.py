@@ -150,13 +150,16 @@ class TemplatePipeline:
         t["t_state"].index_fill_(0, self._slots64["tslot"], 255)
 
     def launch(self, session_agent: torch.Tensor, t0: Optional[int] = None, stats: Optional[torch.Tensor] = None,
-               sync: bool = True) -> tuple:
+               sync: bool = True, variant: Optional[tuple] = None) -> tuple:
         """Run the pipeline for every session; ``session_agent`` = int32 [n] agent
         numbers (which agent joins and captures in each session).  ``stats``
         (int64[6]) accumulates sessions / ok / participants / deltas / commits /
         archived.  Returns ``(id_base, t0)`` of this launch.  ``sync``: make the
         store worker's pending writes visible first and its view of the new rows
-        after (off in a benchmark's steady state, where nothing else writes)."""
+        after (off in a benchmark's steady state, where nothing else writes).
+        ``variant``: ``(waves, small)`` kernel selection for this launch (default:
+        ``AHV_TEMPLATE_WAVES`` / ``AHV_TEMPLATE_SMALL``; ``small`` is the largest
+        batch that takes the one-pass ``<1,6>`` kernel)."""
         from hypervisor._clock import now_us
 
         st = self.store
@@ -187,6 +190,8 @@ class TemplatePipeline:
             "gc_retention_us": self.gc_retention_us, "status": tens["status"].data_ptr(),
             "stats": self._spread.begin().data_ptr() if stats is not None else None,
         }
+        if variant is not None:
+            args["waves"], args["small"] = int(variant[0]), int(variant[1])
         cuda = dev.type == "cuda"
         if cuda:
             if sync:
@@ -201,6 +206,7 @@ class TemplatePipeline:
             torch.cuda.synchronize(dev)
             st.acquire()  # the worker sees the batch's rows
         self.t0 = t0
+        self.last_id_base = id_base
         self._keep = sa  # the launch reads it asynchronously
         return id_base, t0
 
@@ -248,7 +254,7 @@ class _TemplateSpecs:
 
 def run(hv, n: int, agents: Optional[AgentSet] = None, session_agent=None, deltas: int = 3,
         changes=REFERENCE_CHANGES, now_us: Optional[int] = None, config=None,
-        creator_did: str = "did:mesh:admin"):
+        creator_did: str = "did:mesh:admin", variant: Optional[tuple] = None):
     """One template batch of ``n`` sessions registered with ``hv`` (lazily): returns
     a :class:`~agent_hypervisor_amd.models.store_pipeline.PipelineRun`.  Without
     ``agents``, a synthetic population the size of the batch (random-init σ) is
@@ -267,7 +273,7 @@ def run(hv, n: int, agents: Optional[AgentSet] = None, session_agent=None, delta
     if session_agent is None:
         session_agent = torch.arange(n, dtype=torch.int32) % agents.count
     sa = torch.as_tensor(session_agent, dtype=torch.int32)
-    id_base, t0 = tp.launch(sa, t0=now_us)
+    id_base, t0 = tp.launch(sa, t0=now_us, variant=variant)
     ids = tp.session_ids(id_base)
     # what the lazy views need, in one copy each (the batched API's finish step)
     status = tp.tens["status"].cpu().numpy()
@@ -300,3 +306,87 @@ def run(hv, n: int, agents: Optional[AgentSet] = None, session_agent=None, delta
                          join_codes=np.zeros(0, np.uint8))
     out._roots = (committed, flat)
     return out
+
+
+def reference_records(session_id: str, did: str, t0: int, deltas: int, changes=REFERENCE_CHANGES) -> list:
+    """The canonical-JSON records the scalar API renders for one template session
+    (reference ``audit/delta.py:41-64``): delta k at ``t0 + 1 + k`` µs, chained."""
+    import hashlib
+
+    from hypervisor._clock import from_us
+    from hypervisor.audit.delta import SemanticDelta, VFSChange, _payload_json
+
+    out, parent = [], None
+    for k in range(deltas):
+        chs = []
+        for spec in changes:
+            p, o, h = spec[0], spec[1], spec[2]
+            ph = spec[3] if len(spec) > 3 else None
+            chs.append(VFSChange(path=p.format(i=k), operation=o.format(i=k),
+                                 content_hash=h.format(i=k) if h is not None else None,
+                                 previous_hash=ph.format(i=k) if ph is not None else None))
+        d = SemanticDelta(delta_id=f"delta:{k + 1}", turn_id=k + 1, session_id=session_id, agent_did=did,
+                          timestamp=from_us(t0 + 1 + k), changes=chs, parent_hash=parent)
+        raw = _payload_json(d).encode()
+        out.append(raw)
+        parent = hashlib.sha256(raw).hexdigest()
+    return out
+
+
+def reference_merkle(leaves: list) -> Optional[str]:
+    """Reference ``compute_merkle_root`` (``audit/delta.py:117-134``) over hex leaves."""
+    import hashlib
+
+    if not leaves:
+        return None
+    level = list(leaves)
+    while len(level) > 1:
+        if len(level) % 2:
+            level.append(level[-1])
+        level = [hashlib.sha256((level[k] + level[k + 1]).encode()).hexdigest() for k in range(0, len(level), 2)]
+    return level[0]
+
+
+def check_sessions(tp: TemplatePipeline, id_base: int, t0: int, session_agent, idx) -> int:
+    """Oracle check of sessions ``idx`` of one :meth:`TemplatePipeline.launch`
+    (``id_base``, ``t0`` and the ``session_agent`` it was given) against the host:
+    every arena record equals the scalar renderer's bytes, every ``d_hash`` is
+    hashlib's SHA-256 of it, ``s_head`` is the last digest and ``s_root`` the
+    reference Merkle root.  Raises ``AssertionError`` naming the first mismatch;
+    returns the number of sessions checked."""
+    st = tp.store
+    idx = np.asarray(idx, dtype=np.int64)
+    if not len(idx):
+        return 0
+    D = tp.deltas
+    sa = torch.as_tensor(session_agent).to("cpu", torch.int64).numpy()[idx]
+    slots = tp.slots[idx].astype(np.int64)
+    rows = tp.drows.reshape(-1, D)[idx].astype(np.int64) if D else np.zeros((len(idx), 0), np.int64)
+    offs = tp.doff.reshape(-1, D)[idx] if D else np.zeros((len(idx), 0), np.int64)
+    w8 = np.arange(8, dtype=np.int64)
+    flat = rows.reshape(-1)
+    g = st.gather({"d_len": flat, "d_hash": (flat[:, None] * 8 + w8).reshape(-1),
+                   "s_head": (slots[:, None] * 8 + w8).reshape(-1), "s_root": (slots[:, None] * 8 + w8).reshape(-1),
+                   "s_committed": slots, "s_state": slots})
+    lens = g["d_len"].astype(np.int64).reshape(len(idx), D)
+    hx = lambda w: w.astype(np.uint32).byteswap().tobytes().hex()  # noqa: E731 - 8 digest words → hex
+    dh = g["d_hash"].reshape(len(idx), D, 8)
+    heads, roots = g["s_head"].reshape(-1, 8), g["s_root"].reshape(-1, 8)
+    audit = bool(tp.config.enable_audit) and D > 0
+    for k, i in enumerate(idx.tolist()):
+        sid = C.uuids_from_counters(tp.seed, id_base + i, 1, "session:")[0]
+        did = tp.agents.dids[int(sa[k])]
+        recs = reference_records(sid, did, t0, D, tp.changes)
+        got = st._c.payload_gather(offs[k].astype(np.int64), lens[k]) if D else b""
+        assert got == b"".join(recs), f"session {i} ({sid}): arena records differ from the scalar renderer"
+        import hashlib
+
+        leaves = [hashlib.sha256(r).hexdigest() for r in recs]
+        dev_leaves = [hx(dh[k, d]) for d in range(D)]
+        assert dev_leaves == leaves, f"session {i}: d_hash differs from hashlib"
+        if D:
+            assert hx(heads[k]) == leaves[-1], f"session {i}: s_head is not the chain's last digest"
+        if audit:
+            assert int(g["s_committed"][k]) != 0, f"session {i}: not committed"
+            assert hx(roots[k]) == reference_merkle(leaves), f"session {i}: s_root is not the reference Merkle root"
+    return len(idx)

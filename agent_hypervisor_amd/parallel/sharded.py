@@ -73,6 +73,12 @@ from agent_hypervisor_amd.parallel.directory import stable_rank
 from hypervisor.models import ConsistencyMode, SessionConfig
 
 _CTRL: dict = {}
+
+
+class ViewAborted(RuntimeError):
+    """An agent-global view whose collective was abandoned by :meth:`ShardedHypervisor.failover`."""
+
+
 _EPOCH_US = 1_577_836_800_000_000  # 2020-01-01T00:00:00Z: creation keys are µs after this
 
 
@@ -207,6 +213,7 @@ class ShardedHypervisor:
         self.local = Hypervisor(device=device, **hv_kwargs)
         self.bus = self.local.event_bus
         self._comm: Optional[ThreadPoolExecutor] = None  # the communication thread of the views
+        self._inflight: set = set()  # asyncio futures of view collectives running on that thread
         self.members = list(range(self.world))
         self._live = frozenset(self.members)
         self.group = None if self.world == 1 else control_group()
@@ -260,8 +267,14 @@ class ShardedHypervisor:
         if self.rpc is not None:
             await self.rpc.close()
             self.rpc = None
+        self._drop_comm()
+
+    def _drop_comm(self) -> None:
+        """Abandon the views' communication thread without waiting for it: a
+        collective still blocked on a group that lost a rank must not hold up
+        shutdown or the next view (it ends when its backend times out)."""
         if self._comm is not None:
-            self._comm.shutdown(wait=True)
+            self._comm.shutdown(wait=False, cancel_futures=True)
             self._comm = None
 
     async def _handle(self, name: str, args: list, kwargs: dict) -> Any:
@@ -741,7 +754,17 @@ class ShardedHypervisor:
         if t is not None and (self.world > 1 or wait_s):
             if self._comm is None:
                 self._comm = ThreadPoolExecutor(max_workers=1, thread_name_prefix="ahv-comm")
-            await asyncio.get_running_loop().run_in_executor(self._comm, self._blocking_collective, t, op, wait_s)
+            fut = asyncio.get_running_loop().run_in_executor(self._comm, self._blocking_collective, t, op, wait_s)
+            self._inflight.add(fut)
+            try:
+                await fut
+            except asyncio.CancelledError:
+                if fut.cancelled():  # failover() abandoned it: the group lost a member
+                    raise ViewAborted(f"view {name!r} aborted: a member failed while its collective was open") \
+                        from None
+                raise
+            finally:
+                self._inflight.discard(fut)
         return self._finish(name, args, part, t)
 
     def _blocking_collective(self, t: torch.Tensor, op, wait_s: float) -> None:
@@ -1027,7 +1050,12 @@ class ShardedHypervisor:
                 self._sagas.update({g: s for g, s in m.get("sagas", {}).items() if s in mine_set})
                 for vid, key in m.get("vouch_key", {}).items():
                     self._vouch_key.setdefault(vid, tuple(key))
-        # only the survivors synchronise on these groups (the failed ranks never call in)
+        # only the survivors synchronise on these groups (the failed ranks never call in);
+        # a view collective still blocked on the old group stays on the old thread, and the
+        # next view gets a fresh communication thread bound to the new groups
+        for fut in list(self._inflight):  # their callers get ViewAborted instead of waiting on the old group
+            fut.cancel()
+        self._drop_comm()
         self.group = dist.new_group(ranks=self.members, backend="gloo", use_local_synchronization=True)
         self.data_group = dist.new_group(ranks=self.members, use_local_synchronization=True)
         self.failovers.append({"failed": failed, "moves": len(moves)})

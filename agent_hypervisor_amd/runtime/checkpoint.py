@@ -94,11 +94,20 @@ def read_manifest(d: str, kind: str) -> dict:
         raise CheckpointError(f"{d}: format version {man['version']} is newer than supported {VERSION}")
     if man.get("kind") != kind:
         raise CheckpointError(f"{d}: checkpoint kind {man.get('kind')!r}, expected {kind!r}")
+    if kind == "engine" and man.get("version", 0) < VERSION:
+        # v1 engine checkpoints hold a list-shaped interner and no participant/arena
+        # tables: refuse them here instead of failing inside load_engine
+        raise CheckpointError(f"{d}: engine checkpoint format version {man.get('version', 0)} is no longer "
+                              f"supported (current {VERSION}); re-save it with this version")
     for f, digest in man["files"].items():
         fp = os.path.join(d, f)
         if not os.path.exists(fp):
             raise CheckpointError(f"{d}: missing {f}")
-        if digest == "k10":  # verified record by record by the loader (store_checkpoint.load_store)
+        if digest == "k10":
+            # only the columnar hypervisor layout's arena.bin is verified record by record by
+            # its loader (store_checkpoint.load_store): anywhere else "k10" is a forged entry
+            if not (f == "arena.bin" and kind == "hypervisor" and man.get("layout") == "columnar"):
+                raise CheckpointError(f"{d}: {f} carries a record-verified digest outside the columnar arena")
             continue
         if _sha(fp) != digest:
             raise CheckpointError(f"{d}: {f} is corrupt (sha256 mismatch)")

@@ -382,9 +382,11 @@ class _Collect:
         g0, g1 = b.goff[idx], b.goff[idx + 1]
         gcnt = g1 - g0
         ng = int(gcnt.sum())
-        for i in idx.tolist():
-            if i in b.extras:
-                self.extras[base + int(np.searchsorted(idx, i))] = b.extras[i]
+        if b.extras:  # position of each batch index in `idx` (any order)
+            for k, i in enumerate(idx.tolist()):
+                ex = b.extras.get(i)
+                if ex is not None:
+                    self.extras[base + k] = ex
         if not ng:
             return
         gix = np.repeat(g0 - np.concatenate([[0], np.cumsum(gcnt)[:-1]]), gcnt) + np.arange(ng)

@@ -205,7 +205,9 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
                     if verbose and err.strip():
                         print(err, file=sys.stderr)
         out = ext_path()
-        if todo or not out.exists():
+        # relink when anything compiled, the .so is missing, or an object is newer than
+        # it (an interrupted earlier build): exactly the objects needs_build() checks
+        if todo or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
             tmp = out.with_suffix(".tmp.so")
             r = subprocess.run(_link_cmd(objs, tmp), capture_output=True, text=True)
             if r.returncode != 0:

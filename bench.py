@@ -137,10 +137,20 @@ def api_section(args, scalar_p50) -> dict:
     }
 
 
+def _headline_kernel(n: int) -> str:
+    """The store_template_kernel variant a batch of ``n`` sessions runs (store_template.hip)."""
+    if n <= int(os.environ.get("AHV_TEMPLATE_SMALL", "65536")):
+        return "store_template_kernel<1,6>"
+    w = int(os.environ.get("AHV_TEMPLATE_WAVES", "3"))
+    return {2: "store_template_kernel<2,3>", 4: "store_template_kernel<4,2>"}.get(w, "store_template_kernel<3,3>")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--verify-sessions", type=int, default=64,
+                    help="sessions of the last timed step oracle-checked against the host after timing")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sessions", type=int, default=1 << 22,
                     help="sessions per GPU per step (4M: the launch amortises its tail; 1M measured 7%% lower)")
@@ -295,10 +305,13 @@ def main() -> None:
         hetero = {"hv": hv, "p": hp, "status0": status0,
                   "deltas": int(hp.nd), "committed": len(hp.committed), "ok": int((status0 == 0).sum())}
 
+    last_launch: dict = {}
+
     def run_batch(st, agents):
         if tmpl is not None:
             tmpl.reset()
-            tmpl.launch(agents, stats=st, sync=False)
+            last_launch["ids"] = tmpl.launch(agents, stats=st, sync=False)
+            last_launch["agents"] = agents
             return
         if hetero is None:
             eng.run_pipeline(S, agents=agents, deltas=args.deltas, stats=st)
@@ -430,9 +443,14 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_api and dev.type == "cuda":  # 1-GPU runs (the N>1 scaling runs skip it)
         api = api_section(args, scalar_p50)
 
-    if tmpl is not None:  # the rows the timed steps wrote are ordinary store sessions: spot-check one
+    verified = None
+    if tmpl is not None:  # the rows the timed steps wrote are ordinary store sessions: oracle-check some
         sync()
         assert bool((tmpl.tens["status"] == 0).all()), "template pipeline refused sessions"
+        id_base, t0 = last_launch["ids"]
+        pick = torch.randint(0, S, (args.verify_sessions,), generator=torch.Generator().manual_seed(99 + rank))
+        # arena records, d_hash, s_head and s_root of the last timed step vs scalar render + hashlib
+        verified = TT.check_sessions(tmpl, id_base, t0, last_launch["agents"], pick.numpy())
     if rank == 0:
         total_sessions = S * world * args.steps
         value = total_sessions / elapsed
@@ -479,6 +497,9 @@ def main() -> None:
                 "x01_exposure_allreduce_bytes": x01_bytes if liab is not None else 0,
                 "x02_slash_allgather_bytes_per_rank": x02_bytes if liab is not None else 0,
             },
+            "headline_verified": bool(verified) if tmpl is not None else None,
+            "headline_verified_sessions": verified,
+            "headline_kernel": (_headline_kernel(S) if dev.type == "cuda" else "host twin") if tmpl is not None else None,
             "mix": args.mix,
             "state": "governance_tables (--graph)" if eng is not None else "store rows",
             "hetero": None if hetero is None else {

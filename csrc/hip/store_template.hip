@@ -272,13 +272,17 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
     }
     b.t.payload = scratch;
   }
+  // variant selection: per call ("waves" / "small" in the argument dict: oracle tests of
+  // every variant in one process) or per process (AHV_TEMPLATE_WAVES / AHV_TEMPLATE_SMALL)
+  const int waves = d.contains("waves") && !d["waves"].is_none() ? d["waves"].cast<int>() : template_waves();
+  const int64_t small = d.contains("small") && !d["small"].is_none() ? d["small"].cast<int64_t>() : template_small();
   py::gil_scoped_release nogil;
   const dim3 grid(static_cast<uint32_t>((a.n + kWaveLanes - 1) / kWaveLanes)), block(kWaveLanes);
-  if (a.n <= template_small())  // latency-bound: one pass per record
+  if (a.n <= small)  // latency-bound: one pass per record
     hipLaunchKernelGGL((store_template_kernel<1, 6>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
-  else if (template_waves() == 2)  // 231 VGPRs, no scratch
+  else if (waves == 2)  // 231 VGPRs, no scratch
     hipLaunchKernelGGL((store_template_kernel<2, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
-  else if (template_waves() == 4)  // 2-block window (8.5 KiB LDS): 4 waves per SIMD, one more emission pass
+  else if (waves == 4)  // 2-block window (8.5 KiB LDS): 4 waves per SIMD, one more emission pass
     hipLaunchKernelGGL((store_template_kernel<4, 2>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else  // 168 VGPRs (3 waves/SIMD) with a small spill
     hipLaunchKernelGGL((store_template_kernel<3, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);

@@ -341,6 +341,8 @@ class Store : public StoreCore {
     d["ring_waits"] = ring_waits();
     d["ring_wait_us"] = static_cast<double>(ring_wait_ns()) / 1e3;
     d["launches"] = launches_;
+    d["reclaims"] = reclaims();
+    d["reclaim_waits"] = reclaim_waits();
     d["nslots"] = nslots_;
     d["payload_live"] = payload_live();
     d["payload_head"] = payload_head();

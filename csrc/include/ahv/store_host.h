@@ -693,6 +693,8 @@ class StoreCore {
         a[2] = static_cast<uint64_t>(stage_raw(raw, 4 * n));
         q = post_raw(OP_FREE_ROWS, a, 3, nullptr, 0);
       }
+      volatile uint64_t* rs = res_ + (q % static_cast<uint64_t>(nslots_)) * store::kResWords;
+      if (rs[0] < q + 1) ++reclaim_waits_;  // not answered yet: this wait blocks
       const uint64_t* r = wait(q);
       if (r[1] != ST_OK) throw std::runtime_error("OP_FREE_ROWS failed with status " + std::to_string(r[1]));
     }
@@ -787,6 +789,7 @@ class StoreCore {
       if (dpend_.empty()) return 0;
       std::vector<int32_t> rows;
       rows.swap(dpend_);
+      ++reclaims_;
       free_deltas(rows);
       return static_cast<int64_t>(rows.size());
     }
@@ -795,6 +798,7 @@ class StoreCore {
     check_frees();
     std::vector<int32_t> rows;
     rows.swap(p.pend);
+    ++reclaims_;
     post_frees(kind, rows);
     p.free.insert(p.free.end(), rows.begin(), rows.end());
     return static_cast<int64_t>(rows.size());
@@ -842,6 +846,7 @@ class StoreCore {
       } else {
         volatile uint64_t* r = res_ + (q % static_cast<uint64_t>(nslots_)) * store::kResWords;
         if (r[0] < q + 1 && !block) break;
+        if (r[0] < q + 1) ++reclaim_waits_;
         st = wait(q)[1];
         watched_.erase(q);
       }
@@ -880,6 +885,8 @@ class StoreCore {
   uint64_t ring_waits() const { return ring_waits_; }
   uint64_t ring_wait_ns() const { return ring_wait_ns_; }
   uint64_t launches() const { return launches_; }
+  uint64_t reclaims() const { return reclaims_; }
+  uint64_t reclaim_waits() const { return reclaim_waits_; }
   int64_t nslots() const { return nslots_; }
   size_t kept() const { return watched_.size() + saved_.size(); }
   const int64_t* tail() const { return tail_; }
@@ -925,6 +932,8 @@ class StoreCore {
   uint64_t ring_waits_ = 0;    // posts that found the ring full (waited for the worker)
   uint64_t ring_wait_ns_ = 0;  // host time spent in those waits
   uint64_t launches_ = 0;
+  uint64_t reclaims_ = 0;        // reclaim_pool passes that returned queued rows (any table)
+  uint64_t reclaim_waits_ = 0;   // times a reclaim blocked on a FREE_ROWS result
   size_t stage_head_ = 0;
   ArenaAlloc arena_;
   std::unordered_map<uint64_t, int> watched_;                             // seqs with a pending async waiter

@@ -36,6 +36,8 @@ import struct
 from datetime import datetime, timedelta
 from typing import Any, Callable, Optional
 
+import numpy as np
+
 from agent_hypervisor_amd._native import C as _C
 from agent_hypervisor_amd.models import store as _st
 from agent_hypervisor_amd.models.store import GovernanceStore, bitsd, dbits
@@ -1540,6 +1542,94 @@ def saga_rows(store: GovernanceStore, sagas: list) -> dict:
     out = store.gather({"g_state": gi, "g_created": gi, "g_completed": gi,
                         "t_state": ti, "t_retry": ti, "t_started": ti, "t_completed": ti})
     return out
+
+
+class _ClosedStore:
+    """Stands in for the store in the views of a closed hypervisor: their rows were
+    returned by :func:`close_hypervisor`, so any use raises (a freed row may already
+    hold another session) and a late finaliser releases nothing twice."""
+
+    __slots__ = ()
+
+    def release(self, kind, row) -> None:
+        pass
+
+    def release_many(self, kind, rows) -> None:
+        pass
+
+    def release_tenant(self, tenant, edges) -> None:
+        pass
+
+    def __getattr__(self, name):
+        raise _st.StoreError("this session belongs to a closed Hypervisor: its store rows were released")
+
+    def __bool__(self) -> bool:
+        return True
+
+
+CLOSED = _ClosedStore()
+
+
+def _close_views(st: GovernanceStore, m) -> None:
+    """Release the rows of one built device session and detach its views."""
+    sso, de, orch = m.sso, m.delta_engine, m.saga
+    if getattr(sso, "_store", None) is not st:
+        return
+    st.release("S", sso.slot)
+    sso._store = CLOSED
+    if isinstance(de, DeviceDeltaEngine):
+        if de._rows:
+            st.release_many("D", de._rows)
+        de._rows = []
+        for d in de._deltas:
+            d.__dict__["_store"] = CLOSED
+        de._store = CLOSED
+    if isinstance(orch, DeviceSagaOrchestrator):
+        for g in orch._sagas.values():
+            st.release("G", g.slot)
+            g.__dict__["_store"] = CLOSED
+            for x in g.steps:
+                st.release("T", x.slot)
+                x.__dict__["_store"] = CLOSED
+        orch._store = CLOSED
+
+
+def close_hypervisor(hv) -> int:
+    """Return every store row a device-backed hypervisor holds — sessions, their
+    participants' rows, delta chains with their arena records, sagas, steps, vouch
+    edges and liability-session rows — to the store, whatever Python still refers
+    to them; afterwards its views raise :class:`StoreError`.  Returns the number
+    of sessions closed.  Called by :meth:`Hypervisor.close` (and when the
+    hypervisor object goes away)."""
+    st = hv._store
+    if st is None or st is CLOSED or getattr(st, "_closed", False):
+        return 0
+    try:
+        st.verify_deferred(block=True)  # speculated posts of these rows complete first
+    except Exception:  # noqa: BLE001 - a divergence belongs to a session being closed anyway
+        pass
+    n = 0
+    for kind, seg in list(hv._sessions.segments()):
+        if kind == "own":
+            for m in seg:
+                _close_views(st, m)
+                n += 1
+            continue
+        for m in list(seg.views.values()):
+            _close_views(st, m)
+        seg.release(np.arange(len(seg.slots), dtype=np.int64))
+        n += len(seg.index)
+    ve = hv.vouching
+    if isinstance(ve, DeviceVouchingEngine) and ve._store is st:
+        st.release_tenant(ve._tenant, list(ve._by_edge))
+        for rec in ve._by_edge.values():
+            rec.__dict__["_store"] = CLOSED
+        ve._by_edge = {}
+        ve._store = CLOSED
+    if isinstance(hv.commitment, DeviceCommitmentEngine):
+        hv.commitment._store = CLOSED
+    hv._store = CLOSED
+    return n
 
 
 def session_views(store: GovernanceStore, sso: DeviceSession):

@@ -157,6 +157,37 @@ class Hypervisor:
         self._sessions = SessionTable()
         self.batched_sessions = 0  # sessions written by pipeline_batch / run_pipelines (ordinary sessions)
 
+    # -- lifetime ------------------------------------------------------------
+    def close(self) -> int:
+        """Device-backed: return every store row this hypervisor holds (sessions,
+        participants, delta chains and their records, sagas, steps, vouch edges)
+        to the shared store now, whatever Python still refers to them; its session
+        views raise afterwards.  Also runs when the hypervisor object is dropped, so
+        row lifetime follows the hypervisor, not the collector.  Returns the number
+        of sessions closed (0 for host engines, which hold no device rows)."""
+        if self._store is None:
+            return 0
+        return _device_mod().close_hypervisor(self)
+
+    def __del__(self) -> None:
+        try:
+            if getattr(self, "_store", None) is not None:
+                self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown / store already closed
+            pass
+
+    def __enter__(self) -> "Hypervisor":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    async def __aenter__(self) -> "Hypervisor":
+        return self
+
+    async def __aexit__(self, *exc) -> None:
+        self.close()
+
     # -- events --------------------------------------------------------------
     def _emit(self, etype, session_id=None, agent_did=None, **payload) -> None:
         bus = self.event_bus

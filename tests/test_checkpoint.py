@@ -122,6 +122,59 @@ async def test_tampered_payload_with_fixed_manifest_fails_chain_check(tmp_path):
         load_hypervisor(d)
 
 
+async def _populated_device() -> Hypervisor:
+    hv = Hypervisor(device="cpu")
+    for k in range(2):
+        m = await hv.create_session(SessionConfig(), "did:admin")
+        sid = m.sso.session_id
+        await hv.join_session(sid, f"did:a{k}", sigma_raw=0.8)
+        await hv.activate_session(sid)
+        for t in range(3):
+            m.delta_engine.capture(f"did:a{k}", [VFSChange(f"/f{t}", "add", f"h{t}")])
+    return hv
+
+
+async def test_columnar_arena_byte_flip_fails_reverification(tmp_path):
+    """arena.bin is protected by the K10 pass, not a file digest — one
+    flipped byte (manifest untouched) must fail the chain re-verification."""
+    hv = await _populated_device()
+    d = save_hypervisor(hv, str(tmp_path / "ck"))
+    man = json.load(open(os.path.join(d, "manifest.json")))
+    assert man["layout"] == "columnar" and man["files"]["arena.bin"] == "k10"
+    p = os.path.join(d, "arena.bin")
+    raw = bytearray(open(p, "rb").read())
+    raw[len(raw) // 2] ^= 0x01
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(CheckpointError, match="re-verification"):
+        load_hypervisor(d, hv=Hypervisor(device="cpu"))
+
+
+async def test_forged_k10_entry_is_refused(tmp_path):
+    """"k10" is accepted only for the columnar arena: a manifest marking
+    store.json (or a store.safetensors) as record-verified is rejected."""
+    hv = await _populated_device()
+    d = save_hypervisor(hv, str(tmp_path / "ck"))
+    mp_ = os.path.join(d, "manifest.json")
+    man = json.load(open(mp_))
+    man["files"]["store.json"] = "k10"
+    json.dump(man, open(mp_, "w"))
+    with pytest.raises(CheckpointError, match="record-verified"):
+        load_hypervisor(d, hv=Hypervisor(device="cpu"))
+
+
+def test_v1_engine_checkpoint_refused_cleanly(tmp_path):
+    """a version-1 engine manifest fails with CheckpointError up front."""
+    eng = GovernanceEngine(device="cpu", session_capacity=64, agent_capacity=64, seed=1)
+    eng.register_synthetic_agents(10)
+    d = save_engine(eng, str(tmp_path / "eng"))
+    mp_ = os.path.join(d, "manifest.json")
+    man = json.load(open(mp_))
+    man["version"] = 1
+    json.dump(man, open(mp_, "w"))
+    with pytest.raises(CheckpointError, match="no longer supported"):
+        load_engine(d, device="cpu")
+
+
 def test_missing_manifest_and_kind(tmp_path):
     with pytest.raises(CheckpointError, match="manifest"):
         load_hypervisor(str(tmp_path))

@@ -362,6 +362,92 @@ def test_failover_rehydrates_dead_rank(tmp_path):
     assert res["new_owner"] in (0, 1) and res["saga_steps"] == 1 and res["root_changed"]
 
 
+def _abort_worker(rank: int, world: int, root: str, q) -> None:
+    """Rank 2 dies while every rank sits in a ``hold`` view's collective; the
+    survivors fail over and their next views complete."""
+    os.environ.update(AHV_STORE="host")
+    dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
+    import time
+
+    from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor, ViewAborted
+    from hypervisor import SessionConfig
+
+    shv = ShardedHypervisor(device="host", policy="round_robin")
+    shv.start_heartbeat(0.2)
+
+    async def main():
+        await shv.start()
+        from agent_hypervisor_amd.parallel.resilience import _store
+
+        st = _store()
+        if rank == 0:
+            for k in range(4):
+                await shv.create_session(SessionConfig(), f"did:admin-{k}", rank=k % 2)
+            st.set("test/built", "1")
+        else:
+            await asyncio.get_running_loop().run_in_executor(None, st.wait, ["test/built"])
+        shv.checkpoint(root)
+        if rank == 0:
+            view = asyncio.ensure_future(shv.hold(4.0))  # every rank enters a 4 s collective
+            await asyncio.sleep(0.5)
+            st.set("test/in_view", "1")
+        else:
+            await asyncio.get_running_loop().run_in_executor(None, st.wait, ["test/in_view"])
+            view = None
+        if rank == world - 1:  # dies inside the view's collective
+            shv.heartbeat.stop()
+            os._exit(0)
+        deadline = time.time() + 60
+        dead = []
+        while time.time() < deadline and not dead:
+            await asyncio.sleep(0.2)
+            dead = shv.dead_ranks(2.0)
+        verdict = shv.agree_failed(dead)
+        t0 = time.time()
+        await shv.failover(verdict, root)
+        if rank != 0:
+            await shv.serve_forever()
+            return None
+        aborted = None
+        try:
+            await asyncio.wait_for(view, 30)
+        except ViewAborted:
+            aborted = True
+        except Exception as e:  # noqa: BLE001 - the collective itself failed first (peer reset)
+            aborted = type(e).__name__
+        stats = await asyncio.wait_for(shv.stats(), 60)
+        res = dict(verdict=verdict, aborted=aborted, stats=stats, members=shv.members, after_s=time.time() - t0)
+        await shv.shutdown()
+        await shv.close()
+        return res
+
+    res = asyncio.run(main())
+    if rank == 0:
+        q.put(res)
+        q.close()
+        q.join_thread()
+    os._exit(0)
+
+
+def test_view_in_flight_when_a_rank_dies_does_not_block_later_views(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_abort_worker, args=(r, 3, str(tmp_path), q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    try:
+        res = q.get(timeout=150)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert res["verdict"] == [2] and res["members"] == [0, 1]
+    assert res["aborted"] is not None  # the open view ended (aborted) instead of hanging
+    assert res["stats"]["total_sessions"] == 4  # the next view runs on the survivors' groups
+    assert res["after_s"] < 30
+
+
 def _agree_worker(rank: int, world: int, root: str, q) -> None:
     dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
     from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor

@@ -14,6 +14,7 @@ from agent_hypervisor_amd.models import store as st_mod
 from agent_hypervisor_amd.models.store import StoreError, dbits
 from hypervisor._clock import now_us as _now_us
 from hypervisor import Hypervisor, SessionConfig
+from hypervisor.audit.delta import VFSChange
 from hypervisor.models import SessionState
 
 
@@ -156,41 +157,94 @@ def test_dropped_sessions_release_rows_without_the_cyclic_collector():
         assert after[k] == before[k], (k, before, after)
 
 
-def test_create_session_latency_under_a_full_table_has_no_collector_spikes():
-    """A full session table reclaims the queued rows (one OP_FREE_ROWS) instead of
-    running the cyclic collector: p99 of create_session stays within 2x its p50."""
-    import statistics
-    import time
+def test_full_session_table_recycles_rows_without_collector_or_blocking_waits(monkeypatch):
+    """3,000 pipelines through a 64-row session table with the cyclic collector
+    off: rows come back only by reference counting and the store's own reclaim.
+    Counted, not timed: no explicit gc.collect, the table never
+    grows, the reclaim runs in batches (one OP_FREE_ROWS per ≥ 8 rows) and no
+    create_session ever blocks on a FREE_ROWS result."""
+    import gc
 
     from agent_hypervisor_amd.models.store import GovernanceStore
 
     st = GovernanceStore("cpu", caps={"S": 64, "G": 64, "T": 64}, max_caps={"S": 64})
-    junk = [[object()] * 8 for _ in range(200_000)]  # a large heap: a collector pass would cost milliseconds
+    collects = []
+    real_collect = gc.collect
+    monkeypatch.setattr(gc, "collect", lambda *a, **k: collects.append(1) or real_collect(*a, **k))
+    create_waits = []
 
     async def go():
-        times = []
         for i in range(3000):
             hv = Hypervisor(store=st)
-            t0 = time.perf_counter_ns()
+            w0 = st.info()["reclaim_waits"]
             m = await hv.create_session(SessionConfig(), "did:admin")
-            times.append(time.perf_counter_ns() - t0)
+            create_waits.append(st.info()["reclaim_waits"] - w0)
             await hv.join_session(m.sso.session_id, "did:a", sigma_raw=0.8)
             await hv.activate_session(m.sso.session_id)
             await hv.terminate_session(m.sso.session_id)
-        return times
 
-    ratios = []
-    for _ in range(3):  # timing on a shared CPU: the best of three runs (a collector spike shows in all)
-        times = _run(go())[500:]
-        p50 = statistics.median(times)
-        p99 = sorted(times)[int(0.99 * len(times))]
-        ratios.append((p99 / p50, p50, p99))
-        if p99 <= 2 * p50:
-            break
-    del junk
-    if os.environ.get("PYTEST_XDIST_WORKER"):
-        return  # other test processes share the CPUs: tail latency is theirs too
-    assert min(r[0] for r in ratios) <= 2.0, ratios
+    info0 = st.info()
+    gc.disable()
+    try:
+        _run(go())
+    finally:
+        gc.enable()
+    info1 = st.info()
+    reclaims = info1["reclaims"] - info0["reclaims"]
+    assert not collects
+    assert st.caps["S"] == 64 and st.grows["S"] == 0
+    assert 3000 // 64 <= reclaims <= 3000 // 8 + 4, reclaims  # batched: never one command per row
+    assert sum(create_waits) == 0
+
+
+async def test_close_returns_every_row_while_views_are_still_held():
+    """Row lifetime follows the hypervisor: ``close()`` (or
+    dropping the hypervisor, with the collector off) returns its rows even though
+    the caller still holds session views, which then refuse to be used."""
+    import gc
+
+    from agent_hypervisor_amd.models.store import GovernanceStore, StoreError
+
+    st = GovernanceStore("cpu")
+    st.verify_deferred(block=True)
+    st.reclaim()
+    base = dict(st.live_rows())
+    held = []
+    gc.disable()
+    try:
+        for closing in (True, False):
+            hv = Hypervisor(store=st)
+            for k in range(3):
+                m = await hv.create_session(SessionConfig(), "did:admin")
+                sid = m.sso.session_id
+                await hv.join_session(sid, "did:a", sigma_raw=0.8)
+                await hv.activate_session(sid)
+                for t in range(2):
+                    m.delta_engine.capture("did:a", [VFSChange(path=f"/f{t}", operation="add", content_hash="h")])
+                g = m.saga.create_saga(sid)
+                m.saga.add_step(g.saga_id, "a", "did:a", "/x")
+                hv.vouching.vouch("did:a", "did:b", sid, 0.9)
+                held.append(m)
+            run = await hv.run_pipelines(_spec(), 5)
+            held.append(hv.get_session(run.session_ids[0]))
+            if closing:
+                assert hv.close() == 3 + 5
+            del hv  # dropped: the second round is released by the drop itself
+            st.verify_deferred(block=True)
+            st.reclaim()
+            assert dict(st.live_rows()) == base
+    finally:
+        gc.enable()
+    with pytest.raises(StoreError, match="closed Hypervisor"):
+        held[0].sso.participants
+    with pytest.raises(StoreError, match="closed Hypervisor"):
+        held[-1].delta_engine.compute_merkle_root()
+
+
+def _spec():
+    from agent_hypervisor_amd.models.store_pipeline import PipelineSpec
+
+    return PipelineSpec()
 
 
 def test_speculation_off_gives_the_same_results(monkeypatch):
