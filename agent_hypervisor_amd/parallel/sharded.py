@@ -23,13 +23,17 @@ sessions it owns) and serves requests *independently*:
   =======================================  ======================================
   reference route (api/server.py)          combination
   =======================================  ======================================
-  ``GET /api/v1/stats`` (:145-163)         X04 all-reduce of the counters, each
-                                           rank's from one batched device read
+  ``GET /api/v1/stats`` (:145-163)         X04: each rank's counters reduced on
+                                           the device over its rows (no snapshot
+                                           per session), one 48-byte all-reduce
   ``GET /agents/{did}/ring`` (:319-331)    X05 all-reduce MIN of (creation time,
                                            rank, ring) keys
-  ``GET /agents/{did}/liability`` (:570)   the agent's vouch records from every
-                                           rank, summed in global vouch order
-                                           (bit-exact with one rank)
+  ``GET /agents/{did}/liability`` (:570)   owner-routed (P02): the agent's owner
+                                           rank gathers every rank's compact
+                                           record set from its per-agent index
+                                           point to point and sums exposure in
+                                           global vouch order (bit-exact with
+                                           one rank); no rank-0 sequencing
   dense per-agent exposure                 X01: K04 over each rank's store edge
                                            columns → [A] fp64 all-reduce
   ``GET /api/v1/sessions``                 per-rank snapshots, merged by creation
@@ -148,6 +152,7 @@ _SERVED = (
     "capture", "merkle_root", "vouch", "compute_sigma_eff", "get_total_exposure", "release_session_bonds",
     "slash", "create_saga", "add_step", "execute_step", "compensate", "get_saga",
     "ring_distribution", "list_sagas", "list_vouches", "sso",
+    "agent_liability_owner", "liability_part",
     "_view", "_view_enter", "_stop",
 )
 
@@ -226,6 +231,8 @@ class ShardedHypervisor:
         self._sagas: dict[str, str] = {}  # saga id → session id (sagas this rank owns)
         self._vouch_seq = 0
         self._vouch_key: dict[str, tuple] = {}  # vouch id → global order key (created µs, rank, seq)
+        self._agent_ix: dict[str, list] = {}  # agent DID → its vouch records on this rank (creation order)
+        self._agent_ix_n = 0  # records the index covers
         self._view_lock: Optional[asyncio.Lock] = None
         self._stopped: Optional[asyncio.Event] = None
         self.heartbeat = None
@@ -442,6 +449,7 @@ class ShardedHypervisor:
         v = self.local.vouching.vouch(voucher_did, vouchee_did, session_id, voucher_sigma, bond_pct, exp)
         self._vouch_seq += 1
         self._vouch_key[v.vouch_id] = (_us(v.created_at), self.rank, self._vouch_seq)
+        self._index_vouch(v)
         if emit:  # the REST route's event (reference api/server.py vouch handler)
             from hypervisor.observability.event_bus import EventType
 
@@ -695,8 +703,29 @@ class ShardedHypervisor:
 
     async def agent_liability(self, agent_did: str) -> dict:
         """The agent's vouches given/received on every rank in global vouch order;
-        exposure = Σ live bonds given, summed in that order (bit-exact with one rank)."""
-        return await self._view("agent_liability", agent_did)
+        exposure = Σ live bonds given, summed in that order (bit-exact with one rank).
+
+        Owner-routed (P02): the agent's owner rank — a stable hash of its DID over
+        the live ranks — asks every rank for its compact record set (point to point,
+        no collective, no rank-0 sequencing) and combines them.  Each rank answers
+        from its per-agent vouch index (O(the agent's records), never a scan of all
+        vouches) with bond state from one gather of the store's edge columns."""
+        self.counters["views"] += 1
+        o = self.owner(agent_did)
+        if o == self.rank:
+            return await self._local_agent_liability_owner(agent_did)
+        self.counters["forwarded"] += 1
+        return await self.rpc.call(o, "agent_liability_owner", agent_did)
+
+    async def _local_agent_liability_owner(self, agent_did: str) -> dict:
+        parts = [self._local_liability(agent_did)]
+        others = [r for r in self.members if r != self.rank]
+        if others:
+            parts += await asyncio.gather(*[self.rpc.call(r, "liability_part", agent_did) for r in others])
+        return self._combine("agent_liability", (agent_did,), parts)
+
+    async def _local_liability_part(self, agent_did: str) -> list:
+        return self._local_liability(agent_did)
 
     async def exposure_vector(self, agent_dids: list[str]) -> list[float]:
         """X01 dense: live bonded exposure of each agent over every rank's sessions —
@@ -786,20 +815,15 @@ class ShardedHypervisor:
         hv = self.local
         dev = _tensor_device()
         if name == "stats":
-            snaps = hv.snapshots()  # one batched device read
-            sagas = hv.saga_summaries()
-            vals = [len(snaps), sum(1 for x in snaps if x.state.value not in ("archived", "terminating")),
-                    sum(x.participant_count for x in snaps),
-                    sum(1 for g in sagas if g["state"] in ("running", "compensating")),
-                    len(hv.vouching.records()), len(sagas)]
+            # device counters over the rank's rows (one reduction, no snapshot per
+            # session), then the 48-byte X04 all-reduce
+            c = hv.counters()
+            vals = [c[k] for k in _STAT_KEYS]
             return None, torch.tensor(vals, dtype=torch.int64, device=dev), dist.ReduceOp.SUM, 0.0
         if name == "agent_ring":
             (agent_did,) = args
             best, sid = self._local_first_ring(agent_did)
             return (best, sid), torch.tensor([best], dtype=torch.int64, device=dev), dist.ReduceOp.MIN, 0.0
-        if name == "agent_liability":
-            (agent_did,) = args
-            return self._local_liability(agent_did), None, None, 0.0
         if name == "exposure_vector":
             (dids,) = args
             return None, self._local_exposure(dids), dist.ReduceOp.SUM, 0.0
@@ -883,11 +907,33 @@ class ShardedHypervisor:
                     break
         return best, sid
 
+    def _agent_records(self, agent_did: str) -> list:
+        """This rank's vouch records naming the agent (voucher or vouchee), in
+        creation order, from the per-agent index (rebuilt in one pass whenever
+        records arrived by another path: checkpoint re-hydration, migration)."""
+        recs = self.local.vouching.records()
+        if self._agent_ix_n != len(recs):
+            ix: dict = {}
+            for v in recs:
+                ix.setdefault(v.voucher_did, []).append(v)
+                if v.vouchee_did != v.voucher_did:
+                    ix.setdefault(v.vouchee_did, []).append(v)
+            self._agent_ix, self._agent_ix_n = ix, len(recs)
+        return self._agent_ix.get(agent_did, [])
+
+    def _index_vouch(self, v) -> None:
+        if self._agent_ix_n == len(self.local.vouching.records()) - 1:
+            self._agent_ix.setdefault(v.voucher_did, []).append(v)
+            if v.vouchee_did != v.voucher_did:
+                self._agent_ix.setdefault(v.vouchee_did, []).append(v)
+            self._agent_ix_n += 1
+
     def _local_liability(self, agent_did: str) -> list:
-        """This rank's vouch records naming the agent, each with its global order
-        key; bond state for all of them from one gather of the edge columns."""
+        """This rank's compact record set for the agent: ``[created µs, rank, seq,
+        vouch id, voucher, vouchee, session id, bond pct, bonded, active, expired]``
+        per record; bond state for all of them from one gather of the edge columns."""
         hv = self.local
-        recs = [v for v in hv.vouching.records() if v.voucher_did == agent_did or v.vouchee_did == agent_did]
+        recs = self._agent_records(agent_did)
         st = hv._store
         state = {}
         if st is not None:
@@ -898,8 +944,9 @@ class ShardedHypervisor:
         out = []
         for v in recs:
             key = self._vouch_key.get(v.vouch_id, (_us(v.created_at), self.rank, 1 << 40))
-            d = _vouch_dict(v, state.get(getattr(v, "edge", -1)) if st is not None else None)
-            out.append([list(key), d])
+            act = state.get(getattr(v, "edge", -1)) if st is not None else None
+            out.append([*key, v.vouch_id, v.voucher_did, v.vouchee_did, v.session_id, v.bonded_sigma_pct,
+                        v.bonded_amount, int(bool(v.is_active) if act is None else act), int(bool(v.is_expired))])
         return out
 
     def _combine(self, name: str, args, parts: list) -> Any:
@@ -920,9 +967,7 @@ class ShardedHypervisor:
         if name == "hold":
             return parts[0]
         if name == "stats":
-            keys = ("total_sessions", "active_sessions", "total_participants", "active_sagas", "total_vouches",
-                    "total_sagas")
-            return dict(zip(keys, parts[0]))
+            return dict(zip(_STAT_KEYS, parts[0]))
         if name == "agent_ring":
             g = parts[0][0]
             if g >= (1 << 62) - 1:
@@ -931,7 +976,7 @@ class ShardedHypervisor:
             return {"agent_did": args[0], "ring": g & 0xF, "session_id": sid}
         if name == "agent_liability":
             agent_did = args[0]
-            allv = sorted(((tuple(k), d) for part in parts for k, d in part), key=lambda r: r[0])
+            allv = sorted(((tuple(r[:3]), _compact_vouch(r)) for part in parts for r in part), key=lambda r: r[0])
             given = [d for _, d in allv if d["voucher_did"] == agent_did]
             received = [d for _, d in allv if d["vouchee_did"] == agent_did]
             exposure = 0.0
@@ -1063,6 +1108,14 @@ class ShardedHypervisor:
 
 
 _NO_RING = (1 << 62) - 1
+_STAT_KEYS = ("total_sessions", "active_sessions", "total_participants", "active_sagas", "total_vouches",
+              "total_sagas")
+
+
+def _compact_vouch(r: list) -> dict:
+    """A compact record of :meth:`ShardedHypervisor._local_liability` as the route's dict."""
+    return {"vouch_id": r[3], "voucher_did": r[4], "vouchee_did": r[5], "session_id": r[6],
+            "bonded_sigma_pct": r[7], "bonded_amount": r[8], "is_active": bool(r[9]), "is_expired": bool(r[10])}
 
 
 def _vouch_dict(v, active: Optional[bool] = None) -> dict:

@@ -692,7 +692,7 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
             for k, w in enumerate(_device._words(c["merkle_root"])):
                 put("s_root", 8 * s + k, w)
             hv.commitment.register(sso)
-        saga_orch = _device.DeviceSagaOrchestrator(st, sso)
+        saga_orch = _device.DeviceSagaOrchestrator(st, sso, hv._sessions.saga_rows)
         for g in r["sagas"]:
             gslot = st.alloc("G")
             saga = _device.DeviceSaga(st, gslot, g["saga_id"], g["session_id"])
@@ -716,6 +716,7 @@ def _load_device(hv, d: str, records: list, verify: bool, only=None):
                     put(col, tslot, v)
                 saga.steps.append(step)
             saga_orch._sagas[saga.saga_id] = saga
+            hv._sessions.saga_rows.append(gslot)
         m = ManagedSession(sso, de, saga_orch)
         for e in r["reversibility"]:
             m.reversibility.register(ActionDescriptor(

@@ -343,6 +343,7 @@ class Store : public StoreCore {
     d["launches"] = launches_;
     d["reclaims"] = reclaims();
     d["reclaim_waits"] = reclaim_waits();
+    d["double_releases"] = double_releases();
     d["nslots"] = nslots_;
     d["payload_live"] = payload_live();
     d["payload_head"] = payload_head();

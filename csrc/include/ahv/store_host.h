@@ -671,6 +671,7 @@ class StoreCore {
         throw std::invalid_argument("free_deltas: row " + std::to_string(d) + " is not allocated");
     free_rows_cmd(store::RK_D, rows);
     for (int32_t d : rows) {
+      mark(dreleased_, d, 0);
       arena_.free(d_off_[static_cast<size_t>(d)], d_len_[static_cast<size_t>(d)]);
       d_off_[static_cast<size_t>(d)] = -1;
       d_len_[static_cast<size_t>(d)] = 0;
@@ -717,7 +718,17 @@ class StoreCore {
   struct RowPool {
     int64_t cap = 0, hw = 0;
     std::vector<int32_t> free, pend;
+    std::vector<uint8_t> live;  // 1 while handed out and not released (double-release guard)
   };
+
+  static void mark(std::vector<uint8_t>& v, int64_t row, uint8_t x) {
+    if (row < 0) return;
+    if (static_cast<size_t>(row) >= v.size()) v.resize(std::max<size_t>(static_cast<size_t>(row) + 1, 2 * v.size()), 0);
+    v[static_cast<size_t>(row)] = x;
+  }
+  static bool is_set(const std::vector<uint8_t>& v, int64_t row) {
+    return row >= 0 && static_cast<size_t>(row) < v.size() && v[static_cast<size_t>(row)] != 0;
+  }
 
   static size_t pool_index(uint64_t kind) {
     switch (kind) {
@@ -746,9 +757,13 @@ class StoreCore {
     if (!p.free.empty()) {
       const int32_t r = p.free.back();
       p.free.pop_back();
+      mark(p.live, r, 1);
       return r;
     }
-    if (p.hw < p.cap) return p.hw++;
+    if (p.hw < p.cap) {
+      mark(p.live, p.hw, 1);
+      return p.hw++;
+    }
     return -1;
   }
 
@@ -763,25 +778,43 @@ class StoreCore {
       p.free.pop_back();
     }
     while (k < n) out[k++] = static_cast<int32_t>(p.hw++);
+    for (int64_t i = 0; i < n; ++i) mark(p.live, out[i], 1);
     return true;
   }
 
+  // A released row leaves the live set once: a second release of the same row (two
+  // views that both believed they owned it) is counted and ignored, so a row can
+  // never enter the free list twice and be handed to two sessions.
   void release_row(uint64_t kind, int64_t row) {
     if (kind == store::RK_D) {
+      if (row < 0 || row >= dhw_ || d_off_[static_cast<size_t>(row)] < 0 || is_set(dreleased_, row)) {
+        ++double_releases_;
+        return;
+      }
+      mark(dreleased_, row, 1);
       dpend_.push_back(static_cast<int32_t>(row));
       return;
     }
-    pool(kind).pend.push_back(static_cast<int32_t>(row));
+    RowPool& p = pool(kind);
+    if (!is_set(p.live, row)) {
+      ++double_releases_;
+      return;
+    }
+    mark(p.live, row, 0);
+    p.pend.push_back(static_cast<int32_t>(row));
   }
 
   void release_rows_raw(uint64_t kind, const int32_t* rows, int64_t n) {
-    std::vector<int32_t>& v = kind == store::RK_D ? dpend_ : pool(kind).pend;
-    v.insert(v.end(), rows, rows + n);
+    for (int64_t i = 0; i < n; ++i) release_row(kind, rows[i]);
   }
 
   // A row that was allocated but never written on the device (a refused vouch):
   // straight back to the free list.
-  void return_row(uint64_t kind, int64_t row) { pool(kind).free.push_back(static_cast<int32_t>(row)); }
+  void return_row(uint64_t kind, int64_t row) {
+    RowPool& p = pool(kind);
+    mark(p.live, row, 0);
+    p.free.push_back(static_cast<int32_t>(row));
+  }
 
   // Return the queued rows of `kind` to its free list; returns their count.
   int64_t reclaim_pool(uint64_t kind) {
@@ -887,6 +920,7 @@ class StoreCore {
   uint64_t launches() const { return launches_; }
   uint64_t reclaims() const { return reclaims_; }
   uint64_t reclaim_waits() const { return reclaim_waits_; }
+  uint64_t double_releases() const { return double_releases_; }
   int64_t nslots() const { return nslots_; }
   size_t kept() const { return watched_.size() + saved_.size(); }
   const int64_t* tail() const { return tail_; }
@@ -932,6 +966,8 @@ class StoreCore {
   uint64_t ring_waits_ = 0;    // posts that found the ring full (waited for the worker)
   uint64_t ring_wait_ns_ = 0;  // host time spent in those waits
   uint64_t launches_ = 0;
+  uint64_t double_releases_ = 0;  // releases of rows that were not live (ignored)
+  std::vector<uint8_t> dreleased_;  // delta rows released and not yet reclaimed
   uint64_t reclaims_ = 0;        // reclaim_pool passes that returned queued rows (any table)
   uint64_t reclaim_waits_ = 0;   // times a reclaim blocked on a FREE_ROWS result
   size_t stage_head_ = 0;

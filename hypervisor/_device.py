@@ -196,9 +196,12 @@ class DeviceSession(SharedSessionObject):
 
     def __del__(self) -> None:
         # the row stays allocated while this view (or a delta engine / saga built
-        # on it) exists; afterwards the store may reclaim it
+        # on it) exists; afterwards the store may reclaim it.  The view is detached
+        # first: in cyclic garbage another finaliser (Hypervisor.close) may still
+        # see this object and must not release the row a second time.
         try:
-            self._store.release("S", self.slot)
+            st, self._store = self._store, CLOSED
+            st.release("S", self.slot)
         except Exception:
             pass
 
@@ -598,8 +601,10 @@ class DeviceDeltaEngine(DeltaEngine):
 
     def __del__(self) -> None:
         try:
-            if self._rows:
-                self._store.release_many("D", self._rows)
+            rows, self._rows = self._rows, []
+            st, self._store = self._store, CLOSED
+            if rows:
+                st.release_many("D", rows)
         except Exception:
             pass
 
@@ -835,7 +840,9 @@ class DeviceVouchingEngine(VouchingEngine):
 
     def __del__(self) -> None:
         try:
-            self._store.release_tenant(self._tenant, list(self._by_edge))
+            edges, self._by_edge = list(self._by_edge), {}
+            st, self._store = self._store, CLOSED
+            st.release_tenant(self._tenant, edges)
         except Exception:
             pass
 
@@ -1176,7 +1183,9 @@ class DeviceSagaStep(SagaStep):
 
     def __del__(self) -> None:
         try:
-            self._store.release("T", self.slot)
+            st = self.__dict__.get("_store")
+            self.__dict__["_store"] = CLOSED
+            st.release("T", self.slot)
         except Exception:
             pass
 
@@ -1279,7 +1288,9 @@ class DeviceSaga(Saga):
 
     def __del__(self) -> None:
         try:
-            self._store.release("G", self.slot)
+            st = self.__dict__.get("_store")
+            self.__dict__["_store"] = CLOSED
+            st.release("G", self.slot)
         except Exception:
             pass
 
@@ -1357,10 +1368,11 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
     loop; every state change they cause is a device command.
     """
 
-    def __init__(self, store: GovernanceStore, owner: Optional[DeviceSession] = None) -> None:
+    def __init__(self, store: GovernanceStore, owner: Optional[DeviceSession] = None, reg=None) -> None:
         self._store = store
         self._sagas: dict[str, DeviceSaga] = {}
         self._owner = owner  # the session whose speculated step transitions these are
+        self._reg = reg  # the hypervisor's saga-row registry (SessionTable.saga_rows), when known
 
     def _guard(self) -> None:
         o = self._owner
@@ -1379,6 +1391,9 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         saga = DeviceSaga(self._store, slot, saga_id or _C.uuid4("saga:"), session_id)
         self._store.post(_st.OP_SAGA_CREATE, [slot, _now_us()])
         self._sagas[saga.saga_id] = saga
+        reg = self._reg
+        if reg is not None:
+            reg.append(slot)
         return saga
 
     def add_step(self, saga_id: str, action_id: str, agent_did: str, execute_api: str,
@@ -1571,26 +1586,30 @@ CLOSED = _ClosedStore()
 
 
 def _close_views(st: GovernanceStore, m) -> None:
-    """Release the rows of one built device session and detach its views."""
+    """Release the rows of one built device session and detach its views.  Each
+    view is handled on its own: in cyclic garbage some of them may already have
+    run their finaliser (which detached them after releasing their row)."""
     sso, de, orch = m.sso, m.delta_engine, m.saga
-    if getattr(sso, "_store", None) is not st:
-        return
-    st.release("S", sso.slot)
-    sso._store = CLOSED
+    if getattr(sso, "_store", None) is st:
+        st.release("S", sso.slot)
+        sso._store = CLOSED
     if isinstance(de, DeviceDeltaEngine):
-        if de._rows:
-            st.release_many("D", de._rows)
-        de._rows = []
+        if de._store is st:
+            rows, de._rows = de._rows, []
+            if rows:
+                st.release_many("D", rows)
+            de._store = CLOSED
         for d in de._deltas:
             d.__dict__["_store"] = CLOSED
-        de._store = CLOSED
     if isinstance(orch, DeviceSagaOrchestrator):
         for g in orch._sagas.values():
-            st.release("G", g.slot)
-            g.__dict__["_store"] = CLOSED
+            if g.__dict__.get("_store") is st:
+                st.release("G", g.slot)
+                g.__dict__["_store"] = CLOSED
             for x in g.steps:
-                st.release("T", x.slot)
-                x.__dict__["_store"] = CLOSED
+                if x.__dict__.get("_store") is st:
+                    st.release("T", x.slot)
+                    x.__dict__["_store"] = CLOSED
         orch._store = CLOSED
 
 
@@ -1632,9 +1651,51 @@ def close_hypervisor(hv) -> int:
     return n
 
 
-def session_views(store: GovernanceStore, sso: DeviceSession):
-    """(delta engine, saga orchestrator) for a device session."""
-    return DeviceDeltaEngine(store, sso.slot, sso.session_id, sso), DeviceSagaOrchestrator(store, sso)
+def session_views(store: GovernanceStore, sso: DeviceSession, saga_reg=None):
+    """(delta engine, saga orchestrator) for a device session (``saga_reg``: the
+    hypervisor's saga-row registry the orchestrator appends to)."""
+    return DeviceDeltaEngine(store, sso.slot, sso.session_id, sso), DeviceSagaOrchestrator(store, sso, saga_reg)
+
+
+_S_ARCHIVED, _S_TERMINATING = _STATES.index(SessionState.ARCHIVED), _STATES.index(SessionState.TERMINATING)
+_G_LIVE = (_SAGAS.index(SagaState.RUNNING), _SAGAS.index(SagaState.COMPENSATING))
+
+
+def counters(hv) -> dict:
+    """The REST ``/stats`` counters of a device-backed hypervisor, reduced on the
+    device over its rows: sessions (table size), active sessions (row state not
+    archived / terminating), participants (Σ active participant rows), active
+    sagas (RUNNING or COMPENSATING) and sagas, vouches (the engine's records).
+    O(1) store commands (one release of the worker's writes) and one 4-word copy
+    back, however many sessions (reference api/server.py:144-163)."""
+    import torch
+
+    st = hv._store
+    tab = hv._sessions
+    slots = tab.session_slots()
+    g_own = np.frombuffer(tab.saga_rows, dtype=np.int64) if len(tab.saga_rows) else np.zeros(0, np.int64)
+    grows = np.concatenate([g_own, tab.batch_saga_rows()])
+    out = {"total_sessions": len(tab), "total_vouches": len(hv.vouching.records()), "total_sagas": int(len(grows))}
+    if not len(slots) and not len(grows):
+        out.update(active_sessions=0, total_participants=0, active_sagas=0)
+        return out
+    st.drain()
+    if st.device.type == "cuda":
+        st.flush()
+    dev = st.device
+    t = st.tables
+    res = torch.zeros(3, dtype=torch.int64, device=dev)
+    if len(slots):
+        ix = torch.from_numpy(slots).to(dev)
+        sst = t["s_state"].index_select(0, ix)
+        res[0] = ((sst != _S_ARCHIVED) & (sst != _S_TERMINATING)).sum()
+        res[1] = t["s_pactive"].index_select(0, ix).to(torch.int64).sum()
+    if len(grows):
+        gs = t["g_state"].index_select(0, torch.from_numpy(grows).to(dev))
+        res[2] = ((gs == _G_LIVE[0]) | (gs == _G_LIVE[1])).sum()
+    a, p, g = res.cpu().tolist()
+    out.update(active_sessions=int(a), total_participants=int(p), active_sagas=int(g))
+    return out
 
 
 __all__ = [

@@ -111,15 +111,14 @@ async def health_check() -> dict[str, str]:
 async def get_stats(request: Request) -> StatsResponse:
     st = _state(request)
     hv = st.hv
-    snaps = hv.snapshots()  # one batched device read for all sessions
-    sagas = hv.saga_summaries()
+    c = hv.counters()  # device-backed: one reduction over the rows, no per-session snapshot
     return StatsResponse(
         version=__version__,
-        total_sessions=len(snaps),
-        active_sessions=sum(1 for x in snaps if x.state.value not in ("archived", "terminating")),
-        total_participants=sum(x.participant_count for x in snaps),
-        active_sagas=sum(1 for g in sagas if g["state"] in ("running", "compensating")),
-        total_vouches=len(hv.vouching.records()),
+        total_sessions=c["total_sessions"],
+        active_sessions=c["active_sessions"],
+        total_participants=c["total_participants"],
+        active_sagas=c["active_sagas"],
+        total_vouches=c["total_vouches"],
         event_count=st.bus.event_count,
         batched_sessions=hv.batched_sessions,
     )

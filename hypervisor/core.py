@@ -206,7 +206,7 @@ class Hypervisor:
         if self._store is not None:
             _device = _device_mod()
             sso = _device.DeviceSession(self._store, config, creator_did, session_id=session_id)  # HANDSHAKING
-            managed = ManagedSession(sso, *_device.session_views(self._store, sso))
+            managed = ManagedSession(sso, *_device.session_views(self._store, sso, self._sessions.saga_rows))
         else:
             sso = SharedSessionObject(config=config, creator_did=creator_did, session_id=session_id)
             sso.begin_handshake()
@@ -378,6 +378,22 @@ class Hypervisor:
         from agent_hypervisor_amd.models import store_pipeline
 
         return store_pipeline.run(self, specs, n)
+
+    def counters(self) -> dict:
+        """``/api/v1/stats`` counters: ``total_sessions``, ``active_sessions``,
+        ``total_participants``, ``active_sagas``, ``total_sagas``, ``total_vouches``.
+        Device-backed: reduced on the device over the hypervisor's rows (O(1) store
+        commands, no snapshot or view per session); host engines: from the objects
+        (reference api/server.py:144-163)."""
+        if self._store is not None:
+            return _device_mod().counters(self)
+        ms = list(self._sessions.values())
+        sagas = [g for m in ms for g in m.saga.sagas]
+        return {"total_sessions": len(ms),
+                "active_sessions": sum(1 for m in ms if m.sso.state.value not in ("archived", "terminating")),
+                "total_participants": sum(m.sso.participant_count for m in ms),
+                "active_sagas": sum(1 for g in sagas if g.state.value in ("running", "compensating")),
+                "total_sagas": len(sagas), "total_vouches": len(self.vouching.records())}
 
     def get_session(self, session_id: str) -> Optional[ManagedSession]:
         return self._sessions.get(session_id)

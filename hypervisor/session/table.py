@@ -15,16 +15,26 @@ none yet (its attributes build the views).
 
 from __future__ import annotations
 
+from array import array
 from typing import Iterator, Optional
+
+import numpy as np
 
 
 class SessionTable:
-    __slots__ = ("_own", "_segs", "_lazy")
+    __slots__ = ("_own", "_segs", "_lazy", "_slots", "_pos", "saga_rows", "_bcache")
 
     def __init__(self) -> None:
         self._own: dict = {}   # ordinary (and restored) sessions
         self._segs: list = []  # creation order: a list of own ids, or a batch
         self._lazy: dict = {}  # batched session id → its batch
+        # device rows of the own sessions in insertion order (-1: host session or
+        # removed) and of the sagas created through their orchestrators: the
+        # counters views reduce these on the device without walking the sessions
+        self._slots = array("q")
+        self._pos: dict = {}
+        self.saga_rows = array("q")
+        self._bcache: dict = {}  # id(batch) → (live count, its live session rows)
 
     def __len__(self) -> int:
         return len(self._own) + len(self._lazy)
@@ -39,7 +49,11 @@ class SessionTable:
         b = self._lazy.get(sid)
         if b is None:
             return default
-        return b.view(b.index[sid])
+        m = b.view(b.index[sid])
+        orch = m.saga
+        if getattr(orch, "_reg", False) is None:  # sagas created on it later are counted too
+            orch._reg = self.saga_rows
+        return m
 
     def __getitem__(self, sid):
         m = self.get(sid)
@@ -54,6 +68,8 @@ class SessionTable:
             if not self._segs or not isinstance(self._segs[-1], list):
                 self._segs.append([])
             self._segs[-1].append(sid)
+            self._pos[sid] = len(self._slots)
+            self._slots.append(getattr(m.sso, "slot", -1))
         self._own[sid] = m
 
     def add_batch(self, batch, ids: list) -> None:
@@ -64,6 +80,9 @@ class SessionTable:
     def pop(self, sid, default=None):
         m = self._own.pop(sid, None)
         if m is not None:
+            k = self._pos.pop(sid, None)
+            if k is not None:
+                self._slots[k] = -1
             for seg in self._segs:
                 if isinstance(seg, list) and sid in seg:
                     seg.remove(sid)
@@ -126,3 +145,38 @@ class SessionTable:
 
     def batch_of(self, sid) -> Optional[object]:
         return self._lazy.get(sid)
+
+    # -- device rows (counter views) ---------------------------------------------
+    def session_slots(self) -> np.ndarray:
+        """Device session rows of every session in the table (int64; host sessions
+        have none): the own sessions' array as kept, plus each batch's live rows
+        (cached until the batch loses a session).  No view is built."""
+        own = np.frombuffer(self._slots, dtype=np.int64) if len(self._slots) else np.zeros(0, np.int64)
+        parts = [own[own >= 0]]
+        for seg in self._segs:
+            if isinstance(seg, list) or not seg.index:
+                continue
+            n = len(seg.index)
+            c = self._bcache.get(id(seg))
+            if c is None or c[0] != n or c[2] is not seg:
+                idx = np.fromiter(seg.index.values(), dtype=np.int64, count=n)
+                c = (n, seg.slots[idx].astype(np.int64), seg)
+                self._bcache[id(seg)] = c
+            parts.append(c[1])
+        return np.concatenate(parts) if len(parts) > 1 else parts[0]
+
+    def batch_saga_rows(self) -> np.ndarray:
+        """Saga rows the batches wrote (their pipelines' sagas), int64."""
+        out = []
+        for seg in self._segs:
+            if isinstance(seg, list) or not seg.index:
+                continue
+            g = np.asarray(seg.gslots, dtype=np.int64)
+            out.append(g[g >= 0])
+        return np.concatenate(out) if out else np.zeros(0, np.int64)
+
+    def forget_sagas(self, rows) -> None:
+        """Drop saga rows of sessions that left the table (bulk: one pass)."""
+        drop = set(int(r) for r in rows)
+        if drop:
+            self.saga_rows = array("q", (r for r in self.saga_rows if r not in drop))

@@ -35,3 +35,19 @@ def test_restored_extras_follow_positions_not_sort_order():
     col.restored(b, np.array([4, 0, 1], dtype=np.int64))  # not ascending
     assert col.ids == ["s4", "s0", "s1"]
     assert col.extras == {0: {"vfs": "four"}, 2: {"vfs": "one"}}
+
+
+def test_a_row_released_twice_enters_the_free_list_once():
+    st = GovernanceStore("cpu", caps={"S": 64, "P": 4, "D": 64, "E": 64, "V": 64, "G": 64, "T": 64, "X": 1 << 16,
+                                      "B": 1 << 16})
+    try:
+        r = st.alloc("S")
+        st.release("S", r)
+        st.release("S", r)  # a second owner that believed it held the row
+        st.release("G", 5)  # never allocated
+        assert st.info()["double_releases"] == 2
+        st.reclaim()
+        rows = [st.alloc("S") for _ in range(64)]
+        assert len(set(rows)) == 64  # the row was handed out once
+    finally:
+        st.close()

@@ -24,7 +24,7 @@ N = 262_144
 @pytest.mark.parametrize("dev,waves,n", [pytest.param("cuda", 3, N, marks=pytest.mark.gpu),
                                          pytest.param("cuda", 2, N, marks=pytest.mark.gpu),
                                          pytest.param("cuda", 4, N, marks=pytest.mark.gpu),
-                                         ("cpu", 3, 3000)])
+                                         ("cpu", 3, 3000), pytest.param("cpu", 3, N, marks=pytest.mark.slow)])
 def test_headline_variant_matches_the_host_oracle(dev, waves, n):
     """(The CPU case runs the host twin of the same body at a smaller batch.)"""
     from hypervisor import Hypervisor

@@ -172,3 +172,76 @@ def test_rank_local_serving_scales(tmp_path, world):
         assert eff >= 0.8, (world, one, agg, a_rates, aggs)
     else:  # as many busy ranks as CPUs: the host itself is the limit
         assert eff >= 0.5, (world, one, agg, a_rates, aggs)
+
+
+def _views_worker(rank: int, world: int, root: str, n: int, q) -> None:
+    os.environ.update(OMP_NUM_THREADS="1", AHV_STORE="cpu", AHV_STORE_SESSIONS=str(1 << 18))
+    import torch
+
+    torch.set_num_threads(1)  # ranks share this host's CPUs (torch was imported before the env var)
+    dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
+    from agent_hypervisor_amd.models.store_pipeline import PipelineSpec
+    from agent_hypervisor_amd.parallel.resilience import _store
+    from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
+    from hypervisor import SessionConfig
+
+    kv = _store()
+
+    async def main():
+        shv = await ShardedHypervisor(device="cpu").start()
+        await shv.local.run_pipelines(PipelineSpec(), n)  # n batched sessions on this rank (archived)
+        sids = [await shv.create_session(SessionConfig(), "did:admin", rank=rank) for _ in range(3)]
+        for sid in sids:
+            await shv.join_session(sid, "did:v0", sigma_raw=0.9)
+            await shv.vouch("did:v0", f"did:x{rank}", sid, 0.9, bond_pct=0.1)
+            await shv.vouch(f"did:y{rank}", "did:v0", sid, 0.8, bond_pct=0.2)
+        kv.set(f"views/built/{rank}", "1")
+        await asyncio.get_running_loop().run_in_executor(None, kv.wait, [f"views/built/{r}" for r in range(world)])
+        if rank != 0:
+            await shv.serve_forever()
+            return None
+        st = shv.local._store
+        out = {}
+        await shv.stats()  # first view: connections and the batch row caches
+        for name, call in (("stats", lambda: shv.stats()), ("liability", lambda: shv.agent_liability("did:v0"))):
+            p0, c0 = st.info()["posted"], dict(shv.counters)
+            t0 = time.perf_counter()
+            res = await call()
+            dt = time.perf_counter() - t0
+            out[name] = (res, st.info()["posted"] - p0, shv.counters["collectives"] - c0["collectives"], dt)
+        await shv.shutdown()
+        return out
+
+    res = asyncio.run(main())
+    if rank == 0:
+        q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def test_agent_views_cost_o1_commands_at_1e5_sessions_per_rank(tmp_path):
+    """with 10⁵ sessions per rank, ``stats`` is one device
+    reduction per rank plus one 48-byte all-reduce, and the owner-routed
+    ``agent_liability`` reads only the agent's records (per-agent index) with no
+    collective — both O(1) store commands per rank, whatever the session count."""
+    world, n = 2, 100_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_views_worker, args=(r, world, str(tmp_path), n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=60)
+    stats, s_cmds, s_coll, s_dt = res["stats"]
+    assert stats["total_sessions"] == world * (n + 3) and stats["total_sagas"] == world * n
+    assert stats["active_sessions"] == world * 3 and stats["total_vouches"] == world * 6
+    assert s_cmds <= 2 and s_coll == 1, (s_cmds, s_coll)
+    lia, l_cmds, l_coll, l_dt = res["liability"]
+    assert len(lia["vouches_given"]) == world * 3 and len(lia["vouches_received"]) == world * 3
+    assert lia["total_exposure"] == sum(v["bonded_amount"] for v in lia["vouches_given"])
+    assert l_cmds <= 2 and l_coll == 0, (l_cmds, l_coll)
+    print(f"stats {s_dt * 1e3:.1f} ms, agent_liability {l_dt * 1e3:.1f} ms at {n} sessions per rank")

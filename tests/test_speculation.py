@@ -375,3 +375,36 @@ def test_terminate_awaits_when_not_predictable(dev, monkeypatch):
         assert hv.commitment.get_commitment(sid).merkle_root == root
 
     _run(go())
+
+
+async def test_cyclic_garbage_never_releases_a_row_twice():
+    """A hypervisor and its views collected together as cyclic garbage run their
+    finalisers in any order: each row is released exactly once (a double release
+    would hand one row to two sessions later)."""
+    import gc
+
+    from agent_hypervisor_amd.models.store import GovernanceStore
+
+    st = GovernanceStore("cpu")
+    base = dict(st.live_rows())
+    for order in range(4):
+        hv = Hypervisor(store=st)
+        ms = []
+        for k in range(3):
+            m = await hv.create_session(SessionConfig(), "did:admin")
+            sid = m.sso.session_id
+            await hv.join_session(sid, "did:a", sigma_raw=0.8)
+            m.delta_engine.capture("did:a", [VFSChange(path="/f", operation="add", content_hash="h")])
+            g = m.saga.create_saga(sid)
+            m.saga.add_step(g.saga_id, "a", "did:a", "/x")
+            ms.append(m)
+        await hv.run_pipelines(_spec(), 4)
+        junk = [hv, ms] if order % 2 else [ms, hv]
+        junk.append(junk)  # a reference cycle: the collector decides the finaliser order
+        del hv, ms, m, g, junk
+        gc.collect()
+        st.verify_deferred(block=True)
+        st.reclaim()
+        assert dict(st.live_rows()) == base, (order, st.live_rows(), base)
+    rows = st.alloc_many("S", 64).tolist()
+    assert len(set(rows)) == len(rows)

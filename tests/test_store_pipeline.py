@@ -17,6 +17,8 @@ import random
 
 import pytest
 
+from agent_hypervisor_amd.models.store import StoreError
+
 from agent_hypervisor_amd.models.store import GovernanceStore
 from agent_hypervisor_amd.models.store_pipeline import PipelineSpec
 from hypervisor import Hypervisor, SessionConfig
@@ -211,11 +213,13 @@ def test_lazy_rows_released_in_bulk_and_materialized_rows_kept(monkeypatch):
     gc.collect()
     st.reclaim()
     assert st.live_rows()["S"] == base["S"] + 40 - 14  # two flushes of 7; 6 wait for the batch
-    del hv, run
+    del hv, run  # row lifetime follows the hypervisor: the held views' rows go with it
     gc.collect()
     st.reclaim()
-    assert st.live_rows()["S"] == base["S"] + 5 and st.live_rows()["G"] == base["G"] + 5
+    assert {k: st.live_rows()[k] for k in ("S", "G", "T", "D")} == base
     assert [m.sso.session_id for m in keep] and all(m.delta_engine.deltas[2].delta_id == "delta:3" for m in keep)
+    with pytest.raises(StoreError, match="closed Hypervisor"):
+        keep[0].sso.participants
     del keep
     gc.collect()
     st.reclaim()
