@@ -616,6 +616,13 @@ class GovernanceStore:
                 continue
             t = self.tables[col]
             ix = torch.as_tensor(np.ascontiguousarray(idx, dtype=np.int64)).to(self.device)
+            if isinstance(vals, torch.Tensor):  # device-resident values (migration): no host copy
+                v = vals.reshape(-1)
+                if v.dtype != t.dtype:  # same-width integers are bit patterns (uint32 words)
+                    v = v.view(t.dtype) if v.element_size() == t.element_size() and not v.is_floating_point() \
+                        and not t.is_floating_point() else v.to(t.dtype)
+                t.index_copy_(0, ix, v.to(self.device))
+                continue
             want = _NP_OF[t.dtype]
             a = np.ascontiguousarray(vals)
             if a.dtype != want:  # same-width integers are bit patterns (uint32 words); else convert

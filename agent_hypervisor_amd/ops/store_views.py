@@ -175,3 +175,31 @@ def sigma_batch(store, vsess: list[int], agents: list[int], sigma=None, omega=No
             "e_bonded": t["e_bonded"], "out": out},
            {"sigma": f64, "omega": f64, "out": f64})
     return out
+
+
+def move_records(store, offs: torch.Tensor, lens: torch.Tensor, buf: torch.Tensor | None = None) -> torch.Tensor:
+    """Move audit records between the payload arena and a contiguous buffer on the
+    store device (session migration, P08): without ``buf``, the records at arena
+    offsets ``offs`` (``lens`` bytes each) are packed back to back into a new uint8
+    tensor; with ``buf``, the packed records are written to the arena at ``offs``.
+    int64 ``offs`` / ``lens`` on the store device; one wave per record."""
+    from agent_hypervisor_amd.ops._launch import launch
+
+    dev = store.device
+    offs = offs.to(dev, torch.int64).contiguous()
+    lens = lens.to(dev, torch.int64).contiguous()
+    n = int(offs.numel())
+    pos = torch.zeros(n, dtype=torch.int64, device=dev)
+    if n > 1:
+        torch.cumsum(lens[:-1], 0, out=pos[1:])
+    pack = buf is None
+    if pack:
+        total = int(lens.sum()) if n else 0
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    if n:
+        launch("store_records",
+               {"n": n, "payload": store._c.payload_ptr, "payload_cap": int(store._c.payload_cap),
+                "to_arena": 0 if pack else 1},
+               {"offs": offs, "lens": lens, "pos": pos, "buf": buf},
+               {"offs": torch.int64, "lens": torch.int64, "pos": torch.int64, "buf": torch.uint8})
+    return buf

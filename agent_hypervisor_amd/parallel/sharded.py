@@ -231,6 +231,7 @@ class ShardedHypervisor:
         self._sagas: dict[str, str] = {}  # saga id → session id (sagas this rank owns)
         self._vouch_seq = 0
         self._vouch_key: dict[str, tuple] = {}  # vouch id → global order key (created µs, rank, seq)
+        self._moved: dict[str, int] = {}  # session / saga id → owner after a migration (same on every rank)
         self._agent_ix: dict[str, list] = {}  # agent DID → its vouch records on this rank (creation order)
         self._agent_ix_n = 0  # records the index covers
         self._view_lock: Optional[asyncio.Lock] = None
@@ -300,8 +301,11 @@ class ShardedHypervisor:
         hash over the world — or, when the home rank has failed, the next live rank
         after it.  Re-homing by home rank (not by key) keeps a saga with its session
         (their ids were minted for the same home) on every survivor's routing."""
-        h = stable_rank(key, self.world)
         live = self._live
+        m = self._moved.get(key)
+        if m is not None and m in live:  # migrated (rebalance / retire): its current owner
+            return m
+        h = stable_rank(key, self.world)
         while h not in live:
             h = (h + 1) % self.world
         return h
@@ -1019,6 +1023,97 @@ class ShardedHypervisor:
         if self.world > 1:
             self.counters["collectives"] += 1
             dist.all_reduce(t, op=op, group=self.data_group)
+
+    # -- migration: rebalance and planned leave, no files -------------------
+    def migrate(self, moves: dict) -> dict:
+        """Collective over the members (every member calls, each with the moves of
+        sessions *it* owns: ``{session_id: destination rank}``): the sessions —
+        rows, chains with their records, sagas, steps, vouch bonds, commitments,
+        extras — move device to device (:mod:`agent_hypervisor_amd.parallel.migrate`;
+        RCCL ``all_to_all`` over xGMI on MI355X), their sagas and global vouch
+        order keys with them, and every member routes them to their new owner
+        afterwards.  Serving pauses on every member while it runs.  Returns
+        ``{"sent", "received"}`` for this rank."""
+        from agent_hypervisor_amd.parallel import migrate as MG
+
+        if self.world == 1 or len(self.members) == 1:
+            return {"sent": 0, "received": 0}
+        hv = self.local
+        bad = [s for s, d in moves.items() if d not in self._live or hv.get_session(s) is None]
+        if bad:
+            raise ValueError(f"cannot move {bad[:3]}: unknown here or destination not a live member")
+        moves = {s: int(d) for s, d in moves.items() if int(d) != self.rank}
+        by_sess: dict = {}
+        for g, sid in self._sagas.items():
+            if sid in moves:
+                by_sess.setdefault(sid, []).append(g)
+        vkeys = {v.vouch_id: list(self._vouch_key[v.vouch_id]) for v in hv.vouching.records()
+                 if v.session_id in moves and v.vouch_id in self._vouch_key}
+        mine = {"keys": {**moves, **{g: moves[s] for s, gs in by_sess.items() for g in gs}},
+                "sagas": {g: s for s, gs in by_sess.items() for g in gs}, "vouch_key": vkeys,
+                "dst": moves}
+        allm = MG.all_gather_json(mine, len(self.members), group=self.group)
+        plan: dict = {}
+        for s_, d in moves.items():
+            plan.setdefault(d, []).append(s_)
+        got = MG.exchange(hv, plan, self.rank, self.members, ctrl_group=self.group, data_group=self.data_group)
+        MG.evict(hv, list(moves))
+        for m in allm:  # every member: the new routes; receivers: the moved sessions' sagas and vouch keys
+            self._moved.update({k: int(v) for k, v in m["keys"].items()})
+            for g, sid in m["sagas"].items():
+                if int(m["dst"][sid]) == self.rank:
+                    self._sagas[g] = sid
+            for vid, key in m["vouch_key"].items():
+                self._vouch_key[vid] = tuple(key)
+        for g in [g for g, sid in self._sagas.items() if sid in moves]:
+            del self._sagas[g]
+        self._agent_ix_n = -1  # the per-agent vouch index is rebuilt on next use
+        self.counters["migrations"] = self.counters.get("migrations", 0) + 1
+        return {"sent": len(moves), "received": len(got)}
+
+    def rebalance(self) -> dict:
+        """Collective: even out the members' session counts (within one session of
+        the mean) by moving sessions from the most loaded members (their newest
+        sessions) — :meth:`migrate` under a plan every member computes alike."""
+        from agent_hypervisor_amd.parallel import migrate as MG
+
+        if self.world == 1 or len(self.members) == 1:
+            return {"sent": 0, "received": 0}
+        loads_m = MG.all_gather_json(len(self.local._sessions), len(self.members), group=self.group)
+        loads = {r: n for r, n in zip(self.members, loads_m)}
+        moves: dict = {}
+        ids = None
+        for src, dst, c in MG.balance_plan(loads, self.members):
+            if src != self.rank:
+                continue
+            if ids is None:
+                ids = [s for s in self.local._sessions if s not in moves]
+            take, ids = ids[-c:], ids[:-c]
+            moves.update(dict.fromkeys(take, dst))
+        return self.migrate(moves)
+
+    def retire(self, rank: int) -> dict:
+        """Collective: planned leave of member ``rank`` without checkpoint files —
+        its sessions move to the other members (round robin, :meth:`migrate`), then
+        every member drops it and the collectives move to sub-groups of the rest
+        (crash failover, where the rank cannot send, still re-hydrates from its
+        checkpoint: :meth:`failover`)."""
+        if rank not in self.members or len(self.members) == 1:
+            raise ValueError(f"rank {rank} is not a member that can leave {self.members}")
+        rest = [r for r in self.members if r != rank]
+        moves = {}
+        if self.rank == rank:
+            moves = {s: rest[i % len(rest)] for i, s in enumerate(list(self.local._sessions))}
+        out = self.migrate(moves)
+        self.members = rest
+        self._live = frozenset(rest)
+        if self.rank != rank:
+            if self.rpc is not None:
+                self.rpc.drop(rank)
+            self._drop_comm()
+            self.group = dist.new_group(ranks=self.members, backend="gloo", use_local_synchronization=True)
+            self.data_group = dist.new_group(ranks=self.members, use_local_synchronization=True)
+        return out
 
     # -- resilience (SURVEY §5.3): heartbeat, checkpoint, failover -----------------------
     def start_heartbeat(self, interval_s: float = 0.5):

@@ -225,6 +225,8 @@ class _Collect:
         self.t_str = {k: _Strs() for k in ("step_id", "action_id", "agent_did", "execute_api", "undo_api", "error",
                                            "execute_result", "compensation_result")}
         self.extras: dict = {}
+        self.drows: list = []  # each session's delta rows in chain order (host-known: no device walk)
+        self.dcnt: list = []
         self.n = 0
         self.ng = 0
 
@@ -243,7 +245,10 @@ class _Collect:
         self.cfg_maxdur.append(np.asarray([math.nan if md is None else float(md)]))
         self.cfg_chain.append(np.asarray([int(bool(cfg.enable_blockchain_commitment))], dtype=np.uint8))
         de = m.delta_engine
-        self.dskip.append(np.asarray([len(getattr(de, "_rows", ())) - len(de._deltas)], dtype=np.int32))
+        rows = list(getattr(de, "_rows", ()))
+        self.dskip.append(np.asarray([len(rows) - len(de._deltas)], dtype=np.int32))
+        self.drows.append(np.asarray(rows, dtype=np.int64))
+        self.dcnt.append(np.asarray([len(rows)], dtype=np.int64))
         for g in m.saga._sagas.values():
             self.g_sess.append(np.asarray([i], dtype=np.int64))
             self.g_row.append(np.asarray([g.slot], dtype=np.int64))
@@ -304,6 +309,7 @@ class _Collect:
             self.cfg_chain.append(np.asarray([int(bool(c.enable_blockchain_commitment)) for c in cfgs],
                                              dtype=np.uint8))
         self.dskip.append(np.zeros(k, dtype=np.int32))
+        self._batch_drows(b, idx)
         # sagas: at most one per batch session, its steps from the spec
         g = b.gslots[idx]
         has = np.flatnonzero(g >= 0)
@@ -379,6 +385,7 @@ class _Collect:
         self.cfg_maxdur.append(b.cfg_maxdur[idx])
         self.cfg_chain.append(b.cfg_chain[idx])
         self.dskip.append(b.dskip[idx])
+        self._batch_drows(b, idx)
         g0, g1 = b.goff[idx], b.goff[idx + 1]
         gcnt = g1 - g0
         ng = int(gcnt.sum())
@@ -409,6 +416,18 @@ class _Collect:
         self.t_ctr.append(sid.ctr[tix])
         self.t_seed.append(sid.seed[tix])
         self.ng += ng
+
+
+def _batch_drows(self, b, idx: np.ndarray) -> None:
+    """Delta rows of batch sessions ``idx`` (chain order), from the batch's arrays."""
+    off = np.asarray(b.delta_off, dtype=np.int64)
+    cnt = off[idx + 1] - off[idx]
+    self.dcnt.append(cnt)
+    self.drows.append(np.asarray(b.drows, dtype=np.int64)[_ragged(off[idx], cnt)] if int(cnt.sum())
+                      else np.zeros(0, np.int64))
+
+
+_Collect._batch_drows = _batch_drows
 
 
 def _ctr_append(ctr: list, seed: list, n: int, s: Optional[int] = None, c: Optional[np.ndarray] = None) -> None:
@@ -461,34 +480,39 @@ def _ragged(off_lo: np.ndarray, cnt: np.ndarray) -> np.ndarray:
     return np.repeat(off_lo.astype(np.int64) - starts, cnt) + np.arange(n, dtype=np.int64)
 
 
-def _take(st, name: str, rows: np.ndarray, width: int = 1) -> torch.Tensor:
+def _take(st, name: str, rows: np.ndarray, width: int = 1, device: bool = False) -> torch.Tensor:
+    """Rows of a store column (``width`` words per row), gathered on the device;
+    copied to the host unless ``device``."""
     t = st.tables[name]
     ix = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int64)).to(t.device)
-    if width > 1:
-        return t.view(-1, width).index_select(0, ix).cpu().contiguous()
-    return t.index_select(0, ix).cpu().contiguous()
+    out = t.view(-1, width).index_select(0, ix) if width > 1 else t.index_select(0, ix)
+    return out.contiguous() if device else out.cpu().contiguous()
 
 
-# ---------------------------------------------------------------- save
+# host-side copies of these columns travel with the host part even when the
+# columns themselves stay on the device (the receiver's allocators and lazy views
+# need them; a few bytes per row)
+HOST_COLS = ("S.s_pcount", "S.s_dcount", "S.s_maxpart", "S.s_minsig", "S.s_audit", "S.s_committed",
+             "S.s_commit_n", "D.d_len")
 
 
-def save_store(hv, d: str) -> dict:
-    """Write the columnar files of ``hv`` (device-backed) into directory ``d``;
-    returns the manifest extras (``{"layout", "sessions"}``) and the file digests
-    the caller lists."""
-    from safetensors.torch import save_file
-
+def _selected(hv, only: Optional[set]) -> _Collect:
+    """The sessions to save (all of ``hv``'s, or the ids in ``only``), collected in
+    creation order: built views through their objects, unbuilt batch sessions
+    vectorized."""
     from agent_hypervisor_amd.models.store_pipeline import _Batch
 
-    st = hv._store
-    st.verify_deferred(block=True)
     col = _Collect()
     for kind, seg in hv._sessions.segments():
         if kind == "own":
             for m in seg:
-                col.view(m)
+                if only is None or m.sso.session_id in only:
+                    col.view(m)
             continue
         order = np.fromiter(seg.index.values(), dtype=np.int64, count=len(seg.index))
+        if only is not None:
+            ids = seg.ids
+            order = order[np.fromiter((ids[i] in only for i in order.tolist()), dtype=bool, count=len(order))]
         built = np.fromiter((i in seg.views for i in order.tolist()), dtype=bool, count=len(order))
         # runs of unbuilt sessions vectorized, built ones through their views (creation order kept)
         edges = np.flatnonzero(np.diff(built.astype(np.int8))) + 1
@@ -505,6 +529,26 @@ def save_store(hv, d: str) -> dict:
                 col.batch(seg, ix)
             else:
                 raise CheckpointError(f"unknown session segment {type(seg).__name__}")
+    return col
+
+
+def collect(hv, only: Optional[set] = None, device: bool = False) -> tuple:
+    """The columnar image of ``hv``'s sessions (``only``: just these ids, with their
+    vouches, commitments and extras): ``(cols, host, arena, meta)``.
+
+    * ``cols`` — every table column of the sessions' rows (``S.*`` sessions,
+      ``P.*`` participants, ``D.*`` delta chains in chain order, ``G.*`` sagas,
+      ``T.*`` steps), gathered on the device and left there with ``device`` (the
+      migration path: nothing crosses to the host), copied to the host otherwise;
+    * ``host`` — host tensors: ragged offsets, configs, dictionary-encoded string
+      columns (ids, DIDs, descriptors) and the :data:`HOST_COLS` copies;
+    * ``arena`` — the chains' records concatenated in ``D`` order: a device uint8
+      tensor with ``device`` (one record-move kernel), else bytes;
+    * ``meta`` — counts, vouch records, host-held commitments, VFS/reversibility extras.
+    """
+    st = hv._store
+    st.verify_deferred(block=True)
+    col = _selected(hv, only)
     n = len(col.ids)
     assert col.n == n
     cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
@@ -512,101 +556,119 @@ def save_store(hv, d: str) -> dict:
     st.drain()
     if st.device.type == "cuda":
         st.flush()
+    take = lambda name, rows, w=1: _take(st, name, rows, w, device)  # noqa: E731
     T: dict = {}
     # -- sessions ------------------------------------------------------------------
     for name in S_COLS:
-        T[f"S.{name}"] = _take(st, name, slots)
+        T[f"S.{name}"] = take(name, slots)
     for name, w in S_WIDE.items():
-        T[f"S.{name}"] = _take(st, name, slots, w)
-    P, S_cap = st.caps["P"], st.caps["S"]
-    pcnt = T["S.s_pcount"].numpy().astype(np.int64)
+        T[f"S.{name}"] = take(name, slots, w)
+    S_cap = st.caps["S"]
+    pcnt = T["S.s_pcount"].cpu().numpy().astype(np.int64)
     kpos = np.arange(int(pcnt.sum()), dtype=np.int64) - np.repeat(np.concatenate([[0], np.cumsum(pcnt)[:-1]]), pcnt)
     prow = kpos * S_cap + np.repeat(slots, pcnt)  # participant-major columns (store.h prow)
     for name in P_COLS:
-        T[f"P.{name}"] = _take(st, name, prow)
-    # -- delta chains: walk d_prev back from s_dlast (chain order, every live row) --
-    dcnt = T["S.s_dcount"].numpy().astype(np.int64)
+        T[f"P.{name}"] = take(name, prow)
+    # -- delta chains, in chain order (the rows each session's views / batch hold) ----
+    dcnt = cat(col.dcnt, np.int64)
+    drow = cat(col.drows, np.int64)
+    dev_cnt = T["S.s_dcount"].to(torch.int64).cpu().numpy()
+    if len(dcnt) != n or not np.array_equal(dcnt, dev_cnt):
+        raise CheckpointError("delta chains differ from their sessions' delta counts (store corrupt)")
     doff = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(dcnt, out=doff[1:])
     nd = int(doff[-1])
-    drow = np.empty(nd, dtype=np.int64)
-    prev_col = st.tables["d_prev"].cpu().numpy() if nd else None
-    cur = _take(st, "s_dlast", slots).numpy().astype(np.int64)
-    pos = doff[1:] - 1
-    live = np.flatnonzero(dcnt > 0)
-    while len(live):
-        if (cur[live] < 0).any():
-            raise CheckpointError("delta chain shorter than its session's delta count (store corrupt)")
-        drow[pos[live]] = cur[live]
-        cur[live] = prev_col[cur[live]]
-        pos[live] -= 1
-        live = live[pos[live] >= doff[:-1][live]]
     for name in D_COLS:
-        T[f"D.{name}"] = _take(st, name, drow)
-    T["D.d_hash"] = _take(st, "d_hash", drow, 8)
-    dlen = T["D.d_len"].numpy().astype(np.int64)
-    arena = st._c.payload_gather(_take(st, "d_off", drow).numpy().astype(np.int64), dlen) if nd else b""
+        T[f"D.{name}"] = take(name, drow)
+    T["D.d_hash"] = take("d_hash", drow, 8)
+    dlen = T["D.d_len"].to(torch.int64).cpu().numpy()
+    aoff_src = take("d_off", drow).to(torch.int64)
+    if device:
+        from agent_hypervisor_amd.ops.store_views import move_records
+
+        arena = move_records(st, aoff_src, torch.from_numpy(dlen).to(st.device), None)
+    else:
+        arena = st._c.payload_gather(aoff_src.numpy(), dlen) if nd else b""
     # -- sagas / steps ---------------------------------------------------------------
     g_row, t_row = cat(col.g_row, np.int64), cat(col.t_row, np.int64)
     g_sess, t_saga = cat(col.g_sess, np.int64), cat(col.t_saga, np.int64)
     for name in G_COLS:
-        T[f"G.{name}"] = _take(st, name, g_row)
+        T[f"G.{name}"] = take(name, g_row)
     for name in T_COLS:
-        T[f"T.{name}"] = _take(st, name, t_row)
+        T[f"T.{name}"] = take(name, t_row)
     goff = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(np.bincount(g_sess, minlength=n), out=goff[1:])
     toff = np.zeros(len(g_row) + 1, dtype=np.int64)
     np.cumsum(np.bincount(t_saga, minlength=len(g_row)), out=toff[1:])
     if (np.diff(g_sess) < 0).any() or (np.diff(t_saga) < 0).any():
         raise CheckpointError("saga rows collected out of session order")
-    T["off.delta"] = torch.from_numpy(doff)
-    T["off.part"] = torch.from_numpy(np.concatenate([[0], np.cumsum(pcnt)]).astype(np.int64))
-    T["off.saga"] = torch.from_numpy(goff)
-    T["off.step"] = torch.from_numpy(toff)
-    T["sess.cfg_mode"] = torch.from_numpy(cat(col.cfg_mode, np.uint8))
-    T["sess.cfg_maxdur"] = torch.from_numpy(cat(col.cfg_maxdur, np.float64))
-    T["sess.cfg_chain"] = torch.from_numpy(cat(col.cfg_chain, np.uint8))
-    T["sess.dskip"] = torch.from_numpy(cat(col.dskip, np.int32))
-    T["step.timeout"] = torch.from_numpy(cat(col.t_timeout, np.float64))
+    H: dict = {}
+    H["off.delta"] = torch.from_numpy(doff)
+    H["off.part"] = torch.from_numpy(np.concatenate([[0], np.cumsum(pcnt)]).astype(np.int64))
+    H["off.saga"] = torch.from_numpy(goff)
+    H["off.step"] = torch.from_numpy(toff)
+    H["sess.cfg_mode"] = torch.from_numpy(cat(col.cfg_mode, np.uint8))
+    H["sess.cfg_maxdur"] = torch.from_numpy(cat(col.cfg_maxdur, np.float64))
+    H["sess.cfg_chain"] = torch.from_numpy(cat(col.cfg_chain, np.uint8))
+    H["sess.dskip"] = torch.from_numpy(cat(col.dskip, np.int32))
+    H["step.timeout"] = torch.from_numpy(cat(col.t_timeout, np.float64))
     ids = _Strs()
     ids.many(col.ids)
-    T.update(ids.tensors("session_id"))
-    T.update(col.g_id.tensors("saga_id"))
-    T["ctr.saga_id"] = torch.from_numpy(cat(col.g_ctr, np.int64))
-    T["seed.saga_id"] = torch.from_numpy(cat(col.g_seed, np.int64))
-    T["ctr.step.step_id"] = torch.from_numpy(cat(col.t_ctr, np.int64))
-    T["seed.step.step_id"] = torch.from_numpy(cat(col.t_seed, np.int64))
-    T.update(col.g_err.tensors("saga_error"))
-    for k, s in col.t_str.items():
-        T.update(s.tensors(f"step.{k}"))
-    # -- agents referenced by the rows (DIDs) ------------------------------------------
-    ag = np.concatenate([T["S.s_creator"].numpy(), T["P.p_agent"].numpy()]).astype(np.int64)
-    uniq, inv = np.unique(ag, return_inverse=True) if len(ag) else (np.zeros(0, np.int64), np.zeros(0, np.int64))
-    T["S.s_creator"] = torch.from_numpy(inv[:n].astype(np.int32))
-    T["P.p_agent"] = torch.from_numpy(inv[n:].astype(np.int32))
+    H.update(ids.tensors("session_id"))
+    H.update(col.g_id.tensors("saga_id"))
+    H["ctr.saga_id"] = torch.from_numpy(cat(col.g_ctr, np.int64))
+    H["seed.saga_id"] = torch.from_numpy(cat(col.g_seed, np.int64))
+    H["ctr.step.step_id"] = torch.from_numpy(cat(col.t_ctr, np.int64))
+    H["seed.step.step_id"] = torch.from_numpy(cat(col.t_seed, np.int64))
+    H.update(col.g_err.tensors("saga_error"))
+    for k, s_ in col.t_str.items():
+        H.update(s_.tensors(f"step.{k}"))
+    # -- agents referenced by the rows: dictionary codes (re-interned by the reader) ----
+    ag = torch.cat([T["S.s_creator"].to(torch.int64), T["P.p_agent"].to(torch.int64)])
+    if ag.numel():
+        uniq, inv = torch.unique(ag, return_inverse=True)
+    else:
+        uniq, inv = ag, ag
+    T["S.s_creator"] = inv[:n].to(torch.int32).contiguous()
+    T["P.p_agent"] = inv[n:].to(torch.int32).contiguous()
     agents = _Strs()
-    agents.many([st.did(int(a)) for a in uniq.tolist()])
-    T.update(agents.tensors("agents"))
+    agents.many([st.did(int(a)) for a in uniq.cpu().tolist()])
+    H.update(agents.tensors("agents"))
+    for k in HOST_COLS:
+        H["host." + k] = T[k].cpu()
+    meta = {
+        "layout": LAYOUT, "sessions": n, "deltas": nd, "sagas": len(g_row), "steps": len(t_row),
+        "participant_rows": st.caps["P"], "arena_bytes": int(dlen.sum()) if nd else 0,
+        "batched_sessions": int(getattr(hv, "batched_sessions", 0)),
+        "vouches": _vouches(hv, only), "commitments": _host_commitments(hv, only),
+        "extras": {str(k): v for k, v in col.extras.items()},
+    }
+    return T, H, arena, meta
+
+
+def save_store(hv, d: str) -> dict:
+    """Write the columnar files of ``hv`` (device-backed) into directory ``d``;
+    returns the manifest extras (``{"layout", "sessions"}``) and the file digests
+    the caller lists."""
+    from safetensors.torch import save_file
+
+    T, H, arena, meta = collect(hv)
+    T.update({k: v for k, v in H.items() if not k.startswith("host.")})
     save_file(T, os.path.join(d, "store.safetensors"), metadata={"format": "ahv-checkpoint", "layout": LAYOUT})
     with open(os.path.join(d, "arena.bin"), "wb") as f:
         f.write(arena)
-    # -- vouches, host commitments, extras ----------------------------------------------
-    meta = {
-        "layout": LAYOUT, "sessions": n, "deltas": nd, "sagas": len(g_row), "steps": len(t_row),
-        "participant_rows": P, "arena_bytes": len(arena),
-        "batched_sessions": int(getattr(hv, "batched_sessions", 0)),
-        "vouches": _vouches(hv), "commitments": _host_commitments(hv),
-        "extras": {str(k): v for k, v in col.extras.items()},
-    }
     with open(os.path.join(d, "store.json"), "w") as f:
         json.dump(meta, f)
-    return {"layout": LAYOUT, "sessions": n}
+    return {"layout": LAYOUT, "sessions": meta["sessions"]}
 
 
-def _vouches(hv) -> list:
-    """Vouch records in creation order; bond state from the edge rows (one gather)."""
+def _vouches(hv, only: Optional[set] = None) -> list:
+    """Vouch records in creation order (of the sessions ``only``, when given); bond
+    state from the edge rows (one gather)."""
     ve = hv.vouching
     recs = list(getattr(ve, "_order", ()))
+    if only is not None:
+        recs = [r for r in recs if r.session_id in only]
     st = hv._store
     live = [r.edge for r in recs if getattr(r, "edge", -1) >= 0]
     g = st.gather({"e_active": live, "e_released": live}) if live else {}
@@ -625,11 +687,13 @@ def _vouches(hv) -> list:
     return out
 
 
-def _host_commitments(hv) -> list:
+def _host_commitments(hv, only: Optional[set] = None) -> list:
     from agent_hypervisor_amd.runtime.checkpoint import _iso
 
     out = []
     for c in getattr(hv.commitment, "_commitments", {}).values():
+        if only is not None and c.session_id not in only:
+            continue
         out.append({"session_id": c.session_id, "merkle_root": c.merkle_root, "participant_dids": c.participant_dids,
                     "delta_count": c.delta_count, "committed_at": _iso(c.committed_at),
                     "blockchain_tx_id": c.blockchain_tx_id, "committed_to": c.committed_to})
@@ -661,29 +725,58 @@ def session_keys(d: str) -> list:
 
 def load_store(hv, d: str, verify: bool = True, only=None):
     """Restore the columnar checkpoint in ``d`` into the device-backed ``hv``
-    (``only``: just these session ids, with their vouches and commitments)."""
-    from hypervisor.models import ConsistencyMode  # noqa: F401 - view construction needs it loaded
-
-    st = hv._store
+    (``only``: just these session ids, with their vouches and commitments).  The
+    arena file's integrity check is the host K10/K09 re-verification (always)."""
     t, meta = read_tables(d)
-    P = st.caps["P"]
-    if meta["participant_rows"] > P:
-        pc = t["S.s_pcount"].numpy()
-        if len(pc) and int(pc.max()) > P:
-            raise CheckpointError(f"checkpoint sessions have up to {int(pc.max())} participants; store rows hold {P}")
-    ids_col = _Col(t, "session_id")
-    ids_all = ids_col.all()
-    n_all = len(ids_all)
-    doff_all, poff_all = t["off.delta"].numpy(), t["off.part"].numpy()
-    goff_all, toff_all = t["off.saga"].numpy(), t["off.step"].numpy()
     with open(os.path.join(d, "arena.bin"), "rb") as f:
         arena = f.read()
     if len(arena) != meta["arena_bytes"] or len(arena) != int(t["D.d_len"].numpy().astype(np.int64).sum()):
         raise CheckpointError(f"{d}: arena.bin is {len(arena)} bytes, expected {meta['arena_bytes']}")
+    cols = {k: v for k, v in t.items() if k[:2] in ("S.", "P.", "D.", "G.", "T.")}
+    host = {k: v for k, v in t.items() if k not in cols}
+    return restore(hv, cols, host, arena, meta, verify="host", only=only)
+
+
+def _host(cols: dict, host: dict, key: str) -> np.ndarray:
+    """Host values of column ``key``: the host part's copy, else the column itself."""
+    v = host.get("host." + key)
+    if v is None:
+        v = cols[key]
+    return v.cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+
+
+def restore(hv, cols: dict, host: dict, arena, meta: dict, verify: str = "host", only=None):
+    """Write a columnar image (:func:`collect`'s ``cols``/``host``/``arena``/``meta``)
+    into ``hv``'s store as new rows, registered lazily (:class:`RestoredBatch`).
+
+    ``cols`` may be host tensors (checkpoint files) or tensors on the store device
+    (a migration's received buffer: columns and ``arena`` are then written device
+    to device, every row reference rewritten on the device).  ``verify``: ``"host"``
+    re-verifies every chain and committed root over the bytes on the host before
+    writing (checkpoint files), ``"device"`` runs K10/K09 over the written rows in
+    place, ``"none"`` trusts the image."""
+    from hypervisor.models import ConsistencyMode  # noqa: F401 - view construction needs it loaded
+
+    st = hv._store
+    sdev = st.device
+    P = st.caps["P"]
+    pcount_all = _host(cols, host, "S.s_pcount")
+    if meta["participant_rows"] > P and len(pcount_all) and int(pcount_all.max()) > P:
+        raise CheckpointError(f"checkpoint sessions have up to {int(pcount_all.max())} participants; "
+                              f"store rows hold {P}")
+    ids_col = _Col(host, "session_id")
+    ids_all = ids_col.all()
+    n_all = len(ids_all)
+    doff_all, poff_all = host["off.delta"].numpy(), host["off.part"].numpy()
+    goff_all, toff_all = host["off.saga"].numpy(), host["off.step"].numpy()
+    dlen_all = _host(cols, host, "D.d_len").astype(np.int64)
+    on_dev = isinstance(arena, torch.Tensor)
     # -- selection ----------------------------------------------------------------------
     if only is not None:
+        if on_dev:
+            raise ValueError("restore(only=...) reads a host image (checkpoint files)")
         want = set(only)
-        sel = np.fromiter((s in want for s in ids_all), dtype=bool, count=n_all)
+        sel = np.fromiter((s_ in want for s_ in ids_all), dtype=bool, count=n_all)
         si = np.flatnonzero(sel)
     else:
         si = np.arange(n_all, dtype=np.int64)
@@ -698,30 +791,34 @@ def load_store(hv, d: str, verify: bool = True, only=None):
     ti = _ragged(toff_all[gi], tcnt)
     doff = np.concatenate([[0], np.cumsum(dcnt)]).astype(np.int64)
     nd = len(di)
-    sub = (lambda a, ix: a[ix]) if only is not None else (lambda a, ix: a)  # noqa: E731 - all rows: no copies
-    S = {k: sub(v.numpy(), si) for k, v in t.items() if k.startswith("S.")}
-    Pc = {k: sub(v.numpy(), pi) for k, v in t.items() if k.startswith("P.")}
-    D = {k: sub(v.numpy(), di) for k, v in t.items() if k.startswith("D.")}
-    G = {k: sub(v.numpy(), gi) for k, v in t.items() if k.startswith("G.")}
-    Tt = {k: sub(v.numpy(), ti) for k, v in t.items() if k.startswith("T.")}
-    dlen = D["D.d_len"].astype(np.int64)
-    rec_all = np.zeros(len(doff_all) and int(doff_all[-1]) + 1, dtype=np.int64)
-    if len(rec_all) > 1:
-        np.cumsum(t["D.d_len"].numpy().astype(np.int64), out=rec_all[1:])
-    rec_off = rec_all[di] if nd else np.zeros(0, np.int64)
-    if only is not None and nd:  # the selected records, contiguous
-        mv = memoryview(arena)
-        blob = b"".join(mv[int(o):int(o) + int(ln)] for o, ln in zip(rec_off.tolist(), dlen.tolist()))
-        rec_off = np.concatenate([[0], np.cumsum(dlen)[:-1]]).astype(np.int64)
-    else:
-        blob = arena
-    # -- K10 / K09 over the bytes about to be written --------------------------------------
-    # (always: the arena file's integrity check is this re-verification — see the manifest's "k10")
-    commit_n = np.where(S["S.s_committed"] != 0, S["S.s_commit_n"], 0).astype(np.int32)
-    if n:
-        bad_c, bad_r = C.verify_chain_records(blob, rec_off, dlen, D["D.d_hole"].astype(np.int32),
-                                              D["D.d_hash"].astype(np.int32).view(np.uint32).reshape(-1),
-                                              doff, S["S.s_root"].astype(np.int32).view(np.uint32).reshape(-1),
+
+    def sub(v, ix):
+        if only is None:
+            return v
+        return v[ix] if not isinstance(v, torch.Tensor) else v.index_select(0, torch.from_numpy(ix).to(v.device))
+
+    grp = lambda pfx, ix: {k: sub(v, ix) for k, v in cols.items() if k.startswith(pfx)}  # noqa: E731
+    S, Pc, D, G, Tt = grp("S.", si), grp("P.", pi), grp("D.", di), grp("G.", gi), grp("T.", ti)
+    hs = lambda key, ix: sub(_host(cols, host, key), ix)  # noqa: E731 - host values of the selection
+    dlen = dlen_all[di] if only is not None else dlen_all
+    committed_h = hs("S.s_committed", si)
+    # -- host K10 / K09 over the bytes about to be written -------------------------------------
+    if verify == "host" and n:
+        rec_all = np.zeros(len(dlen_all) + 1, dtype=np.int64)
+        np.cumsum(dlen_all, out=rec_all[1:])
+        rec_off = rec_all[di] if nd else np.zeros(0, np.int64)
+        if only is not None and nd:  # the selected records, contiguous
+            mv = memoryview(arena)
+            blob = b"".join(mv[int(o):int(o) + int(ln)] for o, ln in zip(rec_off.tolist(), dlen.tolist()))
+            rec_off = np.concatenate([[0], np.cumsum(dlen)[:-1]]).astype(np.int64)
+        else:
+            blob = arena
+        commit_n = np.where(committed_h != 0, hs("S.s_commit_n", si), 0).astype(np.int32)
+        dh = D["D.d_hash"].cpu().numpy() if isinstance(D["D.d_hash"], torch.Tensor) else D["D.d_hash"]
+        sr = S["S.s_root"].cpu().numpy() if isinstance(S["S.s_root"], torch.Tensor) else S["S.s_root"]
+        bad_c, bad_r = C.verify_chain_records(blob, rec_off, dlen, _as_np(D["D.d_hole"]).astype(np.int32),
+                                              dh.astype(np.int32).view(np.uint32).reshape(-1),
+                                              doff, sr.astype(np.int32).view(np.uint32).reshape(-1),
                                               commit_n, os.cpu_count() or 4)
         bc = np.frombuffer(bad_c, dtype=np.uint8)
         br = np.frombuffer(bad_r, dtype=np.uint8)
@@ -733,15 +830,29 @@ def load_store(hv, d: str, verify: bool = True, only=None):
             k = int(np.flatnonzero(br)[0])
             raise CheckpointError(f"session {ids_all[si[k]]}: Merkle root fails re-verification against its "
                                   f"commitment ({int(br.sum())} in total)")
+        arena_sel = blob
+    elif only is not None and nd:
+        rec_all = np.concatenate([[0], np.cumsum(dlen_all)]).astype(np.int64)
+        mv = memoryview(arena)
+        arena_sel = b"".join(mv[int(rec_all[k]):int(rec_all[k] + dlen_all[k])] for k in di.tolist())
+    else:
+        arena_sel = arena
     # -- rows in the target store -------------------------------------------------------------
-    agents = _Col(t, "agents").all()
+    agents = _Col(host, "agents").all()
     amap = np.asarray(st.agents.intern_many(agents), dtype=np.int64) if agents else np.zeros(0, np.int64)
+    lut = torch.from_numpy(amap.astype(np.int32)).to(sdev) if len(amap) else None
     slots = st.alloc_many("S", n).astype(np.int64)
     if nd:
         rb, ob = st.reserve_deltas(dlen.astype(np.int32))
         drows = np.frombuffer(rb, dtype=np.int32).astype(np.int64)
         aoff = np.frombuffer(ob, dtype=np.int64).copy()
-        st._c.write_records(aoff, dlen, blob)
+        if on_dev:
+            from agent_hypervisor_amd.ops.store_views import move_records
+
+            st.drain()
+            move_records(st, torch.from_numpy(aoff).to(sdev), torch.from_numpy(dlen).to(sdev), arena_sel)
+        else:
+            st._c.write_records(aoff, dlen, arena_sel)
     else:
         drows = np.zeros(0, np.int64)
         aoff = np.zeros(0, np.int64)
@@ -749,12 +860,12 @@ def load_store(hv, d: str, verify: bool = True, only=None):
     gslots = st.alloc_many("G", ng).astype(np.int64) if ng else np.zeros(0, np.int64)
     tslots = st.alloc_many("T", nt).astype(np.int64) if nt else np.zeros(0, np.int64)
     # -- columns with every row reference rewritten -------------------------------------------
+    remap = lambda v: (lut.to(v.device)[v.to(torch.int64)] if isinstance(v, torch.Tensor)  # noqa: E731
+                       else amap[v.astype(np.int64)].astype(np.int32)) if len(v) else v
     W: dict = {}
     for name in S_COLS:
         v = S[f"S.{name}"]
-        if name == "s_creator":
-            v = amap[v.astype(np.int64)] if len(v) else v
-        W[name] = (slots, v)
+        W[name] = (slots, remap(v) if name == "s_creator" else v)
     for name, w in S_WIDE.items():
         W[name] = ((slots[:, None] * w + np.arange(w)[None, :]).reshape(-1), S[f"S.{name}"].reshape(-1))
     last = np.where(dcnt > 0, drows[np.maximum(doff[1:] - 1, 0)] if nd else -1, -1)
@@ -764,9 +875,7 @@ def load_store(hv, d: str, verify: bool = True, only=None):
     prow = kpos * st.caps["S"] + np.repeat(slots, pcnt)  # participant-major (store.h prow), S after the allocs
     for name in P_COLS:
         v = Pc[f"P.{name}"]
-        if name == "p_agent":
-            v = amap[v.astype(np.int64)] if len(v) else v
-        W[name] = (prow, v)
+        W[name] = (prow, remap(v) if name == "p_agent" else v)
     if nd:
         sess_of_d = np.repeat(np.arange(n, dtype=np.int64), dcnt)
         first = np.zeros(nd, dtype=bool)
@@ -785,26 +894,29 @@ def load_store(hv, d: str, verify: bool = True, only=None):
     for name in T_COLS:
         W[name] = (tslots, Tt[f"T.{name}"])
     st.write_columns(W)
+    if verify == "device" and n:
+        _verify_on_device(st, slots, drows, doff, committed_h, ids_all, si)
     # -- lazy registration ----------------------------------------------------------------------
     b = RestoredBatch()
     b.store = st
     b.ids = [ids_all[i] for i in si.tolist()] if only is not None else ids_all
     b.slots = slots.astype(np.int32)
     b.delta_off, b.drows, b.doff, b.dlen = doff, drows.astype(np.int32), aoff, dlen
-    b.dhash = D["D.d_hash"].astype(np.int32).view(np.uint32).reshape(-1, 8) if nd else np.zeros((0, 8), np.uint32)
-    b.dskip = t["sess.dskip"].numpy()[si]
-    b.cfg_mode, b.cfg_maxdur, b.cfg_chain = t["sess.cfg_mode"].numpy()[si], t["sess.cfg_maxdur"].numpy()[si], \
-        t["sess.cfg_chain"].numpy()[si]
-    b.maxpart, b.minsig, b.audit = S["S.s_maxpart"], S["S.s_minsig"], S["S.s_audit"]
-    b.creator = amap[S["S.s_creator"].astype(np.int64)] if n else np.zeros(0, np.int64)
+    b.dhash = None if on_dev else (_as_np(D["D.d_hash"]).astype(np.int32).view(np.uint32).reshape(-1, 8) if nd
+                                   else np.zeros((0, 8), np.uint32))
+    b.dskip = host["sess.dskip"].numpy()[si]
+    b.cfg_mode, b.cfg_maxdur, b.cfg_chain = host["sess.cfg_mode"].numpy()[si], host["sess.cfg_maxdur"].numpy()[si], \
+        host["sess.cfg_chain"].numpy()[si]
+    b.maxpart, b.minsig, b.audit = hs("S.s_maxpart", si), hs("S.s_minsig", si), hs("S.s_audit", si)
+    b.creator = amap[hs("S.s_creator", si).astype(np.int64)] if n else np.zeros(0, np.int64)
     b.goff = np.concatenate([[0], np.cumsum(gcnt)]).astype(np.int64)
     b.gslots = gslots.astype(np.int32)
     b.toff = np.concatenate([[0], np.cumsum(tcnt)]).astype(np.int64)
     b.tslots = tslots.astype(np.int32)
-    b.gid = _Col(t, "saga_id", mint="saga:").take(gi)
-    b.gerr = _Col(t, "saga_error").take(gi)
-    b.t_timeout = t["step.timeout"].numpy()[ti]
-    b.tcols = {k: _Col(t, f"step.{k}", mint="step:" if k == "step_id" else None).take(ti)
+    b.gid = _Col(host, "saga_id", mint="saga:").take(gi)
+    b.gerr = _Col(host, "saga_error").take(gi)
+    b.t_timeout = host["step.timeout"].numpy()[ti]
+    b.tcols = {k: _Col(host, f"step.{k}", mint="step:" if k == "step_id" else None).take(ti)
                for k in ("step_id", "action_id", "agent_did", "execute_api", "undo_api", "error",
                          "execute_result", "compensation_result")}
     ex = meta.get("extras", {})
@@ -819,7 +931,7 @@ def load_store(hv, d: str, verify: bool = True, only=None):
     b.built, b.released, b.dead = np.zeros(n, dtype=bool), np.zeros(n, dtype=bool), []
     b.index = dict(zip(b.ids, range(n)))
     b.views = {}
-    b.committed = S["S.s_committed"] != 0 if n else np.zeros(0, dtype=bool)
+    b.committed = committed_h != 0 if n else np.zeros(0, dtype=bool)
     b._saga_ids = b._step_ids = None
     hv.commitment.register_batch(b)
     hv._sessions.add_batch(b, b.ids)
@@ -827,6 +939,30 @@ def load_store(hv, d: str, verify: bool = True, only=None):
     _restore_vouches(hv, meta["vouches"], None if only is None else set(only))
     _restore_commitments(hv, meta["commitments"], None if only is None else set(only))
     return hv
+
+
+def _as_np(v) -> np.ndarray:
+    return v.cpu().numpy() if isinstance(v, torch.Tensor) else v
+
+
+def _verify_on_device(st, slots, drows, doff, committed, ids, si) -> None:
+    """K10 over the written rows (records re-hashed in the arena, parent links) and
+    K09 over the committed chains, on the store's device."""
+    from agent_hypervisor_amd.ops.store_views import store_roots, verify_store_chains
+
+    chains = [drows[int(doff[i]):int(doff[i + 1])].tolist() for i in range(len(slots))]
+    _, ok = verify_store_chains(st, chains)
+    okh = ok.cpu().numpy()
+    if not okh.all():
+        k = int(np.flatnonzero(okh == 0)[0])
+        raise CheckpointError(f"session {ids[si[k]]}: audit chain fails re-verification after the move")
+    c = np.flatnonzero(committed != 0)
+    if len(c):
+        roots = store_roots(st, [chains[i] for i in c.tolist()]).cpu().numpy()
+        want = st.gather({"s_root": (slots[c][:, None] * 8 + np.arange(8)[None, :]).reshape(-1)})["s_root"]
+        if not np.array_equal(roots.reshape(-1).astype(np.int64) & 0xFFFFFFFF,
+                              want.astype(np.int64) & 0xFFFFFFFF):
+            raise CheckpointError("Merkle root fails re-verification against its commitment after the move")
 
 
 def _restore_vouches(hv, vouches: list, only: Optional[set]) -> None:
@@ -1016,7 +1152,7 @@ class RestoredBatch(_restored_batch_base()):
                                      previous_hash=c["previous_hash"]) for c in p["changes"]]
                 v = _device.DeviceDelta(de, p["delta_id"], p["turn_id"], p["session_id"], p["agent_did"],
                                         datetime.fromisoformat(p["timestamp"]), changes, prev)
-                h = "".join(f"{int(w):08x}" for w in self.dhash[g])
+                h = "".join(f"{int(w):08x}" for w in self.dhash[g]) if self.dhash is not None else None
                 v.__dict__.update(_didx=int(self.drows[g]), _poff=int(self.doff[g]), _plen=ln, _seq=-1, _dev_hash=h)
                 de._rows.append(int(self.drows[g]))
                 if g - d0 >= skip:

@@ -136,6 +136,52 @@ __global__ __launch_bounds__(256) void store_sigma_kernel(SigmaBatchArgs a) {
     a.out[i] = sigma_batch_row(a, i);
 }
 
+// Record moves between the payload arena and a contiguous device buffer (session
+// migration between ranks, P08): record i is the `lens[i]` bytes at arena offset
+// `offs[i]` ↔ buffer position `pos[i]`.  One 64-lane wave per record; the arena
+// is fine-grained (host-visible) memory, read with system-scope word loads.
+struct RecordMoveArgs {
+  int64_t n;
+  uint8_t* payload;
+  int64_t payload_cap;
+  const int64_t* offs;
+  const int64_t* lens;
+  const int64_t* pos;
+  uint8_t* buf;
+  int32_t to_arena;  // 0: arena → buf (pack), 1: buf → arena (unpack)
+};
+
+AHV_HD bool record_ok(const RecordMoveArgs& a, int64_t i) {
+  return a.offs[i] >= 0 && a.lens[i] >= 0 && a.offs[i] + a.lens[i] <= a.payload_cap;
+}
+
+__global__ __launch_bounds__(256) void store_records_kernel(RecordMoveArgs a) {
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  for (int64_t i = wave; i < a.n; i += nwaves) {
+    if (!record_ok(a, i)) continue;
+    const int64_t off = a.offs[i], len = a.lens[i], p = a.pos[i];
+    for (int64_t j = lane; j < len; j += 64) {
+      if (a.to_arena) {
+        a.payload[off + j] = a.buf[p + j];
+      } else {
+        const uint64_t b = static_cast<uint64_t>(off + j);
+        const uint32_t w = ld32f(a.payload + (b & ~uint64_t(3)));
+        a.buf[p + j] = static_cast<uint8_t>((w >> (8 * (b & 3))) & 0xffu);
+      }
+    }
+  }
+}
+
+void records_host(const RecordMoveArgs& a) {
+  for (int64_t i = 0; i < a.n; ++i) {
+    if (!record_ok(a, i)) continue;
+    if (a.to_arena) std::copy(a.buf + a.pos[i], a.buf + a.pos[i] + a.lens[i], a.payload + a.offs[i]);
+    else std::copy(a.payload + a.offs[i], a.payload + a.offs[i] + a.lens[i], a.buf + a.pos[i]);
+  }
+}
+
 template <class T>
 T* P(const py::dict& d, const char* k) {
   return reinterpret_cast<T*>(d[k].cast<uintptr_t>());
@@ -156,6 +202,12 @@ SigmaBatchArgs to_sigma(const py::dict& d) {
                         P<const int32_t>(d, "e_voucher"), P<const int32_t>(d, "e_vouchee"),
                         P<const uint8_t>(d, "e_active"), P<const int64_t>(d, "e_expiry"),
                         P<const double>(d, "e_bonded"), d["cap_v"].cast<int64_t>(), P<double>(d, "out")};
+}
+
+RecordMoveArgs to_records(const py::dict& d) {
+  return RecordMoveArgs{d["n"].cast<int64_t>(), P<uint8_t>(d, "payload"), d["payload_cap"].cast<int64_t>(),
+                        P<const int64_t>(d, "offs"), P<const int64_t>(d, "lens"), P<const int64_t>(d, "pos"),
+                        P<uint8_t>(d, "buf"), d["to_arena"].cast<int32_t>()};
 }
 
 }  // namespace
@@ -185,6 +237,18 @@ void register_store_views(py::module_& m) {
         check_hip(hipGetLastError(), "store_sigma");
       },
       py::arg("args"), py::arg("stream"));
+  m.def(
+      "store_records",
+      [](const py::dict& d, uintptr_t stream) {
+        const RecordMoveArgs a = to_records(d);
+        py::gil_scoped_release nogil;
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((a.n + 3) / 4, 16384));  // 4 waves per block
+        hipLaunchKernelGGL(store_records_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), a);
+        check_hip(hipGetLastError(), "store_records");
+      },
+      py::arg("args"), py::arg("stream"));
+  m.def("store_records_host", [](const py::dict& d) { records_host(to_records(d)); });
   m.def("store_sigma_host", [](const py::dict& d) {
     const SigmaBatchArgs a = to_sigma(d);
     for (int64_t i = 0; i < a.n; ++i) a.out[i] = sigma_batch_row(a, i);

@@ -752,8 +752,8 @@ _OK = (0,)  # a speculated post's expected result: status 0
 
 def _resolve(store: GovernanceStore, d: DeviceDelta) -> str:
     """The device digest of a captured delta (its capture result, or its arena row)."""
-    r = store.result(d._seq, 9)
-    if r is None:  # result slot recycled: read the arena row
+    r = store.result(d._seq, 9) if d._seq >= 0 else None
+    if r is None:  # result slot recycled (or a restored / moved row): read the arena row
         n, off, inl = store.index_args([d._didx])
         store.call(_st.OP_DELTA_READ, [n, off, 0], 1, inl)
         raw = store.bulk(0, 96)

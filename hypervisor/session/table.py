@@ -147,32 +147,41 @@ class SessionTable:
         return self._lazy.get(sid)
 
     # -- device rows (counter views) ---------------------------------------------
+    def _batch_rows(self, seg) -> tuple:
+        """(live session rows, live saga rows) of a batch, cached until it loses a session."""
+        n = len(seg.index)
+        c = self._bcache.get(id(seg))
+        if c is None or c[0] != n or c[3] is not seg:
+            idx = np.fromiter(seg.index.values(), dtype=np.int64, count=n)
+            gs = np.asarray(seg.gslots, dtype=np.int64)
+            goff = getattr(seg, "goff", None)
+            if goff is not None:  # restored batch: any number of sagas per session
+                g0, g1 = goff[idx], goff[idx + 1]
+                cnt = (g1 - g0).astype(np.int64)
+                k = int(cnt.sum())
+                rows = gs[np.repeat(g0 - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt) + np.arange(k)] \
+                    if k else np.zeros(0, np.int64)
+            else:  # pipeline batch: at most one saga per session
+                rows = gs[idx]
+                rows = rows[rows >= 0]
+            c = (n, seg.slots[idx].astype(np.int64), rows.astype(np.int64), seg)
+            self._bcache[id(seg)] = c
+        return c[1], c[2]
+
     def session_slots(self) -> np.ndarray:
         """Device session rows of every session in the table (int64; host sessions
-        have none): the own sessions' array as kept, plus each batch's live rows
-        (cached until the batch loses a session).  No view is built."""
+        have none): the own sessions' array as kept, plus each batch's live rows.
+        No view is built."""
         own = np.frombuffer(self._slots, dtype=np.int64) if len(self._slots) else np.zeros(0, np.int64)
         parts = [own[own >= 0]]
         for seg in self._segs:
-            if isinstance(seg, list) or not seg.index:
-                continue
-            n = len(seg.index)
-            c = self._bcache.get(id(seg))
-            if c is None or c[0] != n or c[2] is not seg:
-                idx = np.fromiter(seg.index.values(), dtype=np.int64, count=n)
-                c = (n, seg.slots[idx].astype(np.int64), seg)
-                self._bcache[id(seg)] = c
-            parts.append(c[1])
+            if not isinstance(seg, list) and seg.index:
+                parts.append(self._batch_rows(seg)[0])
         return np.concatenate(parts) if len(parts) > 1 else parts[0]
 
     def batch_saga_rows(self) -> np.ndarray:
-        """Saga rows the batches wrote (their pipelines' sagas), int64."""
-        out = []
-        for seg in self._segs:
-            if isinstance(seg, list) or not seg.index:
-                continue
-            g = np.asarray(seg.gslots, dtype=np.int64)
-            out.append(g[g >= 0])
+        """Saga rows the batches wrote for their sessions still in the table, int64."""
+        out = [self._batch_rows(seg)[1] for seg in self._segs if not isinstance(seg, list) and seg.index]
         return np.concatenate(out) if out else np.zeros(0, np.int64)
 
     def forget_sagas(self, rows) -> None:

@@ -30,7 +30,8 @@ def test_restored_extras_follow_positions_not_sort_order():
     b = types.SimpleNamespace(
         ids=[f"s{i}" for i in range(5)], slots=np.arange(5, dtype=np.int32),
         cfg_mode=np.zeros(5, np.uint8), cfg_maxdur=np.zeros(5), cfg_chain=np.zeros(5, np.uint8),
-        dskip=np.zeros(5, np.int32), goff=np.zeros(6, np.int64), extras={4: {"vfs": "four"}, 1: {"vfs": "one"}})
+        dskip=np.zeros(5, np.int32), goff=np.zeros(6, np.int64), delta_off=np.zeros(6, np.int64),
+        drows=np.zeros(0, np.int32), extras={4: {"vfs": "four"}, 1: {"vfs": "one"}})
     col = _Collect()
     col.restored(b, np.array([4, 0, 1], dtype=np.int64))  # not ascending
     assert col.ids == ["s4", "s0", "s1"]

@@ -1,0 +1,149 @@
+"""Whole-session migration between ranks: 10⁴ sessions
+built on rank 0 are rebalanced over 2 / 4 gloo ranks (device buffers exchanged
+with ``all_to_all_single``; RCCL over xGMI on MI355X), then one rank retires —
+its sessions move again, with no checkpoint file.  Every route answer (session
+detail, Merkle roots, vouches, σ_eff / exposure, sagas, stats, agent liability,
+exposure vectors) equals the answer before any move, and every rank's
+``verify_audit`` passes over the rows it received."""
+
+from __future__ import annotations
+
+import asyncio
+import os
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N = 10_000
+HEAVY = 200  # sessions that also get audit deltas, a saga, a vouch (and some a terminate)
+
+
+async def build(shv) -> list:
+    from hypervisor import SessionConfig
+    from hypervisor.audit.delta import VFSChange
+
+    sids = []
+    for i in range(N):
+        sid = await shv.create_session(SessionConfig(max_participants=4), f"did:admin-{i % 7}", rank=0)
+        await shv.join_session(sid, f"did:a{i % 11}", sigma_raw=0.55 + 0.04 * (i % 10))
+        if i < HEAVY:
+            await shv.activate_session(sid)
+            for t in range(i % 4):
+                await shv.capture(sid, f"did:a{i % 11}",
+                                  [VFSChange(path=f"/f{t}", operation="add", content_hash=f"h{i}-{t}")])
+            gid = await shv.create_saga(sid)
+            st = await shv.add_step(gid, "deploy", f"did:a{i % 11}", "/d", undo_api="/u")
+            await shv.execute_step(gid, st, "noop")
+            await shv.vouch(f"did:a{i % 11}", f"did:b{i % 5}", sid, 0.9, bond_pct=0.1 + 0.01 * (i % 7))
+            if i % 9 == 0:
+                await shv.terminate_session(sid)
+        sids.append(sid)
+    return sids
+
+
+async def answers(shv, sids: list) -> dict:
+    out = {"sessions": [], "roots": [], "vouches": [], "sagas": [], "sigma": [], "expo": []}
+    for sid in sids[:HEAVY] + sids[HEAVY::397]:
+        d = await shv.get_session(sid)
+        d.pop("rank", None)
+        out["sessions"].append(d)
+        out["roots"].append(await shv.merkle_root(sid))
+        out["vouches"].append(await shv.list_vouches(sid))
+        out["sagas"].append([await shv.get_saga(g) for g in d["sagas"]])
+    for i, sid in enumerate(sids[:HEAVY:13]):
+        out["sigma"].append(await shv.compute_sigma_eff(f"did:b{i % 5}", sid, 0.5, 0.65))
+        out["expo"].append(await shv.get_total_exposure(f"did:a{i % 11}", sid))
+    st = await shv.stats()
+    out["stats"] = {k: st[k] for k in ("total_sessions", "active_sessions", "total_participants", "active_sagas",
+                                       "total_vouches", "total_sagas")}
+    out["liability"] = [await shv.agent_liability(f"did:a{k}") for k in range(11)] + \
+        [await shv.agent_liability(f"did:b{k}") for k in range(5)]
+    out["xvec"] = await shv.exposure_vector([f"did:a{k}" for k in range(11)])
+    return out
+
+
+def _worker(rank: int, world: int, root: str, q) -> None:
+    os.environ.update(OMP_NUM_THREADS="1", AHV_STORE="cpu")
+    import torch
+
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
+    from agent_hypervisor_amd.parallel.resilience import _store
+    from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
+
+    kv = _store()
+
+    async def wait_key(key):
+        await asyncio.get_running_loop().run_in_executor(None, kv.wait, [key])
+
+    async def main():
+        shv = await ShardedHypervisor(device="cpu").start()
+        res = None
+        if rank == 0:
+            sids = await build(shv)
+            before = await answers(shv, sids)
+            kv.set("mig/built", "1")
+        else:
+            await wait_key("mig/built")
+        moved = shv.rebalance()
+        load1 = None
+        if rank == 0:
+            load1 = await shv.load()
+            after = await answers(shv, sids)
+        audit1 = shv.local.verify_audit()
+        kv.set(f"mig/audit1/{rank}", repr((audit1.ok, audit1.sessions)))
+        if rank == 0:
+            kv.set("mig/phase2", "1")
+        else:
+            await wait_key("mig/phase2")
+        retired = None
+        if world > 2:
+            leaver = world - 1
+            retired = shv.retire(leaver)
+            if rank == leaver:
+                kv.set("mig/left", "1")
+                return None
+            if rank == 0:
+                await wait_key("mig/left")
+                load2 = await shv.load()
+                after2 = await answers(shv, sids)
+                res = dict(load2=load2, same2=after2 == before, retired=retired)
+        if rank == 0:
+            audits = [eval(kv.get(f"mig/audit1/{r}").decode()) for r in range(world)]  # noqa: S307 - own repr
+            res = dict(res or {}, moved=moved, load1=load1, same=after == before, audits=audits,
+                       diff=[k for k in before if before[k] != after[k]])
+            await shv.shutdown()
+        else:
+            await shv.serve_forever()
+        return res
+
+    res = asyncio.run(main())
+    if rank == 0:
+        q.put(res)
+        q.close()
+        q.join_thread()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rebalance_and_retire_move_sessions_with_identical_answers(tmp_path, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = q.get(timeout=900)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert res["same"], res["diff"]
+    assert res["moved"]["sent"] == N - N // world
+    assert max(res["load1"]) - min(res["load1"]) <= 1 and sum(res["load1"]) == N
+    assert all(ok and n > 0 for ok, n in res["audits"]), res["audits"]
+    if world > 2:
+        assert res["same2"]
+        assert res["load2"][world - 1] == 0 and sum(res["load2"]) == N
