@@ -439,7 +439,7 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         nd_ = len(d_pool)
         cnt = np.diff(delta_off)
         turn = np.arange(nd_, dtype=np.int64) - np.repeat(delta_off[:-1].astype(np.int64), cnt) + 1
-        digits = np.char.str_len(turn.astype(str)) if nd_ else np.zeros(0, np.int64)
+        digits = 1 + sum((turn >= 10 ** k).astype(np.int64) for k in range(1, 10)) if nd_ else np.zeros(0, np.int64)
         caps = ((base_caps + 2 * digits + np.where(turn > 1, 66, 4) + 8 + 63) & ~63).astype(np.int32)
     nd = len(caps)
     # Lane orders that balance the waves.  Render: records grouped by shape (turn 1 —
@@ -517,8 +517,10 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
     args.update(prefix_in_render=_SP_PREFIX_IN_RENDER,
                 max_nch=int(np.diff(np.asarray(ch_off_all, dtype=np.int64)).max()) if nd else 0)
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
-    committed = [i for i in range(n) if (int(flags[i]) & 9) == 9 and delta_off[i + 1] > delta_off[i]] \
-        if not shared else (list(range(n)) if (int(flags[0]) & 9) == 9 and delta_off[1] > 0 else [])
+    if shared:
+        committed = list(range(n)) if (int(flags[0]) & 9) == 9 and delta_off[1] > 0 else []
+    else:  # audit on, terminate requested, at least one delta (vectorized)
+        committed = np.flatnonzero(((np.asarray(flags) & 9) == 9) & (np.diff(delta_off) > 0)).tolist()
     p = Prepared()
     p.store, p.specs, p.shared, p.n, p.nd, p.ids, p.slots, p.t0 = st, specs, shared, n, nd, ids, slots, t0
     p.tens, p.args, p.flags, p.committed, p.j_agent = tens, args, flags, committed, j_agent

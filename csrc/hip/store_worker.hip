@@ -42,6 +42,19 @@ namespace ahv {
 namespace store {
 
 constexpr int kJobs = 64;  // LDS capture-job ring
+
+// Optional timeline (AHV_STORE_TRACE=<entries>): per command [seq+1, op, t_seen, t_done]
+// at trace[4·(seq mod cap)], per hash-engine job [seq+1, blocks | batch << 32, t_start,
+// t_end] at trace[4·(cap + seq mod cap)]; s_memrealtime ticks (100 MHz), pinned memory.
+__device__ __forceinline__ void trace_put(uint64_t* tr, int64_t cap, int64_t half, uint64_t seq, uint64_t a,
+                                          uint64_t t0, uint64_t t1) {
+  if (tr == nullptr || cap <= 0) return;
+  uint64_t* e = tr + 4 * (half * cap + static_cast<int64_t>(seq % static_cast<uint64_t>(cap)));
+  __hip_atomic_store(e + 1, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(e + 2, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(e + 3, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(e, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 constexpr uint64_t kFreeScan = 8192;  // session / delta rows a FREE_ROWS checks against the queue (longer: full drain)
 
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
@@ -107,8 +120,10 @@ __device__ int batch_size(const HashJob* jobs, uint32_t done, uint32_t avail, in
 
 // Lane `lane` < n hashes job jobs[(done + lane) % kJobs] and completes it.
 __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, int n, uint32_t* win,
-                           uint32_t* kwrows, uint64_t* res, int64_t nslots, int lane, bool light) {
+                           uint32_t* kwrows, uint64_t* res, int64_t nslots, int lane, bool light, uint64_t* tr,
+                           int64_t tcap) {
   if (lane >= n) return;
+  const uint64_t tj0 = __builtin_amdgcn_s_memrealtime();
   const HashJob j = jobs[(done + lane) % kJobs];
   uint32_t* w = win + kBatchStride * lane;
   const uint64_t len = static_cast<uint64_t>(j.len);
@@ -176,12 +191,14 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
   out64(r + 1, ST_OK);
   publish_fence(light);  // digest rows + result words before the sequence word
   out64(r, j.seq + 1);
+  trace_put(tr, tcap, 1, j.seq, static_cast<uint64_t>(nblk) | (static_cast<uint64_t>(n) << 32), tj0,
+            __builtin_amdgcn_s_memrealtime());
 }
 
 __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
                                                            uint64_t* res, uint8_t* bulk, uint64_t* alive,
                                                            int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks,
-                                                           int speculate) {
+                                                           int speculate, uint64_t* tr, int64_t tcap) {
   __shared__ uint64_t inl[kInlineWords];
   __shared__ uint32_t lds1[kLdsWords];      // wave 1: capture message staging
   __shared__ uint32_t kw1[64 * kKwStride];  // wave 1: per-lane K+W schedule rows
@@ -232,7 +249,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         // several captures queued: hash the distinct-session prefix one job per lane
         const int nb = batch_size(jobs, done, head - done, batch_sess, lane);
         if (nb >= 2) {
-          hash_batch(t, jobs, done, nb, batch_win, kw1, res, nslots, lane, false);
+          hash_batch(t, jobs, done, nb, batch_win, kw1, res, nslots, lane, false, tr, tcap);
           done += static_cast<uint32_t>(nb);
           L.sync();
           if (lane == 0) lds_release(&q_done, done);
@@ -245,6 +262,8 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       if (lane == 0) {
         publish_fence(false);  // digest row + result words before the sequence word
         out64(r, j.seq + 1);
+        trace_put(tr, tcap, 1, j.seq, static_cast<uint64_t>(job_blocks(j)) | (1ull << 32), e_start,
+                  __builtin_amdgcn_s_memrealtime());
       }
       ++done;
       // Idle next?  Then compute the chain's provisional Merkle root now, so a
@@ -414,8 +433,9 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       out64(r, next + 1);
     }
     if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    ++next;
     last = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) trace_put(tr, tcap, 0, next, c.op, c_start, last);
+    ++next;
     // utilisation telemetry (host-visible, pinned): busy ticks of the command wave
     // (decode → result written; waits for the hash engine included) and commands
     busy += last - c_start;
@@ -443,8 +463,8 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
 extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64_t* ring, int64_t nslots,
                                        uint64_t* res, uint8_t* bulk, uint64_t* alive, int64_t* tail,
                                        uint64_t idle_ticks, uint64_t max_ticks, int speculate,
-                                       hipStream_t stream) {
+                                       uint64_t* trace, int64_t trace_cap, hipStream_t stream) {
   hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(128), 0, stream, *t, ring, nslots, res, bulk,
-                     alive, tail, idle_ticks, max_ticks, speculate);
+                     alive, tail, idle_ticks, max_ticks, speculate, trace, trace_cap);
   return static_cast<int>(hipGetLastError());
 }

@@ -210,73 +210,106 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   std::vector<uint8_t> flags(n), s_undo, s_fail;
   std::vector<int64_t> base_caps;
   std::unordered_map<PyObject*, std::tuple<int32_t, double, uint8_t>> cfg_cache;
-  std::unordered_map<PyObject*, int32_t> str_cache;  // per-call: the same str object interned once
+  std::unordered_map<PyObject*, int32_t> str_cache, agent_cache;  // per call: a str object interned once per pool
   auto intern = [&](StringPool& p, const py::handle& o) -> int32_t {
-    auto it = str_cache.find(o.ptr());
-    if (&p == &pool && it != str_cache.end()) return it->second;
+    auto& cache = &p == &pool ? str_cache : agent_cache;
+    auto it = cache.find(o.ptr());
+    if (it != cache.end()) return it->second;
     const int32_t id = p.intern(utf8_of(o));
-    if (&p == &pool) str_cache.emplace(o.ptr(), id);
+    cache.emplace(o.ptr(), id);
     return id;
   };
   auto esc = [&](const py::handle& o) -> int64_t {  // escaped length with quotes, "null" for None
     return o.is_none() ? 4 : pool.esc_len(intern(pool, o)) + 2;
   };
+  // One spec object's packed columns.  Batches drawn from a pool of specs (the same
+  // PipelineSpec object for many sessions) are packed once per object and copied.
+  struct Rec {
+    int32_t creator = 0, maxpart = 0;
+    double minsig = 0.0;
+    uint8_t flags = 0;
+    std::vector<int32_t> join_agent, d_pool, ch_cnt, ch_rows, s_retry;
+    std::vector<double> join_sigma;
+    std::vector<int64_t> base_caps;
+    std::vector<uint8_t> s_undo, s_fail;
+  };
+  std::unordered_map<PyObject*, Rec> recs;
   static const py::str kJoins("joins"), kDeltas("deltas"), kSteps("steps"), kAct("activate"), kTerm("terminate"),
       kComp("compensate"), kCfg("config"), kCreator("creator_did");
   for (size_t i = 0; i < n; ++i) {
     py::handle sp = specs[i];
-    py::object cfg = sp.attr(kCfg);
-    auto ci = cfg_cache.find(cfg.ptr());
-    if (ci == cfg_cache.end()) {
-      if (cfg.is_none()) {  // the default SessionConfig, resolved by the caller
-        py::tuple r = cfg_of(cfg);
-        ci = cfg_cache.emplace(cfg.ptr(), std::make_tuple(r[0].cast<int32_t>(), r[1].cast<double>(),
-                                                          r[2].cast<uint8_t>())).first;
-      } else {
-        ci = cfg_cache.emplace(cfg.ptr(), config_row(cfg)).first;
+    auto ri = recs.find(sp.ptr());
+    if (ri == recs.end()) {
+      Rec r;
+      py::object cfg = sp.attr(kCfg);
+      auto ci = cfg_cache.find(cfg.ptr());
+      if (ci == cfg_cache.end()) {
+        if (cfg.is_none()) {  // the default SessionConfig, resolved by the caller
+          py::tuple t = cfg_of(cfg);
+          ci = cfg_cache.emplace(cfg.ptr(), std::make_tuple(t[0].cast<int32_t>(), t[1].cast<double>(),
+                                                            t[2].cast<uint8_t>())).first;
+        } else {
+          ci = cfg_cache.emplace(cfg.ptr(), config_row(cfg)).first;
+        }
       }
+      r.maxpart = std::get<0>(ci->second);
+      r.minsig = std::get<1>(ci->second);
+      r.flags = static_cast<uint8_t>(std::get<2>(ci->second) | (PyObject_IsTrue(sp.attr(kAct).ptr()) ? 4 : 0) |
+                                     (PyObject_IsTrue(sp.attr(kTerm).ptr()) ? 8 : 0) |
+                                     (PyObject_IsTrue(sp.attr(kComp).ptr()) ? 16 : 0));
+      r.creator = intern(agents, sp.attr(kCreator));
+      for (py::handle j : sp.attr(kJoins)) {
+        py::sequence t = py::reinterpret_borrow<py::sequence>(j);
+        r.join_agent.push_back(intern(agents, t[0]));
+        r.join_sigma.push_back(py::float_(t[1]).cast<double>());
+      }
+      for (py::handle d : sp.attr(kDeltas)) {
+        py::sequence t = py::reinterpret_borrow<py::sequence>(d);
+        py::object did = t[0];
+        r.d_pool.push_back(intern(pool, did));
+        int64_t cap = fixed + esc(did);
+        int k = 0;
+        for (py::handle c : py::reinterpret_borrow<py::sequence>(t[1])) {
+          py::sequence ct = py::reinterpret_borrow<py::sequence>(c);
+          const size_t cn = py::len(ct);
+          py::object path = ct[0], op = ct[1], h = ct[2];
+          py::object prev = cn > 3 ? py::object(ct[3]) : py::object(py::none());
+          r.ch_rows.push_back(intern(pool, path));
+          r.ch_rows.push_back(intern(pool, op));
+          r.ch_rows.push_back(h.is_none() ? -1 : intern(pool, h));
+          r.ch_rows.push_back(prev.is_none() ? -1 : intern(pool, prev));
+          cap += 17 + 15 + 10 + 19 + 1 + (k ? 2 : 0) + esc(h) + esc(op) + esc(path) + esc(prev);
+          ++k;
+        }
+        r.ch_cnt.push_back(k);
+        r.base_caps.push_back(cap);
+      }
+      for (py::handle st : sp.attr(kSteps)) {
+        py::sequence t = py::reinterpret_borrow<py::sequence>(st);
+        r.s_undo.push_back(PyObject_IsTrue(py::object(t[3]).ptr()) ? 1 : 0);
+        r.s_retry.push_back(py::int_(t[4]).cast<int32_t>());
+        const int64_t f = py::int_(t[5]).cast<int64_t>();
+        r.s_fail.push_back(static_cast<uint8_t>(f < 255 ? f : 255));
+      }
+      ri = recs.emplace(sp.ptr(), std::move(r)).first;
     }
-    maxpart[i] = std::get<0>(ci->second);
-    minsig[i] = std::get<1>(ci->second);
-    flags[i] = static_cast<uint8_t>(std::get<2>(ci->second) | (PyObject_IsTrue(sp.attr(kAct).ptr()) ? 4 : 0) |
-                                    (PyObject_IsTrue(sp.attr(kTerm).ptr()) ? 8 : 0) |
-                                    (PyObject_IsTrue(sp.attr(kComp).ptr()) ? 16 : 0));
-    creator[i] = intern(agents, sp.attr(kCreator));
-    for (py::handle j : sp.attr(kJoins)) {
-      py::sequence t = py::reinterpret_borrow<py::sequence>(j);
-      join_agent.push_back(intern(agents, t[0]));
-      join_sigma.push_back(py::float_(t[1]).cast<double>());
-    }
+    const Rec& r = ri->second;
+    maxpart[i] = r.maxpart;
+    minsig[i] = r.minsig;
+    flags[i] = r.flags;
+    creator[i] = r.creator;
+    join_agent.insert(join_agent.end(), r.join_agent.begin(), r.join_agent.end());
+    join_sigma.insert(join_sigma.end(), r.join_sigma.begin(), r.join_sigma.end());
     join_off.push_back(static_cast<int32_t>(join_agent.size()));
-    for (py::handle d : sp.attr(kDeltas)) {
-      py::sequence t = py::reinterpret_borrow<py::sequence>(d);
-      py::object did = t[0];
-      d_pool.push_back(intern(pool, did));
-      int64_t cap = fixed + esc(did);
-      int k = 0;
-      for (py::handle c : py::reinterpret_borrow<py::sequence>(t[1])) {
-        py::sequence ct = py::reinterpret_borrow<py::sequence>(c);
-        const size_t cn = py::len(ct);
-        py::object path = ct[0], op = ct[1], h = ct[2];
-        py::object prev = cn > 3 ? py::object(ct[3]) : py::object(py::none());
-        ch_rows.push_back(intern(pool, path));
-        ch_rows.push_back(intern(pool, op));
-        ch_rows.push_back(h.is_none() ? -1 : intern(pool, h));
-        ch_rows.push_back(prev.is_none() ? -1 : intern(pool, prev));
-        cap += 17 + 15 + 10 + 19 + 1 + (k ? 2 : 0) + esc(h) + esc(op) + esc(path) + esc(prev);
-        ++k;
-      }
-      ch_off.push_back(static_cast<int32_t>(ch_rows.size() / 4));
-      base_caps.push_back(cap);
-    }
+    d_pool.insert(d_pool.end(), r.d_pool.begin(), r.d_pool.end());
+    base_caps.insert(base_caps.end(), r.base_caps.begin(), r.base_caps.end());
+    ch_rows.insert(ch_rows.end(), r.ch_rows.begin(), r.ch_rows.end());
+    int32_t c0 = ch_off.back();
+    for (int32_t k : r.ch_cnt) ch_off.push_back(c0 += k);
     delta_off.push_back(static_cast<int32_t>(d_pool.size()));
-    for (py::handle st : sp.attr(kSteps)) {
-      py::sequence t = py::reinterpret_borrow<py::sequence>(st);
-      s_undo.push_back(PyObject_IsTrue(py::object(t[3]).ptr()) ? 1 : 0);
-      s_retry.push_back(py::int_(t[4]).cast<int32_t>());
-      const int64_t f = py::int_(t[5]).cast<int64_t>();
-      s_fail.push_back(static_cast<uint8_t>(f < 255 ? f : 255));
-    }
+    s_undo.insert(s_undo.end(), r.s_undo.begin(), r.s_undo.end());
+    s_retry.insert(s_retry.end(), r.s_retry.begin(), r.s_retry.end());
+    s_fail.insert(s_fail.end(), r.s_fail.begin(), r.s_fail.end());
     step_off.push_back(static_cast<int32_t>(s_undo.size()));
   }
   py::dict out;

@@ -333,6 +333,16 @@ class Store : public StoreCore {
     for (auto r : rows) release_row(kind, r.cast<int64_t>());
   }
 
+  // The worker timeline (AHV_STORE_TRACE): (commands uint64[cap,4], engine jobs uint64[cap,4],
+  // host post times uint64[cap]) as bytes, or None when tracing is off.
+  py::object trace() const {
+    if (trace_buf() == nullptr) return py::none();
+    const size_t cap = static_cast<size_t>(trace_cap());
+    const char* b = reinterpret_cast<const char*>(trace_buf());
+    return py::make_tuple(py::bytes(b, cap * 32), py::bytes(b + cap * 32, cap * 32),
+                          py::bytes(reinterpret_cast<const char*>(post_ns().data()), cap * 8));
+  }
+
   py::dict info() const {
     py::dict d;
     d["gpu"] = gpu_;
@@ -430,6 +440,7 @@ void register_store(py::module_& m) {
       .def("grow_payload", &Store::grow_payload)
       .def("close", &Store::close)
       .def("info", &Store::info)
+      .def("trace", &Store::trace)
       .def("set_timeout", &Store::set_timeout)
       .def_property_readonly("delta_live", &Store::delta_live)
       .def_property_readonly("payload_cap", &Store::payload_cap)

@@ -35,7 +35,8 @@
 
 extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64_t* ring, int64_t nslots,
                                        uint64_t* res, uint8_t* bulk, uint64_t* alive, int64_t* tail,
-                                       uint64_t idle_ticks, uint64_t max_ticks, int speculate, hipStream_t stream);
+                                       uint64_t idle_ticks, uint64_t max_ticks, int speculate, uint64_t* trace,
+                                       int64_t trace_cap, hipStream_t stream);
 
 namespace ahv {
 namespace host {
@@ -197,6 +198,16 @@ class StoreCore {
                    ((lp == nullptr || std::atoi(lp) != 0) ? 32 : 0) |
                    ((pf2 == nullptr || std::atoi(pf2) != 0) ? 64 : 0);
       max_ticks_ = static_cast<uint64_t>(max_ms) * 100000;
+      // command / hash-engine timeline (AHV_STORE_TRACE=<entries>, off by default)
+      const char* tr = std::getenv("AHV_STORE_TRACE");
+      if (tr != nullptr && std::atoll(tr) > 0) {
+        trace_cap_ = std::atoll(tr);
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&trace_), static_cast<size_t>(trace_cap_) * 64,
+                                hipHostMallocCoherent),
+                  "store trace");
+        std::memset(trace_, 0, static_cast<size_t>(trace_cap_) * 64);
+        post_ns_.assign(static_cast<size_t>(trace_cap_), 0);
+      }
     } else {
       ring_ = static_cast<uint64_t*>(std::calloc(ring_bytes / 8, 8));
       staging_ = static_cast<uint8_t*>(std::calloc(static_cast<size_t>(staging_cap_), 1));
@@ -233,6 +244,7 @@ class StoreCore {
       (void)hipHostFree(bulk_);
       (void)hipHostFree(alive_);
       (void)hipHostFree(tail_);
+      if (trace_) (void)hipHostFree(trace_);
       if (stream_) (void)hipStreamDestroy(stream_);
     } else {
       std::free(ring_);
@@ -347,6 +359,10 @@ class StoreCore {
     for (int k = 3; k < kSlotWords; ++k) x ^= w[k];
     w[2] = x;
     ++posted_;
+    if (trace_cap_ > 0)
+      post_ns_[static_cast<size_t>(q % static_cast<uint64_t>(trace_cap_))] = static_cast<uint64_t>(
+          std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+              .count());
     if (!gpu_) {
       uint64_t* slot = ring_ + idx * kSlotWords;
       std::memcpy(slot, w, sizeof w);
@@ -400,7 +416,7 @@ class StoreCore {
     if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) != 0) return;
     __atomic_store_n(alive_, 1ull, __ATOMIC_RELEASE);
     const int rc = ahv_store_launch_worker(&t_, ring_, nslots_, res_, bulk_, alive_, tail_, idle_ticks_, max_ticks_,
-                                           speculate_, stream_);
+                                           speculate_, trace_, trace_cap_, stream_);
     if (rc != 0) {
       __atomic_store_n(alive_, 0ull, __ATOMIC_RELEASE);
       throw std::runtime_error(std::string("store worker launch failed: ") +
@@ -921,6 +937,9 @@ class StoreCore {
   uint64_t reclaims() const { return reclaims_; }
   uint64_t reclaim_waits() const { return reclaim_waits_; }
   uint64_t double_releases() const { return double_releases_; }
+  const uint64_t* trace_buf() const { return trace_; }
+  int64_t trace_cap() const { return trace_cap_; }
+  const std::vector<uint64_t>& post_ns() const { return post_ns_; }
   int64_t nslots() const { return nslots_; }
   size_t kept() const { return watched_.size() + saved_.size(); }
   const int64_t* tail() const { return tail_; }
@@ -968,6 +987,9 @@ class StoreCore {
   uint64_t launches_ = 0;
   uint64_t double_releases_ = 0;  // releases of rows that were not live (ignored)
   std::vector<uint8_t> dreleased_;  // delta rows released and not yet reclaimed
+  uint64_t* trace_ = nullptr;       // worker timeline (AHV_STORE_TRACE): [2·cap][4] words, pinned
+  int64_t trace_cap_ = 0;
+  std::vector<uint64_t> post_ns_;   // host post time of each traced sequence number (steady clock)
   uint64_t reclaims_ = 0;        // reclaim_pool passes that returned queued rows (any table)
   uint64_t reclaim_waits_ = 0;   // times a reclaim blocked on a FREE_ROWS result
   size_t stage_head_ = 0;

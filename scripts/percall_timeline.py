@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""Timeline of the per-call reference pipeline on the device store worker.
+
+Runs the reference-harness pipeline (``benchmarks/bench_hypervisor.py:217-239``)
+``ITERS`` times through ``Hypervisor(device="cuda")`` with the worker's timeline
+trace on (``AHV_STORE_TRACE``), then prints, per command of the pipeline (median
+over the pipelines), when the host posted it, when the worker picked it up and
+finished it, and for captures when the hash engine hashed the record — all in µs
+from the pipeline's first post.  Host and device clocks are aligned on the
+earliest pickup (transit ≈ 0 for the fastest command).
+
+    AHV_STORE_TRACE=65536 python scripts/percall_timeline.py
+"""
+
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import statistics
+import sys
+import time
+
+os.environ.setdefault("AHV_STORE_TRACE", "65536")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> None:
+    import numpy as np
+
+    from hypervisor import Hypervisor, SessionConfig
+    from hypervisor.audit.delta import VFSChange
+
+    iters = int(os.environ.get("ITERS", "400"))
+    dev = os.environ.get("DEV", "cuda")
+    marks = []
+
+    async def one():
+        p = time.perf_counter_ns
+        m = {"t0": p()}
+        hv = Hypervisor(device=dev)
+        st = hv._store
+        m["q0"] = st._c.info()["posted"]
+        s = await hv.create_session(config=SessionConfig(enable_audit=True), creator_did="did:mesh:admin")
+        sid = s.sso.session_id
+        await hv.join_session(sid, "did:mesh:a", sigma_raw=0.8)
+        await hv.activate_session(sid)
+        for i in range(3):
+            s.delta_engine.capture("did:mesh:a", [VFSChange(path=f"/f{i}", operation="add", content_hash=f"h{i}")])
+        saga = s.saga.create_saga(sid)
+        step = s.saga.add_step(saga.saga_id, "action", "did:mesh:a", "/api/action")
+        await s.saga.execute_step(saga.saga_id, step.step_id, executor=lambda: asyncio.sleep(0))
+        m["t_term"] = p()
+        await hv.terminate_session(sid)
+        m["t_end"] = p()
+        m["q1"] = st._c.info()["posted"]
+        marks.append(m)
+        return st
+
+    async def run(n):
+        st = None
+        for _ in range(n):
+            st = await one()
+        return st
+
+    asyncio.run(run(50))
+    marks.clear()
+    st = asyncio.run(run(iters))
+    st.drain()
+    tr = st._c.trace()
+    if tr is None:
+        raise SystemExit("tracing is off (AHV_STORE_TRACE)")
+    cmd = np.frombuffer(tr[0], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+    eng = np.frombuffer(tr[1], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+    post = np.frombuffer(tr[2], dtype=np.uint64).astype(np.int64)
+    cap = len(post)
+    ok = cmd[:, 0] > 0
+    seqs = cmd[ok, 0] - 1
+    # clock alignment: device ticks are 10 ns; offset so that the fastest pickup has transit 0
+    off = np.min(cmd[ok, 2] * 10 - post[seqs % cap])
+    rows = {}
+    for m in marks:
+        base = None
+        for k, q in enumerate(range(m["q0"], m["q1"])):
+            c = cmd[q % cap]
+            if c[0] != q + 1:
+                continue
+            pt = post[q % cap]
+            if base is None:
+                base = pt
+            e = eng[q % cap]
+            r = rows.setdefault(k, {"op": int(c[1]), "post": [], "seen": [], "done": [], "eng0": [], "eng1": [],
+                                    "blocks": []})
+            r["post"].append((pt - base) / 1e3)
+            r["seen"].append((c[2] * 10 - off - base) / 1e3)
+            r["done"].append((c[3] * 10 - off - base) / 1e3)
+            if e[0] == q + 1:
+                r["eng0"].append((e[2] * 10 - off - base) / 1e3)
+                r["eng1"].append((e[3] * 10 - off - base) / 1e3)
+                r["blocks"].append(int(e[1] & 0xFFFFFFFF))
+        m["term_host"] = (m["t_term"] - m["t0"]) / 1e3
+    from agent_hypervisor_amd.models.store import OPS
+
+    name = {v: k for k, v in OPS.items()}
+    med = lambda xs: round(statistics.median(xs), 2) if xs else None  # noqa: E731
+    out = []
+    for k in sorted(rows):
+        r = rows[k]
+        out.append({"k": k, "op": name.get(r["op"], r["op"]), "post": med(r["post"]), "seen": med(r["seen"]),
+                    "done": med(r["done"]), "engine_start": med(r["eng0"]), "engine_end": med(r["eng1"]),
+                    "blocks": med(r["blocks"])})
+    lat = [(m["t_end"] - m["t0"]) / 1e3 for m in marks]
+    print(json.dumps({"device": dev, "iters": iters, "p50_us": med(lat),
+                      "terminate_called_us": med([m["term_host"] for m in marks]),
+                      "spec_terminate": os.environ.get("AHV_SPEC_TERMINATE", "1")}))
+    for o in out:
+        print(json.dumps(o))
+
+
+if __name__ == "__main__":
+    main()
