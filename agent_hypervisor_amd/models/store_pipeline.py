@@ -77,6 +77,8 @@ class PipelineRun:
     join_rings: np.ndarray    # per join, in spec order
     join_codes: np.ndarray
     device_seconds: float = 0.0
+    prepare_seconds: float = 0.0   # host packing + row allocation + argument upload
+    finish_seconds: float = 0.0    # read-back + lazy registration
     _roots: tuple = field(default=(), repr=False)  # (committed session indices, their roots as one hex string)
 
     @property
@@ -329,7 +331,16 @@ class _CfgHolder:
 
 def run(hv, specs, n: Optional[int] = None) -> PipelineRun:
     """Build the batch arrays, run the store pipeline, register lazy sessions."""
-    return finish(hv, launch(prepare(hv, specs, n)))
+    import time
+
+    t0 = time.perf_counter()
+    p = prepare(hv, specs, n)
+    t1 = time.perf_counter()
+    launch(p)
+    t2 = time.perf_counter()
+    r = finish(hv, p)
+    r.prepare_seconds, r.finish_seconds = t1 - t0, time.perf_counter() - t2
+    return r
 
 
 class Prepared:

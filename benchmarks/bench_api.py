@@ -93,12 +93,18 @@ def batch_api_throughput(device: str, n: int = 100_000, rounds: int = 3, hetero:
     else:
         specs = PipelineSpec()
 
+    marks: dict = {}
+
     async def one():
+        t = time.perf_counter()
         hv = Hypervisor(device=device)
-        return await hv.run_pipelines(specs, None if hetero else n)
+        marks["init"] = time.perf_counter() - t
+        r = await hv.run_pipelines(specs, None if hetero else n)
+        marks["teardown0"] = time.perf_counter()
+        return r
 
     asyncio.run(one())  # warm-up (allocations, kernel load)
-    rates, dev = [], []
+    rates, dev, phases = [], [], []
     ok = True
     for _ in range(rounds):
         gc.collect()
@@ -107,9 +113,12 @@ def batch_api_throughput(device: str, n: int = 100_000, rounds: int = 3, hetero:
         dt = time.perf_counter() - t0
         rates.append(n / dt)
         dev.append(run.device_seconds)
+        phases.append({"hv_init": marks["init"], "prepare": run.prepare_seconds, "device": run.device_seconds,
+                       "finish": run.finish_seconds, "teardown": time.perf_counter() - marks["teardown0"]})
         ok = ok and (hetero or (run.ok == n and len(run.roots) == n))
     return {"device": device, "sessions": n, "hetero": hetero, "sessions_per_s": round(statistics.median(rates), 1),
-            "rounds": [round(r, 1) for r in rates], "device_ms": [round(1000 * x, 2) for x in dev], "ok": ok}
+            "rounds": [round(r, 1) for r in rates], "device_ms": [round(1000 * x, 2) for x in dev],
+            "phases_ms": {k: round(1000 * statistics.median(p[k] for p in phases), 2) for k in phases[0]}, "ok": ok}
 
 
 def main() -> None:

@@ -28,9 +28,17 @@ namespace py = pybind11;
 namespace ahv {
 namespace {
 
-template <int W>
+template <int W, bool Pair = false>
 struct TeeWindowSink : WordWindowSink<W> {
   using B = WordWindowSink<W>;
+  // Pair: Merkle interior nodes two at a time (sha256_compress2, ILP 2) — for the
+  // register-rich variant; at 168 VGPRs the pair spills.
+  static constexpr bool kPairNodes = Pair;
+  __device__ __forceinline__ void node2(const uint32_t l0[8], const uint32_t r0[8], uint32_t o0[8],
+                                        const uint32_t l1[8], const uint32_t r1[8], uint32_t o1[8]) const {
+    merkle_node2(l0, r0, o0, l1, r1, o1);
+  }
+  bool nohash = false;  // A/B: emission and tee only
 
   // Hash the record `emit(*this)` produces (midstate modes as WordWindowSink::
   // hash_mid) and store its bytes at `dst` (memory order); `len` = its length.
@@ -78,7 +86,7 @@ struct TeeWindowSink : WordWindowSink<W> {
       }
 #pragma nounroll
       for (int blk = 0; blk < W; ++blk) {
-        if (this->lo + 16 * blk < total) {
+        if (!nohash && this->lo + 16 * blk < total) {
           uint32_t w[16];
 #pragma unroll
           for (int k = 0; k < 16; ++k) w[k] = this->g_win[(blk * 16 + k) * kWaveLanes + this->lane];
@@ -106,7 +114,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 // A/B switches (AHV_TEMPLATE_AB, measurement only): bit 0 — skip the record tee
 // (digests and rows only); bit 1 — tee into a coarse-grained scratch buffer
-// instead of the store's fine-grained payload arena.
+// instead of the store's fine-grained payload arena; bit 2 — no Merkle root;
+// bit 3 — no record compressions (emission + tee only).
 static int template_ab() {
   static const int v = [] {
     const char* e = std::getenv("AHV_TEMPLATE_AB");
@@ -135,13 +144,13 @@ static int template_waves() {
   return v;
 }
 
-template <int MinWaves, int W>
+template <int MinWaves, int W, bool Pair = false>
 __global__ __launch_bounds__(kWaveLanes, MinWaves) void store_template_kernel(TemplateArgs a) {
   const uint32_t lane = threadIdx.x;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
   PipeCounters c{};
   if (i < a.n) {
-    TeeWindowSink<W> sink;
+    TeeWindowSink<W, Pair> sink;
     sink.g_win = win_lds<W>();
     sink.lane = lane;
     c = template_session(a, i, sink);
@@ -262,6 +271,7 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
   TemplateArgs b = a;
   const int ab = template_ab();
   if (ab & 1) b.notee = 1;
+  b.ab = ab & 12;
   if (ab & 2) {
     static uint8_t* scratch = nullptr;
     static int64_t scratch_cap = 0;
@@ -282,6 +292,10 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
     hipLaunchKernelGGL((store_template_kernel<1, 6>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else if (waves == 2)  // 231 VGPRs, no scratch
     hipLaunchKernelGGL((store_template_kernel<2, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
+  else if (waves == 12)  // 2 waves/SIMD, Merkle nodes paired (ILP 2), no scratch
+    hipLaunchKernelGGL((store_template_kernel<2, 3, true>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
+  else if (waves == 13)  // 3 waves/SIMD, Merkle nodes paired
+    hipLaunchKernelGGL((store_template_kernel<3, 3, true>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else if (waves == 4)  // 2-block window (8.5 KiB LDS): 4 waves per SIMD, one more emission pass
     hipLaunchKernelGGL((store_template_kernel<4, 2>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else  // 168 VGPRs (3 waves/SIMD) with a small spill
@@ -294,6 +308,8 @@ void kernels_store_template(std::vector<KernelEntry>& out) {
   out.push_back({"store_template_kernel<2,3>", reinterpret_cast<const void*>(&store_template_kernel<2, 3>)});
   out.push_back({"store_template_kernel<1,6>", reinterpret_cast<const void*>(&store_template_kernel<1, 6>)});
   out.push_back({"store_template_kernel<4,2>", reinterpret_cast<const void*>(&store_template_kernel<4, 2>)});
+  out.push_back({"store_template_kernel<2,3,pair>", reinterpret_cast<const void*>(&store_template_kernel<2, 3, true>)});
+  out.push_back({"store_template_kernel<3,3,pair>", reinterpret_cast<const void*>(&store_template_kernel<3, 3, true>)});
 }
 
 }  // namespace ahv

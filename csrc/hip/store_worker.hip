@@ -191,8 +191,10 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
   out64(r + 1, ST_OK);
   publish_fence(light);  // digest rows + result words before the sequence word
   out64(r, j.seq + 1);
-  trace_put(tr, tcap, 1, j.seq, static_cast<uint64_t>(nblk) | (static_cast<uint64_t>(n) << 32), tj0,
-            __builtin_amdgcn_s_memrealtime());
+  trace_put(tr, tcap, 1, j.seq,
+            (static_cast<uint64_t>(nblk) & 0xff) | (static_cast<uint64_t>(skip & 0xff) << 8) |
+                (static_cast<uint64_t>(n) << 16),
+            tj0, __builtin_amdgcn_s_memrealtime());
 }
 
 __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
@@ -258,12 +260,12 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       }
       const HashJob j = jobs[done % kJobs];
       uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;
-      capture_finish(L, t, j, r);
+      uint64_t tele = 0;
+      capture_finish(L, t, j, r, &tele);
       if (lane == 0) {
         publish_fence(false);  // digest row + result words before the sequence word
         out64(r, j.seq + 1);
-        trace_put(tr, tcap, 1, j.seq, static_cast<uint64_t>(job_blocks(j)) | (1ull << 32), e_start,
-                  __builtin_amdgcn_s_memrealtime());
+        trace_put(tr, tcap, 1, j.seq, tele | (1ull << 16), e_start, __builtin_amdgcn_s_memrealtime());
       }
       ++done;
       // Idle next?  Then compute the chain's provisional Merkle root now, so a
@@ -399,6 +401,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     if (c.op == OP_ACQUIRE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     uint64_t* r = res + (next % static_cast<uint64_t>(nslots)) * kResWords;
     HashJob job;
+    job.mid_blocks = 0;
     const int rc = store_exec(L, t, c, next, r, bulk, &job);
     if (c.op == OP_FLUSH) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     L.sync();
@@ -434,7 +437,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     }
     if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     last = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) trace_put(tr, tcap, 0, next, c.op, c_start, last);
+    if (lane == 0) trace_put(tr, tcap, 0, next, c.op | (static_cast<uint64_t>(job.mid_blocks & 0xff) << 32), c_start, last);
     ++next;
     // utilisation telemetry (host-visible, pinned): busy ticks of the command wave
     // (decode → result written; waits for the hash engine included) and commands

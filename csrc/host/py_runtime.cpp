@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -64,17 +66,21 @@ static void escape_json_utf8(const std::string& in, std::vector<uint8_t>& out) {
 
 class StringPool {
  public:
-  int32_t intern(const std::string& s) {
+  int32_t intern(const std::string& s) { return intern(std::string_view(s)); }
+
+  // Lookup without building a std::string (keys are views of the stable raw_
+  // entries: a deque never moves its elements).
+  int32_t intern(std::string_view s) {
     auto it = ids_.find(s);
     if (it != ids_.end()) return it->second;
     const int32_t id = static_cast<int32_t>(raw_.size());
-    ids_.emplace(s, id);
-    raw_.push_back(s);
+    raw_.emplace_back(s);
+    ids_.emplace(std::string_view(raw_.back()), id);
     // every string starts 16-byte aligned so kernels read it with 16-byte loads
     bytes_.resize((bytes_.size() + 15) & ~size_t(15), 0);
     offsets_.push_back(static_cast<int64_t>(bytes_.size()));
     const size_t before = bytes_.size();
-    escape_json_utf8(s, bytes_);
+    escape_json_utf8(raw_.back(), bytes_);
     lengths_.push_back(static_cast<int32_t>(bytes_.size() - before));
     // keep the pool a multiple of 16 bytes: kernels read whole 16-byte chunks
     bytes_.resize((bytes_.size() + 15) & ~size_t(15), 0);
@@ -89,7 +95,7 @@ class StringPool {
   }
 
   int32_t lookup(const std::string& s) const {
-    auto it = ids_.find(s);
+    auto it = ids_.find(std::string_view(s));
     return it == ids_.end() ? -1 : it->second;
   }
 
@@ -119,8 +125,8 @@ class StringPool {
   }
 
  private:
-  std::unordered_map<std::string, int32_t> ids_;
-  std::vector<std::string> raw_;
+  std::unordered_map<std::string_view, int32_t> ids_;
+  std::deque<std::string> raw_;
   std::vector<uint8_t> bytes_;
   std::vector<int64_t> offsets_;
   std::vector<int32_t> lengths_;
@@ -190,17 +196,77 @@ static py::bytes as_bytes(const std::vector<T>& v) {
   return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(T));
 }
 
-static std::tuple<int32_t, double, uint8_t> config_row(const py::handle& c) {
+// Borrowed items of a list / tuple (any other sequence is converted once).
+struct FastSeq {
+  PyObject* o;
+  PyObject** it;
+  Py_ssize_t n;
+  explicit FastSeq(PyObject* x) : o(PySequence_Fast(x, "expected a sequence")) {
+    if (o == nullptr) throw py::error_already_set();
+    it = PySequence_Fast_ITEMS(o);
+    n = PySequence_Fast_GET_SIZE(o);
+  }
+  ~FastSeq() { Py_DECREF(o); }
+  FastSeq(const FastSeq&) = delete;
+  FastSeq& operator=(const FastSeq&) = delete;
+  PyObject* operator[](Py_ssize_t i) const {
+    if (i >= n) throw py::index_error("spec tuple too short");
+    return it[i];
+  }
+};
+
+static py::object getattr_(PyObject* o, const py::str& name) {
+  PyObject* r = PyObject_GetAttr(o, name.ptr());
+  if (r == nullptr) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(r);
+}
+
+static int truth(PyObject* o) {
+  const int v = PyObject_IsTrue(o);
+  if (v < 0) throw py::error_already_set();
+  return v;
+}
+
+static double as_double(PyObject* o) {
+  const double v = PyFloat_AsDouble(o);
+  if (v == -1.0 && PyErr_Occurred()) throw py::error_already_set();
+  return v;
+}
+
+static int64_t as_int(PyObject* o) {
+  const long long v = PyLong_AsLongLong(o);
+  if (v == -1 && PyErr_Occurred()) throw py::error_already_set();
+  return v;
+}
+
+// UTF-8 of a str without copying (CPython caches it in the object; ASCII strings
+// return their own data).  Lone surrogates take the surrogatepass copy in `tmp`.
+static std::string_view utf8_view(PyObject* o, std::string& tmp) {
+  Py_ssize_t n = 0;
+  const char* c = PyUnicode_AsUTF8AndSize(o, &n);
+  if (c != nullptr) return std::string_view(c, static_cast<size_t>(n));
+  PyErr_Clear();
+  tmp = utf8_of(py::handle(o));
+  return std::string_view(tmp);
+}
+
+static std::tuple<int32_t, double, uint8_t> config_row(PyObject* c) {
   static const py::str kMode("consistency_mode"), kMax("max_participants"), kMin("min_sigma_eff"),
       kAudit("enable_audit");
-  const std::string mode = utf8_of(c.attr(kMode));
-  if (mode != "strong" && mode != "eventual") throw py::value_error("'" + mode + "' is not a valid ConsistencyMode");
-  const int audit = PyObject_IsTrue(c.attr(kAudit).ptr());
-  if (audit < 0) throw py::error_already_set();
-  return {py::int_(c.attr(kMax)).cast<int32_t>(), py::float_(c.attr(kMin)).cast<double>(),
+  std::string tmp;
+  py::object m = getattr_(c, kMode);
+  if (!PyUnicode_Check(m.ptr())) m = getattr_(m.ptr(), py::str("value"));  // a non-str enum: its value
+  const std::string_view mode = utf8_view(m.ptr(), tmp);
+  if (mode != "strong" && mode != "eventual")
+    throw py::value_error("'" + std::string(mode) + "' is not a valid ConsistencyMode");
+  const int audit = truth(getattr_(c, kAudit).ptr());
+  return {static_cast<int32_t>(as_int(getattr_(c, kMax).ptr())), as_double(getattr_(c, kMin).ptr()),
           static_cast<uint8_t>((audit ? 1 : 0) | (mode == "strong" ? 2 : 0))};
 }
 
+// Spec packing works straight on the CPython objects: borrowed tuple items, no
+// per-spec containers.  A spec object seen before in the batch (batches drawn
+// from a pool of specs) copies its first occurrence's rows.
 static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool& pool, const py::object& cfg_of,
                            int64_t fixed) {
   const size_t n = specs.size();
@@ -209,107 +275,125 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   std::vector<double> minsig(n), join_sigma;
   std::vector<uint8_t> flags(n), s_undo, s_fail;
   std::vector<int64_t> base_caps;
+  join_agent.reserve(3 * n);
+  join_sigma.reserve(3 * n);
+  d_pool.reserve(2 * n);
+  base_caps.reserve(2 * n);
+  ch_rows.reserve(16 * n);
   std::unordered_map<PyObject*, std::tuple<int32_t, double, uint8_t>> cfg_cache;
-  std::unordered_map<PyObject*, int32_t> str_cache, agent_cache;  // per call: a str object interned once per pool
-  auto intern = [&](StringPool& p, const py::handle& o) -> int32_t {
-    auto& cache = &p == &pool ? str_cache : agent_cache;
-    auto it = cache.find(o.ptr());
-    if (it != cache.end()) return it->second;
-    const int32_t id = p.intern(utf8_of(o));
-    cache.emplace(o.ptr(), id);
-    return id;
+  std::string tmp;
+  auto intern = [&](StringPool& p, PyObject* o) -> int32_t {
+    if (!PyUnicode_Check(o)) throw py::type_error("spec strings must be str");
+    return p.intern(utf8_view(o, tmp));
   };
-  auto esc = [&](const py::handle& o) -> int64_t {  // escaped length with quotes, "null" for None
-    return o.is_none() ? 4 : pool.esc_len(intern(pool, o)) + 2;
+  auto esc_of = [&](int32_t id) -> int64_t { return id < 0 ? 4 : pool.esc_len(id) + 2; };
+  // first occurrence of a spec object: where its rows start in every column
+  struct First {
+    size_t spec, j0, d0, st0;
   };
-  // One spec object's packed columns.  Batches drawn from a pool of specs (the same
-  // PipelineSpec object for many sessions) are packed once per object and copied.
-  struct Rec {
-    int32_t creator = 0, maxpart = 0;
-    double minsig = 0.0;
-    uint8_t flags = 0;
-    std::vector<int32_t> join_agent, d_pool, ch_cnt, ch_rows, s_retry;
-    std::vector<double> join_sigma;
-    std::vector<int64_t> base_caps;
-    std::vector<uint8_t> s_undo, s_fail;
-  };
-  std::unordered_map<PyObject*, Rec> recs;
+  std::unordered_map<PyObject*, First> seen;
   static const py::str kJoins("joins"), kDeltas("deltas"), kSteps("steps"), kAct("activate"), kTerm("terminate"),
       kComp("compensate"), kCfg("config"), kCreator("creator_did");
+  PyObject* const* items = PySequence_Fast_ITEMS(specs.ptr());
+  auto copy_range = [](auto& v, size_t a, size_t cnt) {
+    v.reserve(v.size() + cnt);
+    for (size_t k = 0; k < cnt; ++k) v.push_back(v[a + k]);
+  };
   for (size_t i = 0; i < n; ++i) {
-    py::handle sp = specs[i];
-    auto ri = recs.find(sp.ptr());
-    if (ri == recs.end()) {
-      Rec r;
-      py::object cfg = sp.attr(kCfg);
-      auto ci = cfg_cache.find(cfg.ptr());
-      if (ci == cfg_cache.end()) {
-        if (cfg.is_none()) {  // the default SessionConfig, resolved by the caller
-          py::tuple t = cfg_of(cfg);
-          ci = cfg_cache.emplace(cfg.ptr(), std::make_tuple(t[0].cast<int32_t>(), t[1].cast<double>(),
-                                                            t[2].cast<uint8_t>())).first;
-        } else {
-          ci = cfg_cache.emplace(cfg.ptr(), config_row(cfg)).first;
-        }
+    PyObject* sp = items[i];
+    if (seen.size() < 65536) {  // (bounded: a batch of all-distinct specs gains nothing from the map)
+      auto hit = seen.find(sp);
+      if (hit != seen.end()) {
+        const First& f = hit->second;
+        creator[i] = creator[f.spec];
+        maxpart[i] = maxpart[f.spec];
+        minsig[i] = minsig[f.spec];
+        flags[i] = flags[f.spec];
+        const size_t nj = static_cast<size_t>(join_off[f.spec + 1] - join_off[f.spec]);
+        copy_range(join_agent, f.j0, nj);
+        copy_range(join_sigma, f.j0, nj);
+        join_off.push_back(static_cast<int32_t>(join_agent.size()));
+        const size_t nd = static_cast<size_t>(delta_off[f.spec + 1] - delta_off[f.spec]);
+        copy_range(d_pool, f.d0, nd);
+        copy_range(base_caps, f.d0, nd);
+        const int32_t cfirst = ch_off[f.d0];
+        const size_t nch = static_cast<size_t>(ch_off[f.d0 + nd] - cfirst);
+        const size_t c0 = ch_rows.size();
+        copy_range(ch_rows, static_cast<size_t>(cfirst) * 4, nch * 4);
+        for (size_t k = 0; k < nd; ++k) ch_off.push_back(static_cast<int32_t>(c0 / 4) + ch_off[f.d0 + k + 1] - cfirst);
+        delta_off.push_back(static_cast<int32_t>(d_pool.size()));
+        const size_t ns = static_cast<size_t>(step_off[f.spec + 1] - step_off[f.spec]);
+        copy_range(s_undo, f.st0, ns);
+        copy_range(s_retry, f.st0, ns);
+        copy_range(s_fail, f.st0, ns);
+        step_off.push_back(static_cast<int32_t>(s_undo.size()));
+        continue;
       }
-      r.maxpart = std::get<0>(ci->second);
-      r.minsig = std::get<1>(ci->second);
-      r.flags = static_cast<uint8_t>(std::get<2>(ci->second) | (PyObject_IsTrue(sp.attr(kAct).ptr()) ? 4 : 0) |
-                                     (PyObject_IsTrue(sp.attr(kTerm).ptr()) ? 8 : 0) |
-                                     (PyObject_IsTrue(sp.attr(kComp).ptr()) ? 16 : 0));
-      r.creator = intern(agents, sp.attr(kCreator));
-      for (py::handle j : sp.attr(kJoins)) {
-        py::sequence t = py::reinterpret_borrow<py::sequence>(j);
-        r.join_agent.push_back(intern(agents, t[0]));
-        r.join_sigma.push_back(py::float_(t[1]).cast<double>());
-      }
-      for (py::handle d : sp.attr(kDeltas)) {
-        py::sequence t = py::reinterpret_borrow<py::sequence>(d);
-        py::object did = t[0];
-        r.d_pool.push_back(intern(pool, did));
-        int64_t cap = fixed + esc(did);
-        int k = 0;
-        for (py::handle c : py::reinterpret_borrow<py::sequence>(t[1])) {
-          py::sequence ct = py::reinterpret_borrow<py::sequence>(c);
-          const size_t cn = py::len(ct);
-          py::object path = ct[0], op = ct[1], h = ct[2];
-          py::object prev = cn > 3 ? py::object(ct[3]) : py::object(py::none());
-          r.ch_rows.push_back(intern(pool, path));
-          r.ch_rows.push_back(intern(pool, op));
-          r.ch_rows.push_back(h.is_none() ? -1 : intern(pool, h));
-          r.ch_rows.push_back(prev.is_none() ? -1 : intern(pool, prev));
-          cap += 17 + 15 + 10 + 19 + 1 + (k ? 2 : 0) + esc(h) + esc(op) + esc(path) + esc(prev);
-          ++k;
-        }
-        r.ch_cnt.push_back(k);
-        r.base_caps.push_back(cap);
-      }
-      for (py::handle st : sp.attr(kSteps)) {
-        py::sequence t = py::reinterpret_borrow<py::sequence>(st);
-        r.s_undo.push_back(PyObject_IsTrue(py::object(t[3]).ptr()) ? 1 : 0);
-        r.s_retry.push_back(py::int_(t[4]).cast<int32_t>());
-        const int64_t f = py::int_(t[5]).cast<int64_t>();
-        r.s_fail.push_back(static_cast<uint8_t>(f < 255 ? f : 255));
-      }
-      ri = recs.emplace(sp.ptr(), std::move(r)).first;
+      seen.emplace(sp, First{i, join_agent.size(), d_pool.size(), s_undo.size()});
     }
-    const Rec& r = ri->second;
-    maxpart[i] = r.maxpart;
-    minsig[i] = r.minsig;
-    flags[i] = r.flags;
-    creator[i] = r.creator;
-    join_agent.insert(join_agent.end(), r.join_agent.begin(), r.join_agent.end());
-    join_sigma.insert(join_sigma.end(), r.join_sigma.begin(), r.join_sigma.end());
+    py::object cfg = getattr_(sp, kCfg);
+    auto ci = cfg_cache.find(cfg.ptr());
+    if (ci == cfg_cache.end()) {
+      if (cfg.is_none()) {  // the default SessionConfig, resolved by the caller
+        py::tuple t = cfg_of(cfg);
+        ci = cfg_cache.emplace(cfg.ptr(), std::make_tuple(t[0].cast<int32_t>(), t[1].cast<double>(),
+                                                          t[2].cast<uint8_t>())).first;
+      } else {
+        ci = cfg_cache.emplace(cfg.ptr(), config_row(cfg.ptr())).first;
+      }
+    }
+    maxpart[i] = std::get<0>(ci->second);
+    minsig[i] = std::get<1>(ci->second);
+    flags[i] = static_cast<uint8_t>(std::get<2>(ci->second) | (truth(getattr_(sp, kAct).ptr()) ? 4 : 0) |
+                                    (truth(getattr_(sp, kTerm).ptr()) ? 8 : 0) |
+                                    (truth(getattr_(sp, kComp).ptr()) ? 16 : 0));
+    creator[i] = intern(agents, getattr_(sp, kCreator).ptr());
+    {
+      py::object js = getattr_(sp, kJoins);
+      FastSeq jl(js.ptr());
+      for (Py_ssize_t k = 0; k < jl.n; ++k) {
+        FastSeq t(jl.it[k]);
+        join_agent.push_back(intern(agents, t[0]));
+        join_sigma.push_back(as_double(t[1]));
+      }
+    }
     join_off.push_back(static_cast<int32_t>(join_agent.size()));
-    d_pool.insert(d_pool.end(), r.d_pool.begin(), r.d_pool.end());
-    base_caps.insert(base_caps.end(), r.base_caps.begin(), r.base_caps.end());
-    ch_rows.insert(ch_rows.end(), r.ch_rows.begin(), r.ch_rows.end());
-    int32_t c0 = ch_off.back();
-    for (int32_t k : r.ch_cnt) ch_off.push_back(c0 += k);
+    {
+      py::object ds = getattr_(sp, kDeltas);
+      FastSeq dl(ds.ptr());
+      for (Py_ssize_t k = 0; k < dl.n; ++k) {
+        FastSeq t(dl.it[k]);
+        const int32_t did = intern(pool, t[0]);
+        d_pool.push_back(did);
+        int64_t cap = fixed + esc_of(did);
+        FastSeq cl(t[1]);
+        for (Py_ssize_t q = 0; q < cl.n; ++q) {
+          FastSeq ct(cl.it[q]);
+          const int32_t path = intern(pool, ct[0]), op = intern(pool, ct[1]);
+          const int32_t h = ct[2] == Py_None ? -1 : intern(pool, ct[2]);
+          const int32_t prev = ct.n > 3 && ct.it[3] != Py_None ? intern(pool, ct.it[3]) : -1;
+          ch_rows.push_back(path);
+          ch_rows.push_back(op);
+          ch_rows.push_back(h);
+          ch_rows.push_back(prev);
+          cap += 17 + 15 + 10 + 19 + 1 + (q ? 2 : 0) + esc_of(h) + esc_of(op) + esc_of(path) + esc_of(prev);
+        }
+        ch_off.push_back(static_cast<int32_t>(ch_rows.size() / 4));
+        base_caps.push_back(cap);
+      }
+    }
     delta_off.push_back(static_cast<int32_t>(d_pool.size()));
-    s_undo.insert(s_undo.end(), r.s_undo.begin(), r.s_undo.end());
-    s_retry.insert(s_retry.end(), r.s_retry.begin(), r.s_retry.end());
-    s_fail.insert(s_fail.end(), r.s_fail.begin(), r.s_fail.end());
+    {
+      py::object ss = getattr_(sp, kSteps);
+      FastSeq sl(ss.ptr());
+      for (Py_ssize_t k = 0; k < sl.n; ++k) {
+        FastSeq t(sl.it[k]);
+        s_undo.push_back(truth(t[3]) ? 1 : 0);
+        s_retry.push_back(static_cast<int32_t>(as_int(t[4])));
+        const int64_t f = as_int(t[5]);
+        s_fail.push_back(static_cast<uint8_t>(f < 255 ? f : 255));
+      }
+    }
     step_off.push_back(static_cast<int32_t>(s_undo.size()));
   }
   py::dict out;
@@ -431,7 +515,7 @@ static py::list round_many(const std::vector<double>& xs, int n) {
 void register_runtime(py::module_& m) {
   py::class_<StringPool>(m, "StringPool", "Host string interner feeding the device string pool")
       .def(py::init<>())
-      .def("intern", &StringPool::intern)
+      .def("intern", static_cast<int32_t (StringPool::*)(const std::string&)>(&StringPool::intern))
       .def("intern_many", &StringPool::intern_many)
       .def("lookup", &StringPool::lookup)
       // bytes (UTF-8, lone surrogates in surrogatepass form): the Python wrapper decodes

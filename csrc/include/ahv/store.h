@@ -1714,7 +1714,7 @@ AHV_HD uint64_t engine_clock() {
 #endif
 }
 
-AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, uint64_t* r) {
+AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, uint64_t* r, uint64_t* tele = nullptr) {
   const uint64_t c0 = engine_clock();
   uint8_t* p = t.payload + j.off;
   const uint32_t* parent = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
@@ -1729,6 +1729,11 @@ AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, ui
   out64(r + 10, c1 - c0);
   out64(r + 11, engine_clock() - c1);
   out64(r + 12, static_cast<uint64_t>(nblk));
+  if (tele) {  // worker timeline: blocks | skipped << 8 | stage ticks << 24 | hash ticks << 44
+    const uint64_t c2 = engine_clock();
+    tele[0] = (static_cast<uint64_t>(nblk) & 0xff) | (static_cast<uint64_t>(skip & 0xff) << 8) |
+              ((c1 - c0) & 0xfffff) << 24 | ((c2 - c1) & 0xfffff) << 44;
+  }
   if (nblk < 0) sha256_fine(p, static_cast<uint64_t>(j.len), h);  // record larger than the LDS window
   store8(t.d_hash + 8 * j.d, h);
   store8(t.s_head + 8 * j.s, h);

@@ -57,6 +57,7 @@ struct TemplateArgs {
   int32_t* status;               // [n] out (StorePipeStatus codes), or null
   unsigned long long* stats;     // [kStatSpread·kPipeStats] spread batch counters (X04), or null
   int32_t notee;                 // A/B only: digests without storing the records (AHV_TEMPLATE_AB)
+  int32_t ab;                    // A/B only (measurement, wrong digests): 4 no Merkle root, 8 no record SHA
   // Ring mode (ring_cap > 0; GovernanceEngine's private store, which owns every row):
   // session i uses row (slot_base + i) % ring_cap for its session / saga / step rows,
   // delta rows row·dstride + d with records at off_base + (row·dstride + d)·rec_bytes,
@@ -123,6 +124,7 @@ AHV_HD uint32_t record_suffix_len(int64_t ts_us, uint32_t turn) {
 // Host twin of the device's record sink: streams the record into SHA-256 and
 // into the arena at once.
 struct HostTeeSink : HostSink {
+  bool nohash = false;  // (device A/B knob; the host twin always hashes)
   uint8_t* dst = nullptr;
   uint32_t nb = 0;
   AHV_HD void put4(uint32_t v) {
@@ -272,6 +274,7 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
     const ChangeIds* ch = a.changes + d * nch;
     uint32_t h[8];
     uint32_t len = 0;
+    sink.nohash = (a.ab & 8) != 0;
     sink.hash_record([=](Sink& k) {
       emit_delta_payload(k, pool, did, ch, nch, -1, turn, d > 0, prev, sid, tsd);
     }, h, mid, mode, dst, len);
@@ -302,7 +305,7 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
 
   // ---- terminate: Merkle root (K09) → commitment ---------------------------------------
   uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (committed) {
+  if (committed && !(a.ab & 4)) {
     merkle_root_levels(
         sink, static_cast<uint32_t>(D),
         [&](uint32_t d, uint32_t hh[8]) {

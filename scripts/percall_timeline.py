@@ -90,15 +90,22 @@ def main() -> None:
             if base is None:
                 base = pt
             e = eng[q % cap]
-            r = rows.setdefault(k, {"op": int(c[1]), "post": [], "seen": [], "done": [], "eng0": [], "eng1": [],
-                                    "blocks": []})
+            r = rows.setdefault(k, {"op": int(c[1]) & 0xFFFFFFFF, "post": [], "seen": [], "done": [], "eng0": [],
+                                    "eng1": [], "blocks": [], "prefix": [], "skip": [], "batch": [], "stage": [],
+                                    "hash": []})
+            r["prefix"].append(int(c[1]) >> 32 & 0xFF)
             r["post"].append((pt - base) / 1e3)
             r["seen"].append((c[2] * 10 - off - base) / 1e3)
             r["done"].append((c[3] * 10 - off - base) / 1e3)
             if e[0] == q + 1:
                 r["eng0"].append((e[2] * 10 - off - base) / 1e3)
                 r["eng1"].append((e[3] * 10 - off - base) / 1e3)
-                r["blocks"].append(int(e[1] & 0xFFFFFFFF))
+                f = int(e[1])
+                r["blocks"].append(f & 0xFF)
+                r["skip"].append(f >> 8 & 0xFF)
+                r["batch"].append(f >> 16 & 0xFF)
+                r["stage"].append((f >> 24 & 0xFFFFF) / 100)  # 10 ns ticks → µs
+                r["hash"].append((f >> 44 & 0xFFFFF) / 100)
         m["term_host"] = (m["t_term"] - m["t0"]) / 1e3
     from agent_hypervisor_amd.models.store import OPS
 
@@ -109,7 +116,8 @@ def main() -> None:
         r = rows[k]
         out.append({"k": k, "op": name.get(r["op"], r["op"]), "post": med(r["post"]), "seen": med(r["seen"]),
                     "done": med(r["done"]), "engine_start": med(r["eng0"]), "engine_end": med(r["eng1"]),
-                    "blocks": med(r["blocks"])})
+                    "blocks": med(r["blocks"]), "cmd_prefix_blocks": med(r["prefix"]), "skip": med(r["skip"]),
+                    "batch": med(r["batch"]), "stage_us": med(r["stage"]), "hash_us": med(r["hash"])})
     lat = [(m["t_end"] - m["t0"]) / 1e3 for m in marks]
     print(json.dumps({"device": dev, "iters": iters, "p50_us": med(lat),
                       "terminate_called_us": med([m["term_host"] for m in marks]),
