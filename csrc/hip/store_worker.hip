@@ -209,6 +209,10 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   __shared__ HashJob jobs[kJobs];
   __shared__ uint32_t batch_win[64 * kBatchStride];  // wave 1: per-lane record windows (batched hashing)
   __shared__ int32_t batch_sess[64];
+  // wave 1: the leaf digests of the chain it last extended (session cc_s, cc_n leaves,
+  // the last one delta row cc_d), for the provisional Merkle root
+  __shared__ uint32_t chain_cache[64 * 8];
+  __shared__ int32_t cc_s, cc_n, cc_d;
   __shared__ uint32_t q_head, q_done, stop, bye, spec_s;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -218,6 +222,9 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     stop = 0;
     bye = 0;
     spec_s = 0;  // session + 1 whose provisional Merkle root wave 1 is computing (0: none)
+    cc_s = -1;
+    cc_n = 0;
+    cc_d = -1;
   }
   __syncthreads();  // the only workgroup barrier: both waves pass it once
 
@@ -252,6 +259,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         const int nb = batch_size(jobs, done, head - done, batch_sess, lane);
         if (nb >= 2) {
           hash_batch(t, jobs, done, nb, batch_win, kw1, res, nslots, lane, false, tr, tcap);
+          if (lane == 0) cc_s = -1;
           done += static_cast<uint32_t>(nb);
           L.sync();
           if (lane == 0) lds_release(&q_done, done);
@@ -261,8 +269,22 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       const HashJob j = jobs[done % kJobs];
       uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;
       uint64_t tele = 0;
-      capture_finish(L, t, j, r, &tele);
+      uint32_t hd[8];
+      capture_finish(L, t, j, r, &tele, hd);
       if (lane == 0) {
+        // extend the cached chain (turn 1 starts one; anything else invalidates it)
+        const bool extend = j.prev >= 0 && cc_s == static_cast<int32_t>(j.s) && cc_d == static_cast<int32_t>(j.prev) &&
+                            cc_n < 64;
+        if (j.prev < 0 || extend) {
+          const int32_t k = j.prev < 0 ? 0 : cc_n;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) chain_cache[8 * k + q] = hd[q];
+          cc_s = static_cast<int32_t>(j.s);
+          cc_n = k + 1;
+          cc_d = static_cast<int32_t>(j.d);
+        } else {
+          cc_s = -1;
+        }
         publish_fence(false);  // digest row + result words before the sequence word
         out64(r, j.seq + 1);
         trace_put(tr, tcap, 1, j.seq, tele | (1ull << 16), e_start, __builtin_amdgcn_s_memrealtime());
@@ -279,8 +301,11 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         lds_release(&q_done, done);
       }
       if (idle) {
-        const int64_t n = static_cast<int64_t>(t.d_turn[j.d]);
-        merkle_provisional(L, t, j.s, j.d, n, lds1, [&] { return lds_acquire(&q_head) != done; });
+        L.sync();  // the leader's cache update is visible to every lane
+        const bool hit = cc_s == static_cast<int32_t>(j.s) && cc_d == static_cast<int32_t>(j.d);
+        const int64_t n = hit ? static_cast<int64_t>(cc_n) : static_cast<int64_t>(t.d_turn[j.d]);
+        merkle_provisional(L, t, j.s, j.d, n, lds1, [&] { return lds_acquire(&q_head) != done; },
+                           hit ? chain_cache : nullptr);
         if (lane == 0) lds_release(&spec_s, 0u);  // the s_proot rows precede this release
       }
     }

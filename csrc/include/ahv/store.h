@@ -659,12 +659,16 @@ AHV_HD int32_t capture_prefix(const Lanes& L, const Tables& t, const HashJob& j,
 // schedule folds at compile time).  `abort()` is polled between levels (a new
 // capture is queued: its digest comes first); returns false when abandoned or
 // when the chain is not the expected one.  `lv`: 8·64 words of LDS.
+// `cached` (or null): the chain's n leaf digests, in order, already at hand (the
+// hash engine keeps the chain it is extending in LDS) — no walk over d_prev.
 template <class Abort>
 AHV_HD bool merkle_provisional(const Lanes& L, const Tables& t, int64_t s, int64_t d, int64_t n, uint32_t* lv,
-                               const Abort& abort) {
+                               const Abort& abort, const uint32_t* cached = nullptr) {
   if (n < 1 || n > 64 || L.kw == nullptr) return false;
   int ok = 1;
-  if (L.leader()) {
+  if (cached) {
+    for (int64_t i = L.lane; i < 8 * n; i += L.n) lv[i] = cached[i];
+  } else if (L.leader()) {
     int64_t k = d;
     for (int64_t i = n - 1; i >= 0; --i) {
       if (k < 0 || k >= t.cap.D || t.d_sess[k] != s || t.d_turn[k] != i + 1) {
@@ -1714,7 +1718,8 @@ AHV_HD uint64_t engine_clock() {
 #endif
 }
 
-AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, uint64_t* r, uint64_t* tele = nullptr) {
+AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, uint64_t* r, uint64_t* tele = nullptr,
+                           uint32_t* hout = nullptr) {
   const uint64_t c0 = engine_clock();
   uint8_t* p = t.payload + j.off;
   const uint32_t* parent = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
@@ -1739,6 +1744,8 @@ AHV_HD void capture_finish(const Lanes& L, const Tables& t, const HashJob& j, ui
   store8(t.s_head + 8 * j.s, h);
   for (int k = 0; k < 8; ++k) out64(r + 2 + k, h[k]);
   out64(r + 1, ST_OK);
+  if (hout)
+    for (int k = 0; k < 8; ++k) hout[k] = h[k];
 }
 
 AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* r, uint8_t* bulk) {

@@ -73,6 +73,8 @@ _SPEC_LIFECYCLE = os.environ.get("AHV_SPEC_LIFECYCLE", "1") != "0"
 # predictions (K08/K09 on the host beside the device; the device's own root is what
 # it commits, and it must equal the prediction)
 _SPEC_TERMINATE = os.environ.get("AHV_SPEC_TERMINATE", "1") != "0"
+# awaited terminates compare the device's root with the host's prediction (AHV_CHECK_TERMINATE=0: off)
+_CHECK_TERMINATE = os.environ.get("AHV_CHECK_TERMINATE", "1") != "0"
 _STEPS = list(StepState)
 _STEP_IDX = {**{x: i for i, x in enumerate(_STEPS)}, **{x.value: i for i, x in enumerate(_STEPS)}}
 _COMMITTED_IDX = _STEP_IDX[StepState.COMMITTED]
@@ -693,12 +695,14 @@ class DeviceDeltaEngine(DeltaEngine):
         return n
 
 
-def close_prediction(sso, de: "DeviceDeltaEngine", vsess: int, audit: bool, cutoff_us: int):
+def close_prediction(sso, de: "DeviceDeltaEngine", vsess: int, audit: bool, cutoff_us: int, check: bool = False):
     """(root, expired) the device's OP_SESS_CLOSE of this session will produce, when
     the host knows it: the row is mirrored in a state terminate accepts, the session
     holds no liability rows (their release is awaited), and every delta of the chain
-    was captured here with a predicted digest.  None otherwise (the caller awaits)."""
-    if not _SPEC_TERMINATE or vsess >= 0 or sso._poisoned is not None:
+    was captured here with a predicted digest.  None otherwise (the caller awaits).
+    ``check``: the prediction an awaited terminate compares the device's root with
+    (computed whatever AHV_SPEC_TERMINATE says, liability sessions included)."""
+    if (not check and (not _SPEC_TERMINATE or vsess >= 0)) or sso._poisoned is not None:
         return None
     if sso._m_state != _S_ACTIVE and sso._m_state != _S_HANDSHAKING:
         return None

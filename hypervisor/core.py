@@ -325,6 +325,9 @@ class Hypervisor:
         audit = bool(sso.config.enable_audit)
         args = [sso.slot, n, off, now_us, v, cutoff, int(audit)]
         spec = _d.close_prediction(sso, de, v, audit, cutoff) if guard is not None else None
+        # awaited: the device's root is returned, checked against the host's prediction
+        check = _d.close_prediction(sso, de, v, audit, cutoff, check=True) \
+            if spec is None and guard is not None and _d._CHECK_TERMINATE else None
         sso._m_forget()  # the row leaves the mirrored states (terminate → archive)
         if spec is not None:
             # the host knows the outcome (root from its digest predictions): post the
@@ -348,7 +351,17 @@ class Hypervisor:
         root = _d._hex(r[2:10]) if r[1] else None
         if v >= 0:  # every bond of the session is released now: freeze the records, reuse the edge rows
             self.vouching.retire_session(session_id)
-        return self._terminated(session_id, sso, de, root, int(r[11]), n)
+        out = self._terminated(session_id, sso, de, root, int(r[11]), n)
+        if check is not None and audit and check[0] != root:
+            # the device committed its own root; the host's view of this chain (the
+            # digests it rendered and predicted) disagrees with it: the session is
+            # poisoned and the terminate raises rather than hand out a root the
+            # caller's records do not hash to
+            err = _d._st.StoreError(f"device Merkle root {root} of session {session_id} differs from the host "
+                                    f"prediction {check[0]}")
+            sso._poisoned = err
+            raise err
+        return out
 
     def _terminated(self, session_id: str, sso, de, root: Optional[str], expired: int, n: int) -> Optional[str]:
         """Host bookkeeping after a device close: commitment, GC, events."""

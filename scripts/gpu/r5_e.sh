@@ -6,6 +6,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp AHV_SKIP_AUTOBUILD=1
 OUT=gpurun_out/r5e
 mkdir -p $OUT
+# the worker changed (engine chain cache): its oracle tests first
+timeout -k 10 400 python -u -m pytest tests/test_reference_trace.py tests/test_speculation.py tests/test_gpu_store.py -m gpu -x -q \
+  -p no:cacheprovider --timeout 240 --timeout-method thread > $OUT/worker_tests.log 2>&1; rc=$?
+tail -3 $OUT/worker_tests.log; [ $rc -eq 0 ] || exit $rc
 AHV_SPEC_TERMINATE=0 timeout -k 10 300 python scripts/percall_timeline.py > $OUT/timeline_awaited.jsonl 2>&1 && \
 timeout -k 10 300 python benchmarks/bench_api.py --device cuda --n 200 --batch 20000 --rounds 5 > $OUT/api.json 2>&1
 rc=$?

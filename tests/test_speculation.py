@@ -408,3 +408,35 @@ async def test_cyclic_garbage_never_releases_a_row_twice():
         assert dict(st.live_rows()) == base, (order, st.live_rows(), base)
     rows = st.alloc_many("S", 64).tolist()
     assert len(set(rows)) == len(rows)
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+def test_awaited_terminate_raises_on_a_divergent_chain(dev, monkeypatch):
+    """Device-awaited terminate (the store's root is what terminate returns): when
+    a digest the host handed out for a capture differs from the device's, the
+    terminate of that session raises instead of committing a root the caller's
+    view disagrees with (VERDICT r4 #1)."""
+    from hypervisor import _device as D
+    from hypervisor.audit.delta import VFSChange
+
+    monkeypatch.setattr(D, "_SPEC_TERMINATE", False)
+
+    async def go():
+        hv = Hypervisor(device=dev)
+        m = await hv.create_session(SessionConfig(enable_audit=True), "did:admin")
+        sid = m.sso.session_id
+        await hv.join_session(sid, "did:a", sigma_raw=0.8)
+        await hv.activate_session(sid)
+        m.delta_engine.capture("did:a", [VFSChange(path="/f", operation="add", content_hash="h")])
+        m.delta_engine.deltas[0].__dict__["_pred"] = "0" * 64  # the next prediction chains off a wrong digest
+        m.delta_engine.capture("did:a", [VFSChange(path="/g", operation="add", content_hash="i")])
+        with pytest.raises(StoreError, match="differs from the host prediction"):
+            await hv.terminate_session(sid)
+        # a healthy session of the same hypervisor terminates normally
+        m2 = await hv.create_session(SessionConfig(enable_audit=True), "did:admin")
+        await hv.join_session(m2.sso.session_id, "did:a", sigma_raw=0.8)
+        await hv.activate_session(m2.sso.session_id)
+        m2.delta_engine.capture("did:a", [VFSChange(path="/f", operation="add", content_hash="h")])
+        assert await hv.terminate_session(m2.sso.session_id) == m2.delta_engine.deltas[0].device_hash()
+
+    _run(go())
