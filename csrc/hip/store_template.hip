@@ -28,16 +28,9 @@ namespace py = pybind11;
 namespace ahv {
 namespace {
 
-template <int W, bool Pair = false>
+template <int W>
 struct TeeWindowSink : WordWindowSink<W> {
   using B = WordWindowSink<W>;
-  // Pair: Merkle interior nodes two at a time (sha256_compress2, ILP 2) — for the
-  // register-rich variant; at 168 VGPRs the pair spills.
-  static constexpr bool kPairNodes = Pair;
-  __device__ __forceinline__ void node2(const uint32_t l0[8], const uint32_t r0[8], uint32_t o0[8],
-                                        const uint32_t l1[8], const uint32_t r1[8], uint32_t o1[8]) const {
-    merkle_node2(l0, r0, o0, l1, r1, o1);
-  }
   bool nohash = false;  // A/B: emission and tee only
 
   // Hash the record `emit(*this)` produces (midstate modes as WordWindowSink::
@@ -144,13 +137,13 @@ static int template_waves() {
   return v;
 }
 
-template <int MinWaves, int W, bool Pair = false>
+template <int MinWaves, int W>
 __global__ __launch_bounds__(kWaveLanes, MinWaves) void store_template_kernel(TemplateArgs a) {
   const uint32_t lane = threadIdx.x;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
   PipeCounters c{};
   if (i < a.n) {
-    TeeWindowSink<W, Pair> sink;
+    TeeWindowSink<W> sink;
     sink.g_win = win_lds<W>();
     sink.lane = lane;
     c = template_session(a, i, sink);
@@ -292,10 +285,6 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
     hipLaunchKernelGGL((store_template_kernel<1, 6>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else if (waves == 2)  // 231 VGPRs, no scratch
     hipLaunchKernelGGL((store_template_kernel<2, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
-  else if (waves == 12)  // 2 waves/SIMD, Merkle nodes paired (ILP 2), no scratch
-    hipLaunchKernelGGL((store_template_kernel<2, 3, true>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
-  else if (waves == 13)  // 3 waves/SIMD, Merkle nodes paired
-    hipLaunchKernelGGL((store_template_kernel<3, 3, true>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else if (waves == 4)  // 2-block window (8.5 KiB LDS): 4 waves per SIMD, one more emission pass
     hipLaunchKernelGGL((store_template_kernel<4, 2>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else  // 168 VGPRs (3 waves/SIMD) with a small spill
@@ -308,8 +297,6 @@ void kernels_store_template(std::vector<KernelEntry>& out) {
   out.push_back({"store_template_kernel<2,3>", reinterpret_cast<const void*>(&store_template_kernel<2, 3>)});
   out.push_back({"store_template_kernel<1,6>", reinterpret_cast<const void*>(&store_template_kernel<1, 6>)});
   out.push_back({"store_template_kernel<4,2>", reinterpret_cast<const void*>(&store_template_kernel<4, 2>)});
-  out.push_back({"store_template_kernel<2,3,pair>", reinterpret_cast<const void*>(&store_template_kernel<2, 3, true>)});
-  out.push_back({"store_template_kernel<3,3,pair>", reinterpret_cast<const void*>(&store_template_kernel<3, 3, true>)});
 }
 
 }  // namespace ahv

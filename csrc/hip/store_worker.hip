@@ -1,6 +1,6 @@
 // Resident command worker of the device state store (csrc/include/ahv/store.h).
 //
-// One workgroup of two waves on one CU:
+// One workgroup of three waves on one CU:
 //
 //   wave 0 — command wave: polls the command ring (512-byte slots in fine-grained
 //            device memory the host writes through the PCIe BAR), executes each
@@ -43,9 +43,12 @@ namespace store {
 
 constexpr int kJobs = 64;  // LDS capture-job ring
 
-// Optional timeline (AHV_STORE_TRACE=<entries>): per command [seq+1, op, t_seen, t_done]
-// at trace[4·(seq mod cap)], per hash-engine job [seq+1, blocks | batch << 32, t_start,
-// t_end] at trace[4·(cap + seq mod cap)]; s_memrealtime ticks (100 MHz), pinned memory.
+// Optional timeline (AHV_STORE_TRACE=<entries>): per command [seq+1, op | prefix blocks
+// << 32 | waited ticks << 40, t_seen, t_done] at trace[4·(seq mod cap)], per hash-engine
+// job [seq+1, blocks | skipped << 8 | batch << 16 | stage << 24 | hash << 44, t_start,
+// t_end] at trace[4·(cap + seq mod cap)], per provisional Merkle tree (keyed by the
+// capture job after which it ran) [seq+1, leaves | done << 8 | cached << 9, t_start,
+// t_end] at trace[4·(2·cap + seq mod cap)]; s_memrealtime ticks (100 MHz), pinned memory.
 __device__ __forceinline__ void trace_put(uint64_t* tr, int64_t cap, int64_t half, uint64_t seq, uint64_t a,
                                           uint64_t t0, uint64_t t1) {
   if (tr == nullptr || cap <= 0) return;
@@ -81,6 +84,19 @@ __device__ __forceinline__ void publish_fence(bool light) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // and no compiler motion of the seq store above it
   } else {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+}
+
+// Per-job prefix state (see the header): wave 1 takes a job — CAS 0 → 3, or waits
+// for a running prefix (1) to become ready (2).  `ps` is LDS.
+__device__ __forceinline__ uint32_t lds_cas(uint32_t* p, uint32_t expect, uint32_t want) {
+  __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+  return expect;  // the value found (== the old expect on success)
+}
+__device__ __forceinline__ void take_job(uint32_t* ps) {
+  if (lds_cas(ps, 0u, 3u) == 1u) {
+    while (lds_acquire(ps) != 2u) __builtin_amdgcn_s_sleep(1);
   }
 }
 
@@ -197,7 +213,7 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
             tj0, __builtin_amdgcn_s_memrealtime());
 }
 
-__global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
+__global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
                                                            uint64_t* res, uint8_t* bulk, uint64_t* alive,
                                                            int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks,
                                                            int speculate, uint64_t* tr, int64_t tcap) {
@@ -213,7 +229,12 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   // the last one delta row cc_d), for the provisional Merkle root
   __shared__ uint32_t chain_cache[64 * 8];
   __shared__ int32_t cc_s, cc_n, cc_d;
-  __shared__ uint32_t q_head, q_done, stop, bye, spec_s;
+  // wave 2: per-job prefix state, staging (≤ kPrefixBlocks blocks) and K+W rows
+  constexpr int kPrefixBlocks = 8;
+  __shared__ uint32_t pstate[kJobs];
+  __shared__ uint32_t lds2[16 * kPrefixBlocks];
+  __shared__ uint32_t kw2[kPrefixBlocks * kKwStride];
+  __shared__ uint32_t q_head, q_done, stop, bye, bye2, spec_s;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   if (threadIdx.x == 0) {
@@ -221,12 +242,51 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     q_done = 0;
     stop = 0;
     bye = 0;
+    bye2 = 0;
     spec_s = 0;  // session + 1 whose provisional Merkle root wave 1 is computing (0: none)
     cc_s = -1;
     cc_n = 0;
     cc_d = -1;
   }
-  __syncthreads();  // the only workgroup barrier: both waves pass it once
+  __syncthreads();  // the only workgroup barrier: every wave passes it once
+
+  if (wave == 2) {
+    // ------------------------------------------------------------ prefix wave
+    const Lanes L{lane, 64, lds2, kw2};
+    uint32_t pos = 0;
+    for (;;) {
+      const uint32_t head = lds_acquire(&q_head);
+      const uint32_t dn = lds_acquire(&q_done);
+      if (static_cast<int32_t>(pos - dn) < 0) pos = dn;  // jobs wave 1 finished need nothing
+      if (pos == head || !(speculate & 2)) {
+        if (lds_acquire(&stop)) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      HashJob* jp = &jobs[pos % kJobs];
+      uint32_t* ps = &pstate[pos % kJobs];
+      int claimed = 0;
+      if (lane == 0 && jp->hole >= 64) claimed = lds_cas(ps, 0u, 1u) == 0u;
+      if (__shfl(claimed, 0)) {
+        HashJob jb;
+        jb.off = jp->off;
+        jb.hole = jp->hole;
+        uint32_t mid[8];
+        const int32_t pb = capture_prefix(L, t, jb, lds2, 16 * kPrefixBlocks, kPrefixBlocks, mid);
+        if (lane == 0) {
+          if (pb > 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) jp->mid[k] = mid[k];
+            jp->mid_blocks = pb;
+          }
+          lds_release(ps, 2u);
+        }
+      }
+      ++pos;
+    }
+    if (lane == 0) lds_release(&bye2, 1u);
+    return;
+  }
 
   if (wave == 1) {
     // ------------------------------------------------------------ hash engine
@@ -258,6 +318,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         // several captures queued: hash the distinct-session prefix one job per lane
         const int nb = batch_size(jobs, done, head - done, batch_sess, lane);
         if (nb >= 2) {
+          if (lane < nb) take_job(&pstate[(done + lane) % kJobs]);
           hash_batch(t, jobs, done, nb, batch_win, kw1, res, nslots, lane, false, tr, tcap);
           if (lane == 0) cc_s = -1;
           done += static_cast<uint32_t>(nb);
@@ -266,6 +327,8 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
           continue;
         }
       }
+      if (lane == 0) take_job(&pstate[done % kJobs]);
+      L.sync();  // the job (with any midstate wave 2 wrote) is read after taking it
       const HashJob j = jobs[done % kJobs];
       uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;
       uint64_t tele = 0;
@@ -304,9 +367,14 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
         L.sync();  // the leader's cache update is visible to every lane
         const bool hit = cc_s == static_cast<int32_t>(j.s) && cc_d == static_cast<int32_t>(j.d);
         const int64_t n = hit ? static_cast<int64_t>(cc_n) : static_cast<int64_t>(t.d_turn[j.d]);
-        merkle_provisional(L, t, j.s, j.d, n, lds1, [&] { return lds_acquire(&q_head) != done; },
-                           hit ? chain_cache : nullptr);
+        const uint64_t tt0 = __builtin_amdgcn_s_memrealtime();
+        const bool ok = merkle_provisional(L, t, j.s, j.d, n, lds1, [&] { return lds_acquire(&q_head) != done; },
+                                           hit ? chain_cache : nullptr);
         if (lane == 0) lds_release(&spec_s, 0u);  // the s_proot rows precede this release
+        if (lane == 0)
+          trace_put(tr, tcap, 2, j.seq,
+                    static_cast<uint64_t>(n & 0xff) | (ok ? 256ull : 0ull) | (hit ? 512ull : 0ull), tt0,
+                    __builtin_amdgcn_s_memrealtime());
       }
     }
     if (lane == 0) lds_release(&bye, 1u);
@@ -424,6 +492,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
       while (queued - lds_acquire(&q_done) >= static_cast<uint32_t>(kJobs)) __builtin_amdgcn_s_sleep(1);
     }
     if (c.op == OP_ACQUIRE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint64_t c_waited = __builtin_amdgcn_s_memrealtime() - c_start;
     uint64_t* r = res + (next % static_cast<uint64_t>(nslots)) * kResWords;
     HashJob job;
     job.mid_blocks = 0;
@@ -431,27 +500,10 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     if (c.op == OP_FLUSH) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     L.sync();
     if (rc == EXEC_DEFERRED) {
-      // A capture with a parent: while the hash engine works through the queue,
-      // compress the record's blocks that precede the parent hole here — unless
-      // the next command is already waiting and feature bit 8 is off (then wave 1
-      // does all of it).
-      const int64_t jhole = bcast(L, job.hole);
-      if ((speculate & 2) && jhole >= 64 && lds_acquire(&q_done) != queued) {
-        const uint64_t* nslot = ring + ((next + 1) % static_cast<uint64_t>(nslots)) * kSlotWords;
-        if ((speculate & 8) || __shfl(ld_sys(nslot + lane), 0) != next + 2) {
-          HashJob jb;
-          jb.off = bcast(L, job.off);
-          jb.hole = jhole;
-          uint32_t mid[8];
-          const int32_t pb = capture_prefix(L, t, jb, lds0, kLdsWords / 4, 4, mid);
-          if (lane == 0 && pb > 0) {
-            job.mid_blocks = pb;
-            for (int k = 0; k < 8; ++k) job.mid[k] = mid[k];
-          }
-        }
-      }
       if (lane == 0) {
-        jobs[queued % kJobs] = job;
+        jobs[queued % kJobs] = job;  // (mid_blocks 0: wave 2 may add a midstate)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        pstate[queued % kJobs] = 0u;
         lds_release(&q_head, queued + 1);  // the capture's global row writes precede this release
       }
       ++queued;
@@ -462,7 +514,10 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
     }
     if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     last = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) trace_put(tr, tcap, 0, next, c.op | (static_cast<uint64_t>(job.mid_blocks & 0xff) << 32), c_start, last);
+    if (lane == 0)
+      trace_put(tr, tcap, 0, next,
+                c.op | (static_cast<uint64_t>(job.mid_blocks & 0xff) << 32) | ((c_waited & 0xffffff) << 40), c_start,
+                last);
     ++next;
     // utilisation telemetry (host-visible, pinned): busy ticks of the command wave
     // (decode → result written; waits for the hash engine included) and commands
@@ -477,7 +532,7 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
   // drain the hash engine, stop it, wait for its goodbye, then release the queue
   while (lds_acquire(&q_done) != queued) __builtin_amdgcn_s_sleep(1);
   if (lane == 0) lds_release(&stop, 1u);
-  while (!lds_acquire(&bye)) __builtin_amdgcn_s_sleep(1);
+  while (!lds_acquire(&bye) || !lds_acquire(&bye2)) __builtin_amdgcn_s_sleep(1);
   if (lane == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -487,12 +542,12 @@ __global__ __launch_bounds__(128) void store_worker_kernel(Tables t, const uint6
 }  // namespace store
 }  // namespace ahv
 
-// Host-callable launcher (one workgroup: command wave + hash-engine wave).
+// Host-callable launcher (one workgroup: command wave, hash-engine wave, prefix wave).
 extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64_t* ring, int64_t nslots,
                                        uint64_t* res, uint8_t* bulk, uint64_t* alive, int64_t* tail,
                                        uint64_t idle_ticks, uint64_t max_ticks, int speculate,
                                        uint64_t* trace, int64_t trace_cap, hipStream_t stream) {
-  hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(128), 0, stream, *t, ring, nslots, res, bulk,
+  hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(192), 0, stream, *t, ring, nslots, res, bulk,
                      alive, tail, idle_ticks, max_ticks, speculate, trace, trace_cap);
   return static_cast<int>(hipGetLastError());
 }

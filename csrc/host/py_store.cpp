@@ -334,13 +334,15 @@ class Store : public StoreCore {
   }
 
   // The worker timeline (AHV_STORE_TRACE): (commands uint64[cap,4], engine jobs uint64[cap,4],
-  // host post times uint64[cap]) as bytes, or None when tracing is off.
+  // host post times uint64[cap], provisional Merkle trees uint64[cap,4]) as bytes, or None
+  // when tracing is off.
   py::object trace() const {
     if (trace_buf() == nullptr) return py::none();
     const size_t cap = static_cast<size_t>(trace_cap());
     const char* b = reinterpret_cast<const char*>(trace_buf());
     return py::make_tuple(py::bytes(b, cap * 32), py::bytes(b + cap * 32, cap * 32),
-                          py::bytes(reinterpret_cast<const char*>(post_ns().data()), cap * 8));
+                          py::bytes(reinterpret_cast<const char*>(post_ns().data()), cap * 8),
+                          py::bytes(b + cap * 64, cap * 32));
   }
 
   py::dict info() const {

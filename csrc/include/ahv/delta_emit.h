@@ -16,8 +16,6 @@
 // quotes) by the host interner (agent_hypervisor_amd/utils/interner.py).
 #pragma once
 
-#include <type_traits>
-
 #include "ahv/canon_json.h"
 #include "ahv/sha256.h"
 
@@ -74,7 +72,6 @@ AHV_HD uint32_t iso_utc(int64_t us, uint8_t* out) {
 // ---------------------------------------------------------------- host sink
 
 struct HostSink {
-  static constexpr bool kPairNodes = true;  // (host: node2 is two nodes; exercises the paired level loop)
   Sha256Stream h;
   uint32_t scratch[8][8];
   AHV_HD bool seg(uint32_t) { return true; }
@@ -120,11 +117,6 @@ struct HostSink {
     merkle_node(l, r, t);
     for (int k = 0; k < 8; ++k) out[k] = t[k];
   }
-  AHV_HD void node2(const uint32_t l0[8], const uint32_t r0[8], uint32_t o0[8], const uint32_t l1[8],
-                    const uint32_t r1[8], uint32_t o1[8]) const {
-    node(l0, r0, o0);
-    node(l1, r1, o1);
-  }
 };
 
 // Merkle root of `n` leaves read by `leaf(i, out)`, with the reference's level-wise
@@ -163,13 +155,6 @@ AHV_HD void merkle_root_counter(Sink& s, uint32_t n, Leaf&& leaf, uint32_t root[
   }
 }
 
-// Sinks that declare `static constexpr bool kPairNodes = true` (and node2) get
-// their interior nodes hashed two at a time.
-template <class S, class = void>
-struct PairNodes : std::false_type {};
-template <class S>
-struct PairNodes<S, std::void_t<decltype(S::kPairNodes)>> : std::integral_constant<bool, S::kPairNodes> {};
-
 // Level-wise Merkle root of `n` leaves read by `leaf(i, out)` (reference
 // audit/delta.py:117-134: odd node duplicated), with every interior node hashed
 // at ONE call site: level 1 reads the leaves, later levels work in place on the
@@ -183,39 +168,21 @@ AHV_HD void merkle_root_levels(Sink& s, uint32_t n, Leaf&& leaf, uint32_t root[8
   }
   uint32_t m = n;
   bool from_leaves = true;
-  auto get = [&](bool lv, uint32_t i, uint32_t d[8]) {
-    if (lv) leaf(i, d);
-    else s.load(static_cast<int>(i), d);
-  };
   while (m > 1) {
     const uint32_t half = (m + 1) >> 1;
-    // sinks with kPairNodes: nodes in pairs (sink.node2: two compressions
-    // interleaved), the odd one alone; node j overwrites slot j only after nodes
-    // 2j, 2j+1 — and a pair's four children (slots ≥ 2j) — were read
-    uint32_t j0 = 0;
-    if constexpr (PairNodes<Sink>::value) {
 #pragma nounroll
-    for (uint32_t j = 0; j + 1 < half; j += 2) {
-      const uint32_t ri = 2 * j + 3 < m ? 2 * j + 3 : 2 * j + 2;
-      uint32_t l0[8], r0[8], l1[8], r1[8];
-      get(from_leaves, 2 * j, l0);
-      get(from_leaves, 2 * j + 1, r0);
-      get(from_leaves, 2 * j + 2, l1);
-      get(from_leaves, ri, r1);
-      s.node2(l0, r0, l0, l1, r1, l1);
-      s.stash(static_cast<int>(j), l0);
-      s.stash(static_cast<int>(j + 1), l1);
-    }
-    j0 = half & ~1u;
-    }
-#pragma nounroll
-    for (uint32_t j = j0; j < half; ++j) {
+    for (uint32_t j = 0; j < half; ++j) {
       const uint32_t ri = 2 * j + 1 < m ? 2 * j + 1 : 2 * j;
-      uint32_t l[8], r[8];
-      get(from_leaves, 2 * j, l);
-      get(from_leaves, ri, r);
-      s.node(l, r, l);
-      s.stash(static_cast<int>(j), l);
+      uint32_t l[8], r[8], o[8];
+      if (from_leaves) {
+        leaf(2 * j, l);
+        leaf(ri, r);
+      } else {
+        s.load(static_cast<int>(2 * j), l);
+        s.load(static_cast<int>(ri), r);
+      }
+      s.node(l, r, o);
+      s.stash(static_cast<int>(j), o);
     }
     m = half;
     from_leaves = false;

@@ -105,47 +105,6 @@ AHV_HD void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// Two independent compressions in one instruction stream (ILP 2): each round
-// of message A and message B is issued back to back, so a wave whose rounds
-// wait on their own dependency chain (Σ → add3 → add) has the other message's
-// independent instructions to issue in between.
-AHV_HD void sha256_compress2(uint32_t sa[8], const uint32_t ba[16], uint32_t sb[8], const uint32_t bb[16]) {
-  uint32_t wa[16], wb[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    wa[i] = ba[i];
-    wb[i] = bb[i];
-  }
-  uint32_t a0 = sa[0], b0 = sa[1], c0 = sa[2], d0 = sa[3], e0 = sa[4], f0 = sa[5], g0 = sa[6], h0 = sa[7];
-  uint32_t a1 = sb[0], b1 = sb[1], c1 = sb[2], d1 = sb[3], e1 = sb[4], f1 = sb[5], g1 = sb[6], h1 = sb[7];
-#pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    uint32_t xa, xb;
-    if (i < 16) {
-      xa = wa[i];
-      xb = wb[i];
-    } else {
-      const uint32_t pa = wa[(i + 1) & 15], qa = wa[(i + 14) & 15];
-      const uint32_t pb = wb[(i + 1) & 15], qb = wb[(i + 14) & 15];
-      xa = wa[i & 15] + xor3(rotr32(pa, 7), rotr32(pa, 18), pa >> 3) + wa[(i + 9) & 15] +
-           xor3(rotr32(qa, 17), rotr32(qa, 19), qa >> 10);
-      xb = wb[i & 15] + xor3(rotr32(pb, 7), rotr32(pb, 18), pb >> 3) + wb[(i + 9) & 15] +
-           xor3(rotr32(qb, 17), rotr32(qb, 19), qb >> 10);
-      wa[i & 15] = xa;
-      wb[i & 15] = xb;
-    }
-    const uint32_t k = sha256_k(i);
-    const uint32_t t1a = h0 + xor3(rotr32(e0, 6), rotr32(e0, 11), rotr32(e0, 25)) + sha_ch(e0, f0, g0) + k + xa;
-    const uint32_t t1b = h1 + xor3(rotr32(e1, 6), rotr32(e1, 11), rotr32(e1, 25)) + sha_ch(e1, f1, g1) + k + xb;
-    const uint32_t t2a = xor3(rotr32(a0, 2), rotr32(a0, 13), rotr32(a0, 22)) + sha_maj(a0, b0, c0);
-    const uint32_t t2b = xor3(rotr32(a1, 2), rotr32(a1, 13), rotr32(a1, 22)) + sha_maj(a1, b1, c1);
-    h0 = g0; g0 = f0; f0 = e0; e0 = d0 + t1a; d0 = c0; c0 = b0; b0 = a0; a0 = t1a + t2a;
-    h1 = g1; g1 = f1; f1 = e1; e1 = d1 + t1b; d1 = c1; c1 = b1; b1 = a1; a1 = t1b + t2b;
-  }
-  sa[0] += a0; sa[1] += b0; sa[2] += c0; sa[3] += d0; sa[4] += e0; sa[5] += f0; sa[6] += g0; sa[7] += h0;
-  sb[0] += a1; sb[1] += b1; sb[2] += c1; sb[3] += d1; sb[4] += e1; sb[5] += f1; sb[6] += g1; sb[7] += h1;
-}
-
 // Final padding block for a message whose length is an exact multiple of 64
 // bytes: 0x80 then zeros then the 64-bit bit length.  All words are constants
 // for a constant `total_bytes`, so the schedule folds away.
@@ -205,33 +164,6 @@ AHV_HD void merkle_node(const uint32_t left[8], const uint32_t right[8], uint32_
   digest_to_hex_words(right, blk);
   sha256_compress(out, blk);
   sha256_compress_pad_only(out, 128u);
-}
-
-// Two Merkle nodes at once (ILP 2; see sha256_compress2): o0 = node(l0, r0),
-// o1 = node(l1, r1).  Outputs may alias inputs.
-AHV_HD void merkle_node2(const uint32_t l0[8], const uint32_t r0[8], uint32_t o0[8], const uint32_t l1[8],
-                         const uint32_t r1[8], uint32_t o1[8]) {
-  uint32_t s0[8], s1[8], b0[16], b1[16];
-  sha256_init(s0);
-  sha256_init(s1);
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma nounroll
-#endif
-  for (int blk = 0; blk < 2; ++blk) {  // one loop body for both data blocks (code size)
-    digest_to_hex_words(blk ? r0 : l0, b0);
-    digest_to_hex_words(blk ? r1 : l1, b1);
-    sha256_compress2(s0, b0, s1, b1);
-  }
-  b0[0] = 0x80000000u;
-#pragma unroll
-  for (int i = 1; i < 15; ++i) b0[i] = 0u;
-  b0[15] = 1024u;  // 128 bytes
-  sha256_compress2(s0, b0, s1, b0);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    o0[k] = s0[k];
-    o1[k] = s1[k];
-  }
 }
 
 // Byte-oriented streaming hasher (host and device).  Used where messages are

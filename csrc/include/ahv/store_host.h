@@ -174,16 +174,11 @@ class StoreCore {
       hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "store stream");
       idle_ticks_ = static_cast<uint64_t>(idle_us) * 100;  // s_memrealtime: 100 MHz
       // worker feature bits: 1 = provisional Merkle roots on the idle hash engine,
-      // 2 = capture prefix midstates on the command wave,
+      // 2 = capture prefix midstates on the prefix wave (wave 2),
       const char* sp = std::getenv("AHV_STORE_SPECULATE");
       const char* pf = std::getenv("AHV_STORE_PREFIX");
       // 4 = batched hashing: queued captures of distinct sessions hashed one per lane
       const char* bt = std::getenv("AHV_STORE_BATCH");
-      // 8 = compute the capture prefix even when the next command is already waiting (off by
-      //     default: it shortens the engine's later captures but the command wave's SHA work
-      //     slows the engine's current one — both waves issue on one CU; p50 measured equal or
-      //     slightly worse, profiles/r3/prefix_always_ab_r3aj.*)
-      const char* pw = std::getenv("AHV_STORE_PREFIX_ALWAYS");
       // 16 = FREE_ROWS waits only for the queued captures of the rows it frees (S, D) or
       //      not at all (G, T, E, V), instead of draining the hash engine
       const char* nf = std::getenv("AHV_STORE_NARROW_FREE");
@@ -193,7 +188,7 @@ class StoreCore {
       // 64 = prefetch the next command slot while the current command executes
       const char* pf2 = std::getenv("AHV_STORE_SLOT_PREFETCH");
       speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
-                   ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) | ((pw != nullptr && std::atoi(pw) != 0) ? 8 : 0) |
+                   ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) |
                    ((nf == nullptr || std::atoi(nf) != 0) ? 16 : 0) |
                    ((lp == nullptr || std::atoi(lp) != 0) ? 32 : 0) |
                    ((pf2 == nullptr || std::atoi(pf2) != 0) ? 64 : 0);
@@ -202,10 +197,10 @@ class StoreCore {
       const char* tr = std::getenv("AHV_STORE_TRACE");
       if (tr != nullptr && std::atoll(tr) > 0) {
         trace_cap_ = std::atoll(tr);
-        hip_check(hipHostMalloc(reinterpret_cast<void**>(&trace_), static_cast<size_t>(trace_cap_) * 64,
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&trace_), static_cast<size_t>(trace_cap_) * 96,
                                 hipHostMallocCoherent),
                   "store trace");
-        std::memset(trace_, 0, static_cast<size_t>(trace_cap_) * 64);
+        std::memset(trace_, 0, static_cast<size_t>(trace_cap_) * 96);
         post_ns_.assign(static_cast<size_t>(trace_cap_), 0);
       }
     } else {
@@ -987,7 +982,7 @@ class StoreCore {
   uint64_t launches_ = 0;
   uint64_t double_releases_ = 0;  // releases of rows that were not live (ignored)
   std::vector<uint8_t> dreleased_;  // delta rows released and not yet reclaimed
-  uint64_t* trace_ = nullptr;       // worker timeline (AHV_STORE_TRACE): [2·cap][4] words, pinned
+  uint64_t* trace_ = nullptr;       // worker timeline (AHV_STORE_TRACE): [3·cap][4] words, pinned
   int64_t trace_cap_ = 0;
   std::vector<uint64_t> post_ns_;   // host post time of each traced sequence number (steady clock)
   uint64_t reclaims_ = 0;        // reclaim_pool passes that returned queued rows (any table)

@@ -74,50 +74,60 @@ def main() -> None:
     cmd = np.frombuffer(tr[0], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
     eng = np.frombuffer(tr[1], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
     post = np.frombuffer(tr[2], dtype=np.uint64).astype(np.int64)
+    tree = np.frombuffer(tr[3], dtype=np.uint64).reshape(-1, 4).astype(np.int64) if len(tr) > 3 else None
     cap = len(post)
     ok = cmd[:, 0] > 0
     seqs = cmd[ok, 0] - 1
     # clock alignment: device ticks are 10 ns; offset so that the fastest pickup has transit 0
     off = np.min(cmd[ok, 2] * 10 - post[seqs % cap])
-    rows = {}
+    us = lambda ticks, base: (ticks * 10 - off - base) / 1e3  # noqa: E731
+    per = []  # per pipeline: list of per-command dicts
     for m in marks:
         base = None
-        for k, q in enumerate(range(m["q0"], m["q1"])):
+        rows_m = []
+        for q in range(m["q0"], m["q1"]):
             c = cmd[q % cap]
             if c[0] != q + 1:
                 continue
             pt = post[q % cap]
             if base is None:
                 base = pt
+            f = int(c[1])
+            r = {"op": f & 0xFFFFFFFF, "post": (pt - base) / 1e3, "seen": us(c[2], base), "done": us(c[3], base),
+                 "cmd_prefix_blocks": f >> 32 & 0xFF, "waited": (f >> 40 & 0xFFFFFF) / 100}
             e = eng[q % cap]
-            r = rows.setdefault(k, {"op": int(c[1]) & 0xFFFFFFFF, "post": [], "seen": [], "done": [], "eng0": [],
-                                    "eng1": [], "blocks": [], "prefix": [], "skip": [], "batch": [], "stage": [],
-                                    "hash": []})
-            r["prefix"].append(int(c[1]) >> 32 & 0xFF)
-            r["post"].append((pt - base) / 1e3)
-            r["seen"].append((c[2] * 10 - off - base) / 1e3)
-            r["done"].append((c[3] * 10 - off - base) / 1e3)
             if e[0] == q + 1:
-                r["eng0"].append((e[2] * 10 - off - base) / 1e3)
-                r["eng1"].append((e[3] * 10 - off - base) / 1e3)
-                f = int(e[1])
-                r["blocks"].append(f & 0xFF)
-                r["skip"].append(f >> 8 & 0xFF)
-                r["batch"].append(f >> 16 & 0xFF)
-                r["stage"].append((f >> 24 & 0xFFFFF) / 100)  # 10 ns ticks → µs
-                r["hash"].append((f >> 44 & 0xFFFFF) / 100)
+                g = int(e[1])
+                r.update(engine_start=us(e[2], base), engine_end=us(e[3], base), blocks=g & 0xFF, skip=g >> 8 & 0xFF,
+                         batch=g >> 16 & 0xFF, stage_us=(g >> 24 & 0xFFFFF) / 100, hash_us=(g >> 44 & 0xFFFFF) / 100)
+            if tree is not None and tree[q % cap][0] == q + 1:
+                t = tree[q % cap]
+                r.update(tree_start=us(t[2], base), tree_end=us(t[3], base), tree_leaves=int(t[1]) & 0xFF,
+                         tree_done=int(t[1]) >> 8 & 1, tree_cached=int(t[1]) >> 9 & 1)
+            rows_m.append(r)
         m["term_host"] = (m["t_term"] - m["t0"]) / 1e3
+        per.append(rows_m)
+    from collections import Counter
+
     from agent_hypervisor_amd.models.store import OPS
 
     name = {v: k for k, v in OPS.items()}
+    # pipelines interleave with the previous hypervisor's teardown commands: aggregate the
+    # pipelines whose command sequence is the most common one
+    sig = Counter(tuple(r["op"] for r in rm) for rm in per).most_common(1)[0][0]
+    keep = [rm for rm in per if tuple(r["op"] for r in rm) == sig]
     med = lambda xs: round(statistics.median(xs), 2) if xs else None  # noqa: E731
     out = []
-    for k in sorted(rows):
-        r = rows[k]
-        out.append({"k": k, "op": name.get(r["op"], r["op"]), "post": med(r["post"]), "seen": med(r["seen"]),
-                    "done": med(r["done"]), "engine_start": med(r["eng0"]), "engine_end": med(r["eng1"]),
-                    "blocks": med(r["blocks"]), "cmd_prefix_blocks": med(r["prefix"]), "skip": med(r["skip"]),
-                    "batch": med(r["batch"]), "stage_us": med(r["stage"]), "hash_us": med(r["hash"])})
+    for k, op in enumerate(sig):
+        o = {"k": k, "op": name.get(op, op)}
+        for f in ("post", "seen", "waited", "done", "cmd_prefix_blocks", "engine_start", "stage_us", "hash_us",
+                  "engine_end", "blocks", "skip", "batch", "tree_start", "tree_end", "tree_leaves", "tree_done",
+                  "tree_cached"):
+            v = [rm[k][f] for rm in keep if f in rm[k]]
+            if v:
+                o[f] = med(v)
+        out.append(o)
+    print(json.dumps({"pipelines_with_this_sequence": len(keep), "of": len(per)}))
     lat = [(m["t_end"] - m["t0"]) / 1e3 for m in marks]
     print(json.dumps({"device": dev, "iters": iters, "p50_us": med(lat),
                       "terminate_called_us": med([m["term_host"] for m in marks]),
