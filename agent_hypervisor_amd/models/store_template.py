@@ -23,6 +23,7 @@ Two ways in:
 
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -133,6 +134,19 @@ class TemplatePipeline:
             "changes": torch.tensor(rows or [[0, 0, 0, 0]], dtype=torch.int32).to(dev),
             "status": torch.zeros(n, dtype=torch.int32, device=dev),
         }
+        # each delta's changes fragment (`, "changes": [...], ..., "parent_hash": `) is the
+        # same for every session: rendered once here, copied by the kernel through the
+        # scalar cache (AHV_TEMPLATE_FRAG=0: rendered per session and pass from the pool)
+        if deltas and os.environ.get("AHV_TEMPLATE_FRAG", "1") != "0":
+            words, offs, lens = [], [], []
+            for d in range(deltas):
+                b = C.render_fragment(pool._pool, rows[d * nch:(d + 1) * nch], d + 1, d > 0)
+                offs.append(sum(len(x) for x in words))
+                lens.append(len(b))
+                words.append(np.frombuffer(b + b"\0" * (-len(b) % 4), dtype=">u4").astype(np.uint32))
+            self.tens["frag"] = T(np.concatenate(words).view(np.int32))
+            self.tens["frag_off"] = T(np.asarray(offs, dtype=np.int32))
+            self.tens["frag_len"] = T(np.asarray(lens, dtype=np.int32))
         self._slots64 = {k: self.tens[k].to(torch.int64) for k in ("slot", "gslot", "tslot")}
         self.seed = int(seed if seed is not None else st.seed) & ((1 << 63) - 1)
         self._own_seed = seed is not None
@@ -190,6 +204,9 @@ class TemplatePipeline:
             "gc_retention_us": self.gc_retention_us, "status": tens["status"].data_ptr(),
             "stats": self._spread.begin().data_ptr() if stats is not None else None,
         }
+        if "frag" in tens:
+            args.update(frag=tens["frag"].data_ptr(), frag_off=tens["frag_off"].data_ptr(),
+                        frag_len=tens["frag_len"].data_ptr())
         if variant is not None:
             args["waves"], args["small"] = int(variant[0]), int(variant[1])
         cuda = dev.type == "cuda"

@@ -199,6 +199,11 @@ TemplateArgs template_args(const store::Tables& t, const py::dict& d) {
   a.agent_pool = P<const int32_t>(d, "agent_pool");
   a.agent_sigma = P<const double>(d, "agent_sigma");
   a.changes = P<const ChangeIds>(d, "changes");
+  if (d.contains("frag") && !d["frag"].is_none()) {
+    a.frag = P<const uint32_t>(d, "frag");
+    a.frag_off = P<const int32_t>(d, "frag_off");
+    a.frag_len = P<const int32_t>(d, "frag_len");
+  }
   a.pool = StrPool{P<const uint8_t>(d, "pool_bytes"), P<const int64_t>(d, "pool_off"), P<const int32_t>(d, "pool_len")};
   a.deltas = d["deltas"].cast<int32_t>();
   a.nch = d["nch"].cast<int32_t>();

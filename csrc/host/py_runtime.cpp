@@ -9,6 +9,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -106,6 +107,8 @@ class StringPool {
 
   int32_t esc_len(int32_t id) const { return lengths_[static_cast<size_t>(id)]; }
   size_t size() const { return raw_.size(); }
+  // The pool as the emitters read it (host memory; valid until the next intern).
+  StrPool str_pool() const { return StrPool{bytes_.data(), offsets_.data(), lengths_.data()}; }
   size_t nbytes() const { return bytes_.size(); }
 
   py::bytes escaped(int32_t id) const {
@@ -417,6 +420,24 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
 }
 
 
+// The changes fragment of a template delta (ahv/delta_emit.h emit_changes_fragment)
+// rendered from the pool's escaped strings: `changes` = [[path, op, content_hash,
+// previous_hash], ...] pool ids (-1 = null).  The device copies these bytes.
+static py::bytes render_fragment(const StringPool& pool, const std::vector<std::array<int32_t, 4>>& changes,
+                                 uint32_t turn, bool has_parent) {
+  std::vector<ChangeIds> ch;
+  for (const auto& c : changes) {
+    for (int32_t id : c)
+      if (id >= static_cast<int32_t>(pool.size())) throw py::index_error("string id out of range");
+    ch.push_back(ChangeIds{c[0], c[1], c[2], c[3]});
+  }
+  const StrPool sp = pool.str_pool();
+  std::vector<uint8_t> out;
+  ByteSink sink{&out};
+  emit_changes_fragment(sink, sp, ch.data(), static_cast<uint32_t>(ch.size()), -1, turn, has_parent);
+  return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
+}
+
 // ------------------------------------------------------------------ attribution packing
 // CausalAttributor.attribute_batch: the K21 columns of many failure cases, read
 // natively from their dicts.  Per case the agents are listed in the iteration
@@ -543,6 +564,8 @@ void register_runtime(py::module_& m) {
       },
       py::arg("state"), py::arg("duplicate"), py::arg("active"), py::arg("max_participants"), py::arg("sigma_eff"),
       py::arg("min_sigma"), py::arg("trustworthy"), "(JoinCode, ring) the device join would produce");
+  m.def("render_fragment", &render_fragment, py::arg("pool"), py::arg("changes"), py::arg("turn"),
+        py::arg("has_parent"));
   m.def("pack_specs", &pack_specs, py::arg("specs"), py::arg("agents"), py::arg("pool"), py::arg("cfg_of"),
         py::arg("fixed"), "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py)");
   m.def("iso_from_us", &iso_from_us, "datetime.isoformat() text of an epoch-µs UTC instant");

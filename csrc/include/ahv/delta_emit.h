@@ -16,6 +16,8 @@
 // quotes) by the host interner (agent_hypervisor_amd/utils/interner.py).
 #pragma once
 
+#include <vector>
+
 #include "ahv/canon_json.h"
 #include "ahv/sha256.h"
 
@@ -478,21 +480,14 @@ struct Digest {
 };
 
 // The full canonical payload of one delta.
+// The part of a delta record between the agent DID value and the parent digest:
+// `, "changes": [...], "delta_id": "…", "parent_hash": ` — plus `null` for a
+// record without parent.  It does not depend on the session: a template batch
+// renders it once per delta on the host (render_fragment) and the device copies
+// it (emit_frag) instead of assembling the change objects per session and pass.
 template <class Sink>
-AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const ChangeIds* ch,
-                               uint32_t nch, int32_t delta_id_str, uint32_t turn, bool has_parent,
-                               Digest parent, SessionIdent sid, int64_t ts_us) {
-  // The device sink calls this once per window pass; laundering the per-lane
-  // inputs stops the compiler from hoisting every derived hex word (parent
-  // digest, uuid) out of the pass loop and keeping them all live in VGPRs.
-  // (turn and the timestamp are wave-uniform: their digits live in SGPRs.)
-  s.launder(agent.n);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s.launder(parent.v[k]);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) s.launder(sid.uuid[k]);
-  emit_lit(s, canon::K_OPEN_AGENT);
-  emit_str_ref(s, agent);
+AHV_HD void emit_changes_fragment(Sink& s, const StrPool& pool, const ChangeIds* ch, uint32_t nch,
+                                  int32_t delta_id_str, uint32_t turn, bool has_parent) {
   emit_lit(s, canon::K_CHANGES);
   for (uint32_t c = 0; c < nch; ++c) {
     if (c) emit_lit(s, canon::K_CH_SEP);
@@ -515,8 +510,51 @@ AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const
     emit_char(s, 0x22u);
   }
   emit_lit(s, canon::K_PARENT);
+  if (!has_parent) emit_lit(s, canon::K_NULL);
+}
+
+// A pre-rendered fragment: `n` bytes as big-endian words (first byte in the top
+// byte).  Its address and length are the same for every lane of the batch, so on
+// the device the words come through the scalar cache (constant address space:
+// s_load, no per-lane vector load and no dependent string-pool lookups).
+AHV_HD uint32_t frag_word(const uint32_t* w, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) uint32_t* cword;  // NOLINT: address-space cast
+  return ((cword)w)[k];
+#else
+  return w[k];
+#endif
+}
+
+template <class Sink>
+AHV_HD void emit_frag(Sink& s, const uint32_t* w, uint32_t n) {
+  if (!s.seg(n)) return;
+  const uint32_t full = n >> 2;
+  for (uint32_t k = 0; k < full; ++k) s.put4(frag_word(w, k));
+  if (n & 3u) s.put(frag_word(w, full), n & 3u);
+}
+
+// Canonical JSON payload of one delta (reference audit/delta.py:41-64).  With
+// `frag` (n `frag_n` bytes) the changes fragment is copied instead of rendered.
+template <class Sink>
+AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const ChangeIds* ch,
+                               uint32_t nch, int32_t delta_id_str, uint32_t turn, bool has_parent,
+                               Digest parent, SessionIdent sid, int64_t ts_us, const uint32_t* frag = nullptr,
+                               uint32_t frag_n = 0) {
+  // The device sink calls this once per window pass; laundering the per-lane
+  // inputs stops the compiler from hoisting every derived hex word (parent
+  // digest, uuid) out of the pass loop and keeping them all live in VGPRs.
+  // (turn and the timestamp are wave-uniform: their digits live in SGPRs.)
+  s.launder(agent.n);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s.launder(parent.v[k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s.launder(sid.uuid[k]);
+  emit_lit(s, canon::K_OPEN_AGENT);
+  emit_str_ref(s, agent);
+  if (frag) emit_frag(s, frag, frag_n);
+  else emit_changes_fragment(s, pool, ch, nch, delta_id_str, turn, has_parent);
   if (has_parent) emit_hex_digest_quoted(s, parent.v);
-  else emit_lit(s, canon::K_NULL);
   emit_lit(s, canon::K_SESSION);
   if (sid.str_id >= 0) emit_pool_str(s, pool, sid.str_id);
   else emit_session_uuid_quoted(s, sid.uuid);
@@ -526,6 +564,21 @@ AHV_HD void emit_delta_payload(Sink& s, const StrPool& pool, StrRef agent, const
   emit_uint(s, turn);
   emit_lit(s, canon::K_CLOSE);
 }
+
+// Byte collector (host): what an emitter produces, as bytes.
+struct ByteSink {
+  std::vector<uint8_t>* out;
+  bool seg(uint32_t) { return true; }
+  void put4(uint32_t v) {
+    for (int j = 0; j < 4; ++j) out->push_back(static_cast<uint8_t>(v >> (24 - 8 * j)));
+  }
+  void put(uint32_t v, uint32_t n) {
+    for (uint32_t j = 0; j < n; ++j) out->push_back(static_cast<uint8_t>(v >> (24 - 8 * j)));
+  }
+  bool any(bool b) const { return b; }
+  template <class T>
+  void launder(T&) const {}
+};
 
 // Midstate reuse across the deltas of one session.  The payload's first 64 bytes
 // are `{"agent_did": "<did>", "changes": [{"content_hash": ` (47 + |did| bytes) or,

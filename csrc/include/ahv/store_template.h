@@ -43,6 +43,11 @@ struct TemplateArgs {
   const int32_t* agent_pool;     // [A] pool id of the agent's DID (rendered)
   const double* agent_sigma;     // [A] σ_raw (= σ_eff: no Nexus adapter in batches)
   const ChangeIds* changes;      // [D·nch] change fields per delta (shared)
+  // Optional pre-rendered changes fragments (emit_changes_fragment, one per delta):
+  // words [frag_off[d], …) holding frag_len[d] bytes, big-endian; null: rendered per pass
+  const uint32_t* frag;
+  const int32_t* frag_off;
+  const int32_t* frag_len;
   StrPool pool;
   int32_t deltas;                // D ≤ kMaxDeltasPipeline
   int32_t nch;                   // changes per delta
@@ -272,11 +277,13 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
     const int64_t tsd = t0 + 1 + d;
     const int mode = !share_block0 ? MID_OFF : (d == 0 ? MID_CAPTURE : MID_RESUME);
     const ChangeIds* ch = a.changes + d * nch;
+    const uint32_t* fw = a.frag ? a.frag + frag_word(reinterpret_cast<const uint32_t*>(a.frag_off), d) : nullptr;
+    const uint32_t fn = a.frag ? frag_word(reinterpret_cast<const uint32_t*>(a.frag_len), d) : 0u;
     uint32_t h[8];
     uint32_t len = 0;
     sink.nohash = (a.ab & 8) != 0;
     sink.hash_record([=](Sink& k) {
-      emit_delta_payload(k, pool, did, ch, nch, -1, turn, d > 0, prev, sid, tsd);
+      emit_delta_payload(k, pool, did, ch, nch, -1, turn, d > 0, prev, sid, tsd, fw, fn);
     }, h, mid, mode, dst, len);
     if (mode == MID_RESUME && dst) {  // block 0 was not re-emitted: it is the first record's
       const uint32_t* src = reinterpret_cast<const uint32_t*>(t.payload + R.doff(a, 0));
