@@ -31,7 +31,11 @@ Also reported (not the headline value):
   ``Hypervisor(device="cuda")`` API, reference harness methodology (2,000
   iterations after warm-up): every state change, ring gate, audit digest,
   Merkle root, bond release and saga transition is executed by the resident
-  gfx950 store worker (hypervisor/_device.py, csrc/hip/store_worker.hip);
+  gfx950 store worker (hypervisor/_device.py, csrc/hip/store_worker.hip), and
+  terminate returns the Merkle root the device computed (awaited);
+* ``device_p50_speculated_us`` — the same with ``AHV_SPEC_TERMINATE=1``: terminate
+  returns the host's SHA-NI prediction of the root at once and the device's
+  committed root is checked afterwards (a divergence poisons the session);
 * ``scalar_p50_us`` — the same harness on the pure host engines (CPU only);
 * ``batch_p50_ms`` — p50 wall time of one synchronised pipeline step;
 * ``api`` — public-API throughput after the timed region (rank 0, 1 GPU runs),
@@ -70,13 +74,18 @@ BASELINE_P50_US = 267.5
 METRIC = "p50 pipeline latency (µs) + session-ops/sec, bench_hypervisor.py at 1/2/4/8 GPU"
 
 
-def scalar_pipeline_p50(iters: int = 2000, device: str = "host") -> tuple[float, float]:
+def scalar_pipeline_p50(iters: int = 2000, device: str = "host", speculate: bool = False) -> tuple[float, float]:
     """Reference-harness timing of the public-API pipeline (bench_hypervisor.py:217-239).
 
     ``device="host"``: pure host engines; ``device="cuda"``: the device-authoritative
-    store (every call is a command to the gfx950 worker)."""
+    store (every call is a command to the gfx950 worker; terminate returns the root
+    the device computed).  ``speculate``: terminate returns the host's prediction of
+    the root at once and the device's answer is checked afterwards."""
     from hypervisor import Hypervisor, SessionConfig
+    from hypervisor import _device as D
     from hypervisor.audit.delta import VFSChange
+
+    D._SPEC_TERMINATE = speculate
 
     async def one():
         hv = Hypervisor(device=device)
@@ -101,7 +110,10 @@ def scalar_pipeline_p50(iters: int = 2000, device: str = "host") -> tuple[float,
             times.append(time.perf_counter_ns() - t0)
         return times
 
-    times = asyncio.run(run())
+    try:
+        times = asyncio.run(run())
+    finally:
+        D._SPEC_TERMINATE = os.environ.get("AHV_SPEC_TERMINATE", "0") != "0"
     return statistics.median(times) / 1000.0, statistics.mean(times) / 1000.0
 
 
@@ -433,11 +445,12 @@ def main() -> None:
         hist[min(31, max(0, int(x * 1e6).bit_length() - 1))] += 1
     hist = reduce_histogram(hist.to(dev)).cpu().tolist()
 
-    scalar_p50 = scalar_mean = device_p50 = device_mean = None
+    scalar_p50 = scalar_mean = device_p50 = device_mean = spec_p50 = spec_mean = None
     if rank == 0 and not args.no_scalar:
         scalar_p50, scalar_mean = scalar_pipeline_p50(args.scalar_iters, "host")
         if dev.type == "cuda":
             device_p50, device_mean = scalar_pipeline_p50(args.scalar_iters, "cuda")
+            spec_p50, spec_mean = scalar_pipeline_p50(args.scalar_iters, "cuda", speculate=True)
 
     api = None
     if rank == 0 and world == 1 and not args.no_api and dev.type == "cuda":  # 1-GPU runs (the N>1 scaling runs skip it)
@@ -480,6 +493,8 @@ def main() -> None:
             "pipeline_launch": "hipgraph" if args.graph else "stream",
             "vs_baseline_note": "batched GPU throughput / single-threaded Python reference rate (not like-for-like)",
             "device_p50_us": round(device_p50, 2) if device_p50 is not None else None,
+            "device_p50_speculated_us": round(spec_p50, 2) if spec_p50 is not None else None,
+            "device_mean_speculated_us": round(spec_mean, 2) if spec_mean is not None else None,
             "device_mean_us": round(device_mean, 2) if device_mean is not None else None,
             "device_vs_baseline_p50": round(BASELINE_P50_US / device_p50, 3) if device_p50 else None,
             "scalar_p50_us": round(scalar_p50, 2) if scalar_p50 is not None else None,

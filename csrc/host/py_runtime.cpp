@@ -255,16 +255,31 @@ static std::string_view utf8_view(PyObject* o, std::string& tmp) {
 
 static std::tuple<int32_t, double, uint8_t> config_row(PyObject* c) {
   static const py::str kMode("consistency_mode"), kMax("max_participants"), kMin("min_sigma_eff"),
-      kAudit("enable_audit");
-  std::string tmp;
+      kAudit("enable_audit"), kValue("value");
+  // ConsistencyMode members are singletons: their mode is resolved once (an Enum's
+  // `.value` is a descriptor call) and remembered by identity
+  static std::unordered_map<PyObject*, bool> members;
   py::object m = getattr_(c, kMode);
-  if (!PyUnicode_Check(m.ptr())) m = getattr_(m.ptr(), py::str("value"));  // a non-str enum: its value
-  const std::string_view mode = utf8_view(m.ptr(), tmp);
-  if (mode != "strong" && mode != "eventual")
-    throw py::value_error("'" + std::string(mode) + "' is not a valid ConsistencyMode");
+  bool strong;
+  auto it = members.find(m.ptr());
+  if (it != members.end()) {
+    strong = it->second;
+  } else {
+    const bool is_str = PyUnicode_Check(m.ptr());
+    py::object v = is_str ? m : getattr_(m.ptr(), kValue);
+    std::string tmp;
+    const std::string_view mode = utf8_view(v.ptr(), tmp);
+    if (mode != "strong" && mode != "eventual")
+      throw py::value_error("'" + std::string(mode) + "' is not a valid ConsistencyMode");
+    strong = mode == "strong";
+    if (!is_str && members.size() < 16) {
+      Py_INCREF(m.ptr());  // kept alive: the cache holds the member by identity
+      members.emplace(m.ptr(), strong);
+    }
+  }
   const int audit = truth(getattr_(c, kAudit).ptr());
   return {static_cast<int32_t>(as_int(getattr_(c, kMax).ptr())), as_double(getattr_(c, kMin).ptr()),
-          static_cast<uint8_t>((audit ? 1 : 0) | (mode == "strong" ? 2 : 0))};
+          static_cast<uint8_t>((audit ? 1 : 0) | (strong ? 2 : 0))};
 }
 
 // Spec packing works straight on the CPython objects: borrowed tuple items, no
@@ -285,9 +300,23 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   ch_rows.reserve(16 * n);
   std::unordered_map<PyObject*, std::tuple<int32_t, double, uint8_t>> cfg_cache;
   std::string tmp;
+  // per call, per pool: str object → id (the same object recurs across specs — agent
+  // DIDs drawn from one list, shared literals — and skips hashing its bytes)
+  struct PtrCache {
+    std::vector<std::pair<PyObject*, int32_t>> slot = std::vector<std::pair<PyObject*, int32_t>>(4096);
+    int32_t* find(PyObject* o) {
+      auto& e = slot[(reinterpret_cast<uintptr_t>(o) >> 4) & 4095];
+      return e.first == o ? &e.second : nullptr;
+    }
+    void put(PyObject* o, int32_t id) { slot[(reinterpret_cast<uintptr_t>(o) >> 4) & 4095] = {o, id}; }
+  } pc_agents, pc_pool;
   auto intern = [&](StringPool& p, PyObject* o) -> int32_t {
+    PtrCache& pc = &p == &pool ? pc_pool : pc_agents;
+    if (int32_t* hit = pc.find(o)) return *hit;
     if (!PyUnicode_Check(o)) throw py::type_error("spec strings must be str");
-    return p.intern(utf8_view(o, tmp));
+    const int32_t id = p.intern(utf8_view(o, tmp));
+    pc.put(o, id);
+    return id;
   };
   auto esc_of = [&](int32_t id) -> int64_t { return id < 0 ? 4 : pool.esc_len(id) + 2; };
   // first occurrence of a spec object: where its rows start in every column

@@ -72,7 +72,10 @@ _SPEC_LIFECYCLE = os.environ.get("AHV_SPEC_LIFECYCLE", "1") != "0"
 # ... and a terminate whose Merkle root the host predicted from its SHA-NI digest
 # predictions (K08/K09 on the host beside the device; the device's own root is what
 # it commits, and it must equal the prediction)
-_SPEC_TERMINATE = os.environ.get("AHV_SPEC_TERMINATE", "1") != "0"
+# terminate awaits the device's Merkle root by default (the store is the authority);
+# AHV_SPEC_TERMINATE=1 returns the host's SHA-NI prediction at once and checks the
+# device's committed root afterwards (a divergence poisons the session)
+_SPEC_TERMINATE = os.environ.get("AHV_SPEC_TERMINATE", "0") != "0"
 # awaited terminates compare the device's root with the host's prediction (AHV_CHECK_TERMINATE=0: off)
 _CHECK_TERMINATE = os.environ.get("AHV_CHECK_TERMINATE", "1") != "0"
 _STEPS = list(StepState)

@@ -299,13 +299,16 @@ def test_refused_create_never_lets_a_speculated_join_touch_the_live_row(dev):
 
 
 @pytest.mark.parametrize("dev", DEVICES)
-def test_terminate_root_is_predicted_and_equals_the_devices(dev):
+def test_terminate_root_is_predicted_and_equals_the_devices(dev, monkeypatch):
     """The terminate of a session whose every delta was captured here is posted
     without waiting: the returned root is the host's SHA-NI prediction over the
     same records, and the device's committed root (K08 + K09 on the store) equals
     it — for chains of 1..9 deltas (odd Merkle levels included)."""
+    from hypervisor import _device as D
     from hypervisor.audit.delta import VFSChange
     from agent_hypervisor_amd import _C
+
+    monkeypatch.setattr(D, "_SPEC_TERMINATE", True)  # (the default awaits the device's root)
 
     async def go():
         hv = Hypervisor(device=dev)
@@ -331,8 +334,11 @@ def test_terminate_root_is_predicted_and_equals_the_devices(dev):
 
 
 @pytest.mark.parametrize("dev", DEVICES)
-def test_a_wrong_root_prediction_poisons_the_session(dev):
+def test_a_wrong_root_prediction_poisons_the_session(dev, monkeypatch):
+    from hypervisor import _device as D
     from hypervisor.audit.delta import VFSChange
+
+    monkeypatch.setattr(D, "_SPEC_TERMINATE", True)
 
     async def go():
         hv = Hypervisor(device=dev)
