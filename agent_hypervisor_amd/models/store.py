@@ -490,7 +490,7 @@ class GovernanceStore:
     # CPU than a short spin when the round trip is a few µs (AHV_STORE_SPIN_BUSY_NS)
     SPIN_BUSY_NS = _env_int("AHV_STORE_SPIN_BUSY_NS", 15_000)
 
-    async def result_async(self, seq: int, nres: int = 4) -> tuple:
+    async def result_async(self, seq: int, nres: int = 4, spin_busy: Optional[int] = None) -> tuple:
         """The results of ``seq`` without blocking the event loop: when other tasks
         are ready (many sessions in flight) the caller suspends at once and a
         loop-driven poller resumes it; otherwise it spins briefly first (a lone
@@ -499,7 +499,7 @@ class GovernanceStore:
 
         loop = asyncio.get_running_loop()
         ready = getattr(loop, "_ready", None)
-        spin = self.SPIN_BUSY_NS if ready else self.SPIN_NS
+        spin = (self.SPIN_BUSY_NS if spin_busy is None else spin_busy) if ready else self.SPIN_NS
         r = self._c.try_result(seq, nres, spin)
         if r is not None:
             return r
@@ -548,9 +548,13 @@ class GovernanceStore:
         else:
             self._polling = False
 
-    async def call_async(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None) -> tuple:
+    async def call_async(self, op: int, args: list, nres: int = 4, inline: Optional[bytes] = None,
+                         spin_busy: Optional[int] = None) -> tuple:
+        """Post and await.  ``spin_busy``: how long to spin for the result while other
+        tasks are ready (default SPIN_BUSY_NS); 0 for commands that wait for the hash
+        engine (a terminate's root), whose answer is tens of µs away."""
         self.verify_deferred()
-        return await self.result_async(self._c.post(op, args, inline), nres)
+        return await self.result_async(self._c.post(op, args, inline), nres, spin_busy)
 
     def drain(self) -> None:
         self._c.drain()

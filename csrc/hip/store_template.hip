@@ -31,7 +31,8 @@ namespace {
 template <int W>
 struct TeeWindowSink : WordWindowSink<W> {
   using B = WordWindowSink<W>;
-  bool nohash = false;  // A/B: emission and tee only
+  bool nohash = false;    // A/B: emission and tee only
+  bool lane_tee = false;  // A/B: per-lane record stores instead of the transposed tee
 
   // Hash the record `emit(*this)` produces (midstate modes as WordWindowSink::
   // hash_mid) and store its bytes at `dst` (memory order); `len` = its length.
@@ -68,13 +69,41 @@ struct TeeWindowSink : WordWindowSink<W> {
       // tee: the record's words in this window → the arena (whole 16-byte chunks up to
       // the record's last word; bytes past `L` are padding inside the reservation)
       const int32_t nw = dst ? static_cast<int32_t>((L + 3u) >> 2) - this->lo : 0;
+      // (the transposed form needs every lane of the wave here: a partial wave — the
+      // grid's tail, lanes whose row was refused — stores per lane)
+      if (lane_tee || __builtin_amdgcn_read_exec() != ~0ull) {  // each lane stores its own record
 #pragma unroll
-      for (int k = 0; k < B::kWinWords; k += 4) {
-        if (k < nw) {
-          const uint32_t* w = this->g_win + k * kWaveLanes + this->lane;
-          *reinterpret_cast<uint4*>(dst + this->lo + k) =
-              make_uint4(bswap_word(w[0]), bswap_word(w[kWaveLanes]), bswap_word(w[2 * kWaveLanes]),
-                         bswap_word(w[3 * kWaveLanes]));
+        for (int k = 0; k < B::kWinWords; k += 4) {
+          if (k < nw) {
+            const uint32_t* w = this->g_win + k * kWaveLanes + this->lane;
+            *reinterpret_cast<uint4*>(dst + this->lo + k) =
+                make_uint4(bswap_word(w[0]), bswap_word(w[kWaveLanes]), bswap_word(w[2 * kWaveLanes]),
+                           bswap_word(w[3 * kWaveLanes]));
+          }
+        }
+      } else {
+        // transposed: lane 4a + b stores 16-byte chunk 4·ln + b (line ln, quarter b) of
+        // record 16·rg + a, so four consecutive lanes fill one 64-byte line of one record
+        // — 16 whole lines per store instead of 64 partial ones
+        constexpr int C = B::kWinWords / 4;  // chunks of a record in the window
+        const uint64_t mine = reinterpret_cast<uint64_t>(dst);
+        const int qa = static_cast<int>(this->lane) >> 2, qb = static_cast<int>(this->lane) & 3;
+#pragma nounroll
+        for (int rg = 0; rg < kWaveLanes / 16; ++rg) {
+          const int r = 16 * rg + qa;
+          const int32_t nwr = __shfl(nw, r);
+          const int32_t lor = __shfl(this->lo, r);  // per lane: 16 for a record resumed from the midstate
+          const uint64_t dr = __shfl(mine, r);
+#pragma nounroll
+          for (int ln = 0; ln < C / 4; ++ln) {
+            const int q = 4 * ln + qb;
+            if (4 * q < nwr) {
+              const uint32_t* w = this->g_win + (4 * q) * kWaveLanes + r;
+              *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(dr) + lor + 4 * q) =
+                  make_uint4(bswap_word(w[0]), bswap_word(w[kWaveLanes]), bswap_word(w[2 * kWaveLanes]),
+                             bswap_word(w[3 * kWaveLanes]));
+            }
+          }
         }
       }
 #pragma nounroll
@@ -108,7 +137,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // A/B switches (AHV_TEMPLATE_AB, measurement only): bit 0 — skip the record tee
 // (digests and rows only); bit 1 — tee into a coarse-grained scratch buffer
 // instead of the store's fine-grained payload arena; bit 2 — no Merkle root;
-// bit 3 — no record compressions (emission + tee only).
+// bit 3 — no record compressions (emission + tee only); bit 6 — per-lane record
+// stores instead of the transposed tee.
 static int template_ab() {
   static const int v = [] {
     const char* e = std::getenv("AHV_TEMPLATE_AB");
@@ -269,7 +299,7 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
   TemplateArgs b = a;
   const int ab = template_ab();
   if (ab & 1) b.notee = 1;
-  b.ab = ab & 12;
+  b.ab = ab & (4 | 8 | 64);
   if (ab & 2) {
     static uint8_t* scratch = nullptr;
     static int64_t scratch_cap = 0;

@@ -62,7 +62,7 @@ struct TemplateArgs {
   int32_t* status;               // [n] out (StorePipeStatus codes), or null
   unsigned long long* stats;     // [kStatSpread·kPipeStats] spread batch counters (X04), or null
   int32_t notee;                 // A/B only: digests without storing the records (AHV_TEMPLATE_AB)
-  int32_t ab;                    // A/B only (measurement, wrong digests): 4 no Merkle root, 8 no record SHA
+  int32_t ab;                    // A/B only: 4 no Merkle root, 8 no record SHA (wrong digests), 64 per-lane tee
   // Ring mode (ring_cap > 0; GovernanceEngine's private store, which owns every row):
   // session i uses row (slot_base + i) % ring_cap for its session / saga / step rows,
   // delta rows row·dstride + d with records at off_base + (row·dstride + d)·rec_bytes,
@@ -129,7 +129,8 @@ AHV_HD uint32_t record_suffix_len(int64_t ts_us, uint32_t turn) {
 // Host twin of the device's record sink: streams the record into SHA-256 and
 // into the arena at once.
 struct HostTeeSink : HostSink {
-  bool nohash = false;  // (device A/B knob; the host twin always hashes)
+  bool nohash = false;    // (device A/B knobs; the host twin always hashes and tees
+  bool lane_tee = false;  //  byte by byte)
   uint8_t* dst = nullptr;
   uint32_t nb = 0;
   AHV_HD void put4(uint32_t v) {
@@ -282,6 +283,7 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
     uint32_t h[8];
     uint32_t len = 0;
     sink.nohash = (a.ab & 8) != 0;
+    sink.lane_tee = (a.ab & 64) != 0;
     sink.hash_record([=](Sink& k) {
       emit_delta_payload(k, pool, did, ch, nch, -1, turn, d > 0, prev, sid, tsd, fw, fn);
     }, h, mid, mode, dst, len);

@@ -55,7 +55,7 @@ struct WordWindowSink {
   uint32_t trash;  // (kWinWords·64 + lane)·4, this lane's trash-row offset
   uint32_t sh;     // 8 × bytes pending (0, 8, 16, 24)
   uint32_t prev;   // the pending bytes, RIGHT-aligned (the tail of the last chunk)
-  int32_t lo;      // window start (word index), wave-uniform
+  int32_t lo;      // window start (word index); per lane: a record resumed from a midstate starts at 16
 
   // Word at LDS byte offset `a` (already relative to the window); anything
   // outside [0, kWinWords) rows — including wrapped negatives — hits the trash row.

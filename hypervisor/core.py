@@ -337,7 +337,7 @@ class Hypervisor:
             st.post_expect(_d._st.OP_SESS_CLOSE, args, _d.close_expect(root, expired), (sso, _d._close_diverged, sso.slot),
                            inl)
             return self._terminated(session_id, sso, de, root, expired, n)
-        r = await st.call_async(_d._st.OP_SESS_CLOSE, args, 13, inl)
+        r = await st.call_async(_d._st.OP_SESS_CLOSE, args, 13, inl, spin_busy=0)
         if guard is not None:
             # every post before the close has completed now: a prediction of this
             # session that the device refused is this terminate's error
