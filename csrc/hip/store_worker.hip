@@ -415,7 +415,7 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
     // the slot still holds an older command and reads as zero
     const uint32_t nwr = static_cast<uint32_t>(__shfl(w, 1) >> 32) & 0x7fu;
     const uint64_t v = static_cast<uint32_t>(lane) < (nwr ? nwr : 64u) ? w : 0ull;
-    uint64_t x = (lane == 0 || lane == 2) ? 0ull : v;
+    uint64_t x = (lane == 0 || lane == 2) ? 0ull : slot_mix(v, static_cast<uint64_t>(lane));
     for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
     if (x != __shfl(v, 2)) continue;  // torn read of a slot still being written: poll again
     const uint64_t c_start = __builtin_amdgcn_s_memrealtime();

@@ -37,6 +37,17 @@ namespace ahv {
 namespace store {
 
 constexpr int kSlotWords = 64;
+
+// Command-slot checksum term of word k (w[2] = XOR of slot_mix(w[k], k) over k = 1
+// and k ≥ 3).  Write-combined 32-byte chunks of a slot can reach the device in any
+// order, so the worker may read a slot half new, half from its previous occupant;
+// the checksum rejects that read.  A plain XOR of the words did not: two captures
+// differ in their record length and parent-hole offset by the same amount (the
+// suffix after the hole has a fixed length), and those two word changes cancelled
+// in the XOR about once per few thousand torn reads — the worker then hashed a
+// record with another capture's length and hole.  Each word is multiplied by its
+// own odd constant first, so correlated changes of different words do not cancel.
+AHV_HD uint64_t slot_mix(uint64_t w, uint64_t k) { return w * (0x9E3779B97F4A7C15ull + 2ull * k); }
 constexpr int kArgs = 13;
 constexpr int kInlineWords = 48;  // w[16..63]
 constexpr int kResWords = 64;     // result slot: r[0] seq, r[1] status, r[2..63] values

@@ -350,8 +350,8 @@ class StoreCore {
     w[1] = op | (static_cast<uint64_t>(nw) << 32);
     for (size_t k = 0; k < nargs; ++k) w[3 + k] = args[k];
     if (inl_bytes) std::memcpy(w + 16, inl, inl_bytes);
-    uint64_t x = w[1];
-    for (int k = 3; k < kSlotWords; ++k) x ^= w[k];
+    uint64_t x = slot_mix(w[1], 1);
+    for (int k = 3; k < kSlotWords; ++k) x ^= slot_mix(w[k], static_cast<uint64_t>(k));
     w[2] = x;
     ++posted_;
     if (trace_cap_ > 0)

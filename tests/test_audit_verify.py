@@ -161,7 +161,14 @@ def test_gpu_batched_audit_matches_host_twin():
     cpu = hv.verify_audit(device="cpu", checkpoints=[mgr])
     assert gpu.device.startswith("cuda")
     assert gpu.to_dict() | {"device": ""} == cpu.to_dict() | {"device": ""}
-    assert sorted(gpu.bad_chains) == sorted(_scalar_bad_chains(hv))
+    from hypervisor.audit.delta import canonical_payload
+
+    detail = [(ms[k].sso.session_id, ms[k].sso.session_id in gpu.bad_chains,
+               [d.__dict__.get("_dirty") for d in ms[k].delta_engine.deltas],
+               ms[k].delta_engine.deltas[0].delta_hash,
+               hashlib.sha256(canonical_payload(ms[k].delta_engine.deltas[0])).hexdigest())
+              for k in (3, 77, 150)]
+    assert sorted(gpu.bad_chains) == sorted(_scalar_bad_chains(hv)), detail
     assert len(gpu.bad_files) == 1 and len(gpu.bad_checkpoints) == 1
     h = hashlib.sha256("x".encode()).hexdigest()
     assert h not in {e.content_hash for e in ms[10].sso.vfs.edit_log}
