@@ -270,9 +270,19 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
   for (int k = 0; k < 8; ++k) prev.v[k] = 0;
   const StrPool pool = a.pool;  // captured by value below (not the whole argument block)
   const uint32_t nch = static_cast<uint32_t>(a.nch);
+  // Row / arena loads of delta d+1 are issued before delta d's record stores: a load
+  // waited for behind stores waits for the stores too (vmcnt counts both), so nothing
+  // is loaded after the first record's stores until the block-0 copies at the end.
+  int32_t dr_next = D > 0 ? static_cast<int32_t>(R.drow(a, 0)) : -1;  // delta rows fit int32 (cap.D)
+  int64_t off_next = D > 0 ? R.doff(a, 0) : 0;
+  int32_t dr_prev = -1;
   for (int32_t d = 0; d < D; ++d) {
-    const int64_t dr = R.drow(a, d);
-    const int64_t off = R.doff(a, d);
+    const int64_t dr = dr_next;
+    const int64_t off = off_next;
+    if (d + 1 < D) {
+      dr_next = static_cast<int32_t>(R.drow(a, d + 1));
+      off_next = R.doff(a, d + 1);
+    }
     uint32_t* dst = a.notee ? nullptr : reinterpret_cast<uint32_t*>(t.payload + off);
     const uint32_t turn = static_cast<uint32_t>(d + 1);
     const int64_t tsd = t0 + 1 + d;
@@ -287,18 +297,9 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
     sink.hash_record([=](Sink& k) {
       emit_delta_payload(k, pool, did, ch, nch, -1, turn, d > 0, prev, sid, tsd, fw, fn);
     }, h, mid, mode, dst, len);
-    if (mode == MID_RESUME && dst) {  // block 0 was not re-emitted: it is the first record's
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(t.payload + R.doff(a, 0));
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(dst)[q] = reinterpret_cast<const uint4*>(src)[q];
-#else
-      for (int q = 0; q < 16; ++q) dst[q] = src[q];
-#endif
-    }
     t.d_sess[dr] = static_cast<int32_t>(s);
     t.d_turn[dr] = static_cast<int32_t>(turn);
-    t.d_prev[dr] = d > 0 ? static_cast<int32_t>(R.drow(a, d - 1)) : -1;
+    t.d_prev[dr] = dr_prev;
     t.d_ts[dr] = tsd;
     t.d_off[dr] = off;
     t.d_len[dr] = static_cast<int32_t>(len);
@@ -308,6 +309,29 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
       t.d_hash[8 * dr + k] = h[k];
       prev.v[k] = h[k];
     }
+    dr_prev = static_cast<int32_t>(dr);
+  }
+  // Records resumed from the midstate did not re-emit block 0: it is the first
+  // record's, copied once all the stores are out (one wait, shared with the Merkle
+  // leaves' reads below).
+  if (share_block0 && !a.notee && D > 1) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(t.payload + R.doff(a, 0));
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    const uint4 c0 = s4[0], c1 = s4[1], c2 = s4[2], c3 = s4[3];  // named: no scratch array
+    for (int32_t d = 1; d < D; ++d) {
+      uint4* dst = reinterpret_cast<uint4*>(t.payload + R.doff(a, d));
+      dst[0] = c0;
+      dst[1] = c1;
+      dst[2] = c2;
+      dst[3] = c3;
+    }
+#else
+    for (int32_t d = 1; d < D; ++d) {
+      uint32_t* dst = reinterpret_cast<uint32_t*>(t.payload + R.doff(a, d));
+      for (int q = 0; q < 16; ++q) dst[q] = src[q];
+    }
+#endif
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) t.s_head[8 * s + k] = prev.v[k];
