@@ -201,15 +201,26 @@ static py::bytes as_bytes(const std::vector<T>& v) {
 
 // Borrowed items of a list / tuple (any other sequence is converted once).
 struct FastSeq {
-  PyObject* o;
+  PyObject* o;    // a new reference when the argument had to be converted, else null
   PyObject** it;
   Py_ssize_t n;
-  explicit FastSeq(PyObject* x) : o(PySequence_Fast(x, "expected a sequence")) {
+  explicit FastSeq(PyObject* x) : o(nullptr) {
+    if (PyTuple_CheckExact(x)) {  // the common case: items borrowed in place, no reference taken
+      it = reinterpret_cast<PyTupleObject*>(x)->ob_item;
+      n = PyTuple_GET_SIZE(x);
+      return;
+    }
+    if (PyList_CheckExact(x)) {
+      it = reinterpret_cast<PyListObject*>(x)->ob_item;
+      n = PyList_GET_SIZE(x);
+      return;
+    }
+    o = PySequence_Fast(x, "expected a sequence");
     if (o == nullptr) throw py::error_already_set();
     it = PySequence_Fast_ITEMS(o);
     n = PySequence_Fast_GET_SIZE(o);
   }
-  ~FastSeq() { Py_DECREF(o); }
+  ~FastSeq() { Py_XDECREF(o); }
   FastSeq(const FastSeq&) = delete;
   FastSeq& operator=(const FastSeq&) = delete;
   PyObject* operator[](Py_ssize_t i) const {
@@ -218,19 +229,62 @@ struct FastSeq {
   }
 };
 
+// Pointer-keyed open-addressing table (no allocation per insert: batches of
+// distinct spec / config objects insert one entry each).
+template <class V>
+struct PtrTable {
+  std::vector<PyObject*> key;
+  std::vector<V> val;
+  size_t mask = 0, used = 0;
+  explicit PtrTable(size_t want) {
+    size_t c = 16;
+    while (c < 2 * want) c <<= 1;
+    key.assign(c, nullptr);
+    val.resize(c);
+    mask = c - 1;
+  }
+  static size_t h(PyObject* o) { return (reinterpret_cast<uintptr_t>(o) >> 4) * 0x9E3779B97F4A7C15ull >> 17; }
+  V* find(PyObject* o) {
+    for (size_t i = h(o) & mask;; i = (i + 1) & mask) {
+      if (key[i] == o) return &val[i];
+      if (key[i] == nullptr) return nullptr;
+    }
+  }
+  bool full() const { return 2 * (used + 1) > key.size(); }
+  V* insert(PyObject* o, const V& v) {  // caller checks full() first
+    size_t i = h(o) & mask;
+    while (key[i] != nullptr && key[i] != o) i = (i + 1) & mask;
+    if (key[i] == nullptr) ++used;
+    key[i] = o;
+    val[i] = v;
+    return &val[i];
+  }
+};
+
+// Attribute of a spec / config object: straight from the instance __dict__ when the
+// name is there (dataclass fields), else the full attribute protocol.
 static py::object getattr_(PyObject* o, const py::str& name) {
+  PyObject** dp = _PyObject_GetDictPtr(o);
+  if (dp != nullptr && *dp != nullptr) {
+    PyObject* v = PyDict_GetItemWithError(*dp, name.ptr());  // borrowed
+    if (v != nullptr) return py::reinterpret_borrow<py::object>(v);
+    if (PyErr_Occurred()) throw py::error_already_set();
+  }
   PyObject* r = PyObject_GetAttr(o, name.ptr());
   if (r == nullptr) throw py::error_already_set();
   return py::reinterpret_steal<py::object>(r);
 }
 
 static int truth(PyObject* o) {
+  if (o == Py_True) return 1;
+  if (o == Py_False || o == Py_None) return 0;
   const int v = PyObject_IsTrue(o);
   if (v < 0) throw py::error_already_set();
   return v;
 }
 
 static double as_double(PyObject* o) {
+  if (PyFloat_CheckExact(o)) return PyFloat_AS_DOUBLE(o);
   const double v = PyFloat_AsDouble(o);
   if (v == -1.0 && PyErr_Occurred()) throw py::error_already_set();
   return v;
@@ -298,7 +352,7 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   d_pool.reserve(2 * n);
   base_caps.reserve(2 * n);
   ch_rows.reserve(16 * n);
-  std::unordered_map<PyObject*, std::tuple<int32_t, double, uint8_t>> cfg_cache;
+  PtrTable<std::tuple<int32_t, double, uint8_t>> cfg_cache(std::min<size_t>(n, 65536) + 1);
   std::string tmp;
   // per call, per pool: str object → id (the same object recurs across specs — agent
   // DIDs drawn from one list, shared literals — and skips hashing its bytes)
@@ -323,7 +377,7 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   struct First {
     size_t spec, j0, d0, st0;
   };
-  std::unordered_map<PyObject*, First> seen;
+  PtrTable<First> seen(std::min<size_t>(n, 65536));
   static const py::str kJoins("joins"), kDeltas("deltas"), kSteps("steps"), kAct("activate"), kTerm("terminate"),
       kComp("compensate"), kCfg("config"), kCreator("creator_did");
   PyObject* const* items = PySequence_Fast_ITEMS(specs.ptr());
@@ -333,10 +387,10 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   };
   for (size_t i = 0; i < n; ++i) {
     PyObject* sp = items[i];
-    if (seen.size() < 65536) {  // (bounded: a batch of all-distinct specs gains nothing from the map)
-      auto hit = seen.find(sp);
-      if (hit != seen.end()) {
-        const First& f = hit->second;
+    if (!seen.full()) {  // (bounded: a batch of all-distinct specs gains nothing from the table)
+      const First* hit = seen.find(sp);
+      if (hit != nullptr) {
+        const First& f = *hit;
         creator[i] = creator[f.spec];
         maxpart[i] = maxpart[f.spec];
         minsig[i] = minsig[f.spec];
@@ -361,22 +415,24 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
         step_off.push_back(static_cast<int32_t>(s_undo.size()));
         continue;
       }
-      seen.emplace(sp, First{i, join_agent.size(), d_pool.size(), s_undo.size()});
+      seen.insert(sp, First{i, join_agent.size(), d_pool.size(), s_undo.size()});
     }
     py::object cfg = getattr_(sp, kCfg);
-    auto ci = cfg_cache.find(cfg.ptr());
-    if (ci == cfg_cache.end()) {
+    const std::tuple<int32_t, double, uint8_t>* ci = cfg_cache.find(cfg.ptr());
+    std::tuple<int32_t, double, uint8_t> row;
+    if (ci == nullptr) {
       if (cfg.is_none()) {  // the default SessionConfig, resolved by the caller
         py::tuple t = cfg_of(cfg);
-        ci = cfg_cache.emplace(cfg.ptr(), std::make_tuple(t[0].cast<int32_t>(), t[1].cast<double>(),
-                                                          t[2].cast<uint8_t>())).first;
+        row = std::make_tuple(t[0].cast<int32_t>(), t[1].cast<double>(), t[2].cast<uint8_t>());
       } else {
-        ci = cfg_cache.emplace(cfg.ptr(), config_row(cfg.ptr())).first;
+        row = config_row(cfg.ptr());
       }
+      if (!cfg_cache.full()) cfg_cache.insert(cfg.ptr(), row);
+      ci = &row;
     }
-    maxpart[i] = std::get<0>(ci->second);
-    minsig[i] = std::get<1>(ci->second);
-    flags[i] = static_cast<uint8_t>(std::get<2>(ci->second) | (truth(getattr_(sp, kAct).ptr()) ? 4 : 0) |
+    maxpart[i] = std::get<0>(*ci);
+    minsig[i] = std::get<1>(*ci);
+    flags[i] = static_cast<uint8_t>(std::get<2>(*ci) | (truth(getattr_(sp, kAct).ptr()) ? 4 : 0) |
                                     (truth(getattr_(sp, kTerm).ptr()) ? 8 : 0) |
                                     (truth(getattr_(sp, kComp).ptr()) ? 16 : 0));
     creator[i] = intern(agents, getattr_(sp, kCreator).ptr());
