@@ -337,7 +337,18 @@ class Hypervisor:
             st.post_expect(_d._st.OP_SESS_CLOSE, args, _d.close_expect(root, expired), (sso, _d._close_diverged, sso.slot),
                            inl)
             return self._terminated(session_id, sso, de, root, expired, n)
-        r = await st.call_async(_d._st.OP_SESS_CLOSE, args, 13, inl, spin_busy=0)
+        early = check is not None and not (v >= 0)
+        if early:
+            # the host knows the outcome: post the close, do the host bookkeeping that
+            # needs no device answer (GC of the views with the predicted retention count,
+            # the commitment record) while the hash engine finishes the chain, then await
+            # the root; events go out only after the device's answer
+            st.verify_deferred()
+            seq = st._c.post(_d._st.OP_SESS_CLOSE, args, inl)
+            self._terminate_bookkeeping(session_id, sso, de, check[0] is not None and audit, check[1], n)
+            r = await st.result_async(seq, 13, 0)
+        else:
+            r = await st.call_async(_d._st.OP_SESS_CLOSE, args, 13, inl, spin_busy=0)
         if guard is not None:
             # every post before the close has completed now: a prediction of this
             # session that the device refused is this terminate's error
@@ -351,7 +362,16 @@ class Hypervisor:
         root = _d._hex(r[2:10]) if r[1] else None
         if v >= 0:  # every bond of the session is released now: freeze the records, reuse the edge rows
             self.vouching.retire_session(session_id)
-        out = self._terminated(session_id, sso, de, root, int(r[11]), n)
+        if early:
+            self._terminate_events(session_id, root)
+            out = root
+            if int(r[11]) != check[1]:
+                err = _d._st.StoreError(f"device GC count {int(r[11])} of session {session_id} differs from the "
+                                        f"host prediction {check[1]}")
+                sso._poisoned = err
+                raise err
+        else:
+            out = self._terminated(session_id, sso, de, root, int(r[11]), n)
         if check is not None and audit and check[0] != root:
             # the device committed its own root; the host's view of this chain (the
             # digests it rendered and predicted) disagrees with it: the session is
@@ -365,12 +385,20 @@ class Hypervisor:
 
     def _terminated(self, session_id: str, sso, de, root: Optional[str], expired: int, n: int) -> Optional[str]:
         """Host bookkeeping after a device close: commitment, GC, events."""
-        if root:
+        self._terminate_bookkeeping(session_id, sso, de, bool(root), expired, n)
+        self._terminate_events(session_id, root)
+        return root
+
+    def _terminate_bookkeeping(self, session_id: str, sso, de, committed: bool, expired: int, n: int) -> None:
+        """Commitment record and GC of a device close (no device answer needed)."""
+        if committed:
             self.commitment.register(sso)
-        # the device counted the deltas past retention (result word 12); with none
+        # the device counts the deltas past retention (result word 12); with none
         # expired the host GC has nothing to prune and needs no walk over the views
         self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de if expired else None,
                         delta_count=de.turn_count if expired else n)
+
+    def _terminate_events(self, session_id: str, root: Optional[str]) -> None:
         if self.event_bus is not None:
             from hypervisor.observability.event_bus import EventType
 
@@ -379,7 +407,6 @@ class Hypervisor:
                 self._emit(EventType.AUDIT_COMMITTED, session_id, merkle_root=root)
             self._emit(EventType.AUDIT_GC_COLLECTED, session_id)
             self._emit(EventType.SESSION_ARCHIVED, session_id)
-        return root
 
     async def run_pipelines(self, specs, n: Optional[int] = None):
         """Run governance pipelines for many sessions at once on the device store
