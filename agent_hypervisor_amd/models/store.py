@@ -299,7 +299,8 @@ class GovernanceStore:
 
     def release_tenant(self, tenant: int, edges) -> None:
         """A vouching engine is gone: its edge rows and liability-session rows are reclaimable."""
-        self.release_many("E", list(edges))
+        if edges:
+            self.release_many("E", list(edges))
         vs = self._tenant_v.pop(tenant, None)
         if vs:
             self.release_many("V", list(vs.values()))

@@ -417,6 +417,26 @@ static py::object uuid4(const std::string& prefix) {
   return py::reinterpret_steal<py::object>(s);
 }
 
+// uuid4_id(prefix="") -> (prefix + uuid4 string, hi, lo): the uuid's two 64-bit
+// halves as signed int64 (the store's session id words), no re-parse of the string.
+static py::tuple uuid4_id(const std::string& prefix) {
+  uint64_t hi = g_rng.next(), lo = g_rng.next();
+  hi = (hi & 0xffffffffffff0fffull) | 0x0000000000004000ull;
+  lo = (lo & 0x3fffffffffffffffull) | 0x8000000000000000ull;
+  const size_t pl = prefix.size();
+  PyObject* s = PyUnicode_New(static_cast<Py_ssize_t>(pl + 36), 127);
+  if (!s) throw py::error_already_set();
+  char* o = reinterpret_cast<char*>(PyUnicode_1BYTE_DATA(s));
+  std::memcpy(o, prefix.data(), pl);
+  o += pl;
+  put_hex(o, hi >> 32, 8); o[8] = '-';
+  put_hex(o + 9, (hi >> 16) & 0xffff, 4); o[13] = '-';
+  put_hex(o + 14, hi & 0xffff, 4); o[18] = '-';
+  put_hex(o + 19, lo >> 48, 4); o[23] = '-';
+  put_hex(o + 24, lo & 0xffffffffffffull, 12);
+  return py::make_tuple(py::reinterpret_steal<py::object>(s), static_cast<int64_t>(hi), static_cast<int64_t>(lo));
+}
+
 // uuid4_many(n, prefix) -> ([prefix + uuid4] * n, bytes of n×4 native u32 words):
 // the words are the uuid's 32 hex digits as four big-endian 8-digit numbers
 // (the layout of the store's s_uuid rows and of the device renderer).
@@ -572,6 +592,8 @@ void register_audit(py::module_& m) {
         "Merkle root over n digests given as native u32 words (host SHA-NI oracle)");
   m.def("sha256_hex", &sha256_hex, "SHA-256 hex digest of str (UTF-8) or bytes");
   m.def("uuid4", &uuid4, py::arg("prefix") = std::string(), "prefix + random uuid4 string");
+  m.def("uuid4_id", &uuid4_id, py::arg("prefix") = std::string(),
+        "(prefix + random uuid4 string, hi, lo) with the halves as signed int64");
   m.def("hex_id", &hex_id, py::arg("prefix"), py::arg("nchars"), "prefix + random hex digits");
   m.def("uuid4_many", &uuid4_many, py::arg("n"), py::arg("prefix") = std::string(),
         "n uuid4 strings and their 4 u32 words each");

@@ -130,6 +130,19 @@ def _shared_store(mode: str) -> GovernanceStore:
     return st
 
 
+def _id_words(session_id: str, store: GovernanceStore) -> tuple:
+    """(hi, lo) signed id words of a session row: the uuid's halves, or for an id
+    that is not a uuid, 0 and a per-store serial."""
+    u = session_id.rsplit(":", 1)[-1].replace("-", "")
+    try:
+        hi, lo = int(u[:16], 16), int(u[16:32], 16)
+    except ValueError:
+        hi = lo = 0
+    if len(u) != 32 or not lo:  # not a uuid id: a per-store serial stands in for its id words
+        hi, lo = 0, store.next_stamp()
+    return _i64(hi), _i64(lo)
+
+
 def _check(res: tuple, what: str) -> tuple:
     if res[0] in (_st.ST_BAD_ARG, _st.ST_SCRATCH) or res[0] >= 90:
         raise _st.StoreError(f"store command {what} failed with status {res[0]}")
@@ -153,11 +166,14 @@ class DeviceSession(SharedSessionObject):
         create: bool = True,
     ) -> None:
         self._store = store
-        self.session_id = session_id or _C.uuid4("session:")
+        words = None
+        if session_id is None:
+            session_id, hi, lo = _C.uuid4_id("session:")  # the id and its row id words
+            words = (hi, lo)
+        self.session_id = session_id
         self.creator_did = creator_did
         self.config = config
-        self.vfs_namespace = "/sessions/" + self.session_id
-        self.vfs = SessionVFS(self.session_id, namespace=self.vfs_namespace)
+        self.vfs_namespace = "/sessions/" + session_id
         self._vfs_snapshots: dict[str, Any] = {}
         self.slot = store.alloc("S") if slot is None else slot
         self._cseq = -1
@@ -175,29 +191,40 @@ class DeviceSession(SharedSessionObject):
         self._stamp = 0  # creation stamp this object sent (0: not created here)
         self._poisoned: Optional[Exception] = None  # a speculated post of this session the device refused
         if create:
-            u = self.session_id.rsplit(":", 1)[-1].replace("-", "")
-            try:
-                hi, lo = int(u[:16], 16), int(u[16:32], 16)
-            except ValueError:
-                hi = lo = 0
-            if len(u) != 32 or not lo:  # not a uuid id: a per-store serial stands in for its id words
-                hi, lo = 0, store.next_stamp()
+            if words is None:
+                words = _id_words(session_id, store)
+            hi, lo = words
             # the creation stamp later posts carry is the row's id words (row_stamp in
             # store.h), not a clock value: creates in one µs / under a pinned clock differ
-            stamp = lo
             args = [
                 self.slot, store.agent_id(creator_did), _now_us(), _MODE[config.consistency_mode],
                 int(config.max_participants), dbits(config.min_sigma_eff), int(bool(config.enable_audit)),
-                _i64(hi), _i64(lo), 0 if handshake else 1,
+                hi, lo, 0 if handshake else 1,
             ]
-            if self._m_state is not None and stamp:
+            if self._m_state is not None and lo:
                 # posted and verified later: the join / activate that follow carry the stamp,
                 # so a row holding another session (a refused create) refuses them on the device
-                self._stamp = _i64(stamp)
+                self._stamp = lo
                 slot = self.slot
                 store.post_expect(_st.OP_SESS_CREATE, args, _OK, (self, _create_refused, slot))
             else:
                 self._cseq = store.post(_st.OP_SESS_CREATE, args)
+
+    @property
+    def vfs(self) -> SessionVFS:  # type: ignore[override]
+        """The session's VFS, built on first use (most sessions never touch it)."""
+        v = self.__dict__.get("_vfs")
+        if v is None:
+            v = self.__dict__["_vfs"] = SessionVFS(self.session_id, namespace=self.vfs_namespace)
+        return v
+
+    @vfs.setter
+    def vfs(self, v: SessionVFS) -> None:
+        self.__dict__["_vfs"] = v
+
+    def vfs_if_built(self) -> Optional[SessionVFS]:
+        """The VFS if anything has used it, else None (an unused VFS holds no files)."""
+        return self.__dict__.get("_vfs")
 
     def __del__(self) -> None:
         # the row stays allocated while this view (or a delta engine / saga built
@@ -1592,32 +1619,47 @@ class _ClosedStore:
 CLOSED = _ClosedStore()
 
 
-def _close_views(st: GovernanceStore, m) -> None:
+def _close_views(st: GovernanceStore, m, acc: Optional[tuple] = None) -> None:
     """Release the rows of one built device session and detach its views.  Each
     view is handled on its own: in cyclic garbage some of them may already have
-    run their finaliser (which detached them after releasing their row)."""
+    run their finaliser (which detached them after releasing their row).
+    ``acc``: (session, delta, saga, step) row lists the caller releases in one
+    native call per table instead."""
+    own = acc is None
+    if own:
+        acc = ([], [], [], [])
+    s_rows, d_rows, g_rows, t_rows = acc
     sso, de, orch = m.sso, m.delta_engine, m.saga
     if getattr(sso, "_store", None) is st:
-        st.release("S", sso.slot)
+        s_rows.append(sso.slot)
         sso._store = CLOSED
-    if isinstance(de, DeviceDeltaEngine):
+    if type(de) is DeviceDeltaEngine or isinstance(de, DeviceDeltaEngine):
         if de._store is st:
             rows, de._rows = de._rows, []
-            if rows:
-                st.release_many("D", rows)
+            d_rows.extend(rows)
             de._store = CLOSED
         for d in de._deltas:
             d.__dict__["_store"] = CLOSED
-    if isinstance(orch, DeviceSagaOrchestrator):
+    if type(orch) is DeviceSagaOrchestrator or isinstance(orch, DeviceSagaOrchestrator):
         for g in orch._sagas.values():
-            if g.__dict__.get("_store") is st:
-                st.release("G", g.slot)
-                g.__dict__["_store"] = CLOSED
+            gd = g.__dict__
+            if gd.get("_store") is st:
+                g_rows.append(g.slot)
+                gd["_store"] = CLOSED
             for x in g.steps:
-                if x.__dict__.get("_store") is st:
-                    st.release("T", x.slot)
-                    x.__dict__["_store"] = CLOSED
+                xd = x.__dict__
+                if xd.get("_store") is st:
+                    t_rows.append(x.slot)
+                    xd["_store"] = CLOSED
         orch._store = CLOSED
+    if own:
+        _release_acc(st, acc)
+
+
+def _release_acc(st: GovernanceStore, acc: tuple) -> None:
+    for kind, rows in zip("SDGT", acc):
+        if rows:
+            st.release_many(kind, rows)
 
 
 def close_hypervisor(hv) -> int:
@@ -1634,25 +1676,30 @@ def close_hypervisor(hv) -> int:
     # the FREE_ROWS that later reclaims these rows executes after every command posted
     # for them (a divergence of a speculated post goes to its session, now closed).
     n = 0
+    acc = ([], [], [], [])
     for kind, seg in list(hv._sessions.segments()):
         if kind == "own":
             for m in seg:
-                _close_views(st, m)
+                _close_views(st, m, acc)
                 n += 1
             continue
         for m in list(seg.views.values()):
-            _close_views(st, m)
+            _close_views(st, m, acc)
         seg.release(np.arange(len(seg.slots), dtype=np.int64))
         n += len(seg.index)
-    ve = hv.vouching
+    _release_acc(st, acc)
+    ve = hv.__dict__.get("vouching")  # engines never used were never built (Hypervisor.__getattr__)
     if isinstance(ve, DeviceVouchingEngine) and ve._store is st:
         st.release_tenant(ve._tenant, list(ve._by_edge))
         for rec in ve._by_edge.values():
             rec.__dict__["_store"] = CLOSED
         ve._by_edge = {}
         ve._store = CLOSED
-    if isinstance(hv.commitment, DeviceCommitmentEngine):
-        hv.commitment._store = CLOSED
+    elif ve is None:
+        st.release_tenant(hv._tenant, [])
+    cm = hv.__dict__.get("commitment")
+    if isinstance(cm, DeviceCommitmentEngine):
+        cm._store = CLOSED
     hv._store = CLOSED
     return n
 

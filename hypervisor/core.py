@@ -141,9 +141,10 @@ class Hypervisor:
             _device = _device_mod()
             self._store = store if store is not None else _device._shared_store(mode)
             self._tenant = self._store.new_tenant()
-            self.vouching = _device.DeviceVouchingEngine(self._store, self._tenant, max_exposure)
-            self.slashing = _device.DeviceSlashingEngine(self.vouching)
-            self.commitment = _device.DeviceCommitmentEngine(self._store)
+            # the device vouching / slashing / commitment engines are built on first
+            # use (__getattr__): a hypervisor that runs a few pipelines and closes
+            # never pays for the ones it does not touch
+            self._max_exposure = max_exposure
         self.device = mode
         self.ring_enforcer = RingEnforcer()
         self.classifier = ActionClassifier()
@@ -156,6 +157,21 @@ class Hypervisor:
         self.demote_on_slash = demote_on_slash
         self._sessions = SessionTable()
         self.batched_sessions = 0  # sessions written by pipeline_batch / run_pipelines (ordinary sessions)
+
+    _LAZY_ENGINES = frozenset(("vouching", "slashing", "commitment"))
+
+    def __getattr__(self, name: str):
+        # only reached for attributes not set yet: the device engines of a
+        # device-backed hypervisor, built together on first use
+        d = self.__dict__
+        if name in Hypervisor._LAZY_ENGINES and d.get("_store") is not None:
+            _device = _device_mod()
+            st = d["_store"]
+            ve = d["vouching"] = _device.DeviceVouchingEngine(st, d["_tenant"], d.get("_max_exposure"))
+            d["slashing"] = _device.DeviceSlashingEngine(ve)
+            d["commitment"] = _device.DeviceCommitmentEngine(st)
+            return d[name]
+        raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
 
     # -- lifetime ------------------------------------------------------------
     def close(self) -> int:
@@ -395,7 +411,8 @@ class Hypervisor:
             self.commitment.register(sso)
         # the device counts the deltas past retention (result word 12); with none
         # expired the host GC has nothing to prune and needs no walk over the views
-        self.gc.collect(session_id=session_id, vfs=sso.vfs, delta_engine=de if expired else None,
+        # a VFS nothing ever built holds no files: the collector has nothing to purge
+        self.gc.collect(session_id=session_id, vfs=sso.vfs_if_built(), delta_engine=de if expired else None,
                         delta_count=de.turn_count if expired else n)
 
     def _terminate_events(self, session_id: str, root: Optional[str]) -> None:

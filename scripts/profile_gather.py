@@ -59,7 +59,7 @@ def main() -> None:
     asyncio.run(batch(n // 4))
     pr.disable()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(30)
+    pstats.Stats(pr, stream=s).sort_stats(os.environ.get("SORT", "tottime")).print_stats(int(os.environ.get("TOP", "30")))
     print("\n".join(ln for ln in s.getvalue().splitlines() if ln.strip()))
 
 
