@@ -318,8 +318,10 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
     const uint32_t* src = reinterpret_cast<const uint32_t*>(t.payload + R.doff(a, 0));
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    const uint4 c0 = s4[0], c1 = s4[1], c2 = s4[2], c3 = s4[3];  // named: no scratch array
     for (int32_t d = 1; d < D; ++d) {
+      // re-read per record (L1/L2 hits): 16 words held across the loop were spilled
+      // to scratch at the kernel's register cap
+      const uint4 c0 = s4[0], c1 = s4[1], c2 = s4[2], c3 = s4[3];
       uint4* dst = reinterpret_cast<uint4*>(t.payload + R.doff(a, d));
       dst[0] = c0;
       dst[1] = c1;
