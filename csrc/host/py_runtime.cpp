@@ -6,10 +6,12 @@
 //   * time base helpers (N09): epoch-µs ↔ ISO text with the exact
 //     datetime.isoformat() rendering used in delta hashes.
 #include <Python.h>
+#include <longintrepr.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +19,7 @@
 #include <deque>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -307,12 +310,23 @@ static std::string_view utf8_view(PyObject* o, std::string& tmp) {
   return std::string_view(tmp);
 }
 
+// ConsistencyMode members are singletons: their mode is resolved once (an Enum's
+// `.value` is a descriptor call) and remembered by identity (strong?)
+static std::unordered_map<PyObject*, bool>& mode_members() {
+  static std::unordered_map<PyObject*, bool> m;
+  return m;
+}
+
+static const py::str& cfg_name(int k) {
+  static const py::str names[] = {py::str("consistency_mode"), py::str("max_participants"), py::str("min_sigma_eff"),
+                                  py::str("enable_audit")};
+  return names[k];
+}
+
 static std::tuple<int32_t, double, uint8_t> config_row(PyObject* c) {
-  static const py::str kMode("consistency_mode"), kMax("max_participants"), kMin("min_sigma_eff"),
-      kAudit("enable_audit"), kValue("value");
-  // ConsistencyMode members are singletons: their mode is resolved once (an Enum's
-  // `.value` is a descriptor call) and remembered by identity
-  static std::unordered_map<PyObject*, bool> members;
+  static const py::str kValue("value");
+  const py::str &kMode = cfg_name(0), &kMax = cfg_name(1), &kMin = cfg_name(2), &kAudit = cfg_name(3);
+  auto& members = mode_members();
   py::object m = getattr_(c, kMode);
   bool strong;
   auto it = members.find(m.ptr());
@@ -339,8 +353,8 @@ static std::tuple<int32_t, double, uint8_t> config_row(PyObject* c) {
 // Spec packing works straight on the CPython objects: borrowed tuple items, no
 // per-spec containers.  A spec object seen before in the batch (batches drawn
 // from a pool of specs) copies its first occurrence's rows.
-static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool& pool, const py::object& cfg_of,
-                           int64_t fixed) {
+static py::dict pack_specs_serial(const py::list& specs, StringPool& agents, StringPool& pool,
+                                  const py::object& cfg_of, int64_t fixed) {
   const size_t n = specs.size();
   std::vector<int32_t> creator(n), maxpart(n), join_off{0}, join_agent, delta_off{0}, d_pool, ch_off{0}, ch_rows,
       step_off{0}, s_retry;
@@ -505,6 +519,490 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
 }
 
 
+// ------------------------------------------------------- parallel spec walk
+// The serial walk above is bound by reading CPython objects one spec at a time
+// (≈35 objects per random spec).  Here T threads walk disjoint spec ranges while
+// the calling thread holds the GIL and waits: no Python code can run meanwhile,
+// and the workers only READ objects through borrowed pointers — no reference
+// counts, no allocation, no Python error state.  Anything off the fast shapes
+// (a str that is not compact ASCII, a sequence that is not a tuple / list, an
+// attribute not in the instance __dict__, a truth value that is not a bool /
+// None / str, a number that is not a float or a one-digit int) marks the walk
+// failed and the serial walk redoes the whole batch (same columns, its errors).
+//
+// Workers give strings part-local ids (first-occurrence order); the merge, back
+// on the calling thread, interns each part's strings in that order — the same
+// global ids the serial walk assigns — and rewrites the columns.
+namespace pack {
+
+inline bool ascii_view(PyObject* o, std::string_view& out) {
+  if (!PyUnicode_CheckExact(o) || !PyUnicode_IS_COMPACT_ASCII(o)) return false;
+  const PyASCIIObject* a = reinterpret_cast<const PyASCIIObject*>(o);
+  out = std::string_view(reinterpret_cast<const char*>(a + 1), static_cast<size_t>(a->length));
+  return true;
+}
+
+// Instance-__dict__ attribute (borrowed) or null.  `name` is a str whose hash the
+// caller computed beforehand, so the lookup only reads.
+inline PyObject* dict_attr(PyObject* o, PyObject* name) {
+  PyObject** dp = _PyObject_GetDictPtr(o);
+  if (dp == nullptr || *dp == nullptr || !PyDict_CheckExact(*dp)) return nullptr;
+  return PyDict_GetItemWithError(*dp, name);
+}
+
+inline bool seq(PyObject* o, PyObject* const*& it, Py_ssize_t& n) {
+  if (PyTuple_CheckExact(o)) {
+    it = reinterpret_cast<PyTupleObject*>(o)->ob_item;
+    n = PyTuple_GET_SIZE(o);
+    return true;
+  }
+  if (PyList_CheckExact(o)) {
+    it = reinterpret_cast<PyListObject*>(o)->ob_item;
+    n = PyList_GET_SIZE(o);
+    return true;
+  }
+  return false;
+}
+
+inline bool small_int(PyObject* o, int64_t& v) {
+  if (!PyLong_CheckExact(o)) return false;
+  const Py_ssize_t sz = Py_SIZE(o);
+  if (sz == 0) {
+    v = 0;
+    return true;
+  }
+  if (sz != 1 && sz != -1) return false;
+  v = static_cast<int64_t>(reinterpret_cast<PyLongObject*>(o)->ob_digit[0]);
+  if (sz < 0) v = -v;
+  return true;
+}
+
+inline bool number(PyObject* o, double& v) {
+  if (PyFloat_CheckExact(o)) {
+    v = PyFloat_AS_DOUBLE(o);
+    return true;
+  }
+  int64_t i;
+  if (!small_int(o, i)) return false;
+  v = static_cast<double>(i);
+  return true;
+}
+
+inline bool truth(PyObject* o, bool& v) {
+  if (o == Py_True || o == Py_False || o == Py_None) {
+    v = o == Py_True;
+    return true;
+  }
+  std::string_view s;
+  if (ascii_view(o, s)) {
+    v = !s.empty();
+    return true;
+  }
+  return false;
+}
+
+// Part-local string ids by content; a direct-mapped memo skips re-hashing an
+// object seen before (agent DIDs drawn from one list, shared literals).
+struct LocalPool {
+  std::vector<std::string_view> strs;
+  std::vector<PyObject*> objs;  // a str that is not compact ASCII: encoded by the merge (GIL held)
+  std::vector<int32_t> table;
+  std::vector<uint64_t> hashes;
+  size_t mask = 0;
+  std::vector<std::pair<PyObject*, int32_t>> memo = std::vector<std::pair<PyObject*, int32_t>>(4096);
+  LocalPool() : table(1024, -1), mask(1023) {}
+  static uint64_t hash(std::string_view s) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ s.size();
+    size_t i = 0;
+    for (; i + 8 <= s.size(); i += 8) {
+      uint64_t w;
+      std::memcpy(&w, s.data() + i, 8);
+      h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+      h ^= h >> 31;
+    }
+    uint64_t w = 0;
+    std::memcpy(&w, s.data() + i, s.size() - i);
+    h = (h ^ w) * 0x94D049BB133111EBull;
+    return h ^ (h >> 29);
+  }
+  void grow() {
+    const size_t cap = table.size() * 2;
+    std::vector<int32_t> t(cap, -1);
+    for (size_t id = 0; id < strs.size(); ++id) {
+      if (id < objs.size() && objs[id] != nullptr) continue;  // identity-keyed: not in the content table
+      size_t i = hashes[id] & (cap - 1);
+      while (t[i] >= 0) i = (i + 1) & (cap - 1);
+      t[i] = static_cast<int32_t>(id);
+    }
+    table.swap(t);
+    mask = cap - 1;
+  }
+  // -1 if `o` is not a str (the caller fails the walk)
+  int32_t get(PyObject* o) {
+    auto& m = memo[(reinterpret_cast<uintptr_t>(o) >> 4) & 4095];
+    if (m.first == o) return m.second;
+    std::string_view s;
+    if (!ascii_view(o, s)) {
+      if (!PyUnicode_CheckExact(o)) return -1;
+      // no UTF-8 to read without allocating: keyed by identity, encoded by the merge
+      const int32_t id = static_cast<int32_t>(strs.size());
+      strs.emplace_back();
+      hashes.push_back(0);
+      objs.resize(strs.size(), nullptr);
+      objs[static_cast<size_t>(id)] = o;
+      m = {o, id};
+      return id;
+    }
+    const uint64_t h = hash(s);
+    size_t i = h & mask;
+    for (;; i = (i + 1) & mask) {
+      const int32_t id = table[i];
+      if (id < 0) break;
+      if (hashes[id] == h && strs[id] == s) {
+        m = {o, id};
+        return id;
+      }
+    }
+    const int32_t id = static_cast<int32_t>(strs.size());
+    strs.push_back(s);
+    hashes.push_back(h);
+    if (!objs.empty()) objs.push_back(nullptr);
+    table[i] = id;
+    if (2 * strs.size() > table.size()) grow();
+    m = {o, id};
+    return id;
+  }
+};
+
+struct Names {
+  PyObject *joins, *deltas, *steps, *act, *term, *comp, *cfg, *creator;
+  PyObject *mode, *maxp, *mins, *audit;
+  const std::vector<std::pair<PyObject*, bool>>* members;  // resolved ConsistencyMode members
+};
+
+struct Part {
+  size_t lo = 0, hi = 0;
+  bool ok = true;
+  LocalPool agents, pool;
+  std::vector<PyObject*> cfg;
+  std::vector<std::tuple<int32_t, double, uint8_t>> cfg_row;  // valid where cfg_ok
+  std::vector<uint8_t> cfg_ok;
+  std::vector<int32_t> creator, njoin, join_agent, ndelta, d_pool, nch, ch_rows, nstep, s_retry;
+  std::vector<double> join_sigma;
+  std::vector<uint8_t> bits, s_undo, s_fail;
+
+  int bad_line = 0;
+  bool fail(int line) {
+    bad_line = line;
+    return false;
+  }
+  bool walk_one(PyObject* sp, const Names& k) {
+    PyObject* c = dict_attr(sp, k.cfg);
+    if (c == nullptr) return fail(__LINE__);
+    cfg.push_back(c);
+    config(c, k);
+    bool a, t, m;
+    PyObject *pa = dict_attr(sp, k.act), *pt = dict_attr(sp, k.term), *pm = dict_attr(sp, k.comp);
+    if (!pa || !pt || !pm || !truth(pa, a) || !truth(pt, t) || !truth(pm, m)) return fail(__LINE__);
+    bits.push_back(static_cast<uint8_t>((a ? 4 : 0) | (t ? 8 : 0) | (m ? 16 : 0)));
+    PyObject* cr = dict_attr(sp, k.creator);
+    if (cr == nullptr) return fail(__LINE__);
+    const int32_t cid = agents.get(cr);
+    if (cid < 0) return fail(__LINE__);
+    creator.push_back(cid);
+    PyObject* const* it;
+    Py_ssize_t n;
+    PyObject* js = dict_attr(sp, k.joins);
+    if (js == nullptr || !seq(js, it, n)) return fail(__LINE__);
+    njoin.push_back(static_cast<int32_t>(n));
+    for (Py_ssize_t q = 0; q < n; ++q) {
+      PyObject* const* jt;
+      Py_ssize_t jn;
+      if (!seq(it[q], jt, jn) || jn < 2) return fail(__LINE__);
+      const int32_t id = agents.get(jt[0]);
+      double sg;
+      if (id < 0 || !number(jt[1], sg)) return fail(__LINE__);
+      join_agent.push_back(id);
+      join_sigma.push_back(sg);
+    }
+    PyObject* ds = dict_attr(sp, k.deltas);
+    if (ds == nullptr || !seq(ds, it, n)) return fail(__LINE__);
+    ndelta.push_back(static_cast<int32_t>(n));
+    for (Py_ssize_t q = 0; q < n; ++q) {
+      PyObject* const* dt;
+      Py_ssize_t dn;
+      if (!seq(it[q], dt, dn) || dn < 2) return fail(__LINE__);
+      const int32_t did = pool.get(dt[0]);
+      if (did < 0) return fail(__LINE__);
+      d_pool.push_back(did);
+      PyObject* const* ct;
+      Py_ssize_t cn;
+      if (!seq(dt[1], ct, cn)) return fail(__LINE__);
+      nch.push_back(static_cast<int32_t>(cn));
+      for (Py_ssize_t r = 0; r < cn; ++r) {
+        PyObject* const* x;
+        Py_ssize_t xn;
+        if (!seq(ct[r], x, xn) || xn < 3) return fail(__LINE__);
+        const int32_t path = pool.get(x[0]), op = pool.get(x[1]);
+        const int32_t h = x[2] == Py_None ? -1 : pool.get(x[2]);
+        const int32_t prev = xn > 3 && x[3] != Py_None ? pool.get(x[3]) : -1;
+        if (path < 0 || op < 0 || (h < 0 && x[2] != Py_None) || (prev < 0 && xn > 3 && x[3] != Py_None)) return fail(__LINE__);
+        ch_rows.push_back(path);
+        ch_rows.push_back(op);
+        ch_rows.push_back(h);
+        ch_rows.push_back(prev);
+      }
+    }
+    PyObject* ss = dict_attr(sp, k.steps);
+    if (ss == nullptr || !seq(ss, it, n)) return fail(__LINE__);
+    nstep.push_back(static_cast<int32_t>(n));
+    for (Py_ssize_t q = 0; q < n; ++q) {
+      PyObject* const* st;
+      Py_ssize_t sn;
+      if (!seq(it[q], st, sn) || sn < 6) return fail(__LINE__);
+      bool undo;
+      int64_t retry, nfail;
+      if (!truth(st[3], undo) || !small_int(st[4], retry) || !small_int(st[5], nfail)) return fail(__LINE__);
+      s_undo.push_back(undo ? 1 : 0);
+      s_retry.push_back(static_cast<int32_t>(retry));
+      s_fail.push_back(static_cast<uint8_t>(nfail < 255 ? nfail : 255));
+    }
+    return true;
+  }
+
+  // A SessionConfig's row when every field is on the fast shapes and its mode
+  // member was resolved before the walk; else the merge resolves it (GIL held).
+  void config(PyObject* c, const Names& k) {
+    cfg_row.emplace_back();
+    cfg_ok.push_back(0);
+    if (c == Py_None) return;
+    PyObject *m = dict_attr(c, k.mode), *mx = dict_attr(c, k.maxp), *mn = dict_attr(c, k.mins),
+             *au = dict_attr(c, k.audit);
+    if (!m || !mx || !mn || !au) return;
+    int64_t maxp;
+    double mins;
+    bool audit;
+    if (!small_int(mx, maxp) || !number(mn, mins) || !truth(au, audit)) return;
+    for (const auto& e : *k.members)
+      if (e.first == m) {
+        cfg_row.back() = std::make_tuple(static_cast<int32_t>(maxp), mins,
+                                         static_cast<uint8_t>((audit ? 1 : 0) | (e.second ? 2 : 0)));
+        cfg_ok.back() = 1;
+        return;
+      }
+  }
+
+  double ms = 0;
+  void walk(PyObject* const* items, const Names& k) {
+    const auto t0 = std::chrono::steady_clock::now();
+    walk_(items, k);
+    ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  void walk_(PyObject* const* items, const Names& k) {
+    const size_t m = hi - lo;
+    cfg.reserve(m);
+    bits.reserve(m);
+    creator.reserve(m);
+    for (size_t i = lo; i < hi && ok; ++i) ok = walk_one(items[i], k);
+  }
+};
+
+}  // namespace pack
+
+static int pack_threads_default() {
+  static const int v = [] {
+    const char* e = std::getenv("AHV_PACK_THREADS");
+    if (e != nullptr) return std::atoi(e);
+    // a GPU box grants one process about 16 CPUs (20k random specs: 16.9 ms serial,
+    // 7.1 ms on 8 threads, 6.1 ms on 16; MI355X box)
+    const unsigned h = std::thread::hardware_concurrency();
+    return static_cast<int>(h == 0 ? 1 : h < 16 ? h : 16);
+  }();
+  return v;
+}
+
+// threads: < 0 → AHV_PACK_THREADS or min(16, cores) for batches of ≥ 4,096 specs;
+// 0 / 1 → the serial walk.
+static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool& pool, const py::object& cfg_of,
+                           int64_t fixed, int threads) {
+  const size_t n = specs.size();
+  int T = threads;
+  if (T < 0) T = n >= 4096 ? pack_threads_default() : 1;
+  if (T > 64) T = 64;
+  if (T <= 1 || n < static_cast<size_t>(2 * T)) return pack_specs_serial(specs, agents, pool, cfg_of, fixed);
+  static const py::str kJoins("joins"), kDeltas("deltas"), kSteps("steps"), kAct("activate"), kTerm("terminate"),
+      kComp("compensate"), kCfg("config"), kCreator("creator_did");
+  for (const py::str* nm : {&kJoins, &kDeltas, &kSteps, &kAct, &kTerm, &kComp, &kCfg, &kCreator, &cfg_name(0),
+                            &cfg_name(1), &cfg_name(2), &cfg_name(3)})
+    if (PyObject_Hash(nm->ptr()) == -1) throw py::error_already_set();  // cached: the workers' lookups only read
+  PyObject* const* items = PySequence_Fast_ITEMS(specs.ptr());
+  {
+    // resolve the first spec's consistency mode member here, so the workers find it
+    PyObject* c0 = pack::dict_attr(items[0], kCfg.ptr());
+    if (c0 != nullptr && c0 != Py_None) {
+      try {
+        config_row(c0);
+      } catch (py::error_already_set&) {
+        // reported by the merge / serial walk, which reads the same object
+        PyErr_Clear();
+      }
+    }
+  }
+  std::vector<std::pair<PyObject*, bool>> members(mode_members().begin(), mode_members().end());
+  const pack::Names names{kJoins.ptr(), kDeltas.ptr(), kSteps.ptr(), kAct.ptr(), kTerm.ptr(), kComp.ptr(),
+                          kCfg.ptr(), kCreator.ptr(), cfg_name(0).ptr(), cfg_name(1).ptr(), cfg_name(2).ptr(),
+                          cfg_name(3).ptr(), &members};
+  std::vector<pack::Part> parts(static_cast<size_t>(T));
+  for (int t = 0; t < T; ++t) {
+    parts[t].lo = n * static_cast<size_t>(t) / static_cast<size_t>(T);
+    parts[t].hi = n * static_cast<size_t>(t + 1) / static_cast<size_t>(T);
+  }
+  const auto tw0 = std::chrono::steady_clock::now();
+  {
+    // the GIL stays held by this thread: nothing else touches the objects meanwhile
+    std::vector<std::thread> pool_threads;
+    pool_threads.reserve(static_cast<size_t>(T - 1));
+    for (int t = 1; t < T; ++t)
+      pool_threads.emplace_back([&parts, items, &names, t] {
+        try {
+          parts[t].walk(items, names);
+        } catch (...) {
+          parts[t].ok = false;
+        }
+      });
+    try {
+      parts[0].walk(items, names);
+    } catch (...) {
+      parts[0].ok = false;
+    }
+    for (auto& th : pool_threads) th.join();
+  }
+  const auto tw1 = std::chrono::steady_clock::now();
+  for (const auto& p : parts)
+    if (!p.ok) {
+      if (std::getenv("AHV_PACK_DEBUG")) std::fprintf(stderr, "[pack] serial walk: part fell back at line %d\n", p.bad_line);
+      return pack_specs_serial(specs, agents, pool, cfg_of, fixed);
+    }
+  // ---- merge (GIL held): intern each part's strings in first-occurrence order
+  std::vector<int32_t> creator(n), maxpart(n), join_off{0}, join_agent, delta_off{0}, d_pool, ch_off{0}, ch_rows,
+      step_off{0}, s_retry;
+  std::vector<double> minsig(n), join_sigma;
+  std::vector<uint8_t> flags(n), s_undo, s_fail;
+  std::vector<int64_t> base_caps;
+  size_t tj = 0, td = 0, tc = 0, ts = 0;
+  for (const auto& p : parts) {
+    tj += p.join_agent.size();
+    td += p.d_pool.size();
+    tc += p.ch_rows.size();
+    ts += p.s_undo.size();
+  }
+  join_off.reserve(n + 1);
+  join_agent.reserve(tj);
+  join_sigma.reserve(tj);
+  delta_off.reserve(n + 1);
+  d_pool.reserve(td);
+  base_caps.reserve(td);
+  ch_off.reserve(td + 1);
+  ch_rows.reserve(tc);
+  step_off.reserve(n + 1);
+  s_undo.reserve(ts);
+  s_retry.reserve(ts);
+  s_fail.reserve(ts);
+  PtrTable<std::tuple<int32_t, double, uint8_t>> cfg_cache(std::min<size_t>(n, 65536) + 1);
+  std::vector<int32_t> amap, pmap;
+  std::vector<int64_t> pesc;
+  std::string tmp;
+  auto local = [&tmp](const pack::LocalPool& lp, size_t l) -> std::string_view {
+    if (l < lp.objs.size() && lp.objs[l] != nullptr) return utf8_view(lp.objs[l], tmp);
+    return lp.strs[l];
+  };
+  for (const auto& p : parts) {
+    amap.resize(p.agents.strs.size());
+    for (size_t l = 0; l < amap.size(); ++l) amap[l] = agents.intern(local(p.agents, l));
+    pmap.resize(p.pool.strs.size());
+    pesc.resize(pmap.size());
+    for (size_t l = 0; l < pmap.size(); ++l) {
+      pmap[l] = pool.intern(local(p.pool, l));
+      pesc[l] = pool.esc_len(pmap[l]) + 2;
+    }
+    auto P = [&](int32_t l) { return l < 0 ? -1 : pmap[static_cast<size_t>(l)]; };
+    auto E = [&](int32_t l) -> int64_t { return l < 0 ? 4 : pesc[static_cast<size_t>(l)]; };
+    size_t jk = 0, dk = 0, ck = 0, sk = 0;
+    for (size_t i = p.lo, r = 0; i < p.hi; ++i, ++r) {
+      PyObject* cfg = p.cfg[r];
+      const std::tuple<int32_t, double, uint8_t>* ci = p.cfg_ok[r] ? &p.cfg_row[r] : cfg_cache.find(cfg);
+      std::tuple<int32_t, double, uint8_t> row;
+      if (ci == nullptr) {
+        if (cfg == Py_None) {
+          py::tuple t = cfg_of(py::none());
+          row = std::make_tuple(t[0].cast<int32_t>(), t[1].cast<double>(), t[2].cast<uint8_t>());
+        } else {
+          row = config_row(cfg);
+        }
+        if (!cfg_cache.full()) cfg_cache.insert(cfg, row);
+        ci = &row;
+      }
+      maxpart[i] = std::get<0>(*ci);
+      minsig[i] = std::get<1>(*ci);
+      flags[i] = static_cast<uint8_t>(std::get<2>(*ci) | p.bits[r]);
+      creator[i] = amap[static_cast<size_t>(p.creator[r])];
+      for (int32_t q = 0; q < p.njoin[r]; ++q, ++jk) {
+        join_agent.push_back(amap[static_cast<size_t>(p.join_agent[jk])]);
+        join_sigma.push_back(p.join_sigma[jk]);
+      }
+      join_off.push_back(static_cast<int32_t>(join_agent.size()));
+      for (int32_t q = 0; q < p.ndelta[r]; ++q, ++dk) {
+        const int32_t ld = p.d_pool[dk];
+        d_pool.push_back(P(ld));
+        int64_t cap = fixed + E(ld);
+        for (int32_t c = 0; c < p.nch[dk]; ++c, ck += 4) {
+          const int32_t path = p.ch_rows[ck], op = p.ch_rows[ck + 1], h = p.ch_rows[ck + 2], prev = p.ch_rows[ck + 3];
+          ch_rows.push_back(P(path));
+          ch_rows.push_back(P(op));
+          ch_rows.push_back(P(h));
+          ch_rows.push_back(P(prev));
+          cap += 17 + 15 + 10 + 19 + 1 + (c ? 2 : 0) + E(h) + E(op) + E(path) + E(prev);
+        }
+        ch_off.push_back(static_cast<int32_t>(ch_rows.size() / 4));
+        base_caps.push_back(cap);
+      }
+      delta_off.push_back(static_cast<int32_t>(d_pool.size()));
+      for (int32_t q = 0; q < p.nstep[r]; ++q, ++sk) {
+        s_undo.push_back(p.s_undo[sk]);
+        s_retry.push_back(p.s_retry[sk]);
+        s_fail.push_back(p.s_fail[sk]);
+      }
+      step_off.push_back(static_cast<int32_t>(s_undo.size()));
+    }
+  }
+  if (std::getenv("AHV_PACK_DEBUG")) {
+    const auto tw2 = std::chrono::steady_clock::now();
+    for (const auto& p : parts) std::fprintf(stderr, "[pack]   part %zu..%zu %.2f ms, %zu+%zu strings\n", p.lo, p.hi, p.ms,
+                                             p.agents.strs.size(), p.pool.strs.size());
+    std::fprintf(stderr, "[pack] T=%d walk %.2f ms merge %.2f ms\n", T,
+                 std::chrono::duration<double, std::milli>(tw1 - tw0).count(),
+                 std::chrono::duration<double, std::milli>(tw2 - tw1).count());
+  }
+  py::dict out;
+  out["creator"] = as_bytes(creator);
+  out["maxpart"] = as_bytes(maxpart);
+  out["minsig"] = as_bytes(minsig);
+  out["flags"] = as_bytes(flags);
+  out["join_off"] = as_bytes(join_off);
+  out["join_agent"] = as_bytes(join_agent);
+  out["join_sigma"] = as_bytes(join_sigma);
+  out["delta_off"] = as_bytes(delta_off);
+  out["d_pool"] = as_bytes(d_pool);
+  out["base_caps"] = as_bytes(base_caps);
+  out["ch_off"] = as_bytes(ch_off);
+  out["ch_rows"] = as_bytes(ch_rows);
+  out["step_off"] = as_bytes(step_off);
+  out["s_undo"] = as_bytes(s_undo);
+  out["s_retry"] = as_bytes(s_retry);
+  out["s_fail"] = as_bytes(s_fail);
+  return out;
+}
+
 // The changes fragment of a template delta (ahv/delta_emit.h emit_changes_fragment)
 // rendered from the pool's escaped strings: `changes` = [[path, op, content_hash,
 // previous_hash], ...] pool ids (-1 = null).  The device copies these bytes.
@@ -652,7 +1150,9 @@ void register_runtime(py::module_& m) {
   m.def("render_fragment", &render_fragment, py::arg("pool"), py::arg("changes"), py::arg("turn"),
         py::arg("has_parent"));
   m.def("pack_specs", &pack_specs, py::arg("specs"), py::arg("agents"), py::arg("pool"), py::arg("cfg_of"),
-        py::arg("fixed"), "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py)");
+        py::arg("fixed"), py::arg("threads") = -1,
+        "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py); threads: < 0 auto "
+        "(AHV_PACK_THREADS), 1 serial");
   m.def("iso_from_us", &iso_from_us, "datetime.isoformat() text of an epoch-µs UTC instant");
   m.def("uuids_from_counters", &uuids_from_counters, py::arg("seed"), py::arg("base"), py::arg("n"),
         py::arg("prefix") = std::string(), "uuid_from_counter(seed, base + i, prefix) for i < n");

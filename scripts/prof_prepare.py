@@ -25,9 +25,13 @@ for _ in range(2):
     p = SP.prepare(hv, specs)
     SP.launch(p)
     r = SP.finish(hv, p)
-t = time.perf_counter()
-C.pack_specs(specs, st.agents._pool, st.pool._pool, lambda c: (4, 0.5, 1), SP._FIXED)
-print("pack_specs alone", round((time.perf_counter() - t) * 1e3, 2), "ms")
+for th in (1, 2, 4, 8, 16, -1):
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        C.pack_specs(specs, st.agents._pool, st.pool._pool, lambda c: (4, 0.5, 1), SP._FIXED, th)
+        ts.append(time.perf_counter() - t)
+    print("pack_specs threads", th, "ms", [round(x * 1e3, 2) for x in ts], flush=True)
 pr = cProfile.Profile()
 pr.enable()
 p = SP.prepare(hv, specs)

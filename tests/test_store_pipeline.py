@@ -278,3 +278,35 @@ def test_dashboard_and_stats_over_batches_build_no_views():
     assert not b.views
     assert d["overview"]["sessions"] == 500
     st.close()
+
+
+@pytest.mark.parametrize("threads", [2, 4, 8])
+def test_parallel_spec_walk_packs_the_serial_columns(threads):
+    """pack_specs' GIL-free parallel walk (disjoint spec ranges per thread, strings
+    merged in first-occurrence order) yields the serial walk's columns and pool ids,
+    with non-ASCII strings (encoded by the merge) and a spec off the fast shapes
+    (a list config field read through the attribute protocol → serial redo)."""
+    from agent_hypervisor_amd._native import C
+    from agent_hypervisor_amd.models import store_pipeline as SP
+
+    rng = random.Random(11)
+    specs = [random_spec(rng) for _ in range(3000)]
+    specs[5] = PipelineSpec(joins=(("did:mesh:été", 0.7),), deltas=(("did:mesh:été", (("/ü", "add", None),)),),
+                            steps=(), config=None)
+
+    def pack(sp, th):
+        a, p = C.StringPool(), C.StringPool()
+        out = C.pack_specs(sp, a, p, lambda c: (4, 0.5, 1), SP._FIXED, th)
+        return out, [a.str(i) for i in range(len(a))], [p.str(i) for i in range(len(p))]
+
+    ref = pack(specs, 1)
+    got = pack(specs, threads)
+    assert got[1] == ref[1] and got[2] == ref[2]
+    assert all(got[0][k] == ref[0][k] for k in ref[0])
+
+    class Odd:  # a spec object without an instance __dict__ entry for its fields
+        joins, deltas, steps, activate, terminate, compensate, config, creator_did = (
+            (), (), (), True, True, True, None, "did:mesh:odd")
+
+    mixed = specs[:100] + [Odd()] + specs[100:200]
+    assert all(pack(mixed, threads)[0][k] == pack(mixed, 1)[0][k] for k in ref[0])
