@@ -883,97 +883,114 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
       if (std::getenv("AHV_PACK_DEBUG")) std::fprintf(stderr, "[pack] serial walk: part fell back at line %d\n", p.bad_line);
       return pack_specs_serial(specs, agents, pool, cfg_of, fixed);
     }
-  // ---- merge (GIL held): intern each part's strings in first-occurrence order
-  std::vector<int32_t> creator(n), maxpart(n), join_off{0}, join_agent, delta_off{0}, d_pool, ch_off{0}, ch_rows,
-      step_off{0}, s_retry;
-  std::vector<double> minsig(n), join_sigma;
-  std::vector<uint8_t> flags(n), s_undo, s_fail;
-  std::vector<int64_t> base_caps;
-  size_t tj = 0, td = 0, tc = 0, ts = 0;
-  for (const auto& p : parts) {
-    tj += p.join_agent.size();
-    td += p.d_pool.size();
-    tc += p.ch_rows.size();
-    ts += p.s_undo.size();
+  // ---- merge: (1) with the GIL, intern each part's strings in first-occurrence
+  // order (the serial walk's global ids) and resolve the configs the workers could
+  // not; (2) the workers write their ranges of the columns, ids remapped, at offsets
+  // from a prefix sum over the parts.
+  const size_t P = parts.size();
+  std::vector<size_t> jb(P + 1, 0), db(P + 1, 0), cb(P + 1, 0), sb(P + 1, 0);
+  for (size_t t = 0; t < P; ++t) {
+    jb[t + 1] = jb[t] + parts[t].join_agent.size();
+    db[t + 1] = db[t] + parts[t].d_pool.size();
+    cb[t + 1] = cb[t] + parts[t].ch_rows.size() / 4;
+    sb[t + 1] = sb[t] + parts[t].s_undo.size();
   }
-  join_off.reserve(n + 1);
-  join_agent.reserve(tj);
-  join_sigma.reserve(tj);
-  delta_off.reserve(n + 1);
-  d_pool.reserve(td);
-  base_caps.reserve(td);
-  ch_off.reserve(td + 1);
-  ch_rows.reserve(tc);
-  step_off.reserve(n + 1);
-  s_undo.reserve(ts);
-  s_retry.reserve(ts);
-  s_fail.reserve(ts);
-  PtrTable<std::tuple<int32_t, double, uint8_t>> cfg_cache(std::min<size_t>(n, 65536) + 1);
-  std::vector<int32_t> amap, pmap;
-  std::vector<int64_t> pesc;
-  std::string tmp;
-  auto local = [&tmp](const pack::LocalPool& lp, size_t l) -> std::string_view {
-    if (l < lp.objs.size() && lp.objs[l] != nullptr) return utf8_view(lp.objs[l], tmp);
-    return lp.strs[l];
-  };
-  for (const auto& p : parts) {
-    amap.resize(p.agents.strs.size());
-    for (size_t l = 0; l < amap.size(); ++l) amap[l] = agents.intern(local(p.agents, l));
-    pmap.resize(p.pool.strs.size());
-    pesc.resize(pmap.size());
-    for (size_t l = 0; l < pmap.size(); ++l) {
-      pmap[l] = pool.intern(local(p.pool, l));
-      pesc[l] = pool.esc_len(pmap[l]) + 2;
-    }
-    auto P = [&](int32_t l) { return l < 0 ? -1 : pmap[static_cast<size_t>(l)]; };
-    auto E = [&](int32_t l) -> int64_t { return l < 0 ? 4 : pesc[static_cast<size_t>(l)]; };
-    size_t jk = 0, dk = 0, ck = 0, sk = 0;
-    for (size_t i = p.lo, r = 0; i < p.hi; ++i, ++r) {
-      PyObject* cfg = p.cfg[r];
-      const std::tuple<int32_t, double, uint8_t>* ci = p.cfg_ok[r] ? &p.cfg_row[r] : cfg_cache.find(cfg);
-      std::tuple<int32_t, double, uint8_t> row;
-      if (ci == nullptr) {
-        if (cfg == Py_None) {
-          py::tuple t = cfg_of(py::none());
-          row = std::make_tuple(t[0].cast<int32_t>(), t[1].cast<double>(), t[2].cast<uint8_t>());
+  std::vector<int32_t> creator(n), maxpart(n), join_off(n + 1), join_agent(jb[P]), delta_off(n + 1), d_pool(db[P]),
+      ch_off(db[P] + 1), ch_rows(4 * cb[P]), step_off(n + 1), s_retry(sb[P]);
+  std::vector<double> minsig(n), join_sigma(jb[P]);
+  std::vector<uint8_t> flags(n), s_undo(sb[P]), s_fail(sb[P]);
+  std::vector<int64_t> base_caps(db[P]);
+  join_off[0] = delta_off[0] = ch_off[0] = step_off[0] = 0;
+  std::vector<std::vector<int32_t>> amap(P), pmap(P);
+  std::vector<std::vector<int64_t>> pesc(P);
+  {
+    PtrTable<std::tuple<int32_t, double, uint8_t>> cfg_cache(std::min<size_t>(n, 65536) + 1);
+    std::string tmp;
+    auto local = [&tmp](const pack::LocalPool& lp, size_t l) -> std::string_view {
+      if (l < lp.objs.size() && lp.objs[l] != nullptr) return utf8_view(lp.objs[l], tmp);
+      return lp.strs[l];
+    };
+    for (size_t t = 0; t < P; ++t) {
+      pack::Part& p = parts[t];
+      amap[t].resize(p.agents.strs.size());
+      for (size_t l = 0; l < amap[t].size(); ++l) amap[t][l] = agents.intern(local(p.agents, l));
+      pmap[t].resize(p.pool.strs.size());
+      pesc[t].resize(pmap[t].size());
+      for (size_t l = 0; l < pmap[t].size(); ++l) {
+        pmap[t][l] = pool.intern(local(p.pool, l));
+        pesc[t][l] = pool.esc_len(pmap[t][l]) + 2;
+      }
+      for (size_t r = 0; r < p.cfg.size(); ++r) {
+        if (p.cfg_ok[r]) continue;
+        PyObject* cfg = p.cfg[r];
+        const std::tuple<int32_t, double, uint8_t>* ci = cfg_cache.find(cfg);
+        if (ci == nullptr) {
+          std::tuple<int32_t, double, uint8_t> row;
+          if (cfg == Py_None) {
+            py::tuple tt = cfg_of(py::none());
+            row = std::make_tuple(tt[0].cast<int32_t>(), tt[1].cast<double>(), tt[2].cast<uint8_t>());
+          } else {
+            row = config_row(cfg);
+          }
+          if (!cfg_cache.full()) ci = cfg_cache.insert(cfg, row);
+          p.cfg_row[r] = row;
         } else {
-          row = config_row(cfg);
+          p.cfg_row[r] = *ci;
         }
-        if (!cfg_cache.full()) cfg_cache.insert(cfg, row);
-        ci = &row;
+        p.cfg_ok[r] = 1;
       }
-      maxpart[i] = std::get<0>(*ci);
-      minsig[i] = std::get<1>(*ci);
-      flags[i] = static_cast<uint8_t>(std::get<2>(*ci) | p.bits[r]);
-      creator[i] = amap[static_cast<size_t>(p.creator[r])];
-      for (int32_t q = 0; q < p.njoin[r]; ++q, ++jk) {
-        join_agent.push_back(amap[static_cast<size_t>(p.join_agent[jk])]);
-        join_sigma.push_back(p.join_sigma[jk]);
+    }
+  }
+  auto fill = [&](size_t t) {
+    const pack::Part& p = parts[t];
+    const std::vector<int32_t>& am = amap[t];
+    const std::vector<int32_t>& pm = pmap[t];
+    const std::vector<int64_t>& pe = pesc[t];
+    auto Pm = [&pm](int32_t l) { return l < 0 ? -1 : pm[static_cast<size_t>(l)]; };
+    auto E = [&pe](int32_t l) -> int64_t { return l < 0 ? 4 : pe[static_cast<size_t>(l)]; };
+    size_t jk = 0, dk = 0, ck = 0, sk = 0;
+    size_t jo = jb[t], dd = db[t], co = cb[t], so = sb[t];
+    for (size_t i = p.lo, r = 0; i < p.hi; ++i, ++r) {
+      const auto& ci = p.cfg_row[r];
+      maxpart[i] = std::get<0>(ci);
+      minsig[i] = std::get<1>(ci);
+      flags[i] = static_cast<uint8_t>(std::get<2>(ci) | p.bits[r]);
+      creator[i] = am[static_cast<size_t>(p.creator[r])];
+      for (int32_t q = 0; q < p.njoin[r]; ++q, ++jk, ++jo) {
+        join_agent[jo] = am[static_cast<size_t>(p.join_agent[jk])];
+        join_sigma[jo] = p.join_sigma[jk];
       }
-      join_off.push_back(static_cast<int32_t>(join_agent.size()));
-      for (int32_t q = 0; q < p.ndelta[r]; ++q, ++dk) {
+      join_off[i + 1] = static_cast<int32_t>(jo);
+      for (int32_t q = 0; q < p.ndelta[r]; ++q, ++dk, ++dd) {
         const int32_t ld = p.d_pool[dk];
-        d_pool.push_back(P(ld));
+        d_pool[dd] = Pm(ld);
         int64_t cap = fixed + E(ld);
-        for (int32_t c = 0; c < p.nch[dk]; ++c, ck += 4) {
+        for (int32_t c = 0; c < p.nch[dk]; ++c, ck += 4, ++co) {
           const int32_t path = p.ch_rows[ck], op = p.ch_rows[ck + 1], h = p.ch_rows[ck + 2], prev = p.ch_rows[ck + 3];
-          ch_rows.push_back(P(path));
-          ch_rows.push_back(P(op));
-          ch_rows.push_back(P(h));
-          ch_rows.push_back(P(prev));
+          ch_rows[4 * co] = Pm(path);
+          ch_rows[4 * co + 1] = Pm(op);
+          ch_rows[4 * co + 2] = Pm(h);
+          ch_rows[4 * co + 3] = Pm(prev);
           cap += 17 + 15 + 10 + 19 + 1 + (c ? 2 : 0) + E(h) + E(op) + E(path) + E(prev);
         }
-        ch_off.push_back(static_cast<int32_t>(ch_rows.size() / 4));
-        base_caps.push_back(cap);
+        ch_off[dd + 1] = static_cast<int32_t>(co);
+        base_caps[dd] = cap;
       }
-      delta_off.push_back(static_cast<int32_t>(d_pool.size()));
-      for (int32_t q = 0; q < p.nstep[r]; ++q, ++sk) {
-        s_undo.push_back(p.s_undo[sk]);
-        s_retry.push_back(p.s_retry[sk]);
-        s_fail.push_back(p.s_fail[sk]);
+      delta_off[i + 1] = static_cast<int32_t>(dd);
+      for (int32_t q = 0; q < p.nstep[r]; ++q, ++sk, ++so) {
+        s_undo[so] = p.s_undo[sk];
+        s_retry[so] = p.s_retry[sk];
+        s_fail[so] = p.s_fail[sk];
       }
-      step_off.push_back(static_cast<int32_t>(s_undo.size()));
+      step_off[i + 1] = static_cast<int32_t>(so);
     }
+  };
+  {
+    std::vector<std::thread> fill_threads;
+    fill_threads.reserve(P - 1);
+    for (size_t t = 1; t < P; ++t) fill_threads.emplace_back(fill, t);
+    fill(0);
+    for (auto& th : fill_threads) th.join();
   }
   if (std::getenv("AHV_PACK_DEBUG")) {
     const auto tw2 = std::chrono::steady_clock::now();
