@@ -382,7 +382,7 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
   }
 
   // ------------------------------------------------------------ command wave
-  const Lanes L{lane, 64, lds0, kw0};
+  const Lanes L{lane, 64, lds0, kw0, &spec_s};
   uint64_t next = static_cast<uint64_t>(__hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
   uint32_t queued = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -484,10 +484,8 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    if (c.op == OP_SESS_CLOSE || c.op == OP_DELTA_MERKLE) {  // wait for the tree in flight
-      const uint32_t want = static_cast<uint32_t>(c.a[0]) + 1u;
-      while (lds_acquire(&spec_s) == want) __builtin_amdgcn_s_sleep(1);
-    }
+    // (a close / Merkle command waits for the tree in flight inside its execution,
+    // right before it reads the provisional root: Lanes::wait_tree)
     if (c.op == OP_DELTA_CAPTURE) {
       while (queued - lds_acquire(&q_done) >= static_cast<uint32_t>(kJobs)) __builtin_amdgcn_s_sleep(1);
     }

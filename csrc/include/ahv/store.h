@@ -218,7 +218,21 @@ struct Lanes {
   int n;
   uint32_t* lds;
   uint32_t* kw = nullptr;  // [n][kKwStride] per-lane K+W schedule rows (hash-engine wave), or null
+  // worker command wave: session + 1 whose provisional Merkle root the hash-engine
+  // wave is computing (LDS, 0 = none); a close / Merkle command waits on it only
+  // right before it reads that root (null: host twin, nothing to wait for)
+  const uint32_t* tree_busy = nullptr;
   AHV_HD bool leader() const { return lane == 0; }
+  AHV_HD void wait_tree(int64_t s) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (tree_busy == nullptr) return;
+    const uint32_t want = static_cast<uint32_t>(s) + 1u;
+    while (__hip_atomic_load(tree_busy, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == want)
+      __builtin_amdgcn_s_sleep(1);
+#else
+    (void)s;
+#endif
+  }
   // Lanes of ONE wave exchange data through LDS / global memory: a wave-level
   // barrier with wavefront-scope fences (the worker runs two waves with
   // different roles, so a workgroup barrier here would deadlock).
@@ -1773,15 +1787,16 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
         return;
       }
       const bool close = c.op == OP_SESS_CLOSE;
-      // the row words this command reads, requested together (one memory round
-      // trip for the lone command wave instead of one per check)
+      // The hash engine may still be computing this chain's provisional root: every
+      // step that does not read it (row checks, leaf gather, the close's row writes)
+      // runs first, the wait for the tree (L.wait_tree) comes right before the root.
+      // The row words this command reads, requested together (one memory round
+      // trip for the lone command wave instead of one per check).
       uint8_t st_raw = 0;
-      int64_t dcount_raw = 0, proot_n_raw = 0, proot_last_raw = 0;
+      int64_t dcount_raw = 0;
       if (L.leader()) {
         st_raw = t.s_state[s];
         dcount_raw = static_cast<int64_t>(t.s_dcount[s]);
-        proot_n_raw = static_cast<int64_t>(t.s_proot_n[s]);
-        proot_last_raw = static_cast<int64_t>(t.s_proot_last[s]);
       }
       const uint8_t st0 = bcast(L, st_raw);
       if (close && !((session_op_allowed_from(OP_TERMINATE) >> st0) & 1u)) {
@@ -1805,31 +1820,40 @@ AHV_HD void exec_delta(const Lanes& L, const Tables& t, const Cmd& c, uint64_t* 
         return;
       }
       const bool want_root = n > 0 && (!close || c.a[6]);
+      const int64_t now = static_cast<int64_t>(c.a[3]);
+      int32_t rel = 0;
+      if (close && L.leader()) {  // everything of the close that does not need the root
+        t.s_state[s] = SS_TERMINATING;
+        t.s_terminated[s] = now;
+        if (want_root) mark_committed_participants(t, s);
+        rel = release_vsess(t, static_cast<int32_t>(static_cast<int64_t>(c.a[4])), now);  // K07
+        t.s_released[s] = rel;
+        t.s_retained[s] = static_cast<int32_t>(n - expired);  // EphemeralGC retention
+      }
+      L.wait_tree(s);
       // the hash engine's provisional root, when it covers exactly these leaves
+      // (its tag and digest requested together)
       const IndexList il = index_list(t, c, static_cast<uint64_t>(n), c.a[2]);
-      const bool have = want_root && bcast(L, L.leader() ? static_cast<int>(proot_n_raw == n &&
-                                                                            proot_last_raw == il[n - 1])
-                                                         : 0) != 0;
+      uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      int have_raw = 0;
+      if (want_root && L.leader()) {
+        const int64_t pn = static_cast<int64_t>(t.s_proot_n[s]);
+        const int64_t pl = static_cast<int64_t>(t.s_proot_last[s]);
+        load8(t.s_proot + 8 * s, root);
+        have_raw = pn == n && pl == il[n - 1];
+      }
+      const bool have = want_root && bcast(L, have_raw) != 0;
       if (want_root && !have) merkle_inplace(L, lv, n);  // K09
       if (!L.leader()) return;
-      uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (have) load8(t.s_proot + 8 * s, root);
-      else if (want_root) load8(lv, root);
+      if (want_root && !have) load8(lv, root);
       for (int k = 0; k < 8; ++k) out64(r + 3 + k, root[k]);
       out64(r + 2, want_root ? 1u : 0u);
       if (close) {
-        const int64_t now = static_cast<int64_t>(c.a[3]);
-        t.s_state[s] = SS_TERMINATING;
-        t.s_terminated[s] = now;
         if (want_root) {  // CommitmentEngine.commit
           store8(t.s_root + 8 * s, root);
           t.s_committed[s] = now;
           t.s_commit_n[s] = static_cast<int32_t>(n);
-          mark_committed_participants(t, s);
         }
-        const int32_t rel = release_vsess(t, static_cast<int32_t>(static_cast<int64_t>(c.a[4])), now);  // K07
-        t.s_released[s] = rel;
-        t.s_retained[s] = static_cast<int32_t>(n - expired);  // EphemeralGC retention
         t.s_state[s] = SS_ARCHIVED;
         out64(r + 11, static_cast<uint64_t>(rel));
         out64(r + 12, static_cast<uint64_t>(expired));
