@@ -463,9 +463,13 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         turn1[delta_off[:-1][cnt_d > 0]] = True
     capl = caps.astype(np.int64)
     render_order = None
+    # (the multi-key orders below are one stable argsort over a packed int64 key —
+    # the same permutation as np.lexsort, at a fraction of its cost)
+    cap_desc = (int(capl.max()) - capl) if nd else capl  # ≥ 0, < 2^40 (record reservations)
+    t1_last = (~turn1).astype(np.int64) << 62
     if nd and _SP_ORDER & 2:
         nch = np.diff(np.asarray(ch_off_all, dtype=np.int64))
-        render_order = np.lexsort((-capl, -nch, ~turn1)).astype(np.int32)
+        render_order = np.argsort(t1_last | ((int(nch.max()) - nch) << 40) | cap_desc, kind="stable").astype(np.int32)
         rows_s, offs_s = st.reserve_deltas(caps[render_order])
         dr = np.empty(nd, dtype=np.int32)
         do = np.empty(nd, dtype=np.int64)
@@ -520,7 +524,7 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
     if _SP_PREFIX == "sorted" and nd:
         # prefix SHA lanes grouped by work: turn-1 records (hashed whole) first, then by
         # reserved size (∝ the blocks before the parent hole), so a wave's lanes finish together
-        tens["prefix_order"] = T(np.lexsort((-capl, ~turn1)).astype(np.int32))
+        tens["prefix_order"] = T(np.argsort(t1_last | cap_desc, kind="stable").astype(np.int32))
     if _SP_PREFIX != "chain":
         tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
         tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
