@@ -50,7 +50,9 @@ single-threaded Python pipeline rate — a capability ratio, not a like-for-like
 one; ``device_vs_baseline_p50`` compares like with like (one session, public
 API, same harness).
 
-Launch: ``python bench.py`` (1 GPU) or via ``torch.distributed.run`` for N GPUs.
+Launch: ``python bench.py`` (1 GPU); ``python bench.py --gpus N`` starts N rank
+processes itself (one per GPU, RCCL over xGMI; see :func:`launch_ranks`), and under
+``torch.distributed.run`` the launcher's ``WORLD_SIZE`` must equal ``--gpus``.
 """
 
 from __future__ import annotations
@@ -157,6 +159,60 @@ def _headline_kernel(n: int) -> str:
     return {2: "store_template_kernel<2,3>", 4: "store_template_kernel<4,2>"}.get(w, "store_template_kernel<3,3>")
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str], grace_s: float = 30.0) -> int:
+    """``bench.py --gpus N`` without a launcher: start N rank processes (one per GPU).
+
+    Runs in the parent BEFORE any GPU call (``torch.cuda.device_count()`` does not
+    initialise HIP on this image, nothing else here touches the device), and starts
+    every rank as a fresh child — the parent is never re-executed.  Each child gets
+    RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT as
+    ``torch.distributed.run`` would set them, inherits stdout (rank 0 prints the one
+    JSON line) and stderr.  If a rank fails, the others get ``grace_s`` to finish and
+    are then terminated (a peer blocked in a collective would otherwise wait for
+    ever).  Returns the worst exit code over the ranks (0 iff every rank succeeded).
+
+    The reference harness is single-process (bench_hypervisor.py:246-304); the
+    multi-rank launch is this framework's own (weak scaling, one process per GPU)."""
+    import subprocess
+
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port),
+                   AHV_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env, cwd=ROOT))
+    codes: dict[int, int] = {}
+    failed_at = None
+    while len(codes) < n:
+        for r, p in enumerate(procs):
+            if r not in codes and p.poll() is not None:
+                codes[r] = p.returncode
+                if p.returncode != 0 and failed_at is None:
+                    failed_at = time.monotonic()
+                    print(f"bench.py: rank {r} exited with {p.returncode}", file=sys.stderr, flush=True)
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for r, p in enumerate(procs):
+                if r not in codes:
+                    p.terminate()
+                    try:
+                        codes[r] = p.wait(10)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[r] = p.wait()
+        time.sleep(0.05)
+    bad = [c for c in codes.values() if c != 0]
+    return (max(bad, key=abs) if bad else 0)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -191,7 +247,18 @@ def main() -> None:
                     help="cpu runs the host twin of the kernel over gloo (multi-process CPU rehearsal)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # No launcher around us: start the N ranks ourselves (fresh children, before any
+        # GPU call in this process) and exit with the worst rank's code.
+        if args.device == "cuda" and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPUs are visible")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # under a launcher the job's world size IS the GPU count the run reports
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; the run would not measure N GPUs")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # AHV_BENCH_FORCE_DIST=1 (under torch.distributed.run) takes the multi-rank path
@@ -464,6 +531,11 @@ def main() -> None:
         pick = torch.randint(0, S, (args.verify_sessions,), generator=torch.Generator().manual_seed(99 + rank))
         # arena records, d_hash, s_head and s_root of the last timed step vs scalar render + hashlib
         verified = TT.check_sessions(tmpl, id_base, t0, last_launch["agents"], pick.numpy())
+    rccl_ranks = dist.get_world_size() if (multi and dev.type == "cuda" and dist.get_backend() == "nccl") else 0
+    if dev.type == "cuda" and args.gpus > 1 and rccl_ranks != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} ran over {rccl_ranks} RCCL ranks")
+    if multi and dist.get_world_size() != args.gpus:
+        raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     if rank == 0:
         total_sessions = S * world * args.steps
         value = total_sessions / elapsed
@@ -505,7 +577,9 @@ def main() -> None:
             "api": api,
             "last_step_counters": dict(zip(["sessions", "ok", "participants", "deltas", "commits", "archived"], totals)),
             "step_latency_hist_log2_us": {str(1 << b): c for b, c in enumerate(hist) if c},
-            "rccl_ranks": world if (multi and dev.type == "cuda") else 0,
+            "rccl_ranks": rccl_ranks,
+            "launcher": "bench.py (self-spawned ranks)" if os.environ.get("AHV_BENCH_SPAWNED") == "1"
+                        else ("external" if "WORLD_SIZE" in os.environ else "none (1 rank)"),
             "collective_backend": dist.get_backend() if multi else None,
             "collectives_per_step": {
                 "x04_counters_bytes": 48,

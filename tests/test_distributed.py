@@ -206,6 +206,49 @@ def test_bench_ranks_over_gloo(world):
     assert out["value"] > 0 and out["steps"] == 3 and out["warmup"] == 1
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_self_launches_ranks(world):
+    """``bench.py --gpus N`` with no launcher around it starts N rank processes by
+    itself (the driver's scaling command is exactly this): the JSON line reports N
+    ranks over the collective backend and N times the per-rank sessions."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", AHV_SKIP_AUTOBUILD="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--device", "cpu",
+           "--sessions", "256", "--agents", "2048", "--steps", "3", "--warmup", "1", "--no-scalar"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["config"]["parallelism"] == f"dp{world}"
+    assert out["collective_backend"] == "gloo" and out["launcher"].startswith("bench.py")
+    assert out["last_step_counters"]["sessions"] == 256 * world
+
+
+def test_bench_refuses_world_mismatch():
+    """Under a launcher, ``WORLD_SIZE`` must equal ``--gpus`` (a silent 1-rank run
+    reported as N GPUs is impossible)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", AHV_SKIP_AUTOBUILD="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--sessions", "64", "--agents", "256", "--steps", "1", "--warmup", "0", "--no-scalar"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in p.stderr
+
+
+def test_bench_launcher_reports_worst_rank_code():
+    """A failing rank fails the whole self-launched run (its peers are stopped)."""
+    import bench
+
+    env_keep = dict(os.environ)
+    try:
+        os.environ.pop("WORLD_SIZE", None)
+        code = bench.launch_ranks(2, ["--gpus", "2", "--device", "cpu", "--mix", "bogus"], grace_s=5.0)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_keep)
+    assert code != 0
+
+
 @pytest.mark.slow
 def test_bench_hetero_mix_over_gloo():
     """``bench.py --mix hetero`` at 2 ranks on the CPU twin: each rank re-runs its
