@@ -361,7 +361,7 @@ class Hypervisor:
             # the root; events go out only after the device's answer
             st.verify_deferred()
             seq = st._c.post(_d._st.OP_SESS_CLOSE, args, inl)
-            self._terminate_bookkeeping(session_id, sso, de, check[0] is not None and audit, check[1], n)
+            self._terminate_gc(session_id, sso, de, check[1], n)
             r = await st.result_async(seq, 13, 0)
         else:
             r = await st.call_async(_d._st.OP_SESS_CLOSE, args, 13, inl, spin_busy=0)
@@ -378,16 +378,14 @@ class Hypervisor:
         root = _d._hex(r[2:10]) if r[1] else None
         if v >= 0:  # every bond of the session is released now: freeze the records, reuse the edge rows
             self.vouching.retire_session(session_id)
-        if early:
-            self._terminate_events(session_id, root)
-            out = root
-            if int(r[11]) != check[1]:
-                err = _d._st.StoreError(f"device GC count {int(r[11])} of session {session_id} differs from the "
-                                        f"host prediction {check[1]}")
-                sso._poisoned = err
-                raise err
-        else:
-            out = self._terminated(session_id, sso, de, root, int(r[11]), n)
+        # validate before publishing: a terminate whose device answer disagrees with
+        # the host's view raises with nothing registered and no event emitted (the
+        # commitment engine holds no record of a poisoned session)
+        if early and int(r[11]) != check[1]:
+            err = _d._st.StoreError(f"device GC count {int(r[11])} of session {session_id} differs from the "
+                                    f"host prediction {check[1]}")
+            sso._poisoned = err
+            raise err
         if check is not None and audit and check[0] != root:
             # the device committed its own root; the host's view of this chain (the
             # digests it rendered and predicted) disagrees with it: the session is
@@ -397,7 +395,12 @@ class Hypervisor:
                                     f"prediction {check[0]}")
             sso._poisoned = err
             raise err
-        return out
+        if early:
+            if root is not None:
+                self.commitment.register(sso)
+            self._terminate_events(session_id, root)
+            return root
+        return self._terminated(session_id, sso, de, root, int(r[11]), n)
 
     def _terminated(self, session_id: str, sso, de, root: Optional[str], expired: int, n: int) -> Optional[str]:
         """Host bookkeeping after a device close: commitment, GC, events."""
@@ -406,9 +409,13 @@ class Hypervisor:
         return root
 
     def _terminate_bookkeeping(self, session_id: str, sso, de, committed: bool, expired: int, n: int) -> None:
-        """Commitment record and GC of a device close (no device answer needed)."""
+        """Commitment record and GC of a device close."""
         if committed:
             self.commitment.register(sso)
+        self._terminate_gc(session_id, sso, de, expired, n)
+
+    def _terminate_gc(self, session_id: str, sso, de, expired: int, n: int) -> None:
+        """GC of a device close's host views (no device answer needed)."""
         # the device counts the deltas past retention (result word 12); with none
         # expired the host GC has nothing to prune and needs no walk over the views
         # a VFS nothing ever built holds no files: the collector has nothing to purge

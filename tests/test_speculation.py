@@ -446,3 +446,42 @@ def test_awaited_terminate_raises_on_a_divergent_chain(dev, monkeypatch):
         assert await hv.terminate_session(m2.sso.session_id) == m2.delta_engine.deltas[0].device_hash()
 
     _run(go())
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+def test_a_failing_terminate_publishes_nothing(dev, monkeypatch):
+    """A device-awaited terminate validates before it publishes: the
+    root divergence raises with no ``SESSION_TERMINATED`` / ``AUDIT_COMMITTED`` on the
+    bus and no commitment registered for the poisoned session."""
+    from hypervisor import _device as D
+    from hypervisor.observability.event_bus import EventType, HypervisorEventBus
+
+    monkeypatch.setattr(D, "_SPEC_TERMINATE", False)
+
+    async def go():
+        bus = HypervisorEventBus()
+        hv = Hypervisor(device=dev, event_bus=bus)
+        m = await hv.create_session(SessionConfig(enable_audit=True), "did:admin")
+        sid = m.sso.session_id
+        await hv.join_session(sid, "did:a", sigma_raw=0.8)
+        await hv.activate_session(sid)
+        m.delta_engine.capture("did:a", [VFSChange(path="/f", operation="add", content_hash="h")])
+        m.delta_engine.deltas[0].__dict__["_pred"] = "0" * 64
+        m.delta_engine.capture("did:a", [VFSChange(path="/g", operation="add", content_hash="i")])
+        with pytest.raises(StoreError, match="differs from the host prediction"):
+            await hv.terminate_session(sid)
+        kinds = [e.event_type for e in bus.query_by_session(sid)]
+        assert EventType.SESSION_TERMINATED not in kinds and EventType.AUDIT_COMMITTED not in kinds
+        assert hv.commitment.get_commitment(sid) is None and m.sso._poisoned is not None
+        # a healthy session publishes both after its device root
+        m2 = await hv.create_session(SessionConfig(enable_audit=True), "did:admin")
+        sid2 = m2.sso.session_id
+        await hv.join_session(sid2, "did:a", sigma_raw=0.8)
+        await hv.activate_session(sid2)
+        m2.delta_engine.capture("did:a", [VFSChange(path="/f", operation="add", content_hash="h")])
+        root = await hv.terminate_session(sid2)
+        kinds = [e.event_type for e in bus.query_by_session(sid2)]
+        assert EventType.SESSION_TERMINATED in kinds and EventType.AUDIT_COMMITTED in kinds
+        assert hv.commitment.get_commitment(sid2).merkle_root == root
+
+    _run(go())
