@@ -126,10 +126,13 @@ def evict(hv, session_ids: list) -> int:
         ce = hv.commitment
         getattr(ce, "_device", {}).pop(sid, None)
         getattr(ce, "_commitments", {}).pop(sid, None)
-    for kind, seg in list(hv._sessions.segments()):  # unbuilt batch sessions dropped above: released now
-        if kind != "own" and seg.dead:
+    # unbuilt batch sessions dropped above: released now — every batch, including one
+    # this eviction emptied (segments() no longer lists it, its dead rows still wait)
+    for seg in hv._sessions.batches():
+        if seg.dead:
             seg.release(np.asarray(seg.dead, dtype=np.int64))
             seg.dead = []
+    hv._sessions.prune_batches()
     hv._sessions.forget_sagas(saga_rows)
     _evict_vouches(hv, ids)
     return n

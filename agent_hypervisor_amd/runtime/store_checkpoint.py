@@ -895,7 +895,8 @@ def restore(hv, cols: dict, host: dict, arena, meta: dict, verify: str = "host",
         W[name] = (tslots, Tt[f"T.{name}"])
     st.write_columns(W)
     if verify == "device" and n:
-        _verify_on_device(st, slots, drows, doff, committed_h, ids_all, si)
+        cn = np.where(committed_h != 0, hs("S.s_commit_n", si), 0).astype(np.int64) if n else np.zeros(0, np.int64)
+        _verify_on_device(st, slots, drows, doff, committed_h, ids_all, si, cn)
     # -- lazy registration ----------------------------------------------------------------------
     b = RestoredBatch()
     b.store = st
@@ -945,9 +946,13 @@ def _as_np(v) -> np.ndarray:
     return v.cpu().numpy() if isinstance(v, torch.Tensor) else v
 
 
-def _verify_on_device(st, slots, drows, doff, committed, ids, si) -> None:
+def _verify_on_device(st, slots, drows, doff, committed, ids, si, commit_n=None) -> None:
     """K10 over the written rows (records re-hashed in the arena, parent links) and
-    K09 over the committed chains, on the store's device."""
+    K09 over the committed chains, on the store's device.  A commitment covers the
+    first ``s_commit_n`` deltas of its chain (the reference's ``capture`` has no state
+    check, so a terminated session can gain deltas afterwards): the root is
+    recomputed over that prefix, the same rule as the host path
+    (``verify_chain_records(..., commit_n)``)."""
     from agent_hypervisor_amd.ops.store_views import store_roots, verify_store_chains
 
     chains = [drows[int(doff[i]):int(doff[i + 1])].tolist() for i in range(len(slots))]
@@ -958,7 +963,8 @@ def _verify_on_device(st, slots, drows, doff, committed, ids, si) -> None:
         raise CheckpointError(f"session {ids[si[k]]}: audit chain fails re-verification after the move")
     c = np.flatnonzero(committed != 0)
     if len(c):
-        roots = store_roots(st, [chains[i] for i in c.tolist()]).cpu().numpy()
+        cut = [chains[i] if commit_n is None else chains[i][:int(commit_n[i])] for i in c.tolist()]
+        roots = store_roots(st, cut).cpu().numpy()
         want = st.gather({"s_root": (slots[c][:, None] * 8 + np.arange(8)[None, :]).reshape(-1)})["s_root"]
         if not np.array_equal(roots.reshape(-1).astype(np.int64) & 0xFFFFFFFF,
                               want.astype(np.int64) & 0xFFFFFFFF):

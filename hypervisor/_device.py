@@ -1677,11 +1677,14 @@ def close_hypervisor(hv) -> int:
     # for them (a divergence of a speculated post goes to its session, now closed).
     n = 0
     acc = ([], [], [], [])
-    for kind, seg in list(hv._sessions.segments()):
-        if kind == "own":
-            for m in seg:
-                _close_views(st, m, acc)
-                n += 1
+    own = hv._sessions._own
+    for seg in list(hv._sessions._segs):  # every segment, including emptied batches (their dead rows)
+        if isinstance(seg, list):
+            for sid in seg:
+                m = own.get(sid)
+                if m is not None:
+                    _close_views(st, m, acc)
+                    n += 1
             continue
         for m in list(seg.views.values()):
             _close_views(st, m, acc)

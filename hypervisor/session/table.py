@@ -143,6 +143,20 @@ class SessionTable:
             elif seg.index:
                 yield "batch", seg
 
+    def batches(self) -> list:
+        """Every batch segment, including batches whose sessions have all left the
+        table (their unbuilt rows may still wait in ``dead`` for release)."""
+        return [seg for seg in self._segs if not isinstance(seg, list)]
+
+    def prune_batches(self) -> None:
+        """Drop batch segments with no session left in the table and no built view
+        (call after their ``dead`` rows were released)."""
+        keep = [seg for seg in self._segs if isinstance(seg, list) or seg.index or seg.views]
+        for seg in self._segs:
+            if not isinstance(seg, list) and not (seg.index or seg.views):
+                self._bcache.pop(id(seg), None)
+        self._segs = keep
+
     def batch_of(self, sid) -> Optional[object]:
         return self._lazy.get(sid)
 

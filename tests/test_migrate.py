@@ -91,3 +91,61 @@ def test_sessions_move_between_stores_with_identical_answers(dev):
         return True
 
     assert asyncio.run(go())
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_evicting_a_whole_unbuilt_batch_returns_its_rows(dev):
+    """a batch whose sessions all leave unbuilt is no longer listed by
+    ``segments()``; its dropped rows must still come back (evict and close)."""
+    async def go():
+        a = Hypervisor(store=GovernanceStore(dev))
+        b = Hypervisor(store=GovernanceStore(dev))
+        base = dict(a._store.live_rows())
+        run = await a.run_pipelines(PipelineSpec(), 50)
+        sids = list(run.session_ids)
+        buf, host = MG.pack(a, sids)
+        MG.unpack(b, buf, host, verify="device")
+        assert MG.evict(a, sids) == 50
+        a._store.verify_deferred(block=True)
+        a._store.reclaim()
+        assert dict(a._store.live_rows()) == base
+        # close() of a hypervisor holding an emptied batch with dead rows
+        c = Hypervisor(store=GovernanceStore(dev))
+        cst = c._store
+        base_c = dict(cst.live_rows())
+        run = await c.run_pipelines(PipelineSpec(), 20)
+        for sid in run.session_ids:
+            c._sessions.pop(sid)
+        c.close()
+        cst.verify_deferred(block=True)
+        cst.reclaim()
+        assert dict(cst.live_rows()) == base_c
+        return True
+
+    assert asyncio.run(go())
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_a_session_captured_after_terminate_migrates(dev):
+    """the device root check covers the first ``s_commit_n`` deltas (what
+    the commitment covers), like the host check, so a delta captured after
+    terminate does not fail the move."""
+    async def go():
+        a = Hypervisor(store=GovernanceStore(dev))
+        b = Hypervisor(store=GovernanceStore(dev))
+        m = await a.create_session(SessionConfig(), "did:admin")
+        sid = m.sso.session_id
+        await a.join_session(sid, "did:a", sigma_raw=0.8)
+        await a.activate_session(sid)
+        m.delta_engine.capture("did:a", [VFSChange(path="/f", operation="add", content_hash="h")])
+        root = await a.terminate_session(sid)
+        m.delta_engine.capture("did:a", [VFSChange(path="/g", operation="add", content_hash="i")])
+        before = answers(a, [sid])
+        buf, host = MG.pack(a, [sid])
+        MG.unpack(b, buf, host, verify="device")
+        MG.evict(a, [sid])
+        after = answers(b, [sid])
+        assert before == after and b.commitment.get_commitment(sid).merkle_root == root
+        return True
+
+    assert asyncio.run(go())
