@@ -204,15 +204,34 @@ def exchange(hv, plan: dict, rank: int, members: list, ctrl_group=None, data_gro
     got = []
     ho = do = 0
     hr = hrecv.numpy().tobytes()
-    for j in range(k):
-        hn, dn = int(r_in[j, 0]), int(r_in[j, 1])
-        if hn:
-            b = unpack(hv, drecv[do:do + dn], hr[ho:ho + hn], verify=verify)
-            if b is not None:
-                got.extend(b.ids)
-        ho += hn
-        do += dn
-    return got
+    err = None
+    try:
+        for j in range(k):
+            hn, dn = int(r_in[j, 0]), int(r_in[j, 1])
+            if hn:
+                b = unpack(hv, drecv[do:do + dn], hr[ho:ho + hn], verify=verify)
+                if b is not None:
+                    got.extend(b.ids)
+            ho += hn
+            do += dn
+    except Exception as e:  # noqa: BLE001 - reported to every member below
+        err = e
+    # acknowledgement round: the move commits only if every receiver registered
+    # everything it was sent; otherwise every receiver undoes what it registered and
+    # every member raises, so senders keep their sessions and routes stay unchanged
+    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=ctrl_group)
+    if int(ok) == 1:
+        return got
+    if got:
+        evict(hv, got)
+    if err is not None:
+        raise MigrationError(f"rank {rank}: receiving migrated sessions failed: {err}") from err
+    raise MigrationError(f"rank {rank}: another member failed to receive its sessions; the move was undone")
+
+
+class MigrationError(RuntimeError):
+    """A migration that did not commit on every member (nothing moved)."""
 
 
 def all_gather_json(obj, world: int, group=None) -> list:
@@ -252,4 +271,4 @@ def balance_plan(loads: list, members: list) -> list:
     return out
 
 
-__all__ = ["pack", "unpack", "evict", "exchange", "all_gather_json", "balance_plan"]
+__all__ = ["pack", "unpack", "evict", "exchange", "all_gather_json", "balance_plan", "MigrationError"]

@@ -1150,12 +1150,36 @@ class ShardedHypervisor:
         from agent_hypervisor_amd.runtime.checkpoint import save_hypervisor
 
         meta = {"rank": self.rank, "vouch_key": {k: list(v) for k, v in self._vouch_key.items()},
-                "sagas": self._sagas}
+                "sagas": self._sagas, "moved": self._moved, "members": self.members}
         d = save_hypervisor(self.local, os.path.join(root, f"rank{self.rank}"),
                             extra_files={"sharded.json": json.dumps(meta)})
         if self.world > 1:
             dist.barrier(group=self.group)
         return d
+
+    def restore(self, root: str) -> int:
+        """Collective: every rank re-loads its own ``root/rank<r>`` checkpoint (audit
+        chains re-verified) and the job's routing state saved with it — saga homes,
+        global vouch order keys and the routes of migrated sessions, so a session
+        moved by :meth:`rebalance` / :meth:`retire` before the checkpoint still
+        resolves to the rank that holds its rows.  Returns the sessions loaded here."""
+        from agent_hypervisor_amd.runtime.checkpoint import load_hypervisor
+
+        src = os.path.join(root, f"rank{self.rank}")
+        n0 = len(self.local._sessions)
+        load_hypervisor(src, hv=self.local)
+        meta = os.path.join(src, "sharded.json")
+        if os.path.exists(meta):
+            with open(meta) as fh:
+                m = json.load(fh)
+            self._sagas.update(m.get("sagas", {}))
+            for vid, key in m.get("vouch_key", {}).items():
+                self._vouch_key.setdefault(vid, tuple(key))
+            self._moved.update({k: int(v) for k, v in m.get("moved", {}).items()})
+        self._agent_ix_n = -1
+        if self.world > 1:
+            dist.barrier(group=self.group)
+        return len(self.local._sessions) - n0
 
     async def failover(self, failed: list[int], root: str) -> list[tuple[str, int, int]]:
         """Survivors (every remaining member calls this): drop the failed ranks,
@@ -1190,6 +1214,8 @@ class ShardedHypervisor:
                 self._sagas.update({g: s for g, s in m.get("sagas", {}).items() if s in mine_set})
                 for vid, key in m.get("vouch_key", {}).items():
                     self._vouch_key.setdefault(vid, tuple(key))
+                for k, v in m.get("moved", {}).items():  # routes of migrated ids (same on every rank)
+                    self._moved.setdefault(k, int(v))
         # only the survivors synchronise on these groups (the failed ranks never call in);
         # a view collective still blocked on the old group stays on the old thread, and the
         # next view gets a fresh communication thread bound to the new groups

@@ -896,7 +896,18 @@ def restore(hv, cols: dict, host: dict, arena, meta: dict, verify: str = "host",
     st.write_columns(W)
     if verify == "device" and n:
         cn = np.where(committed_h != 0, hs("S.s_commit_n", si), 0).astype(np.int64) if n else np.zeros(0, np.int64)
-        _verify_on_device(st, slots, drows, doff, committed_h, ids_all, si, cn)
+        try:
+            _verify_on_device(st, slots, drows, doff, committed_h, ids_all, si, cn)
+        except Exception:
+            # nothing was registered: the rows written for the refused image go back
+            st.release_many("S", slots)
+            if nd:
+                st.release_many("D", drows)
+            if ng:
+                st.release_many("G", gslots)
+            if nt:
+                st.release_many("T", tslots)
+            raise
     # -- lazy registration ----------------------------------------------------------------------
     b = RestoredBatch()
     b.store = st

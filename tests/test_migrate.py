@@ -149,3 +149,63 @@ def test_a_session_captured_after_terminate_migrates(dev):
         return True
 
     assert asyncio.run(go())
+
+
+def _atomic_worker(rank: int, world: int, root: str, q) -> None:
+    import os
+
+    os.environ.update(OMP_NUM_THREADS="1")
+    import torch.distributed as dist
+
+    from agent_hypervisor_amd.runtime import store_checkpoint as SC
+
+    dist.init_process_group("gloo", init_method=f"file://{os.path.join(root, 'pg')}", rank=rank, world_size=world)
+
+    async def go():
+        hv = Hypervisor(store=GovernanceStore("cpu"))
+        base = dict(hv._store.live_rows())
+        sids, before = [], None
+        if rank == 0:
+            sids = await build(hv)
+            before = answers(hv, sids)
+        else:
+            def refuse(*a, **k):
+                raise SC.CheckpointError("forced re-verification failure")
+
+            SC._verify_on_device = refuse  # this receiver refuses what it is sent
+        raised = None
+        try:
+            MG.exchange(hv, {1: sids} if rank == 0 else {}, rank, [0, 1])
+        except MG.MigrationError as e:
+            raised = str(e)
+        if rank == 0:
+            assert raised is not None and "another member" in raised
+            assert answers(hv, sids) == before and len(hv._sessions) == len(sids)
+        else:
+            assert raised is not None and "forced re-verification failure" in raised
+            hv._store.verify_deferred(block=True)
+            hv._store.reclaim()
+            assert dict(hv._store.live_rows()) == base and len(hv._sessions) == 0
+        return True
+
+    ok = asyncio.run(go())
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_a_failed_receiver_undoes_the_whole_move(tmp_path):
+    """migration commits only when every receiver registered what it was
+    sent (an acknowledgement all-reduce before eviction).  A receiver whose device
+    re-verification fails returns the rows it wrote; the sender keeps every session
+    with unchanged answers; every member raises ``MigrationError``."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_atomic_worker, args=(r, 2, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True} and all(p.exitcode == 0 for p in procs)

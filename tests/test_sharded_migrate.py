@@ -98,6 +98,22 @@ def _worker(rank: int, world: int, root: str, q) -> None:
         else:
             await wait_key("mig/phase2")
         retired = None
+        if world == 2:
+            # checkpoint after the rebalance, then restore the job into fresh state: the
+            # migrated sessions' routes come back with the rows
+            from hypervisor import Hypervisor
+
+            ck = os.path.join(root, "ck")
+            shv.checkpoint(ck)
+            shv.local = Hypervisor(device="cpu")
+            shv.bus = shv.local.event_bus
+            shv._moved.clear()
+            shv._sagas.clear()
+            shv.restore(ck)
+            if rank == 0:
+                after_restore = await answers(shv, sids)
+                res = dict(same_restore=after_restore == before,
+                           diff_restore=[k for k in before if before[k] != after_restore[k]])
         if world > 2:
             leaver = world - 1
             retired = shv.retire(leaver)
@@ -144,6 +160,8 @@ def test_rebalance_and_retire_move_sessions_with_identical_answers(tmp_path, wor
     assert res["moved"]["sent"] == N - N // world
     assert max(res["load1"]) - min(res["load1"]) <= 1 and sum(res["load1"]) == N
     assert all(ok and n > 0 for ok, n in res["audits"]), res["audits"]
+    if world == 2:
+        assert res["same_restore"], res["diff_restore"]
     if world > 2:
         assert res["same2"]
         assert res["load2"][world - 1] == 0 and sum(res["load2"]) == N
