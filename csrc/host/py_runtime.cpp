@@ -537,8 +537,9 @@ namespace pack {
 
 inline bool ascii_view(PyObject* o, std::string_view& out) {
   if (!PyUnicode_CheckExact(o) || !PyUnicode_IS_COMPACT_ASCII(o)) return false;
-  const PyASCIIObject* a = reinterpret_cast<const PyASCIIObject*>(o);
-  out = std::string_view(reinterpret_cast<const char*>(a + 1), static_cast<size_t>(a->length));
+  // PyUnicode_DATA / GET_LENGTH read the object's own fields on every version (no
+  // allocation; the compact-ASCII data offset moved when 3.12 dropped wstr)
+  out = std::string_view(static_cast<const char*>(PyUnicode_DATA(o)), static_cast<size_t>(PyUnicode_GET_LENGTH(o)));
   return true;
 }
 
@@ -566,6 +567,14 @@ inline bool seq(PyObject* o, PyObject* const*& it, Py_ssize_t& n) {
 
 inline bool small_int(PyObject* o, int64_t& v) {
   if (!PyLong_CheckExact(o)) return false;
+#if PY_VERSION_HEX >= 0x030C0000
+  // 3.12 replaced ob_size / ob_digit with lv_tag; the unstable compact accessors
+  // are inline reads of that layout (no allocation, no error state)
+  PyLongObject* l = reinterpret_cast<PyLongObject*>(o);
+  if (!PyUnstable_Long_IsCompact(l)) return false;
+  v = static_cast<int64_t>(PyUnstable_Long_CompactValue(l));
+  return true;
+#else
   const Py_ssize_t sz = Py_SIZE(o);
   if (sz == 0) {
     v = 0;
@@ -575,6 +584,7 @@ inline bool small_int(PyObject* o, int64_t& v) {
   v = static_cast<int64_t>(reinterpret_cast<PyLongObject*>(o)->ob_digit[0]);
   if (sz < 0) v = -v;
   return true;
+#endif
 }
 
 inline bool number(PyObject* o, double& v) {
@@ -821,15 +831,31 @@ static int pack_threads_default() {
   return v;
 }
 
+// The GIL-free walk reads instance dicts through _PyObject_GetDictPtr.  Up to 3.10
+// that only returns the slot; from 3.11 objects keep "managed" inline values and the
+// call MATERIALISES a dict (allocates and stores into the object) — never allowed
+// off the GIL thread.  So the parallel walk exists only where it is read-only.
+#if PY_VERSION_HEX < 0x030B0000
+#define AHV_PARALLEL_SPEC_WALK 1
+#else
+#define AHV_PARALLEL_SPEC_WALK 0
+#endif
+
+static const char* g_last_walk = "none";  // "serial" / "parallel" / "parallel->serial" (tests, profiling)
+
 // threads: < 0 → AHV_PACK_THREADS or min(16, cores) for batches of ≥ 4,096 specs;
-// 0 / 1 → the serial walk.
+// 0 / 1 → the serial walk (always, on Python ≥ 3.11).
 static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool& pool, const py::object& cfg_of,
                            int64_t fixed, int threads) {
   const size_t n = specs.size();
   int T = threads;
   if (T < 0) T = n >= 4096 ? pack_threads_default() : 1;
   if (T > 64) T = 64;
-  if (T <= 1 || n < static_cast<size_t>(2 * T)) return pack_specs_serial(specs, agents, pool, cfg_of, fixed);
+  if (!AHV_PARALLEL_SPEC_WALK || T <= 1 || n < static_cast<size_t>(2 * T)) {
+    g_last_walk = "serial";
+    return pack_specs_serial(specs, agents, pool, cfg_of, fixed);
+  }
+  g_last_walk = "parallel";
   static const py::str kJoins("joins"), kDeltas("deltas"), kSteps("steps"), kAct("activate"), kTerm("terminate"),
       kComp("compensate"), kCfg("config"), kCreator("creator_did");
   for (const py::str* nm : {&kJoins, &kDeltas, &kSteps, &kAct, &kTerm, &kComp, &kCfg, &kCreator, &cfg_name(0),
@@ -881,6 +907,7 @@ static py::dict pack_specs(const py::list& specs, StringPool& agents, StringPool
   for (const auto& p : parts)
     if (!p.ok) {
       if (std::getenv("AHV_PACK_DEBUG")) std::fprintf(stderr, "[pack] serial walk: part fell back at line %d\n", p.bad_line);
+      g_last_walk = "parallel->serial";
       return pack_specs_serial(specs, agents, pool, cfg_of, fixed);
     }
   // ---- merge: (1) with the GIL, intern each part's strings in first-occurrence
@@ -1170,6 +1197,9 @@ void register_runtime(py::module_& m) {
         py::arg("fixed"), py::arg("threads") = -1,
         "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py); threads: < 0 auto "
         "(AHV_PACK_THREADS), 1 serial");
+  m.def("pack_walk_info", [] {
+    return py::make_tuple(static_cast<bool>(AHV_PARALLEL_SPEC_WALK), std::string(g_last_walk));
+  }, "(parallel walk compiled in for this Python, the last pack_specs call's walk)");
   m.def("iso_from_us", &iso_from_us, "datetime.isoformat() text of an epoch-µs UTC instant");
   m.def("uuids_from_counters", &uuids_from_counters, py::arg("seed"), py::arg("base"), py::arg("n"),
         py::arg("prefix") = std::string(), "uuid_from_counter(seed, base + i, prefix) for i < n");

@@ -310,3 +310,28 @@ def test_parallel_spec_walk_packs_the_serial_columns(threads):
 
     mixed = specs[:100] + [Odd()] + specs[100:200]
     assert all(pack(mixed, threads)[0][k] == pack(mixed, 1)[0][k] for k in ref[0])
+
+
+def test_spec_walk_is_version_guarded():
+    """the GIL-free walk reads instance dicts through
+    ``_PyObject_GetDictPtr``, which materialises (allocates) a dict on Python ≥ 3.11;
+    the extension compiles it in only below 3.11 and takes the serial walk otherwise,
+    and the forced serial walk gives the parallel walk's columns and pool ids."""
+    import sys
+
+    from agent_hypervisor_amd._native import C
+    from agent_hypervisor_amd.models import store_pipeline as SP
+
+    rng = random.Random(3)
+    specs = [random_spec(rng) for _ in range(2000)]
+
+    def pack(th):
+        a, p = C.StringPool(), C.StringPool()
+        out = C.pack_specs(specs, a, p, lambda c: (4, 0.5, 1), SP._FIXED, th)
+        return out, [a.str(i) for i in range(len(a))], [p.str(i) for i in range(len(p))], C.pack_walk_info()[1]
+
+    compiled, _ = C.pack_walk_info()
+    assert compiled == (sys.version_info < (3, 11))
+    ser, par = pack(1), pack(4)
+    assert ser[3] == "serial" and par[3] == ("parallel" if compiled else "serial")
+    assert ser[1] == par[1] and ser[2] == par[2] and all(ser[0][k] == par[0][k] for k in ser[0])
