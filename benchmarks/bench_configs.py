@@ -8,9 +8,11 @@
            cross-session vouch exposure all-reduce (X01, [A] fp64 over RCCL)
   config4  saga orchestrator: 10-step compensation chains, fused kernel and
            the hipGraph-captured step loop
-  config5  liability slash storm: 10M vouch-bond updates (K06 cascade, bonds
-           released) + σ_eff recompute + full delta re-chain (K08) and Merkle
-           roots (K09) of the affected sessions
+  config5  liability slash storm: every session slashed (K06 cascade) and its
+           remaining bonds released (K07) — all 10M resident bonds change
+           state, device-counted — + σ_eff recompute + full delta re-chain (K08)
+           and Merkle roots (K09) of every session; config5_subset: the 10 %
+           storm with only the touched sessions re-chained
 
 Each prints one JSON line per measurement.  ``--device cpu`` runs the host
 twins at small scale (harness check).  Multi-rank: launch with
@@ -402,21 +404,45 @@ class AuditArena:
         }, touched
 
 
+def storm_counts(out, released: torch.Tensor) -> torch.Tensor:
+    """[bond updates by slash clips, bond updates by the session release] as one
+    device int64 pair (no host sync): every clip releases its bond (the reference
+    ``SlashingEngine.slash`` calls ``release_bond`` per clip, slashing.py:93-112),
+    and K07 releases each session's remaining active bonds
+    (``release_session_bonds``, vouching.py:176-184)."""
+    return torch.stack([out.clip_count.sum(dtype=i64), released.sum(dtype=i64)])
+
+
 def config5(ctx: Ctx, args):
+    """BASELINE config 5 as stated: "Liability slash storm: 10M bond updates + full
+    Merkle re-chain".  Every session is slashed (storm fraction 1.0: one vouchee per
+    session, cascades included) and then has its remaining bonds released, so every
+    one of the 10M resident edges changes state; every session gets its slash delta
+    and its WHOLE chain is re-hashed and Merkle-rooted.  The bond-update count is
+    the device's (clip counts + K07 release counts), not the resident edge count.
+    ``--storm-fraction f < 1`` gives the secondary storm over a session subset with
+    only the touched sessions re-chained (the round-5 measurement)."""
+    frac = args.storm_fraction
+    _storm(ctx, args, frac, rechain_all=frac >= 1.0, release_all=frac >= 1.0)
+
+
+def _storm(ctx: Ctx, args, frac: float, rechain_all: bool, release_all: bool):
     E_total = args.edges or 10_000_000
     per = 16
     S = E_total // per
     vb0 = random_vouch_batch(S, per, ctx.dev, seed=5)
     g = torch.Generator().manual_seed(9)
-    # the storm hits a random subset of the sessions; the others keep target 255 (no slash)
+    # the storm hits a random subset of the sessions (all of them at fraction 1.0);
+    # the others keep target 255 (no slash)
     tgt = torch.full((S,), 255, dtype=u8)
-    hit = torch.randperm(S, generator=g)[: max(1, int(S * args.storm_fraction))]
+    hit = torch.randperm(S, generator=g)[: max(1, int(round(S * frac)))]
     tgt[hit] = torch.randint(0, 16, (hit.numel(),), generator=g, dtype=u8)
     tgt = tgt.to(ctx.dev)
     omega = torch.full((S,), 0.95, dtype=f64, device=ctx.dev)
     scores0 = torch.rand((S, 16), generator=g, dtype=f64).to(ctx.dev)
     D = args.deltas or 3
     arena = AuditArena(S, D, ctx.dev)
+    every = torch.arange(S, dtype=i64, device=ctx.dev)
     last = {}
     # Every storm starts from the same resident state.  The slash mutates only
     # `active`, `released_us` and the scores, so one fresh copy of those per storm
@@ -429,13 +455,18 @@ def config5(ctx: Ctx, args):
         vb = LI.VouchBatch(vb0.offsets, vb0.voucher, vb0.vouchee, vb0.bonded, active, vb0.expiry_us, released)
         # ≤ 1 clip per edge; σ_eff over the post-slash bonds fused into the same pass (K06+K03)
         out = LI.slash(vb, tgt, omega, scores, 1, clip_cap=per, zero_records=False, with_sigma_eff=not args.unfused,
-                       with_touched=True)
+                       with_touched=not rechain_all)
         se = out.sigma_eff if not args.unfused else LI.sigma_eff_exact(vb, out.scores, omega, 1)
-        # re-chain exactly the sessions the slash touched, after it (data dependency):
-        # each gets a slash delta carrying its post-slash scores, then its whole
-        # chain is re-hashed (K08) and its Merkle root recomputed (K09); the touched
-        # list comes compacted from the cascade kernel (one 8-byte count read)
-        touched = out.touched
+        if release_all:  # K07: the storm's sessions end — every bond still active is released
+            rel = LI.release_bonds(vb, 2)
+        else:
+            rel = torch.zeros(1, dtype=i32, device=ctx.dev)
+        last["counts"] = storm_counts(out, rel)
+        # re-chain after the slash (data dependency): each session gets a slash delta
+        # carrying its post-slash scores, then its whole chain is re-hashed (K08) and
+        # its Merkle root recomputed (K09) — every session, or (subset storm) the ones
+        # the slash touched, compacted on the device (one 8-byte count read)
+        touched = every if rechain_all else out.touched
         arena.write_slash_deltas(touched, out.scores)
         packed, sel = arena.resident(touched)
         digests = A.chain_hashes(packed, midstate=not args.no_midstate, uniform_len=D + 1, sel=sel, check=False)
@@ -445,16 +476,38 @@ def config5(ctx: Ctx, args):
 
     el, lat = ctx.timed(step, args.steps, args.warmup)
     T = int(last["T"])
-    rechain_bytes = T * (arena.L + arena.Ls) + T * (D + 1) * 32 * 2 + T * 16 * 8
-    slash_bytes = S * per * (1 + 1 + 1 + 8 + 8) + S * 16 * 8 * 3 + S * 4
-    ctx.emit(config="config5", what="slash storm on a session subset + sigma_eff + re-chain/merkle of the "
-                                    "touched sessions", bond_edges=S * per, sessions=S,
-             sessions_slashed=int(hit.numel()), sessions_touched=T, deltas_rechained=T * (D + 1),
+    by_slash, by_release = (int(x) for x in last["counts"].cpu().tolist())
+    updates = by_slash + by_release
+    ms = el / args.steps * 1e3
+    # HBM traffic per storm (bytes, lower bound: each array touched once)
+    slash_bytes = S * per * (1 + 1 + 2 + 8 + 8 + 8) + S * 16 * 8 * 2 + S * 16 * 8 + S * 4
+    release_bytes = (S * per * (2 + 8 + 8) + S * 8) if release_all else 0
+    rechain_bytes = T * (arena.L + 2 * arena.pitch) + T * (D + 1) * 32 * 2 + T * 32 + T * 16 * 8
+    hbm = slash_bytes + release_bytes + rechain_bytes
+    # SHA-256 compressions on the re-chain path (records + Merkle nodes)
+    blocks_per_chain = int(sum((int(x) + 9 + 63) // 64 for x in (arena.pre_len[0] + arena.suf_len[0]).tolist())) \
+        + 2 * max(1, D)  # ~2 blocks per Merkle node (hex-pair message), D nodes for D+1 leaves
+    ctx.emit(config="config5" if rechain_all else "config5_subset",
+             what=("slash storm over every session (all bonds clipped or released) + sigma_eff + full re-chain/"
+                   "Merkle of every session" if rechain_all else
+                   "slash storm on a session subset + sigma_eff + re-chain/merkle of the touched sessions"),
+             bond_edges_resident=S * per, sessions=S, storm_fraction=frac,
+             sessions_slashed=int(hit.numel()), bond_updates=updates, bond_updates_by_slash=by_slash,
+             bond_updates_by_release=by_release, sessions_rechained=T, deltas_rechained=T * (D + 1),
              arena_bytes_resident=int(arena.bytes.numel()), distinct_payloads=True,
              state_reset="one pre-made copy of (active, released_us, scores) per storm, made before timing",
-             hbm_bytes_est=dict(slash_sigma=slash_bytes, rechain=rechain_bytes),
-             ms_per_storm=el / args.steps * 1e3, storm_p50_ms=statistics.median(lat) * 1e3,
-             bond_updates_per_s=S * per * ctx.world * args.steps / el)
+             hbm_bytes_est=dict(slash_sigma=slash_bytes, release=release_bytes, rechain=rechain_bytes, total=hbm),
+             hbm_roofline_ms=round(hbm / 8.0e12 * 1e3, 4), hbm_achieved_tb_s=round(hbm / (ms * 1e-3) / 1e12, 3),
+             sha_compressions_est=T * blocks_per_chain,
+             ms_per_storm=ms, storm_p50_ms=statistics.median(lat) * 1e3,
+             bond_updates_per_s=updates * ctx.world / (ms * 1e-3),
+             sessions_rechained_per_s=T * ctx.world / (ms * 1e-3))
+
+
+def config5_subset(ctx: Ctx, args):
+    """Secondary config-5 line: the storm over ``--subset-fraction`` (10 %) of the
+    sessions, only the touched sessions re-chained (no session release)."""
+    _storm(ctx, args, args.subset_fraction, rechain_all=False, release_all=False)
 
 
 # ------------------------------------------------------------------ config 2 (public API)
@@ -484,7 +537,7 @@ def config2_api(ctx: Ctx, args):
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("configs", nargs="*", default=["config2", "config3", "config4", "config5"])
+    ap.add_argument("configs", nargs="*", default=["config2", "config3", "config4", "config5", "config5_subset"])
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
@@ -492,7 +545,9 @@ def main():
     ap.add_argument("--agents", type=int, default=0)
     ap.add_argument("--edges", type=int, default=0)
     ap.add_argument("--deltas", type=int, default=0)
-    ap.add_argument("--storm-fraction", type=float, default=0.1, help="config5: share of sessions slashed")
+    ap.add_argument("--storm-fraction", type=float, default=1.0,
+                    help="config5: share of sessions slashed (1.0: BASELINE config 5 as stated)")
+    ap.add_argument("--subset-fraction", type=float, default=0.1, help="config5_subset: share of sessions slashed")
     ap.add_argument("--coroutine-sagas", type=int, default=4096, help="config4: sagas in the coroutine mode")
     ap.add_argument("--unfused", action="store_true", help="config5: separate slash and sigma_eff passes (A/B)")
     ap.add_argument("--unfused-graph", action="store_true",
@@ -506,7 +561,7 @@ def main():
     ctx = Ctx(args.device)
     for c in args.configs:
         {"config2": config2, "config2_api": config2_api, "config3": config3, "config4": config4,
-         "config5": config5}[c](ctx, args)
+         "config5": config5, "config5_subset": config5_subset}[c](ctx, args)
     if ctx.world > 1:
         dist.destroy_process_group()
 

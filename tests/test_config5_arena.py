@@ -108,3 +108,63 @@ def test_render_rows_gfx950_long_rows_and_wide_hex(cuda_device):
                           hex_field=(pos, src.to(dev), hb), pitch=1504)
             outs.append(out.cpu())
         assert torch.equal(outs[0], outs[1]), hb
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_storm_bond_update_counts_match_slashing_engine(dev):
+    """Config 5's reported ``bond_updates`` are device counts: on a
+    10⁴-edge instance, the full storm (every session slashed, K06 cascade, then its
+    remaining bonds released, K07) changes exactly the bonds the scalar
+    ``SlashingEngine.slash`` + ``VouchingEngine.release_session_bonds`` change, per
+    session and in total — and that is every edge."""
+    import random
+
+    from benchmarks.bench_configs import storm_counts
+    from hypervisor.liability.slashing import SlashingEngine
+    from hypervisor.liability.vouching import VouchingEngine, VouchingError
+    from agent_hypervisor_amd.ops import liability as LI
+
+    T0 = datetime(2026, 3, 1, 12, tzinfo=timezone.utc)
+    _clock.set_clock(lambda: T0)
+    try:
+        rng = random.Random(21)
+        ve = VouchingEngine()
+        sids, parts, sig = [], [], []
+        while len(ve._vouches) < 10_000:
+            s = len(sids)
+            sid, p = f"s{s}", [f"did:{s}:{k}" for k in range(16)]
+            sg = {d: rng.uniform(0.3, 1.0) for d in p}
+            for _ in range(24):
+                a, b = rng.sample(p, 2)
+                try:
+                    ve.vouch(a, b, sid, sg[a], bond_pct=rng.choice([0.1, 0.2, 0.3]))
+                except VouchingError:
+                    pass
+            sids.append(sid)
+            parts.append(p)
+            sig.append(sg)
+        E = len(ve._vouches)
+        S = len(sids)
+        vb = LI.from_engine(ve, sids, parts, device=dev)
+        targets = [rng.randrange(16) for _ in range(S)]
+        omega = torch.full((S,), 0.95, dtype=torch.float64)
+        scores = torch.tensor([[sig[s][d] for d in parts[s]] for s in range(S)], dtype=torch.float64)
+        now = _clock.to_us(T0)
+        out = LI.slash(vb, torch.tensor(targets, dtype=torch.uint8, device=dev), omega.to(dev), scores.to(dev), now,
+                       clip_cap=16, zero_records=False, with_sigma_eff=True)
+        rel = LI.release_bonds(vb, now)
+        counts = storm_counts(out, rel).cpu().tolist()
+        se = SlashingEngine(ve)
+        want_slash, want_rel = [], []
+        for s, (sid, p) in enumerate(zip(sids, parts)):
+            before = len(se.history)
+            d = dict(sig[s])
+            se.slash(p[targets[s]], sid, d[p[targets[s]]], 0.95, "storm", d)
+            want_slash.append(sum(len(r.voucher_clips) for r in se.history[before:]))
+            want_rel.append(ve.release_session_bonds(sid))
+        assert out.clip_count.cpu().tolist() == want_slash
+        assert rel.cpu().tolist() == want_rel
+        assert counts == [sum(want_slash), sum(want_rel)] and sum(counts) == E >= 10_000
+        assert int(vb.active.sum()) == 0 and not any(v.is_active for v in ve._vouches.values())
+    finally:
+        _clock.set_clock(None)
