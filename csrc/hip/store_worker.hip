@@ -48,7 +48,9 @@ constexpr int kJobs = 64;  // LDS capture-job ring
 // job [seq+1, blocks | skipped << 8 | batch << 16 | stage << 24 | hash << 44, t_start,
 // t_end] at trace[4·(cap + seq mod cap)], per provisional Merkle tree (keyed by the
 // capture job after which it ran) [seq+1, leaves | done << 8 | cached << 9, t_start,
-// t_end] at trace[4·(2·cap + seq mod cap)]; s_memrealtime ticks (100 MHz), pinned memory.
+// t_end] at trace[4·(2·cap + seq mod cap)], per helper-wave job [seq+1, mode (1 whole record, 2
+// prefix) | blocks << 8 | helper << 16, t_start, t_end] at trace[4·(3·cap + seq mod cap)];
+// s_memrealtime ticks (100 MHz), pinned memory.
 __device__ __forceinline__ void trace_put(uint64_t* tr, int64_t cap, int64_t half, uint64_t seq, uint64_t a,
                                           uint64_t t0, uint64_t t1) {
   if (tr == nullptr || cap <= 0) return;
@@ -134,14 +136,10 @@ __device__ int batch_size(const HashJob* jobs, uint32_t done, uint32_t avail, in
   return bad ? __builtin_ctzll(bad) : 64;
 }
 
-// Lane `lane` < n hashes job jobs[(done + lane) % kJobs] and completes it.
-__device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, int n, uint32_t* win,
-                           uint32_t* kwrows, uint64_t* res, int64_t nslots, int lane, bool light, uint64_t* tr,
-                           int64_t tcap) {
-  if (lane >= n) return;
-  const uint64_t tj0 = __builtin_amdgcn_s_memrealtime();
-  const HashJob j = jobs[(done + lane) % kJobs];
-  uint32_t* w = win + kBatchStride * lane;
+// One lane's record of a batch: staged into its window `w` with the parent's quoted
+// digest spliced in, then compressed (from the prefix wave's midstate when there is
+// one).  `skip`: blocks taken from the midstate.
+__device__ __forceinline__ void hash_one(const Tables& t, const HashJob& j, uint32_t* w, uint32_t* kw, uint32_t h[8], int64_t& skip) {
   const uint64_t len = static_cast<uint64_t>(j.len);
   const int64_t nblk = job_blocks(j);
   const int64_t nw = nblk * 16;
@@ -181,8 +179,7 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
     }
     put(65, 0x22u);
   }
-  uint32_t h[8];
-  const int64_t skip = j.mid_blocks > 0 && j.mid_blocks < nblk ? j.mid_blocks : 0;
+  skip = j.mid_blocks > 0 && j.mid_blocks < nblk ? j.mid_blocks : 0;
   if (skip) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) h[k] = j.mid[k];
@@ -191,10 +188,42 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
   }
   // per block: message schedule (+K) into the lane's K+W row, then the rounds
   // (the split form keeps the round state in registers; see sha256_rounds_kw)
-  uint32_t* kw = kwrows + kKwStride * lane;
   for (int64_t b = skip; b < nblk; ++b) {
     sha256_expand_kw(w + 16 * b, kw);
     sha256_rounds_kw(h, kw);
+  }
+}
+
+// The helper's whole-record digest of a speculated link (HashJob::spec), usable
+// when the parent digest its hole held equals the parent's final digest: the
+// previous delta's row (earlier in the queue, so already done) or, for the
+// chain's first hole, the session head.
+__device__ __forceinline__ bool spec_link_ok(const Tables& t, const HashJob& j) {
+  if (!j.full || j.hole < 0) return false;
+  const uint32_t* head = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
+  uint32_t hd[8];
+  load8(head, hd);
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ok = ok && hd[k] == j.ppar[k];
+  return ok;
+}
+
+// Lane `lane` < n hashes job jobs[(done + lane) % kJobs] and completes it.
+__device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, int n, uint32_t* win,
+                           uint32_t* kwrows, uint64_t* res, int64_t nslots, int lane, bool light, uint64_t* tr,
+                           int64_t tcap) {
+  if (lane >= n) return;
+  const uint64_t tj0 = __builtin_amdgcn_s_memrealtime();
+  const HashJob& j = jobs[(done + lane) % kJobs];
+  uint32_t h[8];
+  int64_t nblk = job_blocks(j), skip = 0;
+  if (spec_link_ok(t, j)) {  // a helper hashed the whole record and its parent is final and equal
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = j.sdig[k];
+    skip = nblk;
+  } else {
+    hash_one(t, j, win + kBatchStride * lane, kwrows + kKwStride * lane, h, skip);
   }
   store8(t.d_hash + 8 * j.d, h);
   store8(t.s_head + 8 * j.s, h);
@@ -213,7 +242,7 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
             tj0, __builtin_amdgcn_s_memrealtime());
 }
 
-__global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
+__global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
                                                            uint64_t* res, uint8_t* bulk, uint64_t* alive,
                                                            int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks,
                                                            int speculate, uint64_t* tr, int64_t tcap) {
@@ -229,12 +258,15 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
   // the last one delta row cc_d), for the provisional Merkle root
   __shared__ uint32_t chain_cache[64 * 8];
   __shared__ int32_t cc_s, cc_n, cc_d;
-  // wave 2: per-job prefix state, staging (≤ kPrefixBlocks blocks) and K+W rows
+  // waves 2, 3 (helpers): per-job helper state, and per helper a staging window
+  // (≤ kPrefixBlocks blocks) and K+W rows
   constexpr int kPrefixBlocks = 8;
+  constexpr uint32_t kHelperScan = 8;  // pending jobs a helper looks at (from the oldest)
+  constexpr uint32_t kSpecQueue = 4;   // whole-record hashing only while ≤ this many are pending
   __shared__ uint32_t pstate[kJobs];
-  __shared__ uint32_t lds2[16 * kPrefixBlocks];
-  __shared__ uint32_t kw2[kPrefixBlocks * kKwStride];
-  __shared__ uint32_t q_head, q_done, stop, bye, bye2, spec_s;
+  __shared__ uint32_t lds2[2 * 16 * kPrefixBlocks];
+  __shared__ uint32_t kw2[2 * kPrefixBlocks * kKwStride];
+  __shared__ uint32_t q_head, q_done, stop, bye, bye2, bye3, spec_s;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   if (threadIdx.x == 0) {
@@ -243,6 +275,7 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
     stop = 0;
     bye = 0;
     bye2 = 0;
+    bye3 = 0;
     spec_s = 0;  // session + 1 whose provisional Merkle root wave 1 is computing (0: none)
     cc_s = -1;
     cc_n = 0;
@@ -250,41 +283,88 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
   }
   __syncthreads();  // the only workgroup barrier: every wave passes it once
 
-  if (wave == 2) {
-    // ------------------------------------------------------------ prefix wave
-    const Lanes L{lane, 64, lds2, kw2};
-    uint32_t pos = 0;
+  if (wave >= 2) {
+    // ------------------------------------------------------------ helper waves
+    // Two helpers (waves 2, 3 — their own SIMDs) claim pending capture jobs the hash
+    // engine has not taken (pstate CAS 0 → 1, done = 2):
+    //  * a speculated link (the host prefilled the predicted parent digest, `spec`)
+    //    while the queue is short (the per-call regime): the whole record is hashed
+    //    now, off the chain — the engine only checks the parent (spec_link_ok);
+    //  * otherwise the midstate of the blocks before the parent hole (prefix).
+    // Under a long queue (many sessions) the engine batches jobs one per lane and
+    // the helpers only do prefixes, so a batch never waits on a whole-record hash.
+    const int hw = wave - 2;
+    uint32_t* hl = lds2 + hw * 16 * kPrefixBlocks;
+    uint32_t* hk = kw2 + hw * kPrefixBlocks * kKwStride;
+    const Lanes L{lane, 64, hl, hk};
     for (;;) {
       const uint32_t head = lds_acquire(&q_head);
       const uint32_t dn = lds_acquire(&q_done);
-      if (static_cast<int32_t>(pos - dn) < 0) pos = dn;  // jobs wave 1 finished need nothing
-      if (pos == head || !(speculate & 2)) {
+      int32_t pick = -1;
+      int32_t mode = 0;  // 1 whole record (spec), 2 prefix
+      if (lane == 0 && (speculate & (2 | 128)) && head != dn) {
+        const uint32_t pend = head - dn;
+        const uint32_t lim = pend < kHelperScan ? head : dn + kHelperScan;
+        const bool short_q = pend <= kSpecQueue;
+        for (uint32_t p = dn; p != lim; ++p) {
+          const HashJob* jp = &jobs[p % kJobs];
+          const int32_t m = ((speculate & 128) && short_q && jp->spec && job_blocks(*jp) <= kPrefixBlocks) ? 1
+                            : ((speculate & 2) && jp->hole >= 64)                                          ? 2
+                                                                                                            : 0;
+          if (m && lds_acquire(&pstate[p % kJobs]) == 0u && lds_cas(&pstate[p % kJobs], 0u, 1u) == 0u) {
+            pick = static_cast<int32_t>(p % kJobs);
+            mode = m;
+            break;
+          }
+        }
+      }
+      pick = __shfl(pick, 0);
+      mode = __shfl(mode, 0);
+      if (pick < 0) {
         if (lds_acquire(&stop)) break;
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
-      HashJob* jp = &jobs[pos % kJobs];
-      uint32_t* ps = &pstate[pos % kJobs];
-      int claimed = 0;
-      if (lane == 0 && jp->hole >= 64) claimed = lds_cas(ps, 0u, 1u) == 0u;
-      if (__shfl(claimed, 0)) {
-        HashJob jb;
-        jb.off = jp->off;
-        jb.hole = jp->hole;
-        uint32_t mid[8];
-        const int32_t pb = capture_prefix(L, t, jb, lds2, 16 * kPrefixBlocks, kPrefixBlocks, mid);
-        if (lane == 0) {
-          if (pb > 0) {
+      const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
+      HashJob* jp = &jobs[pick];
+      HashJob jb;
+      jb.off = jp->off;
+      jb.len = jp->len;
+      jb.hole = jp->hole;
+      jb.spec = jp->spec;
+      bool whole = false;
+      if (mode == 1) {
+        uint32_t dig[8], par[8];
+        whole = capture_spec_full(L, t, jb, hl, kPrefixBlocks, dig, par);
+        if (whole && lane == 0) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) jp->mid[k] = mid[k];
-            jp->mid_blocks = pb;
+          for (int k = 0; k < 8; ++k) {
+            jp->sdig[k] = dig[k];
+            jp->ppar[k] = par[k];
           }
-          lds_release(ps, 2u);
+          jp->full = 1;
         }
       }
-      ++pos;
+      if (!whole && jb.hole >= 64 && (speculate & 2)) {
+        uint32_t mid[8];
+        const int32_t pb = capture_prefix(L, t, jb, hl, 16 * kPrefixBlocks, kPrefixBlocks, mid);
+        if (lane == 0 && pb > 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) jp->mid[k] = mid[k];
+          jp->mid_blocks = pb;
+        }
+      }
+      if (lane == 0) {
+        const uint64_t seq = jp->seq;
+        const int32_t done_blocks = whole ? static_cast<int32_t>(job_blocks(*jp)) : jp->mid_blocks;
+        lds_release(&pstate[pick], 2u);
+        trace_put(tr, tcap, 3, seq,
+                  static_cast<uint64_t>(whole ? 1 : 2) | (static_cast<uint64_t>(done_blocks & 0xff) << 8) |
+                      (static_cast<uint64_t>(hw) << 16),
+                  th0, __builtin_amdgcn_s_memrealtime());
+      }
     }
-    if (lane == 0) lds_release(&bye2, 1u);
+    if (lane == 0) lds_release(hw == 0 ? &bye2 : &bye3, 1u);
     return;
   }
 
@@ -329,11 +409,30 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
       }
       if (lane == 0) take_job(&pstate[done % kJobs]);
       L.sync();  // the job (with any midstate wave 2 wrote) is read after taking it
-      const HashJob j = jobs[done % kJobs];
+      const HashJob& j = jobs[done % kJobs];
       uint64_t* r = res + (j.seq % static_cast<uint64_t>(nslots)) * kResWords;
       uint64_t tele = 0;
       uint32_t hd[8];
-      capture_finish(L, t, j, r, &tele, hd);
+      if (spec_link_ok(t, j)) {
+        // a helper already hashed this record with the parent digest the engine just
+        // computed: take its digest (rows and result words as capture_finish writes them)
+        const int64_t nb = job_blocks(j);
+        if (lane == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) hd[k] = j.sdig[k];
+          store8(t.d_hash + 8 * j.d, hd);
+          store8(t.s_head + 8 * j.s, hd);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) out64(r + 2 + k, hd[k]);
+          out64(r + 10, 0);
+          out64(r + 11, 0);
+          out64(r + 12, static_cast<uint64_t>(nb));
+          out64(r + 1, ST_OK);
+          tele = (static_cast<uint64_t>(nb) & 0xff) | ((static_cast<uint64_t>(nb) & 0xff) << 8);
+        }
+      } else {
+        capture_finish(L, t, j, r, &tele, hd);
+      }
       if (lane == 0) {
         // extend the cached chain (turn 1 starts one; anything else invalidates it)
         const bool extend = j.prev >= 0 && cc_s == static_cast<int32_t>(j.s) && cc_d == static_cast<int32_t>(j.prev) &&
@@ -530,7 +629,7 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
   // drain the hash engine, stop it, wait for its goodbye, then release the queue
   while (lds_acquire(&q_done) != queued) __builtin_amdgcn_s_sleep(1);
   if (lane == 0) lds_release(&stop, 1u);
-  while (!lds_acquire(&bye) || !lds_acquire(&bye2)) __builtin_amdgcn_s_sleep(1);
+  while (!lds_acquire(&bye) || !lds_acquire(&bye2) || !lds_acquire(&bye3)) __builtin_amdgcn_s_sleep(1);
   if (lane == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(alive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -540,12 +639,12 @@ __global__ __launch_bounds__(192) void store_worker_kernel(Tables t, const uint6
 }  // namespace store
 }  // namespace ahv
 
-// Host-callable launcher (one workgroup: command wave, hash-engine wave, prefix wave).
+// Host-callable launcher (one workgroup: command wave, hash-engine wave, two helper waves).
 extern "C" int ahv_store_launch_worker(const ahv::store::Tables* t, const uint64_t* ring, int64_t nslots,
                                        uint64_t* res, uint8_t* bulk, uint64_t* alive, int64_t* tail,
                                        uint64_t idle_ticks, uint64_t max_ticks, int speculate,
                                        uint64_t* trace, int64_t trace_cap, hipStream_t stream) {
-  hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(192), 0, stream, *t, ring, nslots, res, bulk,
+  hipLaunchKernelGGL(ahv::store::store_worker_kernel, dim3(1), dim3(256), 0, stream, *t, ring, nslots, res, bulk,
                      alive, tail, idle_ticks, max_ticks, speculate, trace, trace_cap);
   return static_cast<int>(hipGetLastError());
 }

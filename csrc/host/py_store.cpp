@@ -215,8 +215,19 @@ class Store : public StoreCore {
     thread_local std::string buf;
     size_t at = 0;
     if (!render_delta(delta.ptr(), buf, &at)) return py::make_tuple(-1, -1, -1, -1, py::none());
-    const Placed p = capture_rendered(slot, turn, ts_us, buf, at);
+    const Placed p = capture_rendered(slot, turn, ts_us, buf, at, parent_hex(turn, parent));
     return py::make_tuple(p.didx, p.off, p.len, p.seq, p.didx >= 0 ? predict(buf, at, turn, parent) : py::none());
+  }
+
+  // The predicted parent digest's 64 hex chars (turn > 1 and a canonical hex str), or null.
+  static const char* parent_hex(int64_t turn, const py::object& parent) {
+    if (turn <= 1 || parent.is_none() || !PyUnicode_Check(parent.ptr())) return nullptr;
+    PyObject* o = parent.ptr();
+    if (PyUnicode_GET_LENGTH(o) != 64 || !PyUnicode_IS_COMPACT_ASCII(o)) return nullptr;
+    const char* ph = static_cast<const char*>(PyUnicode_DATA(o));
+    for (int k = 0; k < 64; ++k)
+      if (!((ph[k] >= '0' && ph[k] <= '9') || (ph[k] >= 'a' && ph[k] <= 'f'))) return nullptr;
+    return ph;
   }
 
   // Released delta rows reclaimed per batch.  The reclaim's OP_FREE_ROWS waits for the
@@ -233,7 +244,7 @@ class Store : public StoreCore {
     std::string buf = payload;
     if (null_at < 0 || static_cast<size_t>(null_at) + 4 > buf.size() || buf.compare(null_at, 4, "null") != 0)
       throw std::invalid_argument("capture_bytes: null_at does not point at the parent's null");
-    const Placed p = capture_rendered(slot, turn, ts_us, buf, static_cast<size_t>(null_at));
+    const Placed p = capture_rendered(slot, turn, ts_us, buf, static_cast<size_t>(null_at), parent_hex(turn, parent));
     return py::make_tuple(p.didx, p.off, p.len, p.seq,
                           p.didx >= 0 ? predict(buf, static_cast<size_t>(null_at), turn, parent) : py::none());
   }
@@ -334,15 +345,15 @@ class Store : public StoreCore {
   }
 
   // The worker timeline (AHV_STORE_TRACE): (commands uint64[cap,4], engine jobs uint64[cap,4],
-  // host post times uint64[cap], provisional Merkle trees uint64[cap,4]) as bytes, or None
-  // when tracing is off.
+  // host post times uint64[cap], provisional Merkle trees uint64[cap,4], helper-wave jobs
+  // uint64[cap,4]) as bytes, or None when tracing is off.
   py::object trace() const {
     if (trace_buf() == nullptr) return py::none();
     const size_t cap = static_cast<size_t>(trace_cap());
     const char* b = reinterpret_cast<const char*>(trace_buf());
     return py::make_tuple(py::bytes(b, cap * 32), py::bytes(b + cap * 32, cap * 32),
                           py::bytes(reinterpret_cast<const char*>(post_ns().data()), cap * 8),
-                          py::bytes(b + cap * 64, cap * 32));
+                          py::bytes(b + cap * 64, cap * 32), py::bytes(b + cap * 96, cap * 32));
   }
 
   py::dict info() const {

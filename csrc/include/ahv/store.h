@@ -253,6 +253,15 @@ struct HashJob {
   int64_t prev;        // parent delta index (-1 for turn 1)
   int32_t mid_blocks;  // leading blocks already compressed into `mid` (0: none)
   uint32_t mid[8];     // SHA-256 state after those blocks (they precede the parent hole)
+  // Speculated chain link (worker): the host wrote its predicted parent digest into
+  // the hole (`spec`), so a helper wave may hash the whole record before the parent
+  // is final (`full`: `sdig` is the digest of the record as stored, `ppar` the
+  // parent digest its hole holds).  The hash engine takes `sdig` only when `ppar`
+  // equals the parent digest it computed; otherwise it splices and re-hashes.
+  int32_t spec;
+  int32_t full;
+  uint32_t sdig[8];
+  uint32_t ppar[8];
 };
 
 enum ExecResult : int { EXEC_STOP = 0, EXEC_DONE = 1, EXEC_DEFERRED = 2 };
@@ -1728,6 +1737,45 @@ AHV_HD bool capture_begin(const Lanes& L, const Tables& t, const Cmd& c, uint64_
   j.len = static_cast<int64_t>(c.a[5]);
   j.hole = hole;
   j.prev = prev;
+  j.spec = hole >= 0 && (c.a[7] & 1u) ? 1 : 0;
+  j.full = 0;
+  return true;
+}
+
+// Speculated link (worker helper waves): SHA-256 of a record stored with its
+// predicted parent digest already in the hole (HashJob::spec), and that parent
+// parsed back from its hex — the whole record hashed before the parent is final.
+// ≤ `max_blocks` blocks (false otherwise: the engine hashes it).  `w`: LDS staging
+// of max_blocks·16 words; the lanes expand the schedules, the leader runs the rounds.
+// Valid on the leader.
+AHV_HD bool capture_spec_full(const Lanes& L, const Tables& t, const HashJob& j, uint32_t* w, int32_t max_blocks,
+                              uint32_t dig[8], uint32_t par[8]) {
+  if (!j.spec || j.hole < 0) return false;
+  const int64_t nblk = (j.len + 9 + 63) / 64;
+  if (nblk > max_blocks) return false;
+  if (stage_words(L, t.payload + j.off, static_cast<uint64_t>(j.len), w, 16 * max_blocks) < 0) return false;
+  // the quoted parent hex at the hole, back to 8 digest words: lane k decodes char k
+  // (the nibbles are gathered by shuffles)
+  const uint8_t* lb = reinterpret_cast<const uint8_t*>(w);
+  int bad = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t b = static_cast<uint64_t>(j.hole) + 1 + static_cast<uint64_t>(L.lane);
+  const uint32_t ch = lb[(b & ~uint64_t(3)) | (3 - (b & 3))];
+  const uint32_t dg = ch - 0x30u, lc = ch - 0x61u;
+  const uint32_t nib = dg < 10u ? dg : lc + 10u;
+  bad = __any(dg >= 10u && lc >= 6u) ? 1 : 0;
+  uint32_t v = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v = (v << 4) | __shfl(nib, 8 * (L.lane & 7) + e);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) par[k] = __shfl(v, k);
+#else
+  (void)lb;
+  bad = 1;  // host twin (one lane): spec jobs are a worker feature
+#endif
+  if (bad) return false;
+  sha256_lds_blocks_par(L, w, nblk, dig);
+  L.sync();
   return true;
 }
 

@@ -187,7 +187,10 @@ class StoreCore {
       const char* lp = std::getenv("AHV_STORE_LIGHT_PUBLISH");
       // 64 = prefetch the next command slot while the current command executes
       const char* pf2 = std::getenv("AHV_STORE_SLOT_PREFETCH");
-      speculate_ = ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
+      // 128 = helper waves hash a capture whose parent the host predicted (hole prefilled)
+      //       as a whole record, off the chain; the engine checks the parent and takes it
+      const char* sc = std::getenv("AHV_STORE_SPEC_CHAIN");
+      speculate_ = ((sc == nullptr || std::atoi(sc) != 0) ? 128 : 0) | ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
                    ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) |
                    ((nf == nullptr || std::atoi(nf) != 0) ? 16 : 0) |
                    ((lp == nullptr || std::atoi(lp) != 0) ? 32 : 0) |
@@ -197,10 +200,10 @@ class StoreCore {
       const char* tr = std::getenv("AHV_STORE_TRACE");
       if (tr != nullptr && std::atoll(tr) > 0) {
         trace_cap_ = std::atoll(tr);
-        hip_check(hipHostMalloc(reinterpret_cast<void**>(&trace_), static_cast<size_t>(trace_cap_) * 96,
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&trace_), static_cast<size_t>(trace_cap_) * 128,
                                 hipHostMallocCoherent),
                   "store trace");
-        std::memset(trace_, 0, static_cast<size_t>(trace_cap_) * 96);
+        std::memset(trace_, 0, static_cast<size_t>(trace_cap_) * 128);
         post_ns_.assign(static_cast<size_t>(trace_cap_), 0);
       }
     } else {
@@ -602,7 +605,13 @@ class StoreCore {
   // with a 66-byte hole for the quoted parent digest (turn > 1), and post
   // OP_DELTA_CAPTURE.  The device splices the chain head into the hole and hashes
   // (K08).  Nothing is recycled while it is live; full tables report -2 / -3.
-  Placed capture_rendered(int64_t slot, int64_t turn, int64_t ts_us, const std::string& buf, size_t at) {
+  // `phex` (or null): the parent's predicted digest as 64 lowercase hex chars.  It
+  // is written into the hole (quoted) and flagged in the command (a7 bit 0), so the
+  // worker's helper waves can hash the whole record at once instead of waiting for
+  // the parent's digest; the hash engine still splices and re-hashes when the
+  // parent it computed differs (store_worker.hip, spec jobs).
+  Placed capture_rendered(int64_t slot, int64_t turn, int64_t ts_us, const std::string& buf, size_t at,
+                          const char* phex = nullptr) {
     const bool hole = turn > 1;
     const size_t len = hole ? buf.size() - 4 + 66 : buf.size();
     const int64_t didx = take_delta_row();
@@ -617,15 +626,21 @@ class StoreCore {
     uint8_t* dst = payload_ + off;
     if (hole) {
       std::memcpy(dst, buf.data(), at);
+      if (phex != nullptr) {
+        dst[at] = '"';
+        std::memcpy(dst + at + 1, phex, 64);
+        dst[at + 65] = '"';
+      }
       std::memcpy(dst + at + 66, buf.data() + at + 4, buf.size() - at - 4);
     } else {
       std::memcpy(dst, buf.data(), buf.size());
     }
     if (gpu_) _mm_sfence();
-    uint64_t a[7] = {static_cast<uint64_t>(slot), static_cast<uint64_t>(didx), static_cast<uint64_t>(turn),
+    const bool spec = hole && phex != nullptr;
+    uint64_t a[8] = {static_cast<uint64_t>(slot), static_cast<uint64_t>(didx), static_cast<uint64_t>(turn),
                      static_cast<uint64_t>(ts_us), static_cast<uint64_t>(off), static_cast<uint64_t>(len),
-                     hole ? static_cast<uint64_t>(at) : ~0ull};
-    const uint64_t q = post_raw(store::OP_DELTA_CAPTURE, a, 7, nullptr, 0);
+                     hole ? static_cast<uint64_t>(at) : ~0ull, spec ? 1ull : 0ull};
+    const uint64_t q = post_raw(store::OP_DELTA_CAPTURE, a, spec ? 8 : 7, nullptr, 0);
     return Placed{didx, off, static_cast<int64_t>(len), static_cast<int64_t>(q)};
   }
 
@@ -982,7 +997,7 @@ class StoreCore {
   uint64_t launches_ = 0;
   uint64_t double_releases_ = 0;  // releases of rows that were not live (ignored)
   std::vector<uint8_t> dreleased_;  // delta rows released and not yet reclaimed
-  uint64_t* trace_ = nullptr;       // worker timeline (AHV_STORE_TRACE): [3·cap][4] words, pinned
+  uint64_t* trace_ = nullptr;       // worker timeline (AHV_STORE_TRACE): [4·cap][4] words, pinned
   int64_t trace_cap_ = 0;
   std::vector<uint64_t> post_ns_;   // host post time of each traced sequence number (steady clock)
   uint64_t reclaims_ = 0;        // reclaim_pool passes that returned queued rows (any table)

@@ -75,6 +75,7 @@ def main() -> None:
     eng = np.frombuffer(tr[1], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
     post = np.frombuffer(tr[2], dtype=np.uint64).astype(np.int64)
     tree = np.frombuffer(tr[3], dtype=np.uint64).reshape(-1, 4).astype(np.int64) if len(tr) > 3 else None
+    helper = np.frombuffer(tr[4], dtype=np.uint64).reshape(-1, 4).astype(np.int64) if len(tr) > 4 else None
     cap = len(post)
     ok = cmd[:, 0] > 0
     seqs = cmd[ok, 0] - 1
@@ -100,6 +101,10 @@ def main() -> None:
                 g = int(e[1])
                 r.update(engine_start=us(e[2], base), engine_end=us(e[3], base), blocks=g & 0xFF, skip=g >> 8 & 0xFF,
                          batch=g >> 16 & 0xFF, stage_us=(g >> 24 & 0xFFFFF) / 100, hash_us=(g >> 44 & 0xFFFFF) / 100)
+            if helper is not None and helper[q % cap][0] == q + 1:
+                h = helper[q % cap]
+                r.update(helper_start=us(h[2], base), helper_end=us(h[3], base), helper_mode=int(h[1]) & 0xFF,
+                         helper_blocks=int(h[1]) >> 8 & 0xFF, helper_wave=int(h[1]) >> 16 & 0xFF)
             if tree is not None and tree[q % cap][0] == q + 1:
                 t = tree[q % cap]
                 r.update(tree_start=us(t[2], base), tree_end=us(t[3], base), tree_leaves=int(t[1]) & 0xFF,
@@ -121,8 +126,8 @@ def main() -> None:
     for k, op in enumerate(sig):
         o = {"k": k, "op": name.get(op, op)}
         for f in ("post", "seen", "waited", "done", "cmd_prefix_blocks", "engine_start", "stage_us", "hash_us",
-                  "engine_end", "blocks", "skip", "batch", "tree_start", "tree_end", "tree_leaves", "tree_done",
-                  "tree_cached"):
+                  "engine_end", "blocks", "skip", "batch", "helper_start", "helper_end", "helper_mode",
+                  "helper_blocks", "helper_wave", "tree_start", "tree_end", "tree_leaves", "tree_done", "tree_cached"):
             v = [rm[k][f] for rm in keep if f in rm[k]]
             if v:
                 o[f] = med(v)
