@@ -116,6 +116,7 @@ class TemplatePipeline:
                              pool.intern(ph.format(i=d)) if ph is not None else -1])
         nch = len(changes)
         caps = [_record_cap(st, rows[d * nch:(d + 1) * nch], d + 1, agents.max_did) for d in range(deltas)]
+        self.max_rec = max(caps) if caps else 0  # the cooperative small-batch kernel needs ≤ 512 (8 blocks)
         self.slots = st.alloc_many("S", n)
         self.gslots = st.alloc_many("G", n)
         self.tslots = st.alloc_many("T", n)
@@ -203,6 +204,7 @@ class TemplatePipeline:
             "audit": int(bool(cfg.enable_audit)), "t0": t0, "seed": self.seed, "id_base": id_base,
             "gc_retention_us": self.gc_retention_us, "status": tens["status"].data_ptr(),
             "stats": self._spread.begin().data_ptr() if stats is not None else None,
+            "max_rec": self.max_rec,
         }
         if "frag" in tens:
             args.update(frag=tens["frag"].data_ptr(), frag_off=tens["frag_off"].data_ptr(),

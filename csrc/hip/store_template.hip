@@ -158,6 +158,23 @@ static int64_t template_small() {
   return v;
 }
 
+// Cooperative small-batch kernel (store_template_coop_kernel): AHV_TEMPLATE_COOP=0 off;
+// used up to AHV_TEMPLATE_COOP_MAX sessions (default 16,384: one workgroup per CU).
+static int template_coop() {
+  static const int v = [] {
+    const char* e = std::getenv("AHV_TEMPLATE_COOP");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+static int64_t coop_max_sessions() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("AHV_TEMPLATE_COOP_MAX");
+    return e ? std::atoll(e) : int64_t(16384);
+  }();
+  return v;
+}
+
 // Occupancy variant (AHV_TEMPLATE_WAVES = 2, 3 or 4 waves per SIMD; 4 uses a 2-block window).
 static int template_waves() {
   static const int v = [] {
@@ -202,6 +219,217 @@ __global__ __launch_bounds__(kWaveLanes, MinWaves) void store_template_kernel(Te
     if (lane == 0 && total) base = atomicAdd(a.ev.cursor + seg, static_cast<unsigned long long>(total));
     base = __shfl(base, 0, kWaveLanes);
     if (i < a.n) {
+      const unsigned long long first = base + (incl - nev);
+      template_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
+        event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
+      });
+    }
+  }
+}
+
+// ---- small batches: four cooperating waves per 64 sessions ------------------------
+//
+// A batch smaller than the chip (config 2: 10⁴ sessions = 157 waves for 1,024 SIMDs)
+// is latency-bound: each wave runs alone on its SIMD and its time is its
+// instruction stream — one lane per session doing all of the session's serial work
+// (three records chained through their parent digests, then a 3-leaf Merkle root:
+// 25 compressions).  Here a workgroup of four waves (one per SIMD) shares 64
+// sessions, one lane per session in every wave:
+//
+//   wave 3      the session rows (create → join/K01 → activate → saga/K13 →
+//               terminate bookkeeping), counters and events;
+//   wave q < D  renders record q into its own LDS window (all records at once; the
+//               parent digest a placeholder), hashes the blocks before its parent
+//               hole, waits for record q−1's digest, patches its hex in and hashes
+//               the rest, writes its delta row and stores the record;
+//   Merkle      wave 0 computes node(l0, l1) and the root's first block (hex of that
+//               node) while wave 2 finishes record 2; wave 1 then computes
+//               node(l2, l2) and the root's last two blocks.
+//
+// The serial path is record 0 (all blocks) → record 1's tail → record 2's tail →
+// node(l2, l2) → root tail: 19 compressions instead of 25, and one record
+// emission instead of three.  D ∈ {1, 2, 3}; ≤ W blocks per record (the host
+// checks the reservation size).  Same rows, records and digests as
+// template_session (one semantics source: template_head, emit_delta_payload).
+constexpr int kCoopWaves = 4;
+
+template <int W>
+__global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coop_kernel(TemplateArgs a) {
+  constexpr int kWinWords = (W * 16 + 1) * kWaveLanes;
+  __shared__ uint32_t win[3 * kWinWords];
+  __shared__ uint32_t dig[3][8][kWaveLanes];  // record digests (Merkle leaves, parents)
+  __shared__ uint32_t mid[8][kWaveLanes];     // root state after its first block (D = 3)
+  __shared__ uint8_t live_c[kWaveLanes];      // the session committed a root (wave 3's answer)
+  const int wave = static_cast<int>(threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
+  const store::Tables& t = a.t;
+  const int32_t D = a.deltas;
+  const TemplateRows R = template_rows(a, i < a.n ? i : 0);
+  // every wave decides liveness before wave 3 writes the row (barrier below)
+  const bool live = i < a.n && (R.ring || t.s_state[R.s] == store::kFree8);
+  __syncthreads();
+
+  PipeCounters c{};
+  uint32_t u[4];
+  const int64_t t0 = tp_t0(a);
+  if (live) uuid4_words(a.seed, tp_id_base(a) + a.id_stride * static_cast<uint64_t>(i), u);
+  if (wave == 3) {
+    c.v[0] = i < a.n ? 1u : 0u;
+    bool committed = false;
+    if (live) {
+      committed = template_head(a, i, R, c, u);
+    } else if (i < a.n && a.status) {
+      a.status[i] = TP_ROW_IN_USE;
+    }
+    live_c[lane] = committed ? 1 : 0;
+  }
+
+  // ---- records: render, prefix, (wait for the parent) tail, rows, tee -------------------
+  WordWindowSink<W> sink;
+  sink.g_win = win + (wave < 3 ? wave : 0) * kWinWords;
+  sink.lane = lane;
+  const int q = wave;
+  const bool mine = live && q < D && q < 3;
+  uint32_t st[8];
+  uint32_t len = 0;
+  int32_t total = 0, hb = 0;
+  uint32_t hole = 0;
+  const int32_t ag = live ? a.session_agent[i] : 0;
+  const int64_t tsd = t0 + 1 + q;
+  const uint32_t turn = static_cast<uint32_t>(q + 1);
+  if (q < D && q < 3) {
+    SessionIdent sid;
+    sid.str_id = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sid.uuid[k] = live ? u[k] : 0u;
+    const StrRef did = pool_ref(a.pool, a.agent_pool[ag]);
+    const StrPool pool = a.pool;
+    const uint32_t nch = static_cast<uint32_t>(a.nch);
+    const ChangeIds* ch = a.changes + q * nch;
+    const uint32_t* fw = a.frag ? a.frag + frag_word(reinterpret_cast<const uint32_t*>(a.frag_off), q) : nullptr;
+    const uint32_t fn = a.frag ? frag_word(reinterpret_cast<const uint32_t*>(a.frag_len), q) : 0u;
+    Digest ph;  // placeholder parent (patched once the parent's digest is known)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ph.v[k] = 0;
+    total = sink.render([=](WordWindowSink<W>& k) {
+      emit_delta_payload(k, pool, did, ch, nch, -1, turn, q > 0, ph, sid, tsd, fw, fn);
+    }, len);
+    // the parent's hex starts one byte after the hole's opening quote
+    hole = q > 0 ? len - record_suffix_len(tsd, turn) : 0u;
+    hb = q > 0 ? static_cast<int32_t>(hole / 64u) : total / 16;
+    sha256_init(st);
+    sink.compress_blocks(st, 0, mine ? hb : 0);  // parent-independent blocks
+  }
+  const int64_t dr = (q < D && q < 3) ? R.drow(a, q) : 0;
+  const int64_t off = (q < D && q < 3) ? R.doff(a, q) : 0;
+  auto finish = [&](void) {  // wave q, its digest in st: rows, LDS leaf, record bytes
+    if (!mine) return;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dig[q][k][lane] = st[k];
+    t.d_sess[dr] = static_cast<int32_t>(R.s);
+    t.d_turn[dr] = static_cast<int32_t>(turn);
+    t.d_prev[dr] = q > 0 ? static_cast<int32_t>(R.drow(a, q - 1)) : -1;
+    t.d_ts[dr] = tsd;
+    t.d_off[dr] = off;
+    t.d_len[dr] = static_cast<int32_t>(len);
+    t.d_hole[dr] = q > 0 ? static_cast<int32_t>(hole) : -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t.d_hash[8 * dr + k] = st[k];
+    if (q == D - 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t.s_head[8 * R.s + k] = st[k];
+    }
+    if (!a.notee) sink.tee(reinterpret_cast<uint32_t*>(t.payload + off), static_cast<int32_t>((len + 3u) >> 2));
+  };
+  if (q == 0) finish();
+  // record q (1, 2) after record q − 1: patch the parent's hex, hash the tail
+#pragma unroll
+  for (int step = 1; step < 3; ++step) {
+    __syncthreads();  // dig[step − 1] is complete
+    if (step < D && q == step) {
+      uint32_t par[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) par[k] = dig[step - 1][k][lane];
+      if (mine) sink.patch_hex(hole + 1u, par);
+      sink.compress_blocks(st, mine ? hb : 0, mine ? total / 16 : 0);
+      finish();
+    }
+    if (step == 2 && D == 3 && q == 0) {
+      // node(l0, l1) and the root's first block (its hex) while record 2 is hashed
+      uint32_t l0[8], l1[8], n01[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        l0[k] = dig[0][k][lane];
+        l1[k] = dig[1][k][lane];
+      }
+      sink.node(l0, l1, n01);
+      uint32_t w[16], m[8];
+      digest_to_hex_words(n01, w);
+      sha256_init(m);
+      sha256_compress(m, w);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mid[k][lane] = m[k];
+    }
+  }
+  __syncthreads();  // every digest (and the root's first block) is in LDS
+
+  // ---- Merkle root (K09) → s_root --------------------------------------------------------
+  if (wave == 1 && live) {
+    uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (live_c[lane] && !(a.ab & 4)) {
+      if (D == 3) {
+        uint32_t l2[8], n22[8], w[16];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) l2[k] = dig[2][k][lane];
+        sink.node(l2, l2, n22);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) root[k] = mid[k][lane];
+        digest_to_hex_words(n22, w);
+        sha256_compress(root, w);
+        sha256_compress_pad_only(root, 128u);
+      } else if (D == 2) {
+        uint32_t l0[8], l1[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          l0[k] = dig[0][k][lane];
+          l1[k] = dig[1][k][lane];
+        }
+        sink.node(l0, l1, root);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) root[k] = dig[0][k][lane];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t.s_root[8 * R.s + k] = root[k];
+  }
+
+  // ---- counters (X04) and lifecycle events (N08): wave 3 ----------------------------------
+  if (wave != 3) return;
+  if (a.stats) {
+#pragma unroll
+    for (int k = 0; k < kPipeStats; ++k) {
+      const uint32_t sm = wave_sum(c.v[k]);
+      if (lane == 0 && sm)
+        atomicAdd(a.stats + (blockIdx.x % kStatSpread) * kPipeStats + k, static_cast<unsigned long long>(sm));
+    }
+  }
+  if (a.ev.cursor) {
+    uint32_t nev = 0;
+    if (live) nev = template_event_count(c, t.s_terminated[R.s] != 0);
+    uint32_t incl = nev;
+#pragma unroll
+    for (int o = 1; o < kWaveLanes; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, kWaveLanes);
+      if (lane >= static_cast<uint32_t>(o)) incl += y;
+    }
+    const uint32_t tot = __shfl(incl, kWaveLanes - 1, kWaveLanes);
+    const int seg = static_cast<int>(blockIdx.x % kStatSpread);
+    unsigned long long base = 0;
+    if (lane == 0 && tot) base = atomicAdd(a.ev.cursor + seg, static_cast<unsigned long long>(tot));
+    base = __shfl(base, 0, kWaveLanes);
+    if (live) {
       const unsigned long long first = base + (incl - nev);
       template_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
         event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
@@ -314,9 +542,23 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
   // every variant in one process) or per process (AHV_TEMPLATE_WAVES / AHV_TEMPLATE_SMALL)
   const int waves = d.contains("waves") && !d["waves"].is_none() ? d["waves"].cast<int>() : template_waves();
   const int64_t small = d.contains("small") && !d["small"].is_none() ? d["small"].cast<int64_t>() : template_small();
+  // cooperative small-batch kernel: D ≤ 3 records of ≤ 8 blocks (the caller's record
+  // reservation `max_rec` bytes, or the ring's), at most one workgroup per CU
+  const int64_t max_rec = a.ring_cap > 0 ? a.rec_bytes
+                          : (d.contains("max_rec") && !d["max_rec"].is_none() ? d["max_rec"].cast<int64_t>() : 0);
+  const int coop = template_coop();
+  const bool use_coop = coop != 0 && a.n <= coop_max_sessions() && a.deltas >= 1 && a.deltas <= 3 && max_rec > 0 &&
+                        max_rec <= 512 && !(b.ab & 64) &&
+                        !(d.contains("waves") && !d["waves"].is_none() && d["waves"].cast<int>() == -1);
   py::gil_scoped_release nogil;
   const dim3 grid(static_cast<uint32_t>((a.n + kWaveLanes - 1) / kWaveLanes)), block(kWaveLanes);
-  if (a.n <= small)  // latency-bound: one pass per record
+  if (use_coop) {
+    const dim3 cblock(kCoopWaves * kWaveLanes);
+    if (max_rec <= 384)
+      hipLaunchKernelGGL((store_template_coop_kernel<6>), grid, cblock, 0, reinterpret_cast<hipStream_t>(stream), b);
+    else
+      hipLaunchKernelGGL((store_template_coop_kernel<8>), grid, cblock, 0, reinterpret_cast<hipStream_t>(stream), b);
+  } else if (a.n <= small)  // latency-bound: one pass per record
     hipLaunchKernelGGL((store_template_kernel<1, 6>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
   else if (waves == 2)  // 231 VGPRs, no scratch
     hipLaunchKernelGGL((store_template_kernel<2, 3>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), b);
@@ -332,6 +574,8 @@ void kernels_store_template(std::vector<KernelEntry>& out) {
   out.push_back({"store_template_kernel<2,3>", reinterpret_cast<const void*>(&store_template_kernel<2, 3>)});
   out.push_back({"store_template_kernel<1,6>", reinterpret_cast<const void*>(&store_template_kernel<1, 6>)});
   out.push_back({"store_template_kernel<4,2>", reinterpret_cast<const void*>(&store_template_kernel<4, 2>)});
+  out.push_back({"store_template_coop_kernel<6>", reinterpret_cast<const void*>(&store_template_coop_kernel<6>)});
+  out.push_back({"store_template_coop_kernel<8>", reinterpret_cast<const void*>(&store_template_coop_kernel<8>)});
 }
 
 }  // namespace ahv

@@ -152,24 +152,18 @@ struct HostTeeSink : HostSink {
   }
 };
 
-// Per-session body (`i` = batch index).
-template <class Sink>
-AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sink) {
+// Everything of session `i` but its audit records and Merkle root: create →
+// join (K01 ring gate) → activate → saga step (K13) → terminate bookkeeping.
+// `u`: the session's uuid words; returns whether the terminate commits a root.
+// (The caller checked that the row is free.)
+AHV_HD bool template_head(const TemplateArgs& a, int64_t i, const TemplateRows& R, PipeCounters& c, uint32_t u[4]) {
   const store::Tables& t = a.t;
-  PipeCounters c{};
-  c.v[0] = 1;
-  const TemplateRows R = template_rows(a, i);
   const int64_t s = R.s;
-  if (!R.ring && t.s_state[s] != store::kFree8) {  // a live row is never overwritten
-    if (a.status) a.status[i] = TP_ROW_IN_USE;
-    return c;
-  }
   const int64_t t0 = tp_t0(a);
   const int32_t D = a.deltas;
   int32_t status = TP_OK;
 
   // ---- create_session + begin_handshake (OP_SESS_CREATE) ------------------------
-  uint32_t u[4];
   uuid4_words(a.seed, tp_id_base(a) + a.id_stride * static_cast<uint64_t>(i), u);
 #pragma unroll
   for (int k = 0; k < 4; ++k) t.s_uuid[4 * s + k] = u[k];
@@ -257,6 +251,27 @@ AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sin
   c.v[3] = static_cast<uint32_t>(D);
   c.v[4] = committed ? 1u : 0u;
   c.v[5] = st == SS_ARCHIVED ? 1u : 0u;
+
+  return committed;
+}
+
+// Per-session body (`i` = batch index).
+template <class Sink>
+AHV_HD PipeCounters template_session(const TemplateArgs& a, int64_t i, Sink& sink) {
+  const store::Tables& t = a.t;
+  PipeCounters c{};
+  c.v[0] = 1;
+  const TemplateRows R = template_rows(a, i);
+  const int64_t s = R.s;
+  if (!R.ring && t.s_state[s] != store::kFree8) {  // a live row is never overwritten
+    if (a.status) a.status[i] = TP_ROW_IN_USE;
+    return c;
+  }
+  const int64_t t0 = tp_t0(a);
+  const int32_t D = a.deltas;
+  uint32_t u[4];
+  const bool committed = template_head(a, i, R, c, u);
+  const int32_t ag = a.session_agent[i];
 
   // ---- D × capture: record into the arena + SHA-256 chain (K08) ------------------------
   SessionIdent sid;

@@ -193,6 +193,77 @@ struct WordWindowSink {
     for (int k = 0; k < 8; ++k) out[k] = st[k];
   }
 
+  // Render the whole message `emit(*this)` into the window (one pass: it must fit
+  // in kWinBlocks blocks) with its SHA padding and bit length, without hashing it.
+  // Returns the padded length in words; `len` = message bytes.
+  template <class Emit>
+  __device__ __forceinline__ int32_t render(Emit&& emit, uint32_t& len) {
+#pragma unroll
+    for (int k = 0; k < kWinWords; ++k) g_win[k * kWaveLanes + lane] = 0u;
+    trash = (static_cast<uint32_t>(kWinWords) * kWaveLanes + lane) * 4u;
+    lo = 0;
+    seek(0);
+    sh = 0;
+    prev = 0;
+    emit(*this);
+    const uint32_t L = static_cast<uint32_t>(rel) * 4u + (sh >> 3);
+    const int32_t total = static_cast<int32_t>(((L + 8u) / 64u + 1u) * 16u);
+    put(0x80000000u, 1);
+    store_at(sh ? addr : trash, __builtin_amdgcn_alignbit(prev, 0u, sh));
+    const uint64_t bits = static_cast<uint64_t>(L) * 8u;
+    store(total - 2, static_cast<uint32_t>(bits >> 32));
+    store(total - 1, static_cast<uint32_t>(bits));
+    len = L;
+    return total;
+  }
+
+  // Compress window blocks [b0, b1) (per lane) into `st`: one compression site.
+  __device__ __forceinline__ void compress_blocks(uint32_t st[8], int32_t b0, int32_t b1) const {
+#pragma nounroll
+    for (int blk = 0; blk < kWinBlocks; ++blk) {
+      if (blk >= b0 && blk < b1) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = g_win[(blk * 16 + k) * kWaveLanes + lane];
+        sha256_compress(st, w);
+      }
+    }
+  }
+
+  // Overwrite the 64 hex chars at byte `at` of the rendered message (the quoted
+  // parent digest's inside, rendered as a placeholder) with the hex of `d`.
+  __device__ __forceinline__ void patch_hex(uint32_t at, const uint32_t d[8]) const {
+    uint32_t hw[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) word_to_hex_words(d[k], hw[2 * k], hw[2 * k + 1]);
+    const uint32_t sh8 = (at & 3u) * 8u;
+    const uint32_t base = at >> 2;
+    uint32_t* col = g_win + lane;
+    const uint32_t keep = sh8 ? ~(0xffffffffu >> sh8) : 0u;  // bytes before `at` in the first word
+    uint32_t w0 = col[base * kWaveLanes];
+    col[base * kWaveLanes] = (w0 & keep) | (sh8 ? hw[0] >> sh8 : hw[0]);
+#pragma unroll
+    for (int j = 1; j < 16; ++j) col[(base + j) * kWaveLanes] = __builtin_amdgcn_alignbit(hw[j - 1], hw[j], sh8);
+    if (sh8) {  // the last word keeps the bytes after the hex
+      const uint32_t w16 = col[(base + 16) * kWaveLanes];
+      col[(base + 16) * kWaveLanes] = (hw[15] << (32u - sh8)) | (w16 & (0xffffffffu >> sh8));
+    }
+  }
+
+  // Store the rendered message's bytes (memory order) at `dst` (16-byte aligned):
+  // `nw` words, per lane.
+  __device__ __forceinline__ void tee(uint32_t* dst, int32_t nw) const {
+#pragma nounroll
+    for (int k = 0; k < kWinWords; k += 4) {
+      if (k < nw) {
+        const uint32_t* w = g_win + k * kWaveLanes + lane;
+        *reinterpret_cast<uint4*>(dst + k) =
+            make_uint4(bswap_word(w[0]), bswap_word(w[kWaveLanes]), bswap_word(w[2 * kWaveLanes]),
+                       bswap_word(w[3 * kWaveLanes]));
+      }
+    }
+  }
+
   // Merkle digest scratch: slot j (< kWinWords / 8) lives in window words 8j..8j+7.
   __device__ __forceinline__ void stash(int j, const uint32_t d[8]) {
 #pragma unroll

@@ -55,3 +55,30 @@ def test_headline_variant_matches_the_host_oracle(dev, waves, n):
     assert rep.ok and rep.deltas >= 3 * N and rep.roots_checked >= N, rep
     # row-index lists at most: no record bytes cross to the device
     assert sum(staged) <= 64 * N, sum(staged)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,deltas,did", [(10_000, 3, "did:mesh:coop-agent-"), (16_384, 3, "did:x:"),
+                                          (5_000, 2, "did:mesh:coop2-"), (3_000, 1, "did:mesh:coop1-"),
+                                          (4_000, 3, "did:mesh:a-much-longer-decentralised-identifier-")])
+def test_small_batch_cooperative_kernel_matches_the_host_oracle(n, deltas, did):
+    """``store_template_coop_kernel`` (batches ≤ 16,384 sessions, D ≤ 3: four waves
+    per 64 sessions, records rendered at once and chained through LDS, Merkle
+    level 1 beside the last record) writes the same records, digests, heads and
+    roots as the scalar renderer + hashlib + the reference Merkle rule, for 6- and
+    8-block records (the long DID); then verify_audit over every row."""
+    from hypervisor import Hypervisor
+
+    hv = Hypervisor(device="cuda")
+    st = hv._store
+    agents = TT.AgentSet.synthetic(st, 2048, seed=5, prefix=did)
+    sa = torch.randint(0, agents.count, (n,), dtype=torch.int32, generator=torch.Generator().manual_seed(n))
+    run = TT.run(hv, n, agents=agents, session_agent=sa, deltas=deltas)
+    assert run.ok == n
+    b = hv._sessions.batch_of(run.session_ids[0])
+    tp = b.specs.tp
+    assert tp.max_rec <= 512
+    pick = np.sort(np.random.default_rng(n).choice(n, size=min(n, 1000), replace=False))
+    assert TT.check_sessions(tp, tp.last_id_base, tp.t0, sa, pick) == len(pick)
+    rep = hv.verify_audit()
+    assert rep.ok and rep.deltas >= deltas * n, rep
