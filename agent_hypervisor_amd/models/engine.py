@@ -335,16 +335,31 @@ class GovernanceEngine:
                 rows.append([pool.intern(p.format(i=d)), pool.intern(o.format(i=d)),
                              pool.intern(h.format(i=d)) if h is not None else -1, -1])
         t = torch.tensor(rows or [[0, 0, 0, 0]], dtype=torch.int32, device=self.device)
-        self._change_cache[key] = (t, rows)
-        return t, rows
+        # each delta's changes fragment is the same for every session of the batch:
+        # rendered once here (the device emitter's own code) and copied by the kernel
+        # (store_template.h, TemplateArgs::frag), as TemplatePipeline does
+        frag = None
+        if deltas and os.environ.get("AHV_TEMPLATE_FRAG", "1") != "0":
+            nch = len(specs)
+            words, offs, lens = [], [], []
+            for d in range(deltas):
+                b = C.render_fragment(pool._pool, rows[d * nch:(d + 1) * nch], d + 1, d > 0)
+                offs.append(sum(len(x) for x in words))
+                lens.append(len(b))
+                words.append(np.frombuffer(b + b"\0" * (-len(b) % 4), dtype=">u4").astype(np.uint32))
+            dev = self.device
+            frag = (torch.from_numpy(np.concatenate(words).view(np.int32).copy()).to(dev),
+                    torch.tensor(offs, dtype=torch.int32, device=dev), torch.tensor(lens, dtype=torch.int32, device=dev))
+        self._change_cache[key] = (t, rows, frag)
+        return t, rows, frag
 
-    def _ensure_arena(self, rows: list, deltas: int, nch: int) -> None:
+    def _ensure_arena(self, rows: list, deltas: int, nch: int) -> int:
         """Reserve the ring's arena (one record slot per delta row) large enough for
-        the longest record this batch can produce."""
+        the longest record this batch can produce; returns that record's padded size."""
         need = max((_record_cap(self.store, rows[d * nch:(d + 1) * nch], d + 1, self.agents.max_did)
                     for d in range(deltas)), default=64)
         if need <= self._rec_bytes:
-            return
+            return need
         st = self.store
         rec = (need + need // 4 + 63) & ~63
         cap, dmax = self.sessions.capacity, self.dmax
@@ -356,6 +371,7 @@ class GovernanceEngine:
         st._c.grow_payload(off + cap * dmax * rec)
         st.caps["B"] = st._c.payload_cap
         self._off_base, self._rec_bytes = off, rec
+        return need
 
     def run_pipeline(
         self,
@@ -408,8 +424,8 @@ class GovernanceEngine:
         if len(specs) > 4:
             raise ValueError("at most 4 changes per delta")
         self._last_specs = list(specs)
-        ch, rows = self._changes(deltas, specs)
-        self._ensure_arena(rows, deltas, len(specs))
+        ch, rows, frag = self._changes(deltas, specs)
+        need = self._ensure_arena(rows, deltas, len(specs))
         st = self.store
         pb, po, pl = st.pool.device_view(self.device)
         now = int(now_us if now_us is not None else _clock.now_us())
@@ -427,7 +443,10 @@ class GovernanceEngine:
             "ring_cap": cap, "slot_base": slot_base, "dstride": self.dmax, "rec_bytes": self._rec_bytes,
             "off_base": self._off_base, "id_stride": 3,
             "cursor": cursor.data_ptr() if cursor is not None else None,
+            "max_rec": need,  # the longest record (the ring slot is larger): small-batch kernel choice
         }
+        if frag is not None:
+            args.update(frag=frag[0].data_ptr(), frag_off=frag[1].data_ptr(), frag_len=frag[2].data_ptr())
         if cursor is not None:
             if cursor.dtype != torch.int64 or cursor.numel() not in (3, 4) or cursor.device != self.device:
                 raise ValueError("cursor must be an int64[3] (or [4]) tensor on the engine device")
@@ -439,7 +458,7 @@ class GovernanceEngine:
                                     "status": self._status})
         if stats is not None and fold:
             self._spread.add_into(stats)
-        self._keep = (agents, ch)
+        self._keep = (agents, ch, frag)
         if cursor is not None:
             return PipelineBatch(self, -1, n, -1, -1, deltas, list(specs), agents)
         self._next_slot = (slot_base + n) % cap

@@ -165,7 +165,7 @@ class TemplatePipeline:
         t["t_state"].index_fill_(0, self._slots64["tslot"], 255)
 
     def launch(self, session_agent: torch.Tensor, t0: Optional[int] = None, stats: Optional[torch.Tensor] = None,
-               sync: bool = True, variant: Optional[tuple] = None) -> tuple:
+               sync: bool = True, variant: Optional[tuple] = None, extra: Optional[dict] = None) -> tuple:
         """Run the pipeline for every session; ``session_agent`` = int32 [n] agent
         numbers (which agent joins and captures in each session).  ``stats``
         (int64[6]) accumulates sessions / ok / participants / deltas / commits /
@@ -211,6 +211,8 @@ class TemplatePipeline:
                         frag_len=tens["frag_len"].data_ptr())
         if variant is not None:
             args["waves"], args["small"] = int(variant[0]), int(variant[1])
+        if extra:  # measurement knobs (e.g. "phase_ticks": a uint64 device pointer)
+            args.update(extra)
         cuda = dev.type == "cuda"
         if cuda:
             if sync:

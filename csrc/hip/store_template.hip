@@ -266,6 +266,12 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
   const store::Tables& t = a.t;
   const int32_t D = a.deltas;
   const TemplateRows R = template_rows(a, i < a.n ? i : 0);
+  int ph = 0;  // phase timestamps (measurement: AHV template args "phase_ticks")
+  auto mark = [&]() {
+    if (a.phase_ticks && blockIdx.x == 0 && lane == 0) a.phase_ticks[16 * wave + ph] = __builtin_amdgcn_s_memrealtime();
+    ++ph;
+  };
+  mark();
   // every wave decides liveness before wave 3 writes the row (barrier below)
   const bool live = i < a.n && (R.ring || t.s_state[R.s] == store::kFree8);
   __syncthreads();
@@ -283,6 +289,7 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
       a.status[i] = TP_ROW_IN_USE;
     }
     live_c[lane] = committed ? 1 : 0;
+    mark();
   }
 
   // ---- records: render, prefix, (wait for the parent) tail, rows, tee -------------------
@@ -318,15 +325,21 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
     // the parent's hex starts one byte after the hole's opening quote
     hole = q > 0 ? len - record_suffix_len(tsd, turn) : 0u;
     hb = q > 0 ? static_cast<int32_t>(hole / 64u) : total / 16;
+    mark();
     sha256_init(st);
     sink.compress_blocks(st, 0, mine ? hb : 0);  // parent-independent blocks
+    mark();
   }
   const int64_t dr = (q < D && q < 3) ? R.drow(a, q) : 0;
   const int64_t off = (q < D && q < 3) ? R.doff(a, q) : 0;
-  auto finish = [&](void) {  // wave q, its digest in st: rows, LDS leaf, record bytes
+  auto publish = [&](void) {  // wave q: its digest → LDS (the next record's parent, a leaf)
     if (!mine) return;
 #pragma unroll
     for (int k = 0; k < 8; ++k) dig[q][k][lane] = st[k];
+  };
+  // rows + record bytes: after the barrier that hands the digest on (off the chain)
+  auto finish = [&](void) {
+    if (!mine) return;
     t.d_sess[dr] = static_cast<int32_t>(R.s);
     t.d_turn[dr] = static_cast<int32_t>(turn);
     t.d_prev[dr] = q > 0 ? static_cast<int32_t>(R.drow(a, q - 1)) : -1;
@@ -342,18 +355,23 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
     }
     if (!a.notee) sink.tee(reinterpret_cast<uint32_t*>(t.payload + off), static_cast<int32_t>((len + 3u) >> 2));
   };
-  if (q == 0) finish();
+  if (q == 0) publish();
+  mark();
   // record q (1, 2) after record q − 1: patch the parent's hex, hash the tail
 #pragma unroll
   for (int step = 1; step < 3; ++step) {
     __syncthreads();  // dig[step − 1] is complete
+    mark();
+    if (q == step - 1 && q < D) finish();  // the previous record's rows, beside the next record's tail
     if (step < D && q == step) {
       uint32_t par[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) par[k] = dig[step - 1][k][lane];
       if (mine) sink.patch_hex(hole + 1u, par);
       sink.compress_blocks(st, mine ? hb : 0, mine ? total / 16 : 0);
-      finish();
+      mark();
+      publish();
+      mark();
     }
     if (step == 2 && D == 3 && q == 0) {
       // node(l0, l1) and the root's first block (its hex) while record 2 is hashed
@@ -370,9 +388,12 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
       sha256_compress(m, w);
 #pragma unroll
       for (int k = 0; k < 8; ++k) mid[k][lane] = m[k];
+      mark();
     }
   }
   __syncthreads();  // every digest (and the root's first block) is in LDS
+  mark();
+  if (q == 2 && q < D) finish();  // the last record's rows, beside the root
 
   // ---- Merkle root (K09) → s_root --------------------------------------------------------
   if (wave == 1 && live) {
@@ -403,6 +424,7 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) t.s_root[8 * R.s + k] = root[k];
+    mark();
   }
 
   // ---- counters (X04) and lifecycle events (N08): wave 3 ----------------------------------
@@ -436,6 +458,7 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
       });
     }
   }
+  mark();
 }
 
 template <class T>
@@ -483,6 +506,7 @@ TemplateArgs template_args(const store::Tables& t, const py::dict& d) {
   a.off_base = opt("off_base") ? d["off_base"].cast<int64_t>() : 0;
   a.id_stride = opt("id_stride") ? d["id_stride"].cast<uint64_t>() : 1;
   a.cursor = opt("cursor") ? P<const int64_t>(d, "cursor") : nullptr;
+  a.phase_ticks = opt("phase_ticks") ? P<uint64_t>(d, "phase_ticks") : nullptr;
   if (opt("ev_cursor")) {
     a.ev = EventRing{P<uint8_t>(d, "ev_type"), P<int32_t>(d, "ev_slot"), P<int32_t>(d, "ev_agent"),
                      P<int64_t>(d, "ev_ts_us"), P<int32_t>(d, "ev_aux"), P<unsigned long long>(d, "ev_cursor"),
@@ -544,8 +568,9 @@ void store_template_run(const store::Tables& t, bool gpu, const py::dict& d, uin
   const int64_t small = d.contains("small") && !d["small"].is_none() ? d["small"].cast<int64_t>() : template_small();
   // cooperative small-batch kernel: D ≤ 3 records of ≤ 8 blocks (the caller's record
   // reservation `max_rec` bytes, or the ring's), at most one workgroup per CU
-  const int64_t max_rec = a.ring_cap > 0 ? a.rec_bytes
-                          : (d.contains("max_rec") && !d["max_rec"].is_none() ? d["max_rec"].cast<int64_t>() : 0);
+  // (ring mode: the slot size bounds it; the caller's exact bound wins when given)
+  const int64_t max_rec = d.contains("max_rec") && !d["max_rec"].is_none() ? d["max_rec"].cast<int64_t>()
+                          : (a.ring_cap > 0 ? a.rec_bytes : 0);
   const int coop = template_coop();
   const bool use_coop = coop != 0 && a.n <= coop_max_sessions() && a.deltas >= 1 && a.deltas <= 3 && max_rec > 0 &&
                         max_rec <= 512 && !(b.ab & 64) &&

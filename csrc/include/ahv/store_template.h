@@ -77,6 +77,7 @@ struct TemplateArgs {
   // scalars, so a launch captured in a hipGraph stays correct on replay (N07/N09).
   const int64_t* cursor;
   EventRing ev;                  // lifecycle events (N08); ev.cursor == null: none
+  uint64_t* phase_ticks;         // measurement only (or null): per-wave phase timestamps of workgroup 0
 };
 
 AHV_HD int64_t tp_slot_base(const TemplateArgs& a) { return a.cursor ? a.cursor[0] : a.slot_base; }
