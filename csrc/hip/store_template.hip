@@ -253,18 +253,96 @@ __global__ __launch_bounds__(kWaveLanes, MinWaves) void store_template_kernel(Te
 // template_session (one semantics source: template_head, emit_delta_payload).
 constexpr int kCoopWaves = 4;
 
+// Workgroup-scope flags between the cooperating waves (LDS).
+__device__ __forceinline__ uint32_t coop_get(const uint32_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void coop_wait(const uint32_t* f, uint32_t v) {
+  while (coop_get(f) < v) __builtin_amdgcn_s_sleep(1);
+}
+// Publish `v`: every LDS write this wave issued before is visible to a wave that
+// reads `v` with coop_get (the fence waits for the wave's LDS operations).
+__device__ __forceinline__ void coop_set(uint32_t* f, uint32_t v, uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// K+W schedule of one message block held in a [word][lane] LDS column (stride 64)
+// into a [t][lane] column of the K+W ring.
+__device__ __forceinline__ void coop_expand(const uint32_t* w, uint32_t* kw) {
+  uint32_t x[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    x[k] = w[k * kWaveLanes];
+    kw[k * kWaveLanes] = x[k] + sha256_k(k);
+  }
+#pragma unroll
+  for (int k = 16; k < 64; ++k) {
+    const uint32_t a = x[(k + 1) & 15], b = x[(k + 14) & 15];
+    const uint32_t s0 = xor3(rotr32(a, 7), rotr32(a, 18), a >> 3);
+    const uint32_t s1 = xor3(rotr32(b, 17), rotr32(b, 19), b >> 10);
+    const uint32_t v = x[k & 15] + s0 + x[(k + 9) & 15] + s1;
+    x[k & 15] = v;
+    kw[k * kWaveLanes] = v + sha256_k(k);
+  }
+}
+
+// The 64 rounds over a K+W column (store::sha256_rounds_kw with stride 64).
+__device__ __forceinline__ void coop_rounds(uint32_t st[8], const uint32_t* kw) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+  uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
+  uint32_t q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) q[k] = kw[k * kWaveLanes];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    const uint32_t kwi = q[k & 7];
+    if (k + 8 < 64) q[k & 7] = kw[(k + 8) * kWaveLanes];
+    const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    const uint32_t t1 = store::add3u(h + kwi, S1, sha_ch(e, f, g));
+    const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+    const uint32_t na = store::add3u(t1, S0, sha_maj(a, b, c));
+    h = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = na;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t y = __shfl_xor(v, o, kWaveLanes);
+    v = y > v ? y : v;
+  }
+  return v;
+}
+
+// The chain's compressions (record 0 whole, records 1 and 2 after the parent hole)
+// run as rounds only: wave 3, once the session rows are written, expands each
+// block's message schedule into a two-slot K+W ring in LDS one block ahead of the
+// hashing wave (the schedule is a third of a compression).  Waves hand off
+// through LDS flags (no workgroup barrier after the first): digests d0..d2,
+// segment ready (window final, block ranges set), produced / consumed ring
+// blocks, the root's first-block state, the committed flags.
+enum CoopFlag : int { CF_DIG = 0, CF_MID = 3, CF_LIVE = 4, CF_SEG = 5, CF_PROD = 8, CF_CONS = 9, CF_N = 10 };
+
 template <int W>
 __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coop_kernel(TemplateArgs a) {
   constexpr int kWinWords = (W * 16 + 1) * kWaveLanes;
   __shared__ uint32_t win[3 * kWinWords];
-  __shared__ uint32_t dig[3][8][kWaveLanes];  // record digests (Merkle leaves, parents)
-  __shared__ uint32_t mid[8][kWaveLanes];     // root state after its first block (D = 3)
-  __shared__ uint8_t live_c[kWaveLanes];      // the session committed a root (wave 3's answer)
+  __shared__ uint32_t kwb[2][64 * kWaveLanes];  // K+W ring, [t][lane]
+  __shared__ uint32_t dig[3][8][kWaveLanes];    // record digests (Merkle leaves, parents)
+  __shared__ uint32_t mid[8][kWaveLanes];       // root state after its first block (D = 3)
+  __shared__ int32_t seglo[3][kWaveLanes], seghi[3][kWaveLanes], segK[3];
+  __shared__ uint8_t live_c[kWaveLanes];        // the session committed a root (wave 3's answer)
+  __shared__ uint32_t flags[CF_N];
   const int wave = static_cast<int>(threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63u;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaveLanes + lane;
   const store::Tables& t = a.t;
   const int32_t D = a.deltas;
+  const int nrec = D < 3 ? D : 3;
   const TemplateRows R = template_rows(a, i < a.n ? i : 0);
   int ph = 0;  // phase timestamps (measurement: AHV template args "phase_ticks")
   auto mark = [&]() {
@@ -272,7 +350,8 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
     ++ph;
   };
   mark();
-  // every wave decides liveness before wave 3 writes the row (barrier below)
+  if (threadIdx.x < CF_N) flags[threadIdx.x] = 0;
+  // every wave decides liveness before wave 3 writes the row
   const bool live = i < a.n && (R.ring || t.s_state[R.s] == store::kFree8);
   __syncthreads();
 
@@ -280,7 +359,9 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
   uint32_t u[4];
   const int64_t t0 = tp_t0(a);
   if (live) uuid4_words(a.seed, tp_id_base(a) + a.id_stride * static_cast<uint64_t>(i), u);
+
   if (wave == 3) {
+    // ---- session rows, then the schedule producer, then counters and events ----------
     c.v[0] = i < a.n ? 1u : 0u;
     bool committed = false;
     if (live) {
@@ -289,15 +370,60 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
       a.status[i] = TP_ROW_IN_USE;
     }
     live_c[lane] = committed ? 1 : 0;
+    coop_set(&flags[CF_LIVE], 1, lane);
     mark();
+    uint32_t idx = 0;
+    for (int sg = 0; sg < nrec; ++sg) {
+      coop_wait(&flags[CF_SEG + sg], 1);
+      const int32_t K = segK[sg], lo = seglo[sg][lane], hi = seghi[sg][lane];
+      const uint32_t* col = win + sg * kWinWords + lane;
+      for (int32_t k = 0; k < K; ++k, ++idx) {
+        while (idx - coop_get(&flags[CF_CONS]) >= 2u) __builtin_amdgcn_s_sleep(1);
+        if (lo + k < hi) coop_expand(col + (lo + k) * 16 * kWaveLanes, kwb[idx & 1] + lane);
+        coop_set(&flags[CF_PROD], idx + 1, lane);
+      }
+    }
+    mark();
+    if (a.stats) {
+#pragma unroll
+      for (int k = 0; k < kPipeStats; ++k) {
+        const uint32_t sm = wave_sum(c.v[k]);
+        if (lane == 0 && sm)
+          atomicAdd(a.stats + (blockIdx.x % kStatSpread) * kPipeStats + k, static_cast<unsigned long long>(sm));
+      }
+    }
+    if (a.ev.cursor) {
+      uint32_t nev = 0;
+      if (live) nev = template_event_count(c, t.s_terminated[R.s] != 0);
+      uint32_t incl = nev;
+#pragma unroll
+      for (int o = 1; o < kWaveLanes; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, kWaveLanes);
+        if (lane >= static_cast<uint32_t>(o)) incl += y;
+      }
+      const uint32_t tot = __shfl(incl, kWaveLanes - 1, kWaveLanes);
+      const int seg = static_cast<int>(blockIdx.x % kStatSpread);
+      unsigned long long base = 0;
+      if (lane == 0 && tot) base = atomicAdd(a.ev.cursor + seg, static_cast<unsigned long long>(tot));
+      base = __shfl(base, 0, kWaveLanes);
+      if (live) {
+        const unsigned long long first = base + (incl - nev);
+        template_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
+          event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
+        });
+      }
+    }
+    mark();
+    return;
   }
 
-  // ---- records: render, prefix, (wait for the parent) tail, rows, tee -------------------
+  // ---- waves 0..2: record q --------------------------------------------------------------
   WordWindowSink<W> sink;
-  sink.g_win = win + (wave < 3 ? wave : 0) * kWinWords;
+  sink.g_win = win + wave * kWinWords;
   sink.lane = lane;
   const int q = wave;
-  const bool mine = live && q < D && q < 3;
+  const bool rec = q < nrec;  // this wave owns a record
+  const bool mine = live && rec;
   uint32_t st[8];
   uint32_t len = 0;
   int32_t total = 0, hb = 0;
@@ -305,7 +431,9 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
   const int32_t ag = live ? a.session_agent[i] : 0;
   const int64_t tsd = t0 + 1 + q;
   const uint32_t turn = static_cast<uint32_t>(q + 1);
-  if (q < D && q < 3) {
+  const int64_t dr = rec ? R.drow(a, q) : 0;
+  const int64_t off = rec ? R.doff(a, q) : 0;
+  if (rec) {
     SessionIdent sid;
     sid.str_id = -1;
 #pragma unroll
@@ -324,20 +452,26 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
     }, len);
     // the parent's hex starts one byte after the hole's opening quote
     hole = q > 0 ? len - record_suffix_len(tsd, turn) : 0u;
-    hb = q > 0 ? static_cast<int32_t>(hole / 64u) : total / 16;
+    hb = q > 0 ? static_cast<int32_t>(hole / 64u) : 0;
+    // the chain segment: record 0 whole, records 1, 2 from the block holding the hole
+    const int32_t lo = mine ? hb : 0, hi = mine ? total / 16 : 0;
+    seglo[q][lane] = lo;
+    seghi[q][lane] = hi;
+    const int32_t K = wave_max(hi - lo);
+    if (lane == 0) segK[q] = K;
     mark();
     sha256_init(st);
-    sink.compress_blocks(st, 0, mine ? hb : 0);  // parent-independent blocks
+    if (q > 0) sink.compress_blocks(st, 0, mine ? hb : 0);  // parent-independent blocks
     mark();
   }
-  const int64_t dr = (q < D && q < 3) ? R.drow(a, q) : 0;
-  const int64_t off = (q < D && q < 3) ? R.doff(a, q) : 0;
-  auto publish = [&](void) {  // wave q: its digest → LDS (the next record's parent, a leaf)
-    if (!mine) return;
+  auto publish = [&](void) {  // its digest → LDS (the next record's parent, a leaf)
+    if (mine) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dig[q][k][lane] = st[k];
+      for (int k = 0; k < 8; ++k) dig[q][k][lane] = st[k];
+    }
+    coop_set(&flags[CF_DIG + q], 1, lane);
   };
-  // rows + record bytes: after the barrier that hands the digest on (off the chain)
+  // rows + record bytes (after the digest is handed on: off the chain)
   auto finish = [&](void) {
     if (!mine) return;
     t.d_sess[dr] = static_cast<int32_t>(R.s);
@@ -355,55 +489,62 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
     }
     if (!a.notee) sink.tee(reinterpret_cast<uint32_t*>(t.payload + off), static_cast<int32_t>((len + 3u) >> 2));
   };
-  if (q == 0) publish();
-  mark();
-  // record q (1, 2) after record q − 1: patch the parent's hex, hash the tail
-#pragma unroll
-  for (int step = 1; step < 3; ++step) {
-    __syncthreads();  // dig[step − 1] is complete
-    mark();
-    if (q == step - 1 && q < D) finish();  // the previous record's rows, beside the next record's tail
-    if (step < D && q == step) {
+  if (rec) {
+    if (q > 0) {  // the parent's digest → its hex into the hole
+      coop_wait(&flags[CF_DIG + q - 1], 1);
       uint32_t par[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) par[k] = dig[step - 1][k][lane];
+      for (int k = 0; k < 8; ++k) par[k] = dig[q - 1][k][lane];
       if (mine) sink.patch_hex(hole + 1u, par);
-      sink.compress_blocks(st, mine ? hb : 0, mine ? total / 16 : 0);
-      mark();
-      publish();
-      mark();
     }
-    if (step == 2 && D == 3 && q == 0) {
-      // node(l0, l1) and the root's first block (its hex) while record 2 is hashed
-      uint32_t l0[8], l1[8], n01[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        l0[k] = dig[0][k][lane];
-        l1[k] = dig[1][k][lane];
-      }
-      sink.node(l0, l1, n01);
-      uint32_t w[16], m[8];
-      digest_to_hex_words(n01, w);
-      sha256_init(m);
-      sha256_compress(m, w);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) mid[k][lane] = m[k];
-      mark();
+    coop_set(&flags[CF_SEG + q], 1, lane);  // the window is final: the producer may expand it
+    // the chain segment as rounds over the producer's K+W ring
+    uint32_t base = 0;
+    for (int sg = 0; sg < q; ++sg) base += static_cast<uint32_t>(segK[sg]);
+    const int32_t K = segK[q], lo = seglo[q][lane], hi = seghi[q][lane];
+    for (int32_t k = 0; k < K; ++k) {
+      const uint32_t idx = base + static_cast<uint32_t>(k);
+      coop_wait(&flags[CF_PROD], idx + 1);
+      if (lo + k < hi) coop_rounds(st, kwb[idx & 1] + lane);
+      coop_set(&flags[CF_CONS], idx + 1, lane);
     }
+    mark();
+    publish();
+    mark();
+    finish();
   }
-  __syncthreads();  // every digest (and the root's first block) is in LDS
-  mark();
-  if (q == 2 && q < D) finish();  // the last record's rows, beside the root
+  if (q == 0 && D == 3) {
+    // node(l0, l1) and the root's first block (its hex) while record 2 is hashed
+    coop_wait(&flags[CF_DIG + 1], 1);
+    uint32_t l0[8], l1[8], n01[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      l0[k] = dig[0][k][lane];
+      l1[k] = dig[1][k][lane];
+    }
+    sink.node(l0, l1, n01);
+    uint32_t w[16], m[8];
+    digest_to_hex_words(n01, w);
+    sha256_init(m);
+    sha256_compress(m, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mid[k][lane] = m[k];
+    coop_set(&flags[CF_MID], 1, lane);
+    mark();
+  }
 
-  // ---- Merkle root (K09) → s_root --------------------------------------------------------
-  if (wave == 1 && live) {
+  // ---- Merkle root (K09) → s_root: wave 1 ------------------------------------------------
+  if (wave == 1 && D >= 1) {
+    coop_wait(&flags[CF_DIG + nrec - 1], 1);
+    coop_wait(&flags[CF_LIVE], 1);
     uint32_t root[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (live_c[lane] && !(a.ab & 4)) {
+    if (live && live_c[lane] && !(a.ab & 4)) {
       if (D == 3) {
         uint32_t l2[8], n22[8], w[16];
 #pragma unroll
         for (int k = 0; k < 8; ++k) l2[k] = dig[2][k][lane];
         sink.node(l2, l2, n22);
+        coop_wait(&flags[CF_MID], 1);
 #pragma unroll
         for (int k = 0; k < 8; ++k) root[k] = mid[k][lane];
         digest_to_hex_words(n22, w);
@@ -422,43 +563,12 @@ __global__ __launch_bounds__(kCoopWaves * kWaveLanes, 1) void store_template_coo
         for (int k = 0; k < 8; ++k) root[k] = dig[0][k][lane];
       }
     }
+    if (live) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t.s_root[8 * R.s + k] = root[k];
+      for (int k = 0; k < 8; ++k) t.s_root[8 * R.s + k] = root[k];
+    }
     mark();
   }
-
-  // ---- counters (X04) and lifecycle events (N08): wave 3 ----------------------------------
-  if (wave != 3) return;
-  if (a.stats) {
-#pragma unroll
-    for (int k = 0; k < kPipeStats; ++k) {
-      const uint32_t sm = wave_sum(c.v[k]);
-      if (lane == 0 && sm)
-        atomicAdd(a.stats + (blockIdx.x % kStatSpread) * kPipeStats + k, static_cast<unsigned long long>(sm));
-    }
-  }
-  if (a.ev.cursor) {
-    uint32_t nev = 0;
-    if (live) nev = template_event_count(c, t.s_terminated[R.s] != 0);
-    uint32_t incl = nev;
-#pragma unroll
-    for (int o = 1; o < kWaveLanes; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, kWaveLanes);
-      if (lane >= static_cast<uint32_t>(o)) incl += y;
-    }
-    const uint32_t tot = __shfl(incl, kWaveLanes - 1, kWaveLanes);
-    const int seg = static_cast<int>(blockIdx.x % kStatSpread);
-    unsigned long long base = 0;
-    if (lane == 0 && tot) base = atomicAdd(a.ev.cursor + seg, static_cast<unsigned long long>(tot));
-    base = __shfl(base, 0, kWaveLanes);
-    if (live) {
-      const unsigned long long first = base + (incl - nev);
-      template_events(a, i, c, [&](uint32_t k, int64_t slot, const EventRec& e) {
-        event_store(a.ev, seg, first + k, static_cast<int32_t>(slot), e);
-      });
-    }
-  }
-  mark();
 }
 
 template <class T>

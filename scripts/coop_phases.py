@@ -16,11 +16,10 @@ from agent_hypervisor_amd.models import store_template as TT  # noqa: E402
 from agent_hypervisor_amd.models.store import GovernanceStore  # noqa: E402
 
 NAMES = {
-    0: ["start", "render", "hash r0", "rows+tee r0", "barrier1", "barrier2", "n01+root blk1", "barrier3"],
-    1: ["start", "render", "prefix r1", "-", "barrier1", "tail r1", "rows+tee r1", "barrier2", "barrier3",
-        "n22+root"],
-    2: ["start", "render", "prefix r2", "-", "barrier1", "barrier2", "tail r2", "rows+tee r2", "barrier3"],
-    3: ["start", "session rows", "-", "barrier1", "barrier2", "barrier3", "events"],
+    0: ["start", "render", "-", "chain r0", "published", "n01+root blk1"],
+    1: ["start", "render", "prefix r1", "chain r1", "published", "root"],
+    2: ["start", "render", "prefix r2", "chain r2", "published"],
+    3: ["start", "session rows", "schedules produced", "events"],
 }
 
 
