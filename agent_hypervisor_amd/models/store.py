@@ -396,14 +396,7 @@ class GovernanceStore:
         if block:
             self._c.check_frees(True)  # row reclaims posted without waiting (native allocator)
         bad = self._c.verify_expects(block)
-        err = None
-        if bad is not None:
-            for (owner, make, arg), r in bad:
-                e = make(arg, r)
-                if owner is not None:
-                    owner._spec_failed(e)
-                elif err is None:
-                    err = e
+        err = self._distribute(bad) if bad is not None else None
         ds = self._deferred
         if not ds:
             if err is not None:
@@ -432,6 +425,19 @@ class GovernanceStore:
         self._deferred = pending + self._deferred
         if err is not None:
             raise err
+
+    @staticmethod
+    def _distribute(bad) -> Optional[Exception]:
+        """Hand each mismatched expectation ``((owner, make_error, arg), result)`` to
+        its owner; returns the first unowned error (the caller raises it)."""
+        err = None
+        for (owner, make, arg), r in bad:
+            e = make(arg, r)
+            if owner is not None:
+                owner._spec_failed(e)
+            elif err is None:
+                err = e
+        return err
 
     def discard(self, seq: int) -> None:
         """Forget a kept result (``post(..., keep=True)``) that will never be read."""

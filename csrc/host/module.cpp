@@ -18,6 +18,7 @@ void register_store(py::module_& m);
 void register_global_liability(py::module_& m);
 void register_merkle_tree(py::module_& m);
 void register_store_views(py::module_& m);
+void register_control(py::module_& m);
 }  // namespace host
 }  // namespace ahv
 
@@ -32,4 +33,5 @@ PYBIND11_MODULE(_C, m) {
   ahv::host::register_global_liability(m);
   ahv::host::register_merkle_tree(m);
   ahv::host::register_store_views(m);
+  ahv::host::register_control(m);
 }

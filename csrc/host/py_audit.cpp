@@ -164,6 +164,9 @@ static int utc_isoformat(PyObject* dt, char* out) {
 // With `null_parent_at` set, `parent_hash` is not read: the payload is rendered
 // with a `null` parent and the byte offset of that `null` is stored, so the
 // device store can splice the chain head's digest in (csrc/host/py_store.cpp).
+bool render_delta_fields(PyObject* agent, PyObject* changes, PyObject* delta_id, PyObject* parent, PyObject* session,
+                         PyObject* ts, PyObject* turn, std::string& out, size_t* null_parent_at);
+
 bool render_delta(PyObject* d, std::string& out, size_t* null_parent_at = nullptr) {
   Names* nm = names();
   Ref agent(PyObject_GetAttr(d, nm->agent_did));
@@ -175,6 +178,19 @@ bool render_delta(PyObject* d, std::string& out, size_t* null_parent_at = nullpt
   Ref turn(PyObject_GetAttr(d, nm->turn_id));
   if (!agent.p || !changes.p || !delta_id.p || !parent.p || !session.p || !ts.p || !turn.p)
     throw py::error_already_set();
+  return render_delta_fields(agent.p, changes.p, delta_id.p, parent.p, session.p, ts.p, turn.p, out, null_parent_at);
+}
+
+// The same rendering from the field values themselves (the native control plane
+// renders a capture before its delta object exists: no attribute lookups).
+bool render_delta_fields(PyObject* agent_p, PyObject* changes_p, PyObject* delta_id_p, PyObject* parent_p,
+                         PyObject* session_p, PyObject* ts_p, PyObject* turn_p, std::string& out,
+                         size_t* null_parent_at) {
+  Names* nm = names();
+  struct Field {
+    PyObject* p;
+  } agent{agent_p}, changes{changes_p}, delta_id{delta_id_p}, parent{parent_p}, session{session_p}, ts{ts_p},
+      turn{turn_p};
   if (!PyLong_CheckExact(turn.p)) return false;
   char isobuf[40];
   int isolen = utc_isoformat(ts.p, isobuf);
@@ -415,6 +431,27 @@ static py::object uuid4(const std::string& prefix) {
   put_hex(o + 19, lo >> 48, 4); o[23] = '-';
   put_hex(o + 24, lo & 0xffffffffffffull, 12);
   return py::reinterpret_steal<py::object>(s);
+}
+
+// prefix + a fresh uuid4 as a new str reference (nullptr on allocation failure),
+// and the uuid's two halves: the native control plane's id minting (py_control.cpp).
+PyObject* mint_uuid4(const char* prefix, size_t pl, uint64_t* hi_out, uint64_t* lo_out) {
+  uint64_t hi = g_rng.next(), lo = g_rng.next();
+  hi = (hi & 0xffffffffffff0fffull) | 0x0000000000004000ull;
+  lo = (lo & 0x3fffffffffffffffull) | 0x8000000000000000ull;
+  PyObject* s = PyUnicode_New(static_cast<Py_ssize_t>(pl + 36), 127);
+  if (!s) return nullptr;
+  char* o = reinterpret_cast<char*>(PyUnicode_1BYTE_DATA(s));
+  std::memcpy(o, prefix, pl);
+  o += pl;
+  put_hex(o, hi >> 32, 8); o[8] = '-';
+  put_hex(o + 9, (hi >> 16) & 0xffff, 4); o[13] = '-';
+  put_hex(o + 14, hi & 0xffff, 4); o[18] = '-';
+  put_hex(o + 19, lo >> 48, 4); o[23] = '-';
+  put_hex(o + 24, lo & 0xffffffffffffull, 12);
+  if (hi_out) *hi_out = hi;
+  if (lo_out) *lo_out = lo;
+  return s;
 }
 
 // uuid4_id(prefix="") -> (prefix + uuid4 string, hi, lo): the uuid's two 64-bit

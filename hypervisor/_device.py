@@ -1444,7 +1444,10 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         return step
 
     async def execute_step(self, saga_id: str, step_id: str, executor: Callable[..., Any]) -> Any:
-        self._guard()
+        if _CTL:
+            _C.ctl_guard(self._owner)
+        else:
+            self._guard()
         saga = self._get_saga(saga_id)
         step = self._get_step(saga, step_id)
         attempts = 1 + step.max_retries
@@ -1452,8 +1455,11 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
         for attempt in range(attempts):
             # the EXECUTING transition is posted and the executor starts at once when this
             # process knows the step's state allows it (its result is checked right after)
-            seq = step.post_transition(StepState.EXECUTING, retry=attempt) \
-                if step.can_speculate(StepState.EXECUTING) else None
+            if _CTL and _SPECULATE and type(step) is DeviceSagaStep:
+                seq = _C.ctl_step_begin(step, attempt)
+            else:
+                seq = step.post_transition(StepState.EXECUTING, retry=attempt) \
+                    if step.can_speculate(StepState.EXECUTING) else None
             if seq is None:
                 await step.transition_async(StepState.EXECUTING, retry=attempt)
             try:
@@ -1475,6 +1481,9 @@ class DeviceSagaOrchestrator(SagaOrchestrator):
                     # EXECUTING was known-valid when posted, and COMMITTED is allowed from
                     # EXECUTING: neither needs the device's answer before returning —
                     # both are verified with the store's next interaction
+                    if _CTL and type(step) is DeviceSagaStep:
+                        _C.ctl_step_commit(self._owner, step, seq)
+                        return result
                     st = self._store
                     slot = step.slot
                     st.expect(seq, _OK, (self._owner, _transition_refused, (slot, StepState.EXECUTING)))
@@ -1672,6 +1681,10 @@ def close_hypervisor(hv) -> int:
     st = hv._store
     if st is None or st is CLOSED or getattr(st, "_closed", False):
         return 0
+    if _CTL:
+        n = _C.ctl_close_hypervisor(hv)  # one native pass (own sessions, no vouching engine)
+        if n >= 0:
+            return n
     # No wait for the commands still in flight: the worker runs commands in order, so
     # the FREE_ROWS that later reclaims these rows executes after every command posted
     # for them (a divergence of a speculated post goes to its session, now closed).
@@ -1752,6 +1765,44 @@ def counters(hv) -> dict:
     a, p, g = res.cpu().tolist()
     out.update(active_sessions=int(a), total_participants=int(p), active_sagas=int(g))
     return out
+
+
+# ------------------------------------------------------------------ native control plane
+
+# The per-call hot paths in C++ (csrc/host/py_control.cpp): the same objects and
+# semantics, without a Python frame per command (AHV_NATIVE_CTL=0: the Python path).
+_CTL = os.environ.get("AHV_NATIVE_CTL", "1") != "0" and hasattr(_C, "ctl_init")
+
+
+def _install_native() -> None:
+    from hypervisor import _clock
+
+    DeviceDeltaEngine._py_capture = DeviceDeltaEngine.__dict__["capture"]
+    DeviceSagaOrchestrator._py_create_saga = DeviceSagaOrchestrator.__dict__["create_saga"]
+    DeviceSagaOrchestrator._py_add_step = DeviceSagaOrchestrator.__dict__["add_step"]
+    _C.ctl_init({
+        "GovernanceStore": GovernanceStore, "DeviceSession": DeviceSession, "DeviceDelta": DeviceDelta,
+        "DeviceDeltaEngine": DeviceDeltaEngine, "DeviceSagaOrchestrator": DeviceSagaOrchestrator,
+        "DeviceSaga": DeviceSaga, "DeviceSagaStep": DeviceSagaStep, "DeviceCommitmentEngine": DeviceCommitmentEngine,
+        "CLOSED": CLOSED, "clock_dict": _clock.__dict__, "now": _clock.now, "to_us": _clock.to_us,
+        "mode_eventual": ConsistencyMode.EVENTUAL, "mode_strong": ConsistencyMode.STRONG,
+        "step_pending": StepState.PENDING, "step_executing": StepState.EXECUTING,
+        "step_committed": StepState.COMMITTED,
+        "exec_from": frozenset(s for s in StepState if StepState.EXECUTING in STEP_TRANSITIONS.get(s, ())),
+        "err_create": _create_refused, "err_join": _join_diverged, "err_activate": _activate_refused,
+        "err_transition": _transition_refused, "fb_capture": DeviceDeltaEngine._py_capture,
+        "fb_create_saga": DeviceSagaOrchestrator._py_create_saga, "fb_add_step": DeviceSagaOrchestrator._py_add_step,
+        "s_handshaking": _S_HANDSHAKING, "s_active": _S_ACTIVE, "step_executing_idx": _STEP_IDX[StepState.EXECUTING],
+        "step_committed_idx": _COMMITTED_IDX, "spec_lifecycle": _SPEC_LIFECYCLE, "step_speculate": _SPECULATE,
+        "spec_terminate": _SPEC_TERMINATE, "check_terminate": _CHECK_TERMINATE,
+    })
+    DeviceDeltaEngine.capture = _C.ctl_method(_C.ctl_capture)
+    DeviceSagaOrchestrator.create_saga = _C.ctl_method(_C.ctl_create_saga)
+    DeviceSagaOrchestrator.add_step = _C.ctl_method(_C.ctl_add_step)
+
+
+if _CTL:
+    _install_native()
 
 
 __all__ = [

@@ -167,9 +167,13 @@ class Hypervisor:
         if name in Hypervisor._LAZY_ENGINES and d.get("_store") is not None:
             _device = _device_mod()
             st = d["_store"]
+            if name == "commitment":  # every terminate registers here; no vouching engine needed
+                d["commitment"] = _device.DeviceCommitmentEngine(st)
+                return d[name]
             ve = d["vouching"] = _device.DeviceVouchingEngine(st, d["_tenant"], d.get("_max_exposure"))
             d["slashing"] = _device.DeviceSlashingEngine(ve)
-            d["commitment"] = _device.DeviceCommitmentEngine(st)
+            if "commitment" not in d:
+                d["commitment"] = _device.DeviceCommitmentEngine(st)
             return d[name]
         raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
 
@@ -221,8 +225,13 @@ class Hypervisor:
             raise ValueError(f"Session {session_id} already exists")
         if self._store is not None:
             _device = _device_mod()
-            sso = _device.DeviceSession(self._store, config, creator_did, session_id=session_id)  # HANDSHAKING
-            managed = ManagedSession(sso, *_device.session_views(self._store, sso, self._sessions.saga_rows))
+            views = _device._C.ctl_session(self._store, config, creator_did, session_id, self._sessions.saga_rows) \
+                if _device._CTL and _device._SPEC_LIFECYCLE else None  # native: row + views in one call
+            if views is None:
+                sso = _device.DeviceSession(self._store, config, creator_did, session_id=session_id)  # HANDSHAKING
+                views = (sso, *_device.session_views(self._store, sso, self._sessions.saga_rows))
+            managed = ManagedSession(*views)
+            sso = views[0]
         else:
             sso = SharedSessionObject(config=config, creator_did=creator_did, session_id=session_id)
             sso.begin_handshake()
@@ -272,7 +281,14 @@ class Hypervisor:
                 sigma_eff = min(sigma_raw, self.nexus.resolve_sigma(agent_did, history=agent_history))
 
         if self._store is not None:  # ring gate (K01) + admission on the device
-            ring = await managed.sso.join_gated_async(agent_did, sigma_raw, sigma_eff, verification.is_trustworthy)
+            _d = _device_mod()
+            got = _d._C.ctl_join(managed.sso, agent_did, sigma_raw, sigma_eff, verification.is_trustworthy) \
+                if _d._CTL else None  # a join the device will admit: posted, verified later
+            if got is not None:
+                ring = _d._RINGS[got]
+            else:
+                ring = await managed.sso.join_gated_async(agent_did, sigma_raw, sigma_eff,
+                                                          verification.is_trustworthy)
         else:
             ring = self.ring_enforcer.compute_ring(sigma_eff)
             if not verification.is_trustworthy:
@@ -288,7 +304,9 @@ class Hypervisor:
     async def activate_session(self, session_id: str) -> None:
         sso = self._get_session(session_id).sso
         if self._store is not None:
-            await sso.activate_async()
+            _d = _device_mod()
+            if not (_d._CTL and _d._C.ctl_activate(sso)):  # native: a known-good activation is posted
+                await sso.activate_async()
         else:
             sso.activate()
         if self.event_bus is not None:
@@ -331,6 +349,16 @@ class Hypervisor:
         session's bonds (K07) → GC retention count → archive."""
         _d = _device_mod()
         sso, de, st = managed.sso, managed.delta_engine, self._store
+        pre = _d._C.ctl_close(self, session_id, sso, de) \
+            if _d._CTL and _d._CHECK_TERMINATE and not _d._SPEC_TERMINATE else None
+        if pre is not None:
+            # native: guard, GC cutoff, the host's root / GC-count prediction and the
+            # posted close in one call; the bookkeeping that needs no device answer
+            # runs while the hash engine finishes, then the root is awaited
+            seq, root_pred, expired_pred, n = pre
+            self._terminate_gc(session_id, sso, de, expired_pred, n)
+            r = await st.result_async(seq, 13, 0)
+            return self._terminate_checked(session_id, sso, r, (root_pred, expired_pred))
         guard = getattr(sso, "_guard", None)
         if guard is not None:  # a speculation of this session the device refused raises here
             guard()
@@ -401,6 +429,35 @@ class Hypervisor:
             self._terminate_events(session_id, root)
             return root
         return self._terminated(session_id, sso, de, root, int(r[11]), n)
+
+    def _terminate_checked(self, session_id: str, sso, r: tuple, check: tuple) -> Optional[str]:
+        """The device's answer to a terminate posted with the host's prediction
+        ``check`` = (root, GC count) of a session with no liability rows: validate
+        (speculations, status, GC count, root), then register and publish."""
+        _d = _device_mod()
+        st = self._store
+        st.verify_deferred()  # every post before the close has completed now
+        if sso._poisoned is not None:
+            raise sso._poisoned
+        if r[0]:
+            if r[0] == _d._st.ST_BAD_STATE:
+                raise _d._lifecycle(r[1], SessionState.ACTIVE, SessionState.HANDSHAKING)
+            _d._check(r, "terminate")
+        root = _d._hex(r[2:10]) if r[1] else None
+        if int(r[11]) != check[1]:
+            err = _d._st.StoreError(f"device GC count {int(r[11])} of session {session_id} differs from the "
+                                    f"host prediction {check[1]}")
+            sso._poisoned = err
+            raise err
+        if sso.config.enable_audit and check[0] != root:
+            err = _d._st.StoreError(f"device Merkle root {root} of session {session_id} differs from the host "
+                                    f"prediction {check[0]}")
+            sso._poisoned = err
+            raise err
+        if root is not None:
+            self.commitment.register(sso)
+        self._terminate_events(session_id, root)
+        return root
 
     def _terminated(self, session_id: str, sso, de, root: Optional[str], expired: int, n: int) -> Optional[str]:
         """Host bookkeeping after a device close: commitment, GC, events."""
