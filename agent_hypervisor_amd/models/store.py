@@ -132,6 +132,9 @@ class GovernanceStore:
     """
 
     RECLAIM_BATCH = 4096  # released delta rows per reclaim (native: py_store.cpp kReclaimDeltas)
+    # Command ring slots (512 B each, fine-grained device memory; AHV_STORE_SLOTS): a
+    # post finding its slot still unexecuted spins until the worker catches up
+    RING_SLOTS = 32768
 
     def __init__(self, device: str = "cuda", caps: Optional[dict] = None, idle_us: Optional[int] = None,
                  max_caps: Optional[dict] = None) -> None:
@@ -159,6 +162,7 @@ class GovernanceStore:
         ptrs = {k: v.data_ptr() for k, v in self.tables.items()}
         self._c = C.Store(
             dev.index if dev.type == "cuda" else -1, ptrs, dict(c),
+            nslots=_env_int("AHV_STORE_SLOTS", self.RING_SLOTS),
             idle_us=idle_us if idle_us is not None else _env_int("AHV_STORE_IDLE_US", 500),
         )
         self._lock = threading.RLock()

@@ -70,7 +70,8 @@ struct Names {
   X(min_sigma_eff) X(enable_audit) X(consistency_mode) X(saga_id) X(steps) X(error) X(execute_result)                 \
   X(compensation_result) X(step_id) X(action_id) X(execute_api) X(undo_api) X(timeout_seconds) X(max_retries)        \
   X(_hint) X(append) X(capture) X(alloc) X(_tenant_v) X(_tenant) X(gc) X(policy) X(delta_retention_days) X(sso)      \
-  X(delta_engine) X(saga) X(_sessions) X(_segs) X(_own) X(vouching) X(commitment) X(_closed)
+  X(delta_engine) X(saga) X(_sessions) X(_segs) X(_own) X(vouching) X(commitment) X(_closed) X(event_bus)   \
+  X(_device)
 #define AHV_DECL(n) PyObject* n = nullptr;
   AHV_NAMES(AHV_DECL)
 #undef AHV_DECL
@@ -107,6 +108,7 @@ struct Ctl {
   int step_executing_idx = 0, step_committed_idx = 0;
   bool spec_lifecycle = true, step_speculate = true, spec_terminate = false, check_terminate = true;
   PyObject* empty_tuple = nullptr;
+  PyObject* close_hv_fast = nullptr;  // _C.ctl_close_hypervisor
 };
 Ctl C;
 
@@ -1041,6 +1043,87 @@ PyObject* ctl_close(PyObject*, PyObject* const* args, Py_ssize_t nargsf) {
   });
 }
 
+// Hypervisor._terminate_checked for an answer that agrees with the prediction:
+// verify the session's speculations, take the device's root, register the
+// commitment; anything else (a device error, a divergence, an event bus to
+// publish to) goes to the Python implementation, which raises or publishes.
+PyObject* ctl_close_finish(PyObject*, PyObject* const* args, Py_ssize_t nargsf) {
+  return guarded([&]() -> PyObject* {
+    if (PyVectorcall_NARGS(nargsf) != 5) {
+      PyErr_SetString(PyExc_TypeError, "ctl_close_finish(hv, session_id, sso, r, check)");
+      return nullptr;
+    }
+    PyObject* hv = args[0];
+    PyObject* sid = args[1];
+    PyObject* sso = args[2];
+    PyObject* r = args[3];
+    PyObject* check = args[4];
+    auto slow = [&]() -> PyObject* {
+      return PyObject_CallMethod(hv, "_terminate_checked", "OOOO", sid, sso, r, check);
+    };
+    if (!PyTuple_CheckExact(r) || PyTuple_GET_SIZE(r) < 12 || !PyTuple_CheckExact(check) ||
+        PyTuple_GET_SIZE(check) != 2)
+      return slow();
+    Own hd(idict(hv));
+    Own sd(idict(sso));
+    if (!hd || !sd) return nullptr;
+    PyObject* bus = dget(hd.p, N.event_bus);
+    PyObject* gs = dget(sd.p, N._store);
+    Store* s = gs ? store_of(gs) : nullptr;
+    if (s == nullptr || (bus != nullptr && bus != Py_None)) return slow();
+    bool ok = true;
+    const int64_t status = as_i64(PyTuple_GET_ITEM(r, 0), &ok);
+    const int64_t has_root = ok ? as_i64(PyTuple_GET_ITEM(r, 1), &ok) : 0;
+    const int64_t gc_n = ok ? as_i64(PyTuple_GET_ITEM(r, 11), &ok) : 0;
+    const int64_t want_gc = ok ? as_i64(PyTuple_GET_ITEM(check, 1), &ok) : 0;
+    if (!ok || status != 0 || gc_n != want_gc) return slow();
+    if (!guard(gs, s, sd.p)) return nullptr;  // every post before the close has completed
+    Own root;
+    if (has_root) {
+      root.p = PyUnicode_New(64, 127);
+      if (!root) return nullptr;
+      uint32_t w[8];
+      for (int k = 0; k < 8; ++k) {
+        const int64_t v = as_i64(PyTuple_GET_ITEM(r, 2 + k), &ok);
+        w[k] = static_cast<uint32_t>(v);
+        if (!ok || v < 0 || v > 0xffffffffLL) return slow();
+      }
+      host::hex_bytes(w, PyUnicode_1BYTE_DATA(root.p));
+    } else {
+      Py_INCREF(Py_None);
+      root.p = Py_None;
+    }
+    Own cfg(PyObject_GetAttr(sso, N.config));
+    Own aud(cfg ? PyObject_GetAttr(cfg.p, N.enable_audit) : nullptr);
+    if (!aud) return nullptr;
+    const int audit = PyObject_IsTrue(aud.p);
+    if (audit < 0) return nullptr;
+    if (audit) {
+      const int same = PyObject_RichCompareBool(PyTuple_GET_ITEM(check, 0), root.p, Py_EQ);
+      if (same < 0) return nullptr;
+      if (!same) return slow();  // divergence: the Python path poisons the session and raises
+    }
+    if (root.p != Py_None) {
+      Own cm(PyObject_GetAttr(hv, N.commitment));  // built on first use (Hypervisor.__getattr__)
+      if (!cm) return nullptr;
+      if (Py_TYPE(cm.p) == reinterpret_cast<PyTypeObject*>(C.DeviceCommitmentEngine)) {
+        Own cd(idict(cm.p));
+        if (!cd) return nullptr;
+        PyObject* dev = dget(cd.p, N._device);
+        if (dev == nullptr || !PyDict_CheckExact(dev) || PyDict_SetItem(dev, sid, sso) < 0) {
+          if (PyErr_Occurred()) return nullptr;
+          Own rr(PyObject_CallMethod(cm.p, "register", "O", sso));
+          if (!rr) return nullptr;
+        }
+      } else {
+        Own rr(PyObject_CallMethod(cm.p, "register", "O", sso));
+        if (!rr) return nullptr;
+      }
+    }
+    return root.release();
+  });
+}
+
 // ------------------------------------------------------------------ teardown
 
 // close_hypervisor(hv) for a hypervisor whose sessions were all created one by
@@ -1198,6 +1281,111 @@ PyObject* ctl_close_hypervisor(PyObject*, PyObject* const* args, Py_ssize_t narg
   });
 }
 
+// ------------------------------------------------------------------ finalisers
+
+// `__del__` of the device views (DeviceSession / DeviceDeltaEngine / DeviceSaga /
+// DeviceSagaStep): detach the view (its store becomes CLOSED) and queue its row(s)
+// for reclaim — a view the hypervisor's close already detached does nothing.
+// Finalisers never raise (the Python versions swallow every error).
+PyObject* ctl_view_del(PyObject*, PyObject* self) {
+  PyObject* type = reinterpret_cast<PyObject*>(Py_TYPE(self));
+  uint64_t kind;
+  const bool engine = type == C.DeviceDeltaEngine;
+  if (type == C.DeviceSession) kind = store::RK_S;
+  else if (type == C.DeviceSaga) kind = store::RK_G;
+  else if (type == C.DeviceSagaStep) kind = store::RK_T;
+  else if (engine) kind = store::RK_D;
+  else Py_RETURN_NONE;
+  Own d(idict(self));
+  if (!d) {
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+  PyObject* st = dget(d.p, N._store);
+  if (st == nullptr || st == C.CLOSED) {
+    PyErr_Clear();
+    if (st == nullptr) Py_RETURN_NONE;
+    if (!engine) Py_RETURN_NONE;
+  }
+  Py_INCREF(st);
+  Own st_ref(st);
+  if (PyDict_SetItem(d.p, N._store, C.CLOSED) < 0) {
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+  Store* s = store_of(st);
+  if (engine) {
+    PyObject* rows = dget(d.p, N._rows);
+    if (rows == nullptr) {
+      PyErr_Clear();
+      Py_RETURN_NONE;
+    }
+    Py_INCREF(rows);
+    Own rows_ref(rows);
+    Own empty(PyList_New(0));
+    if (!empty || PyDict_SetItem(d.p, N._rows, empty.p) < 0) {
+      PyErr_Clear();
+      Py_RETURN_NONE;
+    }
+    if (st == C.CLOSED || !PyList_CheckExact(rows) || PyList_GET_SIZE(rows) == 0) Py_RETURN_NONE;
+    if (s != nullptr) {
+      bool ok = true;
+      for (Py_ssize_t i = 0; i < PyList_GET_SIZE(rows); ++i) {
+        const int64_t r = as_i64(PyList_GET_ITEM(rows, i), &ok);
+        if (ok) s->release_row(kind, r);
+        ok = true;
+      }
+    } else {  // some other store object: its own release_many
+      Own r(PyObject_CallMethod(st, "release_many", "sO", "D", rows));
+      PyErr_Clear();
+    }
+    Py_RETURN_NONE;
+  }
+  PyObject* so = dget(d.p, N.slot);
+  bool ok = so != nullptr;
+  const int64_t slot = ok ? as_i64(so, &ok) : 0;
+  if (s != nullptr && ok) {
+    try {
+      s->release_row(kind, slot);
+    } catch (...) {
+    }
+  } else if (so != nullptr) {
+    static const char* kinds = "SGTEDV";
+    const char k[2] = {kinds[kind], 0};
+    Own r(PyObject_CallMethod(st, "release", "sO", k, so));
+    PyErr_Clear();
+  }
+  PyErr_Clear();
+  Py_RETURN_NONE;
+}
+
+// Hypervisor.__del__: close a device-backed hypervisor (native close when it can).
+PyObject* ctl_hv_del(PyObject*, PyObject* hv) {
+  Own d(idict(hv));
+  if (!d) {
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+  PyObject* st = dget(d.p, N._store);
+  if (st == nullptr || st == Py_None || st == C.CLOSED) {
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+  PyObject* args[1] = {hv};
+  Own n(C.ready ? PyObject_Vectorcall(C.close_hv_fast, args, 1, nullptr) : nullptr);
+  bool done = false;
+  if (n) {
+    const long v = PyLong_AsLong(n.p);
+    done = v >= 0;
+  }
+  PyErr_Clear();
+  if (!done) {
+    Own r(PyObject_CallMethod(hv, "close", nullptr));
+    PyErr_Clear();
+  }
+  Py_RETURN_NONE;
+}
+
 // ------------------------------------------------------------------ setup
 
 PyObject* ctl_init(PyObject*, PyObject* const* args, Py_ssize_t nargsf) {
@@ -1259,6 +1447,7 @@ PyObject* ctl_init(PyObject*, PyObject* const* args, Py_ssize_t nargsf) {
     return nullptr;
   }
   if (C.empty_tuple == nullptr) C.empty_tuple = PyTuple_New(0);
+  if (!get("close_hv_fast", &C.close_hv_fast)) return nullptr;
   C.ready = true;
   Py_RETURN_NONE;
 }
@@ -1290,8 +1479,12 @@ PyMethodDef kMethods[] = {
      "verify EXECUTING later, post COMMITTED speculated"},
     {"ctl_close", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(ctl_close)), METH_FASTCALL,
      "awaited terminate up to its post: (seq, root, expired, n) or None"},
+    {"ctl_close_finish", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(ctl_close_finish)),
+     METH_FASTCALL, "the device's root of an awaited terminate that agrees with the prediction"},
     {"ctl_close_hypervisor", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(ctl_close_hypervisor)),
      METH_FASTCALL, "close_hypervisor (native); -1: the Python path"},
+    {"ctl_view_del", ctl_view_del, METH_O, "__del__ of the device views (native)"},
+    {"ctl_hv_del", ctl_hv_del, METH_O, "Hypervisor.__del__ (native close)"},
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace

@@ -1795,7 +1795,17 @@ def _install_native() -> None:
         "s_handshaking": _S_HANDSHAKING, "s_active": _S_ACTIVE, "step_executing_idx": _STEP_IDX[StepState.EXECUTING],
         "step_committed_idx": _COMMITTED_IDX, "spec_lifecycle": _SPEC_LIFECYCLE, "step_speculate": _SPECULATE,
         "spec_terminate": _SPEC_TERMINATE, "check_terminate": _CHECK_TERMINATE,
+        "close_hv_fast": _C.ctl_close_hypervisor,
     })
+    # finalisers: a view the hypervisor's close detached costs one native call
+    vdel = _C.ctl_method(_C.ctl_view_del)
+    for cls in (DeviceSession, DeviceDeltaEngine, DeviceSaga, DeviceSagaStep):
+        cls._py_del = cls.__dict__["__del__"]
+        cls.__del__ = vdel
+    from hypervisor.core import Hypervisor
+
+    Hypervisor._py_del = Hypervisor.__dict__["__del__"]
+    Hypervisor.__del__ = _C.ctl_method(_C.ctl_hv_del)
     DeviceDeltaEngine.capture = _C.ctl_method(_C.ctl_capture)
     DeviceSagaOrchestrator.create_saga = _C.ctl_method(_C.ctl_create_saga)
     DeviceSagaOrchestrator.add_step = _C.ctl_method(_C.ctl_add_step)

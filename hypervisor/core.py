@@ -358,7 +358,7 @@ class Hypervisor:
             seq, root_pred, expired_pred, n = pre
             self._terminate_gc(session_id, sso, de, expired_pred, n)
             r = await st.result_async(seq, 13, 0)
-            return self._terminate_checked(session_id, sso, r, (root_pred, expired_pred))
+            return _d._C.ctl_close_finish(self, session_id, sso, r, (root_pred, expired_pred))
         guard = getattr(sso, "_guard", None)
         if guard is not None:  # a speculation of this session the device refused raises here
             guard()
