@@ -44,6 +44,9 @@ _SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "5"))
 # render | kernel | sorted (its own kernel, lanes grouped by SHA work) | chain (no split: the chain lane hashes all)
 _SP_PREFIX = _os.environ.get("AHV_SP_PREFIX", "sorted")
 _SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX in ("kernel", "sorted") else 1
+# record heads rendered once per distinct (agent, changes) of a batch and copied by
+# the render kernel (C.frag_pack); AHV_SP_FRAGS=0: every record emits its own head
+_SP_FRAGS = _os.environ.get("AHV_SP_FRAGS", "1") != "0"
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
            5: "terminate_refused", 6: "record_overflow"}
@@ -492,6 +495,12 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         arr = np.array(a if dtype is None else np.asarray(a, dtype=dtype), copy=True, order="C")
         return torch.from_numpy(arr).to(dev)
 
+    frag = None
+    if nd and _SP_FRAGS and hasattr(C, "frag_pack"):
+        frag = C.frag_pack(pool._pool, np.ascontiguousarray(d_pool, dtype=np.int32).tobytes(),
+                           np.ascontiguousarray(ch_off_all, dtype=np.int32).tobytes(),
+                           np.ascontiguousarray(ch_rows if len(ch_rows) else np.zeros((0, 4)),
+                                                dtype=np.int32).tobytes())
     pb, po, pl = pool.device_view(dev)
     tens = {
         "slot": T(slots), "uuid": T(np.frombuffer(words, dtype=np.int32).reshape(n, 4)),
@@ -525,6 +534,11 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         # prefix SHA lanes grouped by work: turn-1 records (hashed whole) first, then by
         # reserved size (∝ the blocks before the parent hole), so a wave's lanes finish together
         tens["prefix_order"] = T(np.argsort(t1_last | cap_desc, kind="stable").astype(np.int32))
+    if frag is not None:
+        tens["dfrag"] = T(np.frombuffer(frag["dfrag"], dtype=np.int32))
+        tens["frag_bytes"] = T(np.frombuffer(frag["fbytes"], dtype=np.uint8))
+        tens["frag_off"] = T(np.frombuffer(frag["foff"], dtype=np.int64))
+        tens["frag_len"] = T(np.frombuffer(frag["flen"], dtype=np.int32))
     if _SP_PREFIX != "chain":
         tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
         tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)

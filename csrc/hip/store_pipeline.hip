@@ -91,6 +91,12 @@ struct StorePipeArgs {
   const int32_t* prefix_order;  // [Dn] deltas grouped by prefix SHA work (prefix kernel lane order), or null
   int32_t max_nch;              // most changes of any record
   int32_t wide_only;            // lane renderer: only records with more than coop::kCoopChanges changes
+  // record heads (`{"agent_did": …, "changes": […], "delta_id": "delta:`) rendered once
+  // per distinct (agent, changes) of the batch (frag_pack), or null: emitted per record
+  const int32_t* dfrag;         // [Dn] head of each delta
+  const uint8_t* frag_bytes;    // heads, each 16-byte aligned and zero-padded
+  const int64_t* frag_off;      // [F]
+  const int32_t* frag_len;      // [F]
 };
 
 enum StorePipeStatus : int32_t {
@@ -418,23 +424,49 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   const ChangeIds* ch = a.changes + a.dch_off[g];
   const uint32_t nch = static_cast<uint32_t>(a.dch_off[g + 1] - a.dch_off[g]);
   const uint32_t turn = static_cast<uint32_t>(k + 1);
-  emit_lit(snk, canon::K_OPEN_AGENT);
-  emit_str_ref(snk, pool_ref(a.pool, a.dagent_pool[g]));
-  emit_lit(snk, canon::K_CHANGES);
-  for (uint32_t c = 0; c < nch; ++c) {
-    if (c) emit_lit(snk, canon::K_CH_SEP);
-    emit_lit(snk, canon::K_CH_OPEN);
-    emit_pool_str(snk, a.pool, ch[c].content_hash);
-    emit_lit(snk, canon::K_CH_OP);
-    emit_pool_str(snk, a.pool, ch[c].op);
-    emit_lit(snk, canon::K_CH_PATH);
-    emit_pool_str(snk, a.pool, ch[c].path);
-    emit_lit(snk, canon::K_CH_PREV);
-    emit_pool_str(snk, a.pool, ch[c].previous_hash);
-    emit_lit(snk, canon::K_CH_CLOSE);
+  if (a.dfrag != nullptr) {
+    // the head, pre-rendered: whole 16-byte chunks straight into the record (both
+    // 16-aligned), its last partial chunk into the sink, which continues after it
+    const int32_t f = a.dfrag[g];
+    const uint32_t hl = static_cast<uint32_t>(a.frag_len[f]);
+    const U4* src = reinterpret_cast<const U4*>(a.frag_bytes + a.frag_off[f]);
+    const uint32_t full = hl / 16;
+    for (uint32_t c = 0; c < full; ++c) {
+      const U4 v = src[c];
+      if (4 * c + 4 <= snk.cap_w) store4(snk.dst + 4 * c, v.a, v.b, v.c, v.d);
+    }
+    snk.nw = 4 * full;
+    const uint32_t rem = hl - 16 * full;
+    if (rem) {
+      const U4 v = src[full];  // zero-padded past the head
+      const uint32_t nwd = rem / 4, nb = rem % 4;
+      if (nwd > 0) snk.word(v.a);
+      if (nwd > 1) snk.word(v.b);
+      if (nwd > 2) snk.word(v.c);
+      if (nb) {
+        snk.acc = nwd == 0 ? v.a : nwd == 1 ? v.b : nwd == 2 ? v.c : v.d;
+        snk.nb = nb;
+      }
+    }
+  } else {
+    emit_lit(snk, canon::K_OPEN_AGENT);
+    emit_str_ref(snk, pool_ref(a.pool, a.dagent_pool[g]));
+    emit_lit(snk, canon::K_CHANGES);
+    for (uint32_t c = 0; c < nch; ++c) {
+      if (c) emit_lit(snk, canon::K_CH_SEP);
+      emit_lit(snk, canon::K_CH_OPEN);
+      emit_pool_str(snk, a.pool, ch[c].content_hash);
+      emit_lit(snk, canon::K_CH_OP);
+      emit_pool_str(snk, a.pool, ch[c].op);
+      emit_lit(snk, canon::K_CH_PATH);
+      emit_pool_str(snk, a.pool, ch[c].path);
+      emit_lit(snk, canon::K_CH_PREV);
+      emit_pool_str(snk, a.pool, ch[c].previous_hash);
+      emit_lit(snk, canon::K_CH_CLOSE);
+    }
+    emit_lit(snk, canon::K_DELTA_ID);
+    emit_lit(snk, canon::K_DELTA_PFX);
   }
-  emit_lit(snk, canon::K_DELTA_ID);
-  emit_lit(snk, canon::K_DELTA_PFX);
   emit_uint(snk, turn);
   emit_char(snk, 0x22u);
   emit_lit(snk, canon::K_PARENT);
@@ -933,6 +965,12 @@ StorePipeArgs to_args(const Tables& t, const py::dict& d) {
   a.prefix_order = d.contains("prefix_order") ? P<const int32_t>(d, "prefix_order") : nullptr;
   a.max_nch = d.contains("max_nch") ? d["max_nch"].cast<int32_t>() : 1 << 30;
   a.wide_only = 0;
+  if (d.contains("dfrag")) {
+    a.dfrag = P<const int32_t>(d, "dfrag");
+    a.frag_bytes = P<const uint8_t>(d, "frag_bytes");
+    a.frag_off = P<const int64_t>(d, "frag_off");
+    a.frag_len = P<const int32_t>(d, "frag_len");
+  }
   return a;
 }
 

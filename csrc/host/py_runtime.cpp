@@ -960,6 +960,94 @@ static py::bytes render_fragment(const StringPool& pool, const std::vector<std::
   return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
 }
 
+// ------------------------------------------------------------------ record head fragments
+// The batched store pipeline's records all begin `{"agent_did": <did>, "changes":
+// [...], "delta_id": "delta:` — bytes fixed by the delta's agent and change list
+// (canonical JSON, sorted keys).  A batch's deltas draw those from far fewer
+// distinct (agent, changes) pairs than it has deltas, so each distinct head is
+// rendered once here with the device's own emitters (ahv/delta_emit.h), and the
+// render kernel copies it into each record with 16-byte stores before emitting the
+// per-record rest (turn, parent hole, session id, timestamp).  Every record is
+// still written and hashed in full.
+//
+// frag_pack(pool, d_pool, ch_off, ch_rows) -> {"dfrag": int32[nd] bytes, "fbytes":
+// bytes (entries 16-aligned, zero-padded), "foff": int64[F], "flen": int32[F]}
+static py::dict frag_pack(const StringPool& pool, const py::bytes& d_pool_b, const py::bytes& ch_off_b,
+                          const py::bytes& ch_rows_b) {
+  std::string_view dpv = d_pool_b, cov = ch_off_b, crv = ch_rows_b;
+  const size_t nd = dpv.size() / 4;
+  if (cov.size() / 4 != nd + 1) throw py::value_error("frag_pack: ch_off must have nd + 1 entries");
+  const int32_t* dp = reinterpret_cast<const int32_t*>(dpv.data());
+  const int32_t* co = reinterpret_cast<const int32_t*>(cov.data());
+  const int32_t* cr = reinterpret_cast<const int32_t*>(crv.data());
+  const size_t nrows = crv.size() / 16;
+  const int32_t np = static_cast<int32_t>(pool.size());
+  std::string dfrag(4 * nd, '\0');
+  int32_t* df = reinterpret_cast<int32_t*>(dfrag.data());
+  std::vector<uint8_t> bytes;
+  std::vector<int64_t> foff;
+  std::vector<int32_t> flen;
+  std::unordered_map<std::string, int32_t> seen;
+  seen.reserve(1024);
+  std::string key;
+  const StrPool sp = pool.str_pool();
+  std::vector<ChangeIds> ch;
+  {
+    py::gil_scoped_release nogil;
+    for (size_t g = 0; g < nd; ++g) {
+      const int32_t lo = co[g], hi = co[g + 1];
+      if (lo < 0 || hi < lo || static_cast<size_t>(hi) > nrows) throw std::out_of_range("frag_pack: change range");
+      key.assign(reinterpret_cast<const char*>(dp + g), 4);
+      key.append(reinterpret_cast<const char*>(cr + 4 * lo), 16 * static_cast<size_t>(hi - lo));
+      auto it = seen.find(key);
+      if (it != seen.end()) {
+        df[g] = it->second;
+        continue;
+      }
+      const int32_t f = static_cast<int32_t>(foff.size());
+      seen.emplace(key, f);
+      df[g] = f;
+      if (dp[g] >= np) throw std::out_of_range("frag_pack: agent string id");
+      ch.clear();
+      for (int32_t c = lo; c < hi; ++c) {
+        const int32_t* r = cr + 4 * c;
+        for (int k = 0; k < 4; ++k)
+          if (r[k] >= np) throw std::out_of_range("frag_pack: change string id");
+        ch.push_back(ChangeIds{r[0], r[1], r[2], r[3]});
+      }
+      foff.push_back(static_cast<int64_t>(bytes.size()));
+      const size_t b0 = bytes.size();
+      ByteSink sink{&bytes};
+      emit_lit(sink, canon::K_OPEN_AGENT);
+      emit_pool_str(sink, sp, dp[g]);
+      emit_lit(sink, canon::K_CHANGES);
+      for (size_t c = 0; c < ch.size(); ++c) {
+        if (c) emit_lit(sink, canon::K_CH_SEP);
+        emit_lit(sink, canon::K_CH_OPEN);
+        emit_pool_str(sink, sp, ch[c].content_hash);
+        emit_lit(sink, canon::K_CH_OP);
+        emit_pool_str(sink, sp, ch[c].op);
+        emit_lit(sink, canon::K_CH_PATH);
+        emit_pool_str(sink, sp, ch[c].path);
+        emit_lit(sink, canon::K_CH_PREV);
+        emit_pool_str(sink, sp, ch[c].previous_hash);
+        emit_lit(sink, canon::K_CH_CLOSE);
+      }
+      emit_lit(sink, canon::K_DELTA_ID);
+      emit_lit(sink, canon::K_DELTA_PFX);
+      flen.push_back(static_cast<int32_t>(bytes.size() - b0));
+      bytes.resize((bytes.size() + 15) & ~size_t(15), 0);  // the next entry starts 16-aligned
+    }
+  }
+  bytes.resize(bytes.size() + 16, 0);  // a tail read of the last entry stays in bounds
+  py::dict out;
+  out["dfrag"] = py::bytes(dfrag);
+  out["fbytes"] = py::bytes(reinterpret_cast<const char*>(bytes.data()), bytes.size());
+  out["foff"] = py::bytes(reinterpret_cast<const char*>(foff.data()), 8 * foff.size());
+  out["flen"] = py::bytes(reinterpret_cast<const char*>(flen.data()), 4 * flen.size());
+  return out;
+}
+
 // ------------------------------------------------------------------ attribution packing
 // CausalAttributor.attribute_batch: the K21 columns of many failure cases, read
 // natively from their dicts.  Per case the agents are listed in the iteration
@@ -1088,6 +1176,8 @@ void register_runtime(py::module_& m) {
       py::arg("min_sigma"), py::arg("trustworthy"), "(JoinCode, ring) the device join would produce");
   m.def("render_fragment", &render_fragment, py::arg("pool"), py::arg("changes"), py::arg("turn"),
         py::arg("has_parent"));
+  m.def("frag_pack", &frag_pack, py::arg("pool"), py::arg("d_pool"), py::arg("ch_off"), py::arg("ch_rows"),
+        "Distinct record heads ({\"agent_did\" ... \"delta:) of a batch's deltas, rendered once each");
   m.def("pack_specs", &pack_specs, py::arg("specs"), py::arg("agents"), py::arg("pool"), py::arg("cfg_of"),
         py::arg("fixed"), py::arg("threads") = -1,
         "Flatten PipelineSpecs into the batch kernels' columns (models/store_pipeline.py); threads: < 0 auto "
