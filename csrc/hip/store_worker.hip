@@ -199,7 +199,8 @@ __device__ __forceinline__ void hash_one(const Tables& t, const HashJob& j, uint
 // previous delta's row (earlier in the queue, so already done) or, for the
 // chain's first hole, the session head.
 __device__ __forceinline__ bool spec_link_ok(const Tables& t, const HashJob& j) {
-  if (!j.full || j.hole < 0) return false;
+  if (!j.full) return false;
+  if (j.hole < 0) return true;  // a null-parent record (turn 1): its digest depends on its bytes only
   const uint32_t* head = j.prev >= 0 ? t.d_hash + 8 * j.prev : t.s_head + 8 * j.s;
   uint32_t hd[8];
   load8(head, hd);
@@ -242,6 +243,192 @@ __device__ void hash_batch(const Tables& t, const HashJob* jobs, uint32_t done, 
             tj0, __builtin_amdgcn_s_memrealtime());
 }
 
+// ------------------------------------------------------- ring lookahead
+//
+// Feature 256: the helper waves read the command ring past the command wave
+// (`cw_next`, published after each command) and hash the captures they find there
+// as whole records — a turn-1 record (its digest depends on its bytes only) or a
+// link whose predicted parent the host already wrote into the hole — into a small
+// LDS table.  The command wave, queuing the capture's job later, takes a ready
+// digest with it (the job starts `full`, and the engine only has to check the
+// parent, spec_link_ok); a digest that finishes after its job was queued is handed
+// to the job if no wave has taken it yet.  Per-call pipelines post their captures
+// faster than the command wave works through create / join / activate, so the
+// records hash while those commands run instead of after.  Entry states: 0 free,
+// 1 hashing, 2 ready, 3 not hashable here, 4 being handed over, 5 hashing for a job
+// the command wave queued meanwhile (the job waits, claimed, until the helper completes it).
+constexpr int kPre = 8;
+constexpr int kAheadSlots = 4;  // slots a scan looks at (16 lanes each: a capture uses ≤ 16 words)
+
+struct PreTab {
+  uint32_t st[kPre];
+  uint64_t seq[kPre];
+  uint32_t dig[kPre][8];
+  uint32_t par[kPre][8];
+  uint32_t lock;     // one helper scans at a time
+  uint64_t cw_next;  // the command wave's next sequence number
+};
+
+__device__ __forceinline__ uint64_t lds_acquire64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Leader: give entry e's digest (state 4, held by the caller) to its queued job,
+// if the job is still untaken (pstate 0 → 1 → 2); the job is re-identified by its
+// sequence number after the claim (its ring slot may have been reused).
+__device__ void pre_deliver(PreTab& P, int e, HashJob* jobs, uint32_t* pstate, const uint32_t* q_head,
+                            const uint32_t* q_done) {
+  const uint64_t seq = P.seq[e];
+  const uint32_t d0 = lds_acquire(q_done), h = lds_acquire(q_head);
+  for (uint32_t p = d0; p != h; ++p) {
+    HashJob* jp = &jobs[p % kJobs];
+    if (jp->seq != seq) continue;
+    if (lds_cas(&pstate[p % kJobs], 0u, 1u) != 0u) return;  // taken (engine / helper) or done
+    if (jp->seq != seq) {  // the slot was reused before the claim: give it back
+      lds_release(&pstate[p % kJobs], 0u);
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      jp->sdig[k] = P.dig[e][k];
+      jp->ppar[k] = P.par[e][k];
+    }
+    jp->full = 1;
+    lds_release(&pstate[p % kJobs], 2u);
+    return;
+  }
+}
+
+// Leader: entries the command wave has passed — a ready digest goes to its job
+// (if still useful), then the entry is freed.
+__device__ void pre_sweep(PreTab& P, uint64_t cw, HashJob* jobs, uint32_t* pstate, const uint32_t* q_head,
+                          const uint32_t* q_done) {
+  for (int e = 0; e < kPre; ++e) {
+    const uint32_t sv = lds_acquire(&P.st[e]);
+    if ((sv != 2u && sv != 3u) || P.seq[e] >= cw) continue;
+    if (lds_cas(&P.st[e], sv, 4u) != sv) continue;
+    if (sv == 2u) pre_deliver(P, e, jobs, pstate, q_head, q_done);
+    lds_release(&P.st[e], 0u);
+  }
+}
+
+// One lookahead pass of a helper wave; true when it hashed a record.
+__device__ bool lookahead(const Lanes& L, const Tables& t, const uint64_t* ring, int64_t nslots, uint32_t* w,
+                          int32_t max_blocks, PreTab& P, HashJob* jobs, uint32_t* pstate, const uint32_t* q_head,
+                          const uint32_t* q_done, uint64_t* tr, int64_t tcap, int hw) {
+  const int lane = L.lane;
+  int locked = 0;
+  if (lane == 0) locked = lds_cas(&P.lock, 0u, 1u) == 0u ? 1 : 0;
+  locked = __shfl(locked, 0);
+  if (!locked) return false;
+  const uint64_t cw = lds_acquire64(&P.cw_next);
+  if (lane == 0) pre_sweep(P, cw, jobs, pstate, q_head, q_done);
+  // lane → word (lane & 15) of slot cw + (lane >> 4); a capture uses ≤ 16 slot words
+  const int base = lane & ~15, wi = lane & 15;
+  const uint64_t sq = cw + static_cast<uint64_t>(lane >> 4);
+  const uint64_t v0 = ld_sys(ring + (sq % static_cast<uint64_t>(nslots)) * kSlotWords + wi);
+  const uint64_t w0 = __shfl(v0, base), w1 = __shfl(v0, base + 1), w2 = __shfl(v0, base + 2);
+  const uint32_t nwr = static_cast<uint32_t>(w1 >> 32) & 0x7fu;
+  const uint64_t v = static_cast<uint32_t>(wi) < nwr ? v0 : 0ull;
+  uint64_t x = (wi == 0 || wi == 2) ? 0ull : slot_mix(v, static_cast<uint64_t>(wi));
+  for (int o = 8; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
+  const uint64_t off = __shfl(v0, base + 7), len = __shfl(v0, base + 8);
+  const int64_t hole = static_cast<int64_t>(__shfl(v0, base + 9));
+  const uint64_t flags = __shfl(v0, base + 10);
+  const uint64_t nblk = (len + 9 + 63) / 64;
+  const bool cand = w0 == sq + 1 && static_cast<uint32_t>(w1) == OP_DELTA_CAPTURE && nwr >= 10 && nwr <= 16 &&
+                    x == w2 && (hole < 0 || (flags & 1u)) && nblk <= static_cast<uint64_t>(max_blocks) &&
+                    off + len <= static_cast<uint64_t>(t.cap.B) && len > 0;
+  const uint64_t cb = __ballot(cand && wi == 0);
+  int pick_g = -1, pick_e = -1;
+  if (lane == 0) {
+    for (int g = 0; g < kAheadSlots && pick_g < 0; ++g) {
+      if (!((cb >> (16 * g)) & 1ull)) continue;
+      const uint64_t sg = cw + static_cast<uint64_t>(g);
+      bool have = false;
+      for (int e = 0; e < kPre; ++e) have = have || (lds_acquire(&P.st[e]) != 0u && P.seq[e] == sg);
+      if (have) continue;
+      for (int e = 0; e < kPre; ++e) {
+        if (lds_cas(&P.st[e], 0u, 1u) == 0u) {
+          P.seq[e] = sg;
+          pick_g = g;
+          pick_e = e;
+          break;
+        }
+      }
+      break;  // no free entry: nothing more this pass
+    }
+    lds_release(&P.lock, 0u);
+  }
+  pick_g = __shfl(pick_g, 0);
+  pick_e = __shfl(pick_e, 0);
+  if (pick_g < 0) return false;
+  const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
+  HashJob jb;
+  jb.off = static_cast<int64_t>(__shfl(off, 16 * pick_g));
+  jb.len = static_cast<int64_t>(__shfl(len, 16 * pick_g));
+  jb.hole = __shfl(hole, 16 * pick_g);
+  jb.spec = jb.hole >= 0 ? 1 : 0;
+  uint32_t dig[8] = {0, 0, 0, 0, 0, 0, 0, 0}, par[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool whole;
+  if (jb.hole >= 0) {
+    whole = capture_spec_full(L, t, jb, w, max_blocks, dig, par);
+  } else {
+    const int64_t nb = (jb.len + 9 + 63) / 64;
+    whole = stage_words(L, t.payload + jb.off, static_cast<uint64_t>(jb.len), w, 16 * max_blocks) >= 0;
+    if (whole) sha256_lds_blocks_par(L, w, nb, dig);
+    L.sync();
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      P.dig[pick_e][k] = dig[k];
+      P.par[pick_e][k] = par[k];
+    }
+    const uint64_t sg = P.seq[pick_e];
+    const uint32_t fin = whole ? 2u : 3u;
+    if (lds_cas(&P.st[pick_e], 1u, fin) == 5u) {
+      // the command wave queued this capture while we hashed and bound the job to us
+      // (pstate 1): complete it — with the digest, or without (the engine re-hashes)
+      // (the command wave binds before it publishes the job: wait for it to appear;
+      // bounded, so a binding that was undone can never hold this wave)
+      bool found = false;
+      for (int tries = 0; !found && tries < (1 << 16); ++tries) {
+        const uint32_t d0 = lds_acquire(q_done), h = lds_acquire(q_head);
+        for (uint32_t p = d0; p != h; ++p) {
+          HashJob* jp = &jobs[p % kJobs];
+          if (jp->seq != sg || lds_acquire(&pstate[p % kJobs]) != 1u) continue;
+          if (whole) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              jp->sdig[k] = dig[k];
+              jp->ppar[k] = par[k];
+            }
+            jp->full = 1;
+          }
+          lds_release(&pstate[p % kJobs], 2u);
+          found = true;
+          break;
+        }
+        if (!found) __builtin_amdgcn_s_sleep(1);
+      }
+      lds_release(&P.st[pick_e], 0u);
+    } else {
+      // the command wave may have queued this capture meanwhile: hand the digest over
+      const uint64_t cw2 = lds_acquire64(&P.cw_next);
+      if (sg < cw2 && lds_cas(&P.st[pick_e], fin, 4u) == fin) {
+        if (whole) pre_deliver(P, pick_e, jobs, pstate, q_head, q_done);
+        lds_release(&P.st[pick_e], 0u);
+      }
+    }
+    trace_put(tr, tcap, 3, sg,
+              static_cast<uint64_t>(whole ? 5 : 6) | (static_cast<uint64_t>((jb.len + 9 + 63) / 64 & 0xff) << 8) |
+                  (static_cast<uint64_t>(hw) << 16),
+              th0, __builtin_amdgcn_s_memrealtime());
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint64_t* ring, int64_t nslots,
                                                            uint64_t* res, uint8_t* bulk, uint64_t* alive,
                                                            int64_t* tail, uint64_t idle_ticks, uint64_t max_ticks,
@@ -267,9 +454,16 @@ __global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint6
   __shared__ uint32_t lds2[2 * 16 * kPrefixBlocks];
   __shared__ uint32_t kw2[2 * kPrefixBlocks * kKwStride];
   __shared__ uint32_t q_head, q_done, stop, bye, bye2, bye3, spec_s;
+  __shared__ PreTab ptab;  // ring lookahead (feature 256)
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   if (threadIdx.x == 0) {
+    for (int e = 0; e < kPre; ++e) {
+      ptab.st[e] = 0;
+      ptab.seq[e] = 0;
+    }
+    ptab.lock = 0;
+    ptab.cw_next = static_cast<uint64_t>(__hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     q_head = 0;
     q_done = 0;
     stop = 0;
@@ -322,6 +516,9 @@ __global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint6
       mode = __shfl(mode, 0);
       if (pick < 0) {
         if (lds_acquire(&stop)) break;
+        if ((speculate & 256) &&
+            lookahead(L, t, ring, nslots, hl, kPrefixBlocks, ptab, jobs, pstate, &q_head, &q_done, tr, tcap, hw))
+          continue;
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
@@ -598,9 +795,39 @@ __global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint6
     L.sync();
     if (rc == EXEC_DEFERRED) {
       if (lane == 0) {
+        uint32_t ps0 = 0u;
+        if (speculate & 256) {  // a helper hashed (or is hashing) this record from the ring
+          for (int e = 0; e < kPre; ++e) {
+            if (ptab.seq[e] != next) continue;
+            if (lds_cas(&ptab.st[e], 2u, 4u) == 2u) {
+              if (ptab.seq[e] == next) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                  job.sdig[k] = ptab.dig[e][k];
+                  job.ppar[k] = ptab.par[e][k];
+                }
+                job.full = 1;
+                ps0 = 2u;  // done: no helper claims it, the engine takes it at once
+              }
+              lds_release(&ptab.st[e], 0u);
+              break;
+            }
+            if (lds_cas(&ptab.st[e], 1u, 5u) == 1u) {
+              // still hashing: the job is queued as claimed (pstate 1), so neither the
+              // engine nor the other helper hashes it again — the engine waits for the
+              // helper, which completes the job (pstate 2) when its digest is ready
+              if (ptab.seq[e] == next) {
+                ps0 = 1u;
+              } else {  // (the entry moved on meanwhile: undo)
+                lds_release(&ptab.st[e], 1u);
+              }
+              break;
+            }
+          }
+        }
         jobs[queued % kJobs] = job;  // (mid_blocks 0: wave 2 may add a midstate)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        pstate[queued % kJobs] = 0u;
+        pstate[queued % kJobs] = ps0;
         lds_release(&q_head, queued + 1);  // the capture's global row writes precede this release
       }
       ++queued;
@@ -610,6 +837,7 @@ __global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint6
       out64(r, next + 1);
     }
     if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) __hip_atomic_store(&ptab.cw_next, next + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     last = __builtin_amdgcn_s_memrealtime();
     if (lane == 0)
       trace_put(tr, tcap, 0, next,

@@ -71,7 +71,7 @@ struct Names {
   X(compensation_result) X(step_id) X(action_id) X(execute_api) X(undo_api) X(timeout_seconds) X(max_retries)        \
   X(_hint) X(append) X(capture) X(alloc) X(_tenant_v) X(_tenant) X(gc) X(policy) X(delta_retention_days) X(sso)      \
   X(delta_engine) X(saga) X(_sessions) X(_segs) X(_own) X(vouching) X(commitment) X(_closed) X(event_bus)   \
-  X(_device)
+  X(_device) X(_commits)
 #define AHV_DECL(n) PyObject* n = nullptr;
   AHV_NAMES(AHV_DECL)
 #undef AHV_DECL
@@ -1103,8 +1103,19 @@ PyObject* ctl_close_finish(PyObject*, PyObject* const* args, Py_ssize_t nargsf) 
       if (same < 0) return nullptr;
       if (!same) return slow();  // divergence: the Python path poisons the session and raises
     }
-    if (root.p != Py_None) {
-      Own cm(PyObject_GetAttr(hv, N.commitment));  // built on first use (Hypervisor.__getattr__)
+    if (root.p != Py_None && dget(hd.p, N.commitment) == nullptr) {
+      // no commitment engine yet (most hypervisors never read one): the committed
+      // session waits in `_commits`, which the engine absorbs when it is built
+      if (PyErr_Occurred()) return nullptr;
+      PyObject* pend = dget(hd.p, N._commits);
+      if (pend == nullptr) {
+        if (PyErr_Occurred()) return nullptr;
+        if (!dset_steal(hd.p, N._commits, PyDict_New())) return nullptr;
+        pend = dget(hd.p, N._commits);
+      }
+      if (pend == nullptr || PyDict_SetItem(pend, sid, sso) < 0) return nullptr;
+    } else if (root.p != Py_None) {
+      Own cm(PyObject_GetAttr(hv, N.commitment));
       if (!cm) return nullptr;
       if (Py_TYPE(cm.p) == reinterpret_cast<PyTypeObject*>(C.DeviceCommitmentEngine)) {
         Own cd(idict(cm.p));

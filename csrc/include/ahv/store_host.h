@@ -190,7 +190,14 @@ class StoreCore {
       // 128 = helper waves hash a capture whose parent the host predicted (hole prefilled)
       //       as a whole record, off the chain; the engine checks the parent and takes it
       const char* sc = std::getenv("AHV_STORE_SPEC_CHAIN");
-      speculate_ = ((sc == nullptr || std::atoi(sc) != 0) ? 128 : 0) | ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
+      // 256 = helper waves hash captures straight from the command ring, ahead of the
+      //       command wave (turn-1 records and predicted-parent links).  Off by default
+      //       (AHV_STORE_LOOKAHEAD=1 on): measured slower — the waves of the one worker CU
+      //       hash at 3.2-3.4 µs per block side by side against 2.4 µs for the engine alone
+      //       (per-call p50 76.4 vs 69.4 µs, profiles/r6/lookahead_ab_r6v.txt)
+      const char* la = std::getenv("AHV_STORE_LOOKAHEAD");
+      speculate_ = ((la != nullptr && std::atoi(la) != 0) ? 256 : 0) |
+                   ((sc == nullptr || std::atoi(sc) != 0) ? 128 : 0) | ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
                    ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) |
                    ((nf == nullptr || std::atoi(nf) != 0) ? 16 : 0) |
                    ((lp == nullptr || std::atoi(lp) != 0) ? 32 : 0) |

@@ -146,8 +146,11 @@ class Hypervisor:
             # never pays for the ones it does not touch
             self._max_exposure = max_exposure
         self.device = mode
-        self.ring_enforcer = RingEnforcer()
-        self.classifier = ActionClassifier()
+        if mode == "host":
+            self.ring_enforcer = RingEnforcer()
+            self.classifier = ActionClassifier()
+        # (device-backed: the ring gate runs on the device; ring_enforcer / classifier
+        # are built on first use, see __getattr__)
         self.verifier = TransactionHistoryVerifier()
         self.gc = EphemeralGC(retention_policy)
         self.nexus = nexus
@@ -164,16 +167,23 @@ class Hypervisor:
         # only reached for attributes not set yet: the device engines of a
         # device-backed hypervisor, built together on first use
         d = self.__dict__
+        if name == "ring_enforcer" or name == "classifier":
+            d["ring_enforcer"] = RingEnforcer()
+            d["classifier"] = ActionClassifier()
+            return d[name]
         if name in Hypervisor._LAZY_ENGINES and d.get("_store") is not None:
             _device = _device_mod()
             st = d["_store"]
             if name == "commitment":  # every terminate registers here; no vouching engine needed
-                d["commitment"] = _device.DeviceCommitmentEngine(st)
+                cm = d["commitment"] = _device.DeviceCommitmentEngine(st)
+                pend = d.pop("_commits", None)  # sessions terminates committed before it existed
+                if pend:
+                    cm._device.update(pend)
                 return d[name]
             ve = d["vouching"] = _device.DeviceVouchingEngine(st, d["_tenant"], d.get("_max_exposure"))
             d["slashing"] = _device.DeviceSlashingEngine(ve)
             if "commitment" not in d:
-                d["commitment"] = _device.DeviceCommitmentEngine(st)
+                self.__getattr__("commitment")
             return d[name]
         raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
 
