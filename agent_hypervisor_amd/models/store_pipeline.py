@@ -45,8 +45,10 @@ _SP_ORDER = int(_os.environ.get("AHV_SP_ORDER", "5"))
 _SP_PREFIX = _os.environ.get("AHV_SP_PREFIX", "sorted")
 _SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX in ("kernel", "sorted") else 1
 # record heads rendered once per distinct (agent, changes) of a batch and copied by
-# the render kernel (C.frag_pack); AHV_SP_FRAGS=0: every record emits its own head
-_SP_FRAGS = _os.environ.get("AHV_SP_FRAGS", "1") != "0"
+# the render kernel (C.frag_pack), AHV_SP_FRAGS=1.  Off by default: the kernel gains
+# 18 µs per 10^6 sessions (render 707 -> 689 µs, profiles/r6/hetero_frags_r6s.jsonl)
+# but the host pass costs ≈ 0.4 µs per delta in prepare, which the public API times
+_SP_FRAGS = _os.environ.get("AHV_SP_FRAGS", "0") != "0"
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
            5: "terminate_refused", 6: "record_overflow"}
