@@ -349,7 +349,8 @@ class GovernanceEngine:
                 words.append(np.frombuffer(b + b"\0" * (-len(b) % 4), dtype=">u4").astype(np.uint32))
             dev = self.device
             frag = (torch.from_numpy(np.concatenate(words).view(np.int32).copy()).to(dev),
-                    torch.tensor(offs, dtype=torch.int32, device=dev), torch.tensor(lens, dtype=torch.int32, device=dev))
+                    torch.tensor(offs, dtype=torch.int32, device=dev), torch.tensor(lens, dtype=torch.int32,
+                                                                                    device=dev))
         self._change_cache[key] = (t, rows, frag)
         return t, rows, frag
 

@@ -34,8 +34,6 @@ from typing import Any, Callable, Optional, Sequence
 import torch
 
 from agent_hypervisor_amd.models.saga_engine import (
-    ERR_COMP,
-    ERR_COMP_TIMEOUT,
     ERR_EXEC,
     ERR_NO_UNDO,
     ERR_NONE,

@@ -253,7 +253,8 @@ class GovernanceStore:
         cur, mx = self.caps[kind], self.max_caps[kind]
         if cur >= mx:
             raise StoreError(
-                f"store table {kind} full ({cur} live rows; ceiling AHV_STORE_MAX_* = {mx}): refusing to reuse live rows")
+                f"store table {kind} full ({cur} live rows; ceiling AHV_STORE_MAX_* = {mx}): "
+                "refusing to reuse live rows")
         new = min(mx, 2 * cur)
         with self._lock:
             self.drain()

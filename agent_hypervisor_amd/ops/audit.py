@@ -76,7 +76,8 @@ def render_rows(out: torch.Tensor, template: torch.Tensor, ids: torch.Tensor, st
         if nb > stride:
             raise ValueError("hex field longer than its source rows")
     launch("render_rows",
-           {"rows": rows, "len": L, "pitch": P, "stamps": [tuple(int(x) for x in st) for st in stamps], "hex_pos": int(hp),
+           {"rows": rows, "len": L, "pitch": P, "stamps": [tuple(int(x) for x in st) for st in stamps],
+            "hex_pos": int(hp),
             "hex_bytes": int(nb), "hex_stride": int(stride)},
            dict(tmpl=template, out=out, ids=ids, hex_src=src), dict(tmpl=u8, out=u8, ids=i64, hex_src=u8))
 

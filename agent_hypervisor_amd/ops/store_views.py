@@ -101,7 +101,6 @@ def verify_store_chains(store, chains: list[list[int]]) -> tuple[torch.Tensor, t
     (each a session's chain in turn order).  Returns ``(row_ok u8 [Σ], chain_ok u8
     [len(chains)])`` on the store device.  Only the int32 row lists travel to the
     device; the records are re-hashed from the payload arena where they live."""
-    from agent_hypervisor_amd._native import C
     from agent_hypervisor_amd.ops._launch import launch
 
     dev = store.device
@@ -169,7 +168,8 @@ def sigma_batch(store, vsess: list[int], agents: list[int], sigma=None, omega=No
     launch("store_sigma",
            {"n": n, "mode": int(mode), "now_us": int(now if now is not None else now_us()),
             "cap_v": int(store.caps["V"])},
-           {"vsess": torch.tensor(vsess, dtype=torch.int32).to(dev), "agent": torch.tensor(agents, dtype=torch.int32).to(dev),
+           {"vsess": torch.tensor(vsess, dtype=torch.int32).to(dev), "agent": torch.tensor(agents,
+                                                                                           dtype=torch.int32).to(dev),
             "sigma": sig, "omega": om, "v_head": t["v_head"], "e_next": t["e_next"], "e_voucher": t["e_voucher"],
             "e_vouchee": t["e_vouchee"], "e_active": t["e_active"], "e_expiry": t["e_expiry"],
             "e_bonded": t["e_bonded"], "out": out},

@@ -1129,7 +1129,8 @@ class RestoredBatch(_restored_batch_base()):
                     steps.append({"step_id": tc["step_id"][k], "action_id": tc["action_id"][k],
                                   "agent_did": tc["agent_did"][k], "state": sst[int(rows["t_state"][tk]) & 0xFF].value,
                                   "retry_count": int(rows["t_retry"][tk]), "error": tc["error"][k],
-                                  "started_at": from_us(t0) if t0 else None, "completed_at": from_us(t1) if t1 else None})
+                                  "started_at": from_us(t0) if t0 else None,
+                                      "completed_at": from_us(t1) if t1 else None})
                     tk += 1
                 c1 = int(rows["g_completed"][gk])
                 out.append({"saga_id": self.gid[g], "session_id": self.ids[i],

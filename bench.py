@@ -575,7 +575,8 @@ def main() -> None:
             "api_batch_pipelines_per_s": api["batch_pipelines_per_s"] if api else None,
             "api_gather_pipelines_per_s": api["gather_pipelines_per_s"] if api else None,
             "api": api,
-            "last_step_counters": dict(zip(["sessions", "ok", "participants", "deltas", "commits", "archived"], totals)),
+            "last_step_counters": dict(zip(["sessions", "ok", "participants", "deltas", "commits", "archived"],
+                                           totals)),
             "step_latency_hist_log2_us": {str(1 << b): c for b, c in enumerate(hist) if c},
             "rccl_ranks": rccl_ranks,
             "launcher": "bench.py (self-spawned ranks)" if os.environ.get("AHV_BENCH_SPAWNED") == "1"
@@ -588,7 +589,8 @@ def main() -> None:
             },
             "headline_verified": bool(verified) if tmpl is not None else None,
             "headline_verified_sessions": verified,
-            "headline_kernel": (_headline_kernel(S) if dev.type == "cuda" else "host twin") if tmpl is not None else None,
+            "headline_kernel": ((_headline_kernel(S) if dev.type == "cuda" else "host twin")
+                                if tmpl is not None else None),
             "mix": args.mix,
             "state": "governance_tables (--graph)" if eng is not None else "store rows",
             "hetero": None if hetero is None else {

@@ -30,7 +30,6 @@ fields are read from the device when accessed.
 from __future__ import annotations
 
 import asyncio
-import json
 import os
 import struct
 from datetime import datetime, timedelta
@@ -622,7 +621,8 @@ def _host_digest(d) -> str:
 class DeviceDeltaEngine(DeltaEngine):
     """Audit chain of one device session: the device links, hashes and roots it."""
 
-    def __init__(self, store: GovernanceStore, slot: int, session_id: str, owner: Optional[DeviceSession] = None) -> None:
+    def __init__(self, store: GovernanceStore, slot: int, session_id: str,
+                 owner: Optional[DeviceSession] = None) -> None:
         self._store = store
         self.slot = slot
         self.session_id = session_id

@@ -49,7 +49,7 @@ from agent_hypervisor_amd.ops import session as SN
 from hypervisor import _clock
 from hypervisor._clock import now as _now
 from hypervisor.liability.ledger import AgentRiskProfile, LedgerEntryType, LiabilityLedger
-from hypervisor.liability.quarantine import QuarantineManager, QuarantineReason, QuarantineRecord
+from hypervisor.liability.quarantine import QuarantineManager, QuarantineRecord
 from hypervisor.models import ExecutionRing
 from hypervisor.rings.breach_detector import BreachEvent, BreachSeverity, RingBreachDetector
 from hypervisor.rings.elevation import RingElevation, RingElevationError, RingElevationManager

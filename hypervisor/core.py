@@ -388,7 +388,8 @@ class Hypervisor:
             # close without waiting for the hash engine; the device's answer is
             # checked later and a disagreement goes to this session (post_checked)
             root, expired = spec
-            st.post_expect(_d._st.OP_SESS_CLOSE, args, _d.close_expect(root, expired), (sso, _d._close_diverged, sso.slot),
+            st.post_expect(_d._st.OP_SESS_CLOSE, args, _d.close_expect(root, expired), (sso, _d._close_diverged,
+                                                                                        sso.slot),
                            inl)
             return self._terminated(session_id, sso, de, root, expired, n)
         early = check is not None and not (v >= 0)
@@ -685,7 +686,8 @@ class Hypervisor:
                     steps.append({"step_id": x.step_id, "action_id": x.action_id, "agent_did": x.agent_did,
                                   "state": sst[int(rows["t_state"][k]) & 0xFF].value,
                                   "retry_count": int(rows["t_retry"][k]), "error": x.error,
-                                  "started_at": from_us(t0) if t0 else None, "completed_at": from_us(t1) if t1 else None})
+                                  "started_at": from_us(t0) if t0 else None,
+                                      "completed_at": from_us(t1) if t1 else None})
                     k += 1
                 c1 = int(rows["g_completed"][i])
                 out.append({"saga_id": g.saga_id, "session_id": g.session_id,

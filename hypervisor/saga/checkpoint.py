@@ -114,7 +114,8 @@ class CheckpointManager:
         ]
 
     @classmethod
-    def from_records(cls, records: list[dict], verify: bool = True, device: Optional[str] = None) -> "CheckpointManager":
+    def from_records(cls, records: list[dict], verify: bool = True,
+                     device: Optional[str] = None) -> "CheckpointManager":
         """Rebuild a manager from :meth:`export_records`; with ``verify`` every goal
         hash is re-derived (K12) and a mismatch raises ``ValueError``."""
         mgr = cls()

@@ -73,7 +73,8 @@ def record(seed: int = SEED) -> dict:
     env = {k: v for k, v in os.environ.items() if k not in ("PYTHONPATH",)}
     env.update(PYTHONPATH=REF_SRC, PYTHONDONTWRITEBYTECODE="1")
     _, sessions, nops = FIXTURES[seed]
-    p = subprocess.run([sys.executable, "-c", "import importlib; " + _CHILD, os.path.join(ROOT, "tests", "golden_trace.py"),
+    p = subprocess.run([sys.executable, "-c", "import importlib; " + _CHILD, os.path.join(ROOT, "tests",
+                                                                                          "golden_trace.py"),
                         REF_SRC, str(seed), str(sessions), str(nops)], capture_output=True, text=True, env=env,
                        cwd="/tmp", timeout=600)
     if p.returncode != 0:
@@ -92,7 +93,8 @@ def main() -> int:
             with open(fixture) as f:
                 old = json.load(f)
             same = old == json.loads(json.dumps(rec))
-            print(f"{os.path.basename(fixture)}: " + ("matches the reference" if same else "DIFFERS from the reference"))
+            verdict = "matches the reference" if same else "DIFFERS from the reference"
+            print(f"{os.path.basename(fixture)}: {verdict}")
             bad += 0 if same else 1
             continue
         os.makedirs(os.path.dirname(fixture), exist_ok=True)

@@ -34,6 +34,7 @@ for k in tam:
     d0 = ds[0]
     raw = canonical_payload(d0)
     print(k, m.sso.session_id in rep.bad_chains, "dirty", [d.__dict__.get("_dirty") for d in ds],
-          "stored", d0.delta_hash[:16], "recomputed", hashlib.sha256(raw.encode() if isinstance(raw, str) else raw).hexdigest()[:16],
+          "stored", d0.delta_hash[:16], "recomputed",
+          hashlib.sha256(raw.encode() if isinstance(raw, str) else raw).hexdigest()[:16],
           "turn", d0.turn_id, "n", len(ds), "seq", d0._seq, "didx", d0._didx,
           "dev_hash", (d0.__dict__.get("_dev_hash") or "")[:16], "res", hv._store.result(d0._seq, 9) is not None)

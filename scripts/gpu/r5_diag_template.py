@@ -5,7 +5,7 @@ with the session each row was given?"""
 import sys
 
 import numpy as np
-import torch
+import torch  # noqa: F401 - loaded before the native extension
 
 sys.path.insert(0, ".")
 from agent_hypervisor_amd.models import store_template as TT  # noqa: E402

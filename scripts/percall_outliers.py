@@ -47,7 +47,6 @@ if os.environ.get("WRAP", "1") == "1":
         _wrap(st, nm, "store." + nm)
     _wrap(_device, "DeviceSession", "DeviceSession()")
     _wrap(_device, "session_views", "session_views")
-    import hypervisor.session.sso as _sso
     _wrap(_device, "SessionVFS", "SessionVFS()") if hasattr(_device, "SessionVFS") else None
     _wrap(_device._C, "uuid4", "_C.uuid4") if hasattr(_device, "_C") else None
 def _launches():
@@ -55,7 +54,8 @@ def _launches():
 async def one():
     p = time.perf_counter_ns; t = {}
     a = p(); hv = Hypervisor(device=dev); t["init"] = p() - a
-    a = p(); s = await hv.create_session(config=SessionConfig(enable_audit=True), creator_did="did:mesh:admin"); t["create"] = p() - a
+    a = p(); s = await hv.create_session(config=SessionConfig(enable_audit=True),
+                                         creator_did="did:mesh:admin"); t["create"] = p() - a
     sid = s.sso.session_id
     a = p(); await hv.join_session(sid, "did:mesh:a", sigma_raw=0.8); t["join"] = p() - a
     a = p(); await hv.activate_session(sid); t["activate"] = p() - a
@@ -63,8 +63,10 @@ async def one():
     for i in range(3):
         s.delta_engine.capture("did:mesh:a", [VFSChange(path=f"/f{i}", operation="add", content_hash=f"h{i}")])
     t["capture"] = p() - a
-    a = p(); saga = s.saga.create_saga(sid); step = s.saga.add_step(saga.saga_id, "action", "did:mesh:a", "/api/action"); t["saga"] = p() - a
-    a = p(); await s.saga.execute_step(saga.saga_id, step.step_id, executor=lambda: asyncio.sleep(0)); t["exec"] = p() - a
+    a = p(); saga = s.saga.create_saga(sid); step = s.saga.add_step(saga.saga_id, "action", "did:mesh:a",
+                                                                    "/api/action"); t["saga"] = p() - a
+    a = p(); await s.saga.execute_step(saga.saga_id, step.step_id,
+                                       executor=lambda: asyncio.sleep(0)); t["exec"] = p() - a
     a = p(); await hv.terminate_session(sid); t["term"] = p() - a
     a = p(); del s, hv, saga, step; t["teardown"] = p() - a
     return t

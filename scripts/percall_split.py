@@ -16,7 +16,8 @@ def rec(k, dt): T.setdefault(k, []).append(dt)
 async def one():
     p = time.perf_counter_ns
     a = p(); hv = Hypervisor(device=dev); rec("hv_init", p() - a)
-    a = p(); s = await hv.create_session(config=SessionConfig(enable_audit=True), creator_did="did:mesh:admin"); rec("create", p() - a)
+    a = p(); s = await hv.create_session(config=SessionConfig(enable_audit=True),
+                                         creator_did="did:mesh:admin"); rec("create", p() - a)
     sid = s.sso.session_id
     a = p(); await hv.join_session(sid, "did:mesh:a", sigma_raw=0.8); rec("join", p() - a)
     a = p(); await hv.activate_session(sid); rec("activate", p() - a)
@@ -26,7 +27,8 @@ async def one():
     rec("capture x3", p() - a)
     a = p(); saga = s.saga.create_saga(sid); rec("create_saga", p() - a)
     a = p(); step = s.saga.add_step(saga.saga_id, "action", "did:mesh:a", "/api/action"); rec("add_step", p() - a)
-    a = p(); await s.saga.execute_step(saga.saga_id, step.step_id, executor=lambda: asyncio.sleep(0)); rec("execute_step", p() - a)
+    a = p(); await s.saga.execute_step(saga.saga_id, step.step_id,
+                                       executor=lambda: asyncio.sleep(0)); rec("execute_step", p() - a)
     a = p(); await hv.terminate_session(sid); rec("terminate", p() - a)
     a = p(); del s, hv, saga, step; rec("teardown", p() - a)
 async def run(n):

@@ -22,7 +22,8 @@ def main(path: str) -> None:
     ).fetchall()
     total = sum(r[2] for r in rows) or 1
     print(f"source: `{path}`  (durations in µs, from rocprofv3 --kernel-trace)\n")
-    print("| kernel | calls | total µs | mean µs | min µs | max µs | % GPU | VGPR | AGPR | SGPR | LDS B | scratch B | grid | wg |")
+    print("| kernel | calls | total µs | mean µs | min µs | max µs | % GPU | VGPR | AGPR | SGPR | LDS B "
+          "| scratch B | grid | wg |")
     print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
     for r in rows:
         name = r[0] if len(r[0]) < 90 else r[0][:87] + "..."

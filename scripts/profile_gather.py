@@ -44,7 +44,8 @@ def main() -> None:
         asyncio.run(batch(n))
         wall, cpu = time.perf_counter() - w0, time.process_time() - c0
         i1 = st.info() if st else {}
-        d = {k: i1[k] - i0[k] for k in i1 if isinstance(i1.get(k), (int, float)) and isinstance(i0.get(k), (int, float))}
+        d = {k: i1[k] - i0[k] for k in i1 if isinstance(i1.get(k), (int, float)) and isinstance(i0.get(k), (int,
+                                                                                                            float))}
         print(json.dumps({
             "device": dev, "round": rnd, "pipelines": n, "pipelines_per_s": round(n / wall, 1),
             "host_cpu_us_per_pipeline": round(cpu / n * 1e6, 2),
@@ -59,7 +60,8 @@ def main() -> None:
     asyncio.run(batch(n // 4))
     pr.disable()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats(os.environ.get("SORT", "tottime")).print_stats(int(os.environ.get("TOP", "30")))
+    pstats.Stats(pr, stream=s).sort_stats(os.environ.get("SORT", "tottime")).print_stats(int(os.environ.get("TOP",
+                                                                                                            "30")))
     print("\n".join(ln for ln in s.getvalue().splitlines() if ln.strip()))
 
 

@@ -53,10 +53,12 @@ def main() -> int:
     checks = {
         "all_reduce": bool(torch.all(a == tot)),
         "all_gather": g.cpu().tolist() == [[r] * 4 for r in range(world)],
-        "reduce_scatter": torch.equal(rs.cpu(), (torch.arange(8 * world, dtype=torch.float64) * world)[8 * rank:8 * rank + 8]),
+        "reduce_scatter": torch.equal(rs.cpu(), (torch.arange(8 * world,
+                                                              dtype=torch.float64) * world)[8 * rank:8 * rank + 8]),
         "broadcast": bool(torch.all(b == 7)),
         # block r of rank q's input (4 ints) lands in block q of rank r's output
-        "all_to_all": y.cpu().tolist() == [v for q in range(world) for v in range(4 * rank + 100 * q, 4 * rank + 4 + 100 * q)],
+        "all_to_all": y.cpu().tolist() == [v for q in range(world) for v in range(4 * rank + 100 * q,
+                                                                                  4 * rank + 4 + 100 * q)],
     }
     out["rccl_version"] = Communicator.version()
     out["communicator"] = checks

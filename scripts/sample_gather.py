@@ -89,7 +89,8 @@ def main() -> None:
     dt = time.perf_counter() - t0
     cpu = time.process_time() - t_cpu
     us_per = dt / n * 1e6  # samples are of wall time (the run is host-CPU bound)
-    out = {"device": dev, "pipelines": n, "pipelines_per_s": round(n / dt, 1), "cpu_us_per_pipeline": round(cpu / n * 1e6, 2),
+    out = {"device": dev, "pipelines": n, "pipelines_per_s": round(n / dt, 1),
+           "cpu_us_per_pipeline": round(cpu / n * 1e6, 2),
            "wall_us_per_pipeline": round(us_per, 2),
            "samples": total[0]}
     print(json.dumps(out))

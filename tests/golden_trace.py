@@ -104,7 +104,8 @@ def make_ops(seed: int = 2026, n_sessions: int = 32, n_ops: int = 1200) -> list:
         elif r < 0.76:
             voucher, vouchee = rng.sample(DIDS[:6], 2)
             expiry = rng.choice([None, None, None, -OP_US, 3 * OP_US, 40 * OP_US])
-            ops.append(["vouch", voucher, vouchee, k, rng.choice(SIGMAS), rng.choice([None, 0.1, 0.2, 0.35, 0.5, 1.5, -0.1]),
+            ops.append(["vouch", voucher, vouchee, k, rng.choice(SIGMAS), rng.choice([None, 0.1, 0.2, 0.35, 0.5, 1.5,
+                                                                                      -0.1]),
                         expiry])
         elif r < 0.80:
             ops.append(["sigma_eff", did, k, rng.choice(SIGMAS), rng.choice(RISK)])
@@ -321,7 +322,8 @@ async def run_ops(ops: list, set_now: Callable[[int], None], hv_kwargs: Optional
                 r = hv.slashing.slash(vouchee, sids[k], sigma, w, reason, sc)
                 hist = hv.slashing.history[before:]
                 out = {"before": r.vouchee_sigma_before, "after": r.vouchee_sigma_after,
-                       "clips": [[c.voucher_did, c.sigma_before, c.sigma_after, c.risk_weight] for c in r.voucher_clips],
+                       "clips": [[c.voucher_did, c.sigma_before, c.sigma_after,
+                                  c.risk_weight] for c in r.voucher_clips],
                        "cascade": [[h.vouchee_did, h.cascade_depth, h.reason, len(h.voucher_clips)] for h in hist],
                        "scores": sorted(sc.items())}
             elif kind == "ring_check":

@@ -7,7 +7,6 @@ import hashlib
 import socket
 
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 

@@ -6,7 +6,7 @@ from __future__ import annotations
 import hashlib
 
 import pytest
-import torch
+import torch  # noqa: F401 - loaded before the native extension
 
 from agent_hypervisor_amd._native import C
 from agent_hypervisor_amd.models.engine import GovernanceEngine

@@ -55,7 +55,8 @@ def test_ring_check_matches_enforcer():
         )
         rows.append((rng.randint(0, 3), act, rng.choice([rng.random(), 0.6, 0.95, 0.97]),
                      rng.random() < 0.5, rng.random() < 0.5))
-    flags = [R.action_flags(a.is_admin, a.is_read_only, a.reversibility == ReversibilityLevel.NONE) for _, a, *_ in rows]
+    flags = [R.action_flags(a.is_admin, a.is_read_only, a.reversibility == ReversibilityLevel.NONE) for _, a,
+             *_ in rows]
     req, reason = R.ring_check(
         torch.tensor([r[0] for r in rows], dtype=u8), torch.tensor(flags, dtype=u8),
         torch.tensor([r[2] for r in rows], dtype=f64), torch.tensor([r[3] for r in rows], dtype=u8),
@@ -149,7 +150,8 @@ def test_vouch_admit_matches_engine_sequence():
                         else LI.ADMIT_CYCLE if "Circular" in msg else LI.ADMIT_EXPOSURE)
                 want_code.append(code)
                 want_bonded.append(0.0)
-    empty = LI.VouchBatch(torch.zeros(S + 1, dtype=i32), *(torch.zeros(0, dtype=d) for d in (u8, u8, f64, u8, i64, i64)))
+    empty = LI.VouchBatch(torch.zeros(S + 1, dtype=i32), *(torch.zeros(0, dtype=d) for d in (u8, u8, f64, u8, i64,
+                                                                                             i64)))
     r_off = [0]
     for s in range(S):
         r_off.append(r_off[-1] + len(reqs[s]))
@@ -642,7 +644,8 @@ def test_render_rows_stamps_and_hex():
     out = torch.zeros(5 * L, dtype=u8)
     src = torch.arange(5 * 4, dtype=torch.int32).reshape(5, 4)  # 16 bytes per row
     ids = torch.tensor([4, 0, 2], dtype=torch.int64)
-    p_id, p_us, p_h = bytes(tmpl.tolist()).index(b"#"), bytes(tmpl.tolist()).index(b"."), bytes(tmpl.tolist()).index(b"?")
+    tb = bytes(tmpl.tolist())
+    p_id, p_us, p_h = tb.index(b"#"), tb.index(b"."), tb.index(b"?")
     A.render_rows(out, tmpl, ids, stamps=[(p_id, 7, 0, 0), (p_us, 6, 3, 998)], hex_field=(p_h, src, 4))
     rows = out.view(5, L)
     for i in ids.tolist():

@@ -6,7 +6,6 @@ next interaction (``GovernanceStore.post_checked`` / ``verify_deferred``)."""
 from __future__ import annotations
 
 import asyncio
-import os
 
 import pytest
 
@@ -254,7 +253,8 @@ def test_speculation_off_gives_the_same_results(monkeypatch):
         hv = Hypervisor(device="cpu")
         m = await hv.create_session(SessionConfig(), "did:admin")
         sid = m.sso.session_id
-        r = [int(await hv.join_session(sid, d, sigma_raw=s)) for d, s in (("did:a", 0.8), ("did:b", 0.96), ("did:c", 0.3))]
+        r = [int(await hv.join_session(sid, d, sigma_raw=s)) for d, s in (("did:a", 0.8), ("did:b", 0.96), ("did:c",
+                                                                                                            0.3))]
         await hv.activate_session(sid)
         g = m.saga.create_saga(sid)
         st_ = m.saga.add_step(g.saga_id, "a", "did:a", "/x")

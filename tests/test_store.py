@@ -240,7 +240,8 @@ def test_parity_suites_through_cpu_twin_store():
 def test_reference_oracle_through_cpu_twin_store():
     env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
     env.update(PYTHONPATH=ROOT, PYTHONDONTWRITEBYTECODE="1", AHV_SKIP_AUTOBUILD="1", AHV_STORE="cpu")
-    cmd = [sys.executable, "-m", "pytest", "/root/reference/tests", "-q", "-p", "agent_hypervisor_amd.utils.pytest_async",
+    cmd = [sys.executable, "-m", "pytest", "/root/reference/tests", "-q", "-p",
+           "agent_hypervisor_amd.utils.pytest_async",
            "-p", "no:cacheprovider", "-c", os.devnull, "--rootdir", "/tmp"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd="/tmp")
     assert p.returncode == 0 and "326 passed" in p.stdout, p.stdout[-3000:]

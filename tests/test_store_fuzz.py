@@ -134,7 +134,8 @@ async def run(device: str, ops: list) -> list:
             elif kind == "saga":
                 m = sess(op[1])
                 saga = m.saga.create_saga(m.sso.session_id)
-                steps = [m.saga.add_step(saga.saga_id, f"a{j}", op[5], f"/x/{j}", undo_api=f"/u/{j}" if j % 2 == 0 else None)
+                steps = [m.saga.add_step(saga.saga_id, f"a{j}", op[5], f"/x/{j}",
+                                         undo_api=f"/u/{j}" if j % 2 == 0 else None)
                          for j in range(op[2])]
                 fail = op[3]
                 trail = []

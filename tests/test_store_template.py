@@ -17,7 +17,7 @@ import pytest
 import torch
 
 from agent_hypervisor_amd.models import store_template as TT
-from hypervisor import Hypervisor, SessionConfig
+from hypervisor import Hypervisor
 from hypervisor.session import SessionLifecycleError
 
 DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]

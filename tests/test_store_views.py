@@ -29,7 +29,8 @@ async def _sessions(hv, n: int, deltas: int = 3) -> list:
         await hv.join_session(sid, f"did:a{i % 7}", sigma_raw=0.8)
         await hv.activate_session(sid)
         for k in range(deltas + i % 3):
-            m.delta_engine.capture(f"did:a{i % 7}", [VFSChange(path=f"/f{k}", operation="add", content_hash=f"h{i}.{k}")])
+            m.delta_engine.capture(f"did:a{i % 7}", [VFSChange(path=f"/f{k}", operation="add",
+                                                               content_hash=f"h{i}.{k}")])
         if i % 2:
             await hv.terminate_session(sid)
         out.append(m)

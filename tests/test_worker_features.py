@@ -31,7 +31,8 @@ pytestmark = pytest.mark.gpu
 _BITS = ("AHV_STORE_NARROW_FREE", "AHV_STORE_LIGHT_PUBLISH", "AHV_STORE_SLOT_PREFETCH")
 
 
-@pytest.mark.parametrize("on", [(0, 0, 0), (1, 0, 0), (0, 1, 1), (1, 1, 1)], ids=["off", "narrow", "light+prefetch", "all"])
+@pytest.mark.parametrize("on", [(0, 0, 0), (1, 0, 0), (0, 1, 1), (1, 1, 1)], ids=["off", "narrow", "light+prefetch",
+                                                                                  "all"])
 def test_worker_feature_bits_keep_results(cuda_device, monkeypatch, on):
     for name, v in zip(_BITS, on):
         monkeypatch.setenv(name, str(v))  # read when the store's native core is built
