@@ -390,6 +390,19 @@ AHV_HD void emit_pool_str(Sink& s, const StrPool& pool, int32_t id) {
 // by a runtime position would live in scratch memory on the device).
 template <class Sink>
 AHV_HD void emit_uint(Sink& s, uint64_t v) {
+  // turn numbers and counts: one or two digits in one put, 32-bit arithmetic (the
+  // general form divides 64-bit values by a variable power of ten, a long
+  // instruction sequence on the device, twice per rendered record)
+  if (v < 100u) {
+    const uint32_t x = static_cast<uint32_t>(v);
+    if (x < 10u) {
+      if (s.seg(1)) s.put(('0' + x) << 24, 1);
+    } else if (s.seg(2)) {
+      const uint32_t t = x / 10u;
+      s.put((('0' + t) << 24) | (('0' + x - 10u * t) << 16), 2);
+    }
+    return;
+  }
   if (!s.seg(canon::dec_digits(v))) return;
   uint64_t p = 1;
   while (v / p >= 10) p *= 10;
