@@ -722,7 +722,9 @@ __global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint6
     if (lane >= 16) inl[lane - 16] = v;
     L.sync();
     c.inl = inl;
-    if (speculate & 64) {
+    // (feature 512: issued after the command's publication instead — the publication
+    // waits for every outstanding vector memory op, a prefetch issued before it too)
+    if ((speculate & 64) && !(speculate & 512)) {
       pre = ld_sys(ring + ((next + 1) % static_cast<uint64_t>(nslots)) * kSlotWords + lane);
       have_pre = true;
     }
@@ -835,6 +837,10 @@ __global__ __launch_bounds__(256) void store_worker_kernel(Tables t, const uint6
       // (captures complete payload bytes the host may read by DMA: full release)
       publish_fence((speculate & 32) != 0 && !needs_drain(c.op) && c.op != OP_DELTA_CAPTURE);
       out64(r, next + 1);
+    }
+    if ((speculate & 64) && (speculate & 512)) {
+      pre = ld_sys(ring + ((next + 1) % static_cast<uint64_t>(nslots)) * kSlotWords + lane);
+      have_pre = true;
     }
     if (lane == 0) __hip_atomic_store(tail, static_cast<int64_t>(next + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 0) __hip_atomic_store(&ptab.cw_next, next + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);

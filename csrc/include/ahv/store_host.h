@@ -196,7 +196,11 @@ class StoreCore {
       //       hash at 3.2-3.4 µs per block side by side against 2.4 µs for the engine alone
       //       (per-call p50 76.4 vs 69.4 µs, profiles/r6/lookahead_ab_r6v.txt)
       const char* la = std::getenv("AHV_STORE_LOOKAHEAD");
+      // 512 = the next slot's prefetch is issued after the current command's result is
+      //       published (not before its execution: the publication's wait covers it)
+      const char* lp2 = std::getenv("AHV_STORE_LATE_PREFETCH");
       speculate_ = ((la != nullptr && std::atoi(la) != 0) ? 256 : 0) |
+                   ((lp2 != nullptr && std::atoi(lp2) != 0) ? 512 : 0) |
                    ((sc == nullptr || std::atoi(sc) != 0) ? 128 : 0) | ((sp == nullptr || std::atoi(sp) != 0) ? 1 : 0) | ((pf == nullptr || std::atoi(pf) != 0) ? 2 : 0) |
                    ((bt == nullptr || std::atoi(bt) != 0) ? 4 : 0) |
                    ((nf == nullptr || std::atoi(nf) != 0) ? 16 : 0) |
