@@ -124,7 +124,8 @@ def main() -> None:
         eng.run_pipeline(1, agents=one)
         stream.synchronize()
 
-    emit(rank, what="batched pipeline, 1 session, launch+sync", p50_us=round(p50_us(pipe1, max(200, args.iters // 4)), 2))
+    p50 = round(p50_us(pipe1, max(200, args.iters // 4)), 2)
+    emit(rank, what="batched pipeline, 1 session, launch+sync", p50_us=p50)
 
     if world > 1:
         for nbytes in (8, 1 << 10, 1 << 16, 1 << 20, 8 << 20, 64 << 20):

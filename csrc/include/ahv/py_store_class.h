@@ -162,26 +162,39 @@ class Store : public StoreCore {
   // returns [(token, result words)] for the mismatches, or None.
   py::object verify_expects(bool block) {
     if (expects_.empty() && expect_bad_.size() == 0) return py::none();
-    py::list bad = expect_bad_;
-    expect_bad_ = py::list();
+    py::object bad = py::none();  // a list only once there is a mismatch
+    if (expect_bad_.size()) {
+      bad = expect_bad_;
+      expect_bad_ = py::list();
+    }
     while (!expects_.empty()) {
       Expect& e = expects_.front();
-      uint64_t r[kSaveWords];
-      if (!try_result_raw(e.seq, 0, r)) {
-        if (!block) break;
-        const auto t0 = std::chrono::steady_clock::now();
-        while (!try_result_raw(e.seq, 1000000, r)) {
-          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
-            throw std::runtime_error("store: speculated command " + std::to_string(e.seq) + " never completed");
+      uint64_t buf[kSaveWords];
+      // completed and still in its slot: compare the expected words in place
+      const uint64_t* r = peek_done(e.seq);
+      if (r == nullptr) {
+        if (!try_result_raw(e.seq, 0, buf)) {
+          if (!block) break;
+          const auto t0 = std::chrono::steady_clock::now();
+          while (!try_result_raw(e.seq, 1000000, buf)) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+              throw std::runtime_error("store: speculated command " + std::to_string(e.seq) + " never completed");
+          }
         }
+        r = buf;
       }
       bool ok = true;
-      for (int k = 0; k < kSaveWords - 1 && ok; ++k)
-        if ((e.mask >> k) & 1u) ok = r[1 + k] == e.want[k];
-      if (!ok) bad.append(py::make_tuple(e.token, words(r, kSaveWords - 1)));
+      for (uint32_t m = e.mask; m && ok; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        ok = r[1 + k] == e.want[k];
+      }
+      if (!ok) {
+        if (bad.is_none()) bad = py::list();
+        py::reinterpret_borrow<py::list>(bad).append(py::make_tuple(e.token, words(r, kSaveWords - 1)));
+      }
       expects_.pop_front();
     }
-    return bad.size() ? py::object(bad) : py::object(py::none());
+    return bad;
   }
 
   size_t n_expects() const { return expects_.size(); }

@@ -234,6 +234,7 @@ class StoreCore {
     set_pool_caps();
     d_off_.assign(static_cast<size_t>(t_.cap.D), -1);
     d_len_.assign(static_cast<size_t>(t_.cap.D), 0);
+    watch_.assign(static_cast<size_t>(nslots_), 0);
   }
 
   StoreCore(const StoreCore&) = delete;
@@ -346,26 +347,25 @@ class StoreCore {
       } else {
         pr = wait(p);
       }
-      if (!watched_.empty()) {
-        auto it = watched_.find(p);
-        if (it != watched_.end()) {
-          std::array<uint64_t, kSaveWords> a;
-          for (int k = 0; k < kSaveWords; ++k) a[k] = pr[k];
-          saved_[p] = a;
-          watched_.erase(it);
-        }
+      if (nwatch_ && watched(p)) {
+        std::array<uint64_t, kSaveWords> a;
+        for (int k = 0; k < kSaveWords; ++k) a[k] = pr[k];
+        saved_[p] = a;
+        unwatch(p);
       }
     }
     uint64_t w[kSlotWords];
-    std::memset(w, 0, sizeof w);
     // words in use (header, arguments, inline payload): only these cross the BAR;
     // the worker reads the count from w[1]'s high half and treats the rest as zero
+    // (zero words add nothing to the checksum: slot_mix(0, k) = 0)
     const uint32_t nw = inl_bytes ? 16u + static_cast<uint32_t>((inl_bytes + 7) / 8) : 3u + static_cast<uint32_t>(nargs);
+    const uint32_t nz = gpu_ ? std::min<uint32_t>((nw + 3u) & ~3u, kSlotWords) : kSlotWords;  // the BAR chunks' words
+    std::memset(w, 0, 8 * static_cast<size_t>(nz));
     w[1] = op | (static_cast<uint64_t>(nw) << 32);
     for (size_t k = 0; k < nargs; ++k) w[3 + k] = args[k];
     if (inl_bytes) std::memcpy(w + 16, inl, inl_bytes);
     uint64_t x = slot_mix(w[1], 1);
-    for (int k = 3; k < kSlotWords; ++k) x ^= slot_mix(w[k], static_cast<uint64_t>(k));
+    for (uint32_t k = 3; k < nw; ++k) x ^= slot_mix(w[k], static_cast<uint64_t>(k));
     w[2] = x;
     ++posted_;
     if (trace_cap_ > 0)
@@ -466,13 +466,26 @@ class StoreCore {
   // under thousands of concurrent pipelines).  Consumed by try_result/result.
   void keep(uint64_t q) {
     if (q >= next_) throw std::out_of_range("store: sequence number not posted");
-    if (q + static_cast<uint64_t>(nslots_) >= next_) watched_[q] = 1;
+    if (q + static_cast<uint64_t>(nslots_) >= next_) watch(q);
   }
 
   // Drop a kept result that will never be read (its awaiting call was cancelled).
   void discard(uint64_t q) {
-    watched_.erase(q);
+    unwatch(q);
     saved_.erase(q);
+  }
+
+  // The result words of `q` in place when it has completed and its slot still holds
+  // it (nullptr otherwise: not done yet, recycled into `saved_`, or posted later) —
+  // the expectation check's fast path, no copy of the result words.
+  const uint64_t* peek_done(uint64_t q) {
+    if (q >= next_) return nullptr;
+    volatile uint64_t* r = res_ + (q % static_cast<uint64_t>(nslots_)) * store::kResWords;
+    const uint64_t v = r[0];
+    if (v < q + 1 || v >= q + 1 + static_cast<uint64_t>(nslots_)) return nullptr;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (nwatch_) unwatch(q);
+    return const_cast<const uint64_t*>(r);
   }
 
   // Non-blocking form for asyncio callers: copies the first kSaveWords result
@@ -494,7 +507,7 @@ class StoreCore {
       // just look: no spin (a 256-pause spin before the first clock check cost ≈3 µs
       // on every speculation check and asyncio poll of a command still in flight)
       if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) == 0) ensure_worker();
-      watched_[q] = 1;
+      watch(q);
       return false;
     }
     if (r[0] < q + 1 && gpu_) {
@@ -509,11 +522,11 @@ class StoreCore {
       }
       if (r[0] < q + 1) {
         if (__atomic_load_n(alive_, __ATOMIC_ACQUIRE) == 0) ensure_worker();
-        watched_[q] = 1;  // keep the results if the slot is recycled before they are collected
+        watch(q);  // keep the results if the slot is recycled before they are collected
         return false;
       }
     }
-    if (!watched_.empty()) watched_.erase(q);
+    if (nwatch_) unwatch(q);
     if (r[0] >= q + 1 + static_cast<uint64_t>(nslots_)) throw ResultGone();
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     for (int k = 0; k < kSaveWords; ++k) out[k] = r[k];
@@ -918,7 +931,7 @@ class StoreCore {
         if (r[0] < q + 1 && !block) break;
         if (r[0] < q + 1) ++reclaim_waits_;
         st = wait(q)[1];
-        watched_.erase(q);
+        unwatch(q);
       }
       if (st != store::ST_OK) {
         frees_.erase(frees_.begin(), frees_.begin() + static_cast<std::ptrdiff_t>(k + 1));
@@ -962,7 +975,7 @@ class StoreCore {
   int64_t trace_cap() const { return trace_cap_; }
   const std::vector<uint64_t>& post_ns() const { return post_ns_; }
   int64_t nslots() const { return nslots_; }
-  size_t kept() const { return watched_.size() + saved_.size(); }
+  size_t kept() const { return nwatch_ + saved_.size(); }
   const int64_t* tail() const { return tail_; }
 
  protected:
@@ -1015,7 +1028,26 @@ class StoreCore {
   uint64_t reclaim_waits_ = 0;   // times a reclaim blocked on a FREE_ROWS result
   size_t stage_head_ = 0;
   ArenaAlloc arena_;
-  std::unordered_map<uint64_t, int> watched_;                             // seqs with a pending async waiter
+  // Per ring slot: seq + 1 of a kept result still in that slot (0: none) — a slot
+  // holds one command at a time, so keeping / releasing a result is an array store
+  // (the per-command hash-map node it replaced showed up under 10^4 concurrent pipelines)
+  std::vector<uint64_t> watch_;
+  size_t nwatch_ = 0;
+  void watch(uint64_t q) {
+    uint64_t& w = watch_[q % static_cast<uint64_t>(nslots_)];
+    if (w != q + 1) {
+      if (w == 0) ++nwatch_;
+      w = q + 1;
+    }
+  }
+  bool watched(uint64_t q) const { return watch_[q % static_cast<uint64_t>(nslots_)] == q + 1; }
+  void unwatch(uint64_t q) {
+    uint64_t& w = watch_[q % static_cast<uint64_t>(nslots_)];
+    if (w == q + 1) {
+      w = 0;
+      --nwatch_;
+    }
+  }
   std::unordered_map<uint64_t, std::array<uint64_t, kSaveWords>> saved_;  // their results, once recycled
   std::vector<int64_t> d_off_, d_len_;  // arena record of each delta row (-1: row free)
   std::vector<int32_t> dfree_;          // reclaimed delta rows
