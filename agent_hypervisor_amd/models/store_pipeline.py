@@ -49,6 +49,13 @@ _SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX in ("kernel", "sorted") else 1
 # 18 µs per 10^6 sessions (render 707 -> 689 µs, profiles/r6/hetero_frags_r6s.jsonl)
 # but the host pass costs ≈ 0.4 µs per delta in prepare, which the public API times
 _SP_FRAGS = _os.environ.get("AHV_SP_FRAGS", "0") != "0"
+# render before the rows pass, whose blocks then share one launch with the prefix SHA
+# blocks (store_pipe_prefix_rows_kernel: memory-bound rows waves beside VALU-bound
+# SHA waves); AHV_SP_OVERLAP=0: rows, render, prefix as three passes
+_SP_OVERLAP = _os.environ.get("AHV_SP_OVERLAP", "1") != "0"
+# the committed chains' Merkle roots (K09) folded in the chain kernel's lanes as the
+# digests are produced; AHV_SP_CHAIN_ROOTS=0: the K09 kernel afterwards (_k09_plan)
+_SP_CHAIN_ROOTS = _os.environ.get("AHV_SP_CHAIN_ROOTS", "1") != "0" and _SP_PREFIX != "chain"
 
 _STATUS = {0: "ok", 1: "row_in_use", 2: "join_refused", 3: "activate_refused", 4: "step_failed",
            5: "terminate_refused", 6: "record_overflow"}
@@ -357,9 +364,14 @@ class Prepared:
         """Free the batch's session / saga / step rows in place (on the stream), so
         :func:`launch` can run the whole pipeline over them again."""
         t = self.store.tables
-        for col, ix in (("s_state", self.tens["slot"]), ("g_state", self.g_live), ("t_state", self.t_live)):
-            if ix is not None and ix.numel():
-                t[col].index_fill_(0, ix.to(torch.int64), 255)  # kFree8
+        ixs = self.__dict__.get("_reset_ix")
+        if ixs is None:  # int64 row indices, converted once
+            ixs = self.__dict__["_reset_ix"] = [
+                (col, ix.to(torch.int64)) for col, ix in (("s_state", self.tens["slot"]), ("g_state", self.g_live),
+                                                          ("t_state", self.t_live)) if ix is not None and ix.numel()]
+        for col, ix in ixs:
+            t[col].index_fill_(0, ix, 255)  # kFree8
+        self.tens["status"].zero_()  # the kernels write only codes other than ok over a zeroed array
 
 
 def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
@@ -545,7 +557,8 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
         tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
     args = {k: v.data_ptr() for k, v in tens.items()}
-    args.update(prefix_in_render=_SP_PREFIX_IN_RENDER,
+    args.update(prefix_in_render=_SP_PREFIX_IN_RENDER, render_first=int(_SP_OVERLAP),
+                chain_roots=int(_SP_CHAIN_ROOTS),
                 max_nch=int(np.diff(np.asarray(ch_off_all, dtype=np.int64)).max()) if nd else 0)
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)
     if shared:
@@ -609,7 +622,8 @@ def launch(p: "Prepared", sync: bool = True) -> "Prepared":
     else:
         st._c.run_pipeline(p.args, 0)
     # K09: roots of the committed chains over the digests just written → s_root
-    plan = _k09_plan(p)
+    # (already there when the chain kernel folded them: chain_roots)
+    plan = None if p.args.get("chain_roots") else _k09_plan(p)
     if plan is not None:
         from agent_hypervisor_amd.ops import audit as A
 

@@ -9,28 +9,30 @@
 // device session of the public API (views, reads, verify, terminate all work on
 // it), unlike the standalone engine tables of models/engine.py.
 //
-// Four launches, all over rows the host allocator handed out (free rows; a row
-// that is not free is refused and reported, never overwritten):
+// Three launches (render_first, the default), all over rows the host allocator
+// handed out (free rows; a row that is not free is refused and reported, never
+// overwritten):
 //
-//   store_pipe_rows_kernel    lane per session: create (+ handshake), joins
-//                             through the K01 ring gate and join admission,
-//                             activate, saga/step FSM (K13) with retries and
-//                             compensation (K14), terminate → commit → GC →
-//                             archive bookkeeping, chain links of its delta rows
-//   store_pipe_render_kernel  lane per delta: the canonical-JSON record (the
-//                             shared emitters of ahv/delta_emit.h) written into
-//                             the payload arena, parent digest left as a hole
-//   store_pipe_prefix_kernel  lane per delta: SHA-256 of the record's blocks
-//                             before the parent hole (all of a turn-1 record)
-//   store_pipe_chain_kernel   lane per session: the serial SHA-256 chain (K08):
-//                             each record's parent hole filled with the previous
-//                             digest, then compressed from the prefix midstate;
-//                             digests and chain head
+//   store_pipe_render_kernel       lane per delta: the canonical-JSON record (the
+//                                  shared emitters of ahv/delta_emit.h) written into
+//                                  the payload arena, parent digest left as a hole
+//   store_pipe_prefix_rows_kernel  two kinds of block, interleaved:
+//     rows    lane per session: create (+ handshake), joins through the K01 ring
+//             gate and join admission, activate, saga/step FSM (K13) with retries
+//             and compensation (K14), terminate → commit → GC → archive
+//             bookkeeping, chain links of its delta rows
+//     prefix  lane per delta: SHA-256 of the record's blocks before the parent
+//             hole (all of a turn-1 record)
+//   store_pipe_chain_kernel        lane per session: the serial SHA-256 chain (K08):
+//                                  each record's parent hole filled with the previous
+//                                  digest, then compressed from the prefix midstate;
+//                                  digests and chain head; then the Merkle root (K09)
+//                                  of a committed chain into s_root (chain_roots)
 //
+// (render_first = 0: rows, render, prefix as passes of their own; chain_roots = 0:
+// the K09 kernel reads the resident digests afterwards — store_pipeline.py.)
 // Lanes take records / sessions in descending-work order (render_order,
-// chain_order) so a wave's lanes finish together.  The Merkle roots (K09) of
-// the committed chains then come from the K09 kernel reading the resident
-// digests in place and writing s_root (agent_hypervisor_amd/models/store_pipeline.py).
+// chain_order) so a wave's lanes finish together.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
@@ -97,6 +99,12 @@ struct StorePipeArgs {
   const uint8_t* frag_bytes;    // heads, each 16-byte aligned and zero-padded
   const int64_t* frag_off;      // [F]
   const int32_t* frag_len;      // [F]
+  // 1: render before rows (the render lane checks its session row itself), rows
+  // blocks interleaved with the prefix SHA blocks in one launch (store_pipe_prefix_rows_kernel)
+  int32_t render_first;
+  // 1: the chain lane folds its session's digests into the Merkle root (K09) as it
+  // produces them and writes s_root of a committed row (needs `mid`: its scratch)
+  int32_t chain_roots;
 };
 
 enum StorePipeStatus : int32_t {
@@ -275,7 +283,16 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
     }
   }
   t.s_state[s] = st;
-  a.status[i] = status;
+  // a record that overflowed its reservation outranks the other stages' codes
+  // (render ran first: its SP_RENDER is already in status)
+  if (!a.render_first || a.status[i] != SP_RENDER) a.status[i] = status;
+}
+
+// The render-first layout: the session row is free for this batch (the rows pass
+// checks the same and has not written s_state yet when the render lanes run).
+AHV_HD bool sp_row_in_use(const StorePipeArgs& a, int64_t i) {
+  const int64_t s = a.slot[i];
+  return s < 0 || s >= a.t.cap.S || a.t.s_state[s] != kFree8;
 }
 
 // Bytes of one record, written straight to the arena (records start 64-byte
@@ -572,6 +589,43 @@ AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
   }
 }
 
+// K09 in the chain lane: the session's Merkle root over the digests its chain just
+// produced (still in this lane's cache lines), as a binary counter whose ≤ ⌊log2 n⌋+1
+// partial subtrees are parked in the session's own `mid` rows — spent by then: a
+// record's row is read before its digest exists, and slot L ≤ log2(k+1) ≤ k.  Same
+// tree as merkle_kernel (reference audit/delta.py:117-134, odd node duplicated).
+struct MidStash {
+  uint32_t* rows;
+  AHV_HD void stash(int j, const uint32_t d[8]) {
+    for (int k = 0; k < 8; ++k) rows[j * 8 + k] = d[k];
+  }
+  AHV_HD void load(int j, uint32_t d[8]) const {
+    for (int k = 0; k < 8; ++k) d[k] = rows[j * 8 + k];
+  }
+  AHV_HD void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) const {
+    uint32_t t[8];
+    merkle_node(l, r, t);
+    for (int k = 0; k < 8; ++k) out[k] = t[k];
+  }
+};
+
+AHV_HD void sp_chain_root(const StorePipeArgs& a, int64_t i) {
+  const Tables& t = a.t;
+  const int64_t s = a.slot[i];
+  const int32_t d0 = a.delta_off[i], d1 = a.delta_off[i + 1];
+  if (d1 <= d0 || t.s_committed[s] == 0) return;  // no root: s_root stays as the rows pass zeroed it
+  MidStash ms{a.mid + 8 * static_cast<int64_t>(d0)};
+  uint32_t r[8];
+  merkle_root_counter(
+      ms, static_cast<uint32_t>(d1 - d0),
+      [&](uint32_t k, uint32_t h[8]) {
+        const int64_t d = a.drow[d0 + static_cast<int32_t>(k)];
+        for (int q = 0; q < 8; ++q) h[q] = t.d_hash[8 * d + q];
+      },
+      r);
+  for (int k = 0; k < 8; ++k) t.s_root[8 * s + k] = r[k];
+}
+
 __global__ __launch_bounds__(256) void store_pipe_rows_kernel(StorePipeArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < a.n) sp_rows(a, i);
@@ -595,8 +649,37 @@ __global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a,
   if (x < nd) {
     const int64_t g = a.render_order ? a.render_order[x] : x;  // records of similar size per wave
     const int64_t i = dsess[g];
-    if (a.status[i] != SP_ROW_IN_USE && (!a.wide_only || a.dch_off[g + 1] - a.dch_off[g] > 4))
+    if (a.render_first) {
+      if (sp_row_in_use(a, i)) a.status[i] = SP_ROW_IN_USE;  // (every lane of the session writes the same)
+      else sp_render(a, i, static_cast<int32_t>(g));
+    } else if (a.status[i] != SP_ROW_IN_USE && (!a.wide_only || a.dch_off[g + 1] - a.dch_off[g] > 4)) {
       sp_render(a, i, static_cast<int32_t>(g));
+    }
+  }
+}
+
+// Render-first layout: the rows pass (memory-latency bound: 672 VALU per lane, r6
+// PMC) and the prefix SHA pass (VALU bound) in one grid, their blocks interleaved
+// in proportion, so each CU runs both kinds of wave side by side and the rows'
+// memory waits hide under SHA issue instead of taking their own 215 µs pass.
+// Neither reads what the other writes: prefix reads the records and status codes
+// the render pass left (SP_ROW_IN_USE, written there for in-use rows); rows writes
+// the session / participant / saga rows and the other codes, never SP_ROW_IN_USE
+// for a row that is free.
+__global__ __launch_bounds__(256) void store_pipe_prefix_rows_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd,
+                                                                     uint32_t nrows_blk, uint32_t nblk) {
+  const uint64_t b = blockIdx.x;
+  const uint64_t r0 = b * nrows_blk / nblk, r1 = (b + 1) * nrows_blk / nblk;  // rows blocks before / through b
+  if (r1 > r0) {
+    const int64_t i = static_cast<int64_t>(r0) * blockDim.x + threadIdx.x;
+    if (i < a.n) sp_rows(a, i);
+    return;
+  }
+  const int64_t x = static_cast<int64_t>(b - r0) * blockDim.x + threadIdx.x;
+  if (x < nd) {
+    const int64_t g = a.prefix_order ? a.prefix_order[x] : a.render_order ? a.render_order[x] : x;
+    if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix(a, g);
+    else a.mid_blocks[g] = 0;
   }
 }
 
@@ -608,7 +691,10 @@ __global__ __launch_bounds__(64) void store_pipe_chain_kernel(StorePipeArgs a) {
   const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (x >= a.n) return;
   const int64_t i = a.chain_order ? a.chain_order[x] : x;
-  if (a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
+  if (a.status[i] != SP_ROW_IN_USE) {
+    sp_chain(a, i);
+    if (a.chain_roots) sp_chain_root(a, i);
+  }
 }
 
 // ------------------------------------------------- wave-cooperative renderer
@@ -965,6 +1051,10 @@ StorePipeArgs to_args(const Tables& t, const py::dict& d) {
   a.prefix_order = d.contains("prefix_order") ? P<const int32_t>(d, "prefix_order") : nullptr;
   a.max_nch = d.contains("max_nch") ? d["max_nch"].cast<int32_t>() : 1 << 30;
   a.wide_only = 0;
+  // only with the prefix pass of its own and the lane renderer (the layout it reorders)
+  a.render_first = d.contains("render_first") && d["render_first"].cast<int32_t>() != 0 && a.mid != nullptr &&
+                   !a.prefix_in_render;
+  a.chain_roots = d.contains("chain_roots") && d["chain_roots"].cast<int32_t>() != 0 && a.mid != nullptr;
   if (d.contains("dfrag")) {
     a.dfrag = P<const int32_t>(d, "dfrag");
     a.frag_bytes = P<const uint8_t>(d, "frag_bytes");
@@ -991,9 +1081,28 @@ static int render_coop() {
 
 // Launch the kernels (rows, render, prefix, chain) on `stream` (device) or run the twin (host tables).
 void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t stream) {
-  const StorePipeArgs a = to_args(t, d);
+  StorePipeArgs a = to_args(t, d);
   const int32_t* dsess = P<const int32_t>(d, "dsess");
   const int64_t nd = d["nd"].cast<int64_t>();
+  if (gpu && render_coop()) a.render_first = 0;
+  if (!gpu && a.render_first) {  // the device's order: render (own row check), rows, prefix, chain
+    for (int64_t g = 0; g < nd; ++g) {
+      const int64_t i = dsess[g];
+      if (sp_row_in_use(a, i)) a.status[i] = SP_ROW_IN_USE;
+      else sp_render(a, i, static_cast<int32_t>(g));
+    }
+    for (int64_t i = 0; i < a.n; ++i) sp_rows(a, i);
+    for (int64_t g = 0; g < nd; ++g) {
+      if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix(a, g);
+      else a.mid_blocks[g] = 0;
+    }
+    for (int64_t i = 0; i < a.n; ++i)
+      if (a.status[i] != SP_ROW_IN_USE) {
+        sp_chain(a, i);
+        if (a.chain_roots) sp_chain_root(a, i);
+      }
+    return;
+  }
   if (!gpu) {
     for (int64_t i = 0; i < a.n; ++i) sp_rows(a, i);
     for (int64_t g = 0; g < nd; ++g)
@@ -1004,12 +1113,21 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
         else a.mid_blocks[g] = 0;
       }
     for (int64_t i = 0; i < a.n; ++i)
-      if (a.status[i] != SP_ROW_IN_USE) sp_chain(a, i);
+      if (a.status[i] != SP_ROW_IN_USE) {
+        sp_chain(a, i);
+        if (a.chain_roots) sp_chain_root(a, i);
+      }
     return;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   py::gil_scoped_release nogil;
-  if (a.n > 0) {
+  if (a.n > 0 && a.render_first) {
+    const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
+    if (nd > 0)
+      hipLaunchKernelGGL(store_pipe_render_kernel, dim3(pb), dim3(256), 0, st, a, dsess, nd);
+    hipLaunchKernelGGL(store_pipe_prefix_rows_kernel, dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
+    hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
+  } else if (a.n > 0) {
     hipLaunchKernelGGL(store_pipe_rows_kernel, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, st, a);
     if (nd > 0) {
       const int cg = render_coop();

@@ -178,10 +178,13 @@ def test_randomized_batch_equals_scalar_api_gpu():
     {"AHV_SP_RENDER": "coop", "AHV_SP_COOP_G": "4"},
     {"AHV_SP_PREFIX": "render", "AHV_SP_ORDER": "1"},
     {"AHV_SP_ORDER": "7"},
+    {"AHV_SP_OVERLAP": "0"},
+    {"AHV_SP_CHAIN_ROOTS": "0"},
 ])
 def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
     """The A/B layouts of the batch kernels (cooperative renderer with 16 / 4 lanes per
-    record, prefix SHA inside the render pass, render lanes by record shape) produce
+    record, prefix SHA inside the render pass, render lanes by record shape, rows before
+    render in a pass of their own, Merkle roots by the K09 kernel) produce
     the same records, digests and roots as the scalar API (a fresh process each: the
     switches are read once)."""
     import os
@@ -194,6 +197,38 @@ def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
     r = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                        env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("render_first", [0, 1])
+def test_status_codes_and_precedence_in_both_kernel_orders(render_first):
+    """Rows pass first, or the render pass first with the rows pass beside the prefix
+    SHA pass (render_first): a row the store holds is refused whole (row_in_use), a
+    record past its reservation reports record_overflow — over a refused join too —
+    and the other sessions of the batch run through (CPU twin of the device order)."""
+    import numpy as np
+
+    from agent_hypervisor_amd.models import store_pipeline as SP
+
+    st = GovernanceStore("cpu", caps={"S": 64, "D": 256, "G": 64, "T": 64})
+    hv = Hypervisor(store=st)
+    dup = (("did:mesh:a", 0.9), ("did:mesh:a", 0.9))  # the second join is a duplicate: join_refused
+    specs = [PipelineSpec(), PipelineSpec(), PipelineSpec(joins=dup), PipelineSpec(), PipelineSpec(joins=dup)]
+    p = SP.prepare(hv, specs)
+    p.args["render_first"] = render_first
+    s_state = st.tables["s_state"]
+    s_state[int(p.slots[1])] = 1  # held by someone else
+    dcap = p.tens["dcap"]
+    d_off = list(p.delta_off)
+    for i in (2, 3):  # the session's last record gets one 64-byte line: it overflows
+        dcap[d_off[i + 1] - 1] = 64
+    st._c.run_pipeline(p.args, 0)
+    status = p.tens["status"].cpu().numpy()
+    assert status.tolist() == [0, 1, 6, 6, 2]
+    assert int(s_state[int(p.slots[1])]) == 1  # not written
+    mb = p.tens["mid_blocks"].cpu().numpy()
+    assert not mb[d_off[1]:d_off[2]].any()  # the refused row's records were not hashed
+    assert mb[d_off[0]:d_off[1]].all() and np.asarray(mb[d_off[4]:d_off[5]]).all()
+    st.close()
 
 
 def test_lazy_rows_released_in_bulk_and_materialized_rows_kept(monkeypatch):
