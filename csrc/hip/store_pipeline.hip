@@ -311,7 +311,13 @@ AHV_HD void store4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) 
 #endif
 }
 
-struct ArenaSink {
+// kFlat (default): put() and word() are straight-line — the word completion and
+// the 16-byte chunk completion are selects, and the one branch left per put is
+// the chunk's store.  The staged form (kFlat = false, AHV_SP_SINK=staged) branches
+// on both, and every divergent branch costs the wave exec-mask bookkeeping (the
+// r6 ISA of the render kernel: ≈ 4 SALU mask / branch instructions per put).
+template <bool kFlat>
+struct ArenaSinkT {
   uint32_t* dst;
   uint32_t cap_w;
   uint32_t nw = 0;   // words in memory (a multiple of 4 until flush)
@@ -324,7 +330,22 @@ struct ArenaSink {
   template <class T>
   AHV_HD void launder(T&) const {}
   AHV_HD uint32_t pos() const { return 4 * (nw + nq) + nb; }
+  // Stage w when `take`; a completed chunk is stored if it lies inside the
+  // reservation (past it the record overflows, SP_RENDER: its bytes are void).
+  AHV_HD void stage(uint32_t w, bool take) {
+    const bool done = take && nq == 3;
+    if (done && nw + 4 <= cap_w) store4(dst + nw, q0, q1, q2, w);
+    q0 = take && nq == 0 ? w : q0;
+    q1 = take && nq == 1 ? w : q1;
+    q2 = take && nq == 2 ? w : q2;
+    nw += done ? 4u : 0u;
+    nq = take ? (nq + 1) & 3u : nq;
+  }
   AHV_HD void word(uint32_t w) {
+    if (kFlat) {
+      stage(w, true);
+      return;
+    }
     if (nq == 3) {
       if (nw + 4 <= cap_w) {
         store4(dst + nw, q0, q1, q2, w);
@@ -355,8 +376,19 @@ struct ArenaSink {
   // lane, and a per-byte loop made every lane of a wave run the longest one.
   AHV_HD void put(uint32_t v, uint32_t n) {
     const uint32_t m = n >= 4 ? 0xffffffffu : (1u << (8 * n)) - 1u;
-    const uint64_t x = static_cast<uint64_t>(acc) | (static_cast<uint64_t>(bswap32(v) & m) << (8 * nb));
     const uint32_t tot = nb + n;
+    if (kFlat) {
+      const uint32_t vv = bswap32(v) & m;
+      const uint32_t sh = 8 * nb;  // 0..24
+      const uint32_t lo = acc | (vv << sh);
+      const uint32_t hi = nb ? vv >> (32u - sh) : 0u;
+      const bool full = tot >= 4;
+      stage(lo, full);
+      acc = full ? hi : lo;
+      nb = full ? tot - 4 : tot;
+      return;
+    }
+    const uint64_t x = static_cast<uint64_t>(acc) | (static_cast<uint64_t>(bswap32(v) & m) << (8 * nb));
     if (tot >= 4) {
       word(static_cast<uint32_t>(x));
       acc = static_cast<uint32_t>(x >> 32);
@@ -430,12 +462,13 @@ AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t 
 
 AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g);
 
+template <bool kFlat = true>
 AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   const Tables& t = a.t;
   const int32_t k = g - a.delta_off[i];
   const int32_t d = a.drow[g];
   const int64_t s = a.slot[i];
-  ArenaSink snk;
+  ArenaSinkT<kFlat> snk;
   snk.dst = reinterpret_cast<uint32_t*>(t.payload + a.doff[g]);
   snk.cap_w = static_cast<uint32_t>(a.dcap[g]) / 4;
   const ChangeIds* ch = a.changes + a.dch_off[g];
@@ -644,6 +677,7 @@ __global__ __launch_bounds__(256) void store_pipe_prefix_kernel(StorePipeArgs a,
 }
 
 // lane per delta; `dsess` maps a delta to its session
+template <bool kFlat>
 __global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd) {
   const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (x < nd) {
@@ -651,9 +685,9 @@ __global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a,
     const int64_t i = dsess[g];
     if (a.render_first) {
       if (sp_row_in_use(a, i)) a.status[i] = SP_ROW_IN_USE;  // (every lane of the session writes the same)
-      else sp_render(a, i, static_cast<int32_t>(g));
+      else sp_render<kFlat>(a, i, static_cast<int32_t>(g));
     } else if (a.status[i] != SP_ROW_IN_USE && (!a.wide_only || a.dch_off[g + 1] - a.dch_off[g] > 4)) {
-      sp_render(a, i, static_cast<int32_t>(g));
+      sp_render<kFlat>(a, i, static_cast<int32_t>(g));
     }
   }
 }
@@ -1077,6 +1111,25 @@ static int render_coop() {
   return v;
 }
 
+// AHV_SP_SINK=staged: the lane renderer's branching arena sink (A/B); default flat.
+static bool sink_flat() {
+  static const bool v = [] {
+    const char* e = std::getenv("AHV_SP_SINK");
+    return e == nullptr || std::string(e) != "staged";
+  }();
+  return v;
+}
+
+using RenderFn = void (*)(StorePipeArgs, const int32_t*, int64_t);
+
+// (Register budgets for 5 / 6 waves per SIMD, __launch_bounds__(256, W), spill the
+// render lane to scratch and ran slower: 1.99 / 2.03 vs 1.93 ms per 1 M-session step;
+// the chain kernel held to 4 / 5 waves: 1.95 / 1.99 ms — profiles/r6/hetero_sink_waves_ab_r6ah.txt.)
+static RenderFn render_fn() {
+  return sink_flat() ? static_cast<RenderFn>(store_pipe_render_kernel<true>)
+                     : static_cast<RenderFn>(store_pipe_render_kernel<false>);
+}
+
 }  // namespace
 
 // Launch the kernels (rows, render, prefix, chain) on `stream` (device) or run the twin (host tables).
@@ -1124,7 +1177,7 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
   if (a.n > 0 && a.render_first) {
     const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
     if (nd > 0)
-      hipLaunchKernelGGL(store_pipe_render_kernel, dim3(pb), dim3(256), 0, st, a, dsess, nd);
+      hipLaunchKernelGGL(render_fn(), dim3(pb), dim3(256), 0, st, a, dsess, nd);
     hipLaunchKernelGGL(store_pipe_prefix_rows_kernel, dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
     hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
   } else if (a.n > 0) {
@@ -1142,11 +1195,11 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
         StorePipeArgs w = a;
         w.wide_only = 1;
         w.prefix_in_render = 0;
-        hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL(render_fn(), dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                            w, dsess, nd);
       }
       if (!cg)
-        hipLaunchKernelGGL(store_pipe_render_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL(render_fn(), dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                            a, dsess, nd);
       if (a.mid && (cg || !a.prefix_in_render))
         hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
