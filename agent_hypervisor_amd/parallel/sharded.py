@@ -152,7 +152,7 @@ _SERVED = (
     "capture", "merkle_root", "vouch", "compute_sigma_eff", "get_total_exposure", "release_session_bonds",
     "slash", "create_saga", "add_step", "execute_step", "compensate", "get_saga",
     "ring_distribution", "list_sagas", "list_vouches", "sso",
-    "agent_liability_owner", "liability_part",
+    "agent_liability_owner", "liability_part", "dir_register",
     "_view", "_view_enter", "_stop",
 )
 
@@ -226,7 +226,8 @@ class ShardedHypervisor:
         self.rpc = None
         self.executors: dict[str, Callable[..., Any]] = {"noop": _noop, "api": _api_executor}
         self.compensators: dict[str, Callable[..., Any]] = {"noop": _noop_comp}
-        self.counters = {"local": 0, "forwarded": 0, "collectives": 0, "views": 0}
+        self.counters = {"local": 0, "forwarded": 0, "collectives": 0, "views": 0, "liability_parts": 0,
+                         "dir_registrations": 0}
         self._rr = 0
         self._sagas: dict[str, str] = {}  # saga id → session id (sagas this rank owns)
         self._vouch_seq = 0
@@ -234,6 +235,11 @@ class ShardedHypervisor:
         self._moved: dict[str, int] = {}  # session / saga id → owner after a migration (same on every rank)
         self._agent_ix: dict[str, list] = {}  # agent DID → its vouch records on this rank (creation order)
         self._agent_ix_n = 0  # records the index covers
+        # P02 owner-resident agent directory: on an agent's owner rank (owner(did)), the
+        # members that hold vouch records naming it — agent_liability asks only those
+        self._agent_dir: dict[str, set] = {}
+        self._dir_sent: set = set()  # agents this rank has registered with their owner
+        self._dir_ok = True  # False: liability views ask every member until the next rebuild
         self._view_lock: Optional[asyncio.Lock] = None
         self._stopped: Optional[asyncio.Event] = None
         self.heartbeat = None
@@ -454,6 +460,7 @@ class ShardedHypervisor:
         self._vouch_seq += 1
         self._vouch_key[v.vouch_id] = (_us(v.created_at), self.rank, self._vouch_seq)
         self._index_vouch(v)
+        await self._dir_note(voucher_did, vouchee_did)
         if emit:  # the REST route's event (reference api/server.py vouch handler)
             from hypervisor.observability.event_bus import EventType
 
@@ -710,10 +717,13 @@ class ShardedHypervisor:
         exposure = Σ live bonds given, summed in that order (bit-exact with one rank).
 
         Owner-routed (P02): the agent's owner rank — a stable hash of its DID over
-        the live ranks — asks every rank for its compact record set (point to point,
-        no collective, no rank-0 sequencing) and combines them.  Each rank answers
-        from its per-agent vouch index (O(the agent's records), never a scan of all
-        vouches) with bond state from one gather of the store's edge columns."""
+        the live ranks — keeps the agent's directory entry (the members holding vouch
+        records that name it, registered once per agent and holding rank by the
+        vouch itself, rebuilt after migration / restore / failover) and asks only
+        those members for their compact record sets (point to point, no collective,
+        no rank-0 sequencing), then combines them.  Each rank answers from its
+        per-agent vouch index (O(the agent's records), never a scan of all vouches)
+        with bond state from one gather of the store's edge columns."""
         self.counters["views"] += 1
         o = self.owner(agent_did)
         if o == self.rank:
@@ -723,10 +733,58 @@ class ShardedHypervisor:
 
     async def _local_agent_liability_owner(self, agent_did: str) -> dict:
         parts = [self._local_liability(agent_did)]
-        others = [r for r in self.members if r != self.rank]
+        if self._dir_ok:  # the members the directory lists (none: the agent has no records elsewhere)
+            others = [r for r in sorted(self._agent_dir.get(agent_did, ())) if r != self.rank and r in self._live]
+        else:
+            others = [r for r in self.members if r != self.rank]
         if others:
+            self.counters["liability_parts"] += len(others)
             parts += await asyncio.gather(*[self.rpc.call(r, "liability_part", agent_did) for r in others])
         return self._combine("agent_liability", (agent_did,), parts)
+
+    # -- P02 agent directory (owner-resident) -----------------------------------------------
+    async def _dir_note(self, *dids: str) -> None:
+        """Register this rank with the owner of each agent the first time it holds a
+        vouch record naming it — awaited, so a liability view issued after the vouch
+        returns finds this rank listed.  One message per (agent, holding rank), not
+        one per view; records that arrive by migration, restore or failover are
+        covered by :meth:`_dir_rebuild`."""
+        if self.world == 1:
+            return
+        for did in dids:
+            if did in self._dir_sent:
+                continue
+            o = self.owner(did)
+            if o == self.rank:
+                self._agent_dir.setdefault(did, set()).add(self.rank)
+            else:
+                self.counters["dir_registrations"] += 1
+                await self.rpc.call(o, "dir_register", did, self.rank)
+            self._dir_sent.add(did)
+
+    async def _local_dir_register(self, did: str, rank: int) -> bool:
+        self._agent_dir.setdefault(did, set()).add(int(rank))
+        return True
+
+    def _dir_rebuild(self) -> None:
+        """Collective over the members: the directory from every member's own records
+        (after records moved between ranks or the owners changed: migration, restore,
+        failover).  Each member sends the agents its records name; each keeps the
+        entries of the agents it owns."""
+        if self.world == 1 or len(self.members) == 1:
+            self._agent_dir, self._dir_sent, self._dir_ok = {}, set(), True
+            return
+        from agent_hypervisor_amd.parallel import migrate as MG
+
+        self._agent_records("")  # refresh the per-agent index
+        mine = sorted(self._agent_ix)
+        allm = MG.all_gather_json(mine, len(self.members), group=self.group)
+        d: dict = {}
+        for r, agents in zip(self.members, allm):
+            for a in agents:
+                if self.owner(a) == self.rank:
+                    d.setdefault(a, set()).add(int(r))
+        self._agent_dir, self._dir_sent, self._dir_ok = d, set(mine), True
 
     async def _local_liability_part(self, agent_did: str) -> list:
         return self._local_liability(agent_did)
@@ -1068,6 +1126,7 @@ class ShardedHypervisor:
         for g in [g for g, sid in self._sagas.items() if sid in moves]:
             del self._sagas[g]
         self._agent_ix_n = -1  # the per-agent vouch index is rebuilt on next use
+        self._dir_rebuild()  # the moved records' holders, at their agents' owners
         self.counters["migrations"] = self.counters.get("migrations", 0) + 1
         return {"sent": len(moves), "received": len(got)}
 
@@ -1113,6 +1172,7 @@ class ShardedHypervisor:
             self._drop_comm()
             self.group = dist.new_group(ranks=self.members, backend="gloo", use_local_synchronization=True)
             self.data_group = dist.new_group(ranks=self.members, use_local_synchronization=True)
+            self._dir_rebuild()  # agents homed on the leaver have new owners
         return out
 
     # -- resilience: heartbeat, checkpoint, failover -----------------------
@@ -1179,6 +1239,7 @@ class ShardedHypervisor:
         self._agent_ix_n = -1
         if self.world > 1:
             dist.barrier(group=self.group)
+        self._dir_rebuild()
         return len(self.local._sessions) - n0
 
     async def failover(self, failed: list[int], root: str) -> list[tuple[str, int, int]]:
@@ -1224,6 +1285,8 @@ class ShardedHypervisor:
         self._drop_comm()
         self.group = dist.new_group(ranks=self.members, backend="gloo", use_local_synchronization=True)
         self.data_group = dist.new_group(ranks=self.members, use_local_synchronization=True)
+        self._agent_ix_n = -1
+        self._dir_rebuild()  # re-homed records and the failed ranks' agents, at their new owners
         self.failovers.append({"failed": failed, "moves": len(moves)})
         return moves
 

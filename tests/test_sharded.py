@@ -362,6 +362,70 @@ def test_failover_rehydrates_dead_rank(tmp_path):
     assert res["new_owner"] in (0, 1) and res["saga_steps"] == 1 and res["root_changed"]
 
 
+def _directory_worker(rank: int, world: int, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), AHV_STORE="host")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from agent_hypervisor_amd.parallel.directory import stable_rank
+        from agent_hypervisor_amd.parallel.sharded import ShardedHypervisor
+        from hypervisor import SessionConfig
+
+        async def main():
+            shv = await ShardedHypervisor(device="host").start()
+            if rank != 0:
+                await shv.serve_forever()
+                return None
+            # agents owned by rank 0 (their stable home): the views' fan-out is counted here
+            x, y, z = [d for d in (f"did:dir-{k}" for k in range(400)) if stable_rank(d, world) == 0][:3]
+            s1 = await shv.create_session(SessionConfig(), "did:admin", rank=1)
+            s2 = await shv.create_session(SessionConfig(), "did:admin", rank=2)
+            await shv.vouch(x, y, s1, 0.9)  # records naming x and y on rank 1
+            await shv.vouch(x, "did:w", s2, 0.8)  # and x on rank 2
+            parts = []
+            lia = {}
+            for a in (x, y, z):
+                c0 = shv.counters["liability_parts"]
+                lia[a] = await shv.agent_liability(a)
+                parts.append(shv.counters["liability_parts"] - c0)
+            res = dict(parts=parts, given=len(lia[x]["vouches_given"]), received=len(lia[y]["vouches_received"]),
+                       empty=not lia[z]["vouches_given"] and not lia[z]["vouches_received"],
+                       exposure=lia[x]["total_exposure"])
+            await shv.shutdown()
+            return res
+
+        res = asyncio.run(main())
+        if rank == 0:
+            q.put(res)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def test_liability_view_asks_only_the_ranks_holding_records():
+    """P02: an agent's owner keeps the members that hold vouch records naming it
+    (registered once per agent and holding rank, awaited inside the vouch), so
+    ``agent_liability`` sends one part request per holding rank — counted, not
+    timed: 2, 1 and 0 requests on 4 ranks where asking everyone costs 3 each."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_directory_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    try:
+        res = q.get(timeout=120)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert res["parts"] == [2, 1, 0]
+    assert res["given"] == 2 and res["received"] == 1 and res["empty"] and res["exposure"] > 0
+
+
 def _abort_worker(rank: int, world: int, root: str, q) -> None:
     """Rank 2 dies while every rank sits in a ``hold`` view's collective; the
     survivors fail over and their next views complete."""
