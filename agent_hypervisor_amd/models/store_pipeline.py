@@ -49,10 +49,13 @@ _SP_PREFIX_IN_RENDER = 0 if _SP_PREFIX in ("kernel", "sorted") else 1
 # 18 µs per 10^6 sessions (render 707 -> 689 µs, profiles/r6/hetero_frags_r6s.jsonl)
 # but the host pass costs ≈ 0.4 µs per delta in prepare, which the public API times
 _SP_FRAGS = _os.environ.get("AHV_SP_FRAGS", "0") != "0"
-# render before the rows pass, whose blocks then share one launch with the prefix SHA
-# blocks (store_pipe_prefix_rows_kernel: memory-bound rows waves beside VALU-bound
-# SHA waves); AHV_SP_OVERLAP=0: rows, render, prefix as three passes
-_SP_OVERLAP = _os.environ.get("AHV_SP_OVERLAP", "1") != "0"
+# the rows pass's blocks share one launch with the render pass's (both wait on memory
+# most of the time: store_pipe_render_rows_kernel), the prefix SHA pass on its own
+# (render + rows 775 µs, prefix 486 per 10^6 sessions: 1.91 vs 1.95 ms per step,
+# profiles/r6/hetero_rows_layout_ab_r6an.txt); AHV_SP_OVERLAP=1: the rows blocks share
+# the prefix pass's launch instead (store_pipe_prefix_rows_kernel); 0: rows, render,
+# prefix as three passes
+_SP_OVERLAP = int(_os.environ.get("AHV_SP_OVERLAP", "2"))
 # the committed chains' Merkle roots (K09) folded in the chain kernel's lanes as the
 # digests are produced; AHV_SP_CHAIN_ROOTS=0: the K09 kernel afterwards (_k09_plan)
 _SP_CHAIN_ROOTS = _os.environ.get("AHV_SP_CHAIN_ROOTS", "1") != "0" and _SP_PREFIX != "chain"
@@ -360,16 +363,18 @@ class Prepared:
     host-side metadata :func:`finish` needs.  :func:`launch` runs it; a benchmark
     may re-run the same batch after :meth:`reset` (the rows freed in place)."""
 
-    def reset(self) -> None:
-        """Free the batch's session / saga / step rows in place (on the stream), so
-        :func:`launch` can run the whole pipeline over them again."""
+    def reset(self, all_rows: bool = False) -> None:
+        """Free the batch's session rows in place (on the stream), so :func:`launch`
+        can run the whole pipeline over them again.  Its saga and step rows stay
+        allocated to it — the rows pass writes them whole without a free-row check —
+        unless ``all_rows`` frees them too."""
         t = self.store.tables
         ixs = self.__dict__.get("_reset_ix")
         if ixs is None:  # int64 row indices, converted once
             ixs = self.__dict__["_reset_ix"] = [
                 (col, ix.to(torch.int64)) for col, ix in (("s_state", self.tens["slot"]), ("g_state", self.g_live),
                                                           ("t_state", self.t_live)) if ix is not None and ix.numel()]
-        for col, ix in ixs:
+        for col, ix in (ixs if all_rows else ixs[:1]):
             t[col].index_fill_(0, ix, 255)  # kFree8
         self.tens["status"].zero_()  # the kernels write only codes other than ok over a zeroed array
 
@@ -557,7 +562,7 @@ def prepare(hv, specs, n: Optional[int] = None) -> "Prepared":
         tens["mid"] = torch.empty((max(1, nd), 8), dtype=torch.int32, device=dev)
         tens["mid_blocks"] = torch.zeros(max(1, nd), dtype=torch.int32, device=dev)
     args = {k: v.data_ptr() for k, v in tens.items()}
-    args.update(prefix_in_render=_SP_PREFIX_IN_RENDER, render_first=int(_SP_OVERLAP),
+    args.update(prefix_in_render=_SP_PREFIX_IN_RENDER, render_first=_SP_OVERLAP,
                 chain_roots=int(_SP_CHAIN_ROOTS),
                 max_nch=int(np.diff(np.asarray(ch_off_all, dtype=np.int64)).max()) if nd else 0)
     args.update(n=n, nd=nd, gc_retention_us=int(hv.gc.policy.delta_retention_days) * 86_400 * 1_000_000)

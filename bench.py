@@ -370,9 +370,10 @@ def main() -> None:
     hetero = None
     if args.mix == "hetero":
         # The public batched API's kernels over the device store (Hypervisor.run_pipelines):
-        # the batch is packed once (host), then every step frees its rows in place and
-        # runs the whole pipeline over them again (create, joins, activate, rendered
-        # and SHA-chained deltas, sagas with retries/compensation, terminate, K09 roots).
+        # the batch is packed once (host), then every step frees its session rows in place
+        # and runs the whole pipeline over them again (create, joins, activate, rendered
+        # and SHA-chained deltas, sagas with retries/compensation rewritten whole in the
+        # batch's saga / step rows, terminate, Merkle roots).
         from agent_hypervisor_amd.models import store_pipeline as SP
         from hypervisor import Hypervisor
 
@@ -419,7 +420,9 @@ def main() -> None:
             with torch.cuda.stream(side):
                 liability_step()
         st.zero_()
-        agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g)
+        # (the heterogeneous batch carries its own agents in its specs)
+        agents = torch.randint(0, args.agents, (S,), device=dev, dtype=torch.int32, generator=g) \
+            if hetero is None else None
         run_batch(st, agents)
         works[b] = dist.all_reduce(st, op=dist.ReduceOp.SUM, async_op=True) if multi else None
         if side is not None:

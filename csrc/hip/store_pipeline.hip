@@ -9,28 +9,30 @@
 // device session of the public API (views, reads, verify, terminate all work on
 // it), unlike the standalone engine tables of models/engine.py.
 //
-// Three launches (render_first, the default), all over rows the host allocator
+// Three launches (render_first = 2, the default), all over rows the host allocator
 // handed out (free rows; a row that is not free is refused and reported, never
 // overwritten):
 //
-//   store_pipe_render_kernel       lane per delta: the canonical-JSON record (the
-//                                  shared emitters of ahv/delta_emit.h) written into
-//                                  the payload arena, parent digest left as a hole
-//   store_pipe_prefix_rows_kernel  two kinds of block, interleaved:
+//   store_pipe_render_rows_kernel  two kinds of block, interleaved:
+//     render  lane per delta: the canonical-JSON record (the shared emitters of
+//             ahv/delta_emit.h) written into the payload arena, parent digest left
+//             as a hole; the lane checks its session row itself
 //     rows    lane per session: create (+ handshake), joins through the K01 ring
 //             gate and join admission, activate, saga/step FSM (K13) with retries
 //             and compensation (K14), terminate → commit → GC → archive
 //             bookkeeping, chain links of its delta rows
-//     prefix  lane per delta: SHA-256 of the record's blocks before the parent
-//             hole (all of a turn-1 record)
+//   store_pipe_prefix_kernel       lane per delta: SHA-256 of the record's blocks
+//                                  before the parent hole (all of a turn-1 record)
 //   store_pipe_chain_kernel        lane per session: the serial SHA-256 chain (K08):
 //                                  each record's parent hole filled with the previous
 //                                  digest, then compressed from the prefix midstate;
 //                                  digests and chain head; then the Merkle root (K09)
 //                                  of a committed chain into s_root (chain_roots)
 //
-// (render_first = 0: rows, render, prefix as passes of their own; chain_roots = 0:
-// the K09 kernel reads the resident digests afterwards — store_pipeline.py.)
+// (render_first = 1: render alone, then store_pipe_prefix_rows_kernel — the rows blocks
+// beside the prefix SHA blocks; render_first = 0: rows, render, prefix as passes of their
+// own; chain_roots = 0: the K09 kernel reads the resident digests afterwards —
+// store_pipeline.py.)
 // Lanes take records / sessions in descending-work order (render_order,
 // chain_order) so a wave's lanes finish together.
 #include <hip/hip_runtime.h>
@@ -100,7 +102,9 @@ struct StorePipeArgs {
   const int64_t* frag_off;      // [F]
   const int32_t* frag_len;      // [F]
   // 1: render before rows (the render lane checks its session row itself), rows
-  // blocks interleaved with the prefix SHA blocks in one launch (store_pipe_prefix_rows_kernel)
+  // blocks interleaved with the prefix SHA blocks in one launch (store_pipe_prefix_rows_kernel);
+  // 2: rows blocks interleaved with the render blocks instead (store_pipe_render_rows_kernel),
+  // the prefix pass on its own
   int32_t render_first;
   // 1: the chain lane folds its session's digests into the Merkle root (K09) as it
   // produces them and writes s_root of a committed row (needs `mid`: its scratch)
@@ -285,7 +289,15 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
   t.s_state[s] = st;
   // a record that overflowed its reservation outranks the other stages' codes
   // (render ran first: its SP_RENDER is already in status)
-  if (!a.render_first || a.status[i] != SP_RENDER) a.status[i] = status;
+  if (a.render_first == 2) {  // the render pass runs beside this one: the larger code wins (SP_RENDER)
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicMax(&a.status[i], status);
+#else
+    a.status[i] = a.status[i] > status ? a.status[i] : status;
+#endif
+  } else if (!a.render_first || a.status[i] != SP_RENDER) {
+    a.status[i] = status;
+  }
 }
 
 // The render-first layout: the session row is free for this batch (the rows pass
@@ -717,6 +729,27 @@ __global__ __launch_bounds__(256) void store_pipe_prefix_rows_kernel(StorePipeAr
   }
 }
 
+// render_first = 2: the rows blocks interleaved with the render blocks (both wait on
+// memory most of the time: rows on its scattered row writes, render on its string loads).
+// Status codes meet through atomicMax (SP_RENDER, the largest, wins).
+__global__ __launch_bounds__(256) void store_pipe_render_rows_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd,
+                                                                     uint32_t nrows_blk, uint32_t nblk) {
+  const uint64_t b = blockIdx.x;
+  const uint64_t r0 = b * nrows_blk / nblk, r1 = (b + 1) * nrows_blk / nblk;
+  if (r1 > r0) {
+    const int64_t i = static_cast<int64_t>(r0) * blockDim.x + threadIdx.x;
+    if (i < a.n) sp_rows(a, i);
+    return;
+  }
+  const int64_t x = static_cast<int64_t>(b - r0) * blockDim.x + threadIdx.x;
+  if (x < nd) {
+    const int64_t g = a.render_order ? a.render_order[x] : x;
+    const int64_t i = dsess[g];
+    if (sp_row_in_use(a, i)) a.status[i] = SP_ROW_IN_USE;
+    else sp_render<true>(a, i, static_cast<int32_t>(g));
+  }
+}
+
 // A lane's chain is serial and its length varies per session (0..k deltas of
 // varying size): lanes take sessions in descending-work order (chain_order), so
 // the 64 chains of a wave are about equally long and the wave does not idle most
@@ -1086,8 +1119,9 @@ StorePipeArgs to_args(const Tables& t, const py::dict& d) {
   a.max_nch = d.contains("max_nch") ? d["max_nch"].cast<int32_t>() : 1 << 30;
   a.wide_only = 0;
   // only with the prefix pass of its own and the lane renderer (the layout it reorders)
-  a.render_first = d.contains("render_first") && d["render_first"].cast<int32_t>() != 0 && a.mid != nullptr &&
-                   !a.prefix_in_render;
+  a.render_first = d.contains("render_first") && a.mid != nullptr && !a.prefix_in_render
+                       ? d["render_first"].cast<int32_t>()
+                       : 0;
   a.chain_roots = d.contains("chain_roots") && d["chain_roots"].cast<int32_t>() != 0 && a.mid != nullptr;
   if (d.contains("dfrag")) {
     a.dfrag = P<const int32_t>(d, "dfrag");
@@ -1174,7 +1208,12 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   py::gil_scoped_release nogil;
-  if (a.n > 0 && a.render_first) {
+  if (a.n > 0 && a.render_first == 2) {
+    const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
+    hipLaunchKernelGGL(store_pipe_render_rows_kernel, dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
+    if (nd > 0) hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(pb), dim3(256), 0, st, a, dsess, nd);
+    hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
+  } else if (a.n > 0 && a.render_first) {
     const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
     if (nd > 0)
       hipLaunchKernelGGL(render_fn(), dim3(pb), dim3(256), 0, st, a, dsess, nd);

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 6, call an: rows blocks beside the render pass (AHV_SP_OVERLAP=2) vs beside the
+# prefix SHA pass (1, default) — batch GPU tests, interleaved hetero A/B, kernel stats
+# (also the first runs with the trimmed bench plumbing: session rows only freed per step).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp AHV_SKIP_AUTOBUILD=1
+OUT=gpurun_out/r6an
+mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests/test_store_pipeline.py tests/test_gpu_pipeline.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/tests.txt 2>&1; rc=$?
+tail -2 $OUT/tests.txt; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2; do
+  for ov in 1 2; do
+    for S in 1048576 4194304; do
+      AHV_SP_OVERLAP=$ov timeout -k 10 300 python bench.py --mix hetero --no-scalar --no-api --sessions $S --steps 20 --warmup 3 \
+        > $OUT/h_o${ov}_${S}_$rep.json 2>$OUT/h_o${ov}_${S}_$rep.err || exit $?
+      echo "rep=$rep overlap=$ov S=$S $(tail -1 $OUT/h_o${ov}_${S}_$rep.json | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+    done
+  done
+done
+for ov in 1 2; do
+  AHV_SP_OVERLAP=$ov timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof$ov -o run --output-format csv -- python bench.py --mix hetero \
+    --no-scalar --no-api --sessions 1048576 --steps 5 --warmup 1 > $OUT/prof$ov.log 2>&1 || exit $?
+  f=$(find $OUT/prof$ov -name "*kernel_stats.csv" | head -1); cp "$f" $OUT/kernel_stats_o$ov.csv
+done

@@ -179,13 +179,14 @@ def test_randomized_batch_equals_scalar_api_gpu():
     {"AHV_SP_PREFIX": "render", "AHV_SP_ORDER": "1"},
     {"AHV_SP_ORDER": "7"},
     {"AHV_SP_OVERLAP": "0"},
+    {"AHV_SP_OVERLAP": "1"},
     {"AHV_SP_CHAIN_ROOTS": "0"},
     {"AHV_SP_SINK": "staged"},
 ])
 def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
     """The A/B layouts of the batch kernels (cooperative renderer with 16 / 4 lanes per
     record, prefix SHA inside the render pass, render lanes by record shape, rows before
-    render in a pass of their own, Merkle roots by the K09 kernel, the branching arena
+    render in a pass of their own, rows beside the prefix pass, Merkle roots by the K09 kernel, the branching arena
     sink) produce the same records, digests and roots as the scalar API (a fresh process each: the
     switches are read once)."""
     import os
@@ -200,7 +201,7 @@ def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
     assert r.returncode == 0, r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("render_first", [0, 1])
+@pytest.mark.parametrize("render_first", [0, 1, 2])
 def test_status_codes_and_precedence_in_both_kernel_orders(render_first):
     """Rows pass first, or the render pass first with the rows pass beside the prefix
     SHA pass (render_first): a row the store holds is refused whole (row_in_use), a
