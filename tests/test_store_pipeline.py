@@ -186,9 +186,9 @@ def test_randomized_batch_equals_scalar_api_gpu():
 def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
     """The A/B layouts of the batch kernels (cooperative renderer with 16 / 4 lanes per
     record, prefix SHA inside the render pass, render lanes by record shape, rows before
-    render in a pass of their own, rows beside the prefix pass, Merkle roots by the K09 kernel, the branching arena
-    sink) produce the same records, digests and roots as the scalar API (a fresh process each: the
-    switches are read once)."""
+    render in a pass of their own, rows beside the prefix pass, Merkle roots by the K09
+    kernel, the branching arena sink) produce the same records, digests and roots as the
+    scalar API (a fresh process each: the switches are read once)."""
     import os
     import subprocess
     import sys
