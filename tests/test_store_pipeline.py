@@ -201,36 +201,49 @@ def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
     assert r.returncode == 0, r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("render_first", [0, 1, 2])
-def test_status_codes_and_precedence_in_both_kernel_orders(render_first):
-    """Rows pass first, or the render pass first with the rows pass beside the prefix
-    SHA pass (render_first): a row the store holds is refused whole (row_in_use), a
-    record past its reservation reports record_overflow — over a refused join too —
-    and the other sessions of the batch run through (CPU twin of the device order)."""
+def check_status_precedence(device: str, render_first: int) -> None:
     import numpy as np
 
     from agent_hypervisor_amd.models import store_pipeline as SP
 
-    st = GovernanceStore("cpu", caps={"S": 64, "D": 256, "G": 64, "T": 64})
+    st = GovernanceStore(device, caps={"S": 64, "D": 256, "G": 64, "T": 64})
     hv = Hypervisor(store=st)
     dup = (("did:mesh:a", 0.9), ("did:mesh:a", 0.9))  # the second join is a duplicate: join_refused
     specs = [PipelineSpec(), PipelineSpec(), PipelineSpec(joins=dup), PipelineSpec(), PipelineSpec(joins=dup)]
     p = SP.prepare(hv, specs)
     p.args["render_first"] = render_first
+    p.args["chain_roots"] = int(render_first != 0)
     s_state = st.tables["s_state"]
     s_state[int(p.slots[1])] = 1  # held by someone else
     dcap = p.tens["dcap"]
     d_off = list(p.delta_off)
     for i in (2, 3):  # the session's last record gets one 64-byte line: it overflows
         dcap[d_off[i + 1] - 1] = 64
-    st._c.run_pipeline(p.args, 0)
+    SP.launch(p)
     status = p.tens["status"].cpu().numpy()
     assert status.tolist() == [0, 1, 6, 6, 2]
     assert int(s_state[int(p.slots[1])]) == 1  # not written
     mb = p.tens["mid_blocks"].cpu().numpy()
     assert not mb[d_off[1]:d_off[2]].any()  # the refused row's records were not hashed
     assert mb[d_off[0]:d_off[1]].all() and np.asarray(mb[d_off[4]:d_off[5]]).all()
+    del hv, p
     st.close()
+
+
+@pytest.mark.parametrize("render_first", [0, 1, 2])
+def test_status_codes_and_precedence_in_every_kernel_order(render_first):
+    """Rows pass first (0), the rows blocks beside the prefix SHA pass (1) or beside the
+    render pass (2, default: codes meet through atomicMax): a row the store holds is
+    refused whole (row_in_use), a record past its reservation reports record_overflow —
+    over a refused join too — and the other sessions of the batch run through (CPU twin
+    of the device order)."""
+    check_status_precedence("cpu", render_first)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("render_first", [0, 1, 2])
+def test_status_codes_and_precedence_in_every_kernel_order_gpu(render_first):
+    check_status_precedence("cuda", render_first)
 
 
 def test_lazy_rows_released_in_bulk_and_materialized_rows_kept(monkeypatch):
