@@ -449,6 +449,9 @@ def _storm(ctx: Ctx, args, frac: float, rechain_all: bool, release_all: bool):
     # is made up front (setup, outside the timed region: ~170 MB each).
     runs = args.warmup + max(3, min(10, args.steps)) + args.steps
     fresh = [(vb0.active.clone(), vb0.released_us.clone(), scores0.clone()) for _ in range(runs)]
+    # K07 (memory bound: the bond columns) on a side stream beside the re-chain's SHA
+    # passes (VALU bound), which read nothing it writes; --serial-release: in line
+    side = torch.cuda.Stream(ctx.dev) if ctx.dev.type == "cuda" and release_all and not args.serial_release else None
 
     def step():
         active, released, scores = fresh.pop()
@@ -457,11 +460,15 @@ def _storm(ctx: Ctx, args, frac: float, rechain_all: bool, release_all: bool):
         out = LI.slash(vb, tgt, omega, scores, 1, clip_cap=per, zero_records=False, with_sigma_eff=not args.unfused,
                        with_touched=not rechain_all)
         se = out.sigma_eff if not args.unfused else LI.sigma_eff_exact(vb, out.scores, omega, 1)
-        if release_all:  # K07: the storm's sessions end — every bond still active is released
+        rel = None
+        if release_all and side is not None:  # K07: the storm's sessions end — every bond still active is released
+            side.wait_stream(torch.cuda.current_stream(ctx.dev))  # after the slash's clips
+            with torch.cuda.stream(side):
+                rel = LI.release_bonds(vb, 2)
+        elif release_all:
             rel = LI.release_bonds(vb, 2)
         else:
             rel = torch.zeros(1, dtype=i32, device=ctx.dev)
-        last["counts"] = storm_counts(out, rel)
         # re-chain after the slash (data dependency): each session gets a slash delta
         # carrying its post-slash scores, then its whole chain is re-hashed (K08) and
         # its Merkle root recomputed (K09) — every session, or (subset storm) the ones
@@ -471,6 +478,10 @@ def _storm(ctx: Ctx, args, frac: float, rechain_all: bool, release_all: bool):
         packed, sel = arena.resident(touched)
         digests = A.chain_hashes(packed, midstate=not args.no_midstate, uniform_len=D + 1, sel=sel, check=False)
         roots = A.merkle_roots(packed["chain_offsets"], digests)
+        if side is not None:  # the release joins before the storm ends
+            torch.cuda.current_stream(ctx.dev).wait_stream(side)
+            rel.record_stream(torch.cuda.current_stream(ctx.dev))
+        last["counts"] = storm_counts(out, rel)
         last.update(T=touched.numel(), roots=roots)
         return se
 
@@ -496,6 +507,7 @@ def _storm(ctx: Ctx, args, frac: float, rechain_all: bool, release_all: bool):
              bond_updates_by_release=by_release, sessions_rechained=T, deltas_rechained=T * (D + 1),
              arena_bytes_resident=int(arena.bytes.numel()), distinct_payloads=True,
              state_reset="one pre-made copy of (active, released_us, scores) per storm, made before timing",
+             release_stream="side (beside the re-chain)" if side is not None else "main",
              hbm_bytes_est=dict(slash_sigma=slash_bytes, release=release_bytes, rechain=rechain_bytes, total=hbm),
              hbm_roofline_ms=round(hbm / 8.0e12 * 1e3, 4), hbm_achieved_tb_s=round(hbm / (ms * 1e-3) / 1e12, 3),
              sha_compressions_est=T * blocks_per_chain,
@@ -553,6 +565,8 @@ def main():
     ap.add_argument("--unfused-graph", action="store_true",
                     help="config2: separate zero/clock/fold/advance graph nodes instead of the fused epilogue (A/B)")
     ap.add_argument("--no-midstate", action="store_true", help="config5: single-phase K08 re-chain (A/B)")
+    ap.add_argument("--serial-release", action="store_true",
+                    help="config5: K07 in line on the main stream, not beside the re-chain (A/B)")
     ap.add_argument("--tiles", action="store_true", help="config3: round-1 build_tiles + bond_tiles pair")
     ap.add_argument("--allreduce-exposure", action="store_true",
                     help="config3: all-reduce the full exposure vector on every rank instead of the default "
