@@ -474,12 +474,33 @@ AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t 
 
 AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g);
 
-template <bool kFlat = true>
+// A pool string's (pointer, length) with unconditional loads (an absent string, id −1,
+// reads entry 0 — a record's agent DID is always in the pool — and reports length −1).
+AHV_HD StrRef pool_ref_flat(const StrPool& pool, int32_t id) {
+  const int32_t j = id < 0 ? 0 : id;
+  const int64_t off = pool.off[j];
+  const int32_t len = pool.len[j];
+  return StrRef{pool.bytes + off, id < 0 ? -1 : len};
+}
+
+// kHoist: the loads whose values are needed only later — the session id words, the
+// base time, the agent DID's pool entry, each change's four pool entries and the next
+// change's ids — are issued ahead of the stores that precede their use, so the lane does
+// not wait for a load after every string it emits (AHV_SP_HOIST=0: in line).
+template <bool kFlat = true, bool kHoist = true>
 AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   const Tables& t = a.t;
   const int32_t k = g - a.delta_off[i];
   const int32_t d = a.drow[g];
   const int64_t s = a.slot[i];
+  uint32_t uw[4] = {0, 0, 0, 0};
+  int64_t ts = 0;
+  StrRef agent{nullptr, -1};
+  if (kHoist) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) uw[q] = a.uuid[4 * i + q];
+    ts = sp_delta_ts(a, i, k);
+  }
   ArenaSinkT<kFlat> snk;
   snk.dst = reinterpret_cast<uint32_t*>(t.payload + a.doff[g]);
   snk.cap_w = static_cast<uint32_t>(a.dcap[g]) / 4;
@@ -510,6 +531,29 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
         snk.nb = nb;
       }
     }
+  } else if (kHoist) {
+    agent = pool_ref_flat(a.pool, a.dagent_pool[g]);
+    ChangeIds nx = nch > 0 ? ch[0] : ChangeIds{-1, -1, -1, -1};
+    emit_lit(snk, canon::K_OPEN_AGENT);
+    emit_str_ref(snk, agent);
+    emit_lit(snk, canon::K_CHANGES);
+    for (uint32_t c = 0; c < nch; ++c) {
+      const StrRef rc = pool_ref_flat(a.pool, nx.content_hash), ro = pool_ref_flat(a.pool, nx.op);
+      const StrRef rp = pool_ref_flat(a.pool, nx.path), rv = pool_ref_flat(a.pool, nx.previous_hash);
+      if (c + 1 < nch) nx = ch[c + 1];
+      if (c) emit_lit(snk, canon::K_CH_SEP);
+      emit_lit(snk, canon::K_CH_OPEN);
+      emit_str_ref(snk, rc);
+      emit_lit(snk, canon::K_CH_OP);
+      emit_str_ref(snk, ro);
+      emit_lit(snk, canon::K_CH_PATH);
+      emit_str_ref(snk, rp);
+      emit_lit(snk, canon::K_CH_PREV);
+      emit_str_ref(snk, rv);
+      emit_lit(snk, canon::K_CH_CLOSE);
+    }
+    emit_lit(snk, canon::K_DELTA_ID);
+    emit_lit(snk, canon::K_DELTA_PFX);
   } else {
     emit_lit(snk, canon::K_OPEN_AGENT);
     emit_str_ref(snk, pool_ref(a.pool, a.dagent_pool[g]));
@@ -541,9 +585,9 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
     emit_lit(snk, canon::K_NULL);
   }
   emit_lit(snk, canon::K_SESSION);
-  emit_session_uuid_quoted(snk, a.uuid + 4 * i);
+  emit_session_uuid_quoted(snk, kHoist ? uw : a.uuid + 4 * i);
   emit_lit(snk, canon::K_TS);
-  emit_iso_quoted(snk, sp_delta_ts(a, i, k));
+  emit_iso_quoted(snk, kHoist ? ts : sp_delta_ts(a, i, k));
   emit_lit(snk, canon::K_TURN);
   emit_uint(snk, turn);
   emit_lit(snk, canon::K_CLOSE);
@@ -689,7 +733,7 @@ __global__ __launch_bounds__(256) void store_pipe_prefix_kernel(StorePipeArgs a,
 }
 
 // lane per delta; `dsess` maps a delta to its session
-template <bool kFlat>
+template <bool kFlat, bool kHoist>
 __global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd) {
   const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (x < nd) {
@@ -697,9 +741,9 @@ __global__ __launch_bounds__(256) void store_pipe_render_kernel(StorePipeArgs a,
     const int64_t i = dsess[g];
     if (a.render_first) {
       if (sp_row_in_use(a, i)) a.status[i] = SP_ROW_IN_USE;  // (every lane of the session writes the same)
-      else sp_render<kFlat>(a, i, static_cast<int32_t>(g));
+      else sp_render<kFlat, kHoist>(a, i, static_cast<int32_t>(g));
     } else if (a.status[i] != SP_ROW_IN_USE && (!a.wide_only || a.dch_off[g + 1] - a.dch_off[g] > 4)) {
-      sp_render<kFlat>(a, i, static_cast<int32_t>(g));
+      sp_render<kFlat, kHoist>(a, i, static_cast<int32_t>(g));
     }
   }
 }
@@ -732,6 +776,7 @@ __global__ __launch_bounds__(256) void store_pipe_prefix_rows_kernel(StorePipeAr
 // render_first = 2: the rows blocks interleaved with the render blocks (both wait on
 // memory most of the time: rows on its scattered row writes, render on its string loads).
 // Status codes meet through atomicMax (SP_RENDER, the largest, wins).
+template <bool kHoist>
 __global__ __launch_bounds__(256) void store_pipe_render_rows_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd,
                                                                      uint32_t nrows_blk, uint32_t nblk) {
   const uint64_t b = blockIdx.x;
@@ -746,7 +791,7 @@ __global__ __launch_bounds__(256) void store_pipe_render_rows_kernel(StorePipeAr
     const int64_t g = a.render_order ? a.render_order[x] : x;
     const int64_t i = dsess[g];
     if (sp_row_in_use(a, i)) a.status[i] = SP_ROW_IN_USE;
-    else sp_render<true>(a, i, static_cast<int32_t>(g));
+    else sp_render<true, kHoist>(a, i, static_cast<int32_t>(g));
   }
 }
 
@@ -1159,9 +1204,25 @@ using RenderFn = void (*)(StorePipeArgs, const int32_t*, int64_t);
 // (Register budgets for 5 / 6 waves per SIMD, __launch_bounds__(256, W), spill the
 // render lane to scratch and ran slower: 1.99 / 2.03 vs 1.93 ms per 1 M-session step;
 // the chain kernel held to 4 / 5 waves: 1.95 / 1.99 ms — profiles/r6/hetero_sink_waves_ab_r6ah.txt.)
+static bool hoist() {
+  static const bool v = [] {
+    const char* e = std::getenv("AHV_SP_HOIST");
+    return e == nullptr || std::string(e) != "0";
+  }();
+  return v;
+}
+
 static RenderFn render_fn() {
-  return sink_flat() ? static_cast<RenderFn>(store_pipe_render_kernel<true>)
-                     : static_cast<RenderFn>(store_pipe_render_kernel<false>);
+  if (!sink_flat()) return static_cast<RenderFn>(store_pipe_render_kernel<false, false>);
+  return hoist() ? static_cast<RenderFn>(store_pipe_render_kernel<true, true>)
+                 : static_cast<RenderFn>(store_pipe_render_kernel<true, false>);
+}
+
+using RowsFn = void (*)(StorePipeArgs, const int32_t*, int64_t, uint32_t, uint32_t);
+
+static RowsFn render_rows_fn() {
+  return hoist() ? static_cast<RowsFn>(store_pipe_render_rows_kernel<true>)
+                 : static_cast<RowsFn>(store_pipe_render_rows_kernel<false>);
 }
 
 }  // namespace
@@ -1210,7 +1271,7 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
   py::gil_scoped_release nogil;
   if (a.n > 0 && a.render_first == 2) {
     const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
-    hipLaunchKernelGGL(store_pipe_render_rows_kernel, dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
+    hipLaunchKernelGGL(render_rows_fn(), dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
     if (nd > 0) hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(pb), dim3(256), 0, st, a, dsess, nd);
     hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
   } else if (a.n > 0 && a.render_first) {
