@@ -1204,6 +1204,8 @@ using RenderFn = void (*)(StorePipeArgs, const int32_t*, int64_t);
 // (Register budgets for 5 / 6 waves per SIMD, __launch_bounds__(256, W), spill the
 // render lane to scratch and ran slower: 1.99 / 2.03 vs 1.93 ms per 1 M-session step;
 // the chain kernel held to 4 / 5 waves: 1.95 / 1.99 ms — profiles/r6/hetero_sink_waves_ab_r6ah.txt.)
+// AHV_SP_HOIST=0: the render lanes' loads in line (A/B).  (Also loading each string's first
+// 16-byte chunk ahead measured no better: profiles/r6/hetero_hoist_levels_ab_r6ay.txt.)
 static bool hoist() {
   static const bool v = [] {
     const char* e = std::getenv("AHV_SP_HOIST");
