@@ -618,7 +618,11 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
 // parallel over records, and the serial chain pass resumes from this state.
 // Kept out of the render pass: the SHA rounds are uniform control flow, the
 // rendering is not (its lanes diverge on string lengths and field kinds).
-AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g) {
+// kPipe: block b+1's four 16-byte loads are issued before block b is compressed, so a
+// lane's next block is in flight while it runs 64 rounds (the prefix blocks lie wholly
+// inside the record: no padding to apply).  AHV_SP_PREFIX_PIPE=0: load, then compress.
+template <bool kPipe>
+AHV_HD void sp_prefix_t(const StorePipeArgs& a, int64_t g) {
   const Tables& t = a.t;
   const int32_t d = a.drow[g];
   const uint32_t len = static_cast<uint32_t>(t.d_len[d]);
@@ -632,15 +636,42 @@ AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g) {
   uint32_t h[8];
   sha256_init(h);
   const uint32_t* w32 = reinterpret_cast<const uint32_t*>(t.payload + a.doff[g]);
-  for (uint64_t b = 0; b < pb; ++b) {
-    uint32_t blk[16];
-    sp_block(w32, len, nblk, b, blk);
-    sha256_compress(h, blk);
+  if (kPipe && hole >= 0) {
+    const U4* src = reinterpret_cast<const U4*>(w32);
+    U4 n0{0u, 0u, 0u, 0u}, n1 = n0, n2 = n0, n3 = n0;
+    if (pb > 0) {
+      n0 = src[0];
+      n1 = src[1];
+      n2 = src[2];
+      n3 = src[3];
+    }
+    for (uint64_t b = 0; b < pb; ++b) {
+      const U4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+      if (b + 1 < pb) {
+        n0 = src[4 * (b + 1)];
+        n1 = src[4 * (b + 1) + 1];
+        n2 = src[4 * (b + 1) + 2];
+        n3 = src[4 * (b + 1) + 3];
+      }
+      const uint32_t blk[16] = {bswap32(c0.a), bswap32(c0.b), bswap32(c0.c), bswap32(c0.d),
+                                bswap32(c1.a), bswap32(c1.b), bswap32(c1.c), bswap32(c1.d),
+                                bswap32(c2.a), bswap32(c2.b), bswap32(c2.c), bswap32(c2.d),
+                                bswap32(c3.a), bswap32(c3.b), bswap32(c3.c), bswap32(c3.d)};
+      sha256_compress(h, blk);
+    }
+  } else {
+    for (uint64_t b = 0; b < pb; ++b) {
+      uint32_t blk[16];
+      sp_block(w32, len, nblk, b, blk);
+      sha256_compress(h, blk);
+    }
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) a.mid[8 * g + k] = h[k];
   a.mid_blocks[g] = static_cast<int32_t>(pb);
 }
+
+AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g) { sp_prefix_t<true>(a, g); }
 
 // Lane per session: the SHA-256 chain over its records (K08).
 AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
@@ -729,13 +760,14 @@ __global__ __launch_bounds__(256) void store_pipe_rows_kernel(StorePipeArgs a) {
 }
 
 // lane per record (records in render_order: similar sizes per wave)
+template <bool kPipe>
 __global__ __launch_bounds__(256) void store_pipe_prefix_kernel(StorePipeArgs a, const int32_t* dsess, int64_t nd) {
   const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (x < nd) {
     // lanes of a wave hash records with the same number of parent-independent blocks
     // (prefix_order: turn-1 records, whole record, first, then by reserved size)
     const int64_t g = a.prefix_order ? a.prefix_order[x] : a.render_order ? a.render_order[x] : x;
-    if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix(a, g);
+    if (a.status[dsess[g]] != SP_ROW_IN_USE) sp_prefix_t<kPipe>(a, g);
     else a.mid_blocks[g] = 0;
   }
 }
@@ -1228,6 +1260,15 @@ static RenderFn render_fn() {
                  : static_cast<RenderFn>(store_pipe_render_kernel<true, false>);
 }
 
+static RenderFn prefix_fn() {
+  static const RenderFn f = [] {
+    const char* e = std::getenv("AHV_SP_PREFIX_PIPE");
+    return (e != nullptr && std::string(e) == "0") ? static_cast<RenderFn>(store_pipe_prefix_kernel<false>)
+                                                   : static_cast<RenderFn>(store_pipe_prefix_kernel<true>);
+  }();
+  return f;
+}
+
 using RowsFn = void (*)(StorePipeArgs, const int32_t*, int64_t, uint32_t, uint32_t);
 
 static RowsFn render_rows_fn() {
@@ -1282,7 +1323,7 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
   if (a.n > 0 && a.render_first == 2) {
     const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
     hipLaunchKernelGGL(render_rows_fn(), dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
-    if (nd > 0) hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(pb), dim3(256), 0, st, a, dsess, nd);
+    if (nd > 0) hipLaunchKernelGGL(prefix_fn(), dim3(pb), dim3(256), 0, st, a, dsess, nd);
     hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
   } else if (a.n > 0 && a.render_first) {
     const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
@@ -1312,7 +1353,7 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
         hipLaunchKernelGGL(render_fn(), dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                            a, dsess, nd);
       if (a.mid && (cg || !a.prefix_in_render))
-        hipLaunchKernelGGL(store_pipe_prefix_kernel, dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL(prefix_fn(), dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                            a, dsess, nd);
     }
     hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
