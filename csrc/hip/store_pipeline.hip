@@ -435,10 +435,10 @@ struct ArenaSinkT {
 // is rendered as 66 placeholder bytes whose offset is recorded (d_hole).
 // Block `b` of the SHA-256 message of a `len`-byte record at w32 (big-endian
 // words, 0x80 terminator and bit length in the last of its `nblk` blocks).
-AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t b, uint32_t blk[16]) {
-  // 16-byte loads of the chunks that start inside the record (reservations are
-  // whole 64-byte lines, so a chunk that starts before `len` lies inside them)
-  uint32_t raw[16];
+// The raw (little-endian) words of block b: 16-byte loads of the chunks that start
+// inside the record (reservations are whole 64-byte lines, so a chunk that starts
+// before `len` lies inside them), zeros past it.
+AHV_HD void sp_block_raw(const uint32_t* w32, uint64_t len, uint64_t b, uint32_t raw[16]) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const uint64_t o = 64 * b + 16 * c;
@@ -462,6 +462,11 @@ AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t 
     raw[4 * c + 2] = x2;
     raw[4 * c + 3] = x3;
   }
+}
+
+// Message words of block b from its raw words: big-endian, the 0x80 terminator and
+// the bit length in the last of the record's `nblk` blocks.
+AHV_HD void sp_block_words(const uint32_t raw[16], uint64_t len, uint64_t nblk, uint64_t b, uint32_t blk[16]) {
 #pragma unroll
   for (int w = 0; w < 16; ++w) {
     const uint64_t o = 64 * b + 4 * w;
@@ -476,6 +481,12 @@ AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t 
     if (b == nblk - 1 && w == 15) x |= static_cast<uint32_t>(len * 8);
     blk[w] = x;
   }
+}
+
+AHV_HD void sp_block(const uint32_t* w32, uint64_t len, uint64_t nblk, uint64_t b, uint32_t blk[16]) {
+  uint32_t raw[16];
+  sp_block_raw(w32, len, b, raw);
+  sp_block_words(raw, len, nblk, b, blk);
 }
 
 AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g);
@@ -674,6 +685,7 @@ AHV_HD void sp_prefix_t(const StorePipeArgs& a, int64_t g) {
 AHV_HD void sp_prefix(const StorePipeArgs& a, int64_t g) { sp_prefix_t<true>(a, g); }
 
 // Lane per session: the SHA-256 chain over its records (K08).
+template <bool kPipe = true>
 AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
   const Tables& t = a.t;
   const int64_t s = a.slot[i];
@@ -700,10 +712,23 @@ AHV_HD void sp_chain(const StorePipeArgs& a, int64_t i) {
     } else {
       sha256_init(h);
     }
-    for (uint64_t b = pb; b < nblk; ++b) {
-      uint32_t blk[16];
-      sp_block(w32, len, nblk, b, blk);
-      sha256_compress(h, blk);
+    if (kPipe) {  // block b+1's loads in flight while block b compresses
+      uint32_t nx[16];
+      if (pb < nblk) sp_block_raw(w32, len, pb, nx);
+      for (uint64_t b = pb; b < nblk; ++b) {
+        uint32_t raw[16], blk[16];
+#pragma unroll
+        for (int w = 0; w < 16; ++w) raw[w] = nx[w];
+        if (b + 1 < nblk) sp_block_raw(w32, len, b + 1, nx);
+        sp_block_words(raw, len, nblk, b, blk);
+        sha256_compress(h, blk);
+      }
+    } else {
+      for (uint64_t b = pb; b < nblk; ++b) {
+        uint32_t blk[16];
+        sp_block(w32, len, nblk, b, blk);
+        sha256_compress(h, blk);
+      }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -839,12 +864,13 @@ __global__ __launch_bounds__(256) void store_pipe_render_rows_kernel(StorePipeAr
 // varying size): lanes take sessions in descending-work order (chain_order), so
 // the 64 chains of a wave are about equally long and the wave does not idle most
 // lanes while its longest chain finishes.
+template <bool kPipe>
 __global__ __launch_bounds__(64) void store_pipe_chain_kernel(StorePipeArgs a) {
   const int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (x >= a.n) return;
   const int64_t i = a.chain_order ? a.chain_order[x] : x;
   if (a.status[i] != SP_ROW_IN_USE) {
-    sp_chain(a, i);
+    sp_chain<kPipe>(a, i);
     if (a.chain_roots) sp_chain_root(a, i);
   }
 }
@@ -1269,6 +1295,18 @@ static RenderFn prefix_fn() {
   return f;
 }
 
+using ChainFn = void (*)(StorePipeArgs);
+
+// AHV_SP_CHAIN_PIPE=0: the chain lanes load each block, then compress it (A/B)
+static ChainFn chain_fn() {
+  static const ChainFn f = [] {
+    const char* e = std::getenv("AHV_SP_CHAIN_PIPE");
+    return (e != nullptr && std::string(e) == "0") ? static_cast<ChainFn>(store_pipe_chain_kernel<false>)
+                                                   : static_cast<ChainFn>(store_pipe_chain_kernel<true>);
+  }();
+  return f;
+}
+
 using RowsFn = void (*)(StorePipeArgs, const int32_t*, int64_t, uint32_t, uint32_t);
 
 static RowsFn render_rows_fn() {
@@ -1324,13 +1362,13 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
     const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
     hipLaunchKernelGGL(render_rows_fn(), dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
     if (nd > 0) hipLaunchKernelGGL(prefix_fn(), dim3(pb), dim3(256), 0, st, a, dsess, nd);
-    hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(chain_fn(), dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
   } else if (a.n > 0 && a.render_first) {
     const unsigned rb = static_cast<unsigned>((a.n + 255) / 256), pb = static_cast<unsigned>((nd + 255) / 256);
     if (nd > 0)
       hipLaunchKernelGGL(render_fn(), dim3(pb), dim3(256), 0, st, a, dsess, nd);
     hipLaunchKernelGGL(store_pipe_prefix_rows_kernel, dim3(rb + pb), dim3(256), 0, st, a, dsess, nd, rb, rb + pb);
-    hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(chain_fn(), dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
   } else if (a.n > 0) {
     hipLaunchKernelGGL(store_pipe_rows_kernel, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, st, a);
     if (nd > 0) {
@@ -1356,7 +1394,7 @@ void store_pipeline_run(const Tables& t, bool gpu, const py::dict& d, uintptr_t 
         hipLaunchKernelGGL(prefix_fn(), dim3(static_cast<unsigned>((nd + 255) / 256)), dim3(256), 0, st,
                            a, dsess, nd);
     }
-    hipLaunchKernelGGL(store_pipe_chain_kernel, dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(chain_fn(), dim3(static_cast<unsigned>((a.n + 63) / 64)), dim3(64), 0, st, a);
   }
   check_hip(hipGetLastError(), "store_pipeline");
 }
