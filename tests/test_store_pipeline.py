@@ -183,12 +183,13 @@ def test_randomized_batch_equals_scalar_api_gpu():
     {"AHV_SP_CHAIN_ROOTS": "0"},
     {"AHV_SP_SINK": "staged"},
     {"AHV_SP_HOIST": "0"},
+    {"AHV_SP_PREFIX_PIPE": "0", "AHV_SP_CHAIN_PIPE": "0"},
 ])
 def test_batch_kernel_layouts_render_the_same_bytes_gpu(layout):
     """The A/B layouts of the batch kernels (cooperative renderer with 16 / 4 lanes per
     record, prefix SHA inside the render pass, render lanes by record shape, rows before
     render in a pass of their own, rows beside the prefix pass, Merkle roots by the K09
-    kernel, the branching arena sink, loads in line) produce the same records, digests and roots as the
+    kernel, the branching arena sink, loads in line, blocks loaded then compressed) produce the same records, digests and roots as the
     scalar API (a fresh process each: the switches are read once)."""
     import os
     import subprocess
