@@ -133,27 +133,15 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
     return;
   }
   int32_t status = SP_OK;
-  // every per-session input loaded before the first row store: a load issued after
-  // stores waits for them too (one memory counter), so loading late costs a round trip each
   const int64_t t0 = a.t0[i];
   const uint8_t fl = a.flags[i];
-  const int32_t maxpart = a.maxpart[i];
-  const double minsig = a.minsig[i];
-  const int32_t creator = a.creator[i];
-  uint32_t uw[4];
-  for (int k = 0; k < 4; ++k) uw[k] = a.uuid[4 * i + k];
-  const int32_t j0 = a.join_off[i], j1 = a.join_off[i + 1];
-  const int32_t d0 = a.delta_off[i], d1 = a.delta_off[i + 1];
-  const int32_t dlast = d1 > d0 ? a.drow[d1 - 1] : -1;
-  const int32_t g = a.gslot[i];
-  const int32_t k0 = g >= 0 ? a.step_off[i] : 0, k1 = g >= 0 ? a.step_off[i + 1] : 0;
   // create + begin_handshake (OP_SESS_CREATE)
   uint8_t st = SS_HANDSHAKING;
   t.s_mode[s] = (fl & 2u) ? 1 : 0;
   t.s_audit[s] = fl & 1u;
-  t.s_maxpart[s] = maxpart;
-  t.s_minsig[s] = minsig;
-  t.s_creator[s] = creator;
+  t.s_maxpart[s] = a.maxpart[i];
+  t.s_minsig[s] = a.minsig[i];
+  t.s_creator[s] = a.creator[i];
   t.s_created[s] = t0;
   t.s_terminated[s] = 0;
   t.s_committed[s] = 0;
@@ -161,7 +149,7 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
   t.s_released[s] = 0;
   t.s_retained[s] = 0;
   t.s_proot_n[s] = 0;
-  for (int k = 0; k < 4; ++k) t.s_uuid[4 * s + k] = uw[k];
+  for (int k = 0; k < 4; ++k) t.s_uuid[4 * s + k] = a.uuid[4 * i + k];
   for (int k = 0; k < 8; ++k) {
     t.s_head[8 * s + k] = 0;
     t.s_root[8 * s + k] = 0;
@@ -171,6 +159,9 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
   // its first 64 joins, in registers) instead of reading back the participant rows
   // just stored: a read after a store waits out a full memory round trip.
   int32_t pc = 0, active = 0;
+  const int32_t j0 = a.join_off[i], j1 = a.join_off[i + 1];
+  const int32_t maxpart = a.maxpart[i];
+  const double minsig = a.minsig[i];
   uint64_t admitted = 0;
   for (int32_t j = j0; j < j1; ++j) {
     const int32_t agent = a.join_agent[j];
@@ -207,15 +198,18 @@ AHV_HD void sp_rows(const StorePipeArgs& a, int64_t i) {
     else if (status == SP_OK) status = SP_ACTIVATE;
   }
   // delta rows: chain links (records and digests come from the render/chain kernels)
+  const int32_t d0 = a.delta_off[i], d1 = a.delta_off[i + 1];
   const int32_t nd = d1 - d0;
   t.s_dcount[s] = nd;
-  t.s_dlast[s] = dlast;
+  t.s_dlast[s] = nd > 0 ? a.drow[d1 - 1] : -1;
   int64_t tnext = t0 + 1 + nd;
   // saga: steps executed in order with their pre-resolved outcomes (K13), retries
   // reset to PENDING between attempts as the reference does (orchestrator.py:124/134).
   // Each step's state is settled in registers and stored once; the committed steps
   // (first 64) are a bit mask for the compensation pass.
+  const int32_t g = a.gslot[i];
   if (g >= 0) {
+    const int32_t k0 = a.step_off[i], k1 = a.step_off[i + 1];
     t.g_state[g] = SG_RUNNING;
     t.g_created[g] = t0;
     t.g_completed[g] = 0;
@@ -512,13 +506,11 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   const int64_t s = a.slot[i];
   uint32_t uw[4] = {0, 0, 0, 0};
   int64_t ts = 0;
-  int32_t dprev = -1;
   StrRef agent{nullptr, -1};
   if (kHoist) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) uw[q] = a.uuid[4 * i + q];
     ts = sp_delta_ts(a, i, k);
-    dprev = k > 0 ? a.drow[g - 1] : -1;
   }
   ArenaSinkT<kFlat> snk;
   snk.dst = reinterpret_cast<uint32_t*>(t.payload + a.doff[g]);
@@ -614,8 +606,8 @@ AHV_HD void sp_render(const StorePipeArgs& a, int64_t i, int32_t g) {
   snk.flush();
   t.d_sess[d] = static_cast<int32_t>(s);
   t.d_turn[d] = static_cast<int32_t>(turn);
-  t.d_prev[d] = kHoist ? dprev : (k > 0 ? a.drow[g - 1] : -1);
-  t.d_ts[d] = kHoist ? ts : sp_delta_ts(a, i, k);
+  t.d_prev[d] = k > 0 ? a.drow[g - 1] : -1;
+  t.d_ts[d] = sp_delta_ts(a, i, k);
   t.d_off[d] = a.doff[g];
   t.d_len[d] = static_cast<int32_t>(len);
   t.d_hole[d] = hole;
